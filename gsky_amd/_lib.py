@@ -1,0 +1,127 @@
+"""ctypes binding of libgskyhip.so (include/gskyhip.h).
+
+The shared library is the product: hand-written HIP kernels for gfx950 plus a
+C-ABI.  This module only loads it and mirrors its structs; there is no CPU
+fallback.  A missing library raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgskyhip.so")
+
+# GDALDataType codes (warp.go:428-431) + 100 = SignedByte (warp.go:354-359)
+BYTE, UINT16, INT16, UINT32, INT32, FLOAT32, FLOAT64, SIGNEDBYTE = 1, 2, 3, 4, 5, 6, 7, 100
+CRS_LONGLAT, CRS_WEBMERC, CRS_AEA, CRS_SINU = 0, 1, 2, 3
+RESAMPLE_NEAREST, RESAMPLE_BILINEAR = 0, 1
+MAX_OVR = 12
+MAX_BIT_TESTS = 8
+
+ERRORS = {0: "OK", -1: "bad argument", -2: "raster type not implemented", -3: "HIP runtime error",
+          -4: "unsupported CRS", -5: "bad mask", -6: "no HIP device", -7: "index out of range",
+          1: "open failed", 2: "band failed", 3: "transformer failed"}
+
+
+class GskyError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__("%s: %s (%d)" % (what or "gskyhip", ERRORS.get(code, "error"), code))
+
+
+class Crs(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("_pad", C.c_int32)] + [
+        (n, C.c_double) for n in ("a", "ra", "es", "e", "one_es", "lam0", "phi0", "phi1", "phi2",
+                                  "x0", "y0", "k0", "n", "c", "dd", "rho0", "ec")]
+
+
+class Granule(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("dtype", C.c_int32), ("xsize", C.c_int32), ("ysize", C.c_int32),
+                ("signed_byte", C.c_int32), ("geot", C.c_double * 6), ("nodata", C.c_double),
+                ("has_nodata", C.c_int32), ("crs", C.c_int32), ("n_ovr", C.c_int32), ("ns", C.c_int32),
+                ("ovr_data", C.c_void_p * MAX_OVR), ("ovr_xsize", C.c_int32 * MAX_OVR),
+                ("ovr_ysize", C.c_int32 * MAX_OVR), ("timestamp", C.c_double),
+                ("polygon_hash", C.c_uint32), ("_pad2", C.c_int32)]
+
+
+class Tile(C.Structure):
+    _fields_ = [("dst_geot", C.c_double * 6), ("width", C.c_int32), ("height", C.c_int32),
+                ("pair_begin", C.c_int32), ("pair_end", C.c_int32)]
+
+
+class ScaleParams(C.Structure):
+    _fields_ = [("offset", C.c_double), ("scale", C.c_double), ("clip", C.c_double),
+                ("colour_scale", C.c_int32), ("_pad", C.c_int32)]
+
+
+class Mask(C.Structure):
+    _fields_ = [("ns", C.c_int32), ("inclusive", C.c_int32), ("n_bit_tests", C.c_int32),
+                ("_pad", C.c_int32), ("value", C.c_char_p), ("bit_tests", C.c_char_p * MAX_BIT_TESTS)]
+
+
+class FlexRasterC(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("data_w", C.c_int32), ("data_h", C.c_int32), ("width", C.c_int32),
+                ("height", C.c_int32), ("off_x", C.c_int32), ("off_y", C.c_int32), ("dtype", C.c_int32),
+                ("ns", C.c_int32), ("nodata", C.c_double), ("timestamp", C.c_double),
+                ("polygon_hash", C.c_uint32), ("_pad", C.c_int32)]
+
+
+# every symbol include/gskyhip.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "gskyhip_crs_from_srs", "gskyhip_register_granule", "gskyhip_unregister_all", "warp_operation_fast",
+    "gskyhip_render_workspace_size", "gskyhip_render_tiles", "gskyhip_render_tiles_phase",
+    "gskyhip_warp_windows",
+    "gskyhip_merge_rasters", "gskyhip_scale", "gskyhip_scale_legacy", "gskyhip_gradient_palette",
+    "gskyhip_encode_rgba", "gskyhip_compute_mask", "gskyhip_drill_rows", "gskyhip_drill",
+    "gskyhip_drill_merge", "gskyhip_fnv32a", "gskyhip_version", "gskyhip_device_count",
+    "gskyhip_render_status",
+]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libgskyhip.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libgskyhip.so not built: run __graft_entry__.build() (%s)" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, d = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    ci = C.c_int
+    L.gskyhip_crs_from_srs.argtypes = [C.c_char_p, C.POINTER(Crs)]
+    L.gskyhip_register_granule.argtypes = [C.c_char_p, ci, C.POINTER(Granule), C.c_char_p]
+    L.warp_operation_fast.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(d), vp, C.c_char_p, C.POINTER(d),
+                                      ci, ci, ci, ci, C.POINTER(vp), C.POINTER(ci), C.POINTER(ci),
+                                      C.POINTER(d), C.POINTER(ci), C.POINTER(ci)]
+    L.gskyhip_render_workspace_size.argtypes = [ci, ci, ci]
+    L.gskyhip_render_workspace_size.restype = i64
+    L.gskyhip_render_tiles.argtypes = [vp, ci, vp, ci, ci, vp, ci, vp, ci, ci, ci, C.POINTER(i32), ci,
+                                       C.POINTER(Mask), ci, C.POINTER(ScaleParams), vp, vp, vp, vp, i64, vp]
+    L.gskyhip_render_tiles_phase.argtypes = [ci] + L.gskyhip_render_tiles.argtypes
+    L.gskyhip_warp_windows.argtypes = [vp, ci, vp, ci, ci, vp, ci, vp, ci, ci, ci, ci, vp, vp, vp, vp, i64,
+                                       vp, i64, vp]
+    L.gskyhip_render_status.argtypes = [vp, ci, ci, ci, vp]
+    L.gskyhip_merge_rasters.argtypes = [C.POINTER(FlexRasterC), ci, C.POINTER(Mask), C.POINTER(vp), ci,
+                                        C.POINTER(i32), C.POINTER(i32), C.POINTER(d), vp]
+    L.gskyhip_scale.argtypes = [vp, ci, i64, d, C.POINTER(ScaleParams), vp, vp]
+    L.gskyhip_scale_legacy.argtypes = [vp, ci, i64, d, C.POINTER(ScaleParams), vp, vp]
+    L.gskyhip_gradient_palette.argtypes = [vp, ci, ci, vp]
+    L.gskyhip_encode_rgba.argtypes = [C.POINTER(vp), ci, ci, ci, vp, vp, vp]
+    L.gskyhip_compute_mask.argtypes = [vp, ci, i64, C.POINTER(Mask), vp, vp]
+    L.gskyhip_drill_rows.argtypes = [ci, ci]
+    L.gskyhip_drill.argtypes = [vp, ci, ci, ci, ci, vp, vp, vp, ci, C.c_float, C.c_float, C.c_float, ci, ci,
+                                vp, vp, vp]
+    L.gskyhip_drill_merge.argtypes = [vp, vp, ci, ci, vp, vp]
+    L.gskyhip_fnv32a.argtypes = [C.c_char_p, i64]
+    L.gskyhip_fnv32a.restype = C.c_uint32
+    L.gskyhip_version.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def check(code: int, what: str = "") -> None:
+    if code != 0:
+        raise GskyError(code, what)

@@ -1,0 +1,332 @@
+// gsky_device.h -- device-side building blocks of the MI355X raster hot path.
+//
+// Projection math restates PROJ 6.1.1 (merc/webmerc, aea, gn_sinu and the
+// pj_fwd / pj_inv wrappers) and GDAL 3.0.1's GenImgProj transformer; numeric
+// conversions restate Go 1.12 on amd64.  All of it
+// is compiled with -ffp-contract=off so every double expression rounds once
+// per operation, as in the reference's SSE2 code.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gskyhip.h"
+
+namespace gsky {
+
+constexpr double kHalfPi = 1.57079632679489661923;
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kTwoPi = 6.2831853071795864769;
+constexpr double kFortPi = 0.78539816339744830962;
+constexpr double kD2R = 0.017453292519943295769236907684886;
+constexpr double kR2D = 1.0 / 0.017453292519943295769236907684886;
+constexpr double kMaxErr = 0.125;   // GDALCreateApproxTransformer(.., 0.125), warp.go:219
+
+// ---------------------------------------------------------------- Go conversions
+__host__ __device__ inline int32_t go_cvtt32(double x) {
+  // CVTTSD2SL: NaN / out of range -> 0x80000000
+  if (!(x > -2147483649.0 && x < 2147483648.0)) return INT32_MIN;
+  return (int32_t)x;
+}
+__host__ __device__ inline int8_t go_i8(double v) { return (int8_t)(uint8_t)(uint32_t)go_cvtt32(v); }
+__host__ __device__ inline uint8_t go_u8(double v) { return (uint8_t)(uint32_t)go_cvtt32(v); }
+__host__ __device__ inline int16_t go_i16(double v) { return (int16_t)(uint16_t)(uint32_t)go_cvtt32(v); }
+__host__ __device__ inline uint16_t go_u16(double v) { return (uint16_t)(uint32_t)go_cvtt32(v); }
+__host__ __device__ inline uint8_t go_f32_u8(float v) { return go_u8((double)v); }
+
+// GDALCopyWord(double -> integer T): round half away from zero, saturate, NaN->0.
+__host__ __device__ inline double gdal_round_clamp(double v, double lo, double hi) {
+  if (v != v) return 0.0;
+  double r = v >= 0.0 ? v + 0.5 : v - 0.5;
+  if (r > hi) r = hi;
+  if (r < lo) r = lo;
+  return trunc(r);
+}
+
+__host__ __device__ inline int type_size(int dtype) {
+  switch (dtype) {
+    case GSKYHIP_BYTE: case GSKYHIP_SIGNEDBYTE: return 1;
+    case GSKYHIP_UINT16: case GSKYHIP_INT16: return 2;
+    case GSKYHIP_UINT32: case GSKYHIP_INT32: case GSKYHIP_FLOAT32: return 4;
+    case GSKYHIP_FLOAT64: return 8;
+    default: return 0;
+  }
+}
+
+// A raster value carried through the fold as raw bits of its output type.
+// Integer types are sign/zero-extended into `i`; float32 lives in `f`.
+struct Val {
+  union { int32_t i; float f; uint32_t u; };
+};
+
+// GDALCopyWords(nodata double -> output dtype), returned as a Val.
+__host__ __device__ inline Val gdal_copy_to(double v, int dtype) {
+  Val o; o.u = 0;
+  switch (dtype) {
+    case GSKYHIP_BYTE: o.i = (int32_t)(uint8_t)gdal_round_clamp(v, 0, 255); break;
+    // a SignedByte band is a GDT_Byte band: GDALCopyWords clamps to [0,255];
+    // the merge then reads those bits as int8 (tile_merger.go:40-46).
+    case GSKYHIP_SIGNEDBYTE: o.i = (int32_t)(int8_t)(uint8_t)gdal_round_clamp(v, 0, 255); break;
+    case GSKYHIP_UINT16: o.i = (int32_t)(uint16_t)gdal_round_clamp(v, 0, 65535); break;
+    case GSKYHIP_INT16: o.i = (int32_t)(int16_t)gdal_round_clamp(v, -32768, 32767); break;
+    case GSKYHIP_FLOAT32: {
+      float f;
+      if (v == INFINITY || v == -INFINITY) f = (float)v;
+      else if (v > 3.402823466e+38) f = 3.402823466e+38f;
+      else if (v < -3.402823466e+38) f = -3.402823466e+38f;
+      else f = (float)v;
+      o.f = f;
+      break;
+    }
+    default: break;
+  }
+  return o;
+}
+
+// Go T(nodata) of the merge (tile_merger.go:46,80,117,155,193) as a Val of the
+// canvas type.  SignedByte values are kept as int8 sign-extended.
+__host__ __device__ inline Val go_conv_to(double v, int dtype) {
+  Val o; o.u = 0;
+  switch (dtype) {
+    case GSKYHIP_SIGNEDBYTE: o.i = go_i8(v); break;
+    case GSKYHIP_BYTE: o.i = go_u8(v); break;
+    case GSKYHIP_INT16: o.i = go_i16(v); break;
+    case GSKYHIP_UINT16: o.i = go_u16(v); break;
+    case GSKYHIP_FLOAT32: o.f = (float)v; break;
+    default: break;
+  }
+  return o;
+}
+
+// Value equality in the canvas type (float compare for Float32: NaN != NaN).
+__device__ __forceinline__ bool val_eq(Val a, Val b, bool is_float) {
+  return is_float ? (a.f == b.f) : (a.i == b.i);
+}
+
+// ---------------------------------------------------------------- projections
+__host__ __device__ inline double adjlon(double lon) {
+  if (fabs(lon) < kPi + 1e-12) return lon;
+  lon += kPi;
+  lon -= kTwoPi * floor(lon / kTwoPi);
+  lon -= kPi;
+  return lon;
+}
+
+__device__ inline double qsfn(double sinphi, double e, double one_es) {
+  if (e >= 1.0e-7) {
+    double con = e * sinphi;
+    double div1 = 1.0 - con * con;
+    double div2 = 1.0 + con;
+    if (div1 == 0.0 || div2 == 0.0) return HUGE_VAL;
+    return one_es * (sinphi / div1 - (.5 / e) * log((1. - con) / div2));
+  }
+  return sinphi + sinphi;
+}
+
+__device__ inline double aea_phi1(double qs, double Te, double Tone_es) {
+  double Phi = asin(.5 * qs);
+  if (Te < 1.0e-7) return Phi;
+  int i = 15;
+  double dphi;
+  do {
+    double sinpi = sin(Phi), cospi = cos(Phi);
+    double con = Te * sinpi;
+    double com = 1. - con * con;
+    dphi = .5 * com * com / cospi *
+           (qs / Tone_es - sinpi / com + .5 / Te * log((1. - con) / (1. + con)));
+    Phi += dphi;
+  } while (fabs(dphi) > 1.0e-10 && --i);
+  return i ? Phi : HUGE_VAL;
+}
+
+// pj_inv: CRS coordinates -> (lam, phi) in radians.
+__device__ inline bool crs_inverse(const gskyhip_crs &c, double x, double y, double &lam, double &phi) {
+  if (x == HUGE_VAL || y == HUGE_VAL) return false;
+  if (c.kind == GSKYHIP_CRS_LONGLAT) {  // +proj=unitconvert deg -> rad
+    lam = x * kD2R;
+    phi = y * kD2R;
+    return true;
+  }
+  double xn = (x * 1.0 - c.x0) * c.ra;
+  double yn = (y * 1.0 - c.y0) * c.ra;
+  double l, p;
+  if (c.kind == GSKYHIP_CRS_WEBMERC) {  // merc.cpp s_inverse
+    p = kHalfPi - 2. * atan(exp(-yn / c.k0));
+    l = xn / c.k0;
+  } else if (c.kind == GSKYHIP_CRS_AEA) {  // aea.cpp e_inverse
+    yn = c.rho0 - yn;
+    double rho = hypot(xn, yn);
+    if (rho != 0.0) {
+      if (c.n < 0.) { rho = -rho; xn = -xn; yn = -yn; }
+      p = rho / c.dd;
+      if (c.es > 0.) {
+        p = (c.c - p * p) / c.n;
+        if (fabs(c.ec - fabs(p)) > 1e-7) {
+          p = aea_phi1(p, c.e, c.one_es);
+          if (p == HUGE_VAL) return false;
+        } else {
+          p = p < 0. ? -kHalfPi : kHalfPi;
+        }
+      } else {
+        p = (c.c - p * p) / (c.n + c.n);
+        if (fabs(p) <= 1.) p = asin(p);
+        else p = p < 0. ? -kHalfPi : kHalfPi;
+      }
+      l = atan2(xn, yn) / c.n;
+    } else {
+      l = 0.;
+      p = c.n > 0. ? kHalfPi : -kHalfPi;
+    }
+  } else if (c.kind == GSKYHIP_CRS_SINU) {  // gn_sinu.cpp s_inverse (m=0, n=1)
+    p = yn;
+    l = xn / cos(yn);
+  } else {
+    return false;
+  }
+  if (l == HUGE_VAL || p == HUGE_VAL || l != l || p != p) return false;
+  l = l + c.lam0;
+  lam = adjlon(l);
+  phi = p;
+  return true;
+}
+
+// pj_fwd: (lam, phi) radians -> CRS coordinates.
+__device__ inline bool crs_forward(const gskyhip_crs &c, double lam, double phi, double &x, double &y) {
+  if (c.kind == GSKYHIP_CRS_LONGLAT) {  // +proj=unitconvert rad -> deg
+    x = lam * kR2D;
+    y = phi * kR2D;
+    return true;
+  }
+  double t = (phi < 0 ? -phi : phi) - kHalfPi;
+  if (t > 1e-12 || lam > 10 || lam < -10) return false;
+  if (phi > kHalfPi) phi = kHalfPi;
+  if (phi < -kHalfPi) phi = -kHalfPi;
+  lam = lam - c.lam0;
+  lam = adjlon(lam);
+  double xn, yn;
+  if (c.kind == GSKYHIP_CRS_WEBMERC) {  // merc.cpp s_forward
+    if (fabs(fabs(phi) - kHalfPi) <= 1.e-10) return false;
+    xn = c.k0 * lam;
+    yn = c.k0 * log(tan(kFortPi + .5 * phi));
+  } else if (c.kind == GSKYHIP_CRS_AEA) {  // aea.cpp e_forward
+    double rho = c.c - (c.es > 0. ? c.n * qsfn(sin(phi), c.e, c.one_es) : (c.n + c.n) * sin(phi));
+    if (rho < 0.) return false;
+    rho = c.dd * sqrt(rho);
+    lam *= c.n;
+    xn = rho * sin(lam);
+    yn = c.rho0 - rho * cos(lam);
+  } else if (c.kind == GSKYHIP_CRS_SINU) {  // gn_sinu.cpp s_forward (m=0, n=1)
+    xn = lam * cos(phi);
+    yn = phi;
+  } else {
+    return false;
+  }
+  if (xn != xn || yn != yn || isinf(xn) || isinf(yn)) return false;
+  x = 1.0 * (c.a * xn + c.x0);
+  y = 1.0 * (c.a * yn + c.y0);
+  return true;
+}
+
+// GenImgProj transformer state of one (tile, granule) pair.
+struct Xform {
+  gskyhip_crs src, dst;
+  double src_gt[6], src_igt[6], dst_gt[6], dst_igt[6];
+  int reproject;
+};
+
+__host__ __device__ inline void inv_geot(const double *gt, double *o) {  // GDALInvGeoTransform
+  if (gt[2] == 0.0 && gt[4] == 0.0 && gt[1] != 0.0 && gt[5] != 0.0) {
+    o[0] = -gt[0] / gt[1];
+    o[1] = 1.0 / gt[1];
+    o[2] = 0.0;
+    o[3] = -gt[3] / gt[5];
+    o[4] = 0.0;
+    o[5] = 1.0 / gt[5];
+    return;
+  }
+  double det = gt[1] * gt[5] - gt[2] * gt[4];
+  double inv_det = 1.0 / det;
+  o[0] = (gt[2] * gt[3] - gt[0] * gt[5]) * inv_det;
+  o[3] = (-gt[1] * gt[3] + gt[0] * gt[4]) * inv_det;
+  o[1] = gt[5] * inv_det;
+  o[4] = -gt[4] * inv_det;
+  o[2] = -gt[2] * inv_det;
+  o[5] = gt[1] * inv_det;
+}
+
+__host__ __device__ inline bool crs_same(const gskyhip_crs &a, const gskyhip_crs &b) {
+  return a.kind == b.kind && a.a == b.a && a.es == b.es && a.lam0 == b.lam0 && a.phi0 == b.phi0 &&
+         a.phi1 == b.phi1 && a.phi2 == b.phi2 && a.x0 == b.x0 && a.y0 == b.y0 && a.k0 == b.k0;
+}
+
+// GDALGenImgProjTransform for one point; dst_to_src selects the direction.
+__device__ inline bool xform_point(const Xform &t, bool dst_to_src, double &x, double &y) {
+  const double *g1 = dst_to_src ? t.dst_gt : t.src_gt;
+  const double *g2 = dst_to_src ? t.src_igt : t.dst_igt;
+  double X = g1[0] + x * g1[1] + y * g1[2];
+  double Y = g1[3] + x * g1[4] + y * g1[5];
+  if (t.reproject) {
+    double lam, phi;
+    if (dst_to_src) {
+      if (!crs_inverse(t.dst, X, Y, lam, phi)) return false;
+      if (!crs_forward(t.src, lam, phi, X, Y)) return false;
+    } else {
+      if (!crs_inverse(t.src, X, Y, lam, phi)) return false;
+      if (!crs_forward(t.dst, lam, phi, X, Y)) return false;
+    }
+  }
+  x = g2[0] + X * g2[1] + Y * g2[2];
+  y = g2[3] + X * g2[4] + Y * g2[5];
+  return true;
+}
+
+// ---------------------------------------------------------------- plans
+// Per (tile, granule) pair, produced by the planning kernels.
+struct PairPlan {
+  double src_gt[6];       // overview-rescaled source geotransform (warp.go:186-189)
+  double src_igt[6];
+  const void *band;       // chosen level (warp.go:181-183)
+  int32_t band_x, band_y;
+  int32_t xoff, yoff, w, h;  // window (warp.go:200-217)
+  int32_t granule, tile;
+  int32_t src_dtype;      // GDAL type of the level
+  int32_t out_dtype;      // after warp.go:236-243 promotion (SignedByte kept as Byte here)
+  int32_t ns;             // namespace slot
+  int32_t is_mask;        // raster of the mask layer
+  int32_t in_stack;       // merged into a canvas (not a non-inclusive mask)
+  int32_t fill_mode;      // 1: r.TimeStamp < canvas.TimeStamp (tile_merger.go:47)
+  int32_t mask_pair;      // pair whose mask applies (maskMap[geoStamp]) or -1
+  int32_t status;         // 0 ok, else error code
+  double nodata;          // Raster.NoData (warp.go:246)
+  Val fill;               // GDALCopyWords(nodata -> out_dtype), warp.go:247
+  int32_t signed_byte;
+  double stamp;           // TimeStamp + fnv32a(Polygon), tile_merger.go:473-475
+  double ts;              // TimeStamp
+  int32_t has_nodata;
+  int32_t _pad;
+};
+
+struct TilePlan {
+  int32_t n_entries;          // pairs merged (in order[] slots)
+  int32_t status;
+  int32_t complex;            // some row needs exact transforms at render time
+  int32_t _pad;
+  int32_t created[4];
+  int32_t dtype[4];
+  double nodata[4];           // canvas NoData (first raster of the ns)
+};
+
+// Row record of the approximate transformer for one window row.
+enum RowKind : int32_t { ROW_LINEAR = 0, ROW_EXACT = 1, ROW_POOL = 2, ROW_DESCEND = 3 };
+struct RowRec {
+  double v[6];   // LINEAR: xs0, ys0, dX, dY ; DESCEND: xs0, ys0, xs1, ys1, xs2, ys2
+  int32_t kind, nleaf, pool_off, _pad;
+};
+struct Leaf {
+  double xs0, ys0, dX, dY;
+  int32_t start, kind;   // kind: 0 linear, 1 exact
+};
+
+constexpr int kMaxLeavesLocal = 16;
+
+}  // namespace gsky

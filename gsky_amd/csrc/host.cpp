@@ -1,0 +1,686 @@
+// host.cpp -- C-ABI of libgskyhip.so (include/gskyhip.h).
+//
+// Host side of the MI355X path: SRS parsing, Go strconv mask parsing, the
+// (path, band) -> HBM granule registry behind the warp_operation_fast
+// drop-in, and the launch sequences.  All pixel work runs in the HIP kernels
+// of render.hip / stages.hip / drill.hip; nothing here falls back to the CPU.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gskyhip.h"
+#include "drill.h"
+#include "gsky_device.h"
+#include "render.h"
+#include "stages.h"
+
+using namespace gsky;
+
+namespace {
+
+// ---------------------------------------------------------------- SRS parsing
+constexpr double kD2R_h = 0.017453292519943295769236907684886;
+
+void set_ellps(gskyhip_crs *c, double a, double rf) {
+  c->a = a;
+  c->ra = 1.0 / a;
+  if (rf == 0.0) c->es = 0.0;
+  else { double f = 1.0 / rf; c->es = 2 * f - f * f; }
+  c->e = std::sqrt(c->es);
+  c->one_es = 1.0 - c->es;
+}
+
+double h_qsfn(double sinphi, double e, double one_es) {
+  if (e >= 1.0e-7) {
+    double con = e * sinphi;
+    double div1 = 1.0 - con * con;
+    double div2 = 1.0 + con;
+    if (div1 == 0.0 || div2 == 0.0) return HUGE_VAL;
+    return one_es * (sinphi / div1 - (.5 / e) * std::log((1. - con) / div2));
+  }
+  return sinphi + sinphi;
+}
+
+// aea.cpp setup() of PROJ 6.1.1
+int aea_setup(gskyhip_crs *c) {
+  const double phi1 = c->phi1, phi2 = c->phi2;
+  if (std::fabs(phi1 + phi2) < 1e-10) return GSKYHIP_E_CRS;
+  double sinphi = std::sin(phi1), cosphi = std::cos(phi1);
+  c->n = sinphi;
+  const bool secant = std::fabs(phi1 - phi2) >= 1e-10;
+  if (c->es > 0.) {
+    const double m1 = cosphi / std::sqrt(1. - c->es * sinphi * sinphi);
+    const double ml1 = h_qsfn(sinphi, c->e, c->one_es);
+    if (secant) {
+      const double s2 = std::sin(phi2), c2 = std::cos(phi2);
+      const double m2 = c2 / std::sqrt(1. - c->es * s2 * s2);
+      const double ml2 = h_qsfn(s2, c->e, c->one_es);
+      if (ml2 == ml1) return GSKYHIP_E_CRS;
+      c->n = (m1 * m1 - m2 * m2) / (ml2 - ml1);
+    }
+    c->ec = 1. - .5 * c->one_es * std::log((1. - c->e) / (1. + c->e)) / c->e;
+    c->c = m1 * m1 + c->n * ml1;
+    c->dd = 1. / c->n;
+    c->rho0 = c->dd * std::sqrt(c->c - c->n * h_qsfn(std::sin(c->phi0), c->e, c->one_es));
+  } else {
+    if (secant) c->n = .5 * (c->n + std::sin(phi2));
+    const double n2 = c->n + c->n;
+    c->c = cosphi * cosphi + n2 * sinphi;
+    c->dd = 1. / c->n;
+    c->rho0 = c->dd * std::sqrt(c->c - n2 * std::sin(c->phi0));
+  }
+  return 0;
+}
+
+double proj_param(const std::string &s, const char *key, double dflt, bool *found = nullptr) {
+  const std::string k = std::string(key) + "=";
+  size_t pos = 0;
+  while ((pos = s.find(k, pos)) != std::string::npos) {
+    if (pos == 0 || s[pos - 1] == ' ' || s[pos - 1] == '+') {
+      if (found) *found = true;
+      return std::strtod(s.c_str() + pos + k.size(), nullptr);
+    }
+    pos += k.size();
+  }
+  if (found) *found = false;
+  return dflt;
+}
+
+int crs_epsg(int code, gskyhip_crs *c) {
+  std::memset(c, 0, sizeof(*c));
+  c->k0 = 1.0;
+  switch (code) {
+    case 4326: c->kind = GSKYHIP_CRS_LONGLAT; set_ellps(c, 6378137.0, 298.257223563); return 0;
+    case 4283: c->kind = GSKYHIP_CRS_LONGLAT; set_ellps(c, 6378137.0, 298.257222101); return 0;
+    case 3857: case 900913: c->kind = GSKYHIP_CRS_WEBMERC; set_ellps(c, 6378137.0, 0.0); return 0;
+    case 3577:
+      c->kind = GSKYHIP_CRS_AEA;
+      set_ellps(c, 6378137.0, 298.257222101);
+      c->lam0 = 132.0 * kD2R_h; c->phi0 = 0.0; c->phi1 = -18.0 * kD2R_h; c->phi2 = -36.0 * kD2R_h;
+      return aea_setup(c);
+    default: return GSKYHIP_E_CRS;
+  }
+}
+
+int crs_proj4(const std::string &s, gskyhip_crs *c) {
+  std::memset(c, 0, sizeof(*c));
+  c->k0 = 1.0;
+  bool has_a = false;
+  double a = proj_param(s, "+a", 0, &has_a);
+  double R = proj_param(s, "+R", 0);
+  double rf = proj_param(s, "+rf", 0);
+  if (s.find("+ellps=GRS80") != std::string::npos) { a = 6378137.0; rf = 298.257222101; has_a = true; }
+  else if (s.find("+ellps=WGS84") != std::string::npos || s.find("+datum=WGS84") != std::string::npos) {
+    a = 6378137.0; rf = 298.257223563; has_a = true;
+  }
+  if (R > 0) { a = R; rf = 0; has_a = true; }
+  if (!has_a) { a = 6378137.0; rf = 298.257223563; }
+  c->lam0 = proj_param(s, "+lon_0", 0) * kD2R_h;
+  c->phi0 = proj_param(s, "+lat_0", 0) * kD2R_h;
+  c->x0 = proj_param(s, "+x_0", 0);
+  c->y0 = proj_param(s, "+y_0", 0);
+  if (s.find("+proj=longlat") != std::string::npos || s.find("+proj=latlong") != std::string::npos) {
+    c->kind = GSKYHIP_CRS_LONGLAT; set_ellps(c, a, rf); return 0;
+  }
+  if (s.find("+proj=webmerc") != std::string::npos || (s.find("+proj=merc") != std::string::npos && R > 0)) {
+    c->kind = GSKYHIP_CRS_WEBMERC; set_ellps(c, a, 0.0); return 0;
+  }
+  if (s.find("+proj=aea") != std::string::npos) {
+    c->kind = GSKYHIP_CRS_AEA; set_ellps(c, a, rf);
+    c->phi1 = proj_param(s, "+lat_1", 0) * kD2R_h;
+    c->phi2 = proj_param(s, "+lat_2", 0) * kD2R_h;
+    return aea_setup(c);
+  }
+  if (s.find("+proj=sinu") != std::string::npos) {
+    c->kind = GSKYHIP_CRS_SINU; set_ellps(c, a, rf);
+    return c->es == 0 ? 0 : GSKYHIP_E_CRS;  // only the spherical form (MODIS)
+  }
+  return GSKYHIP_E_CRS;
+}
+
+int parse_srs(const char *srs, gskyhip_crs *c) {
+  if (!srs) return GSKYHIP_E_CRS;
+  std::string s(srs);
+  auto ieq = [](const std::string &a, const char *b) { return strcasecmp(a.c_str(), b) == 0; };
+  if (ieq(s, "MODIS") || ieq(s, "SR-ORG:6842")) return crs_proj4("+proj=sinu +R=6371007.181", c);
+  if (s.size() > 5 && strncasecmp(s.c_str(), "EPSG:", 5) == 0) return crs_epsg(std::atoi(s.c_str() + 5), c);
+  if (s.find("+proj=") != std::string::npos) return crs_proj4(s, c);
+  // WKT: a Sinusoidal / Albers projection, else the top-level (last) EPSG authority
+  if (s.find("PROJECTION[\"Sinusoidal\"]") != std::string::npos) {
+    size_t p = s.find("SPHEROID[");
+    double a = 6371007.181;
+    if (p != std::string::npos) {
+      size_t q = s.find(',', p);
+      if (q != std::string::npos) a = std::strtod(s.c_str() + q + 1, nullptr);
+    }
+    char buf[96];
+    std::snprintf(buf, sizeof(buf), "+proj=sinu +R=%.17g", a);
+    return crs_proj4(buf, c);
+  }
+  size_t pos = s.rfind("AUTHORITY[\"EPSG\",\"");
+  if (pos != std::string::npos) return crs_epsg(std::atoi(s.c_str() + pos + 18), c);
+  pos = s.rfind("ID[\"EPSG\",");
+  if (pos != std::string::npos) return crs_epsg(std::atoi(s.c_str() + pos + 10), c);
+  return GSKYHIP_E_CRS;
+}
+
+// ---------------------------------------------------------------- Go strconv (base 2)
+uint64_t go_parse_uint2(const char *s, int bits, bool *syntax = nullptr) {
+  const uint64_t maxVal = (bits >= 64) ? UINT64_MAX : ((1ull << bits) - 1);
+  if (syntax) *syntax = false;
+  if (!s || !*s) { if (syntax) *syntax = true; return 0; }
+  uint64_t n = 0;
+  for (const char *p = s; *p; p++) {
+    const char c = *p;
+    int d;
+    if (c >= '0' && c <= '9') d = c - '0';
+    else if ((c | 0x20) >= 'a' && (c | 0x20) <= 'z') d = (c | 0x20) - 'a' + 10;
+    else { if (syntax) *syntax = true; return 0; }
+    if (d >= 2) { if (syntax) *syntax = true; return 0; }
+    if (n >= UINT64_MAX / 2 + 1) return maxVal;
+    n *= 2;
+    const uint64_t n1 = n + (uint64_t)d;
+    if (n1 < n || n1 > maxVal) return maxVal;
+    n = n1;
+  }
+  return n;
+}
+int64_t go_parse_int2(const char *s, int bits) {
+  if (!s || !*s) return 0;
+  bool neg = false;
+  if (*s == '+') s++;
+  else if (*s == '-') { neg = true; s++; }
+  bool syntax = false;
+  const uint64_t un = go_parse_uint2(s, bits, &syntax);
+  if (syntax) return 0;
+  const uint64_t cutoff = 1ull << (bits - 1);
+  if (!neg && un >= cutoff) return (int64_t)(cutoff - 1);
+  if (neg && un > cutoff) return -(int64_t)cutoff;
+  return neg ? -(int64_t)un : (int64_t)un;
+}
+
+// Mask specs for the four mask-raster types (tile_merger.go:328-439).
+int build_mask_specs(const gskyhip_mask *m, MaskSpecS out[4]) {
+  std::memset(out, 0, sizeof(MaskSpecS) * 4);
+  if (!m || m->ns < 0) return 0;
+  const bool has_value = m->value && *m->value;
+  if (!has_value) {
+    if (m->n_bit_tests == 0 || m->n_bit_tests % 2 != 0) return GSKYHIP_E_MASK;
+  }
+  if (m->n_bit_tests > GSKYHIP_MAX_BIT_TESTS) return GSKYHIP_E_ARG;
+  const int dts[4] = {GSKYHIP_SIGNEDBYTE, GSKYHIP_BYTE, GSKYHIP_INT16, GSKYHIP_UINT16};
+  for (int k = 0; k < 4; k++) {
+    MaskSpecS &o = out[k];
+    const int dt = dts[k];
+    const int bits = (dt == GSKYHIP_INT16 || dt == GSKYHIP_UINT16) ? 16 : 8;
+    o.has_value = has_value ? 1 : 0;
+    if (has_value) {
+      switch (dt) {
+        case GSKYHIP_SIGNEDBYTE: o.value = (int8_t)go_parse_uint2(m->value, 8); break;
+        case GSKYHIP_BYTE: o.value = (uint8_t)go_parse_uint2(m->value, 8); break;
+        case GSKYHIP_INT16: o.value = (int16_t)go_parse_int2(m->value, 16); break;
+        default: o.value = (uint16_t)go_parse_uint2(m->value, 16); break;
+      }
+    } else {
+      o.n_tests = m->n_bit_tests / 2;
+      for (int j = 0; j < o.n_tests; j++) {
+        const int64_t f = go_parse_int2(m->bit_tests[2 * j], bits);
+        const int64_t v = go_parse_int2(m->bit_tests[2 * j + 1], bits);
+        switch (dt) {
+          case GSKYHIP_SIGNEDBYTE: o.filt[j] = (int8_t)f; o.want[j] = (int8_t)v; break;
+          case GSKYHIP_BYTE: o.filt[j] = (uint8_t)f; o.want[j] = (uint8_t)v; break;
+          case GSKYHIP_INT16: o.filt[j] = (int16_t)f; o.want[j] = (int16_t)v; break;
+          default: o.filt[j] = (uint16_t)f; o.want[j] = (uint16_t)v; break;
+        }
+      }
+    }
+  }
+  return 0;
+}
+
+int mask_slot_h(int dtype) {
+  switch (dtype) {
+    case GSKYHIP_SIGNEDBYTE: return 0;
+    case GSKYHIP_BYTE: return 1;
+    case GSKYHIP_INT16: return 2;
+    case GSKYHIP_UINT16: return 3;
+    default: return -1;
+  }
+}
+
+// ---------------------------------------------------------------- drop-in state
+struct Registered {
+  gskyhip_granule g;
+  gskyhip_crs crs;
+  bool has_crs;
+};
+
+struct DropIn {
+  std::mutex mu;
+  std::map<std::pair<std::string, int>, Registered> reg;
+  hipStream_t stream = nullptr;
+  void *dev = nullptr;   // descriptors + workspace + window
+  size_t dev_bytes = 0;
+};
+DropIn &dropin() {
+  static DropIn d;
+  return d;
+}
+
+bool have_gpu() {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+}  // namespace
+
+// ======================================================================== C-ABI
+extern "C" {
+
+int gskyhip_crs_from_srs(const char *srs, gskyhip_crs *out) { return parse_srs(srs, out); }
+
+uint32_t gskyhip_fnv32a(const char *s, int64_t n) {
+  uint32_t h = 2166136261u;  // Go hash/fnv New32a (tile_merger.go:473-475)
+  for (int64_t i = 0; i < n; i++) {
+    h ^= (uint8_t)s[i];
+    h *= 16777619u;
+  }
+  return h;
+}
+
+const char *gskyhip_version(void) { return "gskyhip 0.1 gfx950"; }
+
+int gskyhip_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int gskyhip_register_granule(const char *path, int band, const gskyhip_granule *g, const char *srs) {
+  if (!path || !g) return GSKYHIP_E_ARG;
+  Registered r;
+  r.g = *g;
+  r.has_crs = false;
+  if (srs && *srs) {
+    if (parse_srs(srs, &r.crs)) return GSKYHIP_E_CRS;
+    r.has_crs = true;
+  }
+  DropIn &d = dropin();
+  std::lock_guard<std::mutex> lk(d.mu);
+  d.reg[{std::string(path), band}] = r;
+  return 0;
+}
+
+int gskyhip_unregister_all(void) {
+  DropIn &d = dropin();
+  std::lock_guard<std::mutex> lk(d.mu);
+  d.reg.clear();
+  return 0;
+}
+
+// warp.go:82-382 drop-in.  Plans and warps on the GPU (one tile, one pair),
+// then hands the window back in malloc'd host memory.
+int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGeot,
+                        const char **geoLocOpts, const char *dstProjRef, double *dstGeot,
+                        int dstXImageSize, int dstYImageSize, int band, int srsCf, void **dstBuf,
+                        int *dstBufSize, int *dstBbox, double *noData, int *dType, int *bytesRead) {
+  (void)srsCf;
+  *bytesRead = 0;
+  DropIn &d = dropin();
+  std::lock_guard<std::mutex> lk(d.mu);
+  if (!srcFilePath) return 1;
+  // netCDF paths are opened with band_query and read as band 1 (warp.go:89-101)
+  auto it = d.reg.find({std::string(srcFilePath), band});
+  if (it == d.reg.end()) it = d.reg.find({std::string(srcFilePath), 1});
+  if (it == d.reg.end()) return 1;                                   // open failed
+  const Registered &R = it->second;
+  if (!R.g.data) return 2;                                           // band failed
+  if (geoLocOpts) return 3;                                          // geolocation arrays: unsupported
+  if (!have_gpu()) return GSKYHIP_E_NOGPU;
+  gskyhip_crs crs[2];
+  if (srcProjRef) {
+    if (parse_srs(srcProjRef, &crs[0])) return 3;
+  } else if (R.has_crs) {
+    crs[0] = R.crs;
+  } else {
+    crs_epsg(4326, &crs[0]);                                         // warp.go:107-112
+  }
+  int dst_crs = -1;
+  if (dstProjRef) {
+    if (parse_srs(dstProjRef, &crs[1])) return 3;
+    dst_crs = 1;
+  }
+  gskyhip_granule g = R.g;
+  g.crs = 0;
+  g.ns = 0;
+  if (srcGeot) std::memcpy(g.geot, srcGeot, sizeof(g.geot));
+  gskyhip_tile tile;
+  std::memcpy(tile.dst_geot, dstGeot, sizeof(tile.dst_geot));
+  tile.width = dstXImageSize;
+  tile.height = dstYImageSize;
+  tile.pair_begin = 0;
+  tile.pair_end = 1;
+  if (dstXImageSize <= 0 || dstYImageSize <= 0) return GSKYHIP_E_ARG;
+
+  if (!d.stream && hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess) return GSKYHIP_E_HIP;
+  const int64_t ws = render_workspace_size(1, 1, dstYImageSize);
+  const int64_t win_bytes = (int64_t)dstXImageSize * dstYImageSize * 4;
+  const int64_t hdr = 4096;
+  const size_t need = (size_t)(hdr + ws + win_bytes + 256);
+  if (d.dev_bytes < need) {
+    if (d.dev) hipFree(d.dev);
+    d.dev = nullptr;
+    d.dev_bytes = 0;
+    if (hipMalloc(&d.dev, need) != hipSuccess) return GSKYHIP_E_HIP;
+    d.dev_bytes = need;
+  }
+  char *base = (char *)d.dev;
+  // header layout: granule | crs[2] | tile | pair | bbox | dtype | nodata
+  struct Hdr {
+    gskyhip_granule g;
+    gskyhip_crs crs[2];
+    gskyhip_tile tile;
+    int32_t pair;
+    int32_t bbox[4];
+    int32_t dtype;
+    double nodata;
+  };
+  static_assert(sizeof(Hdr) <= 4096, "header");
+  Hdr h;
+  h.g = g;
+  h.crs[0] = crs[0];
+  h.crs[1] = crs[1];
+  h.tile = tile;
+  h.pair = 0;
+  Hdr *dh = (Hdr *)base;
+  if (hipMemcpyAsync(dh, &h, sizeof(Hdr), hipMemcpyHostToDevice, d.stream) != hipSuccess) return GSKYHIP_E_HIP;
+  MaskSpecS ms[4];
+  std::memset(ms, 0, sizeof(ms));
+  RenderCall rc;
+  rc.granules = &dh->g; rc.n_granules = 1;
+  rc.crs = dh->crs; rc.n_crs = 2; rc.dst_crs = dst_crs;
+  rc.tiles = &dh->tile; rc.n_tiles = 1;
+  rc.pair_granule = &dh->pair; rc.n_pairs = 1;
+  rc.max_w = dstXImageSize; rc.max_h = dstYImageSize;
+  rc.mask_ns = -1; rc.mask_inclusive = 0; rc.mask_specs = ms;
+  rc.resample = GSKYHIP_RESAMPLE_NEAREST;
+  rc.workspace = base + hdr; rc.workspace_bytes = ws;
+  rc.stream = d.stream;
+  char *win = base + hdr + ws;
+  int rcode = launch_warp_windows(rc, dh->bbox, &dh->dtype, &dh->nodata, win, win_bytes);
+  if (rcode) return rcode;
+  Hdr back;
+  if (hipMemcpyAsync(&back, dh, sizeof(Hdr), hipMemcpyDeviceToHost, d.stream) != hipSuccess) return GSKYHIP_E_HIP;
+  double gt_back[6];
+  // PairPlan of pair 0 sits at the start of the workspace; its src_gt is the
+  // overview-rescaled geotransform (warp.go:186-189)
+  hipMemcpyAsync(gt_back, rc.workspace, sizeof(gt_back), hipMemcpyDeviceToHost, d.stream);
+  if (hipStreamSynchronize(d.stream) != hipSuccess) return GSKYHIP_E_HIP;
+  const int w = back.bbox[2], hh = back.bbox[3];
+  const int dsz = type_size(back.dtype);
+  *dstBufSize = w * hh * dsz;
+  *dstBuf = std::malloc(*dstBufSize > 0 ? *dstBufSize : 1);
+  if (!*dstBuf) return GSKYHIP_E_ARG;
+  if (*dstBufSize > 0 &&
+      hipMemcpy(*dstBuf, win, (size_t)*dstBufSize, hipMemcpyDeviceToHost) != hipSuccess) {
+    std::free(*dstBuf);
+    *dstBuf = nullptr;
+    return GSKYHIP_E_HIP;
+  }
+  for (int k = 0; k < 4; k++) dstBbox[k] = back.bbox[k];
+  *noData = back.nodata;
+  *dType = back.dtype;
+  if (srcGeot) std::memcpy(srcGeot, gt_back, sizeof(gt_back));
+  return 0;
+}
+
+int64_t gskyhip_render_workspace_size(int n_tiles, int n_pairs, int max_tile_height) {
+  return render_workspace_size(n_tiles, n_pairs, max_tile_height);
+}
+
+int gskyhip_render_tiles_phase(int phase, const gskyhip_granule *granules, int n_granules,
+                               const gskyhip_crs *crs_table, int n_crs, int dst_crs, const gskyhip_tile *tiles,
+                               int n_tiles, const int32_t *pair_granule, int n_pairs, int max_tile_width,
+                               int max_tile_height, const int32_t *out_ns, int n_out_ns, const gskyhip_mask *mask,
+                               int resample, const gskyhip_scale_params *sp, const uint8_t *ramp,
+                               uint8_t *rgba_out, void *canvas_out, void *workspace, int64_t workspace_bytes,
+                               void *stream) {
+  if (!sp || !out_ns || n_tiles < 0 || n_pairs < 0 || phase < 0 || phase > 2) return GSKYHIP_E_ARG;
+  MaskSpecS ms[4];
+  int r = build_mask_specs(mask, ms);
+  if (r) return r;
+  RenderCall rc;
+  rc.granules = granules; rc.n_granules = n_granules;
+  rc.crs = crs_table; rc.n_crs = n_crs; rc.dst_crs = dst_crs;
+  rc.tiles = tiles; rc.n_tiles = n_tiles;
+  rc.pair_granule = pair_granule; rc.n_pairs = n_pairs;
+  rc.max_w = max_tile_width; rc.max_h = max_tile_height;
+  rc.mask_ns = mask ? mask->ns : -1;
+  rc.mask_inclusive = mask ? mask->inclusive : 0;
+  rc.mask_specs = ms;
+  rc.resample = resample;
+  rc.workspace = workspace; rc.workspace_bytes = workspace_bytes;
+  rc.stream = (hipStream_t)stream;
+  return launch_render(rc, out_ns, n_out_ns, *sp, ramp, rgba_out, canvas_out, phase);
+}
+
+int gskyhip_render_tiles(const gskyhip_granule *granules, int n_granules, const gskyhip_crs *crs_table,
+                         int n_crs, int dst_crs, const gskyhip_tile *tiles, int n_tiles,
+                         const int32_t *pair_granule, int n_pairs, int max_tile_width, int max_tile_height,
+                         const int32_t *out_ns, int n_out_ns, const gskyhip_mask *mask, int resample,
+                         const gskyhip_scale_params *sp, const uint8_t *ramp, uint8_t *rgba_out,
+                         void *canvas_out, void *workspace, int64_t workspace_bytes, void *stream) {
+  return gskyhip_render_tiles_phase(0, granules, n_granules, crs_table, n_crs, dst_crs, tiles, n_tiles,
+                                    pair_granule, n_pairs, max_tile_width, max_tile_height, out_ns, n_out_ns,
+                                    mask, resample, sp, ramp, rgba_out, canvas_out, workspace, workspace_bytes,
+                                    stream);
+}
+
+int gskyhip_render_status(void *workspace, int n_tiles, int n_pairs, int max_tile_height, void *stream) {
+  // TilePlan array position: after PairPlan[n_pairs] and Xform[n_pairs]
+  auto al = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+  const int np = n_pairs > 0 ? n_pairs : 1;
+  const int64_t off = al(sizeof(PairPlan) * (int64_t)np) + al(sizeof(Xform) * (int64_t)np);
+  (void)max_tile_height;
+  std::vector<TilePlan> tp((size_t)(n_tiles > 0 ? n_tiles : 0));
+  if (n_tiles <= 0) return 0;
+  if (hipMemcpyAsync(tp.data(), (char *)workspace + off, sizeof(TilePlan) * n_tiles, hipMemcpyDeviceToHost,
+                     (hipStream_t)stream) != hipSuccess)
+    return GSKYHIP_E_HIP;
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return GSKYHIP_E_HIP;
+  for (const auto &t : tp)
+    if (t.status) return t.status;
+  return 0;
+}
+
+int gskyhip_warp_windows(const gskyhip_granule *granules, int n_granules, const gskyhip_crs *crs_table,
+                         int n_crs, int dst_crs, const gskyhip_tile *tiles, int n_tiles,
+                         const int32_t *pair_granule, int n_pairs, int max_tile_width, int max_tile_height,
+                         int resample, int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
+                         void *win_out, int64_t win_stride, void *workspace, int64_t workspace_bytes,
+                         void *stream) {
+  MaskSpecS ms[4];
+  std::memset(ms, 0, sizeof(ms));
+  RenderCall rc;
+  rc.granules = granules; rc.n_granules = n_granules;
+  rc.crs = crs_table; rc.n_crs = n_crs; rc.dst_crs = dst_crs;
+  rc.tiles = tiles; rc.n_tiles = n_tiles;
+  rc.pair_granule = pair_granule; rc.n_pairs = n_pairs;
+  rc.max_w = max_tile_width; rc.max_h = max_tile_height;
+  rc.mask_ns = -1; rc.mask_inclusive = 0; rc.mask_specs = ms;
+  rc.resample = resample;
+  rc.workspace = workspace; rc.workspace_bytes = workspace_bytes;
+  rc.stream = (hipStream_t)stream;
+  if (win_stride < (int64_t)max_tile_width * max_tile_height * 4) return GSKYHIP_E_ARG;
+  return launch_warp_windows(rc, bbox_out, dtype_out, nodata_out, win_out, win_stride);
+}
+
+// RasterMerger.Run for one batch over warped FlexRasters (tile_merger.go:447-503).
+int gskyhip_merge_rasters(const gskyhip_flex_raster *rasters, int n, const gskyhip_mask *mask,
+                          void *const *canvases, int n_ns, int32_t *created, int32_t *dtype, double *nodata,
+                          void *stream) {
+  MaskSpecS ms[4];
+  int r = build_mask_specs(mask, ms);
+  if (r) return r;
+  const int mask_ns = mask ? mask->ns : -1;
+  const bool inclusive = mask && mask->inclusive;
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<double> stamp(n);
+  std::vector<int> keys;
+  std::vector<char> in_stack(n, 0);
+  for (int i = 0; i < n; i++) {
+    stamp[i] = rasters[i].timestamp + (double)rasters[i].polygon_hash;   // 473-475
+    if (mask_ns >= 0 && rasters[i].ns == mask_ns) {
+      if (mask_slot_h(rasters[i].dtype) < 0) return GSKYHIP_E_MASK;      // 440-442
+      if (!inclusive) continue;                                          // 485-487
+    }
+    in_stack[i] = 1;
+  }
+  // stable order: geoStamp descending, arrival order within a key (281-290)
+  std::vector<int> order;
+  for (int i = 0; i < n; i++) if (in_stack[i]) order.push_back(i);
+  for (size_t a = 1; a < order.size(); a++) {
+    const int v = order[a];
+    size_t j = a;
+    while (j > 0 && stamp[order[j - 1]] < stamp[v]) { order[j] = order[j - 1]; j--; }
+    order[j] = v;
+  }
+  for (int k = 0; k < n_ns; k++) { created[k] = 0; dtype[k] = 0; nodata[k] = 0; }
+  std::vector<std::vector<FlexEntry>> per_ns(n_ns);
+  std::vector<double> canvas_ts(n_ns, 0.0);
+  int width = 0, height = 0;
+  for (int idx : order) {
+    const gskyhip_flex_raster &fr = rasters[idx];
+    if (fr.ns < 0 || fr.ns >= n_ns) return GSKYHIP_E_RANGE;
+    width = fr.width; height = fr.height;
+    if (!created[fr.ns]) {                                               // 291-297
+      created[fr.ns] = 1;
+      dtype[fr.ns] = fr.dtype;
+      nodata[fr.ns] = fr.nodata;
+      canvas_ts[fr.ns] = 0;
+    } else if (dtype[fr.ns] != fr.dtype) {
+      return GSKYHIP_E_TYPE;
+    }
+    FlexEntry e;
+    std::memset(&e, 0, sizeof(e));
+    e.data = fr.data;
+    e.data_w = fr.data_w; e.data_h = fr.data_h; e.off_x = fr.off_x; e.off_y = fr.off_y;
+    e.dtype = fr.dtype;
+    e.nodata = fr.nodata;
+    e.fill_mode = fr.timestamp < canvas_ts[fr.ns] ? 1 : 0;              // 47
+    if (!e.fill_mode) canvas_ts[fr.ns] = fr.timestamp;
+    for (int q = 0; q < n; q++) {                                        // maskMap[geoStamp]
+      if (mask_ns >= 0 && rasters[q].ns == mask_ns && stamp[q] == stamp[idx]) {
+        e.mask_data = rasters[q].data;
+        e.mask_dtype = rasters[q].dtype;
+        e.mask_len = (int64_t)rasters[q].data_w * rasters[q].data_h;
+      }
+    }
+    if (e.mask_data && (int64_t)e.data_w * e.data_h > e.mask_len) return GSKYHIP_E_RANGE;
+    per_ns[fr.ns].push_back(e);
+  }
+  for (int k = 0; k < n_ns; k++) {
+    if (!created[k]) continue;
+    const int slot = mask_slot_h(per_ns[k].empty() ? 0 : per_ns[k][0].mask_dtype);
+    const MaskSpecS &m = ms[slot < 0 ? 0 : slot];
+    // all mask rasters of one layer share a dtype; pick its spec
+    MaskSpecS mm = m;
+    for (const auto &e : per_ns[k]) {
+      if (e.mask_data) { int sl = mask_slot_h(e.mask_dtype); if (sl >= 0) mm = ms[sl]; break; }
+    }
+    r = launch_merge_fold(per_ns[k].data(), (int)per_ns[k].size(), width, height, dtype[k], nodata[k], mm,
+                          canvases[k], s);
+    if (r) return r;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return GSKYHIP_E_HIP;
+  return 0;
+}
+
+int gskyhip_scale(void *data, int dtype, int64_t n, double nodata, const gskyhip_scale_params *sp,
+                  uint8_t *out, void *stream) {
+  if (!sp) return GSKYHIP_E_ARG;
+  return launch_scale(data, dtype, n, nodata, *sp, out, (hipStream_t)stream);
+}
+
+int gskyhip_scale_legacy(void *data, int dtype, int64_t n, double nodata, const gskyhip_scale_params *sp,
+                         uint8_t *out, void *stream) {
+  if (!sp) return GSKYHIP_E_ARG;
+  return launch_scale_legacy(data, dtype, n, nodata, *sp, out, (hipStream_t)stream);
+}
+
+// GradientRGBAPalette (utils/palette.go:27-69); 256 entries, host only.
+int gskyhip_gradient_palette(const uint8_t *colours, int n, int interpolate, uint8_t *ramp) {
+  auto interp = [](uint8_t a, uint8_t b, long i, long section) {
+    const long q = (i * ((long)b - (long)a)) / section;   // Go int, truncating division
+    return (uint8_t)(a + (uint8_t)q);                      // uint8 wrap
+  };
+  if (interpolate) {
+    if (n < 2) return GSKYHIP_E_ARG;
+    const int bins = n - 1, section = 256 / bins, bonus = 256 - section * bins;
+    if (section == 0) return GSKYHIP_E_ARG;  // Go: integer divide by zero panic (palette.go:12)
+    int index = 0;
+    for (int s = 0; s < bins; s++) {
+      const uint8_t *a = colours + 4 * s, *b = colours + 4 * (s + 1);
+      const int cnt = section + (s < bonus ? 1 : 0);
+      for (int i = 0; i < cnt; i++, index++) {
+        uint8_t *o = ramp + 4 * index;
+        o[0] = interp(a[0], b[0], i, section);
+        o[1] = interp(a[1], b[1], i, section);
+        o[2] = interp(a[2], b[2], i, section);
+        o[3] = a[3];
+      }
+    }
+  } else {
+    if (n < 1) return GSKYHIP_E_ARG;
+    const int bins = n, section = 256 / bins, bonus = 256 - section * bins;
+    int index = 0;
+    for (int s = 0; s < bins; s++) {
+      const int cnt = section + (s < bonus ? 1 : 0);
+      for (int i = 0; i < cnt; i++, index++) std::memcpy(ramp + 4 * index, colours + 4 * s, 4);
+    }
+  }
+  return 0;
+}
+
+int gskyhip_encode_rgba(const uint8_t *const *bands, int nbands, int w, int h, const uint8_t *ramp,
+                        uint8_t *rgba, void *stream) {
+  if (nbands != 1 && nbands != 3) return GSKYHIP_E_ARG;
+  return launch_encode_rgba(bands[0], nbands == 3 ? bands[1] : nullptr, nbands == 3 ? bands[2] : nullptr,
+                            nbands, (int64_t)w * h, ramp, rgba, (hipStream_t)stream);
+}
+
+int gskyhip_compute_mask(const void *data, int dtype, int64_t n, const gskyhip_mask *mask, uint8_t *out,
+                         void *stream) {
+  gskyhip_mask m = mask ? *mask : gskyhip_mask{};
+  m.ns = 0;
+  MaskSpecS ms[4];
+  int r = build_mask_specs(&m, ms);
+  if (r) return r;
+  const int slot = mask_slot_h(dtype);
+  if (slot < 0) return GSKYHIP_E_MASK;
+  return launch_compute_mask(data, dtype, n, ms[slot], out, (hipStream_t)stream);
+}
+
+int gskyhip_drill_rows(int n_bands, int band_strides) { return drill_rows_per_poly(n_bands, band_strides); }
+
+int gskyhip_drill(const float *stack, int xsize, int ysize, int n_bands, int t_stride, const int32_t *win,
+                  const int64_t *mask_off, const uint8_t *masks, int n_polys, float nodata, float clip_lower,
+                  float clip_upper, int pixel_count, int band_strides, double *out_value, int32_t *out_count,
+                  void *stream) {
+  return launch_drill(stack, xsize, ysize, n_bands, t_stride, win, mask_off, masks, n_polys, nodata, clip_lower,
+                      clip_upper, pixel_count, band_strides, out_value, out_count, (hipStream_t)stream);
+}
+
+int gskyhip_drill_merge(const double *values, const int32_t *counts, int n_files, int n_dates, double *out,
+                        void *stream) {
+  return launch_drill_merge(values, counts, n_files, n_dates, out, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,33 @@
+// render.h -- host launchers of render.hip (batched GetMap path).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gskyhip.h"
+
+namespace gsky {
+
+struct MaskSpecS;
+
+int64_t render_workspace_size(int n_tiles, int n_pairs, int max_h);
+
+// Shared planning: pairs, tiles, rows.  Returns 0 or an error.
+struct RenderCall {
+  const gskyhip_granule *granules; int n_granules;
+  const gskyhip_crs *crs; int n_crs; int dst_crs;
+  const gskyhip_tile *tiles; int n_tiles;
+  const int32_t *pair_granule; int n_pairs;
+  int max_w, max_h;
+  int mask_ns, mask_inclusive;
+  const MaskSpecS *mask_specs;  // 4 entries (host)
+  int resample;
+  void *workspace; int64_t workspace_bytes;
+  hipStream_t stream;
+};
+
+int launch_render(const RenderCall &c, const int32_t *out_ns, int n_out, const gskyhip_scale_params &sp,
+                  const uint8_t *ramp, uint8_t *rgba_out, void *canvas_out, int phase);
+int launch_warp_windows(const RenderCall &c, int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
+                        void *win_out, int64_t win_stride);
+
+}  // namespace gsky

@@ -1,0 +1,1308 @@
+// render.hip -- batched GetMap hot path on gfx950.
+//
+// Pipeline for a batch of tiles (one launch each, all async on one stream):
+//   plan_pairs_kernel   one wavefront per (tile, granule) pair: the window of
+//                       warp.go:154-217 (GDALSuggestedWarpOutput2 edge sampling
+//                       in 64 lanes) and the overview pick of warp.go:156-198.
+//   plan_tiles_kernel   one thread per tile: merge order of ProcessRasterStack
+//                       (tile_merger.go:281-312), maskMap links, fill/overwrite
+//                       mode of MergeMaskedRaster (tile_merger.go:47).
+//   plan_rows_kernel    one thread per (pair, window row): GDALApproxTransform
+//                       (max error 0.125) reduced to row records / leaves.
+//   render_kernel       one lane per 4 output pixels: gather (NN or bilinear)
+//                       from HBM-resident granules, ordered nodata/mask fold,
+//                       utils.Scale, palette/RGBA fill, 16-byte stores.
+// No intermediate FlexRaster ever reaches HBM on the fused path.
+#include "gsky_device.h"
+#include "render.h"
+#include "stages.h"
+#include <algorithm>
+
+namespace gsky {
+
+// Everything the planning kernels need per call.
+struct PlanArgs {
+  const gskyhip_granule *granules;
+  const gskyhip_crs *crs;
+  int n_crs;
+  int dst_crs;                 // -1: no reprojection (warp.go:143-148)
+  const gskyhip_tile *tiles;
+  int n_tiles;
+  const int32_t *pair_granule;
+  int n_pairs;
+  int pair_tile_max;           // scratch sizes
+  int max_h;
+  int mask_ns;
+  int mask_inclusive;
+  PairPlan *pairs;
+  Xform *xforms;
+  TilePlan *tplans;
+  int32_t *order;              // n_pairs: per tile, stack entries in merge order
+  int32_t *pair_tile;          // n_pairs: owning tile of each pair
+  RowRec *rows;                // n_pairs * max_h
+  Leaf *pool;
+  int32_t *counters;           // [0] pool, [1] split rows, [2] complex tiles
+  int pool_cap;
+  int64_t *split_list;         // (pair * max_h + row) of rows that need the recursion
+  int32_t *complex_list;       // tiles that need exact per-pixel transforms
+};
+
+// ---------------------------------------------------------------- pair ownership
+__global__ void pair_tile_kernel(const gskyhip_tile *tiles, int n_tiles, int32_t *pair_tile) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tiles) return;
+  for (int p = tiles[t].pair_begin; p < tiles[t].pair_end; p++) pair_tile[p] = t;
+}
+
+// ---------------------------------------------------------------- wave helpers
+__device__ __forceinline__ double wave_min(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// GDALSuggestedWarpOutput2_MustAdjustFor{Right,Bottom}Border, lanes 0..20.
+__device__ bool must_adjust(const Xform &t, const double *ext, int np, int nl, double psx,
+                            double psy, bool right, int lane) {
+  bool bad = false;
+  if (lane < 21) {
+    // the reference accumulates dfRatio += 0.05 (clamped to 1.0 past 0.99
+    // for the sample points, unclamped for the expected values)
+    double r1 = 0.0, r2 = 0.0;
+    for (int k = 0; k < lane; k++) {
+      r1 += 0.05;
+      r2 += 0.05;
+    }
+    if (r1 > 0.99) r1 = 1.0;
+    double ax, ay;
+    if (right) { ax = ext[2]; ay = ext[3] - psy * r1 * nl; }
+    else { ax = ext[0] + psx * r1 * np; ay = ext[1]; }
+    bool ok1 = xform_point(t, true, ax, ay);
+    bool ok2 = ok1 ? xform_point(t, false, ax, ay) : false;
+    double ex = right ? ext[2] : ext[0] + psx * r2 * np;
+    double ey = right ? ext[3] - psy * r2 * nl : ext[1];
+    bad = !ok1 || !ok2 || fabs(ax - ex) > psx || fabs(ay - ey) > psy;
+  }
+  unsigned long long b = __ballot(bad);
+  return __popcll(b) == 21;
+}
+
+constexpr int kSteps = 20;
+constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
+
+// One wavefront (64 threads) per pair.
+__global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
+  const int p = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (p >= a.n_pairs) return;
+  __shared__ double sx[kGrid], sy[kGrid];
+  __shared__ int sok[kGrid];
+
+  const int t_idx = a.pair_tile[p];
+  const gskyhip_tile &tile = a.tiles[t_idx];
+  const int gi = a.pair_granule[p];
+  const gskyhip_granule &g = a.granules[gi];
+  Xform &xf = a.xforms[p];
+  PairPlan &pp = a.pairs[p];
+
+  // ---- transformer (warp.go:120-148)
+  Xform t;
+  t.src = a.crs[g.crs];
+  t.reproject = 0;
+  if (a.dst_crs >= 0) {
+    t.dst = a.crs[a.dst_crs];
+    t.reproject = crs_same(t.src, t.dst) ? 0 : 1;
+  } else {
+    t.dst = t.src;
+  }
+  for (int k = 0; k < 6; k++) { t.src_gt[k] = g.geot[k]; t.dst_gt[k] = tile.dst_geot[k]; }
+  inv_geot(t.src_gt, t.src_igt);
+  inv_geot(t.dst_gt, t.dst_igt);
+
+  // ---- GDALSuggestedWarpOutput2: 21 samples on each source edge
+  const int nInX = g.xsize, nInY = g.ysize;
+  const double dfStep = 1.0 / kSteps;
+  int ns = 4 * (kSteps + 1);
+  for (int k = lane; k < ns; k += 64) {
+    int i = k >> 2, e = k & 3;
+    double r = (i == kSteps) ? 1.0 : i * dfStep;
+    double x, y;
+    if (e == 0) { x = r * nInX; y = 0.0; }
+    else if (e == 1) { x = r * nInX; y = nInY; }
+    else if (e == 2) { x = 0.0; y = r * nInY; }
+    else { x = nInX; y = r * nInY; }
+    int ok = xform_point(t, false, x, y);
+    sx[k] = x; sy[k] = y; sok[k] = ok;
+  }
+  __syncthreads();
+  int failed = 0;
+  for (int k = lane; k < ns; k += 64) failed += sok[k] ? 0 : 1;
+  for (int o = 32; o > 0; o >>= 1) failed += __shfl_xor(failed, o, 64);
+  if (failed > 0) {  // full grid of the source raster
+    __syncthreads();
+    ns = kGrid;
+    for (int k = lane; k < ns; k += 64) {
+      int iy = k / (kSteps + 1), ix = k % (kSteps + 1);
+      double ry = (iy == kSteps) ? 1.0 : iy * dfStep;
+      double rx = (ix == kSteps) ? 1.0 : ix * dfStep;
+      double x = rx * nInX, y = ry * nInY;
+      int ok = xform_point(t, false, x, y);
+      sx[k] = x; sy[k] = y; sok[k] = ok;
+    }
+    __syncthreads();
+  }
+  double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
+  int got = 0;
+  for (int k = lane; k < ns; k += 64) {
+    if (!sok[k]) continue;
+    got = 1;
+    mnx = fmin(mnx, sx[k]); mny = fmin(mny, sy[k]);
+    mxx = fmax(mxx, sx[k]); mxy = fmax(mxy, sy[k]);
+  }
+  mnx = wave_min(mnx); mny = wave_min(mny); mxx = wave_max(mxx); mxy = wave_max(mxy);
+  got = __ballot(got) != 0ull;
+
+  int err = 1;
+  double ext[4] = {0, 0, 0, 0}, psx = 0, psy = 0;
+  int nPixels = 0, nLines = 0;
+  if (got) {
+    double dX = 0, dY = 0;
+    if (sok[0] && sok[ns - 1]) { dX = sx[ns - 1] - sx[0]; dY = sy[ns - 1] - sy[0]; }
+    if (dX == 0.0 || dY == 0.0) { dX = mxx - mnx; dY = mxy - mny; }
+    const double diag = sqrt(dX * dX + dY * dY);
+    const double ps = diag / sqrt((double)nInX * nInX + (double)nInY * nInY);
+    const double dfPixels = (mxx - mnx) / ps;
+    const double dfLines = (mxy - mny) / ps;
+    if (dfPixels <= 2147483646.0 && dfLines <= 2147483646.0) {
+      err = 0;
+      nPixels = (int)(dfPixels + 0.5);
+      nLines = (int)(dfLines + 0.5);
+      psx = ps; psy = ps;
+      const double ratios[5] = {0.000, 0.001, 0.010, 0.100, 1.000};
+      for (int k = 0; k < 5; k++) {
+        const double tryx = psx - psx * ratios[k] / nPixels;
+        double e[4] = {mnx, mxy - nLines * psy, mnx + nPixels * tryx, mxy};
+        if (!must_adjust(t, e, nPixels, nLines, tryx, psy, true, lane)) { psx = tryx; break; }
+      }
+      for (int k = 0; k < 5; k++) {
+        const double tryy = psy - psy * ratios[k] / nLines;
+        double e[4] = {mnx, mxy - nLines * tryy, mnx + nPixels * psx, mxy};
+        if (!must_adjust(t, e, nPixels, nLines, psx, tryy, false, lane)) { psy = tryy; break; }
+      }
+      ext[0] = mnx;
+      ext[1] = mxy - nLines * psy;
+      ext[2] = mnx + nPixels * psx;
+      ext[3] = mxy;
+    }
+  }
+  if (lane != 0) return;
+
+  // ---- overview pick (warp.go:156-198)
+  const void *band = g.data;
+  int bandX = g.xsize, bandY = g.ysize;
+  if (err == 0 && g.n_ovr > 0) {
+    const double targetRatio = 1.0 / psx;
+    if (targetRatio > 1.0) {
+      int iOvr = -1;
+      for (; iOvr < g.n_ovr - 1; iOvr++) {
+        double ovrRatio = 1.0;
+        if (iOvr >= 0) ovrRatio = (double)nInX / g.ovr_xsize[iOvr];
+        const double nextOvrRatio = (double)nInX / g.ovr_xsize[iOvr + 1];
+        if (ovrRatio < targetRatio && nextOvrRatio > targetRatio) break;
+        const double diff = ovrRatio - targetRatio;
+        if (diff > -1e-1 && diff < 1e-1) break;
+      }
+      if (iOvr >= 0) {
+        band = g.ovr_data[iOvr];
+        bandX = g.ovr_xsize[iOvr];
+        bandY = g.ovr_ysize[iOvr];
+        t.src_gt[1] *= nInX / (double)bandX;
+        t.src_gt[2] *= nInX / (double)bandX;
+        t.src_gt[4] *= nInY / (double)bandY;
+        t.src_gt[5] *= nInY / (double)bandY;
+        inv_geot(t.src_gt, t.src_igt);
+      }
+    }
+  }
+
+  // ---- window (warp.go:200-217; roundCoord 69-80)
+  auto round_coord = [](double c, int maxExtent) {
+    int r;
+    if (c < 0) r = 0;
+    else {
+      r = (int)(c + 1e-10);
+      if (r > maxExtent - 1) r = maxExtent - 1;
+    }
+    return r;
+  };
+  int xoff = 0, yoff = 0, w = tile.width, h = tile.height;
+  if (err == 0) {
+    const int minX = round_coord(ext[0], w), minY = round_coord(ext[1], h);
+    const int maxX = round_coord(ext[2] + 0.5, w), maxY = round_coord(ext[3] + 0.5, h);
+    xoff = minX; yoff = minY;
+    w = maxX - minX + 1;
+    h = maxY - minY + 1;
+  }
+
+  xf = t;
+  for (int k = 0; k < 6; k++) { pp.src_gt[k] = t.src_gt[k]; pp.src_igt[k] = t.src_igt[k]; }
+  pp.band = band;
+  pp.band_x = bandX; pp.band_y = bandY;
+  pp.xoff = xoff; pp.yoff = yoff; pp.w = w; pp.h = h;
+  pp.granule = gi; pp.tile = t_idx;
+  pp.src_dtype = g.dtype;
+  const bool supported = g.dtype == GSKYHIP_BYTE || g.dtype == GSKYHIP_INT16 ||
+                         g.dtype == GSKYHIP_UINT16 || g.dtype == GSKYHIP_FLOAT32;
+  int odt = supported ? g.dtype : GSKYHIP_FLOAT32;
+  pp.signed_byte = (odt == GSKYHIP_BYTE && g.signed_byte) ? 1 : 0;
+  if (pp.signed_byte) odt = GSKYHIP_SIGNEDBYTE;
+  pp.out_dtype = odt;
+  pp.ns = g.ns;
+  pp.is_mask = (a.mask_ns >= 0 && g.ns == a.mask_ns) ? 1 : 0;
+  pp.in_stack = (!pp.is_mask || a.mask_inclusive) ? 1 : 0;
+  pp.fill_mode = 0;
+  pp.mask_pair = -1;
+  pp.status = 0;
+  pp.nodata = g.nodata;
+  pp.has_nodata = g.has_nodata;
+  pp.fill = gdal_copy_to(g.nodata, odt);
+  pp.ts = g.timestamp;
+  pp.stamp = g.timestamp + (double)g.polygon_hash;
+}
+
+// ---------------------------------------------------------------- merge order
+// One thread per tile.  Mirrors RasterMerger.Run for the tile's batch.
+__global__ void plan_tiles_kernel(PlanArgs a) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.n_tiles) return;
+  const gskyhip_tile &tile = a.tiles[t];
+  TilePlan tp;
+  tp.n_entries = 0;
+  tp.status = 0;
+  tp.complex = 0;
+  tp._pad = 0;
+  double canvas_ts[4];
+  for (int k = 0; k < 4; k++) { tp.created[k] = 0; tp.dtype[k] = 0; tp.nodata[k] = 0; canvas_ts[k] = 0; }
+  const int b = tile.pair_begin, e = tile.pair_end;
+  int32_t *ord = a.order + b;
+  // stack entries; stable insertion sort by geoStamp descending (keys sorted
+  // descending, rasters of one key in arrival order: tile_merger.go:286-290)
+  int n = 0;
+  for (int p = b; p < e; p++) {
+    if (!a.pairs[p].in_stack) continue;
+    const double s = a.pairs[p].stamp;
+    int j = n;
+    while (j > 0 && a.pairs[ord[j - 1]].stamp < s) { ord[j] = ord[j - 1]; j--; }
+    ord[j] = p;
+    n++;
+  }
+  tp.n_entries = n;
+  for (int k = 0; k < n; k++) {
+    PairPlan &pp = a.pairs[ord[k]];
+    // maskMap[geoStamp]: the last mask raster of that key (tile_merger.go:478-484)
+    int mp = -1;
+    for (int q = b; q < e; q++)
+      if (a.pairs[q].is_mask && a.pairs[q].stamp == pp.stamp) mp = q;
+    pp.mask_pair = mp;
+    if (mp >= 0) {
+      const PairPlan &mq = a.pairs[mp];
+      const int mdt = mq.out_dtype;
+      if (!(mdt == GSKYHIP_SIGNEDBYTE || mdt == GSKYHIP_BYTE || mdt == GSKYHIP_INT16 || mdt == GSKYHIP_UINT16))
+        tp.status = GSKYHIP_E_MASK;       // "Type %s cannot contain a bit mask"
+      else if ((long)pp.w * pp.h > (long)mq.w * mq.h)
+        tp.status = GSKYHIP_E_RANGE;      // mask[iSrc] out of range: Go panics
+    }
+    const int ns = pp.ns;
+    if (ns < 0 || ns >= 4) { tp.status = GSKYHIP_E_RANGE; continue; }
+    if (!tp.created[ns]) {  // tile_merger.go:291-297
+      tp.created[ns] = 1;
+      tp.dtype[ns] = pp.out_dtype;
+      tp.nodata[ns] = pp.nodata;
+      canvas_ts[ns] = 0;
+    } else if (tp.dtype[ns] != pp.out_dtype) {
+      tp.status = GSKYHIP_E_TYPE;  // the reference would reinterpret the canvas bytes
+    }
+    pp.fill_mode = pp.ts < canvas_ts[ns] ? 1 : 0;  // tile_merger.go:47
+    if (!pp.fill_mode) canvas_ts[ns] = pp.ts;
+  }
+  a.tplans[t] = tp;
+}
+
+// ---------------------------------------------------------------- row plans
+__device__ __forceinline__ void flag_complex(const PlanArgs &a, int tile) {
+  if (atomicOr(&a.tplans[tile].complex, 1) == 0) {
+    const int k = atomicAdd(&a.counters[2], 1);
+    a.complex_list[k] = tile;
+  }
+}
+
+// Light pass, one thread per (pair, window row): the three exact points of
+// GDALApproxTransform (first / middle / last) and its error test.  Rows whose
+// middle error exceeds 0.125 go to the split list (plan_split_kernel).
+__global__ __launch_bounds__(256) void plan_rows_kernel(PlanArgs a) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = (int)(gid / a.max_h);
+  const int row = (int)(gid % a.max_h);
+  if (p >= a.n_pairs) return;
+  const PairPlan &pp = a.pairs[p];
+  if (row >= pp.h) return;
+  const Xform &t = a.xforms[p];
+  RowRec rec;
+  rec.nleaf = 1; rec.pool_off = 0; rec._pad = 0;
+  for (int k = 0; k < 6; k++) rec.v[k] = 0;
+  const int n = pp.w;
+  const int nMiddle = (n - 1) / 2;
+  const double yrow = row + 0.5 + pp.yoff;
+  // GDALApproxTransform preconditions: y constant, x distinct, nPoints > 5
+  if (n <= 5) {
+    rec.kind = ROW_EXACT;
+    flag_complex(a, pp.tile);
+  } else {
+    double xs[3] = {0 + 0.5 + pp.xoff, nMiddle + 0.5 + pp.xoff, (n - 1) + 0.5 + pp.xoff};
+    double ys[3] = {yrow, yrow, yrow};
+    bool ok0 = xform_point(t, true, xs[0], ys[0]);
+    bool ok1 = xform_point(t, true, xs[1], ys[1]);
+    bool ok2 = xform_point(t, true, xs[2], ys[2]);
+    if (!(ok0 && ok1 && ok2)) {
+      rec.kind = ROW_EXACT;
+      flag_complex(a, pp.tile);
+    } else {
+      const double x0 = 0 + 0.5 + pp.xoff, xl = (n - 1) + 0.5 + pp.xoff, xm = nMiddle + 0.5 + pp.xoff;
+      const double dX = (xs[2] - xs[0]) / (xl - x0);
+      const double dY = (ys[2] - ys[0]) / (xl - x0);
+      const double dfError = fabs((xs[0] + dX * (xm - x0)) - xs[1]) + fabs((ys[0] + dY * (xm - x0)) - ys[1]);
+      if (dfError <= kMaxErr) {
+        rec.kind = ROW_LINEAR;
+        rec.v[0] = xs[0]; rec.v[1] = ys[0]; rec.v[2] = dX; rec.v[3] = dY;
+      } else {
+        rec.kind = ROW_DESCEND;  // provisional: root SME kept for the split pass
+        rec.v[0] = xs[0]; rec.v[1] = ys[0]; rec.v[2] = xs[1];
+        rec.v[3] = ys[1]; rec.v[4] = xs[2]; rec.v[5] = ys[2];
+        const int k = atomicAdd(&a.counters[1], 1);
+        a.split_list[k] = (int64_t)p * a.max_h + row;
+      }
+    }
+  }
+  a.rows[(long)p * a.max_h + row] = rec;
+}
+
+struct Node {
+  int lo, n;
+  double xs[3], ys[3];
+  int exact_leaf;  // 1: emit an exact leaf for [lo, lo+n)
+};
+
+// GDALApproxTransformInternal recursion (3.0.1) of one row, emitting ordered
+// leaves into `out` (capacity kMaxLeavesLocal).  -1 on overflow.
+__device__ __noinline__ int approx_leaves(const Xform &t, int xoff, double yrow, int n0, const double *v,
+                                          Leaf *out) {
+  Node stack[14];
+  int sp = 0, nl = 0;
+  Node cur;
+  cur.lo = 0; cur.n = n0; cur.exact_leaf = 0;
+  cur.xs[0] = v[0]; cur.ys[0] = v[1]; cur.xs[1] = v[2]; cur.ys[1] = v[3]; cur.xs[2] = v[4]; cur.ys[2] = v[5];
+  auto xpos = [&](int idx) { return idx + 0.5 + xoff; };
+  for (;;) {
+    if (cur.exact_leaf) {
+      if (nl >= kMaxLeavesLocal) return -1;
+      out[nl].start = cur.lo; out[nl].kind = 1;
+      out[nl].xs0 = out[nl].ys0 = out[nl].dX = out[nl].dY = 0;
+      nl++;
+    } else {
+      const int lo = cur.lo, n = cur.n;
+      const int nMiddle = (n - 1) / 2;
+      const double x0 = xpos(lo), xl = xpos(lo + n - 1), xm = xpos(lo + nMiddle);
+      const double dX = (cur.xs[2] - cur.xs[0]) / (xl - x0);
+      const double dY = (cur.ys[2] - cur.ys[0]) / (xl - x0);
+      const double dfError = fabs((cur.xs[0] + dX * (xm - x0)) - cur.xs[1]) +
+                             fabs((cur.ys[0] + dY * (xm - x0)) - cur.ys[1]);
+      if (dfError <= kMaxErr) {
+        if (nl >= kMaxLeavesLocal) return -1;
+        out[nl].start = lo; out[nl].kind = 0;
+        out[nl].xs0 = cur.xs[0]; out[nl].ys0 = cur.ys[0]; out[nl].dX = dX; out[nl].dY = dY;
+        nl++;
+      } else {
+        const int i0 = lo + (nMiddle - 1) / 2, i1 = lo + nMiddle - 1, i2 = lo + nMiddle + (n - nMiddle - 1) / 2;
+        double mx[3] = {xpos(i0), xpos(i1), xpos(i2)};
+        double my[3] = {yrow, yrow, yrow};
+        const bool base1 = nMiddle <= 5 || x0 == mx[1] || x0 == mx[0];
+        const bool base2 = n - nMiddle <= 5 || xm == xl || xm == mx[2];
+        bool ok = false;
+        if (!base1 && !base2) {
+          ok = xform_point(t, true, mx[0], my[0]);
+          ok = xform_point(t, true, mx[1], my[1]) && ok;
+          ok = xform_point(t, true, mx[2], my[2]) && ok;
+        } else if (!base1) {
+          ok = xform_point(t, true, mx[0], my[0]);
+          ok = xform_point(t, true, mx[1], my[1]) && ok;
+        } else if (!base2) {
+          ok = xform_point(t, true, mx[2], my[2]);
+        }
+        if (!ok) {  // the whole node is transformed exactly
+          if (nl >= kMaxLeavesLocal) return -1;
+          out[nl].start = lo; out[nl].kind = 1;
+          out[nl].xs0 = out[nl].ys0 = out[nl].dX = out[nl].dY = 0;
+          nl++;
+        } else {
+          if (sp >= 14) return -1;
+          Node &h2 = stack[sp++];  // second half deferred, first half next
+          h2.lo = lo + nMiddle; h2.n = n - nMiddle;
+          h2.exact_leaf = base2 ? 1 : 0;
+          h2.xs[0] = cur.xs[1]; h2.ys[0] = cur.ys[1];
+          h2.xs[1] = mx[2]; h2.ys[1] = my[2];
+          h2.xs[2] = cur.xs[2]; h2.ys[2] = cur.ys[2];
+          Node h1;
+          h1.lo = lo; h1.n = nMiddle;
+          h1.exact_leaf = base1 ? 1 : 0;
+          h1.xs[0] = cur.xs[0]; h1.ys[0] = cur.ys[0];
+          h1.xs[1] = mx[0]; h1.ys[1] = my[0];
+          h1.xs[2] = mx[1]; h1.ys[2] = my[1];
+          cur = h1;
+          continue;
+        }
+      }
+    }
+    if (sp == 0) break;
+    cur = stack[--sp];
+  }
+  return nl;
+}
+
+// Split pass over the rows the light pass could not interpolate in one
+// piece: leaves into the pool (ROW_POOL) or, on pool overflow, ROW_DESCEND.
+__global__ __launch_bounds__(64) void plan_split_kernel(PlanArgs a) {
+  const int nsplit = a.counters[1];
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nsplit; k += gridDim.x * blockDim.x) {
+    const int64_t key = a.split_list[k];
+    const int p = (int)(key / a.max_h), row = (int)(key % a.max_h);
+    const PairPlan &pp = a.pairs[p];
+    RowRec &rec = a.rows[key];
+    const double yrow = row + 0.5 + pp.yoff;
+    Leaf local[kMaxLeavesLocal];
+    const int nl = approx_leaves(a.xforms[p], pp.xoff, yrow, pp.w, rec.v, local);
+    int off = -1;
+    if (nl > 0) {
+      off = atomicAdd(&a.counters[0], nl);
+      if (off + nl > a.pool_cap) off = -1;
+    }
+    bool exact = off < 0;
+    if (off >= 0) {
+      for (int j = 0; j < nl; j++) { a.pool[off + j] = local[j]; exact = exact || local[j].kind != 0; }
+      rec.kind = ROW_POOL;
+      rec.nleaf = nl;
+      rec.pool_off = off;
+    }
+    if (exact) flag_complex(a, pp.tile);
+  }
+}
+
+// ---------------------------------------------------------------- sampling
+// Full per-pixel path (exact points, descend): only complex tiles and the
+// drop-in window kernel run it.
+__device__ __noinline__ bool descend_coords(const Xform &t, int xoff, double yrow, int n0, const double *v,
+                                            int i, double &sx, double &sy) {
+  int lo = 0, n = n0;
+  double xs[3] = {v[0], v[2], v[4]}, ys[3] = {v[1], v[3], v[5]};
+  auto xpos = [&](int idx) { return idx + 0.5 + xoff; };
+  for (;;) {
+    const int nMiddle = (n - 1) / 2;
+    const double x0 = xpos(lo), xl = xpos(lo + n - 1), xm = xpos(lo + nMiddle);
+    const double dX = (xs[2] - xs[0]) / (xl - x0);
+    const double dY = (ys[2] - ys[0]) / (xl - x0);
+    const double dfError = fabs((xs[0] + dX * (xm - x0)) - xs[1]) + fabs((ys[0] + dY * (xm - x0)) - ys[1]);
+    if (dfError <= kMaxErr) {
+      const double dist = xpos(i) - x0;
+      sy = ys[0] + dY * dist;
+      sx = xs[0] + dX * dist;
+      return true;
+    }
+    const int i0 = lo + (nMiddle - 1) / 2, i1 = lo + nMiddle - 1, i2 = lo + nMiddle + (n - nMiddle - 1) / 2;
+    double mx[3] = {xpos(i0), xpos(i1), xpos(i2)};
+    double my[3] = {yrow, yrow, yrow};
+    const bool base1 = nMiddle <= 5 || x0 == mx[1] || x0 == mx[0];
+    const bool base2 = n - nMiddle <= 5 || xm == xl || xm == mx[2];
+    bool ok = false;
+    if (!base1 && !base2) {
+      ok = xform_point(t, true, mx[0], my[0]);
+      ok = xform_point(t, true, mx[1], my[1]) && ok;
+      ok = xform_point(t, true, mx[2], my[2]) && ok;
+    } else if (!base1) {
+      ok = xform_point(t, true, mx[0], my[0]);
+      ok = xform_point(t, true, mx[1], my[1]) && ok;
+    } else if (!base2) {
+      ok = xform_point(t, true, mx[2], my[2]);
+    }
+    const bool first = (i - lo) < nMiddle;
+    if (!ok || (first && base1) || (!first && base2)) {
+      sx = xpos(i); sy = yrow;
+      return xform_point(t, true, sx, sy);
+    }
+    if (first) {
+      n = nMiddle;
+      xs[1] = mx[0]; ys[1] = my[0]; xs[2] = mx[1]; ys[2] = my[1];
+    } else {
+      xs[0] = xs[1]; ys[0] = ys[1];
+      xs[1] = mx[2]; ys[1] = my[2];
+      lo = lo + nMiddle;
+      n = n - nMiddle;
+    }
+  }
+}
+
+__device__ __noinline__ bool exact_coords(const Xform &t, int xoff, int yoff, int i, int row, double &sx,
+                                          double &sy) {
+  sx = i + 0.5 + xoff;
+  sy = row + 0.5 + yoff;
+  return xform_point(t, true, sx, sy);
+}
+
+// Source coordinates of window pixel (i, row).  GENERAL=false: the row is
+// LINEAR or POOL with linear leaves only (simple tiles).
+template <bool GENERAL>
+__device__ __forceinline__ bool src_coords(const RowRec &rr, const Leaf *pool, const Xform *xf, int xoff,
+                                           int yoff, int w, int i, int row, double &sx, double &sy) {
+  if (rr.kind == ROW_LINEAR) {
+    const double dist = (double)i;
+    sy = rr.v[1] + rr.v[3] * dist;
+    sx = rr.v[0] + rr.v[2] * dist;
+    return true;
+  }
+  if (rr.kind == ROW_POOL) {
+    const Leaf *lv = pool + rr.pool_off;
+    int k = 0;
+    while (k + 1 < rr.nleaf && lv[k + 1].start <= i) k++;
+    const Leaf &L = lv[k];
+    if (!GENERAL || L.kind == 0) {
+      const double dist = (double)(i - L.start);
+      sy = L.ys0 + L.dY * dist;
+      sx = L.xs0 + L.dX * dist;
+      return true;
+    }
+  }
+  if (GENERAL) {
+    if (rr.kind == ROW_DESCEND) return descend_coords(*xf, xoff, row + 0.5 + yoff, w, rr.v, i, sx, sy);
+    return exact_coords(*xf, xoff, yoff, i, row, sx, sy);
+  }
+  return false;
+}
+
+// Load one source value as a Val of the pair's output dtype (warp.go:339-343).
+__device__ __forceinline__ Val load_val(const void *band, int src_dtype, long idx) {
+  Val o;
+  switch (src_dtype) {
+    case GSKYHIP_BYTE: o.i = ((const uint8_t *)band)[idx]; break;
+    case GSKYHIP_INT16: o.i = ((const int16_t *)band)[idx]; break;
+    case GSKYHIP_UINT16: o.i = ((const uint16_t *)band)[idx]; break;
+    case GSKYHIP_FLOAT32: o.f = ((const float *)band)[idx]; break;
+    case GSKYHIP_INT32: o = gdal_copy_to((double)((const int32_t *)band)[idx], GSKYHIP_FLOAT32); break;
+    case GSKYHIP_UINT32: o = gdal_copy_to((double)((const uint32_t *)band)[idx], GSKYHIP_FLOAT32); break;
+    case GSKYHIP_FLOAT64: o = gdal_copy_to(((const double *)band)[idx], GSKYHIP_FLOAT32); break;
+    default: o.u = 0; break;
+  }
+  return o;
+}
+__device__ __forceinline__ double load_dbl(const void *band, int src_dtype, long idx, int signed_byte) {
+  switch (src_dtype) {
+    case GSKYHIP_BYTE: return signed_byte ? (double)((const int8_t *)band)[idx] : (double)((const uint8_t *)band)[idx];
+    case GSKYHIP_INT16: return ((const int16_t *)band)[idx];
+    case GSKYHIP_UINT16: return ((const uint16_t *)band)[idx];
+    case GSKYHIP_FLOAT32: return ((const float *)band)[idx];
+    case GSKYHIP_INT32: return ((const int32_t *)band)[idx];
+    case GSKYHIP_UINT32: return ((const uint32_t *)band)[idx];
+    case GSKYHIP_FLOAT64: return ((const double *)band)[idx];
+    default: return 0;
+  }
+}
+
+// GWKBilinearResample4Sample semantics (SURVEY 8a parity targets).
+__device__ __noinline__ Val bilinear_value(const PairPlan &pp, double sx, double sy) {
+  int iSrcX = (int)floor(sx - 0.5);
+  int iSrcY = (int)floor(sy - 0.5);
+  double rX = 1.5 - (sx - iSrcX);
+  double rY = 1.5 - (sy - iSrcY);
+  if (iSrcX == -1) { iSrcX = 0; rX = 1; }
+  if (iSrcY == -1) { iSrcY = 0; rY = 1; }
+  double accR = 0.0, accDiv = 0.0;
+  const int xs4[4] = {iSrcX, iSrcX + 1, iSrcX, iSrcX + 1};
+  const int ys4[4] = {iSrcY, iSrcY, iSrcY + 1, iSrcY + 1};
+  const double w4[4] = {rX * rY, (1.0 - rX) * rY, rX * (1.0 - rY), (1.0 - rX) * (1.0 - rY)};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (xs4[k] < 0 || xs4[k] >= pp.band_x || ys4[k] < 0 || ys4[k] >= pp.band_y) continue;
+    const double v = load_dbl(pp.band, pp.src_dtype, (long)ys4[k] * pp.band_x + xs4[k], pp.signed_byte);
+    if (pp.has_nodata && (v == pp.nodata || (pp.nodata != pp.nodata && v != v))) continue;
+    accDiv += w4[k];
+    accR += v * w4[k];
+  }
+  double r;
+  if (accDiv == 1.0) r = accR;
+  else if (accDiv < 0.00001) return pp.fill;
+  else r = accR / accDiv;
+  if (pp.out_dtype == GSKYHIP_FLOAT32) { Val o; o.f = (float)r; return o; }
+  return gdal_copy_to(floor(r + 0.5), pp.out_dtype);
+}
+
+// Warped value of window pixel (i,row) of a pair: the source value or the
+// window's nodata fill (warp.go:246-247, 271-344).
+template <bool GENERAL, int RES>
+__device__ __forceinline__ Val warped_value(const PairPlan &pp, const RowRec &rr, const Leaf *pool,
+                                            const Xform *xf, int i, int row) {
+  double sx, sy;
+  const bool ok = src_coords<GENERAL>(rr, pool, xf, pp.xoff, pp.yoff, pp.w, i, row, sx, sy);
+  if (!ok) return pp.fill;
+  if (RES == GSKYHIP_RESAMPLE_BILINEAR) return bilinear_value(pp, sx, sy);
+  if (sx < 0 || sy < 0) return pp.fill;
+  const double ax = sx + 1.0e-10, ay = sy + 1.0e-10;
+  if (ax >= 2147483647.0 || ay >= 2147483647.0) return pp.fill;
+  const int ix = (int)ax, iy = (int)ay;
+  if (ix >= pp.band_x || iy >= pp.band_y) return pp.fill;
+  Val v = load_val(pp.band, pp.src_dtype, (long)iy * pp.band_x + ix);
+  if (pp.out_dtype == GSKYHIP_SIGNEDBYTE) v.i = (int32_t)(int8_t)(uint8_t)v.i;
+  return v;
+}
+
+// ---------------------------------------------------------------- ComputeMask
+// mask spec per mask-raster dtype: 0 SignedByte, 1 Byte, 2 Int16, 3 UInt16
+__device__ __forceinline__ int mask_slot(int dtype) {
+  switch (dtype) {
+    case GSKYHIP_SIGNEDBYTE: return 0;
+    case GSKYHIP_BYTE: return 1;
+    case GSKYHIP_INT16: return 2;
+    case GSKYHIP_UINT16: return 3;
+    default: return -1;
+  }
+}
+
+__device__ __forceinline__ bool mask_bit(const MaskSpecS &m, int dtype, int32_t v) {
+  if (m.has_value) {
+    int32_t a = v & m.value;
+    switch (dtype) {
+      case GSKYHIP_SIGNEDBYTE: return (int8_t)a > 0;
+      case GSKYHIP_INT16: return (int16_t)a > 0;
+      case GSKYHIP_BYTE: return (uint8_t)a > 0;
+      default: return (uint16_t)a > 0;
+    }
+  }
+  for (int j = 0; j < m.n_tests; j++) {
+    int32_t a = v & m.filt[j];
+    bool eq;
+    switch (dtype) {
+      case GSKYHIP_SIGNEDBYTE: eq = (int8_t)a == (int8_t)m.want[j]; break;
+      case GSKYHIP_INT16: eq = (int16_t)a == (int16_t)m.want[j]; break;
+      case GSKYHIP_BYTE: eq = (uint8_t)a == (uint8_t)m.want[j]; break;
+      default: eq = (uint16_t)a == (uint16_t)m.want[j]; break;
+    }
+    if (eq) return true;
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------- scale
+// utils.scale (raster_scaler.go:30-332) constants of one canvas.
+struct ScaleK {
+  int32_t dtype;
+  int32_t colour_scale;
+  Val noData, off, clp;  // in the canvas type
+  float sc;
+  double nodata64;
+};
+
+// Go math.Log / Log2 / Log10 (Go 1.12, same op sequence as the amd64 asm).
+__device__ __noinline__ double go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (x != x || x == INFINITY) return x;
+  if (x < 0) return NAN;
+  if (x == 0) return -INFINITY;
+  int ki;
+  double f1 = frexp(x, &ki);
+  if (f1 < 1.41421356237309504880168872420969808 / 2) { f1 *= 2; ki--; }
+  double f = f1 - 1;
+  double k = (double)ki;
+  double s = f / (2 + f);
+  double s2 = s * s;
+  double s4 = s2 * s2;
+  double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  double R = t1 + t2;
+  double hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+__device__ __noinline__ double go_log10(double x) {
+  int e;
+  double frac = frexp(x, &e);
+  double l2;
+  if (frac == 0.5) l2 = (double)(e - 1);
+  else l2 = go_log(frac) * (1.0 / 0.693147180559945309417232121458176568) + (double)e;
+  return l2 * 0.301029995663981195213738894724493026768189881462108541310;
+}
+
+// normalise() (raster_scaler.go:15-28); returns false when the value maps to nodata
+__device__ __forceinline__ bool normalise_f(float &value, int colour_scale, double nodata64) {
+  double d = (double)value;
+  if (!(d == nodata64)) {
+    if (colour_scale == 1) d = go_log10(d);
+    if (isinf(d) || d != d) d = nodata64;
+  }
+  if (d == nodata64) return false;
+  value = (float)d;
+  return true;
+}
+
+__device__ __forceinline__ uint8_t scale_px(const ScaleK &k, Val v) {
+  if (k.dtype == GSKYHIP_FLOAT32) {
+    float value = v.f;
+    if (value == k.noData.f) return 0xFF;
+    if (k.colour_scale > 0 && !normalise_f(value, k.colour_scale, k.nodata64)) return 0xFF;
+    value += k.off.f;
+    if (value > k.clp.f) value = k.clp.f;
+    if (value < 0.0f) value = 0.0f;
+    return go_f32_u8(value * k.sc);
+  }
+  int32_t value = v.i;
+  if (value == k.noData.i) return 0xFF;
+  switch (k.dtype) {  // value += offset in the raster's own type (wraps)
+    case GSKYHIP_SIGNEDBYTE: value = (int8_t)(value + k.off.i); break;
+    case GSKYHIP_BYTE: value = (uint8_t)(value + k.off.i); break;
+    case GSKYHIP_INT16: value = (int16_t)(value + k.off.i); break;
+    default: value = (uint16_t)(value + k.off.i); break;
+  }
+  if (value > k.clp.i) value = k.clp.i;
+  if (value < 0) value = 0;
+  return go_f32_u8((float)value * k.sc);
+}
+
+// Scale constants of a canvas; auto mode takes min/max from the fold pass
+// (raster_scaler.go:47-78 and its typed siblings).
+__device__ inline ScaleK make_scale(int dtype, double nodata, const gskyhip_scale_params &sp, bool autom,
+                                    float minVal, float maxVal) {
+  ScaleK k;
+  k.dtype = dtype;
+  k.colour_scale = sp.colour_scale;
+  k.nodata64 = nodata;
+  float sc = (float)sp.scale;
+  if (sc <= 0.0f) sc = (sp.clip <= 0.0) ? 1.0f : (float)(254.0f / (float)sp.clip);
+  k.noData = go_conv_to(nodata, dtype);
+  if (dtype == GSKYHIP_FLOAT32) {
+    k.off.f = (float)sp.offset;
+    k.clp.f = (float)sp.clip;
+    if (autom) {
+      if (minVal == maxVal) maxVal += 0.1f;
+      sc = 254.0f / (maxVal - minVal);
+      k.off.f = -minVal;
+      k.clp.f = maxVal + k.off.f;
+    }
+  } else {
+    k.off = go_conv_to(sp.offset, dtype);
+    k.clp = go_conv_to(sp.clip, dtype);
+    if (autom) {
+      if (minVal == maxVal) maxVal += 0.1f;
+      sc = 254.0f / (maxVal - minVal);
+      const float dfOffset = -minVal;
+      k.off = go_conv_to((double)dfOffset, dtype);
+      k.clp = go_conv_to((double)(maxVal + dfOffset), dtype);
+    }
+  }
+  k.sc = sc;
+  return k;
+}
+
+// ordered-int encoding of float for atomic min/max
+__device__ __forceinline__ int32_t fenc(float f) {
+  int32_t i = __float_as_int(f);
+  return i ^ ((i >> 31) & 0x7FFFFFFF);
+}
+__device__ __forceinline__ float fdec(int32_t i) { return __int_as_float(i ^ ((i >> 31) & 0x7FFFFFFF)); }
+
+// Per (tile, out ns) auto-scale reduction state.
+struct MinMax {
+  int32_t mn, mx;      // fenc, over valid non-NaN values
+  int32_t p0_valid;    // pixel 0 valid (not nodata, and log-normalisable)
+  float p0;            // its (normalised) value
+};
+
+__device__ __forceinline__ void auto_minmax(const MinMax &m, float &mn, float &mx) {
+  // min/max start at 0 unless pixel 0 is valid (raster_scaler.go:55-58)
+  if (m.p0_valid) {
+    if (m.p0 != m.p0) { mn = m.p0; mx = m.p0; }
+    else { mn = fdec(m.mn); mx = fdec(m.mx); }
+  } else {
+    mn = fminf(0.0f, fdec(m.mn));
+    mx = fmaxf(0.0f, fdec(m.mx));
+  }
+}
+
+struct RenderArgs {
+  const PairPlan *pairs;
+  const Xform *xforms;
+  const TilePlan *tplans;
+  const int32_t *order;
+  const gskyhip_tile *tiles;
+  const RowRec *rows;
+  const Leaf *pool;
+  const int32_t *counters;
+  const int32_t *complex_list;
+  int max_h;
+  int n_tiles;
+  int rows_per_block;
+  int n_out;
+  int32_t out_ns[3];
+  MaskSpecS mask[4];
+  gskyhip_scale_params sp;
+  int autom;
+  const uint32_t *ramp;  // 256 packed RGBA or NULL
+  uint8_t *rgba;
+  uint8_t *canvas;       // optional typed canvases
+  long canvas_tile_stride, canvas_ns_stride;
+  MinMax *minmax;        // n_tiles * 3
+  int write_rgba;
+};
+
+// Mask bit for data pair `pp` at its window pixel (ic, ir): mask[iSrc] with
+// iSrc the data window's linear index (tile_merger.go:53/64), read from the
+// warped mask raster of the same geoStamp.
+template <bool GENERAL, int RES>
+__device__ __forceinline__ bool mask_at(const RenderArgs &a, const PairPlan &pp, int ic, int ir) {
+  const int mp = pp.mask_pair;
+  const PairPlan &mq = a.pairs[mp];
+  const long iSrc = (long)ir * pp.w + ic;
+  const int mx = (int)(iSrc % mq.w), my = (int)(iSrc / mq.w);
+  if (my >= mq.h) return false;  // Go would panic; plan_tiles flags it
+  const int slot = mask_slot(mq.out_dtype);
+  if (slot < 0) return false;    // flagged in plan_tiles (not a bit-mask type)
+  const RowRec &mr = a.rows[(long)mp * a.max_h + my];
+  Val v = warped_value<GENERAL, RES>(mq, mr, a.pool, a.xforms + mp, mx, my);
+  return mask_bit(a.mask[slot], mq.out_dtype, v.i);
+}
+
+// Fused warp + merge (+ scale + palette) of a band of rows of one tile: each
+// wave walks rows, each lane 4 consecutive pixels of a 256-pixel chunk.
+template <int NOUT, int RES, bool MASK, bool GENERAL>
+__device__ __forceinline__ void render_band(const RenderArgs &a, int t, int band0, const uint32_t *s_ramp) {
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const gskyhip_tile &tile = a.tiles[t];
+  const TilePlan &tp = a.tplans[t];
+  const int W = tile.width, H = tile.height;
+  const int32_t *ord = a.order + tile.pair_begin;
+  const int n_entries = tp.n_entries;
+
+  Val cnod[NOUT];
+  bool cfloat[NOUT];
+  ScaleK sk[NOUT];
+  bool all_created = true;
+#pragma unroll
+  for (int s = 0; s < NOUT; s++) {
+    const int ns = a.out_ns[s];
+    all_created = all_created && tp.created[ns] != 0;
+    cfloat[s] = tp.dtype[ns] == GSKYHIP_FLOAT32;
+    cnod[s] = go_conv_to(tp.nodata[ns], tp.dtype[ns]);
+    sk[s] = make_scale(tp.dtype[ns], tp.nodata[ns], a.sp, false, 0.f, 0.f);
+  }
+  for (int r = band0 + wave; r < band0 + a.rows_per_block && r < H; r += 4) {
+    for (int cx = 0; cx < W; cx += 256) {
+      const int x0 = cx + lane * 4;
+      Val c[NOUT][4];
+#pragma unroll
+      for (int s = 0; s < NOUT; s++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) c[s][q] = cnod[s];
+      for (int e = 0; e < n_entries; e++) {
+        const int p = ord[e];
+        const PairPlan &pp = a.pairs[p];
+        if (r < pp.yoff || r >= pp.yoff + pp.h) continue;
+        if (cx + 256 <= pp.xoff || cx >= pp.xoff + pp.w) continue;
+        int s = -1;
+#pragma unroll
+        for (int k = 0; k < NOUT; k++) if (a.out_ns[k] == pp.ns) s = k;
+        if (s < 0) continue;  // merged into a canvas that is not rendered
+        const int ir = r - pp.yoff;
+        const RowRec &rr = a.rows[(long)p * a.max_h + ir];
+        const Val nd = go_conv_to(pp.nodata, pp.out_dtype);
+        const bool isf = pp.out_dtype == GSKYHIP_FLOAT32;
+        const bool fill = pp.fill_mode != 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int ic = x0 + q - pp.xoff;
+          if (x0 + q >= W || ic < 0 || ic >= pp.w) continue;
+          const Val v = warped_value<GENERAL, RES>(pp, rr, a.pool, a.xforms + p, ic, ir);
+          if (val_eq(v, nd, isf)) continue;
+          if (MASK && pp.mask_pair >= 0 && mask_at<GENERAL, RES>(a, pp, ic, ir)) continue;
+#pragma unroll
+          for (int k = 0; k < NOUT; k++) {
+            if (k != s) continue;
+            if (fill && !val_eq(c[k][q], nd, isf)) continue;
+            c[k][q] = v;
+          }
+        }
+      }
+      if (x0 >= W) continue;
+      // typed canvases (tile_merger.go:562-652) and the auto-scale reduction
+      if (a.canvas) {
+#pragma unroll
+        for (int s = 0; s < NOUT; s++) {
+          const int dsz = type_size(tp.dtype[a.out_ns[s]]);
+          uint8_t *cb = a.canvas + t * a.canvas_tile_stride + s * a.canvas_ns_stride;
+          for (int q = 0; q < 4 && x0 + q < W; q++) {
+            const long idx = (long)r * W + x0 + q;
+            if (dsz == 1) cb[idx] = (uint8_t)c[s][q].i;
+            else if (dsz == 2) ((uint16_t *)cb)[idx] = (uint16_t)c[s][q].i;
+            else ((uint32_t *)cb)[idx] = c[s][q].u;
+          }
+        }
+      }
+      if (!a.write_rgba) {
+        if (a.autom) {
+#pragma unroll
+          for (int s = 0; s < NOUT; s++) {
+            const int ns = a.out_ns[s];
+            float mn = INFINITY, mx = -INFINITY;
+            for (int q = 0; q < 4 && x0 + q < W; q++) {
+              const Val v = c[s][q];
+              if (val_eq(v, cnod[s], cfloat[s])) continue;
+              float f = cfloat[s] ? v.f : (float)v.i;
+              if (cfloat[s] && a.sp.colour_scale > 0 && !normalise_f(f, a.sp.colour_scale, tp.nodata[ns])) continue;
+              if (r == 0 && x0 + q == 0) {
+                a.minmax[t * 3 + s].p0_valid = 1;
+                a.minmax[t * 3 + s].p0 = f;
+              }
+              if (f == f) { mn = fminf(mn, f); mx = fmaxf(mx, f); }
+            }
+            int32_t emn = fenc(mn), emx = fenc(mx);
+            for (int o = 32; o > 0; o >>= 1) {
+              emn = min(emn, __shfl_xor(emn, o, 64));
+              emx = max(emx, __shfl_xor(emx, o, 64));
+            }
+            if (lane == 0) {
+              if (emn != fenc(INFINITY)) atomicMin(&a.minmax[t * 3 + s].mn, emn);
+              if (emx != fenc(-INFINITY)) atomicMax(&a.minmax[t * 3 + s].mx, emx);
+            }
+          }
+        }
+        continue;
+      }
+      // utils.Scale + EncodePNG pixel loop
+      uint32_t px[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        uint32_t o = 0;
+        if (all_created) {
+          if (NOUT == 1) {
+            const uint8_t b = scale_px(sk[0], c[0][q]);
+            if (b != 0xFF) o = a.ramp ? s_ramp[b] : (0xFF000000u | ((uint32_t)b << 16) | ((uint32_t)b << 8) | b);
+          } else {
+            const uint8_t rr = scale_px(sk[0], c[0][q]);
+            const uint8_t gg = scale_px(sk[NOUT > 1 ? 1 : 0], c[NOUT > 1 ? 1 : 0][q]);
+            const uint8_t bb = scale_px(sk[NOUT > 2 ? 2 : 0], c[NOUT > 2 ? 2 : 0][q]);
+            if (rr != 0xFF || gg != 0xFF || bb != 0xFF)
+              o = 0xFF000000u | ((uint32_t)bb << 16) | ((uint32_t)gg << 8) | rr;
+          }
+        }
+        px[q] = o;
+      }
+      uint8_t *dst = a.rgba + ((long)t * H * W + (long)r * W + x0) * 4;
+      if (x0 + 3 < W && ((((uintptr_t)dst) & 15) == 0)) {
+        *(uint4 *)dst = make_uint4(px[0], px[1], px[2], px[3]);
+      } else {
+        for (int q = 0; q < 4 && x0 + q < W; q++) ((uint32_t *)dst)[q] = px[q];
+      }
+    }
+  }
+}
+
+// Simple tiles: every row LINEAR / linear leaves.  Grid n_tiles * bands.
+template <int NOUT, int RES, bool MASK>
+__global__ __launch_bounds__(256) void render_fast_kernel(RenderArgs a) {
+  __shared__ uint32_t s_ramp[256];
+  if (a.ramp) s_ramp[threadIdx.x] = a.ramp[threadIdx.x];
+  __syncthreads();
+  const int bands_per_tile = (a.max_h + a.rows_per_block - 1) / a.rows_per_block;
+  const int t = blockIdx.x / bands_per_tile;
+  if (t >= a.n_tiles || a.tplans[t].complex) return;
+  render_band<NOUT, RES, MASK, false>(a, t, (blockIdx.x % bands_per_tile) * a.rows_per_block, s_ramp);
+}
+
+// Complex tiles (exact points, recursion leftovers), from the device list.
+template <int NOUT, int RES, bool MASK>
+__global__ __launch_bounds__(256) void render_general_kernel(RenderArgs a) {
+  __shared__ uint32_t s_ramp[256];
+  if (a.ramp) s_ramp[threadIdx.x] = a.ramp[threadIdx.x];
+  __syncthreads();
+  const int bands_per_tile = (a.max_h + a.rows_per_block - 1) / a.rows_per_block;
+  const int items = a.counters[2] * bands_per_tile;
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int t = a.complex_list[it / bands_per_tile];
+    render_band<NOUT, RES, MASK, true>(a, t, (it % bands_per_tile) * a.rows_per_block, s_ramp);
+  }
+}
+
+// Scale + RGBA from typed canvases (auto-scale second pass).
+__global__ __launch_bounds__(256) void canvas_rgba_kernel(RenderArgs a) {
+  __shared__ uint32_t s_ramp[256];
+  const int tid = threadIdx.x;
+  if (a.ramp) s_ramp[tid] = a.ramp[tid];
+  __syncthreads();
+  const int bands_per_tile = (a.max_h + a.rows_per_block - 1) / a.rows_per_block;
+  const int t = blockIdx.x / bands_per_tile;
+  const int band0 = (blockIdx.x % bands_per_tile) * a.rows_per_block;
+  if (t >= a.n_tiles) return;
+  const gskyhip_tile tile = a.tiles[t];
+  const TilePlan tp = a.tplans[t];
+  const int W = tile.width, H = tile.height, n_out = a.n_out;
+  ScaleK sk[3];
+  bool all_created = true;
+  for (int s = 0; s < n_out; s++) {
+    const int ns = a.out_ns[s];
+    all_created = all_created && tp.created[ns];
+    if (!tp.created[ns]) continue;
+    float mn = 0.0f, mx = 0.0f;
+    if (a.autom) auto_minmax(a.minmax[t * 3 + s], mn, mx);
+    sk[s] = make_scale(tp.dtype[ns], tp.nodata[ns], a.sp, a.autom != 0, mn, mx);
+  }
+  for (int r = band0; r < band0 + a.rows_per_block && r < H; r++) {
+    for (int x = tid; x < W; x += 256) {
+      const long idx = (long)r * W + x;
+      uint8_t b[3] = {0xFF, 0xFF, 0xFF};
+      if (all_created) {
+        for (int s = 0; s < n_out; s++) {
+          const int dt = tp.dtype[a.out_ns[s]];
+          const uint8_t *cb = a.canvas + t * a.canvas_tile_stride + s * a.canvas_ns_stride;
+          Val v;
+          switch (dt) {
+            case GSKYHIP_SIGNEDBYTE: v.i = ((const int8_t *)cb)[idx]; break;
+            case GSKYHIP_BYTE: v.i = cb[idx]; break;
+            case GSKYHIP_INT16: v.i = ((const int16_t *)cb)[idx]; break;
+            case GSKYHIP_UINT16: v.i = ((const uint16_t *)cb)[idx]; break;
+            default: v.u = ((const uint32_t *)cb)[idx]; break;
+          }
+          b[s] = scale_px(sk[s], v);
+        }
+      }
+      uint32_t o = 0;
+      if (all_created) {
+        if (n_out == 1) {
+          if (b[0] != 0xFF) o = a.ramp ? s_ramp[b[0]] : (0xFF000000u | ((uint32_t)b[0] << 16) | ((uint32_t)b[0] << 8) | b[0]);
+        } else if (b[0] != 0xFF || b[1] != 0xFF || b[2] != 0xFF) {
+          o = 0xFF000000u | ((uint32_t)b[2] << 16) | ((uint32_t)b[1] << 8) | b[0];
+        }
+      }
+      ((uint32_t *)(a.rgba + (long)t * H * W * 4))[idx] = o;
+    }
+  }
+}
+
+__global__ void minmax_init_kernel(MinMax *m, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  m[i].mn = fenc(INFINITY);
+  m[i].mx = fenc(-INFINITY);
+  m[i].p0_valid = 0;
+  m[i].p0 = 0.0f;
+}
+
+// Warped window of each pair (the FlexRaster data of tile_grpc.go:228-241).
+template <int RES>
+__global__ __launch_bounds__(256) void warp_window_kernel(const PairPlan *pairs, const Xform *xforms,
+                                                          const RowRec *rows, const Leaf *pool, int max_h,
+                                                          int max_w, int n_pairs, uint8_t *out, long stride) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per = (long)max_h * max_w;
+  const int p = (int)(gid / per);
+  if (p >= n_pairs) return;
+  const PairPlan &pp = pairs[p];
+  const long k = gid % per;
+  const int row = (int)(k / max_w), i = (int)(k % max_w);
+  if (row >= pp.h || i >= pp.w) return;
+  const RowRec &rr = rows[(long)p * max_h + row];
+  const Val v = warped_value<true, RES>(pp, rr, pool, xforms + p, i, row);
+  const int dsz = type_size(pp.out_dtype);
+  uint8_t *o = out + p * stride;
+  const long idx = (long)row * pp.w + i;
+  if (dsz == 1) o[idx] = (uint8_t)v.i;
+  else if (dsz == 2) ((uint16_t *)o)[idx] = (uint16_t)v.i;
+  else ((uint32_t *)o)[idx] = v.u;
+}
+
+__global__ void pair_meta_kernel(const PairPlan *pairs, int n_pairs, int32_t *bbox, int32_t *dtype, double *nodata) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  const PairPlan &pp = pairs[p];
+  bbox[4 * p] = pp.xoff; bbox[4 * p + 1] = pp.yoff; bbox[4 * p + 2] = pp.w; bbox[4 * p + 3] = pp.h;
+  dtype[p] = pp.out_dtype;
+  nodata[p] = pp.nodata;
+}
+
+}  // namespace gsky
+
+// ======================================================================== host
+namespace gsky {
+
+static inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+struct Carve {
+  PairPlan *pairs; Xform *xforms; TilePlan *tplans; int32_t *order; int32_t *pair_tile;
+  RowRec *rows; Leaf *pool; int32_t *counters; MinMax *minmax; int64_t *split_list; int32_t *complex_list;
+  int pool_cap;
+  int64_t total;
+};
+
+// Workspace layout; PairPlan[] first and TilePlan[] third are relied upon by
+// host.cpp (drop-in geotransform read-back, gskyhip_render_status).
+static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
+  Carve c;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) { int64_t o = off; off = align256(off + bytes); return o; };
+  const int np = n_pairs > 0 ? n_pairs : 1, nt = n_tiles > 0 ? n_tiles : 1;
+  c.pool_cap = (int)std::min<int64_t>((int64_t)np * max_h / 2 + 4096, 64 << 20);
+  const int64_t o_pairs = take(sizeof(PairPlan) * (int64_t)np);
+  const int64_t o_xf = take(sizeof(Xform) * (int64_t)np);
+  const int64_t o_tp = take(sizeof(TilePlan) * (int64_t)nt);
+  const int64_t o_ord = take(sizeof(int32_t) * (int64_t)np);
+  const int64_t o_pt = take(sizeof(int32_t) * (int64_t)np);
+  const int64_t o_rows = take(sizeof(RowRec) * (int64_t)np * max_h);
+  const int64_t o_pool = take(sizeof(Leaf) * (int64_t)c.pool_cap);
+  const int64_t o_cnt = take(256);
+  const int64_t o_mm = take(sizeof(MinMax) * (int64_t)nt * 3);
+  const int64_t o_split = take(sizeof(int64_t) * (int64_t)np * max_h);
+  const int64_t o_cl = take(sizeof(int32_t) * (int64_t)nt);
+  c.total = off;
+  char *b = (char *)base;
+  c.pairs = (PairPlan *)(b + o_pairs);
+  c.xforms = (Xform *)(b + o_xf);
+  c.tplans = (TilePlan *)(b + o_tp);
+  c.order = (int32_t *)(b + o_ord);
+  c.pair_tile = (int32_t *)(b + o_pt);
+  c.rows = (RowRec *)(b + o_rows);
+  c.pool = (Leaf *)(b + o_pool);
+  c.counters = (int32_t *)(b + o_cnt);
+  c.minmax = (MinMax *)(b + o_mm);
+  c.split_list = (int64_t *)(b + o_split);
+  c.complex_list = (int32_t *)(b + o_cl);
+  return c;
+}
+
+int64_t render_workspace_size(int n_tiles, int n_pairs, int max_h) {
+  return carve(nullptr, n_tiles, n_pairs, max_h).total;
+}
+
+static int plan_all(const RenderCall &rc, Carve &cv) {
+  if (rc.n_tiles <= 0) return 0;
+  if (!rc.workspace || rc.workspace_bytes < render_workspace_size(rc.n_tiles, rc.n_pairs, rc.max_h))
+    return GSKYHIP_E_ARG;
+  cv = carve(rc.workspace, rc.n_tiles, rc.n_pairs, rc.max_h);
+  PlanArgs a;
+  a.granules = rc.granules; a.crs = rc.crs; a.n_crs = rc.n_crs; a.dst_crs = rc.dst_crs;
+  a.tiles = rc.tiles; a.n_tiles = rc.n_tiles; a.pair_granule = rc.pair_granule; a.n_pairs = rc.n_pairs;
+  a.pair_tile_max = 0; a.max_h = rc.max_h; a.mask_ns = rc.mask_ns; a.mask_inclusive = rc.mask_inclusive;
+  a.pairs = cv.pairs; a.xforms = cv.xforms; a.tplans = cv.tplans; a.order = cv.order;
+  a.pair_tile = cv.pair_tile; a.rows = cv.rows; a.pool = cv.pool; a.counters = cv.counters;
+  a.pool_cap = cv.pool_cap; a.split_list = cv.split_list; a.complex_list = cv.complex_list;
+  hipStream_t s = rc.stream;
+  if (hipMemsetAsync(cv.counters, 0, 256, s) != hipSuccess) return GSKYHIP_E_HIP;
+  hipLaunchKernelGGL(pair_tile_kernel, dim3((rc.n_tiles + 255) / 256), dim3(256), 0, s, rc.tiles, rc.n_tiles,
+                     cv.pair_tile);
+  if (rc.n_pairs > 0) hipLaunchKernelGGL(plan_pairs_kernel, dim3(rc.n_pairs), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(plan_tiles_kernel, dim3((rc.n_tiles + 127) / 128), dim3(128), 0, s, a);
+  if (rc.n_pairs > 0) {
+    const int64_t nthreads = (int64_t)rc.n_pairs * rc.max_h;
+    hipLaunchKernelGGL(plan_rows_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(plan_split_kernel, dim3(1024), dim3(64), 0, s, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+}
+
+template <int NOUT, int RES, bool MASK>
+static void launch_render_kernels(const RenderArgs &a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((render_fast_kernel<NOUT, RES, MASK>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((render_general_kernel<NOUT, RES, MASK>), dim3(512), dim3(256), 0, s, a);
+}
+
+template <int NOUT>
+static void dispatch_render(const RenderArgs &a, int resample, bool mask, dim3 grid, hipStream_t s) {
+  if (resample == GSKYHIP_RESAMPLE_BILINEAR) {
+    if (mask) launch_render_kernels<NOUT, GSKYHIP_RESAMPLE_BILINEAR, true>(a, grid, s);
+    else launch_render_kernels<NOUT, GSKYHIP_RESAMPLE_BILINEAR, false>(a, grid, s);
+  } else {
+    if (mask) launch_render_kernels<NOUT, GSKYHIP_RESAMPLE_NEAREST, true>(a, grid, s);
+    else launch_render_kernels<NOUT, GSKYHIP_RESAMPLE_NEAREST, false>(a, grid, s);
+  }
+}
+
+int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const gskyhip_scale_params &sp,
+                  const uint8_t *ramp, uint8_t *rgba_out, void *canvas_out, int phase) {
+  if (n_out != 1 && n_out != 3) return GSKYHIP_E_ARG;  // ogc_encoders.go:135-136
+  for (int k = 0; k < n_out; k++) if (out_ns[k] < 0 || out_ns[k] >= 4) return GSKYHIP_E_ARG;
+  if (rc.resample != GSKYHIP_RESAMPLE_NEAREST && rc.resample != GSKYHIP_RESAMPLE_BILINEAR) return GSKYHIP_E_ARG;
+  // rgba_out == NULL: canvases only (WCS GetCoverage, FusionUnscale, ows.go:728)
+  const bool autom = rgba_out && sp.offset == 0.0 && sp.scale == 0.0 && sp.clip == 0.0;
+  if ((autom || !rgba_out) && !canvas_out) return GSKYHIP_E_ARG;
+  if (rc.n_tiles <= 0) return 0;
+  Carve cv;
+  if (phase != 2) {  // 0: plan + render, 1: plan only, 2: render only (plan done)
+    int rcode = plan_all(rc, cv);
+    if (rcode || phase == 1) return rcode;
+  } else {
+    if (!rc.workspace || rc.workspace_bytes < render_workspace_size(rc.n_tiles, rc.n_pairs, rc.max_h))
+      return GSKYHIP_E_ARG;
+    cv = carve(rc.workspace, rc.n_tiles, rc.n_pairs, rc.max_h);
+  }
+  RenderArgs a;
+  a.pairs = cv.pairs; a.xforms = cv.xforms; a.tplans = cv.tplans; a.order = cv.order;
+  a.tiles = rc.tiles; a.rows = cv.rows; a.pool = cv.pool; a.counters = cv.counters;
+  a.complex_list = cv.complex_list; a.max_h = rc.max_h;
+  a.n_tiles = rc.n_tiles; a.rows_per_block = 16; a.n_out = n_out;
+  for (int k = 0; k < 3; k++) a.out_ns[k] = k < n_out ? out_ns[k] : -1;
+  for (int k = 0; k < 4; k++) a.mask[k] = rc.mask_specs[k];
+  a.sp = sp;
+  a.autom = autom ? 1 : 0;
+  a.ramp = (const uint32_t *)ramp;
+  a.rgba = rgba_out;
+  a.canvas = (uint8_t *)canvas_out;
+  a.canvas_ns_stride = (long)rc.max_w * rc.max_h * 4;
+  a.canvas_tile_stride = a.canvas_ns_stride * n_out;
+  a.minmax = cv.minmax;
+  const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
+  const dim3 grid((unsigned)(rc.n_tiles * bands));
+  hipStream_t s = rc.stream;
+  const bool mask = rc.mask_ns >= 0;
+  if (autom) {
+    hipLaunchKernelGGL(minmax_init_kernel, dim3((rc.n_tiles * 3 + 255) / 256), dim3(256), 0, s, cv.minmax,
+                       rc.n_tiles * 3);
+    a.write_rgba = 0;
+  } else {
+    a.write_rgba = rgba_out ? 1 : 0;
+  }
+  if (n_out == 1) dispatch_render<1>(a, rc.resample, mask, grid, s);
+  else dispatch_render<3>(a, rc.resample, mask, grid, s);
+  if (autom) {
+    a.write_rgba = 1;
+    hipLaunchKernelGGL(canvas_rgba_kernel, grid, dim3(256), 0, s, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+}
+
+int launch_warp_windows(const RenderCall &rc, int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
+                        void *win_out, int64_t win_stride) {
+  Carve cv;
+  int rcode = plan_all(rc, cv);
+  if (rcode || rc.n_pairs <= 0) return rcode;
+  hipStream_t s = rc.stream;
+  hipLaunchKernelGGL(pair_meta_kernel, dim3((rc.n_pairs + 255) / 256), dim3(256), 0, s, cv.pairs, rc.n_pairs,
+                     bbox_out, dtype_out, nodata_out);
+  const int64_t nthreads = (int64_t)rc.n_pairs * rc.max_h * rc.max_w;
+  const dim3 grid((unsigned)((nthreads + 255) / 256));
+  if (rc.resample == GSKYHIP_RESAMPLE_BILINEAR)
+    hipLaunchKernelGGL(warp_window_kernel<GSKYHIP_RESAMPLE_BILINEAR>, grid, dim3(256), 0, s, cv.pairs, cv.xforms,
+                       cv.rows, cv.pool, rc.max_h, rc.max_w, rc.n_pairs, (uint8_t *)win_out, (long)win_stride);
+  else
+    hipLaunchKernelGGL(warp_window_kernel<GSKYHIP_RESAMPLE_NEAREST>, grid, dim3(256), 0, s, cv.pairs, cv.xforms,
+                       cv.rows, cv.pool, rc.max_h, rc.max_w, rc.n_pairs, (uint8_t *)win_out, (long)win_stride);
+  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+}
+
+}  // namespace gsky

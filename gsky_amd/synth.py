@@ -1,0 +1,406 @@
+"""Synthetic workloads of BASELINE.json's configs.
+
+There is no network and no NCI data, so every granule is generated from a
+splitmix64 stream (per-granule seed 0x6A5D0000 + k) with the shapes, CRSs,
+nodata patterns and timestamps the survey fixes.  Each generator takes a
+`scale` so tests can run the same geometry at sizes the CPU oracle finishes in
+seconds; scale=1 is the full benchmark size.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+SEED0 = 0x6A5D0000
+PALETTE_GSKY = [(0, 100, 0, 255), (255, 255, 0, 255), (160, 82, 45, 255)]  # docker/gsky_config.json:26-31
+WEBMERC_A = 6378137.0
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser over uint64 counters (vectorised)."""
+    with np.errstate(over="ignore"):
+        z = (x + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def uniform01(h: np.ndarray) -> np.ndarray:
+    return (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+# ---------------------------------------------------------------- projections for setup only
+# (tile grids and indexer footprints; the warp itself runs in libgskyhip.so)
+def merc_fwd(lon, lat):
+    lon = np.radians(lon)
+    lat = np.radians(lat)
+    return WEBMERC_A * lon, WEBMERC_A * np.log(np.tan(np.pi / 4 + lat / 2))
+
+
+def merc_inv(x, y):
+    return np.degrees(x / WEBMERC_A), np.degrees(np.pi / 2 - 2 * np.arctan(np.exp(-y / WEBMERC_A)))
+
+
+class _Aea:
+    """EPSG:3577 (GRS80, lat1 -18, lat2 -36, lon0 132) for setup geometry."""
+
+    def __init__(self):
+        a, rf = 6378137.0, 298.257222101
+        f = 1 / rf
+        self.a, self.es = a, 2 * f - f * f
+        self.e = math.sqrt(self.es)
+        self.lam0 = math.radians(132.0)
+        p1, p2 = math.radians(-18.0), math.radians(-36.0)
+        m = lambda p: math.cos(p) / math.sqrt(1 - self.es * math.sin(p) ** 2)
+        q = self.q
+        self.n = (m(p1) ** 2 - m(p2) ** 2) / (q(math.sin(p2)) - q(math.sin(p1)))
+        self.c = m(p1) ** 2 + self.n * q(math.sin(p1))
+        self.rho0 = math.sqrt(self.c) / self.n
+
+    def q(self, s):
+        e, es = self.e, self.es
+        return (1 - es) * (s / (1 - es * s * s) - (0.5 / e) * np.log((1 - e * s) / (1 + e * s)))
+
+    def inv(self, x, y):
+        x = np.asarray(x, float) / self.a
+        y = self.rho0 - np.asarray(y, float) / self.a
+        rho = np.hypot(x, y)
+        if self.n < 0:
+            rho, x, y = -rho, -x, -y
+        qv = (self.c - (rho * self.n) ** 2) / self.n
+        phi = np.arcsin(qv / 2)
+        for _ in range(10):
+            s = np.sin(phi)
+            con = self.e * s
+            com = 1 - con * con
+            phi = phi + 0.5 * com * com / np.cos(phi) * (
+                qv / (1 - self.es) - s / com + 0.5 / self.e * np.log((1 - con) / (1 + con)))
+        lam = np.arctan2(x, y) / self.n + self.lam0
+        return np.degrees(lam), np.degrees(phi)
+
+
+AEA = _Aea()
+SINU_R = 6371007.181
+
+
+def sinu_inv(x, y):
+    lat = y / SINU_R
+    return np.degrees(x / (SINU_R * np.cos(lat))), np.degrees(lat)
+
+
+# ---------------------------------------------------------------- containers
+@dataclass
+class SynthGranule:
+    data: np.ndarray
+    geot: List[float]
+    srs: str
+    nodata: Optional[float]
+    timestamp: float = 0.0
+    polygon: str = ""
+    namespace: str = ""
+    overviews: List[np.ndarray] = field(default_factory=list)
+
+
+@dataclass
+class SynthConfig:
+    name: str
+    granules: List[SynthGranule]
+    dst_srs: str
+    tiles: List[Tuple[Tuple[float, float, float, float], int, int]]
+    pairs: List[List[int]]
+    namespaces: List[str]
+    scale: Tuple[float, float, float, int]   # offset, scale, clip, colour_scale
+    palette: Optional[list]
+    resample: int = 0
+    mask: Optional[dict] = None
+
+    @property
+    def out_pixels(self) -> int:
+        return sum(w * h for (_, w, h) in self.tiles)
+
+
+def _footprint_merc(g: SynthGranule, n=16):
+    """Granule footprint (edge samples) in EPSG:3857 -> bbox."""
+    h, w = g.data.shape
+    gt = g.geot
+    t = np.linspace(0.0, 1.0, n)
+    px = np.concatenate([t * w, t * w, np.zeros(n), np.full(n, w)])
+    py = np.concatenate([np.zeros(n), np.full(n, h), t * h, t * h])
+    X = gt[0] + px * gt[1] + py * gt[2]
+    Y = gt[3] + px * gt[4] + py * gt[5]
+    if g.srs == "EPSG:3577":
+        lon, lat = AEA.inv(X, Y)
+    elif g.srs == "EPSG:4326":
+        lon, lat = X, np.clip(Y, -85.05, 85.05)
+    else:
+        lon, lat = sinu_inv(X, Y)
+        lon = np.clip(lon, -180, 180)
+    mx, my = merc_fwd(lon, lat)
+    return mx.min(), my.min(), mx.max(), my.max()
+
+
+def _index_pairs(cfg_granules, tiles):
+    """The indexer's granule list per tile (MAS intersects; bbox test)."""
+    fps = [_footprint_merc(g) for g in cfg_granules]
+    pairs = []
+    for (bb, _, _) in tiles:
+        lst = []
+        for k, f in enumerate(fps):
+            if f[0] < bb[2] and f[2] > bb[0] and f[1] < bb[3] and f[3] > bb[1]:
+                lst.append(k)
+        pairs.append(lst)
+    return pairs
+
+
+def _grid_tiles(bbox, n_x, n_y, px):
+    tw = (bbox[2] - bbox[0]) / n_x
+    th = (bbox[3] - bbox[1]) / n_y
+    tiles = []
+    for j in range(n_y):
+        for i in range(n_x):
+            x0 = bbox[0] + i * tw
+            y1 = bbox[3] - j * th
+            tiles.append(((x0, y1 - th, x0 + tw, y1), px, px))
+    return tiles
+
+
+# ---------------------------------------------------------------- C1
+C1_BBOX = (15028131.257091936, -7514065.628545966, 17532819.79994059, -5009377.085697312)
+
+
+def config_c1(scale: float = 1.0) -> SynthConfig:
+    """Single 256x256 EPSG:3857 GetMap tile from one EPSG:4326 float32 granule."""
+    W, H = int(round(3600 * scale)), int(round(1800 * scale))
+    res = 360.0 / W
+    k = 0
+    idx = np.arange(W * H, dtype=np.uint64).reshape(H, W) + np.uint64((SEED0 + k) << 32)
+    hh = splitmix64(idx)
+    lon = -180 + res * (np.arange(W) + 0.5)
+    lat = 90 - res * (np.arange(H) + 0.5)
+    v = 500 + 400 * np.sin(np.pi * lon[None, :] / 45) * np.cos(np.pi * lat[:, None] / 30)
+    v = v + (uniform01(hh) * 10 - 5)
+    nod = uniform01(splitmix64(hh)) < 0.01
+    v = v.astype(np.float32)
+    v[nod] = -9999.0
+    g = SynthGranule(v, [-180.0, res, 0.0, 90.0, 0.0, -res], "EPSG:4326", -9999.0, 1577836800.0,
+                     "POLYGON ((-180 -90,-180 90,180 90,180 -90,-180 -90))")
+    tiles = [(C1_BBOX, 256, 256)]
+    return SynthConfig("C1", [g], "EPSG:3857", tiles, [[0]], [""], (0.0, 0.0, 1000.0, 0), None)
+
+
+# ---------------------------------------------------------------- C2
+def config_c2(scale: float = 1.0, tiles_per_side: int = 64, tile_px: int = 512, grid: int = 4) -> SynthConfig:
+    """Batch of EPSG:3857 tiles from `grid`^2 Albers EPSG:3577 int16 granules
+    (full size: 16 x 4000^2 at 25 m, 64 x 64 tiles of 512^2)."""
+    n = int(round(4000 * scale))
+    psize = 100000.0 / n        # a granule always spans 100 km
+    granules = []
+    for j in range(grid):
+        for i in range(grid):
+            k = j * grid + i
+            x0 = 1400000.0 + 95000.0 * i
+            y0 = -3800000.0 - 95000.0 * j
+            idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + k) << 32)
+            v = (splitmix64(idx) % np.uint64(10000)).astype(np.int16)
+            nb = (n + 63) // 64
+            bidx = np.arange(nb * nb, dtype=np.uint64) + np.uint64(((SEED0 + k) << 32) | 0xB10C0000)
+            blk = (uniform01(splitmix64(bidx)) < 0.1).reshape(nb, nb)
+            mask = np.repeat(np.repeat(blk, 64, 0), 64, 1)[:n, :n]
+            v[mask] = -999
+            poly = "POLYGON ((%.1f %.1f,%.1f %.1f,%.1f %.1f,%.1f %.1f,%.1f %.1f))" % (
+                x0, y0, x0 + 100000, y0, x0 + 100000, y0 - 100000, x0, y0 - 100000, x0, y0)
+            granules.append(SynthGranule(v, [x0, psize, 0.0, y0, 0.0, -psize], "EPSG:3577", -999.0,
+                                         1577836800.0 + 86400.0 * k, poly))
+    # union bbox forward-projected to EPSG:3857
+    ux0, uy1 = 1400000.0, -3800000.0
+    ux1 = 1400000.0 + 95000.0 * (grid - 1) + 100000.0
+    uy0 = -3800000.0 - 95000.0 * (grid - 1) - 100000.0
+    t = np.linspace(0, 1, 64)
+    X = np.concatenate([ux0 + t * (ux1 - ux0)] * 2 + [np.full(64, ux0), np.full(64, ux1)])
+    Y = np.concatenate([np.full(64, uy0), np.full(64, uy1)] + [uy0 + t * (uy1 - uy0)] * 2)
+    lon, lat = AEA.inv(X, Y)
+    mx, my = merc_fwd(lon, lat)
+    bbox = (float(np.floor(mx.min())), float(np.floor(my.min())), float(np.ceil(mx.max())),
+            float(np.ceil(my.max())))
+    tiles = _grid_tiles(bbox, tiles_per_side, tiles_per_side, tile_px)
+    pairs = _index_pairs(granules, tiles)
+    return SynthConfig("C2", granules, "EPSG:3857", tiles, pairs, [""], (0.0, 0.0, 10000.0, 0), PALETTE_GSKY)
+
+
+def subset(cfg: SynthConfig, tile_ids) -> SynthConfig:
+    """The same config restricted to some tiles (for bounded CPU samples)."""
+    tiles = [cfg.tiles[i] for i in tile_ids]
+    pairs = [cfg.pairs[i] for i in tile_ids]
+    return SynthConfig(cfg.name, cfg.granules, cfg.dst_srs, tiles, pairs, cfg.namespaces, cfg.scale,
+                       cfg.palette, cfg.resample, cfg.mask)
+
+
+def mpix(cfg: SynthConfig) -> float:
+    return cfg.out_pixels / 1e6
+
+
+# ---------------------------------------------------------------- C3
+def config_c3(scale: float = 1.0, chunk_px: int = 1024, grid: int = 8, out_px: int = 16384) -> SynthConfig:
+    """WCS GetCoverage: EPSG:4326 float32 granules (8x8 over lon 112..154,
+    lat -44..-10, 2048^2 each at full size) -> EPSG:3857 float32 bilinear
+    mosaic of out_px^2, split in chunk_px^2 chunks (utils/config.go:55-56)."""
+    n = max(8, int(round(2048 * scale)))
+    lon0, lon1, lat0, lat1 = 112.0, 154.0, -44.0, -10.0
+    gw, gh = (lon1 - lon0) / grid, (lat1 - lat0) / grid
+    granules = []
+    for j in range(grid):
+        for i in range(grid):
+            k = j * grid + i
+            x0, y0 = lon0 + i * gw, lat1 - j * gh
+            rx, ry = gw / n, gh / n
+            lon = x0 + rx * (np.arange(n) + 0.5)
+            lat = y0 - ry * (np.arange(n) + 0.5)
+            idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + k) << 32)
+            hh = splitmix64(idx)
+            v = 200.0 + 50.0 * np.sin(lon[None, :] / 3.0) * np.cos(lat[:, None] / 2.0) + uniform01(hh)
+            v = v.astype(np.float32)
+            v[uniform01(splitmix64(hh)) < 0.01] = -9999.0
+            poly = "POLYGON ((%g %g,%g %g,%g %g,%g %g,%g %g))" % (x0, y0, x0 + gw, y0, x0 + gw, y0 - gh, x0,
+                                                                  y0 - gh, x0, y0)
+            granules.append(SynthGranule(v, [x0, rx, 0.0, y0, 0.0, -ry], "EPSG:4326", -9999.0, 1577836800.0,
+                                         poly))
+    mx0, my0 = merc_fwd(lon0, lat0)
+    mx1, my1 = merc_fwd(lon1, lat1)
+    bbox = (float(mx0), float(my0), float(mx1), float(my1))
+    nch = max(1, out_px // chunk_px)
+    tiles = _grid_tiles(bbox, nch, nch, chunk_px)
+    pairs = _index_pairs(granules, tiles)
+    return SynthConfig("C3", granules, "EPSG:3857", tiles, pairs, [""], (0.0, 1.0, 0.0, 0), None, resample=1)
+
+
+# ---------------------------------------------------------------- C5
+MODIS_T = 1111950.5197665
+MODIS_X0, MODIS_Y0 = -20015109.354, 10007554.677
+
+
+def _webmerc_tile_bbox(z, x, y):
+    n = 2 ** z
+    span = 2 * math.pi * WEBMERC_A
+    x0 = -math.pi * WEBMERC_A + x * span / n
+    y1 = math.pi * WEBMERC_A - y * span / n
+    return (x0, y1 - span / n, x0 + span / n, y1)
+
+
+def config_c5(scale: float = 1.0, dates: int = 4, h_range=(25, 33), v_range=(8, 16), zooms=((4, 11, 8, 4), (5, 22, 16, 8)),
+              tile_px: int = 512) -> SynthConfig:
+    """Zoomed-out MODIS sinusoidal -> EPSG:3857 overview tiles: int16 data +
+    uint8 QA granules (mask value "00000001", not inclusive), overview
+    pyramids /2 down to 75^2 at full size, grey byte scaling (clip 10000)."""
+    n = max(16, int(round(2400 * scale)))
+    px = MODIS_T / n
+    granules = []
+    k = 0
+    for d in range(dates):
+        for v in range(*v_range):
+            for h in range(*h_range):
+                x0 = MODIS_X0 + h * MODIS_T
+                y0 = MODIS_Y0 - v * MODIS_T
+                idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + k) << 32)
+                hh = splitmix64(idx)
+                data = (hh % np.uint64(10000)).astype(np.int16)
+                nb = (n + 31) // 32
+                bidx = np.arange(nb * nb, dtype=np.uint64) + np.uint64(((SEED0 + k) << 32) | 0x0A000000)
+                blk = (uniform01(splitmix64(bidx)) < 0.15).reshape(nb, nb)
+                qa = np.repeat(np.repeat(blk, 32, 0), 32, 1)[:n, :n].astype(np.uint8)
+                qa |= (((hh >> np.uint64(20)) & np.uint64(0x7E)).astype(np.uint8))  # other bits noise
+                ovr_d, ovr_q = [], []
+                lvl = 1
+                while n // (2 ** lvl) >= max(4, int(round(75 * scale))):
+                    s = 2 ** lvl
+                    ovr_d.append(np.ascontiguousarray(data[::s, ::s][: n // s, : n // s]))
+                    ovr_q.append(np.ascontiguousarray(qa[::s, ::s][: n // s, : n // s]))
+                    lvl += 1
+                poly = "MODIS h%02dv%02d" % (h, v)
+                ts = 1577836800.0 + 8 * 86400.0 * d
+                gt = [x0, px, 0.0, y0, 0.0, -px]
+                granules.append(SynthGranule(data, gt, "MODIS", -28672.0, ts, poly, "", ovr_d))
+                granules.append(SynthGranule(qa, gt, "MODIS", 255.0, ts, poly, "qa", ovr_q))
+                k += 1
+    tiles = []
+    for (z, x0t, y0t, cnt) in zooms:
+        for yy in range(y0t, y0t + cnt):
+            for xx in range(x0t, x0t + cnt):
+                tiles.append((_webmerc_tile_bbox(z, xx, yy), tile_px, tile_px))
+    pairs = _index_pairs(granules, tiles)
+    return SynthConfig("C5", granules, "EPSG:3857", tiles, pairs, [""], (0.0, 0.0, 10000.0, 0), None,
+                       mask=dict(id="qa", value="00000001", inclusive=False))
+
+
+# ---------------------------------------------------------------- C4 drill
+def star_polygon(cx, cy, r, k=12, seed=0):
+    rng = np.random.default_rng(seed)
+    ang = np.linspace(0, 2 * np.pi, 2 * k, endpoint=False) + rng.uniform(0, np.pi / k)
+    rad = np.where(np.arange(2 * k) % 2 == 0, r, r * 0.5)
+    return np.stack([cx + rad * np.cos(ang), cy + rad * np.sin(ang)], 1)
+
+
+def _point_in_poly(px, py, poly):
+    inside = np.zeros(px.shape, bool)
+    n = len(poly)
+    for i in range(n):
+        x1, y1 = poly[i]
+        x2, y2 = poly[(i + 1) % n]
+        cond = ((y1 > py) != (y2 > py)) & (px < (x2 - x1) * (py - y1) / (y2 - y1 + 1e-300) + x1)
+        inside ^= cond
+    return inside
+
+
+def drill_mask(poly: np.ndarray, x0: int, y0: int, w: int, h: int) -> np.ndarray:
+    yy, xx = np.mgrid[0:h, 0:w]
+    cx = x0 + xx + 0.5
+    cy = y0 + yy + 0.5
+    m = _point_in_poly(cx, cy, poly)
+    # ALL_TOUCHED: also pixels an edge passes through (sampled along edges)
+    n = len(poly)
+    for i in range(n):
+        a, b = poly[i], poly[(i + 1) % n]
+        L = int(np.ceil(np.hypot(*(b - a)) * 4)) + 2
+        t = np.linspace(0, 1, L)
+        ex = np.floor(a[0] + t * (b[0] - a[0])).astype(int) - x0
+        ey = np.floor(a[1] + t * (b[1] - a[1])).astype(int) - y0
+        ok = (ex >= 0) & (ex < w) & (ey >= 0) & (ey < h)
+        m[ey[ok], ex[ok]] = True
+    return np.where(m, 255, 0).astype(np.uint8)
+
+
+@dataclass
+class DrillConfig:
+    bands: np.ndarray            # (n_bands, ysize, xsize) float32 (host)
+    nodata: float
+    windows: List[Tuple[int, int, int, int]]
+    masks: List[np.ndarray]
+
+
+def config_c4(n_bands: int = 365, size: int = 2048, n_polys: int = 1000, rmin=10.0, rmax=100.0,
+              seed: int = 4) -> DrillConfig:
+    """WPS drill: n_bands daily float32 slices of size^2 + star polygons."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n_bands, dtype=np.float64)
+    base = (0.2 + 0.1 * np.sin(2 * np.pi * t / 365.0)).astype(np.float32)
+    idx = np.arange(size * size, dtype=np.uint64) + np.uint64(SEED0 << 32)
+    noise = (uniform01(splitmix64(idx)) * 0.05).astype(np.float32).reshape(size, size)
+    bands = base[:, None, None] + noise[None, :, :] * (1.0 + (t[:, None, None] % 7) * 0.01).astype(np.float32)
+    bands = bands.astype(np.float32)
+    nod = uniform01(splitmix64(idx + np.uint64(1 << 40))).reshape(size, size) < 0.05
+    bands[:, nod] = -9999.0
+    wins, masks = [], []
+    for p in range(n_polys):
+        r = rng.uniform(rmin, rmax)
+        cx, cy = rng.uniform(r, size - r), rng.uniform(r, size - r)
+        poly = star_polygon(cx, cy, r, seed=p)
+        xmin, ymin = np.floor(poly.min(0)).astype(int)
+        xmax, ymax = np.floor(poly.max(0)).astype(int)
+        xmin, ymin = max(0, xmin), max(0, ymin)
+        w = min(size, xmax + 1) - xmin
+        h = min(size, ymax + 1) - ymin
+        wins.append((int(xmin), int(ymin), int(w), int(h)))
+        masks.append(drill_mask(poly, xmin, ymin, w, h))
+    return DrillConfig(bands, -9999.0, wins, masks)

@@ -1,0 +1,247 @@
+"""Batched WMS GetMap path on MI355X.
+
+Replaces, for a whole batch of output tiles at once, the per-tile chain of the
+reference: gRPC warp fan-out (processor/tile_grpc.go:200-289) ->
+warp_operation_fast (worker/gdalprocess/warp.go:82-382) -> RasterMerger
+(processor/tile_merger.go:447-738) -> utils.Scale (utils/raster_scaler.go:334)
+-> EncodePNG RGBA fill (utils/ogc_encoders.go:82-134).
+
+Granules are HBM-resident (GranuleSet); a TileBatch uploads its descriptor
+tables once and `render()` is then one asynchronous launch sequence on the
+current torch stream (capturable in a HIP graph).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+from .raster import TYPE_CODES, TYPE_NAMES, TORCH_OF, Mask, Palette, ScaleParams, fnv32a, gradient_rgba_palette
+
+DTYPE_OF_TORCH = {torch.uint8: _lib.BYTE, torch.int8: _lib.BYTE, torch.int16: _lib.INT16,
+                  torch.uint16: _lib.UINT16, torch.float32: _lib.FLOAT32, torch.int32: _lib.INT32,
+                  torch.float64: _lib.FLOAT64}
+
+
+def bbox_to_geot(width: int, height: int, bbox: Sequence[float]) -> List[float]:
+    """BBox2Geot (processor/tile_grpc.go:380-382)."""
+    return [bbox[0], (bbox[2] - bbox[0]) / float(width), 0.0, bbox[3], 0.0, (bbox[1] - bbox[3]) / float(height)]
+
+
+def parse_crs(srs: str) -> _lib.Crs:
+    c = _lib.Crs()
+    check(lib().gskyhip_crs_from_srs(srs.encode(), C.byref(c)), "SRS %r" % srs)
+    return c
+
+
+def _to_device_bytes(obj, device) -> torch.Tensor:
+    raw = np.frombuffer(bytes(obj), dtype=np.uint8).copy()
+    return torch.from_numpy(raw).to(device)
+
+
+@dataclass
+class GranuleInfo:
+    data: torch.Tensor
+    overviews: List[torch.Tensor]
+    geot: List[float]
+    srs: str
+    nodata: Optional[float]
+    timestamp: float
+    polygon: str
+    namespace: str
+    signed_byte: bool
+
+
+class GranuleSet:
+    """HBM-resident granules: the stand-in for the GDAL datasets the worker
+    opens (warp.go:89-101).  Overviews are finest first (GDALGetOverview)."""
+
+    def __init__(self, device=None):
+        self.device = torch.device(device or "cuda")
+        self.items: List[GranuleInfo] = []
+
+    def add(self, data: torch.Tensor, geot: Sequence[float], srs: str, nodata: Optional[float] = None,
+            overviews: Sequence[torch.Tensor] = (), timestamp: float = 0.0, polygon: str = "",
+            namespace: str = "", signed_byte: bool = False) -> int:
+        if data.dim() != 2:
+            raise ValueError("granule data must be 2-D (ysize, xsize)")
+        if len(overviews) > _lib.MAX_OVR:
+            raise ValueError("too many overviews")
+        d = data.to(self.device).contiguous()
+        ovr = [o.to(self.device).contiguous() for o in overviews]
+        self.items.append(GranuleInfo(d, ovr, list(geot), srs, nodata, float(timestamp), polygon, namespace,
+                                      signed_byte or data.dtype == torch.int8))
+        return len(self.items) - 1
+
+    def __len__(self):
+        return len(self.items)
+
+
+class TileBatch:
+    """A batch of GetMap tiles over a GranuleSet.
+
+    tiles: list of (bbox [minx, miny, maxx, maxy] in dst_srs, width, height).
+    pairs: per tile, the granule indices the indexer returned (MAS order).
+    namespaces: ConfigPayLoad.NameSpaces (rendered order: 1 -> palette/grey,
+    3 -> RGB); granules of `mask.id` form the mask layer."""
+
+    def __init__(self, granules: GranuleSet, dst_srs: Optional[str], tiles, pairs: Sequence[Sequence[int]],
+                 namespaces: Sequence[str] = ("",), mask: Optional[Mask] = None):
+        if len(tiles) != len(pairs):
+            raise ValueError("one granule list per tile")
+        self.granules = granules
+        self.device = granules.device
+        self.namespaces = list(namespaces)
+        self.mask = mask
+        slots = list(self.namespaces)
+        if mask is not None and mask.id not in slots:
+            slots.append(mask.id)
+        if len(slots) > 4:
+            raise ValueError("at most 4 namespace slots per batch")
+        self.slots = slots
+        # CRS table: distinct SRS strings, destination last
+        specs = []
+        for g in granules.items:
+            if g.srs not in specs:
+                specs.append(g.srs)
+        crs_list = [parse_crs(s) for s in specs]
+        self.dst_crs = -1
+        if dst_srs:
+            crs_list.append(parse_crs(dst_srs))
+            self.dst_crs = len(crs_list) - 1
+        self.n_crs = len(crs_list)
+        self._crs = _to_device_bytes((_lib.Crs * len(crs_list))(*crs_list), self.device)
+        # granule table
+        n = len(granules.items)
+        garr = (_lib.Granule * max(1, n))()
+        for i, g in enumerate(granules.items):
+            c = garr[i]
+            c.data = g.data.data_ptr()
+            c.dtype = DTYPE_OF_TORCH[g.data.dtype]
+            c.ysize, c.xsize = g.data.shape
+            c.signed_byte = int(g.signed_byte)
+            for k in range(6):
+                c.geot[k] = g.geot[k]
+            c.nodata = g.nodata if g.nodata is not None else -1e10
+            c.has_nodata = int(g.nodata is not None)
+            c.crs = specs.index(g.srs)
+            c.n_ovr = len(g.overviews)
+            for k, o in enumerate(g.overviews):
+                c.ovr_data[k] = o.data_ptr()
+                c.ovr_ysize[k], c.ovr_xsize[k] = o.shape
+            c.timestamp = g.timestamp
+            c.polygon_hash = fnv32a(g.polygon)
+            c.ns = slots.index(g.namespace) if g.namespace in slots else 3
+        self.n_granules = n
+        self._gran = _to_device_bytes(garr, self.device)
+        # tiles + pairs (CSR)
+        flat: List[int] = []
+        tarr = (_lib.Tile * max(1, len(tiles)))()
+        self.max_w = 1
+        self.max_h = 1
+        for i, (bbox, w, h) in enumerate(tiles):
+            gt = bbox_to_geot(w, h, bbox)
+            for k in range(6):
+                tarr[i].dst_geot[k] = gt[k]
+            tarr[i].width, tarr[i].height = w, h
+            tarr[i].pair_begin = len(flat)
+            flat.extend(int(p) for p in pairs[i])
+            tarr[i].pair_end = len(flat)
+            self.max_w = max(self.max_w, w)
+            self.max_h = max(self.max_h, h)
+        self.n_tiles = len(tiles)
+        self.n_pairs = len(flat)
+        self.tile_sizes = [(w, h) for (_, w, h) in tiles]
+        self._tiles = _to_device_bytes(tarr, self.device)
+        self._pairs = torch.tensor(flat if flat else [0], dtype=torch.int32, device=self.device)
+        ws = lib().gskyhip_render_workspace_size(self.n_tiles, self.n_pairs, self.max_h)
+        self._ws = torch.empty(int(ws), dtype=torch.uint8, device=self.device)
+        self._mask_c = mask.c(slots.index(mask.id)) if mask is not None else None
+
+    # ------------------------------------------------------------------ render
+    def render(self, params: ScaleParams, palette: Optional[Palette] = None, resample: int = 0,
+               out: Optional[torch.Tensor] = None, canvas: bool = False, phase: int = 0, rgba: bool = True):
+        """Warp + merge + scale + RGBA for every tile.  Returns the RGBA
+        tensor (n_tiles, H, W, 4); with canvas=True also the typed canvases
+        (n_tiles, n_out, H*W*4 bytes).  rgba=False renders canvases only (WCS).
+        phase 1 / 2 run the planning / render kernels alone (same arguments)."""
+        n_out = len(self.namespaces)
+        if n_out not in (1, 3):
+            raise ValueError("Cannot encode other than 1 or 3 namespaces into a PNG: Received %d" % n_out)
+        if rgba and out is None:
+            out = self._out if getattr(self, "_out", None) is not None else None
+            if out is None:
+                out = torch.empty((self.n_tiles, self.max_h, self.max_w, 4), dtype=torch.uint8,
+                                  device=self.device)
+                self._out = out
+        autom = rgba and params.offset == 0 and params.scale == 0 and params.clip == 0
+        cv = None
+        if canvas or autom or not rgba:
+            cv = getattr(self, "_cv", None)
+            if cv is None:
+                cv = torch.empty((self.n_tiles, n_out, self.max_h * self.max_w * 4), dtype=torch.uint8,
+                                 device=self.device)
+                self._cv = cv
+        if not hasattr(self, "_ramp_key") or self._ramp_key != id(palette):
+            ramp = gradient_rgba_palette(palette) if (palette is not None and n_out == 1) else None
+            self._ramp = torch.from_numpy(ramp).to(self.device) if ramp is not None else None
+            self._ramp_key = id(palette)
+        out_ns = (C.c_int32 * 3)(*[self.slots.index(ns) for ns in self.namespaces] + [0] * (3 - n_out))
+        sp = params.c()
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().gskyhip_render_tiles_phase(
+            phase, C.c_void_p(self._gran.data_ptr()), self.n_granules, C.c_void_p(self._crs.data_ptr()),
+            self.n_crs, self.dst_crs, C.c_void_p(self._tiles.data_ptr()), self.n_tiles,
+            C.c_void_p(self._pairs.data_ptr()), self.n_pairs, self.max_w, self.max_h, out_ns, n_out,
+            C.byref(self._mask_c) if self._mask_c is not None else None, resample, C.byref(sp),
+            C.c_void_p(self._ramp.data_ptr()) if self._ramp is not None else None,
+            C.c_void_p(out.data_ptr()) if rgba else None, C.c_void_p(cv.data_ptr()) if cv is not None else None,
+            C.c_void_p(self._ws.data_ptr()), self._ws.numel(), stream), "render_tiles")
+        if not rgba:
+            return cv
+        return (out, cv) if canvas else out
+
+    def status(self) -> int:
+        """TilePlan status of the last call (synchronous): 0 or an error code."""
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        return lib().gskyhip_render_status(C.c_void_p(self._ws.data_ptr()), self.n_tiles, self.n_pairs,
+                                           self.max_h, stream)
+
+    def canvas_view(self, cv: torch.Tensor, tile: int, k: int, type_name: str) -> torch.Tensor:
+        nb = {"Byte": 1, "SignedByte": 1, "Int16": 2, "UInt16": 2, "Float32": 4}[type_name]
+        return cv[tile, k, : self.max_w * self.max_h * nb].view(TORCH_OF[type_name]).reshape(self.max_h,
+                                                                                              self.max_w)
+
+    # ------------------------------------------------------------------ windows
+    def warp_windows(self, resample: int = 0):
+        """The FlexRasters of tile_grpc.go:228-241: per pair
+        (window tensor, bbox [xoff, yoff, w, h], type name, nodata)."""
+        npairs = self.n_pairs
+        bbox = torch.zeros((max(1, npairs), 4), dtype=torch.int32, device=self.device)
+        dt = torch.zeros(max(1, npairs), dtype=torch.int32, device=self.device)
+        nd = torch.zeros(max(1, npairs), dtype=torch.float64, device=self.device)
+        stride = self.max_w * self.max_h * 4
+        win = torch.empty((max(1, npairs), stride), dtype=torch.uint8, device=self.device)
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().gskyhip_warp_windows(
+            C.c_void_p(self._gran.data_ptr()), self.n_granules, C.c_void_p(self._crs.data_ptr()), self.n_crs,
+            self.dst_crs, C.c_void_p(self._tiles.data_ptr()), self.n_tiles, C.c_void_p(self._pairs.data_ptr()),
+            npairs, self.max_w, self.max_h, resample, C.c_void_p(bbox.data_ptr()), C.c_void_p(dt.data_ptr()),
+            C.c_void_p(nd.data_ptr()), C.c_void_p(win.data_ptr()), stride, C.c_void_p(self._ws.data_ptr()),
+            self._ws.numel(), stream), "warp_windows")
+        bb = bbox.cpu().numpy()
+        dts = dt.cpu().numpy()
+        nds = nd.cpu().numpy()
+        out = []
+        for p in range(npairs):
+            tname = TYPE_NAMES[int(dts[p])]
+            w, h = int(bb[p, 2]), int(bb[p, 3])
+            nb = {"Byte": 1, "SignedByte": 1, "Int16": 2, "UInt16": 2, "Float32": 4}[tname]
+            t = win[p, : w * h * nb].view(TORCH_OF[tname]).reshape(h, w)
+            out.append((t, bb[p].tolist(), tname, float(nds[p])))
+        return out

@@ -1,0 +1,281 @@
+/*
+ * gskyhip.h -- C-ABI of the MI355X-native GSKY raster hot path.
+ *
+ * libgskyhip.so (gsky_amd/libgskyhip.so) implements GSKY's per-request
+ * raster hot path on gfx950 with hand-written HIP kernels:
+ *   warp (reprojection + nearest/bilinear resampling)
+ *   -> nodata-aware time-ordered mosaic (merge, masks)
+ *   -> byte scaling -> palette / RGBA fill
+ * and the drill (zonal) reduction.
+ *
+ * Every entry point names the reference interface it replaces
+ * (chuc92man/gsky file:line).  Signatures use plain C types and pointers only.
+ * "dev" pointers are HIP device pointers (hipMalloc / torch CUDA tensors);
+ * `stream` is a hipStream_t passed as void* (NULL = default stream).
+ * Batch entry points are asynchronous on `stream` and never allocate,
+ * synchronise or copy to the host, so they can be captured in a hipGraph.
+ *
+ * Error codes: 0 OK; >0 follow the reference where one exists
+ * (warp.go:103-140: 1 open failed, 2 band failed, 3 transformer failed);
+ * negative values are GSKYHIP_E_* below.
+ */
+#ifndef GSKYHIP_H
+#define GSKYHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes -------------------------------------------------------- */
+#define GSKYHIP_OK 0
+#define GSKYHIP_E_ARG (-1)         /* bad argument / size                     */
+#define GSKYHIP_E_TYPE (-2)        /* raster type not implemented             */
+#define GSKYHIP_E_HIP (-3)         /* HIP runtime error                       */
+#define GSKYHIP_E_CRS (-4)         /* unsupported CRS                          */
+#define GSKYHIP_E_MASK (-5)        /* bad mask spec (tile_merger.go:315-323)   */
+#define GSKYHIP_E_NOGPU (-6)       /* no HIP device                            */
+#define GSKYHIP_E_RANGE (-7)       /* index out of range (Go would panic)      */
+
+/* ---- raster data types: GDALDataType codes (warp.go:428-431) + 100 ------- */
+#define GSKYHIP_BYTE 1
+#define GSKYHIP_UINT16 2
+#define GSKYHIP_INT16 3
+#define GSKYHIP_UINT32 4
+#define GSKYHIP_INT32 5
+#define GSKYHIP_FLOAT32 6
+#define GSKYHIP_FLOAT64 7
+#define GSKYHIP_SIGNEDBYTE 100     /* warp.go:354-359 */
+
+/* ---- coordinate reference systems --------------------------------------- */
+#define GSKYHIP_CRS_LONGLAT 0      /* EPSG:4326, traditional GIS order, deg   */
+#define GSKYHIP_CRS_WEBMERC 1      /* EPSG:3857                                 */
+#define GSKYHIP_CRS_AEA 2          /* EPSG:3577 (GDA94 / Australian Albers)    */
+#define GSKYHIP_CRS_SINU 3         /* MODIS sinusoidal, sphere R=6371007.181    */
+
+typedef struct {
+    int32_t kind;
+    int32_t _pad;
+    double a, ra, es, e, one_es;
+    double lam0, phi0, phi1, phi2, x0, y0, k0;
+    double n, c, dd, rho0, ec;      /* aea constants                           */
+} gskyhip_crs;
+
+/* Parse an SRS as handed over by gsky-ows (tile_grpc.go:127-136 exports the
+ * request CRS as WKT): WKT with a top-level AUTHORITY["EPSG",...], "EPSG:n",
+ * a proj4 string, or "MODIS".  Returns 0 or GSKYHIP_E_CRS. */
+int gskyhip_crs_from_srs(const char *srs, gskyhip_crs *out);
+
+/* ---- granules (the HBM-resident stand-in for an opened GDAL dataset) ----- */
+#define GSKYHIP_MAX_OVR 12
+typedef struct {
+    const void *data;            /* dev: ysize x xsize of dtype, row-major   */
+    int32_t dtype;               /* GSKYHIP_* (Byte for SignedByte data)       */
+    int32_t xsize, ysize;
+    int32_t signed_byte;         /* PIXELTYPE=SIGNEDBYTE                        */
+    double geot[6];              /* GDALGetGeoTransform                          */
+    double nodata;               /* GDALGetRasterNoDataValue (-1e10 if unset)   */
+    int32_t has_nodata;
+    int32_t crs;                 /* index into the CRS table of the call        */
+    int32_t n_ovr;
+    int32_t ns;                  /* namespace slot of this granule (merge)      */
+    const void *ovr_data[GSKYHIP_MAX_OVR];  /* dev, finest first (GDALGetOverview) */
+    int32_t ovr_xsize[GSKYHIP_MAX_OVR];
+    int32_t ovr_ysize[GSKYHIP_MAX_OVR];
+    double timestamp;            /* GeoTileGranule.TimeStamp                     */
+    uint32_t polygon_hash;       /* fnv32a(GeoTileGranule.Polygon)               */
+    int32_t _pad2;
+} gskyhip_granule;
+
+/* One output tile of a GetMap batch.  Granules of the tile are
+ * pair_granule[pair_begin..pair_end) in indexer / gRPC fan-out order
+ * (tile_grpc.go:200-289). */
+typedef struct {
+    double dst_geot[6];          /* BBox2Geot (tile_grpc.go:380-382)             */
+    int32_t width, height;
+    int32_t pair_begin, pair_end;
+} gskyhip_tile;
+
+/* Scale parameters, utils.ScaleParams (raster_scaler.go:8-13). */
+typedef struct {
+    double offset, scale, clip;
+    int32_t colour_scale;
+    int32_t _pad;
+} gskyhip_scale_params;
+
+/* Mask layer, utils.Mask (utils/config.go:73-80).  `ns` is the namespace slot
+ * whose rasters are the mask (Mask.ID == NameSpace); -1 = no mask.  value is
+ * the base-2 Mask.Value string (may be NULL); bit_tests pairs. */
+#define GSKYHIP_MAX_BIT_TESTS 8
+typedef struct {
+    int32_t ns;
+    int32_t inclusive;
+    int32_t n_bit_tests;         /* number of strings in bit_tests (even)        */
+    int32_t _pad;
+    const char *value;
+    const char *bit_tests[GSKYHIP_MAX_BIT_TESTS];
+} gskyhip_mask;
+
+/* ---- drop-in for the cgo entry point of the worker ----------------------- */
+/* Registers an HBM-resident granule under (path, band) so that the drop-in
+ * below can find it (it replaces GDALOpenEx in warp.go:89-101; file decode
+ * stays out of scope).  `g->data` etc. must stay valid until unregistered. */
+int gskyhip_register_granule(const char *path, int band, const gskyhip_granule *g,
+                             const char *srs);
+int gskyhip_unregister_all(void);
+
+/* Same signature, ownership and return codes as
+ *   int warp_operation_fast(const char *srcFilePath, char *srcProjRef,
+ *       double *srcGeot, const char **geoLocOpts, const char *dstProjRef,
+ *       double *dstGeot, int dstXImageSize, int dstYImageSize, int band,
+ *       int srsCf, void **dstBuf, int *dstBufSize, int *dstBbox,
+ *       double *noData, GDALDataType *dType, int *bytesRead)
+ * (worker/gdalprocess/warp.go:82).  *dstBuf is host memory from malloc(); the
+ * caller frees it with free() (warp.go:573-574).  srcGeot, when given, may be
+ * overwritten by the overview pick (warp.go:186-189).  geoLocOpts != NULL is
+ * not supported (returns 3).  Nearest-neighbour, like the reference. */
+int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGeot,
+                        const char **geoLocOpts, const char *dstProjRef, double *dstGeot,
+                        int dstXImageSize, int dstYImageSize, int band, int srsCf,
+                        void **dstBuf, int *dstBufSize, int *dstBbox, double *noData,
+                        int *dType, int *bytesRead);
+
+/* ---- batched GetMap path (the MI355X hot path) --------------------------- */
+/* Workspace bytes needed by gskyhip_render_tiles / gskyhip_warp_windows for
+ * n_tiles tiles with n_pairs pairs whose tiles are at most max_tile_height
+ * rows. */
+int64_t gskyhip_render_workspace_size(int n_tiles, int n_pairs, int max_tile_height);
+
+#define GSKYHIP_RESAMPLE_NEAREST 0
+#define GSKYHIP_RESAMPLE_BILINEAR 1
+
+/* Warp + merge + scale + palette for a batch of tiles, replacing per tile:
+ * gRPC warp fan-out (tile_grpc.go:200-289 -> warp.go:82-382), RasterMerger
+ * (tile_merger.go:447-738), utils.Scale (raster_scaler.go:334) and the
+ * EncodePNG pixel loop (ogc_encoders.go:82-134).
+ *   granules, crs_table, tiles, pair_granule: dev arrays.
+ *   out_ns[0..n_out_ns): HOST array of namespace slots rendered
+ *     (ConfigPayLoad.NameSpaces order; 1 = palette/grey, 3 = RGB).
+ *   mask, sp: HOST structs.
+ *   ramp: dev 256x4 RGBA (GradientRGBAPalette) or NULL for grey.
+ *   rgba_out: dev n_tiles x height x width x 4.
+ *   canvas_out: optional dev buffer n_tiles x n_out_ns x height x width x 4
+ *     bytes receiving the typed merged canvases (tile_merger.go:562-652), or NULL.
+ *   auto_scale (Offset = Scale = Clip = 0) needs canvas_out.
+ *   workspace: dev, gskyhip_render_workspace_size bytes. */
+int gskyhip_render_tiles(const gskyhip_granule *granules, int n_granules,
+                         const gskyhip_crs *crs_table, int n_crs, int dst_crs,
+                         const gskyhip_tile *tiles, int n_tiles,
+                         const int32_t *pair_granule, int n_pairs,
+                         int max_tile_width, int max_tile_height,
+                         const int32_t *out_ns, int n_out_ns,
+                         const gskyhip_mask *mask, int resample,
+                         const gskyhip_scale_params *sp, const uint8_t *ramp,
+                         uint8_t *rgba_out, void *canvas_out,
+                         void *workspace, int64_t workspace_bytes, void *stream);
+
+/* The same call split in phases: 1 = planning kernels only (windows,
+ * merge order, row plans into `workspace`), 2 = render kernels only (needs
+ * a phase-1 call with identical arguments before it on the stream),
+ * 0 = both (= gskyhip_render_tiles).  rgba_out may be NULL: typed canvases
+ * only (WCS GetCoverage, FusionUnscale: ows.go:728), canvas_out required. */
+int gskyhip_render_tiles_phase(int phase, const gskyhip_granule *granules, int n_granules,
+                               const gskyhip_crs *crs_table, int n_crs, int dst_crs,
+                               const gskyhip_tile *tiles, int n_tiles,
+                               const int32_t *pair_granule, int n_pairs,
+                               int max_tile_width, int max_tile_height,
+                               const int32_t *out_ns, int n_out_ns,
+                               const gskyhip_mask *mask, int resample,
+                               const gskyhip_scale_params *sp, const uint8_t *ramp,
+                               uint8_t *rgba_out, void *canvas_out,
+                               void *workspace, int64_t workspace_bytes, void *stream);
+
+/* Warped windows only (the FlexRasters of tile_grpc.go:228-241): for pair p
+ * (tile t, granule g) writes window bbox[4*p..] = {xoff,yoff,w,h} and the
+ * window data (dtype of warp.go:232-243) into win_out + p*win_stride bytes. */
+int gskyhip_warp_windows(const gskyhip_granule *granules, int n_granules,
+                         const gskyhip_crs *crs_table, int n_crs, int dst_crs,
+                         const gskyhip_tile *tiles, int n_tiles,
+                         const int32_t *pair_granule, int n_pairs,
+                         int max_tile_width, int max_tile_height, int resample,
+                         int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
+                         void *win_out, int64_t win_stride,
+                         void *workspace, int64_t workspace_bytes, void *stream);
+
+/* ---- standalone stages (the reference's own operator boundaries) -------- */
+/* FlexRaster (tile_types.go:95-106) as flat fields; data is dev. */
+typedef struct {
+    const void *data;
+    int32_t data_w, data_h, width, height, off_x, off_y;
+    int32_t dtype, ns;
+    double nodata, timestamp;
+    uint32_t polygon_hash;
+    int32_t _pad;
+} gskyhip_flex_raster;
+
+/* RasterMerger.Run for one batch (tile_merger.go:447-503 ->
+ * ProcessRasterStack 281-312 -> MergeMaskedRaster 38-225 / ComputeMask
+ * 314-445).  rasters: HOST array (ordering metadata); their data: dev.
+ * canvases: n_ns dev buffers of width*height*4 bytes (typed by the first
+ * raster of each namespace); created/dtype/nodata: host outputs per ns. */
+int gskyhip_merge_rasters(const gskyhip_flex_raster *rasters, int n,
+                          const gskyhip_mask *mask, void *const *canvases, int n_ns,
+                          int32_t *created, int32_t *dtype, double *nodata, void *stream);
+
+/* utils.Scale for one raster (raster_scaler.go:30-332): data dev (n values),
+ * out dev (n bytes).  Byte input is scaled in place like the reference. */
+int gskyhip_scale(void *data, int dtype, int64_t n, double nodata,
+                  const gskyhip_scale_params *sp, uint8_t *out, void *stream);
+
+/* processor.RasterScaler.Run (tile_scaler.go:17-112, dead in the reference). */
+int gskyhip_scale_legacy(void *data, int dtype, int64_t n, double nodata,
+                         const gskyhip_scale_params *sp, uint8_t *out, void *stream);
+
+/* GradientRGBAPalette (utils/palette.go:27-69): colours host n x RGBA,
+ * ramp host 256 x RGBA. */
+int gskyhip_gradient_palette(const uint8_t *colours, int n, int interpolate, uint8_t *ramp);
+
+/* EncodePNG pixel loop (ogc_encoders.go:86-133): bands dev (1 or 3), ramp
+ * dev or NULL, rgba dev w*h*4. */
+int gskyhip_encode_rgba(const uint8_t *const *bands, int nbands, int w, int h,
+                        const uint8_t *ramp, uint8_t *rgba, void *stream);
+
+/* ComputeMask (tile_merger.go:314-445): data dev, out dev (n bytes 0/1). */
+int gskyhip_compute_mask(const void *data, int dtype, int64_t n, const gskyhip_mask *mask,
+                         uint8_t *out, void *stream);
+
+/* ---- drill (WPS zonal statistics) --------------------------------------- */
+/* readData (worker/gdalprocess/drill.go:90-227), mean / pixel-count mode,
+ * decileCount = 0, for a batch of polygons over one time stack.
+ *   stack: dev float32, time-innermost layout [y][x][t] of an
+ *     xsize x ysize x n_bands stack, t fastest, t padded to t_stride
+ *     (a multiple of 4, >= n_bands; 16-byte aligned pixel vectors).
+ *   win: dev int32 4 per polygon {off_x, off_y, count_x, count_y}.
+ *   mask_off: dev int64 per polygon, offset into masks (dev uint8, 255 = in).
+ *   band_strides as drill.go:110-219.  Rows per polygon = *rows_per_poly.
+ *   out_value: dev f64, out_count: dev i32, n_polys x rows_per_poly. */
+int gskyhip_drill_rows(int n_bands, int band_strides);
+int gskyhip_drill(const float *stack, int xsize, int ysize, int n_bands, int t_stride,
+                  const int32_t *win, const int64_t *mask_off, const uint8_t *masks,
+                  int n_polys, float nodata, float clip_lower, float clip_upper,
+                  int pixel_count, int band_strides, double *out_value,
+                  int32_t *out_count, void *stream);
+
+/* DrillMerger weighted mean (drill_merger.go:79-93): values/counts dev
+ * n_files x n_dates, out dev n_dates (NaN where no count). */
+int gskyhip_drill_merge(const double *values, const int32_t *counts, int n_files,
+                        int n_dates, double *out, void *stream);
+
+/* ---- misc ---------------------------------------------------------------- */
+uint32_t gskyhip_fnv32a(const char *s, int64_t n);
+const char *gskyhip_version(void);
+int gskyhip_device_count(void);
+/* Status of the last render call (TilePlan status of every tile, read back
+ * synchronously): 0 OK or the first error code; n_tiles of the last call. */
+int gskyhip_render_status(void *workspace, int n_tiles, int n_pairs, int max_tile_height, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1417 @@
+/*
+ * gsky_oracle.c -- CPU restatement of GSKY's raster hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see gsky_oracle.h).  Built with
+ * -O2 -ffp-contract=off so every double expression rounds exactly as the
+ * x86-64 SSE2 code of the reference (Go gc / GDAL built without -mfma).
+ *
+ * Reference citations are file:line under chuc92man/gsky; [ext] marks the
+ * restated algorithm of an un-vendored dependency (GDAL 3.0.1, PROJ 6.1.1,
+ * Go 1.12 runtime/strconv/math).
+ */
+#define _GNU_SOURCE
+#include "gsky_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+
+int oracle_type_size(int dtype) {
+    switch (dtype) {
+    case OR_BYTE: case OR_SIGNEDBYTE: return 1;
+    case OR_UINT16: case OR_INT16: return 2;
+    case OR_UINT32: case OR_INT32: case OR_FLOAT32: return 4;
+    case OR_FLOAT64: return 8;
+    default: return 0;
+    }
+}
+
+/* ======================================================================== */
+/* Go 1.12 amd64 conversions [ext]: float -> int{8,16}/uint{8,16} is        */
+/* CVTTSD2SL / CVTTSS2SL to int32 (NaN or out of range -> 0x80000000)       */
+/* followed by truncation to the narrow type.                               */
+/* ======================================================================== */
+static int32_t go_cvtt32(double x) {
+    if (!(x > -2147483649.0 && x < 2147483648.0)) return INT32_MIN;
+    return (int32_t)x;
+}
+int8_t   or_go_f64_i8(double v)  { return (int8_t)(uint8_t)(uint32_t)go_cvtt32(v); }
+uint8_t  or_go_f64_u8(double v)  { return (uint8_t)(uint32_t)go_cvtt32(v); }
+int16_t  or_go_f64_i16(double v) { return (int16_t)(uint16_t)(uint32_t)go_cvtt32(v); }
+uint16_t or_go_f64_u16(double v) { return (uint16_t)(uint32_t)go_cvtt32(v); }
+int8_t   or_go_f32_i8(float v)   { return or_go_f64_i8((double)v); }
+uint8_t  or_go_f32_u8(float v)   { return or_go_f64_u8((double)v); }
+int16_t  or_go_f32_i16(float v)  { return or_go_f64_i16((double)v); }
+uint16_t or_go_f32_u16(float v)  { return or_go_f64_u16((double)v); }
+
+/* GDALCopyWord(double -> T) [ext, gdal_priv_templates.hpp]: integer targets
+ * round half away from zero and saturate, NaN -> 0; float32 saturates at
+ * +-FLT_MAX (infinities kept). */
+static double gdal_round_clamp(double v, double lo, double hi) {
+    if (isnan(v)) return 0.0;
+    double r = v >= 0.0 ? v + 0.5 : v - 0.5;
+    if (r > hi) r = hi;
+    if (r < lo) r = lo;
+    return trunc(r);
+}
+void or_gdal_copy_word(double v, int dtype, void *out) {
+    switch (dtype) {
+    case OR_BYTE: case OR_SIGNEDBYTE: { uint8_t o = (uint8_t)gdal_round_clamp(v, 0, 255); memcpy(out, &o, 1); break; }
+    case OR_UINT16: { uint16_t o = (uint16_t)gdal_round_clamp(v, 0, 65535); memcpy(out, &o, 2); break; }
+    case OR_INT16: { int16_t o = (int16_t)gdal_round_clamp(v, -32768, 32767); memcpy(out, &o, 2); break; }
+    case OR_UINT32: { uint32_t o = (uint32_t)gdal_round_clamp(v, 0, 4294967295.0); memcpy(out, &o, 4); break; }
+    case OR_INT32: { int32_t o = (int32_t)gdal_round_clamp(v, -2147483648.0, 2147483647.0); memcpy(out, &o, 4); break; }
+    case OR_FLOAT32: {
+        float o;
+        if (isinf(v)) o = (float)v;
+        else if (v > FLT_MAX) o = FLT_MAX;
+        else if (v < -FLT_MAX) o = -FLT_MAX;
+        else o = (float)v;
+        memcpy(out, &o, 4); break;
+    }
+    case OR_FLOAT64: memcpy(out, &v, 8); break;
+    default: break;
+    }
+}
+
+/* ======================================================================== */
+/* Go math.Log / Log10 [ext: Go 1.12 math/log.go, log10.go; the amd64        */
+/* assembly runs the same FreeBSD sequence].                                */
+/* ======================================================================== */
+static double go_log(double x) {
+    const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+    const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01,
+                 L3 = 2.857142874366239149e-01, L4 = 2.222219843214978396e-01,
+                 L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+                 L7 = 1.479819860511658591e-01;
+    if (isnan(x) || (isinf(x) && x > 0)) return x;
+    if (x < 0) return NAN;
+    if (x == 0) return -INFINITY;
+    int ki;
+    double f1 = frexp(x, &ki);
+    if (f1 < 1.41421356237309504880168872420969808 / 2) { f1 *= 2; ki--; }
+    double f = f1 - 1;
+    double k = (double)ki;
+    double s = f / (2 + f);
+    double s2 = s * s;
+    double s4 = s2 * s2;
+    double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+    double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+    double R = t1 + t2;
+    double hfsq = 0.5 * f * f;
+    return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+static double go_log2(double x) {
+    int e;
+    double frac = frexp(x, &e);
+    if (frac == 0.5) return (double)(e - 1);
+    return go_log(frac) * (1.0 / 0.693147180559945309417232121458176568) + (double)e;
+}
+static double go_log10(double x) {
+    /* Ln2/Ln10 is an exact Go constant expression rounded once to float64. */
+    return go_log2(x) * 0.301029995663981195213738894724493026768189881462108541310;
+}
+
+/* utils/raster_scaler.go:15-28 normalise() */
+static double go_normalise(double val, int colour_scale, double nodata) {
+    if (val == nodata) return val;
+    double v = val;
+    if (colour_scale == 1) v = go_log10(val); /* ColourLogScale, utils/config.go:34 */
+    if (isinf(v) || isnan(v)) v = nodata;
+    return v;
+}
+
+/* ======================================================================== */
+/* utils/raster_scaler.go:30-332  scale()                                   */
+/* ======================================================================== */
+#define SCALE_INT_CASE(T, CONV32, CONV64)                                          \
+    do {                                                                           \
+        T *d = (T *)data;                                                          \
+        T noData = CONV64(nodata);                                                 \
+        T off = CONV64(offset);                                                    \
+        T clp = CONV64(clip);                                                      \
+        if (autom) {                                                               \
+            float minVal = 0.0f, maxVal = 0.0f;                                    \
+            for (int64_t i = 0; i < n; i++) {                                      \
+                T value = d[i];                                                    \
+                if (value == noData) continue;                                     \
+                float val = (float)value;                                          \
+                if (i == 0) { minVal = val; maxVal = val; }                        \
+                else { if (val < minVal) minVal = val; if (val > maxVal) maxVal = val; } \
+            }                                                                      \
+            if (minVal == maxVal) maxVal += 0.1f;                                  \
+            sc = 254.0f / (maxVal - minVal);                                       \
+            float dfOffset = -minVal;                                              \
+            off = CONV32(dfOffset);                                                \
+            clp = CONV32(maxVal + dfOffset);                                       \
+        }                                                                          \
+        for (int64_t i = 0; i < n; i++) {                                          \
+            T value = d[i];                                                        \
+            if (value == noData) { out[i] = 0xFF; continue; }                      \
+            value = (T)(value + off);                                              \
+            if (value > clp) value = clp;                                          \
+            if (value < 0) value = 0;                                              \
+            out[i] = or_go_f32_u8((float)value * sc);                              \
+        }                                                                          \
+    } while (0)
+
+int oracle_scale(void *data, int dtype, int64_t n, double nodata,
+                 double offset, double scale, double clip, int colour_scale,
+                 uint8_t *out) {
+    float sc = (float)scale;                               /* 31 */
+    if (sc <= 0.0f) {
+        if (clip <= 0.0) sc = 1.0f;
+        else sc = (float)(254.0f / (float)clip);           /* 36 */
+    }
+    const int autom = (scale == 0.0 && clip == 0.0 && offset == 0.0);
+    switch (dtype) {
+    case OR_SIGNEDBYTE: SCALE_INT_CASE(int8_t, or_go_f32_i8, or_go_f64_i8); return 0;   /* 41-94 */
+    case OR_BYTE: {                                                                       /* 96-148 */
+        /* scaled in place: the input raster is overwritten */
+        SCALE_INT_CASE(uint8_t, or_go_f32_u8, or_go_f64_u8);
+        memcpy(data, out, (size_t)n);
+        return 0;
+    }
+    case OR_INT16: SCALE_INT_CASE(int16_t, or_go_f32_i16, or_go_f64_i16); return 0;     /* 150-203 */
+    case OR_UINT16: SCALE_INT_CASE(uint16_t, or_go_f32_u16, or_go_f64_u16); return 0;   /* 205-258 */
+    case OR_FLOAT32: {                                                                    /* 260-327 */
+        float *d = (float *)data;
+        float noData = (float)nodata;
+        float off = (float)offset;
+        float clp = (float)clip;
+        if (autom) {
+            float minVal = 0.0f, maxVal = 0.0f;
+            for (int64_t i = 0; i < n; i++) {
+                float value = d[i];
+                if (value == noData) continue;
+                if (colour_scale > 0) {
+                    double v = go_normalise((double)value, colour_scale, nodata);
+                    if (v == nodata) continue;
+                    value = (float)v;
+                }
+                if (i == 0) { minVal = value; maxVal = value; }
+                else { if (value < minVal) minVal = value; if (value > maxVal) maxVal = value; }
+            }
+            if (minVal == maxVal) maxVal += 0.1f;
+            sc = 254.0f / (maxVal - minVal);
+            off = -minVal;
+            clp = maxVal + off;
+        }
+        for (int64_t i = 0; i < n; i++) {
+            float value = d[i];
+            if (value == noData) { out[i] = 0xFF; continue; }
+            if (colour_scale > 0) {
+                double v = go_normalise((double)value, colour_scale, nodata);
+                if (v == nodata) { out[i] = 0xFF; continue; }
+                value = (float)v;
+            }
+            value += off;
+            if (value > clp) value = clp;
+            if (value < 0.0f) value = 0.0f;
+            out[i] = or_go_f32_u8(value * sc);
+        }
+        return 0;
+    }
+    default:
+        return -1;
+    }
+}
+
+/* processor/tile_scaler.go:17-112 (no callers in the reference) */
+int oracle_scale_legacy(void *data, int dtype, int64_t n, double nodata,
+                        double offset, double scale, double clip, uint8_t *out) {
+    switch (dtype) {
+    case OR_BYTE: {                                           /* 22-40 */
+        uint8_t *d = (uint8_t *)data;
+        uint8_t noData = or_go_f64_u8(nodata);
+        uint8_t clp = or_go_f64_u8(clip);
+        for (int64_t i = 0; i < n; i++) {
+            uint8_t value = d[i];
+            if (value == noData) { d[i] = 0xFF; }
+            else {
+                if (value > clp) value = clp;
+                d[i] = or_go_f64_u8((double)value * scale);
+            }
+            out[i] = d[i];
+        }
+        return 0;
+    }
+    case OR_INT16: {                                          /* 42-62 */
+        int16_t *d = (int16_t *)data;
+        int16_t noData = or_go_f64_i16(nodata);
+        int16_t clp = or_go_f64_i16(clip);
+        for (int64_t i = 0; i < n; i++) {
+            int16_t value = d[i];
+            if (value == noData) { out[i] = 0xFF; continue; }
+            if (value > clp) value = clp;
+            if (value < 0) value = 0;
+            out[i] = or_go_f32_u8((float)value * 254.0f / (float)clp);
+        }
+        return 0;
+    }
+    case OR_UINT16: {                                         /* 64-84 */
+        uint16_t *d = (uint16_t *)data;
+        uint16_t noData = or_go_f64_u16(nodata);
+        uint16_t clp = or_go_f64_u16(clip);
+        for (int64_t i = 0; i < n; i++) {
+            uint16_t value = d[i];
+            if (value == noData) { out[i] = 0xFF; continue; }
+            if (value > clp) value = clp;
+            out[i] = or_go_f32_u8((float)value * 254.0f / (float)clp);
+        }
+        return 0;
+    }
+    case OR_FLOAT32: {                                        /* 86-108 */
+        float *d = (float *)data;
+        float noData = (float)nodata;
+        float sc = (float)scale;
+        uint8_t off = or_go_f64_u8(offset);
+        float clp = (float)clip;
+        for (int64_t i = 0; i < n; i++) {
+            float value = d[i];
+            if (value == noData) { out[i] = 0xFF; continue; }
+            value += (float)off;
+            if (value > clp) value = clp;
+            if (value < 0) value = 0;
+            out[i] = or_go_f32_u8(value * sc);
+        }
+        return 0;
+    }
+    default:
+        return -1;
+    }
+}
+
+/* ======================================================================== */
+/* utils/palette.go:11-69                                                    */
+/* ======================================================================== */
+static uint8_t interp_u8(uint8_t a, uint8_t b, long i, long section) {
+    /* Go int arithmetic, truncating division, uint8 wrap (palette.go:11-13) */
+    long q = (i * ((long)b - (long)a)) / section;
+    return (uint8_t)(a + (uint8_t)q);
+}
+
+int oracle_gradient_palette(const uint8_t *colours, int n, int interpolate, uint8_t *ramp) {
+    if (interpolate) {
+        if (n < 2) return -1;
+        int bins = n - 1;
+        int sectionLength = 256 / bins;
+        if (sectionLength == 0) return -1;  /* Go: integer divide by zero panic (palette.go:12) */
+        int bonus = 256 - sectionLength * bins;
+        int index = 0;
+        for (int section = 0; section < bins; section++) {
+            const uint8_t *a = colours + 4 * section, *b = colours + 4 * (section + 1);
+            int cnt = sectionLength + (section < bonus ? 1 : 0);
+            for (int i = 0; i < cnt; i++) {
+                uint8_t *o = ramp + 4 * index;
+                o[0] = interp_u8(a[0], b[0], i, sectionLength);
+                o[1] = interp_u8(a[1], b[1], i, sectionLength);
+                o[2] = interp_u8(a[2], b[2], i, sectionLength);
+                o[3] = a[3];                           /* alpha of the lower colour (22) */
+                index++;
+            }
+        }
+    } else {
+        if (n < 1) return -1;
+        int bins = n;
+        int sectionLength = 256 / bins;
+        int bonus = 256 - sectionLength * bins;
+        int index = 0;
+        for (int section = 0; section < bins; section++) {
+            int cnt = sectionLength + (section < bonus ? 1 : 0);
+            for (int i = 0; i < cnt; i++) {
+                memcpy(ramp + 4 * index, colours + 4 * section, 4);
+                index++;
+            }
+        }
+    }
+    return 0;
+}
+
+int oracle_encode_rgba(const uint8_t *const *bands, int nbands, int w, int h,
+                       const uint8_t *ramp, uint8_t *rgba) {
+    const int64_t npx = (int64_t)w * h;
+    memset(rgba, 0, (size_t)npx * 4);                  /* image.NewRGBA */
+    if (nbands == 1) {
+        const uint8_t *b = bands[0];
+        for (int64_t i = 0; i < npx; i++) {
+            uint8_t v = b[i];
+            if (v == 0xFF) continue;
+            if (ramp) memcpy(rgba + 4 * i, ramp + 4 * v, 4);          /* 94-100 */
+            else { rgba[4*i] = v; rgba[4*i+1] = v; rgba[4*i+2] = v; rgba[4*i+3] = 0xFF; } /* 102-112 */
+        }
+        return 0;
+    }
+    if (nbands == 3) {                                                  /* 115-133 */
+        for (int64_t i = 0; i < npx; i++) {
+            if (bands[0][i] != 0xFF || bands[1][i] != 0xFF || bands[2][i] != 0xFF) {
+                rgba[4*i] = bands[0][i]; rgba[4*i+1] = bands[1][i];
+                rgba[4*i+2] = bands[2][i]; rgba[4*i+3] = 0xFF;
+            }
+        }
+        return 0;
+    }
+    return -1;                                                          /* 135-136 */
+}
+
+/* ======================================================================== */
+/* processor/tile_merger.go                                                 */
+/* ======================================================================== */
+uint32_t oracle_fnv32a(const char *s, size_t n) {     /* Go hash/fnv New32a [ext] */
+    uint32_t h = 2166136261u;
+    for (size_t i = 0; i < n; i++) { h ^= (uint8_t)s[i]; h *= 16777619u; }
+    return h;
+}
+
+/* strconv.ParseUint / ParseInt (base 2) of Go 1.12 [ext], errors ignored by
+ * the caller exactly as tile_merger.go:332-431 does (value returned anyway). */
+static uint64_t go_parse_uint2(const char *s, int bits) {
+    uint64_t maxVal = (bits >= 64) ? UINT64_MAX : ((1ull << bits) - 1);
+    if (!s || !*s) return 0;
+    uint64_t n = 0;
+    const uint64_t cutoff = UINT64_MAX / 2 + 1;
+    for (const char *p = s; *p; p++) {
+        int d;
+        char c = *p;
+        if (c >= '0' && c <= '9') d = c - '0';
+        else if ((c | 0x20) >= 'a' && (c | 0x20) <= 'z') d = (c | 0x20) - 'a' + 10;
+        else return 0;
+        if (d >= 2) return 0;
+        if (n >= cutoff) return maxVal;
+        n *= 2;
+        uint64_t n1 = n + (uint64_t)d;
+        if (n1 < n || n1 > maxVal) return maxVal;
+        n = n1;
+    }
+    return n;
+}
+static int64_t go_parse_int2(const char *s, int bits) {
+    if (!s || !*s) return 0;
+    int neg = 0;
+    if (*s == '+') s++;
+    else if (*s == '-') { neg = 1; s++; }
+    /* ParseUint with a syntax error -> 0 */
+    uint64_t maxVal = (1ull << bits) - 1;
+    uint64_t un;
+    {
+        if (!*s) return 0;
+        uint64_t n = 0; int syntax = 0, range = 0;
+        for (const char *p = s; *p; p++) {
+            char c = *p; int d;
+            if (c >= '0' && c <= '9') d = c - '0';
+            else if ((c | 0x20) >= 'a' && (c | 0x20) <= 'z') d = (c | 0x20) - 'a' + 10;
+            else { syntax = 1; break; }
+            if (d >= 2) { syntax = 1; break; }
+            if (n >= UINT64_MAX / 2 + 1) { n = maxVal; range = 1; break; }
+            n *= 2;
+            uint64_t n1 = n + (uint64_t)d;
+            if (n1 < n || n1 > maxVal) { n = maxVal; range = 1; break; }
+            n = n1;
+        }
+        if (syntax) return 0;
+        (void)range;
+        un = n;
+    }
+    uint64_t cutoff = 1ull << (bits - 1);
+    if (!neg && un >= cutoff) return (int64_t)(cutoff - 1);
+    if (neg && un > cutoff) return -(int64_t)cutoff;
+    int64_t r = (int64_t)un;
+    return neg ? -r : r;
+}
+
+int oracle_compute_mask(const void *data, int dtype, int64_t n,
+                        const char *value, const char *const *bit_tests,
+                        int n_bit_tests, uint8_t *out) {
+    const int has_value = value && *value;
+    if (!has_value) {                                    /* 315-323 */
+        if (n_bit_tests == 0) return -1;
+        if (n_bit_tests % 2 != 0) return -1;
+    }
+#define MASK_CASE(T, UNSIGNED_VALUE, PARSE_BITS, POSITIVE)                                \
+    do {                                                                                   \
+        const T *d = (const T *)data;                                                      \
+        if (has_value) {                                                                   \
+            T mv = UNSIGNED_VALUE ? (T)go_parse_uint2(value, PARSE_BITS)                   \
+                                  : (T)go_parse_int2(value, PARSE_BITS);                   \
+            for (int64_t i = 0; i < n; i++) { T a = (T)(d[i] & mv); out[i] = POSITIVE(a); } \
+        } else {                                                                           \
+            for (int64_t i = 0; i < n; i++) {                                              \
+                out[i] = 0;                                                                \
+                for (int j = 0; j < n_bit_tests; j += 2) {                                 \
+                    T f = (T)go_parse_int2(bit_tests[j], PARSE_BITS);                      \
+                    T v = (T)go_parse_int2(bit_tests[j + 1], PARSE_BITS);                  \
+                    if ((T)(d[i] & f) == v) { out[i] = 1; break; }                          \
+                }                                                                          \
+            }                                                                              \
+        }                                                                                  \
+    } while (0)
+#define POS_SIGNED(a) ((a) > 0 ? 1 : 0)
+#define POS_UNSIGNED(a) ((a) > 0 ? 1 : 0)
+    switch (dtype) {
+    case OR_SIGNEDBYTE: MASK_CASE(int8_t, 1, 8, POS_SIGNED); return 0;   /* 328-354 */
+    case OR_BYTE: MASK_CASE(uint8_t, 1, 8, POS_UNSIGNED); return 0;      /* 355-381 */
+    case OR_INT16: MASK_CASE(int16_t, 0, 16, POS_SIGNED); return 0;      /* 382-410: ParseInt */
+    case OR_UINT16: MASK_CASE(uint16_t, 1, 16, POS_UNSIGNED); return 0;  /* 411-439 */
+    default: return -2;                                                   /* 440-442 */
+    }
+}
+
+static void init_nodata(void *buf, int dtype, double nodata, int64_t n) {   /* 227-279 */
+    switch (dtype) {
+    case OR_SIGNEDBYTE: { int8_t f = or_go_f64_i8(nodata); for (int64_t i = 0; i < n; i++) ((int8_t *)buf)[i] = f; break; }
+    case OR_BYTE: { uint8_t f = or_go_f64_u8(nodata); for (int64_t i = 0; i < n; i++) ((uint8_t *)buf)[i] = f; break; }
+    case OR_INT16: { int16_t f = or_go_f64_i16(nodata); for (int64_t i = 0; i < n; i++) ((int16_t *)buf)[i] = f; break; }
+    case OR_UINT16: { uint16_t f = or_go_f64_u16(nodata); for (int64_t i = 0; i < n; i++) ((uint16_t *)buf)[i] = f; break; }
+    case OR_FLOAT32: { float f = (float)nodata; for (int64_t i = 0; i < n; i++) ((float *)buf)[i] = f; break; }
+    default: break;
+    }
+}
+
+/* MergeMaskedRaster tile_merger.go:38-225 */
+static int merge_masked_raster(const oracle_flex_raster *r, oracle_canvas *cv,
+                               const uint8_t *mask, int64_t mask_len) {
+    if (r->dtype != cv->dtype) return -4;  /* the reference would reinterpret bytes */
+    if ((int64_t)r->data_w * r->data_h > mask_len) return -3; /* Go would panic */
+    const int fill = r->timestamp < cv->timestamp;
+#define MERGE_CASE(T, NODATA)                                                       \
+    do {                                                                            \
+        T *canvas = (T *)cv->data;                                                  \
+        const T *data = (const T *)r->data;                                         \
+        T nodata = NODATA;                                                          \
+        int64_t iSrc = 0;                                                           \
+        for (int ir = 0; ir < r->data_h; ir++) {                                    \
+            for (int ic = 0; ic < r->data_w; ic++) {                                \
+                T val = data[iSrc];                                                 \
+                int64_t iDst = (int64_t)(ir + r->off_y) * r->width + ic + r->off_x; \
+                if (fill) {                                                         \
+                    if (val != nodata && !mask[iSrc] && canvas[iDst] == nodata)     \
+                        canvas[iDst] = val;                                         \
+                } else {                                                            \
+                    if (val != nodata && !mask[iSrc]) canvas[iDst] = val;           \
+                }                                                                   \
+                iSrc++;                                                             \
+            }                                                                       \
+        }                                                                           \
+    } while (0)
+    switch (r->dtype) {
+    case OR_SIGNEDBYTE: MERGE_CASE(int8_t, or_go_f64_i8(r->nodata)); break;
+    case OR_BYTE: MERGE_CASE(uint8_t, or_go_f64_u8(r->nodata)); break;
+    case OR_INT16: MERGE_CASE(int16_t, or_go_f64_i16(r->nodata)); break;
+    case OR_UINT16: MERGE_CASE(uint16_t, or_go_f64_u16(r->nodata)); break;
+    case OR_FLOAT32: MERGE_CASE(float, (float)r->nodata); break;
+    default: return -5;                                               /* 221-223 */
+    }
+    if (!fill) cv->timestamp = r->timestamp;
+    return 0;
+}
+
+typedef struct { double key; int first; } stack_key;
+static int cmp_key_desc(const void *a, const void *b) {
+    double x = ((const stack_key *)a)->key, y = ((const stack_key *)b)->key;
+    return (x > y) ? -1 : (x < y) ? 1 : 0;
+}
+
+int oracle_merge_batch(const oracle_flex_raster *rasters, int n,
+                       int mask_ns, const char *mask_value,
+                       const char *const *bit_tests, int n_bit_tests,
+                       int mask_inclusive, oracle_canvas *canvases, int n_ns) {
+    int rc = 0;
+    double *stamp = (double *)malloc(sizeof(double) * (n > 0 ? n : 1));
+    int *in_stack = (int *)calloc(n > 0 ? n : 1, sizeof(int));
+    uint8_t **masks = (uint8_t **)calloc(n > 0 ? n : 1, sizeof(uint8_t *));
+    int64_t *mask_len = (int64_t *)calloc(n > 0 ? n : 1, sizeof(int64_t));
+    stack_key *keys = (stack_key *)malloc(sizeof(stack_key) * (n > 0 ? n : 1));
+    int nkeys = 0;
+    /* tile_merger.go:468-492 */
+    for (int i = 0; i < n; i++) {
+        const oracle_flex_raster *r = &rasters[i];
+        stamp[i] = r->timestamp + (double)r->polygon_hash;
+        if (mask_ns >= 0 && r->ns == mask_ns) {
+            int64_t len = (int64_t)r->data_w * r->data_h;
+            masks[i] = (uint8_t *)malloc(len > 0 ? len : 1);
+            mask_len[i] = len;
+            rc = oracle_compute_mask(r->data, r->dtype, len, mask_value, bit_tests, n_bit_tests, masks[i]);
+            if (rc) goto done;
+            if (!mask_inclusive) continue;
+        }
+        in_stack[i] = 1;
+        int found = 0;
+        for (int k = 0; k < nkeys; k++) if (keys[k].key == stamp[i]) { found = 1; break; }
+        if (!found) { keys[nkeys].key = stamp[i]; keys[nkeys].first = i; nkeys++; }
+    }
+    /* ProcessRasterStack 281-312: keys sorted descending */
+    qsort(keys, nkeys, sizeof(stack_key), cmp_key_desc);
+    for (int k = 0; k < nkeys; k++) {
+        const double key = keys[k].key;
+        /* maskMap[geoStamp]: last mask raster stored under that key wins */
+        const uint8_t *mask = NULL; int64_t mlen = 0;
+        for (int i = 0; i < n; i++)
+            if (masks[i] && stamp[i] == key) { mask = masks[i]; mlen = mask_len[i]; }
+        for (int i = 0; i < n; i++) {
+            if (!in_stack[i] || stamp[i] != key) continue;
+            const oracle_flex_raster *r = &rasters[i];
+            if (r->ns < 0 || r->ns >= n_ns) { rc = -6; goto done; }
+            oracle_canvas *cv = &canvases[r->ns];
+            if (!cv->created) {                                      /* 291-297 */
+                cv->created = 1;
+                cv->dtype = r->dtype;
+                cv->nodata = r->nodata;
+                cv->timestamp = 0;
+                init_nodata(cv->data, r->dtype, r->nodata, (int64_t)r->width * r->height);
+            }
+            uint8_t *zero = NULL;
+            const uint8_t *m = mask; int64_t ml = mlen;
+            if (!m) {                                               /* 300-302 */
+                ml = (int64_t)r->height * r->width;
+                zero = (uint8_t *)calloc(ml > 0 ? ml : 1, 1);
+                m = zero;
+            }
+            rc = merge_masked_raster(r, cv, m, ml);
+            free(zero);
+            if (rc) goto done;
+        }
+    }
+done:
+    for (int i = 0; i < n; i++) free(masks[i]);
+    free(masks); free(mask_len); free(stamp); free(in_stack); free(keys);
+    return rc;
+}
+
+/* ======================================================================== */
+/* Projections [ext: PROJ 6.1.1 pj_fwd/pj_inv wrappers, merc.cpp (webmerc),   */
+/* aea.cpp, gn_sinu.cpp; GDAL 3 traditional GIS axis order].                */
+/* ======================================================================== */
+#define OR_HALFPI 1.57079632679489661923
+#define OR_PI 3.14159265358979323846
+#define OR_TWOPI 6.2831853071795864769
+#define OR_FORTPI 0.78539816339744830962
+#define OR_D2R 0.017453292519943295769236907684886
+#define OR_R2D (1.0 / 0.017453292519943295769236907684886)
+
+static double adjlon(double lon) {
+    if (fabs(lon) < OR_PI + 1e-12) return lon;
+    lon += OR_PI;
+    lon -= OR_TWOPI * floor(lon / OR_TWOPI);
+    lon -= OR_PI;
+    return lon;
+}
+static double pj_qsfn(double sinphi, double e, double one_es) {
+    if (e >= 1.0e-7) {
+        double con = e * sinphi;
+        double div1 = 1.0 - con * con;
+        double div2 = 1.0 + con;
+        if (div1 == 0.0 || div2 == 0.0) return HUGE_VAL;
+        return one_es * (sinphi / div1 - (.5 / e) * log((1. - con) / div2));
+    }
+    return sinphi + sinphi;
+}
+static double pj_msfn(double sinphi, double cosphi, double es) {
+    return cosphi / sqrt(1. - es * sinphi * sinphi);
+}
+static double aea_phi1(double qs, double Te, double Tone_es) {
+    double Phi = asin(.5 * qs);
+    if (Te < 1.0e-7) return Phi;
+    int i = 15;
+    double dphi;
+    do {
+        double sinpi = sin(Phi), cospi = cos(Phi);
+        double con = Te * sinpi;
+        double com = 1. - con * con;
+        dphi = .5 * com * com / cospi *
+               (qs / Tone_es - sinpi / com + .5 / Te * log((1. - con) / (1. + con)));
+        Phi += dphi;
+    } while (fabs(dphi) > 1.0e-10 && --i);
+    return i ? Phi : HUGE_VAL;
+}
+
+static void set_ellps(oracle_crs *c, double a, double rf) {
+    c->a = a;
+    c->ra = 1.0 / a;
+    if (rf == 0.0) { c->es = 0.0; }
+    else { double f = 1.0 / rf; c->es = 2 * f - f * f; }
+    c->e = sqrt(c->es);
+    c->one_es = 1.0 - c->es;
+}
+
+static int aea_setup(oracle_crs *c) {
+    double phi1 = c->phi1, phi2 = c->phi2;
+    if (fabs(phi1 + phi2) < 1e-10) return -1;
+    double sinphi = sin(phi1), cosphi = cos(phi1);
+    c->n = sinphi;
+    int secant = fabs(phi1 - phi2) >= 1e-10;
+    if (c->es > 0.) {
+        double m1 = pj_msfn(sinphi, cosphi, c->es);
+        double ml1 = pj_qsfn(sinphi, c->e, c->one_es);
+        if (secant) {
+            double s2 = sin(phi2), c2 = cos(phi2);
+            double m2 = pj_msfn(s2, c2, c->es);
+            double ml2 = pj_qsfn(s2, c->e, c->one_es);
+            if (ml2 == ml1) return -1;
+            c->n = (m1 * m1 - m2 * m2) / (ml2 - ml1);
+        }
+        c->ec = 1. - .5 * c->one_es * log((1. - c->e) / (1. + c->e)) / c->e;
+        c->c = m1 * m1 + c->n * ml1;
+        c->dd = 1. / c->n;
+        c->rho0 = c->dd * sqrt(c->c - c->n * pj_qsfn(sin(c->phi0), c->e, c->one_es));
+    } else {
+        if (secant) c->n = .5 * (c->n + sin(phi2));
+        double n2 = c->n + c->n;
+        c->c = cosphi * cosphi + n2 * sinphi;
+        c->dd = 1. / c->n;
+        c->rho0 = c->dd * sqrt(c->c - n2 * sin(c->phi0));
+    }
+    return 0;
+}
+
+static double param_of(const char *s, const char *key, double dflt, int *found) {
+    const char *p = s;
+    size_t kl = strlen(key);
+    while ((p = strstr(p, key)) != NULL) {
+        if ((p == s || p[-1] == ' ' || p[-1] == '+') && p[kl] == '=') {
+            if (found) *found = 1;
+            return strtod(p + kl + 1, NULL);
+        }
+        p += kl;
+    }
+    if (found) *found = 0;
+    return dflt;
+}
+
+int oracle_crs_init(oracle_crs *c, const char *spec) {
+    memset(c, 0, sizeof(*c));
+    c->k0 = 1.0;
+    if (!spec) return -1;
+    if (!strcasecmp(spec, "EPSG:4326")) { c->kind = OR_CRS_LONGLAT; set_ellps(c, 6378137.0, 298.257223563); return 0; }
+    if (!strcasecmp(spec, "EPSG:3857") || !strcasecmp(spec, "EPSG:900913")) {
+        c->kind = OR_CRS_WEBMERC; set_ellps(c, 6378137.0, 0.0); return 0;
+    }
+    if (!strcasecmp(spec, "EPSG:3577")) {
+        c->kind = OR_CRS_AEA; set_ellps(c, 6378137.0, 298.257222101);
+        c->lam0 = 132.0 * OR_D2R; c->phi0 = 0.0; c->phi1 = -18.0 * OR_D2R; c->phi2 = -36.0 * OR_D2R;
+        return aea_setup(c);
+    }
+    if (!strcasecmp(spec, "SR-ORG:6842") || !strcasecmp(spec, "MODIS")) {
+        c->kind = OR_CRS_SINU; set_ellps(c, 6371007.181, 0.0); return 0;
+    }
+    if (strstr(spec, "+proj=")) {
+        int f = 0;
+        double a = param_of(spec, "+a", 0, &f);
+        double R = param_of(spec, "+R", 0, NULL);
+        double rf = param_of(spec, "+rf", 0, NULL);
+        int has_a = f;
+        if (strstr(spec, "+ellps=GRS80")) { a = 6378137.0; rf = 298.257222101; has_a = 1; }
+        else if (strstr(spec, "+ellps=WGS84") || strstr(spec, "+datum=WGS84")) { a = 6378137.0; rf = 298.257223563; has_a = 1; }
+        if (R > 0) { a = R; rf = 0; has_a = 1; }
+        if (!has_a) { a = 6378137.0; rf = 298.257223563; }
+        c->lam0 = param_of(spec, "+lon_0", 0, NULL) * OR_D2R;
+        c->phi0 = param_of(spec, "+lat_0", 0, NULL) * OR_D2R;
+        c->x0 = param_of(spec, "+x_0", 0, NULL);
+        c->y0 = param_of(spec, "+y_0", 0, NULL);
+        if (strstr(spec, "+proj=longlat") || strstr(spec, "+proj=latlong")) {
+            c->kind = OR_CRS_LONGLAT; set_ellps(c, a, rf); return 0;
+        }
+        if (strstr(spec, "+proj=webmerc") ||
+            (strstr(spec, "+proj=merc") && R > 0)) {
+            c->kind = OR_CRS_WEBMERC; set_ellps(c, a, 0.0); return 0;
+        }
+        if (strstr(spec, "+proj=aea")) {
+            c->kind = OR_CRS_AEA; set_ellps(c, a, rf);
+            c->phi1 = param_of(spec, "+lat_1", 0, NULL) * OR_D2R;
+            c->phi2 = param_of(spec, "+lat_2", 0, NULL) * OR_D2R;
+            return aea_setup(c);
+        }
+        if (strstr(spec, "+proj=sinu")) { c->kind = OR_CRS_SINU; set_ellps(c, a, rf == 0 ? 0 : rf); if (c->es != 0) return -1; return 0; }
+    }
+    return -1;
+}
+
+static int crs_equal(const oracle_crs *a, const oracle_crs *b) {
+    return memcmp(a, b, sizeof(*a)) == 0;
+}
+
+/* inverse: CRS coordinates -> (lam, phi) radians.  pj_inv wrapper. */
+static int crs_inverse(const oracle_crs *c, double x, double y, double *lam, double *phi) {
+    if (x == HUGE_VAL || y == HUGE_VAL) return 0;
+    if (c->kind == OR_CRS_LONGLAT) {            /* unitconvert deg -> rad */
+        *lam = x * OR_D2R; *phi = y * OR_D2R; return 1;
+    }
+    double xn = (x * 1.0 - c->x0) * c->ra;
+    double yn = (y * 1.0 - c->y0) * c->ra;
+    double l, p;
+    switch (c->kind) {
+    case OR_CRS_WEBMERC:                        /* merc.cpp s_inverse */
+        p = OR_HALFPI - 2. * atan(exp(-yn / c->k0));
+        l = xn / c->k0;
+        break;
+    case OR_CRS_AEA: {                          /* aea.cpp e_inverse */
+        double rho;
+        yn = c->rho0 - yn;
+        if ((rho = hypot(xn, yn)) != 0.0) {
+            if (c->n < 0.) { rho = -rho; xn = -xn; yn = -yn; }
+            p = rho / c->dd;
+            if (c->es > 0.) {
+                p = (c->c - p * p) / c->n;
+                if (fabs(c->ec - fabs(p)) > 1e-7) {
+                    if ((p = aea_phi1(p, c->e, c->one_es)) == HUGE_VAL) return 0;
+                } else {
+                    p = p < 0. ? -OR_HALFPI : OR_HALFPI;
+                }
+            } else {
+                p = (c->c - p * p) / (c->n + c->n);
+                if (fabs(p) <= 1.) p = asin(p);
+                else p = p < 0. ? -OR_HALFPI : OR_HALFPI;
+            }
+            l = atan2(xn, yn) / c->n;
+        } else {
+            l = 0.;
+            p = c->n > 0. ? OR_HALFPI : -OR_HALFPI;
+        }
+        break;
+    }
+    case OR_CRS_SINU:                           /* gn_sinu.cpp s_inverse, m=0 n=1 */
+        p = yn;
+        l = xn / cos(yn);
+        break;
+    default:
+        return 0;
+    }
+    if (l == HUGE_VAL || p == HUGE_VAL || isnan(l) || isnan(p)) return 0;
+    l = l + c->lam0;
+    l = adjlon(l);
+    *lam = l; *phi = p;
+    return 1;
+}
+
+/* forward: (lam, phi) radians -> CRS coordinates.  pj_fwd wrapper. */
+static int crs_forward(const oracle_crs *c, double lam, double phi, double *x, double *y) {
+    if (c->kind == OR_CRS_LONGLAT) {            /* unitconvert rad -> deg */
+        *x = lam * OR_R2D; *y = phi * OR_R2D; return 1;
+    }
+    double t = (phi < 0 ? -phi : phi) - OR_HALFPI;
+    if (t > 1e-12 || lam > 10 || lam < -10) return 0;
+    if (phi > OR_HALFPI) phi = OR_HALFPI;
+    if (phi < -OR_HALFPI) phi = -OR_HALFPI;
+    lam = lam - c->lam0;
+    lam = adjlon(lam);
+    double xn, yn;
+    switch (c->kind) {
+    case OR_CRS_WEBMERC:                        /* merc.cpp s_forward */
+        if (fabs(fabs(phi) - OR_HALFPI) <= 1.e-10) return 0;
+        xn = c->k0 * lam;
+        yn = c->k0 * log(tan(OR_FORTPI + .5 * phi));
+        break;
+    case OR_CRS_AEA: {                          /* aea.cpp e_forward */
+        double rho = c->c - (c->es > 0. ? c->n * pj_qsfn(sin(phi), c->e, c->one_es)
+                                        : (c->n + c->n) * sin(phi));
+        if (rho < 0.) return 0;
+        rho = c->dd * sqrt(rho);
+        lam *= c->n;
+        xn = rho * sin(lam);
+        yn = c->rho0 - rho * cos(lam);
+        break;
+    }
+    case OR_CRS_SINU:                           /* gn_sinu.cpp s_forward, m=0 n=1 */
+        xn = lam * cos(phi);
+        yn = phi;
+        break;
+    default:
+        return 0;
+    }
+    if (isnan(xn) || isnan(yn) || isinf(xn) || isinf(yn)) return 0;
+    *x = 1.0 * (c->a * xn + c->x0);
+    *y = 1.0 * (c->a * yn + c->y0);
+    return 1;
+}
+
+int oracle_crs_transform(const oracle_crs *src, const oracle_crs *dst, double *x, double *y) {
+    if (crs_equal(src, dst)) return 1;
+    double lam, phi;
+    if (!crs_inverse(src, *x, *y, &lam, &phi)) return 0;
+    return crs_forward(dst, lam, phi, x, y);
+}
+
+/* ======================================================================== */
+/* GDAL GenImgProj / Approx transformers [ext: gdaltransformer.cpp 3.0.1]     */
+/* ======================================================================== */
+static void inv_geot(const double *gt, double *o) {   /* GDALInvGeoTransform */
+    if (gt[2] == 0.0 && gt[4] == 0.0 && gt[1] != 0.0 && gt[5] != 0.0) {
+        o[0] = -gt[0] / gt[1];
+        o[1] = 1.0 / gt[1];
+        o[2] = 0.0;
+        o[3] = -gt[3] / gt[5];
+        o[4] = 0.0;
+        o[5] = 1.0 / gt[5];
+        return;
+    }
+    double det = gt[1] * gt[5] - gt[2] * gt[4];
+    double inv_det = 1.0 / det;
+    o[0] = (gt[2] * gt[3] - gt[0] * gt[5]) * inv_det;
+    o[3] = (-gt[1] * gt[3] + gt[0] * gt[4]) * inv_det;
+    o[1] = gt[5] * inv_det;
+    o[4] = -gt[4] * inv_det;
+    o[2] = -gt[2] * inv_det;
+    o[5] = gt[1] * inv_det;
+}
+
+typedef struct {
+    oracle_crs src, dst;
+    int reproject;
+    double src_gt[6], src_igt[6], dst_gt[6], dst_igt[6];
+} gip_t;
+
+static void gip_init(gip_t *t, const oracle_crs *src, const oracle_crs *dst,
+                     const double *src_gt, const double *dst_gt) {
+    memset(t, 0, sizeof(*t));
+    t->src = *src;
+    if (dst) t->dst = *dst;
+    t->reproject = dst && !crs_equal(src, dst);
+    memcpy(t->src_gt, src_gt, 6 * sizeof(double));
+    memcpy(t->dst_gt, dst_gt, 6 * sizeof(double));
+    inv_geot(t->src_gt, t->src_igt);
+    inv_geot(t->dst_gt, t->dst_igt);
+}
+
+/* GDALGenImgProjTransform for one point. */
+static int gip_point(const gip_t *t, int dst_to_src, double *x, double *y) {
+    const double *g1 = dst_to_src ? t->dst_gt : t->src_gt;
+    const double *g2 = dst_to_src ? t->src_igt : t->dst_igt;
+    double X = g1[0] + *x * g1[1] + *y * g1[2];
+    double Y = g1[3] + *x * g1[4] + *y * g1[5];
+    if (t->reproject) {
+        const oracle_crs *from = dst_to_src ? &t->dst : &t->src;
+        const oracle_crs *to = dst_to_src ? &t->src : &t->dst;
+        if (!oracle_crs_transform(from, to, &X, &Y)) return 0;
+    }
+    *x = g2[0] + X * g2[1] + Y * g2[2];
+    *y = g2[3] + X * g2[4] + Y * g2[5];
+    return 1;
+}
+static int gip_transform(const gip_t *t, int dst_to_src, int n, double *x, double *y, int *ok) {
+    for (int i = 0; i < n; i++) ok[i] = gip_point(t, dst_to_src, &x[i], &y[i]);
+    return 1;
+}
+
+/* GDALApproxTransformInternal (3.0.1) with dfMaxError = 0.125. */
+static int approx_internal(const gip_t *t, int dst2src, int nPoints, double *x, double *y,
+                           int *ok, const double *xs, const double *ys) {
+    const int nMiddle = (nPoints - 1) / 2;
+    const double dfDeltaX = (xs[2] - xs[0]) / (x[nPoints - 1] - x[0]);
+    const double dfDeltaY = (ys[2] - ys[0]) / (x[nPoints - 1] - x[0]);
+    const double dfError = fabs((xs[0] + dfDeltaX * (x[nMiddle] - x[0])) - xs[1]) +
+                           fabs((ys[0] + dfDeltaY * (x[nMiddle] - x[0])) - ys[1]);
+    if (dfError > 0.125) {
+        double xM[3] = {x[(nMiddle - 1) / 2], x[nMiddle - 1], x[nMiddle + (nPoints - nMiddle - 1) / 2]};
+        double yM[3] = {y[(nMiddle - 1) / 2], y[nMiddle - 1], y[nMiddle + (nPoints - nMiddle - 1) / 2]};
+        const int base1 = nMiddle <= 5 || y[0] != y[nMiddle - 1] || y[0] != y[(nMiddle - 1) / 2] ||
+                          x[0] == x[nMiddle - 1] || x[0] == x[(nMiddle - 1) / 2];
+        const int base2 = nPoints - nMiddle <= 5 || y[nMiddle] != y[nPoints - 1] ||
+                          y[nMiddle] != y[nMiddle + (nPoints - nMiddle - 1) / 2] ||
+                          x[nMiddle] == x[nPoints - 1] ||
+                          x[nMiddle] == x[nMiddle + (nPoints - nMiddle - 1) / 2];
+        int s2[3] = {0, 0, 0};
+        int bSuccess = 0;
+        if (!base1 && !base2) {
+            bSuccess = gip_transform(t, dst2src, 3, xM, yM, s2);
+        } else if (!base1) {
+            bSuccess = gip_transform(t, dst2src, 2, xM, yM, s2);
+            s2[2] = 1;
+        } else if (!base2) {
+            bSuccess = gip_transform(t, dst2src, 1, xM + 2, yM + 2, s2 + 2);
+            s2[0] = 1; s2[1] = 1;
+        }
+        if (!bSuccess || !s2[0] || !s2[1] || !s2[2]) {
+            bSuccess = gip_transform(t, dst2src, nMiddle - 1, x + 1, y + 1, ok + 1);
+            bSuccess &= gip_transform(t, dst2src, nPoints - nMiddle - 2, x + nMiddle + 1,
+                                      y + nMiddle + 1, ok + nMiddle + 1);
+            x[0] = xs[0]; y[0] = ys[0]; ok[0] = 1;
+            x[nMiddle] = xs[1]; y[nMiddle] = ys[1]; ok[nMiddle] = 1;
+            x[nPoints - 1] = xs[2]; y[nPoints - 1] = ys[2]; ok[nPoints - 1] = 1;
+            return bSuccess;
+        }
+        double x2[3], y2[3];
+        if (!base1) {
+            x2[0] = xs[0]; y2[0] = ys[0];
+            x2[1] = xM[0]; y2[1] = yM[0];
+            x2[2] = xM[1]; y2[2] = yM[1];
+            bSuccess = approx_internal(t, dst2src, nMiddle, x, y, ok, x2, y2);
+        } else {
+            bSuccess = gip_transform(t, dst2src, nMiddle - 1, x + 1, y + 1, ok + 1);
+            x[0] = xs[0]; y[0] = ys[0]; ok[0] = 1;
+        }
+        if (!bSuccess) return 0;
+        if (!base2) {
+            x2[0] = xs[1]; y2[0] = ys[1];
+            x2[1] = xM[2]; y2[1] = yM[2];
+            x2[2] = xs[2]; y2[2] = ys[2];
+            bSuccess = approx_internal(t, dst2src, nPoints - nMiddle, x + nMiddle, y + nMiddle,
+                                       ok + nMiddle, x2, y2);
+        } else {
+            bSuccess = gip_transform(t, dst2src, nPoints - nMiddle - 2, x + nMiddle + 1,
+                                     y + nMiddle + 1, ok + nMiddle + 1);
+            x[nMiddle] = xs[1]; y[nMiddle] = ys[1]; ok[nMiddle] = 1;
+            x[nPoints - 1] = xs[2]; y[nPoints - 1] = ys[2]; ok[nPoints - 1] = 1;
+        }
+        return bSuccess;
+    }
+    for (int i = nPoints - 1; i >= 0; i--) {
+        const double dfDist = x[i] - x[0];
+        y[i] = ys[0] + dfDeltaY * dfDist;
+        x[i] = xs[0] + dfDeltaX * dfDist;
+        ok[i] = 1;
+    }
+    return 1;
+}
+
+/* GDALApproxTransform (3.0.1) */
+static int approx_transform(const gip_t *t, int dst2src, int nPoints, double *x, double *y, int *ok) {
+    const int nMiddle = (nPoints - 1) / 2;
+    if (y[0] != y[nPoints - 1] || y[0] != y[nMiddle] || x[0] == x[nPoints - 1] ||
+        x[0] == x[nMiddle] || nPoints <= 5)
+        return gip_transform(t, dst2src, nPoints, x, y, ok);
+    double x2[3] = {x[0], x[nMiddle], x[nPoints - 1]};
+    double y2[3] = {y[0], y[nMiddle], y[nPoints - 1]};
+    int s2[3];
+    gip_transform(t, dst2src, 3, x2, y2, s2);
+    if (!s2[0] || !s2[1] || !s2[2]) return gip_transform(t, dst2src, nPoints, x, y, ok);
+    return approx_internal(t, dst2src, nPoints, x, y, ok, x2, y2);
+}
+
+void oracle_approx_row(const oracle_crs *src, const oracle_crs *dst,
+                       const double src_geot[6], const double dst_geot[6],
+                       int n, double *x, double *y, int *success) {
+    gip_t t;
+    gip_init(&t, src, dst, src_geot, dst_geot);
+    approx_transform(&t, 1, n, x, y, success);
+}
+
+/* GDALSuggestedWarpOutput2_MustAdjustFor{Right,Bottom}Border [ext] */
+static int must_adjust(const gip_t *t, const double *ext, int np, int nl, double psx, double psy, int right) {
+    double ax[21], ay[21];
+    int s1[21], s2[21];
+    int ns = 0;
+    for (double r = 0.0; r <= 1.01; r += 0.05) {
+        if (r > 0.99) r = 1.0;
+        if (right) { ax[ns] = ext[2]; ay[ns] = ext[3] - psy * r * nl; }
+        else { ax[ns] = ext[0] + psx * r * np; ay[ns] = ext[1]; }
+        ns++;
+    }
+    gip_transform(t, 1, ns, ax, ay, s1);
+    gip_transform(t, 0, ns, ax, ay, s2);
+    int bad = 0, k = 0;
+    for (double r = 0.0; r <= 1.01; r += 0.05) {
+        double ex = right ? ext[2] : ext[0] + psx * r * np;
+        double ey = right ? ext[3] - psy * r * nl : ext[1];
+        if (!s1[k] || !s2[k] || fabs(ax[k] - ex) > psx || fabs(ay[k] - ey) > psy) bad++;
+        k++;
+    }
+    return bad == ns;
+}
+
+/* GDALSuggestedWarpOutput2 [ext: gdaltransformer.cpp 3.0.1], nOptions = 0,
+ * with the transformer GDALGenImgProjTransform (warp.go:154). */
+static int suggested_warp_output(const gip_t *t, int nInX, int nInY, double *gt_out,
+                                 int *pnPixels, int *pnLines, double *ext) {
+    enum { NSTEPS = 20 };
+    double px[(NSTEPS + 1) * (NSTEPS + 1)], py[(NSTEPS + 1) * (NSTEPS + 1)];
+    int ok[(NSTEPS + 1) * (NSTEPS + 1)];
+    const double dfStep = 1.0 / NSTEPS;
+    int ns = 0;
+    for (int i = 0; i <= NSTEPS; i++) {
+        const double r = (i == NSTEPS) ? 1.0 : i * dfStep;
+        px[ns] = r * nInX; py[ns] = 0.0; ns++;          /* top    */
+        px[ns] = r * nInX; py[ns] = nInY; ns++;         /* bottom */
+        px[ns] = 0.0; py[ns] = r * nInY; ns++;          /* left   */
+        px[ns] = nInX; py[ns] = r * nInY; ns++;         /* right  */
+    }
+    gip_transform(t, 0, ns, px, py, ok);
+    int failed = 0;
+    for (int i = 0; i < ns; i++) if (!ok[i]) failed++;
+    if (failed > 0) {                                    /* fall back to a full grid */
+        ns = 0;
+        for (int iy = 0; iy <= NSTEPS; iy++) {
+            const double ry = (iy == NSTEPS) ? 1.0 : iy * dfStep;
+            for (int ix = 0; ix <= NSTEPS; ix++) {
+                const double rx = (ix == NSTEPS) ? 1.0 : ix * dfStep;
+                px[ns] = rx * nInX; py[ns] = ry * nInY; ns++;
+            }
+        }
+        gip_transform(t, 0, ns, px, py, ok);
+    }
+    double minX = 0, minY = 0, maxX = 0, maxY = 0;
+    int got = 0;
+    for (int i = 0; i < ns; i++) {
+        if (!ok[i]) continue;
+        if (!got) { minX = maxX = px[i]; minY = maxY = py[i]; got = 1; }
+        else {
+            if (px[i] < minX) minX = px[i];
+            if (py[i] < minY) minY = py[i];
+            if (px[i] > maxX) maxX = px[i];
+            if (py[i] > maxY) maxY = py[i];
+        }
+    }
+    if (!got) return -1;
+    double dX = 0, dY = 0;
+    if (ok[0] && ok[ns - 1]) { dX = px[ns - 1] - px[0]; dY = py[ns - 1] - py[0]; }
+    if (dX == 0.0 || dY == 0.0) { dX = maxX - minX; dY = maxY - minY; }
+    const double diag = sqrt(dX * dX + dY * dY);
+    const double ps = diag / sqrt((double)nInX * nInX + (double)nInY * nInY);
+    const double dfPixels = (maxX - minX) / ps;
+    const double dfLines = (maxY - minY) / ps;
+    if (!(dfPixels <= 2147483646.0 && dfLines <= 2147483646.0)) return -1;
+    *pnPixels = (int)(dfPixels + 0.5);
+    *pnLines = (int)(dfLines + 0.5);
+    double psx = ps, psy = ps;
+    static const double ratios[5] = {0.000, 0.001, 0.010, 0.100, 1.000};
+    for (int k = 0; k < 5; k++) {
+        const double tryx = psx - psx * ratios[k] / *pnPixels;
+        double e[4] = {minX, maxY - (*pnLines) * psy, minX + (*pnPixels) * tryx, maxY};
+        if (!must_adjust(t, e, *pnPixels, *pnLines, tryx, psy, 1)) { psx = tryx; break; }
+    }
+    for (int k = 0; k < 5; k++) {
+        const double tryy = psy - psy * ratios[k] / *pnLines;
+        double e[4] = {minX, maxY - (*pnLines) * tryy, minX + (*pnPixels) * psx, maxY};
+        if (!must_adjust(t, e, *pnPixels, *pnLines, psx, tryy, 0)) { psy = tryy; break; }
+    }
+    maxX = minX + (*pnPixels) * psx;
+    minY = maxY - (*pnLines) * psy;
+    ext[0] = minX; ext[1] = minY; ext[2] = maxX; ext[3] = maxY;
+    gt_out[0] = minX; gt_out[1] = psx; gt_out[2] = 0.0;
+    gt_out[3] = maxY; gt_out[4] = 0.0; gt_out[5] = -psy;
+    return 0;
+}
+
+int oracle_suggested_warp_output(const oracle_granule *g, const oracle_crs *src,
+                                 const oracle_crs *dst, const double src_geot[6],
+                                 const double dst_geot[6], double geot_out[6],
+                                 int *n_pixels, int *n_lines, double extent[4]) {
+    gip_t t;
+    gip_init(&t, src, dst, src_geot ? src_geot : g->geot, dst_geot);
+    return suggested_warp_output(&t, g->xsize, g->ysize, geot_out, n_pixels, n_lines, extent);
+}
+
+static int round_coord(double coord, int maxExtent) {     /* warp.go:69-80 */
+    int c;
+    if (coord < 0) c = 0;
+    else {
+        c = (int)(coord + 1e-10);
+        if (c > maxExtent - 1) c = maxExtent - 1;
+    }
+    return c;
+}
+
+static double read_as_double(const void *base, int dtype, int64_t idx) {
+    switch (dtype) {
+    case OR_BYTE: return ((const uint8_t *)base)[idx];
+    case OR_SIGNEDBYTE: return ((const int8_t *)base)[idx];
+    case OR_UINT16: return ((const uint16_t *)base)[idx];
+    case OR_INT16: return ((const int16_t *)base)[idx];
+    case OR_UINT32: return ((const uint32_t *)base)[idx];
+    case OR_INT32: return ((const int32_t *)base)[idx];
+    case OR_FLOAT32: return ((const float *)base)[idx];
+    case OR_FLOAT64: return ((const double *)base)[idx];
+    default: return 0;
+    }
+}
+
+/* GWKBilinearResample4Sample [ext: gdalwarpkernel.cpp] with validity from
+ * the band nodata (UNIFIED_SRC_NODATA); returns 1 and *out when density > 0. */
+static int bilinear_sample(const void *band, int dtype, int nx, int ny, int has_nodata,
+                           double nodata, double sx, double sy, double *out) {
+    int iSrcX = (int)floor(sx - 0.5);
+    int iSrcY = (int)floor(sy - 0.5);
+    double rX = 1.5 - (sx - iSrcX);
+    double rY = 1.5 - (sy - iSrcY);
+    if (iSrcX == -1) { iSrcX = 0; rX = 1; }
+    if (iSrcY == -1) { iSrcY = 0; rY = 1; }
+    double accR = 0.0, accDiv = 0.0;
+    const int xs[4] = {iSrcX, iSrcX + 1, iSrcX, iSrcX + 1};
+    const int ys[4] = {iSrcY, iSrcY, iSrcY + 1, iSrcY + 1};
+    const double w[4] = {rX * rY, (1.0 - rX) * rY, rX * (1.0 - rY), (1.0 - rX) * (1.0 - rY)};
+    for (int k = 0; k < 4; k++) {
+        if (xs[k] < 0 || xs[k] >= nx || ys[k] < 0 || ys[k] >= ny) continue;
+        double v = read_as_double(band, dtype, (int64_t)ys[k] * nx + xs[k]);
+        if (has_nodata && (v == nodata || (isnan(nodata) && isnan(v)))) continue;
+        accDiv += w[k];
+        accR += v * w[k];
+    }
+    if (accDiv == 1.0) { *out = accR; return 1; }
+    if (accDiv < 0.00001) return 0;
+    *out = accR / accDiv;
+    return 1;
+}
+
+int oracle_warp(const oracle_granule *g, const oracle_crs *src,
+                const oracle_crs *dst, const double dst_geot[6],
+                int dst_w, int dst_h, int resample,
+                void **out_buf, int *out_size, int32_t bbox[4],
+                double *nodata, int *dtype, int *bytes_read) {
+    *bytes_read = 0;
+    double srcGeot[6];
+    memcpy(srcGeot, g->geot, sizeof(srcGeot));
+    gip_t t;
+    gip_init(&t, src, dst, srcGeot, dst_geot);                  /* warp.go:130 */
+    double geotOut[6], ext[4];
+    int nPixels = 0, nLines = 0;
+    const int err = suggested_warp_output(&t, g->xsize, g->ysize, geotOut, &nPixels, &nLines, ext);
+
+    /* overview pick, warp.go:156-198 */
+    const void *band = g->data;
+    int bandX = g->xsize, bandY = g->ysize;
+    if (err == 0 && g->n_ovr > 0) {
+        const double targetRatio = 1.0 / geotOut[1];
+        if (targetRatio > 1.0) {
+            const int srcXSize = g->xsize, srcYSize = g->ysize;
+            int iOvr = -1;
+            for (; iOvr < g->n_ovr - 1; iOvr++) {
+                double ovrRatio = 1.0;
+                if (iOvr >= 0) ovrRatio = (double)srcXSize / g->ovr_xsize[iOvr];
+                const double nextOvrRatio = (double)srcXSize / g->ovr_xsize[iOvr + 1];
+                if (ovrRatio < targetRatio && nextOvrRatio > targetRatio) break;
+                const double diff = ovrRatio - targetRatio;
+                if (diff > -1e-1 && diff < 1e-1) break;
+            }
+            if (iOvr >= 0) {
+                band = g->ovr_data[iOvr];
+                bandX = g->ovr_xsize[iOvr];
+                bandY = g->ovr_ysize[iOvr];
+                srcGeot[1] *= srcXSize / (double)bandX;
+                srcGeot[2] *= srcXSize / (double)bandX;
+                srcGeot[4] *= srcYSize / (double)bandY;
+                srcGeot[5] *= srcYSize / (double)bandY;
+                gip_init(&t, src, dst, srcGeot, dst_geot);
+            }
+        }
+    }
+
+    /* window, warp.go:200-217 */
+    int dstXOff = 0, dstYOff = 0, dstXSize = dst_w, dstYSize = dst_h;
+    if (err == 0) {
+        const int minX = round_coord(ext[0], dstXSize);
+        const int minY = round_coord(ext[1], dstYSize);
+        const int maxX = round_coord(ext[2] + 0.5, dstXSize);
+        const int maxY = round_coord(ext[3] + 0.5, dstYSize);
+        dstXOff = minX; dstYOff = minY;
+        dstXSize = maxX - minX + 1;
+        dstYSize = maxY - minY + 1;
+    }
+
+    /* data types, warp.go:232-247 */
+    const int srcType = g->dtype;
+    int outType = srcType;
+    const int supported = srcType == OR_BYTE || srcType == OR_INT16 || srcType == OR_UINT16 ||
+                          srcType == OR_FLOAT32;
+    if (!supported) outType = OR_FLOAT32;
+    const int dsz = oracle_type_size(outType);
+    *out_size = dstXSize * dstYSize * dsz;
+    uint8_t *buf = (uint8_t *)malloc(*out_size > 0 ? *out_size : 1);
+    *nodata = g->nodata;
+    uint8_t fillv[8];
+    or_gdal_copy_word(g->nodata, outType, fillv);
+    for (int64_t i = 0; i < (int64_t)dstXSize * dstYSize; i++) memcpy(buf + i * dsz, fillv, dsz);
+
+    /* per-row approximate transform + gather, warp.go:249-345 */
+    double *dx = (double *)malloc(sizeof(double) * 2 * (dstXSize > 0 ? dstXSize : 1));
+    double *dy = (double *)malloc(sizeof(double) * (dstXSize > 0 ? dstXSize : 1));
+    int *ok = (int *)malloc(sizeof(int) * (dstXSize > 0 ? dstXSize : 1));
+    for (int i = 0; i < dstXSize; i++) dx[dstXSize + i] = i + 0.5 + dstXOff;
+    const int has_nodata = g->nodata != -1e10;
+    for (int iy = 0; iy < dstYSize; iy++) {
+        memcpy(dx, dx + dstXSize, dstXSize * sizeof(double));
+        const double dfY = iy + 0.5 + dstYOff;
+        for (int i = 0; i < dstXSize; i++) dy[i] = dfY;
+        approx_transform(&t, 1, dstXSize, dx, dy, ok);
+        for (int i = 0; i < dstXSize; i++) {
+            if (!ok[i]) continue;
+            uint8_t *o = buf + ((int64_t)iy * dstXSize + i) * dsz;
+            if (resample == 1) {
+                double v;
+                if (!bilinear_sample(band, srcType, bandX, bandY, has_nodata, g->nodata, dx[i], dy[i], &v))
+                    continue;
+                if (outType == OR_FLOAT32) { float f = (float)v; memcpy(o, &f, 4); }
+                else or_gdal_copy_word(floor(v + 0.5), outType, o);
+                continue;
+            }
+            if (dx[i] < 0 || dy[i] < 0) continue;
+            if (dx[i] + 1.0e-10 >= 2147483647.0 || dy[i] + 1.0e-10 >= 2147483647.0) continue;
+            const int iSrcX = (int)(dx[i] + 1.0e-10);
+            const int iSrcY = (int)(dy[i] + 1.0e-10);
+            if (iSrcX >= bandX || iSrcY >= bandY) continue;
+            const int64_t sidx = (int64_t)iSrcY * bandX + iSrcX;
+            if (supported) memcpy(o, (const uint8_t *)band + sidx * dsz, dsz);
+            else or_gdal_copy_word(read_as_double(band, srcType, sidx), OR_FLOAT32, o);
+        }
+    }
+    free(dx); free(dy); free(ok);
+    bbox[0] = dstXOff; bbox[1] = dstYOff; bbox[2] = dstXSize; bbox[3] = dstYSize;
+    if (outType == OR_BYTE && g->signed_byte) outType = OR_SIGNEDBYTE;    /* 354-359 */
+    *dtype = outType;
+    *out_buf = buf;
+    return 0;
+}
+
+/* ======================================================================== */
+/* Tile pipeline for the CPU baseline                                       */
+/* ======================================================================== */
+typedef struct {
+    const oracle_granule *granules; const oracle_crs *src_crs;
+    const double *ts; const uint32_t *ph; const int32_t *ns;
+    const oracle_crs *dst; const oracle_tile *tiles; int n_tiles;
+    const int32_t *pair_granule; int resample;
+    int mask_ns; const char *mask_value; int mask_inclusive; int n_ns;
+    const oracle_scale_params *sp; const uint8_t *ramp; uint8_t *rgba_out;
+    int next; int err; pthread_mutex_t mu;
+} render_job;
+
+static int render_one(render_job *j, int ti) {
+    const oracle_tile *tile = &j->tiles[ti];
+    const int npairs = tile->pair_end - tile->pair_begin;
+    const int64_t npx = (int64_t)tile->width * tile->height;
+    oracle_flex_raster *fr = (oracle_flex_raster *)calloc(npairs > 0 ? npairs : 1, sizeof(*fr));
+    void **bufs = (void **)calloc(npairs > 0 ? npairs : 1, sizeof(void *));
+    int rc = 0;
+    for (int p = 0; p < npairs; p++) {
+        const int gi = j->pair_granule[tile->pair_begin + p];
+        int sz, dt, br; int32_t bb[4]; double nd;
+        rc = oracle_warp(&j->granules[gi], &j->src_crs[gi], j->dst, tile->dst_geot,
+                         tile->width, tile->height, j->resample, &bufs[p], &sz, bb, &nd, &dt, &br);
+        if (rc) goto out;
+        fr[p].data = bufs[p]; fr[p].data_w = bb[2]; fr[p].data_h = bb[3];
+        fr[p].width = tile->width; fr[p].height = tile->height;
+        fr[p].off_x = bb[0]; fr[p].off_y = bb[1]; fr[p].dtype = dt; fr[p].ns = j->ns[gi];
+        fr[p].nodata = nd; fr[p].timestamp = j->ts[gi]; fr[p].polygon_hash = j->ph[gi];
+    }
+    {
+        oracle_canvas cv[4];
+        void *cbuf[4];
+        memset(cv, 0, sizeof(cv));
+        for (int k = 0; k < j->n_ns; k++) { cbuf[k] = malloc((size_t)npx * 8); cv[k].data = cbuf[k]; }
+        const char *bt[1] = {NULL};
+        rc = oracle_merge_batch(fr, npairs, j->mask_ns, j->mask_value, bt, 0, j->mask_inclusive, cv, j->n_ns);
+        uint8_t *rgba = j->rgba_out + (int64_t)ti * npx * 4;
+        if (!rc) {
+            /* output namespaces exclude the mask layer */
+            const uint8_t *bands[3];
+            uint8_t *sb[3] = {NULL, NULL, NULL};
+            int nb = 0, missing = 0;
+            for (int k = 0; k < j->n_ns && nb < 3; k++) {
+                if (k == j->mask_ns) continue;
+                sb[nb] = (uint8_t *)malloc((size_t)npx);
+                if (!cv[k].created) { missing = 1; }
+                else oracle_scale(cv[k].data, cv[k].dtype, npx, cv[k].nodata, j->sp->offset,
+                                  j->sp->scale, j->sp->clip, j->sp->colour_scale, sb[nb]);
+                bands[nb] = sb[nb];
+                nb++;
+            }
+            if (missing) memset(rgba, 0, (size_t)npx * 4);
+            else rc = oracle_encode_rgba(bands, nb, tile->width, tile->height, j->ramp, rgba);
+            for (int k = 0; k < 3; k++) free(sb[k]);
+        }
+        for (int k = 0; k < j->n_ns; k++) free(cbuf[k]);
+    }
+out:
+    for (int p = 0; p < npairs; p++) free(bufs[p]);
+    free(bufs); free(fr);
+    return rc;
+}
+
+static void *render_worker(void *arg) {
+    render_job *j = (render_job *)arg;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        int ti = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (ti >= j->n_tiles) break;
+        int rc = render_one(j, ti);
+        if (rc) { pthread_mutex_lock(&j->mu); if (!j->err) j->err = rc; pthread_mutex_unlock(&j->mu); }
+    }
+    return NULL;
+}
+
+int oracle_render_tiles(const oracle_granule *granules, const oracle_crs *src_crs,
+                        const double *ts, const uint32_t *ph, const int32_t *ns,
+                        int n_granules, const oracle_crs *dst,
+                        const oracle_tile *tiles, int n_tiles,
+                        const int32_t *pair_granule, int resample,
+                        int mask_ns, const char *mask_value, int mask_inclusive,
+                        int n_ns, const oracle_scale_params *sp,
+                        const uint8_t *ramp, uint8_t *rgba_out, int n_threads) {
+    (void)n_granules;
+    if (n_ns > 4) return -7;
+    render_job j = {granules, src_crs, ts, ph, ns, dst, tiles, n_tiles, pair_granule, resample,
+                    mask_ns, mask_value, mask_inclusive, n_ns, sp, ramp, rgba_out, 0, 0,
+                    PTHREAD_MUTEX_INITIALIZER};
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads == 1) { render_worker(&j); return j.err; }
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * n_threads);
+    for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, render_worker, &j);
+    for (int i = 0; i < n_threads; i++) pthread_join(th[i], NULL);
+    free(th);
+    return j.err;
+}
+
+/* ======================================================================== */
+/* worker/gdalprocess/drill.go:90-227 readData                               */
+/* ======================================================================== */
+static void band_mean(const float *d, const uint8_t *mask, int npx, float nodata,
+                      float lo, float hi, int pixel_count, double *v, int32_t *c) {
+    float sum = 0.0f;
+    int32_t total = 0;
+    for (int i = 0; i < npx; i++) {                       /* 153-170 */
+        if (mask[i] == 255 && d[i] != nodata) {
+            const float val = d[i];
+            if (pixel_count != 0) total++;
+            if (val < lo || val > hi) continue;
+            if (pixel_count == 0) { sum += val; total++; }
+            else sum += 1.0f;
+        }
+    }
+    if (total > 0) { *v = (double)(sum / (float)total); *c = total; }   /* 172-177 */
+    else { *v = 0; *c = 0; }
+}
+
+int oracle_drill_read_data(const float *data, int nbands, int count_x, int count_y,
+                           const uint8_t *mask, float nodata, float clip_lower,
+                           float clip_upper, int pixel_count, int band_strides,
+                           double *out_value, int32_t *out_count) {
+    const int npx = count_x * count_y;
+    if (band_strides <= 0) band_strides = 1;             /* 110-112 */
+    int nrow = 0;
+    for (int ibBgn = 0; ibBgn < nbands; ibBgn += band_strides) {   /* 128 */
+        int ibEnd = ibBgn + band_strides;
+        if (ibEnd > nbands) ibEnd = nbands;
+        int bandsRead[2] = {ibBgn, ibEnd - 1};
+        const int eff = band_strides == 1 ? 1 : 2;
+        double bv[2]; int32_t bc[2];
+        for (int ib = 0; ib < eff; ib++)
+            band_mean(data + (int64_t)bandsRead[ib] * npx, mask, npx, nodata, clip_lower,
+                      clip_upper, pixel_count, &bv[ib], &bc[ib]);
+        out_value[nrow] = bv[0]; out_count[nrow] = bc[0]; nrow++;          /* 195 */
+        if (band_strides > 2 && eff > 1) {                                  /* 197-214 */
+            const double beta = (bv[1] - bv[0]) / (double)(band_strides - 1);
+            const double cnt = round((double)(bc[0] + bc[1]) / 2.0);
+            for (int ip = 1; ip < band_strides - 1; ip++) {
+                out_value[nrow] = bv[0] + (double)ip * beta;
+                out_count[nrow] = (int32_t)cnt;
+                nrow++;
+            }
+        }
+        if (eff > 1) { out_value[nrow] = bv[1]; out_count[nrow] = bc[1]; nrow++; }   /* 216-218 */
+    }
+    return nrow;
+}
+
+void oracle_drill_merge(const double *values, const int32_t *counts,
+                        int n_files, int n_dates, double *out) {
+    for (int d = 0; d < n_dates; d++) {                    /* drill_merger.go:79-93 */
+        double total = 0.0;
+        long count = 0;
+        for (int f = 0; f < n_files; f++) {
+            double v = values[(int64_t)f * n_dates + d];
+            if (!isnan(v)) { total += v * (double)counts[(int64_t)f * n_dates + d]; count += counts[(int64_t)f * n_dates + d]; }
+        }
+        out[d] = (!isnan(total) && count > 0) ? total / (double)count : NAN;
+    }
+}

@@ -1,0 +1,342 @@
+"""ctypes binding of the CPU oracle (oracle/gsky_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py as the checker.  The product (gsky_amd/) never
+imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+BYTE, UINT16, INT16, UINT32, INT32, FLOAT32, FLOAT64, SIGNEDBYTE = 1, 2, 3, 4, 5, 6, 7, 100
+NP_OF = {BYTE: np.uint8, UINT16: np.uint16, INT16: np.int16, UINT32: np.uint32,
+         INT32: np.int32, FLOAT32: np.float32, FLOAT64: np.float64, SIGNEDBYTE: np.int8}
+CODE_OF = {np.dtype(v): k for k, v in NP_OF.items() if k != SIGNEDBYTE}
+CODE_OF[np.dtype(np.int8)] = SIGNEDBYTE
+MAX_OVR = 12
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(_HERE, "gsky_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+class Crs(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("_pad", C.c_int32)] + [
+        (n, C.c_double) for n in ("a", "ra", "es", "e", "one_es", "lam0", "phi0", "phi1",
+                                  "phi2", "x0", "y0", "k0", "n", "c", "dd", "rho0", "ec")]
+
+
+class Granule(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("dtype", C.c_int32), ("xsize", C.c_int32),
+                ("ysize", C.c_int32), ("signed_byte", C.c_int32), ("geot", C.c_double * 6),
+                ("nodata", C.c_double), ("n_ovr", C.c_int32), ("_pad", C.c_int32),
+                ("ovr_data", C.c_void_p * MAX_OVR), ("ovr_xsize", C.c_int32 * MAX_OVR),
+                ("ovr_ysize", C.c_int32 * MAX_OVR)]
+
+
+class FlexRaster(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("data_w", C.c_int32), ("data_h", C.c_int32),
+                ("width", C.c_int32), ("height", C.c_int32), ("off_x", C.c_int32),
+                ("off_y", C.c_int32), ("dtype", C.c_int32), ("ns", C.c_int32),
+                ("nodata", C.c_double), ("timestamp", C.c_double),
+                ("polygon_hash", C.c_uint32), ("_pad", C.c_int32)]
+
+
+class Canvas(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("created", C.c_int32), ("dtype", C.c_int32),
+                ("nodata", C.c_double), ("timestamp", C.c_double)]
+
+
+class Tile(C.Structure):
+    _fields_ = [("dst_geot", C.c_double * 6), ("width", C.c_int32), ("height", C.c_int32),
+                ("pair_begin", C.c_int32), ("pair_end", C.c_int32)]
+
+
+class ScaleParams(C.Structure):
+    _fields_ = [("offset", C.c_double), ("scale", C.c_double), ("clip", C.c_double),
+                ("colour_scale", C.c_int32), ("_pad", C.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = C.CDLL(build())
+        L = _lib
+        vp, i32, i64, d = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+        L.oracle_scale.argtypes = [vp, C.c_int, i64, d, d, d, d, C.c_int, vp]
+        L.oracle_scale_legacy.argtypes = [vp, C.c_int, i64, d, d, d, d, vp]
+        L.oracle_gradient_palette.argtypes = [vp, C.c_int, C.c_int, vp]
+        L.oracle_encode_rgba.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, vp]
+        L.oracle_fnv32a.argtypes = [C.c_char_p, C.c_size_t]
+        L.oracle_fnv32a.restype = C.c_uint32
+        L.oracle_compute_mask.argtypes = [vp, C.c_int, i64, C.c_char_p, vp, C.c_int, vp]
+        L.oracle_merge_batch.argtypes = [vp, C.c_int, C.c_int, C.c_char_p, vp, C.c_int,
+                                         C.c_int, vp, C.c_int]
+        L.oracle_crs_init.argtypes = [vp, C.c_char_p]
+        L.oracle_crs_transform.argtypes = [vp, vp, C.POINTER(d), C.POINTER(d)]
+        L.oracle_warp.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp,
+                                  C.POINTER(C.c_int), vp, C.POINTER(d), C.POINTER(C.c_int),
+                                  C.POINTER(C.c_int)]
+        L.oracle_suggested_warp_output.argtypes = [vp, vp, vp, vp, vp, vp, C.POINTER(C.c_int),
+                                                   C.POINTER(C.c_int), vp]
+        L.oracle_approx_row.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, vp]
+        L.oracle_render_tiles.argtypes = [vp, vp, vp, vp, vp, C.c_int, vp, vp, C.c_int, vp,
+                                          C.c_int, C.c_int, C.c_char_p, C.c_int, C.c_int, vp,
+                                          vp, vp, C.c_int]
+        L.oracle_drill_read_data.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, C.c_float,
+                                             C.c_float, C.c_float, C.c_int, C.c_int, vp, vp]
+        L.oracle_drill_merge.argtypes = [vp, vp, C.c_int, C.c_int, vp]
+        L.or_go_f64_u8.argtypes = [d]
+        L.or_go_f64_u8.restype = C.c_uint8
+        L.or_go_f64_i16.argtypes = [d]
+        L.or_go_f64_i16.restype = C.c_int16
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def dtype_code(a: np.ndarray, signed_byte: bool = False) -> int:
+    if a.dtype == np.int8 or signed_byte:
+        return SIGNEDBYTE
+    return CODE_OF[a.dtype]
+
+
+# ---------------------------------------------------------------- scale / palette
+def scale(data: np.ndarray, nodata: float, offset: float, scale_: float, clip: float,
+          colour_scale: int = 0) -> np.ndarray:
+    """utils.scale (raster_scaler.go:30-332).  Byte input is scaled in place
+    by the reference; here a copy is scaled so the caller's array is kept."""
+    d = np.ascontiguousarray(data).copy()
+    out = np.zeros(d.size, np.uint8)
+    rc = lib().oracle_scale(_ptr(d), dtype_code(d), d.size, nodata, offset, scale_, clip,
+                            colour_scale, _ptr(out))
+    if rc:
+        raise ValueError("Raster type not implemented")
+    return out.reshape(data.shape)
+
+
+def scale_legacy(data, nodata, offset, scale_, clip):
+    d = np.ascontiguousarray(data).copy()
+    out = np.zeros(d.size, np.uint8)
+    if lib().oracle_scale_legacy(_ptr(d), dtype_code(d), d.size, nodata, offset, scale_, clip, _ptr(out)):
+        raise ValueError("Raster type not implemented")
+    return out.reshape(data.shape)
+
+
+def gradient_palette(colours, interpolate: bool) -> np.ndarray:
+    c = np.ascontiguousarray(np.asarray(colours, np.uint8).reshape(-1, 4))
+    ramp = np.zeros((256, 4), np.uint8)
+    if lib().oracle_gradient_palette(_ptr(c), len(c), int(bool(interpolate)), _ptr(ramp)):
+        raise ValueError("bad palette")
+    return ramp
+
+
+def encode_rgba(bands, w, h, ramp=None) -> np.ndarray:
+    bs = [np.ascontiguousarray(b, np.uint8).reshape(-1) for b in bands]
+    arr = (C.c_void_p * len(bs))(*[b.ctypes.data for b in bs])
+    out = np.zeros((h, w, 4), np.uint8)
+    rp = _ptr(np.ascontiguousarray(ramp, np.uint8)) if ramp is not None else None
+    if lib().oracle_encode_rgba(arr, len(bs), w, h, rp, _ptr(out)):
+        raise ValueError("Cannot encode other than 1 or 3 namespaces")
+    return out
+
+
+def fnv32a(s: str) -> int:
+    b = s.encode()
+    return lib().oracle_fnv32a(b, len(b))
+
+
+def compute_mask(data: np.ndarray, value=None, bit_tests=(), signed_byte=False) -> np.ndarray:
+    d = np.ascontiguousarray(data)
+    out = np.zeros(d.size, np.uint8)
+    bt = [s.encode() for s in bit_tests]
+    arr = (C.c_char_p * max(1, len(bt)))(*bt) if bt else None
+    rc = lib().oracle_compute_mask(_ptr(d), dtype_code(d, signed_byte), d.size,
+                                   value.encode() if value else None,
+                                   C.cast(arr, C.c_void_p) if arr else None, len(bt), _ptr(out))
+    if rc:
+        raise ValueError("ComputeMask error %d" % rc)
+    return out.reshape(data.shape).astype(bool)
+
+
+def merge_batch(rasters, n_ns, width, height, mask_ns=-1, mask_value=None, bit_tests=(),
+                mask_inclusive=False):
+    """RasterMerger.Run over one batch.  rasters: list of dicts with keys
+    data (2-D window array), off_x, off_y, nodata, timestamp, polygon_hash, ns
+    and optional signed_byte.  Returns list of (canvas array or None, nodata)."""
+    keep = []
+    fr = (FlexRaster * max(1, len(rasters)))()
+    for i, r in enumerate(rasters):
+        d = np.ascontiguousarray(r["data"])
+        keep.append(d)
+        fr[i].data = d.ctypes.data
+        fr[i].data_h, fr[i].data_w = d.shape
+        fr[i].width, fr[i].height = width, height
+        fr[i].off_x, fr[i].off_y = r["off_x"], r["off_y"]
+        fr[i].dtype = dtype_code(d, r.get("signed_byte", False))
+        fr[i].ns = r["ns"]
+        fr[i].nodata = r["nodata"]
+        fr[i].timestamp = r["timestamp"]
+        fr[i].polygon_hash = r["polygon_hash"]
+    bufs = [np.zeros(width * height * 8, np.uint8) for _ in range(n_ns)]
+    cv = (Canvas * n_ns)()
+    for k in range(n_ns):
+        cv[k].data = bufs[k].ctypes.data
+    bt = [s.encode() for s in bit_tests]
+    arr = (C.c_char_p * max(1, len(bt)))(*bt) if bt else None
+    rc = lib().oracle_merge_batch(fr, len(rasters), mask_ns,
+                                  mask_value.encode() if mask_value else None,
+                                  C.cast(arr, C.c_void_p) if arr else None, len(bt),
+                                  int(mask_inclusive), cv, n_ns)
+    if rc:
+        raise ValueError("merge error %d" % rc)
+    out = []
+    for k in range(n_ns):
+        if not cv[k].created:
+            out.append((None, None))
+            continue
+        dt = NP_OF[cv[k].dtype]
+        a = bufs[k].view(dt)[: width * height].reshape(height, width).copy()
+        out.append((a, cv[k].nodata))
+    return out
+
+
+# ---------------------------------------------------------------- projections / warp
+def crs(spec: str) -> Crs:
+    c = Crs()
+    if lib().oracle_crs_init(C.byref(c), spec.encode()):
+        raise ValueError("unsupported CRS %r" % spec)
+    return c
+
+
+def crs_transform(src: Crs, dst: Crs, x: float, y: float):
+    xx, yy = C.c_double(x), C.c_double(y)
+    ok = lib().oracle_crs_transform(C.byref(src), C.byref(dst), C.byref(xx), C.byref(yy))
+    return (xx.value, yy.value) if ok else None
+
+
+def make_granule(data: np.ndarray, geot, nodata=-1e10, overviews=(), signed_byte=False):
+    g = Granule()
+    d = np.ascontiguousarray(data)
+    g.data = d.ctypes.data
+    g.dtype = dtype_code(d, signed_byte)
+    if d.dtype == np.int8:
+        g.dtype = BYTE
+        signed_byte = True
+    g.signed_byte = int(signed_byte)
+    g.ysize, g.xsize = d.shape
+    for i in range(6):
+        g.geot[i] = geot[i]
+    g.nodata = nodata
+    keep = [d]
+    g.n_ovr = len(overviews)
+    for i, o in enumerate(overviews):
+        o = np.ascontiguousarray(o, d.dtype)
+        keep.append(o)
+        g.ovr_data[i] = o.ctypes.data
+        g.ovr_ysize[i], g.ovr_xsize[i] = o.shape
+    g._keep = keep
+    return g
+
+
+def warp(g: Granule, src: Crs, dst, dst_geot, w, h, resample=0):
+    """warp_operation_fast restated; returns (window array, bbox, nodata, dtype)."""
+    buf = C.c_void_p()
+    size = C.c_int()
+    bbox = np.zeros(4, np.int32)
+    nd = C.c_double()
+    dt = C.c_int()
+    br = C.c_int()
+    gt = np.ascontiguousarray(dst_geot, np.float64)
+    rc = lib().oracle_warp(C.byref(g), C.byref(src), C.byref(dst) if dst is not None else None,
+                           _ptr(gt), w, h, resample, C.byref(buf), C.byref(size), _ptr(bbox),
+                           C.byref(nd), C.byref(dt), C.byref(br))
+    if rc:
+        raise RuntimeError("warp_operation() fail: %d" % rc)
+    npdt = NP_OF[dt.value]
+    arr = np.frombuffer(C.string_at(buf, size.value), dtype=npdt).copy()
+    C.CDLL(None).free(buf)
+    arr = arr.reshape(int(bbox[3]), int(bbox[2]))
+    return arr, bbox.copy(), nd.value, dt.value
+
+
+def suggested_warp_output(g: Granule, src: Crs, dst: Crs, dst_geot):
+    gt = np.ascontiguousarray(dst_geot, np.float64)
+    out = np.zeros(6)
+    ext = np.zeros(4)
+    np_, nl = C.c_int(), C.c_int()
+    rc = lib().oracle_suggested_warp_output(C.byref(g), C.byref(src), C.byref(dst), None,
+                                            _ptr(gt), _ptr(out), C.byref(np_), C.byref(nl),
+                                            _ptr(ext))
+    return rc, out, np_.value, nl.value, ext
+
+
+def render_tiles(granules, src_crs, ts, ph, ns, dst, tiles_geot, width, height, pairs,
+                 scale_params, ramp=None, n_ns=1, mask_ns=-1, mask_value=None,
+                 mask_inclusive=False, resample=0, n_threads=1):
+    """CPU baseline of the whole tile path.  pairs: list (per tile) of granule
+    index lists.  Returns (n_tiles, h, w, 4) uint8."""
+    ng = len(granules)
+    garr = (Granule * ng)(*granules)
+    carr = (Crs * ng)(*src_crs)
+    ts = np.ascontiguousarray(ts, np.float64)
+    ph = np.ascontiguousarray(ph, np.uint32)
+    nsa = np.ascontiguousarray(ns, np.int32)
+    nt = len(tiles_geot)
+    tarr = (Tile * nt)()
+    flat = []
+    for i in range(nt):
+        for k in range(6):
+            tarr[i].dst_geot[k] = tiles_geot[i][k]
+        tarr[i].width, tarr[i].height = width, height
+        tarr[i].pair_begin = len(flat)
+        flat.extend(pairs[i])
+        tarr[i].pair_end = len(flat)
+    pg = np.ascontiguousarray(flat if flat else [0], np.int32)
+    sp = ScaleParams(*scale_params[:3], int(scale_params[3]) if len(scale_params) > 3 else 0, 0)
+    out = np.zeros((nt, height, width, 4), np.uint8)
+    rp = _ptr(np.ascontiguousarray(ramp, np.uint8)) if ramp is not None else None
+    rc = lib().oracle_render_tiles(garr, carr, _ptr(ts), _ptr(ph), _ptr(nsa), ng, C.byref(dst),
+                                   tarr, nt, _ptr(pg), resample, mask_ns,
+                                   mask_value.encode() if mask_value else None,
+                                   int(mask_inclusive), n_ns, C.byref(sp), rp, _ptr(out),
+                                   n_threads)
+    if rc:
+        raise RuntimeError("render error %d" % rc)
+    return out
+
+
+def drill_read_data(data, mask, nodata, clip_lower, clip_upper, pixel_count=0, band_strides=1):
+    d = np.ascontiguousarray(data, np.float32)
+    nb, cy, cx = d.shape
+    m = np.ascontiguousarray(mask, np.uint8)
+    cap = nb * max(1, band_strides) + 4
+    v = np.zeros(cap)
+    c = np.zeros(cap, np.int32)
+    n = lib().oracle_drill_read_data(_ptr(d), nb, cx, cy, _ptr(m), nodata, clip_lower,
+                                     clip_upper, pixel_count, band_strides, _ptr(v), _ptr(c))
+    return v[:n].copy(), c[:n].copy()
+
+
+def drill_merge(values, counts):
+    v = np.ascontiguousarray(values, np.float64)
+    c = np.ascontiguousarray(counts, np.int32)
+    nf, nd = v.shape
+    out = np.zeros(nd)
+    lib().oracle_drill_merge(_ptr(v), _ptr(c), nf, nd, _ptr(out))
+    return out

@@ -1,0 +1,334 @@
+"""GPU parity tests: the MI355X path (libgskyhip.so through its C-ABI) against
+the CPU oracle on the same seeded inputs.
+
+Bars (BASELINE.json north_star): scale, palette, merge, mask, drill -- bit
+exact; nearest-neighbour warp and the fused tile path >= 99.99 % pixel
+identical (fp64 transcendental ULPs of the GPU math library vs glibc are the
+only admitted difference); bilinear within 1e-4 relative.
+"""
+import numpy as np
+import pytest
+
+from gsky_amd import synth
+
+from .helpers import gpu_batch, identity, oracle_inputs, oracle_render
+
+pytestmark = pytest.mark.gpu
+
+NN_IDENTITY = 0.9999
+BILINEAR_RTOL = 1e-4
+TYPES = [np.uint8, np.int8, np.int16, np.uint16, np.float32]
+
+
+def _rand(dt, n, rng):
+    if dt == np.float32:
+        v = rng.normal(300, 400, n).astype(np.float32)
+        v[rng.random(n) < 0.05] = -9999.0
+        v[rng.random(n) < 0.01] = np.nan
+        v[:3] = [0.0, -0.0, 1e30]
+        return v
+    info = np.iinfo(dt)
+    v = rng.integers(info.min, int(info.max) + 1, n).astype(dt)
+    return v
+
+
+SCALE_PARAMS = [(0, 0, 0), (0, 0, 1000), (1, 1, 1000), (3, 2, 2), (-5, 0.5, 300), (0, 0, 10000),
+                (100.5, 0, 254), (0, 3.5, 0), (-1e3, 0, 70000)]
+
+
+@pytest.mark.parametrize("dt", TYPES)
+@pytest.mark.parametrize("sp", SCALE_PARAMS)
+def test_scale_parity(gpu, oracle, dt, sp):
+    import torch
+
+    import gsky_amd
+    rng = np.random.default_rng(hash((dt.__name__, sp)) & 0xFFFF)
+    n = 100003
+    data = _rand(dt, n, rng)
+    nodata = -9999.0 if dt == np.float32 else float(data[17])
+    for first_valid in (True, False):
+        d = data.copy()
+        if not first_valid:
+            d[0] = d[17] if dt != np.float32 else np.float32(-9999.0)
+        exp = oracle.scale(d, nodata, *sp)
+        t = torch.from_numpy(d).to(gpu)
+        tname = "SignedByte" if dt == np.int8 else None
+        got = gsky_amd.scale([t], [nodata], gsky_amd.ScaleParams(*sp), [tname] if tname else None)[0]
+        assert np.array_equal(got.cpu().numpy(), exp), (dt, sp, first_valid)
+
+
+def test_scale_log_parity(gpu, oracle):
+    import torch
+
+    import gsky_amd
+    rng = np.random.default_rng(7)
+    d = rng.lognormal(2, 2, 50000).astype(np.float32)
+    d[::97] = 0.0
+    d[::101] = -3.0
+    d[::103] = -9999.0
+    for sp in [(0, 0, 0, 1), (0, 1, 5, 1), (1, 20, 6, 1), (0, 0, 0, 2)]:
+        exp = oracle.scale(d, -9999.0, sp[0], sp[1], sp[2], colour_scale=sp[3])
+        got = gsky_amd.scale([torch.from_numpy(d).to(gpu)], [-9999.0], gsky_amd.ScaleParams(*sp))[0]
+        assert np.array_equal(got.cpu().numpy(), exp), sp
+
+
+@pytest.mark.parametrize("dt", [np.uint8, np.int16, np.uint16, np.float32])
+def test_scale_legacy_parity(gpu, oracle, dt):
+    import torch
+
+    import gsky_amd
+    rng = np.random.default_rng(3)
+    d = _rand(dt, 20000, rng)
+    for sp in [(0, 0.5, 200), (2, 1.5, 1000)]:
+        exp = oracle.scale_legacy(d, -9999.0 if dt == np.float32 else 7, *sp)
+        got = gsky_amd.scale_legacy(torch.from_numpy(d.copy()).to(gpu), -9999.0 if dt == np.float32 else 7,
+                                    gsky_amd.ScaleParams(*sp))
+        assert np.array_equal(got.cpu().numpy(), exp)
+
+
+def test_palette_and_rgba_parity(gpu, oracle):
+    import torch
+
+    import gsky_amd
+    rng = np.random.default_rng(11)
+    for n in (2, 3, 5, 7, 13, 200, 300):
+        cols = rng.integers(0, 256, (n, 4)).astype(np.uint8)
+        for interp in (True, False):
+            if interp and n > 257:   # sectionLength 0: the reference panics (palette.go:12)
+                continue
+            exp = oracle.gradient_palette(cols, interp)
+            got = gsky_amd.gradient_rgba_palette(gsky_amd.Palette(cols.tolist(), interp))
+            assert np.array_equal(got, exp)
+    b = [rng.integers(0, 256, (123, 77)).astype(np.uint8) for _ in range(3)]
+    for bb in b:
+        bb[rng.random(bb.shape) < 0.3] = 255
+    pal = gsky_amd.Palette(synth.PALETTE_GSKY, True)
+    ramp = oracle.gradient_palette(synth.PALETTE_GSKY, True)
+    cases = [([b[0]], pal, ramp), ([b[0]], None, None), (b, None, None)]
+    for bands, p, r in cases:
+        exp = oracle.encode_rgba(bands, 77, 123, r)
+        got = gsky_amd.encode_rgba([torch.from_numpy(x).to(gpu) for x in bands], p)
+        assert np.array_equal(got.cpu().numpy(), exp)
+
+
+MASKS = [("00000001", ()), ("110", ()), ("11111111", ()), ("", ("1", "1", "110", "10")),
+         ("1000000000000000", ()), ("-1", ()), ("", ("11111111", "-1"))]
+
+
+@pytest.mark.parametrize("dt", [np.uint8, np.int8, np.int16, np.uint16])
+@pytest.mark.parametrize("mv", MASKS)
+def test_compute_mask_parity(gpu, oracle, dt, mv):
+    import torch
+
+    import gsky_amd
+    rng = np.random.default_rng(5)
+    d = _rand(dt, 4096, rng)
+    value, tests = mv
+    exp = oracle.compute_mask(d, value or None, tests)
+    tname = "SignedByte" if dt == np.int8 else None
+    got = gsky_amd.compute_mask(gsky_amd.Mask("qa", value, list(tests)), torch.from_numpy(d).to(gpu), tname)
+    assert np.array_equal(got.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_merge_parity(gpu, oracle, seed):
+    """RasterMerger.Run: random windows, timestamps, polygon hashes, masks."""
+    import torch
+
+    import gsky_amd
+    rng = np.random.default_rng(seed)
+    W, H = 97, 61
+    dt = [np.int16, np.float32, np.uint8, np.uint16, np.int8, np.int16][seed]
+    tname = {np.int16: "Int16", np.float32: "Float32", np.uint8: "Byte", np.uint16: "UInt16",
+             np.int8: "SignedByte"}[dt]
+    n = 9
+    nodata = -9999.0 if dt == np.float32 else (0.0 if dt in (np.uint8, np.uint16) else -1.0)
+    polys = ["A", "B", "C"]
+    rasters_o, rasters_g = [], []
+    use_mask = seed % 2 == 1
+    for k in range(n):
+        w, h = int(rng.integers(1, W)), int(rng.integers(1, H))
+        ox, oy = int(rng.integers(0, W - w + 1)), int(rng.integers(0, H - h + 1))
+        d = _rand(dt, w * h, rng).reshape(h, w)
+        d[rng.random((h, w)) < 0.3] = nodata if dt != np.float32 else -9999.0
+        ts = float(rng.integers(0, 4)) * 86400.0
+        pg = polys[int(rng.integers(0, 3))]
+        ns = "" if rng.random() < 0.8 else "b2"
+        rasters_o.append(dict(data=d, off_x=ox, off_y=oy, nodata=nodata, timestamp=ts,
+                              polygon_hash=oracle.fnv32a(pg), ns=0 if ns == "" else 1,
+                              signed_byte=dt == np.int8))
+        rasters_g.append(gsky_amd.FlexRaster(torch.from_numpy(d).to(gpu), W, H, ox, oy, tname, nodata, ns, ts, pg))
+        if use_mask:
+            q = rng.integers(0, 4, (h, w)).astype(np.uint8)
+            rasters_o.append(dict(data=q, off_x=ox, off_y=oy, nodata=255.0, timestamp=ts,
+                                  polygon_hash=oracle.fnv32a(pg), ns=2))
+            rasters_g.append(gsky_amd.FlexRaster(torch.from_numpy(q).to(gpu), W, H, ox, oy, "Byte", 255.0, "qa",
+                                                 ts, pg))
+    mask = gsky_amd.Mask("qa", "01") if use_mask else None
+    exp = oracle.merge_batch(rasters_o, 3, W, H, mask_ns=2 if use_mask else -1,
+                             mask_value="01" if use_mask else None)
+    got = gsky_amd.raster_merger_run(rasters_g, ["", "b2"], mask)
+    for k, ns in enumerate(["", "b2"]):
+        e = exp[k]
+        g = got[ns]
+        if e[0] is None:
+            assert g is None
+            continue
+        assert g is not None and g[1] == e[1]
+        ga = g[0].cpu().numpy()
+        if dt == np.float32:
+            assert np.array_equal(ga.view(np.uint32), e[0].astype(np.float32).view(np.uint32))
+        else:
+            assert np.array_equal(ga, e[0])
+
+
+# ---------------------------------------------------------------- warp / render
+def _check_windows(O, cfg, batch, resample=0):
+    gr, crs, ts, ph, ns, geots, slots, mask_ns = oracle_inputs(O, cfg)
+    wins = batch.warp_windows(resample)
+    p = 0
+    tot = same = 0
+    for t, (bb, w, h) in enumerate(cfg.tiles):
+        for gi in cfg.pairs[t]:
+            arr, bbox, nd, dt = O.warp(gr[gi], crs[gi], O.crs(cfg.dst_srs), geots[t], w, h, resample)
+            g_arr, g_bbox, g_type, g_nd = wins[p]
+            p += 1
+            assert list(bbox) == g_bbox, (t, gi)
+            ga = g_arr.cpu().numpy()
+            if resample == 1:
+                a64, g64 = arr.astype(np.float64), ga.astype(np.float64)
+                close = np.isclose(g64, a64, rtol=BILINEAR_RTOL, atol=0) | (a64 == g64)
+                same += int(close.sum())
+            else:
+                same += int((ga.view(np.uint8) == arr.view(np.uint8)).reshape(ga.shape[0], ga.shape[1], -1).all(-1).sum())
+            tot += ga.size
+    return same / max(1, tot)
+
+
+def test_warp_windows_c1(gpu, oracle):
+    cfg = synth.config_c1(scale=0.5)
+    frac = _check_windows(oracle, cfg, gpu_batch(cfg))
+    assert frac >= NN_IDENTITY
+
+
+def test_warp_windows_c2_small(gpu, oracle):
+    cfg = synth.config_c2(scale=0.05, tiles_per_side=3, tile_px=128)
+    frac = _check_windows(oracle, cfg, gpu_batch(cfg))
+    assert frac >= NN_IDENTITY
+
+
+def test_warp_windows_bilinear_c3_small(gpu, oracle):
+    cfg = synth.config_c3(scale=0.05, chunk_px=96, out_px=288, grid=3)
+    frac = _check_windows(oracle, cfg, gpu_batch(cfg), resample=1)
+    assert frac >= NN_IDENTITY
+
+
+def test_render_c1(gpu, oracle):
+    import gsky_amd
+    cfg = synth.config_c1(scale=1.0)
+    b = gpu_batch(cfg)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale)).cpu().numpy()
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg)
+    assert identity(got, exp) >= NN_IDENTITY
+
+
+def test_render_c2_small(gpu, oracle):
+    import gsky_amd
+    cfg = synth.config_c2(scale=0.1, tiles_per_side=4, tile_px=256)
+    b = gpu_batch(cfg)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True)).cpu().numpy()
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg)
+    assert identity(got, exp) >= NN_IDENTITY
+    assert (exp[..., 3] > 0).mean() > 0.3      # the test exercises real data
+
+
+def test_render_auto_scale(gpu, oracle):
+    import gsky_amd
+    cfg = synth.config_c2(scale=0.05, tiles_per_side=3, tile_px=128)
+    cfg.scale = (0.0, 0.0, 0.0, 0)
+    b = gpu_batch(cfg)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True)).cpu().numpy()
+    exp = oracle_render(oracle, cfg)
+    assert identity(got, exp) >= NN_IDENTITY
+
+
+def test_render_c5_small_masks_overviews(gpu, oracle):
+    import gsky_amd
+    cfg = synth.config_c5(scale=0.05, dates=2, zooms=((4, 11, 8, 2), (5, 22, 16, 3)), tile_px=128)
+    b = gpu_batch(cfg)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale)).cpu().numpy()
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg)
+    assert identity(got, exp) >= NN_IDENTITY
+    assert (exp[..., 3] > 0).mean() > 0.05
+
+
+def test_render_c3_small_bilinear_canvas(gpu, oracle):
+    import gsky_amd
+    cfg = synth.config_c3(scale=0.05, chunk_px=96, out_px=288, grid=3)
+    b = gpu_batch(cfg)
+    cfg.scale = (0.0, 1.0, 255.0, 0)   # byte = trunc(value): grey image of the float mosaic
+    rgba, cv = b.render(gsky_amd.ScaleParams(*cfg.scale), resample=1, canvas=True)
+    exp = oracle_render(oracle, cfg)
+    assert identity(rgba.cpu().numpy(), exp) >= 0.999
+
+
+def test_warp_operation_fast_dropin(gpu, oracle):
+    """warp.go:82 drop-in through the worker mirror (WarpRaster)."""
+    import torch
+
+    from gsky_amd import worker
+    from gsky_amd.tiles import bbox_to_geot
+    cfg = synth.config_c2(scale=0.1, tiles_per_side=4, tile_px=256)
+    g = cfg.granules[5]
+    worker.register_granule("/g/data/c2/g5.tif", 1, torch.from_numpy(g.data).to(gpu), g.geot, "EPSG:3577",
+                            g.nodata)
+    bb, w, h = cfg.tiles[5]
+    dst_gt = bbox_to_geot(w, h, bb)
+    res = worker.warp_raster(worker.GeoRPCGranule(path="/g/data/c2/g5.tif", bands=[1], width=w, height=h,
+                                                  dstSRS="EPSG:3857", dstGeot=dst_gt))
+    assert res.error == "OK", res.error
+    og = oracle.make_granule(g.data, g.geot, g.nodata)
+    arr, bbox, nd, dt = oracle.warp(og, oracle.crs("EPSG:3577"), oracle.crs("EPSG:3857"), dst_gt, w, h)
+    assert res.raster.bbox == list(bbox) and res.raster.rasterType == "Int16" and res.raster.noData == nd
+    got = worker.raster_array(res.raster)
+    assert identity(got, arr) >= NN_IDENTITY
+    bad = worker.warp_raster(worker.GeoRPCGranule(path="/nope", bands=[1], width=w, height=h,
+                                                  dstSRS="EPSG:3857", dstGeot=dst_gt))
+    assert bad.error == "warp_operation() fail: 1"
+    worker.unregister_all()
+
+
+# ---------------------------------------------------------------- drill
+@pytest.mark.parametrize("strides,pc,clip", [(1, 0, (-1e30, 1e30)), (1, 1, (0.21, 0.26)), (3, 0, (0.2, 0.3)),
+                                             (2, 0, (-1e30, 1e30))])
+def test_drill_parity(gpu, oracle, strides, pc, clip):
+    import torch
+
+    from gsky_amd import drill
+    dc = synth.config_c4(n_bands=37, size=256, n_polys=12, rmin=4, rmax=40)
+    st = drill.DrillStack(torch.from_numpy(dc.bands), dc.nodata, gpu)
+    win, off, masks = drill.pack_masks(dc.windows, dc.masks, gpu)
+    vals, cnts = drill.read_data(st, win, off, masks, clip[0], clip[1], pc, strides)
+    vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
+    for p, (x0, y0, w, h) in enumerate(dc.windows):
+        sub = dc.bands[:, y0:y0 + h, x0:x0 + w]
+        ev, ec = oracle.drill_read_data(sub, dc.masks[p], dc.nodata, clip[0], clip[1], pc, strides)
+        assert np.array_equal(cnts[p], ec), p
+        assert np.array_equal(vals[p].view(np.uint64), ev.view(np.uint64)), p   # bit exact
+
+
+def test_drill_merge_parity(gpu, oracle):
+    import torch
+
+    from gsky_amd import drill
+    rng = np.random.default_rng(2)
+    v = rng.normal(0.3, 0.1, (5, 365))
+    v[rng.random(v.shape) < 0.1] = np.nan
+    c = rng.integers(0, 1000, v.shape).astype(np.int32)
+    exp = oracle.drill_merge(v, c)
+    got = drill.drill_merge(torch.from_numpy(v).to(gpu), torch.from_numpy(c).to(gpu)).cpu().numpy()
+    assert np.array_equal(np.isnan(exp), np.isnan(got))
+    assert np.allclose(got[~np.isnan(got)], exp[~np.isnan(exp)], rtol=0, atol=0)
