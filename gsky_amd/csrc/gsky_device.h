@@ -310,10 +310,23 @@ struct TilePlan {
   int32_t n_entries;          // pairs merged (in order[] slots)
   int32_t status;
   int32_t complex;            // some row needs exact transforms at render time
-  int32_t _pad;
+  int32_t vt;                 // common value type of every entry (0: mixed -> general kernel)
   int32_t created[4];
   int32_t dtype[4];
   double nodata[4];           // canvas NoData (first raster of the ns)
+};
+
+// Render-time descriptor of one pair (indexed by pair), written by
+// plan_tiles_kernel: everything the fused kernel reads per (row, pair).
+struct EntryD {
+  const void *band;
+  int32_t band_x, band_y;
+  int32_t xoff, yoff, w, h;
+  int32_t ns, fill_mode, mask_pair, src_dtype;
+  int32_t out_dtype, has_nodata;
+  Val nd, fill;               // Go T(r.NoData) of the merge; GDALCopyWords window fill
+  double nodata64;
+  int64_t row_base;           // pair * max_h (index of row 0 in the row records)
 };
 
 // Row record of the approximate transformer for one window row.

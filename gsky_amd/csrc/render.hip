@@ -17,6 +17,7 @@
 #include "render.h"
 #include "stages.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace gsky {
 
@@ -45,6 +46,7 @@ struct PlanArgs {
   int pool_cap;
   int64_t *split_list;         // (pair * max_h + row) of rows that need the recursion
   int32_t *complex_list;       // tiles that need exact per-pixel transforms
+  EntryD *entries;             // n_pairs render descriptors
 };
 
 // ---------------------------------------------------------------- pair ownership
@@ -283,7 +285,7 @@ __global__ void plan_tiles_kernel(PlanArgs a) {
   tp.n_entries = 0;
   tp.status = 0;
   tp.complex = 0;
-  tp._pad = 0;
+  tp.vt = 0;
   double canvas_ts[4];
   for (int k = 0; k < 4; k++) { tp.created[k] = 0; tp.dtype[k] = 0; tp.nodata[k] = 0; canvas_ts[k] = 0; }
   const int b = tile.pair_begin, e = tile.pair_end;
@@ -327,6 +329,35 @@ __global__ void plan_tiles_kernel(PlanArgs a) {
     }
     pp.fill_mode = pp.ts < canvas_ts[ns] ? 1 : 0;  // tile_merger.go:47
     if (!pp.fill_mode) canvas_ts[ns] = pp.ts;
+  }
+  // render descriptors of every pair of the tile (mask pairs included)
+  int vt = -1;
+  for (int p = b; p < e; p++) {
+    const PairPlan &pp = a.pairs[p];
+    EntryD d;
+    d.band = pp.band;
+    d.band_x = pp.band_x; d.band_y = pp.band_y;
+    d.xoff = pp.xoff; d.yoff = pp.yoff; d.w = pp.w; d.h = pp.h;
+    d.ns = pp.ns; d.fill_mode = pp.fill_mode; d.mask_pair = pp.mask_pair; d.src_dtype = pp.src_dtype;
+    d.out_dtype = pp.out_dtype; d.has_nodata = pp.has_nodata;
+    d.nd = go_conv_to(pp.nodata, pp.out_dtype);
+    d.fill = pp.fill;
+    d.nodata64 = pp.nodata;
+    d.row_base = (int64_t)p * a.max_h;
+    a.entries[p] = d;
+    if (!pp.in_stack) continue;
+    // the typed fast path needs one value type and no GDALCopyWords promotion
+    const bool same = pp.src_dtype == pp.out_dtype ||
+                      (pp.src_dtype == GSKYHIP_BYTE && pp.out_dtype == GSKYHIP_SIGNEDBYTE);
+    if (!same) vt = 0;
+    else if (vt < 0) vt = pp.out_dtype;
+    else if (vt != pp.out_dtype) vt = 0;
+  }
+  tp.vt = vt < 0 ? 0 : vt;
+  if (n > 0 && tp.vt == 0) {
+    tp.complex = 1;
+    const int k = atomicAdd(&a.counters[2], 1);
+    a.complex_list[k] = t;
   }
   a.tplans[t] = tp;
 }
@@ -861,6 +892,7 @@ struct RenderArgs {
   long canvas_tile_stride, canvas_ns_stride;
   MinMax *minmax;        // n_tiles * 3
   int write_rgba;
+  const EntryD *entries;
 };
 
 // Mask bit for data pair `pp` at its window pixel (ic, ir): mask[iSrc] with
@@ -885,7 +917,7 @@ __device__ __forceinline__ bool mask_at(const RenderArgs &a, const PairPlan &pp,
 template <int NOUT, int RES, bool MASK, bool GENERAL>
 __device__ __forceinline__ void render_band(const RenderArgs &a, int t, int band0, const uint32_t *s_ramp) {
   const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const gskyhip_tile &tile = a.tiles[t];
   const TilePlan &tp = a.tplans[t];
   const int W = tile.width, H = tile.height;
@@ -941,9 +973,9 @@ __device__ __forceinline__ void render_band(const RenderArgs &a, int t, int band
           }
         }
       }
-      if (x0 >= W) continue;
+      const bool active = x0 < W;   // inactive lanes still join the wave reduction below
       // typed canvases (tile_merger.go:562-652) and the auto-scale reduction
-      if (a.canvas) {
+      if (a.canvas && active) {
 #pragma unroll
         for (int s = 0; s < NOUT; s++) {
           const int dsz = type_size(tp.dtype[a.out_ns[s]]);
@@ -986,6 +1018,7 @@ __device__ __forceinline__ void render_band(const RenderArgs &a, int t, int band
         }
         continue;
       }
+      if (!active) continue;
       // utils.Scale + EncodePNG pixel loop
       uint32_t px[4];
 #pragma unroll
@@ -1015,9 +1048,302 @@ __device__ __forceinline__ void render_band(const RenderArgs &a, int t, int band
   }
 }
 
-// Simple tiles: every row LINEAR / linear leaves.  Grid n_tiles * bands.
+// ---------------------------------------------------------------- typed fast path
+// Every entry of a simple tile shares one value type T (vt) and needs no
+// GDALCopyWords promotion, every row is LINEAR or POOL with linear leaves,
+// so a pixel is: two fp64 affine evaluations, truncation, one typed gather,
+// a branch-free ordered fold, the scale and the palette lookup.
+#define GPTR(T) __attribute__((address_space(1))) T *
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <typename T> struct VOf { using type = int32_t; };
+template <> struct VOf<float> { using type = float; };
+
+template <typename T>
+__device__ __forceinline__ typename VOf<T>::type as_v(Val x) {
+  if constexpr (std::is_same<T, float>::value) return x.f; else return x.i;
+}
+
+// Go uint8(f) of a float32 (CVTTSS2SL, low byte): NaN / out of range -> 0.
+__device__ __forceinline__ uint32_t go_u8_f32(float f) {
+  return (f > -2147483648.0f && f < 2147483648.0f) ? ((uint32_t)(int32_t)f & 0xFFu) : 0u;
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t scale_t(const ScaleK &k, typename VOf<T>::type c) {
+  if constexpr (std::is_same<T, float>::value) {
+    Val v; v.f = c;
+    return scale_px(k, v);   // float32: normalise / log path stays exact and general
+  } else {
+    if (c == k.noData.i) return 0xFFu;
+    int32_t value = c + k.off.i;
+    if constexpr (std::is_same<T, int8_t>::value) value = (int8_t)value;
+    else if constexpr (std::is_same<T, uint8_t>::value) value = (uint8_t)value;
+    else if constexpr (std::is_same<T, int16_t>::value) value = (int16_t)value;
+    else value = (uint16_t)value;
+    value = min(value, k.clp.i);
+    value = max(value, 0);
+    return go_u8_f32((float)value * k.sc);
+  }
+}
+
+// Source coordinates of window pixel i of a LINEAR / POOL(linear) row.
+__device__ __forceinline__ void lin_coords(const RowRec &rr, const Leaf *__restrict__ pool, int i, double &sx,
+                                           double &sy) {
+  double xs0 = rr.v[0], ys0 = rr.v[1], dX = rr.v[2], dY = rr.v[3];
+  int start = 0;
+  if (rr.kind == ROW_POOL) {
+    const Leaf *lv = pool + rr.pool_off;
+    int k = 0;
+    while (k + 1 < rr.nleaf && lv[k + 1].start <= i) k++;
+    xs0 = lv[k].xs0; ys0 = lv[k].ys0; dX = lv[k].dX; dY = lv[k].dY; start = lv[k].start;
+  }
+  const double dist = (double)(i - start);
+  sy = ys0 + dY * dist;
+  sx = xs0 + dX * dist;
+}
+
+// NN gather of one window pixel in type T; returns false -> window fill.
+template <typename T>
+__device__ __forceinline__ bool nn_fetch(const EntryD &e, double sx, double sy, typename VOf<T>::type &v) {
+  if (sx < 0 || sy < 0) return false;
+  const double ax = sx + 1.0e-10, ay = sy + 1.0e-10;
+  if (ax >= 2147483647.0 || ay >= 2147483647.0) return false;
+  const int ix = (int)ax, iy = (int)ay;
+  if (ix >= e.band_x || iy >= e.band_y) return false;
+  v = (typename VOf<T>::type)((const T *)e.band)[(long)iy * e.band_x + ix];
+  return true;
+}
+
+template <typename T>
+__device__ __forceinline__ bool bil_fetch(const EntryD &e, double sx, double sy, typename VOf<T>::type &v) {
+  int iSrcX = (int)floor(sx - 0.5);
+  int iSrcY = (int)floor(sy - 0.5);
+  double rX = 1.5 - (sx - iSrcX);
+  double rY = 1.5 - (sy - iSrcY);
+  if (iSrcX == -1) { iSrcX = 0; rX = 1; }
+  if (iSrcY == -1) { iSrcY = 0; rY = 1; }
+  double accR = 0.0, accDiv = 0.0;
+  const T *band = (const T *)e.band;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int xx = iSrcX + (k & 1), yy = iSrcY + (k >> 1);
+    const double w = ((k & 1) ? (1.0 - rX) : rX) * ((k >> 1) ? (1.0 - rY) : rY);
+    if (xx < 0 || xx >= e.band_x || yy < 0 || yy >= e.band_y) continue;
+    const double d = (double)band[(long)yy * e.band_x + xx];
+    if (e.has_nodata && (d == e.nodata64 || (e.nodata64 != e.nodata64 && d != d))) continue;
+    accDiv += w;
+    accR += d * w;
+  }
+  double r;
+  if (accDiv == 1.0) r = accR;
+  else if (accDiv < 0.00001) return false;
+  else r = accR / accDiv;
+  if constexpr (std::is_same<T, float>::value) v = (float)r;
+  else v = gdal_copy_to(floor(r + 0.5), e.out_dtype).i;
+  return true;
+}
+
+// Mask raster value (its own dtype, NN) for data window index (ic, ir).
+template <int RES>
+__device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const RowRec *__restrict__ rows,
+                                          const Leaf *__restrict__ pool, const MaskSpecS *ms, const EntryD &e,
+                                          int ic, int ir) {
+  const EntryD &m = ents[e.mask_pair];
+  int mx = ic, my = ir;
+  if (m.w != e.w) {
+    const long iSrc = (long)ir * e.w + ic;
+    mx = (int)(iSrc % m.w);
+    my = (int)(iSrc / m.w);
+  }
+  if (my >= m.h) return false;
+  double sx, sy;
+  lin_coords(rows[m.row_base + my], pool, mx, sx, sy);
+  int32_t v;
+  bool ok;
+  switch (m.out_dtype) {
+    case GSKYHIP_BYTE: ok = nn_fetch<uint8_t>(m, sx, sy, v); break;
+    case GSKYHIP_SIGNEDBYTE: ok = nn_fetch<int8_t>(m, sx, sy, v); break;
+    case GSKYHIP_INT16: ok = nn_fetch<int16_t>(m, sx, sy, v); break;
+    default: ok = nn_fetch<uint16_t>(m, sx, sy, v); break;
+  }
+  if (!ok) v = m.fill.i;
+  const int slot = mask_slot(m.out_dtype);
+  return slot >= 0 && mask_bit(ms[slot], m.out_dtype, v);
+}
+
+// Branch-free NN sample of window pixel (sx, sy): the source value, or the
+// window fill when the pixel is outside the window or maps off the source
+// (warp.go:271-344).  One unconditional gather (index 0 when invalid).
+template <typename T>
+__device__ __forceinline__ typename VOf<T>::type nn_px(const EntryD &e, double sx, double sy, bool in,
+                                                       typename VOf<T>::type fillv) {
+  const double ax = sx + 1.0e-10, ay = sy + 1.0e-10;
+  const int ix = __double2int_rz(ax), iy = __double2int_rz(ay);
+  const bool ok = in && !(sx < 0) && !(sy < 0) && ax < 2147483647.0 && ay < 2147483647.0 && ix < e.band_x &&
+                  iy < e.band_y;
+  const long idx = ok ? (long)iy * e.band_x + ix : 0;
+  const typename VOf<T>::type raw = (typename VOf<T>::type)((const GPTR(T))e.band)[idx];
+  return ok ? raw : fillv;
+}
+
+// One wave owns a 4-row x 256-pixel block (4 x 4 pixels per lane): each
+// entry descriptor and row record is loaded once (scalar) per block.
+template <int NOUT, int RES, bool MASK, typename T>
+__device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD *__restrict__ ents,
+                                              const int32_t *__restrict__ order, const RowRec *__restrict__ rows,
+                                              const Leaf *__restrict__ pool, const gskyhip_tile &tile,
+                                              const TilePlan &tp, int t, int band0, const uint32_t *s_ramp) {
+  using V = typename VOf<T>::type;
+  // wave index in an SGPR: rows, row records and window tests become scalar
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int W = tile.width, H = tile.height;
+  const int r0 = band0 + wave * 4;
+  if (r0 >= H) return;
+  const int32_t *ord = order + tile.pair_begin;
+  const int n_entries = tp.n_entries;
+  V cnod[NOUT];
+  ScaleK sk[NOUT];
+  bool all_created = true;
+#pragma unroll
+  for (int s = 0; s < NOUT; s++) {
+    const int ns = a.out_ns[s];
+    all_created = all_created && tp.created[ns] != 0;
+    cnod[s] = as_v<T>(go_conv_to(tp.nodata[ns], tp.dtype[ns]));
+    sk[s] = make_scale(tp.dtype[ns], tp.nodata[ns], a.sp, false, 0.f, 0.f);
+  }
+  const bool has_ramp = a.ramp != nullptr;
+  uint8_t *rgba_tile = a.rgba + (long)t * H * W * 4;
+  for (int cx = 0; cx < W; cx += 256) {
+    const int x0 = cx + lane * 4;
+    V c[NOUT][4][4];
+#pragma unroll
+    for (int s = 0; s < NOUT; s++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) c[s][j][q] = cnod[s];
+    for (int k = 0; k < n_entries; k++) {
+      const EntryD e = ents[ord[k]];
+      if (r0 + 3 < e.yoff || r0 >= e.yoff + e.h) continue;
+      if (cx + 256 <= e.xoff || cx >= e.xoff + e.w) continue;
+      int slot = -1;
+#pragma unroll
+      for (int s = 0; s < NOUT; s++) if (a.out_ns[s] == e.ns) slot = s;
+      if (slot < 0) continue;
+      const V nd = as_v<T>(e.nd), fillv = as_v<T>(e.fill);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int ir = r0 + j - e.yoff;
+        if (r0 + j >= H || ir < 0 || ir >= e.h) continue;
+        const RowRec &rr = rows[e.row_base + ir];
+        const bool linear = rr.kind == ROW_LINEAR;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int ic = x0 + q - e.xoff;
+          const bool in = (unsigned)ic < (unsigned)e.w && x0 + q < W;
+          double sx, sy;
+          if (linear) {
+            const double dist = (double)ic;
+            sy = rr.v[1] + rr.v[3] * dist;
+            sx = rr.v[0] + rr.v[2] * dist;
+          } else {
+            lin_coords(rr, pool, in ? ic : 0, sx, sy);
+          }
+          V v;
+          if (RES == GSKYHIP_RESAMPLE_BILINEAR) {
+            v = fillv;
+            V got;
+            if (in && bil_fetch<T>(e, sx, sy, got)) v = got;
+          } else {
+            v = nn_px<T>(e, sx, sy, in, fillv);
+          }
+          bool take = in && (v != nd);
+          if (MASK && e.mask_pair >= 0) take = take && !mask_fast<RES>(ents, rows, pool, a.mask, e, ic, ir);
+#pragma unroll
+          for (int s = 0; s < NOUT; s++) {
+            if (s != slot) continue;
+            const bool t2 = take && (!e.fill_mode || c[s][j][q] == nd);
+            c[s][j][q] = t2 ? v : c[s][j][q];
+          }
+        }
+      }
+    }
+    if (x0 >= W) continue;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int r = r0 + j;
+      if (r >= H) break;
+      if (a.canvas) {
+#pragma unroll
+        for (int s = 0; s < NOUT; s++) {
+          T *cb = (T *)(a.canvas + t * a.canvas_tile_stride + s * a.canvas_ns_stride);
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (x0 + q < W) cb[(long)r * W + x0 + q] = (T)c[s][j][q];
+        }
+      }
+      if (!a.write_rgba) continue;
+      uint32_t px[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        uint32_t o;
+        if (NOUT == 1) {
+          const uint32_t b = scale_t<T>(sk[0], c[0][j][q]);
+          const uint32_t col = has_ramp ? s_ramp[b & 0xFFu] : (0xFF000000u | (b << 16) | (b << 8) | b);
+          o = (b == 0xFFu) ? 0u : col;
+        } else {
+          const uint32_t rr8 = scale_t<T>(sk[0], c[0][j][q]);
+          const uint32_t gg8 = scale_t<T>(sk[NOUT > 1 ? 1 : 0], c[NOUT > 1 ? 1 : 0][j][q]);
+          const uint32_t bb8 = scale_t<T>(sk[NOUT > 2 ? 2 : 0], c[NOUT > 2 ? 2 : 0][j][q]);
+          o = (rr8 != 0xFFu || gg8 != 0xFFu || bb8 != 0xFFu) ? (0xFF000000u | (bb8 << 16) | (gg8 << 8) | rr8) : 0u;
+        }
+        px[q] = all_created ? o : 0u;
+      }
+      uint8_t *dst = rgba_tile + ((long)r * W + x0) * 4;
+      if (x0 + 3 < W && ((((uintptr_t)dst) & 15) == 0)) {
+        u32x4 v4 = {px[0], px[1], px[2], px[3]};
+        *(GPTR(u32x4))dst = v4;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (x0 + q < W) ((uint32_t *)dst)[q] = px[q];
+      }
+    }
+  }
+}
+
+// Simple tiles (every row LINEAR / linear leaves, one value type).
+// Grid n_tiles * bands; complex tiles go to render_general_kernel.
 template <int NOUT, int RES, bool MASK>
-__global__ __launch_bounds__(256) void render_fast_kernel(RenderArgs a) {
+__global__ __launch_bounds__(256) void render_fast_kernel(RenderArgs a, const EntryD *__restrict__ ents,
+                                                          const int32_t *__restrict__ order,
+                                                          const RowRec *__restrict__ rows,
+                                                          const Leaf *__restrict__ pool,
+                                                          const TilePlan *__restrict__ tplans,
+                                                          const gskyhip_tile *__restrict__ tiles) {
+  __shared__ uint32_t s_ramp[256];
+  if (a.ramp) s_ramp[threadIdx.x] = a.ramp[threadIdx.x];
+  __syncthreads();
+  const int bands_per_tile = (a.max_h + a.rows_per_block - 1) / a.rows_per_block;
+  const int t = blockIdx.x / bands_per_tile;
+  if (t >= a.n_tiles) return;
+  const TilePlan &tp = tplans[t];
+  if (tp.complex) return;
+  const gskyhip_tile &tile = tiles[t];
+  const int band0 = (blockIdx.x % bands_per_tile) * a.rows_per_block;
+  switch (tp.vt) {
+    case GSKYHIP_INT16: render_fast_t<NOUT, RES, MASK, int16_t>(a, ents, order, rows, pool, tile, tp, t, band0, s_ramp); break;
+    case GSKYHIP_UINT16: render_fast_t<NOUT, RES, MASK, uint16_t>(a, ents, order, rows, pool, tile, tp, t, band0, s_ramp); break;
+    case GSKYHIP_FLOAT32: render_fast_t<NOUT, RES, MASK, float>(a, ents, order, rows, pool, tile, tp, t, band0, s_ramp); break;
+    case GSKYHIP_SIGNEDBYTE: render_fast_t<NOUT, RES, MASK, int8_t>(a, ents, order, rows, pool, tile, tp, t, band0, s_ramp); break;
+    default: render_fast_t<NOUT, RES, MASK, uint8_t>(a, ents, order, rows, pool, tile, tp, t, band0, s_ramp); break;
+  }
+}
+
+// Auto-scale pass 1 over simple tiles: typed canvases + per-tile min/max
+// (raster_scaler.go:47-78) with the generic body.
+template <int NOUT, int RES, bool MASK>
+__global__ __launch_bounds__(256) void render_auto_kernel(RenderArgs a) {
   __shared__ uint32_t s_ramp[256];
   if (a.ramp) s_ramp[threadIdx.x] = a.ramp[threadIdx.x];
   __syncthreads();
@@ -1147,6 +1473,7 @@ static inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 struct Carve {
   PairPlan *pairs; Xform *xforms; TilePlan *tplans; int32_t *order; int32_t *pair_tile;
   RowRec *rows; Leaf *pool; int32_t *counters; MinMax *minmax; int64_t *split_list; int32_t *complex_list;
+  EntryD *entries;
   int pool_cap;
   int64_t total;
 };
@@ -1170,6 +1497,7 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   const int64_t o_mm = take(sizeof(MinMax) * (int64_t)nt * 3);
   const int64_t o_split = take(sizeof(int64_t) * (int64_t)np * max_h);
   const int64_t o_cl = take(sizeof(int32_t) * (int64_t)nt);
+  const int64_t o_ent = take(sizeof(EntryD) * (int64_t)np);
   c.total = off;
   char *b = (char *)base;
   c.pairs = (PairPlan *)(b + o_pairs);
@@ -1183,6 +1511,7 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   c.minmax = (MinMax *)(b + o_mm);
   c.split_list = (int64_t *)(b + o_split);
   c.complex_list = (int32_t *)(b + o_cl);
+  c.entries = (EntryD *)(b + o_ent);
   return c;
 }
 
@@ -1202,6 +1531,7 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   a.pairs = cv.pairs; a.xforms = cv.xforms; a.tplans = cv.tplans; a.order = cv.order;
   a.pair_tile = cv.pair_tile; a.rows = cv.rows; a.pool = cv.pool; a.counters = cv.counters;
   a.pool_cap = cv.pool_cap; a.split_list = cv.split_list; a.complex_list = cv.complex_list;
+  a.entries = cv.entries;
   hipStream_t s = rc.stream;
   if (hipMemsetAsync(cv.counters, 0, 256, s) != hipSuccess) return GSKYHIP_E_HIP;
   hipLaunchKernelGGL(pair_tile_kernel, dim3((rc.n_tiles + 255) / 256), dim3(256), 0, s, rc.tiles, rc.n_tiles,
@@ -1218,7 +1548,11 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
 
 template <int NOUT, int RES, bool MASK>
 static void launch_render_kernels(const RenderArgs &a, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((render_fast_kernel<NOUT, RES, MASK>), grid, dim3(256), 0, s, a);
+  if (a.autom && !a.write_rgba)
+    hipLaunchKernelGGL((render_auto_kernel<NOUT, RES, MASK>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((render_fast_kernel<NOUT, RES, MASK>), grid, dim3(256), 0, s, a, a.entries, a.order,
+                       a.rows, a.pool, a.tplans, a.tiles);
   hipLaunchKernelGGL((render_general_kernel<NOUT, RES, MASK>), dim3(512), dim3(256), 0, s, a);
 }
 
@@ -1266,6 +1600,7 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.canvas_ns_stride = (long)rc.max_w * rc.max_h * 4;
   a.canvas_tile_stride = a.canvas_ns_stride * n_out;
   a.minmax = cv.minmax;
+  a.entries = cv.entries;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;
