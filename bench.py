@@ -89,7 +89,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scale", type=float, default=1.0, help="granule size scale (1 = 4000^2)")
     ap.add_argument("--tiles", type=int, default=64, help="tiles per side (64 -> 4096 tiles)")
-    ap.add_argument("--cpu-tiles", type=int, default=256, help="CPU baseline sample (tiles)")
+    ap.add_argument("--cpu-tiles", type=int, default=4096, help="CPU baseline sample (tiles)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c1", action="store_true")
     args = ap.parse_args()

@@ -165,8 +165,15 @@ def test_merge_parity(gpu, oracle, seed):
             rasters_g.append(gsky_amd.FlexRaster(torch.from_numpy(q).to(gpu), W, H, ox, oy, "Byte", 255.0, "qa",
                                                  ts, pg))
     mask = gsky_amd.Mask("qa", "01") if use_mask else None
-    exp = oracle.merge_batch(rasters_o, 3, W, H, mask_ns=2 if use_mask else -1,
-                             mask_value="01" if use_mask else None)
+    try:
+        exp = oracle.merge_batch(rasters_o, 3, W, H, mask_ns=2 if use_mask else -1,
+                                 mask_value="01" if use_mask else None)
+    except ValueError as ex:
+        # mask[iSrc] beyond the mask raster: the reference panics; both sides must refuse
+        assert "-3" in str(ex)
+        with pytest.raises(gsky_amd.GskyError):
+            gsky_amd.raster_merger_run(rasters_g, ["", "b2"], mask)
+        return
     got = gsky_amd.raster_merger_run(rasters_g, ["", "b2"], mask)
     for k, ns in enumerate(["", "b2"]):
         e = exp[k]
