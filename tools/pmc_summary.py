@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 --pmc passes of tools/pmc.sh for one kernel.
+
+Reads gpurun_out/pmc/p*/run_counter_collection.csv and writes a JSON summary
+(per-launch means of every counter for the kernel) with the HBM traffic
+estimate bench.py reports as roofline.traffic:
+
+  traffic = 2 * FETCH_SIZE + WRITE_SIZE   (bytes per launch)
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  The factor 2 is the gfx950 correction of
+MI355X_MICROARCH.md ("FETCH_SIZE reports exactly 1/2 of the bytes of a wide
+coalesced streaming read"); it is calibrated for 16-B streaming loads, not
+for the 2-byte gathers of the warp, so the read half of `traffic` is an
+estimate bracketed by [FETCH_SIZE, 2 * FETCH_SIZE].
+
+usage: python tools/pmc_summary.py [pmc_dir] [kernel_substring] [out.json]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main():
+    d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+    kern = sys.argv[2] if len(sys.argv) > 2 else "render_fast"
+    out = sys.argv[3] if len(sys.argv) > 3 else None
+    agg = collections.defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            if kern in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    means = {k: sum(v) / len(v) for k, v in agg.items()}
+    res = {"kernel_substring": kern, "counters_per_launch": means}
+    if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
+        fetch = means["FETCH_SIZE"] * 1024.0
+        write = means["WRITE_SIZE"] * 1024.0
+        res["fetch_bytes_raw"] = fetch
+        res["write_bytes"] = write
+        res["hbm_bytes_per_launch"] = 2.0 * fetch + write
+        res["note"] = "traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE correction; gathers uncalibrated)"
+    s = json.dumps(res, indent=1, sort_keys=True)
+    if out:
+        with open(out, "w") as fh:
+            fh.write(s + "\n")
+    print(s)
+
+
+if __name__ == "__main__":
+    main()
