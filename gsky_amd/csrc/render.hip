@@ -1236,19 +1236,32 @@ __device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD 
         const int ir = r0 + j - e.yoff;
         if (r0 + j >= H || ir < 0 || ir >= e.h) continue;
         const RowRec &rr = rows[e.row_base + ir];
-        const bool linear = rr.kind == ROW_LINEAR;
+        // wave-uniform row kind: LINEAR rows (the common case) take a straight
+        // 4-pixel body whose gathers issue back to back; the source
+        // coordinates are the same fp64 expressions as lin_coords().
+        double sxq[4], syq[4];
+        const int ic0 = x0 - e.xoff;
+        if (rr.kind == ROW_LINEAR) {
+          const double xs0 = rr.v[0], ys0 = rr.v[1], dX = rr.v[2], dY = rr.v[3];
+          const double d0 = (double)ic0;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const double dist = d0 + (double)q;   // exact: small integers
+            syq[q] = ys0 + dY * dist;
+            sxq[q] = xs0 + dX * dist;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int ic = ic0 + q;
+            lin_coords(rr, pool, ((unsigned)ic < (unsigned)e.w) ? ic : 0, sxq[q], syq[q]);
+          }
+        }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-          const int ic = x0 + q - e.xoff;
+          const int ic = ic0 + q;
           const bool in = (unsigned)ic < (unsigned)e.w && x0 + q < W;
-          double sx, sy;
-          if (linear) {
-            const double dist = (double)ic;
-            sy = rr.v[1] + rr.v[3] * dist;
-            sx = rr.v[0] + rr.v[2] * dist;
-          } else {
-            lin_coords(rr, pool, in ? ic : 0, sx, sy);
-          }
+          const double sx = sxq[q], sy = syq[q];
           V v;
           if (RES == GSKYHIP_RESAMPLE_BILINEAR) {
             v = fillv;
