@@ -14,6 +14,11 @@ namespace gsky {
 
 constexpr int kDrillUnroll = 16;
 
+// TPL time slices per lane (4: one 16-B word per lane; 1: one dword per lane,
+// 4x the waves per polygon for latency hiding -- each wave-instruction still
+// reads 256 contiguous bytes of the pixel's time vector).  Either way lane
+// sums are sequential float32 in the reference's row-major pixel order.
+template <int TPL>
 __global__ __launch_bounds__(128) void drill_kernel(const float *__restrict__ stack, int xsize, int ysize,
                                                     int n_bands, int t_stride,
                                                     const int32_t *__restrict__ win,
@@ -24,34 +29,40 @@ __global__ __launch_bounds__(128) void drill_kernel(const float *__restrict__ st
                                                     int32_t *__restrict__ band_count) {
   const int p = blockIdx.x;
   if (p >= n_polys) return;
-  const int t0 = (blockIdx.y * blockDim.x + threadIdx.x) * 4;
+  const int t0 = (blockIdx.y * blockDim.x + threadIdx.x) * TPL;
   const int offX = win[4 * p], offY = win[4 * p + 1], cx = win[4 * p + 2], cy = win[4 * p + 3];
   const uint8_t *m = masks + mask_off[p];
   const bool active = t0 < n_bands;
-  float sum[4] = {0.f, 0.f, 0.f, 0.f};
-  int32_t total[4] = {0, 0, 0, 0};
-  const long npx = (long)cx * cy;
+  float sum[TPL];
+  int32_t total[TPL];
+#pragma unroll
+  for (int j = 0; j < TPL; j++) { sum[j] = 0.f; total[j] = 0; }
   const float *base = stack + t0;
   for (int iy = 0; iy < cy; iy++) {
     const long rowbase = ((long)(offY + iy) * xsize + offX) * t_stride;
     const uint8_t *mrow = m + (long)iy * cx;
     for (int ix0 = 0; ix0 < cx; ix0 += kDrillUnroll) {
-      float4 v[kDrillUnroll];
+      float v[kDrillUnroll][TPL];
       bool use[kDrillUnroll];
 #pragma unroll
       for (int k = 0; k < kDrillUnroll; k++) {
         const int ix = ix0 + k;
         use[k] = ix < cx && mrow[ix] == 255;
-        if (use[k] && active) v[k] = *(const float4 *)(base + rowbase + (long)ix * t_stride);
-        else v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float *src = base + rowbase + (long)ix * t_stride;
+        if constexpr (TPL == 4) {
+          float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (use[k] && active) w = *(const float4 *)src;
+          v[k][0] = w.x; v[k][TPL > 1 ? 1 : 0] = w.y; v[k][TPL > 2 ? 2 : 0] = w.z; v[k][TPL > 3 ? 3 : 0] = w.w;
+        } else {
+          v[k][0] = (use[k] && active) ? *src : 0.f;
+        }
       }
 #pragma unroll
       for (int k = 0; k < kDrillUnroll; k++) {
         if (!use[k]) continue;
-        const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const float val = vv[j];
+        for (int j = 0; j < TPL; j++) {
+          const float val = v[k][j];
           if (val == nodata) continue;
           if (pixel_count != 0) total[j]++;
           if (val < lo || val > hi) continue;
@@ -65,10 +76,9 @@ __global__ __launch_bounds__(128) void drill_kernel(const float *__restrict__ st
       }
     }
   }
-  (void)npx;
   (void)ysize;
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
+  for (int j = 0; j < TPL; j++) {
     const int t = t0 + j;
     if (t >= n_bands) break;
     const long o = (long)p * n_bands + t;
@@ -156,9 +166,9 @@ int launch_drill(const float *stack, int xsize, int ysize, int n_bands, int t_st
     if (hipMallocAsync((void **)&bc, sizeof(int32_t) * (size_t)n_polys * n_bands, stream) != hipSuccess)
       return GSKYHIP_E_HIP;
   }
-  const int lanes = (n_bands + 3) / 4;
-  dim3 grid(n_polys, (lanes + 127) / 128);
-  hipLaunchKernelGGL(drill_kernel, grid, dim3(128), 0, stream, stack, xsize, ysize, n_bands, t_stride,
+  // one time slice per lane: n_bands lanes per polygon (C4: 3 x 2 waves)
+  dim3 grid(n_polys, (n_bands + 127) / 128);
+  hipLaunchKernelGGL(drill_kernel<1>, grid, dim3(128), 0, stream, stack, xsize, ysize, n_bands, t_stride,
                      win, mask_off, masks, n_polys, nodata, lo, hi, pixel_count, bv, bc);
   if (!direct) {
     const int rows = drill_rows_per_poly(n_bands, band_strides);
