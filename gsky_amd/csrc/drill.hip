@@ -12,13 +12,16 @@
 
 namespace gsky {
 
-constexpr int kDrillUnroll = 16;
+constexpr int kDrillBatch = 32;
 
-// TPL time slices per lane (4: one 16-B word per lane; 1: one dword per lane,
-// 4x the waves per polygon for latency hiding -- each wave-instruction still
-// reads 256 contiguous bytes of the pixel's time vector).  Either way lane
-// sums are sequential float32 in the reference's row-major pixel order.
-template <int TPL>
+// One time slice per lane (n_bands lanes per polygon): each wave-instruction
+// reads 256 contiguous bytes of a pixel's time vector.  The polygon window is
+// walked as its flattened row-major pixel sequence -- the reference order of
+// drill.go:153-170 -- in batches of 32 pixels; the batch's 32 mask bytes are
+// two 16-B words (masks are 16-B aligned and padded, pack_masks) fetched one
+// batch ahead, so each batch costs one memory round trip, and every lane
+// issues its 32 loads branch-free.  Lane sums stay sequential float32, so the
+// means are bit-exact.
 __global__ __launch_bounds__(128) void drill_kernel(const float *__restrict__ stack, int xsize, int ysize,
                                                     int n_bands, int t_stride,
                                                     const int32_t *__restrict__ win,
@@ -29,66 +32,64 @@ __global__ __launch_bounds__(128) void drill_kernel(const float *__restrict__ st
                                                     int32_t *__restrict__ band_count) {
   const int p = blockIdx.x;
   if (p >= n_polys) return;
-  const int t0 = (blockIdx.y * blockDim.x + threadIdx.x) * TPL;
+  const int t0 = blockIdx.y * blockDim.x + threadIdx.x;
   const int offX = win[4 * p], offY = win[4 * p + 1], cx = win[4 * p + 2], cy = win[4 * p + 3];
   const uint8_t *m = masks + mask_off[p];
   const bool active = t0 < n_bands;
-  float sum[TPL];
-  int32_t total[TPL];
-#pragma unroll
-  for (int j = 0; j < TPL; j++) { sum[j] = 0.f; total[j] = 0; }
+  const long npx = (long)cx * cy;
+  float sum = 0.f;
+  int32_t total = 0;
   const float *base = stack + t0;
-  for (int iy = 0; iy < cy; iy++) {
-    const long rowbase = ((long)(offY + iy) * xsize + offX) * t_stride;
-    const uint8_t *mrow = m + (long)iy * cx;
-    for (int ix0 = 0; ix0 < cx; ix0 += kDrillUnroll) {
-      float v[kDrillUnroll][TPL];
-      bool use[kDrillUnroll];
+  const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
+  uint4 mw0 = npx > 0 ? *(const uint4 *)m : zero4;
+  uint4 mw1 = npx > 16 ? *(const uint4 *)(m + 16) : zero4;
+  int iy = 0, ix = 0;
+  for (long i0 = 0; i0 < npx; i0 += kDrillBatch) {
+    const uint4 nw0 = (i0 + 32 < npx) ? *(const uint4 *)(m + i0 + 32) : zero4;
+    const uint4 nw1 = (i0 + 48 < npx) ? *(const uint4 *)(m + i0 + 48) : zero4;
+    const uint32_t mw[8] = {mw0.x, mw0.y, mw0.z, mw0.w, mw1.x, mw1.y, mw1.z, mw1.w};
+    float x[kDrillBatch];
+    bool use[kDrillBatch];
+    long rowbase = ((long)(offY + iy) * xsize + offX) * t_stride;
 #pragma unroll
-      for (int k = 0; k < kDrillUnroll; k++) {
-        const int ix = ix0 + k;
-        use[k] = ix < cx && mrow[ix] == 255;
-        const float *src = base + rowbase + (long)ix * t_stride;
-        if constexpr (TPL == 4) {
-          float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (use[k] && active) w = *(const float4 *)src;
-          v[k][0] = w.x; v[k][TPL > 1 ? 1 : 0] = w.y; v[k][TPL > 2 ? 2 : 0] = w.z; v[k][TPL > 3 ? 3 : 0] = w.w;
-        } else {
-          v[k][0] = (use[k] && active) ? *src : 0.f;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kDrillUnroll; k++) {
-        if (!use[k]) continue;
-#pragma unroll
-        for (int j = 0; j < TPL; j++) {
-          const float val = v[k][j];
-          if (val == nodata) continue;
-          if (pixel_count != 0) total[j]++;
-          if (val < lo || val > hi) continue;
-          if (pixel_count == 0) {
-            sum[j] += val;
-            total[j]++;
-          } else {
-            sum[j] += 1.0f;
-          }
-        }
+    for (int k = 0; k < kDrillBatch; k++) {
+      use[k] = (i0 + k < npx) && ((mw[k >> 2] >> (8 * (k & 3))) & 0xFFu) == 0xFFu;
+      const bool ok = use[k] && active;
+      const float *src = base + rowbase + (long)ix * t_stride;
+      const float v = *(ok ? src : stack);
+      x[k] = ok ? v : 0.f;
+      if (++ix == cx) {
+        ix = 0;
+        iy++;
+        rowbase = ((long)(offY + iy) * xsize + offX) * t_stride;
       }
     }
+#pragma unroll
+    for (int k = 0; k < kDrillBatch; k++) {
+      if (!use[k]) continue;
+      const float val = x[k];
+      if (val == nodata) continue;
+      if (pixel_count != 0) total++;
+      if (val < lo || val > hi) continue;
+      if (pixel_count == 0) {
+        sum += val;
+        total++;
+      } else {
+        sum += 1.0f;
+      }
+    }
+    mw0 = nw0;
+    mw1 = nw1;
   }
   (void)ysize;
-#pragma unroll
-  for (int j = 0; j < TPL; j++) {
-    const int t = t0 + j;
-    if (t >= n_bands) break;
-    const long o = (long)p * n_bands + t;
-    if (total[j] > 0) {
-      band_value[o] = (double)(sum[j] / (float)total[j]);  // drill.go:172-174
-      band_count[o] = total[j];
-    } else {
-      band_value[o] = 0.0;
-      band_count[o] = 0;
-    }
+  if (!active) return;
+  const long o = (long)p * n_bands + t0;
+  if (total > 0) {
+    band_value[o] = (double)(sum / (float)total);  // drill.go:172-174
+    band_count[o] = total;
+  } else {
+    band_value[o] = 0.0;
+    band_count[o] = 0;
   }
 }
 
@@ -157,6 +158,7 @@ int launch_drill(const float *stack, int xsize, int ysize, int n_bands, int t_st
   if (band_strides <= 0) band_strides = 1;
   if (n_polys <= 0) return 0;
   if (t_stride % 4 != 0 || t_stride < n_bands) return GSKYHIP_E_ARG;
+  if (((uintptr_t)masks & 15u) != 0) return GSKYHIP_E_ARG;   // 16-B mask words
   double *bv = out_value;
   int32_t *bc = out_count;
   const bool direct = band_strides == 1;
@@ -168,7 +170,7 @@ int launch_drill(const float *stack, int xsize, int ysize, int n_bands, int t_st
   }
   // one time slice per lane: n_bands lanes per polygon (C4: 3 x 2 waves)
   dim3 grid(n_polys, (n_bands + 127) / 128);
-  hipLaunchKernelGGL(drill_kernel<1>, grid, dim3(128), 0, stream, stack, xsize, ysize, n_bands, t_stride,
+  hipLaunchKernelGGL(drill_kernel, grid, dim3(128), 0, stream, stack, xsize, ysize, n_bands, t_stride,
                      win, mask_off, masks, n_polys, nodata, lo, hi, pixel_count, bv, bc);
   if (!direct) {
     const int rows = drill_rows_per_poly(n_bands, band_strides);

@@ -252,7 +252,11 @@ int gskyhip_compute_mask(const void *data, int dtype, int64_t n, const gskyhip_m
  *     xsize x ysize x n_bands stack, t fastest, t padded to t_stride
  *     (a multiple of 4, >= n_bands; 16-byte aligned pixel vectors).
  *   win: dev int32 4 per polygon {off_x, off_y, count_x, count_y}.
- *   mask_off: dev int64 per polygon, offset into masks (dev uint8, 255 = in).
+ *   mask_off: dev int64 per polygon, offset into masks (dev uint8, 255 = in,
+ *     row-major count_x*count_y).  masks must be 16-byte aligned, every
+ *     mask_off a multiple of 16 and every polygon's mask padded to a multiple
+ *     of 16 bytes (the kernel reads masks in 16-byte words; gsky_amd.drill.
+ *     pack_masks lays them out so); a misaligned masks pointer -> E_ARG.
  *   band_strides as drill.go:110-219.  Rows per polygon = *rows_per_poly.
  *   out_value: dev f64, out_count: dev i32, n_polys x rows_per_poly. */
 int gskyhip_drill_rows(int n_bands, int band_strides);
