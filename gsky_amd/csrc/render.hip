@@ -1315,7 +1315,8 @@ __device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD 
       uint8_t *dst = rgba_tile + ((long)r * W + x0) * 4;
       if (x0 + 3 < W && ((((uintptr_t)dst) & 15) == 0)) {
         u32x4 v4 = {px[0], px[1], px[2], px[3]};
-        *(GPTR(u32x4))dst = v4;
+        // streaming output, never re-read: non-temporal, keeps L2 for source rows
+        __builtin_nontemporal_store(v4, (GPTR(u32x4))dst);
       } else {
 #pragma unroll
         for (int q = 0; q < 4; q++)
