@@ -42,7 +42,8 @@ class Granule(C.Structure):
                 ("has_nodata", C.c_int32), ("crs", C.c_int32), ("n_ovr", C.c_int32), ("ns", C.c_int32),
                 ("ovr_data", C.c_void_p * MAX_OVR), ("ovr_xsize", C.c_int32 * MAX_OVR),
                 ("ovr_ysize", C.c_int32 * MAX_OVR), ("timestamp", C.c_double),
-                ("polygon_hash", C.c_uint32), ("_pad2", C.c_int32)]
+                ("polygon_hash", C.c_uint32), ("block_x", C.c_int32), ("block_y", C.c_int32),
+                ("_pad2", C.c_int32)]
 
 
 class Tile(C.Structure):

@@ -1,107 +1,150 @@
 """WCS GetCoverage over several MI355X (BASELINE.json configs[2]).
 
 The reference splits a large coverage into chunk requests of at most
-1024x1024 (utils/config.go:55-56, ows.go:815-833), fans them out over HTTP to
-other gsky-ows instances and merges the returned GeoTIFFs through temporary
-files (ows.go:930-995, 1094-1150).  Here the chunks are partitioned into
-contiguous row bands, one per rank (one process per GPU); each rank renders its
-band's chunks as typed canvases with the batched tile path (no RGBA,
-TileBatch.render(rgba=False)) and the bands are gathered to rank 0 with
+WcsMaxTileWidth x WcsMaxTileHeight (1024 x 1024 by default,
+utils/config.go:55-56; chunking at ows.go:815-833), fans them out over HTTP
+to other gsky-ows instances and merges the returned GeoTIFFs through temporary
+files (ows.go:930-995, 1094-1150).  Here the chunk list is built exactly as
+ows.go:817-831 does (south to north, west to east, `int(.5 + extent/res)`
+sizes, image offset `(x, Height - y - tileYSize)`), the chunk rows are
+partitioned into contiguous bands, one per rank (one process per GPU), each
+rank uploads only the granules its chunks intersect and renders its chunks as
+typed canvases with the batched tile path (no RGBA: TileBatch.render(rgba=False),
+FusionUnscale of ows.go:728), and the bands are gathered to rank 0 with
 torch.distributed -- RCCL over xGMI on the GPU box, gloo in the CPU tests.
 That gather is the only data-path collective of the whole hot path.
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
-import torch
+
+@dataclass
+class Chunk:
+    """One GeoTileRequest of the chunked coverage (ows.go:822-830)."""
+    bbox: Tuple[float, float, float, float]
+    width: int
+    height: int
+    off_x: int          # image column of the chunk's west edge
+    off_y: int          # image row of the chunk's north edge
+    row: int            # chunk row in list order (0 = southernmost)
 
 
-def chunk_grid(bbox: Sequence[float], width: int, height: int, chunk: int = 1024):
-    """Row-major chunk bboxes of a width x height coverage (ows.go:815-833:
-    xRes/yRes from the request, chunks of at most `chunk` pixels a side)."""
-    nx = (width + chunk - 1) // chunk
-    ny = (height + chunk - 1) // chunk
-    xres = (bbox[2] - bbox[0]) / width
-    yres = (bbox[3] - bbox[1]) / height
+def chunk_requests(bbox: Sequence[float], width: int, height: int, max_x: int = 1024,
+                   max_y: int = 1024) -> List[Chunk]:
+    """The reference's chunk list (ows.go:817-831), in its order."""
+    x_res = (bbox[2] - bbox[0]) / float(width)
+    y_res = (bbox[3] - bbox[1]) / float(height)
     out = []
-    for j in range(ny):
-        for i in range(nx):
-            w = min(chunk, width - i * chunk)
-            h = min(chunk, height - j * chunk)
-            x0 = bbox[0] + i * chunk * xres
-            y1 = bbox[3] - j * chunk * yres
-            out.append(((x0, y1 - h * yres, x0 + w * xres, y1), w, h))
-    return out, nx, ny
+    for row, y in enumerate(range(0, height, max_y)):
+        for x in range(0, width, max_x):
+            y_min = bbox[1] + float(y) * y_res
+            y_max = min(bbox[1] + float(y + max_y) * y_res, bbox[3])
+            x_min = bbox[0] + float(x) * x_res
+            x_max = min(bbox[0] + float(x + max_x) * x_res, bbox[2])
+            tw = int(.5 + (x_max - x_min) / x_res)
+            th = int(.5 + (y_max - y_min) / y_res)
+            out.append(Chunk((x_min, y_min, x_max, y_max), tw, th, x, height - y - th, row))
+    return out
 
 
-def band_of_rank(n_chunk_rows: int, rank: int, world: int) -> Tuple[int, int]:
+def n_chunk_rows(chunks: Sequence[Chunk]) -> int:
+    return 1 + max(c.row for c in chunks) if chunks else 0
+
+
+def band_of_rank(n_rows: int, rank: int, world: int) -> Tuple[int, int]:
     """Contiguous chunk rows [start, end) served by `rank` (balanced within one
-    row when world does not divide n_chunk_rows)."""
+    row when world does not divide n_rows; empty when world > n_rows)."""
     if world <= 0 or not 0 <= rank < world:
         raise ValueError("bad rank/world")
-    base, extra = divmod(n_chunk_rows, world)
+    base, extra = divmod(n_rows, world)
     start = rank * base + min(rank, extra)
     return start, start + base + (1 if rank < extra else 0)
 
 
-def assemble_band(chunks: torch.Tensor, n_rows: int, nx: int, chunk_h: int, chunk_w: int,
-                  width: Optional[int] = None) -> torch.Tensor:
-    """(n_rows*nx, chunk_h, chunk_w) chunk canvases, row-major -> one
-    (n_rows*chunk_h, width) row band."""
-    b = chunks.reshape(n_rows, nx, chunk_h, chunk_w).permute(0, 2, 1, 3).reshape(n_rows * chunk_h, nx * chunk_w)
-    return b[:, :width] if width is not None else b
+def band_extent(chunks: Sequence[Chunk], rows: Tuple[int, int]) -> Tuple[int, int]:
+    """Image rows [top, bottom) covered by chunk rows [rows) (empty -> (0, 0))."""
+    sel = [c for c in chunks if rows[0] <= c.row < rows[1]]
+    if not sel:
+        return 0, 0
+    return min(c.off_y for c in sel), max(c.off_y + c.height for c in sel)
 
 
-def gather_coverage(band: torch.Tensor, band_rows: Sequence[Tuple[int, int]], chunk_h: int, height: int,
-                    group=None) -> Optional[torch.Tensor]:
-    """Gathers every rank's row band to rank 0 and returns the full coverage
-    there (None elsewhere).  Bands are padded to the largest band so one
-    fixed-size gather serves uneven partitions."""
+def place_chunks(canvases, chunks: Sequence[Chunk], top: int, n_rows: int, width: int, dtype=None,
+                 device=None):
+    """Writes each chunk canvas (its own height x width) at its image offset
+    into one (n_rows, width) band whose first row is image row `top`."""
+    import torch
+    band = torch.empty((n_rows, width), dtype=dtype or torch.float32, device=device)
+    for cv, c in zip(canvases, chunks):
+        band[c.off_y - top: c.off_y - top + c.height, c.off_x: c.off_x + c.width] = cv
+    return band
+
+
+def gather_coverage(band, extents: Sequence[Tuple[int, int]], height: int, width: int, group=None):
+    """Gathers every rank's row band to rank 0 and returns the full
+    (height, width) coverage there (None elsewhere).  Bands are padded to
+    the largest band so one fixed-size gather serves uneven and empty bands."""
+    import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    max_rows = max(e - s for s, e in band_rows) * chunk_h
-    pad = torch.zeros((max_rows, band.shape[1]), dtype=band.dtype, device=band.device)
+    max_rows = max(1, max(b - t for t, b in extents))
+    pad = torch.zeros((max_rows, width), dtype=band.dtype, device=band.device)
     pad[: band.shape[0]] = band
     bufs = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
     dist.gather(pad, bufs, dst=0, group=group)
     if rank != 0:
         return None
-    parts = []
-    for r, (s, e) in enumerate(band_rows):
-        parts.append(bufs[r][: (e - s) * chunk_h])
-    return torch.cat(parts, 0)[:height]
+    full = torch.empty((height, width), dtype=band.dtype, device=band.device)
+    for r, (t, b) in enumerate(extents):
+        if b > t:
+            full[t:b] = bufs[r][: b - t]
+    return full
 
 
-def render_band_gpu(cfg, rows: Tuple[int, int], nx: int, device) -> torch.Tensor:
-    """Renders chunk rows [rows) of a synth-style coverage config (tiles =
-    row-major chunks, one namespace, Float32 canvas) on `device`."""
+def render_band_gpu(cfg, chunks: Sequence[Chunk], rows: Tuple[int, int], width: int, device):
+    """Renders the chunks of chunk rows [rows) of a synth-style coverage config
+    on `device` (one namespace, Float32 canvases, cfg.resample) and returns the
+    (band rows, width) band.  Only granules intersecting the band's chunks are
+    uploaded."""
+    import numpy as np
+    import torch
+
     from . import ScaleParams
     from .tiles import GranuleSet, TileBatch
-    import numpy as np
-    s, e = rows
-    ids = list(range(s * nx, e * nx))
+    top, bottom = band_extent(chunks, rows)
+    sel = [c for c in chunks if rows[0] <= c.row < rows[1]]
+    if not sel:
+        return torch.zeros((0, width), dtype=torch.float32, device=device)
+    pairs = [cfg.index_chunk(c.bbox) for c in sel]
+    used = sorted({g for p in pairs for g in p})
+    remap = {g: i for i, g in enumerate(used)}
     gs = GranuleSet(device)
-    for g in cfg.granules:
-        gs.add(torch.from_numpy(np.ascontiguousarray(g.data)), g.geot, g.srs, g.nodata, [], g.timestamp,
-               g.polygon, g.namespace)
-    tb = TileBatch(gs, cfg.dst_srs, [cfg.tiles[i] for i in ids], [cfg.pairs[i] for i in ids], cfg.namespaces)
+    for g in used:
+        gr = cfg.granules[g]
+        gs.add(torch.from_numpy(np.ascontiguousarray(gr.data)), gr.geot, gr.srs, gr.nodata, [], gr.timestamp,
+               gr.polygon, gr.namespace)
+    tiles = [(c.bbox, c.width, c.height) for c in sel]
+    tb = TileBatch(gs, cfg.dst_srs, tiles, [[remap[g] for g in p] for p in pairs], cfg.namespaces)
     cv = tb.render(ScaleParams(*cfg.scale), resample=cfg.resample, rgba=False)
-    ch, cw = tb.max_h, tb.max_w
-    chunks = cv[:, 0, : ch * cw * 4].contiguous().view(torch.float32).reshape(len(ids), ch, cw)
-    return assemble_band(chunks, e - s, nx, ch, cw)
+    canv = [tb.canvas_view(cv, i, 0, "Float32")[: c.height, : c.width] for i, c in enumerate(sel)]
+    return place_chunks(canv, sel, top, bottom - top, width, device=device)
 
 
-def render_coverage(cfg, nx: int, ny: int, renderer: Callable = render_band_gpu, device=None,
-                    group=None) -> Tuple[Optional[torch.Tensor], List[Tuple[int, int]]]:
-    """The whole multi-rank GetCoverage: partition, render own band, gather."""
+def render_coverage(cfg, width: int, height: int, renderer: Callable = render_band_gpu, device=None,
+                    group=None, max_x: int = 1024, max_y: int = 1024):
+    """The whole multi-rank GetCoverage: chunk, partition, render own band,
+    gather.  Returns (coverage on rank 0 / None elsewhere, band extents)."""
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    bands = [band_of_rank(ny, r, world) for r in range(world)]
-    band = renderer(cfg, bands[rank], nx, device)
-    chunk_h = cfg.tiles[0][2]
+    chunks = chunk_requests(cfg.bbox, width, height, max_x, max_y)
+    nrows = n_chunk_rows(chunks)
+    rows = [band_of_rank(nrows, r, world) for r in range(world)]
+    extents = [band_extent(chunks, rw) for rw in rows]
+    band = renderer(cfg, chunks, rows[rank], width, device)
     if world == 1:
-        return band, bands
-    return gather_coverage(band, bands, chunk_h, ny * chunk_h, group), bands
+        return band, extents
+    return gather_coverage(band, extents, height, width, group), extents

@@ -336,10 +336,18 @@ int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGe
   DropIn &d = dropin();
   std::lock_guard<std::mutex> lk(d.mu);
   if (!srcFilePath) return 1;
-  // netCDF paths are opened with band_query and read as band 1 (warp.go:89-101)
-  auto it = d.reg.find({std::string(srcFilePath), band});
-  if (it == d.reg.end()) it = d.reg.find({std::string(srcFilePath), 1});
-  if (it == d.reg.end()) return 1;                                   // open failed
+  const std::string path(srcFilePath);
+  // warp.go:89-101: "NETCDF:..." and "*.nc" are opened through GSKY_netCDF
+  // with band_query=<band>, which exposes that band as band 1; any other
+  // path is opened whole and GDALGetRasterBand(band) may fail (114-118).
+  const bool netcdf = path.compare(0, 7, "NETCDF:") == 0 ||
+                      (path.size() >= 3 && path.compare(path.size() - 3, 3, ".nc") == 0);
+  auto it = d.reg.find({path, band});
+  if (it == d.reg.end()) {
+    bool path_known = false;
+    for (const auto &kv : d.reg) if (kv.first.first == path) { path_known = true; break; }
+    return (netcdf || !path_known) ? 1 : 2;                          // open failed / band failed
+  }
   const Registered &R = it->second;
   if (!R.g.data) return 2;                                           // band failed
   if (geoLocOpts) return 3;                                          // geolocation arrays: unsupported
@@ -373,7 +381,15 @@ int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGe
   const int64_t ws = render_workspace_size(1, 1, dstYImageSize);
   const int64_t win_bytes = (int64_t)dstXImageSize * dstYImageSize * 4;
   const int64_t hdr = 4096;
-  const size_t need = (size_t)(hdr + ws + win_bytes + 256);
+  // bytesRead bookkeeping: block grid of level 0 (overviews have fewer blocks)
+  const int bx = R.g.block_x > 0 ? R.g.block_x : 0;    // 0: one scanline of the chosen level
+  const int by = R.g.block_y > 0 ? R.g.block_y : 1;
+  const int bx0 = bx > 0 ? bx : R.g.xsize;
+  const int64_t nblocks = ((int64_t)(R.g.xsize + bx0 - 1) / bx0) * ((R.g.ysize + by - 1) / by);
+  const int64_t n_words = (nblocks + 31) / 32;
+  const int64_t n_px = (int64_t)dstXImageSize * dstYImageSize;
+  const int64_t st_bytes = (block_stats_scratch_bytes(n_px, n_words) + 255) & ~(int64_t)255;
+  const size_t need = (size_t)(hdr + ws + win_bytes + 256 + st_bytes);
   if (d.dev_bytes < need) {
     if (d.dev) hipFree(d.dev);
     d.dev = nullptr;
@@ -391,6 +407,7 @@ int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGe
     int32_t bbox[4];
     int32_t dtype;
     double nodata;
+    int32_t stats[4];  // block_stats: first valid pixel, valid count, bytesRead
   };
   static_assert(sizeof(Hdr) <= 4096, "header");
   Hdr h;
@@ -416,6 +433,9 @@ int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGe
   char *win = base + hdr + ws;
   int rcode = launch_warp_windows(rc, dh->bbox, &dh->dtype, &dh->nodata, win, win_bytes);
   if (rcode) return rcode;
+  char *scratch = win + ((win_bytes + 255) & ~(int64_t)255);
+  rcode = launch_block_stats(rc, bx, by, scratch, n_px, n_words, dh->stats);
+  if (rcode) return rcode;
   Hdr back;
   if (hipMemcpyAsync(&back, dh, sizeof(Hdr), hipMemcpyDeviceToHost, d.stream) != hipSuccess) return GSKYHIP_E_HIP;
   double gt_back[6];
@@ -437,6 +457,7 @@ int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGe
   for (int k = 0; k < 4; k++) dstBbox[k] = back.bbox[k];
   *noData = back.nodata;
   *dType = back.dtype;
+  *bytesRead = back.stats[2];
   if (srcGeot) std::memcpy(srcGeot, gt_back, sizeof(gt_back));
   return 0;
 }

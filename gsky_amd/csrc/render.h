@@ -29,5 +29,9 @@ int launch_render(const RenderCall &c, const int32_t *out_ns, int n_out, const g
                   const uint8_t *ramp, uint8_t *rgba_out, void *canvas_out, int phase);
 int launch_warp_windows(const RenderCall &c, int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
                         void *win_out, int64_t win_stride);
+// bytesRead of the drop-in (pair 0 of a planned call): stats[2] receives it.
+int64_t block_stats_scratch_bytes(int64_t n_px, int64_t n_words);
+int launch_block_stats(const RenderCall &c, int bx, int by, void *scratch, int64_t n_px, int64_t n_words,
+                       int32_t *stats);
 
 }  // namespace gsky

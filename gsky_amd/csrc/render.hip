@@ -32,7 +32,7 @@ struct PlanArgs {
   const int32_t *pair_granule;
   int n_pairs;
   int pair_tile_max;           // scratch sizes
-  int max_h;
+  int max_h, max_w;            // tile slot of the batch (rgba / canvas layout)
   int mask_ns;
   int mask_inclusive;
   PairPlan *pairs;
@@ -241,6 +241,8 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
     return r;
   };
   int xoff = 0, yoff = 0, w = tile.width, h = tile.height;
+  const bool fits = tile.width > 0 && tile.height > 0 && tile.width <= a.max_w && tile.height <= a.max_h;
+  if (!fits) { w = 0; h = 0; err = 1; }
   if (err == 0) {
     const int minX = round_coord(ext[0], w), minY = round_coord(ext[1], h);
     const int maxX = round_coord(ext[2] + 0.5, w), maxY = round_coord(ext[3] + 0.5, h);
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
   pp.in_stack = (!pp.is_mask || a.mask_inclusive) ? 1 : 0;
   pp.fill_mode = 0;
   pp.mask_pair = -1;
-  pp.status = 0;
+  pp.status = fits ? 0 : GSKYHIP_E_ARG;
   pp.nodata = g.nodata;
   pp.has_nodata = g.has_nodata;
   pp.fill = gdal_copy_to(g.nodata, odt);
@@ -290,6 +292,12 @@ __global__ void plan_tiles_kernel(PlanArgs a) {
   for (int k = 0; k < 4; k++) { tp.created[k] = 0; tp.dtype[k] = 0; tp.nodata[k] = 0; canvas_ts[k] = 0; }
   const int b = tile.pair_begin, e = tile.pair_end;
   int32_t *ord = a.order + b;
+  if (tile.width <= 0 || tile.height <= 0 || tile.width > a.max_w || tile.height > a.max_h) {
+    tp.status = GSKYHIP_E_ARG;   // outside the batch's max_h x max_w slot
+    tp.complex = 1;              // no render kernel touches it
+    a.tplans[t] = tp;
+    return;
+  }
   // stack entries; stable insertion sort by geoStamp descending (keys sorted
   // descending, rasters of one key in arrival order: tile_merger.go:286-290)
   int n = 0;
@@ -878,7 +886,7 @@ struct RenderArgs {
   const Leaf *pool;
   const int32_t *counters;
   const int32_t *complex_list;
-  int max_h;
+  int max_h, max_w;     // tile slot: rgba / canvas row stride is max_w
   int n_tiles;
   int rows_per_block;
   int n_out;
@@ -981,7 +989,7 @@ __device__ __forceinline__ void render_band(const RenderArgs &a, int t, int band
           const int dsz = type_size(tp.dtype[a.out_ns[s]]);
           uint8_t *cb = a.canvas + t * a.canvas_tile_stride + s * a.canvas_ns_stride;
           for (int q = 0; q < 4 && x0 + q < W; q++) {
-            const long idx = (long)r * W + x0 + q;
+            const long idx = (long)r * a.max_w + x0 + q;
             if (dsz == 1) cb[idx] = (uint8_t)c[s][q].i;
             else if (dsz == 2) ((uint16_t *)cb)[idx] = (uint16_t)c[s][q].i;
             else ((uint32_t *)cb)[idx] = c[s][q].u;
@@ -1038,7 +1046,7 @@ __device__ __forceinline__ void render_band(const RenderArgs &a, int t, int band
         }
         px[q] = o;
       }
-      uint8_t *dst = a.rgba + ((long)t * H * W + (long)r * W + x0) * 4;
+      uint8_t *dst = a.rgba + (((long)t * a.max_h + r) * a.max_w + x0) * 4;
       if (x0 + 3 < W && ((((uintptr_t)dst) & 15) == 0)) {
         *(uint4 *)dst = make_uint4(px[0], px[1], px[2], px[3]);
       } else {
@@ -1212,7 +1220,7 @@ __device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD 
     sk[s] = make_scale(tp.dtype[ns], tp.nodata[ns], a.sp, false, 0.f, 0.f);
   }
   const bool has_ramp = a.ramp != nullptr;
-  uint8_t *rgba_tile = a.rgba + (long)t * H * W * 4;
+  uint8_t *rgba_tile = a.rgba + (long)t * a.max_h * a.max_w * 4;
   for (int cx = 0; cx < W; cx += 256) {
     const int x0 = cx + lane * 4;
     V c[NOUT][4][4];
@@ -1292,7 +1300,7 @@ __device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD 
           T *cb = (T *)(a.canvas + t * a.canvas_tile_stride + s * a.canvas_ns_stride);
 #pragma unroll
           for (int q = 0; q < 4; q++)
-            if (x0 + q < W) cb[(long)r * W + x0 + q] = (T)c[s][j][q];
+            if (x0 + q < W) cb[(long)r * a.max_w + x0 + q] = (T)c[s][j][q];
         }
       }
       if (!a.write_rgba) continue;
@@ -1312,7 +1320,7 @@ __device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD 
         }
         px[q] = all_created ? o : 0u;
       }
-      uint8_t *dst = rgba_tile + ((long)r * W + x0) * 4;
+      uint8_t *dst = rgba_tile + ((long)r * a.max_w + x0) * 4;
       if (x0 + 3 < W && ((((uintptr_t)dst) & 15) == 0)) {
         u32x4 v4 = {px[0], px[1], px[2], px[3]};
         // streaming output, never re-read: non-temporal, keeps L2 for source rows
@@ -1393,6 +1401,7 @@ __global__ __launch_bounds__(256) void canvas_rgba_kernel(RenderArgs a) {
   if (t >= a.n_tiles) return;
   const gskyhip_tile tile = a.tiles[t];
   const TilePlan tp = a.tplans[t];
+  if (tp.status == GSKYHIP_E_ARG) return;   // tile outside the slot: never written
   const int W = tile.width, H = tile.height, n_out = a.n_out;
   ScaleK sk[3];
   bool all_created = true;
@@ -1406,7 +1415,7 @@ __global__ __launch_bounds__(256) void canvas_rgba_kernel(RenderArgs a) {
   }
   for (int r = band0; r < band0 + a.rows_per_block && r < H; r++) {
     for (int x = tid; x < W; x += 256) {
-      const long idx = (long)r * W + x;
+      const long idx = (long)r * a.max_w + x;
       uint8_t b[3] = {0xFF, 0xFF, 0xFF};
       if (all_created) {
         for (int s = 0; s < n_out; s++) {
@@ -1431,7 +1440,7 @@ __global__ __launch_bounds__(256) void canvas_rgba_kernel(RenderArgs a) {
           o = 0xFF000000u | ((uint32_t)b[2] << 16) | ((uint32_t)b[1] << 8) | b[0];
         }
       }
-      ((uint32_t *)(a.rgba + (long)t * H * W * 4))[idx] = o;
+      ((uint32_t *)(a.rgba + (long)t * a.max_h * a.max_w * 4))[idx] = o;
     }
   }
 }
@@ -1466,6 +1475,75 @@ __global__ __launch_bounds__(256) void warp_window_kernel(const PairPlan *pairs,
   if (dsz == 1) o[idx] = (uint8_t)v.i;
   else if (dsz == 2) ((uint16_t *)o)[idx] = (uint16_t)v.i;
   else ((uint32_t *)o)[idx] = v.u;
+}
+
+// bytesRead of the drop-in (warp.go:278-347), pair 0: per window pixel the
+// reference's two tests -- the cache heuristic's x test (success, dx >= 0,
+// iSrcX < srcXSize; no dy test) and the full gather test -- plus the set of
+// source blocks that valid pixels touch.
+__global__ __launch_bounds__(256) void block_stats_kernel(const PairPlan *pairs, const Xform *xforms,
+                                                          const RowRec *rows, const Leaf *pool, int bx, int by,
+                                                          int32_t *xsrc, uint32_t *bits, int32_t *stats) {
+  const PairPlan &pp = pairs[0];
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)pp.w * pp.h) return;
+  const int row = (int)(gid / pp.w), i = (int)(gid % pp.w);
+  double sx, sy;
+  const bool ok = src_coords<true>(rows[row], pool, xforms, pp.xoff, pp.yoff, pp.w, i, row, sx, sy);
+  int xs = -1;
+  bool valid = false;
+  int ix = 0, iy = 0;
+  if (ok && !(sx < 0)) {
+    const double ax = sx + 1.0e-10;
+    if (ax < 2147483647.0) {
+      ix = (int)ax;
+      if (ix < pp.band_x) xs = ix;
+    }
+  }
+  if (xs >= 0 && !(sy < 0)) {
+    const double ay = sy + 1.0e-10;
+    if (ay < 2147483647.0) {
+      iy = (int)ay;
+      valid = iy < pp.band_y;
+    }
+  }
+  xsrc[gid] = xs;
+  if (!valid) return;
+  atomicMin(&stats[0], (int32_t)gid);
+  atomicAdd(&stats[1], 1);
+  if (bx <= 0) bx = pp.band_x;        // default block: one scanline of the chosen level
+  const int nxb = (pp.band_x + bx - 1) / bx;
+  const long blk = (long)(ix / bx) + (long)(iy / by) * nxb;
+  atomicOr(&bits[blk >> 5], 1u << (blk & 31));
+}
+
+// warp.go:281-313 (the cache decision at the first valid pixel) and 347.
+__global__ void block_stats_resolve_kernel(const PairPlan *pairs, int bx, int by, const int32_t *xsrc,
+                                           const uint32_t *bits, int n_words, int32_t *stats) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const PairPlan &pp = pairs[0];
+  if (bx <= 0) bx = pp.band_x;
+  const int i0 = stats[0];
+  if (i0 == 0x7FFFFFFF) { stats[2] = 0; return; }
+  const int r0 = i0 / pp.w, c0 = i0 % pp.w;
+  const int prev = xsrc[i0];
+  int curr = -1;
+  for (int c = c0 + 1; c < pp.w; c++) {
+    const int v = xsrc[(long)r0 * pp.w + c];
+    if (v >= 0) { curr = v; break; }
+  }
+  if (curr < prev) curr = prev;
+  const int stride = curr - prev;
+  const bool cache = stride >= 0 && stride < bx;
+  long nread = 0;
+  if (cache) {
+    for (int k = 0; k < n_words; k++) nread += __popc(bits[k]);
+  } else {
+    nread = stats[1];   // one GDALReadBlock per valid pixel (warp.go:319-322)
+  }
+  // C int arithmetic of warp.go:347 (wraps like the reference's 32-bit int)
+  const long long b = (long long)bx * by * type_size(pp.src_dtype) * nread;
+  stats[2] = (int32_t)(uint32_t)(unsigned long long)b;
 }
 
 __global__ void pair_meta_kernel(const PairPlan *pairs, int n_pairs, int32_t *bbox, int32_t *dtype, double *nodata) {
@@ -1541,7 +1619,7 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   PlanArgs a;
   a.granules = rc.granules; a.crs = rc.crs; a.n_crs = rc.n_crs; a.dst_crs = rc.dst_crs;
   a.tiles = rc.tiles; a.n_tiles = rc.n_tiles; a.pair_granule = rc.pair_granule; a.n_pairs = rc.n_pairs;
-  a.pair_tile_max = 0; a.max_h = rc.max_h; a.mask_ns = rc.mask_ns; a.mask_inclusive = rc.mask_inclusive;
+  a.pair_tile_max = 0; a.max_h = rc.max_h; a.max_w = rc.max_w; a.mask_ns = rc.mask_ns; a.mask_inclusive = rc.mask_inclusive;
   a.pairs = cv.pairs; a.xforms = cv.xforms; a.tplans = cv.tplans; a.order = cv.order;
   a.pair_tile = cv.pair_tile; a.rows = cv.rows; a.pool = cv.pool; a.counters = cv.counters;
   a.pool_cap = cv.pool_cap; a.split_list = cv.split_list; a.complex_list = cv.complex_list;
@@ -1602,7 +1680,7 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   RenderArgs a;
   a.pairs = cv.pairs; a.xforms = cv.xforms; a.tplans = cv.tplans; a.order = cv.order;
   a.tiles = rc.tiles; a.rows = cv.rows; a.pool = cv.pool; a.counters = cv.counters;
-  a.complex_list = cv.complex_list; a.max_h = rc.max_h;
+  a.complex_list = cv.complex_list; a.max_h = rc.max_h; a.max_w = rc.max_w;
   a.n_tiles = rc.n_tiles; a.rows_per_block = 16; a.n_out = n_out;
   for (int k = 0; k < 3; k++) a.out_ns[k] = k < n_out ? out_ns[k] : -1;
   for (int k = 0; k < 4; k++) a.mask[k] = rc.mask_specs[k];
@@ -1634,6 +1712,25 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   }
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
+
+int launch_block_stats(const RenderCall &rc, int bx, int by, void *scratch, int64_t n_px, int64_t n_words,
+                       int32_t *stats) {
+  const Carve cv = carve(rc.workspace, rc.n_tiles, rc.n_pairs, rc.max_h);
+  int32_t *xsrc = (int32_t *)scratch;
+  uint32_t *bits = (uint32_t *)((char *)scratch + align256(n_px * 4));
+  hipStream_t s = rc.stream;
+  const int32_t init[3] = {0x7FFFFFFF, 0, 0};
+  if (hipMemsetAsync(bits, 0, (size_t)n_words * 4, s) != hipSuccess) return GSKYHIP_E_HIP;
+  if (hipMemcpyAsync(stats, init, sizeof(init), hipMemcpyHostToDevice, s) != hipSuccess) return GSKYHIP_E_HIP;
+  if (n_px > 0)
+    hipLaunchKernelGGL(block_stats_kernel, dim3((unsigned)((n_px + 255) / 256)), dim3(256), 0, s, cv.pairs,
+                       cv.xforms, cv.rows, cv.pool, bx, by, xsrc, bits, stats);
+  hipLaunchKernelGGL(block_stats_resolve_kernel, dim3(1), dim3(64), 0, s, cv.pairs, bx, by, xsrc, bits,
+                     (int)n_words, stats);
+  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+}
+
+int64_t block_stats_scratch_bytes(int64_t n_px, int64_t n_words) { return align256(n_px * 4) + n_words * 4; }
 
 int launch_warp_windows(const RenderCall &rc, int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
                         void *win_out, int64_t win_stride) {

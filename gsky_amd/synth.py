@@ -9,6 +9,8 @@ seconds; scale=1 is the full benchmark size.
 from __future__ import annotations
 
 import math
+import os
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
@@ -30,6 +32,17 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
 
 def uniform01(h: np.ndarray) -> np.ndarray:
     return (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+def _pmap(fn, items):
+    """Map over granules / bands on a thread pool (numpy releases the GIL in
+    its ufuncs); results in input order, bit-identical to a serial loop."""
+    items = list(items)
+    workers = max(1, min(16, os.cpu_count() or 1, len(items)))
+    if workers == 1:
+        return [fn(x) for x in items]
+    with ThreadPoolExecutor(workers) as ex:
+        return list(ex.map(fn, items))
 
 
 # ---------------------------------------------------------------- projections for setup only
@@ -116,10 +129,20 @@ class SynthConfig:
     palette: Optional[list]
     resample: int = 0
     mask: Optional[dict] = None
+    bbox: Optional[Tuple[float, float, float, float]] = None   # whole coverage (C3)
+    out_w: int = 0
+    out_h: int = 0
 
     @property
     def out_pixels(self) -> int:
         return sum(w * h for (_, w, h) in self.tiles)
+
+    def index_chunk(self, bbox) -> List[int]:
+        """The indexer's granule list for one request bbox (MAS intersects)."""
+        fps = getattr(self, "_fps", None)
+        if fps is None:
+            fps = self._fps = [_footprint_merc(g) for g in self.granules]
+        return [k for k, f in enumerate(fps) if f[0] < bbox[2] and f[2] > bbox[0] and f[1] < bbox[3] and f[3] > bbox[1]]
 
 
 def _footprint_merc(g: SynthGranule, n=16):
@@ -197,23 +220,23 @@ def config_c2(scale: float = 1.0, tiles_per_side: int = 64, tile_px: int = 512, 
     (full size: 16 x 4000^2 at 25 m, 64 x 64 tiles of 512^2)."""
     n = int(round(4000 * scale))
     psize = 100000.0 / n        # a granule always spans 100 km
-    granules = []
-    for j in range(grid):
-        for i in range(grid):
-            k = j * grid + i
-            x0 = 1400000.0 + 95000.0 * i
-            y0 = -3800000.0 - 95000.0 * j
-            idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + k) << 32)
-            v = (splitmix64(idx) % np.uint64(10000)).astype(np.int16)
-            nb = (n + 63) // 64
-            bidx = np.arange(nb * nb, dtype=np.uint64) + np.uint64(((SEED0 + k) << 32) | 0xB10C0000)
-            blk = (uniform01(splitmix64(bidx)) < 0.1).reshape(nb, nb)
-            mask = np.repeat(np.repeat(blk, 64, 0), 64, 1)[:n, :n]
-            v[mask] = -999
-            poly = "POLYGON ((%.1f %.1f,%.1f %.1f,%.1f %.1f,%.1f %.1f,%.1f %.1f))" % (
-                x0, y0, x0 + 100000, y0, x0 + 100000, y0 - 100000, x0, y0 - 100000, x0, y0)
-            granules.append(SynthGranule(v, [x0, psize, 0.0, y0, 0.0, -psize], "EPSG:3577", -999.0,
-                                         1577836800.0 + 86400.0 * k, poly))
+    def make(k):
+        j, i = divmod(k, grid)
+        x0 = 1400000.0 + 95000.0 * i
+        y0 = -3800000.0 - 95000.0 * j
+        idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + k) << 32)
+        v = (splitmix64(idx) % np.uint64(10000)).astype(np.int16)
+        nb = (n + 63) // 64
+        bidx = np.arange(nb * nb, dtype=np.uint64) + np.uint64(((SEED0 + k) << 32) | 0xB10C0000)
+        blk = (uniform01(splitmix64(bidx)) < 0.1).reshape(nb, nb)
+        mask = np.repeat(np.repeat(blk, 64, 0), 64, 1)[:n, :n]
+        v[mask] = -999
+        poly = "POLYGON ((%.1f %.1f,%.1f %.1f,%.1f %.1f,%.1f %.1f,%.1f %.1f))" % (
+            x0, y0, x0 + 100000, y0, x0 + 100000, y0 - 100000, x0, y0 - 100000, x0, y0)
+        return SynthGranule(v, [x0, psize, 0.0, y0, 0.0, -psize], "EPSG:3577", -999.0,
+                            1577836800.0 + 86400.0 * k, poly)
+
+    granules = _pmap(make, range(grid * grid))
     # union bbox forward-projected to EPSG:3857
     ux0, uy1 = 1400000.0, -3800000.0
     ux1 = 1400000.0 + 95000.0 * (grid - 1) + 100000.0
@@ -235,7 +258,7 @@ def subset(cfg: SynthConfig, tile_ids) -> SynthConfig:
     tiles = [cfg.tiles[i] for i in tile_ids]
     pairs = [cfg.pairs[i] for i in tile_ids]
     return SynthConfig(cfg.name, cfg.granules, cfg.dst_srs, tiles, pairs, cfg.namespaces, cfg.scale,
-                       cfg.palette, cfg.resample, cfg.mask)
+                       cfg.palette, cfg.resample, cfg.mask, cfg.bbox, cfg.out_w, cfg.out_h)
 
 
 def mpix(cfg: SynthConfig) -> float:
@@ -243,37 +266,41 @@ def mpix(cfg: SynthConfig) -> float:
 
 
 # ---------------------------------------------------------------- C3
-def config_c3(scale: float = 1.0, chunk_px: int = 1024, grid: int = 8, out_px: int = 16384) -> SynthConfig:
+def config_c3(scale: float = 1.0, chunk_px: int = 1024, grid: int = 8, out_px: int = 16384,
+              out_h: Optional[int] = None) -> SynthConfig:
     """WCS GetCoverage: EPSG:4326 float32 granules (8x8 over lon 112..154,
     lat -44..-10, 2048^2 each at full size) -> EPSG:3857 float32 bilinear
     mosaic of out_px^2, split in chunk_px^2 chunks (utils/config.go:55-56)."""
     n = max(8, int(round(2048 * scale)))
     lon0, lon1, lat0, lat1 = 112.0, 154.0, -44.0, -10.0
     gw, gh = (lon1 - lon0) / grid, (lat1 - lat0) / grid
-    granules = []
-    for j in range(grid):
-        for i in range(grid):
-            k = j * grid + i
-            x0, y0 = lon0 + i * gw, lat1 - j * gh
-            rx, ry = gw / n, gh / n
-            lon = x0 + rx * (np.arange(n) + 0.5)
-            lat = y0 - ry * (np.arange(n) + 0.5)
-            idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + k) << 32)
-            hh = splitmix64(idx)
-            v = 200.0 + 50.0 * np.sin(lon[None, :] / 3.0) * np.cos(lat[:, None] / 2.0) + uniform01(hh)
-            v = v.astype(np.float32)
-            v[uniform01(splitmix64(hh)) < 0.01] = -9999.0
-            poly = "POLYGON ((%g %g,%g %g,%g %g,%g %g,%g %g))" % (x0, y0, x0 + gw, y0, x0 + gw, y0 - gh, x0,
-                                                                  y0 - gh, x0, y0)
-            granules.append(SynthGranule(v, [x0, rx, 0.0, y0, 0.0, -ry], "EPSG:4326", -9999.0, 1577836800.0,
-                                         poly))
+    def make(k):
+        j, i = divmod(k, grid)
+        x0, y0 = lon0 + i * gw, lat1 - j * gh
+        rx, ry = gw / n, gh / n
+        lon = x0 + rx * (np.arange(n) + 0.5)
+        lat = y0 - ry * (np.arange(n) + 0.5)
+        idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + k) << 32)
+        hh = splitmix64(idx)
+        v = 200.0 + 50.0 * np.sin(lon[None, :] / 3.0) * np.cos(lat[:, None] / 2.0) + uniform01(hh)
+        v = v.astype(np.float32)
+        v[uniform01(splitmix64(hh)) < 0.01] = -9999.0
+        poly = "POLYGON ((%g %g,%g %g,%g %g,%g %g,%g %g))" % (x0, y0, x0 + gw, y0, x0 + gw, y0 - gh, x0,
+                                                              y0 - gh, x0, y0)
+        return SynthGranule(v, [x0, rx, 0.0, y0, 0.0, -ry], "EPSG:4326", -9999.0, 1577836800.0, poly)
+
+    granules = _pmap(make, range(grid * grid))
     mx0, my0 = merc_fwd(lon0, lat0)
     mx1, my1 = merc_fwd(lon1, lat1)
     bbox = (float(mx0), float(my0), float(mx1), float(my1))
-    nch = max(1, out_px // chunk_px)
-    tiles = _grid_tiles(bbox, nch, nch, chunk_px)
-    pairs = _index_pairs(granules, tiles)
-    return SynthConfig("C3", granules, "EPSG:3857", tiles, pairs, [""], (0.0, 1.0, 0.0, 0), None, resample=1)
+    from .coverage import chunk_requests   # the reference's chunking, ows.go:817-831
+    out_h = out_px if out_h is None else out_h
+    chunks = chunk_requests(bbox, out_px, out_h, chunk_px, chunk_px)
+    tiles = [(c.bbox, c.width, c.height) for c in chunks]
+    cfg = SynthConfig("C3", granules, "EPSG:3857", tiles, [], [""], (0.0, 1.0, 0.0, 0), None, resample=1,
+                      bbox=bbox, out_w=out_px, out_h=out_h)
+    cfg.pairs = [cfg.index_chunk(bb) for (bb, _, _) in tiles]
+    return cfg
 
 
 # ---------------------------------------------------------------- C5
@@ -296,34 +323,34 @@ def config_c5(scale: float = 1.0, dates: int = 4, h_range=(25, 33), v_range=(8, 
     pyramids /2 down to 75^2 at full size, grey byte scaling (clip 10000)."""
     n = max(16, int(round(2400 * scale)))
     px = MODIS_T / n
-    granules = []
-    k = 0
-    for d in range(dates):
-        for v in range(*v_range):
-            for h in range(*h_range):
-                x0 = MODIS_X0 + h * MODIS_T
-                y0 = MODIS_Y0 - v * MODIS_T
-                idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + k) << 32)
-                hh = splitmix64(idx)
-                data = (hh % np.uint64(10000)).astype(np.int16)
-                nb = (n + 31) // 32
-                bidx = np.arange(nb * nb, dtype=np.uint64) + np.uint64(((SEED0 + k) << 32) | 0x0A000000)
-                blk = (uniform01(splitmix64(bidx)) < 0.15).reshape(nb, nb)
-                qa = np.repeat(np.repeat(blk, 32, 0), 32, 1)[:n, :n].astype(np.uint8)
-                qa |= (((hh >> np.uint64(20)) & np.uint64(0x7E)).astype(np.uint8))  # other bits noise
-                ovr_d, ovr_q = [], []
-                lvl = 1
-                while n // (2 ** lvl) >= max(4, int(round(75 * scale))):
-                    s = 2 ** lvl
-                    ovr_d.append(np.ascontiguousarray(data[::s, ::s][: n // s, : n // s]))
-                    ovr_q.append(np.ascontiguousarray(qa[::s, ::s][: n // s, : n // s]))
-                    lvl += 1
-                poly = "MODIS h%02dv%02d" % (h, v)
-                ts = 1577836800.0 + 8 * 86400.0 * d
-                gt = [x0, px, 0.0, y0, 0.0, -px]
-                granules.append(SynthGranule(data, gt, "MODIS", -28672.0, ts, poly, "", ovr_d))
-                granules.append(SynthGranule(qa, gt, "MODIS", 255.0, ts, poly, "qa", ovr_q))
-                k += 1
+    keys = [(d, v, h) for d in range(dates) for v in range(*v_range) for h in range(*h_range)]
+
+    def make(item):
+        k, (d, v, h) = item
+        x0 = MODIS_X0 + h * MODIS_T
+        y0 = MODIS_Y0 - v * MODIS_T
+        idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + k) << 32)
+        hh = splitmix64(idx)
+        data = (hh % np.uint64(10000)).astype(np.int16)
+        nb = (n + 31) // 32
+        bidx = np.arange(nb * nb, dtype=np.uint64) + np.uint64(((SEED0 + k) << 32) | 0x0A000000)
+        blk = (uniform01(splitmix64(bidx)) < 0.15).reshape(nb, nb)
+        qa = np.repeat(np.repeat(blk, 32, 0), 32, 1)[:n, :n].astype(np.uint8)
+        qa |= (((hh >> np.uint64(20)) & np.uint64(0x7E)).astype(np.uint8))  # other bits noise
+        ovr_d, ovr_q = [], []
+        lvl = 1
+        while n // (2 ** lvl) >= max(4, int(round(75 * scale))):
+            s = 2 ** lvl
+            ovr_d.append(np.ascontiguousarray(data[::s, ::s][: n // s, : n // s]))
+            ovr_q.append(np.ascontiguousarray(qa[::s, ::s][: n // s, : n // s]))
+            lvl += 1
+        poly = "MODIS h%02dv%02d" % (h, v)
+        ts = 1577836800.0 + 8 * 86400.0 * d
+        gt = [x0, px, 0.0, y0, 0.0, -px]
+        return (SynthGranule(data, gt, "MODIS", -28672.0, ts, poly, "", ovr_d),
+                SynthGranule(qa, gt, "MODIS", 255.0, ts, poly, "qa", ovr_q))
+
+    granules = [g for pair in _pmap(make, enumerate(keys)) for g in pair]
     tiles = []
     for (z, x0t, y0t, cnt) in zooms:
         for yy in range(y0t, y0t + cnt):
@@ -387,10 +414,16 @@ def config_c4(n_bands: int = 365, size: int = 2048, n_polys: int = 1000, rmin=10
     base = (0.2 + 0.1 * np.sin(2 * np.pi * t / 365.0)).astype(np.float32)
     idx = np.arange(size * size, dtype=np.uint64) + np.uint64(SEED0 << 32)
     noise = (uniform01(splitmix64(idx)) * 0.05).astype(np.float32).reshape(size, size)
-    bands = base[:, None, None] + noise[None, :, :] * (1.0 + (t[:, None, None] % 7) * 0.01).astype(np.float32)
-    bands = bands.astype(np.float32)
+    fac = (1.0 + (t % 7) * 0.01).astype(np.float32)
     nod = uniform01(splitmix64(idx + np.uint64(1 << 40))).reshape(size, size) < 0.05
-    bands[:, nod] = -9999.0
+    bands = np.empty((n_bands, size, size), np.float32)
+
+    def fill(b):  # float32 throughout: base + noise * factor, nodata burnt in
+        np.multiply(noise, fac[b], out=bands[b])
+        bands[b] += base[b]
+        bands[b][nod] = -9999.0
+
+    _pmap(fill, range(n_bands))
     wins, masks = [], []
     for p in range(n_polys):
         r = rng.uniform(rmin, rmax)

@@ -70,11 +70,14 @@ class Result:
 
 
 def register_granule(path: str, band: int, data: torch.Tensor, geot, srs: str = "",
-                     nodata: Optional[float] = None, overviews=(), signed_byte: bool = False) -> None:
-    """Make an HBM-resident band visible to warp_operation_fast under (path, band)."""
+                     nodata: Optional[float] = None, overviews=(), signed_byte: bool = False,
+                     block=(0, 0)) -> None:
+    """Make an HBM-resident band visible to warp_operation_fast under (path, band).
+    `block` = GDALGetBlockSize of the band ((0, 0): xsize x 1), for bytesRead."""
     d = data.contiguous()
     ovr = [o.contiguous() for o in overviews]
     g = _lib.Granule()
+    g.block_x, g.block_y = block
     g.data = d.data_ptr()
     g.dtype = DTYPE_OF_TORCH[d.dtype]
     g.ysize, g.xsize = d.shape

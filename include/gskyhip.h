@@ -85,6 +85,8 @@ typedef struct {
     int32_t ovr_ysize[GSKYHIP_MAX_OVR];
     double timestamp;            /* GeoTileGranule.TimeStamp                     */
     uint32_t polygon_hash;       /* fnv32a(GeoTileGranule.Polygon)               */
+    int32_t block_x, block_y;    /* GDALGetBlockSize of the band (0: xsize x 1);  *
+                                  * only bytesRead (warp.go:347) depends on it    */
     int32_t _pad2;
 } gskyhip_granule;
 
@@ -134,7 +136,12 @@ int gskyhip_unregister_all(void);
  * (worker/gdalprocess/warp.go:82).  *dstBuf is host memory from malloc(); the
  * caller frees it with free() (warp.go:573-574).  srcGeot, when given, may be
  * overwritten by the overview pick (warp.go:186-189).  geoLocOpts != NULL is
- * not supported (returns 3).  Nearest-neighbour, like the reference. */
+ * not supported (returns 3).  Nearest-neighbour, like the reference.
+ * Lookup (warp.go:89-118): "NETCDF:..." / "*.nc" paths are opened per band
+ * (band_query) and read as band 1, i.e. (path, band) is looked up; other
+ * paths: unregistered path -> 1, registered path without that band -> 2.
+ * *bytesRead = block bytes x blocks read, with the reference's block-cache
+ * heuristic (warp.go:278-347) over the granule's block_x x block_y. */
 int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGeot,
                         const char **geoLocOpts, const char *dstProjRef, double *dstGeot,
                         int dstXImageSize, int dstYImageSize, int band, int srsCf,

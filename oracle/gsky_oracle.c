@@ -1218,6 +1218,12 @@ int oracle_warp(const oracle_granule *g, const oracle_crs *src,
     int *ok = (int *)malloc(sizeof(int) * (dstXSize > 0 ? dstXSize : 1));
     for (int i = 0; i < dstXSize; i++) dx[dstXSize + i] = i + 0.5 + dstXOff;
     const int has_nodata = g->nodata != -1e10;
+    /* bytesRead bookkeeping, warp.go:221-231, 259-260, 278-332, 347 */
+    const int bx = g->block_x > 0 ? g->block_x : bandX;   /* default: one scanline of the level */
+    const int by = g->block_y > 0 ? g->block_y : 1;
+    const int nXBlocks = (bandX + bx - 1) / bx, nYBlocks = (bandY + by - 1) / by;
+    int bCache = -1, nBlocksRead = 0;
+    uint8_t *seen = NULL;
     for (int iy = 0; iy < dstYSize; iy++) {
         memcpy(dx, dx + dstXSize, dstXSize * sizeof(double));
         const double dfY = iy + 0.5 + dstYOff;
@@ -1239,12 +1245,32 @@ int oracle_warp(const oracle_granule *g, const oracle_crs *src,
             const int iSrcX = (int)(dx[i] + 1.0e-10);
             const int iSrcY = (int)(dy[i] + 1.0e-10);
             if (iSrcX >= bandX || iSrcY >= bandY) continue;
+            if (bCache == -1) {      /* stride of the first two usable columns of this row */
+                int prev = -1, curr = -1;
+                for (int j = i; j < dstXSize; j++) {
+                    if (!ok[j] || dx[j] < 0 || dx[j] + 1.0e-10 >= 2147483647.0) continue;
+                    const int sxj = (int)(dx[j] + 1.0e-10);
+                    if (sxj >= bandX) continue;
+                    if (prev < 0) prev = sxj;
+                    else { curr = sxj; break; }
+                }
+                if (prev >= 0 && curr < prev) curr = prev;
+                const int stride = curr - prev;
+                bCache = stride >= 0 && stride < bx;
+                if (bCache) seen = (uint8_t *)calloc((size_t)nXBlocks * nYBlocks, 1);
+            }
+            if (!bCache) nBlocksRead++;
+            else {
+                const int64_t blk = (int64_t)(iSrcX / bx) + (int64_t)(iSrcY / by) * nXBlocks;
+                if (!seen[blk]) { seen[blk] = 1; nBlocksRead++; }
+            }
             const int64_t sidx = (int64_t)iSrcY * bandX + iSrcX;
             if (supported) memcpy(o, (const uint8_t *)band + sidx * dsz, dsz);
             else or_gdal_copy_word(read_as_double(band, srcType, sidx), OR_FLOAT32, o);
         }
     }
-    free(dx); free(dy); free(ok);
+    free(dx); free(dy); free(ok); free(seen);
+    *bytes_read = (int32_t)(uint32_t)(uint64_t)((int64_t)bx * by * oracle_type_size(srcType) * nBlocksRead);
     bbox[0] = dstXOff; bbox[1] = dstYOff; bbox[2] = dstXSize; bbox[3] = dstYSize;
     if (outType == OR_BYTE && g->signed_byte) outType = OR_SIGNEDBYTE;    /* 354-359 */
     *dtype = outType;
@@ -1262,6 +1288,9 @@ typedef struct {
     const int32_t *pair_granule; int resample;
     int mask_ns; const char *mask_value; int mask_inclusive; int n_ns;
     const oracle_scale_params *sp; const uint8_t *ramp; uint8_t *rgba_out;
+    int max_w, max_h;            /* output slot of every tile (row stride max_w) */
+    uint8_t *canvas_out;         /* optional typed canvases, n_tiles x n_out x max_h*max_w*4 B */
+    int32_t *created_out;        /* optional n_tiles x 3 flags */
     int next; int err; pthread_mutex_t mu;
 } render_job;
 
@@ -1290,7 +1319,8 @@ static int render_one(render_job *j, int ti) {
         for (int k = 0; k < j->n_ns; k++) { cbuf[k] = malloc((size_t)npx * 8); cv[k].data = cbuf[k]; }
         const char *bt[1] = {NULL};
         rc = oracle_merge_batch(fr, npairs, j->mask_ns, j->mask_value, bt, 0, j->mask_inclusive, cv, j->n_ns);
-        uint8_t *rgba = j->rgba_out + (int64_t)ti * npx * 4;
+        const int64_t slot = (int64_t)j->max_w * j->max_h;
+        uint8_t *rgba = (uint8_t *)malloc((size_t)npx * 4);
         if (!rc) {
             /* output namespaces exclude the mask layer */
             const uint8_t *bands[3];
@@ -1299,6 +1329,14 @@ static int render_one(render_job *j, int ti) {
             for (int k = 0; k < j->n_ns && nb < 3; k++) {
                 if (k == j->mask_ns) continue;
                 sb[nb] = (uint8_t *)malloc((size_t)npx);
+                if (j->created_out) j->created_out[(int64_t)ti * 3 + nb] = cv[k].created;
+                if (cv[k].created && j->canvas_out) {     /* tile_merger.go:562-652 typed canvas */
+                    const int tsz = oracle_type_size(cv[k].dtype);
+                    uint8_t *dst = j->canvas_out + ((int64_t)ti * (j->n_ns - (j->mask_ns >= 0 ? 1 : 0)) + nb) * slot * 4;
+                    for (int r = 0; r < tile->height; r++)
+                        memcpy(dst + (int64_t)r * j->max_w * tsz, (const uint8_t *)cv[k].data + (int64_t)r * tile->width * tsz,
+                               (size_t)tile->width * tsz);
+                }
                 if (!cv[k].created) { missing = 1; }
                 else oracle_scale(cv[k].data, cv[k].dtype, npx, cv[k].nodata, j->sp->offset,
                                   j->sp->scale, j->sp->clip, j->sp->colour_scale, sb[nb]);
@@ -1308,7 +1346,13 @@ static int render_one(render_job *j, int ti) {
             if (missing) memset(rgba, 0, (size_t)npx * 4);
             else rc = oracle_encode_rgba(bands, nb, tile->width, tile->height, j->ramp, rgba);
             for (int k = 0; k < 3; k++) free(sb[k]);
+            if (!rc && j->rgba_out) {
+                uint8_t *o = j->rgba_out + (int64_t)ti * slot * 4;
+                for (int r = 0; r < tile->height; r++)
+                    memcpy(o + (int64_t)r * j->max_w * 4, rgba + (int64_t)r * tile->width * 4, (size_t)tile->width * 4);
+            }
         }
+        free(rgba);
         for (int k = 0; k < j->n_ns; k++) free(cbuf[k]);
     }
 out:
@@ -1330,6 +1374,31 @@ static void *render_worker(void *arg) {
     return NULL;
 }
 
+int oracle_render_tiles2(const oracle_granule *granules, const oracle_crs *src_crs,
+                         const double *ts, const uint32_t *ph, const int32_t *ns,
+                         int n_granules, const oracle_crs *dst,
+                         const oracle_tile *tiles, int n_tiles,
+                         const int32_t *pair_granule, int resample,
+                         int mask_ns, const char *mask_value, int mask_inclusive,
+                         int n_ns, const oracle_scale_params *sp,
+                         const uint8_t *ramp, uint8_t *rgba_out, int max_w, int max_h,
+                         uint8_t *canvas_out, int32_t *created_out, int n_threads) {
+    (void)n_granules;
+    if (n_ns > 4) return -7;
+    for (int t = 0; t < n_tiles; t++)
+        if (tiles[t].width <= 0 || tiles[t].height <= 0 || tiles[t].width > max_w || tiles[t].height > max_h) return -1;
+    render_job j = {granules, src_crs, ts, ph, ns, dst, tiles, n_tiles, pair_granule, resample,
+                    mask_ns, mask_value, mask_inclusive, n_ns, sp, ramp, rgba_out, max_w, max_h,
+                    canvas_out, created_out, 0, 0, PTHREAD_MUTEX_INITIALIZER};
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads == 1) { render_worker(&j); return j.err; }
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * n_threads);
+    for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, render_worker, &j);
+    for (int i = 0; i < n_threads; i++) pthread_join(th[i], NULL);
+    free(th);
+    return j.err;
+}
+
 int oracle_render_tiles(const oracle_granule *granules, const oracle_crs *src_crs,
                         const double *ts, const uint32_t *ph, const int32_t *ns,
                         int n_granules, const oracle_crs *dst,
@@ -1338,18 +1407,14 @@ int oracle_render_tiles(const oracle_granule *granules, const oracle_crs *src_cr
                         int mask_ns, const char *mask_value, int mask_inclusive,
                         int n_ns, const oracle_scale_params *sp,
                         const uint8_t *ramp, uint8_t *rgba_out, int n_threads) {
-    (void)n_granules;
-    if (n_ns > 4) return -7;
-    render_job j = {granules, src_crs, ts, ph, ns, dst, tiles, n_tiles, pair_granule, resample,
-                    mask_ns, mask_value, mask_inclusive, n_ns, sp, ramp, rgba_out, 0, 0,
-                    PTHREAD_MUTEX_INITIALIZER};
-    if (n_threads < 1) n_threads = 1;
-    if (n_threads == 1) { render_worker(&j); return j.err; }
-    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * n_threads);
-    for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, render_worker, &j);
-    for (int i = 0; i < n_threads; i++) pthread_join(th[i], NULL);
-    free(th);
-    return j.err;
+    int mw = 1, mh = 1;
+    for (int t = 0; t < n_tiles; t++) {
+        if (tiles[t].width > mw) mw = tiles[t].width;
+        if (tiles[t].height > mh) mh = tiles[t].height;
+    }
+    return oracle_render_tiles2(granules, src_crs, ts, ph, ns, n_granules, dst, tiles, n_tiles, pair_granule,
+                                resample, mask_ns, mask_value, mask_inclusive, n_ns, sp, ramp, rgba_out, mw, mh,
+                                NULL, NULL, n_threads);
 }
 
 /* ======================================================================== */

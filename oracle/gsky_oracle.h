@@ -150,6 +150,7 @@ typedef struct {
     const void *ovr_data[OR_MAX_OVR];
     int32_t ovr_xsize[OR_MAX_OVR];
     int32_t ovr_ysize[OR_MAX_OVR];
+    int32_t block_x, block_y;    /* GDALGetBlockSize (0: xsize x 1), bytesRead only */
 } oracle_granule;
 
 /* warp_operation_fast (warp.go:82-382) over an in-memory granule.
@@ -202,6 +203,21 @@ int oracle_render_tiles(const oracle_granule *granules, const oracle_crs *src_cr
                         int mask_ns, const char *mask_value, int mask_inclusive,
                         int n_ns, const oracle_scale_params *sp,
                         const uint8_t *ramp, uint8_t *rgba_out, int n_threads);
+
+/* The same with tiles of mixed sizes: every tile t lands in an output slot
+ * of max_h x max_w (row stride max_w) -- rgba_out n_tiles*max_h*max_w*4
+ * (may be NULL), canvas_out (may be NULL) n_tiles x n_out x max_h*max_w*4
+ * bytes receiving the typed merged canvases of the rendered namespaces
+ * (tile_merger.go:562-652), created_out (may be NULL) n_tiles x 3 flags. */
+int oracle_render_tiles2(const oracle_granule *granules, const oracle_crs *src_crs,
+                         const double *ts, const uint32_t *ph, const int32_t *ns,
+                         int n_granules, const oracle_crs *dst,
+                         const oracle_tile *tiles, int n_tiles,
+                         const int32_t *pair_granule, int resample,
+                         int mask_ns, const char *mask_value, int mask_inclusive,
+                         int n_ns, const oracle_scale_params *sp,
+                         const uint8_t *ramp, uint8_t *rgba_out, int max_w, int max_h,
+                         uint8_t *canvas_out, int32_t *created_out, int n_threads);
 
 /* ---- worker/gdalprocess/drill.go:90-227 readData -------------------------- */
 /* data: band-sequential float32 [nbands][count_y*count_x] already read as in

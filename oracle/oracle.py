@@ -41,7 +41,7 @@ class Granule(C.Structure):
                 ("ysize", C.c_int32), ("signed_byte", C.c_int32), ("geot", C.c_double * 6),
                 ("nodata", C.c_double), ("n_ovr", C.c_int32), ("_pad", C.c_int32),
                 ("ovr_data", C.c_void_p * MAX_OVR), ("ovr_xsize", C.c_int32 * MAX_OVR),
-                ("ovr_ysize", C.c_int32 * MAX_OVR)]
+                ("ovr_ysize", C.c_int32 * MAX_OVR), ("block_x", C.c_int32), ("block_y", C.c_int32)]
 
 
 class FlexRaster(C.Structure):
@@ -96,6 +96,9 @@ def lib():
         L.oracle_render_tiles.argtypes = [vp, vp, vp, vp, vp, C.c_int, vp, vp, C.c_int, vp,
                                           C.c_int, C.c_int, C.c_char_p, C.c_int, C.c_int, vp,
                                           vp, vp, C.c_int]
+        L.oracle_render_tiles2.argtypes = [vp, vp, vp, vp, vp, C.c_int, vp, vp, C.c_int, vp,
+                                           C.c_int, C.c_int, C.c_char_p, C.c_int, C.c_int, vp,
+                                           vp, vp, C.c_int, C.c_int, vp, vp, C.c_int]
         L.oracle_drill_read_data.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, C.c_float,
                                              C.c_float, C.c_float, C.c_int, C.c_int, vp, vp]
         L.oracle_drill_merge.argtypes = [vp, vp, C.c_int, C.c_int, vp]
@@ -230,8 +233,9 @@ def crs_transform(src: Crs, dst: Crs, x: float, y: float):
     return (xx.value, yy.value) if ok else None
 
 
-def make_granule(data: np.ndarray, geot, nodata=-1e10, overviews=(), signed_byte=False):
+def make_granule(data: np.ndarray, geot, nodata=-1e10, overviews=(), signed_byte=False, block=(0, 0)):
     g = Granule()
+    g.block_x, g.block_y = block
     d = np.ascontiguousarray(data)
     g.data = d.ctypes.data
     g.dtype = dtype_code(d, signed_byte)
@@ -272,6 +276,7 @@ def warp(g: Granule, src: Crs, dst, dst_geot, w, h, resample=0):
     arr = np.frombuffer(C.string_at(buf, size.value), dtype=npdt).copy()
     C.CDLL(None).free(buf)
     arr = arr.reshape(int(bbox[3]), int(bbox[2]))
+    warp.bytes_read = br.value        # warp.go:347 of the last call
     return arr, bbox.copy(), nd.value, dt.value
 
 
@@ -288,9 +293,12 @@ def suggested_warp_output(g: Granule, src: Crs, dst: Crs, dst_geot):
 
 def render_tiles(granules, src_crs, ts, ph, ns, dst, tiles_geot, width, height, pairs,
                  scale_params, ramp=None, n_ns=1, mask_ns=-1, mask_value=None,
-                 mask_inclusive=False, resample=0, n_threads=1):
+                 mask_inclusive=False, resample=0, n_threads=1, sizes=None, canvas=False):
     """CPU baseline of the whole tile path.  pairs: list (per tile) of granule
-    index lists.  Returns (n_tiles, h, w, 4) uint8."""
+    index lists; sizes: optional per-tile (w, h) (default width x height).
+    Returns (n_tiles, max_h, max_w, 4) uint8 RGBA (tile t in [t, :h, :w]);
+    with canvas=True also the typed merged canvases (n_tiles, n_out,
+    max_h*max_w*4 bytes, row stride max_w) and their created flags (n_tiles, 3)."""
     ng = len(granules)
     garr = (Granule * ng)(*granules)
     carr = (Crs * ng)(*src_crs)
@@ -298,27 +306,34 @@ def render_tiles(granules, src_crs, ts, ph, ns, dst, tiles_geot, width, height, 
     ph = np.ascontiguousarray(ph, np.uint32)
     nsa = np.ascontiguousarray(ns, np.int32)
     nt = len(tiles_geot)
-    tarr = (Tile * nt)()
+    sizes = list(sizes) if sizes is not None else [(width, height)] * nt
+    max_w = max([w for w, _ in sizes] + [1])
+    max_h = max([h for _, h in sizes] + [1])
+    tarr = (Tile * max(1, nt))()
     flat = []
     for i in range(nt):
         for k in range(6):
             tarr[i].dst_geot[k] = tiles_geot[i][k]
-        tarr[i].width, tarr[i].height = width, height
+        tarr[i].width, tarr[i].height = sizes[i]
         tarr[i].pair_begin = len(flat)
         flat.extend(pairs[i])
         tarr[i].pair_end = len(flat)
     pg = np.ascontiguousarray(flat if flat else [0], np.int32)
     sp = ScaleParams(*scale_params[:3], int(scale_params[3]) if len(scale_params) > 3 else 0, 0)
-    out = np.zeros((nt, height, width, 4), np.uint8)
+    out = np.zeros((nt, max_h, max_w, 4), np.uint8)
+    n_out = n_ns - (1 if mask_ns >= 0 else 0)
+    cv = np.zeros((nt, n_out, max_h * max_w * 4), np.uint8) if canvas else None
+    created = np.zeros((nt, 3), np.int32) if canvas else None
     rp = _ptr(np.ascontiguousarray(ramp, np.uint8)) if ramp is not None else None
-    rc = lib().oracle_render_tiles(garr, carr, _ptr(ts), _ptr(ph), _ptr(nsa), ng, C.byref(dst),
-                                   tarr, nt, _ptr(pg), resample, mask_ns,
-                                   mask_value.encode() if mask_value else None,
-                                   int(mask_inclusive), n_ns, C.byref(sp), rp, _ptr(out),
-                                   n_threads)
+    rc = lib().oracle_render_tiles2(garr, carr, _ptr(ts), _ptr(ph), _ptr(nsa), ng, C.byref(dst),
+                                    tarr, nt, _ptr(pg), resample, mask_ns,
+                                    mask_value.encode() if mask_value else None,
+                                    int(mask_inclusive), n_ns, C.byref(sp), rp, _ptr(out), max_w, max_h,
+                                    _ptr(cv) if canvas else None, _ptr(created) if canvas else None,
+                                    n_threads)
     if rc:
         raise RuntimeError("render error %d" % rc)
-    return out
+    return (out, cv, created) if canvas else out
 
 
 def drill_read_data(data, mask, nodata, clip_lower, clip_upper, pixel_count=0, band_strides=1):

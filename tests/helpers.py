@@ -24,16 +24,18 @@ def oracle_inputs(O, cfg: synth.SynthConfig):
     return gr, crs, ts, ph, ns, geots, slots, mask_ns
 
 
-def oracle_render(O, cfg: synth.SynthConfig, tile_ids=None, n_threads=8):
+def oracle_render(O, cfg: synth.SynthConfig, tile_ids=None, n_threads=8, canvas=False):
+    """The oracle's rendering of a synth config: RGBA (n_tiles, max_h, max_w, 4),
+    with canvas=True also (typed canvases, created flags)."""
     sub = synth.subset(cfg, tile_ids) if tile_ids is not None else cfg
     gr, crs, ts, ph, ns, geots, slots, mask_ns = oracle_inputs(O, sub)
-    w, h = sub.tiles[0][1], sub.tiles[0][2]
     ramp = O.gradient_palette(sub.palette, True) if sub.palette else None
-    return O.render_tiles(gr, crs, ts, ph, ns, O.crs(sub.dst_srs), geots, w, h, sub.pairs, sub.scale, ramp=ramp,
+    return O.render_tiles(gr, crs, ts, ph, ns, O.crs(sub.dst_srs), geots, 0, 0, sub.pairs, sub.scale, ramp=ramp,
                           n_ns=len(slots), mask_ns=mask_ns,
                           mask_value=sub.mask["value"] if sub.mask else None,
                           mask_inclusive=bool(sub.mask["inclusive"]) if sub.mask else False,
-                          resample=sub.resample, n_threads=n_threads)
+                          resample=sub.resample, n_threads=n_threads,
+                          sizes=[(w, h) for (_, w, h) in sub.tiles], canvas=canvas)
 
 
 def gpu_batch(cfg: synth.SynthConfig, device="cuda"):

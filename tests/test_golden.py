@@ -17,7 +17,7 @@ from tests.golden import make_golden as G
 from .helpers import gpu_batch, identity
 
 HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-NN_IDENTITY = 0.9999
+NN_IDENTITY = 1.0   # every golden case is 100 % identical
 
 
 def _load(name):
