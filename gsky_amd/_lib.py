@@ -16,6 +16,8 @@ LIB_PATH = os.path.join(_HERE, "libgskyhip.so")
 BYTE, UINT16, INT16, UINT32, INT32, FLOAT32, FLOAT64, SIGNEDBYTE = 1, 2, 3, 4, 5, 6, 7, 100
 CRS_LONGLAT, CRS_WEBMERC, CRS_AEA, CRS_SINU = 0, 1, 2, 3
 RESAMPLE_NEAREST, RESAMPLE_BILINEAR = 0, 1
+# value-type hint bits of gskyhip_render_tiles_typed
+VT_BIT = {BYTE: 1, SIGNEDBYTE: 2, INT16: 4, UINT16: 8, FLOAT32: 16}
 MAX_OVR = 12
 MAX_BIT_TESTS = 8
 
@@ -72,7 +74,7 @@ class FlexRasterC(C.Structure):
 EXPORTS = [
     "gskyhip_crs_from_srs", "gskyhip_register_granule", "gskyhip_unregister_all", "warp_operation_fast",
     "gskyhip_render_workspace_size", "gskyhip_render_tiles", "gskyhip_render_tiles_phase",
-    "gskyhip_warp_windows",
+    "gskyhip_render_tiles_typed", "gskyhip_warp_windows",
     "gskyhip_merge_rasters", "gskyhip_scale", "gskyhip_scale_legacy", "gskyhip_gradient_palette",
     "gskyhip_encode_rgba", "gskyhip_compute_mask", "gskyhip_drill_rows", "gskyhip_drill",
     "gskyhip_drill_merge", "gskyhip_fnv32a", "gskyhip_version", "gskyhip_device_count",
@@ -102,6 +104,7 @@ def lib() -> C.CDLL:
     L.gskyhip_render_tiles.argtypes = [vp, ci, vp, ci, ci, vp, ci, vp, ci, ci, ci, C.POINTER(i32), ci,
                                        C.POINTER(Mask), ci, C.POINTER(ScaleParams), vp, vp, vp, vp, i64, vp]
     L.gskyhip_render_tiles_phase.argtypes = [ci] + L.gskyhip_render_tiles.argtypes
+    L.gskyhip_render_tiles_typed.argtypes = [ci, C.c_uint32] + L.gskyhip_render_tiles.argtypes
     L.gskyhip_warp_windows.argtypes = [vp, ci, vp, ci, ci, vp, ci, vp, ci, ci, ci, ci, vp, vp, vp, vp, i64,
                                        vp, i64, vp]
     L.gskyhip_render_status.argtypes = [vp, ci, ci, ci, vp]

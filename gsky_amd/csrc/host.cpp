@@ -428,6 +428,7 @@ int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGe
   rc.max_w = dstXImageSize; rc.max_h = dstYImageSize;
   rc.mask_ns = -1; rc.mask_inclusive = 0; rc.mask_specs = ms;
   rc.resample = GSKYHIP_RESAMPLE_NEAREST;
+  rc.value_types = 0;
   rc.workspace = base + hdr; rc.workspace_bytes = ws;
   rc.stream = d.stream;
   char *win = base + hdr + ws;
@@ -473,6 +474,18 @@ int gskyhip_render_tiles_phase(int phase, const gskyhip_granule *granules, int n
                                int resample, const gskyhip_scale_params *sp, const uint8_t *ramp,
                                uint8_t *rgba_out, void *canvas_out, void *workspace, int64_t workspace_bytes,
                                void *stream) {
+  return gskyhip_render_tiles_typed(phase, 0u, granules, n_granules, crs_table, n_crs, dst_crs, tiles, n_tiles,
+                                    pair_granule, n_pairs, max_tile_width, max_tile_height, out_ns, n_out_ns, mask,
+                                    resample, sp, ramp, rgba_out, canvas_out, workspace, workspace_bytes, stream);
+}
+
+int gskyhip_render_tiles_typed(int phase, uint32_t value_types, const gskyhip_granule *granules,
+                               int n_granules, const gskyhip_crs *crs_table, int n_crs, int dst_crs,
+                               const gskyhip_tile *tiles, int n_tiles, const int32_t *pair_granule, int n_pairs,
+                               int max_tile_width, int max_tile_height, const int32_t *out_ns, int n_out_ns,
+                               const gskyhip_mask *mask, int resample, const gskyhip_scale_params *sp,
+                               const uint8_t *ramp, uint8_t *rgba_out, void *canvas_out, void *workspace,
+                               int64_t workspace_bytes, void *stream) {
   if (!sp || !out_ns || n_tiles < 0 || n_pairs < 0 || phase < 0 || phase > 2) return GSKYHIP_E_ARG;
   MaskSpecS ms[4];
   int r = build_mask_specs(mask, ms);
@@ -487,6 +500,7 @@ int gskyhip_render_tiles_phase(int phase, const gskyhip_granule *granules, int n
   rc.mask_inclusive = mask ? mask->inclusive : 0;
   rc.mask_specs = ms;
   rc.resample = resample;
+  rc.value_types = value_types;
   rc.workspace = workspace; rc.workspace_bytes = workspace_bytes;
   rc.stream = (hipStream_t)stream;
   return launch_render(rc, out_ns, n_out_ns, *sp, ramp, rgba_out, canvas_out, phase);
@@ -537,6 +551,7 @@ int gskyhip_warp_windows(const gskyhip_granule *granules, int n_granules, const 
   rc.max_w = max_tile_width; rc.max_h = max_tile_height;
   rc.mask_ns = -1; rc.mask_inclusive = 0; rc.mask_specs = ms;
   rc.resample = resample;
+  rc.value_types = 0;
   rc.workspace = workspace; rc.workspace_bytes = workspace_bytes;
   rc.stream = (hipStream_t)stream;
   if (win_stride < (int64_t)max_tile_width * max_tile_height * 4) return GSKYHIP_E_ARG;

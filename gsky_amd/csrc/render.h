@@ -21,6 +21,7 @@ struct RenderCall {
   int mask_ns, mask_inclusive;
   const MaskSpecS *mask_specs;  // 4 entries (host)
   int resample;
+  uint32_t value_types;         // GSKYHIP_VT_* of the stack entries (0 = unknown)
   void *workspace; int64_t workspace_bytes;
   hipStream_t stream;
 };

@@ -16,6 +16,7 @@
 #include "gsky_device.h"
 #include "render.h"
 #include "stages.h"
+#include "render_common.h"
 #include <algorithm>
 #include <type_traits>
 
@@ -703,206 +704,6 @@ __device__ __forceinline__ Val warped_value(const PairPlan &pp, const RowRec &rr
   return v;
 }
 
-// ---------------------------------------------------------------- ComputeMask
-// mask spec per mask-raster dtype: 0 SignedByte, 1 Byte, 2 Int16, 3 UInt16
-__device__ __forceinline__ int mask_slot(int dtype) {
-  switch (dtype) {
-    case GSKYHIP_SIGNEDBYTE: return 0;
-    case GSKYHIP_BYTE: return 1;
-    case GSKYHIP_INT16: return 2;
-    case GSKYHIP_UINT16: return 3;
-    default: return -1;
-  }
-}
-
-__device__ __forceinline__ bool mask_bit(const MaskSpecS &m, int dtype, int32_t v) {
-  if (m.has_value) {
-    int32_t a = v & m.value;
-    switch (dtype) {
-      case GSKYHIP_SIGNEDBYTE: return (int8_t)a > 0;
-      case GSKYHIP_INT16: return (int16_t)a > 0;
-      case GSKYHIP_BYTE: return (uint8_t)a > 0;
-      default: return (uint16_t)a > 0;
-    }
-  }
-  for (int j = 0; j < m.n_tests; j++) {
-    int32_t a = v & m.filt[j];
-    bool eq;
-    switch (dtype) {
-      case GSKYHIP_SIGNEDBYTE: eq = (int8_t)a == (int8_t)m.want[j]; break;
-      case GSKYHIP_INT16: eq = (int16_t)a == (int16_t)m.want[j]; break;
-      case GSKYHIP_BYTE: eq = (uint8_t)a == (uint8_t)m.want[j]; break;
-      default: eq = (uint16_t)a == (uint16_t)m.want[j]; break;
-    }
-    if (eq) return true;
-  }
-  return false;
-}
-
-// ---------------------------------------------------------------- scale
-// utils.scale (raster_scaler.go:30-332) constants of one canvas.
-struct ScaleK {
-  int32_t dtype;
-  int32_t colour_scale;
-  Val noData, off, clp;  // in the canvas type
-  float sc;
-  double nodata64;
-};
-
-// Go math.Log / Log2 / Log10 (Go 1.12, same op sequence as the amd64 asm).
-__device__ __noinline__ double go_log(double x) {
-  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
-  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
-               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
-               L7 = 1.479819860511658591e-01;
-  if (x != x || x == INFINITY) return x;
-  if (x < 0) return NAN;
-  if (x == 0) return -INFINITY;
-  int ki;
-  double f1 = frexp(x, &ki);
-  if (f1 < 1.41421356237309504880168872420969808 / 2) { f1 *= 2; ki--; }
-  double f = f1 - 1;
-  double k = (double)ki;
-  double s = f / (2 + f);
-  double s2 = s * s;
-  double s4 = s2 * s2;
-  double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
-  double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
-  double R = t1 + t2;
-  double hfsq = 0.5 * f * f;
-  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
-}
-__device__ __noinline__ double go_log10(double x) {
-  int e;
-  double frac = frexp(x, &e);
-  double l2;
-  if (frac == 0.5) l2 = (double)(e - 1);
-  else l2 = go_log(frac) * (1.0 / 0.693147180559945309417232121458176568) + (double)e;
-  return l2 * 0.301029995663981195213738894724493026768189881462108541310;
-}
-
-// normalise() (raster_scaler.go:15-28); returns false when the value maps to nodata
-__device__ __forceinline__ bool normalise_f(float &value, int colour_scale, double nodata64) {
-  double d = (double)value;
-  if (!(d == nodata64)) {
-    if (colour_scale == 1) d = go_log10(d);
-    if (isinf(d) || d != d) d = nodata64;
-  }
-  if (d == nodata64) return false;
-  value = (float)d;
-  return true;
-}
-
-__device__ __forceinline__ uint8_t scale_px(const ScaleK &k, Val v) {
-  if (k.dtype == GSKYHIP_FLOAT32) {
-    float value = v.f;
-    if (value == k.noData.f) return 0xFF;
-    if (k.colour_scale > 0 && !normalise_f(value, k.colour_scale, k.nodata64)) return 0xFF;
-    value += k.off.f;
-    if (value > k.clp.f) value = k.clp.f;
-    if (value < 0.0f) value = 0.0f;
-    return go_f32_u8(value * k.sc);
-  }
-  int32_t value = v.i;
-  if (value == k.noData.i) return 0xFF;
-  switch (k.dtype) {  // value += offset in the raster's own type (wraps)
-    case GSKYHIP_SIGNEDBYTE: value = (int8_t)(value + k.off.i); break;
-    case GSKYHIP_BYTE: value = (uint8_t)(value + k.off.i); break;
-    case GSKYHIP_INT16: value = (int16_t)(value + k.off.i); break;
-    default: value = (uint16_t)(value + k.off.i); break;
-  }
-  if (value > k.clp.i) value = k.clp.i;
-  if (value < 0) value = 0;
-  return go_f32_u8((float)value * k.sc);
-}
-
-// Scale constants of a canvas; auto mode takes min/max from the fold pass
-// (raster_scaler.go:47-78 and its typed siblings).
-__device__ inline ScaleK make_scale(int dtype, double nodata, const gskyhip_scale_params &sp, bool autom,
-                                    float minVal, float maxVal) {
-  ScaleK k;
-  k.dtype = dtype;
-  k.colour_scale = sp.colour_scale;
-  k.nodata64 = nodata;
-  float sc = (float)sp.scale;
-  if (sc <= 0.0f) sc = (sp.clip <= 0.0) ? 1.0f : (float)(254.0f / (float)sp.clip);
-  k.noData = go_conv_to(nodata, dtype);
-  if (dtype == GSKYHIP_FLOAT32) {
-    k.off.f = (float)sp.offset;
-    k.clp.f = (float)sp.clip;
-    if (autom) {
-      if (minVal == maxVal) maxVal += 0.1f;
-      sc = 254.0f / (maxVal - minVal);
-      k.off.f = -minVal;
-      k.clp.f = maxVal + k.off.f;
-    }
-  } else {
-    k.off = go_conv_to(sp.offset, dtype);
-    k.clp = go_conv_to(sp.clip, dtype);
-    if (autom) {
-      if (minVal == maxVal) maxVal += 0.1f;
-      sc = 254.0f / (maxVal - minVal);
-      const float dfOffset = -minVal;
-      k.off = go_conv_to((double)dfOffset, dtype);
-      k.clp = go_conv_to((double)(maxVal + dfOffset), dtype);
-    }
-  }
-  k.sc = sc;
-  return k;
-}
-
-// ordered-int encoding of float for atomic min/max
-__device__ __forceinline__ int32_t fenc(float f) {
-  int32_t i = __float_as_int(f);
-  return i ^ ((i >> 31) & 0x7FFFFFFF);
-}
-__device__ __forceinline__ float fdec(int32_t i) { return __int_as_float(i ^ ((i >> 31) & 0x7FFFFFFF)); }
-
-// Per (tile, out ns) auto-scale reduction state.
-struct MinMax {
-  int32_t mn, mx;      // fenc, over valid non-NaN values
-  int32_t p0_valid;    // pixel 0 valid (not nodata, and log-normalisable)
-  float p0;            // its (normalised) value
-};
-
-__device__ __forceinline__ void auto_minmax(const MinMax &m, float &mn, float &mx) {
-  // min/max start at 0 unless pixel 0 is valid (raster_scaler.go:55-58)
-  if (m.p0_valid) {
-    if (m.p0 != m.p0) { mn = m.p0; mx = m.p0; }
-    else { mn = fdec(m.mn); mx = fdec(m.mx); }
-  } else {
-    mn = fminf(0.0f, fdec(m.mn));
-    mx = fmaxf(0.0f, fdec(m.mx));
-  }
-}
-
-struct RenderArgs {
-  const PairPlan *pairs;
-  const Xform *xforms;
-  const TilePlan *tplans;
-  const int32_t *order;
-  const gskyhip_tile *tiles;
-  const RowRec *rows;
-  const Leaf *pool;
-  const int32_t *counters;
-  const int32_t *complex_list;
-  int max_h, max_w;     // tile slot: rgba / canvas row stride is max_w
-  int n_tiles;
-  int rows_per_block;
-  int n_out;
-  int32_t out_ns[3];
-  MaskSpecS mask[4];
-  gskyhip_scale_params sp;
-  int autom;
-  const uint32_t *ramp;  // 256 packed RGBA or NULL
-  uint8_t *rgba;
-  uint8_t *canvas;       // optional typed canvases
-  long canvas_tile_stride, canvas_ns_stride;
-  MinMax *minmax;        // n_tiles * 3
-  int write_rgba;
-  const EntryD *entries;
-};
-
 // Mask bit for data pair `pp` at its window pixel (ic, ir): mask[iSrc] with
 // iSrc the data window's linear index (tile_merger.go:53/64), read from the
 // warped mask raster of the same geoStamp.
@@ -1054,129 +855,6 @@ __device__ __forceinline__ void render_band(const RenderArgs &a, int t, int band
       }
     }
   }
-}
-
-// ---------------------------------------------------------------- typed fast path
-// Every entry of a simple tile shares one value type T (vt) and needs no
-// GDALCopyWords promotion, every row is LINEAR or POOL with linear leaves,
-// so a pixel is: two fp64 affine evaluations, truncation, one typed gather,
-// a branch-free ordered fold, the scale and the palette lookup.
-#define GPTR(T) __attribute__((address_space(1))) T *
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-template <typename T> struct VOf { using type = int32_t; };
-template <> struct VOf<float> { using type = float; };
-
-template <typename T>
-__device__ __forceinline__ typename VOf<T>::type as_v(Val x) {
-  if constexpr (std::is_same<T, float>::value) return x.f; else return x.i;
-}
-
-// Go uint8(f) of a float32 (CVTTSS2SL, low byte): NaN / out of range -> 0.
-__device__ __forceinline__ uint32_t go_u8_f32(float f) {
-  return (f > -2147483648.0f && f < 2147483648.0f) ? ((uint32_t)(int32_t)f & 0xFFu) : 0u;
-}
-
-template <typename T>
-__device__ __forceinline__ uint32_t scale_t(const ScaleK &k, typename VOf<T>::type c) {
-  if constexpr (std::is_same<T, float>::value) {
-    Val v; v.f = c;
-    return scale_px(k, v);   // float32: normalise / log path stays exact and general
-  } else {
-    if (c == k.noData.i) return 0xFFu;
-    int32_t value = c + k.off.i;
-    if constexpr (std::is_same<T, int8_t>::value) value = (int8_t)value;
-    else if constexpr (std::is_same<T, uint8_t>::value) value = (uint8_t)value;
-    else if constexpr (std::is_same<T, int16_t>::value) value = (int16_t)value;
-    else value = (uint16_t)value;
-    value = min(value, k.clp.i);
-    value = max(value, 0);
-    return go_u8_f32((float)value * k.sc);
-  }
-}
-
-// Source coordinates of window pixel i of a LINEAR / POOL(linear) row.
-__device__ __forceinline__ void lin_coords(const RowRec &rr, const Leaf *__restrict__ pool, int i, double &sx,
-                                           double &sy) {
-  double xs0 = rr.v[0], ys0 = rr.v[1], dX = rr.v[2], dY = rr.v[3];
-  int start = 0;
-  if (rr.kind == ROW_POOL) {
-    const Leaf *lv = pool + rr.pool_off;
-    int k = 0;
-    while (k + 1 < rr.nleaf && lv[k + 1].start <= i) k++;
-    xs0 = lv[k].xs0; ys0 = lv[k].ys0; dX = lv[k].dX; dY = lv[k].dY; start = lv[k].start;
-  }
-  const double dist = (double)(i - start);
-  sy = ys0 + dY * dist;
-  sx = xs0 + dX * dist;
-}
-
-// NN gather of one window pixel in type T; returns false -> window fill.
-template <typename T>
-__device__ __forceinline__ bool nn_fetch(const EntryD &e, double sx, double sy, typename VOf<T>::type &v) {
-  if (sx < 0 || sy < 0) return false;
-  const double ax = sx + 1.0e-10, ay = sy + 1.0e-10;
-  if (ax >= 2147483647.0 || ay >= 2147483647.0) return false;
-  const int ix = (int)ax, iy = (int)ay;
-  if (ix >= e.band_x || iy >= e.band_y) return false;
-  v = (typename VOf<T>::type)((const T *)e.band)[(long)iy * e.band_x + ix];
-  return true;
-}
-
-template <typename T>
-__device__ __forceinline__ bool bil_fetch(const EntryD &e, double sx, double sy, typename VOf<T>::type &v) {
-  int iSrcX = (int)floor(sx - 0.5);
-  int iSrcY = (int)floor(sy - 0.5);
-  double rX = 1.5 - (sx - iSrcX);
-  double rY = 1.5 - (sy - iSrcY);
-  if (iSrcX == -1) { iSrcX = 0; rX = 1; }
-  if (iSrcY == -1) { iSrcY = 0; rY = 1; }
-  double accR = 0.0, accDiv = 0.0;
-  const T *band = (const T *)e.band;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int xx = iSrcX + (k & 1), yy = iSrcY + (k >> 1);
-    const double w = ((k & 1) ? (1.0 - rX) : rX) * ((k >> 1) ? (1.0 - rY) : rY);
-    if (xx < 0 || xx >= e.band_x || yy < 0 || yy >= e.band_y) continue;
-    const double d = (double)band[(long)yy * e.band_x + xx];
-    if (e.has_nodata && (d == e.nodata64 || (e.nodata64 != e.nodata64 && d != d))) continue;
-    accDiv += w;
-    accR += d * w;
-  }
-  double r;
-  if (accDiv == 1.0) r = accR;
-  else if (accDiv < 0.00001) return false;
-  else r = accR / accDiv;
-  if constexpr (std::is_same<T, float>::value) v = (float)r;
-  else v = gdal_copy_to(floor(r + 0.5), e.out_dtype).i;
-  return true;
-}
-
-// Mask raster value (its own dtype, NN) for data window index (ic, ir).
-template <int RES>
-__device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const RowRec *__restrict__ rows,
-                                          const Leaf *__restrict__ pool, const MaskSpecS *ms, const EntryD &e,
-                                          int ic, int ir) {
-  const EntryD &m = ents[e.mask_pair];
-  int mx = ic, my = ir;
-  if (m.w != e.w) {
-    const long iSrc = (long)ir * e.w + ic;
-    mx = (int)(iSrc % m.w);
-    my = (int)(iSrc / m.w);
-  }
-  if (my >= m.h) return false;
-  double sx, sy;
-  lin_coords(rows[m.row_base + my], pool, mx, sx, sy);
-  int32_t v;
-  bool ok;
-  switch (m.out_dtype) {
-    case GSKYHIP_BYTE: ok = nn_fetch<uint8_t>(m, sx, sy, v); break;
-    case GSKYHIP_SIGNEDBYTE: ok = nn_fetch<int8_t>(m, sx, sy, v); break;
-    case GSKYHIP_INT16: ok = nn_fetch<int16_t>(m, sx, sy, v); break;
-    default: ok = nn_fetch<uint16_t>(m, sx, sy, v); break;
-  }
-  if (!ok) v = m.fill.i;
-  const int slot = mask_slot(m.out_dtype);
-  return slot >= 0 && mask_bit(ms[slot], m.out_dtype, v);
 }
 
 // Branch-free NN sample of window pixel (sx, sy): the source value, or the
@@ -1648,6 +1326,19 @@ static void launch_render_kernels(const RenderArgs &a, dim3 grid, hipStream_t s)
   hipLaunchKernelGGL((render_general_kernel<NOUT, RES, MASK>), dim3(512), dim3(256), 0, s, a);
 }
 
+// One value type for the whole batch (bit mask of GSKYHIP_VT_*): the typed
+// LDS band kernel, else 0.
+static int single_value_type(uint32_t vt) {
+  switch (vt) {
+    case GSKYHIP_VT_BYTE: return GSKYHIP_BYTE;
+    case GSKYHIP_VT_SIGNEDBYTE: return GSKYHIP_SIGNEDBYTE;
+    case GSKYHIP_VT_INT16: return GSKYHIP_INT16;
+    case GSKYHIP_VT_UINT16: return GSKYHIP_UINT16;
+    case GSKYHIP_VT_FLOAT32: return GSKYHIP_FLOAT32;
+    default: return 0;
+  }
+}
+
 template <int NOUT>
 static void dispatch_render(const RenderArgs &a, int resample, bool mask, dim3 grid, hipStream_t s) {
   if (resample == GSKYHIP_RESAMPLE_BILINEAR) {
@@ -1704,8 +1395,19 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   } else {
     a.write_rgba = rgba_out ? 1 : 0;
   }
-  if (n_out == 1) dispatch_render<1>(a, rc.resample, mask, grid, s);
-  else dispatch_render<3>(a, rc.resample, mask, grid, s);
+  const int vt = single_value_type(rc.value_types);
+  if (!autom && a.write_rgba && !canvas_out && n_out == 1 && rc.resample == GSKYHIP_RESAMPLE_NEAREST && vt) {
+    const int n_items = rc.n_tiles * ((rc.max_h + kLdsBandRows - 1) / kLdsBandRows);
+    launch_lds_kernels(a, vt, mask, n_items, s);
+    if (mask)
+      hipLaunchKernelGGL((render_general_kernel<1, GSKYHIP_RESAMPLE_NEAREST, true>), dim3(512), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((render_general_kernel<1, GSKYHIP_RESAMPLE_NEAREST, false>), dim3(512), dim3(256), 0, s, a);
+  } else if (n_out == 1) {
+    dispatch_render<1>(a, rc.resample, mask, grid, s);
+  } else {
+    dispatch_render<3>(a, rc.resample, mask, grid, s);
+  }
   if (autom) {
     a.write_rgba = 1;
     hipLaunchKernelGGL(canvas_rgba_kernel, grid, dim3(256), 0, s, a);

@@ -1,0 +1,16 @@
+// render_lds.hip -- dispatch of the typed LDS-staged band kernels.
+#include "render_lds.h"
+
+namespace gsky {
+
+void launch_lds_kernels(const RenderArgs &a, int vt, bool mask, int n_items, hipStream_t s) {
+  switch (vt) {
+    case GSKYHIP_INT16: launch_lds_i16(a, mask, n_items, s); break;
+    case GSKYHIP_UINT16: launch_lds_u16(a, mask, n_items, s); break;
+    case GSKYHIP_FLOAT32: launch_lds_f32(a, mask, n_items, s); break;
+    case GSKYHIP_SIGNEDBYTE: launch_lds_i8(a, mask, n_items, s); break;
+    default: launch_lds_u8(a, mask, n_items, s); break;
+  }
+}
+
+}  // namespace gsky

@@ -139,6 +139,19 @@ class TileBatch:
             c.ns = slots.index(g.namespace) if g.namespace in slots else 3
         self.n_granules = n
         self._gran = _to_device_bytes(garr, self.device)
+        # value types the stack entries warp to (warp.go:232-243, 354-359);
+        # a non-inclusive mask layer is not merged, so it does not count
+        vts = 0
+        for g in granules.items:
+            if mask is not None and g.namespace == mask.id and not mask.inclusive:
+                continue
+            dt = DTYPE_OF_TORCH[g.data.dtype]
+            if dt not in (_lib.BYTE, _lib.INT16, _lib.UINT16, _lib.FLOAT32):
+                dt = _lib.FLOAT32
+            if dt == _lib.BYTE and g.signed_byte:
+                dt = _lib.SIGNEDBYTE
+            vts |= _lib.VT_BIT[dt]
+        self.value_types = vts
         # tiles + pairs (CSR)
         flat: List[int] = []
         tarr = (_lib.Tile * max(1, len(tiles)))()
@@ -162,6 +175,7 @@ class TileBatch:
         ws = lib().gskyhip_render_workspace_size(self.n_tiles, self.n_pairs, self.max_h)
         self._ws = torch.empty(int(ws), dtype=torch.uint8, device=self.device)
         self._mask_c = mask.c(slots.index(mask.id)) if mask is not None else None
+        self.typed = True   # pass the value-type hint (False: force the generic kernels)
 
     # ------------------------------------------------------------------ render
     def render(self, params: ScaleParams, palette: Optional[Palette] = None, resample: int = 0,
@@ -194,8 +208,8 @@ class TileBatch:
         out_ns = (C.c_int32 * 3)(*[self.slots.index(ns) for ns in self.namespaces] + [0] * (3 - n_out))
         sp = params.c()
         stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-        check(lib().gskyhip_render_tiles_phase(
-            phase, C.c_void_p(self._gran.data_ptr()), self.n_granules, C.c_void_p(self._crs.data_ptr()),
+        check(lib().gskyhip_render_tiles_typed(
+            phase, self.value_types if self.typed else 0, C.c_void_p(self._gran.data_ptr()), self.n_granules, C.c_void_p(self._crs.data_ptr()),
             self.n_crs, self.dst_crs, C.c_void_p(self._tiles.data_ptr()), self.n_tiles,
             C.c_void_p(self._pairs.data_ptr()), self.n_pairs, self.max_w, self.max_h, out_ns, n_out,
             C.byref(self._mask_c) if self._mask_c is not None else None, resample, C.byref(sp),

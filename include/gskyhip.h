@@ -198,6 +198,28 @@ int gskyhip_render_tiles_phase(int phase, const gskyhip_granule *granules, int n
                                uint8_t *rgba_out, void *canvas_out,
                                void *workspace, int64_t workspace_bytes, void *stream);
 
+/* The same with a hint: value_types = OR of GSKYHIP_VT_* over the value types
+ * the batch's stack granules warp to (Byte/SignedByte/Int16/UInt16/Float32;
+ * granules of a non-inclusive mask layer excluded), 0 = unknown.  With exactly
+ * one type, one NN palette/grey namespace, RGBA output and no auto-scale the
+ * batch runs the typed LDS-staged band kernel (the MI355X fast path); every
+ * other combination runs the generic kernels.  Results are identical. */
+#define GSKYHIP_VT_BYTE 1u
+#define GSKYHIP_VT_SIGNEDBYTE 2u
+#define GSKYHIP_VT_INT16 4u
+#define GSKYHIP_VT_UINT16 8u
+#define GSKYHIP_VT_FLOAT32 16u
+int gskyhip_render_tiles_typed(int phase, uint32_t value_types, const gskyhip_granule *granules,
+                               int n_granules, const gskyhip_crs *crs_table, int n_crs, int dst_crs,
+                               const gskyhip_tile *tiles, int n_tiles,
+                               const int32_t *pair_granule, int n_pairs,
+                               int max_tile_width, int max_tile_height,
+                               const int32_t *out_ns, int n_out_ns,
+                               const gskyhip_mask *mask, int resample,
+                               const gskyhip_scale_params *sp, const uint8_t *ramp,
+                               uint8_t *rgba_out, void *canvas_out,
+                               void *workspace, int64_t workspace_bytes, void *stream);
+
 /* Warped windows only (the FlexRasters of tile_grpc.go:228-241): for pair p
  * (tile t, granule g) writes window bbox[4*p..] = {xoff,yoff,w,h} and the
  * window data (dtype of warp.go:232-243) into win_out + p*win_stride bytes. */

@@ -379,3 +379,76 @@ def test_drill_merge_parity(gpu, oracle):
     got = drill.drill_merge(torch.from_numpy(v).to(gpu), torch.from_numpy(c).to(gpu)).cpu().numpy()
     assert np.array_equal(np.isnan(exp), np.isnan(got))
     assert np.allclose(got[~np.isnan(got)], exp[~np.isnan(exp)], rtol=0, atol=0)
+
+
+# ---------------------------------------------------------------- typed LDS band kernel
+def _cast_cfg(cfg, dt):
+    """The same geometry with granule values cast to `dt` (nodata mapped)."""
+    nod = {np.uint8: 0.0, np.int8: -1.0, np.uint16: 0.0, np.float32: -999.0, np.int16: -999.0}[dt]
+    for g in cfg.granules:
+        v = g.data.astype(np.int64)
+        bad = v == -999
+        if dt == np.uint8:
+            v = v % 250 + 1
+        elif dt == np.int8:
+            v = v % 200 - 100
+        g.data = v.astype(dt)
+        g.data[bad] = nod
+        g.nodata = nod
+    return cfg
+
+
+@pytest.mark.parametrize("dt", [np.int16, np.uint16, np.uint8, np.int8, np.float32])
+def test_lds_kernel_types(gpu, oracle, dt):
+    """The typed LDS band kernel (value-type hint) and the generic kernels give
+    the oracle's tiles exactly, for every value type the warp keeps."""
+    import gsky_amd
+    cfg = _cast_cfg(synth.config_c2(scale=0.1, tiles_per_side=4, tile_px=256), dt)
+    if dt == np.uint8:
+        cfg.scale = (0.0, 0.0, 250.0, 0)
+    b = gpu_batch(cfg)
+    assert bin(b.value_types).count("1") == 1
+    sp, pal = gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True)
+    got = b.render(sp, pal).cpu().numpy().copy()
+    b.typed = False
+    gen = b.render(sp, pal).cpu().numpy()
+    exp = oracle_render(oracle, cfg)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(gen, exp)
+    assert (exp[..., 3] > 0).mean() > 0.3
+
+
+def test_lds_kernel_many_entries_multipass(gpu, oracle):
+    """40 overlapping granules on one tile: more entries per band than the
+    kernel stages at once (16), so the band folds in several passes."""
+    import gsky_amd
+    base = synth.config_c2(scale=0.05, tiles_per_side=2, tile_px=128, grid=2)
+    gs = []
+    for k in range(40):
+        g = base.granules[k % len(base.granules)]
+        gt = list(g.geot)
+        gt[0] += 731.0 * (k % 7)
+        gt[3] -= 517.0 * (k % 5)
+        d = np.roll(g.data, k * 13, axis=1).copy()
+        gs.append(synth.SynthGranule(d, gt, g.srs, g.nodata, 1577836800.0 + 3600.0 * ((k * 7) % 11),
+                                     "P%d" % (k % 3)))
+    cfg = synth.SynthConfig("many", gs, base.dst_srs, base.tiles, [list(range(40))] * len(base.tiles), [""],
+                            base.scale, base.palette)
+    b = gpu_batch(cfg)
+    sp, pal = gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True)
+    got = b.render(sp, pal).cpu().numpy().copy()
+    exp = oracle_render(oracle, cfg)
+    assert np.array_equal(got, exp)
+    b.typed = False
+    assert np.array_equal(b.render(sp, pal).cpu().numpy(), exp)
+
+
+def test_lds_kernel_masks(gpu, oracle):
+    """C5-style QA masks (non-inclusive mask layer, overviews) on the typed path."""
+    import gsky_amd
+    cfg = synth.config_c5(scale=0.05, dates=2, zooms=((4, 11, 8, 2), (5, 22, 16, 3)), tile_px=128)
+    b = gpu_batch(cfg)
+    assert b.value_types == 4          # Int16 only: the Byte QA layer is not merged
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale)).cpu().numpy()
+    exp = oracle_render(oracle, cfg)
+    assert np.array_equal(got, exp)
