@@ -3,12 +3,35 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace gsky {
-int drill_rows_per_poly(int n_bands, int band_strides);
-int launch_drill(const float *stack, int xsize, int ysize, int n_bands, int t_stride, const int32_t *win,
-                 const int64_t *mask_off, const uint8_t *masks, int n_polys, float nodata, float lo,
-                 float hi, int pixel_count, int band_strides, double *out_value, int32_t *out_count,
-                 hipStream_t stream);
+
+// One batched readData call (worker/gdalprocess/drill.go:90-227) over a
+// time-innermost stack; see gskyhip_drill_batch in include/gskyhip.h.
+struct DrillCall {
+  const float *stack;
+  int xsize, ysize, n_bands, t_stride;
+  const int32_t *win;          // dev: n_polys x {off_x, off_y, count_x, count_y}
+  const int64_t *mask_off;     // dev: byte offset of each polygon's mask
+  const uint8_t *masks;        // dev
+  int n_polys;
+  int64_t mask_bytes;          // size of masks (bounds the compacted pixel lists)
+  const int32_t *bands;        // HOST band list (1-based) or NULL = 1..n_bands
+  int n_list;
+  float nodata, lo, hi;
+  int pixel_count, band_strides, mode;
+  double *out_value;
+  int32_t *out_count;
+  void *workspace;
+  int64_t workspace_bytes;
+  hipStream_t stream;
+};
+
+int drill_rows_per_poly(int n_list, int band_strides);
+int64_t drill_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides, int mode);
+int launch_drill_batch(const DrillCall &c);
 int launch_drill_merge(const double *values, const int32_t *counts, int n_files, int n_dates, double *out,
                        hipStream_t stream);
+
 }  // namespace gsky

@@ -1,125 +1,245 @@
 // drill.hip -- WPS drill zonal reduction (worker/gdalprocess/drill.go:90-227)
-// over an HBM-resident time stack.
+// over an HBM-resident time stack, for a batch of polygons.
 //
-// Layout: time-innermost [y][x][t] with t padded to t_stride (multiple of 4),
-// so one pixel's time vector is a contiguous run of 16-byte words.  Lane l of
-// a polygon's block owns bands 4l..4l+3 and walks the polygon window in the
-// reference's row-major pixel order, keeping four sequential float32 sums:
-// the additions happen in exactly the order of drill.go:153-170, so means are
-// bit-exact, while every wave-instruction still moves 1 KiB contiguous.
-#include "gsky_device.h"
+// Layout: time-innermost [y][x][t] with t padded to t_stride, so one pixel's
+// time vector is contiguous and a wave-instruction that reads 64 consecutive
+// slices of one pixel moves 256 contiguous bytes.
+//
+// Pipeline (all asynchronous on one stream, workspace from the caller):
+//   drill_compact_kernel   one block per polygon: the in-mask pixels of its
+//                          window (mask byte 255, inside the stack) compacted
+//                          to global pixel indices in row-major order -- the
+//                          order of the reference's `for i < bandSize` loop --
+//                          so the reduction never touches masked-out pixels.
+//   hipcub radix sort      polygons by in-mask pixel count, largest first: the
+//                          longest sequential walks start first.
+//   drill_sum_kernel       mode 0 (reference order): one wave per (polygon,
+//                          64 selected bands); lane j keeps a sequential
+//                          float32 sum over the compacted pixels in order, so
+//                          the means are bit-exact (drill.go:153-177).
+//   drill_seg_kernel       mode 1 (wave split): the compacted list is cut in
+//   + drill_combine_kernel segments of kSeg pixels, one wave per (segment,
+//                          64 bands) keeps a float32 partial, partials are
+//                          combined in float64 in segment order (deterministic);
+//                          the largest polygon no longer bounds the launch.
+//                          Within 1e-5 relative of the reference order.
+//   drill_rows_kernel      bandStrides rows (drill.go:128-219).
+#include <hipcub/hipcub.hpp>
+
+#include <vector>
+
 #include "drill.h"
+#include "gsky_device.h"
 
 namespace gsky {
 
-constexpr int kDrillBatch = 32;
+constexpr int kSeg = 1024;      // pixels per segment in the wave-split mode
+constexpr int kUnroll = 16;     // pixel loads in flight per lane
 
-// One time slice per lane (n_bands lanes per polygon): each wave-instruction
-// reads 256 contiguous bytes of a pixel's time vector.  The polygon window is
-// walked as its flattened row-major pixel sequence -- the reference order of
-// drill.go:153-170 -- in batches of 32 pixels; the batch's 32 mask bytes are
-// two 16-B words (masks are 16-B aligned and padded, pack_masks) fetched one
-// batch ahead, so each batch costs one memory round trip, and every lane
-// issues its 32 loads branch-free.  Lane sums stay sequential float32, so the
-// means are bit-exact.
-__global__ __launch_bounds__(128) void drill_kernel(const float *__restrict__ stack, int xsize, int ysize,
-                                                    int n_bands, int t_stride,
-                                                    const int32_t *__restrict__ win,
-                                                    const int64_t *__restrict__ mask_off,
-                                                    const uint8_t *__restrict__ masks, int n_polys,
-                                                    float nodata, float lo, float hi, int pixel_count,
-                                                    double *__restrict__ band_value,
-                                                    int32_t *__restrict__ band_count) {
+// ---------------------------------------------------------------- compaction
+__global__ __launch_bounds__(256) void drill_compact_kernel(const int32_t *__restrict__ win,
+                                                            const int64_t *__restrict__ mask_off,
+                                                            const uint8_t *__restrict__ masks, int n_polys,
+                                                            int xsize, int ysize, int32_t *__restrict__ idx,
+                                                            int32_t *__restrict__ count) {
   const int p = blockIdx.x;
   if (p >= n_polys) return;
-  const int t0 = blockIdx.y * blockDim.x + threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int offX = win[4 * p], offY = win[4 * p + 1], cx = win[4 * p + 2], cy = win[4 * p + 3];
   const uint8_t *m = masks + mask_off[p];
-  const bool active = t0 < n_bands;
-  const long npx = (long)cx * cy;
-  float sum = 0.f;
-  int32_t total = 0;
-  const float *base = stack + t0;
-  const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
-  uint4 mw0 = npx > 0 ? *(const uint4 *)m : zero4;
-  uint4 mw1 = npx > 16 ? *(const uint4 *)(m + 16) : zero4;
-  int iy = 0, ix = 0;
-  for (long i0 = 0; i0 < npx; i0 += kDrillBatch) {
-    const uint4 nw0 = (i0 + 32 < npx) ? *(const uint4 *)(m + i0 + 32) : zero4;
-    const uint4 nw1 = (i0 + 48 < npx) ? *(const uint4 *)(m + i0 + 48) : zero4;
-    const uint32_t mw[8] = {mw0.x, mw0.y, mw0.z, mw0.w, mw1.x, mw1.y, mw1.z, mw1.w};
-    float x[kDrillBatch];
-    bool use[kDrillBatch];
-    long rowbase = ((long)(offY + iy) * xsize + offX) * t_stride;
-#pragma unroll
-    for (int k = 0; k < kDrillBatch; k++) {
-      use[k] = (i0 + k < npx) && ((mw[k >> 2] >> (8 * (k & 3))) & 0xFFu) == 0xFFu;
-      const bool ok = use[k] && active;
-      const float *src = base + rowbase + (long)ix * t_stride;
-      const float v = *(ok ? src : stack);
-      x[k] = ok ? v : 0.f;
-      if (++ix == cx) {
-        ix = 0;
-        iy++;
-        rowbase = ((long)(offY + iy) * xsize + offX) * t_stride;
-      }
+  int32_t *out = idx + mask_off[p];
+  __shared__ int s_wave[4];
+  const int64_t npx = (cx > 0 && cy > 0) ? (int64_t)cx * cy : 0;
+  int base = 0;
+  for (int64_t i0 = 0; i0 < npx; i0 += 256) {
+    const int64_t i = i0 + tid;
+    bool in = false;
+    int32_t pix = 0;
+    if (i < npx) {
+      const int iy = (int)(i / cx), ix = (int)(i - (int64_t)iy * cx);
+      const int gx = offX + ix, gy = offY + iy;
+      // a window reaching past the stack reads nothing there (the reference
+      // clamps its window to the raster in getDrillFileDescriptor)
+      in = m[i] == 255 && gx >= 0 && gx < xsize && gy >= 0 && gy < ysize;
+      pix = gy * xsize + gx;
     }
-#pragma unroll
-    for (int k = 0; k < kDrillBatch; k++) {
-      if (!use[k]) continue;
-      const float val = x[k];
-      if (val == nodata) continue;
-      if (pixel_count != 0) total++;
-      if (val < lo || val > hi) continue;
-      if (pixel_count == 0) {
+    const unsigned long long b = __ballot(in);
+    const int pos = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wave[wave] = __popcll(b);
+    __syncthreads();
+    int wbase = base;
+    for (int w = 0; w < wave; w++) wbase += s_wave[w];
+    if (in) out[wbase + pos] = pix;
+    base += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    __syncthreads();
+  }
+  if (tid == 0) count[p] = base;
+}
+
+__global__ void iota_kernel(int32_t *v, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = i;
+}
+
+// ---------------------------------------------------------------- per-pixel rule
+// drill.go:154-169 for one value.
+template <bool PC>
+__device__ __forceinline__ void drill_acc(float val, float nodata, float lo, float hi, float &sum, int32_t &total) {
+  if (val != nodata) {
+    if (PC) total++;
+    if (!(val < lo || val > hi)) {
+      if (PC) {
+        sum += 1.0f;
+      } else {
         sum += val;
         total++;
-      } else {
-        sum += 1.0f;
       }
     }
-    mw0 = nw0;
-    mw1 = nw1;
-  }
-  (void)ysize;
-  if (!active) return;
-  const long o = (long)p * n_bands + t0;
-  if (total > 0) {
-    band_value[o] = (double)(sum / (float)total);  // drill.go:172-174
-    band_count[o] = total;
-  } else {
-    band_value[o] = 0.0;
-    band_count[o] = 0;
   }
 }
 
-// bandStrides output rows (drill.go:128-219) from per-band results.
-__global__ void drill_rows_kernel(const double *band_value, const int32_t *band_count, int n_polys,
-                                  int n_bands, int band_strides, int rows_per_poly, double *out_value,
+// Sequential walk of compacted pixels [k0, k1) for the lane's band.
+template <bool PC>
+__device__ __forceinline__ void drill_walk(const float *__restrict__ base, int t_stride,
+                                           const int32_t *__restrict__ ip, int k0, int k1, float nodata, float lo,
+                                           float hi, float &sum, int32_t &total) {
+  int k = k0;
+  for (; k + kUnroll <= k1; k += kUnroll) {
+    float v[kUnroll];
+#pragma unroll
+    for (int q = 0; q < kUnroll; q++) v[q] = base[(int64_t)ip[k + q] * t_stride];
+#pragma unroll
+    for (int q = 0; q < kUnroll; q++) drill_acc<PC>(v[q], nodata, lo, hi, sum, total);
+  }
+  for (; k < k1; k++) drill_acc<PC>(base[(int64_t)ip[k] * t_stride], nodata, lo, hi, sum, total);
+}
+
+// Mode 0, reference order: one wave per (polygon, group of 64 selected bands),
+// polygons largest first.
+template <bool PC>
+__global__ __launch_bounds__(64) void drill_sum_kernel(const float *__restrict__ stack, int t_stride,
+                                                       const int32_t *__restrict__ idx,
+                                                       const int64_t *__restrict__ mask_off,
+                                                       const int32_t *__restrict__ count,
+                                                       const int32_t *__restrict__ order,
+                                                       const int32_t *__restrict__ tsel, int n_sel, int n_groups,
+                                                       float nodata, float lo, float hi,
+                                                       double *__restrict__ band_value,
+                                                       int32_t *__restrict__ band_count) {
+  const int item = blockIdx.x;
+  const int p = order[item / n_groups];
+  const int j = (item % n_groups) * 64 + threadIdx.x;
+  const bool active = j < n_sel;
+  const int t = active ? tsel[j] : 0;
+  float sum = 0.f;
+  int32_t total = 0;
+  drill_walk<PC>(stack + t, t_stride, idx + mask_off[p], 0, count[p], nodata, lo, hi, sum, total);
+  if (!active) return;
+  const int64_t o = (int64_t)p * n_sel + j;
+  band_value[o] = total > 0 ? (double)(sum / (float)total) : 0.0;   // drill.go:172-177
+  band_count[o] = total;
+}
+
+// ---------------------------------------------------------------- wave split
+// Exclusive scan of segments per polygon (one block; n_polys is modest).
+__global__ __launch_bounds__(1024) void drill_seg_scan_kernel(const int32_t *__restrict__ count, int n_polys,
+                                                              int32_t *__restrict__ seg_base) {
+  __shared__ int32_t s_sum[1024];
+  const int tid = threadIdx.x;
+  int carry = 0;
+  for (int c0 = 0; c0 < n_polys; c0 += 1024) {
+    const int i = c0 + tid;
+    const int v = i < n_polys ? (count[i] + kSeg - 1) / kSeg : 0;
+    s_sum[tid] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {   // Hillis-Steele inclusive scan
+      const int add = tid >= o ? s_sum[tid - o] : 0;
+      __syncthreads();
+      s_sum[tid] += add;
+      __syncthreads();
+    }
+    if (i < n_polys) seg_base[i] = carry + s_sum[tid] - v;
+    const int tot = s_sum[1023];
+    __syncthreads();
+    carry += tot;
+  }
+  if (tid == 0) seg_base[n_polys] = carry;
+}
+
+template <bool PC>
+__global__ __launch_bounds__(64) void drill_seg_kernel(const float *__restrict__ stack, int t_stride,
+                                                       const int32_t *__restrict__ idx,
+                                                       const int64_t *__restrict__ mask_off,
+                                                       const int32_t *__restrict__ count,
+                                                       const int32_t *__restrict__ seg_base, int n_polys,
+                                                       const int32_t *__restrict__ tsel, int n_sel, int n_groups,
+                                                       float nodata, float lo, float hi,
+                                                       float *__restrict__ part_sum,
+                                                       int32_t *__restrict__ part_total) {
+  const int seg = blockIdx.x / n_groups;
+  if (seg >= seg_base[n_polys]) return;
+  int lo_p = 0, hi_p = n_polys - 1;   // polygon owning segment `seg`
+  while (lo_p < hi_p) {
+    const int mid = (lo_p + hi_p + 1) >> 1;
+    if (seg_base[mid] <= seg) lo_p = mid; else hi_p = mid - 1;
+  }
+  const int p = lo_p;
+  const int s = seg - seg_base[p];
+  const int j = (blockIdx.x % n_groups) * 64 + threadIdx.x;
+  const bool active = j < n_sel;
+  const int t = active ? tsel[j] : 0;
+  const int k0 = s * kSeg, k1 = min(count[p], k0 + kSeg);
+  float sum = 0.f;
+  int32_t total = 0;
+  drill_walk<PC>(stack + t, t_stride, idx + mask_off[p], k0, k1, nodata, lo, hi, sum, total);
+  if (!active) return;
+  part_sum[(int64_t)seg * n_sel + j] = sum;
+  part_total[(int64_t)seg * n_sel + j] = total;
+}
+
+__global__ void drill_combine_kernel(const float *__restrict__ part_sum, const int32_t *__restrict__ part_total,
+                                     const int32_t *__restrict__ seg_base, int n_polys, int n_sel,
+                                     double *__restrict__ band_value, int32_t *__restrict__ band_count) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)n_polys * n_sel) return;
+  const int p = (int)(gid / n_sel), j = (int)(gid % n_sel);
+  double sum = 0.0;
+  int32_t total = 0;
+  for (int s = seg_base[p]; s < seg_base[p + 1]; s++) {
+    sum += (double)part_sum[(int64_t)s * n_sel + j];
+    total += part_total[(int64_t)s * n_sel + j];
+  }
+  band_value[gid] = total > 0 ? (double)((float)sum / (float)total) : 0.0;
+  band_count[gid] = total;
+}
+
+// ---------------------------------------------------------------- bandStrides rows
+// drill.go:128-219 from the per-read-band results: for band_strides == 1 the
+// read list is the band list; otherwise read j = 2g is band[ibBgn] and
+// j = 2g + 1 band[ibEnd - 1] of group g.
+__global__ void drill_rows_kernel(const double *band_value, const int32_t *band_count, int n_polys, int n_list,
+                                  int n_sel, int band_strides, int rows_per_poly, double *out_value,
                                   int32_t *out_count) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_polys) return;
-  const double *bv = band_value + (long)p * n_bands;
-  const int32_t *bc = band_count + (long)p * n_bands;
-  double *ov = out_value + (long)p * rows_per_poly;
-  int32_t *oc = out_count + (long)p * rows_per_poly;
-  int nrow = 0;
-  for (int ibBgn = 0; ibBgn < n_bands; ibBgn += band_strides) {
-    int ibEnd = ibBgn + band_strides;
-    if (ibEnd > n_bands) ibEnd = n_bands;
-    const int b0 = ibBgn, b1 = ibEnd - 1;
-    const int eff = band_strides == 1 ? 1 : 2;
-    ov[nrow] = bv[b0]; oc[nrow] = bc[b0]; nrow++;
-    if (band_strides > 2 && eff > 1) {
-      const double beta = (bv[b1] - bv[b0]) / (double)(band_strides - 1);
-      const double cnt = round((double)(bc[b0] + bc[b1]) / 2.0);  // math.Round: half away from zero
+  const double *bv = band_value + (int64_t)p * n_sel;
+  const int32_t *bc = band_count + (int64_t)p * n_sel;
+  double *ov = out_value + (int64_t)p * rows_per_poly;
+  int32_t *oc = out_count + (int64_t)p * rows_per_poly;
+  int nrow = 0, g = 0;
+  for (int ibBgn = 0; ibBgn < n_list; ibBgn += band_strides, g++) {
+    const int j0 = 2 * g, j1 = 2 * g + 1;
+    ov[nrow] = bv[j0]; oc[nrow] = bc[j0]; nrow++;
+    if (band_strides > 2) {
+      const double beta = (bv[j1] - bv[j0]) / (double)(band_strides - 1);
+      const double cnt = round((double)(bc[j0] + bc[j1]) / 2.0);  // math.Round: half away from zero
       for (int ip = 1; ip < band_strides - 1; ip++) {
-        ov[nrow] = bv[b0] + (double)ip * beta;
+        ov[nrow] = bv[j0] + (double)ip * beta;
         oc[nrow] = (int32_t)cnt;
         nrow++;
       }
     }
-    if (eff > 1) { ov[nrow] = bv[b1]; oc[nrow] = bc[b1]; nrow++; }
+    ov[nrow] = bv[j1]; oc[nrow] = bc[j1]; nrow++;
   }
 }
 
@@ -140,10 +260,11 @@ __global__ void drill_merge_kernel(const double *values, const int32_t *counts, 
   out[d] = (total == total && count > 0) ? total / (double)count : __longlong_as_double(0x7ff8000000000000LL);
 }
 
-int drill_rows_per_poly(int n_bands, int band_strides) {
+// ======================================================================== host
+int drill_rows_per_poly(int n_list, int band_strides) {
   if (band_strides <= 0) band_strides = 1;
   int nrow = 0;
-  for (int ibBgn = 0; ibBgn < n_bands; ibBgn += band_strides) {
+  for (int ibBgn = 0; ibBgn < n_list; ibBgn += band_strides) {
     nrow++;
     if (band_strides > 2) nrow += band_strides - 2;
     if (band_strides > 1) nrow++;
@@ -151,33 +272,133 @@ int drill_rows_per_poly(int n_bands, int band_strides) {
   return nrow;
 }
 
-int launch_drill(const float *stack, int xsize, int ysize, int n_bands, int t_stride, const int32_t *win,
-                 const int64_t *mask_off, const uint8_t *masks, int n_polys, float nodata, float lo,
-                 float hi, int pixel_count, int band_strides, double *out_value, int32_t *out_count,
-                 hipStream_t stream) {
+static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+// Number of read bands (drill.go:134-137) for a band list of n_list.
+static int read_count(int n_list, int band_strides) {
+  if (band_strides <= 1) return n_list;
+  return 2 * ((n_list + band_strides - 1) / band_strides);
+}
+
+static size_t sort_temp_bytes(int n_polys) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairsDescending(nullptr, bytes, (const int32_t *)nullptr, (int32_t *)nullptr,
+                                               (const int32_t *)nullptr, (int32_t *)nullptr, n_polys);
+  return bytes;
+}
+
+struct DrillWs {
+  int32_t *idx, *count, *order, *keys_out, *ids, *tsel, *seg_base, *part_total;
+  float *part_sum;
+  double *band_value;
+  int32_t *band_count;
+  void *sort_tmp;
+  size_t sort_bytes;
+  int64_t total;
+};
+
+static DrillWs drill_carve(void *base, int n_polys, int64_t mask_bytes, int n_list, int band_strides, int mode) {
+  DrillWs w;
+  const int np = n_polys > 0 ? n_polys : 1;
+  const int n_sel = read_count(n_list, band_strides);
+  const int64_t n_seg_max = mask_bytes / kSeg + np;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) { const int64_t o = off; off = al256(off + bytes); return o; };
+  const int64_t o_idx = take(4 * (mask_bytes > 0 ? mask_bytes : 1));
+  const int64_t o_cnt = take(4 * (int64_t)np);
+  const int64_t o_ord = take(4 * (int64_t)np);
+  const int64_t o_ko = take(4 * (int64_t)np);
+  const int64_t o_ids = take(4 * (int64_t)np);
+  const int64_t o_tsel = take(4 * (int64_t)(n_sel > 0 ? n_sel : 1));
+  const int64_t o_seg = take(4 * ((int64_t)np + 1));
+  const bool split = mode == 1;
+  const int64_t o_ps = take(split ? 4 * n_seg_max * n_sel : 0);
+  const int64_t o_pt = take(split ? 4 * n_seg_max * n_sel : 0);
+  const bool direct = band_strides <= 1;
+  const int64_t o_bv = take(direct ? 0 : 8 * (int64_t)np * n_sel);
+  const int64_t o_bc = take(direct ? 0 : 4 * (int64_t)np * n_sel);
+  w.sort_bytes = sort_temp_bytes(np);
+  const int64_t o_tmp = take((int64_t)w.sort_bytes);
+  w.total = off;
+  char *b = (char *)base;
+  w.idx = (int32_t *)(b + o_idx); w.count = (int32_t *)(b + o_cnt); w.order = (int32_t *)(b + o_ord);
+  w.keys_out = (int32_t *)(b + o_ko); w.ids = (int32_t *)(b + o_ids); w.tsel = (int32_t *)(b + o_tsel);
+  w.seg_base = (int32_t *)(b + o_seg); w.part_sum = (float *)(b + o_ps); w.part_total = (int32_t *)(b + o_pt);
+  w.band_value = (double *)(b + o_bv); w.band_count = (int32_t *)(b + o_bc); w.sort_tmp = b + o_tmp;
+  return w;
+}
+
+int64_t drill_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides, int mode) {
   if (band_strides <= 0) band_strides = 1;
-  if (n_polys <= 0) return 0;
-  if (t_stride % 4 != 0 || t_stride < n_bands) return GSKYHIP_E_ARG;
-  if (((uintptr_t)masks & 15u) != 0) return GSKYHIP_E_ARG;   // 16-B mask words
-  double *bv = out_value;
-  int32_t *bc = out_count;
-  const bool direct = band_strides == 1;
-  if (!direct) {
-    if (hipMallocAsync((void **)&bv, sizeof(double) * (size_t)n_polys * n_bands, stream) != hipSuccess)
-      return GSKYHIP_E_HIP;
-    if (hipMallocAsync((void **)&bc, sizeof(int32_t) * (size_t)n_polys * n_bands, stream) != hipSuccess)
-      return GSKYHIP_E_HIP;
+  return drill_carve(nullptr, n_polys, mask_bytes, n_list, band_strides, mode).total;
+}
+
+int launch_drill_batch(const DrillCall &c) {
+  const int band_strides = c.band_strides <= 0 ? 1 : c.band_strides;
+  const int n_list = c.bands ? c.n_list : c.n_bands;
+  if (c.n_polys <= 0 || n_list <= 0) return 0;
+  if (c.mode != 0 && c.mode != 1) return GSKYHIP_E_ARG;
+  if (c.t_stride < c.n_bands || (int64_t)c.xsize * c.ysize >= 2147483647LL) return GSKYHIP_E_ARG;
+  if (!c.workspace ||
+      c.workspace_bytes < drill_workspace_size(c.n_polys, c.mask_bytes, n_list, band_strides, c.mode))
+    return GSKYHIP_E_ARG;
+  DrillWs w = drill_carve(c.workspace, c.n_polys, c.mask_bytes, n_list, band_strides, c.mode);
+  hipStream_t s = c.stream;
+  // read list (drill.go:128-137): bands are 1-based GDAL band numbers
+  const int n_sel = read_count(n_list, band_strides);
+  std::vector<int32_t> tsel;
+  tsel.reserve(n_sel);
+  for (int ibBgn = 0; ibBgn < n_list; ibBgn += band_strides) {
+    int ibEnd = ibBgn + band_strides;
+    if (ibEnd > n_list) ibEnd = n_list;
+    const int b0 = c.bands ? c.bands[ibBgn] : ibBgn + 1;
+    const int b1 = c.bands ? c.bands[ibEnd - 1] : ibEnd;
+    if (b0 < 1 || b0 > c.n_bands || b1 < 1 || b1 > c.n_bands) return GSKYHIP_E_RANGE;
+    tsel.push_back(b0 - 1);
+    if (band_strides > 1) tsel.push_back(b1 - 1);
   }
-  // one time slice per lane: n_bands lanes per polygon (C4: 3 x 2 waves)
-  dim3 grid(n_polys, (n_bands + 127) / 128);
-  hipLaunchKernelGGL(drill_kernel, grid, dim3(128), 0, stream, stack, xsize, ysize, n_bands, t_stride,
-                     win, mask_off, masks, n_polys, nodata, lo, hi, pixel_count, bv, bc);
+  if (hipMemcpyAsync(w.tsel, tsel.data(), sizeof(int32_t) * n_sel, hipMemcpyHostToDevice, s) != hipSuccess)
+    return GSKYHIP_E_HIP;
+  hipLaunchKernelGGL(drill_compact_kernel, dim3(c.n_polys), dim3(256), 0, s, c.win, c.mask_off, c.masks, c.n_polys,
+                     c.xsize, c.ysize, w.idx, w.count);
+  const bool direct = band_strides <= 1;
+  double *bv = direct ? c.out_value : w.band_value;
+  int32_t *bc = direct ? c.out_count : w.band_count;
+  const int n_groups = (n_sel + 63) / 64;
+  const bool pc = c.pixel_count != 0;
+  if (c.mode == 0) {
+    hipLaunchKernelGGL(iota_kernel, dim3((c.n_polys + 255) / 256), dim3(256), 0, s, w.ids, c.n_polys);
+    size_t bytes = w.sort_bytes;
+    if (hipcub::DeviceRadixSort::SortPairsDescending(w.sort_tmp, bytes, w.count, w.keys_out, w.ids, w.order,
+                                                     c.n_polys, 0, 32, s) != hipSuccess)
+      return GSKYHIP_E_HIP;
+    const dim3 grid((unsigned)((int64_t)c.n_polys * n_groups));
+    if (pc)
+      hipLaunchKernelGGL(drill_sum_kernel<true>, grid, dim3(64), 0, s, c.stack, c.t_stride, w.idx, c.mask_off,
+                         w.count, w.order, w.tsel, n_sel, n_groups, c.nodata, c.lo, c.hi, bv, bc);
+    else
+      hipLaunchKernelGGL(drill_sum_kernel<false>, grid, dim3(64), 0, s, c.stack, c.t_stride, w.idx, c.mask_off,
+                         w.count, w.order, w.tsel, n_sel, n_groups, c.nodata, c.lo, c.hi, bv, bc);
+  } else {
+    hipLaunchKernelGGL(drill_seg_scan_kernel, dim3(1), dim3(1024), 0, s, w.count, c.n_polys, w.seg_base);
+    const int64_t n_seg_max = c.mask_bytes / kSeg + c.n_polys;
+    const dim3 grid((unsigned)(n_seg_max * n_groups));
+    if (pc)
+      hipLaunchKernelGGL(drill_seg_kernel<true>, grid, dim3(64), 0, s, c.stack, c.t_stride, w.idx, c.mask_off,
+                         w.count, w.seg_base, c.n_polys, w.tsel, n_sel, n_groups, c.nodata, c.lo, c.hi, w.part_sum,
+                         w.part_total);
+    else
+      hipLaunchKernelGGL(drill_seg_kernel<false>, grid, dim3(64), 0, s, c.stack, c.t_stride, w.idx, c.mask_off,
+                         w.count, w.seg_base, c.n_polys, w.tsel, n_sel, n_groups, c.nodata, c.lo, c.hi, w.part_sum,
+                         w.part_total);
+    const int64_t n_out = (int64_t)c.n_polys * n_sel;
+    hipLaunchKernelGGL(drill_combine_kernel, dim3((unsigned)((n_out + 255) / 256)), dim3(256), 0, s, w.part_sum,
+                       w.part_total, w.seg_base, c.n_polys, n_sel, bv, bc);
+  }
   if (!direct) {
-    const int rows = drill_rows_per_poly(n_bands, band_strides);
-    hipLaunchKernelGGL(drill_rows_kernel, dim3((n_polys + 127) / 128), dim3(128), 0, stream, bv, bc,
-                       n_polys, n_bands, band_strides, rows, out_value, out_count);
-    hipFreeAsync(bv, stream);
-    hipFreeAsync(bc, stream);
+    const int rows = drill_rows_per_poly(n_list, band_strides);
+    hipLaunchKernelGGL(drill_rows_kernel, dim3((c.n_polys + 127) / 128), dim3(128), 0, s, bv, bc, c.n_polys,
+                       n_list, n_sel, band_strides, rows, c.out_value, c.out_count);
   }
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
@@ -185,8 +406,8 @@ int launch_drill(const float *stack, int xsize, int ysize, int n_bands, int t_st
 int launch_drill_merge(const double *values, const int32_t *counts, int n_files, int n_dates, double *out,
                        hipStream_t stream) {
   if (n_dates <= 0) return 0;
-  hipLaunchKernelGGL(drill_merge_kernel, dim3((n_dates + 255) / 256), dim3(256), 0, stream, values,
-                     counts, n_files, n_dates, out);
+  hipLaunchKernelGGL(drill_merge_kernel, dim3((n_dates + 255) / 256), dim3(256), 0, stream, values, counts,
+                     n_files, n_dates, out);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 

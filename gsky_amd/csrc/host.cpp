@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -706,12 +707,50 @@ int gskyhip_compute_mask(const void *data, int dtype, int64_t n, const gskyhip_m
 
 int gskyhip_drill_rows(int n_bands, int band_strides) { return drill_rows_per_poly(n_bands, band_strides); }
 
+int64_t gskyhip_drill_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides, int mode) {
+  return drill_workspace_size(n_polys, mask_bytes, n_list, band_strides, mode);
+}
+
+int gskyhip_drill_batch(const float *stack, int xsize, int ysize, int n_bands, int t_stride, const int32_t *win,
+                        const int64_t *mask_off, const uint8_t *masks, int n_polys, int64_t mask_bytes,
+                        const int32_t *bands, int n_list, float nodata, float clip_lower, float clip_upper,
+                        int pixel_count, int band_strides, int mode, double *out_value, int32_t *out_count,
+                        void *workspace, int64_t workspace_bytes, void *stream) {
+  DrillCall c;
+  c.stack = stack; c.xsize = xsize; c.ysize = ysize; c.n_bands = n_bands; c.t_stride = t_stride;
+  c.win = win; c.mask_off = mask_off; c.masks = masks; c.n_polys = n_polys; c.mask_bytes = mask_bytes;
+  c.bands = bands; c.n_list = n_list; c.nodata = nodata; c.lo = clip_lower; c.hi = clip_upper;
+  c.pixel_count = pixel_count; c.band_strides = band_strides; c.mode = mode;
+  c.out_value = out_value; c.out_count = out_count;
+  c.workspace = workspace; c.workspace_bytes = workspace_bytes; c.stream = (hipStream_t)stream;
+  return launch_drill_batch(c);
+}
+
+// Round-1 entry point: sizes the workspace from the windows (synchronous
+// read-back) and runs the reference-order batch over bands 1..n_bands.
 int gskyhip_drill(const float *stack, int xsize, int ysize, int n_bands, int t_stride, const int32_t *win,
                   const int64_t *mask_off, const uint8_t *masks, int n_polys, float nodata, float clip_lower,
                   float clip_upper, int pixel_count, int band_strides, double *out_value, int32_t *out_count,
                   void *stream) {
-  return launch_drill(stack, xsize, ysize, n_bands, t_stride, win, mask_off, masks, n_polys, nodata, clip_lower,
-                      clip_upper, pixel_count, band_strides, out_value, out_count, (hipStream_t)stream);
+  if (n_polys <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<int32_t> w(4 * (size_t)n_polys);
+  std::vector<int64_t> off((size_t)n_polys);
+  if (hipMemcpyAsync(w.data(), win, w.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(off.data(), mask_off, off.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return GSKYHIP_E_HIP;
+  int64_t mask_bytes = 0;
+  for (int p = 0; p < n_polys; p++)
+    mask_bytes = std::max<int64_t>(mask_bytes, off[p] + (int64_t)std::max(0, w[4 * p + 2]) * std::max(0, w[4 * p + 3]));
+  const int64_t ws = drill_workspace_size(n_polys, mask_bytes, n_bands, band_strides, 0);
+  void *buf = nullptr;
+  if (hipMallocAsync(&buf, (size_t)ws, s) != hipSuccess) return GSKYHIP_E_HIP;
+  const int r = gskyhip_drill_batch(stack, xsize, ysize, n_bands, t_stride, win, mask_off, masks, n_polys,
+                                    mask_bytes, nullptr, n_bands, nodata, clip_lower, clip_upper, pixel_count,
+                                    band_strides, 0, out_value, out_count, buf, ws, stream);
+  if (hipFreeAsync(buf, s) != hipSuccess) return GSKYHIP_E_HIP;
+  return r;
 }
 
 int gskyhip_drill_merge(const double *values, const int32_t *counts, int n_files, int n_dates, double *out,

@@ -208,6 +208,7 @@ struct RenderArgs {
   MinMax *minmax;        // n_tiles * 3
   int write_rgba;
   const EntryD *entries;
+  int lds_stage;         // render_lds_kernel: 1 stage source windows in LDS, 0 gather from HBM
 };
 
 // ---------------------------------------------------------------- typed fast path

@@ -1,42 +1,49 @@
-// render_lds.h -- the typed LDS-staged band kernel of the batched GetMap path
-// (see the comment on render_lds_kernel).  Instantiated once per value type
-// in render_lds_<type>.hip (separate translation units build in parallel);
-// launched by launch_render (render.hip) when the batch has one value type,
-// one NN namespace and RGBA output.
+// render_lds.h -- the typed band kernel of the batched GetMap path.
+//
+// The common GetMap case -- every stack entry of the tile shares value type T,
+// nearest neighbour, every row LINEAR or POOL(linear leaves), one rendered
+// namespace, RGBA out -- runs as one lean kernel per T (no value-type switch,
+// no SGPR spills).  A 256-thread block owns a band of kBandRows tile rows (all
+// columns); wave w folds rows w, w+4, w+8, w+12, each lane 8 consecutive
+// pixels (two 16-B RGBA stores).  Items are dealt to blocks XCD-aware:
+// blocks b and b+8 share an XCD, so every XCD gets a contiguous run of
+// (tile, band) items and neighbouring bands find their shared source rows in
+// that XCD's L2.
+//
+// STAGE = true additionally stages, per band, in LDS:
+//   * the row records of the band's entries,
+//   * each entry's SOURCE WINDOW under the band: the exact extremes of the
+//     truncated source column / row over every row (the fp64 coordinate is
+//     monotone along a linear leaf, so they sit at the leaf end points) give
+//     a rectangle that is loaded once with dword loads all issued before the
+//     first wait; the per-pixel gathers then read LDS.
+// STAGE = false gathers straight from HBM with scalar row-record loads.
+// Both are bit-identical to lin_coords()/nn_px(): the per-pixel fp64
+// coordinate expressions are the same.
+//
+// Instantiated once per value type in render_lds_<type>.hip (separate
+// translation units build in parallel); launched by launch_render
+// (render.hip) when the batch has one value type, one NN namespace and RGBA
+// output.
 #pragma once
 #include "render_common.h"
 
 namespace gsky {
 
-// ---------------------------------------------------------------- LDS-staged band kernel
-// The common GetMap case -- every stack entry of the tile shares value type T,
-// nearest neighbour, every row LINEAR or POOL(linear leaves), one rendered
-// namespace, RGBA out -- as one lean kernel per T.  A 256-thread block owns a
-// band of kBandRows tile rows (all columns).  Setup stages, in LDS:
-//   * the descriptors of the tile's entries that intersect the band,
-//   * their row records for the band's rows,
-//   * each entry's SOURCE WINDOW under the band: the exact extremes of the
-//     source column / row over every row (the fp64 source coordinate is
-//     monotone along a linear leaf, so the truncated index is extreme at the
-//     leaf's end points) give a rectangle that is loaded once, coalesced,
-//     into LDS;
-// then every wave folds its rows from LDS (the per-pixel fp64 coordinates are
-// the same expressions as lin_coords(), so results are bit-identical), scales,
-// maps through the palette and streams 16-B RGBA stores.  Entries whose window
-// does not fit the LDS budget gather from HBM instead.
 constexpr int kBandRows = kLdsBandRows;
-constexpr int kBandEnt = 16;          // entries staged per pass over the band
-constexpr int kStageBytes = 24 * 1024; // LDS for source windows per block
-constexpr int kLanePx = 8;            // pixels per lane per row (2 x 16-B stores)
+constexpr int kBandEnt = 16;            // entries per pass over the band
+constexpr int kStageBytes = 24 * 1024;  // LDS for source windows per block
+constexpr int kLanePx = 8;              // pixels per lane per row
+constexpr int kStageDw = 8;             // staging dwords per thread per round (in flight together)
 
 struct BandEnt {
   const void *band;
   int32_t band_x, band_y;
   int32_t xoff, yoff, w, h;
   int32_t fill_mode, mask_pair;
-  int32_t nd, fillv;                  // Val bits of the merge nodata / window fill
-  int32_t sx0, sy0, sw, sh;           // staged source rectangle
-  int32_t soff;                       // LDS byte offset of the rectangle, -1: gather from HBM
+  Val nd, fillv;                        // merge nodata / window fill, as Val bits
+  int32_t sx0, sy0, sh, pitch_dw;       // staged rectangle: origin (sx0 dword-aligned), rows, dwords per row
+  int32_t soff;                         // LDS byte offset of the rectangle, -1: gather from HBM
   int32_t pair;
 };
 struct BandRow {
@@ -51,23 +58,15 @@ template <> __device__ constexpr int vt_code<int16_t>() { return GSKYHIP_INT16; 
 template <> __device__ constexpr int vt_code<uint16_t>() { return GSKYHIP_UINT16; }
 template <> __device__ constexpr int vt_code<float>() { return GSKYHIP_FLOAT32; }
 
-// Exact truncated source index of window column i of a linear piece (the
-// expressions of lin_coords() / nn_px()); false if the pixel is off-source.
-__device__ __forceinline__ void piece_index(double s0, double d, int dist, int &idx) {
+// Exact truncated source index at distance `dist` along a linear piece (the
+// expressions of lin_coords() / nn_px()); -1 when the coordinate is negative.
+__device__ __forceinline__ int piece_index(double s0, double d, int dist) {
   const double v = s0 + d * (double)dist;
-  const double a = v + 1.0e-10;
-  idx = __double2int_rz(a);          // saturates (>= 2^31 -> INT_MAX), like the >= size test
-  if (!(v >= 0.0)) idx = -1;         // sx < 0 (and NaN) -> not a source pixel
+  const int idx = __double2int_rz(v + 1.0e-10);   // saturates: >= 2^31 -> INT_MAX, like the >= size test
+  return (v >= 0.0) ? idx : -1;
 }
 
-template <typename T>
-__device__ __forceinline__ typename VOf<T>::type lds_get(const uint8_t *stage, int soff, int sw, int sx0, int sy0,
-                                                         int ix, int iy) {
-  const T *p = (const T *)(stage + soff);
-  return (typename VOf<T>::type)p[(iy - sy0) * sw + (ix - sx0)];
-}
-
-template <typename T, bool MASK>
+template <typename T, bool MASK, bool STAGE>
 __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                          const int32_t *__restrict__ order,
                                                          const RowRec *__restrict__ rows,
@@ -78,14 +77,11 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
   using V = typename VOf<T>::type;
   __shared__ uint32_t s_ramp[256];
   __shared__ BandEnt s_ent[kBandEnt];
-  __shared__ BandRow s_row[kBandEnt][kBandRows];
+  __shared__ BandRow s_row[STAGE ? kBandEnt : 1][STAGE ? kBandRows : 1];
   __shared__ int32_t s_ext[kBandEnt][4];     // min x, max x, min y, max y of the source indices
   __shared__ int32_t s_n, s_next;
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[kStageBytes];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[STAGE ? kStageBytes / 4 : 1];
 
-  // XCD-aware item order: blocks b and b+8 share an XCD, so give each XCD a
-  // contiguous run of (tile, band) items -- neighbouring bands and tiles then
-  // find their shared source rows in that XCD's L2.
   const int item = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (item >= n_items) return;
   const int bands_per_tile = (a.max_h + kBandRows - 1) / kBandRows;
@@ -106,13 +102,12 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
   const int32_t *ord = order + tile.pair_begin;
   const int n_entries = tp.n_entries;
   const int x0 = lane * kLanePx;
-
   const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
   const bool has_ramp = a.ramp != nullptr;
   uint8_t *rgba_tile = a.rgba + (int64_t)t * a.max_h * a.max_w * 4;
 
   // entries in merge order, kBandEnt band-intersecting ones per pass; a band
-  // with more (rare) keeps its partial canvas in its own RGBA slot between passes
+  // with more (rare) parks its partial canvas in its own RGBA slot between passes
   int e0 = 0;
   do {
     __syncthreads();   // previous pass done with the LDS tables
@@ -133,7 +128,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
         b.band = e.band; b.band_x = e.band_x; b.band_y = e.band_y;
         b.xoff = e.xoff; b.yoff = e.yoff; b.w = e.w; b.h = e.h;
         b.fill_mode = e.fill_mode; b.mask_pair = e.mask_pair;
-        b.nd = e.nd.i; b.fillv = e.fill.i;
+        b.nd = e.nd; b.fillv = e.fill;
         b.pair = p;
         b.soff = -1;
       }
@@ -149,73 +144,97 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
         s_next = nxt < n_entries ? nxt : n_entries;
       }
     }
-    if (tid < kBandEnt * 4) s_ext[tid >> 2][tid & 3] = (tid & 1) ? -1 : 0x7FFFFFFF;
+    if (STAGE && tid < kBandEnt * 4) s_ext[tid >> 2][tid & 3] = (tid & 1) ? -1 : 0x7FFFFFFF;
     __syncthreads();
     const int nb = s_n;
     const int next_e0 = s_next;
-    // row records + exact source-index extremes, one thread per (entry, row)
-    {
-      const int k = tid >> 4, rr = tid & 15;
-      const int r = band0 + rr;
-      if (k < nb && r < H) {
-        const BandEnt &b = s_ent[k];
-        const int ir = r - b.yoff;
-        if (ir >= 0 && ir < b.h) {
-          const RowRec &R = rows[(int64_t)b.pair * a.max_h + ir];
-          BandRow o;
-          o.xs0 = R.v[0]; o.ys0 = R.v[1]; o.dX = R.v[2]; o.dY = R.v[3];
-          o.kind = R.kind; o.nleaf = R.nleaf; o.pool_off = R.pool_off; o._pad = 0;
-          s_row[k][rr] = o;
-          int mnx = 0x7FFFFFFF, mxx = -1, mny = 0x7FFFFFFF, mxy = -1;
-          const int nl = R.kind == ROW_LINEAR ? 1 : R.nleaf;
-          for (int l = 0; l < nl; l++) {
-            double xs0 = o.xs0, ys0 = o.ys0, dX = o.dX, dY = o.dY;
-            int st = 0, en = b.w - 1;
-            if (R.kind != ROW_LINEAR) {
-              const Leaf &L = pool[R.pool_off + l];
-              xs0 = L.xs0; ys0 = L.ys0; dX = L.dX; dY = L.dY; st = L.start;
-              en = (l + 1 < nl) ? pool[R.pool_off + l + 1].start - 1 : b.w - 1;
+
+    if (STAGE) {
+      // row records + exact source-index extremes, one thread per (entry, row)
+      {
+        const int k = tid >> 4, rr = tid & 15;
+        const int r = band0 + rr;
+        if (k < nb && r < H) {
+          const BandEnt &b = s_ent[k];
+          const int ir = r - b.yoff;
+          if (ir >= 0 && ir < b.h) {
+            const RowRec &R = rows[(int64_t)b.pair * a.max_h + ir];
+            BandRow o;
+            o.xs0 = R.v[0]; o.ys0 = R.v[1]; o.dX = R.v[2]; o.dY = R.v[3];
+            o.kind = R.kind; o.nleaf = R.nleaf; o.pool_off = R.pool_off; o._pad = 0;
+            s_row[k][rr] = o;
+            int mnx = 0x7FFFFFFF, mxx = -1, mny = 0x7FFFFFFF, mxy = -1;
+            const int nl = R.kind == ROW_LINEAR ? 1 : R.nleaf;
+            for (int l = 0; l < nl; l++) {
+              double xs0 = o.xs0, ys0 = o.ys0, dX = o.dX, dY = o.dY;
+              int st = 0, en = b.w - 1;
+              if (R.kind != ROW_LINEAR) {
+                const Leaf &L = pool[R.pool_off + l];
+                xs0 = L.xs0; ys0 = L.ys0; dX = L.dX; dY = L.dY; st = L.start;
+                en = (l + 1 < nl) ? pool[R.pool_off + l + 1].start - 1 : b.w - 1;
+              }
+              const int ia = piece_index(xs0, dX, 0), ib = piece_index(xs0, dX, en - st);
+              const int ja = piece_index(ys0, dY, 0), jb = piece_index(ys0, dY, en - st);
+              mnx = min(mnx, min(ia, ib)); mxx = max(mxx, max(ia, ib));
+              mny = min(mny, min(ja, jb)); mxy = max(mxy, max(ja, jb));
             }
-            int ia, ib, ja, jb;
-            piece_index(xs0, dX, 0, ia);
-            piece_index(xs0, dX, en - st, ib);
-            piece_index(ys0, dY, 0, ja);
-            piece_index(ys0, dY, en - st, jb);
-            mnx = min(mnx, min(ia, ib)); mxx = max(mxx, max(ia, ib));
-            mny = min(mny, min(ja, jb)); mxy = max(mxy, max(ja, jb));
+            atomicMin(&s_ext[k][0], max(mnx, 0));
+            atomicMax(&s_ext[k][1], min(mxx, b.band_x - 1));
+            atomicMin(&s_ext[k][2], max(mny, 0));
+            atomicMax(&s_ext[k][3], min(mxy, b.band_y - 1));
           }
-          atomicMin(&s_ext[k][0], max(mnx, 0));
-          atomicMax(&s_ext[k][1], min(mxx, b.band_x - 1));
-          atomicMin(&s_ext[k][2], max(mny, 0));
-          atomicMax(&s_ext[k][3], min(mxy, b.band_y - 1));
         }
       }
-    }
-    __syncthreads();
-    if (tid == 0) {   // LDS allocation of the source rectangles, merge order
-      int used = 0;
+      __syncthreads();
+      if (tid == 0) {   // LDS allocation of the source rectangles, merge order
+        int used = 0;
+        for (int k = 0; k < nb; k++) {
+          BandEnt &b = s_ent[k];
+          b.soff = -1;
+          const int sh = s_ext[k][3] - s_ext[k][2] + 1;
+          const bool dw_rows = ((uintptr_t)b.band & 3) == 0 && ((int64_t)b.band_x * sizeof(T)) % 4 == 0;
+          if (s_ext[k][1] < s_ext[k][0] || sh <= 0 || !dw_rows) continue;
+          const int dw0 = (int)(((int64_t)s_ext[k][0] * sizeof(T)) >> 2);
+          const int dw1 = (int)((((int64_t)s_ext[k][1] + 1) * sizeof(T) + 3) >> 2);
+          const int pitch = dw1 - dw0;
+          const int bytes = pitch * sh * 4;
+          if (used + bytes > kStageBytes) continue;
+          b.sx0 = (int)((int64_t)dw0 * 4 / sizeof(T));
+          b.sy0 = s_ext[k][2];
+          b.sh = sh;
+          b.pitch_dw = pitch;
+          b.soff = used;
+          used += bytes;
+        }
+      }
+      __syncthreads();
+      // staging: kStageDw dword loads per thread issued together, then stored
       for (int k = 0; k < nb; k++) {
-        BandEnt &b = s_ent[k];
-        const int sw = s_ext[k][1] - s_ext[k][0] + 1, sh = s_ext[k][3] - s_ext[k][2] + 1;
-        b.sx0 = s_ext[k][0]; b.sy0 = s_ext[k][2]; b.sw = sw > 0 ? sw : 0; b.sh = sh > 0 ? sh : 0;
-        const int bytes = (b.sw * b.sh * (int)sizeof(T) + 15) & ~15;
-        if (b.sw > 0 && b.sh > 0 && used + bytes <= kStageBytes) { b.soff = used; used += bytes; }
-        else b.soff = -1;
+        const BandEnt &b = s_ent[k];
+        if (b.soff < 0) continue;
+        const uint32_t *src = (const uint32_t *)b.band;
+        const int64_t row_dw = (int64_t)b.band_x * sizeof(T) / 4;
+        const int64_t col_dw = (int64_t)b.sx0 * sizeof(T) / 4;
+        const int total = b.sh * b.pitch_dw;
+        uint32_t *dst = s_stage + (b.soff >> 2);
+        for (int d0 = 0; d0 < total; d0 += 256 * kStageDw) {
+          uint32_t v[kStageDw];
+#pragma unroll
+          for (int m = 0; m < kStageDw; m++) {
+            const int d = d0 + m * 256 + tid;
+            const int rr = d / b.pitch_dw, cc = d - rr * b.pitch_dw;
+            v[m] = d < total ? src[(int64_t)(b.sy0 + rr) * row_dw + col_dw + cc] : 0u;
+          }
+#pragma unroll
+          for (int m = 0; m < kStageDw; m++) {
+            const int d = d0 + m * 256 + tid;
+            if (d < total) dst[d] = v[m];
+          }
+        }
       }
+      __syncthreads();
     }
-    __syncthreads();
-    // coalesced staging: wave w copies rows w, w+4, ...; lanes walk the columns
-    for (int k = 0; k < nb; k++) {
-      const BandEnt &b = s_ent[k];
-      if (b.soff < 0) continue;
-      const T *src = (const T *)b.band;
-      T *dst = (T *)(s_stage + b.soff);
-      for (int r = wave; r < b.sh; r += 4) {
-        const T *srow = src + (int64_t)(b.sy0 + r) * b.band_x + b.sx0;
-        for (int cc = lane; cc < b.sw; cc += 64) dst[r * b.sw + cc] = srow[cc];
-      }
-    }
-    __syncthreads();
+
     // fold: wave owns rows wave, wave+4, wave+8, wave+12 of the band
     const bool first = e0 == 0, last = next_e0 >= n_entries;
 #pragma unroll 1
@@ -224,56 +243,80 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
       const int r = band0 + rr;
       if (r >= H || x0 >= W) break;
       uint8_t *dst = rgba_tile + ((int64_t)r * a.max_w + x0) * 4;
-      const bool full = x0 + kLanePx <= W && ((((uintptr_t)dst) & 15) == 0);
       V c[kLanePx];
       if (first) {
 #pragma unroll
         for (int q = 0; q < kLanePx; q++) c[q] = cnod;
       } else {
 #pragma unroll
-        for (int q = 0; q < kLanePx; q++) c[q] = (x0 + q < W) ? (V)((const V *)dst)[q] : cnod;
+        for (int q = 0; q < kLanePx; q++) c[q] = (x0 + q < W) ? ((const V *)dst)[q] : cnod;
       }
       for (int k = 0; k < nb; k++) {
         const BandEnt &b = s_ent[k];
-        const int ir = r - b.yoff;
-        if (ir < 0 || ir >= b.h) continue;
-        const BandRow &R = s_row[k][rr];
-        const V nd = (V)b.nd;
-        const V fillv = (V)b.fillv;
+        const int yoff = __builtin_amdgcn_readfirstlane(b.yoff);
+        const int eh = __builtin_amdgcn_readfirstlane(b.h);
+        const int ir = r - yoff;
+        if (ir < 0 || ir >= eh) continue;
+        const int pair = __builtin_amdgcn_readfirstlane(b.pair);
+        const int ew = b.w, bx = b.band_x, by = b.band_y;
+        const V nd = as_v<T>(b.nd), fillv = as_v<T>(b.fillv);
+        const int fill_mode = b.fill_mode;
+        const int soff = __builtin_amdgcn_readfirstlane(b.soff);
         const int ic0 = x0 - b.xoff;
-        const bool linear = R.kind == ROW_LINEAR;
-#pragma unroll
-        for (int q = 0; q < kLanePx; q++) {
+        double xs0, ys0, dX, dY;
+        int kind, nleaf, pool_off;
+        if (STAGE) {
+          const BandRow &R = s_row[k][rr];
+          xs0 = R.xs0; ys0 = R.ys0; dX = R.dX; dY = R.dY;
+          kind = R.kind; nleaf = R.nleaf; pool_off = R.pool_off;
+        } else {
+          const RowRec &R = rows[(int64_t)pair * a.max_h + ir];   // wave-uniform: scalar loads
+          xs0 = R.v[0]; ys0 = R.v[1]; dX = R.v[2]; dY = R.v[3];
+          kind = R.kind; nleaf = R.nleaf; pool_off = R.pool_off;
+        }
+        kind = __builtin_amdgcn_readfirstlane(kind);
+        const uint8_t *sbase = (const uint8_t *)s_stage + (soff >= 0 ? soff : 0);
+        const int sx0 = b.sx0, sy0 = b.sy0, pitch_b = b.pitch_dw * 4;
+        // one pixel: source value or window fill, then the ordered fold
+        auto px = [&](int q, double sx, double sy) {
           const int ic = ic0 + q;
-          const bool in = (unsigned)ic < (unsigned)b.w && x0 + q < W;
-          double xs0 = R.xs0, ys0 = R.ys0, dX = R.dX, dY = R.dY;
-          double dist = (double)ic0 + (double)q;   // exact: small integers (lin_coords)
-          if (!linear) {                            // POOL row: the leaf holding column ic
-            const Leaf *lv = pool + R.pool_off;
-            const int icc = in ? ic : 0;
-            int l = 0;
-            while (l + 1 < R.nleaf && lv[l + 1].start <= icc) l++;
-            xs0 = lv[l].xs0; ys0 = lv[l].ys0; dX = lv[l].dX; dY = lv[l].dY;
-            dist = (double)(icc - lv[l].start);
-          }
-          const double sy = ys0 + dY * dist;
-          const double sx = xs0 + dX * dist;
+          const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
           const int ix = __double2int_rz(sx + 1.0e-10), iy = __double2int_rz(sy + 1.0e-10);
-          const bool ok = in && (sx >= 0.0) && (sy >= 0.0) && ix < b.band_x && iy < b.band_y;
+          const bool ok = in && (sx >= 0.0) && (sy >= 0.0) && ix < bx && iy < by;
           V v;
-          if (b.soff >= 0) {
-            v = lds_get<T>(s_stage, b.soff, b.sw, b.sx0, b.sy0, ok ? ix : b.sx0, ok ? iy : b.sy0);
+          if (STAGE && soff >= 0) {
+            const int lofs = ok ? (iy - sy0) * pitch_b + (ix - sx0) * (int)sizeof(T) : 0;
+            v = (V)(*(const T *)(sbase + lofs));
           } else {
-            const int64_t idx = ok ? (int64_t)iy * b.band_x + ix : 0;
+            const int64_t idx = ok ? (int64_t)iy * bx + ix : 0;
             v = (V)((const GPTR(T))b.band)[idx];
           }
           v = ok ? v : fillv;
           bool take = in && (v != nd);
           if (MASK && b.mask_pair >= 0) {
-            if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, ents[b.pair], ic, ir);
+            if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, ents[pair], ic, ir);
           }
-          const bool t2 = take && (!b.fill_mode || c[q] == nd);
+          const bool t2 = take && (!fill_mode || c[q] == nd);
           c[q] = t2 ? v : c[q];
+        };
+        if (kind == ROW_LINEAR) {
+          const double d0 = (double)ic0;
+#pragma unroll
+          for (int q = 0; q < kLanePx; q++) {
+            const double dist = d0 + (double)q;   // exact: small integers (lin_coords)
+            px(q, xs0 + dX * dist, ys0 + dY * dist);
+          }
+        } else {                                   // POOL row: the leaf holding each column
+          const Leaf *lv = pool + pool_off;
+#pragma unroll
+          for (int q = 0; q < kLanePx; q++) {
+            const int ic = ic0 + q;
+            const int icc = ((unsigned)ic < (unsigned)ew) ? ic : 0;
+            int l = 0;
+            while (l + 1 < nleaf && lv[l + 1].start <= icc) l++;
+            const double dist = (double)(icc - lv[l].start);
+            px(q, lv[l].xs0 + lv[l].dX * dist, lv[l].ys0 + lv[l].dY * dist);
+          }
         }
       }
       if (!last) {   // partial canvas parked in the slot (raw values), re-read next pass
@@ -283,38 +326,42 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
         continue;
       }
       // utils.Scale + palette / grey, two 16-B non-temporal stores
-      uint32_t px[kLanePx];
+      uint32_t pxo[kLanePx];
 #pragma unroll
       for (int q = 0; q < kLanePx; q++) {
         const uint32_t bb = scale_t<T>(sk, c[q]);
         const uint32_t col = has_ramp ? s_ramp[bb & 0xFFu] : (0xFF000000u | (bb << 16) | (bb << 8) | bb);
-        px[q] = (created && bb != 0xFFu) ? col : 0u;
+        pxo[q] = (created && bb != 0xFFu) ? col : 0u;
       }
-      if (full) {
-        u32x4 v0 = {px[0], px[1], px[2], px[3]};
-        u32x4 v1 = {px[4], px[5], px[6], px[7]};
+      if (x0 + kLanePx <= W && ((((uintptr_t)dst) & 15) == 0)) {
+        u32x4 v0 = {pxo[0], pxo[1], pxo[2], pxo[3]};
+        u32x4 v1 = {pxo[4], pxo[5], pxo[6], pxo[7]};
         __builtin_nontemporal_store(v0, (GPTR(u32x4))dst);
         __builtin_nontemporal_store(v1, (GPTR(u32x4))(dst + 16));
       } else {
 #pragma unroll
         for (int q = 0; q < kLanePx; q++)
-          if (x0 + q < W) ((uint32_t *)dst)[q] = px[q];
+          if (x0 + q < W) ((uint32_t *)dst)[q] = pxo[q];
       }
     }
     e0 = next_e0;
   } while (e0 < n_entries);
 }
 
-
 template <typename T>
 void launch_lds_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
   const int per_xcd = (n_items + 7) / 8;
-  if (mask)
-    hipLaunchKernelGGL((render_lds_kernel<T, true>), dim3((unsigned)per_xcd * 8), dim3(256), 0, s, a, a.entries,
-                       a.order, a.rows, a.pool, a.tplans, a.tiles, n_items, per_xcd);
-  else
-    hipLaunchKernelGGL((render_lds_kernel<T, false>), dim3((unsigned)per_xcd * 8), dim3(256), 0, s, a, a.entries,
-                       a.order, a.rows, a.pool, a.tplans, a.tiles, n_items, per_xcd);
+  const dim3 grid((unsigned)per_xcd * 8);
+#define GSKY_LDS_LAUNCH(M, S)                                                                                   \
+  hipLaunchKernelGGL((render_lds_kernel<T, M, S>), grid, dim3(256), 0, s, a, a.entries, a.order, a.rows, a.pool, \
+                     a.tplans, a.tiles, n_items, per_xcd)
+  const bool stage = a.lds_stage != 0;
+  if (mask) {
+    if (stage) GSKY_LDS_LAUNCH(true, true); else GSKY_LDS_LAUNCH(true, false);
+  } else {
+    if (stage) GSKY_LDS_LAUNCH(false, true); else GSKY_LDS_LAUNCH(false, false);
+  }
+#undef GSKY_LDS_LAUNCH
 }
 
 void launch_lds_i16(const RenderArgs &a, bool mask, int n_items, hipStream_t s);

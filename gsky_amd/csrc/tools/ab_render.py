@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""A/B timing of the C2 render phase (phase-2 kernels only, HIP events on the
+launch stream) for the kernel variants: typed band kernel with LDS-staged
+source windows, typed band kernel gathering from HBM, and the generic kernel.
+One JSON line per variant.  Used to pick defaults; bench.py is the contract."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import gsky_amd  # noqa: E402
+from gsky_amd import synth  # noqa: E402
+from tests.helpers import gpu_batch  # noqa: E402
+
+
+def time_render(b, sp, pal, reps):
+    s = torch.cuda.current_stream()
+    b.render(sp, pal, phase=1)
+    for _ in range(3):
+        b.render(sp, pal, phase=2)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ts = []
+    for _ in range(reps):
+        ev[0].record(s)
+        b.render(sp, pal, phase=2)
+        ev[1].record(s)
+        torch.cuda.synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]))
+    return float(np.median(ts)), float(np.min(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--config", default="c2")
+    args = ap.parse_args()
+    cfg = synth.config_c2() if args.config == "c2" else synth.config_c5()
+    b = gpu_batch(cfg)
+    sp = gsky_amd.ScaleParams(*cfg.scale)
+    pal = gsky_amd.Palette(cfg.palette, True) if cfg.palette else None
+    ref = None
+    for name, typed, stage in [("typed_stage", True, "1"), ("typed_direct", True, "0"), ("generic", False, "1")]:
+        os.environ["GSKYHIP_LDS_STAGE"] = stage
+        b.typed = typed
+        med, mn = time_render(b, sp, pal, args.reps)
+        out = b.render(sp, pal).clone()
+        torch.cuda.synchronize()
+        same = True if ref is None else bool(torch.equal(out, ref))
+        ref = out if ref is None else ref
+        print(json.dumps({"variant": name, "config": args.config, "render_ms_median": round(med, 4),
+                          "render_ms_min": round(mn, 4), "identical_to_first": same}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -9,7 +9,7 @@
 from __future__ import annotations
 
 import ctypes as C
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -47,9 +47,24 @@ class DrillStack:
         return self
 
 
-def pack_masks(windows: Sequence[Tuple[int, int, int, int]], masks: Sequence[np.ndarray], device=None):
+class MaskBatch:
+    """Per-polygon window masks packed for the GPU: `win` (n, 4) int32
+    {off_x, off_y, count_x, count_y}, `mask_off` (n,) int64 byte offsets
+    (16-byte aligned, in polygon order, non-overlapping) and `masks` (uint8,
+    255 = inside).  Iterates as (win, mask_off, masks) for round-1 callers."""
+
+    def __init__(self, win, mask_off, masks):
+        self.win, self.mask_off, self.masks = win, mask_off, masks
+        self.n = int(win.shape[0])
+        self.mask_bytes = int(masks.numel())
+
+    def __iter__(self):
+        return iter((self.win, self.mask_off, self.masks))
+
+
+def pack_masks(windows: Sequence[Tuple[int, int, int, int]], masks: Sequence[np.ndarray], device=None) -> MaskBatch:
     """Concatenate per-polygon window masks (count_y, count_x; 255 = inside),
-    16-byte aligned, into HBM.  Returns (win tensor, mask_off tensor, masks tensor)."""
+    16-byte aligned, into HBM."""
     offs = []
     total = 0
     for m in masks:
@@ -61,25 +76,39 @@ def pack_masks(windows: Sequence[Tuple[int, int, int, int]], masks: Sequence[np.
     dev = torch.device(device or "cuda")
     win = torch.tensor(np.asarray(windows, np.int32).reshape(-1, 4), device=dev)
     off = torch.tensor(np.asarray(offs, np.int64), device=dev)
-    return win, off, torch.from_numpy(buf).to(dev)
+    return MaskBatch(win, off, torch.from_numpy(buf).to(dev))
 
 
-def read_data(stack: DrillStack, win: torch.Tensor, mask_off: torch.Tensor, masks: torch.Tensor,
-              clip_lower: float, clip_upper: float, pixel_count: int = 0, band_strides: int = 1,
-              decile_count: int = 0):
-    """readData for every polygon window -> (values f64, counts i32), each
-    (n_polys, rows) with rows = len(TimeSeries) / nCols of drill.go:225."""
+REFERENCE_ORDER, WAVE_SPLIT = 0, 1
+
+
+def read_data(stack: DrillStack, win, mask_off=None, masks=None, clip_lower: float = -3.4028234663852886e38,
+              clip_upper: float = 3.4028234663852886e38, pixel_count: int = 0, band_strides: int = 1,
+              decile_count: int = 0, bands: Optional[Sequence[int]] = None, mode: int = REFERENCE_ORDER):
+    """readData (drill.go:90-227) for every polygon window -> (values f64,
+    counts i32), each (n_polys, rows) with rows = len(TimeSeries) / nCols of
+    drill.go:225.  `win` is a MaskBatch (or the round-1 (win, mask_off,
+    masks) tensors); `bands` the reference's 1-based band list (default all);
+    mode REFERENCE_ORDER is bit-exact, WAVE_SPLIT within 1e-5 relative."""
     if decile_count:
         raise NotImplementedError("drill deciles (drill.go:229-273) are SURVEY 8f 'next'")
-    n_polys = win.shape[0]
-    rows = lib().gskyhip_drill_rows(stack.n_bands, band_strides)
-    vals = torch.empty((n_polys, rows), dtype=torch.float64, device=stack.stack.device)
-    cnts = torch.empty((n_polys, rows), dtype=torch.int32, device=stack.stack.device)
-    check(lib().gskyhip_drill(C.c_void_p(stack.stack.data_ptr()), stack.xsize, stack.ysize, stack.n_bands,
-                              stack.t_stride, C.c_void_p(win.data_ptr()), C.c_void_p(mask_off.data_ptr()),
-                              C.c_void_p(masks.data_ptr()), n_polys, stack.nodata, clip_lower, clip_upper,
-                              pixel_count, band_strides, C.c_void_p(vals.data_ptr()),
-                              C.c_void_p(cnts.data_ptr()), _stream()), "drill")
+    mb = win if isinstance(win, MaskBatch) else MaskBatch(win, mask_off, masks)
+    n_polys = mb.n
+    blist = None if bands is None else np.ascontiguousarray(bands, np.int32)
+    n_list = stack.n_bands if blist is None else len(blist)
+    rows = lib().gskyhip_drill_rows(n_list, band_strides)
+    dev = stack.stack.device
+    vals = torch.empty((n_polys, rows), dtype=torch.float64, device=dev)
+    cnts = torch.empty((n_polys, rows), dtype=torch.int32, device=dev)
+    ws_bytes = lib().gskyhip_drill_workspace_size(n_polys, mb.mask_bytes, n_list, band_strides, mode)
+    ws = torch.empty(max(1, int(ws_bytes)), dtype=torch.uint8, device=dev)
+    check(lib().gskyhip_drill_batch(C.c_void_p(stack.stack.data_ptr()), stack.xsize, stack.ysize, stack.n_bands,
+                                    stack.t_stride, C.c_void_p(mb.win.data_ptr()), C.c_void_p(mb.mask_off.data_ptr()),
+                                    C.c_void_p(mb.masks.data_ptr()), n_polys, mb.mask_bytes,
+                                    blist.ctypes.data_as(C.c_void_p) if blist is not None else None, n_list,
+                                    stack.nodata, clip_lower, clip_upper, pixel_count, band_strides, mode,
+                                    C.c_void_p(vals.data_ptr()), C.c_void_p(cnts.data_ptr()),
+                                    C.c_void_p(ws.data_ptr()), ws.numel(), _stream()), "drill")
     return vals, cnts
 
 

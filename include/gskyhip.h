@@ -278,17 +278,34 @@ int gskyhip_compute_mask(const void *data, int dtype, int64_t n, const gskyhip_m
 /* readData (worker/gdalprocess/drill.go:90-227), mean / pixel-count mode,
  * decileCount = 0, for a batch of polygons over one time stack.
  *   stack: dev float32, time-innermost layout [y][x][t] of an
- *     xsize x ysize x n_bands stack, t fastest, t padded to t_stride
- *     (a multiple of 4, >= n_bands; 16-byte aligned pixel vectors).
- *   win: dev int32 4 per polygon {off_x, off_y, count_x, count_y}.
- *   mask_off: dev int64 per polygon, offset into masks (dev uint8, 255 = in,
- *     row-major count_x*count_y).  masks must be 16-byte aligned, every
- *     mask_off a multiple of 16 and every polygon's mask padded to a multiple
- *     of 16 bytes (the kernel reads masks in 16-byte words; gsky_amd.drill.
- *     pack_masks lays them out so); a misaligned masks pointer -> E_ARG.
- *   band_strides as drill.go:110-219.  Rows per polygon = *rows_per_poly.
- *   out_value: dev f64, out_count: dev i32, n_polys x rows_per_poly. */
+ *     xsize x ysize x n_bands stack, t fastest, t padded to t_stride >= n_bands
+ *     (xsize * ysize < 2^31).
+ *   win: dev int32 4 per polygon {off_x, off_y, count_x, count_y}
+ *     (DrillFileDescriptor, drill.go:25-29); pixels of a window outside the
+ *     stack count as outside the mask.
+ *   mask_off: dev int64 per polygon, byte offset into masks (dev uint8,
+ *     255 = in, row-major count_x*count_y); the polygons' mask regions must
+ *     not overlap and every region must lie inside [0, mask_bytes).
+ *   bands: HOST int32 list of 1-based band numbers (the reference's
+ *     `bands []int32`), or NULL for 1..n_bands (n_list ignored).
+ *   band_strides as drill.go:110-219.  Rows per polygon =
+ *     gskyhip_drill_rows(n_list, band_strides).
+ *   mode 0: reference summation order, means bit-exact; mode 1: wave-split
+ *     reduction (float32 partials over 1024-pixel segments, combined in
+ *     float64), within 1e-5 relative of mode 0, not bound by the largest polygon.
+ *   out_value: dev f64, out_count: dev i32, n_polys x rows.
+ *   workspace: dev, gskyhip_drill_workspace_size bytes. */
 int gskyhip_drill_rows(int n_bands, int band_strides);
+int64_t gskyhip_drill_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides,
+                                     int mode);
+int gskyhip_drill_batch(const float *stack, int xsize, int ysize, int n_bands, int t_stride,
+                        const int32_t *win, const int64_t *mask_off, const uint8_t *masks,
+                        int n_polys, int64_t mask_bytes, const int32_t *bands, int n_list,
+                        float nodata, float clip_lower, float clip_upper, int pixel_count,
+                        int band_strides, int mode, double *out_value, int32_t *out_count,
+                        void *workspace, int64_t workspace_bytes, void *stream);
+/* Round-1 form (bands 1..n_bands, mode 0): sizes and allocates its workspace
+ * itself (one synchronous read-back of win / mask_off). */
 int gskyhip_drill(const float *stack, int xsize, int ysize, int n_bands, int t_stride,
                   const int32_t *win, const int64_t *mask_off, const uint8_t *masks,
                   int n_polys, float nodata, float clip_lower, float clip_upper,
