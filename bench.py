@@ -1,28 +1,41 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X GSKY raster hot path (BASELINE.json metric).
 
-Workload (N=1): BASELINE.json configs[1] = C2: a batch of 4096 512x512
+Headline (`value`): BASELINE.json configs[1] = C2, a batch of 4096 512x512
 EPSG:3857 GetMap tiles from 16 Albers EPSG:3577 int16 4000x4000 granules,
 nearest-neighbour, time-ordered merge + byte scale + palette.
 A step = one pass of the whole batch: planning kernels (windows, merge order,
 approximate-transformer rows) + the fused warp/merge/scale/palette kernel,
 granules already resident in HBM.
 
-Multi-GPU: one process per GPU (torch.distributed, RCCL); every rank serves
-its own C2 batch (tiles are independent requests, no data-path collective):
-weak scaling, value = all ranks' output pixels / max-over-ranks time.
+Multi-GPU: one process per GPU (torch.distributed, RCCL).  The C2 request
+stream is partitioned -- rank r renders a contiguous block of the 4096 tiles
+(independent requests, contiguous spatial blocks for granule
+locality) and uploads only the granules its tiles touch; no data-path
+collective.  Total work is fixed as N grows: "scaling": "strong", `value` =
+all 4096 tiles' output pixels / max-over-ranks time.
 
-Extra fields: roofline of the dominant kernel (render, HIP events on the
-launch stream), cpu_baseline (the CPU oracle, rank 0, N=1, bounded sample),
-p50_tile_ms (C1 single-tile latency).
+The same line carries the other BASELINE configs under "configs" (each timed
+the same way: warmup, barrier + synchronize, K steps, max over ranks):
+  C1  single 256^2 tile: GPU p50/p99 latency, CPU (oracle) p50/p99 beside it;
+  C3  WCS 16384^2 float32 bilinear coverage, chunk rows sharded over ranks,
+      RCCL gather to rank 0 (the only collective of the path);
+  C4  drill 1000 polygons x 365 slices, reference-order (bit-exact) and
+      wave-split modes, polygons dealt largest-first round-robin to ranks;
+  C5  80 MODIS overview tiles with QA masks: tiles/s and p50 tile latency.
+`roofline` is the dominant kernel of C2 (HIP events on its launch stream);
+`cpu_baseline` the oracle (C restatement, test infrastructure) on the box's
+host cores, rank 0, N=1 only.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
 import time
+import traceback
 
 import numpy as np
 import torch
@@ -34,6 +47,81 @@ import gsky_amd  # noqa: E402
 from gsky_amd import GranuleSet, Mask, Palette, ScaleParams, TileBatch, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "reprojected+merged output Mpix/s (whole node) at 1/2/4/8 MI355X; p50 tile ms"
+CLIP = (-3.4028234663852886e38, 3.4028234663852886e38)   # ows.go:1373-1381
+
+
+# ---------------------------------------------------------------- plumbing
+class Ctx:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.dist = dist
+        else:
+            torch.cuda.set_device(0)
+        self.device = torch.device("cuda", torch.cuda.current_device())
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x: float) -> float:
+        if not self.dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(self, step, steps: int, warmup: int) -> float:
+        """W untimed steps, then K steps bracketed by barrier + synchronize;
+        returns the max-over-ranks seconds of the K steps."""
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        self.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        self.barrier()
+        return self.max_over_ranks(time.perf_counter() - t0)
+
+
+def event_ms(fn, reps: int = 10) -> float:
+    """Mean device time of fn() on the current stream (HIP events)."""
+    s = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ts = []
+    for _ in range(reps):
+        ev[0].record(s)
+        fn()
+        ev[1].record(s)
+        torch.cuda.synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]))
+    return float(np.mean(ts))
+
+
+def block_part(n: int, rank: int, world: int):
+    base, extra = divmod(n, world)
+    s = rank * base + min(rank, extra)
+    return list(range(s, s + base + (1 if rank < extra else 0)))
+
+
+def sub_config(cfg, ids):
+    """Tiles `ids` of cfg with only the granules they touch (indices remapped)."""
+    used = sorted({g for i in ids for g in cfg.pairs[i]})
+    remap = {g: k for k, g in enumerate(used)}
+    sub = synth.SynthConfig(cfg.name, [cfg.granules[g] for g in used], cfg.dst_srs, [cfg.tiles[i] for i in ids],
+                            [[remap[g] for g in cfg.pairs[i]] for i in ids], cfg.namespaces, cfg.scale, cfg.palette,
+                            cfg.resample, cfg.mask, cfg.bbox, cfg.out_w, cfg.out_h)
+    return sub
 
 
 def build_batch(cfg, device):
@@ -47,39 +135,310 @@ def build_batch(cfg, device):
     return TileBatch(gs, cfg.dst_srs, cfg.tiles, cfg.pairs, cfg.namespaces, mask)
 
 
-def algorithmic_bytes(cfg) -> int:
-    """Unique source bytes touched (every granule pixel lies under the tile
-    set) + RGBA output bytes."""
-    src = sum(g.data.nbytes for g in cfg.granules)
-    return src + cfg.out_pixels * 4
+def host_cores():
+    """Cores this process may use: the cgroup CPU quota (the GPU box grants a
+    16-core share of a larger machine) or the affinity mask."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(p))))
+    except Exception:
+        pass
+    return n
 
 
-def cpu_baseline(cfg, n_tiles: int, threads: int):
-    from oracle import oracle as O
-    from tests.helpers import oracle_render
-    ids = np.linspace(0, len(cfg.tiles) - 1, n_tiles).round().astype(int).tolist()
-    sub = synth.subset(cfg, ids)
-    oracle_render(O, synth.subset(cfg, ids[:2]), n_threads=threads)  # warm
-    t0 = time.perf_counter()
-    oracle_render(O, sub, n_threads=threads)
-    dt = time.perf_counter() - t0
-    return sub.out_pixels / dt / 1e6, dt
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
 
 
-def c1_latency(device, reps: int = 50):
+def lib_sha():
+    h = hashlib.sha256()
+    with open(os.path.join(ROOT, "gsky_amd", "libgskyhip.so"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(name: str):
+    """HBM bytes per launch from a committed PMC pass of THIS library build
+    (profiles/pmc_<name>.json records the lib hash it was measured on)."""
+    p = os.path.join(ROOT, "profiles", "pmc_%s.json" % name)
+    try:
+        d = json.load(open(p))
+        if d.get("lib_sha16") == lib_sha():
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def oracle_render(O, cfg, threads):
+    from tests.helpers import oracle_render as orr
+    return orr(O, cfg, n_threads=threads)
+
+
+# ---------------------------------------------------------------- C2 (headline)
+def run_c2(ctx: Ctx, args):
+    full = synth.config_c2()
+    ids = block_part(len(full.tiles), ctx.rank, ctx.world)
+    cfg = sub_config(full, ids)
+    batch = build_batch(cfg, ctx.device)
+    sp, pal = ScaleParams(*cfg.scale), Palette(cfg.palette, True)
+    batch.render(sp, pal)
+    torch.cuda.synchronize()
+    if batch.status() != 0:
+        raise RuntimeError("render status %d" % batch.status())
+    dt = ctx.timed(lambda: batch.render(sp, pal), args.steps, args.warmup)
+    total_px = full.out_pixels * args.steps
+    plan_ms = event_ms(lambda: batch.render(sp, pal, phase=1), max(3, args.steps))
+    render_ms = event_ms(lambda: batch.render(sp, pal, phase=2), max(3, args.steps))
+    # algorithmic bytes of rank 0's launch: unique source bytes under its tiles
+    # (its share of the 0.512 GB, by output pixels; exact at N=1) + RGBA out
+    src = sum(g.data.nbytes for g in full.granules) * cfg.out_pixels / full.out_pixels
+    abytes = int(src + cfg.out_pixels * 4)
+    achieved = abytes / (render_ms / 1e3) / 1e9
+    out = {
+        "value": round(total_px / dt / 1e6, 1), "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "config": {"workload": "C2: %d x 512x512 EPSG:3857 tiles from %d EPSG:3577 int16 4000x4000 granules, "
+                               "nearest, time-ordered merge + scale + palette" % (len(full.tiles), len(full.granules)),
+                   "tiles_per_step": len(full.tiles), "tiles_per_rank": len(ids), "pairs_rank0": batch.n_pairs,
+                   "parallelism": "tile blocks over %d rank(s) (contiguous, granules per rank)" % ctx.world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("render_c2")
+                     if ctx.world == 1 else None,
+                     "kernel": "render_lds_kernel<int16> + render_general_kernel (phase 2, rank 0)",
+                     "kernel_ms": round(render_ms, 4), "plan_ms": round(plan_ms, 4),
+                     "algorithmic_bytes_per_launch": abytes, "lib_sha16": lib_sha()},
+    }
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
+        from oracle import oracle as O
+        cores = host_cores()
+        oracle_render(O, synth.subset(full, [0, 1]), cores)                 # warm
+        runs = []
+        for _ in range(args.cpu_runs):
+            t0 = time.perf_counter()
+            oracle_render(O, full, cores)
+            runs.append(time.perf_counter() - t0)
+        one = synth.subset(full, list(range(0, 4096, 16)))                   # 256 tiles
+        t0 = time.perf_counter()
+        oracle_render(O, one, 1)
+        t1 = time.perf_counter() - t0
+        med = float(np.median(runs))
+        out["cpu_baseline"] = {
+            "value": round(full.out_pixels / med / 1e6, 2), "unit": "Mpix/s", "cores": cores, "kind": "port",
+            "one_core_value": round(one.out_pixels / t1 / 1e6, 2),
+            "cpu": cpu_model(), "runs_s": [round(r, 3) for r in runs],
+            "sample": "all 4096 C2 tiles rendered by oracle/ (C restatement of warp_operation_fast + merge + "
+                      "Scale + palette) on %d threads = the box's CPU share (cgroup quota), median of %d runs; "
+                      "1-core figure on 256 tiles" % (cores, args.cpu_runs)}
+    del batch
+    return out
+
+
+# ---------------------------------------------------------------- C1
+def run_c1(ctx: Ctx, args):
     cfg = synth.config_c1()
-    b = build_batch(cfg, device)
+    b = build_batch(cfg, ctx.device)
     sp = ScaleParams(*cfg.scale)
-    for _ in range(5):
+    for _ in range(10):
         b.render(sp)
     torch.cuda.synchronize()
     ts = []
-    for _ in range(reps):
+    for _ in range(args.c1_reps):
         t0 = time.perf_counter()
         b.render(sp)
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t0) * 1e3)
-    return float(np.median(ts))
+    out = {"workload": "C1: one 256x256 EPSG:3857 tile from a 3600x1800 EPSG:4326 f32 granule, nearest, scale",
+           "p50_tile_ms": round(float(np.percentile(ts, 50)), 4), "p99_tile_ms": round(float(np.percentile(ts, 99)), 4),
+           "reps": args.c1_reps, "timing": "host wall per call incl. launch + synchronize"}
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
+        from oracle import oracle as O
+        cts = []
+        for _ in range(args.c1_cpu_reps):
+            t0 = time.perf_counter()
+            oracle_render(O, cfg, 1)
+            cts.append((time.perf_counter() - t0) * 1e3)
+        out["cpu_p50_tile_ms"] = round(float(np.percentile(cts, 50)), 4)
+        out["cpu_p99_tile_ms"] = round(float(np.percentile(cts, 99)), 4)
+        out["cpu"] = "oracle/, 1 thread (one gsky-gdal-process equivalent), %d reps" % args.c1_cpu_reps
+    return out
+
+
+# ---------------------------------------------------------------- C3
+def run_c3(ctx: Ctx, args):
+    from gsky_amd import coverage
+    cfg = synth.config_c3()
+    W, H = cfg.out_w, cfg.out_h
+    chunks = coverage.chunk_requests(cfg.bbox, W, H)
+    nrows = coverage.n_chunk_rows(chunks)
+    rows = [coverage.band_of_rank(nrows, r, ctx.world) for r in range(ctx.world)]
+    extents = [coverage.band_extent(chunks, rw) for rw in rows]
+    sel = [c for c in chunks if rows[ctx.rank][0] <= c.row < rows[ctx.rank][1]]
+    sub = synth.SynthConfig("C3", cfg.granules, cfg.dst_srs, [(c.bbox, c.width, c.height) for c in sel],
+                            [cfg.index_chunk(c.bbox) for c in sel], cfg.namespaces, cfg.scale, None, cfg.resample)
+    sub = sub_config(sub, list(range(len(sel))))
+    b = build_batch(sub, ctx.device)
+    sp = ScaleParams(*cfg.scale)
+    top, bottom = extents[ctx.rank]
+
+    def render():
+        return b.render(sp, resample=cfg.resample, rgba=False)
+
+    def step():
+        cv = render()
+        canv = [b.canvas_view(cv, i, 0, "Float32")[: c.height, : c.width] for i, c in enumerate(sel)]
+        band = coverage.place_chunks(canv, sel, top, bottom - top, W, device=ctx.device)
+        if ctx.world > 1:
+            coverage.gather_coverage(band, extents, H, W)
+        return band
+
+    dt = ctx.timed(step, args.c3_steps, 1)
+    render_ms = event_ms(render, 3)
+    gather_ms = None
+    if ctx.world > 1:
+        band = step()
+        torch.cuda.synchronize()
+        gather_ms = ctx.max_over_ranks(event_ms(lambda: coverage.gather_coverage(band, extents, H, W), 3))
+    src = sum(cfg.granules[0].data.nbytes for _ in sub.granules)
+    abytes = src + sub.out_pixels * 4
+    ach = abytes / (render_ms / 1e3) / 1e9
+    out = {"workload": "C3: WCS GetCoverage %dx%d float32 bilinear EPSG:4326->3857 mosaic from %d granules, "
+                       "%d chunks of <=1024^2 (ows.go:817-831)" % (W, H, len(cfg.granules), len(chunks)),
+           "value": round(W * H * args.c3_steps / dt / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(dt / args.c3_steps * 1e3, 3),
+           "step": "render own chunk rows (canvases) + place into the band" + (" + RCCL gather to rank 0"
+                                                                             if ctx.world > 1 else ""),
+           "chunk_rows_rank0": rows[0], "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "plan + bilinear render (rank 0)",
+                        "kernel_ms": round(render_ms, 4), "algorithmic_bytes_per_launch": int(abytes)}}
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
+        from oracle import oracle as O
+        ids = list(range(0, len(chunks), max(1, len(chunks) // 16)))[:16]
+        cs = synth.subset(cfg, ids)
+        cores = host_cores()
+        t0 = time.perf_counter()
+        oracle_render(O, cs, cores)
+        ct = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(cs.out_pixels / ct / 1e6, 2), "unit": "Mpix/s", "cores": cores,
+                               "kind": "port", "sample": "%d of the %d chunks by oracle/ (bilinear warp + merge), "
+                                                         "%d threads" % (len(ids), len(chunks), cores)}
+    del b
+    return out
+
+
+# ---------------------------------------------------------------- C4
+def c4_stack(n_bands, size, device):
+    """The C4 time stack built directly in HBM, time-innermost (values equal
+    synth.config_c4's float32 bands)."""
+    from gsky_amd import drill
+    idx = np.arange(size * size, dtype=np.uint64) + np.uint64(synth.SEED0 << 32)
+    noise = (synth.uniform01(synth.splitmix64(idx)) * 0.05).astype(np.float32).reshape(size, size)
+    nod = synth.uniform01(synth.splitmix64(idx + np.uint64(1 << 40))).reshape(size, size) < 0.05
+    t = np.arange(n_bands, dtype=np.float64)
+    base = torch.from_numpy((0.2 + 0.1 * np.sin(2 * np.pi * t / 365.0)).astype(np.float32)).to(device)
+    fac = torch.from_numpy((1.0 + (t % 7) * 0.01).astype(np.float32)).to(device)
+    ts = (n_bands + 3) // 4 * 4
+    st = torch.zeros((size, size, ts), dtype=torch.float32, device=device)
+    nz = torch.from_numpy(noise).to(device)
+    for y0 in range(0, size, 256):
+        st[y0:y0 + 256, :, :n_bands] = base + nz[y0:y0 + 256, :, None] * fac
+    st[torch.from_numpy(nod).to(device)] = -9999.0
+    return drill.DrillStack.from_time_innermost(st, n_bands, -9999.0)
+
+
+def run_c4(ctx: Ctx, args):
+    from gsky_amd import drill
+    geo = synth.config_c4(n_bands=1, size=2048, n_polys=1000)
+    n_bands = 365
+    st = c4_stack(n_bands, 2048, ctx.device)
+    inside = [int((m == 255).sum()) for m in geo.masks]
+    order = sorted(range(len(geo.masks)), key=lambda p: -inside[p])
+    mine = order[ctx.rank::ctx.world]             # largest-first, round-robin over ranks
+    mb = drill.pack_masks([geo.windows[p] for p in mine], [geo.masks[p] for p in mine], ctx.device)
+    res = {}
+    for name, mode in (("reference_order", drill.REFERENCE_ORDER), ("wave_split", drill.WAVE_SPLIT)):
+        dt = ctx.timed(lambda: drill.read_data(st, mb, *CLIP, mode=mode), args.steps, args.warmup)
+        k_ms = event_ms(lambda: drill.read_data(st, mb, *CLIP, mode=mode), 5)
+        px = sum(geo.windows[p][2] * geo.windows[p][3] for p in mine)
+        abytes = sum(inside[p] for p in mine) * n_bands * 4 + px
+        ach = abytes / (k_ms / 1e3) / 1e9
+        res[name] = {"value": round(len(geo.masks) * n_bands * args.steps / dt, 1), "unit": "polygon-slices/s",
+                     "ms_per_step": round(dt / args.steps * 1e3, 4),
+                     "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(k_ms, 4),
+                                  "kernel": "drill compaction + %s reduction (rank 0)" % name,
+                                  "algorithmic_bytes_per_launch": int(abytes)}}
+    out = {"workload": "C4: WPS drill zonal mean, 1000 star polygons x 365 daily f32 slices of 2048^2, "
+                       "ALL_TOUCHED masks, clip +-MaxFloat32", "polygons_rank0": len(mine), **res}
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle import oracle as O
+        ids = order[:: max(1, len(order) // args.c4_cpu_polys)][: args.c4_cpu_polys]
+        subs = {}
+        for p in ids:
+            x0, y0, w, h = geo.windows[p]
+            subs[p] = st.stack[y0:y0 + h, x0:x0 + w, :n_bands].permute(2, 0, 1).contiguous().cpu().numpy()
+        cores = host_cores()
+
+        def one(p):
+            return O.drill_read_data(subs[p], geo.masks[p], -9999.0, CLIP[0], CLIP[1], 0, 1)
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(cores) as ex:
+            list(ex.map(one, ids))
+        ct = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(ids) * n_bands / ct, 1), "unit": "polygon-slices/s",
+                               "cores": cores, "kind": "port",
+                               "sample": "%d polygons (every %d-th by size) x %d slices, oracle readData, %d threads"
+                                         % (len(ids), max(1, len(order) // args.c4_cpu_polys), n_bands, cores)}
+    del st
+    return out
+
+
+# ---------------------------------------------------------------- C5
+def run_c5(ctx: Ctx, args):
+    full = synth.config_c5()
+    ids = block_part(len(full.tiles), ctx.rank, ctx.world)
+    cfg = sub_config(full, ids)
+    b = build_batch(cfg, ctx.device)
+    sp = ScaleParams(*cfg.scale)
+    dt = ctx.timed(lambda: b.render(sp), args.steps, args.warmup)
+    # p50 single-tile latency: each sampled tile as its own request
+    lat = []
+    for i in range(0, len(cfg.tiles), max(1, len(cfg.tiles) // 8)):
+        one = build_batch(sub_config(cfg, [i]), ctx.device)
+        for _ in range(3):
+            one.render(sp)
+        torch.cuda.synchronize()
+        for _ in range(10):
+            t0 = time.perf_counter()
+            one.render(sp)
+            torch.cuda.synchronize()
+            lat.append((time.perf_counter() - t0) * 1e3)
+    out = {"workload": "C5: 80 512x512 EPSG:3857 overview tiles (z4+z5) from 256 MODIS sinusoidal int16 granules + "
+                       "256 QA mask granules with overview pyramids, mask 00000001, grey scaling",
+           "tiles_per_s": round(len(full.tiles) * args.steps / dt, 1),
+           "value": round(full.out_pixels * args.steps / dt / 1e6, 1), "unit": "Mpix/s",
+           "ms_per_step": round(dt / args.steps * 1e3, 4),
+           "p50_tile_ms": round(float(np.percentile(lat, 50)), 4),
+           "p50_timing": "host wall of a one-tile request (plan + render + synchronize), rank 0"}
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
+        from oracle import oracle as O
+        cores = host_cores()
+        t0 = time.perf_counter()
+        oracle_render(O, full, cores)
+        ct = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(full.tiles) / ct, 2), "unit": "tiles/s", "cores": cores,
+                               "kind": "port", "sample": "all 80 tiles by oracle/, %d threads" % cores}
+    del b
+    return out
 
 
 def main():
@@ -87,118 +446,43 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--scale", type=float, default=1.0, help="granule size scale (1 = 4000^2)")
-    ap.add_argument("--tiles", type=int, default=64, help="tiles per side (64 -> 4096 tiles)")
-    ap.add_argument("--cpu-tiles", type=int, default=4096, help="CPU baseline sample (tiles)")
+    ap.add_argument("--only", default="c2,c1,c3,c4,c5", help="comma list of configs (c2 is the headline)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-c1", action="store_true")
+    ap.add_argument("--no-c1", action="store_true", help="(compat) drop C1")
+    ap.add_argument("--cpu-runs", type=int, default=5)
+    ap.add_argument("--c1-reps", type=int, default=1000)
+    ap.add_argument("--c1-cpu-reps", type=int, default=200)
+    ap.add_argument("--c3-steps", type=int, default=3)
+    ap.add_argument("--c4-cpu-polys", type=int, default=160)
     args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    device = torch.device("cuda", torch.cuda.current_device())
-
-    cfg = synth.config_c2(scale=args.scale, tiles_per_side=args.tiles, tile_px=512)
-    batch = build_batch(cfg, device)
-    sp = ScaleParams(*cfg.scale)
-    pal = Palette(cfg.palette, True)
-
-    for _ in range(args.warmup):
-        batch.render(sp, pal)
-    torch.cuda.synchronize()
-    if batch.status() != 0:
-        raise RuntimeError("render status %d" % batch.status())
-
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        batch.render(sp, pal)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    ms_per_step = dt / args.steps * 1e3
-    total_px = cfg.out_pixels * world * args.steps
-    value = total_px / dt / 1e6
-
-    # dominant kernel: the fused render (phase 2), HIP events on its stream
-    stream = torch.cuda.current_stream()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    plan_ms, render_ms = [], []
-    for _ in range(max(3, args.steps)):
-        ev[0].record(stream)
-        batch.render(sp, pal, phase=1)
-        ev[1].record(stream)
-        batch.render(sp, pal, phase=2)
-        ev[2].record(stream)
-        torch.cuda.synchronize()
-        plan_ms.append(ev[0].elapsed_time(ev[1]))
-        render_ms.append(ev[1].elapsed_time(ev[2]))
-    t_render = float(np.mean(render_ms)) / 1e3
-    abytes = algorithmic_bytes(cfg)
-    achieved = abytes / t_render / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_render_c2.json")
-    if os.path.exists(pmc) and args.scale == 1.0 and args.tiles == 64:
+    only = [s.strip().lower() for s in args.only.split(",") if s.strip()]
+    if args.no_c1 and "c1" in only:
+        only.remove("c1")
+    ctx = Ctx()
+    out = {"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": ctx.world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "int16", "data": "synthetic (splitmix64 granules, SURVEY.md 8d)"}
+    if "c2" in only:
+        out.update(run_c2(ctx, args))
+    configs = {}
+    for name, fn in (("C1", run_c1), ("C3", run_c3), ("C4", run_c4), ("C5", run_c5)):
+        if name.lower() not in only:
+            continue
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
-    out = {
-        "metric": "reprojected+merged output Mpix/s (whole node) at 1/2/4/8 MI355X; p50 tile ms",
-        "value": round(value, 1),
-        "unit": "Mpix/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int16",
-        "data": "synthetic (splitmix64 granules, SURVEY.md 8d)",
-        "config": {"workload": "C2: %d x %dx%d EPSG:3857 tiles from %d EPSG:3577 int16 %dx%d granules, nearest, "
-                               "time-ordered merge + scale + palette" % (
-                                   len(cfg.tiles), 512, 512, len(cfg.granules), cfg.granules[0].data.shape[1],
-                                   cfg.granules[0].data.shape[0]),
-                   "tiles_per_step_per_gpu": len(cfg.tiles), "pairs": batch.n_pairs,
-                   "parallelism": "tile batches per GPU, %d rank(s)" % world},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "render_fast_kernel (+ render_general, phase 2)",
-                     "kernel_ms": round(t_render * 1e3, 4), "plan_ms": round(float(np.mean(plan_ms)), 4),
-                     "algorithmic_bytes_per_launch": abytes},
-    }
-    if rank == 0 and world == 1:
-        if not args.no_c1:
-            out["p50_tile_ms"] = round(c1_latency(device), 4)
-            out["p50_tile_config"] = "C1: one 256x256 EPSG:3857 tile from a 3600x1800 EPSG:4326 f32 granule"
-        if not args.no_cpu:
-            threads = min(16, os.cpu_count() or 1)
-            v, secs = cpu_baseline(cfg, args.cpu_tiles, threads)
-            out["cpu_baseline"] = {"value": round(v, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
-                                   "sample": "%d C2 tiles (512x512) rendered by oracle/ (C restatement of "
-                                             "warp_operation_fast + merge + Scale + palette), %d threads, "
-                                             "%.2f s wall" % (args.cpu_tiles, threads, secs)}
-    if rank == 0:
-        print(json.dumps(out))
-    if dist:
-        dist.destroy_process_group()
+            configs[name] = fn(ctx, args)
+        except Exception as ex:   # an auxiliary config must not lose the headline line
+            configs[name] = {"error": "%s: %s" % (type(ex).__name__, ex)}
+            if ctx.rank == 0:
+                traceback.print_exc()
+        torch.cuda.empty_cache()
+    if configs:
+        out["configs"] = configs
+        if "C1" in configs and "p50_tile_ms" in configs["C1"]:
+            out["p50_tile_ms"] = configs["C1"]["p50_tile_ms"]
+    if ctx.rank == 0:
+        print(json.dumps(out), flush=True)
+    if ctx.dist:
+        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

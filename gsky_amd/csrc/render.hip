@@ -1385,10 +1385,7 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.canvas_tile_stride = a.canvas_ns_stride * n_out;
   a.minmax = cv.minmax;
   a.entries = cv.entries;
-  // GSKYHIP_LDS_STAGE=0|1 selects the band kernel's gather source (A/B knob;
-  // results are identical either way)
-  const char *st = getenv("GSKYHIP_LDS_STAGE");
-  a.lds_stage = st ? atoi(st) : 1;
+  a.lds_stage = 0;   // set by launch_lds_kernels
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;

@@ -126,3 +126,24 @@ def test_c4_full_drill_bit_exact(gpu, oracle, c4):
            if not (np.array_equal(cnts[p], ec) and np.array_equal(vals[p].view(np.uint64), ev.view(np.uint64)))]
     assert not bad, "C4: %d polygons differ (first %s)" % (len(bad), bad[:5])
     assert sum(int(ec.sum()) for _, ec in exp) > 1e8
+
+
+def test_c4_full_drill_wave_split(gpu, oracle, c4):
+    """C4 in the wave-split mode: counts exact, means within 1e-5 relative."""
+    import torch
+
+    from gsky_amd import drill
+    clip = (-3.4028234663852886e38, 3.4028234663852886e38)
+    st = drill.DrillStack(torch.from_numpy(c4.bands), c4.nodata, gpu)
+    mb = drill.pack_masks(c4.windows, c4.masks, gpu)
+    vals, cnts = drill.read_data(st, mb, clip[0], clip[1], mode=drill.WAVE_SPLIT)
+    vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
+    del st
+    exp = _drill_oracle(oracle, c4, clip, 0, 1)
+    worst = 0.0
+    for p, (ev, ec) in enumerate(exp):
+        assert np.array_equal(cnts[p], ec), p
+        ok = ec > 0
+        if ok.any():
+            worst = max(worst, float((np.abs(vals[p][ok] - ev[ok]) / np.abs(ev[ok])).max()))
+    assert worst <= 1e-5, worst

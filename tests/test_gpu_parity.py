@@ -452,3 +452,64 @@ def test_lds_kernel_masks(gpu, oracle):
     got = b.render(gsky_amd.ScaleParams(*cfg.scale)).cpu().numpy()
     exp = oracle_render(oracle, cfg)
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("strides", [1, 3])
+def test_drill_band_list(gpu, oracle, strides):
+    """readData's `bands []int32` (drill.go:90, 128-143): an arbitrary 1-based
+    band list, in list order, with bandStrides grouping over list positions."""
+    import torch
+
+    from gsky_amd import drill
+    dc = synth.config_c4(n_bands=37, size=256, n_polys=12, rmin=4, rmax=40)
+    st = drill.DrillStack(torch.from_numpy(dc.bands), dc.nodata, gpu)
+    mb = drill.pack_masks(dc.windows, dc.masks, gpu)
+    blist = [5, 3, 17, 1, 2, 36, 37, 9, 9, 20, 11]
+    vals, cnts = drill.read_data(st, mb, clip_lower=-1e30, clip_upper=1e30, band_strides=strides, bands=blist)
+    vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
+    sel = np.asarray(blist) - 1
+    for p, (x0, y0, w, h) in enumerate(dc.windows):
+        sub = dc.bands[sel][:, y0:y0 + h, x0:x0 + w]
+        ev, ec = oracle.drill_read_data(sub, dc.masks[p], dc.nodata, -1e30, 1e30, 0, strides)
+        assert np.array_equal(cnts[p], ec), p
+        assert np.array_equal(vals[p].view(np.uint64), ev.view(np.uint64)), p
+
+
+@pytest.mark.parametrize("pc,clip", [(0, (-1e30, 1e30)), (1, (0.21, 0.26))])
+def test_drill_wave_split_mode(gpu, oracle, pc, clip):
+    """Mode 1 (wave-split reduction): counts exact, means within 1e-5 relative
+    of the reference summation order."""
+    import torch
+
+    from gsky_amd import drill
+    dc = synth.config_c4(n_bands=70, size=512, n_polys=20, rmin=20, rmax=120)
+    st = drill.DrillStack(torch.from_numpy(dc.bands), dc.nodata, gpu)
+    mb = drill.pack_masks(dc.windows, dc.masks, gpu)
+    vals, cnts = drill.read_data(st, mb, clip_lower=clip[0], clip_upper=clip[1], pixel_count=pc,
+                                 mode=drill.WAVE_SPLIT)
+    vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
+    for p, (x0, y0, w, h) in enumerate(dc.windows):
+        sub = dc.bands[:, y0:y0 + h, x0:x0 + w]
+        ev, ec = oracle.drill_read_data(sub, dc.masks[p], dc.nodata, clip[0], clip[1], pc, 1)
+        assert np.array_equal(cnts[p], ec), p
+        rel = np.abs(vals[p] - ev) / np.maximum(np.abs(ev), 1e-30)
+        assert rel.max() <= 1e-5, (p, rel.max())
+
+
+def test_drill_window_past_stack_edge(gpu, oracle):
+    """A window reaching past the stack reads nothing outside it:
+    equals the reference on the clipped window."""
+    import torch
+
+    from gsky_amd import drill
+    dc = synth.config_c4(n_bands=9, size=128, n_polys=1, rmin=4, rmax=8)
+    st = drill.DrillStack(torch.from_numpy(dc.bands), dc.nodata, gpu)
+    wins = [(118, 120, 30, 20), (-5, -3, 12, 9)]
+    masks = [np.full((20, 30), 255, np.uint8), np.full((9, 12), 255, np.uint8)]
+    vals, cnts = drill.read_data(st, drill.pack_masks(wins, masks, gpu))
+    vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
+    for p, (x0, y0, w, h) in enumerate(wins):
+        xa, ya, xb, yb = max(0, x0), max(0, y0), min(128, x0 + w), min(128, y0 + h)
+        sub = dc.bands[:, ya:yb, xa:xb]
+        ev, ec = oracle.drill_read_data(sub, np.full((yb - ya, xb - xa), 255, np.uint8), dc.nodata, -1e30, 1e30)
+        assert np.array_equal(cnts[p], ec) and np.array_equal(vals[p].view(np.uint64), ev.view(np.uint64))

@@ -40,6 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--config", default="c2")
+    ap.add_argument("--variant", default="", help="run only this variant (for rocprofv3 passes)")
     args = ap.parse_args()
     cfg = synth.config_c2() if args.config == "c2" else synth.config_c5()
     b = gpu_batch(cfg)
@@ -47,6 +48,8 @@ def main():
     pal = gsky_amd.Palette(cfg.palette, True) if cfg.palette else None
     ref = None
     for name, typed, stage in [("typed_stage", True, "1"), ("typed_direct", True, "0"), ("generic", False, "1")]:
+        if args.variant and name != args.variant:
+            continue
         os.environ["GSKYHIP_LDS_STAGE"] = stage
         b.typed = typed
         med, mn = time_render(b, sp, pal, args.reps)

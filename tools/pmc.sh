@@ -1,18 +1,21 @@
 #!/bin/bash
-# PMC passes for the C2 render kernel (one counter group per rocprofv3 run,
-# kernel-trace only: never combined with sys/runtime traces).
+# PMC passes for one kernel, one counter group per rocprofv3 run (kernel-trace
+# only, never combined with sys/runtime traces), each under its own time limit.
+#   PMC_CMD   the program to profile (default: the C2 A/B tool, direct variant)
+#   PMC_OUT   output dir (default gpurun_out/pmc)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmc
+OUT=${PMC_OUT:-gpurun_out/pmc}
+mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --no-cpu --no-c1 ${BENCH_ARGS:-}"
+CMD=${PMC_CMD:-"python3 tools/ab_render.py --variant typed_direct --reps 3"}
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" "TCC_HIT_sum TCC_MISS_sum" \
            "SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/pmc/p$i -o run --output-format csv -- \
-    python3 bench.py $ARGS > gpurun_out/pmc/p$i.log 2>&1
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/p$i" -o run --output-format csv -- \
+    $CMD > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi

@@ -18,9 +18,12 @@ usage: python tools/pmc_summary.py [pmc_dir] [kernel_substring] [out.json]
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
@@ -33,7 +36,15 @@ def main():
             if kern in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     means = {k: sum(v) / len(v) for k, v in agg.items()}
-    res = {"kernel_substring": kern, "counters_per_launch": means}
+    h = hashlib.sha256(open(os.path.join(ROOT, "gsky_amd", "libgskyhip.so"), "rb").read()).hexdigest()[:16]
+    res = {"kernel_substring": kern, "counters_per_launch": means, "lib_sha16": h}
+    m = means
+    if "SQ_WAVE_CYCLES" in m and m.get("SQ_WAVE_CYCLES"):
+        res["wait_any_frac"] = m.get("SQ_WAIT_ANY", 0) / m["SQ_WAVE_CYCLES"]
+        res["valu_active_frac_of_wave_cycles"] = m.get("SQ_ACTIVE_INST_VALU", 0) / m["SQ_WAVE_CYCLES"]
+    if "SQ_INSTS_VALU" in m and m.get("SQ_WAVES"):
+        res["valu_insts_per_wave"] = m["SQ_INSTS_VALU"] / m["SQ_WAVES"]
+        res["vmem_rd_per_wave"] = m.get("SQ_INSTS_VMEM_RD", 0) / m["SQ_WAVES"]
     if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
         fetch = means["FETCH_SIZE"] * 1024.0
         write = means["WRITE_SIZE"] * 1024.0
