@@ -16,6 +16,7 @@
 #include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 #include <strings.h>
 
@@ -1479,4 +1480,323 @@ void oracle_drill_merge(const double *values, const int32_t *counts,
         }
         out[d] = (!isnan(total) && count > 0) ? total / (double)count : NAN;
     }
+}
+
+/* ======================================================================== */
+/* worker/gdalprocess/drill.go:363-423 getDrillFileDescriptor + 275-327      */
+/* createMask, with GDAL 3.0.1's rasterizer (alg/llrasterize.cpp             */
+/* GDALdllImageFilledPolygon + GDALdllImageLineAllTouched, ALL_TOUCHED=TRUE) */
+/* restated [ext].  OGR_G_Buffer(g, 0, 30) is taken as the identity for a    */
+/* valid simple polygon (GEOS buffer(0) keeps its vertex set).               */
+/* ======================================================================== */
+typedef struct { double *x, *y; int *part_size; int n_parts, n_pts, cap_pts, cap_parts; } or_rings;
+
+static void rings_push(or_rings *r, double x, double y) {
+    if (r->n_pts == r->cap_pts) {
+        r->cap_pts = r->cap_pts ? 2 * r->cap_pts : 64;
+        r->x = (double *)realloc(r->x, sizeof(double) * r->cap_pts);
+        r->y = (double *)realloc(r->y, sizeof(double) * r->cap_pts);
+    }
+    r->x[r->n_pts] = x; r->y[r->n_pts] = y; r->n_pts++;
+    r->part_size[r->n_parts - 1]++;
+}
+static void rings_new_part(or_rings *r) {
+    if (r->n_parts == r->cap_parts) {
+        r->cap_parts = r->cap_parts ? 2 * r->cap_parts : 8;
+        r->part_size = (int *)realloc(r->part_size, sizeof(int) * r->cap_parts);
+    }
+    r->part_size[r->n_parts++] = 0;
+}
+static void rings_free(or_rings *r) { free(r->x); free(r->y); free(r->part_size); memset(r, 0, sizeof(*r)); }
+
+/* Nested JSON arrays of numbers: depth of the first '[' below `p` decides
+ * the level of a ring (Polygon 3 = [ring][pt][xy], MultiPolygon 4). */
+static const char *skip_ws(const char *p) { while (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r') p++; return p; }
+
+static const char *parse_coords(const char *p, int depth, int ring_depth, or_rings *r) {
+    p = skip_ws(p);
+    if (*p != '[') return NULL;
+    p++;
+    if (depth == ring_depth) rings_new_part(r);
+    if (depth == ring_depth + 1) {               /* a point [x, y(, z)] */
+        char *e;
+        const double x = strtod(p, &e);
+        if (e == p) return NULL;
+        p = skip_ws(e);
+        if (*p != ',') return NULL;
+        p++;
+        const double y = strtod(p, &e);
+        if (e == p) return NULL;
+        p = skip_ws(e);
+        while (*p == ',') {        /* a third (z) coordinate is ignored */
+            p++;
+            strtod(p, &e);
+            if (e == p) return NULL;
+            p = skip_ws(e);
+        }
+        if (*p != ']') return NULL;
+        rings_push(r, x, y);
+        return p + 1;
+    }
+    p = skip_ws(p);
+    if (*p == ']') return p + 1;
+    for (;;) {
+        p = parse_coords(p, depth + 1, ring_depth, r);
+        if (!p) return NULL;
+        p = skip_ws(p);
+        if (*p == ',') { p++; continue; }
+        if (*p == ']') return p + 1;
+        return NULL;
+    }
+}
+
+/* The geometry of a GeoJSON Feature or a bare Polygon / MultiPolygon. */
+static int parse_geojson(const char *js, or_rings *r) {
+    const char *g = strstr(js, "\"geometry\"");
+    const char *base = g ? g : js;
+    const char *mp = strstr(base, "\"MultiPolygon\"");
+    const char *pg = strstr(base, "\"Polygon\"");
+    const char *c = strstr(base, "\"coordinates\"");
+    if (!c || (!mp && !pg)) return -1;
+    c = strchr(c, ':');
+    if (!c) return -1;
+    const int ring_depth = mp ? 2 : 1;            /* depth (from 0) at which rings start */
+    if (!parse_coords(c + 1, 0, ring_depth, r)) return -1;
+    return r->n_parts > 0 ? 0 : -1;
+}
+
+static int point_in_rings(const or_rings *r, double px, double py) {   /* even-odd over all rings */
+    int inside = 0, off = 0;
+    for (int k = 0; k < r->n_parts; k++) {
+        const int n = r->part_size[k];
+        for (int i = 0, j = n - 1; i < n; j = i++) {
+            const double xi = r->x[off + i], yi = r->y[off + i], xj = r->x[off + j], yj = r->y[off + j];
+            if ((yi > py) != (yj > py) && px < (xj - xi) * (py - yi) / (yj - yi) + xi) inside = !inside;
+        }
+        off += n;
+    }
+    return inside;
+}
+
+/* Envelope of (rings intersect [x0,x1]x[y0,y1]): vertices inside, edge /
+ * side crossings, rectangle corners inside the polygon.  0 = empty. */
+static int intersection_envelope(const or_rings *r, double x0, double y0, double x1, double y1, double env[4]) {
+    double mnx = HUGE_VAL, mny = HUGE_VAL, mxx = -HUGE_VAL, mxy = -HUGE_VAL;
+    int any = 0;
+#define OR_ADD(px, py)                       \
+    do {                                     \
+        const double _x = (px), _y = (py);   \
+        any = 1;                             \
+        mnx = _x < mnx ? _x : mnx;           \
+        mxx = _x > mxx ? _x : mxx;           \
+        mny = _y < mny ? _y : mny;           \
+        mxy = _y > mxy ? _y : mxy;           \
+    } while (0)
+    int off = 0;
+    for (int k = 0; k < r->n_parts; k++) {
+        const int n = r->part_size[k];
+        for (int i = 0; i < n; i++) {
+            const double ax = r->x[off + i], ay = r->y[off + i];
+            if (ax >= x0 && ax <= x1 && ay >= y0 && ay <= y1) OR_ADD(ax, ay);
+            const int j = (i + 1) % n;
+            const double bx = r->x[off + j], by = r->y[off + j];
+            const double xs[2] = {x0, x1}, ys[2] = {y0, y1};
+            for (int s = 0; s < 2; s++) {
+                const double X = xs[s];
+                if ((ax - X) * (bx - X) <= 0 && ax != bx) {
+                    const double y = ay + (X - ax) * (by - ay) / (bx - ax);
+                    if (y >= y0 && y <= y1) OR_ADD(X, y);
+                }
+                const double Y = ys[s];
+                if ((ay - Y) * (by - Y) <= 0 && ay != by) {
+                    const double x = ax + (Y - ay) * (bx - ax) / (by - ay);
+                    if (x >= x0 && x <= x1) OR_ADD(x, Y);
+                }
+            }
+        }
+        off += n;
+    }
+    const double cx[4] = {x0, x1, x1, x0}, cy[4] = {y0, y0, y1, y1};
+    for (int k = 0; k < 4; k++) if (point_in_rings(r, cx[k], cy[k])) OR_ADD(cx[k], cy[k]);
+#undef OR_ADD
+    if (!any) return 0;
+    env[0] = mnx; env[1] = mny; env[2] = mxx; env[3] = mxy;
+    return 1;
+}
+
+static double fmt6(double v) {    /* Go fmt "%f" then OGR's parse: 6 decimals */
+    char buf[64];
+    snprintf(buf, sizeof(buf), "%.6f", v);
+    return strtod(buf, NULL);
+}
+
+static void burn(uint8_t *m, int w, int h, int x, int y) { if (x >= 0 && x < w && y >= 0 && y < h) m[(int64_t)y * w + x] = 255; }
+
+static int cmp_int(const void *a, const void *b) { const int x = *(const int *)a, y = *(const int *)b; return (x > y) - (x < y); }
+
+/* GDALdllImageFilledPolygon (GDAL 3.0.1 alg/llrasterize.cpp). */
+static void filled_polygon(const or_rings *r, uint8_t *m, int w, int h) {
+    const int n = r->n_pts;
+    if (!r->n_parts || n == 0) return;
+    int *ints = (int *)malloc(sizeof(int) * (n + 1));
+    double dminy = r->y[0], dmaxy = r->y[0];
+    for (int i = 1; i < n; i++) { if (r->y[i] < dminy) dminy = r->y[i]; if (r->y[i] > dmaxy) dmaxy = r->y[i]; }
+    int miny = (int)dminy, maxy = (int)dmaxy;
+    if (miny < 0) miny = 0;
+    if (maxy >= h) maxy = h - 1;
+    const int minx = 0, maxx = w - 1;
+    for (int y = miny; y <= maxy; y++) {
+        int partoffset = 0, part = 0, nints = 0;
+        const double dy = y + 0.5;
+        for (int i = 0; i < n; i++) {
+            if (i == partoffset + r->part_size[part]) { partoffset += r->part_size[part]; part++; }
+            int ind1, ind2;
+            if (i == partoffset) { ind1 = partoffset + r->part_size[part] - 1; ind2 = partoffset; }
+            else { ind1 = i - 1; ind2 = i; }
+            double dy1 = r->y[ind1], dy2 = r->y[ind2];
+            if ((dy1 < dy && dy2 < dy) || (dy1 > dy && dy2 > dy)) continue;
+            double dx1, dx2;
+            if (dy1 < dy2) { dx1 = r->x[ind1]; dx2 = r->x[ind2]; }
+            else if (dy1 > dy2) { dy2 = r->y[ind1]; dy1 = r->y[ind2]; dx2 = r->x[ind1]; dx1 = r->x[ind2]; }
+            else {   /* horizontal: bottom segments filled separately, top ones skipped */
+                if (r->x[ind1] > r->x[ind2]) {
+                    const int hx1 = (int)floor(r->x[ind2] + 0.5), hx2 = (int)floor(r->x[ind1] + 0.5);
+                    if (hx1 > maxx || hx2 <= minx) continue;
+                    for (int x = hx1 < 0 ? 0 : hx1; x <= hx2 - 1 && x <= maxx; x++) burn(m, w, h, x, y);
+                }
+                continue;
+            }
+            if (dy < dy2 && dy >= dy1) {
+                const double intersect = (dy - dy1) * (dx2 - dx1) / (dy2 - dy1) + dx1;
+                ints[nints++] = (int)floor(intersect + 0.5);
+            }
+        }
+        qsort(ints, nints, sizeof(int), cmp_int);
+        for (int i = 0; i + 1 < nints; i += 2) {
+            if (ints[i] <= maxx && ints[i + 1] > minx) {
+                int xs = ints[i], xe = ints[i + 1] - 1;
+                if (xs > xe) continue;
+                if (xs < 0) xs = 0;
+                if (xe >= w) xe = w - 1;
+                for (int x = xs; x <= xe; x++) burn(m, w, h, x, y);
+            }
+        }
+    }
+    free(ints);
+}
+
+/* GDALdllImageLineAllTouched (GDAL 3.0.1), burn value only. */
+static void line_all_touched(const or_rings *r, uint8_t *m, int w, int h) {
+    for (int k = 0, n = 0; k < r->n_parts; n += r->part_size[k++]) {
+        for (int j = 1; j < r->part_size[k]; j++) {
+            double dfX = r->x[n + j - 1], dfY = r->y[n + j - 1];
+            double dfXEnd = r->x[n + j], dfYEnd = r->y[n + j];
+            if ((dfY < 0.0 && dfYEnd < 0.0) || (dfY > h && dfYEnd > h) || (dfX < 0.0 && dfXEnd < 0.0) ||
+                (dfX > w && dfXEnd > w))
+                continue;
+            if (dfX > dfXEnd) { double t = dfX; dfX = dfXEnd; dfXEnd = t; t = dfY; dfY = dfYEnd; dfYEnd = t; }
+            if (floor(dfX) == floor(dfXEnd) || fabs(dfX - dfXEnd) < .01) {       /* vertical */
+                if (dfYEnd < dfY) { const double t = dfY; dfY = dfYEnd; dfYEnd = t; }
+                const int iX = (int)floor(dfXEnd);
+                int iY = (int)floor(dfY), iYEnd = (int)floor(dfYEnd);
+                if (iX < 0 || iX >= w) continue;
+                if (iY < 0) iY = 0;
+                if (iYEnd >= h) iYEnd = h - 1;
+                for (; iY <= iYEnd; iY++) burn(m, w, h, iX, iY);
+                continue;
+            }
+            if (floor(dfY) == floor(dfYEnd) || fabs(dfY - dfYEnd) < .01) {       /* horizontal */
+                if (dfXEnd < dfX) { double t = dfX; dfX = dfXEnd; dfXEnd = t; }
+                int iX = (int)floor(dfX);
+                const int iY = (int)floor(dfY);
+                int iXEnd = (int)floor(dfXEnd);
+                if (iY < 0 || iY >= h) continue;
+                if (iX < 0) iX = 0;
+                if (iXEnd >= w) iXEnd = w - 1;
+                for (; iX <= iXEnd; iX++) burn(m, w, h, iX, iY);
+                continue;
+            }
+            const double dfSlope = (dfYEnd - dfY) / (dfXEnd - dfX);              /* general */
+            if (dfXEnd > w) { dfYEnd -= (dfXEnd - w) * dfSlope; dfXEnd = w; }
+            if (dfX < 0.0) { dfY += (0.0 - dfX) * dfSlope; dfX = 0.0; }
+            if (dfYEnd > dfY) {
+                if (dfY < 0.0) { dfX += (0.0 - dfY) / dfSlope; dfY = 0.0; }
+                if (dfYEnd >= h) { dfXEnd += (dfYEnd - h) / dfSlope; dfYEnd = h; }
+            } else {
+                if (dfY >= h) { dfX += (h - dfY) / dfSlope; dfY = h; }
+                if (dfYEnd < 0.0) { dfXEnd -= (dfYEnd - 0) / dfSlope; dfYEnd = 0.0; }
+            }
+            while (dfX >= 0.0 && dfX < dfXEnd) {
+                const int iX = (int)floor(dfX), iY = (int)floor(dfY);
+                if (iY >= 0 && iY < h) burn(m, w, h, iX, iY);
+                double dfStepX = floor(dfX + 1.0) - dfX;
+                double dfStepY = dfStepX * dfSlope;
+                if ((int)floor(dfY + dfStepY) == iY) {
+                    dfX += dfStepX; dfY += dfStepY;
+                } else if (dfSlope < 0) {
+                    dfStepY = iY - dfY;
+                    if (dfStepY > -0.000000001) dfStepY = -0.000000001;
+                    dfStepX = dfStepY / dfSlope;
+                    dfX += dfStepX; dfY += dfStepY;
+                } else {
+                    dfStepY = (iY + 1) - dfY;
+                    if (dfStepY < 0.000000001) dfStepY = 0.000000001;
+                    dfStepX = dfStepY / dfSlope;
+                    dfX += dfStepX; dfY += dfStepY;
+                }
+            }
+        }
+    }
+}
+
+int oracle_drill_descriptor(const char *geometry_json, const oracle_crs *ds_crs, const double geot[6],
+                            int xsize, int ysize, int32_t win[4], uint8_t **mask_out) {
+    *mask_out = NULL;
+    or_rings r;
+    memset(&r, 0, sizeof(r));
+    if (parse_geojson(geometry_json, &r)) { rings_free(&r); return -1; }
+    if (ds_crs) {                                   /* drill.go:371-380: WGS84 lon/lat -> dataset SRS */
+        oracle_crs wgs;
+        oracle_crs_init(&wgs, "EPSG:4326");
+        for (int i = 0; i < r.n_pts; i++)
+            if (!oracle_crs_transform(&wgs, ds_crs, &r.x[i], &r.y[i])) { rings_free(&r); return -1; }
+    }
+    /* envelopePolygon (drill.go:329-361): corners through the geotransform, "%f" */
+    const double ulX = fmt6(geot[0] + 0 * geot[1] + 0 * geot[2]), ulY = fmt6(geot[3] + 0 * geot[4] + 0 * geot[5]);
+    const double lrX = fmt6(geot[0] + xsize * geot[1] + ysize * geot[2]);
+    const double lrY = fmt6(geot[3] + xsize * geot[4] + ysize * geot[5]);
+    double env[4];
+    if (!intersection_envelope(&r, fmin(ulX, lrX), fmin(ulY, lrY), fmax(ulX, lrX), fmax(ulY, lrY), env)) {
+        rings_free(&r);
+        return -2;
+    }
+    double igt[6];
+    inv_geot(geot, igt);
+    const double offMinX = igt[0] + env[0] * igt[1] + env[1] * igt[2], offMinY = igt[3] + env[0] * igt[4] + env[1] * igt[5];
+    const double offMaxX = igt[0] + env[2] * igt[1] + env[3] * igt[2], offMaxY = igt[3] + env[2] * igt[4] + env[3] * igt[5];
+    int32_t offX = go_cvtt32(fmin(offMinX, offMaxX)), offY = go_cvtt32(fmin(offMinY, offMaxY));
+    int32_t cX = go_cvtt32(fmax(offMinX, offMaxX)) - offX, cY = go_cvtt32(fmax(offMinY, offMaxY)) - offY;
+    if (cX == 0) cX++;
+    if (cY == 0) cY++;
+    if (offX < 0) offX = 0;
+    if (offY < 0) offY = 0;
+    win[0] = offX; win[1] = offY; win[2] = cX; win[3] = cY;
+    if (cX <= 0 || cY <= 0) { rings_free(&r); return -2; }
+    /* createMask (drill.go:275-327): MEM raster at the window, burn 255 ALL_TOUCHED */
+    double mgt[6], migt[6];
+    memcpy(mgt, geot, sizeof(mgt));
+    mgt[0] += mgt[1] * (double)offX;
+    mgt[3] += mgt[5] * (double)offY;
+    inv_geot(mgt, migt);
+    for (int i = 0; i < r.n_pts; i++) {
+        const double X = r.x[i], Y = r.y[i];
+        r.x[i] = migt[0] + X * migt[1] + Y * migt[2];
+        r.y[i] = migt[3] + X * migt[4] + Y * migt[5];
+    }
+    uint8_t *m = (uint8_t *)calloc((size_t)cX * cY, 1);
+    line_all_touched(&r, m, cX, cY);
+    filled_polygon(&r, m, cX, cY);
+    rings_free(&r);
+    *mask_out = m;
+    return 0;
 }

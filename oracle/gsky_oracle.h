@@ -231,6 +231,17 @@ int oracle_drill_read_data(const float *data, int nbands, int count_x, int count
                            float clip_upper, int pixel_count, int band_strides,
                            double *out_value, int32_t *out_count);
 
+/* getDrillFileDescriptor + createMask (worker/gdalprocess/drill.go:363-423,
+ * 275-327): the request geometry (GeoJSON Feature or Polygon / MultiPolygon,
+ * WGS84 lon/lat) -> dataset SRS (ds_crs NULL: no projection, no transform)
+ * -> intersection envelope with the "%f"-formatted file envelope -> window
+ * {offX, offY, countX, countY} (Go int32 truncations) and the ALL_TOUCHED
+ * mask (GDAL 3.0.1 GDALdllImageLineAllTouched + GDALdllImageFilledPolygon,
+ * burn 255) in *mask_out (malloc'd countX*countY, caller frees).
+ * Returns 0, -1 unparsable geometry, -2 empty intersection. */
+int oracle_drill_descriptor(const char *geometry_json, const oracle_crs *ds_crs, const double geot[6],
+                            int xsize, int ysize, int32_t win[4], uint8_t **mask_out);
+
 /* drill_merger.go:79-93: per date weighted mean over files. values/counts:
  * n_files x n_dates.  out: n_dates (NaN where count == 0). */
 void oracle_drill_merge(const double *values, const int32_t *counts,

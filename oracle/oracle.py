@@ -102,6 +102,7 @@ def lib():
         L.oracle_drill_read_data.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, C.c_float,
                                              C.c_float, C.c_float, C.c_int, C.c_int, vp, vp]
         L.oracle_drill_merge.argtypes = [vp, vp, C.c_int, C.c_int, vp]
+        L.oracle_drill_descriptor.argtypes = [C.c_char_p, vp, vp, C.c_int, C.c_int, vp, C.POINTER(C.c_void_p)]
         L.or_go_f64_u8.argtypes = [d]
         L.or_go_f64_u8.restype = C.c_uint8
         L.or_go_f64_i16.argtypes = [d]
@@ -355,3 +356,20 @@ def drill_merge(values, counts):
     out = np.zeros(nd)
     lib().oracle_drill_merge(_ptr(v), _ptr(c), nf, nd, _ptr(out))
     return out
+
+
+def drill_descriptor(geometry_json: str, ds_srs, geot, xsize: int, ysize: int):
+    """getDrillFileDescriptor + createMask restated: ((offX, offY, countX,
+    countY), mask uint8 (countY, countX), 255 inside) or raises ValueError."""
+    c = crs(ds_srs) if ds_srs else None
+    gt = np.ascontiguousarray(geot, np.float64)
+    win = np.zeros(4, np.int32)
+    mp = C.c_void_p()
+    rc = lib().oracle_drill_descriptor(geometry_json.encode(), C.byref(c) if c is not None else None, _ptr(gt),
+                                       xsize, ysize, _ptr(win), C.byref(mp))
+    if rc:
+        raise ValueError("drill descriptor error %d" % rc)
+    n = int(win[2]) * int(win[3])
+    m = np.frombuffer(C.string_at(mp, n), np.uint8).reshape(int(win[3]), int(win[2])).copy()
+    C.CDLL(None).free(mp)
+    return tuple(int(v) for v in win), m
