@@ -1245,6 +1245,7 @@ struct Carve {
   PairPlan *pairs; Xform *xforms; TilePlan *tplans; int32_t *order; int32_t *pair_tile;
   RowRec *rows; Leaf *pool; int32_t *counters; MinMax *minmax; int64_t *split_list; int32_t *complex_list;
   EntryD *entries;
+  uint32_t *lut;        // 65536 RGBA: Scale + palette of every 16-bit value (band kernel)
   int pool_cap;
   int64_t total;
 };
@@ -1269,6 +1270,7 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   const int64_t o_split = take(sizeof(int64_t) * (int64_t)np * max_h);
   const int64_t o_cl = take(sizeof(int32_t) * (int64_t)nt);
   const int64_t o_ent = take(sizeof(EntryD) * (int64_t)np);
+  const int64_t o_lut = take(sizeof(uint32_t) * 65536);
   c.total = off;
   char *b = (char *)base;
   c.pairs = (PairPlan *)(b + o_pairs);
@@ -1283,6 +1285,7 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   c.split_list = (int64_t *)(b + o_split);
   c.complex_list = (int32_t *)(b + o_cl);
   c.entries = (EntryD *)(b + o_ent);
+  c.lut = (uint32_t *)(b + o_lut);
   return c;
 }
 
@@ -1386,6 +1389,7 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.minmax = cv.minmax;
   a.entries = cv.entries;
   a.lds_stage = 0;   // set by launch_lds_kernels
+  a.lut = cv.lut;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;

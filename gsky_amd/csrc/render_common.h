@@ -209,6 +209,7 @@ struct RenderArgs {
   int write_rgba;
   const EntryD *entries;
   int lds_stage;         // render_lds_kernel: 1 stage source windows in LDS, 0 gather from HBM
+  uint32_t *lut;         // workspace: RGBA of every value of an integer canvas (render_lds_kernel)
 };
 
 // ---------------------------------------------------------------- typed fast path

@@ -66,6 +66,37 @@ __device__ __forceinline__ int piece_index(double s0, double d, int dist) {
   return (v >= 0.0) ? idx : -1;
 }
 
+// v (|v| < 2^30) as signed 32.32 fixed point, truncated: error < 2^-32.
+__device__ __forceinline__ int64_t to_fix(double v) {
+  const double f = floor(v);
+  const uint32_t lo = (uint32_t)((v - f) * 4294967296.0);   // v - f is exact
+  return (int64_t)(((uint64_t)(uint32_t)(int32_t)f << 32) | lo);
+}
+
+__device__ __forceinline__ const void *uniform_ptr(const void *p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const void *)(((uint64_t)hi << 32) | lo);
+}
+
+// Scale + palette (or grey) of every value of an integer canvas type T,
+// with the nodata rule left out (tested per pixel): lut[v & mask] is the
+// RGBA the EncodePNG loop writes for canvas value v (0 where utils.Scale
+// yields 0xFF).  Float32 canvases keep the arithmetic path.
+template <typename T>
+__global__ void scale_lut_kernel(RenderArgs a, const uint32_t *ramp, uint32_t *lut, int n) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  using V = typename VOf<T>::type;
+  ScaleK sk = make_scale(vt_code<T>(), 0.0, a.sp, false, 0.f, 0.f);
+  sk.noData.i = INT32_MIN;            // never equal to a sign/zero-extended 8/16-bit value
+  const V c = (V)(T)(uint32_t)v;      // the bits of v as a T
+  const uint32_t bb = scale_t<T>(sk, c);
+  const uint32_t col = ramp ? ramp[bb & 0xFFu] : (0xFF000000u | (bb << 16) | (bb << 8) | bb);
+  lut[v] = bb != 0xFFu ? col : 0u;
+}
+
 template <typename T, bool MASK, bool STAGE>
 __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                          const int32_t *__restrict__ order,
@@ -105,6 +136,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
   const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
   const bool has_ramp = a.ramp != nullptr;
   uint8_t *rgba_tile = a.rgba + (int64_t)t * a.max_h * a.max_w * 4;
+  const GPTR(const uint32_t) lut = (GPTR(const uint32_t))a.lut;
 
   // entries in merge order, kBandEnt band-intersecting ones per pass; a band
   // with more (rare) parks its partial canvas in its own RGBA slot between passes
@@ -258,11 +290,14 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
         const int ir = r - yoff;
         if (ir < 0 || ir >= eh) continue;
         const int pair = __builtin_amdgcn_readfirstlane(b.pair);
-        const int ew = b.w, bx = b.band_x, by = b.band_y;
+        const int ew = __builtin_amdgcn_readfirstlane(b.w);
+        const int bx = __builtin_amdgcn_readfirstlane(b.band_x);
+        const int by = __builtin_amdgcn_readfirstlane(b.band_y);
+        const T *bandp = (const T *)uniform_ptr(b.band);
         const V nd = as_v<T>(b.nd), fillv = as_v<T>(b.fillv);
-        const int fill_mode = b.fill_mode;
+        const int fill_mode = __builtin_amdgcn_readfirstlane(b.fill_mode);
         const int soff = __builtin_amdgcn_readfirstlane(b.soff);
-        const int ic0 = x0 - b.xoff;
+        const int ic0 = x0 - __builtin_amdgcn_readfirstlane(b.xoff);
         double xs0, ys0, dX, dY;
         int kind, nleaf, pool_off;
         if (STAGE) {
@@ -275,48 +310,94 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
           kind = R.kind; nleaf = R.nleaf; pool_off = R.pool_off;
         }
         kind = __builtin_amdgcn_readfirstlane(kind);
+        // source index of each of the lane's pixels: (ux, uy) and validity
+        uint32_t ux[kLanePx], uy[kLanePx];
+        uint32_t okm = 0;
+        bool exact = kind != ROW_LINEAR;
+        if (!exact) {
+          // 32.32 fixed point: fx(i) = (xs0 + 1e-10 + dX * i) * 2^32, stepped per
+          // pixel.  Off by at most (|i| + 8) * 2^-32 plus a few fp64 ulps from the
+          // reference's ax = (xs0 + dX * i) + 1e-10, so away from the guard band
+          // around an integer its floor is the reference's (int)ax exactly; a
+          // pixel inside the band sends the wave to the fp64 expressions.
+          const double xe = xs0 + dX * (double)ew, ye = ys0 + dY * (double)ew;
+          const bool fits = fabs(xs0) < 1048576.0 && fabs(ys0) < 1048576.0 && fabs(xe) < 1048576.0 &&
+                            fabs(ye) < 1048576.0 && ew < 65536;
+          if (!fits) {
+            exact = true;
+          } else {
+            const int64_t Dx = to_fix(dX), Dy = to_fix(dY);
+            int64_t fx = to_fix(xs0 + 1.0e-10) + (int64_t)ic0 * Dx;
+            int64_t fy = to_fix(ys0 + 1.0e-10) + (int64_t)ic0 * Dy;
+            const uint32_t G = 4u * (uint32_t)(ew + 16) + 64u;   // guard, in 2^-32 px
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < kLanePx; q++) {
+              const uint32_t lx = (uint32_t)fx, ly = (uint32_t)fy;
+              ux[q] = (uint32_t)(fx >> 32);
+              uy[q] = (uint32_t)(fy >> 32);
+              const int ic = ic0 + q;
+              const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
+              bad = bad || (in && (lx + G < 2u * G || ly + G < 2u * G));
+              if (in && ux[q] < (uint32_t)bx && uy[q] < (uint32_t)by) okm |= 1u << q;
+              fx += Dx;
+              fy += Dy;
+            }
+            exact = __ballot(bad) != 0ull;
+          }
+        }
+        if (exact) {   // the reference's fp64 expressions (lin_coords() / nn_px())
+          okm = 0;
+          const Leaf *lv = pool + pool_off;
+#pragma unroll
+          for (int q = 0; q < kLanePx; q++) {
+            const int ic = ic0 + q;
+            const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
+            double sx, sy;
+            if (kind == ROW_LINEAR) {
+              const double dist = (double)ic0 + (double)q;
+              sy = ys0 + dY * dist;
+              sx = xs0 + dX * dist;
+            } else {
+              const int icc = in ? ic : 0;
+              int l = 0;
+              while (l + 1 < nleaf && lv[l + 1].start <= icc) l++;
+              const double dist = (double)(icc - lv[l].start);
+              sy = lv[l].ys0 + lv[l].dY * dist;
+              sx = lv[l].xs0 + lv[l].dX * dist;
+            }
+            const int ix = __double2int_rz(sx + 1.0e-10), iy = __double2int_rz(sy + 1.0e-10);
+            ux[q] = (uint32_t)ix;
+            uy[q] = (uint32_t)iy;
+            if (in && (sx >= 0.0) && (sy >= 0.0) && ix < bx && iy < by) okm |= 1u << q;
+          }
+        }
+        const bool idx32 = (int64_t)bx * by < 2147483648LL;
         const uint8_t *sbase = (const uint8_t *)s_stage + (soff >= 0 ? soff : 0);
         const int sx0 = b.sx0, sy0 = b.sy0, pitch_b = b.pitch_dw * 4;
-        // one pixel: source value or window fill, then the ordered fold
-        auto px = [&](int q, double sx, double sy) {
+#pragma unroll
+        for (int q = 0; q < kLanePx; q++) {
           const int ic = ic0 + q;
-          const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
-          const int ix = __double2int_rz(sx + 1.0e-10), iy = __double2int_rz(sy + 1.0e-10);
-          const bool ok = in && (sx >= 0.0) && (sy >= 0.0) && ix < bx && iy < by;
+          const bool ok = (okm >> q) & 1u;
           V v;
           if (STAGE && soff >= 0) {
-            const int lofs = ok ? (iy - sy0) * pitch_b + (ix - sx0) * (int)sizeof(T) : 0;
+            const int lofs = ok ? ((int)uy[q] - sy0) * pitch_b + ((int)ux[q] - sx0) * (int)sizeof(T) : 0;
             v = (V)(*(const T *)(sbase + lofs));
+          } else if (idx32) {
+            const uint32_t idx = ok ? __umul24(uy[q], (uint32_t)bx) + ux[q] : 0u;
+            v = (V)((const GPTR(T))bandp)[idx];
           } else {
-            const int64_t idx = ok ? (int64_t)iy * bx + ix : 0;
-            v = (V)((const GPTR(T))b.band)[idx];
+            const int64_t idx = ok ? (int64_t)uy[q] * bx + ux[q] : 0;
+            v = (V)((const GPTR(T))bandp)[idx];
           }
           v = ok ? v : fillv;
+          const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
           bool take = in && (v != nd);
           if (MASK && b.mask_pair >= 0) {
             if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, ents[pair], ic, ir);
           }
           const bool t2 = take && (!fill_mode || c[q] == nd);
           c[q] = t2 ? v : c[q];
-        };
-        if (kind == ROW_LINEAR) {
-          const double d0 = (double)ic0;
-#pragma unroll
-          for (int q = 0; q < kLanePx; q++) {
-            const double dist = d0 + (double)q;   // exact: small integers (lin_coords)
-            px(q, xs0 + dX * dist, ys0 + dY * dist);
-          }
-        } else {                                   // POOL row: the leaf holding each column
-          const Leaf *lv = pool + pool_off;
-#pragma unroll
-          for (int q = 0; q < kLanePx; q++) {
-            const int ic = ic0 + q;
-            const int icc = ((unsigned)ic < (unsigned)ew) ? ic : 0;
-            int l = 0;
-            while (l + 1 < nleaf && lv[l + 1].start <= icc) l++;
-            const double dist = (double)(icc - lv[l].start);
-            px(q, lv[l].xs0 + lv[l].dX * dist, lv[l].ys0 + lv[l].dY * dist);
-          }
         }
       }
       if (!last) {   // partial canvas parked in the slot (raw values), re-read next pass
@@ -325,13 +406,18 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
           if (x0 + q < W) ((V *)dst)[q] = c[q];
         continue;
       }
-      // utils.Scale + palette / grey, two 16-B non-temporal stores
+      // utils.Scale + palette / grey: the per-launch LUT for integer canvases
       uint32_t pxo[kLanePx];
 #pragma unroll
       for (int q = 0; q < kLanePx; q++) {
-        const uint32_t bb = scale_t<T>(sk, c[q]);
-        const uint32_t col = has_ramp ? s_ramp[bb & 0xFFu] : (0xFF000000u | (bb << 16) | (bb << 8) | bb);
-        pxo[q] = (created && bb != 0xFFu) ? col : 0u;
+        if constexpr (std::is_same<T, float>::value) {
+          const uint32_t bb = scale_t<T>(sk, c[q]);
+          const uint32_t col = has_ramp ? s_ramp[bb & 0xFFu] : (0xFF000000u | (bb << 16) | (bb << 8) | bb);
+          pxo[q] = (created && bb != 0xFFu) ? col : 0u;
+        } else {
+          const uint32_t col = lut[(uint32_t)c[q] & (sizeof(T) == 1 ? 0xFFu : 0xFFFFu)];
+          pxo[q] = (created && c[q] != cnod) ? col : 0u;
+        }
       }
       if (x0 + kLanePx <= W && ((((uintptr_t)dst) & 15) == 0)) {
         u32x4 v0 = {pxo[0], pxo[1], pxo[2], pxo[3]};
@@ -355,6 +441,11 @@ void launch_lds_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
 #define GSKY_LDS_LAUNCH(M, S)                                                                                   \
   hipLaunchKernelGGL((render_lds_kernel<T, M, S>), grid, dim3(256), 0, s, a, a.entries, a.order, a.rows, a.pool, \
                      a.tplans, a.tiles, n_items, per_xcd)
+  if (!std::is_same<T, float>::value) {
+    const int n = sizeof(T) == 1 ? 256 : 65536;
+    hipLaunchKernelGGL(scale_lut_kernel<T>, dim3((n + 255) / 256), dim3(256), 0, s, a, (const uint32_t *)a.ramp,
+                       a.lut, n);
+  }
   const bool stage = a.lds_stage != 0;
   if (mask) {
     if (stage) GSKY_LDS_LAUNCH(true, true); else GSKY_LDS_LAUNCH(true, false);
