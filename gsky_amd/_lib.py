@@ -77,7 +77,7 @@ EXPORTS = [
     "gskyhip_render_tiles_typed", "gskyhip_warp_windows",
     "gskyhip_merge_rasters", "gskyhip_scale", "gskyhip_scale_legacy", "gskyhip_gradient_palette",
     "gskyhip_encode_rgba", "gskyhip_compute_mask", "gskyhip_drill_rows", "gskyhip_drill",
-    "gskyhip_drill_workspace_size", "gskyhip_drill_batch",
+    "gskyhip_drill_workspace_size", "gskyhip_drill_batch", "gskyhip_drill_descriptors",
     "gskyhip_drill_merge", "gskyhip_fnv32a", "gskyhip_version", "gskyhip_device_count",
     "gskyhip_render_status",
 ]
@@ -123,6 +123,8 @@ def lib() -> C.CDLL:
     L.gskyhip_drill_workspace_size.restype = i64
     L.gskyhip_drill_batch.argtypes = [vp, ci, ci, ci, ci, vp, vp, vp, ci, i64, vp, ci, C.c_float, C.c_float,
                                       C.c_float, ci, ci, ci, vp, vp, vp, i64, vp]
+    L.gskyhip_drill_descriptors.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci, vp, vp,
+                                            C.POINTER(i64), vp, vp]
     L.gskyhip_drill_merge.argtypes = [vp, vp, ci, ci, vp, vp]
     L.gskyhip_fnv32a.argtypes = [C.c_char_p, i64]
     L.gskyhip_fnv32a.restype = C.c_uint32

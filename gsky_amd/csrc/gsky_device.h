@@ -112,7 +112,7 @@ __host__ __device__ inline double adjlon(double lon) {
   return lon;
 }
 
-__device__ inline double qsfn(double sinphi, double e, double one_es) {
+__host__ __device__ inline double qsfn(double sinphi, double e, double one_es) {
   if (e >= 1.0e-7) {
     double con = e * sinphi;
     double div1 = 1.0 - con * con;
@@ -123,7 +123,7 @@ __device__ inline double qsfn(double sinphi, double e, double one_es) {
   return sinphi + sinphi;
 }
 
-__device__ inline double aea_phi1(double qs, double Te, double Tone_es) {
+__host__ __device__ inline double aea_phi1(double qs, double Te, double Tone_es) {
   double Phi = asin(.5 * qs);
   if (Te < 1.0e-7) return Phi;
   int i = 15;
@@ -140,7 +140,7 @@ __device__ inline double aea_phi1(double qs, double Te, double Tone_es) {
 }
 
 // pj_inv: CRS coordinates -> (lam, phi) in radians.
-__device__ inline bool crs_inverse(const gskyhip_crs &c, double x, double y, double &lam, double &phi) {
+__host__ __device__ inline bool crs_inverse(const gskyhip_crs &c, double x, double y, double &lam, double &phi) {
   if (x == HUGE_VAL || y == HUGE_VAL) return false;
   if (c.kind == GSKYHIP_CRS_LONGLAT) {  // +proj=unitconvert deg -> rad
     lam = x * kD2R;
@@ -191,7 +191,7 @@ __device__ inline bool crs_inverse(const gskyhip_crs &c, double x, double y, dou
 }
 
 // pj_fwd: (lam, phi) radians -> CRS coordinates.
-__device__ inline bool crs_forward(const gskyhip_crs &c, double lam, double phi, double &x, double &y) {
+__host__ __device__ inline bool crs_forward(const gskyhip_crs &c, double lam, double phi, double &x, double &y) {
   if (c.kind == GSKYHIP_CRS_LONGLAT) {  // +proj=unitconvert rad -> deg
     x = lam * kR2D;
     y = phi * kR2D;
@@ -221,7 +221,7 @@ __device__ inline bool crs_forward(const gskyhip_crs &c, double lam, double phi,
   } else {
     return false;
   }
-  if (xn != xn || yn != yn || isinf(xn) || isinf(yn)) return false;
+  if (xn != xn || yn != yn || fabs(xn) == HUGE_VAL || fabs(yn) == HUGE_VAL) return false;
   x = 1.0 * (c.a * xn + c.x0);
   y = 1.0 * (c.a * yn + c.y0);
   return true;

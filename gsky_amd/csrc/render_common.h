@@ -210,6 +210,7 @@ struct RenderArgs {
   const EntryD *entries;
   int lds_stage;         // render_lds_kernel: 1 stage source windows in LDS, 0 gather from HBM
   uint32_t *lut;         // workspace: RGBA of every value of an integer canvas (render_lds_kernel)
+  int lds_flags;         // render_lds_kernel variant (A/B knob, see render_lds.h)
 };
 
 // ---------------------------------------------------------------- typed fast path

@@ -97,7 +97,11 @@ __global__ void scale_lut_kernel(RenderArgs a, const uint32_t *ramp, uint32_t *l
   lut[v] = bb != 0xFFu ? col : 0u;
 }
 
-template <typename T, bool MASK, bool STAGE>
+// FLAGS: bit 0 fixed-point source coordinates, bit 1 Scale+palette LUT
+// (A/B knob GSKYHIP_LDS_FLAGS; every combination is bit-identical).
+constexpr int kFixed = 1, kLut = 2;
+
+template <typename T, bool MASK, bool STAGE, int FLAGS>
 __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                          const int32_t *__restrict__ order,
                                                          const RowRec *__restrict__ rows,
@@ -313,7 +317,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
         // source index of each of the lane's pixels: (ux, uy) and validity
         uint32_t ux[kLanePx], uy[kLanePx];
         uint32_t okm = 0;
-        bool exact = kind != ROW_LINEAR;
+        bool exact = kind != ROW_LINEAR || !(FLAGS & kFixed);
         if (!exact) {
           // 32.32 fixed point: fx(i) = (xs0 + 1e-10 + dX * i) * 2^32, stepped per
           // pixel.  Off by at most (|i| + 8) * 2^-32 plus a few fp64 ulps from the
@@ -410,7 +414,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
       uint32_t pxo[kLanePx];
 #pragma unroll
       for (int q = 0; q < kLanePx; q++) {
-        if constexpr (std::is_same<T, float>::value) {
+        if constexpr (std::is_same<T, float>::value || !(FLAGS & kLut)) {
           const uint32_t bb = scale_t<T>(sk, c[q]);
           const uint32_t col = has_ramp ? s_ramp[bb & 0xFFu] : (0xFF000000u | (bb << 16) | (bb << 8) | bb);
           pxo[q] = (created && bb != 0xFFu) ? col : 0u;
@@ -438,19 +442,23 @@ template <typename T>
 void launch_lds_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
   const int per_xcd = (n_items + 7) / 8;
   const dim3 grid((unsigned)per_xcd * 8);
-#define GSKY_LDS_LAUNCH(M, S)                                                                                   \
-  hipLaunchKernelGGL((render_lds_kernel<T, M, S>), grid, dim3(256), 0, s, a, a.entries, a.order, a.rows, a.pool, \
+#define GSKY_LDS_LAUNCH(M, S, F)                                                                                   \
+  hipLaunchKernelGGL((render_lds_kernel<T, M, S, F>), grid, dim3(256), 0, s, a, a.entries, a.order, a.rows, a.pool, \
                      a.tplans, a.tiles, n_items, per_xcd)
-  if (!std::is_same<T, float>::value) {
-    const int n = sizeof(T) == 1 ? 256 : 65536;
-    hipLaunchKernelGGL(scale_lut_kernel<T>, dim3((n + 255) / 256), dim3(256), 0, s, a, (const uint32_t *)a.ramp,
-                       a.lut, n);
-  }
   const bool stage = a.lds_stage != 0;
+  const int fl = a.lds_flags;
   if (mask) {
-    if (stage) GSKY_LDS_LAUNCH(true, true); else GSKY_LDS_LAUNCH(true, false);
+    if (stage) GSKY_LDS_LAUNCH(true, true, 0); else GSKY_LDS_LAUNCH(true, false, 0);
+  } else if (stage) {
+    GSKY_LDS_LAUNCH(false, true, 0);
+  } else if (fl == 1) {
+    GSKY_LDS_LAUNCH(false, false, 1);
+  } else if (fl == 2) {
+    GSKY_LDS_LAUNCH(false, false, 2);
+  } else if (fl == 3) {
+    GSKY_LDS_LAUNCH(false, false, 3);
   } else {
-    if (stage) GSKY_LDS_LAUNCH(false, true); else GSKY_LDS_LAUNCH(false, false);
+    GSKY_LDS_LAUNCH(false, false, 0);
   }
 #undef GSKY_LDS_LAUNCH
 }

@@ -12,6 +12,8 @@ void launch_lds_kernels(const RenderArgs &a0, int vt, bool mask, int n_items, hi
   RenderArgs a = a0;
   const char *st = getenv("GSKYHIP_LDS_STAGE");
   a.lds_stage = st ? atoi(st) : 0;
+  const char *fl = getenv("GSKYHIP_LDS_FLAGS");
+  a.lds_flags = fl ? atoi(fl) : 0;
   switch (vt) {
     case GSKYHIP_INT16: launch_lds_i16(a, mask, n_items, s); break;
     case GSKYHIP_UINT16: launch_lds_u16(a, mask, n_items, s); break;

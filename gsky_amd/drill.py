@@ -79,6 +79,43 @@ def pack_masks(windows: Sequence[Tuple[int, int, int, int]], masks: Sequence[np.
     return MaskBatch(win, off, torch.from_numpy(buf).to(dev))
 
 
+def drill_descriptors(geometries: Sequence[str], dataset_srs: Optional[str], geot: Sequence[float], xsize: int,
+                      ysize: int):
+    """getDrillFileDescriptor + createMask (drill.go:363-423, 275-327) for a
+    batch of GeoJSON geometries against one dataset: (windows (n, 4) int32,
+    mask_off (n,) int64, masks uint8 host buffer, status (n,) int32)."""
+    n = len(geometries)
+    arr = (C.c_char_p * max(1, n))(*[g.encode() for g in geometries])
+    gt = (C.c_double * 6)(*geot)
+    win = np.zeros((max(1, n), 4), np.int32)
+    off = np.zeros(max(1, n), np.int64)
+    st = np.zeros(max(1, n), np.int32)
+    total = C.c_int64()
+    srs = dataset_srs.encode() if dataset_srs else None
+    L = lib()
+    check(L.gskyhip_drill_descriptors(arr, n, srs, gt, xsize, ysize, win.ctypes.data_as(C.c_void_p),
+                                      off.ctypes.data_as(C.c_void_p), C.byref(total), None,
+                                      st.ctypes.data_as(C.c_void_p)), "drill_descriptors")
+    buf = np.zeros(int(total.value), np.uint8)
+    check(L.gskyhip_drill_descriptors(arr, n, srs, gt, xsize, ysize, win.ctypes.data_as(C.c_void_p),
+                                      off.ctypes.data_as(C.c_void_p), C.byref(total),
+                                      buf.ctypes.data_as(C.c_void_p), st.ctypes.data_as(C.c_void_p)),
+          "drill_descriptors")
+    return win[:n], off[:n], buf, st[:n]
+
+
+def drill_dataset(geometries: Sequence[str], dataset_srs: Optional[str], geot: Sequence[float], xsize: int,
+                  ysize: int, device=None) -> Tuple["MaskBatch", np.ndarray]:
+    """DrillDataset's geometry step for a batch of requests: the windows and
+    ALL_TOUCHED masks, uploaded as a MaskBatch, plus the per-polygon status
+    (0 ok; a polygon that misses the file gets an empty window)."""
+    win, off, buf, st = drill_descriptors(geometries, dataset_srs, geot, xsize, ysize)
+    dev = torch.device(device or "cuda")
+    mb = MaskBatch(torch.from_numpy(win.copy()).to(dev), torch.from_numpy(off.copy()).to(dev),
+                   torch.from_numpy(buf).to(dev))
+    return mb, st
+
+
 REFERENCE_ORDER, WAVE_SPLIT = 0, 1
 
 

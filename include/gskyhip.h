@@ -312,6 +312,25 @@ int gskyhip_drill(const float *stack, int xsize, int ysize, int n_bands, int t_s
                   int pixel_count, int band_strides, double *out_value,
                   int32_t *out_count, void *stream);
 
+/* getDrillFileDescriptor + createMask (drill.go:363-423, 275-327) for n
+ * request geometries against one dataset (HOST function, no device work):
+ *   geometries: GeoJSON (a Feature or a bare Polygon / MultiPolygon) in
+ *     WGS84 lon/lat, as GeoRPCGranule.Geometry;
+ *   dataset_srs: the dataset's SRS (NULL / "" = no projection: no transform);
+ *   geot, xsize, ysize: the dataset's geotransform and size.
+ * Per polygon: win_out[4*i..] = {off_x, off_y, count_x, count_y} with the
+ * reference's int32 truncations, status_out[i] = 0, GSKYHIP_E_ARG (geometry
+ * not parsable), GSKYHIP_E_CRS (transform failed) or GSKYHIP_E_RANGE (the
+ * polygon misses the file; window 0).  mask_off_out[i] = byte offset of its
+ * mask (16-byte aligned, polygon order), *mask_bytes_out = total bytes.
+ * masks_out: NULL sizes only; else a HOST buffer of *mask_bytes_out bytes
+ * that receives the ALL_TOUCHED masks (255 = burnt) -- the layout
+ * gskyhip_drill_batch takes (copy it to the device). */
+int gskyhip_drill_descriptors(const char *const *geometries, int n, const char *dataset_srs,
+                              const double *geot, int xsize, int ysize, int32_t *win_out,
+                              int64_t *mask_off_out, int64_t *mask_bytes_out, uint8_t *masks_out,
+                              int32_t *status_out);
+
 /* DrillMerger weighted mean (drill_merger.go:79-93): values/counts dev
  * n_files x n_dates, out dev n_dates (NaN where no count). */
 int gskyhip_drill_merge(const double *values, const int32_t *counts, int n_files,

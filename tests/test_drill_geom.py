@@ -1,0 +1,111 @@
+"""Drill request geometry (A16): polygon -> window -> ALL_TOUCHED mask,
+worker/gdalprocess/drill.go:363-423 (getDrillFileDescriptor) and 275-327
+(createMask).  The product's host implementation (libgskyhip.so,
+gskyhip_drill_descriptors) against the oracle's independent C restatement on
+the same GeoJSON, plus hand-derived known answers.  GDAL/GEOS are absent, so
+parity with a running reference is unpinned; these tests pin the
+product to the restatement bit for bit.  CPU only: both sides are host code."""
+import json
+
+import numpy as np
+import pytest
+
+from gsky_amd import drill, synth
+
+GT4326 = [130.0, 0.01, 0.0, -20.0, 0.0, -0.01]
+
+
+def feature(rings, multi=False):
+    coords = [[[list(p) for p in r] for r in rings]] if multi else [[list(p) for p in r] for r in rings]
+    return json.dumps({"type": "Feature", "properties": {},
+                       "geometry": {"type": "MultiPolygon" if multi else "Polygon", "coordinates": coords}})
+
+
+def close(pts):
+    pts = [tuple(p) for p in pts]
+    return pts + [pts[0]]
+
+
+def stars(n, gt, size, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for p in range(n):
+        r = rng.uniform(3, 60)
+        cx, cy = rng.uniform(-20, size + 20), rng.uniform(-20, size + 20)   # some cross the file edge
+        pix = synth.star_polygon(cx, cy, r, k=int(rng.integers(3, 13)), seed=p)
+        lon = gt[0] + pix[:, 0] * gt[1]
+        lat = gt[3] + pix[:, 1] * gt[5]
+        out.append(feature([close(np.stack([lon, lat], 1))]))
+    return out
+
+
+def test_descriptor_known_answers(oracle):
+    # a square over pixels 10.25 .. 12.75: offsets truncate and count = int(max) - off (drill.go:404-407)
+    x0, y0 = 130 + 0.1025, -20 - 0.1025
+    sq = feature([close([(x0, y0), (x0 + 0.025, y0), (x0 + 0.025, y0 - 0.025), (x0, y0 - 0.025)])])
+    win, off, buf, st = drill.drill_descriptors([sq], "EPSG:4326", GT4326, 2048, 2048)
+    assert st.tolist() == [0] and win[0].tolist() == [10, 10, 2, 2]
+    assert buf[:4].tolist() == [255] * 4
+    # a polygon entirely outside the file: no window (the reference's
+    # indexer never sends such a file; here it is reported per polygon)
+    far = feature([close([(100, 10), (101, 10), (101, 11), (100, 11)])])
+    win, off, buf, st = drill.drill_descriptors([far, sq], "EPSG:4326", GT4326, 2048, 2048)
+    assert st[0] != 0 and win[0].tolist() == [0, 0, 0, 0] and st[1] == 0
+    # thin diagonal: ALL_TOUCHED burns every pixel the edges cross
+    tri = feature([close([(130.0005, -20.0005), (130.0595, -20.0295), (130.0005, -20.0015)])])
+    win, off, buf, st = drill.drill_descriptors([tri], "EPSG:4326", GT4326, 2048, 2048)
+    m = buf[off[0]:off[0] + win[0][2] * win[0][3]].reshape(win[0][3], win[0][2])
+    ew, em = oracle.drill_descriptor(tri, "EPSG:4326", GT4326, 2048, 2048)
+    assert tuple(win[0]) == ew and np.array_equal(m, em)
+    assert (m == 255).sum() >= win[0][2]      # at least one pixel per column along the long edge
+
+
+@pytest.mark.parametrize("srs,seed", [("EPSG:4326", 1), ("EPSG:4326", 2), ("EPSG:3577", 3)])
+def test_descriptor_matches_oracle(oracle, srs, seed):
+    if srs == "EPSG:4326":
+        gt, size = GT4326, 2048
+        geoms = stars(120, gt, size, seed)
+    else:   # Albers dataset: polygons in lon/lat around lon 132, lat -27
+        gt, size = [-300000.0, 250.0, 0.0, -2800000.0, 0.0, -250.0], 2400
+        rng = np.random.default_rng(seed)
+        geoms = []
+        for p in range(60):
+            lon0, lat0 = rng.uniform(128.5, 135.0), rng.uniform(-31.5, -25.0)
+            r = rng.uniform(0.05, 0.6)
+            pts = synth.star_polygon(lon0, lat0, r, k=9, seed=p)
+            geoms.append(feature([close(pts)]))
+    win, off, buf, st = drill.drill_descriptors(geoms, srs, gt, size, size)
+    n_ok = 0
+    for i, g in enumerate(geoms):
+        try:
+            ew, em = oracle.drill_descriptor(g, srs, gt, size, size)
+        except ValueError:
+            assert st[i] != 0, i
+            continue
+        assert st[i] == 0 and tuple(win[i]) == ew, (i, win[i], ew)
+        m = buf[off[i]:off[i] + ew[2] * ew[3]].reshape(ew[3], ew[2])
+        assert np.array_equal(m, em), i
+        n_ok += 1
+    assert n_ok > len(geoms) // 2
+
+
+def test_descriptor_multipolygon_with_hole(oracle):
+    outer = close([(130.1, -20.1), (130.5, -20.1), (130.5, -20.5), (130.1, -20.5)])
+    hole = close([(130.2, -20.2), (130.4, -20.2), (130.4, -20.4), (130.2, -20.4)])
+    other = close([(130.6, -20.6), (130.7, -20.6), (130.65, -20.7)])
+    g = feature([[outer, hole], [other]][0], multi=False)
+    mp = json.dumps({"type": "MultiPolygon", "coordinates": [[[list(p) for p in outer], [list(p) for p in hole]],
+                                                             [[list(p) for p in other]]]})
+    for geom in (g, mp):
+        win, off, buf, st = drill.drill_descriptors([geom], "EPSG:4326", GT4326, 2048, 2048)
+        ew, em = oracle.drill_descriptor(geom, "EPSG:4326", GT4326, 2048, 2048)
+        assert st[0] == 0 and tuple(win[0]) == ew
+        m = buf[off[0]:off[0] + ew[2] * ew[3]].reshape(ew[3], ew[2])
+        assert np.array_equal(m, em)
+        assert m[25, 25] == 0 and m[5, 5] == 255      # the hole is not burnt, the ring is
+
+
+def test_descriptor_bad_geometry():
+    win, off, buf, st = drill.drill_descriptors(['{"type": "Point", "coordinates": [1, 2]}', "nonsense"],
+                                                "EPSG:4326", GT4326, 2048, 2048)
+    assert (st != 0).all() and (win == 0).all()

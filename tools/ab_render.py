@@ -47,10 +47,14 @@ def main():
     sp = gsky_amd.ScaleParams(*cfg.scale)
     pal = gsky_amd.Palette(cfg.palette, True) if cfg.palette else None
     ref = None
-    for name, typed, stage in [("typed_stage", True, "1"), ("typed_direct", True, "0"), ("generic", False, "1")]:
+    variants = [("typed_stage", True, "1", "0"), ("typed_direct", True, "0", "0"),
+                ("typed_direct_fixed", True, "0", "1"), ("typed_direct_lut", True, "0", "2"),
+                ("typed_direct_fixed_lut", True, "0", "3"), ("generic", False, "1", "0")]
+    for name, typed, stage, flags in variants:
         if args.variant and name != args.variant:
             continue
         os.environ["GSKYHIP_LDS_STAGE"] = stage
+        os.environ["GSKYHIP_LDS_FLAGS"] = flags
         b.typed = typed
         med, mn = time_render(b, sp, pal, args.reps)
         out = b.render(sp, pal).clone()
