@@ -288,13 +288,14 @@ def run_c3(ctx: Ctx, args):
     sp = ScaleParams(*cfg.scale)
     top, bottom = extents[ctx.rank]
 
-    def render():
-        return b.render(sp, resample=cfg.resample, rgba=False)
+    band = torch.empty((bottom - top, W), dtype=torch.float32, device=ctx.device)
+    offs = torch.tensor(coverage.band_offsets(sel, top, W), dtype=torch.int64, device=ctx.device)
+
+    def render():   # chunks straight into the band at their offsets (gskyhip_render_coverage)
+        return b.render_coverage(sp, band, offs, resample=cfg.resample)
 
     def step():
-        cv = render()
-        canv = [b.canvas_view(cv, i, 0, "Float32")[: c.height, : c.width] for i, c in enumerate(sel)]
-        band = coverage.place_chunks(canv, sel, top, bottom - top, W, device=ctx.device)
+        render()
         if ctx.world > 1:
             coverage.gather_coverage(band, extents, H, W)
         return band
@@ -312,8 +313,8 @@ def run_c3(ctx: Ctx, args):
     out = {"workload": "C3: WCS GetCoverage %dx%d float32 bilinear EPSG:4326->3857 mosaic from %d granules, "
                        "%d chunks of <=1024^2 (ows.go:817-831)" % (W, H, len(cfg.granules), len(chunks)),
            "value": round(W * H * args.c3_steps / dt / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(dt / args.c3_steps * 1e3, 3),
-           "step": "render own chunk rows (canvases) + place into the band" + (" + RCCL gather to rank 0"
-                                                                             if ctx.world > 1 else ""),
+           "step": "render own chunk rows straight into the band" + (" + RCCL gather to rank 0"
+                                                                      if ctx.world > 1 else ""),
            "chunk_rows_rank0": rows[0], "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "plan + bilinear render (rank 0)",

@@ -74,7 +74,7 @@ class FlexRasterC(C.Structure):
 EXPORTS = [
     "gskyhip_crs_from_srs", "gskyhip_register_granule", "gskyhip_unregister_all", "warp_operation_fast",
     "gskyhip_render_workspace_size", "gskyhip_render_tiles", "gskyhip_render_tiles_phase",
-    "gskyhip_render_tiles_typed", "gskyhip_warp_windows",
+    "gskyhip_render_tiles_typed", "gskyhip_render_coverage", "gskyhip_warp_windows",
     "gskyhip_merge_rasters", "gskyhip_scale", "gskyhip_scale_legacy", "gskyhip_gradient_palette",
     "gskyhip_encode_rgba", "gskyhip_compute_mask", "gskyhip_drill_rows", "gskyhip_drill",
     "gskyhip_drill_workspace_size", "gskyhip_drill_batch", "gskyhip_drill_descriptors",
@@ -106,6 +106,8 @@ def lib() -> C.CDLL:
                                        C.POINTER(Mask), ci, C.POINTER(ScaleParams), vp, vp, vp, vp, i64, vp]
     L.gskyhip_render_tiles_phase.argtypes = [ci] + L.gskyhip_render_tiles.argtypes
     L.gskyhip_render_tiles_typed.argtypes = [ci, C.c_uint32] + L.gskyhip_render_tiles.argtypes
+    L.gskyhip_render_coverage.argtypes = [ci, C.c_uint32, vp, ci, vp, ci, ci, vp, ci, vp, ci, ci, ci, ci,
+                                          C.POINTER(ScaleParams), vp, i64, vp, vp, i64, vp]
     L.gskyhip_warp_windows.argtypes = [vp, ci, vp, ci, ci, vp, ci, vp, ci, ci, ci, ci, vp, vp, vp, vp, i64,
                                        vp, i64, vp]
     L.gskyhip_render_status.argtypes = [vp, ci, ci, ci, vp]

@@ -128,9 +128,16 @@ def render_band_gpu(cfg, chunks: Sequence[Chunk], rows: Tuple[int, int], width: 
                gr.polygon, gr.namespace)
     tiles = [(c.bbox, c.width, c.height) for c in sel]
     tb = TileBatch(gs, cfg.dst_srs, tiles, [[remap[g] for g in p] for p in pairs], cfg.namespaces)
-    cv = tb.render(ScaleParams(*cfg.scale), resample=cfg.resample, rgba=False)
-    canv = [tb.canvas_view(cv, i, 0, "Float32")[: c.height, : c.width] for i, c in enumerate(sel)]
-    return place_chunks(canv, sel, top, bottom - top, width, device=device)
+    band = torch.empty((bottom - top, width), dtype=torch.float32, device=device)
+    # every chunk is rendered straight into the band at its offset (no assembly copy)
+    tb.render_coverage(ScaleParams(*cfg.scale), band, band_offsets(sel, top, width), resample=cfg.resample)
+    return band
+
+
+def band_offsets(chunks: Sequence[Chunk], top: int, width: int) -> List[int]:
+    """Flat element offset of each chunk's top-left in a band whose first row
+    is image row `top` and whose rows are `width` elements."""
+    return [(c.off_y - top) * width + c.off_x for c in chunks]
 
 
 def render_coverage(cfg, width: int, height: int, renderer: Callable = render_band_gpu, device=None,

@@ -430,6 +430,8 @@ int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGe
   rc.mask_ns = -1; rc.mask_inclusive = 0; rc.mask_specs = ms;
   rc.resample = GSKYHIP_RESAMPLE_NEAREST;
   rc.value_types = 0;
+  rc.cov_offsets = nullptr;
+  rc.cov_stride = 0;
   rc.workspace = base + hdr; rc.workspace_bytes = ws;
   rc.stream = d.stream;
   char *win = base + hdr + ws;
@@ -480,6 +482,27 @@ int gskyhip_render_tiles_phase(int phase, const gskyhip_granule *granules, int n
                                     resample, sp, ramp, rgba_out, canvas_out, workspace, workspace_bytes, stream);
 }
 
+static int render_call(int phase, uint32_t value_types, const gskyhip_granule *granules, int n_granules,
+                       const gskyhip_crs *crs_table, int n_crs, int dst_crs, const gskyhip_tile *tiles,
+                       int n_tiles, const int32_t *pair_granule, int n_pairs, int max_tile_width,
+                       int max_tile_height, const int32_t *out_ns, int n_out_ns, const gskyhip_mask *mask,
+                       int resample, const gskyhip_scale_params *sp, const uint8_t *ramp, uint8_t *rgba_out,
+                       void *canvas_out, const int64_t *cov_offsets, int64_t cov_stride, void *workspace,
+                       int64_t workspace_bytes, void *stream);
+
+int gskyhip_render_coverage(int phase, uint32_t value_types, const gskyhip_granule *granules, int n_granules,
+                            const gskyhip_crs *crs_table, int n_crs, int dst_crs, const gskyhip_tile *tiles,
+                            int n_tiles, const int32_t *pair_granule, int n_pairs, int max_tile_width,
+                            int max_tile_height, int resample, const gskyhip_scale_params *sp,
+                            const int64_t *tile_offsets, int64_t row_stride, void *coverage_out, void *workspace,
+                            int64_t workspace_bytes, void *stream) {
+  if (!tile_offsets || !coverage_out || row_stride < max_tile_width) return GSKYHIP_E_ARG;
+  const int32_t out_ns[1] = {0};
+  return render_call(phase, value_types, granules, n_granules, crs_table, n_crs, dst_crs, tiles, n_tiles,
+                     pair_granule, n_pairs, max_tile_width, max_tile_height, out_ns, 1, nullptr, resample, sp,
+                     nullptr, nullptr, coverage_out, tile_offsets, row_stride, workspace, workspace_bytes, stream);
+}
+
 int gskyhip_render_tiles_typed(int phase, uint32_t value_types, const gskyhip_granule *granules,
                                int n_granules, const gskyhip_crs *crs_table, int n_crs, int dst_crs,
                                const gskyhip_tile *tiles, int n_tiles, const int32_t *pair_granule, int n_pairs,
@@ -487,6 +510,18 @@ int gskyhip_render_tiles_typed(int phase, uint32_t value_types, const gskyhip_gr
                                const gskyhip_mask *mask, int resample, const gskyhip_scale_params *sp,
                                const uint8_t *ramp, uint8_t *rgba_out, void *canvas_out, void *workspace,
                                int64_t workspace_bytes, void *stream) {
+  return render_call(phase, value_types, granules, n_granules, crs_table, n_crs, dst_crs, tiles, n_tiles,
+                     pair_granule, n_pairs, max_tile_width, max_tile_height, out_ns, n_out_ns, mask, resample, sp,
+                     ramp, rgba_out, canvas_out, nullptr, 0, workspace, workspace_bytes, stream);
+}
+
+static int render_call(int phase, uint32_t value_types, const gskyhip_granule *granules, int n_granules,
+                       const gskyhip_crs *crs_table, int n_crs, int dst_crs, const gskyhip_tile *tiles,
+                       int n_tiles, const int32_t *pair_granule, int n_pairs, int max_tile_width,
+                       int max_tile_height, const int32_t *out_ns, int n_out_ns, const gskyhip_mask *mask,
+                       int resample, const gskyhip_scale_params *sp, const uint8_t *ramp, uint8_t *rgba_out,
+                       void *canvas_out, const int64_t *cov_offsets, int64_t cov_stride, void *workspace,
+                       int64_t workspace_bytes, void *stream) {
   if (!sp || !out_ns || n_tiles < 0 || n_pairs < 0 || phase < 0 || phase > 2) return GSKYHIP_E_ARG;
   MaskSpecS ms[4];
   int r = build_mask_specs(mask, ms);
@@ -502,6 +537,8 @@ int gskyhip_render_tiles_typed(int phase, uint32_t value_types, const gskyhip_gr
   rc.mask_specs = ms;
   rc.resample = resample;
   rc.value_types = value_types;
+  rc.cov_offsets = cov_offsets;
+  rc.cov_stride = cov_stride;
   rc.workspace = workspace; rc.workspace_bytes = workspace_bytes;
   rc.stream = (hipStream_t)stream;
   return launch_render(rc, out_ns, n_out_ns, *sp, ramp, rgba_out, canvas_out, phase);
@@ -553,6 +590,8 @@ int gskyhip_warp_windows(const gskyhip_granule *granules, int n_granules, const 
   rc.mask_ns = -1; rc.mask_inclusive = 0; rc.mask_specs = ms;
   rc.resample = resample;
   rc.value_types = 0;
+  rc.cov_offsets = nullptr;
+  rc.cov_stride = 0;
   rc.workspace = workspace; rc.workspace_bytes = workspace_bytes;
   rc.stream = (hipStream_t)stream;
   if (win_stride < (int64_t)max_tile_width * max_tile_height * 4) return GSKYHIP_E_ARG;

@@ -22,6 +22,8 @@ struct RenderCall {
   const MaskSpecS *mask_specs;  // 4 entries (host)
   int resample;
   uint32_t value_types;         // GSKYHIP_VT_* of the stack entries (0 = unknown)
+  const int64_t *cov_offsets;   // canvases placed in one image: per tile element offset (dev) or NULL
+  int64_t cov_stride;           // that image's row stride in elements
   void *workspace; int64_t workspace_bytes;
   hipStream_t stream;
 };

@@ -789,9 +789,10 @@ __device__ __forceinline__ void render_band(const RenderArgs &a, int t, int band
 #pragma unroll
         for (int s = 0; s < NOUT; s++) {
           const int dsz = type_size(tp.dtype[a.out_ns[s]]);
-          uint8_t *cb = a.canvas + t * a.canvas_tile_stride + s * a.canvas_ns_stride;
+          uint8_t *cb = a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride + s * a.canvas_ns_stride;
+          const long row0 = a.cov_offsets ? a.cov_offsets[t] + (long)r * a.cov_stride : (long)r * a.max_w;
           for (int q = 0; q < 4 && x0 + q < W; q++) {
-            const long idx = (long)r * a.max_w + x0 + q;
+            const long idx = row0 + x0 + q;
             if (dsz == 1) cb[idx] = (uint8_t)c[s][q].i;
             else if (dsz == 2) ((uint16_t *)cb)[idx] = (uint16_t)c[s][q].i;
             else ((uint32_t *)cb)[idx] = c[s][q].u;
@@ -976,10 +977,11 @@ __device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD 
       if (a.canvas) {
 #pragma unroll
         for (int s = 0; s < NOUT; s++) {
-          T *cb = (T *)(a.canvas + t * a.canvas_tile_stride + s * a.canvas_ns_stride);
+          T *cb = (T *)(a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride + s * a.canvas_ns_stride);
+          const long row0 = a.cov_offsets ? a.cov_offsets[t] + (long)r * a.cov_stride : (long)r * a.max_w;
 #pragma unroll
           for (int q = 0; q < 4; q++)
-            if (x0 + q < W) cb[(long)r * a.max_w + x0 + q] = (T)c[s][j][q];
+            if (x0 + q < W) cb[row0 + x0 + q] = (T)c[s][j][q];
         }
       }
       if (!a.write_rgba) continue;
@@ -1390,6 +1392,10 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.entries = cv.entries;
   a.lds_stage = 0;   // set by launch_lds_kernels
   a.lut = cv.lut;
+  a.lds_flags = 0;
+  a.lds_mode = 0;
+  a.cov_offsets = rc.cov_offsets;
+  a.cov_stride = rc.cov_stride;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;
@@ -1401,14 +1407,28 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   } else {
     a.write_rgba = rgba_out ? 1 : 0;
   }
+  // One value type, one namespace, no auto-scale: the typed band kernel, for
+  // RGBA output (GetMap) or typed canvases only (GetCoverage); complex tiles
+  // (exact transforms, type promotion) still go to render_general_kernel.
   const int vt = single_value_type(rc.value_types);
-  if (!autom && a.write_rgba && !canvas_out && n_out == 1 && rc.resample == GSKYHIP_RESAMPLE_NEAREST && vt) {
+  const bool bil = rc.resample == GSKYHIP_RESAMPLE_BILINEAR;
+  int lds_mode = -1;
+  if (vt && n_out == 1 && !autom) {
+    if (a.write_rgba && !canvas_out) lds_mode = bil ? kBilinear : 0;
+    else if (!rgba_out && canvas_out) lds_mode = kCanvas | (bil ? kBilinear : 0);
+  }
+  if (lds_mode >= 0) {
+    a.lds_mode = lds_mode;
     const int n_items = rc.n_tiles * ((rc.max_h + kLdsBandRows - 1) / kLdsBandRows);
     launch_lds_kernels(a, vt, mask, n_items, s);
-    if (mask)
-      hipLaunchKernelGGL((render_general_kernel<1, GSKYHIP_RESAMPLE_NEAREST, true>), dim3(512), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((render_general_kernel<1, GSKYHIP_RESAMPLE_NEAREST, false>), dim3(512), dim3(256), 0, s, a);
+    const dim3 g(512), b(256);
+    if (bil) {
+      if (mask) hipLaunchKernelGGL((render_general_kernel<1, GSKYHIP_RESAMPLE_BILINEAR, true>), g, b, 0, s, a);
+      else hipLaunchKernelGGL((render_general_kernel<1, GSKYHIP_RESAMPLE_BILINEAR, false>), g, b, 0, s, a);
+    } else {
+      if (mask) hipLaunchKernelGGL((render_general_kernel<1, GSKYHIP_RESAMPLE_NEAREST, true>), g, b, 0, s, a);
+      else hipLaunchKernelGGL((render_general_kernel<1, GSKYHIP_RESAMPLE_NEAREST, false>), g, b, 0, s, a);
+    }
   } else if (n_out == 1) {
     dispatch_render<1>(a, rc.resample, mask, grid, s);
   } else {

@@ -211,6 +211,9 @@ struct RenderArgs {
   int lds_stage;         // render_lds_kernel: 1 stage source windows in LDS, 0 gather from HBM
   uint32_t *lut;         // workspace: RGBA of every value of an integer canvas (render_lds_kernel)
   int lds_flags;         // render_lds_kernel variant (A/B knob, see render_lds.h)
+  int lds_mode;          // render_lds_kernel: kBilinear | kCanvas bits of the call
+  const int64_t *cov_offsets;  // canvas mode: per tile element offset into one image (NULL: slots)
+  int64_t cov_stride;          // ... and that image's row stride (elements)
 };
 
 // ---------------------------------------------------------------- typed fast path
@@ -337,6 +340,7 @@ __device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const
 }
 
 constexpr int kLdsBandRows = 16;   // rows per block of render_lds_kernel
+constexpr int kBilinear = 4, kCanvas = 8;   // render_lds_kernel modes (RenderArgs.lds_mode)
 
 // The typed LDS-staged band kernels (render_lds.hip) for value type `vt`.
 void launch_lds_kernels(const RenderArgs &a, int vt, bool mask, int n_items, hipStream_t s);

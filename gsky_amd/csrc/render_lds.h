@@ -45,6 +45,8 @@ struct BandEnt {
   int32_t sx0, sy0, sh, pitch_dw;       // staged rectangle: origin (sx0 dword-aligned), rows, dwords per row
   int32_t soff;                         // LDS byte offset of the rectangle, -1: gather from HBM
   int32_t pair;
+  int32_t has_nodata, out_dtype;        // bilinear: nodata taps are dropped (GWKBilinearResample4Sample)
+  double nodata64;
 };
 struct BandRow {
   double xs0, ys0, dX, dY;
@@ -98,8 +100,40 @@ __global__ void scale_lut_kernel(RenderArgs a, const uint32_t *ramp, uint32_t *l
 }
 
 // FLAGS: bit 0 fixed-point source coordinates, bit 1 Scale+palette LUT
-// (A/B knob GSKYHIP_LDS_FLAGS; every combination is bit-identical).
-constexpr int kFixed = 1, kLut = 2;
+// (A/B knob GSKYHIP_LDS_FLAGS; every combination is bit-identical), bit 2
+// bilinear resampling, bit 3 typed canvas output (WCS) instead of RGBA.
+constexpr int kFixed = 1, kLut = 2;   // kBilinear = 4, kCanvas = 8: render_common.h
+
+// GWKBilinearResample4Sample semantics of bil_fetch() (render_common.h), the
+// same fp64 expressions, for the band kernel: false -> window fill.
+template <typename T>
+__device__ __forceinline__ bool bil_sample(const T *band, int bx, int by, bool has_nodata, double nodata64,
+                                           int out_dtype, double sx, double sy, typename VOf<T>::type &v) {
+  int iSrcX = (int)floor(sx - 0.5);
+  int iSrcY = (int)floor(sy - 0.5);
+  double rX = 1.5 - (sx - iSrcX);
+  double rY = 1.5 - (sy - iSrcY);
+  if (iSrcX == -1) { iSrcX = 0; rX = 1; }
+  if (iSrcY == -1) { iSrcY = 0; rY = 1; }
+  double accR = 0.0, accDiv = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int xx = iSrcX + (k & 1), yy = iSrcY + (k >> 1);
+    const double w = ((k & 1) ? (1.0 - rX) : rX) * ((k >> 1) ? (1.0 - rY) : rY);
+    if (xx < 0 || xx >= bx || yy < 0 || yy >= by) continue;
+    const double d = (double)((const GPTR(T))band)[(int64_t)yy * bx + xx];
+    if (has_nodata && (d == nodata64 || (nodata64 != nodata64 && d != d))) continue;
+    accDiv += w;
+    accR += d * w;
+  }
+  double r;
+  if (accDiv == 1.0) r = accR;
+  else if (accDiv < 0.00001) return false;
+  else r = accR / accDiv;
+  if constexpr (std::is_same<T, float>::value) v = (float)r;
+  else v = gdal_copy_to(floor(r + 0.5), out_dtype).i;
+  return true;
+}
 
 template <typename T, bool MASK, bool STAGE, int FLAGS>
 __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const EntryD *__restrict__ ents,
@@ -165,6 +199,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
         b.xoff = e.xoff; b.yoff = e.yoff; b.w = e.w; b.h = e.h;
         b.fill_mode = e.fill_mode; b.mask_pair = e.mask_pair;
         b.nd = e.nd; b.fillv = e.fill;
+        b.has_nodata = e.has_nodata; b.out_dtype = e.out_dtype; b.nodata64 = e.nodata64;
         b.pair = p;
         b.soff = -1;
       }
@@ -279,10 +314,19 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
       const int r = band0 + rr;
       if (r >= H || x0 >= W) break;
       uint8_t *dst = rgba_tile + ((int64_t)r * a.max_w + x0) * 4;
+      T *cdst = nullptr;   // canvas mode: the typed canvas row of this lane
+      if constexpr ((FLAGS & kCanvas) != 0) {
+        const int64_t e = a.cov_offsets ? a.cov_offsets[t] + (int64_t)r * a.cov_stride + x0
+                                        : (int64_t)r * a.max_w + x0;
+        cdst = (T *)(a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride) + e;
+      }
       V c[kLanePx];
       if (first) {
 #pragma unroll
         for (int q = 0; q < kLanePx; q++) c[q] = cnod;
+      } else if constexpr ((FLAGS & kCanvas) != 0) {
+#pragma unroll
+        for (int q = 0; q < kLanePx; q++) c[q] = (x0 + q < W) ? (V)cdst[q] : cnod;
       } else {
 #pragma unroll
         for (int q = 0; q < kLanePx; q++) c[q] = (x0 + q < W) ? ((const V *)dst)[q] : cnod;
@@ -314,6 +358,39 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
           kind = R.kind; nleaf = R.nleaf; pool_off = R.pool_off;
         }
         kind = __builtin_amdgcn_readfirstlane(kind);
+        if constexpr ((FLAGS & kBilinear) != 0) {   // bilinear: exact fp64 coordinates, 4 taps
+          const Leaf *lv = pool + pool_off;
+          const bool hnd = b.has_nodata != 0;
+          const double nd64 = b.nodata64;
+          const int odt = b.out_dtype;
+#pragma unroll
+          for (int q = 0; q < kLanePx; q++) {
+            const int ic = ic0 + q;
+            const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
+            double sx, sy;
+            if (kind == ROW_LINEAR) {
+              const double dist = (double)ic0 + (double)q;
+              sy = ys0 + dY * dist;
+              sx = xs0 + dX * dist;
+            } else {
+              const int icc = in ? ic : 0;
+              int l = 0;
+              while (l + 1 < nleaf && lv[l + 1].start <= icc) l++;
+              const double dist = (double)(icc - lv[l].start);
+              sy = lv[l].ys0 + lv[l].dY * dist;
+              sx = lv[l].xs0 + lv[l].dX * dist;
+            }
+            V v = fillv, got;
+            if (in && bil_sample<T>(bandp, bx, by, hnd, nd64, odt, sx, sy, got)) v = got;
+            bool take = in && (v != nd);
+            if (MASK && b.mask_pair >= 0) {
+              if (take) take = !mask_fast<GSKYHIP_RESAMPLE_BILINEAR>(ents, rows, pool, a.mask, ents[pair], ic, ir);
+            }
+            const bool t2 = take && (!fill_mode || c[q] == nd);
+            c[q] = t2 ? v : c[q];
+          }
+          continue;
+        }
         // source index of each of the lane's pixels: (ux, uy) and validity
         uint32_t ux[kLanePx], uy[kLanePx];
         uint32_t okm = 0;
@@ -404,6 +481,33 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
           c[q] = t2 ? v : c[q];
         }
       }
+      if constexpr ((FLAGS & kCanvas) != 0) {   // typed canvas (tile_merger.go:562-652): T stores
+        T tv[kLanePx];
+#pragma unroll
+        for (int q = 0; q < kLanePx; q++) tv[q] = (T)c[q];
+        if (x0 + kLanePx <= W && (((uintptr_t)cdst) & (sizeof(T) * kLanePx >= 16 ? 15 : sizeof(T) * kLanePx - 1)) == 0) {
+          if constexpr (sizeof(T) == 4) {
+            u32x4 v0, v1;
+            __builtin_memcpy(&v0, tv, 16);
+            __builtin_memcpy(&v1, tv + 4, 16);
+            __builtin_nontemporal_store(v0, (GPTR(u32x4))cdst);
+            __builtin_nontemporal_store(v1, (GPTR(u32x4))(cdst + 4));
+          } else if constexpr (sizeof(T) == 2) {
+            u32x4 v0;
+            __builtin_memcpy(&v0, tv, 16);
+            __builtin_nontemporal_store(v0, (GPTR(u32x4))cdst);
+          } else {
+            uint64_t v0;
+            __builtin_memcpy(&v0, tv, 8);
+            *(uint64_t *)cdst = v0;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < kLanePx; q++)
+            if (x0 + q < W) cdst[q] = tv[q];
+        }
+        continue;
+      }
       if (!last) {   // partial canvas parked in the slot (raw values), re-read next pass
 #pragma unroll
         for (int q = 0; q < kLanePx; q++)
@@ -445,8 +549,24 @@ void launch_lds_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
 #define GSKY_LDS_LAUNCH(M, S, F)                                                                                   \
   hipLaunchKernelGGL((render_lds_kernel<T, M, S, F>), grid, dim3(256), 0, s, a, a.entries, a.order, a.rows, a.pool, \
                      a.tplans, a.tiles, n_items, per_xcd)
+  if (!std::is_same<T, float>::value && (a.lds_flags & kLut) && !(a.lds_mode & (kBilinear | kCanvas))) {
+    const int n = sizeof(T) == 1 ? 256 : 65536;   // Scale + palette LUT of the launch
+    hipLaunchKernelGGL(scale_lut_kernel<T>, dim3((n + 255) / 256), dim3(256), 0, s, a, (const uint32_t *)a.ramp,
+                       a.lut, n);
+  }
   const bool stage = a.lds_stage != 0;
   const int fl = a.lds_flags;
+  if (a.lds_mode & (kBilinear | kCanvas)) {   // bilinear and / or typed canvas output
+    switch ((a.lds_mode & (kBilinear | kCanvas)) | (mask ? 16 : 0)) {
+      case kBilinear: GSKY_LDS_LAUNCH(false, false, kBilinear); break;
+      case kCanvas: GSKY_LDS_LAUNCH(false, false, kCanvas); break;
+      case kBilinear | kCanvas: GSKY_LDS_LAUNCH(false, false, kBilinear | kCanvas); break;
+      case 16 | kBilinear: GSKY_LDS_LAUNCH(true, false, kBilinear); break;
+      case 16 | kCanvas: GSKY_LDS_LAUNCH(true, false, kCanvas); break;
+      default: GSKY_LDS_LAUNCH(true, false, kBilinear | kCanvas); break;
+    }
+    return;
+  }
   if (mask) {
     if (stage) GSKY_LDS_LAUNCH(true, true, 0); else GSKY_LDS_LAUNCH(true, false, 0);
   } else if (stage) {

@@ -220,6 +220,27 @@ class TileBatch:
             return cv
         return (out, cv) if canvas else out
 
+    def render_coverage(self, params: ScaleParams, out: torch.Tensor, offsets, resample: int = 0,
+                        phase: int = 0) -> torch.Tensor:
+        """WCS GetCoverage: every tile's typed canvas of the first namespace
+        written straight into `out` (a 2-D tensor of the canvas type) with
+        tile t's top-left at flat element offset offsets[t]
+        (gskyhip_render_coverage; no per-tile slots, no assembly copy)."""
+        if out.dim() != 2:
+            raise ValueError("coverage must be 2-D")
+        offs = offsets if isinstance(offsets, torch.Tensor) else torch.tensor(list(offsets), dtype=torch.int64)
+        offs = offs.to(self.device, torch.int64).contiguous()
+        self._cov_offs = offs
+        sp = params.c()
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().gskyhip_render_coverage(
+            phase, self.value_types if self.typed else 0, C.c_void_p(self._gran.data_ptr()), self.n_granules,
+            C.c_void_p(self._crs.data_ptr()), self.n_crs, self.dst_crs, C.c_void_p(self._tiles.data_ptr()),
+            self.n_tiles, C.c_void_p(self._pairs.data_ptr()), self.n_pairs, self.max_w, self.max_h, resample,
+            C.byref(sp), C.c_void_p(offs.data_ptr()), out.shape[1], C.c_void_p(out.data_ptr()),
+            C.c_void_p(self._ws.data_ptr()), self._ws.numel(), stream), "render_coverage")
+        return out
+
     def status(self) -> int:
         """TilePlan status of the last call (synchronous): 0 or an error code."""
         stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)

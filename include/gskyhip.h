@@ -220,6 +220,21 @@ int gskyhip_render_tiles_typed(int phase, uint32_t value_types, const gskyhip_gr
                                uint8_t *rgba_out, void *canvas_out,
                                void *workspace, int64_t workspace_bytes, void *stream);
 
+/* WCS GetCoverage (ows.go:815-1150): the chunk tiles rendered as typed
+ * canvases (FusionUnscale, ows.go:728: no Scale / RGBA) of the first
+ * namespace, each written straight into ONE coverage image at its chunk
+ * offset -- tile t's row r lands at coverage_out + (tile_offsets[t] + r *
+ * row_stride) elements -- instead of per-tile slots, so no assembly copy
+ * follows.  tile_offsets: dev int64 per tile; the coverage's value type is
+ * the canvas type (value_types hint as gskyhip_render_tiles_typed). */
+int gskyhip_render_coverage(int phase, uint32_t value_types, const gskyhip_granule *granules,
+                            int n_granules, const gskyhip_crs *crs_table, int n_crs, int dst_crs,
+                            const gskyhip_tile *tiles, int n_tiles, const int32_t *pair_granule,
+                            int n_pairs, int max_tile_width, int max_tile_height, int resample,
+                            const gskyhip_scale_params *sp, const int64_t *tile_offsets,
+                            int64_t row_stride, void *coverage_out, void *workspace,
+                            int64_t workspace_bytes, void *stream);
+
 /* Warped windows only (the FlexRasters of tile_grpc.go:228-241): for pair p
  * (tile t, granule g) writes window bbox[4*p..] = {xoff,yoff,w,h} and the
  * window data (dtype of warp.go:232-243) into win_out + p*win_stride bytes. */
