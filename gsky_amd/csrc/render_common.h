@@ -344,5 +344,8 @@ constexpr int kBilinear = 4, kCanvas = 8;   // render_lds_kernel modes (RenderAr
 
 // The typed LDS-staged band kernels (render_lds.hip) for value type `vt`.
 void launch_lds_kernels(const RenderArgs &a, int vt, bool mask, int n_items, hipStream_t s);
+// Generic kernels (render_generic{1,3}.hip); general_only: complex tiles only.
+void dispatch_render_1(const RenderArgs &a, int resample, bool mask, dim3 grid, bool general_only, hipStream_t s);
+void dispatch_render_3(const RenderArgs &a, int resample, bool mask, dim3 grid, bool general_only, hipStream_t s);
 
 }  // namespace gsky

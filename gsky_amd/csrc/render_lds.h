@@ -34,6 +34,7 @@ constexpr int kBandRows = kLdsBandRows;
 constexpr int kBandEnt = 16;            // entries per pass over the band
 constexpr int kStageBytes = 24 * 1024;  // LDS for source windows per block
 constexpr int kLanePx = 8;              // pixels per lane per row
+constexpr int kBandCols = 64 * kLanePx;  // columns per block (one wave row)
 constexpr int kStageDw = 8;             // staging dwords per thread per round (in flight together)
 
 struct BandEnt {
@@ -153,14 +154,18 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
 
   const int item = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (item >= n_items) return;
+  // item = (tile, 16-row band, 512-column block); column blocks innermost
   const int bands_per_tile = (a.max_h + kBandRows - 1) / kBandRows;
-  const int t = item / bands_per_tile;
+  const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
+  const int t = item / (bands_per_tile * col_blocks);
+  const int in_tile = item - t * bands_per_tile * col_blocks;
   const TilePlan &tp = tplans[t];
   if (tp.complex || tp.vt != vt_code<T>()) return;
   const gskyhip_tile &tile = tiles[t];
   const int W = tile.width, H = tile.height;
-  const int band0 = (item % bands_per_tile) * kBandRows;
-  if (band0 >= H) return;
+  const int band0 = (in_tile / col_blocks) * kBandRows;
+  const int xb = (in_tile % col_blocks) * kBandCols;
+  if (band0 >= H || xb >= W) return;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   if (a.ramp) s_ramp[tid] = a.ramp[tid];
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
   const V cnod = as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]));
   const int32_t *ord = order + tile.pair_begin;
   const int n_entries = tp.n_entries;
-  const int x0 = lane * kLanePx;
+  const int x0 = xb + lane * kLanePx;
   const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
   const bool has_ramp = a.ramp != nullptr;
   uint8_t *rgba_tile = a.rgba + (int64_t)t * a.max_h * a.max_w * 4;
@@ -188,7 +193,8 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
       if (k < n_entries) {
         p = ord[k];
         const EntryD &e = ents[p];
-        hit = e.ns == ns_out && e.w > 0 && e.yoff < band0 + kBandRows && e.yoff + e.h > band0;
+        hit = e.ns == ns_out && e.w > 0 && e.yoff < band0 + kBandRows && e.yoff + e.h > band0 &&
+              e.xoff < xb + kBandCols && e.xoff + e.w > xb;
       }
       const unsigned long long m = __ballot(hit);
       const int pos = __popcll(m & ((1ull << lane) - 1ull));

@@ -418,6 +418,30 @@ def test_lds_kernel_types(gpu, oracle, dt):
     assert (exp[..., 3] > 0).mean() > 0.3
 
 
+@pytest.mark.parametrize("resample", [0, 1])
+def test_lds_kernel_wide_tiles(gpu, oracle, resample):
+    """Tiles wider than one 512-column block of the band kernel (1100 px:
+    three blocks, the last ragged), RGBA and typed canvases, NN and bilinear."""
+    import gsky_amd
+    cfg = synth.config_c2(scale=0.1, tiles_per_side=2, tile_px=1100)
+    cfg.resample = resample
+    b = gpu_batch(cfg)
+    sp, pal = gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True)
+    got = b.render(sp, pal, resample=resample).cpu().numpy().copy()
+    cv = b.render(sp, pal, resample=resample, rgba=False).cpu().numpy().copy()
+    exp, ecv, created = oracle_render(oracle, cfg, canvas=True)
+    if resample == 0:
+        assert np.array_equal(got, exp)
+        assert np.array_equal(cv[:, 0, :1100 * 1100 * 2], ecv[:, 0, :1100 * 1100 * 2])
+    else:
+        e = ecv[:, 0, :1100 * 1100 * 2].view(np.int16)
+        g = cv[:, 0, :1100 * 1100 * 2].view(np.int16)
+        assert np.array_equal(e == -999, g == -999)
+        assert np.abs(e.astype(np.int32) - g.astype(np.int32)).max() <= 1
+        assert (got[..., 3] > 0).sum() == (exp[..., 3] > 0).sum()
+    assert (exp[..., 3] > 0).mean() > 0.3
+
+
 def test_lds_kernel_many_entries_multipass(gpu, oracle):
     """40 overlapping granules on one tile: more entries per band than the
     kernel stages at once (16), so the band folds in several passes."""
