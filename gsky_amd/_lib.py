@@ -80,6 +80,7 @@ EXPORTS = [
     "gskyhip_drill_workspace_size", "gskyhip_drill_batch", "gskyhip_drill_descriptors",
     "gskyhip_drill_merge", "gskyhip_fnv32a", "gskyhip_version", "gskyhip_device_count",
     "gskyhip_render_status",
+    "gskyhip_render_tile_info",
 ]
 
 _lib = None
@@ -111,6 +112,7 @@ def lib() -> C.CDLL:
     L.gskyhip_warp_windows.argtypes = [vp, ci, vp, ci, ci, vp, ci, vp, ci, ci, ci, ci, vp, vp, vp, vp, i64,
                                        vp, i64, vp]
     L.gskyhip_render_status.argtypes = [vp, ci, ci, ci, vp]
+    L.gskyhip_render_tile_info.argtypes = [vp, ci, ci, ci, vp, vp, vp]
     L.gskyhip_merge_rasters.argtypes = [C.POINTER(FlexRasterC), ci, C.POINTER(Mask), C.POINTER(vp), ci,
                                         C.POINTER(i32), C.POINTER(i32), C.POINTER(d), vp]
     L.gskyhip_scale.argtypes = [vp, ci, i64, d, C.POINTER(ScaleParams), vp, vp]

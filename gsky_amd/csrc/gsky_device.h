@@ -280,6 +280,138 @@ __device__ inline bool xform_point(const Xform &t, bool dst_to_src, double &x, d
   return true;
 }
 
+// ---------------------------------------------------------------- separable transform
+// dst -> src of a north-up destination geotransform (gt[2] = gt[4] = 0) and
+// a cylindrical destination CRS (Web Mercator, lon/lat): X and lambda depend
+// on the pixel column only, Y and phi on the row only.  The points of a row
+// record (planning) then share per-column parts (SepCol, once per pair) and
+// a per-row part (SepRow, once per row); sep_point() combines them with the
+// expressions and operation order of xform_point(t, true, ...) -- bit for
+// bit: the dropped y*gt[2] / x*gt[4] terms are signed zeros for the positive
+// pixel coordinates used, and adding a zero leaves every other value alone.
+struct SepCol { double lam, sl, cl; int32_t ok, _pad; };
+struct SepRow { double phi, r1, r2; int32_t ok, _pad; };
+
+__host__ __device__ inline bool sep_possible(const Xform &t) {
+  const int dk = t.dst.kind, sk = t.src.kind;
+  return t.reproject && t.dst_gt[2] == 0.0 && t.dst_gt[4] == 0.0 &&
+         (dk == GSKYHIP_CRS_WEBMERC || dk == GSKYHIP_CRS_LONGLAT) &&
+         (sk == GSKYHIP_CRS_WEBMERC || sk == GSKYHIP_CRS_LONGLAT || sk == GSKYHIP_CRS_AEA ||
+          sk == GSKYHIP_CRS_SINU);
+}
+
+// Column part at pixel column x (y_any: any positive pixel row).
+__host__ __device__ inline SepCol sep_col(const Xform &t, double x, double y_any) {
+  SepCol c;
+  c.sl = c.cl = 0.0;
+  c._pad = 0;
+  const double *g1 = t.dst_gt;
+  const double X = g1[0] + x * g1[1] + y_any * g1[2];
+  bool ok = !(X == HUGE_VAL);
+  double lam;
+  const gskyhip_crs &d = t.dst, &s = t.src;
+  if (d.kind == GSKYHIP_CRS_LONGLAT) {        // crs_inverse, unitconvert
+    lam = X * kD2R;
+  } else {                                    // crs_inverse, merc s_inverse
+    const double xn = (X * 1.0 - d.x0) * d.ra;
+    double l = xn / d.k0;
+    if (l == HUGE_VAL || l != l) ok = false;
+    l = l + d.lam0;
+    lam = adjlon(l);
+  }
+  if (s.kind == GSKYHIP_CRS_LONGLAT) {        // crs_forward, unitconvert
+    c.sl = lam * kR2D;
+  } else {
+    if (lam > 10 || lam < -10) ok = false;
+    lam = lam - s.lam0;
+    lam = adjlon(lam);
+    if (s.kind == GSKYHIP_CRS_WEBMERC) {
+      c.sl = s.k0 * lam;
+    } else if (s.kind == GSKYHIP_CRS_AEA) {
+      lam *= s.n;
+      c.sl = sin(lam);
+      c.cl = cos(lam);
+    } else {                                  // SINU: xn = lam * cos(phi)
+      c.sl = lam;
+    }
+  }
+  c.lam = lam;
+  c.ok = ok ? 1 : 0;
+  return c;
+}
+
+// Row part at pixel row y (x_any: any positive pixel column).
+__host__ __device__ inline SepRow sep_row(const Xform &t, double x_any, double y) {
+  SepRow r;
+  r.r1 = r.r2 = 0.0;
+  r._pad = 0;
+  const double *g1 = t.dst_gt;
+  const double Y = g1[3] + x_any * g1[4] + y * g1[5];
+  bool ok = !(Y == HUGE_VAL);
+  double phi;
+  const gskyhip_crs &d = t.dst, &s = t.src;
+  if (d.kind == GSKYHIP_CRS_LONGLAT) {
+    phi = Y * kD2R;
+  } else {
+    const double yn = (Y * 1.0 - d.y0) * d.ra;
+    const double p = kHalfPi - 2. * atan(exp(-yn / d.k0));
+    if (p == HUGE_VAL || p != p) ok = false;
+    phi = p;
+  }
+  if (s.kind == GSKYHIP_CRS_LONGLAT) {
+    r.r1 = phi * kR2D;
+  } else {
+    const double tt = (phi < 0 ? -phi : phi) - kHalfPi;
+    if (tt > 1e-12) ok = false;
+    if (phi > kHalfPi) phi = kHalfPi;
+    if (phi < -kHalfPi) phi = -kHalfPi;
+    if (s.kind == GSKYHIP_CRS_WEBMERC) {
+      if (fabs(fabs(phi) - kHalfPi) <= 1.e-10) ok = false;
+      r.r1 = s.k0 * log(tan(kFortPi + .5 * phi));
+    } else if (s.kind == GSKYHIP_CRS_AEA) {
+      double rho = s.c - (s.es > 0. ? s.n * qsfn(sin(phi), s.e, s.one_es) : (s.n + s.n) * sin(phi));
+      if (rho < 0.) ok = false;
+      r.r1 = s.dd * sqrt(rho);
+    } else {                                  // SINU
+      r.r1 = cos(phi);
+      r.r2 = phi;
+    }
+  }
+  r.phi = phi;
+  r.ok = ok ? 1 : 0;
+  return r;
+}
+
+// xform_point(t, true, x, y) of the pixel at (column part c, row part r).
+__host__ __device__ inline bool sep_point(const Xform &t, const SepCol &c, const SepRow &r, double &x, double &y) {
+  if (!c.ok || !r.ok) return false;
+  const gskyhip_crs &s = t.src;
+  double X, Y;
+  if (s.kind == GSKYHIP_CRS_LONGLAT) {
+    X = c.sl;
+    Y = r.r1;
+  } else {
+    double xn, yn;
+    if (s.kind == GSKYHIP_CRS_WEBMERC) {
+      xn = c.sl;
+      yn = r.r1;
+    } else if (s.kind == GSKYHIP_CRS_AEA) {
+      xn = r.r1 * c.sl;
+      yn = s.rho0 - r.r1 * c.cl;
+    } else {
+      xn = c.sl * r.r1;
+      yn = r.r2;
+    }
+    if (xn != xn || yn != yn || fabs(xn) == HUGE_VAL || fabs(yn) == HUGE_VAL) return false;
+    X = 1.0 * (s.a * xn + s.x0);
+    Y = 1.0 * (s.a * yn + s.y0);
+  }
+  const double *g2 = t.src_igt;
+  x = g2[0] + X * g2[1] + Y * g2[2];
+  y = g2[3] + X * g2[4] + Y * g2[5];
+  return true;
+}
+
 // ---------------------------------------------------------------- plans
 // Per (tile, granule) pair, produced by the planning kernels.
 struct PairPlan {
@@ -337,8 +469,14 @@ struct RowRec {
 };
 struct Leaf {
   double xs0, ys0, dX, dY;
-  int32_t start, kind;   // kind: 0 linear, 1 exact
+  int32_t start, kind;   // LeafKind
 };
+// LINEAR: xs0 + dX * (i - start); one pixel's exact point is a LINEAR leaf
+// with dX = dY = 0.  EXACT: [start, next start) transformed per pixel at
+// render time (complex tiles only).  FAILED: the pixel's exact transform
+// failed (window fill).  PENDING: planning-internal, pixel `start` of pair
+// (int)dX, window row (int)dY awaiting plan_exact_kernel.
+enum LeafKind : int32_t { LEAF_LINEAR = 0, LEAF_EXACT = 1, LEAF_FAILED = 2, LEAF_PENDING = 3 };
 
 constexpr int kMaxLeavesLocal = 16;
 

@@ -573,6 +573,33 @@ int gskyhip_render_status(void *workspace, int n_tiles, int n_pairs, int max_til
   return 0;
 }
 
+int gskyhip_render_tile_info(void *workspace, int n_tiles, int n_pairs, int max_tile_height, int32_t *info_out,
+                             int32_t *counters_out, void *stream) {
+  if (n_tiles < 0 || n_pairs < 0 || (n_tiles > 0 && (!workspace || !info_out))) return GSKYHIP_E_ARG;
+  auto al = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+  const int np = n_pairs > 0 ? n_pairs : 1;
+  const int64_t off = al(sizeof(PairPlan) * (int64_t)np) + al(sizeof(Xform) * (int64_t)np);
+  if (n_tiles == 0) return 0;
+  if (counters_out) {
+    const int64_t c_off = gsky::render_counters_offset(n_tiles, n_pairs, max_tile_height);
+    if (hipMemcpyAsync(counters_out, (char *)workspace + c_off, 3 * sizeof(int32_t), hipMemcpyDeviceToHost,
+                       (hipStream_t)stream) != hipSuccess)
+      return GSKYHIP_E_HIP;
+  }
+  std::vector<TilePlan> tp((size_t)n_tiles);
+  if (hipMemcpyAsync(tp.data(), (char *)workspace + off, sizeof(TilePlan) * n_tiles, hipMemcpyDeviceToHost,
+                     (hipStream_t)stream) != hipSuccess)
+    return GSKYHIP_E_HIP;
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return GSKYHIP_E_HIP;
+  for (int t = 0; t < n_tiles; t++) {
+    info_out[4 * t] = tp[t].status;
+    info_out[4 * t + 1] = tp[t].complex;
+    info_out[4 * t + 2] = tp[t].vt;
+    info_out[4 * t + 3] = tp[t].n_entries;
+  }
+  return 0;
+}
+
 int gskyhip_warp_windows(const gskyhip_granule *granules, int n_granules, const gskyhip_crs *crs_table,
                          int n_crs, int dst_crs, const gskyhip_tile *tiles, int n_tiles,
                          const int32_t *pair_granule, int n_pairs, int max_tile_width, int max_tile_height,

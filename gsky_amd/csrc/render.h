@@ -9,6 +9,7 @@ namespace gsky {
 
 struct MaskSpecS;
 
+int64_t render_counters_offset(int n_tiles, int n_pairs, int max_h);   // plan counters in the workspace
 int64_t render_workspace_size(int n_tiles, int n_pairs, int max_h);
 
 // Shared planning: pairs, tiles, rows.  Returns 0 or an error.

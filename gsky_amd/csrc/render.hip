@@ -49,6 +49,8 @@ struct PlanArgs {
   int64_t *split_list;         // (pair * max_h + row) of rows that need the recursion
   int32_t *complex_list;       // tiles that need exact per-pixel transforms
   EntryD *entries;             // n_pairs render descriptors
+  SepCol *sepcols;             // 3 per pair: column parts of the separable transform
+  int sep;                     // 1: plan_rows uses the separable transform where it applies
 };
 
 // ---------------------------------------------------------------- pair ownership
@@ -359,7 +361,10 @@ __global__ void plan_tiles_kernel(PlanArgs a) {
     // the typed fast path needs one value type and no GDALCopyWords promotion
     const bool same = pp.src_dtype == pp.out_dtype ||
                       (pp.src_dtype == GSKYHIP_BYTE && pp.out_dtype == GSKYHIP_SIGNEDBYTE);
-    if (!same) vt = 0;
+    // ... and a band the band kernels address with 32-bit offsets (render_nn.h)
+    const bool small = pp.band_x < (1 << 24) && pp.band_y < (1 << 24) &&
+                       (int64_t)pp.band_x * pp.band_y * type_size(pp.src_dtype) < 2147483648LL;
+    if (!same || !small) vt = 0;
     else if (vt < 0) vt = pp.out_dtype;
     else if (vt != pp.out_dtype) vt = 0;
   }
@@ -380,6 +385,32 @@ __device__ __forceinline__ void flag_complex(const PlanArgs &a, int tile) {
   }
 }
 
+__device__ __forceinline__ void push_split(const PlanArgs &a, int p, int row) {
+  const int k = atomicAdd(&a.counters[1], 1);
+  a.split_list[k] = (int64_t)p * a.max_h + row;
+}
+
+__device__ __forceinline__ Leaf pending_leaf(int p, int row, int i) {
+  Leaf L;
+  L.xs0 = 0.0; L.ys0 = 0.0; L.dX = (double)p; L.dY = (double)row;
+  L.start = i; L.kind = LEAF_PENDING;
+  return L;
+}
+
+// Column parts of the separable transform (gsky_device.h) at the three
+// columns every row record transforms: first, middle, last.
+__global__ __launch_bounds__(256) void plan_cols_kernel(PlanArgs a) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = (int)(gid / 3), k = (int)(gid % 3);
+  if (p >= a.n_pairs) return;
+  const PairPlan &pp = a.pairs[p];
+  const Xform &t = a.xforms[p];
+  if (!sep_possible(t) || pp.w <= 5 || pp.h <= 0) return;
+  const int n = pp.w, nMiddle = (n - 1) / 2;
+  const int col = k == 0 ? 0 : (k == 1 ? nMiddle : n - 1);
+  a.sepcols[3 * (int64_t)p + k] = sep_col(t, col + 0.5 + pp.xoff, 0.5 + pp.yoff);
+}
+
 // Light pass, one thread per (pair, window row): the three exact points of
 // GDALApproxTransform (first / middle / last) and its error test.  Rows whose
 // middle error exceeds 0.125 go to the split list (plan_split_kernel).
@@ -397,19 +428,36 @@ __global__ __launch_bounds__(256) void plan_rows_kernel(PlanArgs a) {
   const int n = pp.w;
   const int nMiddle = (n - 1) / 2;
   const double yrow = row + 0.5 + pp.yoff;
-  // GDALApproxTransform preconditions: y constant, x distinct, nPoints > 5
-  if (n <= 5) {
+  // GDALApproxTransform preconditions: y constant, x distinct, nPoints > 5;
+  // otherwise every pixel is transformed exactly: the split pass turns the row
+  // into per-pixel leaves (plan_exact_kernel) so the tile stays simple
+  if (n <= 0) {
+    rec.kind = ROW_LINEAR;   // empty window: no pixel reads the record
+  } else if (n <= 5) {
     rec.kind = ROW_EXACT;
-    flag_complex(a, pp.tile);
+    push_split(a, p, row);
   } else {
     double xs[3] = {0 + 0.5 + pp.xoff, nMiddle + 0.5 + pp.xoff, (n - 1) + 0.5 + pp.xoff};
     double ys[3] = {yrow, yrow, yrow};
-    bool ok0 = xform_point(t, true, xs[0], ys[0]);
-    bool ok1 = xform_point(t, true, xs[1], ys[1]);
-    bool ok2 = xform_point(t, true, xs[2], ys[2]);
+    bool ok0, ok1, ok2;
+    if (a.sep && sep_possible(t)) {   // per-column parts from plan_cols_kernel, one row part
+      const SepCol *sc = a.sepcols + 3 * (int64_t)p;
+      const SepRow sr = sep_row(t, xs[0], yrow);
+      double ox, oy;
+      ok0 = sep_point(t, sc[0], sr, ox, oy);
+      if (ok0) { xs[0] = ox; ys[0] = oy; }
+      ok1 = sep_point(t, sc[1], sr, ox, oy);
+      if (ok1) { xs[1] = ox; ys[1] = oy; }
+      ok2 = sep_point(t, sc[2], sr, ox, oy);
+      if (ok2) { xs[2] = ox; ys[2] = oy; }
+    } else {
+      ok0 = xform_point(t, true, xs[0], ys[0]);
+      ok1 = xform_point(t, true, xs[1], ys[1]);
+      ok2 = xform_point(t, true, xs[2], ys[2]);
+    }
     if (!(ok0 && ok1 && ok2)) {
       rec.kind = ROW_EXACT;
-      flag_complex(a, pp.tile);
+      push_split(a, p, row);
     } else {
       const double x0 = 0 + 0.5 + pp.xoff, xl = (n - 1) + 0.5 + pp.xoff, xm = nMiddle + 0.5 + pp.xoff;
       const double dX = (xs[2] - xs[0]) / (xl - x0);
@@ -422,8 +470,7 @@ __global__ __launch_bounds__(256) void plan_rows_kernel(PlanArgs a) {
         rec.kind = ROW_DESCEND;  // provisional: root SME kept for the split pass
         rec.v[0] = xs[0]; rec.v[1] = ys[0]; rec.v[2] = xs[1];
         rec.v[3] = ys[1]; rec.v[4] = xs[2]; rec.v[5] = ys[2];
-        const int k = atomicAdd(&a.counters[1], 1);
-        a.split_list[k] = (int64_t)p * a.max_h + row;
+        push_split(a, p, row);
       }
     }
   }
@@ -513,7 +560,10 @@ __device__ __noinline__ int approx_leaves(const Xform &t, int xoff, double yrow,
 }
 
 // Split pass over the rows the light pass could not interpolate in one
-// piece: leaves into the pool (ROW_POOL) or, on pool overflow, ROW_DESCEND.
+// piece.  DESCEND rows: the approximation recursion's leaves into the pool,
+// every EXACT piece expanded into per-pixel pending leaves; EXACT rows: one
+// pending leaf per pixel.  The row becomes ROW_POOL; on pool overflow it keeps
+// its kind and the tile goes to the general kernel.
 __global__ __launch_bounds__(64) void plan_split_kernel(PlanArgs a) {
   const int nsplit = a.counters[1];
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nsplit; k += gridDim.x * blockDim.x) {
@@ -521,22 +571,58 @@ __global__ __launch_bounds__(64) void plan_split_kernel(PlanArgs a) {
     const int p = (int)(key / a.max_h), row = (int)(key % a.max_h);
     const PairPlan &pp = a.pairs[p];
     RowRec &rec = a.rows[key];
+    if (rec.kind == ROW_EXACT) {
+      const int n = pp.w;
+      const int off = atomicAdd(&a.counters[0], n);
+      if (off + n > a.pool_cap) { flag_complex(a, pp.tile); continue; }
+      for (int j = 0; j < n; j++) a.pool[off + j] = pending_leaf(p, row, j);
+      rec.kind = ROW_POOL;
+      rec.nleaf = n;
+      rec.pool_off = off;
+      continue;
+    }
     const double yrow = row + 0.5 + pp.yoff;
     Leaf local[kMaxLeavesLocal];
     const int nl = approx_leaves(a.xforms[p], pp.xoff, yrow, pp.w, rec.v, local);
+    int total = 0;
+    for (int j = 0; j < nl; j++)
+      total += local[j].kind == LEAF_LINEAR ? 1 : (j + 1 < nl ? local[j + 1].start : pp.w) - local[j].start;
     int off = -1;
     if (nl > 0) {
-      off = atomicAdd(&a.counters[0], nl);
-      if (off + nl > a.pool_cap) off = -1;
+      off = atomicAdd(&a.counters[0], total);
+      if (off + total > a.pool_cap) off = -1;
     }
-    bool exact = off < 0;
-    if (off >= 0) {
-      for (int j = 0; j < nl; j++) { a.pool[off + j] = local[j]; exact = exact || local[j].kind != 0; }
-      rec.kind = ROW_POOL;
-      rec.nleaf = nl;
-      rec.pool_off = off;
+    if (off < 0) { flag_complex(a, pp.tile); continue; }   // stays ROW_DESCEND
+    int m = off;
+    for (int j = 0; j < nl; j++) {
+      if (local[j].kind == LEAF_LINEAR) {
+        a.pool[m++] = local[j];
+      } else {
+        const int end = j + 1 < nl ? local[j + 1].start : pp.w;
+        for (int i = local[j].start; i < end; i++) a.pool[m++] = pending_leaf(p, row, i);
+      }
     }
-    if (exact) flag_complex(a, pp.tile);
+    rec.kind = ROW_POOL;
+    rec.nleaf = total;
+    rec.pool_off = off;
+  }
+}
+
+// Exact points of the pending leaves (GDALGenImgProjTransform per pixel, the
+// expressions of exact_coords()), one thread per pool entry.
+__global__ __launch_bounds__(256) void plan_exact_kernel(PlanArgs a) {
+  const int used = min(a.counters[0], a.pool_cap);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < used; k += gridDim.x * blockDim.x) {
+    Leaf L = a.pool[k];
+    if (L.kind != LEAF_PENDING) continue;
+    const int p = (int)L.dX, row = (int)L.dY;
+    if (p < 0 || p >= a.n_pairs || row < 0 || row >= a.max_h) continue;   // stale slot of an abandoned reservation
+    const PairPlan &pp = a.pairs[p];
+    double sx, sy;
+    const bool ok = exact_coords(a.xforms[p], pp.xoff, pp.yoff, L.start, row, sx, sy);
+    L.xs0 = sx; L.ys0 = sy; L.dX = 0.0; L.dY = 0.0;
+    L.kind = ok ? LEAF_LINEAR : LEAF_FAILED;
+    a.pool[k] = L;
   }
 }
 
@@ -725,6 +811,7 @@ struct Carve {
   RowRec *rows; Leaf *pool; int32_t *counters; MinMax *minmax; int64_t *split_list; int32_t *complex_list;
   EntryD *entries;
   uint32_t *lut;        // 65536 RGBA: Scale + palette of every 16-bit value (band kernel)
+  SepCol *sepcols;
   int pool_cap;
   int64_t total;
 };
@@ -750,6 +837,7 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   const int64_t o_cl = take(sizeof(int32_t) * (int64_t)nt);
   const int64_t o_ent = take(sizeof(EntryD) * (int64_t)np);
   const int64_t o_lut = take(sizeof(uint32_t) * 65536);
+  const int64_t o_sep = take(sizeof(SepCol) * 3 * (int64_t)np);
   c.total = off;
   char *b = (char *)base;
   c.pairs = (PairPlan *)(b + o_pairs);
@@ -765,7 +853,12 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   c.complex_list = (int32_t *)(b + o_cl);
   c.entries = (EntryD *)(b + o_ent);
   c.lut = (uint32_t *)(b + o_lut);
+  c.sepcols = (SepCol *)(b + o_sep);
   return c;
+}
+
+int64_t render_counters_offset(int n_tiles, int n_pairs, int max_h) {
+  return (int64_t)((char *)carve(nullptr, n_tiles, n_pairs, max_h).counters - (char *)nullptr);
 }
 
 int64_t render_workspace_size(int n_tiles, int n_pairs, int max_h) {
@@ -785,6 +878,9 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   a.pair_tile = cv.pair_tile; a.rows = cv.rows; a.pool = cv.pool; a.counters = cv.counters;
   a.pool_cap = cv.pool_cap; a.split_list = cv.split_list; a.complex_list = cv.complex_list;
   a.entries = cv.entries;
+  a.sepcols = cv.sepcols;
+  const char *sep = getenv("GSKYHIP_PLAN_SEP");   // A/B knob: 0 = three full transforms per row
+  a.sep = sep ? atoi(sep) : 1;
   hipStream_t s = rc.stream;
   if (hipMemsetAsync(cv.counters, 0, 256, s) != hipSuccess) return GSKYHIP_E_HIP;
   hipLaunchKernelGGL(pair_tile_kernel, dim3((rc.n_tiles + 255) / 256), dim3(256), 0, s, rc.tiles, rc.n_tiles,
@@ -792,9 +888,13 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   if (rc.n_pairs > 0) hipLaunchKernelGGL(plan_pairs_kernel, dim3(rc.n_pairs), dim3(64), 0, s, a);
   hipLaunchKernelGGL(plan_tiles_kernel, dim3((rc.n_tiles + 127) / 128), dim3(128), 0, s, a);
   if (rc.n_pairs > 0) {
+    if (a.sep)
+      hipLaunchKernelGGL(plan_cols_kernel, dim3((unsigned)((3 * (int64_t)rc.n_pairs + 255) / 256)), dim3(256), 0, s,
+                         a);
     const int64_t nthreads = (int64_t)rc.n_pairs * rc.max_h;
     hipLaunchKernelGGL(plan_rows_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(plan_split_kernel, dim3(1024), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(plan_exact_kernel, dim3(512), dim3(256), 0, s, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
@@ -852,6 +952,9 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.lds_mode = 0;
   a.cov_offsets = rc.cov_offsets;
   a.cov_stride = rc.cov_stride;
+  a.nn_kernel = 1;   // set by launch_lds_kernels
+  a.nn_shape = 0;
+  a.nn_xcd = 0;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;

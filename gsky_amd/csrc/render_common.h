@@ -214,6 +214,9 @@ struct RenderArgs {
   int lds_mode;          // render_lds_kernel: kBilinear | kCanvas bits of the call
   const int64_t *cov_offsets;  // canvas mode: per tile element offset into one image (NULL: slots)
   int64_t cov_stride;          // ... and that image's row stride (elements)
+  int nn_kernel;               // 1: render_nn_kernel for NN band work (render_nn.h), 0: render_lds_kernel
+  int nn_shape;                // render_nn_kernel pixels x rows per lane (A/B knob, render_nn.h)
+  int nn_xcd;                  // render_nn_kernel: XCD-aware item order (A/B knob)
 };
 
 // ---------------------------------------------------------------- typed fast path
@@ -254,20 +257,36 @@ __device__ __forceinline__ uint32_t scale_t(const ScaleK &k, typename VOf<T>::ty
   }
 }
 
-// Source coordinates of window pixel i of a LINEAR / POOL(linear) row.
-__device__ __forceinline__ void lin_coords(const RowRec &rr, const Leaf *__restrict__ pool, int i, double &sx,
+// The leaf of window pixel i: the last one starting at or before i (leaf 0
+// starts at 0; starts strictly increase), by binary search -- rows of
+// per-pixel leaves can hold a leaf per window column.
+__device__ __forceinline__ int leaf_of(const Leaf *__restrict__ lv, int nleaf, int i) {
+  int lo = 0, hi = nleaf - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (lv[mid].start <= i) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Source coordinates of window pixel i of a LINEAR / POOL row (simple tiles:
+// leaves linear, or per-pixel exact points with dX = dY = 0, or LEAF_FAILED).
+// false: the exact transform of the pixel failed (window fill).
+__device__ __forceinline__ bool lin_coords(const RowRec &rr, const Leaf *__restrict__ pool, int i, double &sx,
                                            double &sy) {
   double xs0 = rr.v[0], ys0 = rr.v[1], dX = rr.v[2], dY = rr.v[3];
   int start = 0;
+  bool ok = true;
   if (rr.kind == ROW_POOL) {
     const Leaf *lv = pool + rr.pool_off;
-    int k = 0;
-    while (k + 1 < rr.nleaf && lv[k + 1].start <= i) k++;
+    const int k = leaf_of(lv, rr.nleaf, i);
     xs0 = lv[k].xs0; ys0 = lv[k].ys0; dX = lv[k].dX; dY = lv[k].dY; start = lv[k].start;
+    ok = lv[k].kind != LEAF_FAILED;
   }
   const double dist = (double)(i - start);
   sy = ys0 + dY * dist;
   sx = xs0 + dX * dist;
+  return ok;
 }
 
 // NN gather of one window pixel in type T; returns false -> window fill.
@@ -311,6 +330,94 @@ __device__ __forceinline__ bool bil_fetch(const EntryD &e, double sx, double sy,
   return true;
 }
 
+// Full per-pixel path (exact points, descend): only complex tiles and the
+// drop-in window kernel run it.
+__device__ __noinline__ bool descend_coords(const Xform &t, int xoff, double yrow, int n0, const double *v,
+                                            int i, double &sx, double &sy) {
+  int lo = 0, n = n0;
+  double xs[3] = {v[0], v[2], v[4]}, ys[3] = {v[1], v[3], v[5]};
+  auto xpos = [&](int idx) { return idx + 0.5 + xoff; };
+  for (;;) {
+    const int nMiddle = (n - 1) / 2;
+    const double x0 = xpos(lo), xl = xpos(lo + n - 1), xm = xpos(lo + nMiddle);
+    const double dX = (xs[2] - xs[0]) / (xl - x0);
+    const double dY = (ys[2] - ys[0]) / (xl - x0);
+    const double dfError = fabs((xs[0] + dX * (xm - x0)) - xs[1]) + fabs((ys[0] + dY * (xm - x0)) - ys[1]);
+    if (dfError <= kMaxErr) {
+      const double dist = xpos(i) - x0;
+      sy = ys[0] + dY * dist;
+      sx = xs[0] + dX * dist;
+      return true;
+    }
+    const int i0 = lo + (nMiddle - 1) / 2, i1 = lo + nMiddle - 1, i2 = lo + nMiddle + (n - nMiddle - 1) / 2;
+    double mx[3] = {xpos(i0), xpos(i1), xpos(i2)};
+    double my[3] = {yrow, yrow, yrow};
+    const bool base1 = nMiddle <= 5 || x0 == mx[1] || x0 == mx[0];
+    const bool base2 = n - nMiddle <= 5 || xm == xl || xm == mx[2];
+    bool ok = false;
+    if (!base1 && !base2) {
+      ok = xform_point(t, true, mx[0], my[0]);
+      ok = xform_point(t, true, mx[1], my[1]) && ok;
+      ok = xform_point(t, true, mx[2], my[2]) && ok;
+    } else if (!base1) {
+      ok = xform_point(t, true, mx[0], my[0]);
+      ok = xform_point(t, true, mx[1], my[1]) && ok;
+    } else if (!base2) {
+      ok = xform_point(t, true, mx[2], my[2]);
+    }
+    const bool first = (i - lo) < nMiddle;
+    if (!ok || (first && base1) || (!first && base2)) {
+      sx = xpos(i); sy = yrow;
+      return xform_point(t, true, sx, sy);
+    }
+    if (first) {
+      n = nMiddle;
+      xs[1] = mx[0]; ys[1] = my[0]; xs[2] = mx[1]; ys[2] = my[1];
+    } else {
+      xs[0] = xs[1]; ys[0] = ys[1];
+      xs[1] = mx[2]; ys[1] = my[2];
+      lo = lo + nMiddle;
+      n = n - nMiddle;
+    }
+  }
+}
+
+__device__ __noinline__ bool exact_coords(const Xform &t, int xoff, int yoff, int i, int row, double &sx,
+                                          double &sy) {
+  sx = i + 0.5 + xoff;
+  sy = row + 0.5 + yoff;
+  return xform_point(t, true, sx, sy);
+}
+
+// Source coordinates of window pixel (i, row).  GENERAL=false: the row is
+// LINEAR or POOL with linear leaves only (simple tiles).
+template <bool GENERAL>
+__device__ __forceinline__ bool src_coords(const RowRec &rr, const Leaf *pool, const Xform *xf, int xoff,
+                                           int yoff, int w, int i, int row, double &sx, double &sy) {
+  if (rr.kind == ROW_LINEAR) {
+    const double dist = (double)i;
+    sy = rr.v[1] + rr.v[3] * dist;
+    sx = rr.v[0] + rr.v[2] * dist;
+    return true;
+  }
+  if (rr.kind == ROW_POOL) {
+    const Leaf *lv = pool + rr.pool_off;
+    const Leaf &L = lv[leaf_of(lv, rr.nleaf, i)];
+    if (L.kind == LEAF_FAILED) return false;
+    if (!GENERAL || L.kind == LEAF_LINEAR) {
+      const double dist = (double)(i - L.start);
+      sy = L.ys0 + L.dY * dist;
+      sx = L.xs0 + L.dX * dist;
+      return true;
+    }
+  }
+  if (GENERAL) {
+    if (rr.kind == ROW_DESCEND) return descend_coords(*xf, xoff, row + 0.5 + yoff, w, rr.v, i, sx, sy);
+    return exact_coords(*xf, xoff, yoff, i, row, sx, sy);
+  }
+  return false;
+}
+
 // Mask raster value (its own dtype, NN) for data window index (ic, ir).
 template <int RES>
 __device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const RowRec *__restrict__ rows,
@@ -325,14 +432,15 @@ __device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const
   }
   if (my >= m.h) return false;
   double sx, sy;
-  lin_coords(rows[m.row_base + my], pool, mx, sx, sy);
-  int32_t v;
-  bool ok;
-  switch (m.out_dtype) {
-    case GSKYHIP_BYTE: ok = nn_fetch<uint8_t>(m, sx, sy, v); break;
-    case GSKYHIP_SIGNEDBYTE: ok = nn_fetch<int8_t>(m, sx, sy, v); break;
-    case GSKYHIP_INT16: ok = nn_fetch<int16_t>(m, sx, sy, v); break;
-    default: ok = nn_fetch<uint16_t>(m, sx, sy, v); break;
+  int32_t v = 0;
+  bool ok = false;
+  if (lin_coords(rows[m.row_base + my], pool, mx, sx, sy)) {   // false: failed transform -> fill
+    switch (m.out_dtype) {
+      case GSKYHIP_BYTE: ok = nn_fetch<uint8_t>(m, sx, sy, v); break;
+      case GSKYHIP_SIGNEDBYTE: ok = nn_fetch<int8_t>(m, sx, sy, v); break;
+      case GSKYHIP_INT16: ok = nn_fetch<int16_t>(m, sx, sy, v); break;
+      default: ok = nn_fetch<uint16_t>(m, sx, sy, v); break;
+    }
   }
   if (!ok) v = m.fill.i;
   const int slot = mask_slot(m.out_dtype);

@@ -14,95 +14,6 @@
 namespace gsky {
 
 // ---------------------------------------------------------------- sampling
-// Full per-pixel path (exact points, descend): only complex tiles and the
-// drop-in window kernel run it.
-__device__ __noinline__ bool descend_coords(const Xform &t, int xoff, double yrow, int n0, const double *v,
-                                            int i, double &sx, double &sy) {
-  int lo = 0, n = n0;
-  double xs[3] = {v[0], v[2], v[4]}, ys[3] = {v[1], v[3], v[5]};
-  auto xpos = [&](int idx) { return idx + 0.5 + xoff; };
-  for (;;) {
-    const int nMiddle = (n - 1) / 2;
-    const double x0 = xpos(lo), xl = xpos(lo + n - 1), xm = xpos(lo + nMiddle);
-    const double dX = (xs[2] - xs[0]) / (xl - x0);
-    const double dY = (ys[2] - ys[0]) / (xl - x0);
-    const double dfError = fabs((xs[0] + dX * (xm - x0)) - xs[1]) + fabs((ys[0] + dY * (xm - x0)) - ys[1]);
-    if (dfError <= kMaxErr) {
-      const double dist = xpos(i) - x0;
-      sy = ys[0] + dY * dist;
-      sx = xs[0] + dX * dist;
-      return true;
-    }
-    const int i0 = lo + (nMiddle - 1) / 2, i1 = lo + nMiddle - 1, i2 = lo + nMiddle + (n - nMiddle - 1) / 2;
-    double mx[3] = {xpos(i0), xpos(i1), xpos(i2)};
-    double my[3] = {yrow, yrow, yrow};
-    const bool base1 = nMiddle <= 5 || x0 == mx[1] || x0 == mx[0];
-    const bool base2 = n - nMiddle <= 5 || xm == xl || xm == mx[2];
-    bool ok = false;
-    if (!base1 && !base2) {
-      ok = xform_point(t, true, mx[0], my[0]);
-      ok = xform_point(t, true, mx[1], my[1]) && ok;
-      ok = xform_point(t, true, mx[2], my[2]) && ok;
-    } else if (!base1) {
-      ok = xform_point(t, true, mx[0], my[0]);
-      ok = xform_point(t, true, mx[1], my[1]) && ok;
-    } else if (!base2) {
-      ok = xform_point(t, true, mx[2], my[2]);
-    }
-    const bool first = (i - lo) < nMiddle;
-    if (!ok || (first && base1) || (!first && base2)) {
-      sx = xpos(i); sy = yrow;
-      return xform_point(t, true, sx, sy);
-    }
-    if (first) {
-      n = nMiddle;
-      xs[1] = mx[0]; ys[1] = my[0]; xs[2] = mx[1]; ys[2] = my[1];
-    } else {
-      xs[0] = xs[1]; ys[0] = ys[1];
-      xs[1] = mx[2]; ys[1] = my[2];
-      lo = lo + nMiddle;
-      n = n - nMiddle;
-    }
-  }
-}
-
-__device__ __noinline__ bool exact_coords(const Xform &t, int xoff, int yoff, int i, int row, double &sx,
-                                          double &sy) {
-  sx = i + 0.5 + xoff;
-  sy = row + 0.5 + yoff;
-  return xform_point(t, true, sx, sy);
-}
-
-// Source coordinates of window pixel (i, row).  GENERAL=false: the row is
-// LINEAR or POOL with linear leaves only (simple tiles).
-template <bool GENERAL>
-__device__ __forceinline__ bool src_coords(const RowRec &rr, const Leaf *pool, const Xform *xf, int xoff,
-                                           int yoff, int w, int i, int row, double &sx, double &sy) {
-  if (rr.kind == ROW_LINEAR) {
-    const double dist = (double)i;
-    sy = rr.v[1] + rr.v[3] * dist;
-    sx = rr.v[0] + rr.v[2] * dist;
-    return true;
-  }
-  if (rr.kind == ROW_POOL) {
-    const Leaf *lv = pool + rr.pool_off;
-    int k = 0;
-    while (k + 1 < rr.nleaf && lv[k + 1].start <= i) k++;
-    const Leaf &L = lv[k];
-    if (!GENERAL || L.kind == 0) {
-      const double dist = (double)(i - L.start);
-      sy = L.ys0 + L.dY * dist;
-      sx = L.xs0 + L.dX * dist;
-      return true;
-    }
-  }
-  if (GENERAL) {
-    if (rr.kind == ROW_DESCEND) return descend_coords(*xf, xoff, row + 0.5 + yoff, w, rr.v, i, sx, sy);
-    return exact_coords(*xf, xoff, yoff, i, row, sx, sy);
-  }
-  return false;
-}
-
 // Load one source value as a Val of the pair's output dtype (warp.go:339-343).
 __device__ __forceinline__ Val load_val(const void *band, int src_dtype, long idx) {
   Val o;
@@ -401,6 +312,7 @@ __device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD 
         // 4-pixel body whose gathers issue back to back; the source
         // coordinates are the same fp64 expressions as lin_coords().
         double sxq[4], syq[4];
+        bool okq[4] = {true, true, true, true};   // false: failed exact transform (window fill)
         const int ic0 = x0 - e.xoff;
         if (rr.kind == ROW_LINEAR) {
           const double xs0 = rr.v[0], ys0 = rr.v[1], dX = rr.v[2], dY = rr.v[3];
@@ -415,7 +327,7 @@ __device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD 
 #pragma unroll
           for (int q = 0; q < 4; q++) {
             const int ic = ic0 + q;
-            lin_coords(rr, pool, ((unsigned)ic < (unsigned)e.w) ? ic : 0, sxq[q], syq[q]);
+            okq[q] = lin_coords(rr, pool, ((unsigned)ic < (unsigned)e.w) ? ic : 0, sxq[q], syq[q]);
           }
         }
 #pragma unroll
@@ -427,9 +339,9 @@ __device__ __forceinline__ void render_fast_t(const RenderArgs &a, const EntryD 
           if (RES == GSKYHIP_RESAMPLE_BILINEAR) {
             v = fillv;
             V got;
-            if (in && bil_fetch<T>(e, sx, sy, got)) v = got;
+            if (in && okq[q] && bil_fetch<T>(e, sx, sy, got)) v = got;
           } else {
-            v = nn_px<T>(e, sx, sy, in, fillv);
+            v = nn_px<T>(e, sx, sy, in && okq[q], fillv);
           }
           bool take = in && (v != nd);
           if (MASK && e.mask_pair >= 0) take = take && !mask_fast<RES>(ents, rows, pool, a.mask, e, ic, ir);

@@ -5,10 +5,9 @@
 // namespace, RGBA out -- runs as one lean kernel per T (no value-type switch,
 // no SGPR spills).  A 256-thread block owns a band of kBandRows tile rows (all
 // columns); wave w folds rows w, w+4, w+8, w+12, each lane 8 consecutive
-// pixels (two 16-B RGBA stores).  Items are dealt to blocks XCD-aware:
-// blocks b and b+8 share an XCD, so every XCD gets a contiguous run of
-// (tile, band) items and neighbouring bands find their shared source rows in
-// that XCD's L2.
+// pixels (two 16-B RGBA stores).  Items go to blocks in linear order: all
+// XCDs then work on neighbouring tiles and share source rows through the
+// MALL, measured faster than XCD-contiguous runs (profiles/r02g_ab_*.jsonl).
 //
 // STAGE = true additionally stages, per band, in LDS:
 //   * the row records of the band's entries,
@@ -105,6 +104,22 @@ __global__ void scale_lut_kernel(RenderArgs a, const uint32_t *ramp, uint32_t *l
 // bilinear resampling, bit 3 typed canvas output (WCS) instead of RGBA.
 constexpr int kFixed = 1, kLut = 2;   // kBilinear = 4, kCanvas = 8: render_common.h
 
+// One raw buffer load of a T (range-checked: out of range reads 0, no fetch).
+template <typename T>
+__device__ __forceinline__ typename VOf<T>::type buf_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  using V = typename VOf<T>::type;
+  if constexpr (sizeof(T) == 1) {
+    const uint8_t b = __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+    return std::is_signed<T>::value ? (V)(int8_t)b : (V)b;
+  } else if constexpr (sizeof(T) == 2) {
+    const uint16_t h = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+    return std::is_signed<T>::value ? (V)(int16_t)h : (V)h;
+  } else {
+    const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    return __builtin_bit_cast(V, w);
+  }
+}
+
 // GWKBilinearResample4Sample semantics of bil_fetch() (render_common.h), the
 // same fp64 expressions, for the band kernel: false -> window fill.
 template <typename T>
@@ -149,12 +164,14 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
   __shared__ BandEnt s_ent[kBandEnt];
   __shared__ BandRow s_row[STAGE ? kBandEnt : 1][STAGE ? kBandRows : 1];
   __shared__ int32_t s_ext[kBandEnt][4];     // min x, max x, min y, max y of the source indices
+  __shared__ int32_t s_nost[STAGE ? kBandEnt : 1];   // entry has exact rows: not staged
   __shared__ int32_t s_n, s_next;
   __shared__ __attribute__((aligned(16))) uint32_t s_stage[STAGE ? kStageBytes / 4 : 1];
 
-  const int item = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  // item = (tile, 16-row band, 512-column block); column blocks innermost;
+  // XCD-aware order when per_xcd > 0 (A/B: linear order measured faster)
+  const int item = per_xcd > 0 ? (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3) : (int)blockIdx.x;
   if (item >= n_items) return;
-  // item = (tile, 16-row band, 512-column block); column blocks innermost
   const int bands_per_tile = (a.max_h + kBandRows - 1) / kBandRows;
   const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
   const int t = item / (bands_per_tile * col_blocks);
@@ -222,6 +239,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
       }
     }
     if (STAGE && tid < kBandEnt * 4) s_ext[tid >> 2][tid & 3] = (tid & 1) ? -1 : 0x7FFFFFFF;
+    if (STAGE && tid < kBandEnt) s_nost[tid] = 0;
     __syncthreads();
     const int nb = s_n;
     const int next_e0 = s_next;
@@ -241,12 +259,14 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
             o.kind = R.kind; o.nleaf = R.nleaf; o.pool_off = R.pool_off; o._pad = 0;
             s_row[k][rr] = o;
             int mnx = 0x7FFFFFFF, mxx = -1, mny = 0x7FFFFFFF, mxy = -1;
-            const int nl = R.kind == ROW_LINEAR ? 1 : R.nleaf;
+            const int nl = R.kind == ROW_LINEAR ? 1 : R.kind == ROW_POOL ? R.nleaf : 0;
+                      if (nl == 0) s_nost[k] = 1;   // exact / descend row: gather this entry from HBM
             for (int l = 0; l < nl; l++) {
               double xs0 = o.xs0, ys0 = o.ys0, dX = o.dX, dY = o.dY;
               int st = 0, en = b.w - 1;
               if (R.kind != ROW_LINEAR) {
                 const Leaf &L = pool[R.pool_off + l];
+                if (L.kind != 0) s_nost[k] = 1;
                 xs0 = L.xs0; ys0 = L.ys0; dX = L.dX; dY = L.dY; st = L.start;
                 en = (l + 1 < nl) ? pool[R.pool_off + l + 1].start - 1 : b.w - 1;
               }
@@ -270,7 +290,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
           b.soff = -1;
           const int sh = s_ext[k][3] - s_ext[k][2] + 1;
           const bool dw_rows = ((uintptr_t)b.band & 3) == 0 && ((int64_t)b.band_x * sizeof(T)) % 4 == 0;
-          if (s_ext[k][1] < s_ext[k][0] || sh <= 0 || !dw_rows) continue;
+          if (s_nost[k] || s_ext[k][1] < s_ext[k][0] || sh <= 0 || !dw_rows) continue;
           const int dw0 = (int)(((int64_t)s_ext[k][0] * sizeof(T)) >> 2);
           const int dw1 = (int)((((int64_t)s_ext[k][1] + 1) * sizeof(T) + 3) >> 2);
           const int pitch = dw1 - dw0;
@@ -365,7 +385,6 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
         }
         kind = __builtin_amdgcn_readfirstlane(kind);
         if constexpr ((FLAGS & kBilinear) != 0) {   // bilinear: exact fp64 coordinates, 4 taps
-          const Leaf *lv = pool + pool_off;
           const bool hnd = b.has_nodata != 0;
           const double nd64 = b.nodata64;
           const int odt = b.out_dtype;
@@ -374,20 +393,16 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
             const int ic = ic0 + q;
             const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
             double sx, sy;
+            bool okc = true;
             if (kind == ROW_LINEAR) {
               const double dist = (double)ic0 + (double)q;
               sy = ys0 + dY * dist;
               sx = xs0 + dX * dist;
-            } else {
-              const int icc = in ? ic : 0;
-              int l = 0;
-              while (l + 1 < nleaf && lv[l + 1].start <= icc) l++;
-              const double dist = (double)(icc - lv[l].start);
-              sy = lv[l].ys0 + lv[l].dY * dist;
-              sx = lv[l].xs0 + lv[l].dX * dist;
+            } else {   // POOL: linear leaves, per-pixel exact points, failed pixels
+              okc = lin_coords(rows[(int64_t)pair * a.max_h + ir], pool, in ? ic : 0, sx, sy);
             }
             V v = fillv, got;
-            if (in && bil_sample<T>(bandp, bx, by, hnd, nd64, odt, sx, sy, got)) v = got;
+            if (in && okc && bil_sample<T>(bandp, bx, by, hnd, nd64, odt, sx, sy, got)) v = got;
             bool take = in && (v != nd);
             if (MASK && b.mask_pair >= 0) {
               if (take) take = !mask_fast<GSKYHIP_RESAMPLE_BILINEAR>(ents, rows, pool, a.mask, ents[pair], ic, ir);
@@ -399,7 +414,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
         }
         // source index of each of the lane's pixels: (ux, uy) and validity
         uint32_t ux[kLanePx], uy[kLanePx];
-        uint32_t okm = 0;
+        bool ok[kLanePx];
         bool exact = kind != ROW_LINEAR || !(FLAGS & kFixed);
         if (!exact) {
           // 32.32 fixed point: fx(i) = (xs0 + 1e-10 + dX * i) * 2^32, stepped per
@@ -426,7 +441,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
               const int ic = ic0 + q;
               const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
               bad = bad || (in && (lx + G < 2u * G || ly + G < 2u * G));
-              if (in && ux[q] < (uint32_t)bx && uy[q] < (uint32_t)by) okm |= 1u << q;
+              ok[q] = in && ux[q] < (uint32_t)bx && uy[q] < (uint32_t)by;
               fx += Dx;
               fy += Dy;
             }
@@ -434,50 +449,56 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
           }
         }
         if (exact) {   // the reference's fp64 expressions (lin_coords() / nn_px())
-          okm = 0;
-          const Leaf *lv = pool + pool_off;
 #pragma unroll
           for (int q = 0; q < kLanePx; q++) {
             const int ic = ic0 + q;
             const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
             double sx, sy;
+            bool okc = true;
             if (kind == ROW_LINEAR) {
               const double dist = (double)ic0 + (double)q;
               sy = ys0 + dY * dist;
               sx = xs0 + dX * dist;
-            } else {
-              const int icc = in ? ic : 0;
-              int l = 0;
-              while (l + 1 < nleaf && lv[l + 1].start <= icc) l++;
-              const double dist = (double)(icc - lv[l].start);
-              sy = lv[l].ys0 + lv[l].dY * dist;
-              sx = lv[l].xs0 + lv[l].dX * dist;
+            } else {   // POOL: linear leaves, per-pixel exact points, failed pixels
+              okc = lin_coords(rows[(int64_t)pair * a.max_h + ir], pool, in ? ic : 0, sx, sy);
             }
             const int ix = __double2int_rz(sx + 1.0e-10), iy = __double2int_rz(sy + 1.0e-10);
             ux[q] = (uint32_t)ix;
             uy[q] = (uint32_t)iy;
-            if (in && (sx >= 0.0) && (sy >= 0.0) && ix < bx && iy < by) okm |= 1u << q;
+            ok[q] = in && okc && (sx >= 0.0) && (sy >= 0.0) && ix < bx && iy < by;
           }
         }
-        const bool idx32 = (int64_t)bx * by < 2147483648LL;
-        const uint8_t *sbase = (const uint8_t *)s_stage + (soff >= 0 ? soff : 0);
-        const int sx0 = b.sx0, sy0 = b.sy0, pitch_b = b.pitch_dw * 4;
+        // gather, branch-free: a raw buffer load per pixel with the range check
+        // in hardware; an invalid pixel gets an out-of-range offset (no fetch)
+        V vv[kLanePx];
+        const int64_t nbytes = (int64_t)bx * by * (int64_t)sizeof(T);
+        if (STAGE && soff >= 0) {
+          const uint8_t *sbase = (const uint8_t *)s_stage + soff;
+          const int sx0 = b.sx0, sy0 = b.sy0, pitch_b = b.pitch_dw * 4;
+#pragma unroll
+          for (int q = 0; q < kLanePx; q++) {
+            const int lofs = ok[q] ? ((int)uy[q] - sy0) * pitch_b + ((int)ux[q] - sx0) * (int)sizeof(T) : 0;
+            vv[q] = (V)(*(const T *)(sbase + lofs));
+          }
+        } else if (nbytes < 2147483648LL && bx < (1 << 24) && by < (1 << 24)) {
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc((void *)bandp, (short)0, (int)nbytes, 0x00020000);
+#pragma unroll
+          for (int q = 0; q < kLanePx; q++) {
+            const uint32_t off = ok[q] ? (__umul24(uy[q], (uint32_t)bx) + ux[q]) * (uint32_t)sizeof(T) : 0x80000000u;
+            vv[q] = buf_load<T>(rs, off);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < kLanePx; q++) {
+            const int64_t idx = ok[q] ? (int64_t)uy[q] * bx + ux[q] : 0;
+            vv[q] = (V)((const GPTR(T))bandp)[idx];
+          }
+        }
 #pragma unroll
         for (int q = 0; q < kLanePx; q++) {
           const int ic = ic0 + q;
-          const bool ok = (okm >> q) & 1u;
-          V v;
-          if (STAGE && soff >= 0) {
-            const int lofs = ok ? ((int)uy[q] - sy0) * pitch_b + ((int)ux[q] - sx0) * (int)sizeof(T) : 0;
-            v = (V)(*(const T *)(sbase + lofs));
-          } else if (idx32) {
-            const uint32_t idx = ok ? __umul24(uy[q], (uint32_t)bx) + ux[q] : 0u;
-            v = (V)((const GPTR(T))bandp)[idx];
-          } else {
-            const int64_t idx = ok ? (int64_t)uy[q] * bx + ux[q] : 0;
-            v = (V)((const GPTR(T))bandp)[idx];
-          }
-          v = ok ? v : fillv;
+          const V v = ok[q] ? vv[q] : fillv;
           const bool in = (unsigned)ic < (unsigned)ew && x0 + q < W;
           bool take = in && (v != nd);
           if (MASK && b.mask_pair >= 0) {
@@ -550,8 +571,8 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
 
 template <typename T>
 void launch_lds_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
-  const int per_xcd = (n_items + 7) / 8;
-  const dim3 grid((unsigned)per_xcd * 8);
+  const int per_xcd = a.nn_xcd ? (n_items + 7) / 8 : 0;
+  const dim3 grid(a.nn_xcd ? (unsigned)per_xcd * 8 : (unsigned)n_items);
 #define GSKY_LDS_LAUNCH(M, S, F)                                                                                   \
   hipLaunchKernelGGL((render_lds_kernel<T, M, S, F>), grid, dim3(256), 0, s, a, a.entries, a.order, a.rows, a.pool, \
                      a.tplans, a.tiles, n_items, per_xcd)

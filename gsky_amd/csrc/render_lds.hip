@@ -1,4 +1,4 @@
-// render_lds.hip -- dispatch of the typed LDS-staged band kernels.
+// render_lds.hip -- dispatch of the typed band kernels (render_nn.h, render_lds.h).
 #include <cstdlib>
 
 #include "render_lds.h"
@@ -14,6 +14,14 @@ void launch_lds_kernels(const RenderArgs &a0, int vt, bool mask, int n_items, hi
   a.lds_stage = st ? atoi(st) : 0;
   const char *fl = getenv("GSKYHIP_LDS_FLAGS");
   a.lds_flags = fl ? atoi(fl) : 0;
+  // NN work goes to render_nn_kernel unless GSKYHIP_NN_KERNEL=0 (A/B);
+  // GSKYHIP_NN_SHAPE picks its pixels x rows per lane (render_nn.h)
+  const char *nk = getenv("GSKYHIP_NN_KERNEL");
+  a.nn_kernel = nk ? atoi(nk) : 1;
+  const char *ns = getenv("GSKYHIP_NN_SHAPE");
+  a.nn_shape = ns ? atoi(ns) : 0;
+  const char *nx = getenv("GSKYHIP_NN_XCD");
+  a.nn_xcd = nx ? atoi(nx) : 0;   // linear item order by default (A/B, profiles/r02g_ab_*.jsonl)
   switch (vt) {
     case GSKYHIP_INT16: launch_lds_i16(a, mask, n_items, s); break;
     case GSKYHIP_UINT16: launch_lds_u16(a, mask, n_items, s); break;

@@ -1,8 +1,8 @@
-// render_lds_f32.hip -- render_lds_kernel<float> (one TU per value type).
-#include "render_lds.h"
+// render_lds_f32.hip -- band kernels of float (one TU per value type).
+#include "render_nn.h"
 
 namespace gsky {
 void launch_lds_f32(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
-  launch_lds_t<float>(a, mask, n_items, s);
+  launch_band_t<float>(a, mask, n_items, s);
 }
 }  // namespace gsky

@@ -247,6 +247,20 @@ class TileBatch:
         return lib().gskyhip_render_status(C.c_void_p(self._ws.data_ptr()), self.n_tiles, self.n_pairs,
                                            self.max_h, stream)
 
+    def tile_info(self):
+        """Per tile (status, complex, value type, merged entries) of the last
+        plan (gskyhip_render_tile_info), an int32 numpy array (n_tiles, 4);
+        also sets self.plan_counters (leaf pool, split rows, complex tiles)."""
+        import numpy as np
+        info = np.zeros((max(1, self.n_tiles), 4), dtype=np.int32)
+        cnt = np.zeros(3, dtype=np.int32)
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().gskyhip_render_tile_info(C.c_void_p(self._ws.data_ptr()), self.n_tiles, self.n_pairs, self.max_h,
+                                             info.ctypes.data_as(C.c_void_p), cnt.ctypes.data_as(C.c_void_p),
+                                             stream), "render_tile_info")
+        self.plan_counters = {"pool_leaves": int(cnt[0]), "split_rows": int(cnt[1]), "complex_tiles": int(cnt[2])}
+        return info[: self.n_tiles]
+
     def canvas_view(self, cv: torch.Tensor, tile: int, k: int, type_name: str) -> torch.Tensor:
         nb = {"Byte": 1, "SignedByte": 1, "Int16": 2, "UInt16": 2, "Float32": 4}[type_name]
         return cv[tile, k, : self.max_w * self.max_h * nb].view(TORCH_OF[type_name]).reshape(self.max_h,

@@ -359,6 +359,14 @@ int gskyhip_device_count(void);
  * synchronously): 0 OK or the first error code; n_tiles of the last call. */
 int gskyhip_render_status(void *workspace, int n_tiles, int n_pairs, int max_tile_height, void *stream);
 
+/* Diagnostics of the last plan in `workspace` (synchronous): per tile
+ * {status, complex (1: some row needs exact per-pixel transforms or the value
+ * types are mixed -> general kernel), common value type (GSKYHIP_* or 0),
+ * merged entries}; counters_out (3 ints, may be NULL): leaf-pool entries used,
+ * rows split by the approximation recursion, complex tiles.  No reference counterpart (an observability hook). */
+int gskyhip_render_tile_info(void *workspace, int n_tiles, int n_pairs, int max_tile_height, int32_t *info_out,
+                             int32_t *counters_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B timing of the C2 render phase (phase-2 kernels only, HIP events on the
-launch stream) for the kernel variants: typed band kernel with LDS-staged
-source windows, typed band kernel gathering from HBM, and the generic kernel.
+launch stream) for the kernel variants: the NN band kernel (render_nn.h) in
+its lane shapes, the first band kernel (render_lds.h: LDS-staged source
+windows, HBM gathers, fixed point, LUT) and the generic kernel.
 One JSON line per variant.  Used to pick defaults; bench.py is the contract."""
 import argparse
 import json
@@ -47,14 +48,21 @@ def main():
     sp = gsky_amd.ScaleParams(*cfg.scale)
     pal = gsky_amd.Palette(cfg.palette, True) if cfg.palette else None
     ref = None
-    variants = [("typed_stage", True, "1", "0"), ("typed_direct", True, "0", "0"),
-                ("typed_direct_fixed", True, "0", "1"), ("typed_direct_lut", True, "0", "2"),
-                ("typed_direct_fixed_lut", True, "0", "3"), ("generic", False, "1", "0")]
-    for name, typed, stage, flags in variants:
+    # (name, typed, LDS_STAGE, LDS_FLAGS, NN_KERNEL, NN_SHAPE[, NN_XCD])
+    variants = [("nn_4x4", True, "0", "0", "1", "0"), ("nn_8x1", True, "0", "0", "1", "1"),
+                ("nn_8x2", True, "0", "0", "1", "2"), ("nn_4x2", True, "0", "0", "1", "3"),
+                ("nn_4x4_fixed", True, "0", "1", "1", "0"), ("nn_4x4_xcd", True, "0", "0", "1", "0", "1"),
+                ("typed_stage", True, "1", "0", "0", "0"), ("typed_direct", True, "0", "0", "0", "0"),
+                ("typed_direct_fixed", True, "0", "1", "0", "0"), ("typed_direct_lut", True, "0", "2", "0", "0"),
+                ("generic", False, "1", "0", "0", "0")]
+    for name, typed, stage, flags, nnk, shape, *xcd in variants:
         if args.variant and name != args.variant:
             continue
         os.environ["GSKYHIP_LDS_STAGE"] = stage
         os.environ["GSKYHIP_LDS_FLAGS"] = flags
+        os.environ["GSKYHIP_NN_KERNEL"] = nnk
+        os.environ["GSKYHIP_NN_SHAPE"] = shape
+        os.environ["GSKYHIP_NN_XCD"] = xcd[0] if xcd else "0"
         b.typed = typed
         med, mn = time_render(b, sp, pal, args.reps)
         out = b.render(sp, pal).clone()

@@ -40,6 +40,20 @@ def main():
         tb.render_coverage(ScaleParams(*cfg.scale), band, offs, resample=cfg.resample)
         torch.cuda.synchronize()
         outs[typed] = band
+    for typed in (True, False):   # render-only (phase 2) time of each path
+        tb.typed = typed
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        tb.render_coverage(ScaleParams(*cfg.scale), outs[typed], offs, resample=cfg.resample, phase=2)
+        ev[0].record()
+        for _ in range(5):
+            tb.render_coverage(ScaleParams(*cfg.scale), outs[typed], offs, resample=cfg.resample, phase=2)
+        ev[1].record()
+        torch.cuda.synchronize()
+        print(json.dumps({"typed": typed, "render_ms": round(ev[0].elapsed_time(ev[1]) / 5, 4)}))
+    info = tb.tile_info()
+    print(json.dumps({"tiles": int(len(info)), "complex": int(info[:, 1].sum()),
+                      "vt": sorted(set(int(v) for v in info[:, 2])), "counters": tb.plan_counters,
+                      "n_pairs": int(sum(len(p) for p in pairs))}))
     a, b = outs[True], outs[False]
     same = (a.view(torch.int32) == b.view(torch.int32))
     print(json.dumps({"pixels": a.numel(), "differ": int((~same).sum().item()),
