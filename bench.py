@@ -44,7 +44,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import gsky_amd  # noqa: E402
-from gsky_amd import GranuleSet, Mask, Palette, ScaleParams, TileBatch, synth  # noqa: E402
+from gsky_amd import GranuleSet, Mask, Palette, ScaleParams, TileBatch, partition, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "reprojected+merged output Mpix/s (whole node) at 1/2/4/8 MI355X; p50 tile ms"
@@ -108,20 +108,8 @@ def event_ms(fn, reps: int = 10) -> float:
     return float(np.mean(ts))
 
 
-def block_part(n: int, rank: int, world: int):
-    base, extra = divmod(n, world)
-    s = rank * base + min(rank, extra)
-    return list(range(s, s + base + (1 if rank < extra else 0)))
-
-
-def sub_config(cfg, ids):
-    """Tiles `ids` of cfg with only the granules they touch (indices remapped)."""
-    used = sorted({g for i in ids for g in cfg.pairs[i]})
-    remap = {g: k for k, g in enumerate(used)}
-    sub = synth.SynthConfig(cfg.name, [cfg.granules[g] for g in used], cfg.dst_srs, [cfg.tiles[i] for i in ids],
-                            [[remap[g] for g in cfg.pairs[i]] for i in ids], cfg.namespaces, cfg.scale, cfg.palette,
-                            cfg.resample, cfg.mask, cfg.bbox, cfg.out_w, cfg.out_h)
-    return sub
+block_part = partition.tile_blocks     # contiguous tile blocks (gsky_amd/partition.py)
+sub_config = partition.sub_config      # a rank uploads only the granules its tiles touch
 
 
 def build_batch(cfg, device):
@@ -360,8 +348,7 @@ def run_c4(ctx: Ctx, args):
     n_bands = 365
     st = c4_stack(n_bands, 2048, ctx.device)
     inside = [int((m == 255).sum()) for m in geo.masks]
-    order = sorted(range(len(geo.masks)), key=lambda p: -inside[p])
-    mine = order[ctx.rank::ctx.world]             # largest-first, round-robin over ranks
+    mine = partition.drill_assignment(inside, ctx.rank, ctx.world)   # largest-first, round-robin
     mb = drill.pack_masks([geo.windows[p] for p in mine], [geo.masks[p] for p in mine], ctx.device)
     res = {}
     for name, mode in (("reference_order", drill.REFERENCE_ORDER), ("wave_split", drill.WAVE_SPLIT)):

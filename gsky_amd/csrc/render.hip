@@ -54,10 +54,23 @@ struct PlanArgs {
 };
 
 // ---------------------------------------------------------------- pair ownership
-__global__ void pair_tile_kernel(const gskyhip_tile *tiles, int n_tiles, int32_t *pair_tile) {
-  int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_tiles) return;
-  for (int p = tiles[t].pair_begin; p < tiles[t].pair_end; p++) pair_tile[p] = t;
+// One thread per pair: its tile is the last one whose CSR range starts at or
+// before it (tiles' pair ranges are consecutive and ascending).
+__global__ void pair_tile_kernel(const gskyhip_tile *tiles, int n_tiles, int n_pairs, int32_t *pair_tile) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  int lo = 0, hi = n_tiles - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tiles[mid].pair_begin <= p) lo = mid; else hi = mid - 1;
+  }
+  while (lo > 0 && tiles[lo].pair_end <= p) lo--;   // empty tiles sharing a begin
+  if (!(p >= tiles[lo].pair_begin && p < tiles[lo].pair_end)) {   // not CSR-ordered: scan
+    lo = -1;
+    for (int t = 0; t < n_tiles; t++)
+      if (p >= tiles[t].pair_begin && p < tiles[t].pair_end) lo = t;
+  }
+  pair_tile[p] = lo;   // -1: no tile references the pair
 }
 
 // ---------------------------------------------------------------- wave helpers
@@ -108,6 +121,15 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
   __shared__ int sok[kGrid];
 
   const int t_idx = a.pair_tile[p];
+  if (t_idx < 0) {   // unreferenced pair: an empty plan nothing reads
+    if (lane == 0) {
+      PairPlan z = {};
+      z.tile = -1;
+      z.mask_pair = -1;
+      a.pairs[p] = z;
+    }
+    return;
+  }
   const gskyhip_tile &tile = a.tiles[t_idx];
   const int gi = a.pair_granule[p];
   const gskyhip_granule &g = a.granules[gi];
@@ -282,10 +304,34 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
 }
 
 // ---------------------------------------------------------------- merge order
-// One thread per tile.  Mirrors RasterMerger.Run for the tile's batch.
-__global__ void plan_tiles_kernel(PlanArgs a) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.n_tiles) return;
+// Entry descriptor of pair p (render kernels) and its value-type vote: the
+// typed band kernels need one value type, no GDALCopyWords promotion and a
+// band addressable with 32-bit offsets.  Returns -1 (not merged), 0 (no) or
+// the value type.
+__device__ __forceinline__ int write_entry(const PlanArgs &a, int p) {
+  const PairPlan &pp = a.pairs[p];
+  EntryD d;
+  d.band = pp.band;
+  d.band_x = pp.band_x; d.band_y = pp.band_y;
+  d.xoff = pp.xoff; d.yoff = pp.yoff; d.w = pp.w; d.h = pp.h;
+  d.ns = pp.ns; d.fill_mode = pp.fill_mode; d.mask_pair = pp.mask_pair; d.src_dtype = pp.src_dtype;
+  d.out_dtype = pp.out_dtype; d.has_nodata = pp.has_nodata;
+  d.nd = go_conv_to(pp.nodata, pp.out_dtype);
+  d.fill = pp.fill;
+  d.nodata64 = pp.nodata;
+  d.row_base = (int64_t)p * a.max_h;
+  a.entries[p] = d;
+  if (!pp.in_stack) return -1;
+  const bool same = pp.src_dtype == pp.out_dtype ||
+                    (pp.src_dtype == GSKYHIP_BYTE && pp.out_dtype == GSKYHIP_SIGNEDBYTE);
+  const bool small = pp.band_x < (1 << 24) && pp.band_y < (1 << 24) &&
+                     (int64_t)pp.band_x * pp.band_y * type_size(pp.src_dtype) < 2147483648LL;
+  return (same && small) ? pp.out_dtype : 0;
+}
+
+// Mirrors RasterMerger.Run for the tile's batch, one thread (tiles with more
+// than kWavePairs pairs; plan_tiles_kernel below is the wave-parallel form).
+__device__ void plan_tile_serial(const PlanArgs &a, int t) {
   const gskyhip_tile &tile = a.tiles[t];
   TilePlan tp;
   tp.n_entries = 0;
@@ -345,30 +391,148 @@ __global__ void plan_tiles_kernel(PlanArgs a) {
   // render descriptors of every pair of the tile (mask pairs included)
   int vt = -1;
   for (int p = b; p < e; p++) {
-    const PairPlan &pp = a.pairs[p];
-    EntryD d;
-    d.band = pp.band;
-    d.band_x = pp.band_x; d.band_y = pp.band_y;
-    d.xoff = pp.xoff; d.yoff = pp.yoff; d.w = pp.w; d.h = pp.h;
-    d.ns = pp.ns; d.fill_mode = pp.fill_mode; d.mask_pair = pp.mask_pair; d.src_dtype = pp.src_dtype;
-    d.out_dtype = pp.out_dtype; d.has_nodata = pp.has_nodata;
-    d.nd = go_conv_to(pp.nodata, pp.out_dtype);
-    d.fill = pp.fill;
-    d.nodata64 = pp.nodata;
-    d.row_base = (int64_t)p * a.max_h;
-    a.entries[p] = d;
-    if (!pp.in_stack) continue;
-    // the typed fast path needs one value type and no GDALCopyWords promotion
-    const bool same = pp.src_dtype == pp.out_dtype ||
-                      (pp.src_dtype == GSKYHIP_BYTE && pp.out_dtype == GSKYHIP_SIGNEDBYTE);
-    // ... and a band the band kernels address with 32-bit offsets (render_nn.h)
-    const bool small = pp.band_x < (1 << 24) && pp.band_y < (1 << 24) &&
-                       (int64_t)pp.band_x * pp.band_y * type_size(pp.src_dtype) < 2147483648LL;
-    if (!same || !small) vt = 0;
-    else if (vt < 0) vt = pp.out_dtype;
-    else if (vt != pp.out_dtype) vt = 0;
+    const int v = write_entry(a, p);
+    if (v == 0) vt = 0;
+    else if (v > 0 && vt < 0) vt = v;
+    else if (v > 0 && vt != v) vt = 0;
   }
   tp.vt = vt < 0 ? 0 : vt;
+  if (n > 0 && tp.vt == 0) {
+    tp.complex = 1;
+    const int k = atomicAdd(&a.counters[2], 1);
+    a.complex_list[k] = t;
+  }
+  a.tplans[t] = tp;
+}
+
+
+constexpr int kWavePairs = 256;   // pairs per tile the wave-parallel merge planner holds in LDS
+
+// One wavefront per tile: RasterMerger.Run's merge order (tile_merger.go:281-312:
+// stable sort by geoStamp descending), maskMap links (478-484), canvas
+// creation and the fill / overwrite mode of MergeMaskedRaster (47), as data-
+// parallel scans over the tile's pairs instead of the serial walk:
+//   rank(p)   = #{q: stamp_q > stamp_p} + #{q < p: stamp_q == stamp_p}
+//   fill(k)   = ts_k < max(0, max{ts_j: j before k in the order, same ns})
+//   status    = the last error in merge order (the serial walk's last write).
+__global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (t >= a.n_tiles) return;
+  const gskyhip_tile &tile = a.tiles[t];
+  const int b = tile.pair_begin, e = tile.pair_end, np = e - b;
+  const bool bad_size = tile.width <= 0 || tile.height <= 0 || tile.width > a.max_w || tile.height > a.max_h;
+  if (np > kWavePairs || bad_size) {
+    if (lane == 0) plan_tile_serial(a, t);
+    return;
+  }
+  __shared__ double s_stamp[kWavePairs], s_ts[kWavePairs];
+  __shared__ int32_t s_info[kWavePairs];   // in_stack | is_mask << 1 | (ns + 1) << 2 | out_dtype << 8
+  __shared__ int32_t s_rank[kWavePairs];   // merge position of an in-stack pair, -1 otherwise
+  for (int i = lane; i < np; i += 64) {
+    const PairPlan &pp = a.pairs[b + i];
+    s_stamp[i] = pp.stamp;
+    s_ts[i] = pp.ts;
+    s_info[i] = (pp.in_stack ? 1 : 0) | (pp.is_mask ? 2 : 0) | ((pp.ns + 1) << 2) | (pp.out_dtype << 8);
+  }
+  __syncthreads();
+  // merge order
+  for (int i = lane; i < np; i += 64) {
+    int rk = -1;
+    if (s_info[i] & 1) {
+      const double s = s_stamp[i];
+      rk = 0;
+      for (int q = 0; q < np; q++)
+        if ((s_info[q] & 1) && (s_stamp[q] > s || (q < i && s_stamp[q] == s))) rk++;
+      a.order[b + rk] = b + i;
+    }
+    s_rank[i] = rk;
+  }
+  __syncthreads();
+  // per merged entry: maskMap link, fill mode, first-of-namespace, error
+  int n_local = 0;
+  for (int i = lane; i < np; i += 64) n_local += (s_info[i] & 1);
+  for (int o = 32; o > 0; o >>= 1) n_local += __shfl_xor(n_local, o, 64);
+  const int n = n_local;
+  int err_k = -1, err_code = 0;                  // this lane's last error (largest merge position)
+  int first_k[4] = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
+  for (int i = lane; i < np; i += 64) {
+    const int k = s_rank[i];
+    if (k < 0) continue;
+    const int p = b + i;
+    PairPlan &pp = a.pairs[p];
+    const double s = s_stamp[i];
+    int mp = -1;
+    for (int q = 0; q < np; q++)
+      if ((s_info[q] & 2) && s_stamp[q] == s) mp = b + q;
+    pp.mask_pair = mp;
+    int st = 0;
+    if (mp >= 0) {
+      const PairPlan &mq = a.pairs[mp];
+      const int mdt = mq.out_dtype;
+      if (!(mdt == GSKYHIP_SIGNEDBYTE || mdt == GSKYHIP_BYTE || mdt == GSKYHIP_INT16 || mdt == GSKYHIP_UINT16))
+        st = GSKYHIP_E_MASK;
+      else if ((long)pp.w * pp.h > (long)mq.w * mq.h)
+        st = GSKYHIP_E_RANGE;
+    }
+    const int ns = ((s_info[i] >> 2) & 63) - 1;
+    int fill = 0;
+    if (ns < 0 || ns >= 4) {
+      st = GSKYHIP_E_RANGE;
+    } else {
+      first_k[ns] = min(first_k[ns], k);
+      // canvas timestamp before k: running max of the namespace's earlier entries, from 0
+      double cts = 0.0;
+      int first_q = -1, first_qk = 0x7FFFFFFF;
+      for (int q = 0; q < np; q++) {
+        const int kq = s_rank[q];
+        if (kq < 0 || ((s_info[q] >> 2) & 63) - 1 != ns) continue;
+        if (kq < k) cts = fmax(cts, s_ts[q]);
+        if (kq < first_qk) { first_qk = kq; first_q = q; }
+      }
+      fill = s_ts[i] < cts ? 1 : 0;
+      if (first_qk < k && (s_info[first_q] >> 8) != (s_info[i] >> 8)) st = GSKYHIP_E_TYPE;
+    }
+    pp.fill_mode = fill;
+    if (st && k > err_k) { err_k = k; err_code = st; }
+  }
+  // wave reductions: last error, first entry of each namespace
+  for (int o = 32; o > 0; o >>= 1) {
+    const int ok_ = __shfl_xor(err_k, o, 64), oc = __shfl_xor(err_code, o, 64);
+    if (ok_ > err_k) { err_k = ok_; err_code = oc; }
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) first_k[s2] = min(first_k[s2], __shfl_xor(first_k[s2], o, 64));
+  }
+  __syncthreads();   // fill_mode / mask_pair of every pair written (same workgroup)
+  // render descriptors of every pair (mask pairs included) + value-type vote
+  int vmin = 0x7FFFFFFF, vmax = -1;
+  bool vzero = false;
+  for (int i = lane; i < np; i += 64) {
+    const int v = write_entry(a, b + i);
+    if (v == 0) vzero = true;
+    if (v > 0) { vmin = min(vmin, v); vmax = max(vmax, v); }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    vmin = min(vmin, __shfl_xor(vmin, o, 64));
+    vmax = max(vmax, __shfl_xor(vmax, o, 64));
+  }
+  vzero = __ballot(vzero) != 0ull;
+  if (lane != 0) return;
+  TilePlan tp;
+  tp.n_entries = n;
+  tp.status = err_code;
+  tp.complex = 0;
+  for (int s2 = 0; s2 < 4; s2++) {
+    tp.created[s2] = first_k[s2] != 0x7FFFFFFF ? 1 : 0;
+    tp.dtype[s2] = 0;
+    tp.nodata[s2] = 0;
+    if (tp.created[s2]) {
+      const PairPlan &pf = a.pairs[a.order[b + first_k[s2]]];
+      tp.dtype[s2] = pf.out_dtype;
+      tp.nodata[s2] = pf.nodata;
+    }
+  }
+  tp.vt = (vzero || vmax < 0 || vmin != vmax) ? 0 : vmax;
   if (n > 0 && tp.vt == 0) {
     tp.complex = 1;
     const int k = atomicAdd(&a.counters[2], 1);
@@ -883,10 +1047,11 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   a.sep = sep ? atoi(sep) : 1;
   hipStream_t s = rc.stream;
   if (hipMemsetAsync(cv.counters, 0, 256, s) != hipSuccess) return GSKYHIP_E_HIP;
-  hipLaunchKernelGGL(pair_tile_kernel, dim3((rc.n_tiles + 255) / 256), dim3(256), 0, s, rc.tiles, rc.n_tiles,
-                     cv.pair_tile);
+  if (rc.n_pairs > 0)
+    hipLaunchKernelGGL(pair_tile_kernel, dim3((rc.n_pairs + 255) / 256), dim3(256), 0, s, rc.tiles, rc.n_tiles,
+                       rc.n_pairs, cv.pair_tile);
   if (rc.n_pairs > 0) hipLaunchKernelGGL(plan_pairs_kernel, dim3(rc.n_pairs), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(plan_tiles_kernel, dim3((rc.n_tiles + 127) / 128), dim3(128), 0, s, a);
+  hipLaunchKernelGGL(plan_tiles_kernel, dim3(rc.n_tiles), dim3(64), 0, s, a);
   if (rc.n_pairs > 0) {
     if (a.sep)
       hipLaunchKernelGGL(plan_cols_kernel, dim3((unsigned)((3 * (int64_t)rc.n_pairs + 255) / 256)), dim3(256), 0, s,
@@ -953,8 +1118,9 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.cov_offsets = rc.cov_offsets;
   a.cov_stride = rc.cov_stride;
   a.nn_kernel = 1;   // set by launch_lds_kernels
-  a.nn_shape = 0;
+  a.nn_shape = 3;
   a.nn_xcd = 0;
+  a.nn_probe = 0;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;

@@ -217,6 +217,7 @@ struct RenderArgs {
   int nn_kernel;               // 1: render_nn_kernel for NN band work (render_nn.h), 0: render_lds_kernel
   int nn_shape;                // render_nn_kernel pixels x rows per lane (A/B knob, render_nn.h)
   int nn_xcd;                  // render_nn_kernel: XCD-aware item order (A/B knob)
+  int nn_probe;                // timing-only probes of render_nn_kernel (0: off; see render_nn.h)
 };
 
 // ---------------------------------------------------------------- typed fast path

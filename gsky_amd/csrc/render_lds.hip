@@ -19,7 +19,9 @@ void launch_lds_kernels(const RenderArgs &a0, int vt, bool mask, int n_items, hi
   const char *nk = getenv("GSKYHIP_NN_KERNEL");
   a.nn_kernel = nk ? atoi(nk) : 1;
   const char *ns = getenv("GSKYHIP_NN_SHAPE");
-  a.nn_shape = ns ? atoi(ns) : 0;
+  a.nn_shape = ns ? atoi(ns) : 3;
+  const char *np = getenv("GSKYHIP_NN_PROBE");   // timing-only probes (wrong images): never set in production
+  a.nn_probe = np ? atoi(np) : 0;
   const char *nx = getenv("GSKYHIP_NN_XCD");
   a.nn_xcd = nx ? atoi(nx) : 0;   // linear item order by default (A/B, profiles/r02g_ab_*.jsonl)
   switch (vt) {

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
   const bool created = tp.created[ns_out] != 0;
   const V cnod = as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]));
   const int32_t *ord = order + tile.pair_begin;
-  const int n_entries = tp.n_entries;
+  const int n_entries = a.nn_probe == 2 ? 0 : tp.n_entries;   // timing probe 2: stores only
   const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
   const bool has_ramp = a.ramp != nullptr;
   uint8_t *rgba_tile = a.rgba + (int64_t)t * a.max_h * a.max_w * 4;
@@ -176,8 +176,10 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
         const int64_t row_base = e.row_base;
         const int ic0 = x0 - exoff;
         const int lim = max(0, min(ew, W - exoff));   // pixel in the entry and the tile: (unsigned)ic < lim
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
+        // timing probe 1 (A/B only): a zero-record descriptor, gathers read 0 without traffic
+        const int nrec = a.nn_probe == 1 ? 0 : (int)((int64_t)bx * by * (int64_t)sizeof(T));
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)uniform_ptr(e.band), (short)0, nrec, 0x00020000);
         uint32_t idx[R][LPX];
         V vv[R][LPX];
         // coordinates and gathers of all R rows first: R x LPX loads in flight
@@ -216,6 +218,7 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
       for (int i = 0; i < R; i++) {
         const int r = rb + i;
         if (r >= H || x0 >= W) continue;
+        if (a.nn_probe == 3) continue;   // timing probe 3: no stores
         if constexpr ((FLAGS & kCanvas) != 0) {
           const int64_t eo = a.cov_offsets ? a.cov_offsets[t] + (int64_t)r * a.cov_stride + x0
                                            : (int64_t)r * a.max_w + x0;
@@ -273,7 +276,8 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
 }
 
 // NN band kernel launch for value type T: lanes shape (LPX pixels x R rows)
-// from RenderArgs.nn_shape (0: 4 x 4, 1: 8 x 1, 2: 8 x 2, 3: 4 x 2), 32.32
+// from RenderArgs.nn_shape (0: 4 x 4, 1: 8 x 1, 2: 8 x 2, 3: 4 x 2, the
+// default: fastest on C2 and C5, profiles/r02h_ab_*.jsonl), 32.32
 // fixed point when lds_flags has kFixed, XCD-aware order when nn_xcd
 // (A/B knobs GSKYHIP_NN_SHAPE, GSKYHIP_LDS_FLAGS, GSKYHIP_NN_XCD).
 template <typename T>
@@ -286,7 +290,7 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
   const bool canvas = (a.lds_mode & kCanvas) != 0;
   const bool fixed = (a.lds_flags & kFixed) != 0;
   if (mask) {
-    if (canvas) GSKY_NN_LAUNCH(true, 4, 4, kCanvas); else GSKY_NN_LAUNCH(true, 4, 4, 0);
+    if (canvas) GSKY_NN_LAUNCH(true, 4, 2, kCanvas); else GSKY_NN_LAUNCH(true, 4, 2, 0);
   } else if (fixed) {
     if (canvas) GSKY_NN_LAUNCH(false, 4, 4, kCanvas | kFixed); else GSKY_NN_LAUNCH(false, 4, 4, kFixed);
   } else if (a.nn_shape == 1) {

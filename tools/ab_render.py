@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--variant", default="", help="run only this variant (for rocprofv3 passes)")
+    ap.add_argument("--probes", action="store_true", help="timing-only probes: no gathers / no stores")
     args = ap.parse_args()
     cfg = synth.config_c2() if args.config == "c2" else synth.config_c5()
     b = gpu_batch(cfg)
@@ -49,20 +50,25 @@ def main():
     pal = gsky_amd.Palette(cfg.palette, True) if cfg.palette else None
     ref = None
     # (name, typed, LDS_STAGE, LDS_FLAGS, NN_KERNEL, NN_SHAPE[, NN_XCD])
-    variants = [("nn_4x4", True, "0", "0", "1", "0"), ("nn_8x1", True, "0", "0", "1", "1"),
-                ("nn_8x2", True, "0", "0", "1", "2"), ("nn_4x2", True, "0", "0", "1", "3"),
+    variants = [("nn_4x2", True, "0", "0", "1", "3"), ("nn_4x4", True, "0", "0", "1", "0"), ("nn_8x1", True, "0", "0", "1", "1"),
+                ("nn_8x2", True, "0", "0", "1", "2"),
                 ("nn_4x4_fixed", True, "0", "1", "1", "0"), ("nn_4x4_xcd", True, "0", "0", "1", "0", "1"),
                 ("typed_stage", True, "1", "0", "0", "0"), ("typed_direct", True, "0", "0", "0", "0"),
                 ("typed_direct_fixed", True, "0", "1", "0", "0"), ("typed_direct_lut", True, "0", "2", "0", "0"),
                 ("generic", False, "1", "0", "0", "0")]
-    for name, typed, stage, flags, nnk, shape, *xcd in variants:
+    if args.probes:   # timing-only probes of the default NN kernel (images are wrong by design)
+        variants = [("nn_4x2", True, "0", "0", "1", "3")] + [
+            ("probe_%s" % p, True, "0", "0", "1", "3", "0", p) for p in ("1", "2", "3")]
+    for name, typed, stage, flags, nnk, shape, *extra in variants:
         if args.variant and name != args.variant:
             continue
+        xcd = extra[:1]
         os.environ["GSKYHIP_LDS_STAGE"] = stage
         os.environ["GSKYHIP_LDS_FLAGS"] = flags
         os.environ["GSKYHIP_NN_KERNEL"] = nnk
         os.environ["GSKYHIP_NN_SHAPE"] = shape
         os.environ["GSKYHIP_NN_XCD"] = xcd[0] if xcd else "0"
+        os.environ["GSKYHIP_NN_PROBE"] = extra[1] if len(extra) > 1 else "0"
         b.typed = typed
         med, mn = time_render(b, sp, pal, args.reps)
         out = b.render(sp, pal).clone()
