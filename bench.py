@@ -44,7 +44,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import gsky_amd  # noqa: E402
-from gsky_amd import GranuleSet, Mask, Palette, ScaleParams, TileBatch, partition, synth  # noqa: E402
+from gsky_amd import GranuleSet, Mask, Palette, PipelinedBatch, ScaleParams, TileBatch, partition, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "reprojected+merged output Mpix/s (whole node) at 1/2/4/8 MI355X; p50 tile ms"
@@ -112,7 +112,7 @@ block_part = partition.tile_blocks     # contiguous tile blocks (gsky_amd/partit
 sub_config = partition.sub_config      # a rank uploads only the granules its tiles touch
 
 
-def build_batch(cfg, device):
+def build_batch(cfg, device, chunks: int = 0):
     gs = GranuleSet(device)
     for g in cfg.granules:
         gs.add(torch.from_numpy(np.ascontiguousarray(g.data)), g.geot, g.srs, g.nodata,
@@ -120,6 +120,8 @@ def build_batch(cfg, device):
                g.namespace)
     mask = Mask(cfg.mask["id"], cfg.mask.get("value", ""), cfg.mask.get("bit_tests", []),
                 cfg.mask.get("inclusive", False)) if cfg.mask else None
+    if chunks > 1:
+        return PipelinedBatch(gs, cfg.dst_srs, cfg.tiles, cfg.pairs, cfg.namespaces, mask, n_chunks=chunks)
     return TileBatch(gs, cfg.dst_srs, cfg.tiles, cfg.pairs, cfg.namespaces, mask)
 
 
@@ -178,11 +180,15 @@ def run_c2(ctx: Ctx, args):
     cfg = sub_config(full, ids)
     batch = build_batch(cfg, ctx.device)
     sp, pal = ScaleParams(*cfg.scale), Palette(cfg.palette, True)
-    batch.render(sp, pal)
-    torch.cuda.synchronize()
-    if batch.status() != 0:
-        raise RuntimeError("render status %d" % batch.status())
-    dt = ctx.timed(lambda: batch.render(sp, pal), args.steps, args.warmup)
+    # the timed step: the batch in chunks on two streams, so each chunk's
+    # planning kernels run under the previous chunk's render (PipelinedBatch)
+    step_batch = build_batch(cfg, ctx.device, chunks=args.c2_chunks) if args.c2_chunks > 1 else batch
+    for bb in (batch, step_batch):
+        bb.render(sp, pal)
+        torch.cuda.synchronize()
+        if bb.status() != 0:
+            raise RuntimeError("render status %d" % bb.status())
+    dt = ctx.timed(lambda: step_batch.render(sp, pal), args.steps, args.warmup)
     total_px = full.out_pixels * args.steps
     plan_ms = event_ms(lambda: batch.render(sp, pal, phase=1), max(3, args.steps))
     render_ms = event_ms(lambda: batch.render(sp, pal, phase=2), max(3, args.steps))
@@ -196,11 +202,13 @@ def run_c2(ctx: Ctx, args):
         "config": {"workload": "C2: %d x 512x512 EPSG:3857 tiles from %d EPSG:3577 int16 4000x4000 granules, "
                                "nearest, time-ordered merge + scale + palette" % (len(full.tiles), len(full.granules)),
                    "tiles_per_step": len(full.tiles), "tiles_per_rank": len(ids), "pairs_rank0": batch.n_pairs,
-                   "parallelism": "tile blocks over %d rank(s) (contiguous, granules per rank)" % ctx.world},
+                   "parallelism": "tile blocks over %d rank(s) (contiguous, granules per rank)" % ctx.world,
+                   "pipeline": "%d chunks on 2 HIP streams (plan of chunk k+1 under render of chunk k)"
+                               % args.c2_chunks if args.c2_chunks > 1 else "one batch, one stream"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("render_c2")
                      if ctx.world == 1 else None,
-                     "kernel": "render_lds_kernel<int16> + render_general_kernel (phase 2, rank 0)",
+                     "kernel": "render_nn2_kernel<int16> + render_general_kernel (phase 2, one batch, rank 0)",
                      "kernel_ms": round(render_ms, 4), "plan_ms": round(plan_ms, 4),
                      "algorithmic_bytes_per_launch": abytes, "lib_sha16": lib_sha()},
     }
@@ -225,7 +233,7 @@ def run_c2(ctx: Ctx, args):
             "sample": "all 4096 C2 tiles rendered by oracle/ (C restatement of warp_operation_fast + merge + "
                       "Scale + palette) on %d threads = the box's CPU share (cgroup quota), median of %d runs; "
                       "1-core figure on 256 tiles" % (cores, args.cpu_runs)}
-    del batch
+    del batch, step_batch
     return out
 
 
@@ -369,6 +377,7 @@ def run_c4(ctx: Ctx, args):
         from concurrent.futures import ThreadPoolExecutor
 
         from oracle import oracle as O
+        order = sorted(range(len(inside)), key=lambda p: -inside[p])   # by size, so the sample spans all sizes
         ids = order[:: max(1, len(order) // args.c4_cpu_polys)][: args.c4_cpu_polys]
         subs = {}
         for p in ids:
@@ -440,6 +449,7 @@ def main():
     ap.add_argument("--cpu-runs", type=int, default=5)
     ap.add_argument("--c1-reps", type=int, default=1000)
     ap.add_argument("--c1-cpu-reps", type=int, default=200)
+    ap.add_argument("--c2-chunks", type=int, default=4, help="C2 step: tile chunks pipelined on 2 streams")
     ap.add_argument("--c3-steps", type=int, default=3)
     ap.add_argument("--c4-cpu-polys", type=int, default=160)
     args = ap.parse_args()

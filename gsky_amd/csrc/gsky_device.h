@@ -465,8 +465,25 @@ struct EntryD {
 enum RowKind : int32_t { ROW_LINEAR = 0, ROW_EXACT = 1, ROW_POOL = 2, ROW_DESCEND = 3 };
 struct RowRec {
   double v[6];   // LINEAR: xs0, ys0, dX, dY ; DESCEND: xs0, ys0, xs1, ys1, xs2, ys2
-  int32_t kind, nleaf, pool_off, _pad;
+  int32_t kind, nleaf, pool_off;
+  int32_t inside;   // LINEAR: 1 when every window pixel's NN source pixel is inside the band
 };
+
+// NN source pixel of window pixel `dist` of a LINEAR row (the expressions of
+// lin_coords() + nn_px()): false where the reference's window fill applies.
+__device__ __forceinline__ bool linear_nn_px(const RowRec &r, int dist, int bx, int by) {
+  const double sx = r.v[0] + r.v[2] * (double)dist, sy = r.v[1] + r.v[3] * (double)dist;
+  const int ix = __double2int_rz(sx + 1.0e-10), iy = __double2int_rz(sy + 1.0e-10);
+  return sx >= 0.0 && sy >= 0.0 && ix < bx && iy < by;
+}
+
+// RowRec.inside: fl(a + fl(b * d)) and the truncation after + 1e-10 are
+// monotone in d, so every pixel of the row [0, n) is inside when both end
+// pixels are.  The NN band kernel then drops the per-pixel range tests and
+// the window fill select (render_nn.h).
+__device__ __forceinline__ bool linear_row_inside(const RowRec &r, int n, int bx, int by) {
+  return n > 0 && linear_nn_px(r, 0, bx, by) && linear_nn_px(r, n - 1, bx, by);
+}
 struct Leaf {
   double xs0, ys0, dX, dY;
   int32_t start, kind;   // LeafKind

@@ -397,7 +397,9 @@ __device__ void plan_tile_serial(const PlanArgs &a, int t) {
     else if (v > 0 && vt != v) vt = 0;
   }
   tp.vt = vt < 0 ? 0 : vt;
-  if (n > 0 && tp.vt == 0) {
+  // mixed types, promotion, or no entry at all: the general kernel renders
+  // the tile (an empty tile must still be written: transparent / nodata)
+  if (tp.vt == 0) {
     tp.complex = 1;
     const int k = atomicAdd(&a.counters[2], 1);
     a.complex_list[k] = t;
@@ -533,7 +535,7 @@ __global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
     }
   }
   tp.vt = (vzero || vmax < 0 || vmin != vmax) ? 0 : vmax;
-  if (n > 0 && tp.vt == 0) {
+  if (tp.vt == 0) {   // as above: empty tiles too
     tp.complex = 1;
     const int k = atomicAdd(&a.counters[2], 1);
     a.complex_list[k] = t;
@@ -587,7 +589,7 @@ __global__ __launch_bounds__(256) void plan_rows_kernel(PlanArgs a) {
   if (row >= pp.h) return;
   const Xform &t = a.xforms[p];
   RowRec rec;
-  rec.nleaf = 1; rec.pool_off = 0; rec._pad = 0;
+  rec.nleaf = 1; rec.pool_off = 0; rec.inside = 0;
   for (int k = 0; k < 6; k++) rec.v[k] = 0;
   const int n = pp.w;
   const int nMiddle = (n - 1) / 2;
@@ -630,6 +632,7 @@ __global__ __launch_bounds__(256) void plan_rows_kernel(PlanArgs a) {
       if (dfError <= kMaxErr) {
         rec.kind = ROW_LINEAR;
         rec.v[0] = xs[0]; rec.v[1] = ys[0]; rec.v[2] = dX; rec.v[3] = dY;
+        rec.inside = linear_row_inside(rec, n, pp.band_x, pp.band_y) ? 1 : 0;
       } else {
         rec.kind = ROW_DESCEND;  // provisional: root SME kept for the split pass
         rec.v[0] = xs[0]; rec.v[1] = ys[0]; rec.v[2] = xs[1];
@@ -1121,6 +1124,9 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.nn_shape = 3;
   a.nn_xcd = 0;
   a.nn_probe = 0;
+  a.nn_gen = 3;
+  a.nn_wpe = 0;
+  a.nn_express = 1;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;

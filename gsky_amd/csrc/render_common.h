@@ -218,6 +218,9 @@ struct RenderArgs {
   int nn_shape;                // render_nn_kernel pixels x rows per lane (A/B knob, render_nn.h)
   int nn_xcd;                  // render_nn_kernel: XCD-aware item order (A/B knob)
   int nn_probe;                // timing-only probes of render_nn_kernel (0: off; see render_nn.h)
+  int nn_wpe;                  // render_nn2_kernel: minimum waves per SIMD it is compiled for (A/B knob)
+  int nn_express;              // render_nn2_kernel: single-entry express path (A/B knob)
+  int nn_gen;                  // NN band kernel generation: 3 render_nn2_kernel (default), 2 render_nn_kernel (A/B)
 };
 
 // ---------------------------------------------------------------- typed fast path

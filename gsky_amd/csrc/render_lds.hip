@@ -22,6 +22,12 @@ void launch_lds_kernels(const RenderArgs &a0, int vt, bool mask, int n_items, hi
   a.nn_shape = ns ? atoi(ns) : 3;
   const char *np = getenv("GSKYHIP_NN_PROBE");   // timing-only probes (wrong images): never set in production
   a.nn_probe = np ? atoi(np) : 0;
+  const char *nw = getenv("GSKYHIP_NN_WPE");
+  a.nn_wpe = nw ? atoi(nw) : 0;
+  const char *ne = getenv("GSKYHIP_NN_EXPRESS");
+  a.nn_express = ne ? atoi(ne) : 1;
+  const char *ng = getenv("GSKYHIP_NN_GEN");
+  a.nn_gen = ng ? atoi(ng) : 3;   // render_nn2_kernel unless GSKYHIP_NN_GEN=2 (A/B)
   const char *nx = getenv("GSKYHIP_NN_XCD");
   a.nn_xcd = nx ? atoi(nx) : 0;   // linear item order by default (A/B, profiles/r02g_ab_*.jsonl)
   switch (vt) {

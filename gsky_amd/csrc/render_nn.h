@@ -26,6 +26,7 @@
 namespace gsky {
 
 constexpr uint32_t kNoPx = 0xFFFFFFFFu;
+constexpr int kExpress = 16;   // render_nn2_kernel: single-entry express path (A/B knob GSKYHIP_NN_EXPRESS)
 
 // Element index of each of the lane's LPX pixels on a LINEAR row, 32.32
 // fixed point.  false (wave-uniform): some valid pixel of the wave sits
@@ -275,6 +276,333 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
   }
 }
 
+// ---------------------------------------------------------------- third generation
+// render_nn2_kernel: the work of render_nn_kernel (no-mask tiles) with the
+// VALU per pixel cut down -- the kernel above measured VALU-issue bound
+// (profiles/pmc_render_nn_c2_r02h.json: ~42 VALU lane-ops per output pixel,
+// SIMDs 61 % VALU-busy):
+//   * rows the planner marked `inside` (every window pixel's NN source pixel
+//     lies in the band, RowRec.inside) skip the per-pixel sign / size tests,
+//     the "no pixel" index and the window-fill select: truncate, index, load;
+//   * 8/16-bit values travel through the fold as zero-extended bit patterns
+//     (the fold only compares and selects), sign-extended once at the output;
+//   * the output is branch-free: utils.Scale in the canvas type, Go's
+//     uint8(float32) range test only when float32(clip) * scale can reach
+//     2^31 (wave-uniform), and the palette / grey ramp in LDS with the
+//     EncodePNG transparency rule baked in (entry 255 and uncreated canvases
+//     are 0), so one LDS read per pixel replaces the select chain.
+// Rows that are not `inside` (window edges, POOL rows) take the exact
+// expressions of nn_row_index() with the fill select, as before.
+template <typename T> struct POf { using type = uint32_t; };
+template <> struct POf<float> { using type = float; };
+
+template <typename T>
+__device__ __forceinline__ typename POf<T>::type to_pat(Val x) {
+  if constexpr (std::is_same<T, float>::value) return x.f;
+  else return (uint32_t)x.i & (sizeof(T) == 1 ? 0xFFu : 0xFFFFu);
+}
+
+template <typename T>
+__device__ __forceinline__ typename POf<T>::type buf_load_pat(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (sizeof(T) == 1) return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+  else if constexpr (sizeof(T) == 2) return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+  else return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// utils.Scale of an integer canvas value given as its bit pattern (the
+// arithmetic of scale_t(): value += offset wrapping in T, clip, clamp at 0,
+// float32 multiply, Go uint8(float32)); 0xFF for the canvas nodata.
+template <typename T, bool SAFE>
+__device__ __forceinline__ uint32_t scale_pat(uint32_t c, uint32_t nd_pat, int32_t off, int32_t clp, float sc) {
+  int32_t value = (int32_t)(c + (uint32_t)off);
+  if constexpr (std::is_same<T, int8_t>::value) value = (int8_t)value;
+  else if constexpr (std::is_same<T, uint8_t>::value) value = (uint8_t)value;
+  else if constexpr (std::is_same<T, int16_t>::value) value = (int16_t)value;
+  else value = (uint16_t)value;
+  value = max(min(value, clp), 0);
+  const float f = (float)value * sc;
+  const uint32_t b = SAFE ? ((uint32_t)(int32_t)f & 0xFFu) : go_u8_f32(f);   // SAFE: 0 <= f < 2^31
+  return c == nd_pat ? 0xFFu : b;
+}
+
+template <typename T, int LPX, int R, int FLAGS, int WPE>
+__global__ __launch_bounds__(256, WPE) void render_nn2_kernel(RenderArgs a, const EntryD *__restrict__ ents,
+                                                         const int32_t *__restrict__ order,
+                                                         const RowRec *__restrict__ rows,
+                                                         const Leaf *__restrict__ pool,
+                                                         const TilePlan *__restrict__ tplans,
+                                                         const gskyhip_tile *__restrict__ tiles, int n_items) {
+  using P = typename POf<T>::type;
+  constexpr bool kInt = !std::is_same<T, float>::value;
+  constexpr bool kCv = (FLAGS & kCanvas) != 0;
+  constexpr int kCols = 64 * LPX;
+  __shared__ uint32_t s_tab[256];
+
+  const int item = blockIdx.x;
+  if (item >= n_items) return;
+  const int bands_per_tile = (a.max_h + kBandRows - 1) / kBandRows;
+  const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
+  const int t = item / (bands_per_tile * col_blocks);
+  const int in_tile = item - t * bands_per_tile * col_blocks;
+  const TilePlan &tp = tplans[t];
+  if (tp.complex || tp.vt != vt_code<T>()) return;
+  const gskyhip_tile &tile = tiles[t];
+  const int W = tile.width, H = tile.height;
+  const int band0 = (in_tile / col_blocks) * kBandRows;
+  const int xb = (in_tile % col_blocks) * kBandCols;
+  if (band0 >= H || xb >= W) return;
+  const int tid = threadIdx.x;
+  const int ns_out = a.out_ns[0];
+  const bool created = tp.created[ns_out] != 0;
+  if constexpr (!kCv) {   // EncodePNG: utils.Scale 0xFF and uncreated canvases are transparent
+    const uint32_t col = a.ramp ? a.ramp[tid] : (0xFF000000u | ((uint32_t)tid * 0x10101u));
+    s_tab[tid] = (created && tid != 255) ? col : 0u;
+    __syncthreads();
+  }
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r0 = band0 + wave * 4;
+  if (r0 >= H) return;
+
+  const P cnod = to_pat<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]));
+  const int32_t *ord = order + tile.pair_begin;
+  const int n_entries = tp.n_entries;
+  const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
+  const bool safe = !kInt || (float)max(sk.clp.i, 0) * sk.sc < 2147483648.0f;   // NaN -> false
+  uint8_t *rgba_tile = a.rgba + (int64_t)t * a.max_h * a.max_w * 4;
+  const int xend = min(xb + kBandCols, W);
+
+  // output of the lane's LPX pixels of row r from x0: typed canvas (WCS) or
+  // utils.Scale + palette / grey RGBA
+  auto emit = [&](int r, int x0, const P *cv) {
+    if (r >= H || x0 >= W) return;
+    if constexpr (kCv) {
+      const int64_t eo = a.cov_offsets ? a.cov_offsets[t] + (int64_t)r * a.cov_stride + x0
+                                       : (int64_t)r * a.max_w + x0;
+      T *cdst = (T *)(a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride) + eo;
+      T tv[LPX];
+#pragma unroll
+      for (int q = 0; q < LPX; q++) {
+        if constexpr (kInt) tv[q] = (T)cv[q]; else tv[q] = cv[q];
+      }
+      constexpr int kBytes = (int)sizeof(T) * LPX;
+      if (x0 + LPX <= W && (((uintptr_t)cdst) & (kBytes >= 16 ? 15 : kBytes - 1)) == 0) {
+        if constexpr (kBytes % 16 == 0) {
+#pragma unroll
+          for (int h = 0; h < kBytes / 16; h++) {
+            u32x4 v4;
+            __builtin_memcpy(&v4, (const char *)tv + 16 * h, 16);
+            __builtin_nontemporal_store(v4, (GPTR(u32x4))((char *)cdst + 16 * h));
+          }
+        } else if constexpr (kBytes == 8) {
+          uint64_t v2;
+          __builtin_memcpy(&v2, tv, 8);
+          *(uint64_t *)cdst = v2;
+        } else {
+          uint32_t v1;
+          __builtin_memcpy(&v1, tv, 4);
+          *(uint32_t *)cdst = v1;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < LPX; q++)
+          if (x0 + q < W) cdst[q] = tv[q];
+      }
+    } else {
+      uint32_t px[LPX];
+      if constexpr (kInt) {
+        const uint32_t ndp = to_pat<T>(sk.noData);
+        if (safe) {
+#pragma unroll
+          for (int q = 0; q < LPX; q++) px[q] = s_tab[scale_pat<T, true>(cv[q], ndp, sk.off.i, sk.clp.i, sk.sc)];
+        } else {
+#pragma unroll
+          for (int q = 0; q < LPX; q++) px[q] = s_tab[scale_pat<T, false>(cv[q], ndp, sk.off.i, sk.clp.i, sk.sc)];
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < LPX; q++) px[q] = s_tab[scale_t<T>(sk, cv[q]) & 0xFFu];
+      }
+      uint8_t *dst = rgba_tile + ((int64_t)r * a.max_w + x0) * 4;
+      if (x0 + LPX <= W && ((((uintptr_t)dst) & 15) == 0)) {
+#pragma unroll
+        for (int h = 0; h < LPX / 4; h++) {
+          u32x4 v4 = {px[4 * h], px[4 * h + 1], px[4 * h + 2], px[4 * h + 3]};
+          __builtin_nontemporal_store(v4, (GPTR(u32x4))(dst + 16 * h));
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < LPX; q++)
+          if (x0 + q < W) ((uint32_t *)dst)[q] = px[q];
+      }
+    }
+  };
+
+  // Express path (wave-uniform): the tile has one entry, it covers the
+  // wave's 4 rows, every one of them `inside`, and the block is at most two
+  // passes wide.  All 2 x 4 x LPX gathers of the wave are issued before the
+  // first wait: one scalar chain and one gather round trip per wave instead
+  // of one per (pass, row) -- the general loops below are latency-bound.
+  if (n_entries == 1 && r0 + 4 <= H && xend - xb <= 2 * kCols && (FLAGS & kExpress)) {
+    const EntryD &e = ents[ord[0]];
+    const int eyoff = e.yoff, exoff = e.xoff, ew = e.w;
+    bool ok = e.ns == ns_out && ew > 0 && r0 >= eyoff && r0 + 4 <= eyoff + e.h;
+    const RowRec *rr = rows + e.row_base + (r0 - eyoff);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      ok = ok && __builtin_amdgcn_readfirstlane(rr[i].kind) == ROW_LINEAR &&
+           __builtin_amdgcn_readfirstlane(rr[i].inside) != 0;
+    if (ok) {
+      const int bx = e.band_x, by = e.band_y;
+      const P nd = to_pat<T>(e.nd);
+      const bool allow = e.fill_mode == 0 || cnod == nd;   // fill mode: only onto canvas nodata
+      const int lim = allow ? max(0, min(ew, W - exoff)) : 0;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
+      const bool two = xend - xb > kCols;
+      P vv[2][4][LPX];
+#pragma unroll
+      for (int pp = 0; pp < 2; pp++) {
+        if (pp == 1 && !two) break;
+        const int ic0 = xb + pp * kCols + lane * LPX - exoff;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const double xs0 = rr[i].v[0], ys0 = rr[i].v[1], dX = rr[i].v[2], dY = rr[i].v[3];
+#pragma unroll
+          for (int q = 0; q < LPX; q++) {
+            const double dist = (double)(ic0 + q);
+            const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
+            const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
+            vv[pp][i][q] = buf_load_pat<T>(rs, (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T));
+          }
+        }
+      }
+      // one entry: the fold is "take the value unless nodata or outside the window"
+#pragma unroll
+      for (int pp = 0; pp < 2; pp++) {
+        if (pp == 1 && !two) break;
+        const int x0 = xb + pp * kCols + lane * LPX;
+        const int ic0 = x0 - exoff;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          P cv[LPX];
+#pragma unroll
+          for (int q = 0; q < LPX; q++)
+            cv[q] = (((unsigned)(ic0 + q) < (unsigned)lim) & (vv[pp][i][q] != nd)) ? vv[pp][i][q] : cnod;
+          emit(r0 + i, x0, cv);
+        }
+      }
+      return;
+    }
+  }
+
+#pragma unroll 1
+  for (int cx = xb; cx < xend; cx += kCols) {
+    const int x0 = cx + lane * LPX;
+#pragma unroll 1
+    for (int j = 0; j < 4; j += R) {
+      const int rb = r0 + j;
+      if (rb >= H) break;
+      P c[R][LPX];
+#pragma unroll
+      for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int q = 0; q < LPX; q++) c[i][q] = cnod;
+
+#pragma unroll 1
+      for (int k = 0; k < n_entries; k++) {
+        const EntryD &e = ents[ord[k]];
+        const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
+        if (e.ns != ns_out || ew <= 0) continue;
+        if (rb + R <= eyoff || rb >= eyoff + eh) continue;
+        if (cx + kCols <= exoff || cx >= exoff + ew) continue;
+        const int bx = e.band_x, by = e.band_y;
+        const P nd = to_pat<T>(e.nd), fillv = to_pat<T>(e.fill);
+        const bool fill_mode = e.fill_mode != 0;
+        const RowRec *rrow = rows + e.row_base;
+        const int ic0 = x0 - exoff;
+        const int lim = max(0, min(ew, W - exoff));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
+        bool inq[LPX];
+#pragma unroll
+        for (int q = 0; q < LPX; q++) inq[q] = (unsigned)(ic0 + q) < (unsigned)lim;
+        // row state (wave-uniform): 0 no pixel, 1 inside (fast), 2 exact tests
+        int st[R];
+        bool all_fast = true;
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+          const int ir = rb + i - eyoff;
+          if (ir < 0 || ir >= eh || rb + i >= H) {
+            st[i] = 0;
+          } else {
+            const RowRec *rr = rrow + ir;
+            const bool in = __builtin_amdgcn_readfirstlane(rr->kind) == ROW_LINEAR &&
+                            __builtin_amdgcn_readfirstlane(rr->inside) != 0;
+            st[i] = in ? 1 : 2;
+            all_fast = all_fast && in;
+          }
+        }
+        P vv[R][LPX];
+        if (all_fast) {
+          // every row inside (or empty): truncate, index, load -- nothing else
+#pragma unroll
+          for (int i = 0; i < R; i++) {
+            if (st[i] == 0) continue;
+            const RowRec *rr = rrow + (rb + i - eyoff);
+            const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
+#pragma unroll
+            for (int q = 0; q < LPX; q++) {
+              const double dist = (double)(ic0 + q);
+              const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
+              const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
+              vv[i][q] = buf_load_pat<T>(rs, (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T));
+            }
+          }
+          // ordered fold (tile_merger.go:47-120); bitwise &, not &&: a short
+          // circuit lets the compiler sink a gather under a branch
+          if (!fill_mode) {
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+              if (st[i] == 0) continue;
+#pragma unroll
+              for (int q = 0; q < LPX; q++) c[i][q] = (inq[q] & (vv[i][q] != nd)) ? vv[i][q] : c[i][q];
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+              if (st[i] == 0) continue;
+#pragma unroll
+              for (int q = 0; q < LPX; q++)
+                c[i][q] = (inq[q] & (vv[i][q] != nd) & (c[i][q] == nd)) ? vv[i][q] : c[i][q];
+            }
+          }
+        } else {
+          // some row needs the exact tests: one row at a time (keeps the
+          // register peak of the R-row fast path)
+#pragma unroll
+          for (int i = 0; i < R; i++) {
+            if (st[i] == 0) continue;
+            uint32_t idx[LPX];
+            P v1[LPX];
+            nn_row_index<LPX, false>(rrow + (rb + i - eyoff), pool, ic0, ew, lim, bx, by, idx);
+#pragma unroll
+            for (int q = 0; q < LPX; q++) v1[q] = buf_load_pat<T>(rs, idx[q] * (uint32_t)sizeof(T));
+#pragma unroll
+            for (int q = 0; q < LPX; q++) {
+              const P v = idx[q] != kNoPx ? v1[q] : fillv;
+              const bool take = inq[q] & (v != nd) & (!fill_mode | (c[i][q] == nd));
+              c[i][q] = take ? v : c[i][q];
+            }
+          }
+        }
+      }
+
+#pragma unroll
+      for (int i = 0; i < R; i++) emit(rb + i, x0, c[i]);
+    }
+  }
+}
+
 // NN band kernel launch for value type T: lanes shape (LPX pixels x R rows)
 // from RenderArgs.nn_shape (0: 4 x 4, 1: 8 x 1, 2: 8 x 2, 3: 4 x 2, the
 // default: fastest on C2 and C5, profiles/r02h_ab_*.jsonl), 32.32
@@ -289,6 +617,33 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
                      a.pool, a.tplans, a.tiles, n_items, per_xcd)
   const bool canvas = (a.lds_mode & kCanvas) != 0;
   const bool fixed = (a.lds_flags & kFixed) != 0;
+  if (!mask && !fixed && a.nn_gen >= 3 && a.nn_probe == 0) {   // third generation (default)
+#define GSKY_NN2_LAUNCH(L, RR, F, WP)                                                                          \
+  hipLaunchKernelGGL((render_nn2_kernel<T, L, RR, F, WP>), dim3((unsigned)n_items), dim3(256), 0, s, a,      \
+                     a.entries, a.order, a.rows, a.pool, a.tplans, a.tiles, n_items)
+#define GSKY_NN2_SHAPE(L, RR, WP) \
+  do { if (canvas) GSKY_NN2_LAUNCH(L, RR, kCanvas, WP); else GSKY_NN2_LAUNCH(L, RR, 0, WP); } while (0)
+#define GSKY_NN2_SHAPE_X(L, RR, WP)                                                  \
+  do {                                                                               \
+    if (a.nn_express) {                                                              \
+      if (canvas) GSKY_NN2_LAUNCH(L, RR, kCanvas | kExpress, WP);                    \
+      else GSKY_NN2_LAUNCH(L, RR, kExpress, WP);                                     \
+    } else GSKY_NN2_SHAPE(L, RR, WP);                                                \
+  } while (0)
+    // A/B knobs: nn_shape (0: 4 x 4, 1: 8 x 1, 4: 4 x 1, else 4 x 2), nn_wpe (minimum waves per SIMD the
+    // compiler must fit: 0 = free, 6, 8), nn_express (single-entry express path, default on)
+    if (a.nn_shape == 0) GSKY_NN2_SHAPE(4, 4, 1);
+    else if (a.nn_shape == 1) GSKY_NN2_SHAPE(8, 1, 1);
+    else if (a.nn_shape == 4) GSKY_NN2_SHAPE_X(4, 1, 1);
+    else {
+      if (a.nn_wpe == 6) GSKY_NN2_SHAPE(4, 2, 6);
+      else GSKY_NN2_SHAPE_X(4, 2, 1);
+    }
+#undef GSKY_NN2_SHAPE_X
+#undef GSKY_NN2_SHAPE
+#undef GSKY_NN2_LAUNCH
+    return;
+  }
   if (mask) {
     if (canvas) GSKY_NN_LAUNCH(true, 4, 2, kCanvas); else GSKY_NN_LAUNCH(true, 4, 2, 0);
   } else if (fixed) {

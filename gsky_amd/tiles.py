@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -91,7 +91,8 @@ class TileBatch:
     3 -> RGB); granules of `mask.id` form the mask layer."""
 
     def __init__(self, granules: GranuleSet, dst_srs: Optional[str], tiles, pairs: Sequence[Sequence[int]],
-                 namespaces: Sequence[str] = ("",), mask: Optional[Mask] = None):
+                 namespaces: Sequence[str] = ("",), mask: Optional[Mask] = None,
+                 slot: Optional[Tuple[int, int]] = None):
         if len(tiles) != len(pairs):
             raise ValueError("one granule list per tile")
         self.granules = granules
@@ -167,6 +168,10 @@ class TileBatch:
             tarr[i].pair_end = len(flat)
             self.max_w = max(self.max_w, w)
             self.max_h = max(self.max_h, h)
+        if slot is not None:   # a fixed (max_w, max_h) tile slot, e.g. a chunk of a PipelinedBatch
+            if slot[0] < self.max_w or slot[1] < self.max_h:
+                raise ValueError("tile larger than the slot")
+            self.max_w, self.max_h = int(slot[0]), int(slot[1])
         self.n_tiles = len(tiles)
         self.n_pairs = len(flat)
         self.tile_sizes = [(w, h) for (_, w, h) in tiles]
@@ -294,3 +299,60 @@ class TileBatch:
             t = win[p, : w * h * nb].view(TORCH_OF[tname]).reshape(h, w)
             out.append((t, bb[p].tolist(), tname, float(nds[p])))
         return out
+
+
+class PipelinedBatch:
+    """A GetMap batch cut into contiguous chunks of tiles, each its own
+    TileBatch (own workspace), issued round-robin on `n_streams` HIP streams:
+    the planning kernels of chunk k+1 (latency-bound fp64 transforms, few
+    waves) run while the render kernel of chunk k streams RGBA.  Tiles are
+    independent requests (tile_grpc.go:96-258), so the RGBA is identical to
+    one TileBatch over all tiles; every chunk uses the batch's tile slot, so
+    the output layout is the same (n_tiles, max_h, max_w, 4) tensor."""
+
+    def __init__(self, granules: GranuleSet, dst_srs: Optional[str], tiles, pairs: Sequence[Sequence[int]],
+                 namespaces: Sequence[str] = ("",), mask: Optional[Mask] = None, n_chunks: int = 4,
+                 n_streams: int = 2):
+        if len(tiles) != len(pairs):
+            raise ValueError("one granule list per tile")
+        n = len(tiles)
+        n_chunks = max(1, min(int(n_chunks), n)) if n else 1
+        self.device = granules.device
+        self.max_w = max([w for (_, w, _) in tiles] + [1])
+        self.max_h = max([h for (_, _, h) in tiles] + [1])
+        self.n_tiles = n
+        bounds = [n * k // n_chunks for k in range(n_chunks + 1)]
+        self.chunks = [(b0, b1, TileBatch(granules, dst_srs, tiles[b0:b1], pairs[b0:b1], namespaces, mask,
+                                          slot=(self.max_w, self.max_h)))
+                       for b0, b1 in zip(bounds[:-1], bounds[1:]) if b1 > b0]
+        self.n_pairs = sum(c[2].n_pairs for c in self.chunks)
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(max(1, int(n_streams)))]
+        self._out = None
+
+    def render(self, params: ScaleParams, palette: Optional[Palette] = None, resample: int = 0,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """RGBA of every tile, (n_tiles, max_h, max_w, 4); ordered after the
+        work already queued on the current stream, and the current stream
+        waits for every chunk."""
+        if out is None:
+            if self._out is None:
+                self._out = torch.empty((self.n_tiles, self.max_h, self.max_w, 4), dtype=torch.uint8,
+                                        device=self.device)
+            out = self._out
+        cur = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            s.wait_stream(cur)
+        for k, (b0, b1, tb) in enumerate(self.chunks):
+            with torch.cuda.stream(self.streams[k % len(self.streams)]):
+                tb.render(params, palette, resample, out=out[b0:b1])
+        for s in self.streams:
+            cur.wait_stream(s)
+        return out
+
+    def status(self) -> int:
+        """First non-zero planning status of any chunk (0: all tiles rendered)."""
+        for _, _, tb in self.chunks:
+            st = tb.status()
+            if st != 0:
+                return st
+        return 0

@@ -38,10 +38,12 @@ def oracle_render(O, cfg: synth.SynthConfig, tile_ids=None, n_threads=8, canvas=
                           sizes=[(w, h) for (_, w, h) in sub.tiles], canvas=canvas)
 
 
-def gpu_batch(cfg: synth.SynthConfig, device="cuda"):
+def gpu_batch(cfg: synth.SynthConfig, device="cuda", chunks: int = 0):
+    """The config's tiles as one TileBatch, or (chunks > 0) a PipelinedBatch
+    of that many chunks."""
     import torch
 
-    from gsky_amd import GranuleSet, Mask, TileBatch
+    from gsky_amd import GranuleSet, Mask, PipelinedBatch, TileBatch
     gs = GranuleSet(device)
     for g in cfg.granules:
         gs.add(torch.from_numpy(np.ascontiguousarray(g.data)), g.geot, g.srs, g.nodata,
@@ -49,6 +51,8 @@ def gpu_batch(cfg: synth.SynthConfig, device="cuda"):
                g.namespace)
     mask = Mask(cfg.mask["id"], cfg.mask.get("value", ""), cfg.mask.get("bit_tests", []),
                 cfg.mask.get("inclusive", False)) if cfg.mask else None
+    if chunks > 0:
+        return PipelinedBatch(gs, cfg.dst_srs, cfg.tiles, cfg.pairs, cfg.namespaces, mask, n_chunks=chunks)
     return TileBatch(gs, cfg.dst_srs, cfg.tiles, cfg.pairs, cfg.namespaces, mask)
 
 

@@ -56,6 +56,19 @@ def test_c2_full_identical(gpu, oracle):
     assert (exp[..., 3] > 0).mean() > 0.5
 
 
+def test_c2_full_pipelined_identical(gpu, oracle):
+    """C2 as bench.py times it: 4 chunks on 2 streams (PipelinedBatch) --
+    every RGBA pixel identical to the oracle, like the one-batch path."""
+    import gsky_amd
+    cfg = synth.config_c2()
+    b = gpu_batch(cfg, chunks=4)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True))
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg, n_threads=THREADS)
+    n, first = _mismatch_report(got, exp)
+    assert n == 0, "C2 pipelined: %d pixels differ, e.g. %s" % (n, first)
+
+
 def test_c5_full_identical(gpu, oracle):
     """C5: 80 x 512^2 overview tiles over 256 MODIS granules + QA masks."""
     import gsky_amd

@@ -312,6 +312,31 @@ def test_render_mixed_tile_sizes(gpu, oracle):
     assert (exp[..., 3] > 0).mean() > 0.2
 
 
+@pytest.mark.parametrize("typed", [True, False])
+def test_render_empty_tiles_written(gpu, oracle, typed):
+    """A tile no granule covers (an empty MAS answer) is still written:
+    transparent RGBA like the oracle, whatever the output buffer held (the
+    caching allocator hands back used memory), on the typed band path and the
+    generic one."""
+    import torch
+
+    import gsky_amd
+    cfg = synth.config_c2(scale=0.1, tiles_per_side=3, tile_px=128)
+    far = (-1.0e7, 8.0e6, -9.9e6, 8.1e6)   # EPSG:3857 box far from the Albers granules
+    cfg.tiles = list(cfg.tiles) + [(far, 128, 128)]
+    cfg.pairs = list(cfg.pairs) + [[]]
+    cfg.tiles.insert(2, (far, 128, 128))
+    cfg.pairs.insert(2, [0])              # a granule listed but not intersecting
+    b = gpu_batch(cfg)
+    b.typed = typed
+    out = torch.full((len(cfg.tiles), b.max_h, b.max_w, 4), 0xAB, dtype=torch.uint8, device="cuda")
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True), out=out).cpu().numpy()
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg)
+    assert np.array_equal(got, exp)
+    assert not got[-1].any() and not got[2].any()
+
+
 def test_warp_operation_fast_dropin(gpu, oracle):
     """warp.go:82 drop-in through the worker mirror (WarpRaster)."""
     import torch

@@ -43,18 +43,26 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--variant", default="", help="run only this variant (for rocprofv3 passes)")
     ap.add_argument("--probes", action="store_true", help="timing-only probes: no gathers / no stores")
+    ap.add_argument("--oracle", action="store_true", help="also count RGBA pixels differing from the oracle")
     args = ap.parse_args()
     cfg = synth.config_c2() if args.config == "c2" else synth.config_c5()
     b = gpu_batch(cfg)
     sp = gsky_amd.ScaleParams(*cfg.scale)
     pal = gsky_amd.Palette(cfg.palette, True) if cfg.palette else None
     ref = None
-    # (name, typed, LDS_STAGE, LDS_FLAGS, NN_KERNEL, NN_SHAPE[, NN_XCD])
-    variants = [("nn_4x2", True, "0", "0", "1", "3"), ("nn_4x4", True, "0", "0", "1", "0"), ("nn_8x1", True, "0", "0", "1", "1"),
+    exp = None
+    if args.oracle:
+        from oracle import oracle as O
+        from tests.helpers import oracle_render
+        exp = torch.from_numpy(oracle_render(O, cfg, n_threads=16)).to("cuda")
+    # (name, typed, LDS_STAGE, LDS_FLAGS, NN_KERNEL, NN_SHAPE[, NN_XCD, NN_PROBE, NN_GEN, NN_WPE, NN_EXPRESS])
+    variants = [("nn3_4x2", True, "0", "0", "1", "3", "0", "0", "3"), ("nn3_4x4", True, "0", "0", "1", "0", "0", "0", "3"),
+                ("nn3_8x1", True, "0", "0", "1", "1", "0", "0", "3"), ("nn3_4x1", True, "0", "0", "1", "4", "0", "0", "3"),
+                ("nn3_4x2_w6", True, "0", "0", "1", "3", "0", "0", "3", "6"),
+                ("nn3_4x2_nox", True, "0", "0", "1", "3", "0", "0", "3", "0", "0"),
+                ("nn3_4x1_nox", True, "0", "0", "1", "4", "0", "0", "3", "0", "0"),
+                ("nn_4x2", True, "0", "0", "1", "3"), ("nn_4x4", True, "0", "0", "1", "0"), ("nn_8x1", True, "0", "0", "1", "1"),
                 ("nn_8x2", True, "0", "0", "1", "2"),
-                ("nn_4x4_fixed", True, "0", "1", "1", "0"), ("nn_4x4_xcd", True, "0", "0", "1", "0", "1"),
-                ("typed_stage", True, "1", "0", "0", "0"), ("typed_direct", True, "0", "0", "0", "0"),
-                ("typed_direct_fixed", True, "0", "1", "0", "0"), ("typed_direct_lut", True, "0", "2", "0", "0"),
                 ("generic", False, "1", "0", "0", "0")]
     if args.probes:   # timing-only probes of the default NN kernel (images are wrong by design)
         variants = [("nn_4x2", True, "0", "0", "1", "3")] + [
@@ -69,14 +77,20 @@ def main():
         os.environ["GSKYHIP_NN_SHAPE"] = shape
         os.environ["GSKYHIP_NN_XCD"] = xcd[0] if xcd else "0"
         os.environ["GSKYHIP_NN_PROBE"] = extra[1] if len(extra) > 1 else "0"
+        os.environ["GSKYHIP_NN_GEN"] = extra[2] if len(extra) > 2 else "2"
+        os.environ["GSKYHIP_NN_WPE"] = extra[3] if len(extra) > 3 else "0"
+        os.environ["GSKYHIP_NN_EXPRESS"] = extra[4] if len(extra) > 4 else "1"
         b.typed = typed
         med, mn = time_render(b, sp, pal, args.reps)
         out = b.render(sp, pal).clone()
         torch.cuda.synchronize()
         same = True if ref is None else bool(torch.equal(out, ref))
         ref = out if ref is None else ref
-        print(json.dumps({"variant": name, "config": args.config, "render_ms_median": round(med, 4),
-                          "render_ms_min": round(mn, 4), "identical_to_first": same}), flush=True)
+        rec = {"variant": name, "config": args.config, "render_ms_median": round(med, 4),
+               "render_ms_min": round(mn, 4), "identical_to_first": same}
+        if exp is not None:
+            rec["differ_from_oracle"] = int((out != exp).any(dim=-1).sum().item())
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
