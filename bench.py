@@ -208,7 +208,7 @@ def run_c2(ctx: Ctx, args):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("render_c2")
                      if ctx.world == 1 else None,
-                     "kernel": "render_nn2_kernel<int16> + render_general_kernel (phase 2, one batch, rank 0)",
+                     "kernel": "render_nn_kernel<int16> + render_general_kernel (phase 2, one batch, rank 0)",
                      "kernel_ms": round(render_ms, 4), "plan_ms": round(plan_ms, 4),
                      "algorithmic_bytes_per_launch": abytes, "lib_sha16": lib_sha()},
     }
@@ -449,7 +449,7 @@ def main():
     ap.add_argument("--cpu-runs", type=int, default=5)
     ap.add_argument("--c1-reps", type=int, default=1000)
     ap.add_argument("--c1-cpu-reps", type=int, default=200)
-    ap.add_argument("--c2-chunks", type=int, default=4, help="C2 step: tile chunks pipelined on 2 streams")
+    ap.add_argument("--c2-chunks", type=int, default=1, help="C2 step: tile chunks pipelined on 2 streams (1: one batch; measured no gain, profiles/r02o_*)")
     ap.add_argument("--c3-steps", type=int, default=3)
     ap.add_argument("--c4-cpu-polys", type=int, default=160)
     args = ap.parse_args()

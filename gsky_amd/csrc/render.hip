@@ -109,6 +109,36 @@ __device__ bool must_adjust(const Xform &t, const double *ext, int np, int nl, d
   return __popcll(b) == 21;
 }
 
+// Both border tests at once (lanes 0..20: right border with er / psxr / psyr,
+// lanes 32..52: bottom border with eb / psxb / psyb) -- the same per-lane
+// expressions as must_adjust().  Bit 0: right must adjust, bit 1: bottom.
+__device__ int must_adjust2(const Xform &t, const double *er, double psxr, double psyr, const double *eb,
+                            double psxb, double psyb, int np, int nl, int lane) {
+  const bool right = lane < 32;
+  const int j = lane & 31;
+  bool bad = false;
+  if (j < 21) {
+    double r1 = 0.0, r2 = 0.0;
+    for (int k = 0; k < j; k++) {
+      r1 += 0.05;
+      r2 += 0.05;
+    }
+    if (r1 > 0.99) r1 = 1.0;
+    const double *ext = right ? er : eb;
+    const double psx = right ? psxr : psxb, psy = right ? psyr : psyb;
+    double ax, ay;
+    if (right) { ax = ext[2]; ay = ext[3] - psy * r1 * nl; }
+    else { ax = ext[0] + psx * r1 * np; ay = ext[1]; }
+    bool ok1 = xform_point(t, true, ax, ay);
+    bool ok2 = ok1 ? xform_point(t, false, ax, ay) : false;
+    double ex = right ? ext[2] : ext[0] + psx * r2 * np;
+    double ey = right ? ext[3] - psy * r2 * nl : ext[1];
+    bad = !ok1 || !ok2 || fabs(ax - ex) > psx || fabs(ay - ey) > psy;
+  }
+  const unsigned long long b = __ballot(bad);
+  return (__popcll(b & 0x1FFFFFull) == 21 ? 1 : 0) | (__popcll((b >> 32) & 0x1FFFFFull) == 21 ? 2 : 0);
+}
+
 constexpr int kSteps = 20;
 constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 
@@ -210,12 +240,33 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
       nLines = (int)(dfLines + 0.5);
       psx = ps; psy = ps;
       const double ratios[5] = {0.000, 0.001, 0.010, 0.100, 1.000};
-      for (int k = 0; k < 5; k++) {
+      // first trial of both borders in one pass of the wave: the bottom test
+      // assumes the right border keeps psx (trial 0 leaves it unchanged:
+      // psx - psx * 0 / nPixels == psx), which holds whenever the right test
+      // passes at trial 0 -- the common case; otherwise the reference's
+      // sequential loops run from where the speculation stopped
+      int kx0 = 0, ky0 = 0;
+      bool xdone = false, ydone = false;
+      {
+        const double tryx = psx - psx * ratios[0] / nPixels;
+        const double tryy = psy - psy * ratios[0] / nLines;
+        const double er[4] = {mnx, mxy - nLines * psy, mnx + nPixels * tryx, mxy};
+        const double eb[4] = {mnx, mxy - nLines * tryy, mnx + nPixels * tryx, mxy};
+        const int adj = must_adjust2(t, er, tryx, psy, eb, tryx, tryy, nPixels, nLines, lane);
+        kx0 = 1;
+        if (!(adj & 1)) {
+          psx = tryx;
+          xdone = true;
+          ky0 = 1;
+          if (!(adj & 2)) { psy = tryy; ydone = true; }
+        }
+      }
+      for (int k = kx0; k < 5 && !xdone; k++) {
         const double tryx = psx - psx * ratios[k] / nPixels;
         double e[4] = {mnx, mxy - nLines * psy, mnx + nPixels * tryx, mxy};
         if (!must_adjust(t, e, nPixels, nLines, tryx, psy, true, lane)) { psx = tryx; break; }
       }
-      for (int k = 0; k < 5; k++) {
+      for (int k = ky0; k < 5 && !ydone; k++) {
         const double tryy = psy - psy * ratios[k] / nLines;
         double e[4] = {mnx, mxy - nLines * tryy, mnx + nPixels * psx, mxy};
         if (!must_adjust(t, e, nPixels, nLines, psx, tryy, false, lane)) { psy = tryy; break; }
@@ -1124,9 +1175,10 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.nn_shape = 3;
   a.nn_xcd = 0;
   a.nn_probe = 0;
-  a.nn_gen = 3;
+  a.nn_gen = 2;
   a.nn_wpe = 0;
   a.nn_express = 1;
+  a.bil_kernel = 1;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;

@@ -220,7 +220,8 @@ struct RenderArgs {
   int nn_probe;                // timing-only probes of render_nn_kernel (0: off; see render_nn.h)
   int nn_wpe;                  // render_nn2_kernel: minimum waves per SIMD it is compiled for (A/B knob)
   int nn_express;              // render_nn2_kernel: single-entry express path (A/B knob)
-  int nn_gen;                  // NN band kernel generation: 3 render_nn2_kernel (default), 2 render_nn_kernel (A/B)
+  int bil_kernel;              // 1: render_bil_kernel for bilinear float canvases (default), 0: render_lds_kernel
+  int nn_gen;                  // NN band kernel generation: 2 render_nn_kernel (default), 3 render_nn2_kernel (A/B)
 };
 
 // ---------------------------------------------------------------- typed fast path

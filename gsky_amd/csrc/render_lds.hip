@@ -26,8 +26,10 @@ void launch_lds_kernels(const RenderArgs &a0, int vt, bool mask, int n_items, hi
   a.nn_wpe = nw ? atoi(nw) : 0;
   const char *ne = getenv("GSKYHIP_NN_EXPRESS");
   a.nn_express = ne ? atoi(ne) : 1;
+  const char *bk = getenv("GSKYHIP_BIL_KERNEL");
+  a.bil_kernel = bk ? atoi(bk) : 1;
   const char *ng = getenv("GSKYHIP_NN_GEN");
-  a.nn_gen = ng ? atoi(ng) : 3;   // render_nn2_kernel unless GSKYHIP_NN_GEN=2 (A/B)
+  a.nn_gen = ng ? atoi(ng) : 2;   // render_nn_kernel unless GSKYHIP_NN_GEN=3 (render_nn2_kernel, A/B: measured 2-4 % slower)
   const char *nx = getenv("GSKYHIP_NN_XCD");
   a.nn_xcd = nx ? atoi(nx) : 0;   // linear item order by default (A/B, profiles/r02g_ab_*.jsonl)
   switch (vt) {

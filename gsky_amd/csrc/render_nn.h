@@ -617,7 +617,7 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
                      a.pool, a.tplans, a.tiles, n_items, per_xcd)
   const bool canvas = (a.lds_mode & kCanvas) != 0;
   const bool fixed = (a.lds_flags & kFixed) != 0;
-  if (!mask && !fixed && a.nn_gen >= 3 && a.nn_probe == 0) {   // third generation (default)
+  if (!mask && !fixed && a.nn_gen >= 3 && a.nn_probe == 0) {   // third generation (A/B)
 #define GSKY_NN2_LAUNCH(L, RR, F, WP)                                                                          \
   hipLaunchKernelGGL((render_nn2_kernel<T, L, RR, F, WP>), dim3((unsigned)n_items), dim3(256), 0, s, a,      \
                      a.entries, a.order, a.rows, a.pool, a.tplans, a.tiles, n_items)
@@ -662,8 +662,21 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
 
 // Band kernel of one call: the NN kernel above (RenderArgs.nn_kernel, the
 // default) or render_lds_kernel (bilinear, LDS staging, A/B variants).
+template <int LPX, int R>
+__global__ void render_bil_kernel(RenderArgs a, const EntryD *__restrict__ ents, const int32_t *__restrict__ order,
+                                  const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
+                                  const TilePlan *__restrict__ tplans, const gskyhip_tile *__restrict__ tiles,
+                                  int n_items);
+void launch_bil(const RenderArgs &a, int n_items, hipStream_t s);   // render_bil.h, render_lds_f32.hip
+
 template <typename T>
 void launch_band_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
+  if constexpr (std::is_same<T, float>::value) {   // bilinear float canvases (C3): render_bil_kernel
+    if (a.bil_kernel && !mask && (a.lds_mode & kBilinear) && (a.lds_mode & kCanvas) && !a.lds_stage) {
+      launch_bil(a, n_items, s);
+      return;
+    }
+  }
   if (a.nn_kernel && !(a.lds_mode & kBilinear) && !a.lds_stage)
     launch_nn_t<T>(a, mask, n_items, s);
   else
