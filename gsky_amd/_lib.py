@@ -23,6 +23,7 @@ MAX_BIT_TESTS = 8
 
 ERRORS = {0: "OK", -1: "bad argument", -2: "raster type not implemented", -3: "HIP runtime error",
           -4: "unsupported CRS", -5: "bad mask", -6: "no HIP device", -7: "index out of range",
+          -8: "GDALSuggestedWarpOutput() failed",
           1: "open failed", 2: "band failed", 3: "transformer failed"}
 
 
@@ -80,7 +81,7 @@ EXPORTS = [
     "gskyhip_drill_workspace_size", "gskyhip_drill_batch", "gskyhip_drill_descriptors",
     "gskyhip_drill_merge", "gskyhip_fnv32a", "gskyhip_version", "gskyhip_device_count",
     "gskyhip_render_status",
-    "gskyhip_render_tile_info",
+    "gskyhip_render_tile_info", "gskyhip_compute_reproject_extent",
 ]
 
 _lib = None
@@ -112,6 +113,7 @@ def lib() -> C.CDLL:
     L.gskyhip_warp_windows.argtypes = [vp, ci, vp, ci, ci, vp, ci, vp, ci, ci, ci, ci, vp, vp, vp, vp, i64,
                                        vp, i64, vp]
     L.gskyhip_render_status.argtypes = [vp, ci, ci, ci, vp]
+    L.gskyhip_compute_reproject_extent.argtypes = [vp, ci, vp, ci, ci, vp, vp, vp, vp]
     L.gskyhip_render_tile_info.argtypes = [vp, ci, ci, ci, vp, vp, vp]
     L.gskyhip_merge_rasters.argtypes = [C.POINTER(FlexRasterC), ci, C.POINTER(Mask), C.POINTER(vp), ci,
                                         C.POINTER(i32), C.POINTER(i32), C.POINTER(d), vp]

@@ -28,6 +28,11 @@ __host__ __device__ inline int32_t go_cvtt32(double x) {
   if (!(x > -2147483649.0 && x < 2147483648.0)) return INT32_MIN;
   return (int32_t)x;
 }
+__host__ __device__ inline int64_t go_cvtt64(double x) {
+  // CVTTSD2SQ (Go int(float64) on amd64): NaN / out of range -> 0x8000000000000000
+  if (!(x >= -9223372036854775808.0 && x < 9223372036854775808.0)) return INT64_MIN;
+  return (int64_t)x;
+}
 __host__ __device__ inline int8_t go_i8(double v) { return (int8_t)(uint8_t)(uint32_t)go_cvtt32(v); }
 __host__ __device__ inline uint8_t go_u8(double v) { return (uint8_t)(uint32_t)go_cvtt32(v); }
 __host__ __device__ inline int16_t go_i16(double v) { return (int16_t)(uint16_t)(uint32_t)go_cvtt32(v); }

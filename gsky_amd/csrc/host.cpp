@@ -625,6 +625,15 @@ int gskyhip_warp_windows(const gskyhip_granule *granules, int n_granules, const 
   return launch_warp_windows(rc, bbox_out, dtype_out, nodata_out, win_out, win_stride);
 }
 
+// ComputeReprojectExtent (warp.go:433-487), batched: one wavefront per granule.
+int gskyhip_compute_reproject_extent(const gskyhip_granule *granules, int n, const gskyhip_crs *crs_table,
+                                     int n_crs, int dst_crs, const double *dst_bbox, int32_t *out,
+                                     int32_t *status, void *stream) {
+  if (n < 0 || n_crs <= 0 || dst_crs >= n_crs || (n > 0 && (!granules || !crs_table || !dst_bbox || !out || !status)))
+    return GSKYHIP_E_ARG;
+  return launch_extent(granules, n, crs_table, dst_crs, dst_bbox, out, status, (hipStream_t)stream);
+}
+
 // RasterMerger.Run for one batch over warped FlexRasters (tile_merger.go:447-503).
 int gskyhip_merge_rasters(const gskyhip_flex_raster *rasters, int n, const gskyhip_mask *mask,
                           void *const *canvases, int n_ns, int32_t *created, int32_t *dtype, double *nodata,

@@ -31,6 +31,8 @@ struct RenderCall {
 
 int launch_render(const RenderCall &c, const int32_t *out_ns, int n_out, const gskyhip_scale_params &sp,
                   const uint8_t *ramp, uint8_t *rgba_out, void *canvas_out, int phase);
+int launch_extent(const gskyhip_granule *granules, int n, const gskyhip_crs *crs, int dst_crs, const double *bbox,
+                  int32_t *out, int32_t *status, hipStream_t s);
 int launch_warp_windows(const RenderCall &c, int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
                         void *win_out, int64_t win_stride);
 // bytesRead of the drop-in (pair 0 of a planned call): stats[2] receives it.

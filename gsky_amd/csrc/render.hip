@@ -142,46 +142,15 @@ __device__ int must_adjust2(const Xform &t, const double *er, double psxr, doubl
 constexpr int kSteps = 20;
 constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 
-// One wavefront (64 threads) per pair.
-__global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
-  const int p = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (p >= a.n_pairs) return;
-  __shared__ double sx[kGrid], sy[kGrid];
-  __shared__ int sok[kGrid];
-
-  const int t_idx = a.pair_tile[p];
-  if (t_idx < 0) {   // unreferenced pair: an empty plan nothing reads
-    if (lane == 0) {
-      PairPlan z = {};
-      z.tile = -1;
-      z.mask_pair = -1;
-      a.pairs[p] = z;
-    }
-    return;
-  }
-  const gskyhip_tile &tile = a.tiles[t_idx];
-  const int gi = a.pair_granule[p];
-  const gskyhip_granule &g = a.granules[gi];
-  Xform &xf = a.xforms[p];
-  PairPlan &pp = a.pairs[p];
-
-  // ---- transformer (warp.go:120-148)
-  Xform t;
-  t.src = a.crs[g.crs];
-  t.reproject = 0;
-  if (a.dst_crs >= 0) {
-    t.dst = a.crs[a.dst_crs];
-    t.reproject = crs_same(t.src, t.dst) ? 0 : 1;
-  } else {
-    t.dst = t.src;
-  }
-  for (int k = 0; k < 6; k++) { t.src_gt[k] = g.geot[k]; t.dst_gt[k] = tile.dst_geot[k]; }
-  inv_geot(t.src_gt, t.src_igt);
-  inv_geot(t.dst_gt, t.dst_igt);
-
-  // ---- GDALSuggestedWarpOutput2: 21 samples on each source edge
-  const int nInX = g.xsize, nInY = g.ysize;
+// GDALSuggestedWarpOutput2 (gdaltransformer.cpp 3.0.1, nOptions = 0) of the
+// transformer t over an nInX x nInY source, by one wavefront: 21 samples on
+// each source edge (the full 21 x 21 grid when an edge point fails), the
+// pixel size from the diagonal, then the right / bottom border adjustment.
+// sx / sy / sok: LDS scratch of kGrid entries.  Returns 0 (CE_None) or 1;
+// ext (dst extent), psx / psy (pixel size), nPixels / nLines on success.
+__device__ int suggested_warp_output2(const Xform &t, int nInX, int nInY, int lane, double *sx, double *sy,
+                                      int *sok, double ext[4], double &psx, double &psy, int &nPixels,
+                                      int &nLines) {
   const double dfStep = 1.0 / kSteps;
   int ns = 4 * (kSteps + 1);
   for (int k = lane; k < ns; k += 64) {
@@ -224,8 +193,9 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
   got = __ballot(got) != 0ull;
 
   int err = 1;
-  double ext[4] = {0, 0, 0, 0}, psx = 0, psy = 0;
-  int nPixels = 0, nLines = 0;
+  ext[0] = ext[1] = ext[2] = ext[3] = 0.0;
+  psx = 0.0; psy = 0.0;
+  nPixels = 0; nLines = 0;
   if (got) {
     double dX = 0, dY = 0;
     if (sok[0] && sok[ns - 1]) { dX = sx[ns - 1] - sx[0]; dY = sy[ns - 1] - sy[0]; }
@@ -277,6 +247,52 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
       ext[3] = mxy;
     }
   }
+  return err;
+}
+
+// One wavefront (64 threads) per pair.
+__global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
+  const int p = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (p >= a.n_pairs) return;
+  __shared__ double sx[kGrid], sy[kGrid];
+  __shared__ int sok[kGrid];
+
+  const int t_idx = a.pair_tile[p];
+  if (t_idx < 0) {   // unreferenced pair: an empty plan nothing reads
+    if (lane == 0) {
+      PairPlan z = {};
+      z.tile = -1;
+      z.mask_pair = -1;
+      a.pairs[p] = z;
+    }
+    return;
+  }
+  const gskyhip_tile &tile = a.tiles[t_idx];
+  const int gi = a.pair_granule[p];
+  const gskyhip_granule &g = a.granules[gi];
+  Xform &xf = a.xforms[p];
+  PairPlan &pp = a.pairs[p];
+
+  // ---- transformer (warp.go:120-148)
+  Xform t;
+  t.src = a.crs[g.crs];
+  t.reproject = 0;
+  if (a.dst_crs >= 0) {
+    t.dst = a.crs[a.dst_crs];
+    t.reproject = crs_same(t.src, t.dst) ? 0 : 1;
+  } else {
+    t.dst = t.src;
+  }
+  for (int k = 0; k < 6; k++) { t.src_gt[k] = g.geot[k]; t.dst_gt[k] = tile.dst_geot[k]; }
+  inv_geot(t.src_gt, t.src_igt);
+  inv_geot(t.dst_gt, t.dst_igt);
+
+  // ---- GDALSuggestedWarpOutput2 (warp.go:154)
+  const int nInX = g.xsize, nInY = g.ysize;
+  double ext[4], psx, psy;
+  int nPixels, nLines;
+  int err = suggested_warp_output2(t, nInX, nInY, lane, sx, sy, sok, ext, psx, psy, nPixels, nLines);
   if (lane != 0) return;
 
   // ---- overview pick (warp.go:156-198)
@@ -352,6 +368,58 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
   pp.fill = gdal_copy_to(g.nodata, odt);
   pp.ts = g.timestamp;
   pp.stamp = g.timestamp + (double)g.polygon_hash;
+}
+
+// ---------------------------------------------------------------- extent op
+// ComputeReprojectExtent (worker/gdalprocess/warp.go:433-487), one wavefront
+// per granule: GDALCreateGenImgProjTransformer(src, dst SRS, no dst dataset)
+// maps source pixels to destination georeferenced coordinates (identity
+// destination geotransform), GDALSuggestedWarpOutput = SuggestedWarpOutput2
+// with nOptions 0, then the request's pixel counts for its bbox
+// (xMin, yMin, xMax, yMax) = DstGeot[0..3] at the suggested resolution:
+//   nPixels = int((xMax - xMin + xRes/2) / xRes), nLines likewise.
+__global__ __launch_bounds__(64) void extent_kernel(const gskyhip_granule *granules, int n, const gskyhip_crs *crs,
+                                                    int dst_crs, const double *bbox, int32_t *out, int32_t *status) {
+  const int i = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (i >= n) return;
+  __shared__ double sx[kGrid], sy[kGrid];
+  __shared__ int sok[kGrid];
+  const gskyhip_granule &g = granules[i];
+  Xform t;
+  t.src = crs[g.crs];
+  t.reproject = 0;
+  if (dst_crs >= 0) {
+    t.dst = crs[dst_crs];
+    t.reproject = crs_same(t.src, t.dst) ? 0 : 1;
+  } else {
+    t.dst = t.src;
+  }
+  const double ident[6] = {0.0, 1.0, 0.0, 0.0, 0.0, 1.0};
+  for (int k = 0; k < 6; k++) { t.src_gt[k] = g.geot[k]; t.dst_gt[k] = ident[k]; }
+  inv_geot(t.src_gt, t.src_igt);
+  inv_geot(t.dst_gt, t.dst_igt);
+  double ext[4], psx, psy;
+  int nPixels, nLines;
+  const int err = suggested_warp_output2(t, g.xsize, g.ysize, lane, sx, sy, sok, ext, psx, psy, nPixels, nLines);
+  if (lane != 0) return;
+  if (err) {
+    out[2 * i] = 0; out[2 * i + 1] = 0;
+    status[i] = GSKYHIP_E_XFORM;   // "GDALSuggestedWarpOutput() failed"
+    return;
+  }
+  const double xRes = psx, yRes = fabs(-psy);   // padfGeoTransformOut[1], |padfGeoTransformOut[5]|
+  const double *bb = bbox + 4 * i;
+  out[2 * i] = (int32_t)go_cvtt64((bb[2] - bb[0] + xRes / 2.0) / xRes);
+  out[2 * i + 1] = (int32_t)go_cvtt64((bb[3] - bb[1] + yRes / 2.0) / yRes);
+  status[i] = 0;
+}
+
+int launch_extent(const gskyhip_granule *granules, int n, const gskyhip_crs *crs, int dst_crs, const double *bbox,
+                  int32_t *out, int32_t *status, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(extent_kernel, dim3((unsigned)n), dim3(64), 0, s, granules, n, crs, dst_crs, bbox, out, status);
+  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 
 // ---------------------------------------------------------------- merge order

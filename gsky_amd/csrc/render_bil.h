@@ -191,9 +191,21 @@ __global__ __launch_bounds__(256) void render_bil_kernel(RenderArgs a, const Ent
 
 // Bilinear float canvases (no mask layer) go to render_bil_kernel unless
 // GSKYHIP_BIL_KERNEL=0 (A/B against the first band kernel).
+// Lane shape (LPX pixels x R rows) from RenderArgs.bil_kernel: 1 -> 4 x 1
+// (default: C3 1.35 ms/step vs 1.44-1.49 for the others and 2.30 for the
+// first band kernel, profiles/r02r_bench_c3_bil*.json), 2 -> 4 x 2,
+// 3 -> 2 x 2, 4 -> 8 x 1 (A/B knob GSKYHIP_BIL_KERNEL; 0 = render_lds_kernel).
 void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
-  hipLaunchKernelGGL((render_bil_kernel<4, 2>), dim3((unsigned)n_items), dim3(256), 0, s, a, a.entries, a.order,
-                     a.rows, a.pool, a.tplans, a.tiles, n_items);
+#define GSKY_BIL_LAUNCH(L, RR)                                                                                 \
+  hipLaunchKernelGGL((render_bil_kernel<L, RR>), dim3((unsigned)n_items), dim3(256), 0, s, a, a.entries, a.order, \
+                     a.rows, a.pool, a.tplans, a.tiles, n_items)
+  switch (a.bil_kernel) {
+    case 2: GSKY_BIL_LAUNCH(4, 2); break;
+    case 3: GSKY_BIL_LAUNCH(2, 2); break;
+    case 4: GSKY_BIL_LAUNCH(8, 1); break;
+    default: GSKY_BIL_LAUNCH(4, 1); break;
+  }
+#undef GSKY_BIL_LAUNCH
 }
 
 }  // namespace gsky

@@ -1,4 +1,4 @@
-"""Worker-side mirror of the gRPC `warp` op over the MI355X drop-in.
+"""Worker-side mirror of the gRPC `warp` and `extent` ops over the MI355X drop-in.
 
 `warp_raster(GeoRPCGranule) -> Result` follows WarpRaster
 (worker/gdalprocess/warp.go:489-584): it marshals the request into the C-ABI
@@ -7,6 +7,8 @@ exact signature, warp.go:82), copies the malloc'd window back and frees it,
 and maps the data type code to the RasterType name (warp.go:576-581).  The
 granule behind `Path` must have been registered (HBM-resident) first:
 `register_granule` replaces GDALOpenEx for this path.
+`compute_reproject_extent(GeoRPCGranule) -> Result` follows
+ComputeReprojectExtent (warp.go:433-487) over gskyhip_compute_reproject_extent.
 """
 from __future__ import annotations
 
@@ -19,7 +21,7 @@ import torch
 
 from . import _lib
 from ._lib import check, lib
-from .tiles import DTYPE_OF_TORCH
+from .tiles import DTYPE_OF_TORCH, _to_device_bytes, parse_crs
 
 GDAL_TYPES = {0: "Unkown", 1: "Byte", 2: "UInt16", 3: "Int16", 4: "UInt32", 5: "Int32", 6: "Float32",
               7: "Float64", 8: "CInt16", 9: "CInt32", 10: "CFloat32", 11: "CFloat64", 12: "TypeCount"}
@@ -92,7 +94,7 @@ def register_granule(path: str, band: int, data: torch.Tensor, geot, srs: str = 
         g.ovr_ysize[k], g.ovr_xsize[k] = o.shape
     check(lib().gskyhip_register_granule(path.encode(), band, C.byref(g), srs.encode() if srs else None),
           "register")
-    _REGISTERED[(path, band)] = (d, ovr)  # keep the HBM buffers alive
+    _REGISTERED[(path, band)] = (d, ovr, g, srs)  # keep the HBM buffers alive
 
 
 def unregister_all() -> None:
@@ -132,3 +134,40 @@ def warp_raster(req: GeoRPCGranule) -> Result:
 def raster_array(r: Raster) -> np.ndarray:
     """Result.Raster -> (h, w) array (what tile_grpc.go:228-241 reinterprets)."""
     return np.frombuffer(r.data, dtype=NP_OF[r.rasterType]).reshape(r.bbox[3], r.bbox[2])
+
+
+def compute_reproject_extent(req: GeoRPCGranule) -> Result:
+    """ComputeReprojectExtent (warp.go:433-487): the pixel counts of the
+    request's bbox req.dstGeot[0..3] (xMin, yMin, xMax, yMax) at the
+    resolution GDALSuggestedWarpOutput suggests for the dataset at req.path in
+    req.dstSRS.  Result.Raster: two Go ints (int64, little endian)
+    [nPixels, nLines], RasterType "Int", NoData 0."""
+    ent = next((v for (p, _), v in sorted(_REGISTERED.items(), key=lambda kv: kv[0][1]) if p == req.path), None)
+    if ent is None:   # GDALOpenEx failed
+        return Result(error="Failed to open existing dataset: %s" % req.path)
+    d, _, g, srs = ent
+    try:
+        crs = [parse_crs(srs)]
+        dst_crs = -1
+        if req.dstSRS:
+            crs.append(parse_crs(req.dstSRS))
+            dst_crs = 1
+    except Exception:
+        return Result(error="GDALCreateGenImgProjTransformer() failed")
+    dev = d.device
+    gc = _lib.Granule.from_buffer_copy(g)
+    gc.crs = 0
+    gran = _to_device_bytes(gc, dev)
+    crs_t = _to_device_bytes((_lib.Crs * len(crs))(*crs), dev)
+    bbox = torch.tensor([float(v) for v in req.dstGeot[:4]], dtype=torch.float64, device=dev)
+    out = torch.zeros(2, dtype=torch.int32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    check(lib().gskyhip_compute_reproject_extent(C.c_void_p(gran.data_ptr()), 1, C.c_void_p(crs_t.data_ptr()),
+                                                 len(crs), dst_crs, C.c_void_p(bbox.data_ptr()),
+                                                 C.c_void_p(out.data_ptr()), C.c_void_p(status.data_ptr()),
+                                                 stream), "compute_reproject_extent")
+    if int(status.item()) != 0:
+        return Result(error="GDALSuggestedWarpOutput() failed")
+    data = np.asarray(out.cpu().numpy(), dtype="<i8").tobytes()   # []int{nPixels, nLines}
+    return Result(raster=Raster(data=data, noData=0.0, rasterType="Int"), error="OK")

@@ -37,6 +37,7 @@ extern "C" {
 #define GSKYHIP_E_MASK (-5)        /* bad mask spec (tile_merger.go:315-323)   */
 #define GSKYHIP_E_NOGPU (-6)       /* no HIP device                            */
 #define GSKYHIP_E_RANGE (-7)       /* index out of range (Go would panic)      */
+#define GSKYHIP_E_XFORM (-8)       /* GDALSuggestedWarpOutput() failed         */
 
 /* ---- raster data types: GDALDataType codes (warp.go:428-431) + 100 ------- */
 #define GSKYHIP_BYTE 1
@@ -246,6 +247,22 @@ int gskyhip_warp_windows(const gskyhip_granule *granules, int n_granules,
                          int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
                          void *win_out, int64_t win_stride,
                          void *workspace, int64_t workspace_bytes, void *stream);
+
+/* ComputeReprojectExtent (worker/gdalprocess/warp.go:433-487, the worker's
+ * "extent" operation), batched over n granules: for granule i,
+ * GDALSuggestedWarpOutput of its GenImgProj transformer to crs_table[dst_crs]
+ * (no destination dataset: destination georeferenced coordinates; dst_crs
+ * -1 = the granule's own CRS), then its request's pixel counts
+ *   out[2i]   = nPixels = int((bbox[2] - bbox[0] + xRes/2) / xRes)
+ *   out[2i+1] = nLines  = int((bbox[3] - bbox[1] + yRes/2) / yRes)
+ * with bbox = dst_bbox[4i..4i+3] (the request's DstGeot[0..3]) and xRes /
+ * yRes the suggested geotransform's gt[1] / |gt[5]|.  status[i] = 0, or
+ * GSKYHIP_E_XFORM where the reference returns "GDALSuggestedWarpOutput()
+ * failed".  granules, crs_table, dst_bbox, out and status are device
+ * pointers; asynchronous on `stream`. */
+int gskyhip_compute_reproject_extent(const gskyhip_granule *granules, int n, const gskyhip_crs *crs_table,
+                                     int n_crs, int dst_crs, const double *dst_bbox, int32_t *out,
+                                     int32_t *status, void *stream);
 
 /* ---- standalone stages (the reference's own operator boundaries) -------- */
 /* FlexRaster (tile_types.go:95-106) as flat fields; data is dev. */

@@ -292,6 +292,23 @@ def suggested_warp_output(g: Granule, src: Crs, dst: Crs, dst_geot):
     return rc, out, np_.value, nl.value, ext
 
 
+def compute_reproject_extent(g: Granule, src: Crs, dst: Crs, dst_bbox):
+    """ComputeReprojectExtent (worker/gdalprocess/warp.go:433-487): the
+    GenImgProj transformer of the dataset to dst (no destination dataset, so
+    destination coordinates are georeferenced: identity geotransform),
+    GDALSuggestedWarpOutput (= SuggestedWarpOutput2, nOptions 0), then
+    nPixels = int((xMax - xMin + xRes/2) / xRes), nLines likewise, with
+    (xMin, yMin, xMax, yMax) = dst_bbox (the request's DstGeot[0..3]).
+    Returns (nPixels, nLines), or None where the reference answers
+    "GDALSuggestedWarpOutput() failed"."""
+    rc, gt, _, _, _ = suggested_warp_output(g, src, dst, [0.0, 1.0, 0.0, 0.0, 0.0, 1.0])
+    if rc != 0:
+        return None
+    x_res, y_res = float(gt[1]), abs(float(gt[5]))
+    x_min, y_min, x_max, y_max = (float(v) for v in dst_bbox[:4])
+    return int((x_max - x_min + x_res / 2.0) / x_res), int((y_max - y_min + y_res / 2.0) / y_res)
+
+
 def render_tiles(granules, src_crs, ts, ph, ns, dst, tiles_geot, width, height, pairs,
                  scale_params, ramp=None, n_ns=1, mask_ns=-1, mask_value=None,
                  mask_inclusive=False, resample=0, n_threads=1, sizes=None, canvas=False):

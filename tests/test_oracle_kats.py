@@ -219,3 +219,27 @@ def test_approx_row_error_bound(oracle):
         ex.append((i, (sx - src_gt[0]) / 25.0, (sy - src_gt[3]) / -25.0))
     for i, sx, sy in ex:
         assert abs(xa[i] - sx) + abs(ya[i] - sy) < 0.25
+
+
+def test_compute_reproject_extent_kat(oracle):
+    """ComputeReprojectExtent (warp.go:433-487) by hand: with no
+    reprojection GDALSuggestedWarpOutput keeps the source pixel size along
+    the diagonal, 0.1 deg for a 3600 x 1800 global lon/lat grid, so a
+    10 x 5 deg request is int((10 + 0.05) / 0.1) = 100 x 50 pixels; a
+    Web Mercator request of the same granule gets the Mercator pixel size of
+    the diagonal (about 2 x 0.1 deg of equatorial metres, the Mercator
+    stretch of the polar edge samples), and an empty request one pixel."""
+    wgs, wm = oracle.crs("EPSG:4326"), oracle.crs("EPSG:3857")
+    g = oracle.make_granule(np.zeros((1800, 3600), np.float32), [-180.0, 0.1, 0.0, 90.0, 0.0, -0.1])
+    assert oracle.compute_reproject_extent(g, wgs, wgs, [0.0, 0.0, 10.0, 5.0]) == (100, 50)
+    assert oracle.compute_reproject_extent(g, wgs, wgs, [0.0, 0.0, 0.0, 0.0]) == (0, 0)
+    rc, gt, npx, nln, _ = oracle.suggested_warp_output(g, wgs, wgs, [0.0, 1.0, 0.0, 0.0, 0.0, 1.0])
+    assert rc == 0 and gt[1] == pytest.approx(0.1, rel=1e-12) and gt[5] == pytest.approx(-0.1, rel=1e-12)
+    assert (npx, nln) == (3600, 1800)
+    # a granule that stays clear of the poles reprojects without failures
+    g2 = oracle.make_granule(np.zeros((500, 600), np.float32), [110.0, 0.05, 0.0, -10.0, 0.0, -0.05])
+    rc, gt, npx, nln, _ = oracle.suggested_warp_output(g2, wgs, wm, [0.0, 1.0, 0.0, 0.0, 0.0, 1.0])
+    assert rc == 0 and gt[1] > 0 and gt[5] < 0
+    bb = [12245143.98, -4865942.28, 15584728.71, -1118889.97]
+    px, ln = oracle.compute_reproject_extent(g2, wgs, wm, bb)
+    assert px == int((bb[2] - bb[0] + gt[1] / 2.0) / gt[1]) and ln == int((bb[3] - bb[1] - gt[5] / 2.0) / -gt[5])
