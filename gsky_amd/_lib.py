@@ -23,7 +23,7 @@ MAX_BIT_TESTS = 8
 
 ERRORS = {0: "OK", -1: "bad argument", -2: "raster type not implemented", -3: "HIP runtime error",
           -4: "unsupported CRS", -5: "bad mask", -6: "no HIP device", -7: "index out of range",
-          -8: "GDALSuggestedWarpOutput() failed",
+          -8: "GDALSuggestedWarpOutput() failed", -9: "warp service unreachable",
           1: "open failed", 2: "band failed", 3: "transformer failed"}
 
 
@@ -82,6 +82,8 @@ EXPORTS = [
     "gskyhip_drill_merge", "gskyhip_fnv32a", "gskyhip_version", "gskyhip_device_count",
     "gskyhip_render_status",
     "gskyhip_render_tile_info", "gskyhip_compute_reproject_extent",
+    "gskyhip_service_run", "gskyhip_service_register_granule", "gskyhip_service_unregister_all",
+    "gskyhip_service_stats", "gskyhip_service_shutdown",
 ]
 
 _lib = None
@@ -114,6 +116,12 @@ def lib() -> C.CDLL:
                                        vp, i64, vp]
     L.gskyhip_render_status.argtypes = [vp, ci, ci, ci, vp]
     L.gskyhip_compute_reproject_extent.argtypes = [vp, ci, vp, ci, ci, vp, vp, vp, vp]
+    L.gskyhip_service_run.argtypes = [C.c_char_p, ci, ci]
+    L.gskyhip_service_register_granule.argtypes = [C.c_char_p, C.c_char_p, ci, C.POINTER(Granule), vp,
+                                                   C.POINTER(vp), C.c_char_p]
+    L.gskyhip_service_unregister_all.argtypes = [C.c_char_p]
+    L.gskyhip_service_stats.argtypes = [C.c_char_p, C.POINTER(i64)]
+    L.gskyhip_service_shutdown.argtypes = [C.c_char_p]
     L.gskyhip_render_tile_info.argtypes = [vp, ci, ci, ci, vp, vp, vp]
     L.gskyhip_merge_rasters.argtypes = [C.POINTER(FlexRasterC), ci, C.POINTER(Mask), C.POINTER(vp), ci,
                                         C.POINTER(i32), C.POINTER(i32), C.POINTER(d), vp]

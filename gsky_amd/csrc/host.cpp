@@ -21,6 +21,8 @@
 #include "gsky_device.h"
 #include "render.h"
 #include "stages.h"
+#include "service.h"
+#include "warp_batch.h"
 
 using namespace gsky;
 
@@ -326,143 +328,234 @@ int gskyhip_unregister_all(void) {
   return 0;
 }
 
-// warp.go:82-382 drop-in.  Plans and warps on the GPU (one tile, one pair),
-// then hands the window back in malloc'd host memory.
+}  // extern "C"
+
+// ---------------------------------------------------------------- warp batches
+namespace gsky {
+
+// warp.go:82-382 for n requests at once: per request the registry lookup and
+// the reference's early returns (open / band / transformer failures), then
+// every request with the same destination SRS planned and warped in one set
+// of launches (one tile + one pair per request), bytesRead per request, and
+// one read-back.  The device buffer grows as needed and is kept.
+void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
+  DropIn &d = dropin();
+  std::lock_guard<std::mutex> lk(d.mu);
+  struct Item { int req; gskyhip_granule g; gskyhip_crs src; int bx, by; };
+  std::map<std::pair<int, std::string>, std::vector<Item>> groups;   // (has dst, dst srs) -> items
+  for (int i = 0; i < n; i++) {
+    const WarpReq &q = reqs[i];
+    WarpResp &r = out[i];
+    r = WarpResp();
+    // warp.go:89-101: "NETCDF:..." and "*.nc" are opened through GSKY_netCDF
+    // with band_query=<band>, which exposes that band as band 1; any other
+    // path is opened whole and GDALGetRasterBand(band) may fail (114-118).
+    const bool netcdf = q.path.compare(0, 7, "NETCDF:") == 0 ||
+                        (q.path.size() >= 3 && q.path.compare(q.path.size() - 3, 3, ".nc") == 0);
+    auto it = d.reg.find({q.path, q.band});
+    if (it == d.reg.end()) {
+      bool path_known = false;
+      for (const auto &kv : d.reg) if (kv.first.first == q.path) { path_known = true; break; }
+      r.rc = (netcdf || !path_known) ? 1 : 2;                         // open failed / band failed
+      continue;
+    }
+    const Registered &R = it->second;
+    if (!R.g.data) { r.rc = 2; continue; }                             // band failed
+    if (q.geoloc) { r.rc = 3; continue; }                              // geolocation arrays: unsupported
+    if (q.width <= 0 || q.height <= 0) { r.rc = GSKYHIP_E_ARG; continue; }
+    Item it2;
+    it2.req = i;
+    if (q.has_src_srs) {
+      if (parse_srs(q.src_srs.c_str(), &it2.src)) { r.rc = 3; continue; }
+    } else if (R.has_crs) {
+      it2.src = R.crs;
+    } else {
+      crs_epsg(4326, &it2.src);                                        // warp.go:107-112
+    }
+    if (q.has_dst_srs) {
+      gskyhip_crs tmp;
+      if (parse_srs(q.dst_srs.c_str(), &tmp)) { r.rc = 3; continue; }
+    }
+    it2.g = R.g;
+    it2.g.ns = 0;
+    if (q.has_src_gt) std::memcpy(it2.g.geot, q.src_gt, sizeof(it2.g.geot));
+    it2.bx = R.g.block_x > 0 ? R.g.block_x : 0;                      // 0: one scanline of the chosen level
+    it2.by = R.g.block_y > 0 ? R.g.block_y : 1;
+    groups[{q.has_dst_srs, q.has_dst_srs ? q.dst_srs : std::string()}].push_back(it2);
+  }
+  if (groups.empty()) return;
+  if (!have_gpu()) {
+    for (auto &kv : groups) for (const Item &it : kv.second) out[it.req].rc = GSKYHIP_E_NOGPU;
+    return;
+  }
+  if (!d.stream && hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess) {
+    for (auto &kv : groups) for (const Item &it : kv.second) out[it.req].rc = GSKYHIP_E_HIP;
+    return;
+  }
+  auto a256 = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
+  for (auto &kv : groups) {
+    const std::vector<Item> &items = kv.second;
+    const int m = (int)items.size();
+    int max_w = 1, max_h = 1;
+    int64_t st_bytes = 0;
+    std::vector<int64_t> n_px(m), n_words(m);
+    for (int k = 0; k < m; k++) {
+      const WarpReq &q = reqs[items[k].req];
+      max_w = std::max(max_w, q.width);
+      max_h = std::max(max_h, q.height);
+      const gskyhip_granule &g = items[k].g;
+      const int bx0 = items[k].bx > 0 ? items[k].bx : g.xsize;
+      const int64_t nblocks = ((int64_t)(g.xsize + bx0 - 1) / bx0) * ((g.ysize + items[k].by - 1) / items[k].by);
+      n_words[k] = (nblocks + 31) / 32;
+      n_px[k] = (int64_t)q.width * q.height;
+      st_bytes = std::max(st_bytes, a256(block_stats_scratch_bytes(n_px[k], n_words[k])));
+    }
+    // device layout: granules | crs (m sources + dst) | tiles | pairs | bbox | dtype | nodata | stats
+    //                | workspace | windows (m x stride) | block-stats scratch
+    const int64_t o_crs = a256((int64_t)m * sizeof(gskyhip_granule));
+    const int64_t o_tiles = o_crs + a256((int64_t)(m + 1) * sizeof(gskyhip_crs));
+    const int64_t o_pairs = o_tiles + a256((int64_t)m * sizeof(gskyhip_tile));
+    const int64_t o_bbox = o_pairs + a256((int64_t)m * 4);
+    const int64_t o_dtype = o_bbox + a256((int64_t)m * 16);
+    const int64_t o_nodata = o_dtype + a256((int64_t)m * 4);
+    const int64_t o_stats = o_nodata + a256((int64_t)m * 8);
+    const int64_t o_ws = o_stats + a256((int64_t)m * 16);
+    const int64_t ws = render_workspace_size(m, m, max_h);
+    const int64_t stride = a256((int64_t)max_w * max_h * 4);
+    const int64_t o_win = o_ws + a256(ws);
+    const int64_t o_scr = o_win + stride * m;
+    const size_t need = (size_t)(o_scr + st_bytes);
+    auto fail = [&](int code) { for (const Item &it : items) out[it.req].rc = code; };
+    if (d.dev_bytes < need) {
+      if (d.dev) hipFree(d.dev);
+      d.dev = nullptr;
+      d.dev_bytes = 0;
+      if (hipMalloc(&d.dev, need) != hipSuccess) { fail(GSKYHIP_E_HIP); continue; }
+      d.dev_bytes = need;
+    }
+    char *base = (char *)d.dev;
+    std::vector<char> hdr((size_t)o_ws, 0);
+    gskyhip_granule *hg = (gskyhip_granule *)hdr.data();
+    gskyhip_crs *hc = (gskyhip_crs *)(hdr.data() + o_crs);
+    gskyhip_tile *ht = (gskyhip_tile *)(hdr.data() + o_tiles);
+    int32_t *hp = (int32_t *)(hdr.data() + o_pairs);
+    int dst_crs = -1;
+    if (kv.first.first) {
+      parse_srs(kv.first.second.c_str(), &hc[m]);
+      dst_crs = m;
+    }
+    for (int k = 0; k < m; k++) {
+      const WarpReq &q = reqs[items[k].req];
+      hg[k] = items[k].g;
+      hg[k].crs = k;
+      hc[k] = items[k].src;
+      std::memcpy(ht[k].dst_geot, q.dst_gt, sizeof(ht[k].dst_geot));
+      ht[k].width = q.width;
+      ht[k].height = q.height;
+      ht[k].pair_begin = k;
+      ht[k].pair_end = k + 1;
+      hp[k] = k;
+    }
+    if (hipMemcpyAsync(base, hdr.data(), hdr.size(), hipMemcpyHostToDevice, d.stream) != hipSuccess) {
+      fail(GSKYHIP_E_HIP);
+      continue;
+    }
+    MaskSpecS ms[4];
+    std::memset(ms, 0, sizeof(ms));
+    RenderCall rc;
+    rc.granules = (const gskyhip_granule *)base; rc.n_granules = m;
+    rc.crs = (const gskyhip_crs *)(base + o_crs); rc.n_crs = m + 1; rc.dst_crs = dst_crs;
+    rc.tiles = (const gskyhip_tile *)(base + o_tiles); rc.n_tiles = m;
+    rc.pair_granule = (const int32_t *)(base + o_pairs); rc.n_pairs = m;
+    rc.max_w = max_w; rc.max_h = max_h;
+    rc.mask_ns = -1; rc.mask_inclusive = 0; rc.mask_specs = ms;
+    rc.resample = GSKYHIP_RESAMPLE_NEAREST;
+    rc.value_types = 0;
+    rc.cov_offsets = nullptr;
+    rc.cov_stride = 0;
+    rc.workspace = base + o_ws; rc.workspace_bytes = ws;
+    rc.stream = d.stream;
+    int32_t *dbbox = (int32_t *)(base + o_bbox), *ddt = (int32_t *)(base + o_dtype);
+    double *dnd = (double *)(base + o_nodata);
+    int32_t *dst = (int32_t *)(base + o_stats);
+    int code = launch_warp_windows(rc, dbbox, ddt, dnd, base + o_win, stride);
+    for (int k = 0; k < m && !code; k++)
+      code = launch_block_stats(rc, k, items[k].bx, items[k].by, base + o_scr, n_px[k], n_words[k], dst + 4 * k);
+    if (code) { fail(code); continue; }
+    std::vector<int32_t> bb(4 * m), dt(m), stv(4 * m);
+    std::vector<double> nd(m), gts(6 * m);
+    std::vector<PairPlan> pps(m);
+    hipMemcpyAsync(bb.data(), dbbox, 16 * m, hipMemcpyDeviceToHost, d.stream);
+    hipMemcpyAsync(dt.data(), ddt, 4 * m, hipMemcpyDeviceToHost, d.stream);
+    hipMemcpyAsync(nd.data(), dnd, 8 * m, hipMemcpyDeviceToHost, d.stream);
+    hipMemcpyAsync(stv.data(), dst, 16 * m, hipMemcpyDeviceToHost, d.stream);
+    // PairPlan[] opens the workspace; its src_gt is the overview-rescaled geotransform
+    hipMemcpyAsync(pps.data(), rc.workspace, sizeof(PairPlan) * m, hipMemcpyDeviceToHost, d.stream);
+    if (hipStreamSynchronize(d.stream) != hipSuccess) { fail(GSKYHIP_E_HIP); continue; }
+    for (int k = 0; k < m; k++) {
+      WarpResp &r = out[items[k].req];
+      for (int j = 0; j < 4; j++) r.bbox[j] = bb[4 * k + j];
+      r.dtype = dt[k];
+      r.nodata = nd[k];
+      r.bytes_read = stv[4 * k + 2];
+      std::memcpy(r.src_gt, pps[k].src_gt, sizeof(r.src_gt));
+      const int64_t sz = (int64_t)r.bbox[2] * r.bbox[3] * type_size(r.dtype);
+      r.data.resize((size_t)std::max<int64_t>(sz, 0));
+      if (sz > 0 && hipMemcpyAsync(r.data.data(), base + o_win + stride * k, (size_t)sz, hipMemcpyDeviceToHost,
+                                   d.stream) != hipSuccess)
+        r.rc = GSKYHIP_E_HIP;
+    }
+    if (hipStreamSynchronize(d.stream) != hipSuccess) fail(GSKYHIP_E_HIP);
+  }
+}
+
+}  // namespace gsky
+
+extern "C" {
+
+// warp.go:82 drop-in: one request through warp_batch -- in this process, or
+// forwarded to the per-node service when GSKYHIP_SERVICE names its socket
+// (service.cpp; the worker process then never touches the GPU).  The window
+// comes back in malloc'd host memory the caller frees (warp.go:573-574).
 int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGeot,
                         const char **geoLocOpts, const char *dstProjRef, double *dstGeot,
                         int dstXImageSize, int dstYImageSize, int band, int srsCf, void **dstBuf,
                         int *dstBufSize, int *dstBbox, double *noData, int *dType, int *bytesRead) {
-  (void)srsCf;
   *bytesRead = 0;
-  DropIn &d = dropin();
-  std::lock_guard<std::mutex> lk(d.mu);
   if (!srcFilePath) return 1;
-  const std::string path(srcFilePath);
-  // warp.go:89-101: "NETCDF:..." and "*.nc" are opened through GSKY_netCDF
-  // with band_query=<band>, which exposes that band as band 1; any other
-  // path is opened whole and GDALGetRasterBand(band) may fail (114-118).
-  const bool netcdf = path.compare(0, 7, "NETCDF:") == 0 ||
-                      (path.size() >= 3 && path.compare(path.size() - 3, 3, ".nc") == 0);
-  auto it = d.reg.find({path, band});
-  if (it == d.reg.end()) {
-    bool path_known = false;
-    for (const auto &kv : d.reg) if (kv.first.first == path) { path_known = true; break; }
-    return (netcdf || !path_known) ? 1 : 2;                          // open failed / band failed
-  }
-  const Registered &R = it->second;
-  if (!R.g.data) return 2;                                           // band failed
-  if (geoLocOpts) return 3;                                          // geolocation arrays: unsupported
-  if (!have_gpu()) return GSKYHIP_E_NOGPU;
-  gskyhip_crs crs[2];
-  if (srcProjRef) {
-    if (parse_srs(srcProjRef, &crs[0])) return 3;
-  } else if (R.has_crs) {
-    crs[0] = R.crs;
+  if (!dstGeot) return GSKYHIP_E_ARG;
+  WarpReq q;
+  q.path = srcFilePath;
+  q.band = band;
+  q.has_src_srs = srcProjRef ? 1 : 0;
+  if (srcProjRef) q.src_srs = srcProjRef;
+  q.has_src_gt = srcGeot ? 1 : 0;
+  if (srcGeot) std::memcpy(q.src_gt, srcGeot, sizeof(q.src_gt));
+  q.geoloc = geoLocOpts ? 1 : 0;
+  q.has_dst_srs = dstProjRef ? 1 : 0;
+  if (dstProjRef) q.dst_srs = dstProjRef;
+  std::memcpy(q.dst_gt, dstGeot, sizeof(q.dst_gt));
+  q.width = dstXImageSize;
+  q.height = dstYImageSize;
+  q.srs_cf = srsCf;
+  WarpResp r;
+  const char *svc = std::getenv("GSKYHIP_SERVICE");
+  if (svc && *svc) {
+    const int e = service_warp(svc, q, r);
+    if (e) return e;
   } else {
-    crs_epsg(4326, &crs[0]);                                         // warp.go:107-112
+    warp_batch(&q, 1, &r);
   }
-  int dst_crs = -1;
-  if (dstProjRef) {
-    if (parse_srs(dstProjRef, &crs[1])) return 3;
-    dst_crs = 1;
-  }
-  gskyhip_granule g = R.g;
-  g.crs = 0;
-  g.ns = 0;
-  if (srcGeot) std::memcpy(g.geot, srcGeot, sizeof(g.geot));
-  gskyhip_tile tile;
-  std::memcpy(tile.dst_geot, dstGeot, sizeof(tile.dst_geot));
-  tile.width = dstXImageSize;
-  tile.height = dstYImageSize;
-  tile.pair_begin = 0;
-  tile.pair_end = 1;
-  if (dstXImageSize <= 0 || dstYImageSize <= 0) return GSKYHIP_E_ARG;
-
-  if (!d.stream && hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess) return GSKYHIP_E_HIP;
-  const int64_t ws = render_workspace_size(1, 1, dstYImageSize);
-  const int64_t win_bytes = (int64_t)dstXImageSize * dstYImageSize * 4;
-  const int64_t hdr = 4096;
-  // bytesRead bookkeeping: block grid of level 0 (overviews have fewer blocks)
-  const int bx = R.g.block_x > 0 ? R.g.block_x : 0;    // 0: one scanline of the chosen level
-  const int by = R.g.block_y > 0 ? R.g.block_y : 1;
-  const int bx0 = bx > 0 ? bx : R.g.xsize;
-  const int64_t nblocks = ((int64_t)(R.g.xsize + bx0 - 1) / bx0) * ((R.g.ysize + by - 1) / by);
-  const int64_t n_words = (nblocks + 31) / 32;
-  const int64_t n_px = (int64_t)dstXImageSize * dstYImageSize;
-  const int64_t st_bytes = (block_stats_scratch_bytes(n_px, n_words) + 255) & ~(int64_t)255;
-  const size_t need = (size_t)(hdr + ws + win_bytes + 256 + st_bytes);
-  if (d.dev_bytes < need) {
-    if (d.dev) hipFree(d.dev);
-    d.dev = nullptr;
-    d.dev_bytes = 0;
-    if (hipMalloc(&d.dev, need) != hipSuccess) return GSKYHIP_E_HIP;
-    d.dev_bytes = need;
-  }
-  char *base = (char *)d.dev;
-  // header layout: granule | crs[2] | tile | pair | bbox | dtype | nodata
-  struct Hdr {
-    gskyhip_granule g;
-    gskyhip_crs crs[2];
-    gskyhip_tile tile;
-    int32_t pair;
-    int32_t bbox[4];
-    int32_t dtype;
-    double nodata;
-    int32_t stats[4];  // block_stats: first valid pixel, valid count, bytesRead
-  };
-  static_assert(sizeof(Hdr) <= 4096, "header");
-  Hdr h;
-  h.g = g;
-  h.crs[0] = crs[0];
-  h.crs[1] = crs[1];
-  h.tile = tile;
-  h.pair = 0;
-  Hdr *dh = (Hdr *)base;
-  if (hipMemcpyAsync(dh, &h, sizeof(Hdr), hipMemcpyHostToDevice, d.stream) != hipSuccess) return GSKYHIP_E_HIP;
-  MaskSpecS ms[4];
-  std::memset(ms, 0, sizeof(ms));
-  RenderCall rc;
-  rc.granules = &dh->g; rc.n_granules = 1;
-  rc.crs = dh->crs; rc.n_crs = 2; rc.dst_crs = dst_crs;
-  rc.tiles = &dh->tile; rc.n_tiles = 1;
-  rc.pair_granule = &dh->pair; rc.n_pairs = 1;
-  rc.max_w = dstXImageSize; rc.max_h = dstYImageSize;
-  rc.mask_ns = -1; rc.mask_inclusive = 0; rc.mask_specs = ms;
-  rc.resample = GSKYHIP_RESAMPLE_NEAREST;
-  rc.value_types = 0;
-  rc.cov_offsets = nullptr;
-  rc.cov_stride = 0;
-  rc.workspace = base + hdr; rc.workspace_bytes = ws;
-  rc.stream = d.stream;
-  char *win = base + hdr + ws;
-  int rcode = launch_warp_windows(rc, dh->bbox, &dh->dtype, &dh->nodata, win, win_bytes);
-  if (rcode) return rcode;
-  char *scratch = win + ((win_bytes + 255) & ~(int64_t)255);
-  rcode = launch_block_stats(rc, bx, by, scratch, n_px, n_words, dh->stats);
-  if (rcode) return rcode;
-  Hdr back;
-  if (hipMemcpyAsync(&back, dh, sizeof(Hdr), hipMemcpyDeviceToHost, d.stream) != hipSuccess) return GSKYHIP_E_HIP;
-  double gt_back[6];
-  // PairPlan of pair 0 sits at the start of the workspace; its src_gt is the
-  // overview-rescaled geotransform (warp.go:186-189)
-  hipMemcpyAsync(gt_back, rc.workspace, sizeof(gt_back), hipMemcpyDeviceToHost, d.stream);
-  if (hipStreamSynchronize(d.stream) != hipSuccess) return GSKYHIP_E_HIP;
-  const int w = back.bbox[2], hh = back.bbox[3];
-  const int dsz = type_size(back.dtype);
-  *dstBufSize = w * hh * dsz;
-  *dstBuf = std::malloc(*dstBufSize > 0 ? *dstBufSize : 1);
+  if (r.rc) return r.rc;
+  *dstBufSize = (int)r.data.size();
+  *dstBuf = std::malloc(r.data.empty() ? 1 : r.data.size());
   if (!*dstBuf) return GSKYHIP_E_ARG;
-  if (*dstBufSize > 0 &&
-      hipMemcpy(*dstBuf, win, (size_t)*dstBufSize, hipMemcpyDeviceToHost) != hipSuccess) {
-    std::free(*dstBuf);
-    *dstBuf = nullptr;
-    return GSKYHIP_E_HIP;
-  }
-  for (int k = 0; k < 4; k++) dstBbox[k] = back.bbox[k];
-  *noData = back.nodata;
-  *dType = back.dtype;
-  *bytesRead = back.stats[2];
-  if (srcGeot) std::memcpy(srcGeot, gt_back, sizeof(gt_back));
+  if (!r.data.empty()) std::memcpy(*dstBuf, r.data.data(), r.data.size());
+  for (int k = 0; k < 4; k++) dstBbox[k] = r.bbox[k];
+  *noData = r.nodata;
+  *dType = r.dtype;
+  *bytesRead = r.bytes_read;
+  if (srcGeot) std::memcpy(srcGeot, r.src_gt, sizeof(r.src_gt));
   return 0;
 }
 

@@ -35,9 +35,9 @@ int launch_extent(const gskyhip_granule *granules, int n, const gskyhip_crs *crs
                   int32_t *out, int32_t *status, hipStream_t s);
 int launch_warp_windows(const RenderCall &c, int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
                         void *win_out, int64_t win_stride);
-// bytesRead of the drop-in (pair 0 of a planned call): stats[2] receives it.
+// bytesRead of the drop-in (pair `pair` of a planned call): stats[2] receives it.
 int64_t block_stats_scratch_bytes(int64_t n_px, int64_t n_words);
-int launch_block_stats(const RenderCall &c, int bx, int by, void *scratch, int64_t n_px, int64_t n_words,
-                       int32_t *stats);
+int launch_block_stats(const RenderCall &c, int pair, int bx, int by, void *scratch, int64_t n_px,
+                       int64_t n_words, int32_t *stats);
 
 }  // namespace gsky

@@ -1285,8 +1285,8 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 
-int launch_block_stats(const RenderCall &rc, int bx, int by, void *scratch, int64_t n_px, int64_t n_words,
-                       int32_t *stats) {
+int launch_block_stats(const RenderCall &rc, int pair, int bx, int by, void *scratch, int64_t n_px,
+                       int64_t n_words, int32_t *stats) {
   const Carve cv = carve(rc.workspace, rc.n_tiles, rc.n_pairs, rc.max_h);
   int32_t *xsrc = (int32_t *)scratch;
   uint32_t *bits = (uint32_t *)((char *)scratch + align256(n_px * 4));
@@ -1295,9 +1295,9 @@ int launch_block_stats(const RenderCall &rc, int bx, int by, void *scratch, int6
   if (hipMemsetAsync(bits, 0, (size_t)n_words * 4, s) != hipSuccess) return GSKYHIP_E_HIP;
   if (hipMemcpyAsync(stats, init, sizeof(init), hipMemcpyHostToDevice, s) != hipSuccess) return GSKYHIP_E_HIP;
   if (n_px > 0)
-    hipLaunchKernelGGL(block_stats_kernel, dim3((unsigned)((n_px + 255) / 256)), dim3(256), 0, s, cv.pairs,
-                       cv.xforms, cv.rows, cv.pool, bx, by, xsrc, bits, stats);
-  hipLaunchKernelGGL(block_stats_resolve_kernel, dim3(1), dim3(64), 0, s, cv.pairs, bx, by, xsrc, bits,
+    hipLaunchKernelGGL(block_stats_kernel, dim3((unsigned)((n_px + 255) / 256)), dim3(256), 0, s, cv.pairs + pair,
+                       cv.xforms + pair, cv.rows + (int64_t)pair * rc.max_h, cv.pool, bx, by, xsrc, bits, stats);
+  hipLaunchKernelGGL(block_stats_resolve_kernel, dim3(1), dim3(64), 0, s, cv.pairs + pair, bx, by, xsrc, bits,
                      (int)n_words, stats);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }

@@ -1,0 +1,433 @@
+// service.cpp -- per-node GPU warp service: client side (forwarding from
+// warp_operation_fast) and the daemon loop (gskyhip_service_run, gskyhipd).
+// See service.h for the design.
+#include <errno.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/gskyhip.h"
+#include "gsky_device.h"
+#include "service.h"
+
+namespace gsky {
+namespace {
+
+// ---------------------------------------------------------------- framing
+struct Out {
+  std::vector<char> b;
+  template <typename T> void put(const T &v) {
+    const char *p = (const char *)&v;
+    b.insert(b.end(), p, p + sizeof(T));
+  }
+  void put_bytes(const void *p, size_t n) {
+    put<uint64_t>(n);
+    b.insert(b.end(), (const char *)p, (const char *)p + n);
+  }
+  void put_str(const std::string &s) { put_bytes(s.data(), s.size()); }
+};
+
+struct In {
+  const char *p, *e;
+  bool ok = true;
+  template <typename T> T get() {
+    T v{};
+    if (e - p < (ptrdiff_t)sizeof(T)) { ok = false; return v; }
+    std::memcpy(&v, p, sizeof(T));
+    p += sizeof(T);
+    return v;
+  }
+  std::string get_str() {
+    const uint64_t n = get<uint64_t>();
+    if (!ok || (uint64_t)(e - p) < n) { ok = false; return std::string(); }
+    std::string s(p, p + n);
+    p += n;
+    return s;
+  }
+  const char *get_bytes(uint64_t &n) {
+    n = get<uint64_t>();
+    if (!ok || (uint64_t)(e - p) < n) { ok = false; return nullptr; }
+    const char *q = p;
+    p += n;
+    return q;
+  }
+};
+
+bool write_all(int fd, const void *buf, size_t n) {
+  const char *p = (const char *)buf;
+  while (n > 0) {
+    const ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);   // a dead peer must not SIGPIPE the daemon
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    p += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+bool read_all(int fd, void *buf, size_t n) {
+  char *p = (char *)buf;
+  while (n > 0) {
+    const ssize_t k = ::recv(fd, p, n, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    p += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+bool send_msg(int fd, uint32_t op, const std::vector<char> &payload) {
+  char hdr[16];
+  const uint64_t n = payload.size();
+  std::memcpy(hdr, &kSvcMagic, 4);
+  std::memcpy(hdr + 4, &op, 4);
+  std::memcpy(hdr + 8, &n, 8);
+  return write_all(fd, hdr, 16) && (n == 0 || write_all(fd, payload.data(), n));
+}
+
+bool recv_msg(int fd, uint32_t &op, std::vector<char> &payload) {
+  char hdr[16];
+  if (!read_all(fd, hdr, 16)) return false;
+  uint32_t magic;
+  uint64_t n;
+  std::memcpy(&magic, hdr, 4);
+  std::memcpy(&op, hdr + 4, 4);
+  std::memcpy(&n, hdr + 8, 8);
+  if (magic != kSvcMagic || n > (1ull << 36)) return false;
+  payload.resize(n);
+  return n == 0 || read_all(fd, payload.data(), n);
+}
+
+int connect_to(const char *sock) {
+  const int fd = ::socket(AF_UNIX, SOCK_STREAM, 0);
+  if (fd < 0) return -1;
+  sockaddr_un a;
+  std::memset(&a, 0, sizeof(a));
+  a.sun_family = AF_UNIX;
+  std::strncpy(a.sun_path, sock, sizeof(a.sun_path) - 1);
+  if (::connect(fd, (sockaddr *)&a, sizeof(a)) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  return fd;
+}
+
+// one request / reply exchange on a fresh connection
+bool exchange(const char *sock, uint32_t op, const std::vector<char> &req, std::vector<char> &rep) {
+  const int fd = connect_to(sock);
+  if (fd < 0) return false;
+  uint32_t rop = 0;
+  const bool ok = send_msg(fd, op, req) && recv_msg(fd, rop, rep) && rop == op;
+  ::close(fd);
+  return ok;
+}
+
+void put_req(Out &o, const WarpReq &q) {
+  o.put_str(q.path);
+  o.put(q.band);
+  o.put(q.has_src_srs); o.put(q.has_src_gt); o.put(q.geoloc); o.put(q.has_dst_srs);
+  o.put_str(q.src_srs);
+  o.put_str(q.dst_srs);
+  for (double v : q.src_gt) o.put(v);
+  for (double v : q.dst_gt) o.put(v);
+  o.put(q.width); o.put(q.height); o.put(q.srs_cf);
+}
+
+bool get_req(In &in, WarpReq &q) {
+  q.path = in.get_str();
+  q.band = in.get<int32_t>();
+  q.has_src_srs = in.get<int32_t>(); q.has_src_gt = in.get<int32_t>();
+  q.geoloc = in.get<int32_t>(); q.has_dst_srs = in.get<int32_t>();
+  q.src_srs = in.get_str();
+  q.dst_srs = in.get_str();
+  for (double &v : q.src_gt) v = in.get<double>();
+  for (double &v : q.dst_gt) v = in.get<double>();
+  q.width = in.get<int32_t>(); q.height = in.get<int32_t>(); q.srs_cf = in.get<int32_t>();
+  return in.ok;
+}
+
+void put_resp(Out &o, const WarpResp &r) {
+  o.put(r.rc);
+  for (int32_t v : r.bbox) o.put(v);
+  o.put(r.nodata); o.put(r.dtype); o.put(r.bytes_read);
+  for (double v : r.src_gt) o.put(v);
+  o.put_bytes(r.data.data(), r.data.size());
+}
+
+bool get_resp(In &in, WarpResp &r) {
+  r.rc = in.get<int32_t>();
+  for (int32_t &v : r.bbox) v = in.get<int32_t>();
+  r.nodata = in.get<double>(); r.dtype = in.get<int32_t>(); r.bytes_read = in.get<int32_t>();
+  for (double &v : r.src_gt) v = in.get<double>();
+  uint64_t n = 0;
+  const char *p = in.get_bytes(n);
+  if (!in.ok) return false;
+  r.data.assign(p, p + n);
+  return true;
+}
+
+// ---------------------------------------------------------------- daemon state
+struct Pending {
+  WarpReq q;
+  WarpResp r;
+  bool done = false;
+};
+
+struct Service {
+  std::mutex mu;
+  std::condition_variable cv_queue, cv_done;
+  std::deque<std::shared_ptr<Pending>> queue;
+  std::atomic<bool> stop{false};
+  int max_batch = 64;
+  int window_us = 500;
+  int listen_fd = -1;
+  // statistics: warp requests, batches, largest batch, registered granules
+  std::atomic<int64_t> n_req{0}, n_batches{0}, max_seen{0}, n_reg{0};
+  std::mutex reg_mu;
+  std::vector<void *> device_allocs;   // granule data uploaded through SVC_REGISTER
+};
+
+Service *g_svc = nullptr;
+
+// The batching thread: waits for work, lets the window fill (up to max_batch),
+// runs one warp_batch over everything it took.
+void batch_loop(Service *s) {
+  for (;;) {
+    std::vector<std::shared_ptr<Pending>> take;
+    {
+      std::unique_lock<std::mutex> lk(s->mu);
+      s->cv_queue.wait(lk, [&] { return s->stop || !s->queue.empty(); });
+      if (s->stop && s->queue.empty()) return;
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(s->window_us);
+      s->cv_queue.wait_until(lk, until, [&] { return s->stop || (int)s->queue.size() >= s->max_batch; });
+      while (!s->queue.empty() && (int)take.size() < s->max_batch) {
+        take.push_back(s->queue.front());
+        s->queue.pop_front();
+      }
+    }
+    const int m = (int)take.size();
+    std::vector<WarpReq> reqs(m);
+    std::vector<WarpResp> resps(m);
+    for (int i = 0; i < m; i++) reqs[i] = take[i]->q;
+    {
+      std::lock_guard<std::mutex> rl(s->reg_mu);   // registrations do not race a batch
+      warp_batch(reqs.data(), m, resps.data());
+    }
+    s->n_batches++;
+    int64_t prev = s->max_seen.load();
+    while (m > prev && !s->max_seen.compare_exchange_weak(prev, m)) {}
+    {
+      std::lock_guard<std::mutex> lk(s->mu);
+      for (int i = 0; i < m; i++) {
+        take[i]->r = std::move(resps[i]);
+        take[i]->done = true;
+      }
+    }
+    s->cv_done.notify_all();
+  }
+}
+
+// SVC_REGISTER payload: path, band, srs, granule header (host struct; data
+// pointers ignored), level-0 bytes, n_ovr x overview bytes.
+int do_register(Service *s, In &in) {
+  const std::string path = in.get_str();
+  const int32_t band = in.get<int32_t>();
+  const std::string srs = in.get_str();
+  gskyhip_granule g = in.get<gskyhip_granule>();
+  if (!in.ok || g.n_ovr < 0 || g.n_ovr > GSKYHIP_MAX_OVR) return GSKYHIP_E_ARG;
+  std::lock_guard<std::mutex> rl(s->reg_mu);
+  auto upload = [&](const char *p, uint64_t n, void **dev) -> int {
+    if (hipMalloc(dev, n > 0 ? n : 1) != hipSuccess) return GSKYHIP_E_HIP;
+    s->device_allocs.push_back(*dev);
+    if (n > 0 && hipMemcpy(*dev, p, n, hipMemcpyHostToDevice) != hipSuccess) return GSKYHIP_E_HIP;
+    return 0;
+  };
+  uint64_t n = 0;
+  const char *p = in.get_bytes(n);
+  if (!in.ok || n != (uint64_t)g.xsize * g.ysize * type_size(g.dtype)) return GSKYHIP_E_ARG;
+  void *dev = nullptr;
+  int e = upload(p, n, &dev);
+  if (e) return e;
+  g.data = dev;
+  for (int k = 0; k < g.n_ovr; k++) {
+    const char *po = in.get_bytes(n);
+    if (!in.ok || n != (uint64_t)g.ovr_xsize[k] * g.ovr_ysize[k] * type_size(g.dtype)) return GSKYHIP_E_ARG;
+    void *od = nullptr;
+    if ((e = upload(po, n, &od))) return e;
+    g.ovr_data[k] = od;
+  }
+  e = gskyhip_register_granule(path.c_str(), band, &g, srs.empty() ? nullptr : srs.c_str());
+  if (!e) s->n_reg++;
+  return e;
+}
+
+void conn_loop(Service *s, int fd) {
+  for (;;) {
+    uint32_t op = 0;
+    std::vector<char> payload;
+    if (!recv_msg(fd, op, payload)) break;
+    In in{payload.data(), payload.data() + payload.size()};
+    Out o;
+    if (op == SVC_WARP) {
+      auto pd = std::make_shared<Pending>();
+      if (!get_req(in, pd->q)) break;
+      s->n_req++;
+      {
+        std::unique_lock<std::mutex> lk(s->mu);
+        s->queue.push_back(pd);
+        s->cv_queue.notify_one();
+        s->cv_done.wait(lk, [&] { return pd->done; });
+      }
+      put_resp(o, pd->r);
+    } else if (op == SVC_REGISTER) {
+      o.put<int32_t>(do_register(s, in));
+    } else if (op == SVC_UNREGISTER_ALL) {
+      std::lock_guard<std::mutex> rl(s->reg_mu);
+      gskyhip_unregister_all();
+      for (void *p : s->device_allocs) hipFree(p);
+      s->device_allocs.clear();
+      s->n_reg = 0;
+      o.put<int32_t>(0);
+    } else if (op == SVC_STATS) {
+      o.put<int64_t>(s->n_req.load()); o.put<int64_t>(s->n_batches.load());
+      o.put<int64_t>(s->max_seen.load()); o.put<int64_t>(s->n_reg.load());
+    } else if (op == SVC_SHUTDOWN) {
+      o.put<int32_t>(0);
+      send_msg(fd, op, o.b);
+      s->stop = true;
+      s->cv_queue.notify_all();
+      ::shutdown(s->listen_fd, SHUT_RDWR);
+      break;
+    } else {
+      break;
+    }
+    if (!send_msg(fd, op, o.b)) break;   // the worker died (SIGKILL): drop the reply
+  }
+  ::close(fd);
+}
+
+}  // namespace
+
+int service_warp(const char *sock, const WarpReq &q, WarpResp &r) {
+  Out o;
+  put_req(o, q);
+  std::vector<char> rep;
+  if (!exchange(sock, SVC_WARP, o.b, rep)) return GSKYHIP_E_SERVICE;
+  In in{rep.data(), rep.data() + rep.size()};
+  return get_resp(in, r) ? 0 : GSKYHIP_E_SERVICE;
+}
+
+}  // namespace gsky
+
+using namespace gsky;
+
+extern "C" {
+
+int gskyhip_service_run(const char *socket_path, int max_batch, int window_us) {
+  if (!socket_path || !*socket_path || std::strlen(socket_path) >= sizeof(sockaddr_un::sun_path))
+    return GSKYHIP_E_ARG;
+  Service s;
+  s.max_batch = std::max(1, max_batch);
+  s.window_us = std::max(0, window_us);
+  const int fd = ::socket(AF_UNIX, SOCK_STREAM, 0);
+  if (fd < 0) return GSKYHIP_E_SERVICE;
+  sockaddr_un a;
+  std::memset(&a, 0, sizeof(a));
+  a.sun_family = AF_UNIX;
+  std::strncpy(a.sun_path, socket_path, sizeof(a.sun_path) - 1);
+  ::unlink(socket_path);
+  if (::bind(fd, (sockaddr *)&a, sizeof(a)) != 0 || ::listen(fd, 256) != 0) {
+    ::close(fd);
+    return GSKYHIP_E_SERVICE;
+  }
+  s.listen_fd = fd;
+  g_svc = &s;
+  std::thread batcher(batch_loop, &s);
+  std::vector<std::thread> conns;
+  while (!s.stop) {
+    const int c = ::accept(fd, nullptr, nullptr);
+    if (c < 0) {
+      if (errno == EINTR) continue;
+      break;
+    }
+    conns.emplace_back(conn_loop, &s, c);
+  }
+  s.stop = true;
+  s.cv_queue.notify_all();
+  batcher.join();
+  {   // release connections still waiting on a batch
+    std::lock_guard<std::mutex> lk(s.mu);
+    for (auto &p : s.queue) { p->r.rc = GSKYHIP_E_SERVICE; p->done = true; }
+    s.queue.clear();
+  }
+  s.cv_done.notify_all();
+  for (auto &t : conns) t.join();
+  ::close(fd);
+  ::unlink(socket_path);
+  gskyhip_unregister_all();
+  for (void *p : s.device_allocs) hipFree(p);
+  g_svc = nullptr;
+  return 0;
+}
+
+int gskyhip_service_register_granule(const char *socket_path, const char *path, int band,
+                                     const gskyhip_granule *g, const void *data, const void *const *ovr_data,
+                                     const char *srs) {
+  if (!socket_path || !path || !g || !data) return GSKYHIP_E_ARG;
+  if (g->n_ovr < 0 || g->n_ovr > GSKYHIP_MAX_OVR || (g->n_ovr > 0 && !ovr_data)) return GSKYHIP_E_ARG;
+  const int ts = type_size(g->dtype);
+  if (ts <= 0) return GSKYHIP_E_TYPE;
+  Out o;
+  o.put_str(path);
+  o.put<int32_t>(band);
+  o.put_str(srs ? srs : "");
+  o.put(*g);
+  o.put_bytes(data, (size_t)g->xsize * g->ysize * ts);
+  for (int k = 0; k < g->n_ovr; k++) o.put_bytes(ovr_data[k], (size_t)g->ovr_xsize[k] * g->ovr_ysize[k] * ts);
+  std::vector<char> rep;
+  if (!exchange(socket_path, SVC_REGISTER, o.b, rep) || rep.size() < 4) return GSKYHIP_E_SERVICE;
+  int32_t rc;
+  std::memcpy(&rc, rep.data(), 4);
+  return rc;
+}
+
+int gskyhip_service_unregister_all(const char *socket_path) {
+  std::vector<char> rep;
+  if (!socket_path || !exchange(socket_path, SVC_UNREGISTER_ALL, {}, rep) || rep.size() < 4)
+    return GSKYHIP_E_SERVICE;
+  int32_t rc;
+  std::memcpy(&rc, rep.data(), 4);
+  return rc;
+}
+
+int gskyhip_service_stats(const char *socket_path, int64_t *stats) {
+  std::vector<char> rep;
+  if (!socket_path || !stats || !exchange(socket_path, SVC_STATS, {}, rep) || rep.size() < 32)
+    return GSKYHIP_E_SERVICE;
+  std::memcpy(stats, rep.data(), 32);
+  return 0;
+}
+
+int gskyhip_service_shutdown(const char *socket_path) {
+  std::vector<char> rep;
+  if (!socket_path || !exchange(socket_path, SVC_SHUTDOWN, {}, rep)) return GSKYHIP_E_SERVICE;
+  return 0;
+}
+
+}  // extern "C"

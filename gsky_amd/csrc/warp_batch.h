@@ -1,0 +1,44 @@
+// warp_batch.h -- warp_operation_fast (worker/gdalprocess/warp.go:82-382) as
+// a batch: n independent requests (each one (tile, granule) pair) planned and
+// warped in ONE set of launches.  The C-ABI drop-in calls it with n = 1; the
+// per-node service (service.cpp) with every request that arrived from the N
+// worker processes within its batching window.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace gsky {
+
+// One warp_operation_fast call, by value (the strings and geotransforms the
+// caller owns are copied).
+struct WarpReq {
+  std::string path;
+  int32_t band = 1;
+  int32_t has_src_srs = 0, has_src_gt = 0, geoloc = 0, has_dst_srs = 0;
+  std::string src_srs, dst_srs;
+  double src_gt[6] = {0, 0, 0, 0, 0, 0};
+  double dst_gt[6] = {0, 0, 0, 0, 0, 0};
+  int32_t width = 0, height = 0, srs_cf = 0;
+};
+
+// Its outputs: return code (0, 1 open failed, 2 band failed, 3 transformer
+// failed, or a GSKYHIP_E_* code), window bbox / nodata / dtype / bytesRead,
+// the overview-rescaled source geotransform (warp.go:186-189) and the window
+// bytes (bbox[2] x bbox[3] values of dtype).
+struct WarpResp {
+  int32_t rc = 0;
+  int32_t bbox[4] = {0, 0, 0, 0};
+  double nodata = 0;
+  int32_t dtype = 0;
+  int32_t bytes_read = 0;
+  double src_gt[6] = {0, 0, 0, 0, 0, 0};
+  std::vector<char> data;
+};
+
+// Runs the batch against this process's granule registry (HBM-resident,
+// gskyhip_register_granule).  Thread-safe (one batch at a time).
+void warp_batch(const WarpReq *reqs, int n, WarpResp *out);
+
+}  // namespace gsky

@@ -38,6 +38,7 @@ extern "C" {
 #define GSKYHIP_E_NOGPU (-6)       /* no HIP device                            */
 #define GSKYHIP_E_RANGE (-7)       /* index out of range (Go would panic)      */
 #define GSKYHIP_E_XFORM (-8)       /* GDALSuggestedWarpOutput() failed         */
+#define GSKYHIP_E_SERVICE (-9)     /* per-node service unreachable / protocol  */
 
 /* ---- raster data types: GDALDataType codes (warp.go:428-431) + 100 ------- */
 #define GSKYHIP_BYTE 1
@@ -263,6 +264,25 @@ int gskyhip_warp_windows(const gskyhip_granule *granules, int n_granules,
 int gskyhip_compute_reproject_extent(const gskyhip_granule *granules, int n, const gskyhip_crs *crs_table,
                                      int n_crs, int dst_crs, const double *dst_bbox, int32_t *out,
                                      int32_t *status, void *stream);
+
+/* ---- per-node warp service (SURVEY 8b threading contract, 8f row 1) ------
+ * The reference runs N = NumCPU single-threaded gsky-gdal-process workers per
+ * node (grpc-server/main.go:58, gdal-process/main.go:115-123; pool.go:19-74
+ * and process.go:108-160 spawn, feed and kill them).  One daemon per GPU
+ * (gskyhipd = gskyhip_service_run) owns the HIP context and the HBM-resident
+ * granules; a worker whose environment has GSKYHIP_SERVICE=<socket> sends
+ * each warp_operation_fast call there over a Unix socket and never touches
+ * the GPU, so N workers share one context and a SIGKILLed worker leaves no
+ * device state.  The daemon plans and warps every request that arrived within
+ * `window_us` (up to `max_batch`) in one launch set.  All pointers are host. */
+int gskyhip_service_run(const char *socket_path, int max_batch, int window_us);   /* blocks until shutdown */
+int gskyhip_service_register_granule(const char *socket_path, const char *path, int band,
+                                     const gskyhip_granule *g, const void *data, const void *const *ovr_data,
+                                     const char *srs);   /* data / ovr_data: host arrays, uploaded by the daemon */
+int gskyhip_service_unregister_all(const char *socket_path);
+/* stats[4]: warp requests served, batches run, largest batch, registered granules */
+int gskyhip_service_stats(const char *socket_path, int64_t *stats);
+int gskyhip_service_shutdown(const char *socket_path);
 
 /* ---- standalone stages (the reference's own operator boundaries) -------- */
 /* FlexRaster (tile_types.go:95-106) as flat fields; data is dev. */

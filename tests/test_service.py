@@ -1,0 +1,165 @@
+"""Per-node GPU warp service (gskyhipd; include/gskyhip.h, gsky_amd/service.py).
+
+N worker processes -- the reference's gsky-gdal-process pool (pool.go:19-74,
+process.go:108-160, grpc-server/main.go:58) -- call the unchanged
+warp_operation_fast C-ABI with GSKYHIP_SERVICE set and never open the GPU; one
+daemon per GPU batches their requests.
+
+CPU tests (no GPU): the socket protocol, the batching queue and the
+reference's early returns across processes, a client dying mid-message, an
+unreachable service.  GPU test: 8 workers x their (tile, granule) warps of a
+C2 batch against the oracle (bit-exact windows, bbox, nodata, bytesRead),
+batches larger than one request, and a worker SIGKILLed mid-stream.
+"""
+import multiprocessing as mp
+import os
+import signal
+import socket
+import tempfile
+import time
+
+import pytest
+
+from gsky_amd import synth
+
+
+def _sock_path():
+    return os.path.join(tempfile.mkdtemp(prefix="gskyhip-"), "svc.sock")
+
+
+def _unknown_paths(sock, n, q):
+    os.environ["GSKYHIP_SERVICE"] = sock
+    from gsky_amd import worker as W
+    out = []
+    for i in range(n):
+        r = W.warp_raster(W.GeoRPCGranule(path="/nope/%d.tif" % i, bands=[1], width=8, height=8,
+                                          dstSRS="EPSG:3857", dstGeot=[0.0, 1.0, 0.0, 0.0, 0.0, -1.0]))
+        out.append(r.error)
+    q.put(out)
+
+
+def test_service_protocol_and_batching_queue():
+    from gsky_amd import WarpService
+    sock = _sock_path()
+    svc = WarpService(sock, max_batch=16, window_us=2000)
+    try:
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        procs = [ctx.Process(target=_unknown_paths, args=(sock, 8, q)) for _ in range(4)]
+        for p in procs:
+            p.start()
+        errs = [e for _ in procs for e in q.get(timeout=120)]
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+        # GDALOpenEx fails for an unregistered path: warp.go:103-105 -> "fail: 1"
+        assert errs == ["warp_operation() fail: 1"] * 32
+        st = svc.stats()
+        assert st["requests"] == 32 and 1 <= st["batches"] <= 32 and st["max_batch"] >= 1
+        # a client that dies in the middle of a message does not take the daemon down
+        c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        c.connect(sock)
+        c.send(b"GSKY\x01\x00")
+        c.close()
+        q2 = ctx.Queue()
+        p = ctx.Process(target=_unknown_paths, args=(sock, 1, q2))
+        p.start()
+        assert q2.get(timeout=60) == ["warp_operation() fail: 1"]
+        p.join(60)
+        assert svc.stats()["requests"] == 33
+    finally:
+        assert svc.shutdown() == 0
+    assert not os.path.exists(sock)
+
+
+def test_service_unreachable():
+    """No daemon behind GSKYHIP_SERVICE: the drop-in reports the failure (the
+    OWS retries an errored request, process.go:147-150)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_unknown_paths, args=(_sock_path(), 1, q))
+    p.start()
+    assert q.get(timeout=60) == ["warp_operation() fail: -9"]
+    p.join(60)
+
+
+# ---------------------------------------------------------------- GPU
+def _warp_jobs(sock, wid, jobs, q):
+    """A worker process: warp_raster over the service for its (tile, granule) jobs."""
+    os.environ["GSKYHIP_SERVICE"] = sock
+    from gsky_amd import worker as W
+    res = []
+    for (k, gt, w, h) in jobs:
+        r = W.warp_raster(W.GeoRPCGranule(path="/g/data/c2/g%d.tif" % k, bands=[1], width=w, height=h,
+                                          dstSRS="EPSG:3857", dstGeot=list(gt)))
+        res.append((r.error, r.raster.data if r.raster else b"", r.raster.bbox if r.raster else [],
+                    r.raster.noData if r.raster else 0.0, r.raster.rasterType if r.raster else "", r.bytesRead))
+    q.put((wid, res))
+
+
+def _spin(sock, job):
+    os.environ["GSKYHIP_SERVICE"] = sock
+    from gsky_amd import worker as W
+    k, gt, w, h = job
+    while True:
+        W.warp_raster(W.GeoRPCGranule(path="/g/data/c2/g%d.tif" % k, bands=[1], width=w, height=h,
+                                      dstSRS="EPSG:3857", dstGeot=list(gt)))
+
+
+@pytest.mark.gpu
+def test_service_workers_share_one_gpu(oracle):
+    """8 worker processes (no HIP context of their own) warp every (tile,
+    granule) pair of a C2 batch through one gskyhipd: each window bit-exact
+    against the oracle, requests batched across workers, a SIGKILLed worker
+    leaving the daemon serving."""
+    from gsky_amd import WarpService
+    from gsky_amd.tiles import bbox_to_geot
+    cfg = synth.config_c2(scale=0.1, tiles_per_side=4, tile_px=256)
+    sock = _sock_path()
+    svc = WarpService(sock, max_batch=64, window_us=2000)
+    try:
+        for k, g in enumerate(cfg.granules):
+            svc.register_granule("/g/data/c2/g%d.tif" % k, 1, g.data, g.geot, "EPSG:3577", g.nodata,
+                                 block=(128, 64))
+        assert svc.stats()["granules"] == len(cfg.granules)
+        jobs = [(k, bbox_to_geot(w, h, bb), w, h) for (bb, w, h), ks in zip(cfg.tiles, cfg.pairs) for k in ks]
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        n_workers = 8
+        procs = [ctx.Process(target=_warp_jobs, args=(sock, r, jobs[r::n_workers], q)) for r in range(n_workers)]
+        for p in procs:
+            p.start()
+        got = dict(q.get(timeout=300) for _ in procs)
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+        aea, wm = oracle.crs("EPSG:3577"), oracle.crs("EPSG:3857")
+        n_checked = 0
+        for r in range(n_workers):
+            for (k, gt, w, h), (err, data, bbox, nd, rtype, br) in zip(jobs[r::n_workers], got[r]):
+                g = cfg.granules[k]
+                og = oracle.make_granule(g.data, g.geot, g.nodata, block=(128, 64))
+                arr, ebbox, end, _ = oracle.warp(og, aea, wm, list(gt), w, h)
+                assert err == "OK" and bbox == list(ebbox), (k, gt, err)
+                assert data == arr.tobytes() and nd == end and rtype == "Int16", (k, gt)
+                assert br == oracle.warp.bytes_read, (k, gt)               # warp.go:347
+                n_checked += 1
+        assert n_checked == len(jobs)
+        st = svc.stats()
+        assert st["requests"] == len(jobs) and st["max_batch"] > 1 and st["batches"] < len(jobs), st
+        # a worker SIGKILLed while its requests are in flight (gdal-process is killed after 120 s,
+        # gdal-process/main.go:57-68): the daemon keeps serving
+        p = ctx.Process(target=_spin, args=(sock, jobs[0]))
+        p.start()
+        time.sleep(3.0)
+        os.kill(p.pid, signal.SIGKILL)
+        p.join(30)
+        q2 = ctx.Queue()
+        p2 = ctx.Process(target=_warp_jobs, args=(sock, 0, jobs[:3], q2))
+        p2.start()
+        _, again = q2.get(timeout=120)
+        p2.join(60)
+        assert [e for e, *_ in again] == ["OK"] * 3
+        assert svc.stats()["requests"] > st["requests"] + 3
+    finally:
+        assert svc.shutdown() == 0
