@@ -28,6 +28,36 @@ struct DrillCall {
   hipStream_t stream;
 };
 
+// computeDeciles (drill.go:229-273) for a batch of polygons: see
+// gskyhip_drill_deciles in include/gskyhip.h.
+struct DecileCall {
+  const float *stack;
+  int xsize, ysize, n_bands, t_stride;
+  const int32_t *win;
+  const int64_t *mask_off;
+  const uint8_t *masks;
+  int n_polys;
+  int64_t mask_bytes;
+  const int32_t *bands;        // HOST band list (1-based) or NULL = 1..n_bands
+  int n_list;
+  float nodata;
+  int decile_count, band_chunk;
+  const int32_t *totals;       // dev n_polys x n_list: the mean pass's totals (drill.go:172-191)
+  float *out;                  // dev n_polys x n_list x decile_count
+  int32_t *status;             // dev n_polys x n_list
+  void *workspace;
+  int64_t workspace_bytes;
+  hipStream_t stream;
+};
+
+__global__ __launch_bounds__(256) void drill_compact_kernel(const int32_t *__restrict__ win,
+                                                            const int64_t *__restrict__ mask_off,
+                                                            const uint8_t *__restrict__ masks, int n_polys,
+                                                            int xsize, int ysize, int32_t *__restrict__ idx,
+                                                            int32_t *__restrict__ count);
+int64_t drill_deciles_workspace_size(int n_polys, int64_t mask_bytes, int band_chunk);
+int launch_drill_deciles(const DecileCall &c);
+
 int drill_rows_per_poly(int n_list, int band_strides);
 int64_t drill_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides, int mode);
 int launch_drill_batch(const DrillCall &c);

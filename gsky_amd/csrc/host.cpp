@@ -727,6 +727,26 @@ int gskyhip_compute_reproject_extent(const gskyhip_granule *granules, int n, con
   return launch_extent(granules, n, crs_table, dst_crs, dst_bbox, out, status, (hipStream_t)stream);
 }
 
+int64_t gskyhip_drill_deciles_workspace_size(int n_polys, int64_t mask_bytes, int band_chunk) {
+  return drill_deciles_workspace_size(n_polys, mask_bytes, band_chunk);
+}
+
+// computeDeciles (drill.go:229-273) for a polygon batch: segmented GPU sort.
+int gskyhip_drill_deciles(const float *stack, int xsize, int ysize, int n_bands, int t_stride, const int32_t *win,
+                          const int64_t *mask_off, const uint8_t *masks, int n_polys, int64_t mask_bytes,
+                          const int32_t *bands, int n_list, float nodata, int decile_count, int band_chunk,
+                          const int32_t *totals, float *out, int32_t *status, void *workspace,
+                          int64_t workspace_bytes, void *stream) {
+  if (!stack || !win || !mask_off || !masks || !totals || !out || !status) return GSKYHIP_E_ARG;
+  DecileCall c;
+  c.stack = stack; c.xsize = xsize; c.ysize = ysize; c.n_bands = n_bands; c.t_stride = t_stride;
+  c.win = win; c.mask_off = mask_off; c.masks = masks; c.n_polys = n_polys; c.mask_bytes = mask_bytes;
+  c.bands = bands; c.n_list = n_list; c.nodata = nodata; c.decile_count = decile_count;
+  c.band_chunk = band_chunk; c.totals = totals; c.out = out; c.status = status;
+  c.workspace = workspace; c.workspace_bytes = workspace_bytes; c.stream = (hipStream_t)stream;
+  return launch_drill_deciles(c);
+}
+
 // RasterMerger.Run for one batch over warped FlexRasters (tile_merger.go:447-503).
 int gskyhip_merge_rasters(const gskyhip_flex_raster *rasters, int n, const gskyhip_mask *mask,
                           void *const *canvases, int n_ns, int32_t *created, int32_t *dtype, double *nodata,

@@ -126,10 +126,26 @@ def read_data(stack: DrillStack, win, mask_off=None, masks=None, clip_lower: flo
     counts i32), each (n_polys, rows) with rows = len(TimeSeries) / nCols of
     drill.go:225.  `win` is a MaskBatch (or the round-1 (win, mask_off,
     masks) tensors); `bands` the reference's 1-based band list (default all);
-    mode REFERENCE_ORDER is bit-exact, WAVE_SPLIT within 1e-5 relative."""
-    if decile_count:
-        raise NotImplementedError("drill deciles (drill.go:229-273) are SURVEY 8f 'next'")
+    mode REFERENCE_ORDER is bit-exact, WAVE_SPLIT within 1e-5 relative.
+    decile_count > 0 (band_strides 1): values / counts (n_polys, rows, 1 +
+    decile_count), each row [mean, decile 1..k] as the reference's TimeSeries
+    (drill.go:172-191: Count 1 per decile, zeros with Count 0 where the band
+    total is 0); the deciles by segmented GPU sort (gskyhip_drill_deciles)."""
     mb = win if isinstance(win, MaskBatch) else MaskBatch(win, mask_off, masks)
+    if decile_count:
+        if band_strides > 1:
+            raise NotImplementedError("deciles with bandStrides > 1 (drill.go:197-218 interpolates mean rows)")
+        vals, cnts = read_data(stack, mb, clip_lower=clip_lower, clip_upper=clip_upper, pixel_count=pixel_count,
+                               band_strides=1, bands=bands, mode=mode)
+        dec, st = compute_deciles(stack, mb, cnts, decile_count, bands)
+        bad = st == -7
+        if bool(bad.any()):
+            from ._lib import GskyError
+            raise GskyError(-7, "computeDeciles indexes past the values (the reference panics)")
+        ok = (st == 0).unsqueeze(-1)
+        dv = torch.where(ok, dec.to(torch.float64), torch.zeros_like(dec, dtype=torch.float64))
+        dcnt = ok.to(torch.int32).expand(-1, -1, decile_count)
+        return torch.cat([vals.unsqueeze(-1), dv], -1), torch.cat([cnts.unsqueeze(-1), dcnt], -1)
     n_polys = mb.n
     blist = None if bands is None else np.ascontiguousarray(bands, np.int32)
     n_list = stack.n_bands if blist is None else len(blist)
@@ -147,6 +163,35 @@ def read_data(stack: DrillStack, win, mask_off=None, masks=None, clip_lower: flo
                                     C.c_void_p(vals.data_ptr()), C.c_void_p(cnts.data_ptr()),
                                     C.c_void_p(ws.data_ptr()), ws.numel(), _stream()), "drill")
     return vals, cnts
+
+
+def compute_deciles(stack: DrillStack, mb: "MaskBatch", totals: torch.Tensor, decile_count: int,
+                    bands: Optional[Sequence[int]] = None, band_chunk: int = 0):
+    """computeDeciles (drill.go:229-273) of every polygon and band:
+    (deciles float32 (n_polys, n_list, decile_count), status int32 (n_polys,
+    n_list): 0, 1 = band total 0, -7 = the reference would panic).  `totals`:
+    the mean pass's counts (n_polys, n_list)."""
+    n_polys = mb.n
+    blist = None if bands is None else np.ascontiguousarray(bands, np.int32)
+    n_list = stack.n_bands if blist is None else len(blist)
+    dev = stack.stack.device
+    if band_chunk <= 0:   # bound the sort buffers (mask_bytes x chunk values, 2 copies)
+        band_chunk = int(max(1, min(n_list, (1 << 29) // max(1, mb.mask_bytes), 2147483646 // max(1, mb.mask_bytes))))
+    ws_bytes = lib().gskyhip_drill_deciles_workspace_size(n_polys, mb.mask_bytes, band_chunk)
+    if ws_bytes < 0:
+        raise ValueError("deciles workspace: mask_bytes x band_chunk must stay below 2^31")
+    ws = torch.empty(max(1, int(ws_bytes)), dtype=torch.uint8, device=dev)
+    out = torch.empty((n_polys, n_list, decile_count), dtype=torch.float32, device=dev)
+    st = torch.empty((n_polys, n_list), dtype=torch.int32, device=dev)
+    tot = totals.to(dev, torch.int32).contiguous()
+    check(lib().gskyhip_drill_deciles(C.c_void_p(stack.stack.data_ptr()), stack.xsize, stack.ysize, stack.n_bands,
+                                      stack.t_stride, C.c_void_p(mb.win.data_ptr()),
+                                      C.c_void_p(mb.mask_off.data_ptr()), C.c_void_p(mb.masks.data_ptr()), n_polys,
+                                      mb.mask_bytes, blist.ctypes.data_as(C.c_void_p) if blist is not None else None,
+                                      n_list, stack.nodata, decile_count, band_chunk, C.c_void_p(tot.data_ptr()),
+                                      C.c_void_p(out.data_ptr()), C.c_void_p(st.data_ptr()),
+                                      C.c_void_p(ws.data_ptr()), ws.numel(), _stream()), "drill_deciles")
+    return out, st
 
 
 def drill_merge(values: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:

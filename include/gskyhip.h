@@ -356,6 +356,26 @@ int gskyhip_drill_batch(const float *stack, int xsize, int ysize, int n_bands, i
                         float nodata, float clip_lower, float clip_upper, int pixel_count,
                         int band_strides, int mode, double *out_value, int32_t *out_count,
                         void *workspace, int64_t workspace_bytes, void *stream);
+/* computeDeciles (worker/gdalprocess/drill.go:229-273; decileCount > 0,
+ * bandStrides 1) for the same batch as gskyhip_drill_batch: per polygon and
+ * selected band the in-mask, non-nodata values (no clipping) sorted
+ * ascending (segmented GPU sort) and the reference's decile_count picks.
+ *   totals: dev int32 n_polys x n_list, the out_count of the mean pass
+ *     (gskyhip_drill_batch, same bands, band_strides 1): deciles only where
+ *     total > 0, zeros elsewhere (drill.go:179-191);
+ *   out: dev float32 n_polys x n_list x decile_count;
+ *   status: dev int32 n_polys x n_list -- 0, 1 (total 0: the reference's
+ *     Count-0 zeros), GSKYHIP_E_RANGE (the reference indexes past the values
+ *     and panics: len % (dc+1) == 0 with len == dc+1);
+ *   band_chunk: bands sorted per pass (workspace scales with
+ *     mask_bytes x band_chunk; mask_bytes x band_chunk < 2^31). */
+int64_t gskyhip_drill_deciles_workspace_size(int n_polys, int64_t mask_bytes, int band_chunk);
+int gskyhip_drill_deciles(const float *stack, int xsize, int ysize, int n_bands, int t_stride,
+                          const int32_t *win, const int64_t *mask_off, const uint8_t *masks, int n_polys,
+                          int64_t mask_bytes, const int32_t *bands, int n_list, float nodata, int decile_count,
+                          int band_chunk, const int32_t *totals, float *out, int32_t *status, void *workspace,
+                          int64_t workspace_bytes, void *stream);
+
 /* Round-1 form (bands 1..n_bands, mode 0): sizes and allocates its workspace
  * itself (one synchronous read-back of win / mask_off). */
 int gskyhip_drill(const float *stack, int xsize, int ysize, int n_bands, int t_stride,

@@ -366,6 +366,45 @@ def drill_read_data(data, mask, nodata, clip_lower, clip_upper, pixel_count=0, b
     return v[:n].copy(), c[:n].copy()
 
 
+def compute_deciles(values, mask, nodata, decile_count):
+    """computeDeciles (worker/gdalprocess/drill.go:229-273) of one band, a
+    pure-Python restatement (small cases): the in-mask (255), non-nodata
+    values (no clipping) in row-major order, sorted ascending; step =
+    len // (dc + 1); step > 0: buf[(i+1)*step], or the float32 mean with the
+    next value when len % (dc + 1) == 0; otherwise each value repeated by its
+    padding count.  Returns float32 (dc,), or None where the reference
+    indexes past the slice (Go panics)."""
+    v = np.asarray(values, np.float32).reshape(-1)
+    m = np.asarray(mask, np.uint8).reshape(-1)
+    nd = np.float32(nodata)
+    buf = sorted(float(x) for x, k in zip(v, m) if k == 255 and np.float32(x) != nd)
+    buf = [np.float32(x) for x in buf]
+    dc = int(decile_count)
+    out = np.zeros(dc, np.float32)
+    step = len(buf) // (dc + 1)
+    if step > 0:
+        even = len(buf) % (dc + 1) == 0
+        for i in range(dc):
+            j = (i + 1) * step
+            de = buf[j]
+            if even:
+                if j + 1 >= len(buf):
+                    return None
+                de = np.float32((buf[j] + buf[j + 1]) / np.float32(2.0))
+            out[i] = de
+    else:
+        pad = {}
+        for i in range(dc):
+            k = i % len(buf)
+            pad[k] = pad.get(k, 0) + 1
+        idx = 0
+        for i in range(len(buf)):
+            for _ in range(pad.get(i, 0)):
+                out[idx] = buf[i]
+                idx += 1
+    return out
+
+
 def drill_merge(values, counts):
     v = np.ascontiguousarray(values, np.float64)
     c = np.ascontiguousarray(counts, np.int32)

@@ -428,6 +428,64 @@ def test_drill_parity(gpu, oracle, strides, pc, clip):
         assert np.array_equal(vals[p].view(np.uint64), ev.view(np.uint64)), p   # bit exact
 
 
+@pytest.mark.parametrize("dcount,pc,clip", [(9, 0, (-1e30, 1e30)), (4, 0, (0.21, 0.24)), (3, 1, (-1e30, 1e30))])
+def test_drill_deciles_parity(gpu, oracle, dcount, pc, clip):
+    """computeDeciles (drill.go:229-273) by segmented GPU sort: every decile
+    of every (polygon, band) equal to the oracle's float32 value, the
+    [mean, deciles] rows and their Counts as the reference's TimeSeries, small
+    polygons exercising the padding branch; a band list and a small band chunk
+    (several sort passes)."""
+    import torch
+
+    from gsky_amd import drill
+    dc = synth.config_c4(n_bands=23, size=200, n_polys=15, rmin=1, rmax=30)
+    # two tiny polygons: 2 and 3 in-mask pixels -> the padding branch (len < dc + 1)
+    dc.windows = list(dc.windows) + [(10, 12, 2, 1), (150, 40, 2, 2)]
+    dc.masks = list(dc.masks) + [np.full((1, 2), 255, np.uint8), np.array([[255, 0], [255, 255]], np.uint8)]
+    st = drill.DrillStack(torch.from_numpy(dc.bands), dc.nodata, gpu)
+    mb = drill.pack_masks(dc.windows, dc.masks, gpu)
+    bands = [1, 4, 5, 9, 23, 17, 2]
+    vals, cnts = drill.read_data(st, mb, clip_lower=clip[0], clip_upper=clip[1], pixel_count=pc,
+                                 decile_count=dcount, bands=bands)
+    vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
+    assert vals.shape == (len(dc.windows), len(bands), 1 + dcount)
+    mv, mc = drill.read_data(st, mb, clip_lower=clip[0], clip_upper=clip[1], pixel_count=pc, bands=bands)
+    assert np.array_equal(vals[..., 0], mv.cpu().numpy()) and np.array_equal(cnts[..., 0], mc.cpu().numpy())
+    small = 0
+    for p, (x0, y0, w, h) in enumerate(dc.windows):
+        for j, b in enumerate(bands):
+            sub = dc.bands[b - 1, y0:y0 + h, x0:x0 + w]
+            if cnts[p, j, 0] == 0:
+                assert not vals[p, j, 1:].any() and not cnts[p, j, 1:].any()
+                continue
+            exp = oracle.compute_deciles(sub, dc.masks[p], dc.nodata, dcount)
+            assert exp is not None
+            assert np.array_equal(vals[p, j, 1:].astype(np.float32), exp), (p, b)
+            assert (cnts[p, j, 1:] == 1).all()
+            small += int(((dc.masks[p] == 255) & (sub != dc.nodata)).sum() < dcount + 1)
+    assert small >= len(bands)
+    # several sort passes over the band list
+    dec, stt = drill.compute_deciles(st, mb, mc, dcount, bands, band_chunk=2)
+    assert np.array_equal(dec.cpu().numpy()[stt.cpu().numpy() == 0],
+                          vals[..., 1:].astype(np.float32)[stt.cpu().numpy() == 0])
+
+
+def test_drill_deciles_reference_panic(gpu, oracle):
+    """len == decileCount + 1 values: the reference reads buf[len] and panics
+    (drill.go:244-249); the GPU path reports GSKYHIP_E_RANGE instead."""
+    import torch
+
+    from gsky_amd import GskyError, drill
+    data = np.full((3, 64, 64), 0.25, np.float32)
+    st = drill.DrillStack(torch.from_numpy(data), -9999.0, gpu)
+    mb = drill.pack_masks([(5, 5, 2, 2)], [np.full((2, 2), 255, np.uint8)], gpu)
+    assert oracle.compute_deciles(data[0, 5:7, 5:7], np.full((2, 2), 255, np.uint8), -9999.0, 3) is None
+    with pytest.raises(GskyError):
+        drill.read_data(st, mb, decile_count=3)
+    _, stt = drill.compute_deciles(st, mb, torch.full((1, 3), 4, dtype=torch.int32, device=gpu), 3)
+    assert (stt.cpu().numpy() == -7).all()
+
+
 def test_drill_merge_parity(gpu, oracle):
     import torch
 

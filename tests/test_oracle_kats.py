@@ -243,3 +243,21 @@ def test_compute_reproject_extent_kat(oracle):
     bb = [12245143.98, -4865942.28, 15584728.71, -1118889.97]
     px, ln = oracle.compute_reproject_extent(g2, wgs, wm, bb)
     assert px == int((bb[2] - bb[0] + gt[1] / 2.0) / gt[1]) and ln == int((bb[3] - bb[1] - gt[5] / 2.0) / -gt[5])
+
+
+def test_compute_deciles_kats(oracle):
+    """computeDeciles (drill.go:229-273) by hand: the three branches."""
+    m = np.full(12, 255, np.uint8)
+    v = np.array([5, 1, 9, 3, 7, 11, 2, 8, 4, 10, 6, 12], np.float32)
+    # len 12, dc 3: step 3, 12 % 4 == 0 -> means of sorted[3,4], [6,7], [9,10]
+    assert oracle.compute_deciles(v, m, -1.0, 3).tolist() == [4.5, 7.5, 10.5]
+    # len 12, dc 4: step 2, 12 % 5 != 0 -> sorted[2], [4], [6], [8]
+    assert oracle.compute_deciles(v, m, -1.0, 4).tolist() == [3.0, 5.0, 7.0, 9.0]
+    # nodata (1) and masked-out pixels do not count: len 2 < dc + 1 = 5, padding {0: 2, 1: 2}
+    m2 = m.copy()
+    m2[3:] = 0
+    assert oracle.compute_deciles(v, m2, 1.0, 4).tolist() == [5.0, 5.0, 9.0, 9.0]
+    # len 2 (values 5, 9 after dropping nodata 1), dc 3: padding {0: 2, 1: 1} -> 5, 5, 9
+    assert oracle.compute_deciles(v, m2, 1.0, 3).tolist() == [5.0, 5.0, 9.0]
+    # len == dc + 1 with step 1: buf[len] is read -> the reference panics
+    assert oracle.compute_deciles(v[:4], m[:4], -1.0, 3) is None
