@@ -371,6 +371,13 @@ def run_c4(ctx: Ctx, args):
                                   "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(k_ms, 4),
                                   "kernel": "drill compaction + %s reduction (rank 0)" % name,
                                   "algorithmic_bytes_per_launch": int(abytes)}}
+    # decileCount = 9 (drill.go:229-273): segmented GPU sort of every (polygon, slice)
+    if not args.no_deciles:
+        _, cnts = drill.read_data(st, mb, *CLIP)
+        dt_dec = ctx.timed(lambda: drill.compute_deciles(st, mb, cnts, 9), 1, 1)
+        res["deciles"] = {"value": round(len(mine) * n_bands / dt_dec, 1), "unit": "polygon-slices/s",
+                          "ms_per_step": round(dt_dec * 1e3, 3), "decile_count": 9,
+                          "step": "count + scan + gather + segmented radix sort + pick, band chunks (rank 0)"}
     out = {"workload": "C4: WPS drill zonal mean, 1000 star polygons x 365 daily f32 slices of 2048^2, "
                        "ALL_TOUCHED masks, clip +-MaxFloat32", "polygons_rank0": len(mine), **res}
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
@@ -452,6 +459,7 @@ def main():
     ap.add_argument("--c2-chunks", type=int, default=1, help="C2 step: tile chunks pipelined on 2 streams (1: one batch; measured no gain, profiles/r02o_*)")
     ap.add_argument("--c3-steps", type=int, default=3)
     ap.add_argument("--c4-cpu-polys", type=int, default=160)
+    ap.add_argument("--no-deciles", action="store_true", help="C4: skip the decileCount=9 line")
     args = ap.parse_args()
     only = [s.strip().lower() for s in args.only.split(",") if s.strip()]
     if args.no_c1 and "c1" in only:

@@ -6,7 +6,7 @@ hand-written HIP kernels for gfx950 behind a C-ABI (include/gskyhip.h,
 libgskyhip.so).  See DESIGN.md.
 """
 from ._lib import GskyError, lib  # noqa: F401
-from .raster import (FlexRaster, Mask, Palette, ScaleParams, compute_mask, encode_rgba,  # noqa: F401
+from .raster import (FlexRaster, Mask, Palette, ScaleParams, band_math, compute_mask, encode_rgba,  # noqa: F401
                      gradient_rgba_palette, raster_merger_run, scale, scale_legacy)
 from .tiles import GranuleSet, PipelinedBatch, TileBatch, bbox_to_geot  # noqa: F401
 from .service import WarpService  # noqa: F401

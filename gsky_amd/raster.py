@@ -232,3 +232,30 @@ def raster_merger_run(rasters: Sequence[FlexRaster], namespaces: Sequence[str],
         t = canv[k][: width * height * nbytes].view(TORCH_OF[tname]).reshape(height, width)
         out[ns] = (t, nod[k])
     return out
+
+
+# ---------------------------------------------------------------- band-math
+def band_math(expr: str, variables: Sequence[tuple], out_nodata: float) -> torch.Tensor:
+    """Band-math of RasterMerger.Run (tile_merger.go:654-731) for one
+    expression over one axis: `variables` = [(name, canvas tensor, nodata)]
+    (typed canvases of the merged namespaces, all the same shape), result a
+    float32 tensor of that shape.  Pixels where any variable is its nodata,
+    and non-finite results, are `out_nodata` (the first namespace's nodata).
+    Raises GskyError(-1) on a parse error or unknown variable."""
+    if not variables:
+        raise ValueError("band_math needs the axis variables")
+    if len(variables) > 8:
+        raise ValueError("at most 8 variables per axis (GSKYHIP_BANDMATH_MAX_VARS)")
+    shape = variables[0][1].shape
+    ts = [_dev(v[1]) for v in variables]
+    if any(t.shape != shape for t in ts):
+        raise ValueError("variables must share one canvas shape")
+    out = torch.empty(shape, dtype=torch.float32, device=ts[0].device)
+    names = (C.c_char_p * len(ts))(*[v[0].encode() for v in variables])
+    ptrs = (C.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+    dts = np.array([TYPE_CODES[type_of_tensor(t)] for t in ts], np.int32)
+    nds = np.array([float(v[2]) for v in variables], np.float64)
+    check(lib().gskyhip_band_math(expr.encode(), names, ptrs, dts.ctypes.data_as(C.c_void_p),
+                                  nds.ctypes.data_as(C.c_void_p), len(ts), int(out.numel()), float(out_nodata),
+                                  C.c_void_p(out.data_ptr()), _stream()), "bandExpr %r" % expr)
+    return out

@@ -284,6 +284,20 @@ int gskyhip_service_unregister_all(const char *socket_path);
 int gskyhip_service_stats(const char *socket_path, int64_t *stats);
 int gskyhip_service_shutdown(const char *socket_path);
 
+/* Band-math on merged canvases (processor/tile_merger.go:523-731): evaluate
+ * `expr` (govaluate subset: ?: || && == != < <= > >= + - * / % ** unary - ! +,
+ * numbers, the variable names, parentheses; float32 per element) over the
+ * canvases of one axis -- var_names[k] names canvases[k] (dev, n_px values
+ * of dtypes[k], nodata nodatas[k]) -- into out (dev float32 n_px).  A pixel
+ * where any variable equals its nodata, or whose result is not finite,
+ * becomes out_nodata (the first namespace's nodata); an expression without
+ * variables fills every valid pixel.  GSKYHIP_E_ARG: parse error / unknown
+ * variable (govaluate's errors); GSKYHIP_E_TYPE: canvas type. */
+#define GSKYHIP_BANDMATH_MAX_VARS 8
+int gskyhip_band_math(const char *expr, const char *const *var_names, const void *const *canvases,
+                      const int32_t *dtypes, const double *nodatas, int n_vars, int64_t n_px, double out_nodata,
+                      float *out, void *stream);
+
 /* ---- standalone stages (the reference's own operator boundaries) -------- */
 /* FlexRaster (tile_types.go:95-106) as flat fields; data is dev. */
 typedef struct {

@@ -405,6 +405,145 @@ def compute_deciles(values, mask, nodata, decile_count):
     return out
 
 
+def band_math(expr, variables, out_nodata):
+    """Band-math of RasterMerger.Run (processor/tile_merger.go:654-731) for
+    one expression over one axis, a pure-Python restatement: variables =
+    [(name, array, nodata)] converted to float32; the grammar of
+    gskyhip_band_math (a govaluate subset) evaluated with numpy float32
+    element-wise arithmetic and constants rounded to float32; pixels where
+    any variable is its nodata, and non-finite results, -> out_nodata; a
+    constant expression fills every valid pixel.  (The govaluate fork is
+    absent from /root/reference: parity with it is unpinned.)"""
+    import re
+    toks = re.findall(r"\d+\.\d*(?:[eE][-+]?\d+)?|\.\d+(?:[eE][-+]?\d+)?|\d+(?:[eE][-+]?\d+)?|"
+                      r"[A-Za-z_][A-Za-z0-9_.]*|\*\*|&&|\|\||==|!=|<=|>=|[-+*/%<>!?:()]", expr)
+    if "".join(toks) != re.sub(r"\s+", "", expr):
+        raise ValueError("bad token in %r" % expr)
+    env = {n: np.asarray(a).astype(np.float32) for n, a, _ in variables}
+    f32 = np.float32
+    pos = [0]
+    used = [False]
+
+    def peek():
+        return toks[pos[0]] if pos[0] < len(toks) else None
+
+    def take(t=None):
+        tok = peek()
+        if t is not None and tok != t:
+            raise ValueError("expected %r in %r" % (t, expr))
+        pos[0] += 1
+        return tok
+
+    def b(x):
+        return np.where(x, f32(1), f32(0))
+
+    def ternary():
+        c = logic_or()
+        if peek() == "?":
+            take("?")
+            a = ternary()
+            take(":")
+            bb = ternary()
+            return np.where(c != 0, a, bb).astype(f32)
+        return c
+
+    def logic_or():
+        v = logic_and()
+        while peek() == "||":
+            take()
+            w = logic_and()
+            v = b((v != 0) | (w != 0))
+        return v
+
+    def logic_and():
+        v = equality()
+        while peek() == "&&":
+            take()
+            w = equality()
+            v = b((v != 0) & (w != 0))
+        return v
+
+    def equality():
+        v = relation()
+        while peek() in ("==", "!="):
+            op = take()
+            w = relation()
+            v = b(v == w) if op == "==" else b(v != w)
+        return v
+
+    def relation():
+        v = additive()
+        while peek() in ("<", "<=", ">", ">="):
+            op = take()
+            w = additive()
+            v = b({"<": v < w, "<=": v <= w, ">": v > w, ">=": v >= w}[op])
+        return v
+
+    def additive():
+        v = multiplicative()
+        while peek() in ("+", "-"):
+            op = take()
+            w = multiplicative()
+            v = (v + w) if op == "+" else (v - w)
+        return v
+
+    def multiplicative():
+        v = power()
+        while peek() in ("*", "/", "%"):
+            op = take()
+            w = power()
+            with np.errstate(all="ignore"):
+                v = v * w if op == "*" else (v / w if op == "/" else np.fmod(v, w))
+        return v
+
+    def power():
+        v = unary()
+        if peek() == "**":
+            take()
+            w = power()
+            with np.errstate(all="ignore"):
+                v = np.power(v, w)
+        return v
+
+    def unary():
+        if peek() == "-":
+            take()
+            return -unary()
+        if peek() == "+":
+            take()
+            return unary()
+        if peek() == "!":
+            take()
+            return b(unary() == 0)
+        return primary()
+
+    def primary():
+        tok = take()
+        if tok == "(":
+            v = ternary()
+            take(")")
+            return v
+        if tok is not None and (tok[0].isdigit() or tok[0] == "."):
+            return f32(float(tok))
+        if tok in env:
+            used[0] = True
+            return env[tok]
+        raise ValueError("No parameter %r found." % tok)
+
+    with np.errstate(all="ignore"):
+        res = ternary()
+    if pos[0] != len(toks):
+        raise ValueError("trailing tokens in %r" % expr)
+    shape = np.asarray(variables[0][1]).shape
+    valid = np.ones(shape, bool)
+    for n, a, nd in variables:
+        valid &= np.asarray(a).astype(np.float32).astype(np.float64) != float(nd)
+    res = np.broadcast_to(np.asarray(res, np.float32), shape)
+    if used[0]:
+        res = np.where(np.isfinite(res), res, f32(out_nodata))
+    return np.where(valid, res, f32(out_nodata)).astype(np.float32)
+
+
 def drill_merge(values, counts):
     v = np.ascontiguousarray(values, np.float64)
     c = np.ascontiguousarray(counts, np.int32)

@@ -486,6 +486,38 @@ def test_drill_deciles_reference_panic(gpu, oracle):
     assert (stt.cpu().numpy() == -7).all()
 
 
+@pytest.mark.parametrize("expr", ["(nir - red) / (nir + red)", "nir * 0.0001 - red * 2 + qa", "nir > red ? nir : -red",
+                                  "(nir % 7 + 1) ** 0.5", "3.25", "!(qa == 1) && nir >= 100 || red < 10",
+                                  "red / (nir - nir)"])
+def test_band_math_parity(gpu, oracle, expr):
+    """gskyhip_band_math against the oracle's restatement on merged-canvas-like
+    int16 / uint8 / float32 inputs with nodata: bit-identical (pow within 2
+    ulp: device powf vs numpy)."""
+    import torch
+
+    from gsky_amd import GskyError, band_math
+    rng = np.random.default_rng(7)
+    n = 300 * 257
+    nir = rng.integers(-50, 10000, n).astype(np.int16)
+    nir[rng.random(n) < 0.05] = -999
+    red = (rng.random(n) * 500).astype(np.float32)
+    red[rng.random(n) < 0.05] = -9999.0
+    qa = rng.integers(0, 3, n).astype(np.uint8)
+    vs = [("nir", nir, -999.0), ("red", red, -9999.0), ("qa", qa, 2.0)]
+    got = band_math(expr, [(nm, torch.from_numpy(a).to(gpu), nd) for nm, a, nd in vs], -999.0).cpu().numpy()
+    exp = oracle.band_math(expr, vs, -999.0)
+    if "**" in expr:
+        np.testing.assert_array_max_ulp(got, exp, maxulp=2)
+    else:
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
+    if "(nir - nir)" in expr:   # division by zero everywhere: every pixel nodata
+        assert (exp == -999.0).all()
+    else:
+        assert (exp == -999.0).mean() < 0.6
+    with pytest.raises(GskyError):
+        band_math("nir + swir", [(nm, torch.from_numpy(a).to(gpu), nd) for nm, a, nd in vs], -999.0)
+
+
 def test_drill_merge_parity(gpu, oracle):
     import torch
 

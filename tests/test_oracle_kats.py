@@ -261,3 +261,21 @@ def test_compute_deciles_kats(oracle):
     assert oracle.compute_deciles(v, m2, 1.0, 3).tolist() == [5.0, 5.0, 9.0]
     # len == dc + 1 with step 1: buf[len] is read -> the reference panics
     assert oracle.compute_deciles(v[:4], m[:4], -1.0, 3) is None
+
+
+def test_band_math_kats(oracle):
+    """Band-math (tile_merger.go:654-731) by hand: NDVI, nodata of ANY axis
+    variable masks the pixel (used or not), non-finite -> nodata, a constant
+    expression fills every valid pixel, ternary / comparisons as 1.0 / 0.0."""
+    nir = np.array([3, 2, 1, -9999, 5], np.float32)
+    red = np.array([1, 2, 0, 4, 7], np.float32)
+    qa = np.array([0, 0, 0, 0, 255], np.uint8)
+    vs = [("nir", nir, -9999.0), ("red", red, -9999.0), ("qa", qa, 255.0)]
+    got = oracle.band_math("(nir - red) / (nir + red)", vs, -9999.0)
+    assert got.tolist() == [0.5, 0.0, 1.0, -9999.0, -9999.0]
+    assert oracle.band_math("nir / (red - red)", vs, -1.0).tolist() == [-1.0, -1.0, -1.0, -1.0, -1.0]
+    assert oracle.band_math("2.5", vs, -1.0).tolist() == [2.5, 2.5, 2.5, -1.0, -1.0]
+    assert oracle.band_math("nir > red ? nir : 0 - red", vs, -1.0).tolist() == [3.0, -2.0, 1.0, -1.0, -1.0]
+    assert oracle.band_math("!(nir == 2) && red < 3", vs, -1.0).tolist() == [1.0, 0.0, 1.0, -1.0, -1.0]
+    with pytest.raises(ValueError):
+        oracle.band_math("nir + swir", vs, -1.0)
