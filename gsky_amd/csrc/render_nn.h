@@ -27,6 +27,7 @@ namespace gsky {
 
 constexpr uint32_t kNoPx = 0xFFFFFFFFu;
 constexpr int kExpress = 16;   // render_nn2_kernel: single-entry express path (A/B knob GSKYHIP_NN_EXPRESS)
+constexpr int kWide = 32;      // render_nn2_kernel: 16-B source-row loads for 16-bit values (GSKYHIP_NN_WIDE)
 
 // Element index of each of the lane's LPX pixels on a LINEAR row, 32.32
 // fixed point.  false (wave-uniform): some valid pixel of the wave sits
@@ -325,6 +326,59 @@ __device__ __forceinline__ uint32_t scale_pat(uint32_t c, uint32_t nd_pat, int32
   return c == nd_pat ? 0xFFu : b;
 }
 
+// NN gathers of a lane's LPX consecutive pixels on an `inside` LINEAR row of
+// a 16-bit band with one 16-byte load per source row the pixels touch: at
+// the ~2x upsampling of C2 four destination pixels fall on 2-3 source pixels
+// of 1-2 rows, so 1-2 wide loads replace 4 two-byte gathers (the gather
+// instruction count is what the kernel issues most).  The indices are the
+// reference's fp64 expressions (lin_coords() + nn_px()); the coordinates are
+// monotone along the row, so the end pixels bound the span.  A lane whose
+// pixels span more than 7 elements or 2 rows, or reach the band's last 8
+// elements, gathers per pixel as before.  Values come back zero-extended
+// (the fold's bit patterns).
+template <int LPX>
+__device__ __forceinline__ void wide_gather16(__amdgpu_buffer_rsrc_t rs, const RowRec *rr, int ic0, int bx,
+                                              uint32_t nel, uint32_t *v) {
+  const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
+  int ix[LPX], iy[LPX];
+#pragma unroll
+  for (int q = 0; q < LPX; q++) {
+    const double dist = (double)(ic0 + q);
+    ix[q] = __double2int_rz(xs0 + dX * dist + 1.0e-10);
+    iy[q] = __double2int_rz(ys0 + dY * dist + 1.0e-10);
+  }
+  const int xa = min(ix[0], ix[LPX - 1]), xz = max(ix[0], ix[LPX - 1]);
+  const int ya = min(iy[0], iy[LPX - 1]), yz = max(iy[0], iy[LPX - 1]);
+  const bool wide = xa >= 0 && ya >= 0 && xz - xa <= 6 && yz - ya <= 1 &&
+                    (uint64_t)(ya + 1) * (uint32_t)bx + (uint32_t)xa + 8u <= (uint64_t)nel;
+  if (wide) {
+    const uint32_t e0 = __umul24((uint32_t)ya, (uint32_t)bx) + (uint32_t)xa;
+    const uint32_t s0 = e0 & 1u;
+    const u32x4 w0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (e0 & ~1u) * 2u, 0, 0);
+    u32x4 w1 = w0;
+    uint32_t s1 = s0;
+    if (yz != ya) {
+      const uint32_t e1 = e0 + (uint32_t)bx;
+      s1 = e1 & 1u;
+      w1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (e1 & ~1u) * 2u, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < LPX; q++) {
+      const bool r1 = iy[q] != ya;
+      const uint32_t k = (r1 ? s1 : s0) + (uint32_t)(ix[q] - xa);
+      const uint32_t d0 = r1 ? w1.x : w0.x, d1 = r1 ? w1.y : w0.y;
+      const uint32_t d2 = r1 ? w1.z : w0.z, d3 = r1 ? w1.w : w0.w;
+      const uint32_t d = k < 4u ? (k < 2u ? d0 : d1) : (k < 6u ? d2 : d3);
+      v[q] = (d >> ((k & 1u) * 16u)) & 0xFFFFu;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < LPX; q++)
+      v[q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
+          rs, (__umul24((uint32_t)iy[q], (uint32_t)bx) + (uint32_t)ix[q]) * 2u, 0, 0);
+  }
+}
+
 template <typename T, int LPX, int R, int FLAGS, int WPE>
 __global__ __launch_bounds__(256, WPE) void render_nn2_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                          const int32_t *__restrict__ order,
@@ -335,6 +389,7 @@ __global__ __launch_bounds__(256, WPE) void render_nn2_kernel(RenderArgs a, cons
   using P = typename POf<T>::type;
   constexpr bool kInt = !std::is_same<T, float>::value;
   constexpr bool kCv = (FLAGS & kCanvas) != 0;
+  constexpr bool kWide16 = (FLAGS & kWide) != 0 && sizeof(T) == 2;
   constexpr int kCols = 64 * LPX;
   __shared__ uint32_t s_tab[256];
 
@@ -466,6 +521,10 @@ __global__ __launch_bounds__(256, WPE) void render_nn2_kernel(RenderArgs a, cons
         const int ic0 = xb + pp * kCols + lane * LPX - exoff;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
+          if constexpr (kWide16) {
+            wide_gather16<LPX>(rs, rr + i, ic0, bx, (uint32_t)bx * (uint32_t)by, vv[pp][i]);
+            continue;
+          }
           const double xs0 = rr[i].v[0], ys0 = rr[i].v[1], dX = rr[i].v[2], dY = rr[i].v[3];
 #pragma unroll
           for (int q = 0; q < LPX; q++) {
@@ -549,6 +608,10 @@ __global__ __launch_bounds__(256, WPE) void render_nn2_kernel(RenderArgs a, cons
           for (int i = 0; i < R; i++) {
             if (st[i] == 0) continue;
             const RowRec *rr = rrow + (rb + i - eyoff);
+            if constexpr (kWide16) {
+              wide_gather16<LPX>(rs, rr, ic0, bx, (uint32_t)bx * (uint32_t)by, vv[i]);
+              continue;
+            }
             const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
 #pragma unroll
             for (int q = 0; q < LPX; q++) {
@@ -625,7 +688,13 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
   do { if (canvas) GSKY_NN2_LAUNCH(L, RR, kCanvas, WP); else GSKY_NN2_LAUNCH(L, RR, 0, WP); } while (0)
 #define GSKY_NN2_SHAPE_X(L, RR, WP)                                                  \
   do {                                                                               \
-    if (a.nn_express) {                                                              \
+    if (a.nn_express && a.nn_wide) {                                                 \
+      if (canvas) GSKY_NN2_LAUNCH(L, RR, kCanvas | kExpress | kWide, WP);            \
+      else GSKY_NN2_LAUNCH(L, RR, kExpress | kWide, WP);                             \
+    } else if (a.nn_wide) {                                                          \
+      if (canvas) GSKY_NN2_LAUNCH(L, RR, kCanvas | kWide, WP);                       \
+      else GSKY_NN2_LAUNCH(L, RR, kWide, WP);                                        \
+    } else if (a.nn_express) {                                                       \
       if (canvas) GSKY_NN2_LAUNCH(L, RR, kCanvas | kExpress, WP);                    \
       else GSKY_NN2_LAUNCH(L, RR, kExpress, WP);                                     \
     } else GSKY_NN2_SHAPE(L, RR, WP);                                                \

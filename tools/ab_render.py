@@ -55,8 +55,11 @@ def main():
         from oracle import oracle as O
         from tests.helpers import oracle_render
         exp = torch.from_numpy(oracle_render(O, cfg, n_threads=16)).to("cuda")
-    # (name, typed, LDS_STAGE, LDS_FLAGS, NN_KERNEL, NN_SHAPE[, NN_XCD, NN_PROBE, NN_GEN, NN_WPE, NN_EXPRESS])
-    variants = [("nn3_4x2", True, "0", "0", "1", "3", "0", "0", "3"), ("nn3_4x4", True, "0", "0", "1", "0", "0", "0", "3"),
+    # (name, typed, LDS_STAGE, LDS_FLAGS, NN_KERNEL, NN_SHAPE[, NN_XCD, NN_PROBE, NN_GEN, NN_WPE, NN_EXPRESS, NN_WIDE])
+    variants = [("nn3w_4x1", True, "0", "0", "1", "4", "0", "0", "3", "0", "1", "1"),
+                ("nn3w_4x2", True, "0", "0", "1", "3", "0", "0", "3", "0", "1", "1"),
+                ("nn3w_4x1_nox", True, "0", "0", "1", "4", "0", "0", "3", "0", "0", "1"),
+                ("nn3_4x2", True, "0", "0", "1", "3", "0", "0", "3"), ("nn3_4x4", True, "0", "0", "1", "0", "0", "0", "3"),
                 ("nn3_8x1", True, "0", "0", "1", "1", "0", "0", "3"), ("nn3_4x1", True, "0", "0", "1", "4", "0", "0", "3"),
                 ("nn3_4x2_w6", True, "0", "0", "1", "3", "0", "0", "3", "6"),
                 ("nn3_4x2_nox", True, "0", "0", "1", "3", "0", "0", "3", "0", "0"),
@@ -80,6 +83,7 @@ def main():
         os.environ["GSKYHIP_NN_GEN"] = extra[2] if len(extra) > 2 else "2"
         os.environ["GSKYHIP_NN_WPE"] = extra[3] if len(extra) > 3 else "0"
         os.environ["GSKYHIP_NN_EXPRESS"] = extra[4] if len(extra) > 4 else "1"
+        os.environ["GSKYHIP_NN_WIDE"] = extra[5] if len(extra) > 5 else "0"
         b.typed = typed
         med, mn = time_render(b, sp, pal, args.reps)
         out = b.render(sp, pal).clone()
