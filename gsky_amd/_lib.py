@@ -84,7 +84,7 @@ EXPORTS = [
     "gskyhip_render_tile_info", "gskyhip_compute_reproject_extent",
     "gskyhip_service_run", "gskyhip_service_register_granule", "gskyhip_service_unregister_all",
     "gskyhip_service_stats", "gskyhip_service_shutdown", "gskyhip_drill_deciles_workspace_size",
-    "gskyhip_drill_deciles", "gskyhip_band_math",
+    "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device",
 ]
 
 _lib = None
@@ -141,6 +141,8 @@ def lib() -> C.CDLL:
     L.gskyhip_drill_descriptors.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci, vp, vp,
                                             C.POINTER(i64), vp, vp]
     L.gskyhip_drill_merge.argtypes = [vp, vp, ci, ci, vp, vp]
+    L.gskyhip_drill_descriptors_device.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci,
+                                                   vp, vp, C.POINTER(i64), vp, vp, vp]
     L.gskyhip_band_math.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(vp), vp, vp, ci, i64, d,
                                     vp, vp]
     L.gskyhip_drill_deciles_workspace_size.argtypes = [ci, i64, ci]

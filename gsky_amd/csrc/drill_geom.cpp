@@ -32,6 +32,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/gskyhip.h"
 #include "gsky_device.h"
 
@@ -344,10 +346,228 @@ Descriptor describe(const char *geometry, const gskyhip_crs *crs, const double g
   return d;
 }
 
+// ---------------------------------------------------------------- GPU rasterizer
+// The same two passes on the GPU, one workgroup per polygon, straight into
+// the device mask buffer (no host mask, no copy): touch_edge_kernel gives each
+// thread one edge of the rings (GDALdllImageLineAllTouched, the expressions of
+// touch_lines()), fill_rows_kernel one scanline (GDALdllImageFilledPolygon,
+// the expressions of fill_polygon(): intersections collected, insertion-
+// sorted, spans burned).  Both only ever write 255, so the thread order and
+// overlapping writes do not matter; the region is zeroed first.  Polygons
+// with more than kMaxInts edges (more intersections than a thread keeps) are
+// rasterized on the host instead.
+constexpr int kMaxInts = 64;
+
+struct PolyDev {
+  int64_t mask_off;
+  int32_t w, h;
+  int32_t v0, nv;      // vertex range in vx / vy
+  int32_t p0, np;      // ring range in parts (points per ring)
+};
+
+__device__ __forceinline__ void dpoint(uint8_t *m, int w, int h, int x, int y) {
+  if (x >= 0 && x < w && y >= 0 && y < h) m[(int64_t)y * w + x] = 255;
+}
+
+__global__ __launch_bounds__(256) void touch_edge_kernel(const PolyDev *polys, const double *vx, const double *vy,
+                                                         const int32_t *parts, uint8_t *masks) {
+  const PolyDev P = polys[blockIdx.x];
+  uint8_t *m = masks + P.mask_off;
+  const int w = P.w, h = P.h;
+  for (int k = threadIdx.x; k < P.nv; k += blockDim.x) {
+    // edge (k-1, k) of its ring; the first point of a ring starts no edge
+    int start = 0, r = 0;
+    while (r < P.np && k >= start + parts[P.p0 + r]) { start += parts[P.p0 + r]; r++; }
+    if (r >= P.np || k == start) continue;
+    double x = vx[P.v0 + k - 1], y = vy[P.v0 + k - 1], xe = vx[P.v0 + k], ye = vy[P.v0 + k];
+    if ((y < 0.0 && ye < 0.0) || (y > h && ye > h) || (x < 0.0 && xe < 0.0) || (x > w && xe > w)) continue;
+    if (x > xe) { double t = x; x = xe; xe = t; t = y; y = ye; ye = t; }
+    if (floor(x) == floor(xe) || fabs(x - xe) < .01) {   // vertical
+      if (ye < y) { const double t = y; y = ye; ye = t; }
+      const int ix = (int)floor(xe);
+      if (ix < 0 || ix >= w) continue;
+      const int iy0 = max((int)floor(y), 0), iy1 = min((int)floor(ye), h - 1);
+      for (int iy = iy0; iy <= iy1; iy++) dpoint(m, w, h, ix, iy);
+      continue;
+    }
+    if (floor(y) == floor(ye) || fabs(y - ye) < .01) {   // horizontal
+      const int iy = (int)floor(y);
+      if (iy < 0 || iy >= h) continue;
+      const int ix0 = max((int)floor(x), 0), ix1 = min((int)floor(xe), w - 1);
+      for (int ix = ix0; ix <= ix1; ix++) dpoint(m, w, h, ix, iy);
+      continue;
+    }
+    const double slope = (ye - y) / (xe - x);   // general, left to right
+    if (xe > w) { ye -= (xe - w) * slope; xe = w; }
+    if (x < 0.0) { y += (0.0 - x) * slope; x = 0.0; }
+    if (ye > y) {
+      if (y < 0.0) { x += (0.0 - y) / slope; y = 0.0; }
+      if (ye >= h) { xe += (ye - h) / slope; ye = h; }
+    } else {
+      if (y >= h) { x += (h - y) / slope; y = h; }
+      if (ye < 0.0) { xe -= (ye - 0) / slope; ye = 0.0; }
+    }
+    while (x >= 0.0 && x < xe) {
+      const int ix = (int)floor(x), iy = (int)floor(y);
+      if (iy >= 0 && iy < h) dpoint(m, w, h, ix, iy);
+      double sx = floor(x + 1.0) - x;
+      double sy = sx * slope;
+      if ((int)floor(y + sy) == iy) {
+        x += sx; y += sy;
+      } else if (slope < 0) {
+        sy = iy - y;
+        if (sy > -0.000000001) sy = -0.000000001;
+        sx = sy / slope;
+        x += sx; y += sy;
+      } else {
+        sy = (iy + 1) - y;
+        if (sy < 0.000000001) sy = 0.000000001;
+        sx = sy / slope;
+        x += sx; y += sy;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void fill_rows_kernel(const PolyDev *polys, const double *vx, const double *vy,
+                                                        const int32_t *parts, uint8_t *masks) {
+  const PolyDev P = polys[blockIdx.x];
+  uint8_t *m = masks + P.mask_off;
+  const int w = P.w, h = P.h, n = P.nv;
+  if (P.np <= 0 || n == 0) return;
+  const double *X = vx + P.v0, *Y = vy + P.v0;
+  const int32_t *part = parts + P.p0;
+  double dminy = Y[0], dmaxy = Y[0];
+  for (int i = 1; i < n; i++) { dminy = fmin(dminy, Y[i]); dmaxy = fmax(dmaxy, Y[i]); }
+  const int miny = max((int)dminy, 0), maxy = min((int)dmaxy, h - 1);
+  const int minx = 0, maxx = w - 1;
+  int ints[kMaxInts];
+  for (int y = miny + (int)threadIdx.x; y <= maxy; y += blockDim.x) {
+    int ni = 0;
+    const double dy = y + 0.5;
+    int partoffset = 0, pi = 0;
+    for (int i = 0; i < n; i++) {
+      if (i == partoffset + part[pi]) { partoffset += part[pi]; pi++; }
+      const int ind1 = (i == partoffset) ? partoffset + part[pi] - 1 : i - 1;
+      const int ind2 = (i == partoffset) ? partoffset : i;
+      double dy1 = Y[ind1], dy2 = Y[ind2], dx1, dx2;
+      if ((dy1 < dy && dy2 < dy) || (dy1 > dy && dy2 > dy)) continue;
+      if (dy1 < dy2) {
+        dx1 = X[ind1]; dx2 = X[ind2];
+      } else if (dy1 > dy2) {
+        const double t = dy1; dy1 = dy2; dy2 = t;
+        dx1 = X[ind2]; dx2 = X[ind1];
+      } else {   // horizontal: bottom edges filled on their own, top edges skipped
+        if (X[ind1] > X[ind2]) {
+          const int h1 = (int)floor(X[ind2] + 0.5), h2 = (int)floor(X[ind1] + 0.5);
+          if (h1 > maxx || h2 <= minx) continue;
+          for (int xx = max(h1, 0); xx <= min(h2 - 1, w - 1); xx++) dpoint(m, w, h, xx, y);
+        }
+        continue;
+      }
+      if (dy < dy2 && dy >= dy1 && ni < kMaxInts)
+        ints[ni++] = (int)floor((dy - dy1) * (dx2 - dx1) / (dy2 - dy1) + dx1 + 0.5);
+    }
+    for (int a = 1; a < ni; a++) {   // insertion sort (a few intersections per row)
+      const int v = ints[a];
+      int b = a - 1;
+      while (b >= 0 && ints[b] > v) { ints[b + 1] = ints[b]; b--; }
+      ints[b + 1] = v;
+    }
+    for (int i = 0; i + 1 < ni; i += 2)
+      if (ints[i] <= maxx && ints[i + 1] > minx)
+        for (int xx = max(ints[i], 0); xx <= min(ints[i + 1] - 1, w - 1); xx++) dpoint(m, w, h, xx, y);
+  }
+}
+
 }  // namespace
 }  // namespace gsky
 
 using namespace gsky;
+
+// Windows on the host, ALL_TOUCHED masks rasterized on the GPU into masks_dev.
+extern "C" int gskyhip_drill_descriptors_device(const char *const *geometries, int n, const char *dataset_srs,
+                                                const double *geot, int xsize, int ysize, int32_t *win_out,
+                                                int64_t *mask_off_out, int64_t *mask_bytes_out, uint8_t *masks_dev,
+                                                int32_t *status_out, void *stream) {
+  if (n < 0 || !geot || !win_out || !mask_off_out || !mask_bytes_out || !status_out) return GSKYHIP_E_ARG;
+  gskyhip_crs crs;
+  const gskyhip_crs *pc = nullptr;
+  if (dataset_srs && *dataset_srs) {
+    if (gskyhip_crs_from_srs(dataset_srs, &crs)) return GSKYHIP_E_CRS;
+    pc = &crs;
+  }
+  std::vector<PolyDev> polys;
+  std::vector<double> vx, vy;
+  std::vector<int32_t> parts;
+  std::vector<std::pair<int64_t, std::vector<uint8_t>>> host_masks;   // polygons too complex for a thread
+  int64_t off = 0;
+  for (int i = 0; i < n; i++) {
+    Descriptor d = describe(geometries[i], pc, geot, xsize, ysize);
+    status_out[i] = d.status;
+    const int64_t bytes = d.status == 0 ? (int64_t)d.win[2] * d.win[3] : 0;
+    for (int k = 0; k < 4; k++) win_out[4 * i + k] = d.status == 0 ? d.win[k] : 0;
+    mask_off_out[i] = off;
+    if (masks_dev && bytes > 0) {
+      if ((int)d.pix.x.size() > kMaxInts) {
+        std::vector<uint8_t> hm((size_t)bytes, 0);
+        Canvas cv{hm.data(), d.win[2], d.win[3]};
+        touch_lines(d.pix, cv);
+        fill_polygon(d.pix, cv);
+        host_masks.emplace_back(off, std::move(hm));
+      } else {
+        PolyDev P;
+        P.mask_off = off;
+        P.w = d.win[2];
+        P.h = d.win[3];
+        P.v0 = (int32_t)vx.size();
+        P.nv = (int32_t)d.pix.x.size();
+        P.p0 = (int32_t)parts.size();
+        P.np = (int32_t)d.pix.part.size();
+        vx.insert(vx.end(), d.pix.x.begin(), d.pix.x.end());
+        vy.insert(vy.end(), d.pix.y.begin(), d.pix.y.end());
+        parts.insert(parts.end(), d.pix.part.begin(), d.pix.part.end());
+        polys.push_back(P);
+      }
+    }
+    off += (bytes + 15) / 16 * 16;   // 16-byte aligned regions, polygon order
+  }
+  *mask_bytes_out = off > 0 ? off : 16;
+  if (!masks_dev) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(masks_dev, 0, (size_t)*mask_bytes_out, s) != hipSuccess) return GSKYHIP_E_HIP;
+  if (!polys.empty()) {
+    // one staging allocation: polygons | x | y | parts
+    const size_t b0 = polys.size() * sizeof(PolyDev), b1 = vx.size() * 8, b2 = parts.size() * 4;
+    char *dev = nullptr;
+    if (hipMalloc(&dev, b0 + 2 * b1 + b2) != hipSuccess) return GSKYHIP_E_HIP;
+    std::vector<char> host(b0 + 2 * b1 + b2);
+    std::memcpy(host.data(), polys.data(), b0);
+    std::memcpy(host.data() + b0, vx.data(), b1);
+    std::memcpy(host.data() + b0 + b1, vy.data(), b1);
+    std::memcpy(host.data() + b0 + 2 * b1, parts.data(), b2);
+    int rc = 0;
+    if (hipMemcpyAsync(dev, host.data(), host.size(), hipMemcpyHostToDevice, s) != hipSuccess) rc = GSKYHIP_E_HIP;
+    const PolyDev *dp = (const PolyDev *)dev;
+    const double *dx = (const double *)(dev + b0), *dy = (const double *)(dev + b0 + b1);
+    const int32_t *dpart = (const int32_t *)(dev + b0 + 2 * b1);
+    if (!rc) {
+      hipLaunchKernelGGL(touch_edge_kernel, dim3((unsigned)polys.size()), dim3(256), 0, s, dp, dx, dy, dpart,
+                         masks_dev);
+      hipLaunchKernelGGL(fill_rows_kernel, dim3((unsigned)polys.size()), dim3(256), 0, s, dp, dx, dy, dpart,
+                         masks_dev);
+      if (hipGetLastError() != hipSuccess) rc = GSKYHIP_E_HIP;
+    }
+    // the staging buffers must outlive the kernels
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GSKYHIP_E_HIP;
+    (void)hipFree(dev);
+    if (rc) return rc;
+  }
+  for (auto &hm : host_masks)
+    if (hipMemcpy(masks_dev + hm.first, hm.second.data(), hm.second.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return GSKYHIP_E_HIP;
+  return 0;
+}
 
 extern "C" int gskyhip_drill_descriptors(const char *const *geometries, int n, const char *dataset_srs,
                                          const double *geot, int xsize, int ysize, int32_t *win_out,

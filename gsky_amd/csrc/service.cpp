@@ -199,6 +199,7 @@ struct Service {
   int listen_fd = -1;
   // statistics: warp requests, batches, largest batch, registered granules
   std::atomic<int64_t> n_req{0}, n_batches{0}, max_seen{0}, n_reg{0};
+  std::atomic<int> active{0};          // connection threads still running (detached)
   std::mutex reg_mu;
   std::vector<void *> device_allocs;   // granule data uploaded through SVC_REGISTER
 };
@@ -320,6 +321,7 @@ void conn_loop(Service *s, int fd) {
     if (!send_msg(fd, op, o.b)) break;   // the worker died (SIGKILL): drop the reply
   }
   ::close(fd);
+  s->active--;
 }
 
 }  // namespace
@@ -342,7 +344,9 @@ extern "C" {
 int gskyhip_service_run(const char *socket_path, int max_batch, int window_us) {
   if (!socket_path || !*socket_path || std::strlen(socket_path) >= sizeof(sockaddr_un::sun_path))
     return GSKYHIP_E_ARG;
-  Service s;
+  // heap-allocated: connection threads are detached (a long-running daemon
+  // must not accumulate finished threads) and may outlive a forced shutdown
+  Service &s = *new Service;
   s.max_batch = std::max(1, max_batch);
   s.window_us = std::max(0, window_us);
   const int fd = ::socket(AF_UNIX, SOCK_STREAM, 0);
@@ -354,19 +358,20 @@ int gskyhip_service_run(const char *socket_path, int max_batch, int window_us) {
   ::unlink(socket_path);
   if (::bind(fd, (sockaddr *)&a, sizeof(a)) != 0 || ::listen(fd, 256) != 0) {
     ::close(fd);
+    delete &s;
     return GSKYHIP_E_SERVICE;
   }
   s.listen_fd = fd;
   g_svc = &s;
   std::thread batcher(batch_loop, &s);
-  std::vector<std::thread> conns;
   while (!s.stop) {
     const int c = ::accept(fd, nullptr, nullptr);
     if (c < 0) {
       if (errno == EINTR) continue;
       break;
     }
-    conns.emplace_back(conn_loop, &s, c);
+    s.active++;
+    std::thread(conn_loop, &s, c).detach();
   }
   s.stop = true;
   s.cv_queue.notify_all();
@@ -377,12 +382,19 @@ int gskyhip_service_run(const char *socket_path, int max_batch, int window_us) {
     s.queue.clear();
   }
   s.cv_done.notify_all();
-  for (auto &t : conns) t.join();
+  // clients connect per request, so their threads end within one exchange;
+  // give them a few seconds, then leave any idle persistent connection behind
+  for (int k = 0; k < 500 && s.active.load() > 0; k++) std::this_thread::sleep_for(std::chrono::milliseconds(10));
   ::close(fd);
   ::unlink(socket_path);
-  gskyhip_unregister_all();
-  for (void *p : s.device_allocs) hipFree(p);
+  {
+    std::lock_guard<std::mutex> rl(s.reg_mu);
+    gskyhip_unregister_all();
+    for (void *p : s.device_allocs) (void)hipFree(p);
+    s.device_allocs.clear();
+  }
   g_svc = nullptr;
+  if (s.active.load() == 0) delete &s;
   return 0;
 }
 

@@ -105,15 +105,35 @@ def drill_descriptors(geometries: Sequence[str], dataset_srs: Optional[str], geo
 
 
 def drill_dataset(geometries: Sequence[str], dataset_srs: Optional[str], geot: Sequence[float], xsize: int,
-                  ysize: int, device=None) -> Tuple["MaskBatch", np.ndarray]:
+                  ysize: int, device=None, rasterize: str = "gpu") -> Tuple["MaskBatch", np.ndarray]:
     """DrillDataset's geometry step for a batch of requests: the windows and
-    ALL_TOUCHED masks, uploaded as a MaskBatch, plus the per-polygon status
-    (0 ok; a polygon that misses the file gets an empty window)."""
-    win, off, buf, st = drill_descriptors(geometries, dataset_srs, geot, xsize, ysize)
+    ALL_TOUCHED masks as a MaskBatch in HBM, plus the per-polygon status (0
+    ok; a polygon that misses the file gets an empty window).  rasterize
+    "gpu" burns the masks on the device (gskyhip_drill_descriptors_device),
+    "host" rasterizes on the CPU and uploads them."""
     dev = torch.device(device or "cuda")
-    mb = MaskBatch(torch.from_numpy(win.copy()).to(dev), torch.from_numpy(off.copy()).to(dev),
-                   torch.from_numpy(buf).to(dev))
-    return mb, st
+    if rasterize == "host":
+        win, off, buf, st = drill_descriptors(geometries, dataset_srs, geot, xsize, ysize)
+        return MaskBatch(torch.from_numpy(win.copy()).to(dev), torch.from_numpy(off.copy()).to(dev),
+                         torch.from_numpy(buf).to(dev)), st
+    n = len(geometries)
+    arr = (C.c_char_p * max(1, n))(*[g.encode() for g in geometries])
+    gt = (C.c_double * 6)(*geot)
+    win = np.zeros((max(1, n), 4), np.int32)
+    off = np.zeros(max(1, n), np.int64)
+    st = np.zeros(max(1, n), np.int32)
+    total = C.c_int64()
+    srs = dataset_srs.encode() if dataset_srs else None
+    L = lib()
+    args = (arr, n, srs, gt, xsize, ysize, win.ctypes.data_as(C.c_void_p), off.ctypes.data_as(C.c_void_p),
+            C.byref(total))
+    check(L.gskyhip_drill_descriptors_device(*args, None, st.ctypes.data_as(C.c_void_p), _stream()),
+          "drill_descriptors_device")
+    masks = torch.empty(int(total.value), dtype=torch.uint8, device=dev)
+    check(L.gskyhip_drill_descriptors_device(*args, C.c_void_p(masks.data_ptr()), st.ctypes.data_as(C.c_void_p),
+                                             _stream()), "drill_descriptors_device")
+    mb = MaskBatch(torch.from_numpy(win[:n].copy()).to(dev), torch.from_numpy(off[:n].copy()).to(dev), masks)
+    return mb, st[:n]
 
 
 REFERENCE_ORDER, WAVE_SPLIT = 0, 1

@@ -419,6 +419,15 @@ int gskyhip_drill_descriptors(const char *const *geometries, int n, const char *
 
 /* DrillMerger weighted mean (drill_merger.go:79-93): values/counts dev
  * n_files x n_dates, out dev n_dates (NaN where no count). */
+/* The same descriptors with the ALL_TOUCHED masks rasterized on the GPU
+ * straight into masks_dev (dev, mask_bytes: call once with masks_dev NULL to
+ * size it), one workgroup per polygon (edges, then scanlines) -- the
+ * expressions of the host rasterizer, bit-identical masks.  win_out,
+ * mask_off_out, mask_bytes_out, status_out are host arrays as above. */
+int gskyhip_drill_descriptors_device(const char *const *geometries, int n, const char *dataset_srs,
+                                     const double *geot, int xsize, int ysize, int32_t *win_out,
+                                     int64_t *mask_off_out, int64_t *mask_bytes_out, uint8_t *masks_dev,
+                                     int32_t *status_out, void *stream);
 int gskyhip_drill_merge(const double *values, const int32_t *counts, int n_files,
                         int n_dates, double *out, void *stream);
 

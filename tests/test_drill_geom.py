@@ -109,3 +109,47 @@ def test_descriptor_bad_geometry():
     win, off, buf, st = drill.drill_descriptors(['{"type": "Point", "coordinates": [1, 2]}', "nonsense"],
                                                 "EPSG:4326", GT4326, 2048, 2048)
     assert (st != 0).all() and (win == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("srs,seed", [("EPSG:4326", 5), ("EPSG:3577", 6)])
+def test_descriptor_masks_on_gpu(oracle, srs, seed):
+    """The ALL_TOUCHED masks burnt on the GPU (gskyhip_drill_descriptors_device:
+    one workgroup per polygon, edges then scanlines) are the host rasterizer's
+    masks byte for byte, and the oracle's; the windows / offsets / status are
+    the host call's.  Includes polygons crossing the file edge, a multipolygon
+    with a hole and one polygon with more vertices than a GPU thread keeps
+    intersections for (host fallback)."""
+    import torch
+    if srs == "EPSG:4326":
+        gt, size = GT4326, 2048
+        geoms = stars(150, gt, size, seed)
+        outer = close([(130.1, -20.1), (130.5, -20.1), (130.5, -20.5), (130.1, -20.5)])
+        hole = close([(130.2, -20.2), (130.4, -20.2), (130.4, -20.4), (130.2, -20.4)])
+        geoms.append(json.dumps({"type": "MultiPolygon", "coordinates": [[[list(p) for p in outer],
+                                                                          [list(p) for p in hole]]]}))
+        ang = np.linspace(0, 2 * np.pi, 90, endpoint=False)
+        rad = 0.2 + 0.05 * np.sin(ang * 7)
+        geoms.append(feature([close(np.stack([130.9 + rad * np.cos(ang), -20.9 + rad * np.sin(ang)], 1))]))
+    else:
+        gt, size = [-300000.0, 250.0, 0.0, -2800000.0, 0.0, -250.0], 2400
+        rng = np.random.default_rng(seed)
+        geoms = []
+        for p in range(60):
+            lon0, lat0 = rng.uniform(128.5, 135.0), rng.uniform(-31.5, -25.0)
+            geoms.append(feature([close(synth.star_polygon(lon0, lat0, rng.uniform(0.05, 0.6), k=9, seed=p))]))
+    win, off, buf, st = drill.drill_descriptors(geoms, srs, gt, size, size)
+    mb, st2 = drill.drill_dataset(geoms, srs, gt, size, size, device="cuda", rasterize="gpu")
+    torch.cuda.synchronize()
+    assert np.array_equal(st, st2)
+    assert np.array_equal(mb.win.cpu().numpy(), win) and np.array_equal(mb.mask_off.cpu().numpy(), off)
+    gm = mb.masks.cpu().numpy()
+    assert gm.size == buf.size and np.array_equal(gm, buf)
+    n_ok = 0
+    for i, g in enumerate(geoms):
+        if st[i] != 0:
+            continue
+        ew, em = oracle.drill_descriptor(g, srs, gt, size, size)
+        assert np.array_equal(gm[off[i]:off[i] + ew[2] * ew[3]].reshape(ew[3], ew[2]), em), i
+        n_ok += 1
+    assert n_ok > len(geoms) // 2
