@@ -1247,6 +1247,7 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.nn_wpe = 0;
   a.nn_express = 1;
   a.nn_wide = 1;
+  a.nn_rpw = 4;
   a.bil_kernel = 1;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));

@@ -219,6 +219,7 @@ struct RenderArgs {
   int nn_xcd;                  // render_nn_kernel: XCD-aware item order (A/B knob)
   int nn_probe;                // timing-only probes of render_nn_kernel (0: off; see render_nn.h)
   int nn_wpe;                  // render_nn2_kernel: minimum waves per SIMD it is compiled for (A/B knob)
+  int nn_rpw;                  // render_nn_kernel: rows per wave (4 default; 8 / 16 A/B)
   int nn_wide;                 // render_nn2_kernel: 16-B source-row loads for 16-bit values (A/B knob)
   int nn_express;              // render_nn2_kernel: single-entry express path (A/B knob)
   int bil_kernel;              // 1: render_bil_kernel for bilinear float canvases (default), 0: render_lds_kernel

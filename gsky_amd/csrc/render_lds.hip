@@ -24,6 +24,8 @@ void launch_lds_kernels(const RenderArgs &a0, int vt, bool mask, int n_items, hi
   a.nn_probe = np ? atoi(np) : 0;
   const char *nw = getenv("GSKYHIP_NN_WPE");
   a.nn_wpe = nw ? atoi(nw) : 0;
+  const char *rp = getenv("GSKYHIP_NN_RPW");
+  a.nn_rpw = rp ? atoi(rp) : 4;
   const char *nw2 = getenv("GSKYHIP_NN_WIDE");
   a.nn_wide = nw2 ? atoi(nw2) : 1;
   const char *ne = getenv("GSKYHIP_NN_EXPRESS");

@@ -106,7 +106,7 @@ __device__ __forceinline__ void nn_row_index(const RowRec *__restrict__ rr, cons
   }
 }
 
-template <typename T, bool MASK, int LPX, int R, int FLAGS>
+template <typename T, bool MASK, int LPX, int R, int FLAGS, int RPW = 4>
 __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                         const int32_t *__restrict__ order,
                                                         const RowRec *__restrict__ rows,
@@ -123,7 +123,8 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
   // share source rows through the MALL
   const int item = per_xcd > 0 ? (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3) : (int)blockIdx.x;
   if (item >= n_items) return;
-  const int bands_per_tile = (a.max_h + kBandRows - 1) / kBandRows;
+  constexpr int kRowsPerBlock = 4 * RPW;   // RPW rows per wave (A/B knob nn_rpw; 4 = kBandRows)
+  const int bands_per_tile = (a.max_h + kRowsPerBlock - 1) / kRowsPerBlock;
   const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
   const int t = item / (bands_per_tile * col_blocks);
   const int in_tile = item - t * bands_per_tile * col_blocks;
@@ -131,14 +132,14 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
   if (tp.complex || tp.vt != vt_code<T>()) return;
   const gskyhip_tile &tile = tiles[t];
   const int W = tile.width, H = tile.height;
-  const int band0 = (in_tile / col_blocks) * kBandRows;
+  const int band0 = (in_tile / col_blocks) * kRowsPerBlock;
   const int xb = (in_tile % col_blocks) * kBandCols;
   if (band0 >= H || xb >= W) return;
   const int tid = threadIdx.x;
   if (a.ramp) s_ramp[tid] = a.ramp[tid];
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int r0 = band0 + wave * 4;
+  const int r0 = band0 + wave * RPW;
   if (r0 >= H) return;
 
   const int ns_out = a.out_ns[0];
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
   for (int cx = xb; cx < xend; cx += kCols) {
     const int x0 = cx + lane * LPX;
 #pragma unroll 1
-    for (int j = 0; j < 4; j += R) {
+    for (int j = 0; j < RPW; j += R) {
       const int rb = r0 + j;
       if (rb >= H) break;
       V c[R][LPX];
@@ -721,6 +722,21 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
     if (canvas) GSKY_NN_LAUNCH(false, 8, 1, kCanvas); else GSKY_NN_LAUNCH(false, 8, 1, 0);
   } else if (a.nn_shape == 2) {
     if (canvas) GSKY_NN_LAUNCH(false, 8, 2, kCanvas); else GSKY_NN_LAUNCH(false, 8, 2, 0);
+  } else if (a.nn_shape == 3 && a.nn_rpw > 4) {   // A/B: 8 or 16 rows per wave, fewer and longer waves
+    const int rows_blk = 4 * (a.nn_rpw >= 16 ? 16 : 8);
+    const int items = a.n_tiles * ((a.max_h + rows_blk - 1) / rows_blk) * ((a.max_w + kBandCols - 1) / kBandCols);
+    const dim3 g2((unsigned)items);
+    if (a.nn_rpw >= 16) {
+      if (canvas) hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, kCanvas, 16>), g2, dim3(256), 0, s, a,
+                                     a.entries, a.order, a.rows, a.pool, a.tplans, a.tiles, items, 0);
+      else hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, 0, 16>), g2, dim3(256), 0, s, a, a.entries, a.order,
+                              a.rows, a.pool, a.tplans, a.tiles, items, 0);
+    } else {
+      if (canvas) hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, kCanvas, 8>), g2, dim3(256), 0, s, a,
+                                     a.entries, a.order, a.rows, a.pool, a.tplans, a.tiles, items, 0);
+      else hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, 0, 8>), g2, dim3(256), 0, s, a, a.entries, a.order,
+                              a.rows, a.pool, a.tplans, a.tiles, items, 0);
+    }
   } else if (a.nn_shape == 3) {
     if (canvas) GSKY_NN_LAUNCH(false, 4, 2, kCanvas); else GSKY_NN_LAUNCH(false, 4, 2, 0);
   } else {

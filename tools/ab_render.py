@@ -55,8 +55,10 @@ def main():
         from oracle import oracle as O
         from tests.helpers import oracle_render
         exp = torch.from_numpy(oracle_render(O, cfg, n_threads=16)).to("cuda")
-    # (name, typed, LDS_STAGE, LDS_FLAGS, NN_KERNEL, NN_SHAPE[, NN_XCD, NN_PROBE, NN_GEN, NN_WPE, NN_EXPRESS, NN_WIDE])
-    variants = [("nn3w_4x1", True, "0", "0", "1", "4", "0", "0", "3", "0", "1", "1"),
+    # (name, typed, LDS_STAGE, LDS_FLAGS, NN_KERNEL, NN_SHAPE[, NN_XCD, NN_PROBE, NN_GEN, NN_WPE, NN_EXPRESS, NN_WIDE, NN_RPW])
+    variants = [("nn_4x2_rpw16", True, "0", "0", "1", "3", "0", "0", "2", "0", "1", "0", "16"),
+                ("nn_4x2_rpw8", True, "0", "0", "1", "3", "0", "0", "2", "0", "1", "0", "8"),
+                ("nn3w_4x1", True, "0", "0", "1", "4", "0", "0", "3", "0", "1", "1"),
                 ("nn3w_4x2", True, "0", "0", "1", "3", "0", "0", "3", "0", "1", "1"),
                 ("nn3w_4x1_nox", True, "0", "0", "1", "4", "0", "0", "3", "0", "0", "1"),
                 ("nn3_4x2", True, "0", "0", "1", "3", "0", "0", "3"), ("nn3_4x4", True, "0", "0", "1", "0", "0", "0", "3"),
@@ -84,6 +86,7 @@ def main():
         os.environ["GSKYHIP_NN_WPE"] = extra[3] if len(extra) > 3 else "0"
         os.environ["GSKYHIP_NN_EXPRESS"] = extra[4] if len(extra) > 4 else "1"
         os.environ["GSKYHIP_NN_WIDE"] = extra[5] if len(extra) > 5 else "0"
+        os.environ["GSKYHIP_NN_RPW"] = extra[6] if len(extra) > 6 else "4"
         b.typed = typed
         med, mn = time_render(b, sp, pal, args.reps)
         out = b.render(sp, pal).clone()
