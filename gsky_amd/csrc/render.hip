@@ -51,6 +51,23 @@ struct PlanArgs {
   EntryD *entries;             // n_pairs render descriptors
   SepCol *sepcols;             // 3 per pair: column parts of the separable transform
   int sep;                     // 1: plan_rows uses the separable transform where it applies
+  int n_granules;
+  struct GEdge *gedge;         // per granule: SuggestedWarpOutput2 edge samples in dst georef (or NULL)
+};
+
+// The 84 edge samples of GDALSuggestedWarpOutput2 taken through the
+// transformer up to destination GEOREFERENCED coordinates.  They depend on
+// the granule (source geotransform + CRS) and the batch's destination CRS
+// only, not on the tile, so granule_edges_kernel computes them once per
+// granule and every pair of that granule applies just its tile's inverse
+// geotransform -- the last step of xform_point(), the same operations, so
+// the samples are bit-identical to the per-pair transform (C2: ~300 pairs
+// share each granule's PROJ work).  n_fail > 0 sends the pairs of that
+// granule back to the per-pair path (which then samples the 21 x 21 grid).
+struct GEdge {
+  double x[4 * 21], y[4 * 21];
+  int32_t n_fail;
+  int32_t _pad;
 };
 
 // ---------------------------------------------------------------- pair ownership
@@ -142,6 +159,57 @@ __device__ int must_adjust2(const Xform &t, const double *er, double psxr, doubl
 constexpr int kSteps = 20;
 constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 
+// First half of xform_point(t, false, ...): source pixel -> destination
+// georeferenced coordinates (the same expressions and order).
+__device__ __forceinline__ bool src_to_dst_georef(const Xform &t, double x, double y, double &X, double &Y) {
+  const double *g1 = t.src_gt;
+  X = g1[0] + x * g1[1] + y * g1[2];
+  Y = g1[3] + x * g1[4] + y * g1[5];
+  if (t.reproject) {
+    double lam, phi;
+    if (!crs_inverse(t.src, X, Y, lam, phi)) return false;
+    if (!crs_forward(t.dst, lam, phi, X, Y)) return false;
+  }
+  return true;
+}
+
+// One wavefront per granule: its GEdge (see PlanArgs).
+__global__ __launch_bounds__(64) void granule_edges_kernel(PlanArgs a) {
+  const int g = blockIdx.x, lane = threadIdx.x;
+  if (g >= a.n_granules) return;
+  const gskyhip_granule &gr = a.granules[g];
+  Xform t;
+  t.src = a.crs[gr.crs];
+  t.reproject = 0;
+  if (a.dst_crs >= 0) {
+    t.dst = a.crs[a.dst_crs];
+    t.reproject = crs_same(t.src, t.dst) ? 0 : 1;
+  } else {
+    t.dst = t.src;
+  }
+  for (int k = 0; k < 6; k++) t.src_gt[k] = gr.geot[k];
+  const int nInX = gr.xsize, nInY = gr.ysize;
+  const double dfStep = 1.0 / kSteps;
+  GEdge &E = a.gedge[g];
+  int fail = 0;
+  for (int k = lane; k < 4 * (kSteps + 1); k += 64) {
+    const int i = k >> 2, e = k & 3;
+    const double r = (i == kSteps) ? 1.0 : i * dfStep;
+    double x, y;
+    if (e == 0) { x = r * nInX; y = 0.0; }
+    else if (e == 1) { x = r * nInX; y = nInY; }
+    else if (e == 2) { x = 0.0; y = r * nInY; }
+    else { x = nInX; y = r * nInY; }
+    double X = 0.0, Y = 0.0;
+    const bool ok = src_to_dst_georef(t, x, y, X, Y);
+    E.x[k] = X;
+    E.y[k] = Y;
+    fail += ok ? 0 : 1;
+  }
+  for (int o = 32; o > 0; o >>= 1) fail += __shfl_xor(fail, o, 64);
+  if (lane == 0) E.n_fail = fail;
+}
+
 // GDALSuggestedWarpOutput2 (gdaltransformer.cpp 3.0.1, nOptions = 0) of the
 // transformer t over an nInX x nInY source, by one wavefront: 21 samples on
 // each source edge (the full 21 x 21 grid when an edge point fails), the
@@ -150,10 +218,18 @@ constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 // ext (dst extent), psx / psy (pixel size), nPixels / nLines on success.
 __device__ int suggested_warp_output2(const Xform &t, int nInX, int nInY, int lane, double *sx, double *sy,
                                       int *sok, double ext[4], double &psx, double &psy, int &nPixels,
-                                      int &nLines) {
+                                      int &nLines, const GEdge *ge = nullptr) {
   const double dfStep = 1.0 / kSteps;
   int ns = 4 * (kSteps + 1);
-  for (int k = lane; k < ns; k += 64) {
+  if (ge && ge->n_fail == 0) {   // shared georeferenced samples: only this tile's inverse geotransform
+    const double *g2 = t.dst_igt;
+    for (int k = lane; k < ns; k += 64) {
+      const double X = ge->x[k], Y = ge->y[k];
+      sx[k] = g2[0] + X * g2[1] + Y * g2[2];
+      sy[k] = g2[3] + X * g2[4] + Y * g2[5];
+      sok[k] = 1;
+    }
+  } else for (int k = lane; k < ns; k += 64) {
     int i = k >> 2, e = k & 3;
     double r = (i == kSteps) ? 1.0 : i * dfStep;
     double x, y;
@@ -292,7 +368,8 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
   const int nInX = g.xsize, nInY = g.ysize;
   double ext[4], psx, psy;
   int nPixels, nLines;
-  int err = suggested_warp_output2(t, nInX, nInY, lane, sx, sy, sok, ext, psx, psy, nPixels, nLines);
+  int err = suggested_warp_output2(t, nInX, nInY, lane, sx, sy, sok, ext, psx, psy, nPixels, nLines,
+                                   a.gedge ? a.gedge + gi : nullptr);
   if (lane != 0) return;
 
   // ---- overview pick (warp.go:156-198)
@@ -516,9 +593,10 @@ __device__ void plan_tile_serial(const PlanArgs &a, int t) {
     else if (v > 0 && vt != v) vt = 0;
   }
   tp.vt = vt < 0 ? 0 : vt;
-  // mixed types, promotion, or no entry at all: the general kernel renders
-  // the tile (an empty tile must still be written: transparent / nodata)
-  if (tp.vt == 0) {
+  // mixed types or promotion: the general kernel renders the tile; a tile
+  // with no entry at all is written (transparent / zero canvas) by whichever
+  // band kernel the batch launches (n_entries == 0 passes their type test)
+  if (n > 0 && tp.vt == 0) {
     tp.complex = 1;
     const int k = atomicAdd(&a.counters[2], 1);
     a.complex_list[k] = t;
@@ -654,7 +732,7 @@ __global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
     }
   }
   tp.vt = (vzero || vmax < 0 || vmin != vmax) ? 0 : vmax;
-  if (tp.vt == 0) {   // as above: empty tiles too
+  if (n > 0 && tp.vt == 0) {   // as above: empty tiles go to the band kernel
     tp.complex = 1;
     const int k = atomicAdd(&a.counters[2], 1);
     a.complex_list[k] = t;
@@ -1172,6 +1250,17 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   if (rc.n_pairs > 0)
     hipLaunchKernelGGL(pair_tile_kernel, dim3((rc.n_pairs + 255) / 256), dim3(256), 0, s, rc.tiles, rc.n_tiles,
                        rc.n_pairs, cv.pair_tile);
+  // per-granule edge samples, staged in the split-list region (plan_rows
+  // writes that list only after plan_pairs has read the table)
+  a.n_granules = rc.n_granules;
+  a.gedge = nullptr;
+  const char *ge_env = getenv("GSKYHIP_GRANULE_EDGES");   // A/B knob: 0 = per-pair edge transforms
+  const bool ge_on = ge_env ? atoi(ge_env) != 0 : true;
+  if (ge_on && rc.n_granules > 0 && rc.n_pairs > 0 &&
+      (int64_t)sizeof(GEdge) * rc.n_granules <= (int64_t)sizeof(int64_t) * rc.n_pairs * rc.max_h) {
+    a.gedge = (GEdge *)cv.split_list;
+    hipLaunchKernelGGL(granule_edges_kernel, dim3(rc.n_granules), dim3(64), 0, s, a);
+  }
   if (rc.n_pairs > 0) hipLaunchKernelGGL(plan_pairs_kernel, dim3(rc.n_pairs), dim3(64), 0, s, a);
   hipLaunchKernelGGL(plan_tiles_kernel, dim3(rc.n_tiles), dim3(64), 0, s, a);
   if (rc.n_pairs > 0) {

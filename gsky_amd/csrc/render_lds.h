@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void render_lds_kernel(RenderArgs a, const Ent
   const int t = item / (bands_per_tile * col_blocks);
   const int in_tile = item - t * bands_per_tile * col_blocks;
   const TilePlan &tp = tplans[t];
-  if (tp.complex || tp.vt != vt_code<T>()) return;
+  if (tp.complex || (tp.n_entries > 0 && tp.vt != vt_code<T>())) return;   // empty tiles: written here
   const gskyhip_tile &tile = tiles[t];
   const int W = tile.width, H = tile.height;
   const int band0 = (in_tile / col_blocks) * kBandRows;

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
   const int t = item / (bands_per_tile * col_blocks);
   const int in_tile = item - t * bands_per_tile * col_blocks;
   const TilePlan &tp = tplans[t];
-  if (tp.complex || tp.vt != vt_code<T>()) return;
+  if (tp.complex || (tp.n_entries > 0 && tp.vt != vt_code<T>())) return;   // empty tiles: written here
   const gskyhip_tile &tile = tiles[t];
   const int W = tile.width, H = tile.height;
   const int band0 = (in_tile / col_blocks) * kRowsPerBlock;
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256, WPE) void render_nn2_kernel(RenderArgs a, cons
   const int t = item / (bands_per_tile * col_blocks);
   const int in_tile = item - t * bands_per_tile * col_blocks;
   const TilePlan &tp = tplans[t];
-  if (tp.complex || tp.vt != vt_code<T>()) return;
+  if (tp.complex || (tp.n_entries > 0 && tp.vt != vt_code<T>())) return;   // empty tiles: written here
   const gskyhip_tile &tile = tiles[t];
   const int W = tile.width, H = tile.height;
   const int band0 = (in_tile / col_blocks) * kBandRows;
