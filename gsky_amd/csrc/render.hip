@@ -7,7 +7,7 @@
 //   plan_tiles_kernel   one thread per tile: merge order of ProcessRasterStack
 //                       (tile_merger.go:281-312), maskMap links, fill/overwrite
 //                       mode of MergeMaskedRaster (tile_merger.go:47).
-//   plan_rows_kernel    one thread per (pair, window row): GDALApproxTransform
+//   plan_rows_kernel    one thread per window row, workgroups per pair: GDALApproxTransform
 //                       (max error 0.125) reduced to row records / leaves.
 //   render_kernel       one lane per 4 output pixels: gather (NN or bilinear)
 //                       from HBM-resident granules, ordered nodata/mask fold,
@@ -100,6 +100,12 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 
+// xform_point behind a call: the planning wave runs it from six sites, and
+// inlining every copy of the projection math costs the kernel its occupancy.
+__device__ __noinline__ bool xform_point_nl(const Xform &t, bool dst_to_src, double &x, double &y) {
+  return xform_point(t, dst_to_src, x, y);
+}
+
 // GDALSuggestedWarpOutput2_MustAdjustFor{Right,Bottom}Border, lanes 0..20.
 __device__ bool must_adjust(const Xform &t, const double *ext, int np, int nl, double psx,
                             double psy, bool right, int lane) {
@@ -116,8 +122,8 @@ __device__ bool must_adjust(const Xform &t, const double *ext, int np, int nl, d
     double ax, ay;
     if (right) { ax = ext[2]; ay = ext[3] - psy * r1 * nl; }
     else { ax = ext[0] + psx * r1 * np; ay = ext[1]; }
-    bool ok1 = xform_point(t, true, ax, ay);
-    bool ok2 = ok1 ? xform_point(t, false, ax, ay) : false;
+    bool ok1 = xform_point_nl(t, true, ax, ay);
+    bool ok2 = ok1 ? xform_point_nl(t, false, ax, ay) : false;
     double ex = right ? ext[2] : ext[0] + psx * r2 * np;
     double ey = right ? ext[3] - psy * r2 * nl : ext[1];
     bad = !ok1 || !ok2 || fabs(ax - ex) > psx || fabs(ay - ey) > psy;
@@ -146,8 +152,8 @@ __device__ int must_adjust2(const Xform &t, const double *er, double psxr, doubl
     double ax, ay;
     if (right) { ax = ext[2]; ay = ext[3] - psy * r1 * nl; }
     else { ax = ext[0] + psx * r1 * np; ay = ext[1]; }
-    bool ok1 = xform_point(t, true, ax, ay);
-    bool ok2 = ok1 ? xform_point(t, false, ax, ay) : false;
+    bool ok1 = xform_point_nl(t, true, ax, ay);
+    bool ok2 = ok1 ? xform_point_nl(t, false, ax, ay) : false;
     double ex = right ? ext[2] : ext[0] + psx * r2 * np;
     double ey = right ? ext[3] - psy * r2 * nl : ext[1];
     bad = !ok1 || !ok2 || fabs(ax - ex) > psx || fabs(ay - ey) > psy;
@@ -159,7 +165,7 @@ __device__ int must_adjust2(const Xform &t, const double *er, double psxr, doubl
 constexpr int kSteps = 20;
 constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 
-// First half of xform_point(t, false, ...): source pixel -> destination
+// First half of xform_point_nl(t, false, ...): source pixel -> destination
 // georeferenced coordinates (the same expressions and order).
 __device__ __forceinline__ bool src_to_dst_georef(const Xform &t, double x, double y, double &X, double &Y) {
   const double *g1 = t.src_gt;
@@ -237,7 +243,7 @@ __device__ int suggested_warp_output2(const Xform &t, int nInX, int nInY, int la
     else if (e == 1) { x = r * nInX; y = nInY; }
     else if (e == 2) { x = 0.0; y = r * nInY; }
     else { x = nInX; y = r * nInY; }
-    int ok = xform_point(t, false, x, y);
+    int ok = xform_point_nl(t, false, x, y);
     sx[k] = x; sy[k] = y; sok[k] = ok;
   }
   __syncthreads();
@@ -252,7 +258,7 @@ __device__ int suggested_warp_output2(const Xform &t, int nInX, int nInY, int la
       double ry = (iy == kSteps) ? 1.0 : iy * dfStep;
       double rx = (ix == kSteps) ? 1.0 : ix * dfStep;
       double x = rx * nInX, y = ry * nInY;
-      int ok = xform_point(t, false, x, y);
+      int ok = xform_point_nl(t, false, x, y);
       sx[k] = x; sy[k] = y; sok[k] = ok;
     }
     __syncthreads();
@@ -350,19 +356,25 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
   Xform &xf = a.xforms[p];
   PairPlan &pp = a.pairs[p];
 
-  // ---- transformer (warp.go:120-148)
-  Xform t;
-  t.src = a.crs[g.crs];
-  t.reproject = 0;
-  if (a.dst_crs >= 0) {
-    t.dst = a.crs[a.dst_crs];
-    t.reproject = crs_same(t.src, t.dst) ? 0 : 1;
-  } else {
-    t.dst = t.src;
+  // ---- transformer (warp.go:120-148), kept in LDS: the wave-uniform state
+  // would otherwise live in scratch (xform_point selects its geotransforms
+  // through pointers) or cost ~130 VGPRs
+  __shared__ Xform ts;
+  Xform &t = ts;
+  if (lane == 0) {
+    t.src = a.crs[g.crs];
+    t.reproject = 0;
+    if (a.dst_crs >= 0) {
+      t.dst = a.crs[a.dst_crs];
+      t.reproject = crs_same(t.src, t.dst) ? 0 : 1;
+    } else {
+      t.dst = t.src;
+    }
+    for (int k = 0; k < 6; k++) { t.src_gt[k] = g.geot[k]; t.dst_gt[k] = tile.dst_geot[k]; }
+    inv_geot(t.src_gt, t.src_igt);
+    inv_geot(t.dst_gt, t.dst_igt);
   }
-  for (int k = 0; k < 6; k++) { t.src_gt[k] = g.geot[k]; t.dst_gt[k] = tile.dst_geot[k]; }
-  inv_geot(t.src_gt, t.src_igt);
-  inv_geot(t.dst_gt, t.dst_igt);
+  __syncthreads();
 
   // ---- GDALSuggestedWarpOutput2 (warp.go:154)
   const int nInX = g.xsize, nInY = g.ysize;
@@ -777,14 +789,7 @@ __global__ __launch_bounds__(256) void plan_cols_kernel(PlanArgs a) {
 // Light pass, one thread per (pair, window row): the three exact points of
 // GDALApproxTransform (first / middle / last) and its error test.  Rows whose
 // middle error exceeds 0.125 go to the split list (plan_split_kernel).
-__global__ __launch_bounds__(256) void plan_rows_kernel(PlanArgs a) {
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int p = (int)(gid / a.max_h);
-  const int row = (int)(gid % a.max_h);
-  if (p >= a.n_pairs) return;
-  const PairPlan &pp = a.pairs[p];
-  if (row >= pp.h) return;
-  const Xform &t = a.xforms[p];
+__device__ __forceinline__ void plan_row(const PlanArgs &a, int p, const PairPlan &pp, const Xform &t, int row) {
   RowRec rec;
   rec.nleaf = 1; rec.pool_off = 0; rec.inside = 0;
   for (int k = 0; k < 6; k++) rec.v[k] = 0;
@@ -839,6 +844,18 @@ __global__ __launch_bounds__(256) void plan_rows_kernel(PlanArgs a) {
     }
   }
   a.rows[(long)p * a.max_h + row] = rec;
+}
+
+// Workgroups of one pair (blockIdx.x: pair, blockIdx.y: 256-row chunk): the
+// pair's plan and transformer are wave-uniform, so their fields arrive
+// through scalar loads rather than per-lane gathers.
+__global__ __launch_bounds__(256) void plan_rows_kernel(PlanArgs a) {
+  const int p = blockIdx.x;
+  const int row = blockIdx.y * blockDim.x + threadIdx.x;
+  if (p >= a.n_pairs) return;
+  const PairPlan &pp = a.pairs[p];
+  if (row >= pp.h) return;
+  plan_row(a, p, pp, a.xforms[p], row);
 }
 
 struct Node {
@@ -1267,8 +1284,7 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
     if (a.sep)
       hipLaunchKernelGGL(plan_cols_kernel, dim3((unsigned)((3 * (int64_t)rc.n_pairs + 255) / 256)), dim3(256), 0, s,
                          a);
-    const int64_t nthreads = (int64_t)rc.n_pairs * rc.max_h;
-    hipLaunchKernelGGL(plan_rows_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(plan_rows_kernel, dim3(rc.n_pairs, (rc.max_h + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(plan_split_kernel, dim3(1024), dim3(64), 0, s, a);
     hipLaunchKernelGGL(plan_exact_kernel, dim3(512), dim3(256), 0, s, a);
   }
