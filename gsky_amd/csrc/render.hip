@@ -58,7 +58,7 @@ struct PlanArgs {
 // The 84 edge samples of GDALSuggestedWarpOutput2 taken through the
 // transformer up to destination GEOREFERENCED coordinates.  They depend on
 // the granule (source geotransform + CRS) and the batch's destination CRS
-// only, not on the tile, so granule_edges_kernel computes them once per
+// only, not on the tile, so plan_prologue_kernel computes them once per
 // granule and every pair of that granule applies just its tile's inverse
 // geotransform -- the last step of xform_point(), the same operations, so
 // the samples are bit-identical to the per-pair transform (C2: ~300 pairs
@@ -71,11 +71,9 @@ struct GEdge {
 };
 
 // ---------------------------------------------------------------- pair ownership
-// One thread per pair: its tile is the last one whose CSR range starts at or
-// before it (tiles' pair ranges are consecutive and ascending).
-__global__ void pair_tile_kernel(const gskyhip_tile *tiles, int n_tiles, int n_pairs, int32_t *pair_tile) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n_pairs) return;
+// Pair p's tile: the last one whose CSR range starts at or before it (tiles'
+// pair ranges are consecutive and ascending).
+__device__ __forceinline__ int owning_tile(const gskyhip_tile *tiles, int n_tiles, int p) {
   int lo = 0, hi = n_tiles - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -87,7 +85,7 @@ __global__ void pair_tile_kernel(const gskyhip_tile *tiles, int n_tiles, int n_p
     for (int t = 0; t < n_tiles; t++)
       if (p >= tiles[t].pair_begin && p < tiles[t].pair_end) lo = t;
   }
-  pair_tile[p] = lo;   // -1: no tile references the pair
+  return lo;   // -1: no tile references the pair
 }
 
 // ---------------------------------------------------------------- wave helpers
@@ -179,9 +177,17 @@ __device__ __forceinline__ bool src_to_dst_georef(const Xform &t, double x, doub
   return true;
 }
 
-// One wavefront per granule: its GEdge (see PlanArgs).
-__global__ __launch_bounds__(64) void granule_edges_kernel(PlanArgs a) {
-  const int g = blockIdx.x, lane = threadIdx.x;
+// Planning prologue, 128-thread workgroups: the first n_edge_blocks take a
+// granule each, a thread per edge sample (its GEdge, see PlanArgs); the rest
+// a pair each per thread (its owning tile).
+__global__ __launch_bounds__(128) void plan_prologue_kernel(PlanArgs a, int n_edge_blocks) {
+  const int lane = threadIdx.x;
+  if ((int)blockIdx.x >= n_edge_blocks) {
+    const int p = ((int)blockIdx.x - n_edge_blocks) * 128 + lane;
+    if (p < a.n_pairs) a.pair_tile[p] = owning_tile(a.tiles, a.n_tiles, p);
+    return;
+  }
+  const int g = blockIdx.x;
   if (g >= a.n_granules) return;
   const gskyhip_granule &gr = a.granules[g];
   Xform t;
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(64) void granule_edges_kernel(PlanArgs a) {
   const double dfStep = 1.0 / kSteps;
   GEdge &E = a.gedge[g];
   int fail = 0;
-  for (int k = lane; k < 4 * (kSteps + 1); k += 64) {
+  for (int k = lane; k < 4 * (kSteps + 1); k += 128) {
     const int i = k >> 2, e = k & 3;
     const double r = (i == kSteps) ? 1.0 : i * dfStep;
     double x, y;
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(64) void granule_edges_kernel(PlanArgs a) {
     E.y[k] = Y;
     fail += ok ? 0 : 1;
   }
-  for (int o = 32; o > 0; o >>= 1) fail += __shfl_xor(fail, o, 64);
+  fail = __syncthreads_count(fail);
   if (lane == 0) E.n_fail = fail;
 }
 
@@ -1264,20 +1270,20 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   a.sep = sep ? atoi(sep) : 1;
   hipStream_t s = rc.stream;
   if (hipMemsetAsync(cv.counters, 0, 256, s) != hipSuccess) return GSKYHIP_E_HIP;
-  if (rc.n_pairs > 0)
-    hipLaunchKernelGGL(pair_tile_kernel, dim3((rc.n_pairs + 255) / 256), dim3(256), 0, s, rc.tiles, rc.n_tiles,
-                       rc.n_pairs, cv.pair_tile);
   // per-granule edge samples, staged in the split-list region (plan_rows
-  // writes that list only after plan_pairs has read the table)
+  // writes that list only after plan_pairs has read the table), in one launch
+  // with the pairs' owning tiles
   a.n_granules = rc.n_granules;
   a.gedge = nullptr;
   const char *ge_env = getenv("GSKYHIP_GRANULE_EDGES");   // A/B knob: 0 = per-pair edge transforms
   const bool ge_on = ge_env ? atoi(ge_env) != 0 : true;
   if (ge_on && rc.n_granules > 0 && rc.n_pairs > 0 &&
-      (int64_t)sizeof(GEdge) * rc.n_granules <= (int64_t)sizeof(int64_t) * rc.n_pairs * rc.max_h) {
+      (int64_t)sizeof(GEdge) * rc.n_granules <= (int64_t)sizeof(int64_t) * rc.n_pairs * rc.max_h)
     a.gedge = (GEdge *)cv.split_list;
-    hipLaunchKernelGGL(granule_edges_kernel, dim3(rc.n_granules), dim3(64), 0, s, a);
-  }
+  const int n_edge_blocks = a.gedge ? rc.n_granules : 0;
+  if (rc.n_pairs > 0)
+    hipLaunchKernelGGL(plan_prologue_kernel, dim3(n_edge_blocks + (rc.n_pairs + 127) / 128), dim3(128), 0, s, a,
+                       n_edge_blocks);
   if (rc.n_pairs > 0) hipLaunchKernelGGL(plan_pairs_kernel, dim3(rc.n_pairs), dim3(64), 0, s, a);
   hipLaunchKernelGGL(plan_tiles_kernel, dim3(rc.n_tiles), dim3(64), 0, s, a);
   if (rc.n_pairs > 0) {

@@ -224,6 +224,7 @@ struct RenderArgs {
   int nn_express;              // render_nn2_kernel: single-entry express path (A/B knob)
   int bil_kernel;              // 1: render_bil_kernel for bilinear float canvases (default), 0: render_lds_kernel
   int nn_gen;                  // NN band kernel generation: 2 render_nn_kernel (default), 3 render_nn2_kernel (A/B)
+  int nn_lut;                  // render_nn_kernel: Scale of integer canvases through a clamped-value LUT in LDS
 };
 
 // ---------------------------------------------------------------- typed fast path

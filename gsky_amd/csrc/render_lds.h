@@ -53,12 +53,12 @@ struct BandRow {
   int32_t kind, nleaf, pool_off, _pad;
 };
 
-template <typename T> __device__ constexpr int vt_code();
-template <> __device__ constexpr int vt_code<uint8_t>() { return GSKYHIP_BYTE; }
-template <> __device__ constexpr int vt_code<int8_t>() { return GSKYHIP_SIGNEDBYTE; }
-template <> __device__ constexpr int vt_code<int16_t>() { return GSKYHIP_INT16; }
-template <> __device__ constexpr int vt_code<uint16_t>() { return GSKYHIP_UINT16; }
-template <> __device__ constexpr int vt_code<float>() { return GSKYHIP_FLOAT32; }
+template <typename T> __host__ __device__ constexpr int vt_code();
+template <> __host__ __device__ constexpr int vt_code<uint8_t>() { return GSKYHIP_BYTE; }
+template <> __host__ __device__ constexpr int vt_code<int8_t>() { return GSKYHIP_SIGNEDBYTE; }
+template <> __host__ __device__ constexpr int vt_code<int16_t>() { return GSKYHIP_INT16; }
+template <> __host__ __device__ constexpr int vt_code<uint16_t>() { return GSKYHIP_UINT16; }
+template <> __host__ __device__ constexpr int vt_code<float>() { return GSKYHIP_FLOAT32; }
 
 // Exact truncated source index at distance `dist` along a linear piece (the
 // expressions of lin_coords() / nn_px()); -1 when the coordinate is negative.

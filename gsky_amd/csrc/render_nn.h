@@ -28,6 +28,35 @@ namespace gsky {
 constexpr uint32_t kNoPx = 0xFFFFFFFFu;
 constexpr int kExpress = 16;   // render_nn2_kernel: single-entry express path (A/B knob GSKYHIP_NN_EXPRESS)
 constexpr int kWide = 32;      // render_nn2_kernel: 16-B source-row loads for 16-bit values (GSKYHIP_NN_WIDE)
+constexpr int kClampLut = 64;  // render_nn_kernel: Scale through the clamped-value LUT (GSKYHIP_NN_LUT)
+constexpr int kClampLutCap = 16384;   // LUT bytes in LDS: clip values 0 .. 16383
+
+// utils.Scale of an integer canvas (scale_t) is, past the nodata test and
+// the wrap + clamp of value + offset to [0, clip], a function of the clamped
+// value alone: lut8[v] = go_u8_f32((float)v * sc) for v in [0, clip].  One
+// launch builds it for the call's scale parameters; render_nn_kernel copies
+// it to LDS and replaces the per-pixel convert / multiply / range test with
+// one byte read (the palette entry 255 doubles as the transparent pixel).
+template <typename T>
+__global__ void clamp_lut_kernel(RenderArgs a, uint8_t *lut8, int n) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  const ScaleK sk = make_scale(vt_code<T>(), 0.0, a.sp, false, 0.f, 0.f);
+  lut8[v] = (uint8_t)go_u8_f32((float)v * sk.sc);
+}
+
+// Entries of that LUT for value type T under the call's scale parameters
+// (clip in the canvas type, as make_scale() converts it), or 0 when it does
+// not fit in LDS.
+template <typename T>
+__host__ __device__ inline int clamp_lut_size(const RenderArgs &a) {
+  if constexpr (std::is_same<T, float>::value) return 0;
+  else {
+    const int clp = go_conv_to(a.sp.clip, vt_code<T>()).i;
+    const int n = (clp > 0 ? clp : 0) + 1;
+    return n <= kClampLutCap ? n : 0;
+  }
+}
 
 // Element index of each of the lane's LPX pixels on a LINEAR row, 32.32
 // fixed point.  false (wave-uniform): some valid pixel of the wave sits
@@ -116,7 +145,9 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
                                                         int per_xcd) {
   using V = typename VOf<T>::type;
   constexpr int kCols = 64 * LPX;   // columns of one wave pass
+  constexpr bool kLutOut = (FLAGS & kClampLut) != 0 && (FLAGS & kCanvas) == 0 && !std::is_same<T, float>::value;
   __shared__ uint32_t s_ramp[256];
+  __shared__ __attribute__((aligned(16))) uint8_t s_lut[kLutOut ? kClampLutCap : 16];
 
   // linear item order, or XCD-aware (per_xcd > 0: blocks b, b+8, ... share an
   // XCD and its L2) -- linear measured faster: neighbouring tiles on every XCD
@@ -136,13 +167,29 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
   const int xb = (in_tile % col_blocks) * kBandCols;
   if (band0 >= H || xb >= W) return;
   const int tid = threadIdx.x;
-  if (a.ramp) s_ramp[tid] = a.ramp[tid];
+  const int ns_out = a.out_ns[0];
+  // clamped-value LUT: only for canvases of T's own type (empty tiles may carry another)
+  const bool use_lut = kLutOut && tp.dtype[ns_out] == vt_code<T>();
+  int lut_n = 0;
+  if constexpr (kLutOut) {
+    if (use_lut) {
+      const uint32_t g = (uint32_t)tid;
+      s_ramp[tid] = tid == 255 ? 0u : (a.ramp ? a.ramp[tid] : (0xFF000000u | (g << 16) | (g << 8) | g));
+      lut_n = clamp_lut_size<T>(a);
+      const int n16 = (lut_n + 15) >> 4;
+      for (int i = tid; i < n16; i += 256)
+        reinterpret_cast<u32x4 *>(s_lut)[i] = reinterpret_cast<const u32x4 *>(a.lut)[i];
+    } else if (a.ramp) {
+      s_ramp[tid] = a.ramp[tid];
+    }
+  } else if (a.ramp) {
+    s_ramp[tid] = a.ramp[tid];
+  }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r0 = band0 + wave * RPW;
   if (r0 >= H) return;
 
-  const int ns_out = a.out_ns[0];
   const bool created = tp.created[ns_out] != 0;
   const V cnod = as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]));
   const int32_t *ord = order + tile.pair_begin;
@@ -254,11 +301,25 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
           }
         } else {
           uint32_t px[LPX];
+          if (kLutOut && use_lut) {   // scale_t(): nodata test, wrap + clamp, then the LUT byte
 #pragma unroll
-          for (int q = 0; q < LPX; q++) {
-            const uint32_t bb = scale_t<T>(sk, c[i][q]);
-            const uint32_t col = has_ramp ? s_ramp[bb & 0xFFu] : (0xFF000000u | (bb << 16) | (bb << 8) | bb);
-            px[q] = (created && bb != 0xFFu) ? col : 0u;
+            for (int q = 0; q < LPX; q++) {
+              int32_t value = c[i][q] + sk.off.i;
+              if constexpr (std::is_same<T, int8_t>::value) value = (int8_t)value;
+              else if constexpr (std::is_same<T, uint8_t>::value) value = (uint8_t)value;
+              else if constexpr (std::is_same<T, int16_t>::value) value = (int16_t)value;
+              else value = (uint16_t)value;
+              value = max(min(value, sk.clp.i), 0);
+              const uint32_t col = s_ramp[s_lut[value]];
+              px[q] = (created && c[i][q] != sk.noData.i) ? col : 0u;
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < LPX; q++) {
+              const uint32_t bb = scale_t<T>(sk, c[i][q]);
+              const uint32_t col = has_ramp ? s_ramp[bb & 0xFFu] : (0xFF000000u | (bb << 16) | (bb << 8) | bb);
+              px[q] = (created && bb != 0xFFu) ? col : 0u;
+            }
           }
           uint8_t *dst = rgba_tile + ((int64_t)r * a.max_w + x0) * 4;
           if (x0 + LPX <= W && ((((uintptr_t)dst) & 15) == 0)) {
@@ -714,8 +775,15 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
 #undef GSKY_NN2_LAUNCH
     return;
   }
+  // Scale through the clamped-value LUT (RGBA out, integer T, default shape)
+  const int lut_n = (a.nn_lut && !canvas && !fixed && a.lut && a.nn_probe == 0 &&
+                     (mask || (a.nn_shape == 3 && a.nn_rpw <= 4))) ? clamp_lut_size<T>(a) : 0;
+  if (lut_n > 0)
+    hipLaunchKernelGGL(clamp_lut_kernel<T>, dim3((lut_n + 255) / 256), dim3(256), 0, s, a, (uint8_t *)a.lut, lut_n);
   if (mask) {
-    if (canvas) GSKY_NN_LAUNCH(true, 4, 2, kCanvas); else GSKY_NN_LAUNCH(true, 4, 2, 0);
+    if (canvas) GSKY_NN_LAUNCH(true, 4, 2, kCanvas);
+    else if (lut_n > 0) GSKY_NN_LAUNCH(true, 4, 2, kClampLut);
+    else GSKY_NN_LAUNCH(true, 4, 2, 0);
   } else if (fixed) {
     if (canvas) GSKY_NN_LAUNCH(false, 4, 4, kCanvas | kFixed); else GSKY_NN_LAUNCH(false, 4, 4, kFixed);
   } else if (a.nn_shape == 1) {
@@ -738,7 +806,9 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
                               a.rows, a.pool, a.tplans, a.tiles, items, 0);
     }
   } else if (a.nn_shape == 3) {
-    if (canvas) GSKY_NN_LAUNCH(false, 4, 2, kCanvas); else GSKY_NN_LAUNCH(false, 4, 2, 0);
+    if (canvas) GSKY_NN_LAUNCH(false, 4, 2, kCanvas);
+    else if (lut_n > 0) GSKY_NN_LAUNCH(false, 4, 2, kClampLut);
+    else GSKY_NN_LAUNCH(false, 4, 2, 0);
   } else {
     if (canvas) GSKY_NN_LAUNCH(false, 4, 4, kCanvas); else GSKY_NN_LAUNCH(false, 4, 4, 0);
   }
