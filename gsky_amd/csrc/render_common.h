@@ -225,6 +225,7 @@ struct RenderArgs {
   int bil_kernel;              // 1: render_bil_kernel for bilinear float canvases (default), 0: render_lds_kernel
   int nn_gen;                  // NN band kernel generation: 2 render_nn_kernel (default), 3 render_nn2_kernel (A/B)
   int nn_lut;                  // render_nn_kernel: Scale of integer canvases through a clamped-value LUT in LDS
+  int nn_stride;               // render_nn_kernel: lane pixels 64 columns apart (1) or consecutive (0)
 };
 
 // ---------------------------------------------------------------- typed fast path

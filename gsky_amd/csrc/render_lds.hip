@@ -36,6 +36,8 @@ void launch_lds_kernels(const RenderArgs &a0, int vt, bool mask, int n_items, hi
   a.nn_gen = ng ? atoi(ng) : 2;   // render_nn_kernel unless GSKYHIP_NN_GEN=3 (render_nn2_kernel, A/B: measured 2-4 % slower)
   const char *nl = getenv("GSKYHIP_NN_LUT");
   a.nn_lut = nl ? atoi(nl) : 0;   // A/B knob (1: clamped-value LUT; measured 2 % slower on C2, r02z3)
+  const char *nsd = getenv("GSKYHIP_NN_STRIDE");
+  a.nn_stride = nsd ? atoi(nsd) : 1;   // lane pixels 64 columns apart (0: consecutive; A/B r02z4/5: C2 -2 %, C5 -12 %)
   const char *nx = getenv("GSKYHIP_NN_XCD");
   a.nn_xcd = nx ? atoi(nx) : 0;   // linear item order by default (A/B, profiles/r02g_ab_*.jsonl)
   switch (vt) {

@@ -29,6 +29,7 @@ constexpr uint32_t kNoPx = 0xFFFFFFFFu;
 constexpr int kExpress = 16;   // render_nn2_kernel: single-entry express path (A/B knob GSKYHIP_NN_EXPRESS)
 constexpr int kWide = 32;      // render_nn2_kernel: 16-B source-row loads for 16-bit values (GSKYHIP_NN_WIDE)
 constexpr int kClampLut = 64;  // render_nn_kernel: Scale through the clamped-value LUT (GSKYHIP_NN_LUT)
+constexpr int kStrided = 128;  // render_nn_kernel: lane pixels 64 columns apart (GSKYHIP_NN_STRIDE)
 constexpr int kClampLutCap = 16384;   // LUT bytes in LDS: clip values 0 .. 16383
 
 // utils.Scale of an integer canvas (scale_t) is, past the nodata test and
@@ -98,24 +99,28 @@ __device__ __forceinline__ uint32_t nn_index_sxy(double sx, double sy, bool ok, 
 
 // Element indices of the lane's LPX pixels on a window row of an entry
 // (lin_coords() + nn_px(), bit for bit).
-template <int LPX, bool FIXED>
+// S: column stride between the lane's pixels (1: consecutive, 64: the
+// wave's lanes cover 64 consecutive columns per pixel slot).
+template <int LPX, bool FIXED, int S = 1>
 __device__ __forceinline__ void nn_row_index(const RowRec *__restrict__ rr, const Leaf *__restrict__ pool, int ic0,
                                              int ew, int lim, int bx, int by, uint32_t *idx) {
   const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
   if (kind == ROW_LINEAR) {
     const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
-    if (FIXED && nn_index_fixed<LPX>(xs0, ys0, dX, dY, ic0, ew, lim, bx, by, idx)) return;
+    if constexpr (S == 1) {
+      if (FIXED && nn_index_fixed<LPX>(xs0, ys0, dX, dY, ic0, ew, lim, bx, by, idx)) return;
+    }
 #pragma unroll
     for (int q = 0; q < LPX; q++) {
-      const bool in = (unsigned)(ic0 + q) < (unsigned)lim;
-      const double dist = (double)ic0 + (double)q;
+      const bool in = (unsigned)(ic0 + q * S) < (unsigned)lim;
+      const double dist = (double)ic0 + (double)(q * S);
       idx[q] = nn_index_sxy(xs0 + dX * dist, ys0 + dY * dist, in, bx, by);
     }
     return;
   }
-  // POOL (the only other kind in a simple tile): the lane's pixels are
-  // consecutive, so the leaf (the last one starting at or before the pixel,
-  // lin_coords()) only ever moves forward
+  // POOL (the only other kind in a simple tile): the lane's pixels ascend,
+  // so the leaf (the last one starting at or before the pixel, lin_coords())
+  // only ever moves forward
   const int nleaf = __builtin_amdgcn_readfirstlane(rr->nleaf);
   const Leaf *lv = pool + __builtin_amdgcn_readfirstlane(rr->pool_off);
   const int icf = ic0 > 0 ? ic0 : 0;
@@ -123,7 +128,11 @@ __device__ __forceinline__ void nn_row_index(const RowRec *__restrict__ rr, cons
   int nxt = l + 1 < nleaf ? lv[l + 1].start : 0x7FFFFFFF;
 #pragma unroll
   for (int q = 0; q < LPX; q++) {
-    const int ic = ic0 + q;
+    const int ic = ic0 + q * S;
+    if (S > 1 && ic >= nxt) {   // 64 columns on: search again rather than walk
+      l = leaf_of(lv, nleaf, ic > 0 ? ic : 0);
+      nxt = l + 1 < nleaf ? lv[l + 1].start : 0x7FFFFFFF;
+    }
     const bool in = (unsigned)ic < (unsigned)lim;
     if (in && ic >= nxt) {
       while (l + 1 < nleaf && lv[l + 1].start <= ic) l++;
@@ -146,6 +155,10 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
   using V = typename VOf<T>::type;
   constexpr int kCols = 64 * LPX;   // columns of one wave pass
   constexpr bool kLutOut = (FLAGS & kClampLut) != 0 && (FLAGS & kCanvas) == 0 && !std::is_same<T, float>::value;
+  // S: column step between a lane's pixels.  1: LPX consecutive pixels (one
+  // 16-B store); 64: each pixel slot of the wave covers 64 consecutive
+  // columns, so one gather instruction touches about half the source lines
+  constexpr int S = (FLAGS & kStrided) != 0 ? 64 : 1;
   __shared__ uint32_t s_ramp[256];
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[kLutOut ? kClampLutCap : 16];
 
@@ -201,7 +214,7 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
 
 #pragma unroll 1
   for (int cx = xb; cx < xend; cx += kCols) {
-    const int x0 = cx + lane * LPX;
+    const int x0 = cx + (S == 1 ? lane * LPX : lane);
 #pragma unroll 1
     for (int j = 0; j < RPW; j += R) {
       const int rb = r0 + j;
@@ -240,7 +253,7 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
 #pragma unroll
             for (int q = 0; q < LPX; q++) idx[i][q] = kNoPx;
           } else {
-            nn_row_index<LPX, (FLAGS & kFixed) != 0>(rows + row_base + ir, pool, ic0, ew, lim, bx, by, idx[i]);
+            nn_row_index<LPX, (FLAGS & kFixed) != 0, S>(rows + row_base + ir, pool, ic0, ew, lim, bx, by, idx[i]);
           }
 #pragma unroll
           for (int q = 0; q < LPX; q++) vv[i][q] = buf_load<T>(rs, idx[i][q] * (uint32_t)sizeof(T));
@@ -251,11 +264,11 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
           const int ir = rb + i - eyoff;
 #pragma unroll
           for (int q = 0; q < LPX; q++) {
-            const bool in = (unsigned)(ic0 + q) < (unsigned)lim && ir >= 0 && ir < eh;
+            const bool in = (unsigned)(ic0 + q * S) < (unsigned)lim && ir >= 0 && ir < eh;
             const V v = idx[i][q] != kNoPx ? vv[i][q] : fillv;
             bool take = in && (v != nd);
             if (MASK && e.mask_pair >= 0) {
-              if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, e, ic0 + q, ir);
+              if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, e, ic0 + q * S, ir);
             }
             const bool t2 = take && (!fill_mode || c[i][q] == nd);
             c[i][q] = t2 ? v : c[i][q];
@@ -277,7 +290,11 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
 #pragma unroll
           for (int q = 0; q < LPX; q++) tv[q] = (T)c[i][q];
           constexpr int kBytes = (int)sizeof(T) * LPX;
-          if (x0 + LPX <= W && (((uintptr_t)cdst) & (kBytes >= 16 ? 15 : kBytes - 1)) == 0) {
+          if constexpr (S > 1) {
+#pragma unroll
+            for (int q = 0; q < LPX; q++)
+              if (x0 + q * S < W) cdst[q * S] = tv[q];
+          } else if (x0 + LPX <= W && (((uintptr_t)cdst) & (kBytes >= 16 ? 15 : kBytes - 1)) == 0) {
             if constexpr (kBytes % 16 == 0) {
 #pragma unroll
               for (int h = 0; h < kBytes / 16; h++) {
@@ -322,7 +339,11 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
             }
           }
           uint8_t *dst = rgba_tile + ((int64_t)r * a.max_w + x0) * 4;
-          if (x0 + LPX <= W && ((((uintptr_t)dst) & 15) == 0)) {
+          if constexpr (S > 1) {   // 64 lanes x 4 B contiguous per store
+#pragma unroll
+            for (int q = 0; q < LPX; q++)
+              if (x0 + q * S < W) __builtin_nontemporal_store(px[q], (GPTR(uint32_t))(dst + 4 * q * S));
+          } else if (x0 + LPX <= W && ((((uintptr_t)dst) & 15) == 0)) {
 #pragma unroll
             for (int h = 0; h < LPX / 4; h++) {
               u32x4 v4 = {px[4 * h], px[4 * h + 1], px[4 * h + 2], px[4 * h + 3]};
@@ -780,14 +801,22 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
                      (mask || (a.nn_shape == 3 && a.nn_rpw <= 4))) ? clamp_lut_size<T>(a) : 0;
   if (lut_n > 0)
     hipLaunchKernelGGL(clamp_lut_kernel<T>, dim3((lut_n + 255) / 256), dim3(256), 0, s, a, (uint8_t *)a.lut, lut_n);
-  if (mask) {
+  if (mask && a.nn_stride) {
+    if (canvas) GSKY_NN_LAUNCH(true, 4, 2, kCanvas | kStrided);
+    else if (lut_n > 0) GSKY_NN_LAUNCH(true, 4, 2, kClampLut | kStrided);
+    else GSKY_NN_LAUNCH(true, 4, 2, kStrided);
+  } else if (mask) {
     if (canvas) GSKY_NN_LAUNCH(true, 4, 2, kCanvas);
     else if (lut_n > 0) GSKY_NN_LAUNCH(true, 4, 2, kClampLut);
     else GSKY_NN_LAUNCH(true, 4, 2, 0);
   } else if (fixed) {
     if (canvas) GSKY_NN_LAUNCH(false, 4, 4, kCanvas | kFixed); else GSKY_NN_LAUNCH(false, 4, 4, kFixed);
+  } else if (a.nn_shape == 1 && a.nn_stride) {
+    if (canvas) GSKY_NN_LAUNCH(false, 8, 1, kCanvas | kStrided); else GSKY_NN_LAUNCH(false, 8, 1, kStrided);
   } else if (a.nn_shape == 1) {
     if (canvas) GSKY_NN_LAUNCH(false, 8, 1, kCanvas); else GSKY_NN_LAUNCH(false, 8, 1, 0);
+  } else if (a.nn_shape == 2 && a.nn_stride) {
+    if (canvas) GSKY_NN_LAUNCH(false, 8, 2, kCanvas | kStrided); else GSKY_NN_LAUNCH(false, 8, 2, kStrided);
   } else if (a.nn_shape == 2) {
     if (canvas) GSKY_NN_LAUNCH(false, 8, 2, kCanvas); else GSKY_NN_LAUNCH(false, 8, 2, 0);
   } else if (a.nn_shape == 3 && a.nn_rpw > 4) {   // A/B: 8 or 16 rows per wave, fewer and longer waves
@@ -805,6 +834,10 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
       else hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, 0, 8>), g2, dim3(256), 0, s, a, a.entries, a.order,
                               a.rows, a.pool, a.tplans, a.tiles, items, 0);
     }
+  } else if (a.nn_shape == 3 && a.nn_stride) {
+    if (canvas) GSKY_NN_LAUNCH(false, 4, 2, kCanvas | kStrided);
+    else if (lut_n > 0) GSKY_NN_LAUNCH(false, 4, 2, kClampLut | kStrided);
+    else GSKY_NN_LAUNCH(false, 4, 2, kStrided);
   } else if (a.nn_shape == 3) {
     if (canvas) GSKY_NN_LAUNCH(false, 4, 2, kCanvas);
     else if (lut_n > 0) GSKY_NN_LAUNCH(false, 4, 2, kClampLut);

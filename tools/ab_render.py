@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--variant", default="", help="run only this variant (for rocprofv3 passes)")
     ap.add_argument("--probes", action="store_true", help="timing-only probes: no gathers / no stores")
     ap.add_argument("--oracle", action="store_true", help="also count RGBA pixels differing from the oracle")
+    ap.add_argument("--stride", action="store_true", help="lane-pixel layout variants (GSKYHIP_NN_STRIDE / NN_LUT)")
     args = ap.parse_args()
     cfg = synth.config_c2() if args.config == "c2" else synth.config_c5()
     b = gpu_batch(cfg)
@@ -72,9 +73,19 @@ def main():
     if args.probes:   # timing-only probes of the default NN kernel (images are wrong by design)
         variants = [("nn_4x2", True, "0", "0", "1", "3")] + [
             ("probe_%s" % p, True, "0", "0", "1", "3", "0", p) for p in ("1", "2", "3")]
+    if args.stride:   # trailing dict: extra environment of the variant
+        variants = [("nn_4x2", True, "0", "0", "1", "3"),
+                    ("nn_4x2_s", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1"}),
+                    ("nn_8x1_s", True, "0", "0", "1", "1", {"GSKYHIP_NN_STRIDE": "1"}),
+                    ("nn_8x2_s", True, "0", "0", "1", "2", {"GSKYHIP_NN_STRIDE": "1"}),
+                    ("nn_4x2_s_lut", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1", "GSKYHIP_NN_LUT": "1"}),
+                    ("nn_4x2_again", True, "0", "0", "1", "3")]
     for name, typed, stage, flags, nnk, shape, *extra in variants:
         if args.variant and name != args.variant:
             continue
+        env = extra.pop() if extra and isinstance(extra[-1], dict) else {}
+        for k in ("GSKYHIP_NN_STRIDE", "GSKYHIP_NN_LUT"):
+            os.environ[k] = env.get(k, "0")
         xcd = extra[:1]
         os.environ["GSKYHIP_LDS_STAGE"] = stage
         os.environ["GSKYHIP_LDS_FLAGS"] = flags
