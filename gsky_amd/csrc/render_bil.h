@@ -51,14 +51,14 @@ __device__ __forceinline__ bool bil_combine(double sx, double sy, int iSrcX, int
   return true;
 }
 
-template <int LPX, int R>
+template <int LPX, int R, int S>
 __global__ __launch_bounds__(256) void render_bil_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                          const int32_t *__restrict__ order,
                                                          const RowRec *__restrict__ rows,
                                                          const Leaf *__restrict__ pool,
                                                          const TilePlan *__restrict__ tplans,
                                                          const gskyhip_tile *__restrict__ tiles, int n_items) {
-  constexpr int kCols = 64 * LPX;
+  constexpr int kCols = 64 * LPX;   // S: column step between a lane's pixels (1 or 64, render_nn.h)
   const int item = blockIdx.x;
   if (item >= n_items) return;
   const int bands_per_tile = (a.max_h + kBandRows - 1) / kBandRows;
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void render_bil_kernel(RenderArgs a, const Ent
 
 #pragma unroll 1
   for (int cx = xb; cx < xend; cx += kCols) {
-    const int x0 = cx + lane * LPX;
+    const int x0 = cx + (S == 1 ? lane * LPX : lane);
 #pragma unroll 1
     for (int j = 0; j < 4; j += R) {
       const int rb = r0 + j;
@@ -123,12 +123,12 @@ __global__ __launch_bounds__(256) void render_bil_kernel(RenderArgs a, const Ent
           const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
 #pragma unroll
           for (int q = 0; q < LPX; q++) {
-            const int ic = ic0 + q;
+            const int ic = ic0 + q * S;
             const bool in = row_in && (unsigned)ic < (unsigned)lim;
             double sx, sy;
             bool ok = in;
             if (kind == ROW_LINEAR) {
-              const double dist = (double)ic0 + (double)q;
+              const double dist = (double)ic0 + (double)(q * S);
               sy = rr->v[1] + rr->v[3] * dist;
               sx = rr->v[0] + rr->v[2] * dist;
             } else {   // POOL: linear leaves, per-pixel exact points, failed pixels
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void render_bil_kernel(RenderArgs a, const Ent
                                          got))
               v = got;
             const int ir = rb + i - eyoff;
-            const bool in = ir >= 0 && ir < eh && rb + i < H && (unsigned)(ic0 + q) < (unsigned)lim;
+            const bool in = ir >= 0 && ir < eh && rb + i < H && (unsigned)(ic0 + q * S) < (unsigned)lim;
             const bool take = in & (v != nd) & (!fill_mode | (c[i][q] == nd));
             c[i][q] = take ? v : c[i][q];
           }
@@ -172,7 +172,11 @@ __global__ __launch_bounds__(256) void render_bil_kernel(RenderArgs a, const Ent
         const int64_t eo = a.cov_offsets ? a.cov_offsets[t] + (int64_t)r * a.cov_stride + x0
                                          : (int64_t)r * a.max_w + x0;
         float *cdst = (float *)(a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride) + eo;
-        if (x0 + LPX <= W && (((uintptr_t)cdst) & 15) == 0 && LPX % 4 == 0) {
+        if constexpr (S > 1) {   // 64 lanes x 4 B contiguous per store
+#pragma unroll
+          for (int q = 0; q < LPX; q++)
+            if (x0 + q * S < W) __builtin_nontemporal_store(__float_as_uint(c[i][q]), (GPTR(uint32_t))(cdst + q * S));
+        } else if (x0 + LPX <= W && (((uintptr_t)cdst) & 15) == 0 && LPX % 4 == 0) {
 #pragma unroll
           for (int h = 0; h < LPX / 4; h++) {
             u32x4 v4 = {__float_as_uint(c[i][4 * h]), __float_as_uint(c[i][4 * h + 1]),
@@ -192,18 +196,22 @@ __global__ __launch_bounds__(256) void render_bil_kernel(RenderArgs a, const Ent
 // Bilinear float canvases (no mask layer) go to render_bil_kernel unless
 // GSKYHIP_BIL_KERNEL=0 (A/B against the first band kernel).
 // Lane shape (LPX pixels x R rows) from RenderArgs.bil_kernel: 1 -> 4 x 1
-// (default: C3 1.35 ms/step vs 1.44-1.49 for the others and 2.30 for the
-// first band kernel, profiles/r02r_bench_c3_bil*.json), 2 -> 4 x 2,
-// 3 -> 2 x 2, 4 -> 8 x 1 (A/B knob GSKYHIP_BIL_KERNEL; 0 = render_lds_kernel).
+// (C3 1.35 ms/step vs 1.44-1.49 for the others and 2.30 for the first band
+// kernel, profiles/r02r_bench_c3_bil*.json), 2 -> 4 x 2, 3 -> 2 x 2,
+// 4 -> 8 x 1, 5 / 6 -> 4 x 1 / 4 x 2 with lane pixels 64 columns apart
+// (5 is the default: 1.31-1.34 ms, profiles/r02z6_bench_c3_bil.jsonl)
+// (A/B knob GSKYHIP_BIL_KERNEL; 0 = render_lds_kernel).
 void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
-#define GSKY_BIL_LAUNCH(L, RR)                                                                                 \
-  hipLaunchKernelGGL((render_bil_kernel<L, RR>), dim3((unsigned)n_items), dim3(256), 0, s, a, a.entries, a.order, \
+#define GSKY_BIL_LAUNCH(L, RR, SS)                                                                             \
+  hipLaunchKernelGGL((render_bil_kernel<L, RR, SS>), dim3((unsigned)n_items), dim3(256), 0, s, a, a.entries, a.order, \
                      a.rows, a.pool, a.tplans, a.tiles, n_items)
   switch (a.bil_kernel) {
-    case 2: GSKY_BIL_LAUNCH(4, 2); break;
-    case 3: GSKY_BIL_LAUNCH(2, 2); break;
-    case 4: GSKY_BIL_LAUNCH(8, 1); break;
-    default: GSKY_BIL_LAUNCH(4, 1); break;
+    case 2: GSKY_BIL_LAUNCH(4, 2, 1); break;
+    case 3: GSKY_BIL_LAUNCH(2, 2, 1); break;
+    case 4: GSKY_BIL_LAUNCH(8, 1, 1); break;
+    case 6: GSKY_BIL_LAUNCH(4, 2, 64); break;
+    case 1: GSKY_BIL_LAUNCH(4, 1, 1); break;
+    default: GSKY_BIL_LAUNCH(4, 1, 64); break;   // 5
   }
 #undef GSKY_BIL_LAUNCH
 }

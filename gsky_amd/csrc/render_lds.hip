@@ -31,7 +31,7 @@ void launch_lds_kernels(const RenderArgs &a0, int vt, bool mask, int n_items, hi
   const char *ne = getenv("GSKYHIP_NN_EXPRESS");
   a.nn_express = ne ? atoi(ne) : 1;
   const char *bk = getenv("GSKYHIP_BIL_KERNEL");
-  a.bil_kernel = bk ? atoi(bk) : 1;
+  a.bil_kernel = bk ? atoi(bk) : 5;   // 4 x 1, lane pixels 64 columns apart (r02z6: 1.31-1.34 vs 1.35 ms for 1)
   const char *ng = getenv("GSKYHIP_NN_GEN");
   a.nn_gen = ng ? atoi(ng) : 2;   // render_nn_kernel unless GSKYHIP_NN_GEN=3 (render_nn2_kernel, A/B: measured 2-4 % slower)
   const char *nl = getenv("GSKYHIP_NN_LUT");

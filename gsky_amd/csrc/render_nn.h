@@ -850,7 +850,7 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
 
 // Band kernel of one call: the NN kernel above (RenderArgs.nn_kernel, the
 // default) or render_lds_kernel (bilinear, LDS staging, A/B variants).
-template <int LPX, int R>
+template <int LPX, int R, int S>
 __global__ void render_bil_kernel(RenderArgs a, const EntryD *__restrict__ ents, const int32_t *__restrict__ order,
                                   const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
                                   const TilePlan *__restrict__ tplans, const gskyhip_tile *__restrict__ tiles,
