@@ -30,6 +30,7 @@ constexpr int kExpress = 16;   // render_nn2_kernel: single-entry express path (
 constexpr int kWide = 32;      // render_nn2_kernel: 16-B source-row loads for 16-bit values (GSKYHIP_NN_WIDE)
 constexpr int kClampLut = 64;  // render_nn_kernel: Scale through the clamped-value LUT (GSKYHIP_NN_LUT)
 constexpr int kStrided = 128;  // render_nn_kernel: lane pixels 64 columns apart (GSKYHIP_NN_STRIDE)
+constexpr int kPlainStore = 256;   // render_nn_kernel, strided: cached instead of non-temporal RGBA stores (A/B)
 constexpr int kClampLutCap = 16384;   // LUT bytes in LDS: clip values 0 .. 16383
 
 // utils.Scale of an integer canvas (scale_t) is, past the nodata test and
@@ -342,7 +343,10 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
           if constexpr (S > 1) {   // 64 lanes x 4 B contiguous per store
 #pragma unroll
             for (int q = 0; q < LPX; q++)
-              if (x0 + q * S < W) __builtin_nontemporal_store(px[q], (GPTR(uint32_t))(dst + 4 * q * S));
+              if (x0 + q * S < W) {
+                if constexpr ((FLAGS & kPlainStore) != 0) *(GPTR(uint32_t))(dst + 4 * q * S) = px[q];
+                else __builtin_nontemporal_store(px[q], (GPTR(uint32_t))(dst + 4 * q * S));
+              }
           } else if (x0 + LPX <= W && ((((uintptr_t)dst) & 15) == 0)) {
 #pragma unroll
             for (int h = 0; h < LPX / 4; h++) {
@@ -823,7 +827,14 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
     const int rows_blk = 4 * (a.nn_rpw >= 16 ? 16 : 8);
     const int items = a.n_tiles * ((a.max_h + rows_blk - 1) / rows_blk) * ((a.max_w + kBandCols - 1) / kBandCols);
     const dim3 g2((unsigned)items);
-    if (a.nn_rpw >= 16) {
+    if (a.nn_stride && !canvas) {
+      if (a.nn_rpw >= 16)
+        hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, kStrided, 16>), g2, dim3(256), 0, s, a, a.entries,
+                           a.order, a.rows, a.pool, a.tplans, a.tiles, items, 0);
+      else
+        hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, kStrided, 8>), g2, dim3(256), 0, s, a, a.entries,
+                           a.order, a.rows, a.pool, a.tplans, a.tiles, items, 0);
+    } else if (a.nn_rpw >= 16) {
       if (canvas) hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, kCanvas, 16>), g2, dim3(256), 0, s, a,
                                      a.entries, a.order, a.rows, a.pool, a.tplans, a.tiles, items, 0);
       else hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, 0, 16>), g2, dim3(256), 0, s, a, a.entries, a.order,
@@ -834,6 +845,10 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
       else hipLaunchKernelGGL((render_nn_kernel<T, false, 4, 2, 0, 8>), g2, dim3(256), 0, s, a, a.entries, a.order,
                               a.rows, a.pool, a.tplans, a.tiles, items, 0);
     }
+  } else if (a.nn_shape == 3 && a.nn_stride == 2 && !canvas) {   // A/B: cached stores
+    GSKY_NN_LAUNCH(false, 4, 2, kStrided | kPlainStore);
+  } else if (a.nn_shape == 0 && a.nn_stride) {
+    if (canvas) GSKY_NN_LAUNCH(false, 4, 4, kCanvas | kStrided); else GSKY_NN_LAUNCH(false, 4, 4, kStrided);
   } else if (a.nn_shape == 3 && a.nn_stride) {
     if (canvas) GSKY_NN_LAUNCH(false, 4, 2, kCanvas | kStrided);
     else if (lut_n > 0) GSKY_NN_LAUNCH(false, 4, 2, kClampLut | kStrided);

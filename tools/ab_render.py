@@ -79,6 +79,11 @@ def main():
                     ("nn_8x1_s", True, "0", "0", "1", "1", {"GSKYHIP_NN_STRIDE": "1"}),
                     ("nn_8x2_s", True, "0", "0", "1", "2", {"GSKYHIP_NN_STRIDE": "1"}),
                     ("nn_4x2_s_lut", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1", "GSKYHIP_NN_LUT": "1"}),
+                    ("nn_4x4_s", True, "0", "0", "1", "0", {"GSKYHIP_NN_STRIDE": "1"}),
+                    ("nn_4x2_s_rpw8", True, "0", "0", "1", "3", "0", "0", "2", "0", "1", "0", "8",
+                     {"GSKYHIP_NN_STRIDE": "1"}),
+                    ("nn_4x2_s_plain", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "2"}),
+                    ("nn_4x2_s_again", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1"}),
                     ("nn_4x2_again", True, "0", "0", "1", "3")]
     for name, typed, stage, flags, nnk, shape, *extra in variants:
         if args.variant and name != args.variant:
