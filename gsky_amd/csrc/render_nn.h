@@ -331,6 +331,9 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
               const uint32_t col = s_ramp[s_lut[value]];
               px[q] = (created && c[i][q] != sk.noData.i) ? col : 0u;
             }
+          } else if (a.nn_probe == 4) {   // timing probe 4: no Scale / palette (raw values out)
+#pragma unroll
+            for (int q = 0; q < LPX; q++) px[q] = (uint32_t)c[i][q];
           } else {
 #pragma unroll
             for (int q = 0; q < LPX; q++) {

@@ -72,7 +72,8 @@ def main():
                 ("generic", False, "1", "0", "0", "0")]
     if args.probes:   # timing-only probes of the default NN kernel (images are wrong by design)
         variants = [("nn_4x2", True, "0", "0", "1", "3")] + [
-            ("probe_%s" % p, True, "0", "0", "1", "3", "0", p) for p in ("1", "2", "3")]
+            ("probe_%s" % p, True, "0", "0", "1", "3", "0", p) for p in ("1", "2", "3", "4")]
+        variants = [v + ({"GSKYHIP_NN_STRIDE": "1"},) for v in variants]
     if args.stride:   # trailing dict: extra environment of the variant
         variants = [("nn_4x2", True, "0", "0", "1", "3"),
                     ("nn_4x2_s", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1"}),
