@@ -31,6 +31,8 @@ constexpr int kWide = 32;      // render_nn2_kernel: 16-B source-row loads for 1
 constexpr int kClampLut = 64;  // render_nn_kernel: Scale through the clamped-value LUT (GSKYHIP_NN_LUT)
 constexpr int kStrided = 128;  // render_nn_kernel: lane pixels 64 columns apart (GSKYHIP_NN_STRIDE)
 constexpr int kPlainStore = 256;   // render_nn_kernel, strided: cached instead of non-temporal RGBA stores (A/B)
+constexpr int kLdsOut = 1024;      // render_nn_kernel, strided RGBA: rows collected in LDS, stored when the wave ends
+constexpr int kWaves8 = 2048;      // render_nn_kernel: compiled for 8 waves per SIMD (<= 64 VGPRs) (A/B)
 constexpr int kClampLutCap = 16384;   // LUT bytes in LDS: clip values 0 .. 16383
 
 // utils.Scale of an integer canvas (scale_t) is, past the nodata test and
@@ -146,7 +148,7 @@ __device__ __forceinline__ void nn_row_index(const RowRec *__restrict__ rr, cons
 }
 
 template <typename T, bool MASK, int LPX, int R, int FLAGS, int RPW = 4>
-__global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
+__global__ __launch_bounds__(256, (FLAGS & kWaves8) != 0 ? 8 : 1) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                         const int32_t *__restrict__ order,
                                                         const RowRec *__restrict__ rows,
                                                         const Leaf *__restrict__ pool,
@@ -162,6 +164,13 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
   constexpr int S = (FLAGS & kStrided) != 0 ? 64 : 1;
   __shared__ uint32_t s_ramp[256];
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[kLutOut ? kClampLutCap : 16];
+  // kOutLds: the wave's RGBA rows wait in LDS and leave in one burst of
+  // 16-B stores at the end.  vmcnt counts loads and stores in issue order,
+  // so a store issued between two entry iterations makes the next gathers'
+  // wait drain it too; with the stores last, the gather chain never waits
+  // for the write stream
+  constexpr bool kOutLds = (FLAGS & kLdsOut) != 0 && S > 1 && (FLAGS & kCanvas) == 0;
+  __shared__ __attribute__((aligned(16))) uint32_t s_out[kOutLds ? 4 * RPW * kBandCols : 4];
 
   // linear item order, or XCD-aware (per_xcd > 0: blocks b, b+8, ... share an
   // XCD and its L2) -- linear measured faster: neighbouring tiles on every XCD
@@ -343,7 +352,11 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
             }
           }
           uint8_t *dst = rgba_tile + ((int64_t)r * a.max_w + x0) * 4;
-          if constexpr (S > 1) {   // 64 lanes x 4 B contiguous per store
+          if constexpr (kOutLds) {
+            uint32_t *so = s_out + (wave * RPW + j + i) * kBandCols + (cx - xb) + lane;
+#pragma unroll
+            for (int q = 0; q < LPX; q++) so[q * S] = px[q];
+          } else if constexpr (S > 1) {   // 64 lanes x 4 B contiguous per store
 #pragma unroll
             for (int q = 0; q < LPX; q++)
               if (x0 + q * S < W) {
@@ -362,6 +375,30 @@ __global__ __launch_bounds__(256) void render_nn_kernel(RenderArgs a, const Entr
               if (x0 + q < W) ((uint32_t *)dst)[q] = px[q];
           }
         }
+      }
+    }
+  }
+  if constexpr (kOutLds) {
+    if (a.nn_probe == 3) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int ncols = xend - xb;
+    const int c0 = lane * 8;   // a lane's 8 columns of each row: two 16-B stores
+#pragma unroll 1
+    for (int jj = 0; jj < RPW; jj++) {
+      const int r = r0 + jj;
+      if (r >= H) break;
+      const uint32_t *src = s_out + (wave * RPW + jj) * kBandCols + c0;
+      uint8_t *d = rgba_tile + ((int64_t)r * a.max_w + xb + c0) * 4;
+      if (c0 + 8 <= ncols && (((uintptr_t)d) & 15) == 0) {
+        const u32x4 v0 = *(const u32x4 *)src, v1 = *(const u32x4 *)(src + 4);
+        __builtin_nontemporal_store(v0, (GPTR(u32x4))d);
+        __builtin_nontemporal_store(v1, (GPTR(u32x4))(d + 16));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+          if (c0 + q < ncols) __builtin_nontemporal_store(src[q], (GPTR(uint32_t))(d + 4 * q));
       }
     }
   }
@@ -757,10 +794,13 @@ __global__ __launch_bounds__(256, WPE) void render_nn2_kernel(RenderArgs a, cons
 }
 
 // NN band kernel launch for value type T: lanes shape (LPX pixels x R rows)
-// from RenderArgs.nn_shape (0: 4 x 4, 1: 8 x 1, 2: 8 x 2, 3: 4 x 2, the
-// default: fastest on C2 and C5, profiles/r02h_ab_*.jsonl), 32.32
-// fixed point when lds_flags has kFixed, XCD-aware order when nn_xcd
-// (A/B knobs GSKYHIP_NN_SHAPE, GSKYHIP_LDS_FLAGS, GSKYHIP_NN_XCD).
+// from RenderArgs.nn_shape (0: 4 x 4, 1: 8 x 1, 2: 8 x 2, 3: 4 x 2 (the
+// round-2 default until r02z10), 4: 4 x 1 compiled for 8 waves per SIMD, the
+// default), lane pixels 64 columns apart when nn_stride (default; the
+// masked kernel and typed canvases use 4 x 2), 32.32 fixed point when
+// lds_flags has kFixed, XCD-aware order when nn_xcd (A/B knobs
+// GSKYHIP_NN_SHAPE, GSKYHIP_NN_STRIDE, GSKYHIP_LDS_FLAGS, GSKYHIP_NN_XCD;
+// profiles/r02h_ab_*.jsonl, r02z*_ab_*.jsonl).
 template <typename T>
 void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
   const int per_xcd = a.nn_xcd ? (n_items + 7) / 8 : 0;
@@ -850,6 +890,13 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
     }
   } else if (a.nn_shape == 3 && a.nn_stride == 2 && !canvas) {   // A/B: cached stores
     GSKY_NN_LAUNCH(false, 4, 2, kStrided | kPlainStore);
+  } else if (a.nn_shape == 3 && a.nn_stride == 4 && !canvas) {   // A/B: rows through LDS, stores at the end
+    GSKY_NN_LAUNCH(false, 4, 2, kStrided | kLdsOut);
+  } else if (a.nn_shape == 3 && a.nn_stride == 5 && !canvas) {   // A/B: 8 waves per SIMD
+    GSKY_NN_LAUNCH(false, 4, 2, kStrided | kWaves8);
+  } else if (a.nn_shape == 4 && a.nn_stride) {   // default: 4 x 1 strided, 8 waves per SIMD (57 VGPRs)
+    if (canvas) GSKY_NN_LAUNCH(false, 4, 2, kCanvas | kStrided);
+    else GSKY_NN_LAUNCH(false, 4, 1, kStrided | kWaves8);
   } else if (a.nn_shape == 0 && a.nn_stride) {
     if (canvas) GSKY_NN_LAUNCH(false, 4, 4, kCanvas | kStrided); else GSKY_NN_LAUNCH(false, 4, 4, kStrided);
   } else if (a.nn_shape == 3 && a.nn_stride) {

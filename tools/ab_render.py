@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--probes", action="store_true", help="timing-only probes: no gathers / no stores")
     ap.add_argument("--oracle", action="store_true", help="also count RGBA pixels differing from the oracle")
     ap.add_argument("--stride", action="store_true", help="lane-pixel layout variants (GSKYHIP_NN_STRIDE / NN_LUT)")
+    ap.add_argument("--all-layouts", action="store_true", help="with --stride: every layout variant")
     args = ap.parse_args()
     cfg = synth.config_c2() if args.config == "c2" else synth.config_c5()
     b = gpu_batch(cfg)
@@ -77,15 +78,20 @@ def main():
     if args.stride:   # trailing dict: extra environment of the variant
         variants = [("nn_4x2", True, "0", "0", "1", "3"),
                     ("nn_4x2_s", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1"}),
-                    ("nn_8x1_s", True, "0", "0", "1", "1", {"GSKYHIP_NN_STRIDE": "1"}),
-                    ("nn_8x2_s", True, "0", "0", "1", "2", {"GSKYHIP_NN_STRIDE": "1"}),
-                    ("nn_4x2_s_lut", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1", "GSKYHIP_NN_LUT": "1"}),
-                    ("nn_4x4_s", True, "0", "0", "1", "0", {"GSKYHIP_NN_STRIDE": "1"}),
-                    ("nn_4x2_s_rpw8", True, "0", "0", "1", "3", "0", "0", "2", "0", "1", "0", "8",
-                     {"GSKYHIP_NN_STRIDE": "1"}),
-                    ("nn_4x2_s_plain", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "2"}),
+                    ("nn_4x2_s_w8", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "5"}),
+                    ("nn_4x1_s_w8", True, "0", "0", "1", "4", {"GSKYHIP_NN_STRIDE": "1"}),
                     ("nn_4x2_s_again", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1"}),
-                    ("nn_4x2_again", True, "0", "0", "1", "3")]
+                    ("nn_4x2_s_w8_again", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "5"})]
+        if args.all_layouts:   # the round's other layout variants (profiles/r02z7_ab_*.jsonl)
+            variants += [("nn_8x1_s", True, "0", "0", "1", "1", {"GSKYHIP_NN_STRIDE": "1"}),
+                         ("nn_8x2_s", True, "0", "0", "1", "2", {"GSKYHIP_NN_STRIDE": "1"}),
+                         ("nn_4x2_s_lut", True, "0", "0", "1", "3",
+                          {"GSKYHIP_NN_STRIDE": "1", "GSKYHIP_NN_LUT": "1"}),
+                         ("nn_4x4_s", True, "0", "0", "1", "0", {"GSKYHIP_NN_STRIDE": "1"}),
+                         ("nn_4x2_s_plain", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "2"}),
+                         ("nn_4x2_s_ldsout", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "4"}),
+                         ("nn_4x2_s_rpw8", True, "0", "0", "1", "3", "0", "0", "2", "0", "1", "0", "8",
+                          {"GSKYHIP_NN_STRIDE": "1"})]
     for name, typed, stage, flags, nnk, shape, *extra in variants:
         if args.variant and name != args.variant:
             continue
