@@ -51,8 +51,8 @@ __device__ __forceinline__ bool bil_combine(double sx, double sy, int iSrcX, int
   return true;
 }
 
-template <int LPX, int R, int S>
-__global__ __launch_bounds__(256) void render_bil_kernel(RenderArgs a, const EntryD *__restrict__ ents,
+template <int LPX, int R, int S, int W8>
+__global__ __launch_bounds__(256, W8 ? 8 : 1) void render_bil_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                          const int32_t *__restrict__ order,
                                                          const RowRec *__restrict__ rows,
                                                          const Leaf *__restrict__ pool,
@@ -199,11 +199,12 @@ __global__ __launch_bounds__(256) void render_bil_kernel(RenderArgs a, const Ent
 // (C3 1.35 ms/step vs 1.44-1.49 for the others and 2.30 for the first band
 // kernel, profiles/r02r_bench_c3_bil*.json), 2 -> 4 x 2, 3 -> 2 x 2,
 // 4 -> 8 x 1, 5 / 6 -> 4 x 1 / 4 x 2 with lane pixels 64 columns apart
-// (5 is the default: 1.31-1.34 ms, profiles/r02z6_bench_c3_bil.jsonl)
+// (5 is the default: 1.31-1.34 ms, profiles/r02z6_bench_c3_bil.jsonl; forced
+// to 8 waves per SIMD it spills 63 VGPRs, so W8 stays 0)
 // (A/B knob GSKYHIP_BIL_KERNEL; 0 = render_lds_kernel).
 void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
-#define GSKY_BIL_LAUNCH(L, RR, SS)                                                                             \
-  hipLaunchKernelGGL((render_bil_kernel<L, RR, SS>), dim3((unsigned)n_items), dim3(256), 0, s, a, a.entries, a.order, \
+#define GSKY_BIL_LAUNCH(L, RR, SS, ...)                                                                        \
+  hipLaunchKernelGGL((render_bil_kernel<L, RR, SS, (0 __VA_ARGS__)>), dim3((unsigned)n_items), dim3(256), 0, s, a, a.entries, a.order, \
                      a.rows, a.pool, a.tplans, a.tiles, n_items)
   switch (a.bil_kernel) {
     case 2: GSKY_BIL_LAUNCH(4, 2, 1); break;

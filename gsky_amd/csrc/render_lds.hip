@@ -19,7 +19,9 @@ void launch_lds_kernels(const RenderArgs &a0, int vt, bool mask, int n_items, hi
   const char *nk = getenv("GSKYHIP_NN_KERNEL");
   a.nn_kernel = nk ? atoi(nk) : 1;
   const char *ns = getenv("GSKYHIP_NN_SHAPE");
-  a.nn_shape = ns ? atoi(ns) : 4;   // 4 x 1 strided at 8 waves / SIMD (r02z10: 1.83 vs 1.85 ms for 4 x 2)
+  // 5: 4 x 1 strided at 8 waves / SIMD, masked kernel too (r02z10/z11: C2 1.83 vs 1.85 ms, C5 0.58 vs 0.66 ms
+  // for 4 x 2); 4: the same with the masked kernel at 4 x 2
+  a.nn_shape = ns ? atoi(ns) : 5;
   const char *np = getenv("GSKYHIP_NN_PROBE");   // timing-only probes (wrong images): never set in production
   a.nn_probe = np ? atoi(np) : 0;
   const char *nw = getenv("GSKYHIP_NN_WPE");

@@ -795,9 +795,10 @@ __global__ __launch_bounds__(256, WPE) void render_nn2_kernel(RenderArgs a, cons
 
 // NN band kernel launch for value type T: lanes shape (LPX pixels x R rows)
 // from RenderArgs.nn_shape (0: 4 x 4, 1: 8 x 1, 2: 8 x 2, 3: 4 x 2 (the
-// round-2 default until r02z10), 4: 4 x 1 compiled for 8 waves per SIMD, the
-// default), lane pixels 64 columns apart when nn_stride (default; the
-// masked kernel and typed canvases use 4 x 2), 32.32 fixed point when
+// round-2 default until r02z10), 4: 4 x 1 compiled for 8 waves per SIMD,
+// 5: the same for the masked kernel too (the default)), lane pixels 64
+// columns apart when nn_stride (default; typed canvases use 4 x 2), 32.32
+// fixed point when
 // lds_flags has kFixed, XCD-aware order when nn_xcd (A/B knobs
 // GSKYHIP_NN_SHAPE, GSKYHIP_NN_STRIDE, GSKYHIP_LDS_FLAGS, GSKYHIP_NN_XCD;
 // profiles/r02h_ab_*.jsonl, r02z*_ab_*.jsonl).
@@ -848,7 +849,9 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
                      (mask || (a.nn_shape == 3 && a.nn_rpw <= 4))) ? clamp_lut_size<T>(a) : 0;
   if (lut_n > 0)
     hipLaunchKernelGGL(clamp_lut_kernel<T>, dim3((lut_n + 255) / 256), dim3(256), 0, s, a, (uint8_t *)a.lut, lut_n);
-  if (mask && a.nn_stride) {
+  if (mask && a.nn_stride && a.nn_shape == 5 && !canvas) {   // default: masked 4 x 1 at 8 waves per SIMD
+    GSKY_NN_LAUNCH(true, 4, 1, kStrided | kWaves8);
+  } else if (mask && a.nn_stride) {
     if (canvas) GSKY_NN_LAUNCH(true, 4, 2, kCanvas | kStrided);
     else if (lut_n > 0) GSKY_NN_LAUNCH(true, 4, 2, kClampLut | kStrided);
     else GSKY_NN_LAUNCH(true, 4, 2, kStrided);
@@ -894,7 +897,7 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
     GSKY_NN_LAUNCH(false, 4, 2, kStrided | kLdsOut);
   } else if (a.nn_shape == 3 && a.nn_stride == 5 && !canvas) {   // A/B: 8 waves per SIMD
     GSKY_NN_LAUNCH(false, 4, 2, kStrided | kWaves8);
-  } else if (a.nn_shape == 4 && a.nn_stride) {   // default: 4 x 1 strided, 8 waves per SIMD (57 VGPRs)
+  } else if ((a.nn_shape == 4 || a.nn_shape == 5) && a.nn_stride) {   // default: 4 x 1 strided, 8 waves / SIMD
     if (canvas) GSKY_NN_LAUNCH(false, 4, 2, kCanvas | kStrided);
     else GSKY_NN_LAUNCH(false, 4, 1, kStrided | kWaves8);
   } else if (a.nn_shape == 0 && a.nn_stride) {
@@ -915,7 +918,7 @@ void launch_nn_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
 
 // Band kernel of one call: the NN kernel above (RenderArgs.nn_kernel, the
 // default) or render_lds_kernel (bilinear, LDS staging, A/B variants).
-template <int LPX, int R, int S>
+template <int LPX, int R, int S, int W8>
 __global__ void render_bil_kernel(RenderArgs a, const EntryD *__restrict__ ents, const int32_t *__restrict__ order,
                                   const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
                                   const TilePlan *__restrict__ tplans, const gskyhip_tile *__restrict__ tiles,

@@ -78,10 +78,10 @@ def main():
     if args.stride:   # trailing dict: extra environment of the variant
         variants = [("nn_4x2", True, "0", "0", "1", "3"),
                     ("nn_4x2_s", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1"}),
-                    ("nn_4x2_s_w8", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "5"}),
                     ("nn_4x1_s_w8", True, "0", "0", "1", "4", {"GSKYHIP_NN_STRIDE": "1"}),
-                    ("nn_4x2_s_again", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "1"}),
-                    ("nn_4x2_s_w8_again", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "5"})]
+                    ("nn_4x1_s_w8_mask4x1", True, "0", "0", "1", "5", {"GSKYHIP_NN_STRIDE": "1"}),
+                    ("nn_4x1_s_w8_again", True, "0", "0", "1", "4", {"GSKYHIP_NN_STRIDE": "1"}),
+                    ("nn_4x1_s_w8_mask4x1_again", True, "0", "0", "1", "5", {"GSKYHIP_NN_STRIDE": "1"})]
         if args.all_layouts:   # the round's other layout variants (profiles/r02z7_ab_*.jsonl)
             variants += [("nn_8x1_s", True, "0", "0", "1", "1", {"GSKYHIP_NN_STRIDE": "1"}),
                          ("nn_8x2_s", True, "0", "0", "1", "2", {"GSKYHIP_NN_STRIDE": "1"}),
@@ -90,6 +90,7 @@ def main():
                          ("nn_4x4_s", True, "0", "0", "1", "0", {"GSKYHIP_NN_STRIDE": "1"}),
                          ("nn_4x2_s_plain", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "2"}),
                          ("nn_4x2_s_ldsout", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "4"}),
+                         ("nn_4x2_s_w8", True, "0", "0", "1", "3", {"GSKYHIP_NN_STRIDE": "5"}),
                          ("nn_4x2_s_rpw8", True, "0", "0", "1", "3", "0", "0", "2", "0", "1", "0", "8",
                           {"GSKYHIP_NN_STRIDE": "1"})]
     for name, typed, stage, flags, nnk, shape, *extra in variants:
