@@ -1,0 +1,5 @@
+#!/bin/bash
+# r02z14: the whole GPU suite on the final build (as the driver runs it).
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -rf > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log; exit $rc
