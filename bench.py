@@ -251,9 +251,22 @@ def run_c1(ctx: Ctx, args):
         b.render(sp)
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t0) * 1e3)
+    # the same request served from a captured HIP graph (RenderGraph): tile
+    # descriptor upload + one replay + synchronize per request
+    rg = b.graph(sp)
+    gts = []
+    for _ in range(args.c1_reps):
+        t0 = time.perf_counter()
+        b.set_tiles(cfg.tiles)
+        rg.replay()
+        torch.cuda.synchronize()
+        gts.append((time.perf_counter() - t0) * 1e3)
     out = {"workload": "C1: one 256x256 EPSG:3857 tile from a 3600x1800 EPSG:4326 f32 granule, nearest, scale",
            "p50_tile_ms": round(float(np.percentile(ts, 50)), 4), "p99_tile_ms": round(float(np.percentile(ts, 99)), 4),
-           "reps": args.c1_reps, "timing": "host wall per call incl. launch + synchronize"}
+           "reps": args.c1_reps, "timing": "host wall per call incl. launch + synchronize",
+           "p50_tile_ms_graph": round(float(np.percentile(gts, 50)), 4),
+           "p99_tile_ms_graph": round(float(np.percentile(gts, 99)), 4),
+           "graph_timing": "host wall per request: tile descriptor upload + HIP graph replay + synchronize"}
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
         from oracle import oracle as O
         cts = []

@@ -175,6 +175,7 @@ class TileBatch:
         self.n_tiles = len(tiles)
         self.n_pairs = len(flat)
         self.tile_sizes = [(w, h) for (_, w, h) in tiles]
+        self._tarr = tarr
         self._tiles = _to_device_bytes(tarr, self.device)
         self._pairs = torch.tensor(flat if flat else [0], dtype=torch.int32, device=self.device)
         ws = lib().gskyhip_render_workspace_size(self.n_tiles, self.n_pairs, self.max_h)
@@ -224,6 +225,36 @@ class TileBatch:
         if not rgba:
             return cv
         return (out, cv) if canvas else out
+
+    # ------------------------------------------------------------------ graphs
+    def set_tiles(self, tiles) -> None:
+        """New requests of the same shape: every tile's (bbox, width, height)
+        is replaced, its granule list (CSR) kept.  The descriptors go to HBM on
+        the current stream (pinned host buffer, asynchronous), ahead of the
+        next render or graph replay."""
+        if len(tiles) != self.n_tiles:
+            raise ValueError("set_tiles: %d tiles for a batch of %d" % (len(tiles), self.n_tiles))
+        for i, (bbox, w, h) in enumerate(tiles):
+            if w > self.max_w or h > self.max_h:
+                raise ValueError("set_tiles: tile %d larger than the batch slot" % i)
+            gt = bbox_to_geot(w, h, bbox)
+            for k in range(6):
+                self._tarr[i].dst_geot[k] = gt[k]
+            self._tarr[i].width, self._tarr[i].height = w, h
+        self.tile_sizes = [(w, h) for (_, w, h) in tiles]
+        host = getattr(self, "_tiles_pinned", None)
+        if host is None:
+            host = torch.empty(self._tiles.numel(), dtype=torch.uint8).pin_memory()
+            self._tiles_pinned = host
+        else:
+            torch.cuda.current_stream().synchronize()   # the previous upload has left the buffer
+        host.numpy()[:] = np.frombuffer(bytes(self._tarr), dtype=np.uint8)
+        self._tiles.copy_(host, non_blocking=True)
+
+    def graph(self, params: ScaleParams, palette: Optional[Palette] = None, resample: int = 0) -> "RenderGraph":
+        """The batch's render (planning + band kernels, RGBA out) captured as
+        one HIP graph (see RenderGraph)."""
+        return RenderGraph(self, params, palette, resample)
 
     def render_coverage(self, params: ScaleParams, out: torch.Tensor, offsets, resample: int = 0,
                         phase: int = 0) -> torch.Tensor:
@@ -299,6 +330,29 @@ class TileBatch:
             t = win[p, : w * h * nb].view(TORCH_OF[tname]).reshape(h, w)
             out.append((t, bb[p].tolist(), tname, float(nds[p])))
         return out
+
+
+class RenderGraph:
+    """One TileBatch.render() captured as a HIP graph: the ~10 planning and
+    band-kernel launches of a request replay with one host call, which is
+    what bounds the latency of a single small tile (BASELINE C1).  Every
+    kernel reads the tile, pair and granule descriptors from HBM when it
+    runs, so a new request of the same shape (tile count, pair lists, slot
+    size) is served by TileBatch.set_tiles() followed by replay(); the
+    result lands in the same RGBA tensor."""
+
+    def __init__(self, batch: TileBatch, params: ScaleParams, palette: Optional[Palette], resample: int):
+        self.batch = batch
+        batch.render(params, palette, resample)   # loads the kernels, allocates the output and the ramp
+        torch.cuda.synchronize()
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._graph):
+            self.out = batch.render(params, palette, resample)
+        torch.cuda.synchronize()
+
+    def replay(self) -> torch.Tensor:
+        self._graph.replay()
+        return self.out
 
 
 class PipelinedBatch:
