@@ -33,14 +33,66 @@ import argparse
 import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 import traceback
 
-import numpy as np
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the
+    environment): start N rank processes of this script -- before anything
+    here has imported torch or touched a GPU, and as children (never exec) --
+    each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT, wait
+    for them, relay rank 0's JSON line and fail if any rank fails (the others
+    are then terminated, so none waits forever at a barrier)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    import threading
+    out0 = []
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    failed = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.discard(r)
+            if rc != 0 and not failed:
+                failed = rc
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    reader.join()
+    out0 = b"".join(out0)
+    sys.stdout.write(out0.decode())
+    sys.stdout.flush()
+    return failed
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ:
+    _pre = argparse.ArgumentParser(add_help=False)
+    _pre.add_argument("--gpus", type=int, default=1)
+    _n = _pre.parse_known_args()[0].gpus
+    if _n > 1:
+        sys.exit(_launch_ranks(_n))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
 sys.path.insert(0, ROOT)
 
 import gsky_amd  # noqa: E402
@@ -53,19 +105,31 @@ CLIP = (-3.4028234663852886e38, 3.4028234663852886e38)   # ows.go:1373-1381
 
 # ---------------------------------------------------------------- plumbing
 class Ctx:
-    def __init__(self):
+    """Rank context: one process per GPU (RANK / LOCAL_RANK / WORLD_SIZE from
+    the launcher or from _launch_ranks), RCCL ("nccl") process group; the
+    CPU dry run (tests) uses gloo and no device."""
+
+    def __init__(self, dry_run: bool = False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dry = dry_run
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
-            torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            if dry_run:
+                dist.init_process_group("gloo")
+            else:
+                torch.cuda.set_device(self.local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
             self.dist = dist
-        else:
+        elif not dry_run:
             torch.cuda.set_device(0)
-        self.device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device("cpu") if dry_run else torch.device("cuda", torch.cuda.current_device())
+
+    def sync(self):
+        if not self.dry:
+            torch.cuda.synchronize()
 
     def barrier(self):
         if self.dist:
@@ -78,18 +142,27 @@ class Ctx:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def ranks_seen(self):
+        """Every rank's index, gathered (proves the N processes joined)."""
+        if not self.dist:
+            return [self.rank]
+        t = torch.tensor([self.rank], dtype=torch.int64, device=self.device)
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [int(x.item()) for x in out]
+
     def timed(self, step, steps: int, warmup: int) -> float:
         """W untimed steps, then K steps bracketed by barrier + synchronize;
         returns the max-over-ranks seconds of the K steps."""
         for _ in range(warmup):
             step()
-        torch.cuda.synchronize()
+        self.sync()
         self.barrier()
-        torch.cuda.synchronize()
+        self.sync()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
-        torch.cuda.synchronize()
+        self.sync()
         self.barrier()
         return self.max_over_ranks(time.perf_counter() - t0)
 
@@ -112,17 +185,46 @@ block_part = partition.tile_blocks     # contiguous tile blocks (gsky_amd/partit
 sub_config = partition.sub_config      # a rank uploads only the granules its tiles touch
 
 
-def build_batch(cfg, device, chunks: int = 0):
+def build_granules(cfg, device):
+    """The config's granules uploaded once (HBM-resident for every batch)."""
     gs = GranuleSet(device)
     for g in cfg.granules:
         gs.add(torch.from_numpy(np.ascontiguousarray(g.data)), g.geot, g.srs, g.nodata,
                [torch.from_numpy(np.ascontiguousarray(o)) for o in g.overviews], g.timestamp, g.polygon,
                g.namespace)
+    return gs
+
+
+def build_batch(cfg, device, chunks: int = 0, gs=None, ids=None):
+    """A TileBatch (or PipelinedBatch) of the config's tiles -- or of tiles
+    `ids` only -- over `gs` (uploaded here when not given)."""
+    gs = gs if gs is not None else build_granules(cfg, device)
     mask = Mask(cfg.mask["id"], cfg.mask.get("value", ""), cfg.mask.get("bit_tests", []),
                 cfg.mask.get("inclusive", False)) if cfg.mask else None
+    tiles = cfg.tiles if ids is None else [cfg.tiles[i] for i in ids]
+    pairs = cfg.pairs if ids is None else [cfg.pairs[i] for i in ids]
     if chunks > 1:
-        return PipelinedBatch(gs, cfg.dst_srs, cfg.tiles, cfg.pairs, cfg.namespaces, mask, n_chunks=chunks)
-    return TileBatch(gs, cfg.dst_srs, cfg.tiles, cfg.pairs, cfg.namespaces, mask)
+        return PipelinedBatch(gs, cfg.dst_srs, tiles, pairs, cfg.namespaces, mask, n_chunks=chunks)
+    return TileBatch(gs, cfg.dst_srs, tiles, pairs, cfg.namespaces, mask)
+
+
+def tile_latency(ctx, cfg, gs, sp, pal, ids, reps):
+    """Host wall time of one-tile requests (plan + render + synchronize; the
+    reference serves every GetMap tile as its own request, ows.go:257-524),
+    granules resident: list of ms."""
+    lat = []
+    for i in ids:
+        one = build_batch(cfg, ctx.device, gs=gs, ids=[i])
+        for _ in range(3):
+            one.render(sp, pal)
+        torch.cuda.synchronize()
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            one.render(sp, pal)
+            torch.cuda.synchronize()
+            lat.append((time.perf_counter() - t0) * 1e3)
+        del one
+    return lat
 
 
 def host_cores():
@@ -176,13 +278,14 @@ def oracle_render(O, cfg, threads):
 # ---------------------------------------------------------------- C2 (headline)
 def run_c2(ctx: Ctx, args):
     full = synth.config_c2()
-    ids = block_part(len(full.tiles), ctx.rank, ctx.world)
+    ids = block_part(len(full.tiles), ctx.rank, ctx.world, partition.tile_cost(full.pairs))
     cfg = sub_config(full, ids)
-    batch = build_batch(cfg, ctx.device)
+    gs = build_granules(cfg, ctx.device)
+    batch = build_batch(cfg, ctx.device, gs=gs)
     sp, pal = ScaleParams(*cfg.scale), Palette(cfg.palette, True)
     # the timed step: the batch in chunks on two streams, so each chunk's
     # planning kernels run under the previous chunk's render (PipelinedBatch)
-    step_batch = build_batch(cfg, ctx.device, chunks=args.c2_chunks) if args.c2_chunks > 1 else batch
+    step_batch = build_batch(cfg, ctx.device, chunks=args.c2_chunks, gs=gs) if args.c2_chunks > 1 else batch
     for bb in (batch, step_batch):
         bb.render(sp, pal)
         torch.cuda.synchronize()
@@ -197,12 +300,21 @@ def run_c2(ctx: Ctx, args):
     src = sum(g.data.nbytes for g in full.granules) * cfg.out_pixels / full.out_pixels
     abytes = int(src + cfg.out_pixels * 4)
     achieved = abytes / (render_ms / 1e3) / 1e9
+    # p50 GetMap tile latency: evenly spaced tiles of the rank's block, each
+    # as its own request
+    lat_ids = list(range(0, len(ids), max(1, len(ids) // args.c2_lat_tiles)))[: args.c2_lat_tiles]
+    lat = tile_latency(ctx, cfg, gs, sp, pal, lat_ids, args.c2_lat_reps) if lat_ids else [float("nan")]
     out = {
         "value": round(total_px / dt / 1e6, 1), "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "p50_tile_ms": round(float(np.percentile(lat, 50)), 4),
+        "p99_tile_ms": round(float(np.percentile(lat, 99)), 4),
+        "p50_timing": "C2 one-tile GetMap requests (%d tiles x %d reps, rank 0): host wall of plan + render + "
+                      "synchronize, granules resident in HBM" % (len(lat_ids), args.c2_lat_reps),
         "config": {"workload": "C2: %d x 512x512 EPSG:3857 tiles from %d EPSG:3577 int16 4000x4000 granules, "
                                "nearest, time-ordered merge + scale + palette" % (len(full.tiles), len(full.granules)),
                    "tiles_per_step": len(full.tiles), "tiles_per_rank": len(ids), "pairs_rank0": batch.n_pairs,
-                   "parallelism": "tile blocks over %d rank(s) (contiguous, granules per rank)" % ctx.world,
+                   "parallelism": "tile blocks over %d rank(s) (contiguous, balanced by 1 + pairs per tile, "
+                                  "granules per rank)" % ctx.world,
                    "pipeline": "%d chunks on 2 HIP streams (plan of chunk k+1 under render of chunk k)"
                                % args.c2_chunks if args.c2_chunks > 1 else "one batch, one stream"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -233,7 +345,7 @@ def run_c2(ctx: Ctx, args):
             "sample": "all 4096 C2 tiles rendered by oracle/ (C restatement of warp_operation_fast + merge + "
                       "Scale + palette) on %d threads = the box's CPU share (cgroup quota), median of %d runs; "
                       "1-core figure on 256 tiles" % (cores, args.cpu_runs)}
-    del batch, step_batch
+    del batch, step_batch, gs
     return out
 
 
@@ -422,23 +534,14 @@ def run_c4(ctx: Ctx, args):
 # ---------------------------------------------------------------- C5
 def run_c5(ctx: Ctx, args):
     full = synth.config_c5()
-    ids = block_part(len(full.tiles), ctx.rank, ctx.world)
+    ids = block_part(len(full.tiles), ctx.rank, ctx.world, partition.tile_cost(full.pairs))
     cfg = sub_config(full, ids)
-    b = build_batch(cfg, ctx.device)
+    gs = build_granules(cfg, ctx.device)
+    b = build_batch(cfg, ctx.device, gs=gs)
     sp = ScaleParams(*cfg.scale)
     dt = ctx.timed(lambda: b.render(sp), args.steps, args.warmup)
     # p50 single-tile latency: each sampled tile as its own request
-    lat = []
-    for i in range(0, len(cfg.tiles), max(1, len(cfg.tiles) // 8)):
-        one = build_batch(sub_config(cfg, [i]), ctx.device)
-        for _ in range(3):
-            one.render(sp)
-        torch.cuda.synchronize()
-        for _ in range(10):
-            t0 = time.perf_counter()
-            one.render(sp)
-            torch.cuda.synchronize()
-            lat.append((time.perf_counter() - t0) * 1e3)
+    lat = tile_latency(ctx, cfg, gs, sp, None, list(range(0, len(cfg.tiles), max(1, len(cfg.tiles) // 8))), 10)
     out = {"workload": "C5: 80 512x512 EPSG:3857 overview tiles (z4+z5) from 256 MODIS sinusoidal int16 granules + "
                        "256 QA mask granules with overview pyramids, mask 00000001, grey scaling",
            "tiles_per_s": round(len(full.tiles) * args.steps / dt, 1),
@@ -454,8 +557,20 @@ def run_c5(ctx: Ctx, args):
         ct = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": round(len(full.tiles) / ct, 2), "unit": "tiles/s", "cores": cores,
                                "kind": "port", "sample": "all 80 tiles by oracle/, %d threads" % cores}
-    del b
+    del b, gs
     return out
+
+
+def run_dry(ctx: Ctx, args):
+    """CPU dry run of the launch / timing contract (tests): a trivial step per
+    rank over gloo, timed like the real ones."""
+    if ctx.rank == args.dry_fail_rank:
+        raise SystemExit(3)   # a failing rank: the launcher must fail and stop the others
+    x = torch.zeros(1 << 16)
+    dt = ctx.timed(lambda: x.add_(1.0), args.steps, args.warmup)
+    return {"value": round(ctx.world * (1 << 16) * args.steps / dt / 1e6, 3),
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "dry_run": True, "ranks": ctx.ranks_seen(),
+            "config": {"workload": "dry run: 65536-element add per rank (launcher test)"}}
 
 
 def main():
@@ -473,14 +588,26 @@ def main():
     ap.add_argument("--c3-steps", type=int, default=3)
     ap.add_argument("--c4-cpu-polys", type=int, default=160)
     ap.add_argument("--no-deciles", action="store_true", help="C4: skip the decileCount=9 line")
+    ap.add_argument("--c2-lat-tiles", type=int, default=32, help="C2 p50: one-tile requests over this many tiles")
+    ap.add_argument("--c2-lat-reps", type=int, default=10)
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
     only = [s.strip().lower() for s in args.only.split(",") if s.strip()]
     if args.no_c1 and "c1" in only:
         only.remove("c1")
-    ctx = Ctx()
-    out = {"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": ctx.world, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
-           "vs_baseline": None, "dtype": "int16", "data": "synthetic (splitmix64 granules, SURVEY.md 8d)"}
+    ctx = Ctx(dry_run=args.dry_run)
+    if ctx.world != args.gpus and ctx.rank == 0:
+        print("bench.py: --gpus %d but WORLD_SIZE %d: reporting the %d ranks that joined" %
+              (args.gpus, ctx.world, ctx.world), file=sys.stderr)
+    out = {"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": ctx.world, "ranks_seen": None,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "int16",
+           "data": "synthetic (splitmix64 granules, SURVEY.md 8d)"}
+    out["ranks_seen"] = len(ctx.ranks_seen())
+    if args.dry_run:
+        out.update(run_dry(ctx, args))
+        only = []
     if "c2" in only:
         out.update(run_c2(ctx, args))
     configs = {}
@@ -496,8 +623,6 @@ def main():
         torch.cuda.empty_cache()
     if configs:
         out["configs"] = configs
-        if "C1" in configs and "p50_tile_ms" in configs["C1"]:
-            out["p50_tile_ms"] = configs["C1"]["p50_tile_ms"]
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)
     if ctx.dist:

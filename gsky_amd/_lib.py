@@ -10,7 +10,10 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgskyhip.so")
+# GSKYHIP_LIB=ab selects the A/B build (make -C gsky_amd/csrc ab: the same
+# kernels plus the experiment knobs it reads from the environment); tools and
+# A/B scripts only -- the product library reads no knob.
+LIB_PATH = os.path.join(_HERE, "libgskyhip_ab.so" if os.environ.get("GSKYHIP_LIB") == "ab" else "libgskyhip.so")
 
 # GDALDataType codes (warp.go:428-431) + 100 = SignedByte (warp.go:354-359)
 BYTE, UINT16, INT16, UINT32, INT32, FLOAT32, FLOAT64, SIGNEDBYTE = 1, 2, 3, 4, 5, 6, 7, 100

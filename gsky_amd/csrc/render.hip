@@ -1197,7 +1197,6 @@ struct Carve {
   PairPlan *pairs; Xform *xforms; TilePlan *tplans; int32_t *order; int32_t *pair_tile;
   RowRec *rows; Leaf *pool; int32_t *counters; MinMax *minmax; int64_t *split_list; int32_t *complex_list;
   EntryD *entries;
-  uint32_t *lut;        // 65536 RGBA: Scale + palette of every 16-bit value (band kernel)
   SepCol *sepcols;
   int pool_cap;
   int64_t total;
@@ -1223,7 +1222,6 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   const int64_t o_split = take(sizeof(int64_t) * (int64_t)np * max_h);
   const int64_t o_cl = take(sizeof(int32_t) * (int64_t)nt);
   const int64_t o_ent = take(sizeof(EntryD) * (int64_t)np);
-  const int64_t o_lut = take(sizeof(uint32_t) * 65536);
   const int64_t o_sep = take(sizeof(SepCol) * 3 * (int64_t)np);
   c.total = off;
   char *b = (char *)base;
@@ -1239,7 +1237,6 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   c.split_list = (int64_t *)(b + o_split);
   c.complex_list = (int32_t *)(b + o_cl);
   c.entries = (EntryD *)(b + o_ent);
-  c.lut = (uint32_t *)(b + o_lut);
   c.sepcols = (SepCol *)(b + o_sep);
   return c;
 }
@@ -1266,8 +1263,10 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   a.pool_cap = cv.pool_cap; a.split_list = cv.split_list; a.complex_list = cv.complex_list;
   a.entries = cv.entries;
   a.sepcols = cv.sepcols;
-  const char *sep = getenv("GSKYHIP_PLAN_SEP");   // A/B knob: 0 = three full transforms per row
-  a.sep = sep ? atoi(sep) : 1;
+  a.sep = 1;   // separable row transform (plan_cols_kernel); 0 = three full transforms per row
+#ifdef GSKYHIP_AB
+  if (const char *sep = getenv("GSKYHIP_PLAN_SEP")) a.sep = atoi(sep);
+#endif
   hipStream_t s = rc.stream;
   if (hipMemsetAsync(cv.counters, 0, 256, s) != hipSuccess) return GSKYHIP_E_HIP;
   // per-granule edge samples, staged in the split-list region (plan_rows
@@ -1275,8 +1274,10 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   // with the pairs' owning tiles
   a.n_granules = rc.n_granules;
   a.gedge = nullptr;
-  const char *ge_env = getenv("GSKYHIP_GRANULE_EDGES");   // A/B knob: 0 = per-pair edge transforms
-  const bool ge_on = ge_env ? atoi(ge_env) != 0 : true;
+  bool ge_on = true;   // per-granule edge table; false = per-pair edge transforms
+#ifdef GSKYHIP_AB
+  if (const char *ge_env = getenv("GSKYHIP_GRANULE_EDGES")) ge_on = atoi(ge_env) != 0;
+#endif
   if (ge_on && rc.n_granules > 0 && rc.n_pairs > 0 &&
       (int64_t)sizeof(GEdge) * rc.n_granules <= (int64_t)sizeof(int64_t) * rc.n_pairs * rc.max_h)
     a.gedge = (GEdge *)cv.split_list;
@@ -1344,22 +1345,9 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.canvas_tile_stride = a.canvas_ns_stride * n_out;
   a.minmax = cv.minmax;
   a.entries = cv.entries;
-  a.lds_stage = 0;   // set by launch_lds_kernels
-  a.lut = cv.lut;
-  a.lds_flags = 0;
   a.lds_mode = 0;
   a.cov_offsets = rc.cov_offsets;
   a.cov_stride = rc.cov_stride;
-  a.nn_kernel = 1;   // set by launch_lds_kernels
-  a.nn_shape = 3;
-  a.nn_xcd = 0;
-  a.nn_probe = 0;
-  a.nn_gen = 2;
-  a.nn_wpe = 0;
-  a.nn_express = 1;
-  a.nn_wide = 1;
-  a.nn_rpw = 4;
-  a.bil_kernel = 1;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256, W8 ? 8 : 1) void render_bil_kernel(RenderArgs 
           for (int q = 0; q < LPX; q++) {
             const int ic = ic0 + q * S;
             const bool in = row_in && (unsigned)ic < (unsigned)lim;
-            double sx, sy;
+            double sx = 0.0, sy = 0.0;
             bool ok = in;
             if (kind == ROW_LINEAR) {
               const double dist = (double)ic0 + (double)(q * S);
@@ -193,28 +193,13 @@ __global__ __launch_bounds__(256, W8 ? 8 : 1) void render_bil_kernel(RenderArgs 
   }
 }
 
-// Bilinear float canvases (no mask layer) go to render_bil_kernel unless
-// GSKYHIP_BIL_KERNEL=0 (A/B against the first band kernel).
-// Lane shape (LPX pixels x R rows) from RenderArgs.bil_kernel: 1 -> 4 x 1
-// (C3 1.35 ms/step vs 1.44-1.49 for the others and 2.30 for the first band
-// kernel, profiles/r02r_bench_c3_bil*.json), 2 -> 4 x 2, 3 -> 2 x 2,
-// 4 -> 8 x 1, 5 / 6 -> 4 x 1 / 4 x 2 with lane pixels 64 columns apart
-// (5 is the default: 1.31-1.34 ms, profiles/r02z6_bench_c3_bil.jsonl; forced
-// to 8 waves per SIMD it spills 63 VGPRs, so W8 stays 0)
-// (A/B knob GSKYHIP_BIL_KERNEL; 0 = render_lds_kernel).
+// Bilinear float canvases (no mask layer): 4 pixels per lane 64 columns
+// apart, one row at a time (the fastest of the round-2 lane shapes: C3
+// 1.31-1.34 ms against 1.35-1.49 ms for 4 x 1 / 4 x 2 / 2 x 2 / 8 x 1
+// consecutive and 2.30 ms for render_lds_kernel, profiles/r02r_*, r02z6_*).
 void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
-#define GSKY_BIL_LAUNCH(L, RR, SS, ...)                                                                        \
-  hipLaunchKernelGGL((render_bil_kernel<L, RR, SS, (0 __VA_ARGS__)>), dim3((unsigned)n_items), dim3(256), 0, s, a, a.entries, a.order, \
-                     a.rows, a.pool, a.tplans, a.tiles, n_items)
-  switch (a.bil_kernel) {
-    case 2: GSKY_BIL_LAUNCH(4, 2, 1); break;
-    case 3: GSKY_BIL_LAUNCH(2, 2, 1); break;
-    case 4: GSKY_BIL_LAUNCH(8, 1, 1); break;
-    case 6: GSKY_BIL_LAUNCH(4, 2, 64); break;
-    case 1: GSKY_BIL_LAUNCH(4, 1, 1); break;
-    default: GSKY_BIL_LAUNCH(4, 1, 64); break;   // 5
-  }
-#undef GSKY_BIL_LAUNCH
+  hipLaunchKernelGGL((render_bil_kernel<4, 1, 64, 0>), dim3((unsigned)n_items), dim3(256), 0, s, a, a.entries,
+                     a.order, a.rows, a.pool, a.tplans, a.tiles, n_items);
 }
 
 }  // namespace gsky

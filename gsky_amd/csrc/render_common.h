@@ -208,24 +208,9 @@ struct RenderArgs {
   MinMax *minmax;        // n_tiles * 3
   int write_rgba;
   const EntryD *entries;
-  int lds_stage;         // render_lds_kernel: 1 stage source windows in LDS, 0 gather from HBM
-  uint32_t *lut;         // workspace: RGBA of every value of an integer canvas (render_lds_kernel)
-  int lds_flags;         // render_lds_kernel variant (A/B knob, see render_lds.h)
-  int lds_mode;          // render_lds_kernel: kBilinear | kCanvas bits of the call
+  int lds_mode;          // typed band kernels: kBilinear | kCanvas bits of the call
   const int64_t *cov_offsets;  // canvas mode: per tile element offset into one image (NULL: slots)
   int64_t cov_stride;          // ... and that image's row stride (elements)
-  int nn_kernel;               // 1: render_nn_kernel for NN band work (render_nn.h), 0: render_lds_kernel
-  int nn_shape;                // render_nn_kernel pixels x rows per lane (A/B knob, render_nn.h)
-  int nn_xcd;                  // render_nn_kernel: XCD-aware item order (A/B knob)
-  int nn_probe;                // timing-only probes of render_nn_kernel (0: off; see render_nn.h)
-  int nn_wpe;                  // render_nn2_kernel: minimum waves per SIMD it is compiled for (A/B knob)
-  int nn_rpw;                  // render_nn_kernel: rows per wave (4 default; 8 / 16 A/B)
-  int nn_wide;                 // render_nn2_kernel: 16-B source-row loads for 16-bit values (A/B knob)
-  int nn_express;              // render_nn2_kernel: single-entry express path (A/B knob)
-  int bil_kernel;              // 1: render_bil_kernel for bilinear float canvases (default), 0: render_lds_kernel
-  int nn_gen;                  // NN band kernel generation: 2 render_nn_kernel (default), 3 render_nn2_kernel (A/B)
-  int nn_lut;                  // render_nn_kernel: Scale of integer canvases through a clamped-value LUT in LDS
-  int nn_stride;               // render_nn_kernel: lane pixels 64 columns apart (1) or consecutive (0)
 };
 
 // ---------------------------------------------------------------- typed fast path
@@ -459,7 +444,7 @@ __device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const
 constexpr int kLdsBandRows = 16;   // rows per block of render_lds_kernel
 constexpr int kBilinear = 4, kCanvas = 8;   // render_lds_kernel modes (RenderArgs.lds_mode)
 
-// The typed LDS-staged band kernels (render_lds.hip) for value type `vt`.
+// The typed band kernels (render_lds.hip) for value type `vt`.
 void launch_lds_kernels(const RenderArgs &a, int vt, bool mask, int n_items, hipStream_t s);
 // Generic kernels (render_generic{1,3}.hip); general_only: complex tiles only.
 void dispatch_render_1(const RenderArgs &a, int resample, bool mask, dim3 grid, bool general_only, hipStream_t s);

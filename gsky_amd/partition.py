@@ -3,9 +3,12 @@ torch.distributed (RCCL over xGMI on the node, gloo in the CPU tests).
 
 * GetMap tile batches (C2/C5): tiles are independent requests
   (tile_grpc.go:96-258 serves each on its own), so a batch is cut into
-  contiguous blocks of tiles -- neighbouring tiles share granules -- and each
-  rank uploads only the granules its block touches (`sub_config`).  No
-  data-path collective: every rank's RGBA tiles are its own responses.
+  contiguous blocks of tiles -- neighbouring tiles share granules -- balanced
+  by the work of each tile (`tile_cost`: the RGBA slot every tile writes plus
+  one gather pass per granule under it, so the empty tiles at the edge of a
+  union bbox weigh less than the covered ones), and each rank uploads only
+  the granules its block touches (`sub_config`).  No data-path collective:
+  every rank's RGBA tiles are its own responses.
 * Drill (C4): polygons are independent (drill.go:90-158 reads each file's
   window per polygon); they are dealt largest-first round-robin so the ranks'
   pixel counts balance.  `gather_drill` returns every polygon's result to
@@ -17,11 +20,34 @@ from __future__ import annotations
 from typing import List, Optional, Sequence
 
 
-def tile_blocks(n: int, rank: int, world: int) -> List[int]:
-    """Contiguous block of tile indices of `rank` (sizes differ by at most 1)."""
-    base, extra = divmod(n, world)
-    s = rank * base + min(rank, extra)
-    return list(range(s, s + base + (1 if rank < extra else 0)))
+def tile_blocks(n: int, rank: int, world: int, weights: Optional[Sequence[float]] = None) -> List[int]:
+    """Contiguous block of tile indices of `rank`.  Without weights the
+    sizes differ by at most 1; with per-tile weights tile i goes to the rank
+    whose share [r, r+1) * total / world holds the midpoint of i's weight
+    interval, so blocks stay contiguous and their weights balance to within
+    one tile."""
+    if weights is None:
+        base, extra = divmod(n, world)
+        s = rank * base + min(rank, extra)
+        return list(range(s, s + base + (1 if rank < extra else 0)))
+    if len(weights) != n:
+        raise ValueError("tile_blocks: %d weights for %d tiles" % (len(weights), n))
+    total = float(sum(weights))
+    if total <= 0.0:
+        return tile_blocks(n, rank, world)
+    out, acc = [], 0.0
+    for i, w in enumerate(weights):
+        owner = min(world - 1, int((acc + 0.5 * float(w)) * world / total))
+        if owner == rank:
+            out.append(i)
+        acc += float(w)
+    return out
+
+
+def tile_cost(pairs: Sequence[Sequence[int]]) -> List[float]:
+    """Relative render work of each tile: 1 for its RGBA slot (written even
+    when no granule covers it) + 1 per granule pair merged into it."""
+    return [1.0 + len(p) for p in pairs]
 
 
 def sub_config(cfg, ids: Sequence[int]):
