@@ -457,75 +457,97 @@ def run_c3(ctx: Ctx, args):
 
 # ---------------------------------------------------------------- C4
 def c4_stack(n_bands, size, device):
-    """The C4 time stack built directly in HBM, time-innermost (values equal
-    synth.config_c4's float32 bands)."""
+    """The C4 time stack built in HBM, time-innermost, slice by slice from
+    synth.c4_band (per-(pixel, slice) U(0, 0.05) noise and 5 % nodata,
+    SURVEY 8d)."""
     from gsky_amd import drill
-    idx = np.arange(size * size, dtype=np.uint64) + np.uint64(synth.SEED0 << 32)
-    noise = (synth.uniform01(synth.splitmix64(idx)) * 0.05).astype(np.float32).reshape(size, size)
-    nod = synth.uniform01(synth.splitmix64(idx + np.uint64(1 << 40))).reshape(size, size) < 0.05
-    t = np.arange(n_bands, dtype=np.float64)
-    base = torch.from_numpy((0.2 + 0.1 * np.sin(2 * np.pi * t / 365.0)).astype(np.float32)).to(device)
-    fac = torch.from_numpy((1.0 + (t % 7) * 0.01).astype(np.float32)).to(device)
     ts = (n_bands + 3) // 4 * 4
     st = torch.zeros((size, size, ts), dtype=torch.float32, device=device)
-    nz = torch.from_numpy(noise).to(device)
-    for y0 in range(0, size, 256):
-        st[y0:y0 + 256, :, :n_bands] = base + nz[y0:y0 + 256, :, None] * fac
-    st[torch.from_numpy(nod).to(device)] = -9999.0
+    for t0 in range(0, n_bands, 16):
+        bs = synth._pmap(lambda t: synth.c4_band(t, size, n_bands), range(t0, min(n_bands, t0 + 16)))
+        for k, b in enumerate(bs):
+            st[:, :, t0 + k] = torch.from_numpy(b).to(device)
     return drill.DrillStack.from_time_innermost(st, n_bands, -9999.0)
 
 
 def run_c4(ctx: Ctx, args):
+    """C4 through the product: GeoJSON polygons -> getDrillFileDescriptor
+    windows + ALL_TOUCHED masks on the GPU (gskyhip_drill_descriptors_device)
+    -> readData (compaction + reduction) over the HBM time stack."""
     from gsky_amd import drill
-    geo = synth.config_c4(n_bands=1, size=2048, n_polys=1000)
-    n_bands = 365
-    st = c4_stack(n_bands, 2048, ctx.device)
-    inside = [int((m == 255).sum()) for m in geo.masks]
-    mine = partition.drill_assignment(inside, ctx.rank, ctx.world)   # largest-first, round-robin
-    mb = drill.pack_masks([geo.windows[p] for p in mine], [geo.masks[p] for p in mine], ctx.device)
+    size, n_bands = 2048, 365
+    _, _, geoms = synth.c4_polygons(size, 1000)
+    wins, _ = drill.drill_windows(geoms, "EPSG:4326", synth.C4_GT, size, size)
+    area = [int(w[2]) * int(w[3]) for w in wins]
+    mine = partition.drill_assignment(area, ctx.rank, ctx.world)   # largest window first, round-robin
+    my_geoms = [geoms[p] for p in mine]
+    st = c4_stack(n_bands, size, ctx.device)
+
+    def describe():
+        return drill.drill_dataset(my_geoms, "EPSG:4326", synth.C4_GT, size, size, ctx.device)
+    mb, status = describe()
+    torch.cuda.synchronize()
+    if (status != 0).any():
+        raise RuntimeError("C4 descriptors: %d polygons failed" % int((status != 0).sum()))
+    dts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        describe()
+        torch.cuda.synchronize()
+        dts.append((time.perf_counter() - t0) * 1e3)
+    inside = int((mb.masks == 255).sum().item())
+    px = int(sum(int(w[2]) * int(w[3]) for w in mb.win.cpu().numpy()))
     res = {}
     for name, mode in (("reference_order", drill.REFERENCE_ORDER), ("wave_split", drill.WAVE_SPLIT)):
         dt = ctx.timed(lambda: drill.read_data(st, mb, *CLIP, mode=mode), args.steps, args.warmup)
         k_ms = event_ms(lambda: drill.read_data(st, mb, *CLIP, mode=mode), 5)
-        px = sum(geo.windows[p][2] * geo.windows[p][3] for p in mine)
-        abytes = sum(inside[p] for p in mine) * n_bands * 4 + px
+        abytes = inside * n_bands * 4 + px
         ach = abytes / (k_ms / 1e3) / 1e9
-        res[name] = {"value": round(len(geo.masks) * n_bands * args.steps / dt, 1), "unit": "polygon-slices/s",
+        res[name] = {"value": round(len(geoms) * n_bands * args.steps / dt, 1), "unit": "polygon-slices/s",
                      "ms_per_step": round(dt / args.steps * 1e3, 4),
                      "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(k_ms, 4),
                                   "kernel": "drill compaction + %s reduction (rank 0)" % name,
                                   "algorithmic_bytes_per_launch": int(abytes)}}
-    # decileCount = 9 (drill.go:229-273): segmented GPU sort of every (polygon, slice)
+    # decileCount = 9 (drill.go:229-273): radix selection of the picks per (polygon, slice)
     if not args.no_deciles:
-        _, cnts = drill.read_data(st, mb, *CLIP)
-        dt_dec = ctx.timed(lambda: drill.compute_deciles(st, mb, cnts, 9), 1, 1)
-        res["deciles"] = {"value": round(len(mine) * n_bands / dt_dec, 1), "unit": "polygon-slices/s",
-                          "ms_per_step": round(dt_dec * 1e3, 3), "decile_count": 9,
-                          "step": "count + scan + gather + segmented radix sort + pick, band chunks (rank 0)"}
-    out = {"workload": "C4: WPS drill zonal mean, 1000 star polygons x 365 daily f32 slices of 2048^2, "
-                       "ALL_TOUCHED masks, clip +-MaxFloat32", "polygons_rank0": len(mine), **res}
+        dt_dec = ctx.timed(lambda: drill.read_data(st, mb, *CLIP, decile_count=9), 3, 1)
+        res["deciles"] = {"value": round(len(mine) * n_bands * 3 / dt_dec, 1), "unit": "polygon-slices/s",
+                          "ms_per_step": round(dt_dec / 3 * 1e3, 3), "decile_count": 9,
+                          "step": "readData with decileCount 9: mean pass + transposing gather + radix select "
+                                  "(rank 0)"}
+    out = {"workload": "C4: WPS drill zonal mean, 1000 star polygons (GeoJSON, EPSG:4326) x 365 daily f32 slices "
+                       "of 2048^2, product windows + ALL_TOUCHED masks on the GPU, clip +-MaxFloat32",
+           "polygons_rank0": len(mine), "in_mask_px_rank0": inside,
+           "descriptors_ms": round(float(np.median(dts)), 3),
+           "descriptors_timing": "host geometry (parse, envelope, window) + GPU rasterization of rank 0's "
+                                 "polygons, median of 5", **res}
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
         from concurrent.futures import ThreadPoolExecutor
 
         from oracle import oracle as O
-        order = sorted(range(len(inside)), key=lambda p: -inside[p])   # by size, so the sample spans all sizes
+        wn = mb.win.cpu().numpy()
+        offs = mb.mask_off.cpu().numpy()
+        mk = mb.masks.cpu().numpy()
+        order = sorted(range(len(mine)), key=lambda p: -int(wn[p][2]) * int(wn[p][3]))
         ids = order[:: max(1, len(order) // args.c4_cpu_polys)][: args.c4_cpu_polys]
-        subs = {}
+        subs, msk = {}, {}
         for p in ids:
-            x0, y0, w, h = geo.windows[p]
+            x0, y0, w, h = (int(v) for v in wn[p])
             subs[p] = st.stack[y0:y0 + h, x0:x0 + w, :n_bands].permute(2, 0, 1).contiguous().cpu().numpy()
+            msk[p] = mk[offs[p]:offs[p] + w * h].reshape(h, w)
         cores = host_cores()
 
         def one(p):
-            return O.drill_read_data(subs[p], geo.masks[p], -9999.0, CLIP[0], CLIP[1], 0, 1)
+            return O.drill_read_data(subs[p], msk[p], -9999.0, CLIP[0], CLIP[1], 0, 1)
         t0 = time.perf_counter()
         with ThreadPoolExecutor(cores) as ex:
             list(ex.map(one, ids))
         ct = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": round(len(ids) * n_bands / ct, 1), "unit": "polygon-slices/s",
                                "cores": cores, "kind": "port",
-                               "sample": "%d polygons (every %d-th by size) x %d slices, oracle readData, %d threads"
+                               "sample": "%d polygons (every %d-th by window size) x %d slices, oracle readData on "
+                                         "the product masks, %d threads"
                                          % (len(ids), max(1, len(order) // args.c4_cpu_polys), n_bands, cores)}
     del st
     return out

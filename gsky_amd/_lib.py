@@ -88,6 +88,7 @@ EXPORTS = [
     "gskyhip_service_run", "gskyhip_service_register_granule", "gskyhip_service_unregister_all",
     "gskyhip_service_stats", "gskyhip_service_shutdown", "gskyhip_drill_deciles_workspace_size",
     "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device",
+    "gskyhip_drill_read_data_workspace_size", "gskyhip_drill_read_data",
 ]
 
 _lib = None
@@ -152,6 +153,10 @@ def lib() -> C.CDLL:
     L.gskyhip_drill_deciles_workspace_size.restype = i64
     L.gskyhip_drill_deciles.argtypes = [vp, ci, ci, ci, ci, vp, vp, vp, ci, i64, vp, ci, C.c_float, ci, ci, vp, vp,
                                         vp, vp, i64, vp]
+    L.gskyhip_drill_read_data_workspace_size.argtypes = [ci, i64, ci, ci, ci, ci]
+    L.gskyhip_drill_read_data_workspace_size.restype = i64
+    L.gskyhip_drill_read_data.argtypes = [vp, ci, ci, ci, ci, vp, vp, vp, ci, i64, vp, ci, C.c_float, C.c_float,
+                                          C.c_float, ci, ci, ci, ci, vp, vp, vp, vp, i64, vp]
     L.gskyhip_fnv32a.argtypes = [C.c_char_p, i64]
     L.gskyhip_fnv32a.restype = C.c_uint32
     L.gskyhip_version.restype = C.c_char_p

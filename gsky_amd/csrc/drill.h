@@ -50,6 +50,31 @@ struct DecileCall {
   hipStream_t stream;
 };
 
+// readData complete (drill.go:90-227): mean / pixel count, decileCount >= 0,
+// bandStrides >= 1 -- see gskyhip_drill_read_data in include/gskyhip.h.
+struct ReadDataCall {
+  const float *stack;
+  int xsize, ysize, n_bands, t_stride;
+  const int32_t *win;
+  const int64_t *mask_off;
+  const uint8_t *masks;
+  int n_polys;
+  int64_t mask_bytes;
+  const int32_t *bands;        // HOST band list (1-based) or NULL = 1..n_bands
+  int n_list;
+  float nodata, lo, hi;
+  int pixel_count, band_strides, decile_count, mode;
+  double *out_value;           // dev n_polys x rows x (1 + decile_count)
+  int32_t *out_count;
+  int32_t *status;             // dev n_polys: 0, or GSKYHIP_E_RANGE (the reference panics)
+  void *workspace;
+  int64_t workspace_bytes;
+  hipStream_t stream;
+};
+int64_t drill_read_data_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides,
+                                       int decile_count, int mode);
+int launch_drill_read_data(const ReadDataCall &c);
+
 __global__ __launch_bounds__(256) void drill_compact_kernel(const int32_t *__restrict__ win,
                                                             const int64_t *__restrict__ mask_off,
                                                             const uint8_t *__restrict__ masks, int n_polys,

@@ -26,6 +26,7 @@
 //   drill_rows_kernel      bandStrides rows (drill.go:128-219).
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <vector>
 
 #include "drill.h"
@@ -243,6 +244,63 @@ __global__ void drill_rows_kernel(const double *band_value, const int32_t *band_
   }
 }
 
+// readData's TimeSeries with deciles (drill.go:150-219): nCols = 1 + dc
+// columns per row -- the mean / count, then decile i with Count 1 (zeros
+// with Count 0 where the band total is 0) -- and for bandStrides > 2 every
+// column interpolated between the two bound bands of the group, counts
+// math.Round((c0 + c1) / 2).  status[p]: GSKYHIP_E_RANGE if computeDeciles
+// would have panicked on any read band of the polygon.
+__global__ void drill_timeseries_kernel(const double *band_value, const int32_t *band_count,
+                                        const float *dec, const int32_t *dec_status, int n_polys, int n_list,
+                                        int n_sel, int band_strides, int dc, int rows_per_poly, double *out_value,
+                                        int32_t *out_count, int32_t *status) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_polys) return;
+  const int nc = 1 + dc;
+  const double *bv = band_value + (int64_t)p * n_sel;
+  const int32_t *bc = band_count + (int64_t)p * n_sel;
+  double *ov = out_value + (int64_t)p * rows_per_poly * nc;
+  int32_t *oc = out_count + (int64_t)p * rows_per_poly * nc;
+  int st = 0;
+  auto cell = [&](int j, int ic, double &v, int32_t &c) {
+    if (ic == 0) { v = bv[j]; c = bc[j]; return; }
+    const int64_t sj = (int64_t)p * n_sel + j;
+    const int ds = dec_status[sj];
+    if (ds == 0) { v = (double)dec[sj * dc + ic - 1]; c = 1; }
+    else { v = 0.0; c = 0; if (ds != 1) st = ds; }
+  };
+  int nrow = 0;
+  auto emit = [&](int j) {
+    for (int ic = 0; ic < nc; ic++) cell(j, ic, ov[nrow * nc + ic], oc[nrow * nc + ic]);
+    nrow++;
+  };
+  if (band_strides <= 1) {
+    for (int j = 0; j < n_list; j++) emit(j);
+  } else {
+    int g = 0;
+    for (int ibBgn = 0; ibBgn < n_list; ibBgn += band_strides, g++) {
+      const int j0 = 2 * g, j1 = 2 * g + 1;
+      emit(j0);
+      if (band_strides > 2) {
+        for (int ip = 1; ip < band_strides - 1; ip++) {
+          for (int ic = 0; ic < nc; ic++) {
+            double v0, v1;
+            int32_t c0, c1;
+            cell(j0, ic, v0, c0);
+            cell(j1, ic, v1, c1);
+            const double beta = (v1 - v0) / (double)(band_strides - 1);
+            ov[nrow * nc + ic] = v0 + (double)ip * beta;
+            oc[nrow * nc + ic] = (int32_t)round((double)(c0 + c1) / 2.0);   // math.Round: half away from zero
+          }
+          nrow++;
+        }
+      }
+      emit(j1);
+    }
+  }
+  status[p] = st;
+}
+
 // DrillMerger weighted mean (drill_merger.go:79-93).
 __global__ void drill_merge_kernel(const double *values, const int32_t *counts, int n_files, int n_dates,
                                    double *out) {
@@ -400,6 +458,90 @@ int launch_drill_batch(const DrillCall &c) {
     hipLaunchKernelGGL(drill_rows_kernel, dim3((c.n_polys + 127) / 128), dim3(128), 0, s, bv, bc, c.n_polys,
                        n_list, n_sel, band_strides, rows, c.out_value, c.out_count);
   }
+  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+}
+
+// ---- readData complete: the read bands' means (stride 1 over the read list),
+// their deciles, then the TimeSeries rows.
+struct ReadWs {
+  int32_t *sel_dummy;
+  double *bv;
+  int32_t *bc, *dst;
+  float *dec;
+  void *mean_ws, *dec_ws;
+  int64_t mean_bytes, dec_bytes, total;
+  int chunk;
+};
+
+static ReadWs read_carve(void *base, int n_polys, int64_t mask_bytes, int n_list, int band_strides, int dc,
+                         int mode) {
+  ReadWs w;
+  const int n_sel = read_count(n_list, band_strides <= 0 ? 1 : band_strides);
+  const int np = n_polys > 0 ? n_polys : 1;
+  w.chunk = (int)std::max<int64_t>(1, std::min<int64_t>(n_sel, (1LL << 30) / std::max<int64_t>(1, mask_bytes)));
+  w.mean_bytes = drill_workspace_size(np, mask_bytes, n_sel, 1, mode);
+  w.dec_bytes = dc > 0 ? drill_deciles_workspace_size(np, mask_bytes, w.chunk) : 0;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) { const int64_t o = off; off = al256(off + (bytes > 0 ? bytes : 0)); return o; };
+  const int64_t o_bv = take(8 * (int64_t)np * n_sel);
+  const int64_t o_bc = take(4 * (int64_t)np * n_sel);
+  const int64_t o_dst = take(dc > 0 ? 4 * (int64_t)np * n_sel : 0);
+  const int64_t o_dec = take(dc > 0 ? 4 * (int64_t)np * n_sel * dc : 0);
+  const int64_t o_mw = take(w.mean_bytes);
+  const int64_t o_dw = take(w.dec_bytes);
+  w.total = (w.dec_bytes < 0) ? -1 : off;
+  char *b = (char *)base;
+  w.sel_dummy = nullptr;
+  w.bv = (double *)(b + o_bv); w.bc = (int32_t *)(b + o_bc); w.dst = (int32_t *)(b + o_dst);
+  w.dec = (float *)(b + o_dec); w.mean_ws = b + o_mw; w.dec_ws = b + o_dw;
+  return w;
+}
+
+int64_t drill_read_data_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides,
+                                       int decile_count, int mode) {
+  if (n_polys <= 0 || n_list <= 0) return 0;
+  return read_carve(nullptr, n_polys, mask_bytes, n_list, band_strides, decile_count, mode).total;
+}
+
+int launch_drill_read_data(const ReadDataCall &c) {
+  const int band_strides = c.band_strides <= 0 ? 1 : c.band_strides;
+  const int n_list = c.bands ? c.n_list : c.n_bands;
+  if (c.n_polys <= 0 || n_list <= 0) return 0;
+  if (c.decile_count < 0) return GSKYHIP_E_ARG;
+  const int64_t need = drill_read_data_workspace_size(c.n_polys, c.mask_bytes, n_list, band_strides,
+                                                      c.decile_count, c.mode);
+  if (need < 0 || !c.workspace || c.workspace_bytes < need) return GSKYHIP_E_ARG;
+  ReadWs w = read_carve(c.workspace, c.n_polys, c.mask_bytes, n_list, band_strides, c.decile_count, c.mode);
+  // the read list (drill.go:128-137) as 1-based bands, stride 1
+  std::vector<int32_t> sel;
+  for (int ibBgn = 0; ibBgn < n_list; ibBgn += band_strides) {
+    const int ibEnd = std::min(ibBgn + band_strides, n_list);
+    sel.push_back(c.bands ? c.bands[ibBgn] : ibBgn + 1);
+    if (band_strides > 1) sel.push_back(c.bands ? c.bands[ibEnd - 1] : ibEnd);
+  }
+  const int n_sel = (int)sel.size();
+  DrillCall m;
+  m.stack = c.stack; m.xsize = c.xsize; m.ysize = c.ysize; m.n_bands = c.n_bands; m.t_stride = c.t_stride;
+  m.win = c.win; m.mask_off = c.mask_off; m.masks = c.masks; m.n_polys = c.n_polys; m.mask_bytes = c.mask_bytes;
+  m.bands = sel.data(); m.n_list = n_sel; m.nodata = c.nodata; m.lo = c.lo; m.hi = c.hi;
+  m.pixel_count = c.pixel_count; m.band_strides = 1; m.mode = c.mode;
+  m.out_value = w.bv; m.out_count = w.bc; m.workspace = w.mean_ws; m.workspace_bytes = w.mean_bytes;
+  m.stream = c.stream;
+  int rc = launch_drill_batch(m);
+  if (rc) return rc;
+  if (c.decile_count > 0) {
+    DecileCall d;
+    d.stack = c.stack; d.xsize = c.xsize; d.ysize = c.ysize; d.n_bands = c.n_bands; d.t_stride = c.t_stride;
+    d.win = c.win; d.mask_off = c.mask_off; d.masks = c.masks; d.n_polys = c.n_polys; d.mask_bytes = c.mask_bytes;
+    d.bands = sel.data(); d.n_list = n_sel; d.nodata = c.nodata; d.decile_count = c.decile_count;
+    d.band_chunk = w.chunk; d.totals = w.bc; d.out = w.dec; d.status = w.dst;
+    d.workspace = w.dec_ws; d.workspace_bytes = w.dec_bytes; d.stream = c.stream;
+    if ((rc = launch_drill_deciles(d))) return rc;
+  }
+  const int rows = drill_rows_per_poly(n_list, band_strides);
+  hipLaunchKernelGGL(drill_timeseries_kernel, dim3((c.n_polys + 127) / 128), dim3(128), 0, c.stream, w.bv, w.bc,
+                     w.dec, w.dst, c.n_polys, n_list, n_sel, band_strides, c.decile_count, rows, c.out_value,
+                     c.out_count, c.status);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 

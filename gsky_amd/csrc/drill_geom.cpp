@@ -18,12 +18,25 @@
 //   OGR_G_Intersection + envelope the envelope of polygon n file envelope:
 //                                 vertices inside, edge/side crossings and
 //                                 file corners inside the polygon;
-//   GDALRasterizeGeometries       GDAL 3.0.1 alg/llrasterize.cpp with
-//     ALL_TOUCHED=TRUE            ALL_TOUCHED: GDALdllImageLineAllTouched over
-//                                 every ring, then GDALdllImageFilledPolygon
-//                                 (pixel-centre scanlines, even-odd), burn 255.
-// Parity is pinned to oracle/ (an independent C restatement), not to a
-// running GDAL (absent here).
+//   GDALRasterizeGeometries       GDAL 3.0.1 alg/llrasterize.cpp (MIT
+//     ALL_TOUCHED=TRUE            licence, (c) Frank Warmerdam and GDAL
+//                                 contributors): ALL_TOUCHED burns every pixel
+//                                 GDALdllImageLineAllTouched steps through on
+//                                 every ring (its DDA expressions are restated
+//                                 in touch_edge(), bit-exactness needs them),
+//                                 then GDALdllImageFilledPolygon's pixel-centre
+//                                 scanline fill, burn 255.
+// The scanline fill is NOT GDAL's per-row sort of intersections: every edge
+// computes GDAL's intersection abscissa on each pixel-centre line it crosses
+// (the same expression and half-open rule) and toggles one bit of a per-row
+// parity bitmap; a pixel is inside iff an odd number of intersections lie at
+// or left of it, which is exactly what burning the spans between sorted
+// intersection pairs gives (rings are closed, so every line crosses an even
+// number of edges).  This is edge-parallel with no bound on vertices or
+// intersections per row, and the same functions run on the host
+// (gskyhip_drill_descriptors) and on the GPU (..._device).  Parity is pinned
+// to oracle/ (a separate C restatement that sorts intersections the way GDAL
+// does), not to a running GDAL (absent here).
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -173,116 +186,154 @@ double go_f6(double v) {   // fmt.Sprintf("%f") parsed back by OGR
 }
 
 // ---------------------------------------------------------------- rasterizer
-struct Canvas {
-  uint8_t *m;
-  int w, h;
-  void point(int x, int y) const {
-    if (x >= 0 && x < w && y >= 0 && y < h) m[(int64_t)y * w + x] = 255;
-  }
-  void span(int y, int xs, int xe) const {   // gvBurnScanline
-    if (xs > xe) return;
-    xs = std::max(xs, 0);
-    xe = std::min(xe, w - 1);
-    for (int x = xs; x <= xe; x++) point(x, y);
-  }
+// Per-polygon rasterization state: the window canvas and its parity bitmap
+// (one bit per pixel of the rows [miny, maxy] of GDALdllImageFilledPolygon).
+struct RasterJob {
+  uint8_t *m;          // mask, h rows x w bytes
+  uint32_t *bits;      // parity bitmap, (maxy - miny + 1) rows x wpr words
+  int32_t w, h;
+  int32_t miny, maxy;  // scanline range of the fill (clamped to the canvas)
+  int32_t wpr;         // words per bitmap row
 };
 
-// GDALdllImageFilledPolygon (GDAL 3.0.1).
-void fill_polygon(const Rings &r, const Canvas &cv) {
-  const int n = (int)r.x.size();
-  if (r.part.empty() || n == 0) return;
-  double dminy = r.y[0], dmaxy = r.y[0];
-  for (int i = 1; i < n; i++) { dminy = std::min(dminy, r.y[i]); dmaxy = std::max(dmaxy, r.y[i]); }
-  const int miny = std::max((int)dminy, 0), maxy = std::min((int)dmaxy, cv.h - 1);
-  const int minx = 0, maxx = cv.w - 1;
-  std::vector<int> ints;
-  for (int y = miny; y <= maxy; y++) {
-    ints.clear();
+__host__ __device__ inline void burn(const RasterJob &J, int x, int y) {
+  if (x >= 0 && x < J.w && y >= 0 && y < J.h) J.m[(int64_t)y * J.w + x] = 255;
+}
+
+__host__ __device__ inline void toggle(const RasterJob &J, int y, int x) {
+  uint32_t *word = J.bits + (int64_t)(y - J.miny) * J.wpr + (x >> 5);
+#ifdef __HIP_DEVICE_COMPILE__
+  atomicXor(word, 1u << (x & 31));
+#else
+  *word ^= 1u << (x & 31);
+#endif
+}
+
+// Scanline range of GDALdllImageFilledPolygon over every vertex of the rings.
+inline void fill_rows(const double *Y, int n, int h, int32_t &miny, int32_t &maxy) {
+  double dminy = Y[0], dmaxy = Y[0];
+  for (int i = 1; i < n; i++) { dminy = std::min(dminy, Y[i]); dmaxy = std::max(dmaxy, Y[i]); }
+  miny = std::max((int)dminy, 0);
+  maxy = std::min((int)dmaxy, h - 1);
+}
+
+// Edge (ind1 -> ind2) of GDALdllImageFilledPolygon: on every pixel-centre
+// line y + 0.5 it crosses (half-open [dy1, dy2)), GDAL's intersection
+// abscissa toggles the parity bit at max(x, 0) when x <= w - 1 (an
+// intersection right of the canvas never counts); a horizontal edge lying on
+// a pixel-centre line burns its span when it is a bottom edge (x1 > x2).
+__host__ __device__ inline void scan_edge(const RasterJob &J, double dx1, double dy1, double dx2, double dy2) {
+  const int minx = 0, maxx = J.w - 1;
+  if (dy1 == dy2) {
+    if (!(dx1 > dx2)) return;   // top edges skipped
+    const int y = (int)floor(dy1);
+    if (y < J.miny || y > J.maxy || (double)y + 0.5 != dy1) return;
+    const int h1 = (int)floor(dx2 + 0.5), h2 = (int)floor(dx1 + 0.5);
+    if (h1 > maxx || h2 <= minx) return;
+    for (int x = h1 > 0 ? h1 : 0; x <= (h2 - 1 < J.w - 1 ? h2 - 1 : J.w - 1); x++) burn(J, x, y);
+    return;
+  }
+  if (dy1 > dy2) {
+    double t = dy1; dy1 = dy2; dy2 = t;
+    t = dx1; dx1 = dx2; dx2 = t;
+  }
+  // rows whose centre can lie in [dy1, dy2); the test below is GDAL's, exactly
+  const double f0 = floor(dy1 - 0.5) - 1.0, f1 = floor(dy2 - 0.5) + 1.0;
+  const int y0 = f0 > (double)J.miny ? (int)f0 : J.miny;
+  const int y1 = f1 < (double)J.maxy ? (int)f1 : J.maxy;
+  for (int y = y0; y <= y1; y++) {
     const double dy = y + 0.5;
-    int partoffset = 0, part = 0;
-    for (int i = 0; i < n; i++) {
-      if (i == partoffset + r.part[part]) { partoffset += r.part[part]; part++; }
-      const int ind1 = (i == partoffset) ? partoffset + r.part[part] - 1 : i - 1;
-      const int ind2 = (i == partoffset) ? partoffset : i;
-      double dy1 = r.y[ind1], dy2 = r.y[ind2], dx1, dx2;
-      if ((dy1 < dy && dy2 < dy) || (dy1 > dy && dy2 > dy)) continue;
-      if (dy1 < dy2) {
-        dx1 = r.x[ind1]; dx2 = r.x[ind2];
-      } else if (dy1 > dy2) {
-        std::swap(dy1, dy2);
-        dx1 = r.x[ind2]; dx2 = r.x[ind1];
-      } else {   // horizontal: bottom edges filled on their own, top edges skipped
-        if (r.x[ind1] > r.x[ind2]) {
-          const int h1 = (int)std::floor(r.x[ind2] + 0.5), h2 = (int)std::floor(r.x[ind1] + 0.5);
-          if (h1 > maxx || h2 <= minx) continue;
-          cv.span(y, h1, h2 - 1);
-        }
-        continue;
-      }
-      if (dy < dy2 && dy >= dy1) ints.push_back((int)std::floor((dy - dy1) * (dx2 - dx1) / (dy2 - dy1) + dx1 + 0.5));
-    }
-    std::sort(ints.begin(), ints.end());
-    for (size_t i = 0; i + 1 < ints.size(); i += 2)
-      if (ints[i] <= maxx && ints[i + 1] > minx) cv.span(y, ints[i], ints[i + 1] - 1);
+    if (!(dy < dy2 && dy >= dy1)) continue;
+    const int x = (int)floor((dy - dy1) * (dx2 - dx1) / (dy2 - dy1) + dx1 + 0.5);
+    if (x <= maxx) toggle(J, y, x > minx ? x : minx);
   }
 }
 
-// GDALdllImageLineAllTouched (GDAL 3.0.1), burn value only.
-void touch_lines(const Rings &r, const Canvas &cv) {
-  const int w = cv.w, h = cv.h;
-  size_t n0 = 0;
-  for (int np : r.part) {
-    for (int j = 1; j < np; j++) {
-      double x = r.x[n0 + j - 1], y = r.y[n0 + j - 1], xe = r.x[n0 + j], ye = r.y[n0 + j];
-      if ((y < 0.0 && ye < 0.0) || (y > h && ye > h) || (x < 0.0 && xe < 0.0) || (x > w && xe > w)) continue;
-      if (x > xe) { std::swap(x, xe); std::swap(y, ye); }
-      if (std::floor(x) == std::floor(xe) || std::fabs(x - xe) < .01) {   // vertical
-        if (ye < y) std::swap(y, ye);
-        const int ix = (int)std::floor(xe);
-        if (ix < 0 || ix >= w) continue;
-        const int iy0 = std::max((int)std::floor(y), 0), iy1 = std::min((int)std::floor(ye), h - 1);
-        for (int iy = iy0; iy <= iy1; iy++) cv.point(ix, iy);
-        continue;
-      }
-      if (std::floor(y) == std::floor(ye) || std::fabs(y - ye) < .01) {   // horizontal
-        const int iy = (int)std::floor(y);
-        if (iy < 0 || iy >= h) continue;
-        const int ix0 = std::max((int)std::floor(x), 0), ix1 = std::min((int)std::floor(xe), w - 1);
-        for (int ix = ix0; ix <= ix1; ix++) cv.point(ix, iy);
-        continue;
-      }
-      const double slope = (ye - y) / (xe - x);   // general, left to right
-      if (xe > w) { ye -= (xe - w) * slope; xe = w; }
-      if (x < 0.0) { y += (0.0 - x) * slope; x = 0.0; }
-      if (ye > y) {
-        if (y < 0.0) { x += (0.0 - y) / slope; y = 0.0; }
-        if (ye >= h) { xe += (ye - h) / slope; ye = h; }
-      } else {
-        if (y >= h) { x += (h - y) / slope; y = h; }
-        if (ye < 0.0) { xe -= (ye - 0) / slope; ye = 0.0; }
-      }
-      while (x >= 0.0 && x < xe) {
-        const int ix = (int)std::floor(x), iy = (int)std::floor(y);
-        if (iy >= 0 && iy < h) cv.point(ix, iy);
-        double sx = std::floor(x + 1.0) - x;
-        double sy = sx * slope;
-        if ((int)std::floor(y + sy) == iy) {
-          x += sx; y += sy;
-        } else if (slope < 0) {
-          sy = iy - y;
-          if (sy > -0.000000001) sy = -0.000000001;
-          sx = sy / slope;
-          x += sx; y += sy;
-        } else {
-          sy = (iy + 1) - y;
-          if (sy < 0.000000001) sy = 0.000000001;
-          sx = sy / slope;
-          x += sx; y += sy;
-        }
-      }
+// Row y of the fill: prefix parity over the row's bits, burn the odd pixels.
+__host__ __device__ inline void burn_row(const RasterJob &J, int y) {
+  const uint32_t *row = J.bits + (int64_t)(y - J.miny) * J.wpr;
+  uint32_t carry = 0;
+  for (int k = 0; k < J.wpr; k++) {
+    uint32_t p = row[k];
+    p ^= p << 1; p ^= p << 2; p ^= p << 4; p ^= p << 8; p ^= p << 16;   // prefix xor within the word
+    p ^= carry;
+    carry = (p >> 31) ? 0xFFFFFFFFu : 0u;
+    while (p) {
+      const int b = __builtin_ctz(p);
+      burn(J, 32 * k + b, y);
+      p &= p - 1;
     }
-    n0 += np;
   }
+}
+
+// GDALdllImageLineAllTouched (GDAL 3.0.1) for the segment (x, y) -> (xe, ye),
+// burn value only.
+__host__ __device__ inline void touch_edge(const RasterJob &J, double x, double y, double xe, double ye) {
+  const int w = J.w, h = J.h;
+  if ((y < 0.0 && ye < 0.0) || (y > h && ye > h) || (x < 0.0 && xe < 0.0) || (x > w && xe > w)) return;
+  if (x > xe) {
+    double t = x; x = xe; xe = t;
+    t = y; y = ye; ye = t;
+  }
+  if (floor(x) == floor(xe) || fabs(x - xe) < .01) {   // vertical
+    if (ye < y) { const double t = y; y = ye; ye = t; }
+    const int ix = (int)floor(xe);
+    if (ix < 0 || ix >= w) return;
+    const int iy0 = (int)floor(y) > 0 ? (int)floor(y) : 0;
+    const int iy1 = (int)floor(ye) < h - 1 ? (int)floor(ye) : h - 1;
+    for (int iy = iy0; iy <= iy1; iy++) burn(J, ix, iy);
+    return;
+  }
+  if (floor(y) == floor(ye) || fabs(y - ye) < .01) {   // horizontal
+    const int iy = (int)floor(y);
+    if (iy < 0 || iy >= h) return;
+    const int ix0 = (int)floor(x) > 0 ? (int)floor(x) : 0;
+    const int ix1 = (int)floor(xe) < w - 1 ? (int)floor(xe) : w - 1;
+    for (int ix = ix0; ix <= ix1; ix++) burn(J, ix, iy);
+    return;
+  }
+  const double slope = (ye - y) / (xe - x);   // general, left to right
+  if (xe > w) { ye -= (xe - w) * slope; xe = w; }
+  if (x < 0.0) { y += (0.0 - x) * slope; x = 0.0; }
+  if (ye > y) {
+    if (y < 0.0) { x += (0.0 - y) / slope; y = 0.0; }
+    if (ye >= h) { xe += (ye - h) / slope; ye = h; }
+  } else {
+    if (y >= h) { x += (h - y) / slope; y = h; }
+    if (ye < 0.0) { xe -= (ye - 0) / slope; ye = 0.0; }
+  }
+  while (x >= 0.0 && x < xe) {
+    const int ix = (int)floor(x), iy = (int)floor(y);
+    if (iy >= 0 && iy < h) burn(J, ix, iy);
+    double sx = floor(x + 1.0) - x;
+    double sy = sx * slope;
+    if ((int)floor(y + sy) == iy) {
+      x += sx; y += sy;
+    } else if (slope < 0) {
+      sy = iy - y;
+      if (sy > -0.000000001) sy = -0.000000001;
+      sx = sy / slope;
+      x += sx; y += sy;
+    } else {
+      sy = (iy + 1) - y;
+      if (sy < 0.000000001) sy = 0.000000001;
+      sx = sy / slope;
+      x += sx; y += sy;
+    }
+  }
+}
+
+// Edge k of a polygon's rings, k in [0, n): (ind1, ind2) of
+// GDALdllImageFilledPolygon (the closing edge last -> first of its ring for
+// the ring's first point) and, unless k starts its ring, the segment k-1 -> k
+// that GDALdllImageLineAllTouched draws.
+__host__ __device__ inline void edge_of(const int32_t *part, int np, int k, int &ind1, int &ind2, bool &draw) {
+  int start = 0, r = 0;
+  while (r < np && k >= start + part[r]) { start += part[r]; r++; }
+  if (r >= np) { ind1 = ind2 = k; draw = false; return; }
+  draw = k != start;
+  ind1 = draw ? k - 1 : start + part[r] - 1;
+  ind2 = k;
 }
 
 struct Descriptor {
@@ -347,137 +398,67 @@ Descriptor describe(const char *geometry, const gskyhip_crs *crs, const double g
 }
 
 // ---------------------------------------------------------------- GPU rasterizer
-// The same two passes on the GPU, one workgroup per polygon, straight into
-// the device mask buffer (no host mask, no copy): touch_edge_kernel gives each
-// thread one edge of the rings (GDALdllImageLineAllTouched, the expressions of
-// touch_lines()), fill_rows_kernel one scanline (GDALdllImageFilledPolygon,
-// the expressions of fill_polygon(): intersections collected, insertion-
-// sorted, spans burned).  Both only ever write 255, so the thread order and
-// overlapping writes do not matter; the region is zeroed first.  Polygons
-// with more than kMaxInts edges (more intersections than a thread keeps) are
-// rasterized on the host instead.
-constexpr int kMaxInts = 64;
-
+// The same passes on the GPU, straight into the device mask buffer: one
+// workgroup per polygon, a thread per edge for the ALL_TOUCHED lines and the
+// parity toggles (atomic XOR), then a thread per scanline for the burn.  Both
+// only ever write 255, so thread order and overlapping writes do not matter;
+// masks and bitmaps are zeroed first.  No bound on vertices or intersections.
 struct PolyDev {
   int64_t mask_off;
+  int64_t bits_off;    // first parity word
   int32_t w, h;
   int32_t v0, nv;      // vertex range in vx / vy
   int32_t p0, np;      // ring range in parts (points per ring)
+  int32_t miny, maxy, wpr, _pad;
 };
 
-__device__ __forceinline__ void dpoint(uint8_t *m, int w, int h, int x, int y) {
-  if (x >= 0 && x < w && y >= 0 && y < h) m[(int64_t)y * w + x] = 255;
+__device__ inline RasterJob job_of(const PolyDev &P, uint8_t *masks, uint32_t *bits) {
+  RasterJob J;
+  J.m = masks + P.mask_off;
+  J.bits = bits + P.bits_off;
+  J.w = P.w; J.h = P.h; J.miny = P.miny; J.maxy = P.maxy; J.wpr = P.wpr;
+  return J;
 }
 
-__global__ __launch_bounds__(256) void touch_edge_kernel(const PolyDev *polys, const double *vx, const double *vy,
-                                                         const int32_t *parts, uint8_t *masks) {
+__global__ __launch_bounds__(256) void edges_kernel(const PolyDev *polys, const double *vx, const double *vy,
+                                                    const int32_t *parts, uint8_t *masks, uint32_t *bits) {
   const PolyDev P = polys[blockIdx.x];
-  uint8_t *m = masks + P.mask_off;
-  const int w = P.w, h = P.h;
-  for (int k = threadIdx.x; k < P.nv; k += blockDim.x) {
-    // edge (k-1, k) of its ring; the first point of a ring starts no edge
-    int start = 0, r = 0;
-    while (r < P.np && k >= start + parts[P.p0 + r]) { start += parts[P.p0 + r]; r++; }
-    if (r >= P.np || k == start) continue;
-    double x = vx[P.v0 + k - 1], y = vy[P.v0 + k - 1], xe = vx[P.v0 + k], ye = vy[P.v0 + k];
-    if ((y < 0.0 && ye < 0.0) || (y > h && ye > h) || (x < 0.0 && xe < 0.0) || (x > w && xe > w)) continue;
-    if (x > xe) { double t = x; x = xe; xe = t; t = y; y = ye; ye = t; }
-    if (floor(x) == floor(xe) || fabs(x - xe) < .01) {   // vertical
-      if (ye < y) { const double t = y; y = ye; ye = t; }
-      const int ix = (int)floor(xe);
-      if (ix < 0 || ix >= w) continue;
-      const int iy0 = max((int)floor(y), 0), iy1 = min((int)floor(ye), h - 1);
-      for (int iy = iy0; iy <= iy1; iy++) dpoint(m, w, h, ix, iy);
-      continue;
-    }
-    if (floor(y) == floor(ye) || fabs(y - ye) < .01) {   // horizontal
-      const int iy = (int)floor(y);
-      if (iy < 0 || iy >= h) continue;
-      const int ix0 = max((int)floor(x), 0), ix1 = min((int)floor(xe), w - 1);
-      for (int ix = ix0; ix <= ix1; ix++) dpoint(m, w, h, ix, iy);
-      continue;
-    }
-    const double slope = (ye - y) / (xe - x);   // general, left to right
-    if (xe > w) { ye -= (xe - w) * slope; xe = w; }
-    if (x < 0.0) { y += (0.0 - x) * slope; x = 0.0; }
-    if (ye > y) {
-      if (y < 0.0) { x += (0.0 - y) / slope; y = 0.0; }
-      if (ye >= h) { xe += (ye - h) / slope; ye = h; }
-    } else {
-      if (y >= h) { x += (h - y) / slope; y = h; }
-      if (ye < 0.0) { xe -= (ye - 0) / slope; ye = 0.0; }
-    }
-    while (x >= 0.0 && x < xe) {
-      const int ix = (int)floor(x), iy = (int)floor(y);
-      if (iy >= 0 && iy < h) dpoint(m, w, h, ix, iy);
-      double sx = floor(x + 1.0) - x;
-      double sy = sx * slope;
-      if ((int)floor(y + sy) == iy) {
-        x += sx; y += sy;
-      } else if (slope < 0) {
-        sy = iy - y;
-        if (sy > -0.000000001) sy = -0.000000001;
-        sx = sy / slope;
-        x += sx; y += sy;
-      } else {
-        sy = (iy + 1) - y;
-        if (sy < 0.000000001) sy = 0.000000001;
-        sx = sy / slope;
-        x += sx; y += sy;
-      }
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void fill_rows_kernel(const PolyDev *polys, const double *vx, const double *vy,
-                                                        const int32_t *parts, uint8_t *masks) {
-  const PolyDev P = polys[blockIdx.x];
-  uint8_t *m = masks + P.mask_off;
-  const int w = P.w, h = P.h, n = P.nv;
-  if (P.np <= 0 || n == 0) return;
+  const RasterJob J = job_of(P, masks, bits);
   const double *X = vx + P.v0, *Y = vy + P.v0;
-  const int32_t *part = parts + P.p0;
-  double dminy = Y[0], dmaxy = Y[0];
-  for (int i = 1; i < n; i++) { dminy = fmin(dminy, Y[i]); dmaxy = fmax(dmaxy, Y[i]); }
-  const int miny = max((int)dminy, 0), maxy = min((int)dmaxy, h - 1);
-  const int minx = 0, maxx = w - 1;
-  int ints[kMaxInts];
-  for (int y = miny + (int)threadIdx.x; y <= maxy; y += blockDim.x) {
-    int ni = 0;
-    const double dy = y + 0.5;
-    int partoffset = 0, pi = 0;
-    for (int i = 0; i < n; i++) {
-      if (i == partoffset + part[pi]) { partoffset += part[pi]; pi++; }
-      const int ind1 = (i == partoffset) ? partoffset + part[pi] - 1 : i - 1;
-      const int ind2 = (i == partoffset) ? partoffset : i;
-      double dy1 = Y[ind1], dy2 = Y[ind2], dx1, dx2;
-      if ((dy1 < dy && dy2 < dy) || (dy1 > dy && dy2 > dy)) continue;
-      if (dy1 < dy2) {
-        dx1 = X[ind1]; dx2 = X[ind2];
-      } else if (dy1 > dy2) {
-        const double t = dy1; dy1 = dy2; dy2 = t;
-        dx1 = X[ind2]; dx2 = X[ind1];
-      } else {   // horizontal: bottom edges filled on their own, top edges skipped
-        if (X[ind1] > X[ind2]) {
-          const int h1 = (int)floor(X[ind2] + 0.5), h2 = (int)floor(X[ind1] + 0.5);
-          if (h1 > maxx || h2 <= minx) continue;
-          for (int xx = max(h1, 0); xx <= min(h2 - 1, w - 1); xx++) dpoint(m, w, h, xx, y);
-        }
-        continue;
-      }
-      if (dy < dy2 && dy >= dy1 && ni < kMaxInts)
-        ints[ni++] = (int)floor((dy - dy1) * (dx2 - dx1) / (dy2 - dy1) + dx1 + 0.5);
-    }
-    for (int a = 1; a < ni; a++) {   // insertion sort (a few intersections per row)
-      const int v = ints[a];
-      int b = a - 1;
-      while (b >= 0 && ints[b] > v) { ints[b + 1] = ints[b]; b--; }
-      ints[b + 1] = v;
-    }
-    for (int i = 0; i + 1 < ni; i += 2)
-      if (ints[i] <= maxx && ints[i + 1] > minx)
-        for (int xx = max(ints[i], 0); xx <= min(ints[i + 1] - 1, w - 1); xx++) dpoint(m, w, h, xx, y);
+  for (int k = threadIdx.x; k < P.nv; k += blockDim.x) {
+    int ind1, ind2;
+    bool draw;
+    edge_of(parts + P.p0, P.np, k, ind1, ind2, draw);
+    if (draw) touch_edge(J, X[k - 1], Y[k - 1], X[k], Y[k]);
+    if (ind1 != ind2 || draw) scan_edge(J, X[ind1], Y[ind1], X[ind2], Y[ind2]);
   }
+}
+
+__global__ __launch_bounds__(256) void burn_rows_kernel(const PolyDev *polys, uint8_t *masks, uint32_t *bits) {
+  const PolyDev P = polys[blockIdx.x];
+  const RasterJob J = job_of(P, masks, bits);
+  for (int y = P.miny + (int)threadIdx.x; y <= P.maxy; y += blockDim.x) burn_row(J, y);
+}
+
+// Host rasterization of one window (gskyhip_drill_descriptors): the same
+// functions, edges then rows.
+void rasterize_host(const Rings &r, uint8_t *m, int w, int h) {
+  const int n = (int)r.x.size();
+  if (r.part.empty() || n == 0) return;
+  RasterJob J;
+  J.m = m; J.w = w; J.h = h;
+  fill_rows(r.y.data(), n, h, J.miny, J.maxy);
+  J.wpr = (w + 31) / 32;
+  std::vector<uint32_t> bits(J.maxy >= J.miny ? (size_t)(J.maxy - J.miny + 1) * J.wpr : 0, 0u);
+  J.bits = bits.data();
+  for (int k = 0; k < n; k++) {
+    int ind1, ind2;
+    bool draw;
+    edge_of(r.part.data(), (int)r.part.size(), k, ind1, ind2, draw);
+    if (draw) touch_edge(J, r.x[k - 1], r.y[k - 1], r.x[k], r.y[k]);
+    if (J.maxy >= J.miny) scan_edge(J, r.x[ind1], r.y[ind1], r.x[ind2], r.y[ind2]);
+  }
+  for (int y = J.miny; y <= J.maxy; y++) burn_row(J, y);
 }
 
 }  // namespace
@@ -485,7 +466,8 @@ __global__ __launch_bounds__(256) void fill_rows_kernel(const PolyDev *polys, co
 
 using namespace gsky;
 
-// Windows on the host, ALL_TOUCHED masks rasterized on the GPU into masks_dev.
+// Windows on the host, ALL_TOUCHED masks rasterized on the GPU into masks_dev
+// (every polygon, any vertex count), all on `stream`.
 extern "C" int gskyhip_drill_descriptors_device(const char *const *geometries, int n, const char *dataset_srs,
                                                 const double *geot, int xsize, int ysize, int32_t *win_out,
                                                 int64_t *mask_off_out, int64_t *mask_bytes_out, uint8_t *masks_dev,
@@ -500,35 +482,32 @@ extern "C" int gskyhip_drill_descriptors_device(const char *const *geometries, i
   std::vector<PolyDev> polys;
   std::vector<double> vx, vy;
   std::vector<int32_t> parts;
-  std::vector<std::pair<int64_t, std::vector<uint8_t>>> host_masks;   // polygons too complex for a thread
-  int64_t off = 0;
+  int64_t off = 0, words = 0;
   for (int i = 0; i < n; i++) {
     Descriptor d = describe(geometries[i], pc, geot, xsize, ysize);
     status_out[i] = d.status;
     const int64_t bytes = d.status == 0 ? (int64_t)d.win[2] * d.win[3] : 0;
     for (int k = 0; k < 4; k++) win_out[4 * i + k] = d.status == 0 ? d.win[k] : 0;
     mask_off_out[i] = off;
-    if (masks_dev && bytes > 0) {
-      if ((int)d.pix.x.size() > kMaxInts) {
-        std::vector<uint8_t> hm((size_t)bytes, 0);
-        Canvas cv{hm.data(), d.win[2], d.win[3]};
-        touch_lines(d.pix, cv);
-        fill_polygon(d.pix, cv);
-        host_masks.emplace_back(off, std::move(hm));
-      } else {
-        PolyDev P;
-        P.mask_off = off;
-        P.w = d.win[2];
-        P.h = d.win[3];
-        P.v0 = (int32_t)vx.size();
-        P.nv = (int32_t)d.pix.x.size();
-        P.p0 = (int32_t)parts.size();
-        P.np = (int32_t)d.pix.part.size();
-        vx.insert(vx.end(), d.pix.x.begin(), d.pix.x.end());
-        vy.insert(vy.end(), d.pix.y.begin(), d.pix.y.end());
-        parts.insert(parts.end(), d.pix.part.begin(), d.pix.part.end());
-        polys.push_back(P);
-      }
+    if (masks_dev && bytes > 0 && !d.pix.x.empty()) {
+      PolyDev P;
+      P.mask_off = off;
+      P.w = d.win[2];
+      P.h = d.win[3];
+      P.v0 = (int32_t)vx.size();
+      P.nv = (int32_t)d.pix.x.size();
+      P.p0 = (int32_t)parts.size();
+      P.np = (int32_t)d.pix.part.size();
+      fill_rows(d.pix.y.data(), P.nv, P.h, P.miny, P.maxy);
+      P.wpr = (P.w + 31) / 32;
+      P._pad = 0;
+      P.bits_off = words;
+      if (P.maxy >= P.miny) words += (int64_t)(P.maxy - P.miny + 1) * P.wpr;
+      else P.maxy = P.miny - 1;   // no scanline: only the ALL_TOUCHED lines
+      vx.insert(vx.end(), d.pix.x.begin(), d.pix.x.end());
+      vy.insert(vy.end(), d.pix.y.begin(), d.pix.y.end());
+      parts.insert(parts.end(), d.pix.part.begin(), d.pix.part.end());
+      polys.push_back(P);
     }
     off += (bytes + 15) / 16 * 16;   // 16-byte aligned regions, polygon order
   }
@@ -536,37 +515,34 @@ extern "C" int gskyhip_drill_descriptors_device(const char *const *geometries, i
   if (!masks_dev) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(masks_dev, 0, (size_t)*mask_bytes_out, s) != hipSuccess) return GSKYHIP_E_HIP;
-  if (!polys.empty()) {
-    // one staging allocation: polygons | x | y | parts
-    const size_t b0 = polys.size() * sizeof(PolyDev), b1 = vx.size() * 8, b2 = parts.size() * 4;
-    char *dev = nullptr;
-    if (hipMalloc(&dev, b0 + 2 * b1 + b2) != hipSuccess) return GSKYHIP_E_HIP;
-    std::vector<char> host(b0 + 2 * b1 + b2);
-    std::memcpy(host.data(), polys.data(), b0);
-    std::memcpy(host.data() + b0, vx.data(), b1);
-    std::memcpy(host.data() + b0 + b1, vy.data(), b1);
-    std::memcpy(host.data() + b0 + 2 * b1, parts.data(), b2);
-    int rc = 0;
-    if (hipMemcpyAsync(dev, host.data(), host.size(), hipMemcpyHostToDevice, s) != hipSuccess) rc = GSKYHIP_E_HIP;
-    const PolyDev *dp = (const PolyDev *)dev;
-    const double *dx = (const double *)(dev + b0), *dy = (const double *)(dev + b0 + b1);
-    const int32_t *dpart = (const int32_t *)(dev + b0 + 2 * b1);
-    if (!rc) {
-      hipLaunchKernelGGL(touch_edge_kernel, dim3((unsigned)polys.size()), dim3(256), 0, s, dp, dx, dy, dpart,
-                         masks_dev);
-      hipLaunchKernelGGL(fill_rows_kernel, dim3((unsigned)polys.size()), dim3(256), 0, s, dp, dx, dy, dpart,
-                         masks_dev);
-      if (hipGetLastError() != hipSuccess) rc = GSKYHIP_E_HIP;
-    }
-    // the staging buffers must outlive the kernels
-    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GSKYHIP_E_HIP;
-    (void)hipFree(dev);
-    if (rc) return rc;
+  if (polys.empty()) return 0;
+  // one staging allocation: polygons | x | y | parts | parity bitmaps
+  const size_t b0 = polys.size() * sizeof(PolyDev), b1 = vx.size() * 8, b2 = (parts.size() * 4 + 15) / 16 * 16;
+  const size_t b3 = (size_t)std::max<int64_t>(words, 1) * 4;
+  char *dev = nullptr;
+  if (hipMalloc(&dev, b0 + 2 * b1 + b2 + b3) != hipSuccess) return GSKYHIP_E_HIP;
+  std::vector<char> host(b0 + 2 * b1 + b2);
+  std::memcpy(host.data(), polys.data(), b0);
+  std::memcpy(host.data() + b0, vx.data(), b1);
+  std::memcpy(host.data() + b0 + b1, vy.data(), b1);
+  std::memcpy(host.data() + b0 + 2 * b1, parts.data(), parts.size() * 4);
+  int rc = 0;
+  uint32_t *bits = (uint32_t *)(dev + b0 + 2 * b1 + b2);
+  if (hipMemcpyAsync(dev, host.data(), host.size(), hipMemcpyHostToDevice, s) != hipSuccess) rc = GSKYHIP_E_HIP;
+  if (!rc && hipMemsetAsync(bits, 0, b3, s) != hipSuccess) rc = GSKYHIP_E_HIP;
+  const PolyDev *dp = (const PolyDev *)dev;
+  const double *dx = (const double *)(dev + b0), *dy = (const double *)(dev + b0 + b1);
+  const int32_t *dpart = (const int32_t *)(dev + b0 + 2 * b1);
+  if (!rc) {
+    hipLaunchKernelGGL(edges_kernel, dim3((unsigned)polys.size()), dim3(256), 0, s, dp, dx, dy, dpart, masks_dev,
+                       bits);
+    hipLaunchKernelGGL(burn_rows_kernel, dim3((unsigned)polys.size()), dim3(256), 0, s, dp, masks_dev, bits);
+    if (hipGetLastError() != hipSuccess) rc = GSKYHIP_E_HIP;
   }
-  for (auto &hm : host_masks)
-    if (hipMemcpy(masks_dev + hm.first, hm.second.data(), hm.second.size(), hipMemcpyHostToDevice) != hipSuccess)
-      return GSKYHIP_E_HIP;
-  return 0;
+  // the staging buffers (and `host`, read by the async copy) must outlive the work
+  if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GSKYHIP_E_HIP;
+  (void)hipFree(dev);
+  return rc;
 }
 
 extern "C" int gskyhip_drill_descriptors(const char *const *geometries, int n, const char *dataset_srs,
@@ -588,10 +564,8 @@ extern "C" int gskyhip_drill_descriptors(const char *const *geometries, int n, c
     for (int k = 0; k < 4; k++) win_out[4 * i + k] = d.status == 0 ? d.win[k] : 0;
     mask_off_out[i] = off;
     if (masks_out && bytes > 0) {
-      Canvas cv{masks_out + off, d.win[2], d.win[3]};
-      std::memset(cv.m, 0, (size_t)bytes);
-      touch_lines(d.pix, cv);    // ALL_TOUCHED: every pixel an edge passes through
-      fill_polygon(d.pix, cv);   // plus every pixel centre inside
+      std::memset(masks_out + off, 0, (size_t)bytes);
+      rasterize_host(d.pix, masks_out + off, d.win[2], d.win[3]);   // ALL_TOUCHED lines + scanline fill
     }
     off += (bytes + 15) / 16 * 16;   // 16-byte aligned regions, polygon order
   }

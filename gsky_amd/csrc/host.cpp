@@ -307,7 +307,10 @@ int gskyhip_device_count(void) {
 }
 
 int gskyhip_register_granule(const char *path, int band, const gskyhip_granule *g, const char *srs) {
-  if (!path || !g) return GSKYHIP_E_ARG;
+  if (!path || !g || !g->data || g->xsize <= 0 || g->ysize <= 0 || type_size(g->dtype) <= 0) return GSKYHIP_E_ARG;
+  if (g->n_ovr < 0 || g->n_ovr > GSKYHIP_MAX_OVR) return GSKYHIP_E_ARG;
+  for (int k = 0; k < g->n_ovr; k++)
+    if (!g->ovr_data[k] || g->ovr_xsize[k] <= 0 || g->ovr_ysize[k] <= 0) return GSKYHIP_E_ARG;
   Registered r;
   r.g = *g;
   r.has_crs = false;
@@ -745,6 +748,29 @@ int gskyhip_drill_deciles(const float *stack, int xsize, int ysize, int n_bands,
   c.band_chunk = band_chunk; c.totals = totals; c.out = out; c.status = status;
   c.workspace = workspace; c.workspace_bytes = workspace_bytes; c.stream = (hipStream_t)stream;
   return launch_drill_deciles(c);
+}
+
+int64_t gskyhip_drill_read_data_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides,
+                                               int decile_count, int mode) {
+  return drill_read_data_workspace_size(n_polys, mask_bytes, n_list, band_strides, decile_count, mode);
+}
+
+int gskyhip_drill_read_data(const float *stack, int xsize, int ysize, int n_bands, int t_stride, const int32_t *win,
+                            const int64_t *mask_off, const uint8_t *masks, int n_polys, int64_t mask_bytes,
+                            const int32_t *bands, int n_list, float nodata, float clip_lower, float clip_upper,
+                            int pixel_count, int band_strides, int decile_count, int mode, double *out_value,
+                            int32_t *out_count, int32_t *status, void *workspace, int64_t workspace_bytes,
+                            void *stream) {
+  if (!stack || !win || !mask_off || !masks || !out_value || !out_count || !status) return GSKYHIP_E_ARG;
+  if (mode != 0 && mode != 1) return GSKYHIP_E_ARG;
+  ReadDataCall c;
+  c.stack = stack; c.xsize = xsize; c.ysize = ysize; c.n_bands = n_bands; c.t_stride = t_stride;
+  c.win = win; c.mask_off = mask_off; c.masks = masks; c.n_polys = n_polys; c.mask_bytes = mask_bytes;
+  c.bands = bands; c.n_list = n_list; c.nodata = nodata; c.lo = clip_lower; c.hi = clip_upper;
+  c.pixel_count = pixel_count; c.band_strides = band_strides; c.decile_count = decile_count; c.mode = mode;
+  c.out_value = out_value; c.out_count = out_count; c.status = status;
+  c.workspace = workspace; c.workspace_bytes = workspace_bytes; c.stream = (hipStream_t)stream;
+  return launch_drill_read_data(c);
 }
 
 // RasterMerger.Run for one batch over warped FlexRasters (tile_merger.go:447-503).

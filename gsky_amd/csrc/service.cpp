@@ -15,7 +15,9 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <memory>
+#include <new>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -101,7 +103,18 @@ bool send_msg(int fd, uint32_t op, const std::vector<char> &payload) {
   return write_all(fd, hdr, 16) && (n == 0 || write_all(fd, payload.data(), n));
 }
 
-bool recv_msg(int fd, uint32_t &op, std::vector<char> &payload) {
+// Largest payload a message of `op` may carry: a registration holds granule
+// data (up to 64 GiB), a warp request a few strings and numbers, the rest
+// nothing -- so one bad header cannot make the daemon allocate gigabytes.
+uint64_t max_payload(uint32_t op) {
+  switch (op) {
+    case SVC_REGISTER: return 1ull << 36;
+    case SVC_WARP: return 1ull << 20;
+    default: return 64;
+  }
+}
+
+bool recv_msg(int fd, uint32_t &op, std::vector<char> &payload, bool reply = false) {
   char hdr[16];
   if (!read_all(fd, hdr, 16)) return false;
   uint32_t magic;
@@ -109,8 +122,12 @@ bool recv_msg(int fd, uint32_t &op, std::vector<char> &payload) {
   std::memcpy(&magic, hdr, 4);
   std::memcpy(&op, hdr + 4, 4);
   std::memcpy(&n, hdr + 8, 8);
-  if (magic != kSvcMagic || n > (1ull << 36)) return false;
-  payload.resize(n);
+  if (magic != kSvcMagic || n > (reply ? (1ull << 36) : max_payload(op))) return false;
+  try {
+    payload.resize(n);
+  } catch (const std::bad_alloc &) {
+    return false;
+  }
   return n == 0 || read_all(fd, payload.data(), n);
 }
 
@@ -133,7 +150,7 @@ bool exchange(const char *sock, uint32_t op, const std::vector<char> &req, std::
   const int fd = connect_to(sock);
   if (fd < 0) return false;
   uint32_t rop = 0;
-  const bool ok = send_msg(fd, op, req) && recv_msg(fd, rop, rep) && rop == op;
+  const bool ok = send_msg(fd, op, req) && recv_msg(fd, rop, rep, true) && rop == op;
   ::close(fd);
   return ok;
 }
@@ -201,8 +218,26 @@ struct Service {
   std::atomic<int64_t> n_req{0}, n_batches{0}, max_seen{0}, n_reg{0};
   std::atomic<int> active{0};          // connection threads still running (detached)
   std::mutex reg_mu;
-  std::vector<void *> device_allocs;   // granule data uploaded through SVC_REGISTER
+  // granule data uploaded through SVC_REGISTER, per (path, band): freed when
+  // the granule is registered again or everything is unregistered
+  std::map<std::pair<std::string, int32_t>, std::vector<void *>> device_allocs;
+  void free_all() {
+    for (auto &kv : device_allocs)
+      for (void *p : kv.second) (void)hipFree(p);
+    device_allocs.clear();
+  }
 };
+
+// Stop the service: the flag changes under `mu`, so neither the batcher nor a
+// connection waiting to enqueue can miss it.
+void request_stop(Service *s) {
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->stop = true;
+  }
+  s->cv_queue.notify_all();
+  s->cv_done.notify_all();
+}
 
 Service *g_svc = nullptr;
 
@@ -251,34 +286,47 @@ int do_register(Service *s, In &in) {
   const int32_t band = in.get<int32_t>();
   const std::string srs = in.get_str();
   gskyhip_granule g = in.get<gskyhip_granule>();
-  if (!in.ok || g.n_ovr < 0 || g.n_ovr > GSKYHIP_MAX_OVR) return GSKYHIP_E_ARG;
+  if (!in.ok || g.n_ovr < 0 || g.n_ovr > GSKYHIP_MAX_OVR || g.xsize <= 0 || g.ysize <= 0 || type_size(g.dtype) <= 0)
+    return GSKYHIP_E_ARG;
+  for (int k = 0; k < g.n_ovr; k++)
+    if (g.ovr_xsize[k] <= 0 || g.ovr_ysize[k] <= 0) return GSKYHIP_E_ARG;
   std::lock_guard<std::mutex> rl(s->reg_mu);
+  std::vector<void *> mine;   // this registration's uploads: freed again on any failure
+  auto fail = [&](int e) {
+    for (void *p : mine) (void)hipFree(p);
+    return e;
+  };
   auto upload = [&](const char *p, uint64_t n, void **dev) -> int {
     if (hipMalloc(dev, n > 0 ? n : 1) != hipSuccess) return GSKYHIP_E_HIP;
-    s->device_allocs.push_back(*dev);
+    mine.push_back(*dev);
     if (n > 0 && hipMemcpy(*dev, p, n, hipMemcpyHostToDevice) != hipSuccess) return GSKYHIP_E_HIP;
     return 0;
   };
   uint64_t n = 0;
   const char *p = in.get_bytes(n);
-  if (!in.ok || n != (uint64_t)g.xsize * g.ysize * type_size(g.dtype)) return GSKYHIP_E_ARG;
+  if (!in.ok || n != (uint64_t)g.xsize * (uint64_t)g.ysize * (uint64_t)type_size(g.dtype)) return GSKYHIP_E_ARG;
   void *dev = nullptr;
   int e = upload(p, n, &dev);
-  if (e) return e;
+  if (e) return fail(e);
   g.data = dev;
   for (int k = 0; k < g.n_ovr; k++) {
     const char *po = in.get_bytes(n);
-    if (!in.ok || n != (uint64_t)g.ovr_xsize[k] * g.ovr_ysize[k] * type_size(g.dtype)) return GSKYHIP_E_ARG;
+    if (!in.ok || n != (uint64_t)g.ovr_xsize[k] * (uint64_t)g.ovr_ysize[k] * (uint64_t)type_size(g.dtype))
+      return fail(GSKYHIP_E_ARG);
     void *od = nullptr;
-    if ((e = upload(po, n, &od))) return e;
+    if ((e = upload(po, n, &od))) return fail(e);
     g.ovr_data[k] = od;
   }
   e = gskyhip_register_granule(path.c_str(), band, &g, srs.empty() ? nullptr : srs.c_str());
-  if (!e) s->n_reg++;
-  return e;
+  if (e) return fail(e);
+  auto &slot = s->device_allocs[std::make_pair(path, band)];
+  for (void *q : slot) (void)hipFree(q);   // a granule refresh replaces the old upload
+  slot = std::move(mine);
+  s->n_reg = (int64_t)s->device_allocs.size();
+  return 0;
 }
 
-void conn_loop(Service *s, int fd) {
+void conn_serve(Service *s, int fd) {
   for (;;) {
     uint32_t op = 0;
     std::vector<char> payload;
@@ -291,9 +339,14 @@ void conn_loop(Service *s, int fd) {
       s->n_req++;
       {
         std::unique_lock<std::mutex> lk(s->mu);
-        s->queue.push_back(pd);
-        s->cv_queue.notify_one();
-        s->cv_done.wait(lk, [&] { return pd->done; });
+        if (s->stop) {   // shutting down: the batcher may be gone, answer now
+          pd->r.rc = GSKYHIP_E_SERVICE;
+          pd->done = true;
+        } else {
+          s->queue.push_back(pd);
+          s->cv_queue.notify_one();
+          s->cv_done.wait(lk, [&] { return pd->done; });
+        }
       }
       put_resp(o, pd->r);
     } else if (op == SVC_REGISTER) {
@@ -301,8 +354,7 @@ void conn_loop(Service *s, int fd) {
     } else if (op == SVC_UNREGISTER_ALL) {
       std::lock_guard<std::mutex> rl(s->reg_mu);
       gskyhip_unregister_all();
-      for (void *p : s->device_allocs) hipFree(p);
-      s->device_allocs.clear();
+      s->free_all();
       s->n_reg = 0;
       o.put<int32_t>(0);
     } else if (op == SVC_STATS) {
@@ -311,14 +363,20 @@ void conn_loop(Service *s, int fd) {
     } else if (op == SVC_SHUTDOWN) {
       o.put<int32_t>(0);
       send_msg(fd, op, o.b);
-      s->stop = true;
-      s->cv_queue.notify_all();
+      request_stop(s);
       ::shutdown(s->listen_fd, SHUT_RDWR);
       break;
     } else {
       break;
     }
     if (!send_msg(fd, op, o.b)) break;   // the worker died (SIGKILL): drop the reply
+  }
+}
+
+void conn_loop(Service *s, int fd) {
+  try {
+    conn_serve(s, fd);
+  } catch (...) {   // one bad connection must not std::terminate the daemon
   }
   ::close(fd);
   s->active--;
@@ -373,8 +431,7 @@ int gskyhip_service_run(const char *socket_path, int max_batch, int window_us) {
     s.active++;
     std::thread(conn_loop, &s, c).detach();
   }
-  s.stop = true;
-  s.cv_queue.notify_all();
+  request_stop(&s);
   batcher.join();
   {   // release connections still waiting on a batch
     std::lock_guard<std::mutex> lk(s.mu);
@@ -390,8 +447,7 @@ int gskyhip_service_run(const char *socket_path, int max_batch, int window_us) {
   {
     std::lock_guard<std::mutex> rl(s.reg_mu);
     gskyhip_unregister_all();
-    for (void *p : s.device_allocs) (void)hipFree(p);
-    s.device_allocs.clear();
+    s.free_all();
   }
   g_svc = nullptr;
   if (s.active.load() == 0) delete &s;

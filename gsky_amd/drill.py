@@ -104,6 +104,24 @@ def drill_descriptors(geometries: Sequence[str], dataset_srs: Optional[str], geo
     return win[:n], off[:n], buf, st[:n]
 
 
+def drill_windows(geometries: Sequence[str], dataset_srs: Optional[str], geot: Sequence[float], xsize: int,
+                  ysize: int) -> Tuple[np.ndarray, np.ndarray]:
+    """The windows (n, 4) and status (n,) of getDrillFileDescriptor
+    (drill.go:363-423) without rasterizing a mask (host only)."""
+    n = len(geometries)
+    arr = (C.c_char_p * max(1, n))(*[g.encode() for g in geometries])
+    gt = (C.c_double * 6)(*geot)
+    win = np.zeros((max(1, n), 4), np.int32)
+    off = np.zeros(max(1, n), np.int64)
+    st = np.zeros(max(1, n), np.int32)
+    total = C.c_int64()
+    check(lib().gskyhip_drill_descriptors_device(arr, n, dataset_srs.encode() if dataset_srs else None, gt, xsize,
+                                                 ysize, win.ctypes.data_as(C.c_void_p),
+                                                 off.ctypes.data_as(C.c_void_p), C.byref(total), None,
+                                                 st.ctypes.data_as(C.c_void_p), None), "drill_windows")
+    return win[:n], st[:n]
+
+
 def drill_dataset(geometries: Sequence[str], dataset_srs: Optional[str], geot: Sequence[float], xsize: int,
                   ysize: int, device=None, rasterize: str = "gpu") -> Tuple["MaskBatch", np.ndarray]:
     """DrillDataset's geometry step for a batch of requests: the windows and
@@ -147,25 +165,14 @@ def read_data(stack: DrillStack, win, mask_off=None, masks=None, clip_lower: flo
     drill.go:225.  `win` is a MaskBatch (or the round-1 (win, mask_off,
     masks) tensors); `bands` the reference's 1-based band list (default all);
     mode REFERENCE_ORDER is bit-exact, WAVE_SPLIT within 1e-5 relative.
-    decile_count > 0 (band_strides 1): values / counts (n_polys, rows, 1 +
-    decile_count), each row [mean, decile 1..k] as the reference's TimeSeries
-    (drill.go:172-191: Count 1 per decile, zeros with Count 0 where the band
-    total is 0); the deciles by segmented GPU sort (gskyhip_drill_deciles)."""
+    decile_count > 0: values / counts (n_polys, rows, 1 + decile_count),
+    each row [mean, decile 1..k] as the reference's TimeSeries (drill.go:
+    172-214: Count 1 per decile, zeros with Count 0 where the band total is
+    0, interpolated rows for bandStrides > 2); see read_data_deciles."""
     mb = win if isinstance(win, MaskBatch) else MaskBatch(win, mask_off, masks)
     if decile_count:
-        if band_strides > 1:
-            raise NotImplementedError("deciles with bandStrides > 1 (drill.go:197-218 interpolates mean rows)")
-        vals, cnts = read_data(stack, mb, clip_lower=clip_lower, clip_upper=clip_upper, pixel_count=pixel_count,
-                               band_strides=1, bands=bands, mode=mode)
-        dec, st = compute_deciles(stack, mb, cnts, decile_count, bands)
-        bad = st == -7
-        if bool(bad.any()):
-            from ._lib import GskyError
-            raise GskyError(-7, "computeDeciles indexes past the values (the reference panics)")
-        ok = (st == 0).unsqueeze(-1)
-        dv = torch.where(ok, dec.to(torch.float64), torch.zeros_like(dec, dtype=torch.float64))
-        dcnt = ok.to(torch.int32).expand(-1, -1, decile_count)
-        return torch.cat([vals.unsqueeze(-1), dv], -1), torch.cat([cnts.unsqueeze(-1), dcnt], -1)
+        return read_data_deciles(stack, mb, clip_lower, clip_upper, pixel_count, band_strides, decile_count, bands,
+                                 mode)
     n_polys = mb.n
     blist = None if bands is None else np.ascontiguousarray(bands, np.int32)
     n_list = stack.n_bands if blist is None else len(blist)
@@ -185,6 +192,42 @@ def read_data(stack: DrillStack, win, mask_off=None, masks=None, clip_lower: flo
     return vals, cnts
 
 
+def read_data_deciles(stack: DrillStack, mb: "MaskBatch", clip_lower: float, clip_upper: float, pixel_count: int,
+                      band_strides: int, decile_count: int, bands: Optional[Sequence[int]] = None,
+                      mode: int = REFERENCE_ORDER):
+    """readData with decileCount > 0 and any bandStrides in one call
+    (gskyhip_drill_read_data): the read bands' means, their deciles by radix
+    selection, the TimeSeries rows.  Raises GskyError(-7) where the reference's
+    computeDeciles would panic (drill.go:247-253)."""
+    n_polys = mb.n
+    blist = None if bands is None else np.ascontiguousarray(bands, np.int32)
+    n_list = stack.n_bands if blist is None else len(blist)
+    rows = lib().gskyhip_drill_rows(n_list, band_strides)
+    dev = stack.stack.device
+    nc = 1 + decile_count
+    vals = torch.empty((n_polys, rows, nc), dtype=torch.float64, device=dev)
+    cnts = torch.empty((n_polys, rows, nc), dtype=torch.int32, device=dev)
+    st = torch.empty(n_polys, dtype=torch.int32, device=dev)
+    ws_bytes = lib().gskyhip_drill_read_data_workspace_size(n_polys, mb.mask_bytes, n_list, band_strides,
+                                                            decile_count, mode)
+    if ws_bytes < 0:
+        raise ValueError("readData workspace out of range")
+    ws = torch.empty(max(1, int(ws_bytes)), dtype=torch.uint8, device=dev)
+    check(lib().gskyhip_drill_read_data(C.c_void_p(stack.stack.data_ptr()), stack.xsize, stack.ysize,
+                                        stack.n_bands, stack.t_stride, C.c_void_p(mb.win.data_ptr()),
+                                        C.c_void_p(mb.mask_off.data_ptr()), C.c_void_p(mb.masks.data_ptr()),
+                                        n_polys, mb.mask_bytes,
+                                        blist.ctypes.data_as(C.c_void_p) if blist is not None else None, n_list,
+                                        stack.nodata, clip_lower, clip_upper, pixel_count, band_strides,
+                                        decile_count, mode, C.c_void_p(vals.data_ptr()), C.c_void_p(cnts.data_ptr()),
+                                        C.c_void_p(st.data_ptr()), C.c_void_p(ws.data_ptr()), ws.numel(),
+                                        _stream()), "drill_read_data")
+    if bool((st == -7).any()):
+        from ._lib import GskyError
+        raise GskyError(-7, "computeDeciles indexes past the values (the reference panics)")
+    return vals, cnts
+
+
 def compute_deciles(stack: DrillStack, mb: "MaskBatch", totals: torch.Tensor, decile_count: int,
                     bands: Optional[Sequence[int]] = None, band_chunk: int = 0):
     """computeDeciles (drill.go:229-273) of every polygon and band:
@@ -195,8 +238,8 @@ def compute_deciles(stack: DrillStack, mb: "MaskBatch", totals: torch.Tensor, de
     blist = None if bands is None else np.ascontiguousarray(bands, np.int32)
     n_list = stack.n_bands if blist is None else len(blist)
     dev = stack.stack.device
-    if band_chunk <= 0:   # bound the sort buffers (mask_bytes x chunk values, 2 copies)
-        band_chunk = int(max(1, min(n_list, (1 << 29) // max(1, mb.mask_bytes), 2147483646 // max(1, mb.mask_bytes))))
+    if band_chunk <= 0:   # bound the segment buffer (mask_bytes x chunk values) to 4 GiB
+        band_chunk = int(max(1, min(n_list, (1 << 30) // max(1, mb.mask_bytes))))
     ws_bytes = lib().gskyhip_drill_deciles_workspace_size(n_polys, mb.mask_bytes, band_chunk)
     if ws_bytes < 0:
         raise ValueError("deciles workspace: mask_bytes x band_chunk must stay below 2^31")

@@ -8,6 +8,7 @@ seconds; scale=1 is the full benchmark size.
 """
 from __future__ import annotations
 
+import json
 import math
 import os
 from concurrent.futures import ThreadPoolExecutor
@@ -404,27 +405,41 @@ class DrillConfig:
     nodata: float
     windows: List[Tuple[int, int, int, int]]
     masks: List[np.ndarray]
+    geometries: Optional[List[str]] = None   # the polygons as WGS84 GeoJSON (C4_GT grid)
+    geot: Optional[List[float]] = None
 
 
-def config_c4(n_bands: int = 365, size: int = 2048, n_polys: int = 1000, rmin=10.0, rmax=100.0,
-              seed: int = 4) -> DrillConfig:
-    """WPS drill: n_bands daily float32 slices of size^2 + star polygons."""
+C4_GT = [130.0, 0.01, 0.0, -20.0, 0.0, -0.01]   # EPSG:4326, 0.01 deg, origin (130, -20)
+
+
+def c4_band(t: int, size: int, n_bands: int = 365) -> np.ndarray:
+    """Slice t of the C4 time stack: 0.2 + 0.1 sin(2 pi t / 365) +
+    U(0, 0.05) per (pixel, slice), nodata -9999 at 5 % of the (pixel, slice)
+    cells, float32.  One splitmix64 draw per cell: its top 53 bits give the
+    uniform, its low 16 bits the nodata test."""
+    base = np.float32(0.2 + 0.1 * math.sin(2 * math.pi * t / 365.0))
+    idx = np.arange(size * size, dtype=np.uint64) + np.uint64((SEED0 + 0x4C4) << 32) + \
+        np.uint64(t) * np.uint64(size * size)
+    u = splitmix64(idx)
+    v = (uniform01(u) * 0.05).astype(np.float32) + base
+    v[(u & np.uint64(0xFFFF)) < np.uint64(3277)] = np.float32(-9999.0)   # 3277 / 65536 = 5.0 %
+    return v.reshape(size, size)
+
+
+def pixel_polygon_geojson(poly: np.ndarray, gt: Sequence[float]) -> str:
+    """A closed GeoJSON Polygon of pixel-space vertices mapped through `gt`."""
+    lon = gt[0] + poly[:, 0] * gt[1]
+    lat = gt[3] + poly[:, 1] * gt[5]
+    ring = [[float(a), float(b)] for a, b in zip(lon, lat)]
+    ring.append(ring[0])
+    return json.dumps({"type": "Feature", "properties": {},
+                       "geometry": {"type": "Polygon", "coordinates": [ring]}})
+
+
+def c4_polygons(size: int = 2048, n_polys: int = 1000, rmin=10.0, rmax=100.0, seed: int = 4):
+    """The C4 star polygons: (test-generator windows, masks, GeoJSON on C4_GT)."""
     rng = np.random.default_rng(seed)
-    t = np.arange(n_bands, dtype=np.float64)
-    base = (0.2 + 0.1 * np.sin(2 * np.pi * t / 365.0)).astype(np.float32)
-    idx = np.arange(size * size, dtype=np.uint64) + np.uint64(SEED0 << 32)
-    noise = (uniform01(splitmix64(idx)) * 0.05).astype(np.float32).reshape(size, size)
-    fac = (1.0 + (t % 7) * 0.01).astype(np.float32)
-    nod = uniform01(splitmix64(idx + np.uint64(1 << 40))).reshape(size, size) < 0.05
-    bands = np.empty((n_bands, size, size), np.float32)
-
-    def fill(b):  # float32 throughout: base + noise * factor, nodata burnt in
-        np.multiply(noise, fac[b], out=bands[b])
-        bands[b] += base[b]
-        bands[b][nod] = -9999.0
-
-    _pmap(fill, range(n_bands))
-    wins, masks = [], []
+    wins, masks, geoms = [], [], []
     for p in range(n_polys):
         r = rng.uniform(rmin, rmax)
         cx, cy = rng.uniform(r, size - r), rng.uniform(r, size - r)
@@ -436,4 +451,22 @@ def config_c4(n_bands: int = 365, size: int = 2048, n_polys: int = 1000, rmin=10
         h = min(size, ymax + 1) - ymin
         wins.append((int(xmin), int(ymin), int(w), int(h)))
         masks.append(drill_mask(poly, xmin, ymin, w, h))
-    return DrillConfig(bands, -9999.0, wins, masks)
+        geoms.append(pixel_polygon_geojson(poly, C4_GT))
+    return wins, masks, geoms
+
+
+def config_c4(n_bands: int = 365, size: int = 2048, n_polys: int = 1000, rmin=10.0, rmax=100.0,
+              seed: int = 4) -> DrillConfig:
+    """WPS drill: n_bands daily float32 slices of size^2 (c4_band) + star
+    polygons (12 points, radius U[rmin, rmax] px, centres uniform over the
+    grid) as GeoJSON on C4_GT; windows / masks here are the test generator's
+    (point-in-polygon + sampled edges) -- the product's ALL_TOUCHED masks come
+    from drill.drill_dataset(cfg.geometries, ...)."""
+    bands = np.empty((n_bands, size, size), np.float32)
+
+    def fill(b):
+        bands[b] = c4_band(b, size, n_bands)
+
+    _pmap(fill, range(n_bands))
+    wins, masks, geoms = c4_polygons(size, n_polys, rmin, rmax, seed)
+    return DrillConfig(bands, -9999.0, wins, masks, geoms, list(C4_GT))

@@ -372,23 +372,44 @@ int gskyhip_drill_batch(const float *stack, int xsize, int ysize, int n_bands, i
                         void *workspace, int64_t workspace_bytes, void *stream);
 /* computeDeciles (worker/gdalprocess/drill.go:229-273; decileCount > 0,
  * bandStrides 1) for the same batch as gskyhip_drill_batch: per polygon and
- * selected band the in-mask, non-nodata values (no clipping) sorted
- * ascending (segmented GPU sort) and the reference's decile_count picks.
+ * selected band the in-mask, non-nodata values (no clipping) and the
+ * reference's decile_count picks of their ascending order, found by radix
+ * selection (no sort).
  *   totals: dev int32 n_polys x n_list, the out_count of the mean pass
  *     (gskyhip_drill_batch, same bands, band_strides 1): deciles only where
  *     total > 0, zeros elsewhere (drill.go:179-191);
- *   out: dev float32 n_polys x n_list x decile_count;
+ *   out: dev float32 n_polys x n_list x decile_count (decile_count <= 16);
  *   status: dev int32 n_polys x n_list -- 0, 1 (total 0: the reference's
  *     Count-0 zeros), GSKYHIP_E_RANGE (the reference indexes past the values
  *     and panics: len % (dc+1) == 0 with len == dc+1);
- *   band_chunk: bands sorted per pass (workspace scales with
- *     mask_bytes x band_chunk; mask_bytes x band_chunk < 2^31). */
+ *   band_chunk: bands per pass (workspace scales with mask_bytes x band_chunk). */
 int64_t gskyhip_drill_deciles_workspace_size(int n_polys, int64_t mask_bytes, int band_chunk);
 int gskyhip_drill_deciles(const float *stack, int xsize, int ysize, int n_bands, int t_stride,
                           const int32_t *win, const int64_t *mask_off, const uint8_t *masks, int n_polys,
                           int64_t mask_bytes, const int32_t *bands, int n_list, float nodata, int decile_count,
                           int band_chunk, const int32_t *totals, float *out, int32_t *status, void *workspace,
                           int64_t workspace_bytes, void *stream);
+
+/* readData complete (worker/gdalprocess/drill.go:90-227), one call per
+ * batch of polygons over one time stack -- what DrillDataset (drill.go:33-88)
+ * calls after getDrillFileDescriptor: readData(ds, bands, geom, bandStrides,
+ * decileCount, pixelCount, clipUpper, clipLower).  Mean / pixel-count
+ * (pixel_count), decile_count >= 0 (<= 16), band_strides >= 1 with the
+ * reference's bound-band reads and interpolated rows (every column, counts
+ * math.Round of the two bounds' mean).  Arguments as gskyhip_drill_batch;
+ * out_value (dev f64) / out_count (dev i32): n_polys x rows x (1 +
+ * decile_count) = Result.TimeSeries (Value, Count) row-major with Shape
+ * [rows, 1 + decile_count], rows = gskyhip_drill_rows(n_list, band_strides);
+ * status: dev int32 per polygon, 0 or GSKYHIP_E_RANGE where computeDeciles
+ * would panic (the reference's gsky-gdal-process dies; the request fails). */
+int64_t gskyhip_drill_read_data_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides,
+                                               int decile_count, int mode);
+int gskyhip_drill_read_data(const float *stack, int xsize, int ysize, int n_bands, int t_stride,
+                            const int32_t *win, const int64_t *mask_off, const uint8_t *masks, int n_polys,
+                            int64_t mask_bytes, const int32_t *bands, int n_list, float nodata,
+                            float clip_lower, float clip_upper, int pixel_count, int band_strides,
+                            int decile_count, int mode, double *out_value, int32_t *out_count,
+                            int32_t *status, void *workspace, int64_t workspace_bytes, void *stream);
 
 /* Round-1 form (bands 1..n_bands, mode 0): sizes and allocates its workspace
  * itself (one synchronous read-back of win / mask_off). */

@@ -405,6 +405,60 @@ def compute_deciles(values, mask, nodata, decile_count):
     return out
 
 
+def _go_round(x: float) -> float:   # math.Round: half away from zero
+    import math
+    return math.copysign(math.floor(abs(x) + 0.5), x)
+
+
+def drill_read_data_full(data, mask, nodata, clip_lower, clip_upper, pixel_count=0, band_strides=1,
+                         decile_count=0, bands=None):
+    """readData (worker/gdalprocess/drill.go:90-227) with deciles and
+    bandStrides, a pure-Python restatement over one polygon window: data
+    (n_bands, h, w) float32, bands 1-based (default all).  Per group
+    [ibBgn, ibEnd) the bound bands bands[ibBgn], bands[ibEnd-1] (one band when
+    bandStrides is 1, the same band twice for a 1-band group), their mean /
+    count (drill_read_data) and deciles (compute_deciles; zeros with Count 0
+    where the total is 0), appended as rows [mean, d1..dk]; for bandStrides > 2
+    bandStrides - 2 rows interpolated in every column in between, Count
+    math.Round((c0 + c1) / 2).  Returns (values (rows, nCols) float64,
+    counts int32), or None where computeDeciles panics."""
+    d = np.asarray(data, np.float32)
+    blist = list(bands) if bands is not None else list(range(1, d.shape[0] + 1))
+    strides = band_strides if band_strides > 0 else 1
+    nc = 1 + int(decile_count)
+    vals, cnts = [], []
+    for ib in range(0, len(blist), strides):
+        ie = min(ib + strides, len(blist))
+        read = [blist[ib], blist[ie - 1]] if strides > 1 else [blist[ib]]
+        bound = []
+        for b in read:
+            mv, mc = drill_read_data(d[b - 1:b], mask, nodata, clip_lower, clip_upper, pixel_count, 1)
+            row_v, row_c = [float(mv[0])], [int(mc[0])]
+            if decile_count > 0:
+                if mc[0] > 0:
+                    dec = compute_deciles(d[b - 1], mask, nodata, decile_count)
+                    if dec is None:
+                        return None
+                    row_v += [float(x) for x in dec]
+                    row_c += [1] * decile_count
+                else:
+                    row_v += [0.0] * decile_count
+                    row_c += [0] * decile_count
+            bound.append((row_v, row_c))
+        vals.append(bound[0][0])
+        cnts.append(bound[0][1])
+        if strides > 2 and len(bound) > 1:
+            beta = [(bound[1][0][ic] - bound[0][0][ic]) / float(strides - 1) for ic in range(nc)]
+            count = [_go_round(float(bound[0][1][ic] + bound[1][1][ic]) / 2.0) for ic in range(nc)]
+            for ip in range(1, strides - 1):
+                vals.append([bound[0][0][ic] + float(ip) * beta[ic] for ic in range(nc)])
+                cnts.append([int(count[ic]) for ic in range(nc)])
+        if len(bound) > 1:
+            vals.append(bound[1][0])
+            cnts.append(bound[1][1])
+    return np.array(vals, np.float64).reshape(-1, nc), np.array(cnts, np.int32).reshape(-1, nc)
+
+
 def band_math(expr, variables, out_nodata):
     """Band-math of RasterMerger.Run (processor/tile_merger.go:654-731) for
     one expression over one axis, a pure-Python restatement: variables =

@@ -4,8 +4,15 @@ worker/gdalprocess/drill.go:363-423 (getDrillFileDescriptor) and 275-327
 gskyhip_drill_descriptors) against the oracle's independent C restatement on
 the same GeoJSON, plus hand-derived known answers.  GDAL/GEOS are absent, so
 parity with a running reference is unpinned; these tests pin the
-product to the restatement bit for bit.  CPU only: both sides are host code."""
+product to the restatement bit for bit.  The product's rasterizer (scanline
+fill as per-edge parity toggles, drill_geom.cpp) is a different algorithm from
+the oracle's (GDAL's sorted intersection spans); they agree on every polygon
+below, including the reference's own WPS acceptance geometries
+(tests/golden/wps_polygons.json.gz: 32 local-government areas of 359-16,922
+vertices, extracted from acceptance_tests/polygon_requests/*.xml)."""
+import gzip
 import json
+import os
 
 import numpy as np
 import pytest
@@ -13,6 +20,16 @@ import pytest
 from gsky_amd import drill, synth
 
 GT4326 = [130.0, 0.01, 0.0, -20.0, 0.0, -0.01]
+WPS_DATASETS = [("EPSG:4326", [112.0, 0.01, 0.0, -9.0, 0.0, -0.01], 4300, 3500),
+                ("EPSG:4326", [112.0, 0.0025, 0.0, -9.0, 0.0, -0.0025], 17200, 14000),
+                ("EPSG:3577", [-2000000.0, 250.0, 0.0, -1000000.0, 0.0, -250.0], 16000, 16000)]
+
+
+def wps_polygons():
+    """{request file: GeoJSON geometry} of the reference's WPS acceptance requests."""
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "wps_polygons.json.gz")
+    with gzip.open(p, "rt", encoding="utf-8") as f:
+        return json.load(f)
 
 
 def feature(rings, multi=False):
@@ -105,6 +122,32 @@ def test_descriptor_multipolygon_with_hole(oracle):
         assert m[25, 25] == 0 and m[5, 5] == 255      # the hole is not burnt, the ring is
 
 
+@pytest.mark.parametrize("ds", range(len(WPS_DATASETS)))
+def test_wps_acceptance_polygons_match_oracle(oracle, ds):
+    """The reference's 32 WPS polygons (+ its sample polygon payload; the
+    point payload is not a polygon and is refused): windows and ALL_TOUCHED
+    masks equal the oracle's, on a 0.01 and a 0.0025 degree EPSG:4326 grid
+    and a 250 m Albers grid over Australia."""
+    srs, gt, xs, ys = WPS_DATASETS[ds]
+    polys = wps_polygons()
+    names = sorted(polys)
+    geoms = [polys[k] for k in names]
+    win, off, buf, st = drill.drill_descriptors(geoms, srs, gt, xs, ys)
+    n_ok = 0
+    for i, g in enumerate(geoms):
+        try:
+            ew, em = oracle.drill_descriptor(g, srs, gt, xs, ys)
+        except ValueError:
+            assert st[i] != 0, names[i]
+            continue
+        assert st[i] == 0 and tuple(win[i]) == ew, (names[i], win[i], ew)
+        m = buf[off[i]:off[i] + ew[2] * ew[3]].reshape(ew[3], ew[2])
+        assert np.array_equal(m, em), names[i]
+        n_ok += 1
+    assert n_ok >= 32
+    assert st[names.index("point_drill.payload")] != 0
+
+
 def test_descriptor_bad_geometry():
     win, off, buf, st = drill.drill_descriptors(['{"type": "Point", "coordinates": [1, 2]}', "nonsense"],
                                                 "EPSG:4326", GT4326, 2048, 2048)
@@ -118,8 +161,7 @@ def test_descriptor_masks_on_gpu(oracle, srs, seed):
     one workgroup per polygon, edges then scanlines) are the host rasterizer's
     masks byte for byte, and the oracle's; the windows / offsets / status are
     the host call's.  Includes polygons crossing the file edge, a multipolygon
-    with a hole and one polygon with more vertices than a GPU thread keeps
-    intersections for (host fallback)."""
+    with a hole and a 90-vertex ring."""
     import torch
     if srs == "EPSG:4326":
         gt, size = GT4326, 2048
@@ -153,3 +195,34 @@ def test_descriptor_masks_on_gpu(oracle, srs, seed):
         assert np.array_equal(gm[off[i]:off[i] + ew[2] * ew[3]].reshape(ew[3], ew[2]), em), i
         n_ok += 1
     assert n_ok > len(geoms) // 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ds", range(len(WPS_DATASETS)))
+def test_wps_acceptance_polygons_on_gpu(oracle, ds):
+    """The reference's WPS polygons (up to 16,922 vertices) rasterized on the
+    GPU -- no vertex or intersection bound, no host fallback -- equal the
+    host call's and the oracle's windows and masks byte for byte, issued on a
+    non-default stream."""
+    import torch
+    srs, gt, xs, ys = WPS_DATASETS[ds]
+    polys = wps_polygons()
+    names = sorted(polys)
+    geoms = [polys[k] for k in names]
+    win, off, buf, st = drill.drill_descriptors(geoms, srs, gt, xs, ys)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        mb, st2 = drill.drill_dataset(geoms, srs, gt, xs, ys, device="cuda", rasterize="gpu")
+        gm = mb.masks.cpu().numpy()
+    torch.cuda.synchronize()
+    assert np.array_equal(st, st2)
+    assert np.array_equal(mb.win.cpu().numpy(), win) and np.array_equal(mb.mask_off.cpu().numpy(), off)
+    assert gm.size == buf.size and np.array_equal(gm, buf)
+    n_ok = 0
+    for i, g in enumerate(geoms):
+        if st[i] != 0:
+            continue
+        ew, em = oracle.drill_descriptor(g, srs, gt, xs, ys)
+        assert np.array_equal(gm[off[i]:off[i] + ew[2] * ew[3]].reshape(ew[3], ew[2]), em), names[i]
+        n_ok += 1
+    assert n_ok >= 32

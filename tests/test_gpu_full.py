@@ -6,8 +6,11 @@ Bars (north_star):
       100 % of RGBA pixels identical -- no pixel is excepted;
   C3 (bilinear, typed float canvas): identical nodata mask and EVERY valid
       pixel within 1e-4 relative;
-  C4 (drill, reference-order mode): counts identical and means bit-exact for
-      all 1000 polygons x 365 slices.
+  C4 (drill through the product: GeoJSON polygons -> windows + ALL_TOUCHED
+      masks rasterized on the GPU -> readData): windows and masks identical to
+      the oracle's, counts identical and means bit-exact for all 1000
+      polygons x 365 slices (reference order), deciles of a 100-polygon sample
+      equal as float32.
 Comparisons of the big outputs run on the GPU (the oracle's arrays are
 uploaded), so a 4.3 GB RGBA batch compares in well under a second.
 """
@@ -118,20 +121,40 @@ def _drill_oracle(oracle, dc, clip, pc, strides):
 
 
 @pytest.fixture(scope="module")
-def c4():
-    return synth.config_c4()
+def c4(gpu, oracle):
+    """The C4 stack and polygons, the product's windows / masks for the GeoJSON
+    polygons (GPU rasterizer), checked against the oracle's descriptors; the
+    config's windows / masks are replaced by the product's."""
+    from gsky_amd import drill
+    dc = synth.config_c4()
+    size = dc.bands.shape[1]
+    mb, st = drill.drill_dataset(dc.geometries, "EPSG:4326", dc.geot, size, size, device=gpu)
+    assert (st == 0).all()
+    win, off, buf = mb.win.cpu().numpy(), mb.mask_off.cpu().numpy(), mb.masks.cpu().numpy()
+
+    def one(p):
+        ew, em = oracle.drill_descriptor(dc.geometries[p], "EPSG:4326", dc.geot, size, size)
+        w, h = int(win[p][2]), int(win[p][3])
+        return tuple(win[p]) == ew and np.array_equal(buf[off[p]:off[p] + w * h].reshape(h, w), em)
+    with ThreadPoolExecutor(THREADS) as ex:
+        same = list(ex.map(one, range(len(dc.geometries))))
+    assert all(same), "product windows / masks differ from the oracle for %d polygons" % same.count(False)
+    dc.windows = [tuple(int(v) for v in w) for w in win]
+    dc.masks = [buf[off[p]:off[p] + w * h].reshape(h, w) for p, (_, _, w, h) in enumerate(dc.windows)]
+    dc.mb = mb
+    return dc
 
 
 def test_c4_full_drill_bit_exact(gpu, oracle, c4):
     """C4: 1000 polygons x 365 daily float32 slices, mean mode, clip
-    +-MaxFloat32 (ows.go:1373-1381), reference summation order."""
+    +-MaxFloat32 (ows.go:1373-1381), reference summation order, over the
+    product's masks."""
     import torch
 
     from gsky_amd import drill
     clip = (-3.4028234663852886e38, 3.4028234663852886e38)
     st = drill.DrillStack(torch.from_numpy(c4.bands), c4.nodata, gpu)
-    win, off, masks = drill.pack_masks(c4.windows, c4.masks, gpu)
-    vals, cnts = drill.read_data(st, win, off, masks, clip[0], clip[1], 0, 1)
+    vals, cnts = drill.read_data(st, c4.mb, clip[0], clip[1], 0, 1)
     vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
     del st
     exp = _drill_oracle(oracle, c4, clip, 0, 1)
@@ -141,6 +164,48 @@ def test_c4_full_drill_bit_exact(gpu, oracle, c4):
     assert sum(int(ec.sum()) for _, ec in exp) > 1e8
 
 
+def test_c4_full_deciles_sample(gpu, oracle, c4):
+    """readData with decileCount 9 over all 1000 polygons x 365 slices on the
+    GPU (radix selection); 100 polygons checked against numpy's sort of the
+    same in-mask, non-nodata values (the oracle's computeDeciles picks)."""
+    import torch
+
+    from gsky_amd import drill
+    clip = (-3.4028234663852886e38, 3.4028234663852886e38)
+    st = drill.DrillStack(torch.from_numpy(c4.bands), c4.nodata, gpu)
+    vals, cnts = drill.read_data(st, c4.mb, clip[0], clip[1], decile_count=9)
+    vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
+    del st
+    nd = np.float32(c4.nodata)
+
+    def one(p):
+        x0, y0, w, h = c4.windows[p]
+        sub = c4.bands[:, y0:y0 + h, x0:x0 + w].reshape(c4.bands.shape[0], -1)
+        m = c4.masks[p].reshape(-1) == 255
+        for b in range(c4.bands.shape[0]):
+            v = sub[b][m]
+            v = np.sort(v[v != nd])
+            if cnts[p, b, 0] == 0:
+                if vals[p, b, 1:].any():
+                    return False
+                continue
+            step = len(v) // 10
+            exp = np.zeros(9, np.float32)
+            if step > 0:
+                even = len(v) % 10 == 0
+                for i in range(9):
+                    j = (i + 1) * step
+                    exp[i] = np.float32((v[j] + v[j + 1]) / np.float32(2.0)) if even else v[j]
+            else:
+                exp = oracle.compute_deciles(sub[b], m.astype(np.uint8) * 255, c4.nodata, 9)
+            if not np.array_equal(vals[p, b, 1:].astype(np.float32), exp):
+                return False
+        return True
+    with ThreadPoolExecutor(THREADS) as ex:
+        ok = list(ex.map(one, range(0, len(c4.windows), 10)))
+    assert all(ok), "deciles differ for %d of %d sampled polygons" % (ok.count(False), len(ok))
+
+
 def test_c4_full_drill_wave_split(gpu, oracle, c4):
     """C4 in the wave-split mode: counts exact, means within 1e-5 relative."""
     import torch
@@ -148,8 +213,7 @@ def test_c4_full_drill_wave_split(gpu, oracle, c4):
     from gsky_amd import drill
     clip = (-3.4028234663852886e38, 3.4028234663852886e38)
     st = drill.DrillStack(torch.from_numpy(c4.bands), c4.nodata, gpu)
-    mb = drill.pack_masks(c4.windows, c4.masks, gpu)
-    vals, cnts = drill.read_data(st, mb, clip[0], clip[1], mode=drill.WAVE_SPLIT)
+    vals, cnts = drill.read_data(st, c4.mb, clip[0], clip[1], mode=drill.WAVE_SPLIT)
     vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
     del st
     exp = _drill_oracle(oracle, c4, clip, 0, 1)

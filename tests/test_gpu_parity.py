@@ -430,7 +430,7 @@ def test_drill_parity(gpu, oracle, strides, pc, clip):
 
 @pytest.mark.parametrize("dcount,pc,clip", [(9, 0, (-1e30, 1e30)), (4, 0, (0.21, 0.24)), (3, 1, (-1e30, 1e30))])
 def test_drill_deciles_parity(gpu, oracle, dcount, pc, clip):
-    """computeDeciles (drill.go:229-273) by segmented GPU sort: every decile
+    """computeDeciles (drill.go:229-273) by radix selection: every decile
     of every (polygon, band) equal to the oracle's float32 value, the
     [mean, deciles] rows and their Counts as the reference's TimeSeries, small
     polygons exercising the padding branch; a band list and a small band chunk
@@ -468,6 +468,34 @@ def test_drill_deciles_parity(gpu, oracle, dcount, pc, clip):
     dec, stt = drill.compute_deciles(st, mb, mc, dcount, bands, band_chunk=2)
     assert np.array_equal(dec.cpu().numpy()[stt.cpu().numpy() == 0],
                           vals[..., 1:].astype(np.float32)[stt.cpu().numpy() == 0])
+
+
+@pytest.mark.parametrize("strides,dcount,pc,nb", [(2, 9, 0, 23), (3, 9, 0, 23), (3, 4, 1, 22), (5, 9, 0, 21),
+                                                  (1, 9, 0, 23)])
+def test_drill_deciles_strides_parity(gpu, oracle, strides, dcount, pc, nb):
+    """readData with decileCount and bandStrides together (drill.go:128-219,
+    gskyhip_drill_read_data): bound bands read, deciles of both bounds,
+    every column interpolated for bandStrides > 2 with Counts math.Round of
+    the bounds' mean, the 1-band last group read twice -- values bit-exact
+    and Counts equal to the oracle's restatement, for every polygon."""
+    import torch
+
+    from gsky_amd import drill
+    dc = synth.config_c4(n_bands=nb, size=200, n_polys=14, rmin=1, rmax=30)
+    dc.windows = list(dc.windows) + [(10, 12, 2, 1)]            # 2 values: the padding branch
+    dc.masks = list(dc.masks) + [np.full((1, 2), 255, np.uint8)]
+    st = drill.DrillStack(torch.from_numpy(dc.bands), dc.nodata, gpu)
+    mb = drill.pack_masks(dc.windows, dc.masks, gpu)
+    clip = (0.21, 0.26) if pc else (-3.4e38, 3.4e38)
+    vals, cnts = drill.read_data(st, mb, clip_lower=clip[0], clip_upper=clip[1], pixel_count=pc,
+                                 band_strides=strides, decile_count=dcount)
+    vals, cnts = vals.cpu().numpy(), cnts.cpu().numpy()
+    for p, (x0, y0, w, h) in enumerate(dc.windows):
+        ev, ec = oracle.drill_read_data_full(dc.bands[:, y0:y0 + h, x0:x0 + w], dc.masks[p], dc.nodata, clip[0],
+                                             clip[1], pc, strides, dcount)
+        assert vals[p].shape == ev.shape, (p, vals[p].shape, ev.shape)
+        assert np.array_equal(cnts[p], ec), p
+        assert np.array_equal(vals[p].view(np.uint64), ev.view(np.uint64)), p
 
 
 def test_drill_deciles_reference_panic(gpu, oracle):

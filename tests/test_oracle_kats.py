@@ -279,3 +279,21 @@ def test_band_math_kats(oracle):
     assert oracle.band_math("!(nir == 2) && red < 3", vs, -1.0).tolist() == [1.0, 0.0, 1.0, -1.0, -1.0]
     with pytest.raises(ValueError):
         oracle.band_math("nir + swir", vs, -1.0)
+
+
+def test_read_data_full_means_match_c_oracle(oracle):
+    """The pure-Python readData restatement with bandStrides (drill.go:128-219)
+    gives the C oracle's mean / count rows bit for bit, including the
+    reference's extra rows for a short last group (10 bands, stride 3 -> 12
+    rows)."""
+    rng = np.random.default_rng(3)
+    d = (rng.random((10, 7, 9)) * 0.3).astype(np.float32)
+    d[rng.random(d.shape) < 0.1] = -9999.0
+    m = np.where(rng.random((7, 9)) < 0.7, 255, 0).astype(np.uint8)
+    for strides in (1, 2, 3, 4, 11):
+        for pc, lo, hi in ((0, -1e30, 1e30), (1, 0.05, 0.2)):
+            v, c = oracle.drill_read_data_full(d, m, -9999.0, lo, hi, pc, strides, 0)
+            ev, ec = oracle.drill_read_data(d, m, -9999.0, lo, hi, pc, strides)
+            assert np.array_equal(v[:, 0].view(np.uint64), ev.view(np.uint64)) and np.array_equal(c[:, 0], ec)
+    v, _ = oracle.drill_read_data_full(d, m, -9999.0, -1e30, 1e30, 0, 3, 0)
+    assert v.shape[0] == 12

@@ -72,6 +72,63 @@ def test_service_protocol_and_batching_queue():
     assert not os.path.exists(sock)
 
 
+def _spin_unknown(sock):
+    os.environ["GSKYHIP_SERVICE"] = sock
+    from gsky_amd import worker as W
+    while True:
+        W.warp_raster(W.GeoRPCGranule(path="/nope.tif", bands=[1], width=8, height=8, dstSRS="EPSG:3857",
+                                      dstGeot=[0.0, 1.0, 0.0, 0.0, 0.0, -1.0]))
+
+
+def test_service_bad_headers_do_not_kill_the_daemon():
+    """A header announcing a payload far above what its op may carry (a stats
+    request of 1 TiB, a warp request of 64 GiB) or an unknown op closes that
+    connection only: no allocation, no std::terminate, the daemon keeps
+    answering."""
+    import struct
+
+    from gsky_amd import WarpService
+    sock = _sock_path()
+    svc = WarpService(sock, max_batch=4, window_us=100)
+    try:
+        for op, n in ((4, 1 << 40), (1, 1 << 36), (2, 1 << 50), (99, 8)):
+            c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+            c.connect(sock)
+            c.sendall(struct.pack("<IIQ", 0x594B5347, op, n) + (b"\0" * n if n <= 64 else b""))
+            c.settimeout(10)
+            assert c.recv(16) == b""   # the daemon hung up
+            c.close()
+        assert svc.proc.poll() is None
+        assert svc.stats()["requests"] == 0
+    finally:
+        assert svc.shutdown() == 0
+
+
+def test_service_shutdown_under_load():
+    """Shutdown while workers keep sending warps: the daemon stops within a
+    few seconds (no request is queued behind a stopped batcher), and workers
+    then see the service as unreachable."""
+    from gsky_amd import WarpService
+    sock = _sock_path()
+    svc = WarpService(sock, max_batch=8, window_us=500)
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_spin_unknown, args=(sock,)) for _ in range(4)]
+    try:
+        for p in procs:
+            p.start()
+        t0 = time.time()
+        while svc.stats()["requests"] < 20 and time.time() - t0 < 120:
+            time.sleep(0.2)
+        assert svc.stats()["requests"] >= 20
+        t0 = time.time()
+        assert svc.shutdown(timeout=30.0) == 0
+        assert time.time() - t0 < 15.0
+    finally:
+        for p in procs:
+            p.kill()
+            p.join(30)
+
+
 def test_service_unreachable():
     """No daemon behind GSKYHIP_SERVICE: the drop-in reports the failure (the
     OWS retries an errored request, process.go:147-150)."""
