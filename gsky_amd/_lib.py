@@ -89,6 +89,8 @@ EXPORTS = [
     "gskyhip_service_stats", "gskyhip_service_shutdown", "gskyhip_drill_deciles_workspace_size",
     "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device",
     "gskyhip_drill_read_data_workspace_size", "gskyhip_drill_read_data",
+    "gskyhip_png_workspace_size", "gskyhip_png_bound", "gskyhip_encode_png",
+    "gskyhip_geotiff_workspace_size", "gskyhip_geotiff_bound", "gskyhip_encode_geotiff",
 ]
 
 _lib = None
@@ -157,6 +159,17 @@ def lib() -> C.CDLL:
     L.gskyhip_drill_read_data_workspace_size.restype = i64
     L.gskyhip_drill_read_data.argtypes = [vp, ci, ci, ci, ci, vp, vp, vp, ci, i64, vp, ci, C.c_float, C.c_float,
                                           C.c_float, ci, ci, ci, ci, vp, vp, vp, vp, i64, vp]
+    L.gskyhip_png_workspace_size.argtypes = [ci, ci, ci]
+    L.gskyhip_png_workspace_size.restype = i64
+    L.gskyhip_png_bound.argtypes = [ci, ci]
+    L.gskyhip_png_bound.restype = i64
+    L.gskyhip_encode_png.argtypes = [vp, ci, ci, ci, i64, i64, vp, vp, i64, vp, i64, vp, ci, vp]
+    L.gskyhip_geotiff_workspace_size.argtypes = [ci, ci, ci, ci, ci, ci]
+    L.gskyhip_geotiff_workspace_size.restype = i64
+    L.gskyhip_geotiff_bound.argtypes = [ci, ci, ci, ci, ci, ci]
+    L.gskyhip_geotiff_bound.restype = i64
+    L.gskyhip_encode_geotiff.argtypes = [C.POINTER(vp), ci, ci, ci, ci, C.POINTER(d), ci, vp,
+                                         C.POINTER(C.c_char_p), ci, ci, vp, i64, vp, i64, C.POINTER(i64), vp]
     L.gskyhip_fnv32a.argtypes = [C.c_char_p, i64]
     L.gskyhip_fnv32a.restype = C.c_uint32
     L.gskyhip_version.restype = C.c_char_p

@@ -1,0 +1,551 @@
+// encode.hip -- output codecs: EncodePNG's png.Encode (utils/ogc_encoders.go:
+// 139; Go 1.12 image/png) for batches of RGBA tiles in HBM.
+//
+// Go's encoder on the *image.RGBA canvas of EncodePNG (ogc_encoders.go:82):
+//   * colour type: truecolour RGB (cbTC8) when every alpha is 0xff
+//     (image.RGBA.Opaque), else RGBA (cbTCA8) whose bytes are the
+//     color.NRGBAModel conversion of each premultiplied pixel (a = 0 ->
+//     0,0,0,0; a = 0xffff -> the bytes; else r * 0xffff / a in 16 bits, high
+//     byte, wrapping like Go's uint8()) -- image.RGBA stores the palette
+//     colours as they are, so a palette entry with r > a wraps;
+//   * per row the filter of writer.go filter(): the sums of |int8(byte)| of the
+//     Up, Paeth, None, Sub and Average residuals, tried in that order, the
+//     first strictly smaller sum wins (the early exits there never change the
+//     choice); the previous row of the first row is zero;
+//   * zlib at DefaultCompression (level 6) over the filtered rows, written
+//     through a 32 KiB bufio.Writer: IDAT chunks of exactly 32768 bytes, the
+//     last one shorter; IHDR / IDAT / IEND with their CRC-32.
+// Here the colour-type test, the NRGBA conversion and the filter selection run
+// on the GPU (one workgroup per row), the deflate of each tile on host threads
+// (zlib 1.2.11, level 6, 32 KiB window, default strategy).  The filtered rows
+// -- every byte zlib receives -- are Go's exactly; the compressed bytes are
+// zlib's, not Go's compress/flate (both DEFLATE: the decoded image and the
+// filter bytes are identical, byte identity with Go is parity unpinned).
+#include <hip/hip_runtime.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/gskyhip.h"
+
+namespace gsky {
+namespace {
+
+// ------------------------------------------------------------------ GPU pass
+// tile t opaque (image.RGBA.Opaque over its w x h rectangle)?
+__global__ __launch_bounds__(256) void png_opaque_kernel(const uint8_t *__restrict__ rgba, int64_t tile_stride,
+                                                         int64_t row_stride, const int32_t *__restrict__ wh,
+                                                         int32_t *__restrict__ opaque) {
+  const int t = blockIdx.x;
+  const int w = wh[2 * t], h = wh[2 * t + 1];
+  const uint8_t *base = rgba + (int64_t)t * tile_stride;
+  int bad = 0;
+  for (int64_t i = threadIdx.x; i < (int64_t)w * h; i += blockDim.x) {
+    const int y = (int)(i / w), x = (int)(i % w);
+    bad |= base[(int64_t)y * row_stride + 4 * x + 3] != 0xFF;
+  }
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) opaque[t] = bad ? 0 : 1;
+}
+
+// byte k of row y of the image data Go's writeImage feeds the filter: RGB of
+// an opaque canvas, else NRGBA; the row above row 0 is zero
+__device__ __forceinline__ uint32_t png_byte(const uint8_t *__restrict__ tile, int64_t row_stride, int y, int k,
+                                             bool opq) {
+  if (y < 0 || k < 0) return 0u;
+  const int bpp = opq ? 3 : 4;
+  const int x = k / bpp, c = k - x * bpp;
+  const uint8_t *px = tile + (int64_t)y * row_stride + 4 * x;
+  if (opq) return px[c];
+  const uint32_t a = px[3];
+  if (a == 0xFF) return px[c];
+  if (a == 0) return 0u;
+  if (c == 3) return a;
+  const uint32_t a16 = a | (a << 8);
+  const uint32_t v16 = (uint32_t)px[c] | ((uint32_t)px[c] << 8);
+  return ((v16 * 0xFFFFu) / a16 >> 8) & 0xFFu;   // color.nrgbaModel, uint8() truncation
+}
+
+__device__ __forceinline__ uint32_t abs8(uint32_t d) { d &= 0xFFu; return d < 128u ? d : 256u - d; }
+
+__device__ __forceinline__ uint32_t paeth(uint32_t a, uint32_t b, uint32_t c) {   // writer.go paeth()
+  const int pc0 = (int)c;
+  int pa = (int)b - pc0;
+  int pb = (int)a - pc0;
+  int pc = abs(pa + pb);
+  pa = abs(pa);
+  pb = abs(pb);
+  if (pa <= pb && pa <= pc) return a;
+  if (pb <= pc) return b;
+  return c;
+}
+
+// One workgroup per (tile, row): out row = [filter byte][filtered bytes].
+__global__ __launch_bounds__(256) void png_filter_kernel(const uint8_t *__restrict__ rgba, int64_t tile_stride,
+                                                         int64_t row_stride, const int32_t *__restrict__ wh,
+                                                         const int32_t *__restrict__ opaque, int max_h,
+                                                         const int64_t *__restrict__ out_off,
+                                                         uint8_t *__restrict__ out) {
+  const int t = blockIdx.x / max_h, y = blockIdx.x % max_h;
+  const int w = wh[2 * t], h = wh[2 * t + 1];
+  if (y >= h) return;
+  const bool opq = opaque[t] != 0;
+  const int bpp = opq ? 3 : 4;
+  const int n = bpp * w;
+  const uint8_t *tile = rgba + (int64_t)t * tile_stride;
+  __shared__ uint32_t s_sum[5][4];
+  uint32_t sum[5] = {0, 0, 0, 0, 0};
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const uint32_t cur = png_byte(tile, row_stride, y, k, opq), up = png_byte(tile, row_stride, y - 1, k, opq);
+    const uint32_t left = k >= bpp ? png_byte(tile, row_stride, y, k - bpp, opq) : 0u;
+    const uint32_t ul = k >= bpp ? png_byte(tile, row_stride, y - 1, k - bpp, opq) : 0u;
+    sum[0] += abs8(cur - up);                                        // Up
+    sum[1] += abs8(k >= bpp ? cur - paeth(left, up, ul) : cur - up);   // Paeth (first bpp bytes: Up)
+    sum[2] += abs8(cur);                                             // None
+    sum[3] += abs8(cur - left);                                      // Sub
+    sum[4] += abs8(k >= bpp ? cur - ((left + up) >> 1) : cur - (up >> 1));   // Average
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int f = 0; f < 5; f++) {
+    uint32_t s = sum[f];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) s_sum[f][wv] = s;
+  }
+  __syncthreads();
+  // tried in the order Up, Paeth, None, Sub, Average; a strictly smaller sum wins
+  const int order[5] = {2, 4, 0, 1, 3};   // their PNG filter types
+  uint32_t best = 0;
+  int ft = 2;
+#pragma unroll
+  for (int f = 0; f < 5; f++) {
+    const uint32_t s = s_sum[f][0] + s_sum[f][1] + s_sum[f][2] + s_sum[f][3];
+    if (f == 0 || s < best) { best = s; ft = order[f]; }
+  }
+  uint8_t *row = out + out_off[t] + (int64_t)y * (1 + n);
+  if (threadIdx.x == 0) row[0] = (uint8_t)ft;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const uint32_t cur = png_byte(tile, row_stride, y, k, opq), up = png_byte(tile, row_stride, y - 1, k, opq);
+    const uint32_t left = k >= bpp ? png_byte(tile, row_stride, y, k - bpp, opq) : 0u;
+    const uint32_t ul = k >= bpp ? png_byte(tile, row_stride, y - 1, k - bpp, opq) : 0u;
+    uint32_t v;
+    switch (ft) {
+      case 0: v = cur; break;
+      case 1: v = cur - left; break;
+      case 2: v = cur - up; break;
+      case 3: v = k >= bpp ? cur - ((left + up) >> 1) : cur - (up >> 1); break;
+      default: v = k >= bpp ? cur - paeth(left, up, ul) : cur - up; break;
+    }
+    row[1 + k] = (uint8_t)v;
+  }
+}
+
+// ------------------------------------------------------------------ GeoTIFF
+// PackBits (TIFF 6.0 section 9) of one tile row (libtiff encodes tiled
+// PackBits row by row): runs of 3+ equal bytes as replicate runs, the rest
+// as literal runs, at most 128 bytes each.  Returns the encoded length.
+__device__ int packbits_row(const uint8_t *in, int n, uint8_t *out) {
+  int i = 0, o = 0;
+  while (i < n) {
+    int run = 1;
+    while (i + run < n && run < 128 && in[i + run] == in[i]) run++;
+    if (run >= 3) {
+      out[o++] = (uint8_t)(257 - run);   // -(run - 1)
+      out[o++] = in[i];
+      i += run;
+      continue;
+    }
+    // literal: up to the next run of 3 (or 128 bytes)
+    int j = i, lit = 0;
+    while (j < n && lit < 128) {
+      if (j + 2 < n && in[j] == in[j + 1] && in[j] == in[j + 2]) break;
+      j++;
+      lit++;
+    }
+    out[o++] = (uint8_t)(lit - 1);
+    for (int k = 0; k < lit; k++) out[o++] = in[i + k];
+    i += lit;
+  }
+  return o;
+}
+
+// One thread per (band, tile, row of the tile): the row's samples (edge
+// tiles padded with `pad`) PackBits-encoded into its slot.
+__global__ __launch_bounds__(256) void tiff_rows_kernel(const uint8_t *const *__restrict__ bands, int ts, int width,
+                                                        int height, int bx, int by, int ntx, int nty,
+                                                        const uint8_t *__restrict__ pad, int64_t slot,
+                                                        uint8_t *__restrict__ raw, uint8_t *__restrict__ enc,
+                                                        int32_t *__restrict__ len, int64_t n_rows) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const int row = (int)(r % by);
+  const int64_t tb = r / by;
+  const int tile = (int)(tb % ((int64_t)ntx * nty));
+  const int b = (int)(tb / ((int64_t)ntx * nty));
+  const int tx = tile % ntx, ty = tile / ntx;
+  const int y = ty * by + row;
+  const int rb = bx * ts;
+  uint8_t *line = raw + r * (int64_t)rb;
+  const uint8_t *src = bands[b];
+  for (int x = 0; x < bx; x++) {
+    const int gx = tx * bx + x;
+    const bool in = gx < width && y < height;
+    for (int k = 0; k < ts; k++) line[x * ts + k] = in ? src[((int64_t)y * width + gx) * ts + k] : pad[b * 8 + k];
+  }
+  len[r] = packbits_row(line, rb, enc + r * slot);
+}
+
+// ------------------------------------------------------------------ host framing
+void put32(std::vector<uint8_t> &o, uint32_t v) {
+  o.push_back((uint8_t)(v >> 24)); o.push_back((uint8_t)(v >> 16));
+  o.push_back((uint8_t)(v >> 8)); o.push_back((uint8_t)v);
+}
+
+void chunk(std::vector<uint8_t> &o, const char *type, const uint8_t *data, size_t n) {
+  put32(o, (uint32_t)n);
+  const size_t at = o.size();
+  o.insert(o.end(), type, type + 4);
+  if (n) o.insert(o.end(), data, data + n);
+  put32(o, (uint32_t)crc32(0L, o.data() + at, (uInt)(n + 4)));
+}
+
+// One tile: PNG signature, IHDR, the zlib stream in 32 KiB IDAT chunks, IEND.
+int png_tile(const uint8_t *filtered, size_t n_filtered, int w, int h, bool opq, std::vector<uint8_t> &o) {
+  static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+  o.assign(sig, sig + 8);
+  uint8_t ihdr[13];
+  const uint32_t ww = (uint32_t)w, hh = (uint32_t)h;
+  ihdr[0] = ww >> 24; ihdr[1] = ww >> 16; ihdr[2] = ww >> 8; ihdr[3] = ww;
+  ihdr[4] = hh >> 24; ihdr[5] = hh >> 16; ihdr[6] = hh >> 8; ihdr[7] = hh;
+  ihdr[8] = 8;                 // bit depth
+  ihdr[9] = opq ? 2 : 6;       // truecolour / truecolour + alpha
+  ihdr[10] = 0; ihdr[11] = 0; ihdr[12] = 0;
+  chunk(o, "IHDR", ihdr, 13);
+  std::vector<uint8_t> z(compressBound((uLong)n_filtered) + 64);
+  z_stream s;
+  std::memset(&s, 0, sizeof(s));
+  if (deflateInit2(&s, 6, Z_DEFLATED, 15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return GSKYHIP_E_ARG;
+  s.next_in = (Bytef *)filtered;
+  s.avail_in = (uInt)n_filtered;
+  s.next_out = z.data();
+  s.avail_out = (uInt)z.size();
+  const int rc = deflate(&s, Z_FINISH);
+  const size_t zn = z.size() - s.avail_out;
+  deflateEnd(&s);
+  if (rc != Z_STREAM_END) return GSKYHIP_E_ARG;
+  for (size_t p = 0; p < zn; p += 32768) chunk(o, "IDAT", z.data() + p, std::min<size_t>(32768, zn - p));
+  chunk(o, "IEND", nullptr, 0);
+  return 0;
+}
+
+// BigTIFF writer state: IFD entries (sorted by tag on output) + out-of-line data.
+struct TiffEntry {
+  uint16_t tag, type;
+  uint64_t count;
+  std::vector<uint8_t> data;   // little-endian values
+};
+
+template <typename T> void put_le(std::vector<uint8_t> &o, T v) {
+  for (size_t k = 0; k < sizeof(T); k++) o.push_back((uint8_t)((uint64_t)v >> (8 * k)));
+}
+
+TiffEntry tiff_shorts(uint16_t tag, const std::vector<uint16_t> &v) {
+  TiffEntry e{tag, 3, v.size(), {}};
+  for (uint16_t x : v) put_le(e.data, x);
+  return e;
+}
+TiffEntry tiff_long(uint16_t tag, uint32_t v) {
+  TiffEntry e{tag, 4, 1, {}};
+  put_le(e.data, v);
+  return e;
+}
+TiffEntry tiff_long8s(uint16_t tag, const std::vector<uint64_t> &v) {
+  TiffEntry e{tag, 16, v.size(), {}};
+  for (uint64_t x : v) put_le(e.data, x);
+  return e;
+}
+TiffEntry tiff_doubles(uint16_t tag, const std::vector<double> &v) {
+  TiffEntry e{tag, 12, v.size(), {}};
+  for (double x : v) {
+    uint64_t u;
+    std::memcpy(&u, &x, 8);
+    put_le(e.data, u);
+  }
+  return e;
+}
+TiffEntry tiff_ascii(uint16_t tag, const std::string &s) {
+  TiffEntry e{tag, 2, s.size() + 1, {}};
+  e.data.assign(s.begin(), s.end());
+  e.data.push_back(0);
+  return e;
+}
+
+bool epsg_geographic(int epsg) {
+  return epsg == 4326 || epsg == 4283 || epsg == 4269 || epsg == 4258 || epsg == 4167 || epsg == 4674 ||
+         epsg == 7844;
+}
+
+std::string xml_escape(const char *s) {
+  std::string o;
+  for (; s && *s; s++) {
+    switch (*s) {
+      case '&': o += "&amp;"; break;
+      case '<': o += "&lt;"; break;
+      case '>': o += "&gt;"; break;
+      case '"': o += "&quot;"; break;
+      default: o += *s;
+    }
+  }
+  return o;
+}
+
+}  // namespace
+}  // namespace gsky
+
+using namespace gsky;
+
+extern "C" {
+
+int64_t gskyhip_png_workspace_size(int n_tiles, int max_w, int max_h) {
+  if (n_tiles <= 0 || max_w <= 0 || max_h <= 0) return 0;
+  const int64_t per = (int64_t)max_h * (1 + 4 * (int64_t)max_w);
+  return ((int64_t)n_tiles * per + 255) / 256 * 256 + (int64_t)n_tiles * (8 + 8 + 4) + 1024;
+}
+
+int64_t gskyhip_png_bound(int width, int height) {
+  if (width <= 0 || height <= 0) return 0;
+  const uLong raw = (uLong)height * (1 + 4 * (uLong)width);
+  const uLong z = compressBound(raw) + 64;
+  return 8 + 25 + (int64_t)(z / 32768 + 1) * 12 + (int64_t)z + 12;
+}
+
+int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, int64_t tile_stride,
+                       int64_t row_stride, const int32_t *sizes, void *workspace, int64_t workspace_bytes,
+                       uint8_t *png_out, int64_t png_capacity, int64_t *png_sizes, int n_threads, void *stream) {
+  if (n_tiles <= 0) return 0;
+  if (!rgba || !sizes || !png_out || !png_sizes || max_w <= 0 || max_h <= 0 || row_stride < 4LL * max_w ||
+      tile_stride < row_stride * max_h)
+    return GSKYHIP_E_ARG;
+  if (!workspace || workspace_bytes < gskyhip_png_workspace_size(n_tiles, max_w, max_h)) return GSKYHIP_E_ARG;
+  for (int t = 0; t < n_tiles; t++) {
+    const int w = sizes[2 * t], h = sizes[2 * t + 1];
+    if (w <= 0 || h <= 0 || w > max_w || h > max_h || png_capacity < gskyhip_png_bound(w, h)) return GSKYHIP_E_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t per = (int64_t)max_h * (1 + 4 * (int64_t)max_w);
+  char *ws = (char *)workspace;
+  uint8_t *filt = (uint8_t *)ws;
+  char *tail = ws + ((int64_t)n_tiles * per + 255) / 256 * 256;
+  int64_t *d_off = (int64_t *)tail;
+  int32_t *d_wh = (int32_t *)(d_off + n_tiles);
+  int32_t *d_opq = d_wh + 2 * n_tiles;
+  std::vector<int64_t> off(n_tiles);
+  for (int t = 0; t < n_tiles; t++) off[t] = (int64_t)t * per;
+  std::vector<char> meta((size_t)n_tiles * (8 + 8));
+  std::memcpy(meta.data(), off.data(), (size_t)n_tiles * 8);
+  std::memcpy(meta.data() + (size_t)n_tiles * 8, sizes, (size_t)n_tiles * 8);
+  if (hipMemcpyAsync(d_off, meta.data(), meta.size(), hipMemcpyHostToDevice, s) != hipSuccess) return GSKYHIP_E_HIP;
+  hipLaunchKernelGGL(png_opaque_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, rgba, tile_stride, row_stride, d_wh,
+                     d_opq);
+  hipLaunchKernelGGL(png_filter_kernel, dim3((unsigned)((int64_t)n_tiles * max_h)), dim3(256), 0, s, rgba,
+                     tile_stride, row_stride, d_wh, d_opq, max_h, d_off, filt);
+  if (hipGetLastError() != hipSuccess) return GSKYHIP_E_HIP;
+  std::vector<uint8_t> host((size_t)n_tiles * per);
+  std::vector<int32_t> opq(n_tiles);
+  if (hipMemcpyAsync(host.data(), filt, host.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(opq.data(), d_opq, (size_t)n_tiles * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return GSKYHIP_E_HIP;
+  // deflate + framing per tile on host threads
+  std::atomic<int> next(0), err(0);
+  auto work = [&]() {
+    std::vector<uint8_t> o;
+    for (;;) {
+      const int t = next++;
+      if (t >= n_tiles) return;
+      const int w = sizes[2 * t], h = sizes[2 * t + 1];
+      const size_t n = (size_t)h * (1 + (opq[t] ? 3 : 4) * (size_t)w);
+      const int rc = png_tile(host.data() + off[t], n, w, h, opq[t] != 0, o);
+      if (rc || (int64_t)o.size() > png_capacity) { err = rc ? rc : GSKYHIP_E_ARG; png_sizes[t] = 0; continue; }
+      std::memcpy(png_out + (int64_t)t * png_capacity, o.data(), o.size());
+      png_sizes[t] = (int64_t)o.size();
+    }
+  };
+  const int nt = std::max(1, std::min(n_threads > 0 ? n_threads : 1, n_tiles));
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nt; i++) pool.emplace_back(work);
+  work();
+  for (auto &th : pool) th.join();
+  return err.load();
+}
+
+// ---- GeoTIFF (EncodeGdalOpen / EncodeGdal, utils/ogc_encoders.go:277-450)
+static int tiff_sample(int dtype, int &ts, uint16_t &fmt) {
+  switch (dtype) {
+    case GSKYHIP_BYTE: ts = 1; fmt = 1; return 0;
+    case GSKYHIP_SIGNEDBYTE: ts = 1; fmt = 2; return 0;
+    case GSKYHIP_INT16: ts = 2; fmt = 2; return 0;
+    case GSKYHIP_UINT16: ts = 2; fmt = 1; return 0;
+    case GSKYHIP_FLOAT32: ts = 4; fmt = 3; return 0;
+    default: return GSKYHIP_E_TYPE;
+  }
+}
+
+int64_t gskyhip_geotiff_workspace_size(int width, int height, int n_bands, int dtype, int block_x, int block_y) {
+  int ts;
+  uint16_t fmt;
+  if (width <= 0 || height <= 0 || n_bands <= 0 || block_x <= 0 || block_y <= 0 || tiff_sample(dtype, ts, fmt))
+    return 0;
+  const int64_t ntx = (width + block_x - 1) / block_x, nty = (height + block_y - 1) / block_y;
+  const int64_t rows = (int64_t)n_bands * ntx * nty * block_y;
+  const int64_t rb = (int64_t)block_x * ts;
+  const int64_t slot = rb + rb / 128 + 2;
+  return rows * (rb + slot + 4) + 8 * (int64_t)n_bands + 64 * (int64_t)n_bands + 4096;
+}
+
+int64_t gskyhip_geotiff_bound(int width, int height, int n_bands, int dtype, int block_x, int block_y) {
+  int ts;
+  uint16_t fmt;
+  if (width <= 0 || height <= 0 || n_bands <= 0 || block_x <= 0 || block_y <= 0 || tiff_sample(dtype, ts, fmt))
+    return 0;
+  const int64_t ntx = (width + block_x - 1) / block_x, nty = (height + block_y - 1) / block_y;
+  const int64_t rows = (int64_t)n_bands * ntx * nty * block_y;
+  const int64_t rb = (int64_t)block_x * ts;
+  return rows * (rb + rb / 128 + 2) + (int64_t)n_bands * ntx * nty * 16 + 65536 + 512 * (int64_t)n_bands;
+}
+
+int gskyhip_encode_geotiff(const void *const *bands, int n_bands, int dtype, int width, int height,
+                           const double *geot, int epsg, const double *nodata, const char *const *names,
+                           int block_x, int block_y, void *workspace, int64_t workspace_bytes, uint8_t *out,
+                           int64_t capacity, int64_t *size, void *stream) {
+  int ts;
+  uint16_t fmt;
+  if (!bands || !geot || !out || !size || n_bands <= 0 || n_bands > 4096) return GSKYHIP_E_ARG;
+  if (tiff_sample(dtype, ts, fmt)) return GSKYHIP_E_TYPE;
+  if (width <= 0 || height <= 0 || block_x <= 0 || block_y <= 0 || block_x % 16 || block_y % 16) return GSKYHIP_E_ARG;
+  if (!workspace || workspace_bytes < gskyhip_geotiff_workspace_size(width, height, n_bands, dtype, block_x, block_y))
+    return GSKYHIP_E_ARG;
+  if (capacity < gskyhip_geotiff_bound(width, height, n_bands, dtype, block_x, block_y)) return GSKYHIP_E_ARG;
+  const int ntx = (width + block_x - 1) / block_x, nty = (height + block_y - 1) / block_y;
+  const int64_t n_tiles = (int64_t)n_bands * ntx * nty;
+  const int64_t n_rows = n_tiles * block_y;
+  const int64_t rb = (int64_t)block_x * ts;
+  const int64_t slot = rb + rb / 128 + 2;
+  char *ws = (char *)workspace;
+  uint8_t *raw = (uint8_t *)ws;
+  uint8_t *enc = raw + n_rows * rb;
+  int32_t *len = (int32_t *)(enc + n_rows * slot);
+  const uint8_t **d_bands = (const uint8_t **)(((uintptr_t)(len + n_rows) + 15) & ~(uintptr_t)15);
+  uint8_t *d_pad = (uint8_t *)(d_bands + n_bands);
+  // edge-tile padding: the band's nodata in the band type (0 without one)
+  std::vector<char> meta((size_t)n_bands * 8 + (size_t)n_bands * 8, 0);
+  std::memcpy(meta.data(), bands, (size_t)n_bands * 8);
+  for (int b = 0; b < n_bands; b++) {
+    uint8_t *pb = (uint8_t *)meta.data() + (size_t)n_bands * 8 + 8 * b;
+    const double v = nodata ? nodata[b] : 0.0;
+    if (dtype == GSKYHIP_FLOAT32) { const float f = (float)v; std::memcpy(pb, &f, 4); }
+    else if (ts == 2) { const int16_t h = (int16_t)(dtype == GSKYHIP_UINT16 ? (int32_t)(uint16_t)v : (int32_t)v); std::memcpy(pb, &h, 2); }
+    else pb[0] = (uint8_t)(int)v;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(d_bands, meta.data(), meta.size(), hipMemcpyHostToDevice, s) != hipSuccess) return GSKYHIP_E_HIP;
+  hipLaunchKernelGGL(tiff_rows_kernel, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, s, d_bands, ts, width,
+                     height, block_x, block_y, ntx, nty, d_pad, slot, raw, enc, len, n_rows);
+  if (hipGetLastError() != hipSuccess) return GSKYHIP_E_HIP;
+  std::vector<int32_t> lens((size_t)n_rows);
+  std::vector<uint8_t> encs((size_t)(n_rows * slot));
+  if (hipMemcpyAsync(lens.data(), len, (size_t)n_rows * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(encs.data(), enc, encs.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return GSKYHIP_E_HIP;
+  // file: header | tile data (band-major, tiles row-major) | IFD | out-of-line tag data
+  std::vector<uint8_t> o;
+  o.reserve((size_t)std::min<int64_t>(capacity, 1LL << 30));
+  o.push_back('I'); o.push_back('I');
+  put_le<uint16_t>(o, 43); put_le<uint16_t>(o, 8); put_le<uint16_t>(o, 0);
+  put_le<uint64_t>(o, 0);   // first IFD offset, patched below
+  std::vector<uint64_t> toff((size_t)n_tiles), tcnt((size_t)n_tiles);
+  for (int64_t t = 0; t < n_tiles; t++) {
+    toff[t] = o.size();
+    for (int r = 0; r < block_y; r++) {
+      const int64_t i = t * block_y + r;
+      o.insert(o.end(), encs.begin() + i * slot, encs.begin() + i * slot + lens[i]);
+    }
+    tcnt[t] = o.size() - toff[t];
+  }
+  if (o.size() & 1) o.push_back(0);
+  std::vector<TiffEntry> ents;
+  ents.push_back(tiff_long(256, (uint32_t)width));
+  ents.push_back(tiff_long(257, (uint32_t)height));
+  ents.push_back(tiff_shorts(258, std::vector<uint16_t>((size_t)n_bands, (uint16_t)(8 * ts))));
+  ents.push_back(tiff_shorts(259, {32773}));   // PackBits
+  ents.push_back(tiff_shorts(262, {1}));       // BlackIsZero
+  ents.push_back(tiff_shorts(277, {(uint16_t)n_bands}));
+  ents.push_back(tiff_shorts(284, {(uint16_t)(n_bands > 1 ? 2 : 1)}));   // INTERLEAVE=BAND
+  ents.push_back(tiff_long(322, (uint32_t)block_x));
+  ents.push_back(tiff_long(323, (uint32_t)block_y));
+  ents.push_back(tiff_long8s(324, toff));
+  ents.push_back(tiff_long8s(325, tcnt));
+  if (n_bands > 1) ents.push_back(tiff_shorts(338, std::vector<uint16_t>((size_t)n_bands - 1, 0)));
+  ents.push_back(tiff_shorts(339, std::vector<uint16_t>((size_t)n_bands, fmt)));
+  if (geot[2] == 0.0 && geot[4] == 0.0) {
+    ents.push_back(tiff_doubles(33550, {geot[1], -geot[5], 0.0}));
+    ents.push_back(tiff_doubles(33922, {0.0, 0.0, 0.0, geot[0], geot[3], 0.0}));
+  } else {   // ModelTransformationTag for rotated grids
+    ents.push_back(tiff_doubles(34264, {geot[1], geot[2], 0.0, geot[0], geot[4], geot[5], 0.0, geot[3],
+                                        0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0}));
+  }
+  if (epsg > 0) {
+    const bool geo = epsg_geographic(epsg);
+    ents.push_back(tiff_shorts(34735, {1, 1, 0, 3, 1024, 0, 1, (uint16_t)(geo ? 2 : 1), 1025, 0, 1, 1,
+                                       (uint16_t)(geo ? 2048 : 3072), 0, 1, (uint16_t)epsg}));
+  }
+  if (names) {   // GDALSetMetadataItem("long_name", NameSpace) per band
+    std::string md = "<GDALMetadata>\n";
+    for (int b = 0; b < n_bands; b++)
+      if (names[b])
+        md += "  <Item name=\"long_name\" sample=\"" + std::to_string(b) + "\">" + xml_escape(names[b]) + "</Item>\n";
+    md += "</GDALMetadata>";
+    ents.push_back(tiff_ascii(42112, md));
+  }
+  if (nodata) {   // GDAL_NODATA (a single dataset value in GeoTIFF: band 1's)
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "%.18g", nodata[0]);
+    ents.push_back(tiff_ascii(42113, buf));
+  }
+  std::sort(ents.begin(), ents.end(), [](const TiffEntry &a, const TiffEntry &b) { return a.tag < b.tag; });
+  const uint64_t ifd = o.size();
+  const uint64_t ifd_bytes = 8 + 20 * ents.size() + 8;
+  uint64_t extra = ifd + ifd_bytes;
+  std::vector<uint8_t> tail;
+  put_le<uint64_t>(o, ents.size());
+  for (auto &e : ents) {
+    put_le<uint16_t>(o, e.tag);
+    put_le<uint16_t>(o, e.type);
+    put_le<uint64_t>(o, e.count);
+    if (e.data.size() <= 8) {
+      std::vector<uint8_t> v = e.data;
+      v.resize(8, 0);
+      o.insert(o.end(), v.begin(), v.end());
+    } else {
+      put_le<uint64_t>(o, extra + tail.size());
+      tail.insert(tail.end(), e.data.begin(), e.data.end());
+      if (tail.size() & 1) tail.push_back(0);
+    }
+  }
+  put_le<uint64_t>(o, 0);   // no next IFD
+  o.insert(o.end(), tail.begin(), tail.end());
+  for (int k = 0; k < 8; k++) o[8 + k] = (uint8_t)(ifd >> (8 * k));
+  if ((int64_t)o.size() > capacity) return GSKYHIP_E_ARG;
+  std::memcpy(out, o.data(), o.size());
+  *size = (int64_t)o.size();
+  return 0;
+}
+
+}  // extern "C"

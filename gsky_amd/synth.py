@@ -215,6 +215,33 @@ def config_c1(scale: float = 1.0) -> SynthConfig:
     return SynthConfig("C1", [g], "EPSG:3857", tiles, [[0]], [""], (0.0, 0.0, 1000.0, 0), None)
 
 
+def config_acpt(requests, res: float = 0.02) -> SynthConfig:
+    """The reference's acceptance GetMap requests (tests/golden/acpt_bboxes.json:
+    500 EPSG:3857 256^2 tiles over Australia) over six overlapping synthetic
+    EPSG:4326 float32 granules (3 x 2, 20 x 19 degrees at `res`, one day
+    apart, nodata at 1 %), nearest, clip 1000 scale, the docker palette: the
+    indexer's granule lists from the footprints."""
+    def make(k):
+        j, i = divmod(k, 3)
+        x0, y0 = 100.0 + 19.0 * i, -10.0 - 17.0 * j
+        nx, ny = int(round(20.0 / res)), int(round(19.0 / res))
+        idx = np.arange(nx * ny, dtype=np.uint64).reshape(ny, nx) + np.uint64((SEED0 + 0xAC00 + k) << 32)
+        hh = splitmix64(idx)
+        lon = x0 + res * (np.arange(nx) + 0.5)
+        lat = y0 - res * (np.arange(ny) + 0.5)
+        v = 500 + 400 * np.sin(np.pi * lon[None, :] / 7) * np.cos(np.pi * lat[:, None] / 5) + (uniform01(hh) * 10 - 5)
+        v = v.astype(np.float32)
+        v[uniform01(splitmix64(hh)) < 0.01] = -9999.0
+        poly = "POLYGON ((%g %g,%g %g,%g %g,%g %g,%g %g))" % (x0, y0, x0 + 20, y0, x0 + 20, y0 - 19, x0, y0 - 19, x0, y0)
+        return SynthGranule(v, [x0, res, 0.0, y0, 0.0, -res], "EPSG:4326", -9999.0, 1577836800.0 + 86400.0 * k,
+                            poly)
+    granules = _pmap(make, range(6))
+    tiles = [((r[0], r[1], r[2], r[3]), int(r[4]), int(r[5])) for r in requests]
+    cfg = SynthConfig("ACPT", granules, "EPSG:3857", tiles, [], [""], (0.0, 0.0, 1000.0, 0), PALETTE_GSKY)
+    cfg.pairs = [cfg.index_chunk(bb) for (bb, _, _) in tiles]
+    return cfg
+
+
 # ---------------------------------------------------------------- C2
 def config_c2(scale: float = 1.0, tiles_per_side: int = 64, tile_px: int = 512, grid: int = 4) -> SynthConfig:
     """Batch of EPSG:3857 tiles from `grid`^2 Albers EPSG:3577 int16 granules

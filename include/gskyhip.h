@@ -340,6 +340,49 @@ int gskyhip_encode_rgba(const uint8_t *const *bands, int nbands, int w, int h,
 int gskyhip_compute_mask(const void *data, int dtype, int64_t n, const gskyhip_mask *mask,
                          uint8_t *out, void *stream);
 
+/* ---- output codecs ------------------------------------------------------ */
+/* png.Encode of EncodePNG (utils/ogc_encoders.go:139; Go 1.12 image/png) for
+ * a batch of RGBA tiles in HBM, e.g. the rgba_out of gskyhip_render_tiles:
+ *   rgba: dev, tile t row y at rgba + t*tile_stride + y*row_stride (bytes);
+ *   sizes: HOST int32 2 per tile {width, height} (<= max_w, max_h);
+ *   png_out: HOST, png_capacity bytes per tile (>= gskyhip_png_bound(w, h));
+ *   png_sizes: HOST int64 per tile, the PNG's length.
+ * Colour type RGB when every alpha is 0xff else RGBA (NRGBA bytes), Go's
+ * per-row filter choice, zlib level 6, 32 KiB IDAT chunks (see encode.hip:
+ * the filtered rows are Go's bytes, the deflate stream is zlib's).
+ * n_threads host threads deflate the tiles; `stream` runs the GPU pass. */
+int64_t gskyhip_png_workspace_size(int n_tiles, int max_w, int max_h);
+int64_t gskyhip_png_bound(int width, int height);
+int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, int64_t tile_stride,
+                       int64_t row_stride, const int32_t *sizes, void *workspace, int64_t workspace_bytes,
+                       uint8_t *png_out, int64_t png_capacity, int64_t *png_sizes, int n_threads, void *stream);
+
+/* EncodeGdalOpen + EncodeGdal for format "geotiff" (utils/ogc_encoders.go:
+ * 277-450) of one WCS coverage held in HBM: a BigTIFF with the reference's
+ * creation options COMPRESS=PACKBITS, TILED=YES, BIGTIFF=YES,
+ * INTERLEAVE=BAND, BLOCKXSIZE / BLOCKYSIZE (ows.go passes 1024 x 256),
+ * PIXELTYPE=SIGNEDBYTE for int8; the geotransform (ModelPixelScale +
+ * ModelTiepoint, ModelTransformation when rotated), EPSG code as GeoKeys,
+ * per-band long_name (GDAL_METADATA) and nodata (GDAL_NODATA, band 1's value:
+ * GeoTIFF holds one).
+ *   bands: HOST array of n_bands dev pointers, each height x width samples of
+ *     dtype (GSKYHIP_BYTE / SIGNEDBYTE / INT16 / UINT16 / FLOAT32), row-major;
+ *   geot: HOST 6 doubles (GDAL order); epsg <= 0 writes no GeoKeys;
+ *   nodata, names: HOST n_bands each, or NULL;
+ *   block_x, block_y: multiples of 16;
+ *   workspace: dev, gskyhip_geotiff_workspace_size bytes;
+ *   out: HOST, capacity >= gskyhip_geotiff_bound bytes; *size = file length.
+ * PackBits runs on the GPU (one thread per tile row, libtiff encodes tiled
+ * PackBits row by row); the framing on the host.  The bytes are a valid
+ * GeoTIFF of the same samples, tags and keys GDAL writes, not GDAL's file
+ * byte for byte (tag set and tile order differ: parity on decoded content). */
+int64_t gskyhip_geotiff_workspace_size(int width, int height, int n_bands, int dtype, int block_x, int block_y);
+int64_t gskyhip_geotiff_bound(int width, int height, int n_bands, int dtype, int block_x, int block_y);
+int gskyhip_encode_geotiff(const void *const *bands, int n_bands, int dtype, int width, int height,
+                           const double *geot, int epsg, const double *nodata, const char *const *names,
+                           int block_x, int block_y, void *workspace, int64_t workspace_bytes, uint8_t *out,
+                           int64_t capacity, int64_t *size, void *stream);
+
 /* ---- drill (WPS zonal statistics) --------------------------------------- */
 /* readData (worker/gdalprocess/drill.go:90-227), mean / pixel-count mode,
  * decileCount = 0, for a batch of polygons over one time stack.

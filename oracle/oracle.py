@@ -459,6 +459,65 @@ def drill_read_data_full(data, mask, nodata, clip_lower, clip_upper, pixel_count
     return np.array(vals, np.float64).reshape(-1, nc), np.array(cnts, np.int32).reshape(-1, nc)
 
 
+def go_png_rows(rgba):
+    """What Go 1.12 image/png's writeImage hands zlib for EncodePNG's
+    *image.RGBA canvas (utils/ogc_encoders.go:82-139), a numpy restatement:
+    (opaque, bytes).  opaque: every alpha 0xff (image.RGBA.Opaque) -> RGB rows,
+    else NRGBA rows (color.NRGBAModel of each premultiplied pixel, 16-bit
+    arithmetic, uint8() wrap).  Each row = [filter type][residuals] with the
+    filter of writer.go filter(): sums of |int8| residuals of Up, Paeth, None,
+    Sub, Average in that order, the first strictly smaller wins."""
+    px = np.asarray(rgba, np.uint8)
+    h, w, _ = px.shape
+    opaque = bool((px[..., 3] == 0xFF).all())
+    if opaque:
+        img = px[..., :3].astype(np.int64)
+    else:
+        a = px[..., 3].astype(np.int64)
+        a16 = a | (a << 8)
+        img = np.zeros((h, w, 4), np.int64)
+        for c in range(3):
+            v16 = px[..., c].astype(np.int64)
+            v16 = v16 | (v16 << 8)
+            conv = ((v16 * 0xFFFF) // np.maximum(a16, 1)) >> 8
+            img[..., c] = np.where(a == 0xFF, px[..., c], np.where(a == 0, 0, conv & 0xFF))
+        img[..., 3] = a
+    bpp = 3 if opaque else 4
+    rows = img.reshape(h, w * bpp)
+    out = bytearray()
+    prev = np.zeros(w * bpp, np.int64)
+
+    def abs8(d):
+        d = d & 0xFF
+        return np.where(d < 128, d, 256 - d).sum()
+
+    def paeth(a, b, c):
+        pa = b - c
+        pb = a - c
+        pc = np.abs(pa + pb)
+        pa, pb = np.abs(pa), np.abs(pb)
+        return np.where((pa <= pb) & (pa <= pc), a, np.where(pb <= pc, b, c))
+
+    for y in range(h):
+        cur = rows[y]
+        left = np.concatenate([np.zeros(bpp, np.int64), cur[:-bpp]])
+        ul = np.concatenate([np.zeros(bpp, np.int64), prev[:-bpp]])
+        cand = {2: cur - prev,
+                4: np.concatenate([cur[:bpp] - prev[:bpp], cur[bpp:] - paeth(left, prev, ul)[bpp:]]),
+                0: cur,
+                1: cur - left,
+                3: np.concatenate([cur[:bpp] - prev[:bpp] // 2, cur[bpp:] - (left[bpp:] + prev[bpp:]) // 2])}
+        best, ft = None, 2
+        for f in (2, 4, 0, 1, 3):
+            sm = abs8(cand[f])
+            if best is None or sm < best:
+                best, ft = sm, f
+        out.append(ft)
+        out += (cand[ft] & 0xFF).astype(np.uint8).tobytes()
+        prev = cur
+    return opaque, bytes(out)
+
+
 def band_math(expr, variables, out_nodata):
     """Band-math of RasterMerger.Run (processor/tile_merger.go:654-731) for
     one expression over one axis, a pure-Python restatement: variables =

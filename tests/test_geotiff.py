@@ -1,0 +1,158 @@
+"""WCS GeoTIFF writer (EncodeGdalOpen / EncodeGdal, utils/ogc_encoders.go:
+277-450) through the C-ABI gskyhip_encode_geotiff.  GDAL is not in the image,
+so the file is read back by the small BigTIFF reader below (TIFF 6.0 +
+BigTIFF tag layout, PackBits) and checked for what the reference's GDAL call
+sets: the samples of every band (edge tiles cropped), the creation options
+(PackBits, 1024 x 256 tiles, band interleave, BigTIFF, SIGNEDBYTE), the
+geotransform, the EPSG GeoKeys, nodata and the long_name metadata.  Byte
+identity with GDAL's file is not claimed (tag set and layout differ)."""
+import struct
+
+import numpy as np
+import pytest
+
+from gsky_amd import _lib
+
+TYPE_SIZE = {1: 1, 2: 1, 3: 2, 4: 4, 12: 8, 16: 8}
+
+
+def read_bigtiff(buf: bytes):
+    assert buf[:4] == b"II+\x00", "not a little-endian BigTIFF"
+    bytesize, zero, ifd = struct.unpack_from("<HHQ", buf, 4)
+    assert bytesize == 8 and zero == 0
+    (n,) = struct.unpack_from("<Q", buf, ifd)
+    tags = {}
+    prev = -1
+    for i in range(n):
+        tag, typ, count, val = struct.unpack_from("<HHQ8s", buf, ifd + 8 + 20 * i)
+        assert tag > prev, "IFD entries must be sorted"
+        prev = tag
+        size = TYPE_SIZE[typ] * count
+        raw = val[:size] if size <= 8 else buf[struct.unpack("<Q", val)[0]:struct.unpack("<Q", val)[0] + size]
+        if typ == 2:
+            tags[tag] = raw.rstrip(b"\x00").decode()
+        else:
+            fmt = {1: "B", 3: "H", 4: "I", 12: "d", 16: "Q"}[typ]
+            tags[tag] = list(struct.unpack("<%d%s" % (count, fmt), raw))
+    (nxt,) = struct.unpack_from("<Q", buf, ifd + 8 + 20 * n)
+    assert nxt == 0
+    return tags
+
+
+def unpackbits(data: bytes, n: int) -> bytes:
+    out = bytearray()
+    i = 0
+    while len(out) < n:
+        c = data[i]
+        i += 1
+        if c < 128:
+            out += data[i:i + c + 1]
+            i += c + 1
+        elif c > 128:
+            out += bytes([data[i]]) * (257 - c)
+            i += 1
+    assert len(out) == n
+    return bytes(out), i
+
+
+def decode_bands(buf: bytes, tags):
+    w, h = tags[256][0], tags[257][0]
+    nb = tags[277][0]
+    bx, by = tags[322][0], tags[323][0]
+    bits = tags[258][0]
+    fmt = tags[339][0]
+    dt = {(8, 1): np.uint8, (8, 2): np.int8, (16, 1): np.uint16, (16, 2): np.int16, (32, 3): np.float32}[(bits, fmt)]
+    ntx, nty = -(-w // bx), -(-h // by)
+    offs, cnts = tags[324], tags[325]
+    assert len(offs) == nb * ntx * nty
+    out = np.zeros((nb, nty * by, ntx * bx), dt)
+    rb = bx * np.dtype(dt).itemsize
+    for b in range(nb):
+        for ty in range(nty):
+            for tx in range(ntx):
+                t = (b * nty + ty) * ntx + tx
+                data = buf[offs[t]:offs[t] + cnts[t]]
+                pos = 0
+                rows = []
+                for _ in range(by):   # tiled PackBits is row by row
+                    row, used = unpackbits(data[pos:], rb)
+                    pos += used
+                    rows.append(np.frombuffer(row, dt))
+                assert pos == len(data)
+                out[b, ty * by:(ty + 1) * by, tx * bx:(tx + 1) * bx] = np.stack(rows)
+    return out[:, :h, :w]
+
+
+def test_geotiff_exports():
+    for s in ("gskyhip_geotiff_workspace_size", "gskyhip_geotiff_bound", "gskyhip_encode_geotiff"):
+        assert hasattr(_lib.lib(), s)
+    L = _lib.lib()
+    assert L.gskyhip_geotiff_bound(0, 10, 1, 6, 1024, 256) == 0   # bad size
+    assert L.gskyhip_geotiff_bound(10, 10, 1, 9, 1024, 256) == 0   # bad type
+    assert L.gskyhip_geotiff_bound(100, 10, 2, 6, 1024, 256) > 2 * 1024 * 256 * 4
+
+
+def test_packbits_reader_roundtrip():
+    # the reader's decoder on hand-made PackBits (TIFF 6.0 section 9 example)
+    enc = bytes([0xFE, 0xAA, 0x02, 0x80, 0x00, 0x2A, 0xFD, 0xAA, 0x03, 0x80, 0x00, 0x2A, 0x22, 0xF7, 0xAA])
+    dec, used = unpackbits(enc, 24)
+    assert used == len(enc)
+    assert dec == bytes.fromhex("AAAAAA80002AAAAAAAAA80002A22AAAAAAAAAAAAAAAAAAAA")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,w,h,nb", [("float32", 1500, 300, 2), ("int16", 700, 530, 1),
+                                           ("uint8", 1024, 256, 3), ("int8", 33, 17, 1),
+                                           ("uint16", 1030, 260, 2)])
+def test_geotiff_roundtrip(dtype, w, h, nb):
+    import torch
+    from gsky_amd.encode import encode_geotiff
+    rng = np.random.default_rng(hash((dtype, w, h)) & 0xFFFF)
+    np_dt = np.dtype(dtype)
+    if dtype == "float32":
+        arrs = [rng.normal(size=(h, w)).astype(np.float32) for _ in range(nb)]
+        arrs[0][:, : w // 3] = -999.0   # runs: the replicate path
+    else:
+        info = np.iinfo(np_dt)
+        arrs = [rng.integers(info.min, info.max, size=(h, w), endpoint=True).astype(np_dt) for _ in range(nb)]
+        arrs[0][h // 2:, :] = arrs[0][0, 0]
+        arrs[-1][:, ::7] = 3
+    dev = [torch.from_numpy(a.view(np.int16) if dtype == "uint16" else a).cuda() for a in arrs]
+    geot = [1500000.0, 25.0, 0.0, -3900000.0, 0.0, -25.0]
+    nodata = [-999.0] * nb if dtype == "float32" else [0.0] * nb
+    names = ["band_%d&<x>" % i for i in range(nb)]
+    buf = encode_geotiff(dev, geot, 3577, nodata, names, uint16=(dtype == "uint16"))
+    tags = read_bigtiff(buf)
+    assert tags[259] == [32773]                        # COMPRESS=PACKBITS
+    assert tags[322] == [1024] and tags[323] == [256]   # BLOCKXSIZE / BLOCKYSIZE
+    assert tags[277] == [nb]
+    assert tags[284] == [2 if nb > 1 else 1]           # INTERLEAVE=BAND
+    fmt = {"float32": 3, "int16": 2, "uint8": 1, "int8": 2, "uint16": 1}[dtype]
+    assert tags[339] == [fmt] * nb                     # int8: PIXELTYPE=SIGNEDBYTE
+    assert tags[33550] == [25.0, 25.0, 0.0]
+    assert tags[33922] == [0.0, 0.0, 0.0, 1500000.0, -3900000.0, 0.0]
+    keys = tags[34735]
+    assert keys[:4] == [1, 1, 0, 3]
+    kd = {keys[4 + 4 * i]: keys[4 + 4 * i + 3] for i in range(keys[3])}
+    assert kd == {1024: 1, 1025: 1, 3072: 3577}
+    assert float(tags[42113]) == nodata[0]
+    for i in range(nb):
+        assert ('<Item name="long_name" sample="%d">band_%d&amp;&lt;x&gt;</Item>' % (i, i)) in tags[42112]
+    got = decode_bands(buf, tags)
+    for b in range(nb):
+        np.testing.assert_array_equal(got[b], arrs[b])
+
+
+@pytest.mark.gpu
+def test_geotiff_geographic_rotated():
+    import torch
+    from gsky_amd.encode import encode_geotiff
+    a = torch.arange(50 * 40, dtype=torch.float32).reshape(40, 50).cuda()
+    geot = [110.0, 0.01, 0.001, -10.0, 0.002, -0.01]
+    buf = encode_geotiff([a], geot, 4326, None, None, block=(32, 16))
+    tags = read_bigtiff(buf)
+    assert 33550 not in tags and tags[34264][:8] == [0.01, 0.001, 0.0, 110.0, 0.002, -0.01, 0.0, -10.0]
+    kd = {tags[34735][4 + 4 * i]: tags[34735][7 + 4 * i] for i in range(3)}
+    assert kd == {1024: 2, 1025: 1, 2048: 4326}
+    assert 42112 not in tags and 42113 not in tags
+    np.testing.assert_array_equal(decode_bands(buf, tags)[0], a.cpu().numpy())

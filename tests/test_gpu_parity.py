@@ -258,6 +258,28 @@ def test_render_c2_small(gpu, oracle):
     assert (exp[..., 3] > 0).mean() > 0.3      # the test exercises real data
 
 
+def test_render_acceptance_requests(gpu, oracle):
+    """The reference's own 500 acceptance GetMap requests
+    (acceptance_tests/acpt_url.tpl -> tests/golden/acpt_bboxes.json: 256^2
+    EPSG:3857 tiles at zooms 6-9 over Australia, 179 distinct) as one tile
+    batch over six overlapping synthetic EPSG:4326 granules: every RGBA
+    pixel identical to the oracle's."""
+    import json
+    import os
+
+    import gsky_amd
+    reqs = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "acpt_bboxes.json")))
+    assert len(reqs) == 500
+    cfg = synth.config_acpt(reqs)
+    assert all(cfg.pairs) and max(len(p) for p in cfg.pairs) >= 2
+    b = gpu_batch(cfg, gpu)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True)).cpu().numpy()
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg)
+    assert identity(got, exp) == 1.0
+    assert (exp[..., 3] > 0).mean() > 0.5
+
+
 def test_render_auto_scale(gpu, oracle):
     import gsky_amd
     cfg = synth.config_c2(scale=0.05, tiles_per_side=3, tile_px=128)

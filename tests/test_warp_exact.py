@@ -1,0 +1,101 @@
+"""Independent check of the warp (no oracle involved): the source pixel the
+MI355X path picked for every window pixel of a C2-shaped batch, against an
+exact fp64 transform of the pixel centre written here from the published
+formulas -- EPSG:3857 inverse (spherical Mercator) and EPSG:3577 Albers equal
+area forward on GRS80 (Snyder, Map Projections -- A Working Manual, 14-1..
+14-12; phi1 -18, phi2 -36, phi0 0, lambda0 132).  The reference warps through
+GDAL's approximate transformer with a 0.125-pixel error bound
+(warp.go:219); so for every pixel the picked cell [i, i+1) x [j, j+1) must
+reach within 0.125 px of the exact coordinate, and only pixels whose exact
+coordinate lies within 0.125 px of a cell edge may pick a different cell
+than the exact truncation.  The granules hold their own pixel index as
+float32 (exact below 2^24), so each window value names the picked pixel."""
+import math
+
+import numpy as np
+import pytest
+
+from gsky_amd import synth
+
+from .helpers import gpu_batch
+
+pytestmark = pytest.mark.gpu
+
+A, INV_F = 6378137.0, 298.257222101          # GRS80
+E2 = (2 - 1 / INV_F) / INV_F
+E = math.sqrt(E2)
+
+
+def _q(phi):
+    s = np.sin(phi)
+    return (1 - E2) * (s / (1 - E2 * s * s) - (1 / (2 * E)) * np.log((1 - E * s) / (1 + E * s)))
+
+
+def _m(phi):
+    s = np.sin(phi)
+    return np.cos(phi) / np.sqrt(1 - E2 * s * s)
+
+
+P1, P2, P0, L0 = (math.radians(v) for v in (-18.0, -36.0, 0.0, 132.0))
+N = (_m(P1) ** 2 - _m(P2) ** 2) / (_q(P2) - _q(P1))
+CC = _m(P1) ** 2 + N * _q(P1)
+RHO0 = A * np.sqrt(CC - N * _q(P0)) / N
+
+
+def albers(lon, lat):
+    rho = A * np.sqrt(CC - N * _q(lat)) / N
+    th = N * (lon - L0)
+    return rho * np.sin(th), RHO0 - rho * np.cos(th)
+
+
+def merc_inv(x, y):
+    R = 6378137.0
+    return x / R, np.arctan(np.sinh(y / R))
+
+
+def test_warp_within_the_approximation_bound(gpu):
+    import torch
+    cfg = synth.config_c2(scale=0.25, tiles_per_side=8, tile_px=256)
+    for g in cfg.granules:   # each granule holds its pixel index
+        ny, nx = g.data.shape
+        g.data = np.arange(nx * ny, dtype=np.float32).reshape(ny, nx)
+        g.nodata = -1.0
+    b = gpu_batch(cfg, gpu)
+    wins = b.warp_windows()
+    p = 0
+    n_px = n_diff = 0
+    worst = 0.0
+    for t, ((bb, w, h), ks) in enumerate(zip(cfg.tiles, cfg.pairs)):
+        gt_t = [bb[0], (bb[2] - bb[0]) / w, 0.0, bb[3], 0.0, -(bb[3] - bb[1]) / h]
+        for k in ks:
+            arr, (xoff, yoff, ww, hh), tname, nd = wins[p]
+            p += 1
+            assert tname == "Float32"
+            v = arr.cpu().numpy().astype(np.int64)
+            g = cfg.granules[k]
+            ny, nx = g.data.shape
+            jj, ii = np.mgrid[0:hh, 0:ww]
+            X = gt_t[0] + (xoff + ii + 0.5) * gt_t[1]
+            Y = gt_t[3] + (yoff + jj + 0.5) * gt_t[5]
+            lon, lat = merc_inv(X, Y)
+            ax, ay = albers(lon, lat)
+            sx = (ax - g.geot[0]) / g.geot[1]
+            sy = (ay - g.geot[3]) / g.geot[5]
+            ok = v >= 0                                 # picked pixels (nodata = outside)
+            px, py = v % nx, v // nx
+            # the cell reaches within 0.125 px of the exact coordinate on both axes
+            dx = np.maximum(np.maximum(px - sx, sx - (px + 1)), 0.0)
+            dy = np.maximum(np.maximum(py - sy, sy - (py + 1)), 0.0)
+            if ok.any():
+                worst = max(worst, float(np.maximum(dx, dy)[ok].max()))
+            tx, ty = np.floor(sx + 1e-10).astype(np.int64), np.floor(sy + 1e-10).astype(np.int64)
+            diff = ok & ((px != tx) | (py != ty))
+            near = np.minimum(np.abs(sx - np.round(sx)), np.abs(sy - np.round(sy))) <= 0.125
+            assert not (diff & ~near).any(), (t, k)
+            n_px += int(ok.sum())
+            n_diff += int(diff.sum())
+    assert n_px > 1_000_000
+    assert worst <= 0.125 + 1e-6, worst
+    print("warp vs exact transform: %d px, %d (%.4f %%) pick another cell than the exact truncation, "
+          "worst cell distance %.4f px" % (n_px, n_diff, 100.0 * n_diff / n_px, worst))
+    assert n_diff / n_px < 0.01
