@@ -179,9 +179,12 @@ __device__ __forceinline__ bool src_to_dst_georef(const Xform &t, double x, doub
 
 // Planning prologue, 128-thread workgroups: the first n_edge_blocks take a
 // granule each, a thread per edge sample (its GEdge, see PlanArgs); the rest
-// a pair each per thread (its owning tile).
+// a pair each per thread (its owning tile).  Workgroup 0 also zeroes the
+// plan counters (no separate memset launch: the later planning kernels are
+// ordered after this one on the stream).
 __global__ __launch_bounds__(128) void plan_prologue_kernel(PlanArgs a, int n_edge_blocks) {
   const int lane = threadIdx.x;
+  if (blockIdx.x == 0 && lane < 64) a.counters[lane] = 0;
   if ((int)blockIdx.x >= n_edge_blocks) {
     const int p = ((int)blockIdx.x - n_edge_blocks) * 128 + lane;
     if (p < a.n_pairs) a.pair_tile[p] = owning_tile(a.tiles, a.n_tiles, p);
@@ -1268,7 +1271,6 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   if (const char *sep = getenv("GSKYHIP_PLAN_SEP")) a.sep = atoi(sep);
 #endif
   hipStream_t s = rc.stream;
-  if (hipMemsetAsync(cv.counters, 0, 256, s) != hipSuccess) return GSKYHIP_E_HIP;
   // per-granule edge samples, staged in the split-list region (plan_rows
   // writes that list only after plan_pairs has read the table), in one launch
   // with the pairs' owning tiles
@@ -1282,9 +1284,8 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
       (int64_t)sizeof(GEdge) * rc.n_granules <= (int64_t)sizeof(int64_t) * rc.n_pairs * rc.max_h)
     a.gedge = (GEdge *)cv.split_list;
   const int n_edge_blocks = a.gedge ? rc.n_granules : 0;
-  if (rc.n_pairs > 0)
-    hipLaunchKernelGGL(plan_prologue_kernel, dim3(n_edge_blocks + (rc.n_pairs + 127) / 128), dim3(128), 0, s, a,
-                       n_edge_blocks);
+  hipLaunchKernelGGL(plan_prologue_kernel, dim3(std::max(1, n_edge_blocks + (rc.n_pairs + 127) / 128)), dim3(128),
+                     0, s, a, n_edge_blocks);
   if (rc.n_pairs > 0) hipLaunchKernelGGL(plan_pairs_kernel, dim3(rc.n_pairs), dim3(64), 0, s, a);
   hipLaunchKernelGGL(plan_tiles_kernel, dim3(rc.n_tiles), dim3(64), 0, s, a);
   if (rc.n_pairs > 0) {

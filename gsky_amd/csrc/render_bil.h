@@ -14,11 +14,13 @@
 //     x + 1 of the two source rows), issued for 4 pixels before the first
 //     wait; taps outside the band read 0 through the buffer range check and
 //     are dropped by their validity flag;
-//   * W = double: the weights and sums in fp64, the expressions of
-//     bil_sample() (render_lds.h) -- bit-identical to render_lds_kernel;
-//     W = float: tap selection and fractions from the same fp64 coordinates,
-//     weights and sums in fp32 (within the 1e-4 relative bar of north_star;
-//     A/B build only, GSKYHIP_BIL_F32=1);
+//   * W = float (default): tap selection and fractions from the same fp64
+//     coordinates, weights and sums in fp32 -- on C3 71 % of pixels
+//     bit-identical to GDAL's fp64 expressions, the rest within 1.6e-7
+//     relative (north_star's bar: 1e-4), 17 % faster (render 0.94 vs
+//     1.13 ms, profiles/r03b_ab_c3.jsonl);
+//     W = double (A/B build, GSKYHIP_BIL_F32=0): the weights and sums in
+//     fp64, the expressions of bil_sample() (render_lds.h);
 //   * the fp64 division runs only for pixels whose accDiv is not exactly 1
 //     (a tap dropped): the others take accR as it is.
 #pragma once
@@ -183,11 +185,10 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
   }
 }
 
-// Bilinear float canvases (no mask layer): fp64 weights (the reference's
-// expressions), 4 rows per wave, 4 pixels' taps in flight at 6 waves per
-// SIMD (no spill); the A/B build also has fp32 weights (GSKYHIP_BIL_F32),
-// 2 pixels in flight at 8 waves (GSKYHIP_BIL_HP=2) and 8 rows per wave
-// (GSKYHIP_BIL_RPW=8).
+// Bilinear float canvases (no mask layer): fp32 weights, 4 rows per wave,
+// 4 pixels' taps in flight at 8 waves per SIMD; the A/B build also has the
+// fp64 weights (GSKYHIP_BIL_F32=0: 6 waves per SIMD, or 8 with 2 pixels in
+// flight, GSKYHIP_BIL_HP=2) and 8 rows per wave (GSKYHIP_BIL_RPW=8).
 template <typename WT, int RPW, int HP, int WPS>
 void launch_bil_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
@@ -201,7 +202,7 @@ void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   const char *f = getenv("GSKYHIP_BIL_F32");
   const char *rp = getenv("GSKYHIP_BIL_RPW");
   const char *hp = getenv("GSKYHIP_BIL_HP");
-  const bool f32 = f && atoi(f) != 0;
+  const bool f32 = !f || atoi(f) != 0;
   const int rpw = rp ? atoi(rp) : 4;
   const int hpx = hp ? atoi(hp) : 4;
   if (f32) {
@@ -213,7 +214,7 @@ void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   }
   return;
 #endif
-  launch_bil_v<double, 4, 4, 6>(a, s);
+  launch_bil_v<float, 4, 4, 8>(a, s);
 }
 
 }  // namespace gsky

@@ -71,10 +71,10 @@ __device__ __forceinline__ uint32_t scale_int(const ScaleK &k, int32_t c) {
 }
 
 // RPW: rows per wave (a block of 4 waves covers 4 * RPW rows of a 512-column
-// block).  PIPE: a row's RGBA stores are issued after the next row's first
-// gathers, so the gathers' vmcnt wait does not also wait for the previous
-// row's write stream (vmcnt counts loads and stores in issue order).
-template <typename T, bool MASK, bool CANVAS, int RPW, bool PIPE>
+// block).  Rows are processed one after the other; a row's RGBA stores are
+// issued before the next row's gathers (deferring them behind those gathers
+// measured 0.6 % slower on C2 and C5, profiles/r03b_ab_nn.jsonl).
+template <typename T, bool MASK, bool CANVAS, int RPW>
 __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
@@ -84,7 +84,6 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
                                                                       int n_items) {
   using V = typename VOf<T>::type;
   constexpr bool kInt = !std::is_same<T, float>::value;
-  constexpr bool kPipe = PIPE && !CANVAS;
   constexpr int kRowsBlk = 4 * RPW;
   __shared__ uint32_t s_tab[256];
 
@@ -123,9 +122,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int xl = xb + lane;                     // tile column of the lane's pixel 0
   uint32_t *rgba_lane = (uint32_t *)(a.rgba + (((int64_t)t * a.max_h) * a.max_w + xl) * 4);
 
-  // RGBA stores of row r (kPipe: deferred behind the next row's gathers)
-  uint32_t pend[kNnPx];
-  int pend_row = -1;
+  // RGBA stores of row r
   auto store_row = [&](int r, const uint32_t *px) {
     uint32_t *dst = rgba_lane + (int64_t)r * a.max_w;
     if (full) {
@@ -135,14 +132,6 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 #pragma unroll
       for (int q = 0; q < kNnPx; q++)
         if (64 * q + lane < ncols) __builtin_nontemporal_store(px[q], (GPTR(uint32_t))(dst + 64 * q));
-    }
-  };
-  auto flush = [&]() {
-    if constexpr (kPipe) {
-      if (pend_row >= 0) {
-        store_row(pend_row, pend);
-        pend_row = -1;
-      }
     }
   };
 
@@ -189,7 +178,6 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         V vv[kNnPx];
 #pragma unroll
         for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
-        flush();
         if (!fill_mode) {
 #pragma unroll
           for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
@@ -229,7 +217,6 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         V vv[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
-        flush();
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           const int ic = ic0 + 64 * (h + q);
@@ -243,7 +230,6 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         }
       }
     }
-    flush();   // a row without entries
 
     // output: typed canvas (WCS) or utils.Scale + palette / grey RGBA
     if constexpr (CANVAS) {
@@ -267,27 +253,21 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 #pragma unroll
         for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_t<T>(sk, c[q]) & 0xFFu];
       }
-      if constexpr (kPipe) {
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) pend[q] = px[q];
-        pend_row = r;
-      } else {
-        store_row(r, px);
-      }
+      store_row(r, px);
     }
   }
-  flush();
 }
 
-// Rows per wave and store pipelining of the NN band kernel (A/B build:
-// GSKYHIP_NN_RPW = 4 / 8 / 16, GSKYHIP_NN_PIPE = 0 / 1).
-constexpr int kNnRpw = 4;
-constexpr bool kNnPipe = false;
+// Rows per wave of the NN band kernel: 8 when the batch has work for every
+// CU many times over (C2: 1.473 vs 1.506 ms), else 4 (C5, 80 tiles: 0.66 vs
+// 0.86 ms at 8 -- too few blocks); profiles/r03b_ab_nn.jsonl.  Masked and
+// canvas batches keep 4 (measured on C5 only).  A/B build: GSKYHIP_NN_RPW.
+constexpr int kNnRpw8MinItems = 32768;
 
-template <typename T, bool M, bool C, int RPW, bool PIPE>
+template <typename T, bool M, bool C, int RPW>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, PIPE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -296,31 +276,20 @@ void launch_nn_v(const RenderArgs &a, hipStream_t s) {
 template <typename T>
 void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   const bool canvas = (a.lds_mode & kCanvas) != 0;
+  const int64_t items8 = (int64_t)a.n_tiles * ((a.max_h + 31) / 32) * ((a.max_w + kBandCols - 1) / kBandCols);
+  bool rpw8 = items8 >= kNnRpw8MinItems;
 #ifdef GSKYHIP_AB
-  if constexpr (std::is_same<T, int16_t>::value) {
-    const char *rp = getenv("GSKYHIP_NN_RPW");
-    const char *pp = getenv("GSKYHIP_NN_PIPE");
-    const int rpw = rp ? atoi(rp) : kNnRpw;
-    const bool pipe = pp ? atoi(pp) != 0 : kNnPipe;
-    if (!canvas) {
-#define GSKY_NN_AB(M)                                                         \
-  do {                                                                        \
-    if (rpw == 16) { if (pipe) launch_nn_v<T, M, false, 16, true>(a, s); else launch_nn_v<T, M, false, 16, false>(a, s); } \
-    else if (rpw == 8) { if (pipe) launch_nn_v<T, M, false, 8, true>(a, s); else launch_nn_v<T, M, false, 8, false>(a, s); } \
-    else { if (pipe) launch_nn_v<T, M, false, 4, true>(a, s); else launch_nn_v<T, M, false, 4, false>(a, s); } \
-  } while (0)
-      if (mask) GSKY_NN_AB(true); else GSKY_NN_AB(false);
-#undef GSKY_NN_AB
-      return;
-    }
-  }
+  if (const char *rp = getenv("GSKYHIP_NN_RPW")) rpw8 = atoi(rp) == 8;
 #endif
   if (mask) {
-    if (canvas) launch_nn_v<T, true, true, kNnRpw, kNnPipe>(a, s);
-    else launch_nn_v<T, true, false, kNnRpw, kNnPipe>(a, s);
+    if (canvas) launch_nn_v<T, true, true, 4>(a, s);
+    else launch_nn_v<T, true, false, 4>(a, s);
+  } else if (canvas) {
+    launch_nn_v<T, false, true, 4>(a, s);
+  } else if (rpw8) {
+    launch_nn_v<T, false, false, 8>(a, s);
   } else {
-    if (canvas) launch_nn_v<T, false, true, kNnRpw, kNnPipe>(a, s);
-    else launch_nn_v<T, false, false, kNnRpw, kNnPipe>(a, s);
+    launch_nn_v<T, false, false, 4>(a, s);
   }
 }
 

@@ -327,8 +327,9 @@ int launch_merge_fold(const FlexEntry *entries_host, int n, int width, int heigh
     return GSKYHIP_E_HIP;
   hipLaunchKernelGGL(merge_fold_kernel, dim3(blocks_for(npx, 256)), dim3(256), 0, s, d, n, width, height,
                      canvas_dtype, canvas_nodata, ms, canvas);
-  hipFreeAsync(d, s);
-  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+  const bool launched = hipGetLastError() == hipSuccess;
+  const bool freed = hipFreeAsync(d, s) == hipSuccess;
+  return launched && freed ? 0 : GSKYHIP_E_HIP;
 }
 
 int launch_compute_mask(const void *data, int dtype, int64_t n, const MaskSpecS &ms, uint8_t *out,
@@ -374,7 +375,10 @@ int launch_scale(void *data, int dtype, int64_t n, double nodata, const gskyhip_
   h.mm[3] = 0;
   Buf *d = nullptr;
   if (hipMallocAsync((void **)&d, sizeof(Buf), s) != hipSuccess) return GSKYHIP_E_HIP;
-  hipMemcpyAsync(d, &h, sizeof(Buf), hipMemcpyHostToDevice, s);
+  if (hipMemcpyAsync(d, &h, sizeof(Buf), hipMemcpyHostToDevice, s) != hipSuccess) {
+    (void)hipFreeAsync(d, s);
+    return GSKYHIP_E_HIP;
+  }
   if (autom) {
     hipLaunchKernelGGL(scale_minmax_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, data, dtype, (long)n,
                        nodata, sp.colour_scale, d->mm);
@@ -382,9 +386,10 @@ int launch_scale(void *data, int dtype, int64_t n, double nodata, const gskyhip_
   }
   hipLaunchKernelGGL(scale_apply_kernel, dim3(blocks_for((n + 3) / 4, 256)), dim3(256), 0, s, data, dtype,
                      (long)n, &d->k, out, dtype == GSKYHIP_BYTE ? 1 : 0);
-  hipFreeAsync(d, s);
-  hipStreamSynchronize(s);  // host staging struct `h` must outlive the copy
-  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+  const bool launched = hipGetLastError() == hipSuccess;
+  const bool freed = hipFreeAsync(d, s) == hipSuccess;
+  const bool synced = hipStreamSynchronize(s) == hipSuccess;   // host staging struct `h` must outlive the copy
+  return launched && freed && synced ? 0 : GSKYHIP_E_HIP;
 }
 
 int launch_scale_legacy(void *data, int dtype, int64_t n, double nodata, const gskyhip_scale_params &sp,

@@ -55,8 +55,9 @@ def _check(png, rgba, oracle):
 
 
 def test_png_of_rendered_tiles(gpu, oracle):
-    """Palette tiles of a C2 batch (transparent where no granule: RGBA) and a
-    fully covered tile (opaque: RGB), mixed sizes."""
+    """Palette tiles of a C2 batch, mixed sizes (transparent pixels where no
+    granule or the palette's 0xFF index: RGBA; the opaque RGB case is
+    test_png_nrgba_conversion_and_filters' tile 1)."""
     import gsky_amd
     from gsky_amd.encode import encode_png
     cfg = synth.config_c2(scale=0.1, tiles_per_side=3, tile_px=200)
@@ -69,7 +70,7 @@ def test_png_of_rendered_tiles(gpu, oracle):
     kinds = set()
     for t, (w, h) in enumerate(sizes):
         kinds.add(_check(pngs[t], np.ascontiguousarray(host[t, :h, :w]), oracle))
-    assert kinds == {True, False}
+    assert False in kinds
 
 
 def test_png_nrgba_conversion_and_filters(gpu, oracle):
@@ -90,7 +91,7 @@ def test_png_nrgba_conversion_and_filters(gpu, oracle):
     pngs = encode_png(torch.from_numpy(tiles).to(gpu))
     fts = set()
     for t in range(4):
-        _check(pngs[t], tiles[t], oracle)
+        assert _check(pngs[t], tiles[t], oracle) == (t == 1)
         _, rows = oracle.go_png_rows(tiles[t])
         n = len(rows) // h
         fts |= {rows[y * n] for y in range(h)}
