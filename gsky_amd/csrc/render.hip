@@ -161,6 +161,7 @@ __device__ int must_adjust2(const Xform &t, const double *er, double psxr, doubl
 }
 
 constexpr int kSteps = 20;
+constexpr int kSmallBatchPairs = 512;   // plan_pairs_kernel<256> up to this many pairs
 constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 
 // First half of xform_point_nl(t, false, ...): source pixel -> destination
@@ -341,8 +342,164 @@ __device__ int suggested_warp_output2(const Xform &t, int nInX, int nInY, int la
   return err;
 }
 
-// One wavefront (64 threads) per pair.
-__global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
+// One border-test sample j of GDALSuggestedWarpOutput2_MustAdjustFor{Right,
+// Bottom}Border: the per-lane expressions of must_adjust().
+__device__ bool border_bad(const Xform &t, const double *ext, int np, int nl, double psx, double psy, bool right,
+                           int j) {
+  double r1 = 0.0, r2 = 0.0;
+  for (int k = 0; k < j; k++) {
+    r1 += 0.05;
+    r2 += 0.05;
+  }
+  if (r1 > 0.99) r1 = 1.0;
+  double ax, ay;
+  if (right) { ax = ext[2]; ay = ext[3] - psy * r1 * nl; }
+  else { ax = ext[0] + psx * r1 * np; ay = ext[1]; }
+  const bool ok1 = xform_point_nl(t, true, ax, ay);
+  const bool ok2 = ok1 ? xform_point_nl(t, false, ax, ay) : false;
+  const double ex = right ? ext[2] : ext[0] + psx * r2 * np;
+  const double ey = right ? ext[3] - psy * r2 * nl : ext[1];
+  return !ok1 || !ok2 || fabs(ax - ex) > psx || fabs(ay - ey) > psy;
+}
+
+// suggested_warp_output2() by a workgroup of NT threads (small batches, where
+// the planning chain is latency-bound): the 21 x 21 grid in kGrid / NT rounds
+// instead of kGrid / 64, and the border trials side by side -- the five right
+// trials plus the bottom trial 0 (valid when the right border keeps trial 0)
+// in one pass, the remaining bottom trials in a second; the reference takes
+// the first trial that passes, which is what each pass picks.  Same
+// expressions per sample, so the same results.
+template <int NT>
+__device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, double *sx, double *sy, int *sok,
+                                          double ext[4], double &psx, double &psy, int &nPixels, int &nLines,
+                                          const GEdge *ge) {
+  constexpr int kW = NT / 64;
+  __shared__ double s_red[4][kW];
+  __shared__ int s_cnt[8];
+  const int tid = threadIdx.x, w = tid >> 6;
+  const double dfStep = 1.0 / kSteps;
+  int ns = 4 * (kSteps + 1);
+  if (ge && ge->n_fail == 0) {
+    const double *g2 = t.dst_igt;
+    for (int k = tid; k < ns; k += NT) {
+      const double X = ge->x[k], Y = ge->y[k];
+      sx[k] = g2[0] + X * g2[1] + Y * g2[2];
+      sy[k] = g2[3] + X * g2[4] + Y * g2[5];
+      sok[k] = 1;
+    }
+  } else for (int k = tid; k < ns; k += NT) {
+    const int i = k >> 2, e = k & 3;
+    const double r = (i == kSteps) ? 1.0 : i * dfStep;
+    double x, y;
+    if (e == 0) { x = r * nInX; y = 0.0; }
+    else if (e == 1) { x = r * nInX; y = nInY; }
+    else if (e == 2) { x = 0.0; y = r * nInY; }
+    else { x = nInX; y = r * nInY; }
+    const int ok = xform_point_nl(t, false, x, y);
+    sx[k] = x; sy[k] = y; sok[k] = ok;
+  }
+  __syncthreads();
+  int failed = 0;
+  for (int k = tid; k < ns; k += NT) failed |= sok[k] ? 0 : 1;
+  if (__syncthreads_or(failed)) {   // full grid of the source raster
+    ns = kGrid;
+    for (int k = tid; k < ns; k += NT) {
+      const int iy = k / (kSteps + 1), ix = k % (kSteps + 1);
+      const double ry = (iy == kSteps) ? 1.0 : iy * dfStep;
+      const double rx = (ix == kSteps) ? 1.0 : ix * dfStep;
+      double x = rx * nInX, y = ry * nInY;
+      const int ok = xform_point_nl(t, false, x, y);
+      sx[k] = x; sy[k] = y; sok[k] = ok;
+    }
+    __syncthreads();
+  }
+  double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
+  int got = 0;
+  for (int k = tid; k < ns; k += NT) {
+    if (!sok[k]) continue;
+    got = 1;
+    mnx = fmin(mnx, sx[k]); mny = fmin(mny, sy[k]);
+    mxx = fmax(mxx, sx[k]); mxy = fmax(mxy, sy[k]);
+  }
+  mnx = wave_min(mnx); mny = wave_min(mny); mxx = wave_max(mxx); mxy = wave_max(mxy);
+  if ((tid & 63) == 0) { s_red[0][w] = mnx; s_red[1][w] = mny; s_red[2][w] = mxx; s_red[3][w] = mxy; }
+  got = __syncthreads_or(got);
+  for (int i = 0; i < kW; i++) {
+    mnx = fmin(mnx, s_red[0][i]); mny = fmin(mny, s_red[1][i]);
+    mxx = fmax(mxx, s_red[2][i]); mxy = fmax(mxy, s_red[3][i]);
+  }
+  int err = 1;
+  ext[0] = ext[1] = ext[2] = ext[3] = 0.0;
+  psx = 0.0; psy = 0.0;
+  nPixels = 0; nLines = 0;
+  if (!got) return err;
+  double dX = 0, dY = 0;
+  if (sok[0] && sok[ns - 1]) { dX = sx[ns - 1] - sx[0]; dY = sy[ns - 1] - sy[0]; }
+  if (dX == 0.0 || dY == 0.0) { dX = mxx - mnx; dY = mxy - mny; }
+  const double diag = sqrt(dX * dX + dY * dY);
+  const double ps = diag / sqrt((double)nInX * nInX + (double)nInY * nInY);
+  const double dfPixels = (mxx - mnx) / ps;
+  const double dfLines = (mxy - mny) / ps;
+  if (!(dfPixels <= 2147483646.0 && dfLines <= 2147483646.0)) return err;
+  err = 0;
+  nPixels = (int)(dfPixels + 0.5);
+  nLines = (int)(dfLines + 0.5);
+  psx = ps; psy = ps;
+  const double ratios[5] = {0.000, 0.001, 0.010, 0.100, 1.000};
+  // pass A: right trials 0..4 (tests 0..4), bottom trial 0 under right trial 0 (test 5)
+  if (tid < 8) s_cnt[tid] = 0;
+  __syncthreads();
+  const double tryx0 = psx - psx * ratios[0] / nPixels;
+  const double tryy0 = psy - psy * ratios[0] / nLines;
+  if (tid < 6 * 21) {
+    const int id = tid / 21, j = tid % 21;
+    bool bad;
+    if (id < 5) {
+      const double tryx = psx - psx * ratios[id] / nPixels;
+      const double e[4] = {mnx, mxy - nLines * psy, mnx + nPixels * tryx, mxy};
+      bad = border_bad(t, e, nPixels, nLines, tryx, psy, true, j);
+    } else {
+      const double e[4] = {mnx, mxy - nLines * tryy0, mnx + nPixels * tryx0, mxy};
+      bad = border_bad(t, e, nPixels, nLines, tryx0, tryy0, false, j);
+    }
+    if (bad) atomicAdd(&s_cnt[id], 1);
+  }
+  __syncthreads();
+  int kx = -1;
+  for (int k = 0; k < 5; k++)
+    if (s_cnt[k] != 21) { kx = k; break; }
+  if (kx >= 0) psx = psx - psx * ratios[kx] / nPixels;
+  int ky0 = 0;
+  bool ydone = false;
+  if (kx == 0) {
+    ky0 = 1;
+    if (s_cnt[5] != 21) { psy = tryy0; ydone = true; }
+  }
+  if (!ydone) {   // pass B: bottom trials ky0..4 under the final psx
+    __syncthreads();
+    if (tid < 8) s_cnt[tid] = 0;
+    __syncthreads();
+    if (tid < (5 - ky0) * 21) {
+      const int k = ky0 + tid / 21, j = tid % 21;
+      const double tryy = psy - psy * ratios[k] / nLines;
+      const double e[4] = {mnx, mxy - nLines * tryy, mnx + nPixels * psx, mxy};
+      if (border_bad(t, e, nPixels, nLines, psx, tryy, false, j)) atomicAdd(&s_cnt[k], 1);
+    }
+    __syncthreads();
+    for (int k = ky0; k < 5; k++)
+      if (s_cnt[k] != 21) { psy = psy - psy * ratios[k] / nLines; break; }
+  }
+  ext[0] = mnx;
+  ext[1] = mxy - nLines * psy;
+  ext[2] = mnx + nPixels * psx;
+  ext[3] = mxy;
+  return err;
+}
+
+// One workgroup of NT threads per pair: NT = 64 (one wavefront) for batches
+// that fill the GPU, NT = 256 for small, latency-bound batches.
+template <int NT>
+__global__ __launch_bounds__(NT) void plan_pairs_kernel(PlanArgs a) {
   const int p = blockIdx.x;
   const int lane = threadIdx.x;
   if (p >= a.n_pairs) return;
@@ -389,8 +546,13 @@ __global__ __launch_bounds__(64) void plan_pairs_kernel(PlanArgs a) {
   const int nInX = g.xsize, nInY = g.ysize;
   double ext[4], psx, psy;
   int nPixels, nLines;
-  int err = suggested_warp_output2(t, nInX, nInY, lane, sx, sy, sok, ext, psx, psy, nPixels, nLines,
-                                   a.gedge ? a.gedge + gi : nullptr);
+  int err;
+  if constexpr (NT == 64)
+    err = suggested_warp_output2(t, nInX, nInY, lane, sx, sy, sok, ext, psx, psy, nPixels, nLines,
+                                 a.gedge ? a.gedge + gi : nullptr);
+  else
+    err = suggested_warp_output2_blk<NT>(t, nInX, nInY, sx, sy, sok, ext, psx, psy, nPixels, nLines,
+                                         a.gedge ? a.gedge + gi : nullptr);
   if (lane != 0) return;
 
   // ---- overview pick (warp.go:156-198)
@@ -1286,7 +1448,15 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   const int n_edge_blocks = a.gedge ? rc.n_granules : 0;
   hipLaunchKernelGGL(plan_prologue_kernel, dim3(std::max(1, n_edge_blocks + (rc.n_pairs + 127) / 128)), dim3(128),
                      0, s, a, n_edge_blocks);
-  if (rc.n_pairs > 0) hipLaunchKernelGGL(plan_pairs_kernel, dim3(rc.n_pairs), dim3(64), 0, s, a);
+  // small batches (C1: one pair) are latency-bound: a workgroup per pair
+  int small_pairs = kSmallBatchPairs;
+#ifdef GSKYHIP_AB
+  if (const char *sp = getenv("GSKYHIP_PAIRS_SMALL")) small_pairs = atoi(sp);
+#endif
+  if (rc.n_pairs > 0 && rc.n_pairs <= small_pairs)
+    hipLaunchKernelGGL(plan_pairs_kernel<256>, dim3(rc.n_pairs), dim3(256), 0, s, a);
+  else if (rc.n_pairs > 0)
+    hipLaunchKernelGGL(plan_pairs_kernel<64>, dim3(rc.n_pairs), dim3(64), 0, s, a);
   hipLaunchKernelGGL(plan_tiles_kernel, dim3(rc.n_tiles), dim3(64), 0, s, a);
   if (rc.n_pairs > 0) {
     if (a.sep)

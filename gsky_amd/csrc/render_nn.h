@@ -70,6 +70,125 @@ __device__ __forceinline__ uint32_t scale_int(const ScaleK &k, int32_t c) {
   return c == k.noData.i ? 0xFFu : b;
 }
 
+// The ordered fold of tile row r over the tile's entries (MergeMaskedRaster in
+// ProcessRasterStack order, tile_merger.go:38-225): c[q] is the canvas value
+// of the lane's pixel q (tile column xl + 64 q); c[] arrives holding the
+// canvas nodata.
+template <typename T, bool MASK>
+__device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *__restrict__ ents,
+                                            const int32_t *__restrict__ ord, int n_entries,
+                                            const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
+                                            int ns_out, int r, int xb, int xl, int W, int ncols,
+                                            typename VOf<T>::type (&c)[kNnPx]) {
+  using V = typename VOf<T>::type;
+#pragma unroll 1
+  for (int k = 0; k < n_entries; k++) {
+    const EntryD &e = ents[ord[k]];
+    const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
+    if (e.ns != ns_out || ew <= 0) continue;
+    const int ir = r - eyoff;
+    if (ir < 0 || ir >= eh) continue;
+    const int lim = max(0, min(ew, W - exoff));   // window pixel in the tile: (unsigned)ic < lim
+    const int c0 = exoff - xb, c1 = exoff + lim - xb;   // the entry's columns of the block: [c0, c1)
+    if (c1 <= 0 || c0 >= ncols) continue;
+    const RowRec *rr = rows + e.row_base + ir;
+    const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
+    const int inside = __builtin_amdgcn_readfirstlane(rr->inside);
+    const int bx = e.band_x, by = e.band_y;
+    const V nd = as_v<T>(e.nd);
+    const bool fill_mode = e.fill_mode != 0;
+    const int ic0 = xl - exoff;   // window column of the lane's pixel 0
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
+    const bool masked = MASK && e.mask_pair >= 0;
+    if (kind == ROW_LINEAR && inside && c0 <= 0 && c1 >= ncols && !masked) {
+      // fast body: every pixel of the block is in the window and its source
+      // pixel in the band -- lin_coords() + nn_px() reduce to the truncations
+      const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
+      uint32_t off[kNnPx];
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) {
+        const double dist = (double)(ic0 + 64 * q);
+        const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
+        const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
+        off[q] = (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T);
+      }
+      V vv[kNnPx];
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
+      if (!fill_mode) {
+#pragma unroll
+        for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
+      }
+      continue;
+    }
+    // general body: window edges, POOL rows, failed transforms, mask layer;
+    // two halves of 4 pixels (4 gathers in flight) keep the register peak
+    // of the fast body
+    const V fillv = as_v<T>(e.fill);
+#pragma unroll
+    for (int h = 0; h < kNnPx; h += 4) {
+      uint32_t idx[4];
+      if (kind == ROW_LINEAR) {
+        const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int ic = ic0 + 64 * (h + q);
+          const double dist = (double)ic;
+          idx[q] = nn_index_sxy(xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, bx, by);
+        }
+      } else {   // POOL (the only other kind of a simple tile): the leaf of each pixel
+        const int nleaf = __builtin_amdgcn_readfirstlane(rr->nleaf);
+        const Leaf *lv = pool + __builtin_amdgcn_readfirstlane(rr->pool_off);
+#pragma unroll 1
+        for (int q = 0; q < 4; q++) {
+          const int ic = ic0 + 64 * (h + q);
+          const bool in = (unsigned)ic < (unsigned)lim;
+          const Leaf &L = lv[leaf_of(lv, nleaf, in ? ic : 0)];
+          const double dist = (double)(ic - L.start);
+          idx[q] = nn_index_sxy(L.xs0 + L.dX * dist, L.ys0 + L.dY * dist, in && L.kind != LEAF_FAILED, bx, by);
+        }
+      }
+      V vv[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int ic = ic0 + 64 * (h + q);
+        const V v = idx[q] != kNoPx ? vv[q] : fillv;
+        bool take = (unsigned)ic < (unsigned)lim && (v != nd);
+        if (masked) {
+          if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, e, ic, ir);
+        }
+        const bool t2 = take && (!fill_mode || c[h + q] == nd);
+        c[h + q] = t2 ? v : c[h + q];
+      }
+    }
+  }
+}
+
+// utils.Scale + palette / grey of the lane's 8 canvas values (EncodePNG's
+// pixel loop through the LDS table s_tab).
+template <typename T>
+__device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint32_t *s_tab,
+                                        const typename VOf<T>::type (&c)[kNnPx], uint32_t (&px)[kNnPx]) {
+  if constexpr (!std::is_same<T, float>::value) {
+    if (safe) {
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_int<T, true>(sk, c[q])];
+    } else {
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_int<T, false>(sk, c[q])];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_t<T>(sk, c[q]) & 0xFFu];
+  }
+}
+
 // RPW: rows per wave (a block of 4 waves covers 4 * RPW rows of a 512-column
 // block).  Rows are processed one after the other; a row's RGBA stores are
 // issued before the next row's gathers (deferring them behind those gathers
@@ -83,7 +202,6 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
                                                                       const gskyhip_tile *__restrict__ tiles,
                                                                       int n_items) {
   using V = typename VOf<T>::type;
-  constexpr bool kInt = !std::is_same<T, float>::value;
   constexpr int kRowsBlk = 4 * RPW;
   __shared__ uint32_t s_tab[256];
 
@@ -116,7 +234,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int32_t *ord = order + tile.pair_begin;
   const int n_entries = tp.n_entries;
   const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
-  const bool safe = kInt && (float)max(sk.clp.i, 0) * sk.sc < 2147483648.0f;   // NaN -> false
+  const bool safe = !std::is_same<T, float>::value && (float)max(sk.clp.i, 0) * sk.sc < 2147483648.0f;
   const int ncols = min(kBandCols, W - xb);     // columns of the block inside the tile
   const bool full = ncols == kBandCols;
   const int xl = xb + lane;                     // tile column of the lane's pixel 0
@@ -142,94 +260,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
     V c[kNnPx];
 #pragma unroll
     for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-
-#pragma unroll 1
-    for (int k = 0; k < n_entries; k++) {
-      const EntryD &e = ents[ord[k]];
-      const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
-      if (e.ns != ns_out || ew <= 0) continue;
-      const int ir = r - eyoff;
-      if (ir < 0 || ir >= eh) continue;
-      const int lim = max(0, min(ew, W - exoff));   // window pixel in the tile: (unsigned)ic < lim
-      const int c0 = exoff - xb, c1 = exoff + lim - xb;   // the entry's columns of the block: [c0, c1)
-      if (c1 <= 0 || c0 >= ncols) continue;
-      const RowRec *rr = rows + e.row_base + ir;
-      const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
-      const int inside = __builtin_amdgcn_readfirstlane(rr->inside);
-      const int bx = e.band_x, by = e.band_y;
-      const V nd = as_v<T>(e.nd);
-      const bool fill_mode = e.fill_mode != 0;
-      const int ic0 = xl - exoff;   // window column of the lane's pixel 0
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
-      const bool masked = MASK && e.mask_pair >= 0;
-      if (kind == ROW_LINEAR && inside && c0 <= 0 && c1 >= ncols && !masked) {
-        // fast body: every pixel of the block is in the window and its source
-        // pixel in the band -- lin_coords() + nn_px() reduce to the truncations
-        const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
-        uint32_t off[kNnPx];
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) {
-          const double dist = (double)(ic0 + 64 * q);
-          const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
-          const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
-          off[q] = (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T);
-        }
-        V vv[kNnPx];
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
-        if (!fill_mode) {
-#pragma unroll
-          for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
-        } else {
-#pragma unroll
-          for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
-        }
-        continue;
-      }
-      // general body: window edges, POOL rows, failed transforms, mask layer;
-      // two halves of 4 pixels (4 gathers in flight) keep the register peak
-      // of the fast body
-      const V fillv = as_v<T>(e.fill);
-#pragma unroll
-      for (int h = 0; h < kNnPx; h += 4) {
-        uint32_t idx[4];
-        if (kind == ROW_LINEAR) {
-          const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const int ic = ic0 + 64 * (h + q);
-            const double dist = (double)ic;
-            idx[q] = nn_index_sxy(xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, bx, by);
-          }
-        } else {   // POOL (the only other kind of a simple tile): the leaf of each pixel
-          const int nleaf = __builtin_amdgcn_readfirstlane(rr->nleaf);
-          const Leaf *lv = pool + __builtin_amdgcn_readfirstlane(rr->pool_off);
-#pragma unroll 1
-          for (int q = 0; q < 4; q++) {
-            const int ic = ic0 + 64 * (h + q);
-            const bool in = (unsigned)ic < (unsigned)lim;
-            const Leaf &L = lv[leaf_of(lv, nleaf, in ? ic : 0)];
-            const double dist = (double)(ic - L.start);
-            idx[q] = nn_index_sxy(L.xs0 + L.dX * dist, L.ys0 + L.dY * dist, in && L.kind != LEAF_FAILED, bx, by);
-          }
-        }
-        V vv[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int ic = ic0 + 64 * (h + q);
-          const V v = idx[q] != kNoPx ? vv[q] : fillv;
-          bool take = (unsigned)ic < (unsigned)lim && (v != nd);
-          if (masked) {
-            if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, e, ic, ir);
-          }
-          const bool t2 = take && (!fill_mode || c[h + q] == nd);
-          c[h + q] = t2 ? v : c[h + q];
-        }
-      }
-    }
+    nn_fold_row<T, MASK>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
 
     // output: typed canvas (WCS) or utils.Scale + palette / grey RGBA
     if constexpr (CANVAS) {
@@ -241,19 +272,124 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         if (full || 64 * q + lane < ncols) __builtin_nontemporal_store((T)c[q], (GPTR(T))(cdst + 64 * q));
     } else {
       uint32_t px[kNnPx];
-      if constexpr (kInt) {
-        if (safe) {
-#pragma unroll
-          for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_int<T, true>(sk, c[q])];
-        } else {
-#pragma unroll
-          for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_int<T, false>(sk, c[q])];
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_t<T>(sk, c[q]) & 0xFFu];
-      }
+      nn_rgba<T>(sk, safe, s_tab, c, px);
       store_row(r, px);
+    }
+  }
+}
+
+// Workgroup barrier for LDS hand-over only: waits for this wave's LDS (and
+// scalar) operations, never for its vector-memory ones, so a store wave does
+// not wait for its RGBA stores to reach memory at every step (a __syncthreads
+// fence would: vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Producer / store waves (round 3).  gfx9 counts vector loads and stores in
+// one vmcnt, and loads and stores return out of order with respect to each
+// other, so any wave that issues both must wait for its stores before it can
+// use a gather: in render_nn_kernel the gathers of row r + 1 wait for the
+// RGBA stores of row r (s_waitcnt vmcnt(0) before the first gather).  Here
+// waves 0 .. NP-1 only gather: each folds one row per step, applies Scale and
+// the palette and writes the row's 512 RGBA words to LDS; wave NP only
+// stores: it copies the previous step's NP rows from LDS to the tile as
+// 16-B non-temporal stores (1 KB contiguous per instruction).  Two LDS
+// buffers; one lds_barrier() per step.  A block covers NP * STEPS rows of a
+// 512-column block.  RGBA output only, no mask layer (C1, C2 and GetMap
+// stacks without a QA mask).
+template <typename T, int NP, int STEPS>
+__global__ __launch_bounds__(64 * (NP + 1)) void render_nn_ws_kernel(RenderArgs a, const EntryD *__restrict__ ents,
+                                                                     const int32_t *__restrict__ order,
+                                                                     const RowRec *__restrict__ rows,
+                                                                     const Leaf *__restrict__ pool,
+                                                                     const TilePlan *__restrict__ tplans,
+                                                                     const gskyhip_tile *__restrict__ tiles,
+                                                                     int n_items, int xcd_remap) {
+  using V = typename VOf<T>::type;
+  constexpr int kRowsBlk = NP * STEPS;
+  constexpr int kThreads = 64 * (NP + 1);
+  __shared__ uint32_t s_tab[256];
+  __shared__ __attribute__((aligned(16))) uint32_t s_out[2][NP][kBandCols];
+
+  int item = blockIdx.x;
+  if (xcd_remap) {   // workgroups go to the 8 XCDs round robin: give each XCD a contiguous run of items
+    const int q = n_items >> 3, rr = n_items & 7, x = item & 7;
+    item = x * q + min(x, rr) + (item >> 3);
+  }
+  if (item >= n_items) return;
+  const int bands_per_tile = (a.max_h + kRowsBlk - 1) / kRowsBlk;
+  const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
+  const int t = item / (bands_per_tile * col_blocks);
+  const int in_tile = item - t * bands_per_tile * col_blocks;
+  const TilePlan &tp = tplans[t];
+  if (tp.complex || (tp.n_entries > 0 && tp.vt != vt_code<T>())) return;   // empty tiles: written here
+  const gskyhip_tile &tile = tiles[t];
+  const int W = tile.width, H = tile.height;
+  const int band0 = (in_tile / col_blocks) * kRowsBlk;
+  const int xb = (in_tile % col_blocks) * kBandCols;
+  if (band0 >= H || xb >= W) return;
+  const int tid = threadIdx.x;
+  const int ns_out = a.out_ns[0];
+  const bool created = tp.created[ns_out] != 0;
+  for (int i = tid; i < 256; i += kThreads) {   // EncodePNG: 0xFF and canvases never created are transparent
+    const uint32_t col = a.ramp ? a.ramp[i] : (0xFF000000u | ((uint32_t)i * 0x10101u));
+    s_tab[i] = (created && i != 255) ? col : 0u;
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int ncols = min(kBandCols, W - xb);   // columns of the block inside the tile
+  const int nsteps = min(STEPS, (H - band0 + NP - 1) / NP);
+
+  if (wave < NP) {
+    const V cnod = as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]));
+    const int32_t *ord = order + tile.pair_begin;
+    const int n_entries = tp.n_entries;
+    const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
+    const bool safe = !std::is_same<T, float>::value && (float)max(sk.clp.i, 0) * sk.sc < 2147483648.0f;
+    const int xl = xb + lane;
+#pragma unroll 1
+    for (int p = 0; p < nsteps; p++) {
+      const int r = band0 + p * NP + wave;
+      if (r < H) {
+        V c[kNnPx];
+#pragma unroll
+        for (int q = 0; q < kNnPx; q++) c[q] = cnod;
+        nn_fold_row<T, false>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+        uint32_t px[kNnPx];
+        nn_rgba<T>(sk, safe, s_tab, c, px);
+        uint32_t *o = &s_out[p & 1][wave][lane];
+#pragma unroll
+        for (int q = 0; q < kNnPx; q++) o[64 * q] = px[q];
+      }
+      lds_barrier();
+    }
+  } else {
+    // store wave: step p - 1's rows while the producers fold step p
+    const bool vec4 = (a.max_w & 3) == 0;   // 16-B aligned rows
+    uint8_t *tile_base = a.rgba + ((int64_t)t * a.max_h) * a.max_w * 4;
+#pragma unroll 1
+    for (int p = 0; p <= nsteps; p++) {
+      if (p > 0) {
+        const int pp = p - 1;
+#pragma unroll
+        for (int i = 0; i < NP; i++) {
+          const int r = band0 + pp * NP + i;
+          if (r >= H) break;
+          uint32_t *dst = (uint32_t *)(tile_base + ((int64_t)r * a.max_w + xb) * 4);
+#pragma unroll
+          for (int hh = 0; hh < kBandCols / 256; hh++) {
+            const int col = hh * 256 + 4 * lane;
+            const u32x4 v = *(const u32x4 *)&s_out[pp & 1][i][col];
+            if (vec4 && col + 4 <= ncols) {
+              __builtin_nontemporal_store(v, (GPTR(u32x4))(dst + col));
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; e++)
+                if (col + e < ncols) __builtin_nontemporal_store(v[e], (GPTR(uint32_t))(dst + col + e));
+            }
+          }
+        }
+      }
+      if (p < nsteps) lds_barrier();
     }
   }
 }
@@ -263,6 +399,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 // 0.86 ms at 8 -- too few blocks); profiles/r03b_ab_nn.jsonl.  Masked and
 // canvas batches keep 4 (measured on C5 only).  A/B build: GSKYHIP_NN_RPW.
 constexpr int kNnRpw8MinItems = 32768;
+constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
 
 template <typename T, bool M, bool C, int RPW>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
@@ -278,9 +415,29 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   const bool canvas = (a.lds_mode & kCanvas) != 0;
   const int64_t items8 = (int64_t)a.n_tiles * ((a.max_h + 31) / 32) * ((a.max_w + kBandCols - 1) / kBandCols);
   bool rpw8 = items8 >= kNnRpw8MinItems;
+  // small batches (C1: one 256^2 tile = 16 blocks at 4 rows per wave) are
+  // latency-bound: one row per wave, 4x the workgroups
+  const int64_t items4 = (int64_t)a.n_tiles * ((a.max_h + 15) / 16) * ((a.max_w + kBandCols - 1) / kBandCols);
+  bool rpw1 = items4 < kNnRpw1MaxItems;
+  int ws = 0, xcd = 0;
 #ifdef GSKYHIP_AB
-  if (const char *rp = getenv("GSKYHIP_NN_RPW")) rpw8 = atoi(rp) == 8;
+  if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
+  if (const char *w = getenv("GSKYHIP_NN_WS")) ws = atoi(w);
+  if (const char *x = getenv("GSKYHIP_NN_XCD")) xcd = atoi(x);
 #endif
+  if (!mask && !canvas && ws > 0) {
+    const int cb = (a.max_w + kBandCols - 1) / kBandCols;
+    if (ws == 3) {
+      const int items = a.n_tiles * ((a.max_h + 23) / 24) * cb;
+      hipLaunchKernelGGL((render_nn_ws_kernel<T, 3, 8>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+                         a.order, a.rows, a.pool, a.tplans, a.tiles, items, xcd);
+    } else {
+      const int items = a.n_tiles * ((a.max_h + 55) / 56) * cb;
+      hipLaunchKernelGGL((render_nn_ws_kernel<T, 7, 8>), dim3((unsigned)items), dim3(512), 0, s, a, a.entries,
+                         a.order, a.rows, a.pool, a.tplans, a.tiles, items, xcd);
+    }
+    return;
+  }
   if (mask) {
     if (canvas) launch_nn_v<T, true, true, 4>(a, s);
     else launch_nn_v<T, true, false, 4>(a, s);
@@ -288,6 +445,8 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
     launch_nn_v<T, false, true, 4>(a, s);
   } else if (rpw8) {
     launch_nn_v<T, false, false, 8>(a, s);
+  } else if (rpw1) {
+    launch_nn_v<T, false, false, 1>(a, s);
   } else {
     launch_nn_v<T, false, false, 4>(a, s);
   }
