@@ -53,6 +53,7 @@ struct PlanArgs {
   int sep;                     // 1: plan_rows uses the separable transform where it applies
   int n_granules;
   struct GEdge *gedge;         // per granule: SuggestedWarpOutput2 edge samples in dst georef (or NULL)
+  int small;                   // 1: plan_pairs finds each pair's tile itself, plan_small_kernel plans the rest
 };
 
 // The 84 edge samples of GDALSuggestedWarpOutput2 taken through the
@@ -162,6 +163,7 @@ __device__ int must_adjust2(const Xform &t, const double *er, double psxr, doubl
 
 constexpr int kSteps = 20;
 constexpr int kSmallBatchPairs = 512;   // plan_pairs_kernel<256> up to this many pairs
+constexpr int kSmallBatchTiles = 8, kSmallBatchPlanPairs = 32;   // plan_small_kernel batches
 constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 
 // First half of xform_point_nl(t, false, ...): source pixel -> destination
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(NT) void plan_pairs_kernel(PlanArgs a) {
   __shared__ double sx[kGrid], sy[kGrid];
   __shared__ int sok[kGrid];
 
-  const int t_idx = a.pair_tile[p];
+  const int t_idx = a.small ? owning_tile(a.tiles, a.n_tiles, p) : a.pair_tile[p];
   if (t_idx < 0) {   // unreferenced pair: an empty plan nothing reads
     if (lane == 0) {
       PairPlan z = {};
@@ -797,10 +799,23 @@ constexpr int kWavePairs = 256;   // pairs per tile the wave-parallel merge plan
 //   rank(p)   = #{q: stamp_q > stamp_p} + #{q < p: stamp_q == stamp_p}
 //   fill(k)   = ts_k < max(0, max{ts_j: j before k in the order, same ns})
 //   status    = the last error in merge order (the serial walk's last write).
-__global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
-  const int t = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (t >= a.n_tiles) return;
+// The LDS of one wave's tile (plan_tile_wave).
+struct TileLds {
+  double stamp[kWavePairs], ts[kWavePairs];
+  int32_t info[kWavePairs];   // in_stack | is_mask << 1 | (ns + 1) << 2 | out_dtype << 8
+  int32_t rank[kWavePairs];   // merge position of an in-stack pair, -1 otherwise
+};
+
+// Synchronisation of the 64 lanes of one wavefront: its LDS and global
+// accesses are performed in program order, so this only keeps the compiler
+// from moving memory operations across it.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lane, TileLds &L) {
   const gskyhip_tile &tile = a.tiles[t];
   const int b = tile.pair_begin, e = tile.pair_end, np = e - b;
   const bool bad_size = tile.width <= 0 || tile.height <= 0 || tile.width > a.max_w || tile.height > a.max_h;
@@ -808,16 +823,15 @@ __global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
     if (lane == 0) plan_tile_serial(a, t);
     return;
   }
-  __shared__ double s_stamp[kWavePairs], s_ts[kWavePairs];
-  __shared__ int32_t s_info[kWavePairs];   // in_stack | is_mask << 1 | (ns + 1) << 2 | out_dtype << 8
-  __shared__ int32_t s_rank[kWavePairs];   // merge position of an in-stack pair, -1 otherwise
+  double *s_stamp = L.stamp, *s_ts = L.ts;
+  int32_t *s_info = L.info, *s_rank = L.rank;
   for (int i = lane; i < np; i += 64) {
     const PairPlan &pp = a.pairs[b + i];
     s_stamp[i] = pp.stamp;
     s_ts[i] = pp.ts;
     s_info[i] = (pp.in_stack ? 1 : 0) | (pp.is_mask ? 2 : 0) | ((pp.ns + 1) << 2) | (pp.out_dtype << 8);
   }
-  __syncthreads();
+  wave_sync();
   // merge order
   for (int i = lane; i < np; i += 64) {
     int rk = -1;
@@ -830,7 +844,7 @@ __global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
     }
     s_rank[i] = rk;
   }
-  __syncthreads();
+  wave_sync();
   // per merged entry: maskMap link, fill mode, first-of-namespace, error
   int n_local = 0;
   for (int i = lane; i < np; i += 64) n_local += (s_info[i] & 1);
@@ -885,7 +899,7 @@ __global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
 #pragma unroll
     for (int s2 = 0; s2 < 4; s2++) first_k[s2] = min(first_k[s2], __shfl_xor(first_k[s2], o, 64));
   }
-  __syncthreads();   // fill_mode / mask_pair of every pair written (same workgroup)
+  wave_sync();   // fill_mode / mask_pair of every pair written (same workgroup)
   // render descriptors of every pair (mask pairs included) + value-type vote
   int vmin = 0x7FFFFFFF, vmax = -1;
   bool vzero = false;
@@ -923,6 +937,13 @@ __global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
   a.tplans[t] = tp;
 }
 
+__global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
+  const int t = blockIdx.x;
+  if (t >= a.n_tiles) return;
+  __shared__ TileLds L;
+  plan_tile_wave(a, t, threadIdx.x, L);
+}
+
 // ---------------------------------------------------------------- row plans
 __device__ __forceinline__ void flag_complex(const PlanArgs &a, int tile) {
   if (atomicOr(&a.tplans[tile].complex, 1) == 0) {
@@ -945,8 +966,7 @@ __device__ __forceinline__ Leaf pending_leaf(int p, int row, int i) {
 
 // Column parts of the separable transform (gsky_device.h) at the three
 // columns every row record transforms: first, middle, last.
-__global__ __launch_bounds__(256) void plan_cols_kernel(PlanArgs a) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void plan_col(const PlanArgs &a, int64_t gid) {
   const int p = (int)(gid / 3), k = (int)(gid % 3);
   if (p >= a.n_pairs) return;
   const PairPlan &pp = a.pairs[p];
@@ -955,6 +975,10 @@ __global__ __launch_bounds__(256) void plan_cols_kernel(PlanArgs a) {
   const int n = pp.w, nMiddle = (n - 1) / 2;
   const int col = k == 0 ? 0 : (k == 1 ? nMiddle : n - 1);
   a.sepcols[3 * (int64_t)p + k] = sep_col(t, col + 0.5 + pp.xoff, 0.5 + pp.yoff);
+}
+
+__global__ __launch_bounds__(256) void plan_cols_kernel(PlanArgs a) {
+  plan_col(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // Light pass, one thread per (pair, window row): the three exact points of
@@ -1116,9 +1140,8 @@ __device__ __noinline__ int approx_leaves(const Xform &t, int xoff, double yrow,
 // every EXACT piece expanded into per-pixel pending leaves; EXACT rows: one
 // pending leaf per pixel.  The row becomes ROW_POOL; on pool overflow it keeps
 // its kind and the tile goes to the general kernel.
-__global__ __launch_bounds__(64) void plan_split_kernel(PlanArgs a) {
-  const int nsplit = a.counters[1];
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nsplit; k += gridDim.x * blockDim.x) {
+__device__ void plan_split_one(const PlanArgs &a, int k) {
+  {
     const int64_t key = a.split_list[k];
     const int p = (int)(key / a.max_h), row = (int)(key % a.max_h);
     const PairPlan &pp = a.pairs[p];
@@ -1126,12 +1149,12 @@ __global__ __launch_bounds__(64) void plan_split_kernel(PlanArgs a) {
     if (rec.kind == ROW_EXACT) {
       const int n = pp.w;
       const int off = atomicAdd(&a.counters[0], n);
-      if (off + n > a.pool_cap) { flag_complex(a, pp.tile); continue; }
+      if (off + n > a.pool_cap) { flag_complex(a, pp.tile); return; }
       for (int j = 0; j < n; j++) a.pool[off + j] = pending_leaf(p, row, j);
       rec.kind = ROW_POOL;
       rec.nleaf = n;
       rec.pool_off = off;
-      continue;
+      return;
     }
     const double yrow = row + 0.5 + pp.yoff;
     Leaf local[kMaxLeavesLocal];
@@ -1144,7 +1167,7 @@ __global__ __launch_bounds__(64) void plan_split_kernel(PlanArgs a) {
       off = atomicAdd(&a.counters[0], total);
       if (off + total > a.pool_cap) off = -1;
     }
-    if (off < 0) { flag_complex(a, pp.tile); continue; }   // stays ROW_DESCEND
+    if (off < 0) { flag_complex(a, pp.tile); return; }   // stays ROW_DESCEND
     int m = off;
     for (int j = 0; j < nl; j++) {
       if (local[j].kind == LEAF_LINEAR) {
@@ -1160,15 +1183,19 @@ __global__ __launch_bounds__(64) void plan_split_kernel(PlanArgs a) {
   }
 }
 
+__global__ __launch_bounds__(64) void plan_split_kernel(PlanArgs a) {
+  const int nsplit = a.counters[1];
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nsplit; k += gridDim.x * blockDim.x) plan_split_one(a, k);
+}
+
 // Exact points of the pending leaves (GDALGenImgProjTransform per pixel, the
 // expressions of exact_coords()), one thread per pool entry.
-__global__ __launch_bounds__(256) void plan_exact_kernel(PlanArgs a) {
-  const int used = min(a.counters[0], a.pool_cap);
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < used; k += gridDim.x * blockDim.x) {
+__device__ __forceinline__ void plan_exact_one(const PlanArgs &a, int k) {
+  {
     Leaf L = a.pool[k];
-    if (L.kind != LEAF_PENDING) continue;
+    if (L.kind != LEAF_PENDING) return;
     const int p = (int)L.dX, row = (int)L.dY;
-    if (p < 0 || p >= a.n_pairs || row < 0 || row >= a.max_h) continue;   // stale slot of an abandoned reservation
+    if (p < 0 || p >= a.n_pairs || row < 0 || row >= a.max_h) return;   // stale slot of an abandoned reservation
     const PairPlan &pp = a.pairs[p];
     double sx, sy;
     const bool ok = exact_coords(a.xforms[p], pp.xoff, pp.yoff, L.start, row, sx, sy);
@@ -1176,6 +1203,40 @@ __global__ __launch_bounds__(256) void plan_exact_kernel(PlanArgs a) {
     L.kind = ok ? LEAF_LINEAR : LEAF_FAILED;
     a.pool[k] = L;
   }
+}
+
+__global__ __launch_bounds__(256) void plan_exact_kernel(PlanArgs a) {
+  const int used = min(a.counters[0], a.pool_cap);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < used; k += gridDim.x * blockDim.x) plan_exact_one(a, k);
+}
+
+// Small batches (C1: one tile), where every planning kernel is a few us of
+// dispatch for a few us of work: plan_tiles, plan_cols, plan_rows,
+// plan_split and plan_exact as the phases of ONE workgroup (waves take tiles,
+// threads take columns, rows, split rows and pending leaves; a workgroup
+// barrier between phases).  The same device bodies as the separate kernels,
+// so the same plan.  Also zeroes the counters (the prologue does not run).
+__global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
+  __shared__ TileLds L[4];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid < 64) a.counters[tid] = 0;
+  __syncthreads();
+  for (int t = wave; t < a.n_tiles; t += 4) plan_tile_wave(a, t, lane, L[wave]);
+  __syncthreads();
+  if (a.sep)
+    for (int64_t g = tid; g < 3 * (int64_t)a.n_pairs; g += 256) plan_col(a, g);
+  __syncthreads();
+  for (int64_t i = tid; i < (int64_t)a.n_pairs * a.max_h; i += 256) {
+    const int p = (int)(i / a.max_h), row = (int)(i % a.max_h);
+    const PairPlan &pp = a.pairs[p];
+    if (row < pp.h) plan_row(a, p, pp, a.xforms[p], row);
+  }
+  __syncthreads();
+  const int nsplit = a.counters[1];
+  for (int k = tid; k < nsplit; k += 256) plan_split_one(a, k);
+  __syncthreads();
+  const int used = min(a.counters[0], a.pool_cap);
+  for (int k = tid; k < used; k += 256) plan_exact_one(a, k);
 }
 
 }  // namespace gsky
@@ -1438,6 +1499,18 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   // with the pairs' owning tiles
   a.n_granules = rc.n_granules;
   a.gedge = nullptr;
+  // small batches: pairs (a workgroup each, own edge samples and owning
+  // tile), then every later planning step in one workgroup -- 2 launches
+  bool small = rc.n_tiles <= kSmallBatchTiles && rc.n_pairs > 0 && rc.n_pairs <= kSmallBatchPlanPairs;
+#ifdef GSKYHIP_AB
+  if (const char *sm = getenv("GSKYHIP_PLAN_SMALL")) small = small && atoi(sm) != 0;
+#endif
+  a.small = small ? 1 : 0;
+  if (small) {
+    hipLaunchKernelGGL(plan_pairs_kernel<256>, dim3(rc.n_pairs), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(plan_small_kernel, dim3(1), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+  }
   bool ge_on = true;   // per-granule edge table; false = per-pair edge transforms
 #ifdef GSKYHIP_AB
   if (const char *ge_env = getenv("GSKYHIP_GRANULE_EDGES")) ge_on = atoi(ge_env) != 0;

@@ -284,6 +284,32 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 // fence would: vmcnt(0)).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Store wave of the producer / store-wave kernels: n (<= NP) rows of 512
+// 4-byte words from LDS to global rows `stride` elements apart starting at
+// dst, 16 B per lane (1 KB contiguous per instruction) when the rows are
+// 16-B aligned, else a word at a time; columns >= ncols are not written.
+template <int NP>
+__device__ __forceinline__ void ws_store_rows(const uint32_t (*src)[kBandCols], int n, uint32_t *dst, int64_t stride,
+                                              bool vec4, int ncols, int lane) {
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+    if (i >= n) break;
+#pragma unroll
+    for (int hh = 0; hh < kBandCols / 256; hh++) {
+      const int col = hh * 256 + 4 * lane;
+      const u32x4 v = *(const u32x4 *)&src[i][col];
+      if (vec4 && col + 4 <= ncols) {
+        __builtin_nontemporal_store(v, (GPTR(u32x4))(dst + col));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+          if (col + e < ncols) __builtin_nontemporal_store(v[e], (GPTR(uint32_t))(dst + col + e));
+      }
+    }
+    dst += stride;
+  }
+}
+
 // Producer / store waves (round 3).  gfx9 counts vector loads and stores in
 // one vmcnt, and loads and stores return out of order with respect to each
 // other, so any wave that issues both must wait for its stores before it can
@@ -364,30 +390,13 @@ __global__ __launch_bounds__(64 * (NP + 1)) void render_nn_ws_kernel(RenderArgs 
     }
   } else {
     // store wave: step p - 1's rows while the producers fold step p
-    const bool vec4 = (a.max_w & 3) == 0;   // 16-B aligned rows
-    uint8_t *tile_base = a.rgba + ((int64_t)t * a.max_h) * a.max_w * 4;
+    uint32_t *row0 = (uint32_t *)(a.rgba + ((int64_t)t * a.max_h * a.max_w + xb) * 4);
 #pragma unroll 1
     for (int p = 0; p <= nsteps; p++) {
       if (p > 0) {
-        const int pp = p - 1;
-#pragma unroll
-        for (int i = 0; i < NP; i++) {
-          const int r = band0 + pp * NP + i;
-          if (r >= H) break;
-          uint32_t *dst = (uint32_t *)(tile_base + ((int64_t)r * a.max_w + xb) * 4);
-#pragma unroll
-          for (int hh = 0; hh < kBandCols / 256; hh++) {
-            const int col = hh * 256 + 4 * lane;
-            const u32x4 v = *(const u32x4 *)&s_out[pp & 1][i][col];
-            if (vec4 && col + 4 <= ncols) {
-              __builtin_nontemporal_store(v, (GPTR(u32x4))(dst + col));
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; e++)
-                if (col + e < ncols) __builtin_nontemporal_store(v[e], (GPTR(uint32_t))(dst + col + e));
-            }
-          }
-        }
+        const int r = band0 + (p - 1) * NP;
+        ws_store_rows<NP>(s_out[(p - 1) & 1], min(NP, H - r), row0 + (int64_t)r * a.max_w, a.max_w,
+                          (a.max_w & 3) == 0, ncols, lane);
       }
       if (p < nsteps) lds_barrier();
     }

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void read16(const uint4 *__restrict__ in, size
     const uint4 v = in[i];
     acc ^= v.x ^ v.y ^ v.z ^ v.w;
   }
-  if (acc == 0x12345678u) sink[0] = acc;
+  if (acc == 0x1234u) sink[0] = acc;   // reachable for 16-bit values too (else the loop is dead code)
 }
 
 template <typename T>
@@ -41,14 +41,14 @@ __global__ __launch_bounds__(256) void gather_half(const T *__restrict__ in, siz
   uint32_t acc = 0;
   for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < n_out; o += (size_t)gridDim.x * blockDim.x)
     acc ^= (uint32_t)in[o >> 1];
-  if (acc == 0x12345678u) sink[0] = acc;
+  if (acc == 0x1234u) sink[0] = acc;   // reachable for 16-bit values too (else the loop is dead code)
 }
 
 __global__ __launch_bounds__(256) void read2(const uint16_t *__restrict__ in, size_t n, uint32_t *__restrict__ sink) {
   uint32_t acc = 0;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     acc ^= in[i];
-  if (acc == 0x12345678u) sink[0] = acc;
+  if (acc == 0x1234u) sink[0] = acc;   // reachable for 16-bit values too (else the loop is dead code)
 }
 
 __global__ __launch_bounds__(256) void store4(uint32_t *__restrict__ out, size_t n) {
