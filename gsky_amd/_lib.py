@@ -67,6 +67,14 @@ class Mask(C.Structure):
                 ("_pad", C.c_int32), ("value", C.c_char_p), ("bit_tests", C.c_char_p * MAX_BIT_TESTS)]
 
 
+class RasterInfo(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("xsize", "ysize", "n_bands", "dtype", "signed_byte", "block_x", "block_y",
+                                         "compression", "predictor", "planar", "epsg", "has_nodata", "n_ovr",
+                                         "_pad")] + [
+        ("geot", C.c_double * 6), ("nodata", C.c_double), ("ovr_xsize", C.c_int32 * MAX_OVR),
+        ("ovr_ysize", C.c_int32 * MAX_OVR)]
+
+
 class FlexRasterC(C.Structure):
     _fields_ = [("data", C.c_void_p), ("data_w", C.c_int32), ("data_h", C.c_int32), ("width", C.c_int32),
                 ("height", C.c_int32), ("off_x", C.c_int32), ("off_y", C.c_int32), ("dtype", C.c_int32),
@@ -91,6 +99,7 @@ EXPORTS = [
     "gskyhip_drill_read_data_workspace_size", "gskyhip_drill_read_data",
     "gskyhip_png_workspace_size", "gskyhip_png_bound", "gskyhip_encode_png",
     "gskyhip_geotiff_workspace_size", "gskyhip_geotiff_bound", "gskyhip_encode_geotiff",
+    "gskyhip_geotiff_info", "gskyhip_geotiff_read_host", "gskyhip_geotiff_read", "gskyhip_register_geotiff",
 ]
 
 _lib = None
@@ -108,6 +117,10 @@ def lib() -> C.CDLL:
     ci = C.c_int
     L.gskyhip_crs_from_srs.argtypes = [C.c_char_p, C.POINTER(Crs)]
     L.gskyhip_register_granule.argtypes = [C.c_char_p, ci, C.POINTER(Granule), C.c_char_p]
+    L.gskyhip_geotiff_info.argtypes = [C.c_char_p, C.POINTER(RasterInfo)]
+    L.gskyhip_geotiff_read_host.argtypes = [C.c_char_p, ci, ci, vp, i64]
+    L.gskyhip_geotiff_read.argtypes = [C.c_char_p, ci, ci, vp, i64, vp]
+    L.gskyhip_register_geotiff.argtypes = [C.c_char_p, ci]
     L.warp_operation_fast.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(d), vp, C.c_char_p, C.POINTER(d),
                                       ci, ci, ci, ci, C.POINTER(vp), C.POINTER(ci), C.POINTER(ci),
                                       C.POINTER(d), C.POINTER(ci), C.POINTER(ci)]

@@ -12,21 +12,27 @@
 //
 // Pipeline per chunk of bands (asynchronous, workspace from the caller):
 //   drill_compact_kernel (drill.hip)  in-mask pixels of each window, compacted
-//   decile_gather_kernel  one wave per (polygon, 64 bands of the chunk): tiles
-//                         of 64 pixels x 64 bands read coalesced (a pixel's
-//                         bands are contiguous in the time-innermost stack),
-//                         transposed through LDS, compacted per band (ballot)
-//                         and written as contiguous per-band segments -- each
-//                         (polygon, band) gets a slot of count[p] values, so
-//                         no count pass and no scan are needed
-//   decile_select_kernel  one workgroup per (polygon, band) segment: the
+//   decile_chunk_scan_kernel  64-pixel chunks per polygon (exclusive scan)
+//   decile_transpose_kernel   one wave per (64-pixel chunk, 64 bands of the
+//                         chunk): the [pixel][band] tile read coalesced (a
+//                         pixel's bands are contiguous in the time-innermost
+//                         stack), transposed through the wave's LDS tile and
+//                         written band-major at the pixel's place in the
+//                         compacted list -- every polygon is spread over all
+//                         CUs (no largest-polygon bound), no counting, no
+//                         compaction: nodata values are written too and
+//                         skipped by the selection
+//   decile_select_kernel  one workgroup per (polygon, band) segment: one pass
+//                         over the segment counts its non-nodata values and
+//                         finds the bits all their keys share (AND / OR), and
+//                         keeps the keys in LDS when they fit; then the
 //                         distinct ranks the picks need (<= 2 dc), found
 //                         together by MSD radix selection on the order-
-//                         preserving 32-bit keys of the floats -- the bits all
-//                         keys share are skipped (one AND / OR reduction), then
-//                         8-bit digits, one LDS histogram per distinct prefix
-//                         of the pending ranks; the segment is re-read per
-//                         digit (L2-resident) -- then the reference's picks.
+//                         preserving 32-bit keys -- 8-bit digits below the
+//                         shared bits, one LDS histogram per distinct prefix
+//                         of the pending ranks, from the LDS copy (or the
+//                         segment again when it did not fit) -- then the
+//                         reference's picks.
 // Keys order -0.0 before +0.0 where Go's sort may leave them in either order;
 // the picked values are then equal as float32 (NaN-free stacks; with NaNs the
 // reference's order is implementation-defined).
@@ -52,83 +58,111 @@ __device__ __forceinline__ float fdecode(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
-// One wave per (polygon, group of 64 bands of the chunk).  Segment of band j
-// of polygon p: vals[seg0 + j * count[p] ...), seg0 = mask_off[p] * n_chunk
-// (the compacted pixel list of p holds count[p] <= its window bytes).
-__global__ __launch_bounds__(64) void decile_gather_kernel(const float *__restrict__ stack, int t_stride,
-                                                           const int32_t *__restrict__ idx,
-                                                           const int64_t *__restrict__ mask_off,
-                                                           const int32_t *__restrict__ count,
-                                                           const int32_t *__restrict__ tsel, int n_chunk,
-                                                           int n_groups, float nodata, float *__restrict__ vals,
-                                                           int32_t *__restrict__ cnt) {
-  __shared__ float tile[64 * kTilePad];
-  const int p = blockIdx.x / n_groups;
-  const int g = blockIdx.x % n_groups;
-  const int lane = threadIdx.x;
-  const int nb = min(64, n_chunk - g * 64);   // bands of this group
-  const bool band_ok = lane < nb;
-  const float *base = stack + (band_ok ? tsel[g * 64 + lane] : 0);
-  const int32_t *ip = idx + mask_off[p];
-  const int n = count[p];
-  float *seg = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)(g * 64) * n;
-  int32_t mycnt = 0;   // lane j: values kept for band j so far
-  for (int k0 = 0; k0 < n; k0 += 64) {
-    const int m = min(64, n - k0);
-    // 64 pixels x the group's bands: pixel kk's bands are 256 contiguous bytes
-#pragma unroll 16
-    for (int kk = 0; kk < 64; kk++) {
-      if (kk < m) tile[kk * kTilePad + lane] = band_ok ? base[(int64_t)ip[k0 + kk] * t_stride] : 0.0f;
-    }
+constexpr int kDecChunk = 64;        // pixels per transpose item
+constexpr int kSelLds = 60 * 1024;   // dynamic LDS of a select workgroup: histograms + key cache
+
+// Exclusive scan of 64-pixel chunks per polygon (one block; n_polys is modest).
+__global__ __launch_bounds__(1024) void decile_chunk_scan_kernel(const int32_t *__restrict__ count, int n_polys,
+                                                                 int32_t *__restrict__ base) {
+  __shared__ int32_t s_sum[1024];
+  const int tid = threadIdx.x;
+  int carry = 0;
+  for (int c0 = 0; c0 < n_polys; c0 += 1024) {
+    const int i = c0 + tid;
+    const int v = i < n_polys ? (count[i] + kDecChunk - 1) / kDecChunk : 0;
+    s_sum[tid] = v;
     __syncthreads();
-    for (int j = 0; j < nb; j++) {   // lane = pixel k0 + lane, band j
-      const float v = tile[lane * kTilePad + j];
-      const bool keep = lane < m && v != nodata;
-      const unsigned long long bal = __ballot(keep);
-      const int pos = __popcll(bal & ((1ull << lane) - 1ull));
-      const int cj = __shfl(mycnt, j);
-      if (keep) seg[(int64_t)j * n + cj + pos] = v;
-      if (lane == j) mycnt += __popcll(bal);
+    for (int o = 1; o < 1024; o <<= 1) {   // Hillis-Steele inclusive scan
+      const int add = tid >= o ? s_sum[tid - o] : 0;
+      __syncthreads();
+      s_sum[tid] += add;
+      __syncthreads();
     }
+    if (i < n_polys) base[i] = carry + s_sum[tid] - v;
+    const int tot = s_sum[1023];
     __syncthreads();
+    carry += tot;
   }
-  if (band_ok) cnt[(int64_t)p * n_chunk + g * 64 + lane] = mycnt;
+  if (tid == 0) base[n_polys] = carry;
 }
 
-// Block-wide reduction helpers (256 threads).
-__device__ __forceinline__ uint32_t block_and_or(uint32_t a, uint32_t o, uint32_t *red, uint32_t &or_out) {
-  for (int s = 32; s > 0; s >>= 1) {
-    a &= __shfl_xor(a, s);
-    o |= __shfl_xor(o, s);
+// The 64 lanes of one wavefront see each other's LDS writes in program
+// order: keep the compiler from moving LDS accesses across this point.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave per (64-pixel chunk ch, group g of 64 bands of the pass); four
+// independent waves per workgroup.  Band j of polygon p: vals[seg0 + j *
+// count[p] + k] for its pixel k, seg0 = mask_off[p] * n_chunk (the compacted
+// pixel list of p holds count[p] <= its window bytes).
+__global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__restrict__ stack, int t_stride,
+                                                               const int32_t *__restrict__ idx,
+                                                               const int64_t *__restrict__ mask_off,
+                                                               const int32_t *__restrict__ count,
+                                                               const int32_t *__restrict__ chunk_base, int n_polys,
+                                                               const int32_t *__restrict__ tsel, int n_chunk,
+                                                               int n_groups, float *__restrict__ vals) {
+  __shared__ float tile[4][64 * kTilePad];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t item = (int64_t)blockIdx.x * 4 + wave;
+  const int ch = (int)(item / n_groups), g = (int)(item % n_groups);
+  if (ch >= chunk_base[n_polys]) return;   // whole waves; no workgroup barrier below
+  int lo = 0, hi = n_polys - 1;            // polygon owning chunk ch
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (chunk_base[mid] <= ch) lo = mid; else hi = mid - 1;
   }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { red[w] = a; red[4 + w] = o; }
-  __syncthreads();
-  const uint32_t ra = red[0] & red[1] & red[2] & red[3];
-  or_out = red[4] | red[5] | red[6] | red[7];
-  __syncthreads();
-  return ra;
+  const int p = lo;
+  const int n = count[p];
+  const int k0 = (ch - chunk_base[p]) * kDecChunk;
+  const int m = min(kDecChunk, n - k0);
+  const int nb = min(64, n_chunk - g * 64);   // bands of this group
+  // every lane loads from a valid address (band 0 of the group, pixel 0 of
+  // the chunk) so the loads of a group are unconditional and all in flight
+  const float *base = stack + tsel[g * 64 + (lane < nb ? lane : 0)];
+  const int32_t my_px = idx[mask_off[p] + k0 + (lane < m ? lane : 0)];
+  float *T = tile[wave];
+  for (int kb = 0; kb < m; kb += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {   // pixel kb + u: its bands, one per lane (256 contiguous bytes)
+      const int px = __builtin_amdgcn_readlane(my_px, kb + u);
+      v[u] = base[(int64_t)px * t_stride];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u++) T[(kb + u) * kTilePad + lane] = v[u];
+  }
+  wave_lds_sync();
+  float *seg = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)(g * 64) * n + k0;
+  if (lane < m) {
+    for (int j = 0; j < nb; j++) seg[(int64_t)j * n + lane] = T[lane * kTilePad + j];   // lane = pixel
+  }
 }
 
 // computeDeciles of one (polygon, band) segment; status 0, 1 (band total 0:
 // zeros, Count 0 in the reference's TimeSeries) or GSKYHIP_E_RANGE (the
 // reference indexes buf[len] and panics: len % (dc + 1) == 0 with step 1).
+// Dynamic LDS: n_slots histograms of 256 bins, then cache_keys keys.
 __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float *__restrict__ vals,
-                                                                    const int32_t *__restrict__ cnt,
                                                                     const int64_t *__restrict__ mask_off,
                                                                     const int32_t *__restrict__ count,
                                                                     const int32_t *__restrict__ totals, int n_chunk,
-                                                                    int b0, int n_list, int dc,
-                                                                    float *__restrict__ out,
+                                                                    int b0, int n_list, int dc, float nodata,
+                                                                    int n_slots, int cache_keys, float *__restrict__ out,
                                                                     int32_t *__restrict__ status) {
-  __shared__ uint32_t hist[kMaxRanks][256];
+  extern __shared__ uint32_t dyn[];
+  uint32_t (*hist)[256] = (uint32_t (*)[256])dyn;
+  uint32_t *cache = dyn + n_slots * 256;
   __shared__ uint32_t s_pref[kMaxRanks];   // rank r: its key's bits above `pos`
   __shared__ uint32_t s_rem[kMaxRanks];    // rank r: its rank among the keys sharing that prefix
   __shared__ int32_t s_rank[kMaxRanks];    // the distinct ranks, ascending
   __shared__ int32_t s_slot[kMaxRanks];    // rank r -> histogram slot (distinct prefix)
   __shared__ uint32_t s_spref[kMaxRanks];  // slot -> prefix (ascending)
-  __shared__ uint32_t red[8];
-  __shared__ int32_t s_nr, s_ns;
+  __shared__ uint32_t red[12];
+  __shared__ int32_t s_nr, s_ns, s_nc;
   __shared__ float s_small[64];
 
   const int p = blockIdx.x / n_chunk, j = blockIdx.x % n_chunk;
@@ -140,18 +174,56 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     if (tid == 0) status[o] = 1;
     return;
   }
-  const int len = cnt[(int64_t)p * n_chunk + j];
-  const float *buf = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)j * count[p];
+  const int n = count[p];
+  const float *buf = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)j * n;
+  // pass 1: the non-nodata values (the reference's buf, drill.go:231-237):
+  // their count, the bits all their keys share, and the keys themselves in
+  // LDS while they fit (order is irrelevant to order statistics)
+  if (tid == 0) s_nc = 0;
+  __syncthreads();
+  const bool fits = n <= cache_keys;
+  uint32_t ka = 0xFFFFFFFFu, ko = 0u;
+  int valid = 0;
+  for (int i0 = 0; i0 < n; i0 += kSelThreads) {
+    const int i = i0 + tid;
+    const float v = i < n ? buf[i] : nodata;
+    const bool keep = i < n && v != nodata;
+    const uint32_t k = fkey(v);
+    if (keep) { ka &= k; ko |= k; valid++; }
+    if (fits) {
+      const unsigned long long bal = __ballot(keep);
+      int wbase = 0;
+      if ((tid & 63) == 0 && bal) wbase = atomicAdd(&s_nc, __popcll(bal));
+      wbase = __shfl(wbase, 0);
+      if (keep) cache[wbase + __popcll(bal & ((1ull << (tid & 63)) - 1ull))] = k;
+    }
+  }
+  for (int sh = 32; sh > 0; sh >>= 1) {
+    ka &= __shfl_xor(ka, sh);
+    ko |= __shfl_xor(ko, sh);
+    valid += __shfl_xor(valid, sh);
+  }
+  if ((tid & 63) == 0) { red[tid >> 6] = ka; red[4 + (tid >> 6)] = ko; red[8 + (tid >> 6)] = (uint32_t)valid; }
+  __syncthreads();
+  const uint32_t kand = red[0] & red[1] & red[2] & red[3];
+  const uint32_t kor = red[4] | red[5] | red[6] | red[7];
+  const int len = (int)(red[8] + red[9] + red[10] + red[11]);
   if (len <= 0) {   // total > 0 implies a non-nodata value; keep the slot defined anyway
     for (int i = tid; i < dc; i += kSelThreads) dst[i] = 0.f;
     if (tid == 0) status[o] = 0;
     return;
   }
+  auto key_at = [&](int i) -> uint32_t { return cache[i]; };
   const int step = len / (dc + 1);
-  if (step == 0) {   // len <= dc (<= 64): sort the few values, repeat them in order
-    if (tid < len) s_small[tid] = buf[tid];
-    __syncthreads();
+  if (step == 0) {   // len <= dc (<= 16): sort the few values, repeat them in order
     if (tid == 0) {
+      int m = 0;
+      if (fits) {
+        for (int i = 0; i < len; i++) s_small[m++] = fdecode(key_at(i));
+      } else {
+        for (int i = 0; i < n && m < len; i++)
+          if (buf[i] != nodata) s_small[m++] = buf[i];
+      }
       for (int a = 1; a < len; a++) {
         const float v = s_small[a];
         int b = a - 1;
@@ -183,15 +255,7 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     }
     s_nr = nr;
   }
-  // common leading bits of every key
-  uint32_t ka = 0xFFFFFFFFu, ko = 0u;
-  for (int i = tid; i < len; i += kSelThreads) {
-    const uint32_t k = fkey(buf[i]);
-    ka &= k;
-    ko |= k;
-  }
-  uint32_t kor;
-  const uint32_t kand = block_and_or(ka, ko, red, kor);
+  __syncthreads();
   const int nr = s_nr;
   int pos = (kand == kor) ? 0 : 32 - __clz(kand ^ kor);   // bits below pos differ somewhere
   if (tid < nr) {
@@ -214,8 +278,7 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     const int ns = s_ns;
     for (int i = tid; i < ns * 256; i += kSelThreads) hist[i >> 8][i & 255] = 0u;
     __syncthreads();
-    for (int i = tid; i < len; i += kSelThreads) {
-      const uint32_t k = fkey(buf[i]);
+    auto bin = [&](uint32_t k) {
       const uint32_t hi = pos >= 32 ? 0u : (k >> pos);
       int lo = 0, hi_s = ns - 1;   // binary search of the slot with prefix hi
       while (lo < hi_s) {
@@ -223,6 +286,14 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
         if (s_spref[mid] < hi) lo = mid + 1; else hi_s = mid;
       }
       if (s_spref[lo] == hi) atomicAdd(&hist[lo][(k >> shift) & ((1u << d) - 1u)], 1u);
+    };
+    if (fits) {
+      for (int i = tid; i < len; i += kSelThreads) bin(key_at(i));
+    } else {
+      for (int i = tid; i < n; i += kSelThreads) {
+        const float v = buf[i];
+        if (v != nodata) bin(fkey(v));
+      }
     }
     __syncthreads();
     if (tid < nr) {   // the digit bucket holding each rank
@@ -254,21 +325,20 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
 inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 struct DecWs {
-  int32_t *idx, *count, *cnt, *tsel;
+  int32_t *idx, *count, *chunk_base, *tsel;
   float *vals;
   int64_t total;
 };
 
 DecWs decile_carve(void *base, int n_polys, int64_t mask_bytes, int chunk) {
   DecWs w;
-  const int64_t n_seg = (int64_t)n_polys * chunk;
   const int64_t cap = mask_bytes * chunk;
   char *b = (char *)base;
   int64_t o = 0;
   auto take = [&](int64_t bytes) { char *p = b ? b + o : nullptr; o += al256(bytes); return p; };
   w.idx = (int32_t *)take(mask_bytes * 4);
   w.count = (int32_t *)take((int64_t)n_polys * 4);
-  w.cnt = (int32_t *)take(n_seg * 4);
+  w.chunk_base = (int32_t *)take((mask_bytes / kDecChunk + n_polys + 1) * 4);
   w.tsel = (int32_t *)take((int64_t)chunk * 4);
   w.vals = (float *)take(cap * 4);
   w.total = o;
@@ -301,16 +371,24 @@ int launch_drill_deciles(const DecileCall &c) {
   hipStream_t s = c.stream;
   hipLaunchKernelGGL(drill_compact_kernel, dim3(c.n_polys), dim3(256), 0, s, c.win, c.mask_off, c.masks, c.n_polys,
                      c.xsize, c.ysize, w.idx, w.count);
+  hipLaunchKernelGGL(decile_chunk_scan_kernel, dim3(1), dim3(1024), 0, s, w.count, c.n_polys, w.chunk_base);
+  const int64_t max_chunks = c.mask_bytes / kDecChunk + c.n_polys;   // >= sum of ceil(count / 64)
+  const int n_slots = std::min(kMaxRanks, 2 * c.decile_count);
+  const int cache_keys = (kSelLds - n_slots * 256 * 4) / 4;
+  const size_t dyn_lds = (size_t)kSelLds;
   for (int b0 = 0; b0 < n_list; b0 += c.band_chunk) {
     const int n_chunk = std::min(c.band_chunk, n_list - b0);
     const int n_groups = (n_chunk + 63) / 64;
     const int64_t n_seg = (int64_t)c.n_polys * n_chunk;
     if (hipMemcpyAsync(w.tsel, sel.data() + b0, sizeof(int32_t) * n_chunk, hipMemcpyHostToDevice, s) != hipSuccess)
       return GSKYHIP_E_HIP;
-    hipLaunchKernelGGL(decile_gather_kernel, dim3((unsigned)((int64_t)c.n_polys * n_groups)), dim3(64), 0, s, c.stack,
-                       c.t_stride, w.idx, c.mask_off, w.count, w.tsel, n_chunk, n_groups, c.nodata, w.vals, w.cnt);
-    hipLaunchKernelGGL(decile_select_kernel, dim3((unsigned)n_seg), dim3(kSelThreads), 0, s, w.vals, w.cnt,
-                       c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.out, c.status);
+    const int64_t items = max_chunks * n_groups;
+    hipLaunchKernelGGL(decile_transpose_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, c.stack,
+                       c.t_stride, w.idx, c.mask_off, w.count, w.chunk_base, c.n_polys, w.tsel, n_chunk, n_groups,
+                       w.vals);
+    hipLaunchKernelGGL(decile_select_kernel, dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
+                       c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots, cache_keys, c.out,
+                       c.status);
   }
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }

@@ -263,7 +263,13 @@ struct Registered {
   gskyhip_granule g;
   gskyhip_crs crs;
   bool has_crs;
+  std::vector<void *> owned;   // HBM the library allocated for it (ingested files)
 };
+
+void release(Registered &r) {
+  for (void *p : r.owned) hipFree(p);
+  r.owned.clear();
+}
 
 struct DropIn {
   std::mutex mu;
@@ -280,6 +286,59 @@ DropIn &dropin() {
 bool have_gpu() {
   int n = 0;
   return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+// GDALOpenEx + GDALGetRasterBand of a GeoTIFF (warp.go:89-118) for the
+// registry: every level of band `band` decoded into HBM the library owns
+// (ingest.hip), registered under (path, band) with the file's SRS.  Returns
+// 0, 1 (open failed), 2 (no such band) or GSKYHIP_E_*.  d.mu held.
+int ingest_geotiff_locked(DropIn &d, const std::string &path, int band) {
+  gskyhip_raster_info info;
+  int rc = gskyhip_geotiff_info(path.c_str(), &info);
+  if (rc) return rc;
+  if (band < 1 || band > info.n_bands) return 2;
+  if (!have_gpu()) return GSKYHIP_E_NOGPU;
+  Registered r;
+  std::memset(&r.g, 0, sizeof(r.g));
+  const int ts = type_size(info.dtype);
+  if (ts <= 0) return GSKYHIP_E_TYPE;
+  for (int lv = 0; lv <= info.n_ovr; lv++) {
+    const int64_t xs = lv ? info.ovr_xsize[lv - 1] : info.xsize, ys = lv ? info.ovr_ysize[lv - 1] : info.ysize;
+    void *p = nullptr;
+    if (hipMalloc(&p, (size_t)(xs * ys * ts)) != hipSuccess) { release(r); return GSKYHIP_E_HIP; }
+    r.owned.push_back(p);
+    if ((rc = gskyhip_geotiff_read(path.c_str(), band, lv, p, xs * ys * ts, nullptr))) { release(r); return rc; }
+  }
+  gskyhip_granule &g = r.g;
+  g.data = r.owned[0];
+  g.dtype = info.dtype; g.xsize = info.xsize; g.ysize = info.ysize; g.signed_byte = info.signed_byte;
+  for (int k = 0; k < 6; k++) g.geot[k] = info.geot[k];
+  g.nodata = info.nodata; g.has_nodata = info.has_nodata;
+  g.n_ovr = info.n_ovr;
+  for (int k = 0; k < info.n_ovr; k++) {
+    g.ovr_data[k] = r.owned[k + 1]; g.ovr_xsize[k] = info.ovr_xsize[k]; g.ovr_ysize[k] = info.ovr_ysize[k];
+  }
+  g.block_x = info.block_x; g.block_y = info.block_y;
+  r.has_crs = false;
+  char srs[32] = {0};
+  if (info.epsg > 0) std::snprintf(srs, sizeof(srs), "EPSG:%d", info.epsg);
+  else if (info.epsg == -1) std::snprintf(srs, sizeof(srs), "MODIS");
+  if (srs[0] && parse_srs(srs, &r.crs) == 0) r.has_crs = true;
+  auto it = d.reg.find({path, band});
+  if (it != d.reg.end()) release(it->second);
+  d.reg[{path, band}] = std::move(r);
+  return 0;
+}
+
+bool is_geotiff_path(const std::string &p) {
+  auto ends = [&](const char *suf) {
+    const size_t n = std::strlen(suf);
+    if (p.size() < n) return false;
+    for (size_t i = 0; i < n; i++)
+      if (std::tolower((unsigned char)p[p.size() - n + i]) != suf[i]) return false;
+    return true;
+  };
+  return ends(".tif") || ends(".tiff");
 }
 
 }  // namespace
@@ -320,6 +379,8 @@ int gskyhip_register_granule(const char *path, int band, const gskyhip_granule *
   }
   DropIn &d = dropin();
   std::lock_guard<std::mutex> lk(d.mu);
+  auto it = d.reg.find({std::string(path), band});
+  if (it != d.reg.end()) release(it->second);
   d.reg[{std::string(path), band}] = r;
   return 0;
 }
@@ -327,8 +388,16 @@ int gskyhip_register_granule(const char *path, int band, const gskyhip_granule *
 int gskyhip_unregister_all(void) {
   DropIn &d = dropin();
   std::lock_guard<std::mutex> lk(d.mu);
+  for (auto &kv : d.reg) release(kv.second);
   d.reg.clear();
   return 0;
+}
+
+int gskyhip_register_geotiff(const char *path, int band) {
+  if (!path) return GSKYHIP_E_ARG;
+  DropIn &d = dropin();
+  std::lock_guard<std::mutex> lk(d.mu);
+  return ingest_geotiff_locked(d, path, band);
 }
 
 }  // extern "C"
@@ -356,6 +425,11 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     const bool netcdf = q.path.compare(0, 7, "NETCDF:") == 0 ||
                         (q.path.size() >= 3 && q.path.compare(q.path.size() - 3, 3, ".nc") == 0);
     auto it = d.reg.find({q.path, q.band});
+    if (it == d.reg.end() && !netcdf && is_geotiff_path(q.path)) {   // GDALOpenEx of a file nobody registered
+      const int irc = ingest_geotiff_locked(d, q.path, q.band);
+      if (irc == 1 || irc == 2) { r.rc = irc; continue; }
+      it = d.reg.find({q.path, q.band});
+    }
     if (it == d.reg.end()) {
       bool path_known = false;
       for (const auto &kv : d.reg) if (kv.first.first == q.path) { path_known = true; break; }

@@ -1,0 +1,548 @@
+// ingest.hip -- native granule ingest: GeoTIFF files
+// decoded into HBM, the step GDALOpenEx + GDALRasterIO take in the worker
+// (worker/gdalprocess/warp.go:89-101, drill.go:61-69, 142) before the warp.
+//
+// Reader: classic TIFF and BigTIFF, little or big endian; striped or tiled;
+// chunky or planar; 8/16/32/64-bit unsigned, signed and float samples;
+// compression none (1), LZW (5), Deflate (8, 32946) and PackBits (32773);
+// predictor 1 (none), 2 (horizontal differencing) and 3 (floating point).
+// Georeferencing as GDAL's GTiff driver reads it: ModelTransformation, or
+// ModelTiepoint + ModelPixelScale (PixelIsPoint shifted by half a pixel),
+// EPSG from ProjectedCSTypeGeoKey / GeographicTypeGeoKey (user-defined
+// sinusoidal on the MODIS sphere -> "MODIS"), nodata from GDAL_NODATA
+// (42113), internal overviews from the reduced-resolution IFDs in file
+// order (GDALGetOverview order).
+//
+// Device path: the band's blocks are decompressed and un-predicted by host
+// threads (zlib / LZW / PackBits are byte-serial), staged block-major in
+// pinned memory, copied to HBM in one transfer and placed row-major by
+// assemble_kernel (a thread per output element; edge blocks clipped).
+#include <hip/hip_runtime.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/gskyhip.h"
+
+namespace gsky {
+namespace {
+
+struct Ifd {
+  int64_t width = 0, height = 0;
+  int bits = 0, spp = 1, fmt = 1, compression = 1, predictor = 1, planar = 1;
+  int64_t block_w = 0, block_h = 0;   // tile size, or width x RowsPerStrip
+  bool tiled = false;
+  int subfile = 0;
+  std::vector<uint64_t> offsets, counts;
+  std::vector<double> scale, tiepoint, transform;
+  std::vector<uint16_t> geokeys;
+  std::vector<double> geodoubles;
+  std::string nodata;
+};
+
+struct Tiff {
+  std::vector<uint8_t> buf;   // the whole file (memory of a granule band is read whole anyway)
+  bool be = false, big = false;
+  std::vector<Ifd> ifds;
+
+  uint16_t u16(uint64_t o) const {
+    uint16_t v;
+    std::memcpy(&v, &buf[o], 2);
+    return be ? (uint16_t)((v >> 8) | (v << 8)) : v;
+  }
+  uint32_t u32(uint64_t o) const {
+    uint32_t v;
+    std::memcpy(&v, &buf[o], 4);
+    return be ? __builtin_bswap32(v) : v;
+  }
+  uint64_t u64(uint64_t o) const {
+    uint64_t v;
+    std::memcpy(&v, &buf[o], 8);
+    return be ? __builtin_bswap64(v) : v;
+  }
+  double f64(uint64_t o) const {
+    const uint64_t v = u64(o);
+    double d;
+    std::memcpy(&d, &v, 8);
+    return d;
+  }
+};
+
+int type_bytes(int t) {
+  switch (t) {
+    case 1: case 2: case 6: case 7: return 1;
+    case 3: case 8: return 2;
+    case 4: case 9: case 11: case 13: return 4;
+    case 5: case 10: case 12: case 16: case 17: case 18: return 8;
+    default: return 0;
+  }
+}
+
+// Parse every IFD; false on a malformed file.
+bool parse(Tiff &t) {
+  const std::vector<uint8_t> &b = t.buf;
+  if (b.size() < 16) return false;
+  if (b[0] == 'I' && b[1] == 'I') t.be = false;
+  else if (b[0] == 'M' && b[1] == 'M') t.be = true;
+  else return false;
+  const uint16_t magic = t.u16(2);
+  if (magic == 42) t.big = false;
+  else if (magic == 43 && t.u16(4) == 8) t.big = true;
+  else return false;
+  uint64_t off = t.big ? t.u64(8) : t.u32(4);
+  for (int guard = 0; off && guard < 64; guard++) {
+    const uint64_t esz = t.big ? 20 : 12, hdr = t.big ? 8 : 2;
+    if (off + hdr > b.size()) return false;
+    const uint64_t n = t.big ? t.u64(off) : t.u16(off);
+    if (off + hdr + n * esz + (t.big ? 8 : 4) > b.size()) return false;
+    Ifd d;
+    for (uint64_t i = 0; i < n; i++) {
+      const uint64_t e = off + hdr + i * esz;
+      const int tag = t.u16(e), typ = t.u16(e + 2);
+      const uint64_t cnt = t.big ? t.u64(e + 4) : t.u32(e + 4);
+      const int tb = type_bytes(typ);
+      if (tb == 0) continue;
+      const uint64_t inl = t.big ? 8 : 4;
+      const uint64_t voff = e + (t.big ? 12 : 8);
+      const uint64_t data = (uint64_t)tb * cnt <= inl ? voff : (t.big ? t.u64(voff) : t.u32(voff));
+      if (data + (uint64_t)tb * cnt > b.size()) return false;
+      auto ints = [&]() {
+        std::vector<uint64_t> v(cnt);
+        for (uint64_t k = 0; k < cnt; k++) {
+          const uint64_t p = data + k * tb;
+          v[k] = tb == 1 ? b[p] : tb == 2 ? t.u16(p) : tb == 4 ? t.u32(p) : t.u64(p);
+        }
+        return v;
+      };
+      auto dbls = [&]() {
+        std::vector<double> v(cnt);
+        for (uint64_t k = 0; k < cnt; k++) v[k] = typ == 12 ? t.f64(data + 8 * k) : (double)ints()[k];
+        return v;
+      };
+      switch (tag) {
+        case 254: d.subfile = (int)ints()[0]; break;
+        case 256: d.width = (int64_t)ints()[0]; break;
+        case 257: d.height = (int64_t)ints()[0]; break;
+        case 258: d.bits = (int)ints()[0]; break;
+        case 259: d.compression = (int)ints()[0]; break;
+        case 273: case 324: d.offsets = ints(); d.tiled = d.tiled || tag == 324; break;
+        case 277: d.spp = (int)ints()[0]; break;
+        case 278: d.block_h = (int64_t)ints()[0]; break;
+        case 279: case 325: d.counts = ints(); break;
+        case 284: d.planar = (int)ints()[0]; break;
+        case 317: d.predictor = (int)ints()[0]; break;
+        case 322: d.block_w = (int64_t)ints()[0]; break;
+        case 323: d.block_h = (int64_t)ints()[0]; break;
+        case 339: d.fmt = (int)ints()[0]; break;
+        case 33550: d.scale = dbls(); break;
+        case 33922: d.tiepoint = dbls(); break;
+        case 34264: d.transform = dbls(); break;
+        case 34735: { auto v = ints(); d.geokeys.assign(v.begin(), v.end()); break; }
+        case 34736: d.geodoubles = dbls(); break;
+        case 42113: d.nodata.assign((const char *)&b[data], (size_t)cnt); break;
+        default: break;
+      }
+    }
+    if (!d.tiled) {
+      d.block_w = d.width;
+      if (d.block_h <= 0 || d.block_h > d.height) d.block_h = d.height;
+    }
+    if (d.width <= 0 || d.height <= 0 || d.block_w <= 0 || d.block_h <= 0 || d.offsets.empty() ||
+        d.offsets.size() != d.counts.size())
+      return false;
+    t.ifds.push_back(std::move(d));
+    off = t.big ? t.u64(off + hdr + n * esz) : t.u32(off + hdr + n * esz);
+  }
+  return !t.ifds.empty();
+}
+
+bool read_file(const char *path, std::vector<uint8_t> &out) {
+  FILE *f = std::fopen(path, "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  out.resize(n > 0 ? (size_t)n : 0);
+  const bool ok = n > 0 && std::fread(out.data(), 1, (size_t)n, f) == (size_t)n;
+  std::fclose(f);
+  return ok;
+}
+
+int dtype_of(const Ifd &d, int &signed_byte) {
+  signed_byte = 0;
+  if (d.fmt == 3) return d.bits == 32 ? GSKYHIP_FLOAT32 : d.bits == 64 ? GSKYHIP_FLOAT64 : 0;
+  const bool sgn = d.fmt == 2;
+  switch (d.bits) {
+    case 8: signed_byte = sgn ? 1 : 0; return GSKYHIP_BYTE;
+    case 16: return sgn ? GSKYHIP_INT16 : GSKYHIP_UINT16;
+    case 32: return sgn ? GSKYHIP_INT32 : GSKYHIP_UINT32;
+    default: return 0;
+  }
+}
+
+// TIFF LZW (MSB-first codes, the code width grows one code early).
+bool lzw_decode(const uint8_t *in, size_t n, uint8_t *out, size_t cap) {
+  std::vector<uint32_t> prefix(4096), first(4096);
+  std::vector<uint8_t> suffix(4096);
+  std::vector<uint16_t> len(4096);
+  for (int i = 0; i < 256; i++) { suffix[i] = (uint8_t)i; len[i] = 1; prefix[i] = 0xFFFF; first[i] = i; }
+  size_t op = 0;
+  uint64_t bitbuf = 0;
+  int bits = 0, width = 9, next = 258;
+  int old = -1;
+  size_t ip = 0;
+  std::vector<uint8_t> tmp(4096);
+  auto emit = [&](int code) -> bool {
+    const int l = len[code];
+    if (op + l > cap) return false;
+    int c = code;
+    for (int k = l - 1; k >= 0; k--) { out[op + k] = suffix[c]; c = (int)prefix[c]; }
+    op += l;
+    return true;
+  };
+  for (;;) {
+    while (bits < width) {
+      if (ip >= n) return op == cap;
+      bitbuf = (bitbuf << 8) | in[ip++];
+      bits += 8;
+    }
+    const int code = (int)((bitbuf >> (bits - width)) & ((1u << width) - 1));
+    bits -= width;
+    if (code == 257) break;   // EOI
+    if (code == 256) {        // clear
+      width = 9; next = 258; old = -1;
+      continue;
+    }
+    if (old < 0) {
+      if (code > 255 || !emit(code)) return false;
+      old = code;
+      continue;
+    }
+    if (code < next) {
+      if (!emit(code)) return false;
+      if (next < 4096) { prefix[next] = old; suffix[next] = (uint8_t)first[code]; len[next] = len[old] + 1;
+                         first[next] = first[old]; next++; }
+    } else if (code == next && next < 4096) {
+      prefix[next] = old; suffix[next] = (uint8_t)first[old]; len[next] = len[old] + 1; first[next] = first[old];
+      next++;
+      if (!emit(code)) return false;
+    } else {
+      return false;
+    }
+    old = code;
+    if (next + 1 >= (1 << width) && width < 12) width++;
+  }
+  return op == cap;
+}
+
+bool packbits_decode(const uint8_t *in, size_t n, uint8_t *out, size_t cap) {
+  size_t ip = 0, op = 0;
+  while (ip < n && op < cap) {
+    const int8_t h = (int8_t)in[ip++];
+    if (h >= 0) {
+      const size_t l = (size_t)h + 1;
+      if (ip + l > n || op + l > cap) return false;
+      std::memcpy(out + op, in + ip, l);
+      ip += l; op += l;
+    } else if (h != -128) {
+      const size_t l = (size_t)(1 - h);
+      if (ip >= n || op + l > cap) return false;
+      std::memset(out + op, in[ip++], l);
+      op += l;
+    }
+  }
+  return op == cap;
+}
+
+// Decode one block into `out` (block_w x rows x spp samples of `bytes`, the
+// block's own layout): decompression, byte order, predictor.
+bool decode_block(const Tiff &t, const Ifd &d, size_t bi, int64_t rows, int samples, uint8_t *out) {
+  const int bytes = d.bits / 8;
+  const size_t row_bytes = (size_t)d.block_w * samples * bytes;
+  const size_t cap = row_bytes * rows;
+  const uint64_t off = d.offsets[bi], cnt = d.counts[bi];
+  if (off + cnt > t.buf.size()) return false;
+  const uint8_t *in = &t.buf[off];
+  bool ok;
+  switch (d.compression) {
+    case 1: ok = cnt >= cap; if (ok) std::memcpy(out, in, cap); break;
+    case 8: case 32946: { uLongf dl = (uLongf)cap; ok = uncompress(out, &dl, in, (uLong)cnt) == Z_OK && dl == cap;
+                          if (!ok) {   // a block may carry more rows than the image has (strips): accept a short tail
+                            std::vector<uint8_t> big(cap + row_bytes * d.block_h);
+                            uLongf dl2 = (uLongf)big.size();
+                            const int z = uncompress(big.data(), &dl2, in, (uLong)cnt);
+                            ok = (z == Z_OK) && dl2 >= cap;
+                            if (ok) std::memcpy(out, big.data(), cap);
+                          }
+                          break; }
+    case 5: ok = lzw_decode(in, cnt, out, cap); break;
+    case 32773: ok = packbits_decode(in, cnt, out, cap); break;
+    default: return false;
+  }
+  if (!ok) return false;
+  if (t.be && bytes > 1 && d.predictor != 3) {   // to host (little endian) order
+    for (size_t i = 0; i < cap; i += bytes) std::reverse(out + i, out + i + bytes);
+  }
+  if (d.predictor == 2) {   // horizontal differencing per sample
+    for (int64_t r = 0; r < rows; r++) {
+      uint8_t *row = out + r * row_bytes;
+      const int64_t n = d.block_w * samples;
+      if (bytes == 1) { for (int64_t i = samples; i < n; i++) row[i] = (uint8_t)(row[i] + row[i - samples]); }
+      else if (bytes == 2) { uint16_t *v = (uint16_t *)row; for (int64_t i = samples; i < n; i++) v[i] = (uint16_t)(v[i] + v[i - samples]); }
+      else if (bytes == 4) { uint32_t *v = (uint32_t *)row; for (int64_t i = samples; i < n; i++) v[i] += v[i - samples]; }
+      else { uint64_t *v = (uint64_t *)row; for (int64_t i = samples; i < n; i++) v[i] += v[i - samples]; }
+    }
+  } else if (d.predictor == 3) {   // floating point: byte differencing, then byte planes (MSB first)
+    std::vector<uint8_t> tmp(row_bytes);
+    const int64_t n = d.block_w * samples;
+    for (int64_t r = 0; r < rows; r++) {
+      uint8_t *row = out + r * row_bytes;
+      for (size_t i = samples; i < row_bytes; i++) row[i] = (uint8_t)(row[i] + row[i - samples]);
+      for (int64_t i = 0; i < n; i++)
+        for (int k = 0; k < bytes; k++) tmp[i * bytes + k] = row[(size_t)(bytes - 1 - k) * n + i];
+      std::memcpy(row, tmp.data(), row_bytes);
+    }
+  }
+  return true;
+}
+
+struct Layout {
+  int64_t bw, bh, across, down;   // block size, blocks per row / column
+  int samples;                    // samples per pixel inside a block (chunky: spp, planar: 1)
+  size_t block_bytes;             // staged block: bw x bh of ONE sample
+};
+
+Layout layout_of(const Ifd &d) {
+  Layout L;
+  L.bw = d.block_w; L.bh = d.block_h;
+  L.across = (d.width + L.bw - 1) / L.bw;
+  L.down = (d.height + L.bh - 1) / L.bh;
+  L.samples = d.planar == 2 ? 1 : d.spp;
+  L.block_bytes = (size_t)L.bw * L.bh * (d.bits / 8);
+  return L;
+}
+
+// Decode every block of band `band` (0-based sample) into `stage`
+// (block-major, each block bw x bh of one sample); host threads.
+bool decode_band(const Tiff &t, const Ifd &d, int band, uint8_t *stage) {
+  const Layout L = layout_of(d);
+  const int64_t nblk = L.across * L.down;
+  const int64_t plane0 = d.planar == 2 ? (int64_t)band * nblk : 0;
+  if ((int64_t)d.offsets.size() < plane0 + nblk) return false;
+  const int bytes = d.bits / 8;
+  std::atomic<int64_t> next(0);
+  std::atomic<bool> ok(true);
+  const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  auto work = [&]() {
+    std::vector<uint8_t> blk((size_t)L.bw * L.bh * L.samples * bytes);
+    for (int64_t i = next++; i < nblk && ok; i = next++) {
+      // strips: the last one holds only the image's remaining rows
+      const int64_t rows = d.tiled ? L.bh : std::min<int64_t>(L.bh, d.height - (i / L.across) * L.bh);
+      if (!decode_block(t, d, (size_t)(plane0 + i), rows, L.samples, blk.data())) { ok = false; break; }
+      uint8_t *dst = stage + (size_t)i * L.block_bytes;
+      if (L.samples == 1) {
+        std::memcpy(dst, blk.data(), (size_t)L.bw * rows * bytes);
+      } else {
+        for (int64_t k = 0; k < L.bw * rows; k++)
+          std::memcpy(dst + k * bytes, blk.data() + ((size_t)k * L.samples + band) * bytes, bytes);
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned k = 1; k < std::min<unsigned>(nth, (unsigned)std::max<int64_t>(1, nblk)); k++) th.emplace_back(work);
+  work();
+  for (auto &x : th) x.join();
+  return ok;
+}
+
+// Output element (x, y) <- staged block (y / bh) * across + x / bw.
+template <typename W>
+__global__ __launch_bounds__(256) void assemble_kernel(const W *__restrict__ stage, W *__restrict__ out, int64_t width,
+                                                       int64_t height, int64_t bw, int64_t bh, int64_t across) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= width * height) return;
+  const int64_t y = i / width, x = i - y * width;
+  const int64_t by = y / bh, bx = x / bw;
+  out[i] = stage[((by * across + bx) * bh + (y - by * bh)) * bw + (x - bx * bw)];
+}
+
+void assemble_host(const uint8_t *stage, uint8_t *out, const Ifd &d) {
+  const Layout L = layout_of(d);
+  const int bytes = d.bits / 8;
+  for (int64_t y = 0; y < d.height; y++) {
+    const int64_t by = y / L.bh;
+    for (int64_t bx = 0; bx < L.across; bx++) {
+      const int64_t x0 = bx * L.bw, n = std::min(L.bw, d.width - x0);
+      std::memcpy(out + ((size_t)y * d.width + x0) * bytes,
+                  stage + (((size_t)(by * L.across + bx) * L.bh + (y - by * L.bh)) * L.bw) * bytes, (size_t)n * bytes);
+    }
+  }
+}
+
+// GeoKey value (SHORT, inline) or 0.
+int geokey(const Ifd &d, int key) {
+  const auto &g = d.geokeys;
+  if (g.size() < 4) return 0;
+  const int n = g[3];
+  for (int i = 0; i < n && 4 + 4 * i + 3 < (int)g.size(); i++)
+    if (g[4 + 4 * i] == key && g[4 + 4 * i + 1] == 0) return g[4 + 4 * i + 3];
+  return 0;
+}
+
+double geodouble(const Ifd &d, int key, double dflt) {
+  const auto &g = d.geokeys;
+  if (g.size() < 4) return dflt;
+  const int n = g[3];
+  for (int i = 0; i < n && 4 + 4 * i + 3 < (int)g.size(); i++)
+    if (g[4 + 4 * i] == key && g[4 + 4 * i + 1] == 34736 && g[4 + 4 * i + 3] < (int)d.geodoubles.size())
+      return d.geodoubles[g[4 + 4 * i + 3]];
+  return dflt;
+}
+
+// Full-resolution IFD and its reduced-resolution ones (NewSubfileType bit 0).
+void levels(const Tiff &t, std::vector<int> &out) {
+  out.clear();
+  int base = -1;
+  for (int i = 0; i < (int)t.ifds.size(); i++)
+    if (!(t.ifds[i].subfile & 1)) { base = i; break; }
+  if (base < 0) return;
+  out.push_back(base);
+  for (int i = 0; i < (int)t.ifds.size(); i++)
+    if (i != base && (t.ifds[i].subfile & 1) && t.ifds[i].spp == t.ifds[base].spp &&
+        t.ifds[i].bits == t.ifds[base].bits && (int)out.size() <= GSKYHIP_MAX_OVR)
+      out.push_back(i);
+}
+
+int fill_info(const Tiff &t, gskyhip_raster_info *info) {
+  std::vector<int> lv;
+  levels(t, lv);
+  if (lv.empty()) return GSKYHIP_E_ARG;
+  const Ifd &d = t.ifds[lv[0]];
+  std::memset(info, 0, sizeof(*info));
+  int sb = 0;
+  info->dtype = dtype_of(d, sb);
+  if (!info->dtype) return GSKYHIP_E_TYPE;
+  info->signed_byte = sb;
+  info->xsize = (int32_t)d.width; info->ysize = (int32_t)d.height; info->n_bands = d.spp;
+  info->block_x = (int32_t)d.block_w; info->block_y = (int32_t)d.block_h;
+  info->compression = d.compression; info->predictor = d.predictor; info->planar = d.planar;
+  double *g = info->geot;
+  g[0] = 0; g[1] = 1; g[2] = 0; g[3] = 0; g[4] = 0; g[5] = 1;   // GDAL's default geotransform
+  if (d.transform.size() >= 16) {
+    const auto &m = d.transform;
+    g[0] = m[3]; g[1] = m[0]; g[2] = m[1]; g[3] = m[7]; g[4] = m[4]; g[5] = m[5];
+  } else if (d.scale.size() >= 2 && d.tiepoint.size() >= 6) {
+    const auto &tp = d.tiepoint;
+    g[1] = d.scale[0]; g[5] = -d.scale[1];
+    g[0] = tp[3] - tp[0] * g[1];
+    g[3] = tp[4] - tp[1] * g[5];
+    if (geokey(d, 1025) == 2) { g[0] -= 0.5 * g[1]; g[3] -= 0.5 * g[5]; }   // RasterPixelIsPoint
+  }
+  int epsg = geokey(d, 3072);
+  if (!epsg || epsg == 32767) {
+    if (geokey(d, 3075) == 24 &&
+        std::fabs(geodouble(d, 2057, geodouble(d, 2058, 0.0)) - 6371007.181) < 1e-3)   // CT_Sinusoidal, MODIS sphere
+      epsg = -1;
+    else if (!epsg)
+      epsg = geokey(d, 2048);
+  }
+  info->epsg = epsg == 32767 ? 0 : epsg;
+  info->has_nodata = 0;
+  info->nodata = -1e10;   // GDALGetRasterNoDataValue when unset (warp.go:246)
+  if (!d.nodata.empty()) {
+    std::string s(d.nodata.c_str());
+    char *end = nullptr;
+    const double v = std::strtod(s.c_str(), &end);
+    if (end != s.c_str()) { info->nodata = v; info->has_nodata = 1; }
+  }
+  info->n_ovr = (int32_t)lv.size() - 1;
+  for (int k = 1; k < (int)lv.size(); k++) {
+    info->ovr_xsize[k - 1] = (int32_t)t.ifds[lv[k]].width;
+    info->ovr_ysize[k - 1] = (int32_t)t.ifds[lv[k]].height;
+  }
+  return 0;
+}
+
+int open_level(const char *path, int band, int level, Tiff &t, const Ifd *&d) {
+  if (!path) return GSKYHIP_E_ARG;
+  if (!read_file(path, t.buf)) return 1;   // the reference's "open failed" (warp.go:103-110)
+  if (!parse(t)) return GSKYHIP_E_TYPE;
+  std::vector<int> lv;
+  levels(t, lv);
+  if (lv.empty() || level < 0 || level >= (int)lv.size()) return GSKYHIP_E_RANGE;
+  d = &t.ifds[lv[level]];
+  if (band < 1 || band > d->spp) return 2;   // band failed (warp.go:111-118)
+  int sb;
+  if (!dtype_of(*d, sb) || (d->bits % 8) != 0) return GSKYHIP_E_TYPE;
+  return 0;
+}
+
+}  // namespace
+}  // namespace gsky
+
+using namespace gsky;
+
+extern "C" int gskyhip_geotiff_info(const char *path, gskyhip_raster_info *info) {
+  if (!path || !info) return GSKYHIP_E_ARG;
+  Tiff t;
+  if (!read_file(path, t.buf)) return 1;
+  if (!parse(t)) return GSKYHIP_E_TYPE;
+  return fill_info(t, info);
+}
+
+extern "C" int gskyhip_geotiff_read_host(const char *path, int band, int level, void *out, int64_t out_bytes) {
+  Tiff t;
+  const Ifd *d = nullptr;
+  int rc = open_level(path, band, level, t, d);
+  if (rc) return rc;
+  const int64_t need = d->width * d->height * (d->bits / 8);
+  if (!out || out_bytes < need) return GSKYHIP_E_ARG;
+  const Layout L = layout_of(*d);
+  std::vector<uint8_t> stage((size_t)(L.across * L.down) * L.block_bytes);
+  if (!decode_band(t, *d, band - 1, stage.data())) return GSKYHIP_E_TYPE;
+  assemble_host(stage.data(), (uint8_t *)out, *d);
+  return 0;
+}
+
+extern "C" int gskyhip_geotiff_read(const char *path, int band, int level, void *dev_out, int64_t out_bytes,
+                                    void *stream) {
+  Tiff t;
+  const Ifd *d = nullptr;
+  int rc = open_level(path, band, level, t, d);
+  if (rc) return rc;
+  const int bytes = d->bits / 8;
+  const int64_t n = d->width * d->height;
+  if (!dev_out || out_bytes < n * bytes) return GSKYHIP_E_ARG;
+  const Layout L = layout_of(*d);
+  const size_t stage_bytes = (size_t)(L.across * L.down) * L.block_bytes;
+  void *host = nullptr, *dev = nullptr;
+  if (hipHostMalloc(&host, stage_bytes, hipHostMallocDefault) != hipSuccess) return GSKYHIP_E_HIP;
+  if (!decode_band(t, *d, band - 1, (uint8_t *)host)) { hipHostFree(host); return GSKYHIP_E_TYPE; }
+  hipStream_t s = (hipStream_t)stream;
+  rc = 0;
+  if (hipMallocAsync(&dev, stage_bytes, s) != hipSuccess) rc = GSKYHIP_E_HIP;
+  if (!rc && hipMemcpyAsync(dev, host, stage_bytes, hipMemcpyHostToDevice, s) != hipSuccess) rc = GSKYHIP_E_HIP;
+  if (!rc) {
+    const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+    switch (bytes) {
+      case 1: hipLaunchKernelGGL(assemble_kernel<uint8_t>, grid, blk, 0, s, (const uint8_t *)dev, (uint8_t *)dev_out, d->width, d->height, L.bw, L.bh, L.across); break;
+      case 2: hipLaunchKernelGGL(assemble_kernel<uint16_t>, grid, blk, 0, s, (const uint16_t *)dev, (uint16_t *)dev_out, d->width, d->height, L.bw, L.bh, L.across); break;
+      case 4: hipLaunchKernelGGL(assemble_kernel<uint32_t>, grid, blk, 0, s, (const uint32_t *)dev, (uint32_t *)dev_out, d->width, d->height, L.bw, L.bh, L.across); break;
+      default: hipLaunchKernelGGL(assemble_kernel<uint64_t>, grid, blk, 0, s, (const uint64_t *)dev, (uint64_t *)dev_out, d->width, d->height, L.bw, L.bh, L.across); break;
+    }
+    if (hipGetLastError() != hipSuccess) rc = GSKYHIP_E_HIP;
+  }
+  if (dev) hipFreeAsync(dev, s);
+  // the pinned staging buffer is released once the copy has completed
+  if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GSKYHIP_E_HIP;
+  hipHostFree(host);
+  return rc;
+}

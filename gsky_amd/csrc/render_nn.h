@@ -70,102 +70,176 @@ __device__ __forceinline__ uint32_t scale_int(const ScaleK &k, int32_t c) {
   return c == k.noData.i ? 0xFFu : b;
 }
 
-// The ordered fold of tile row r over the tile's entries (MergeMaskedRaster in
-// ProcessRasterStack order, tile_merger.go:38-225): c[q] is the canvas value
-// of the lane's pixel q (tile column xl + 64 q); c[] arrives holding the
-// canvas nodata.
+// One stack entry e of the ordered fold of tile row r (MergeMaskedRaster,
+// tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
+// (tile column xl + 64 q).
+template <typename T, bool MASK>
+__device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
+                                             const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
+                                             int ns_out, int r, int xb, int xl, int W, int ncols,
+                                             typename VOf<T>::type (&c)[kNnPx]) {
+  using V = typename VOf<T>::type;
+  const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
+  if (e.ns != ns_out || ew <= 0) return;
+  const int ir = r - eyoff;
+  if (ir < 0 || ir >= eh) return;
+  const int lim = max(0, min(ew, W - exoff));   // window pixel in the tile: (unsigned)ic < lim
+  const int c0 = exoff - xb, c1 = exoff + lim - xb;   // the entry's columns of the block: [c0, c1)
+  if (c1 <= 0 || c0 >= ncols) return;
+  const RowRec *rr = rows + e.row_base + ir;
+  const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
+  const int inside = __builtin_amdgcn_readfirstlane(rr->inside);
+  const int bx = e.band_x, by = e.band_y;
+  const V nd = as_v<T>(e.nd);
+  const bool fill_mode = e.fill_mode != 0;
+  const int ic0 = xl - exoff;   // window column of the lane's pixel 0
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
+  const bool masked = MASK && e.mask_pair >= 0;
+  if (kind == ROW_LINEAR && inside && c0 <= 0 && c1 >= ncols && !masked) {
+    // fast body: every pixel of the block is in the window and its source
+    // pixel in the band -- lin_coords() + nn_px() reduce to the truncations
+    const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
+    uint32_t off[kNnPx];
+#pragma unroll
+    for (int q = 0; q < kNnPx; q++) {
+      const double dist = (double)(ic0 + 64 * q);
+      const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
+      const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
+      off[q] = (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T);
+    }
+    V vv[kNnPx];
+#pragma unroll
+    for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
+    if (!fill_mode) {
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
+    }
+    return;
+  }
+  // general body: window edges, POOL rows, failed transforms, mask layer;
+  // two halves of 4 pixels (4 gathers in flight) keep the register peak
+  // of the fast body
+  const V fillv = as_v<T>(e.fill);
+#pragma unroll
+  for (int h = 0; h < kNnPx; h += 4) {
+    uint32_t idx[4];
+    if (kind == ROW_LINEAR) {
+      const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int ic = ic0 + 64 * (h + q);
+        const double dist = (double)ic;
+        idx[q] = nn_index_sxy(xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, bx, by);
+      }
+    } else {   // POOL (the only other kind of a simple tile): the leaf of each pixel
+      const int nleaf = __builtin_amdgcn_readfirstlane(rr->nleaf);
+      const Leaf *lv = pool + __builtin_amdgcn_readfirstlane(rr->pool_off);
+#pragma unroll 1
+      for (int q = 0; q < 4; q++) {
+        const int ic = ic0 + 64 * (h + q);
+        const bool in = (unsigned)ic < (unsigned)lim;
+        const Leaf &L = lv[leaf_of(lv, nleaf, in ? ic : 0)];
+        const double dist = (double)(ic - L.start);
+        idx[q] = nn_index_sxy(L.xs0 + L.dX * dist, L.ys0 + L.dY * dist, in && L.kind != LEAF_FAILED, bx, by);
+      }
+    }
+    V vv[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int ic = ic0 + 64 * (h + q);
+      const V v = idx[q] != kNoPx ? vv[q] : fillv;
+      bool take = (unsigned)ic < (unsigned)lim && (v != nd);
+      if (masked) {
+        if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, e, ic, ir);
+      }
+      const bool t2 = take && (!fill_mode || c[h + q] == nd);
+      c[h + q] = t2 ? v : c[h + q];
+    }
+  }
+}
+
+// The ordered fold of tile row r over the tile's entries in ProcessRasterStack
+// order; c[] arrives holding the canvas nodata.
 template <typename T, bool MASK>
 __device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *__restrict__ ents,
                                             const int32_t *__restrict__ ord, int n_entries,
                                             const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
                                             int ns_out, int r, int xb, int xl, int W, int ncols,
                                             typename VOf<T>::type (&c)[kNnPx]) {
+#pragma unroll 1
+  for (int k = 0; k < n_entries; k++)
+    nn_entry_row<T, MASK>(a, ents, ents[ord[k]], rows, pool, ns_out, r, xb, xl, W, ncols, c);
+}
+
+// Rows r and r + 1 together: where an entry takes the fast body on both
+// rows, their 16 gathers are issued before the first wait (twice the loads
+// in flight per wave); otherwise each row takes nn_entry_row.  The same
+// expressions and fold order per row as nn_fold_row.
+template <typename T>
+__device__ __forceinline__ void nn_fold_row2(const RenderArgs &a, const EntryD *__restrict__ ents,
+                                             const int32_t *__restrict__ ord, int n_entries,
+                                             const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
+                                             int ns_out, int r, int xb, int xl, int W, int ncols,
+                                             typename VOf<T>::type (&ca)[kNnPx], typename VOf<T>::type (&cb)[kNnPx]) {
   using V = typename VOf<T>::type;
 #pragma unroll 1
   for (int k = 0; k < n_entries; k++) {
     const EntryD &e = ents[ord[k]];
     const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
-    if (e.ns != ns_out || ew <= 0) continue;
     const int ir = r - eyoff;
-    if (ir < 0 || ir >= eh) continue;
-    const int lim = max(0, min(ew, W - exoff));   // window pixel in the tile: (unsigned)ic < lim
-    const int c0 = exoff - xb, c1 = exoff + lim - xb;   // the entry's columns of the block: [c0, c1)
-    if (c1 <= 0 || c0 >= ncols) continue;
+    const int lim = max(0, min(ew, W - exoff));
+    const int c0 = exoff - xb, c1 = exoff + lim - xb;
+    bool pair_fast = e.ns == ns_out && ew > 0 && ir >= 0 && ir + 1 < eh && c0 <= 0 && c1 >= ncols;
     const RowRec *rr = rows + e.row_base + ir;
-    const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
-    const int inside = __builtin_amdgcn_readfirstlane(rr->inside);
+    if (pair_fast) {
+      const int ka = __builtin_amdgcn_readfirstlane(rr[0].kind), ia = __builtin_amdgcn_readfirstlane(rr[0].inside);
+      const int kb = __builtin_amdgcn_readfirstlane(rr[1].kind), ib = __builtin_amdgcn_readfirstlane(rr[1].inside);
+      pair_fast = ka == ROW_LINEAR && kb == ROW_LINEAR && ia && ib;
+    }
+    if (!pair_fast) {
+      nn_entry_row<T, false>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, ca);
+      nn_entry_row<T, false>(a, ents, e, rows, pool, ns_out, r + 1, xb, xl, W, ncols, cb);
+      continue;
+    }
     const int bx = e.band_x, by = e.band_y;
     const V nd = as_v<T>(e.nd);
     const bool fill_mode = e.fill_mode != 0;
-    const int ic0 = xl - exoff;   // window column of the lane's pixel 0
+    const int ic0 = xl - exoff;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
-    const bool masked = MASK && e.mask_pair >= 0;
-    if (kind == ROW_LINEAR && inside && c0 <= 0 && c1 >= ncols && !masked) {
-      // fast body: every pixel of the block is in the window and its source
-      // pixel in the band -- lin_coords() + nn_px() reduce to the truncations
-      const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
-      uint32_t off[kNnPx];
+    V va[kNnPx], vb[kNnPx];
+    {
+      const double xs0 = rr[0].v[0], ys0 = rr[0].v[1], dX = rr[0].v[2], dY = rr[0].v[3];
 #pragma unroll
       for (int q = 0; q < kNnPx; q++) {
         const double dist = (double)(ic0 + 64 * q);
         const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
         const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
-        off[q] = (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T);
+        va[q] = buf_load<T>(rs, (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T));
       }
-      V vv[kNnPx];
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
-      if (!fill_mode) {
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
-      } else {
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
-      }
-      continue;
     }
-    // general body: window edges, POOL rows, failed transforms, mask layer;
-    // two halves of 4 pixels (4 gathers in flight) keep the register peak
-    // of the fast body
-    const V fillv = as_v<T>(e.fill);
+    {
+      const double xs0 = rr[1].v[0], ys0 = rr[1].v[1], dX = rr[1].v[2], dY = rr[1].v[3];
 #pragma unroll
-    for (int h = 0; h < kNnPx; h += 4) {
-      uint32_t idx[4];
-      if (kind == ROW_LINEAR) {
-        const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int ic = ic0 + 64 * (h + q);
-          const double dist = (double)ic;
-          idx[q] = nn_index_sxy(xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, bx, by);
-        }
-      } else {   // POOL (the only other kind of a simple tile): the leaf of each pixel
-        const int nleaf = __builtin_amdgcn_readfirstlane(rr->nleaf);
-        const Leaf *lv = pool + __builtin_amdgcn_readfirstlane(rr->pool_off);
-#pragma unroll 1
-        for (int q = 0; q < 4; q++) {
-          const int ic = ic0 + 64 * (h + q);
-          const bool in = (unsigned)ic < (unsigned)lim;
-          const Leaf &L = lv[leaf_of(lv, nleaf, in ? ic : 0)];
-          const double dist = (double)(ic - L.start);
-          idx[q] = nn_index_sxy(L.xs0 + L.dX * dist, L.ys0 + L.dY * dist, in && L.kind != LEAF_FAILED, bx, by);
-        }
+      for (int q = 0; q < kNnPx; q++) {
+        const double dist = (double)(ic0 + 64 * q);
+        const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
+        const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
+        vb[q] = buf_load<T>(rs, (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T));
       }
-      V vv[4];
+    }
+    if (!fill_mode) {
 #pragma unroll
-      for (int q = 0; q < 4; q++) vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
+      for (int q = 0; q < kNnPx; q++) { ca[q] = (va[q] != nd) ? va[q] : ca[q]; cb[q] = (vb[q] != nd) ? vb[q] : cb[q]; }
+    } else {
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int ic = ic0 + 64 * (h + q);
-        const V v = idx[q] != kNoPx ? vv[q] : fillv;
-        bool take = (unsigned)ic < (unsigned)lim && (v != nd);
-        if (masked) {
-          if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, e, ic, ir);
-        }
-        const bool t2 = take && (!fill_mode || c[h + q] == nd);
-        c[h + q] = t2 ? v : c[h + q];
-      }
+      for (int q = 0; q < kNnPx; q++) { ca[q] = (ca[q] == nd) ? va[q] : ca[q]; cb[q] = (cb[q] == nd) ? vb[q] : cb[q]; }
     }
   }
 }
@@ -193,8 +267,8 @@ __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint3
 // block).  Rows are processed one after the other; a row's RGBA stores are
 // issued before the next row's gathers (deferring them behind those gathers
 // measured 0.6 % slower on C2 and C5, profiles/r03b_ab_nn.jsonl).
-template <typename T, bool MASK, bool CANVAS, int RPW>
-__global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
+template <typename T, bool MASK, bool CANVAS, int RPW, bool PAIR = false>
+__global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
                                                                       const Leaf *__restrict__ pool,
@@ -254,9 +328,23 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   };
 
 #pragma unroll 1
-  for (int j = 0; j < RPW; j++) {
+  for (int j = 0; j < RPW; j += PAIR ? 2 : 1) {
     const int r = r0 + j;
     if (r >= H) break;
+    if constexpr (PAIR && !MASK && !CANVAS) {
+      if (r + 1 < H) {   // rows r, r + 1 with their gathers in flight together
+        V ca[kNnPx], cb[kNnPx];
+#pragma unroll
+        for (int q = 0; q < kNnPx; q++) { ca[q] = cnod; cb[q] = cnod; }
+        nn_fold_row2<T>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, ca, cb);
+        uint32_t px[kNnPx];
+        nn_rgba<T>(sk, safe, s_tab, ca, px);
+        store_row(r, px);
+        nn_rgba<T>(sk, safe, s_tab, cb, px);
+        store_row(r + 1, px);
+        continue;
+      }
+    }
     V c[kNnPx];
 #pragma unroll
     for (int q = 0; q < kNnPx; q++) c[q] = cnod;
@@ -410,10 +498,10 @@ __global__ __launch_bounds__(64 * (NP + 1)) void render_nn_ws_kernel(RenderArgs 
 constexpr int kNnRpw8MinItems = 32768;
 constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
 
-template <typename T, bool M, bool C, int RPW>
+template <typename T, bool M, bool C, int RPW, bool PAIR = false>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, PAIR>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -433,6 +521,12 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
   if (const char *w = getenv("GSKYHIP_NN_WS")) ws = atoi(w);
   if (const char *x = getenv("GSKYHIP_NN_XCD")) xcd = atoi(x);
+#endif
+#ifdef GSKYHIP_AB
+  if (const char *pr = getenv("GSKYHIP_NN_PAIR")) {
+    if (!mask && !canvas && atoi(pr) == 8) { launch_nn_v<T, false, false, 8, true>(a, s); return; }
+    if (!mask && !canvas && atoi(pr) == 4) { launch_nn_v<T, false, false, 4, true>(a, s); return; }
+  }
 #endif
   if (!mask && !canvas && ws > 0) {
     const int cb = (a.max_w + kBandCols - 1) / kBandCols;

@@ -121,10 +121,44 @@ typedef struct {
     const char *bit_tests[GSKYHIP_MAX_BIT_TESTS];
 } gskyhip_mask;
 
+/* ---- native granule ingest ------------------------- */
+/* What GDALOpenEx + GDALGetGeoTransform / GetRasterNoDataValue / GetOverview
+ * report for a GeoTIFF (warp.go:89-101, 156-198, 246): classic TIFF and
+ * BigTIFF, striped or tiled, chunky or planar, none / LZW / Deflate /
+ * PackBits, predictors 1-3, 8-64 bit samples.  epsg: ProjectedCSTypeGeoKey
+ * or GeographicTypeGeoKey, -1 for a user-defined sinusoidal on the MODIS
+ * sphere, 0 when unknown.  nodata -1e10 when GDAL_NODATA is absent (the
+ * value GDALGetRasterNoDataValue returns, warp.go:246). */
+typedef struct {
+    int32_t xsize, ysize, n_bands, dtype;
+    int32_t signed_byte, block_x, block_y;
+    int32_t compression, predictor, planar;
+    int32_t epsg, has_nodata, n_ovr, _pad;
+    double geot[6];
+    double nodata;
+    int32_t ovr_xsize[GSKYHIP_MAX_OVR], ovr_ysize[GSKYHIP_MAX_OVR];
+} gskyhip_raster_info;
+
+int gskyhip_geotiff_info(const char *path, gskyhip_raster_info *info);
+/* Band `band` (1-based) of level `level` (0 = full resolution, k = overview
+ * k) row-major into HOST memory (no device work; out_bytes >= x*y*size). */
+int gskyhip_geotiff_read_host(const char *path, int band, int level, void *out, int64_t out_bytes);
+/* The same into device memory: blocks decompressed by host threads into
+ * pinned staging, one H2D copy, placed row-major on the GPU; returns after
+ * the copy (the staging buffer is freed). */
+int gskyhip_geotiff_read(const char *path, int band, int level, void *dev_out, int64_t out_bytes, void *stream);
+/* Decode every level of (path, band) into HBM owned by the library and
+ * register it for warp_operation_fast (freed by gskyhip_unregister_all).
+ * warp_operation_fast does this itself for an unregistered *.tif / *.tiff
+ * path, as GDALOpenEx would open it.  Returns 0, 1 (open failed), 2 (no such
+ * band) or GSKYHIP_E_*. */
+int gskyhip_register_geotiff(const char *path, int band);
+
 /* ---- drop-in for the cgo entry point of the worker ----------------------- */
 /* Registers an HBM-resident granule under (path, band) so that the drop-in
- * below can find it (it replaces GDALOpenEx in warp.go:89-101; file decode
- * stays out of scope).  `g->data` etc. must stay valid until unregistered. */
+ * below can find it (it replaces GDALOpenEx in warp.go:89-101; GeoTIFF files
+ * the library decodes itself: gskyhip_register_geotiff above).  `g->data`
+ * etc. must stay valid until unregistered. */
 int gskyhip_register_granule(const char *path, int band, const gskyhip_granule *g,
                              const char *srs);
 int gskyhip_unregister_all(void);

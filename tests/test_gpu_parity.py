@@ -492,6 +492,30 @@ def test_drill_deciles_parity(gpu, oracle, dcount, pc, clip):
                           vals[..., 1:].astype(np.float32)[stt.cpu().numpy() == 0])
 
 
+@pytest.mark.parametrize("side", [100, 150])
+def test_drill_deciles_large_polygon(gpu, oracle, side):
+    """Segments past the select workgroup's LDS key cache (~10k keys for 9
+    deciles): a 150 x 150 in-mask window streams its values from the segment
+    on every radix pass, a 100 x 100 one selects from LDS; both equal to the
+    oracle for every band, nodata values (-9999 at 1 %) skipped."""
+    import torch
+
+    from gsky_amd import drill
+    rng = np.random.default_rng(side)
+    data = rng.uniform(0.0, 0.05, size=(5, 160, 160)).astype(np.float32)
+    data[rng.uniform(size=data.shape) < 0.01] = -9999.0
+    data[2] = np.round(data[2] * 100) / 100   # many equal values: ties across the ranks
+    st = drill.DrillStack(torch.from_numpy(data), -9999.0, gpu)
+    mask = np.full((side, side), 255, np.uint8)
+    mask[::7, ::3] = 0
+    mb = drill.pack_masks([(3, 4, side, side)], [mask], gpu)
+    vals, cnts = drill.read_data(st, mb, decile_count=9)
+    vals = vals.cpu().numpy()
+    for b in range(5):
+        exp = oracle.compute_deciles(data[b, 4:4 + side, 3:3 + side], mask, -9999.0, 9)
+        assert np.array_equal(vals[0, b, 1:].astype(np.float32), exp), b
+
+
 @pytest.mark.parametrize("strides,dcount,pc,nb", [(2, 9, 0, 23), (3, 9, 0, 23), (3, 4, 1, 22), (5, 9, 0, 21),
                                                   (1, 9, 0, 23)])
 def test_drill_deciles_strides_parity(gpu, oracle, strides, dcount, pc, nb):

@@ -1,0 +1,323 @@
+"""Native GeoTIFF ingest (gsky_amd/csrc/ingest.hip): the
+decoder against files written by an independent TIFF implementation
+(Pillow's libtiff: every compression it writes, predictors 2 and 3, chunky
+RGB) and against the layouts Pillow cannot write, made by the small TIFF
+writer below (tiles with edge tiles, BigTIFF, big-endian, planar bands,
+int16 / int8 / float64 samples, predictor 2 on 16-bit samples, GeoTIFF
+georeferencing, GDAL_NODATA, reduced-resolution IFDs as overviews).  CPU
+tests decode on the host (gskyhip_geotiff_read_host, no device work); the
+GPU tests decode into HBM and warp a registered file through
+warp_operation_fast against the same array registered directly."""
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from gsky_amd import ingest
+
+PIL = pytest.importorskip("PIL.Image")
+
+
+# ---------------------------------------------------------------- a small TIFF writer
+def _packbits(b: bytes) -> bytes:
+    out, i = bytearray(), 0
+    while i < len(b):
+        j = i
+        while j + 1 < len(b) and b[j + 1] == b[i] and j - i < 127:
+            j += 1
+        if j > i:
+            out += bytes([(257 - (j - i + 1)) & 0xFF, b[i]])
+            i = j + 1
+        else:
+            k = i
+            while k < len(b) and k - i < 128 and not (k + 1 < len(b) and b[k + 1] == b[k]):
+                k += 1
+            k = max(k, i + 1)
+            out += bytes([k - i - 1]) + b[i:k]
+            i = k
+    return bytes(out)
+
+
+def _predict(block: np.ndarray, predictor: int) -> np.ndarray:
+    """block (rows, cols, samples) -> the bytes the predictor stores."""
+    if predictor == 2:
+        d = block.copy()
+        d[:, 1:] = block[:, 1:] - block[:, :-1]   # wraps in the sample type
+        return d
+    return block
+
+
+def write_tiff(path, planes, tile=None, rows_per_strip=None, compression=1, predictor=1, big=False, be=False,
+               planar=2, geo=None, nodata=None, overviews=()):
+    """planes: list of 2-D arrays (bands) of one dtype; overviews: list of
+    lists of planes written as reduced-resolution IFDs after the first."""
+    bo = ">" if be else "<"
+    dt = planes[0].dtype
+    fmt = {"u": 1, "i": 2, "f": 3}[dt.kind]
+    out = bytearray(b"MM" if be else b"II")
+    out += struct.pack(bo + "H", 43 if big else 42)
+    if big:
+        out += struct.pack(bo + "HHQ", 8, 0, 0)
+    else:
+        out += struct.pack(bo + "I", 0)
+    first_ptr = 8 if big else 4
+    prev_next_ptr = first_ptr
+    levels = [planes] + [list(o) for o in overviews]
+    for lvl, bands in enumerate(levels):
+        h, w = bands[0].shape
+        nb = len(bands)
+        if tile:
+            tw, th = tile
+            across, down = -(-w // tw), -(-h // th)
+        else:
+            tw, th = w, rows_per_strip or h
+            across, down = 1, -(-h // th)
+        chunks = []
+        arr = np.stack(bands, -1).astype(dt.newbyteorder(">" if be else "<"))
+        groups = [[b] for b in range(nb)] if planar == 2 else [list(range(nb))]
+        for grp in groups:
+            for by in range(down):
+                for bx in range(across):
+                    if tile:
+                        blk = np.zeros((th, tw, len(grp)), arr.dtype)
+                        src = arr[by * th:(by + 1) * th, bx * tw:(bx + 1) * tw][..., grp]
+                        blk[:src.shape[0], :src.shape[1]] = src
+                    else:
+                        blk = arr[by * th:(by + 1) * th][..., grp]
+                    raw = _predict(blk, predictor).tobytes()
+                    chunks.append(zlib.compress(raw) if compression == 8 else
+                                  _packbits(raw) if compression == 32773 else raw)
+        offs = []
+        for c in chunks:
+            offs.append(len(out))
+            out += c
+            if len(out) % 2:
+                out += b"\0"
+        ents = []   # (tag, type, values)
+        ents.append((254, 4, [1 if lvl else 0]))
+        ents.append((256, 4, [w]))
+        ents.append((257, 4, [h]))
+        ents.append((258, 3, [dt.itemsize * 8] * nb))
+        ents.append((259, 3, [compression]))
+        ents.append((262, 3, [1]))
+        if not tile:
+            ents.append((273, 16 if big else 4, offs))
+        ents.append((277, 3, [nb]))
+        if not tile:
+            ents.append((278, 4, [th]))
+            ents.append((279, 16 if big else 4, [len(c) for c in chunks]))
+        ents.append((284, 3, [planar]))
+        if predictor != 1:
+            ents.append((317, 3, [predictor]))
+        if tile:
+            ents.append((322, 3, [tw]))
+            ents.append((323, 3, [th]))
+            ents.append((324, 16 if big else 4, offs))
+            ents.append((325, 16 if big else 4, [len(c) for c in chunks]))
+        ents.append((339, 3, [fmt] * nb))
+        if geo and lvl == 0:
+            for tag, typ, vals in geo:
+                ents.append((tag, typ, vals))
+        if nodata is not None and lvl == 0:
+            ents.append((42113, 2, nodata))
+        ents.sort()
+        ifd_off = len(out)
+        out[prev_next_ptr:prev_next_ptr + (8 if big else 4)] = struct.pack(bo + ("Q" if big else "I"), ifd_off)
+        esz, inl = (20, 8) if big else (12, 4)
+        body = bytearray(struct.pack(bo + ("Q" if big else "H"), len(ents)))
+        extra = bytearray()
+        extra_base = ifd_off + len(body) + esz * len(ents) + (8 if big else 4)
+        tcode = {2: "s", 3: "H", 4: "I", 12: "d", 16: "Q"}
+        tsize = {2: 1, 3: 2, 4: 4, 12: 8, 16: 8}
+        for tag, typ, vals in ents:
+            if typ == 2:
+                data = vals.encode() + b"\0"
+                cnt = len(data)
+            else:
+                data = struct.pack(bo + "%d%s" % (len(vals), tcode[typ]), *vals)
+                cnt = len(vals)
+            ent = struct.pack(bo + ("HHQ" if big else "HHI"), tag, typ, cnt)
+            if len(data) <= inl:
+                ent += data + b"\0" * (inl - len(data))
+            else:
+                ent += struct.pack(bo + ("Q" if big else "I"), extra_base + len(extra))
+                extra += data
+                if len(extra) % 2:
+                    extra += b"\0"
+            body += ent
+        prev_next_ptr = ifd_off + len(body)
+        body += b"\0" * (8 if big else 4)
+        out += body + extra
+    with open(path, "wb") as f:
+        f.write(bytes(out))
+
+
+def geokeys(model=1, raster=1, keys=()):
+    """GeoKeyDirectory: (key, value) SHORT keys after GTModelType / GTRasterType."""
+    ks = [(1024, model), (1025, raster)] + list(keys)
+    vals = [1, 1, 0, len(ks)]
+    for k, v in ks:
+        vals += [k, 0, 1, v]
+    return (34735, 3, vals)
+
+
+# ---------------------------------------------------------------- Pillow-written files
+@pytest.mark.parametrize("comp", ["raw", "tiff_deflate", "tiff_lzw", "packbits"])
+@pytest.mark.parametrize("mode", ["L", "I;16", "I", "F"])
+def test_pillow_compressions(tmp_path, comp, mode):
+    rng = np.random.default_rng(len(comp) * 7 + len(mode))
+    a = {"L": lambda: rng.integers(0, 256, (97, 131)).astype(np.uint8),
+         "I;16": lambda: rng.integers(0, 65536, (97, 131)).astype(np.uint16),
+         "I": lambda: rng.integers(-2**31, 2**31 - 1, (97, 131)).astype(np.int32),
+         "F": lambda: rng.standard_normal((97, 131)).astype(np.float32)}[mode]()
+    a[5:9, 10:50] = a[5, 10]   # runs for PackBits / LZW
+    p = str(tmp_path / "a.tif")
+    PIL.fromarray(a).save(p, compression=comp)
+    inf = ingest.info(p)
+    assert (inf.xsize, inf.ysize, inf.n_bands) == (131, 97, 1)
+    assert np.array_equal(ingest.read_host(p), a)
+
+
+@pytest.mark.parametrize("pred", [2, 3])
+def test_pillow_float_predictors(tmp_path, pred):
+    f = np.random.default_rng(pred).standard_normal((61, 203)).astype(np.float32)
+    p = str(tmp_path / "f.tif")
+    PIL.fromarray(f).save(p, compression="tiff_deflate", tiffinfo={317: pred})
+    assert ingest.info(p).predictor == pred
+    assert np.array_equal(ingest.read_host(p), f)
+
+
+def test_pillow_uint16_predictor2_and_rgb(tmp_path):
+    a = np.random.default_rng(5).integers(0, 65536, (40, 300)).astype(np.uint16)
+    p = str(tmp_path / "u.tif")
+    PIL.fromarray(a).save(p, compression="tiff_lzw", tiffinfo={317: 2})
+    assert np.array_equal(ingest.read_host(p), a)
+    rgb = np.random.default_rng(6).integers(0, 256, (50, 61, 3)).astype(np.uint8)
+    p = str(tmp_path / "rgb.tif")
+    PIL.fromarray(rgb).save(p, compression="tiff_deflate")
+    inf = ingest.info(p)
+    assert inf.n_bands == 3 and inf.planar == 1
+    for b in range(3):
+        assert np.array_equal(ingest.read_host(p, b + 1), rgb[..., b])
+
+
+# ---------------------------------------------------------------- layouts Pillow cannot write
+@pytest.mark.parametrize("big,be", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("comp,pred", [(1, 1), (8, 2), (32773, 1), (8, 1)])
+def test_tiled_planar_int16(tmp_path, big, be, comp, pred):
+    rng = np.random.default_rng(comp + pred + 2 * big + be)
+    b1 = rng.integers(-32768, 32767, (150, 210)).astype(np.int16)
+    b2 = (b1 // 3).astype(np.int16)
+    p = str(tmp_path / "t.tif")
+    write_tiff(p, [b1, b2], tile=(64, 48), compression=comp, predictor=pred, big=big, be=be, planar=2)
+    inf = ingest.info(p)
+    assert (inf.xsize, inf.ysize, inf.n_bands, inf.block) == (210, 150, 2, (64, 48))
+    assert inf.dtype == 3 and not inf.signed_byte
+    assert np.array_equal(ingest.read_host(p, 1), b1)
+    assert np.array_equal(ingest.read_host(p, 2), b2)
+
+
+@pytest.mark.parametrize("dt", [np.int8, np.uint8, np.float64, np.uint32])
+def test_strips_chunky_types(tmp_path, dt):
+    rng = np.random.default_rng(11)
+    bands = [(rng.standard_normal((77, 45)) * 100).astype(dt) for _ in range(3)]
+    p = str(tmp_path / "s.tif")
+    write_tiff(p, bands, rows_per_strip=10, compression=8, planar=1)
+    inf = ingest.info(p)
+    assert inf.signed_byte == (dt == np.int8)
+    for k in range(3):
+        got = ingest.read_host(p, k + 1)
+        assert np.array_equal(got.view(dt) if got.dtype != dt else got, bands[k]), k
+
+
+def test_geotiff_georeferencing(tmp_path):
+    """GDAL's reading of the GeoTIFF tags: tiepoint + pixel scale ->
+    geotransform, PixelIsPoint shifted by half a pixel, ModelTransformation,
+    EPSG from the GeoKeys (projected, geographic, MODIS sinusoidal),
+    GDAL_NODATA, -1e10 when absent (warp.go:246), overview sizes."""
+    a = np.arange(40 * 30, dtype=np.int16).reshape(30, 40)
+    ov = [a[::2, ::2].copy()], [a[::4, ::4].copy()]
+    p = str(tmp_path / "g.tif")
+    geo = [(33550, 12, [25.0, 25.0, 0.0]), (33922, 12, [0.0, 0.0, 0.0, 1400000.0, -3800000.0, 0.0]),
+           geokeys(1, 1, [(3072, 3577)])]
+    write_tiff(p, [a], tile=(16, 16), geo=geo, nodata="-999", overviews=ov)
+    inf = ingest.info(p)
+    assert inf.geot == (1400000.0, 25.0, 0.0, -3800000.0, 0.0, -25.0)
+    assert inf.epsg == 3577 and inf.srs == "EPSG:3577" and inf.nodata == -999.0
+    assert inf.overviews == [(20, 15), (10, 8)]
+    assert np.array_equal(ingest.read_host(p, 1, 1), a[::2, ::2])
+    assert np.array_equal(ingest.read_host(p, 1, 2), a[::4, ::4])
+    # PixelIsPoint, geographic CRS, no nodata
+    p2 = str(tmp_path / "g2.tif")
+    write_tiff(p2, [a], geo=[(33550, 12, [0.5, 0.5, 0.0]), (33922, 12, [0, 0, 0, 112.0, -10.0, 0]),
+                             geokeys(2, 2, [(2048, 4326)])])
+    inf = ingest.info(p2)
+    assert inf.geot == (111.75, 0.5, 0.0, -9.75, 0.0, -0.5) and inf.epsg == 4326 and inf.nodata is None
+    # ModelTransformation (rotated grid) and a user-defined sinusoidal on the MODIS sphere
+    p3 = str(tmp_path / "g3.tif")
+    mt = [463.3, 0.1, 0.0, -20015109.354, 0.2, -463.3, 0.0, 10007554.677, 0, 0, 0, 0, 0, 0, 0, 1]
+    keys = geokeys(1, 1, [(3072, 32767), (3075, 24)])
+    keys = (keys[0], keys[1], keys[2][:3] + [keys[2][3] + 1] + keys[2][4:] + [2057, 34736, 1, 0])
+    write_tiff(p3, [a], geo=[(34264, 12, mt), keys, (34736, 12, [6371007.181])])
+    inf = ingest.info(p3)
+    assert inf.geot == (-20015109.354, 463.3, 0.1, 10007554.677, 0.2, -463.3) and inf.srs == "MODIS"
+
+
+def test_missing_file_and_band(tmp_path):
+    from gsky_amd import GskyError
+    with pytest.raises(GskyError) as e:
+        ingest.info(str(tmp_path / "none.tif"))
+    assert e.value.code == 1                     # open failed (warp.go:103-110)
+    p = str(tmp_path / "one.tif")
+    write_tiff(p, [np.zeros((4, 4), np.uint8)])
+    with pytest.raises(GskyError) as e:
+        ingest.read_host(p, 2)
+    assert e.value.code == 2                     # band failed (warp.go:111-118)
+
+
+# ---------------------------------------------------------------- GPU: into HBM, through the drop-in
+@pytest.mark.gpu
+def test_gpu_read_matches_host(tmp_path):
+    import torch
+    rng = np.random.default_rng(3)
+    a = rng.integers(-20000, 20000, (1000, 1300)).astype(np.int16)
+    p = str(tmp_path / "big.tif")
+    write_tiff(p, [a, (a // 2).astype(np.int16)], tile=(256, 256), compression=8, predictor=2, big=True)
+    for band, exp in ((1, a), (2, a // 2)):
+        got = ingest.read(p, band).cpu().numpy()
+        assert got.dtype == np.int16 and np.array_equal(got, exp)
+    f = rng.standard_normal((333, 517)).astype(np.float32)
+    p2 = str(tmp_path / "f.tif")
+    PIL.fromarray(f).save(p2, compression="tiff_lzw", tiffinfo={317: 3})
+    assert np.array_equal(ingest.read(p2).cpu().numpy(), f)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_gpu_drop_in_opens_geotiff(tmp_path):
+    """warp_operation_fast on an unregistered *.tif path decodes it the way
+    GDALOpenEx would (warp.go:89-101) and warps it bit-identically to the
+    same array registered by hand."""
+    import torch
+
+    from gsky_amd import synth, worker
+    cfg = synth.config_c2(scale=0.05, tiles_per_side=2, tile_px=128)
+    g = cfg.granules[0]
+    p = str(tmp_path / "granule.tif")
+    geo = [(33550, 12, [g.geot[1], -g.geot[5], 0.0]), (33922, 12, [0, 0, 0, g.geot[0], g.geot[3], 0]),
+           geokeys(1, 1, [(3072, 3577)])]
+    write_tiff(p, [g.data], tile=(64, 64), compression=8, predictor=2, geo=geo, nodata="%g" % g.nodata)
+    worker.unregister_all()
+    worker.register_granule("hand", 1, torch.from_numpy(g.data).cuda(), g.geot, "EPSG:3577", g.nodata)
+    bbox, w, h = cfg.tiles[0]
+    req = dict(band=1, dst_srs="EPSG:3857", bbox=bbox, width=w, height=h)
+    a = worker.warp_raster(worker.GeoRPCGranule(path="hand", **req))
+    b = worker.warp_raster(worker.GeoRPCGranule(path=p, **req))
+    assert a.error == "OK" and b.error == "OK"
+    assert np.array_equal(np.asarray(a.data), np.asarray(b.data)) and a.bbox == b.bbox
+    assert b.no_data == g.nodata
+    assert worker.warp_raster(worker.GeoRPCGranule(path=str(tmp_path / "absent.tif"), **req)).error == \
+        "warp_operation() fail: 1"
+    worker.unregister_all()
