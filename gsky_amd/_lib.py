@@ -100,6 +100,7 @@ EXPORTS = [
     "gskyhip_png_workspace_size", "gskyhip_png_bound", "gskyhip_encode_png",
     "gskyhip_geotiff_workspace_size", "gskyhip_geotiff_bound", "gskyhip_encode_geotiff",
     "gskyhip_geotiff_info", "gskyhip_geotiff_read_host", "gskyhip_geotiff_read", "gskyhip_register_geotiff",
+    "gskyhip_netcdf_info", "gskyhip_netcdf_read_host", "gskyhip_netcdf_read", "gskyhip_register_netcdf",
 ]
 
 _lib = None
@@ -121,6 +122,10 @@ def lib() -> C.CDLL:
     L.gskyhip_geotiff_read_host.argtypes = [C.c_char_p, ci, ci, vp, i64]
     L.gskyhip_geotiff_read.argtypes = [C.c_char_p, ci, ci, vp, i64, vp]
     L.gskyhip_register_geotiff.argtypes = [C.c_char_p, ci]
+    L.gskyhip_netcdf_info.argtypes = [C.c_char_p, C.POINTER(RasterInfo)]
+    L.gskyhip_netcdf_read_host.argtypes = [C.c_char_p, ci, vp, i64]
+    L.gskyhip_netcdf_read.argtypes = [C.c_char_p, ci, vp, i64, vp]
+    L.gskyhip_register_netcdf.argtypes = [C.c_char_p, ci]
     L.warp_operation_fast.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(d), vp, C.c_char_p, C.POINTER(d),
                                       ci, ci, ci, ci, C.POINTER(vp), C.POINTER(ci), C.POINTER(ci),
                                       C.POINTER(d), C.POINTER(ci), C.POINTER(ci)]

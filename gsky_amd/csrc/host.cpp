@@ -330,6 +330,39 @@ int ingest_geotiff_locked(DropIn &d, const std::string &path, int band) {
   return 0;
 }
 
+// The same for a netCDF classic variable band (band_query semantics,
+// warp.go:89-101: the band is registered under (path, band)).
+int ingest_netcdf_locked(DropIn &d, const std::string &path, int band) {
+  gskyhip_raster_info info;
+  int rc = gskyhip_netcdf_info(path.c_str(), &info);
+  if (rc) return rc;
+  if (band < 1 || band > info.n_bands) return 1;   // band_query past the variable: the open fails
+  if (!have_gpu()) return GSKYHIP_E_NOGPU;
+  const int ts = type_size(info.dtype);
+  if (ts <= 0) return GSKYHIP_E_TYPE;
+  Registered r;
+  std::memset(&r.g, 0, sizeof(r.g));
+  void *p = nullptr;
+  const int64_t bytes = (int64_t)info.xsize * info.ysize * ts;
+  if (hipMalloc(&p, (size_t)bytes) != hipSuccess) return GSKYHIP_E_HIP;
+  r.owned.push_back(p);
+  if ((rc = gskyhip_netcdf_read(path.c_str(), band, p, bytes, nullptr))) { release(r); return rc; }
+  gskyhip_granule &g = r.g;
+  g.data = p;
+  g.dtype = info.dtype; g.xsize = info.xsize; g.ysize = info.ysize; g.signed_byte = info.signed_byte;
+  for (int k = 0; k < 6; k++) g.geot[k] = info.geot[k];
+  g.nodata = info.nodata; g.has_nodata = info.has_nodata;
+  g.block_x = info.block_x; g.block_y = info.block_y;
+  r.has_crs = false;
+  char srs[32] = {0};
+  if (info.epsg > 0) std::snprintf(srs, sizeof(srs), "EPSG:%d", info.epsg);
+  if (srs[0] && parse_srs(srs, &r.crs) == 0) r.has_crs = true;
+  auto it = d.reg.find({path, band});
+  if (it != d.reg.end()) release(it->second);
+  d.reg[{path, band}] = std::move(r);
+  return 0;
+}
+
 bool is_geotiff_path(const std::string &p) {
   auto ends = [&](const char *suf) {
     const size_t n = std::strlen(suf);
@@ -400,6 +433,13 @@ int gskyhip_register_geotiff(const char *path, int band) {
   return ingest_geotiff_locked(d, path, band);
 }
 
+int gskyhip_register_netcdf(const char *path, int band) {
+  if (!path) return GSKYHIP_E_ARG;
+  DropIn &d = dropin();
+  std::lock_guard<std::mutex> lk(d.mu);
+  return ingest_netcdf_locked(d, path, band);
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------- warp batches
@@ -425,8 +465,8 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     const bool netcdf = q.path.compare(0, 7, "NETCDF:") == 0 ||
                         (q.path.size() >= 3 && q.path.compare(q.path.size() - 3, 3, ".nc") == 0);
     auto it = d.reg.find({q.path, q.band});
-    if (it == d.reg.end() && !netcdf && is_geotiff_path(q.path)) {   // GDALOpenEx of a file nobody registered
-      const int irc = ingest_geotiff_locked(d, q.path, q.band);
+    if (it == d.reg.end() && (netcdf || is_geotiff_path(q.path))) {   // GDALOpenEx of a file nobody registered
+      const int irc = netcdf ? ingest_netcdf_locked(d, q.path, q.band) : ingest_geotiff_locked(d, q.path, q.band);
       if (irc == 1 || irc == 2) { r.rc = irc; continue; }
       it = d.reg.find({q.path, q.band});
     }

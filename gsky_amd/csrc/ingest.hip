@@ -13,6 +13,18 @@
 // (42113), internal overviews from the reduced-resolution IFDs in file
 // order (GDALGetOverview order).
 //
+// netCDF classic (CDF-1, CDF-2 64-bit offsets, CDF-5 64-bit data), the
+// format the GSKY_netCDF driver opens with nc_open (libs/gdal/frmts/
+// gsky_netcdf/netcdfdataset.cpp): "NETCDF:file:var" or a file with one data
+// variable; the band is the index along the leading dimension of a 3-D
+// variable (band_query, netcdfdataset.cpp:6994-7021, warp.go:89-101); the
+// geotransform from the 1-D coordinate variables as the driver computes it
+// (netcdfdataset.cpp:3504-3655: actual_range when present, y reversed when
+// increasing -- bBottomUp, rows then read south-up so row 0 is the north);
+// nodata from _FillValue / missing_value; EPSG:4326 for lon / lat axes,
+// else an EPSG from the grid mapping's crs_wkt / spatial_ref AUTHORITY.
+// netCDF-4 (HDF5) files are not read (no HDF5 in the image).
+//
 // Device path: the band's blocks are decompressed and un-predicted by host
 // threads (zlib / LZW / PackBits are byte-serial), staged block-major in
 // pinned memory, copied to HBM in one transfer and placed row-major by
@@ -542,6 +554,381 @@ extern "C" int gskyhip_geotiff_read(const char *path, int band, int level, void 
   }
   if (dev) hipFreeAsync(dev, s);
   // the pinned staging buffer is released once the copy has completed
+  if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GSKYHIP_E_HIP;
+  hipHostFree(host);
+  return rc;
+}
+
+// ======================================================================== netCDF classic
+namespace gsky {
+namespace {
+
+struct NcAtt { std::string name; int type = 0; std::vector<double> num; std::string text; };
+struct NcVar {
+  std::string name;
+  std::vector<int> dims;
+  std::vector<NcAtt> atts;
+  int type = 0;
+  uint64_t vsize = 0, begin = 0;
+  bool record = false;
+};
+struct Nc {
+  std::vector<uint8_t> buf;
+  int version = 1;
+  uint64_t numrecs = 0, recsize = 0;
+  std::vector<std::pair<std::string, uint64_t>> dims;
+  int rec_dim = -1;
+  std::vector<NcAtt> gatts;
+  std::vector<NcVar> vars;
+};
+
+int nc_type_size(int t) {
+  switch (t) {
+    case 1: case 2: case 7: return 1;   // byte, char, ubyte
+    case 3: case 8: return 2;           // short, ushort
+    case 4: case 5: case 9: return 4;   // int, float, uint
+    case 6: case 10: case 11: return 8; // double, int64, uint64
+    default: return 0;
+  }
+}
+
+struct NcCursor {
+  const std::vector<uint8_t> &b;
+  size_t p;
+  bool ok = true;
+  uint32_t u32() {
+    if (p + 4 > b.size()) { ok = false; return 0; }
+    const uint32_t v = ((uint32_t)b[p] << 24) | ((uint32_t)b[p + 1] << 16) | ((uint32_t)b[p + 2] << 8) | b[p + 3];
+    p += 4;
+    return v;
+  }
+  uint64_t u64() { const uint64_t hi = u32(); return (hi << 32) | u32(); }
+  std::string name(int ver) {
+    const uint64_t n = ver == 5 ? u64() : u32();
+    if (!ok || p + n > b.size()) { ok = false; return ""; }
+    std::string s((const char *)&b[p], (size_t)n);
+    p += (n + 3) & ~(uint64_t)3;
+    return s;
+  }
+};
+
+double nc_value(const uint8_t *q, int type) {
+  uint64_t v = 0;
+  const int n = nc_type_size(type);
+  for (int k = 0; k < n; k++) v = (v << 8) | q[k];
+  switch (type) {
+    case 1: return (double)(int8_t)v;
+    case 7: return (double)(uint8_t)v;
+    case 3: return (double)(int16_t)v;
+    case 8: return (double)(uint16_t)v;
+    case 4: return (double)(int32_t)v;
+    case 9: return (double)(uint32_t)v;
+    case 10: return (double)(int64_t)v;
+    case 11: return (double)v;
+    case 5: { uint32_t u = (uint32_t)v; float f; std::memcpy(&f, &u, 4); return f; }
+    case 6: { double d; std::memcpy(&d, &v, 8); return d; }
+    default: return 0.0;
+  }
+}
+
+bool nc_atts(NcCursor &c, int ver, std::vector<NcAtt> &out) {
+  const uint32_t tag = c.u32();
+  const uint64_t n = ver == 5 ? c.u64() : c.u32();
+  if (tag == 0 && n == 0) return c.ok;
+  if (tag != 0x0C) return false;
+  for (uint64_t i = 0; i < n && c.ok; i++) {
+    NcAtt a;
+    a.name = c.name(ver);
+    a.type = (int)c.u32();
+    const uint64_t cnt = ver == 5 ? c.u64() : c.u32();
+    const int ts = nc_type_size(a.type);
+    if (!ts || c.p + cnt * ts > c.b.size()) return false;
+    if (a.type == 2) a.text.assign((const char *)&c.b[c.p], (size_t)cnt);
+    else for (uint64_t k = 0; k < cnt; k++) a.num.push_back(nc_value(&c.b[c.p + k * ts], a.type));
+    c.p += (cnt * ts + 3) & ~(uint64_t)3;
+    out.push_back(std::move(a));
+  }
+  return c.ok;
+}
+
+bool nc_parse(Nc &f) {
+  const std::vector<uint8_t> &b = f.buf;
+  if (b.size() < 8 || b[0] != 'C' || b[1] != 'D' || b[2] != 'F') return false;
+  f.version = b[3];
+  if (f.version != 1 && f.version != 2 && f.version != 5) return false;
+  NcCursor c{b, 4};
+  const int ver = f.version;
+  f.numrecs = ver == 5 ? c.u64() : c.u32();
+  uint32_t tag = c.u32();
+  uint64_t n = ver == 5 ? c.u64() : c.u32();
+  if (tag == 0x0A) {
+    for (uint64_t i = 0; i < n && c.ok; i++) {
+      std::string nm = c.name(ver);
+      const uint64_t len = ver == 5 ? c.u64() : c.u32();
+      if (len == 0) f.rec_dim = (int)i;
+      f.dims.emplace_back(nm, len);
+    }
+  } else if (tag != 0 || n != 0) {
+    return false;
+  }
+  if (!nc_atts(c, ver, f.gatts)) return false;
+  tag = c.u32();
+  n = ver == 5 ? c.u64() : c.u32();
+  if (tag != 0x0B && !(tag == 0 && n == 0)) return false;
+  for (uint64_t i = 0; i < n && c.ok; i++) {
+    NcVar v;
+    v.name = c.name(ver);
+    const uint64_t nd = ver == 5 ? c.u64() : c.u32();
+    for (uint64_t k = 0; k < nd; k++) v.dims.push_back((int)(ver == 5 ? c.u64() : c.u32()));
+    if (!nc_atts(c, ver, v.atts)) return false;
+    v.type = (int)c.u32();
+    v.vsize = ver == 5 ? c.u64() : c.u32();
+    v.begin = ver == 1 ? c.u32() : c.u64();
+    for (int d : v.dims) if (d < 0 || d >= (int)f.dims.size()) return false;
+    v.record = !v.dims.empty() && v.dims[0] == f.rec_dim;
+    f.vars.push_back(std::move(v));
+  }
+  if (!c.ok) return false;
+  int nrec = 0;
+  for (const NcVar &v : f.vars) if (v.record) { f.recsize += v.vsize; nrec++; }
+  if (nrec == 1) {   // one record variable: records are not padded to 4 bytes
+    for (const NcVar &v : f.vars)
+      if (v.record) {
+        uint64_t e = nc_type_size(v.type);
+        for (size_t k = 1; k < v.dims.size(); k++) e *= f.dims[v.dims[k]].second;
+        f.recsize = e;
+      }
+  }
+  return true;
+}
+
+const NcAtt *nc_att(const std::vector<NcAtt> &atts, const char *name) {
+  for (const NcAtt &a : atts) if (a.name == name) return &a;
+  return nullptr;
+}
+
+// "NETCDF:file:var" / "NETCDF:\"file\":var" / "file" -> file, var
+void nc_split(const char *path, std::string &file, std::string &var) {
+  std::string p(path);
+  var.clear();
+  if (p.compare(0, 7, "NETCDF:") == 0) {
+    p = p.substr(7);
+    if (!p.empty() && p[0] == '"') {
+      const size_t q = p.find('"', 1);
+      file = p.substr(1, q == std::string::npos ? std::string::npos : q - 1);
+      if (q != std::string::npos && q + 2 <= p.size()) var = p.substr(q + 2);
+      return;
+    }
+    const size_t k = p.rfind(':');
+    if (k != std::string::npos) { file = p.substr(0, k); var = p.substr(k + 1); return; }
+  }
+  file = p;
+}
+
+struct NcRaster {
+  Nc f;
+  const NcVar *v = nullptr;
+  int64_t nx = 0, ny = 0, nb = 1;
+  bool bottom_up = false;
+};
+
+int nc_open_raster(const char *path, NcRaster &r) {
+  std::string file, var;
+  nc_split(path, file, var);
+  if (!read_file(file.c_str(), r.f.buf)) return 1;
+  if (!nc_parse(r.f)) return GSKYHIP_E_TYPE;
+  auto is_coord = [&](const NcVar &v) { return v.dims.size() == 1 && r.f.dims[v.dims[0]].first == v.name; };
+  const NcVar *pick = nullptr;
+  int n_data = 0;
+  for (const NcVar &v : r.f.vars) {
+    if (!var.empty()) { if (v.name == var) pick = &v; continue; }
+    if (v.dims.size() >= 2 && !is_coord(v)) { n_data++; if (!pick) pick = &v; }
+  }
+  if (!pick || (var.empty() && n_data != 1)) return 1;   // no such variable / subdatasets only
+  if (pick->dims.size() < 2 || pick->dims.size() > 3 || !nc_type_size(pick->type)) return GSKYHIP_E_TYPE;
+  r.v = pick;
+  const auto dimlen = [&](int d) { return d == r.f.rec_dim ? (int64_t)r.f.numrecs : (int64_t)r.f.dims[d].second; };
+  const size_t nd = pick->dims.size();
+  r.nx = dimlen(pick->dims[nd - 1]);
+  r.ny = dimlen(pick->dims[nd - 2]);
+  r.nb = nd == 3 ? dimlen(pick->dims[0]) : 1;
+  if (r.nx <= 0 || r.ny <= 0 || r.nb <= 0) return GSKYHIP_E_ARG;
+  // bBottomUp from the y coordinate variable (netcdfdataset.cpp:3271)
+  const std::string &ydim = r.f.dims[pick->dims[nd - 2]].first;
+  for (const NcVar &cv : r.f.vars)
+    if (cv.name == ydim && cv.dims.size() == 1 && r.ny >= 2 && !cv.record) {
+      const int ts = nc_type_size(cv.type);
+      if (cv.begin + 2 * ts <= r.f.buf.size())
+        r.bottom_up = nc_value(&r.f.buf[cv.begin], cv.type) <= nc_value(&r.f.buf[cv.begin + ts], cv.type);
+    }
+  return 0;
+}
+
+int nc_dtype(const NcVar &v, int &signed_byte) {
+  signed_byte = 0;
+  switch (v.type) {
+    case 1: {   // NC_BYTE: GDAL Byte with PIXELTYPE=SIGNEDBYTE unless _Unsigned = "true"
+      const NcAtt *u = nc_att(v.atts, "_Unsigned");
+      signed_byte = (u && (u->text == "true" || u->text == "TRUE")) ? 0 : 1;
+      return GSKYHIP_BYTE;
+    }
+    case 7: return GSKYHIP_BYTE;
+    case 3: return GSKYHIP_INT16;
+    case 8: return GSKYHIP_UINT16;
+    case 4: return GSKYHIP_INT32;
+    case 9: return GSKYHIP_UINT32;
+    case 5: return GSKYHIP_FLOAT32;
+    case 6: return GSKYHIP_FLOAT64;
+    default: return 0;
+  }
+}
+
+int nc_epsg(const Nc &f, const NcVar &v) {
+  const NcAtt *gm = nc_att(v.atts, "grid_mapping");
+  if (gm)
+    for (const NcVar &m : f.vars)
+      if (m.name == std::string(gm->text.c_str()))   // text attributes may carry a NUL
+        for (const char *k : {"crs_wkt", "spatial_ref"}) {
+          const NcAtt *w = nc_att(m.atts, k);
+          if (!w) continue;
+          const size_t a = w->text.rfind("AUTHORITY[\"EPSG\",\"");
+          if (a != std::string::npos) return std::atoi(w->text.c_str() + a + 18);
+        }
+  const size_t nd = v.dims.size();
+  const std::string &xn = f.dims[v.dims[nd - 1]].first, &yn = f.dims[v.dims[nd - 2]].first;
+  auto low = [](std::string s) { for (auto &ch : s) ch = (char)std::tolower((unsigned char)ch); return s; };
+  const std::string x = low(xn), y = low(yn);
+  if ((x == "lon" || x == "longitude" || x == "x") && (y == "lat" || y == "latitude" || y == "y") &&
+      (x != "x" || y != "y"))
+    return 4326;
+  return 0;
+}
+
+int nc_fill_info(const NcRaster &r, gskyhip_raster_info *info) {
+  std::memset(info, 0, sizeof(*info));
+  const NcVar &v = *r.v;
+  int sb = 0;
+  info->dtype = nc_dtype(v, sb);
+  if (!info->dtype) return GSKYHIP_E_TYPE;
+  info->signed_byte = sb;
+  info->xsize = (int32_t)r.nx; info->ysize = (int32_t)r.ny; info->n_bands = (int32_t)r.nb;
+  info->block_x = (int32_t)r.nx; info->block_y = 1;
+  info->compression = 1; info->predictor = 1; info->planar = 2;
+  double *g = info->geot;
+  g[0] = 0; g[1] = 1; g[2] = 0; g[3] = 0; g[4] = 0; g[5] = 1;
+  const size_t nd = v.dims.size();
+  const Nc &f = r.f;
+  auto coord = [&](const std::string &dn, int64_t n, double mm[2]) {
+    for (const NcVar &cv : f.vars)
+      if (cv.name == dn && cv.dims.size() == 1 && !cv.record) {
+        const int ts = nc_type_size(cv.type);
+        if (cv.begin + (uint64_t)n * ts > f.buf.size() || n < 2) return false;
+        const NcAtt *ar = nc_att(cv.atts, "actual_range");
+        if (ar && ar->num.size() >= 2) { mm[0] = ar->num[0]; mm[1] = ar->num[1]; }
+        else { mm[0] = nc_value(&f.buf[cv.begin], cv.type); mm[1] = nc_value(&f.buf[cv.begin + (n - 1) * ts], cv.type); }
+        const NcAtt *ao = nc_att(cv.atts, "add_offset"), *sf = nc_att(cv.atts, "scale_factor");
+        if (ao && sf && !ao->num.empty() && !sf->num.empty()) {
+          mm[0] = ao->num[0] + mm[0] * sf->num[0];
+          mm[1] = ao->num[0] + mm[1] * sf->num[0];
+        }
+        return true;
+      }
+    return false;
+  };
+  double xm[2], ym[2];
+  if (coord(f.dims[v.dims[nd - 1]].first, r.nx, xm) && coord(f.dims[v.dims[nd - 2]].first, r.ny, ym)) {
+    int node_offset = 0;
+    const NcAtt *no = nc_att(f.gatts, "node_offset");
+    if (no && !no->num.empty()) node_offset = (int)no->num[0];
+    if (ym[0] > ym[1]) std::swap(ym[0], ym[1]);   // netcdfdataset.cpp:3549-3555
+    g[0] = xm[0];
+    g[1] = (xm[1] - xm[0]) / (r.nx + (node_offset - 1));
+    g[3] = ym[1];
+    g[5] = (ym[0] - ym[1]) / (r.ny + (node_offset - 1));
+    if (!node_offset) { g[0] -= g[1] / 2; g[3] -= g[5] / 2; }
+  }
+  info->epsg = nc_epsg(f, v);
+  info->nodata = -1e10;
+  const NcAtt *fv = nc_att(v.atts, "_FillValue");
+  if (!fv) fv = nc_att(v.atts, "missing_value");
+  if (fv && !fv->num.empty()) { info->nodata = fv->num[0]; info->has_nodata = 1; }
+  return 0;
+}
+
+// Byte offset of row y (file order) of band b.
+uint64_t nc_row_offset(const NcRaster &r, int64_t b, int64_t y) {
+  const int ts = nc_type_size(r.v->type);
+  const uint64_t row = (uint64_t)r.nx * ts;
+  if (r.v->record) return r.v->begin + (uint64_t)b * r.f.recsize + (uint64_t)y * row;
+  return r.v->begin + ((uint64_t)b * r.ny + y) * row;
+}
+
+// Band rows into host `out` (big-endian file order -> host order; rows
+// south-up when the y axis increases).
+bool nc_read_rows(const NcRaster &r, int64_t b, uint8_t *out, bool swap) {
+  const int ts = nc_type_size(r.v->type);
+  const uint64_t row = (uint64_t)r.nx * ts;
+  for (int64_t y = 0; y < r.ny; y++) {
+    const uint64_t o = nc_row_offset(r, b, r.bottom_up ? r.ny - 1 - y : y);
+    if (o + row > r.f.buf.size()) return false;
+    uint8_t *d = out + (uint64_t)y * row;
+    std::memcpy(d, &r.f.buf[o], row);
+    if (swap && ts > 1)
+      for (uint64_t i = 0; i < row; i += ts) std::reverse(d + i, d + i + ts);
+  }
+  return true;
+}
+
+template <typename W>
+__global__ __launch_bounds__(256) void byteswap_kernel(W *__restrict__ v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  W x = v[i], y = 0;
+#pragma unroll
+  for (int k = 0; k < (int)sizeof(W); k++) y = (W)((y << 8) | ((x >> (8 * k)) & 0xFF));
+  v[i] = y;
+}
+
+}  // namespace
+}  // namespace gsky
+
+extern "C" int gskyhip_netcdf_info(const char *path, gskyhip_raster_info *info) {
+  if (!path || !info) return GSKYHIP_E_ARG;
+  NcRaster r;
+  const int rc = nc_open_raster(path, r);
+  return rc ? rc : nc_fill_info(r, info);
+}
+
+extern "C" int gskyhip_netcdf_read_host(const char *path, int band, void *out, int64_t out_bytes) {
+  NcRaster r;
+  int rc = nc_open_raster(path, r);
+  if (rc) return rc;
+  if (band < 1 || band > r.nb) return 2;
+  const int64_t need = r.nx * r.ny * nc_type_size(r.v->type);
+  if (!out || out_bytes < need) return GSKYHIP_E_ARG;
+  return nc_read_rows(r, band - 1, (uint8_t *)out, true) ? 0 : GSKYHIP_E_ARG;
+}
+
+extern "C" int gskyhip_netcdf_read(const char *path, int band, void *dev_out, int64_t out_bytes, void *stream) {
+  NcRaster r;
+  int rc = nc_open_raster(path, r);
+  if (rc) return rc;
+  if (band < 1 || band > r.nb) return 2;
+  const int ts = nc_type_size(r.v->type);
+  const int64_t n = r.nx * r.ny;
+  if (!dev_out || out_bytes < n * ts) return GSKYHIP_E_ARG;
+  void *host = nullptr;
+  if (hipHostMalloc(&host, (size_t)(n * ts), hipHostMallocDefault) != hipSuccess) return GSKYHIP_E_HIP;
+  if (!nc_read_rows(r, band - 1, (uint8_t *)host, false)) { hipHostFree(host); return GSKYHIP_E_ARG; }
+  hipStream_t s = (hipStream_t)stream;
+  rc = hipMemcpyAsync(dev_out, host, (size_t)(n * ts), hipMemcpyHostToDevice, s) == hipSuccess ? 0 : GSKYHIP_E_HIP;
+  if (!rc && ts > 1) {   // big-endian file order -> device order on the GPU
+    const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+    if (ts == 2) hipLaunchKernelGGL(byteswap_kernel<uint16_t>, grid, blk, 0, s, (uint16_t *)dev_out, n);
+    else if (ts == 4) hipLaunchKernelGGL(byteswap_kernel<uint32_t>, grid, blk, 0, s, (uint32_t *)dev_out, n);
+    else hipLaunchKernelGGL(byteswap_kernel<uint64_t>, grid, blk, 0, s, (uint64_t *)dev_out, n);
+    if (hipGetLastError() != hipSuccess) rc = GSKYHIP_E_HIP;
+  }
   if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GSKYHIP_E_HIP;
   hipHostFree(host);
   return rc;

@@ -1,5 +1,5 @@
-"""Native granule ingest: GeoTIFF files decoded by
-libgskyhip.so (ingest.hip) -- the GDALOpenEx / GDALRasterIO step of the
+"""Native granule ingest: GeoTIFF and netCDF classic
+files decoded by libgskyhip.so (ingest.hip) -- the GDALOpenEx / GDALRasterIO step of the
 worker (worker/gdalprocess/warp.go:89-118, drill.go:61-69, 142) -- into host
 arrays (tests) or straight into HBM tensors (the product path), plus the
 metadata GDAL reports for the file (size, type, geotransform, nodata, EPSG,
@@ -45,11 +45,17 @@ class GeoTiffInfo:
         return (self.ysize, self.xsize) if level == 0 else self.overviews[level - 1][::-1]
 
 
+def is_netcdf(path: str) -> bool:
+    """warp.go:89-101: "NETCDF:..." and "*.nc" go through the netCDF driver."""
+    return path.startswith("NETCDF:") or path.endswith(".nc")
+
+
 def info(path: str) -> GeoTiffInfo:
     r = RasterInfo()
-    rc = lib().gskyhip_geotiff_info(path.encode(), C.byref(r))
+    fn = lib().gskyhip_netcdf_info if is_netcdf(path) else lib().gskyhip_geotiff_info
+    rc = fn(path.encode(), C.byref(r))
     if rc:
-        raise GskyError(rc, "gskyhip_geotiff_info(%s)" % path)
+        raise GskyError(rc, "raster info (%s)" % path)
     return GeoTiffInfo(r.xsize, r.ysize, r.n_bands, r.dtype, bool(r.signed_byte), (r.block_x, r.block_y),
                        r.compression, r.predictor, r.planar, r.epsg, tuple(r.geot),
                        r.nodata if r.has_nodata else None,
@@ -60,7 +66,10 @@ def read_host(path: str, band: int = 1, level: int = 0) -> np.ndarray:
     """Band `band` (1-based) of `level` decoded on the host (no device work)."""
     inf = info(path)
     out = np.empty(inf.level_shape(level), inf.np_dtype())
-    rc = lib().gskyhip_geotiff_read_host(path.encode(), band, level, out.ctypes.data, out.nbytes)
+    if is_netcdf(path):
+        rc = lib().gskyhip_netcdf_read_host(path.encode(), band, out.ctypes.data, out.nbytes)
+    else:
+        rc = lib().gskyhip_geotiff_read_host(path.encode(), band, level, out.ctypes.data, out.nbytes)
     if rc:
         raise GskyError(rc, "gskyhip_geotiff_read_host(%s)" % path)
     return out
@@ -77,8 +86,12 @@ def read(path: str, band: int = 1, level: int = 0, device=None):
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     out = torch.empty(inf.level_shape(level), dtype=tdt, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    rc = lib().gskyhip_geotiff_read(path.encode(), band, level, C.c_void_p(out.data_ptr()),
-                                    out.numel() * out.element_size(), C.c_void_p(stream))
+    if is_netcdf(path):
+        rc = lib().gskyhip_netcdf_read(path.encode(), band, C.c_void_p(out.data_ptr()),
+                                       out.numel() * out.element_size(), C.c_void_p(stream))
+    else:
+        rc = lib().gskyhip_geotiff_read(path.encode(), band, level, C.c_void_p(out.data_ptr()),
+                                        out.numel() * out.element_size(), C.c_void_p(stream))
     if rc:
         raise GskyError(rc, "gskyhip_geotiff_read(%s)" % path)
     return out
@@ -87,6 +100,7 @@ def read(path: str, band: int = 1, level: int = 0, device=None):
 def register(path: str, band: int = 1) -> None:
     """Decode every level of (path, band) into library-owned HBM and register
     it for warp_operation_fast (worker.warp_raster)."""
-    rc = lib().gskyhip_register_geotiff(path.encode(), band)
+    fn = lib().gskyhip_register_netcdf if is_netcdf(path) else lib().gskyhip_register_geotiff
+    rc = fn(path.encode(), band)
     if rc:
-        raise GskyError(rc, "gskyhip_register_geotiff(%s)" % path)
+        raise GskyError(rc, "register (%s)" % path)

@@ -153,6 +153,18 @@ int gskyhip_geotiff_read(const char *path, int band, int level, void *dev_out, i
  * path, as GDALOpenEx would open it.  Returns 0, 1 (open failed), 2 (no such
  * band) or GSKYHIP_E_*. */
 int gskyhip_register_geotiff(const char *path, int band);
+/* netCDF classic (CDF-1/2/5) the way the GSKY_netCDF driver presents it
+ * (libs/gdal/frmts/gsky_netcdf/netcdfdataset.cpp): path "NETCDF:file:var"
+ * or a file holding one data variable; band = index along the leading
+ * dimension of a 3-D variable (band_query, netcdfdataset.cpp:6994-7021);
+ * geotransform from the coordinate variables (3504-3655, y increasing ->
+ * rows returned north first); nodata from _FillValue / missing_value. */
+int gskyhip_netcdf_info(const char *path, gskyhip_raster_info *info);
+int gskyhip_netcdf_read_host(const char *path, int band, void *out, int64_t out_bytes);
+int gskyhip_netcdf_read(const char *path, int band, void *dev_out, int64_t out_bytes, void *stream);
+/* Decode (path, band) into library-owned HBM and register it; what
+ * warp_operation_fast does itself for an unregistered netCDF path. */
+int gskyhip_register_netcdf(const char *path, int band);
 
 /* ---- drop-in for the cgo entry point of the worker ----------------------- */
 /* Registers an HBM-resident granule under (path, band) so that the drop-in
