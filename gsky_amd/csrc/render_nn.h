@@ -267,7 +267,11 @@ __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint3
 // block).  Rows are processed one after the other; a row's RGBA stores are
 // issued before the next row's gathers (deferring them behind those gathers
 // measured 0.6 % slower on C2 and C5, profiles/r03b_ab_nn.jsonl).
-template <typename T, bool MASK, bool CANVAS, int RPW, bool PAIR = false>
+// ONE (RGBA, no mask layer): tiles with a single stack entry -- most GetMap
+// tiles -- keep the entry's descriptor in scalar registers for all the
+// wave's rows and fetch the next row's record while the current row is
+// gathered, so no row waits for its record.
+template <typename T, bool MASK, bool CANVAS, int RPW, bool PAIR = false, bool ONE = false>
 __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
@@ -327,6 +331,72 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
     }
   };
 
+  if constexpr (ONE && !MASK && !CANVAS && !PAIR) {
+    if (n_entries == 1) {
+      const EntryD &e = ents[ord[0]];
+      const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
+      const int lim = max(0, min(ew, W - exoff));
+      const int c0 = exoff - xb, c1 = exoff + lim - xb;
+      const bool cols_ok = e.ns == ns_out && ew > 0 && c1 > 0 && c0 < ncols;
+      const bool cover = c0 <= 0 && c1 >= ncols;
+      const int bx = e.band_x, by = e.band_y;
+      const V nd = as_v<T>(e.nd);
+      const bool fill_mode = e.fill_mode != 0;
+      const int ic0 = xl - exoff;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
+      const RowRec *rbase = rows + e.row_base;
+      auto fetch = [&](int ir, double (&v)[4], int &ki) {   // kind | inside << 8, or -1 outside the window
+        if (ir < 0 || ir >= eh) { ki = -1; return; }
+        const RowRec *p = rbase + ir;
+        v[0] = p->v[0]; v[1] = p->v[1]; v[2] = p->v[2]; v[3] = p->v[3];
+        ki = __builtin_amdgcn_readfirstlane(p->kind) | (__builtin_amdgcn_readfirstlane(p->inside) << 8);
+      };
+      double cv[4] = {0, 0, 0, 0}, nv[4] = {0, 0, 0, 0};
+      int cki = -1, nki = -1;
+      if (cols_ok) fetch(r0 - eyoff, cv, cki);
+#pragma unroll 1
+      for (int j = 0; j < RPW; j++) {
+        const int r = r0 + j;
+        if (r >= H) break;
+        if (cols_ok && j + 1 < RPW) fetch(r + 1 - eyoff, nv, nki);   // next row's record, in flight now
+        V c[kNnPx];
+#pragma unroll
+        for (int q = 0; q < kNnPx; q++) c[q] = cnod;
+        if (cki >= 0) {
+          if ((cki & 0xFF) == ROW_LINEAR && (cki >> 8) && cover) {
+            uint32_t off[kNnPx];
+#pragma unroll
+            for (int q = 0; q < kNnPx; q++) {
+              const double dist = (double)(ic0 + 64 * q);
+              const int ix = __double2int_rz(cv[0] + cv[2] * dist + 1.0e-10);
+              const int iy = __double2int_rz(cv[1] + cv[3] * dist + 1.0e-10);
+              off[q] = (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T);
+            }
+            V vv[kNnPx];
+#pragma unroll
+            for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
+            if (!fill_mode) {
+#pragma unroll
+              for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
+            } else {
+#pragma unroll
+              for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
+            }
+          } else {
+            nn_entry_row<T, false>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+          }
+        }
+        uint32_t px[kNnPx];
+        nn_rgba<T>(sk, safe, s_tab, c, px);
+        store_row(r, px);
+#pragma unroll
+        for (int k = 0; k < 4; k++) cv[k] = nv[k];
+        cki = nki;
+      }
+      return;
+    }
+  }
 #pragma unroll 1
   for (int j = 0; j < RPW; j += PAIR ? 2 : 1) {
     const int r = r0 + j;
@@ -498,10 +568,10 @@ __global__ __launch_bounds__(64 * (NP + 1)) void render_nn_ws_kernel(RenderArgs 
 constexpr int kNnRpw8MinItems = 32768;
 constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
 
-template <typename T, bool M, bool C, int RPW, bool PAIR = false>
+template <typename T, bool M, bool C, int RPW, bool PAIR = false, bool ONE = false>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, PAIR>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, PAIR, ONE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -523,6 +593,10 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   if (const char *x = getenv("GSKYHIP_NN_XCD")) xcd = atoi(x);
 #endif
 #ifdef GSKYHIP_AB
+  if (const char *on = getenv("GSKYHIP_NN_ONE")) {
+    if (!mask && !canvas && atoi(on) == 8) { launch_nn_v<T, false, false, 8, false, true>(a, s); return; }
+    if (!mask && !canvas && atoi(on) == 4) { launch_nn_v<T, false, false, 4, false, true>(a, s); return; }
+  }
   if (const char *pr = getenv("GSKYHIP_NN_PAIR")) {
     if (!mask && !canvas && atoi(pr) == 8) { launch_nn_v<T, false, false, 8, true>(a, s); return; }
     if (!mask && !canvas && atoi(pr) == 4) { launch_nn_v<T, false, false, 4, true>(a, s); return; }

@@ -18,10 +18,11 @@ for ws in 0 3 7 0; do
   stop $? "ab_c3_ws$ws"
 done
 cat gpurun_out/ab_c3.jsonl
-for pr in 0 8 4 0 8; do
-  GSKYHIP_LIB=ab GSKYHIP_NN_PAIR=$pr timeout -k 10 300 python -u tools/ab_render.py --config c2 --reps 30 --oracle \
-    --label "pair$pr" >> gpurun_out/ab_pair.jsonl 2>> gpurun_out/ab.err
-  stop $? "ab_pair$pr"
+for v in "PAIR 0" "PAIR 8" "PAIR 4" "ONE 8" "ONE 4" "PAIR 0" "PAIR 8" "ONE 8"; do
+  set -- $v
+  env GSKYHIP_LIB=ab GSKYHIP_NN_$1=$2 timeout -k 10 300 python -u tools/ab_render.py --config c2 --reps 30 \
+    --oracle --label "$1 $2" >> gpurun_out/ab_pair.jsonl 2>> gpurun_out/ab.err
+  stop $? "ab_$1_$2"
 done
 cat gpurun_out/ab_pair.jsonl
 timeout -s KILL 60 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/calib_f -o run --output-format csv -- \
