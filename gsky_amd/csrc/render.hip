@@ -164,6 +164,7 @@ __device__ int must_adjust2(const Xform &t, const double *er, double psxr, doubl
 constexpr int kSteps = 20;
 constexpr int kSmallBatchPairs = 512;   // plan_pairs_kernel<256> up to this many pairs
 constexpr int kSmallBatchTiles = 8, kSmallBatchPlanPairs = 32;   // plan_small_kernel batches
+constexpr int kFusedPlanPairs = 2;   // ... that plan their pairs in the same launch
 constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 
 // First half of xform_point_nl(t, false, ...): source pixel -> destination
@@ -498,16 +499,11 @@ __device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, do
   return err;
 }
 
-// One workgroup of NT threads per pair: NT = 64 (one wavefront) for batches
-// that fill the GPU, NT = 256 for small, latency-bound batches.
+// Plan of pair p by one workgroup of NT threads (sx / sy / sok: LDS scratch
+// of kGrid entries, ts: the transformer in LDS).
 template <int NT>
-__global__ __launch_bounds__(NT) void plan_pairs_kernel(PlanArgs a) {
-  const int p = blockIdx.x;
+__device__ void plan_pair(const PlanArgs &a, int p, double *sx, double *sy, int *sok, Xform &ts) {
   const int lane = threadIdx.x;
-  if (p >= a.n_pairs) return;
-  __shared__ double sx[kGrid], sy[kGrid];
-  __shared__ int sok[kGrid];
-
   const int t_idx = a.small ? owning_tile(a.tiles, a.n_tiles, p) : a.pair_tile[p];
   if (t_idx < 0) {   // unreferenced pair: an empty plan nothing reads
     if (lane == 0) {
@@ -527,7 +523,6 @@ __global__ __launch_bounds__(NT) void plan_pairs_kernel(PlanArgs a) {
   // ---- transformer (warp.go:120-148), kept in LDS: the wave-uniform state
   // would otherwise live in scratch (xform_point selects its geotransforms
   // through pointers) or cost ~130 VGPRs
-  __shared__ Xform ts;
   Xform &t = ts;
   if (lane == 0) {
     t.src = a.crs[g.crs];
@@ -630,6 +625,17 @@ __global__ __launch_bounds__(NT) void plan_pairs_kernel(PlanArgs a) {
   pp.fill = gdal_copy_to(g.nodata, odt);
   pp.ts = g.timestamp;
   pp.stamp = g.timestamp + (double)g.polygon_hash;
+}
+
+// One workgroup of NT threads per pair: NT = 64 (one wavefront) for batches
+// that fill the GPU, NT = 256 for small, latency-bound batches.
+template <int NT>
+__global__ __launch_bounds__(NT) void plan_pairs_kernel(PlanArgs a) {
+  if ((int)blockIdx.x >= a.n_pairs) return;
+  __shared__ double sx[kGrid], sy[kGrid];
+  __shared__ int sok[kGrid];
+  __shared__ Xform ts;
+  plan_pair<NT>(a, blockIdx.x, sx, sy, sok, ts);
 }
 
 // ---------------------------------------------------------------- extent op
@@ -1219,6 +1225,15 @@ __global__ __launch_bounds__(256) void plan_exact_kernel(PlanArgs a) {
 __global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
   __shared__ TileLds L[4];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (a.small == 2) {   // the pairs too (one or two): the whole plan is this one launch
+    __shared__ double sx[kGrid], sy[kGrid];
+    __shared__ int sok[kGrid];
+    __shared__ Xform ts;
+    for (int p = 0; p < a.n_pairs; p++) {
+      plan_pair<256>(a, p, sx, sy, sok, ts);
+      __syncthreads();
+    }
+  }
   if (tid < 64) a.counters[tid] = 0;
   __syncthreads();
   for (int t = wave; t < a.n_tiles; t += 4) plan_tile_wave(a, t, lane, L[wave]);
@@ -1505,9 +1520,9 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
 #ifdef GSKYHIP_AB
   if (const char *sm = getenv("GSKYHIP_PLAN_SMALL")) small = small && atoi(sm) != 0;
 #endif
-  a.small = small ? 1 : 0;
+  a.small = small ? (rc.n_pairs <= kFusedPlanPairs ? 2 : 1) : 0;
   if (small) {
-    hipLaunchKernelGGL(plan_pairs_kernel<256>, dim3(rc.n_pairs), dim3(256), 0, s, a);
+    if (a.small == 1) hipLaunchKernelGGL(plan_pairs_kernel<256>, dim3(rc.n_pairs), dim3(256), 0, s, a);
     hipLaunchKernelGGL(plan_small_kernel, dim3(1), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
   }
