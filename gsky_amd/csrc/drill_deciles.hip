@@ -59,7 +59,7 @@ __device__ __forceinline__ float fdecode(uint32_t k) {
 }
 
 constexpr int kDecChunk = 64;        // pixels per transpose item
-constexpr int kSelLds = 60 * 1024;   // dynamic LDS of a select workgroup: histograms + key cache
+constexpr int kSelLds = 48 * 1024;   // dynamic LDS of a select workgroup (histograms + key cache): 3 per CU
 
 // Exclusive scan of 64-pixel chunks per polygon (one block; n_polys is modest).
 __global__ __launch_bounds__(1024) void decile_chunk_scan_kernel(const int32_t *__restrict__ count, int n_polys,
@@ -184,18 +184,27 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   const bool fits = n <= cache_keys;
   uint32_t ka = 0xFFFFFFFFu, ko = 0u;
   int valid = 0;
-  for (int i0 = 0; i0 < n; i0 += kSelThreads) {
-    const int i = i0 + tid;
-    const float v = i < n ? buf[i] : nodata;
-    const bool keep = i < n && v != nodata;
-    const uint32_t k = fkey(v);
-    if (keep) { ka &= k; ko |= k; valid++; }
-    if (fits) {
-      const unsigned long long bal = __ballot(keep);
-      int wbase = 0;
-      if ((tid & 63) == 0 && bal) wbase = atomicAdd(&s_nc, __popcll(bal));
-      wbase = __shfl(wbase, 0);
-      if (keep) cache[wbase + __popcll(bal & ((1ull << (tid & 63)) - 1ull))] = k;
+  constexpr int kU = 8;   // values per thread in flight per round
+  for (int i0 = 0; i0 < n; i0 += kSelThreads * kU) {
+    float v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int i = i0 + u * kSelThreads + tid;
+      v[u] = i < n ? buf[i] : nodata;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int i = i0 + u * kSelThreads + tid;
+      const bool keep = i < n && v[u] != nodata;
+      const uint32_t k = fkey(v[u]);
+      if (keep) { ka &= k; ko |= k; valid++; }
+      if (fits) {
+        const unsigned long long bal = __ballot(keep);
+        int wbase = 0;
+        if ((tid & 63) == 0 && bal) wbase = atomicAdd(&s_nc, __popcll(bal));
+        wbase = __shfl(wbase, 0);
+        if (keep) cache[wbase + __popcll(bal & ((1ull << (tid & 63)) - 1ull))] = k;
+      }
     }
   }
   for (int sh = 32; sh > 0; sh >>= 1) {
@@ -289,10 +298,17 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     };
     if (fits) {
       for (int i = tid; i < len; i += kSelThreads) bin(key_at(i));
-    } else {
-      for (int i = tid; i < n; i += kSelThreads) {
-        const float v = buf[i];
-        if (v != nodata) bin(fkey(v));
+    } else {   // streamed again from the segment, kU values per thread in flight
+      for (int i0 = 0; i0 < n; i0 += kSelThreads * kU) {
+        float v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          const int i = i0 + u * kSelThreads + tid;
+          v[u] = i < n ? buf[i] : nodata;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++)
+          if (i0 + u * kSelThreads + tid < n && v[u] != nodata) bin(fkey(v[u]));
       }
     }
     __syncthreads();

@@ -467,8 +467,10 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     auto it = d.reg.find({q.path, q.band});
     if (it == d.reg.end() && (netcdf || is_geotiff_path(q.path))) {   // GDALOpenEx of a file nobody registered
       const int irc = netcdf ? ingest_netcdf_locked(d, q.path, q.band) : ingest_geotiff_locked(d, q.path, q.band);
-      if (irc == 1 || irc == 2) { r.rc = irc; continue; }
-      it = d.reg.find({q.path, q.band});
+      if (irc == 2) { r.rc = 2; continue; }
+      if (irc == 0) it = d.reg.find({q.path, q.band});
+      // else (no such file): the registry rule below -- a path registered
+      // with other bands is an open dataset without this band (2), else 1
     }
     if (it == d.reg.end()) {
       bool path_known = false;

@@ -30,111 +30,6 @@ namespace gsky {
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-// The bilinear fold of tile row r over the tile's entries (GWKBilinearResample4Sample
-// per entry, MergeMaskedRaster order); c[] arrives holding the canvas nodata.
-template <typename WT, int HP>
-__device__ __forceinline__ void bil_fold_row(const EntryD *__restrict__ ents, const int32_t *__restrict__ ord,
-                                             int n_entries, const RowRec *__restrict__ rows,
-                                             const Leaf *__restrict__ pool, int ns_out, int r, int xb, int xl,
-                                             int W, int ncols, float (&c)[kNnPx]) {
-#pragma unroll 1
-  for (int k = 0; k < n_entries; k++) {
-    const EntryD &e = ents[ord[k]];
-    const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
-    if (e.ns != ns_out || ew <= 0) continue;
-    const int ir = r - eyoff;
-    if (ir < 0 || ir >= eh) continue;
-    const int lim = max(0, min(ew, W - exoff));
-    const int c0 = exoff - xb, c1 = exoff + lim - xb;
-    if (c1 <= 0 || c0 >= ncols) continue;
-    const RowRec *rr = rows + e.row_base + ir;
-    const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
-    const int bx = e.band_x, by = e.band_y;
-    const float nd = e.nd.f, fillv = e.fill.f;
-    const bool fill_mode = e.fill_mode != 0;
-    const bool hnd = e.has_nodata != 0;
-    const double nd64 = e.nodata64;
-    const bool nd_nan = nd64 != nd64;
-    const int ic0 = xl - exoff;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * 4), 0x00020000);
-    // one pixel: tap addresses + fractions (prep), then the sample and the fold (finish)
-    auto prep = [&](int q, double sx, double sy, bool ok, WT &rx, WT &ry, uint32_t &valid, u32x2 &t0, u32x2 &t1) {
-      const double fx = floor(sx - 0.5), fy = floor(sy - 0.5);
-      const int iSrcX = (int)fx, iSrcY = (int)fy;
-      double drx = 1.5 - (sx - (double)iSrcX), dry = 1.5 - (sy - (double)iSrcY);
-      const int lx = iSrcX == -1 ? 0 : iSrcX, ly = iSrcY == -1 ? 0 : iSrcY;
-      drx = iSrcX == -1 ? 1.0 : drx;
-      dry = iSrcY == -1 ? 1.0 : dry;
-      rx = (WT)drx;
-      ry = (WT)dry;
-      const uint32_t x0in = (unsigned)lx < (unsigned)bx, x1in = (unsigned)(lx + 1) < (unsigned)bx;
-      const uint32_t y0in = (unsigned)ly < (unsigned)by, y1in = (unsigned)(ly + 1) < (unsigned)by;
-      // bit k: tap k (x + (k & 1), y + (k >> 1)) inside the band; bit 4: a sample is taken
-      valid = ok ? ((x0in & y0in) | ((x1in & y0in) << 1) | ((x0in & y1in) << 2) | ((x1in & y1in) << 3) | 16u) : 0u;
-      // no sample: an offset past the band (< 2 GiB) reads 0 without a fetch
-      const uint32_t o0 = ok ? (uint32_t)(ly * bx + lx) * 4u : 0x80000000u;
-      const uint32_t o1 = ok ? o0 + (uint32_t)bx * 4u : 0x80000000u;
-      t0 = __builtin_amdgcn_raw_buffer_load_b64(rs, o0, 0, 0);
-      t1 = __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, 0);
-    };
-    auto finish = [&](int q, WT rx, WT ry, uint32_t valid, u32x2 t0, u32x2 t1) {
-      const float tv[4] = {__uint_as_float(t0.x), __uint_as_float(t0.y), __uint_as_float(t1.x),
-                           __uint_as_float(t1.y)};
-      const WT one = (WT)1.0;
-      const WT wx[2] = {rx, one - rx}, wy[2] = {ry, one - ry};
-      WT accR = (WT)0.0, accDiv = (WT)0.0;
-#pragma unroll
-      for (int kk = 0; kk < 4; kk++) {
-        const WT w = wx[kk & 1] * wy[kk >> 1];
-        const double d = (double)tv[kk];
-        const bool use = ((valid >> kk) & 1u) && !(hnd && (d == nd64 || (nd_nan && d != d)));
-        accDiv += use ? w : (WT)0.0;
-        accR += use ? (WT)d * w : (WT)0.0;
-      }
-      float v = fillv;
-      if (valid & 16u) {
-        if (accDiv == (WT)1.0) v = (float)accR;
-        else if (accDiv >= (WT)0.00001) v = (float)(accR / accDiv);
-      }
-      const int ic = ic0 + 64 * q;
-      const bool take = ((unsigned)ic < (unsigned)lim) & (v != nd) & (!fill_mode | (c[q] == nd));
-      c[q] = take ? v : c[q];
-    };
-    if (kind == ROW_LINEAR) {   // HP pixels' taps in flight
-      const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
-#pragma unroll
-      for (int h = 0; h < kNnPx; h += HP) {
-        WT rx[HP], ry[HP];
-        uint32_t valid[HP];
-        u32x2 t0[HP], t1[HP];
-#pragma unroll
-        for (int q = 0; q < HP; q++) {
-          const int ic = ic0 + 64 * (h + q);
-          const double dist = (double)ic;
-          prep(h + q, xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, rx[q], ry[q], valid[q],
-               t0[q], t1[q]);
-        }
-#pragma unroll
-        for (int q = 0; q < HP; q++) finish(h + q, rx[q], ry[q], valid[q], t0[q], t1[q]);
-      }
-    } else {   // POOL: linear leaves, per-pixel exact points, failed pixels; one pixel at a time
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) {
-        const int ic = ic0 + 64 * q;
-        bool ok = (unsigned)ic < (unsigned)lim;
-        double sx = 0.0, sy = 0.0;
-        ok = ok && lin_coords(*rr, pool, ok ? ic : 0, sx, sy);
-        WT rx, ry;
-        uint32_t valid;
-        u32x2 t0, t1;
-        prep(q, sx, sy, ok, rx, ry, valid, t0, t1);
-        finish(q, rx, ry, valid, t0, t1);
-      }
-    }
-  }
-}
-
 // HP: pixels whose taps are in flight together; WPS: waves per SIMD the
 // register budget is sized for.
 template <typename WT, int RPW, int HP, int WPS>
@@ -290,74 +185,6 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
   }
 }
 
-// Producer / store-wave form of render_bil_kernel (the rationale of
-// render_nn_ws_kernel, render_nn.h): NP waves fold a row each per step into
-// LDS (bil_fold_row), wave NP copies the previous step's rows to the float
-// canvas with 16-B non-temporal stores.
-template <int NP, int STEPS>
-__global__ __launch_bounds__(64 * (NP + 1)) void render_bil_ws_kernel(RenderArgs a, const EntryD *__restrict__ ents,
-                                                                      const int32_t *__restrict__ order,
-                                                                      const RowRec *__restrict__ rows,
-                                                                      const Leaf *__restrict__ pool,
-                                                                      const TilePlan *__restrict__ tplans,
-                                                                      const gskyhip_tile *__restrict__ tiles,
-                                                                      int n_items) {
-  constexpr int kRowsBlk = NP * STEPS;
-  __shared__ __attribute__((aligned(16))) uint32_t s_out[2][NP][kBandCols];
-  const int item = blockIdx.x;
-  if (item >= n_items) return;
-  const int bands_per_tile = (a.max_h + kRowsBlk - 1) / kRowsBlk;
-  const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
-  const int t = item / (bands_per_tile * col_blocks);
-  const int in_tile = item - t * bands_per_tile * col_blocks;
-  const TilePlan &tp = tplans[t];
-  if (tp.complex || (tp.n_entries > 0 && tp.vt != GSKYHIP_FLOAT32)) return;   // empty tiles: written here
-  const gskyhip_tile &tile = tiles[t];
-  const int W = tile.width, H = tile.height;
-  const int band0 = (in_tile / col_blocks) * kRowsBlk;
-  const int xb = (in_tile % col_blocks) * kBandCols;
-  if (band0 >= H || xb >= W) return;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int ncols = min(kBandCols, W - xb);
-  const int nsteps = min(STEPS, (H - band0 + NP - 1) / NP);
-  const int ns_out = a.out_ns[0];
-  if (wave < NP) {
-    const float cnod = go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]).f;
-    const int32_t *ord = order + tile.pair_begin;
-    const int n_entries = tp.n_entries;
-    const int xl = xb + lane;
-#pragma unroll 1
-    for (int p = 0; p < nsteps; p++) {
-      const int r = band0 + p * NP + wave;
-      if (r < H) {
-        float c[kNnPx];
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-        bil_fold_row<float, 4>(ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
-        uint32_t *o = &s_out[p & 1][wave][lane];
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) o[64 * q] = __float_as_uint(c[q]);
-      }
-      lds_barrier();
-    }
-  } else {
-    // typed float canvas (tile_merger.go:562-652), at the chunk's place in the coverage
-    const int64_t e0 = a.cov_offsets ? a.cov_offsets[t] + xb : (int64_t)t * (a.canvas_tile_stride / 4) + xb;
-    const int64_t stride = a.cov_offsets ? a.cov_stride : a.max_w;
-    uint32_t *base = (uint32_t *)a.canvas + e0;
-    const bool vec4 = ((e0 | stride) & 3) == 0;
-#pragma unroll 1
-    for (int p = 0; p <= nsteps; p++) {
-      if (p > 0) {
-        const int r = band0 + (p - 1) * NP;
-        ws_store_rows<NP>(s_out[(p - 1) & 1], min(NP, H - r), base + (int64_t)r * stride, stride, vec4, ncols,
-                          lane);
-      }
-      if (p < nsteps) lds_barrier();
-    }
-  }
-}
-
 // Bilinear float canvases (no mask layer): fp32 weights, 4 rows per wave,
 // 4 pixels' taps in flight at 8 waves per SIMD; the A/B build also has the
 // fp64 weights (GSKYHIP_BIL_F32=0: 6 waves per SIMD, or 8 with 2 pixels in
@@ -372,22 +199,6 @@ void launch_bil_v(const RenderArgs &a, hipStream_t s) {
 void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   (void)n_items;
 #ifdef GSKYHIP_AB
-  if (const char *w = getenv("GSKYHIP_BIL_WS")) {
-    const int ws = atoi(w);
-    const int cb = (a.max_w + kBandCols - 1) / kBandCols;
-    if (ws == 3) {
-      const int items = a.n_tiles * ((a.max_h + 23) / 24) * cb;
-      hipLaunchKernelGGL((render_bil_ws_kernel<3, 8>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries, a.order,
-                         a.rows, a.pool, a.tplans, a.tiles, items);
-      return;
-    }
-    if (ws == 7) {
-      const int items = a.n_tiles * ((a.max_h + 55) / 56) * cb;
-      hipLaunchKernelGGL((render_bil_ws_kernel<7, 8>), dim3((unsigned)items), dim3(512), 0, s, a, a.entries, a.order,
-                         a.rows, a.pool, a.tplans, a.tiles, items);
-      return;
-    }
-  }
   const char *f = getenv("GSKYHIP_BIL_F32");
   const char *rp = getenv("GSKYHIP_BIL_RPW");
   const char *hp = getenv("GSKYHIP_BIL_HP");

@@ -70,10 +70,27 @@ __device__ __forceinline__ uint32_t scale_int(const ScaleK &k, int32_t c) {
   return c == k.noData.i ? 0xFFu : b;
 }
 
+// Canvas value domain.  RAW = false: the value as an int (sign-extended for
+// signed T) or float -- what Scale reads.  RAW = true (integer T with the
+// scale+palette LUT): the sample's raw bits, zero-extended -- a load needs
+// no sign extension and the value indexes the LUT directly.  Equality, the
+// only operation the fold applies, means the same in both domains.
+template <typename T, bool RAW>
+__device__ __forceinline__ typename VOf<T>::type dom(typename VOf<T>::type v) {
+  if constexpr (RAW && sizeof(T) < 4) return (typename VOf<T>::type)((uint32_t)v & ((1u << (8 * sizeof(T))) - 1u));
+  else return v;
+}
+template <typename T, bool RAW>
+__device__ __forceinline__ typename VOf<T>::type nn_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (RAW && sizeof(T) == 2) return (typename VOf<T>::type)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+  else if constexpr (RAW && sizeof(T) == 1) return (typename VOf<T>::type)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+  else return buf_load<T>(r, off);
+}
+
 // One stack entry e of the ordered fold of tile row r (MergeMaskedRaster,
 // tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
 // (tile column xl + 64 q).
-template <typename T, bool MASK>
+template <typename T, bool MASK, bool RAW = false>
 __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
                                              const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
                                              int ns_out, int r, int xb, int xl, int W, int ncols,
@@ -90,7 +107,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
   const int inside = __builtin_amdgcn_readfirstlane(rr->inside);
   const int bx = e.band_x, by = e.band_y;
-  const V nd = as_v<T>(e.nd);
+  const V nd = dom<T, RAW>(as_v<T>(e.nd));
   const bool fill_mode = e.fill_mode != 0;
   const int ic0 = xl - exoff;   // window column of the lane's pixel 0
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -110,7 +127,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
     }
     V vv[kNnPx];
 #pragma unroll
-    for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
+    for (int q = 0; q < kNnPx; q++) vv[q] = nn_load<T, RAW>(rs, off[q]);
     if (!fill_mode) {
 #pragma unroll
       for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
@@ -123,7 +140,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   // general body: window edges, POOL rows, failed transforms, mask layer;
   // two halves of 4 pixels (4 gathers in flight) keep the register peak
   // of the fast body
-  const V fillv = as_v<T>(e.fill);
+  const V fillv = dom<T, RAW>(as_v<T>(e.fill));
 #pragma unroll
   for (int h = 0; h < kNnPx; h += 4) {
     uint32_t idx[4];
@@ -149,7 +166,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
     }
     V vv[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
+    for (int q = 0; q < 4; q++) vv[q] = nn_load<T, RAW>(rs, idx[q] * (uint32_t)sizeof(T));
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int ic = ic0 + 64 * (h + q);
@@ -166,7 +183,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
 
 // The ordered fold of tile row r over the tile's entries in ProcessRasterStack
 // order; c[] arrives holding the canvas nodata.
-template <typename T, bool MASK>
+template <typename T, bool MASK, bool RAW = false>
 __device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *__restrict__ ents,
                                             const int32_t *__restrict__ ord, int n_entries,
                                             const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
@@ -174,74 +191,7 @@ __device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *_
                                             typename VOf<T>::type (&c)[kNnPx]) {
 #pragma unroll 1
   for (int k = 0; k < n_entries; k++)
-    nn_entry_row<T, MASK>(a, ents, ents[ord[k]], rows, pool, ns_out, r, xb, xl, W, ncols, c);
-}
-
-// Rows r and r + 1 together: where an entry takes the fast body on both
-// rows, their 16 gathers are issued before the first wait (twice the loads
-// in flight per wave); otherwise each row takes nn_entry_row.  The same
-// expressions and fold order per row as nn_fold_row.
-template <typename T>
-__device__ __forceinline__ void nn_fold_row2(const RenderArgs &a, const EntryD *__restrict__ ents,
-                                             const int32_t *__restrict__ ord, int n_entries,
-                                             const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
-                                             int ns_out, int r, int xb, int xl, int W, int ncols,
-                                             typename VOf<T>::type (&ca)[kNnPx], typename VOf<T>::type (&cb)[kNnPx]) {
-  using V = typename VOf<T>::type;
-#pragma unroll 1
-  for (int k = 0; k < n_entries; k++) {
-    const EntryD &e = ents[ord[k]];
-    const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
-    const int ir = r - eyoff;
-    const int lim = max(0, min(ew, W - exoff));
-    const int c0 = exoff - xb, c1 = exoff + lim - xb;
-    bool pair_fast = e.ns == ns_out && ew > 0 && ir >= 0 && ir + 1 < eh && c0 <= 0 && c1 >= ncols;
-    const RowRec *rr = rows + e.row_base + ir;
-    if (pair_fast) {
-      const int ka = __builtin_amdgcn_readfirstlane(rr[0].kind), ia = __builtin_amdgcn_readfirstlane(rr[0].inside);
-      const int kb = __builtin_amdgcn_readfirstlane(rr[1].kind), ib = __builtin_amdgcn_readfirstlane(rr[1].inside);
-      pair_fast = ka == ROW_LINEAR && kb == ROW_LINEAR && ia && ib;
-    }
-    if (!pair_fast) {
-      nn_entry_row<T, false>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, ca);
-      nn_entry_row<T, false>(a, ents, e, rows, pool, ns_out, r + 1, xb, xl, W, ncols, cb);
-      continue;
-    }
-    const int bx = e.band_x, by = e.band_y;
-    const V nd = as_v<T>(e.nd);
-    const bool fill_mode = e.fill_mode != 0;
-    const int ic0 = xl - exoff;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
-    V va[kNnPx], vb[kNnPx];
-    {
-      const double xs0 = rr[0].v[0], ys0 = rr[0].v[1], dX = rr[0].v[2], dY = rr[0].v[3];
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) {
-        const double dist = (double)(ic0 + 64 * q);
-        const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
-        const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
-        va[q] = buf_load<T>(rs, (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T));
-      }
-    }
-    {
-      const double xs0 = rr[1].v[0], ys0 = rr[1].v[1], dX = rr[1].v[2], dY = rr[1].v[3];
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) {
-        const double dist = (double)(ic0 + 64 * q);
-        const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
-        const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
-        vb[q] = buf_load<T>(rs, (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T));
-      }
-    }
-    if (!fill_mode) {
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) { ca[q] = (va[q] != nd) ? va[q] : ca[q]; cb[q] = (vb[q] != nd) ? vb[q] : cb[q]; }
-    } else {
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) { ca[q] = (ca[q] == nd) ? va[q] : ca[q]; cb[q] = (cb[q] == nd) ? vb[q] : cb[q]; }
-    }
-  }
+    nn_entry_row<T, MASK, RAW>(a, ents, ents[ord[k]], rows, pool, ns_out, r, xb, xl, W, ncols, c);
 }
 
 // utils.Scale + palette / grey of the lane's 8 canvas values (EncodePNG's
@@ -263,16 +213,44 @@ __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint3
   }
 }
 
+// Scale + palette as one table (integer T, RGBA): entry u = the RGBA of the
+// raw sample u -- utils.Scale of a non-nodata value (raster_scaler.go:30-332:
+// offset wrapping in T, clip, float32 multiply, Go uint8) looked up in the
+// palette / grey ramp with EncodePNG's transparency for 0xFF
+// (ogc_encoders.go:94-133).  The same expressions as scale_int() + s_tab, so
+// the same bytes; one table per launch (it depends on T and the scale
+// parameters only), built by nn_lut_kernel.  A pixel is then one compare with
+// the canvas nodata and one 4-byte load instead of ~10 VALU + an LDS read.
+template <typename T>
+__global__ __launch_bounds__(256) void nn_lut_kernel(RenderArgs a, uint32_t *__restrict__ lut) {
+  constexpr uint32_t n = 1u << (8 * sizeof(T));
+  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= n) return;
+  const ScaleK sk = make_scale(vt_code<T>(), 0.0, a.sp, false, 0.f, 0.f);
+  const int32_t c = std::is_signed<T>::value ? (sizeof(T) == 1 ? (int32_t)(int8_t)u : (int32_t)(int16_t)u) : (int32_t)u;
+  int32_t value = c + sk.off.i;
+  if constexpr (std::is_same<T, int8_t>::value) value = (int8_t)value;
+  else if constexpr (std::is_same<T, uint8_t>::value) value = (uint8_t)value;
+  else if constexpr (std::is_same<T, int16_t>::value) value = (int16_t)value;
+  else value = (uint16_t)value;
+  value = max(min(value, sk.clp.i), 0);
+  const uint32_t b = go_u8_f32((float)value * sk.sc);
+  const uint32_t col = a.ramp ? a.ramp[b] : (0xFF000000u | (b * 0x10101u));
+  lut[u] = b == 255 ? 0u : col;
+}
+
 // RPW: rows per wave (a block of 4 waves covers 4 * RPW rows of a 512-column
 // block).  Rows are processed one after the other; a row's RGBA stores are
 // issued before the next row's gathers (deferring them behind those gathers
 // measured 0.6 % slower on C2 and C5, profiles/r03b_ab_nn.jsonl).
+// LUT (integer T, RGBA): canvas values in the RAW domain, Scale + palette
+// through a.lut (nn_lut_kernel).
 // ONE (RGBA, no mask layer): tiles with a single stack entry -- most GetMap
 // tiles -- keep the entry's descriptor in scalar registers for all the
 // wave's rows and fetch the next row's record while the current row is
 // gathered, so no row waits for its record.
-template <typename T, bool MASK, bool CANVAS, int RPW, bool PAIR = false, bool ONE = false>
-__global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
+template <typename T, bool MASK, bool CANVAS, int RPW, bool LUT = false, bool ONE = false>
+__global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
                                                                       const Leaf *__restrict__ pool,
@@ -299,7 +277,8 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
   const int tid = threadIdx.x;
   const int ns_out = a.out_ns[0];
   const bool created = tp.created[ns_out] != 0;
-  if constexpr (!CANVAS) {   // EncodePNG: utils.Scale 0xFF and canvases never created are transparent
+  constexpr bool RAW = LUT && !std::is_same<T, float>::value && !CANVAS;
+  if constexpr (!CANVAS && !RAW) {   // EncodePNG: utils.Scale 0xFF and canvases never created are transparent
     const uint32_t col = a.ramp ? a.ramp[tid] : (0xFF000000u | ((uint32_t)tid * 0x10101u));
     s_tab[tid] = (created && tid != 255) ? col : 0u;
     __syncthreads();
@@ -308,7 +287,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
   const int r0 = band0 + wave * RPW;
   if (r0 >= H) return;
 
-  const V cnod = as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]));
+  const V cnod = dom<T, RAW>(as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out])));
   const int32_t *ord = order + tile.pair_begin;
   const int n_entries = tp.n_entries;
   const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
@@ -317,6 +296,25 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
   const bool full = ncols == kBandCols;
   const int xl = xb + lane;                     // tile column of the lane's pixel 0
   uint32_t *rgba_lane = (uint32_t *)(a.rgba + (((int64_t)t * a.max_h) * a.max_w + xl) * 4);
+
+  // utils.Scale + palette of the row's 8 values: the LUT (RAW domain; the
+  // canvas nodata is transparent) or scale_int + the LDS table
+  const __amdgpu_buffer_rsrc_t lut_rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.lut, (short)0, kLutEntries * 4, 0x00020000);
+  auto rgba = [&](const V (&c)[kNnPx], uint32_t (&px)[kNnPx]) {
+    if constexpr (RAW) {
+      const V nod = dom<T, RAW>(sk.noData.i);
+      uint32_t v[kNnPx];
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) v[q] = __builtin_amdgcn_raw_buffer_load_b32(lut_rs, (uint32_t)c[q] * 4u, 0, 0);
+      // a canvas never created keeps the canvas nodata everywhere, so the
+      // nodata compare also makes it transparent
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) px[q] = c[q] != nod ? v[q] : 0u;
+    } else {
+      nn_rgba<T>(sk, safe, s_tab, c, px);
+    }
+  };
 
   // RGBA stores of row r
   auto store_row = [&](int r, const uint32_t *px) {
@@ -331,7 +329,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
     }
   };
 
-  if constexpr (ONE && !MASK && !CANVAS && !PAIR) {
+  if constexpr (ONE && !MASK && !CANVAS) {
     if (n_entries == 1) {
       const EntryD &e = ents[ord[0]];
       const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
@@ -340,7 +338,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
       const bool cols_ok = e.ns == ns_out && ew > 0 && c1 > 0 && c0 < ncols;
       const bool cover = c0 <= 0 && c1 >= ncols;
       const int bx = e.band_x, by = e.band_y;
-      const V nd = as_v<T>(e.nd);
+      const V nd = dom<T, RAW>(as_v<T>(e.nd));
       const bool fill_mode = e.fill_mode != 0;
       const int ic0 = xl - exoff;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -375,7 +373,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
             }
             V vv[kNnPx];
 #pragma unroll
-            for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
+            for (int q = 0; q < kNnPx; q++) vv[q] = nn_load<T, RAW>(rs, off[q]);
             if (!fill_mode) {
 #pragma unroll
               for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
@@ -384,11 +382,11 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
               for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
             }
           } else {
-            nn_entry_row<T, false>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+            nn_entry_row<T, false, RAW>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
           }
         }
         uint32_t px[kNnPx];
-        nn_rgba<T>(sk, safe, s_tab, c, px);
+        rgba(c, px);
         store_row(r, px);
 #pragma unroll
         for (int k = 0; k < 4; k++) cv[k] = nv[k];
@@ -398,27 +396,13 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
     }
   }
 #pragma unroll 1
-  for (int j = 0; j < RPW; j += PAIR ? 2 : 1) {
+  for (int j = 0; j < RPW; j++) {
     const int r = r0 + j;
     if (r >= H) break;
-    if constexpr (PAIR && !MASK && !CANVAS) {
-      if (r + 1 < H) {   // rows r, r + 1 with their gathers in flight together
-        V ca[kNnPx], cb[kNnPx];
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) { ca[q] = cnod; cb[q] = cnod; }
-        nn_fold_row2<T>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, ca, cb);
-        uint32_t px[kNnPx];
-        nn_rgba<T>(sk, safe, s_tab, ca, px);
-        store_row(r, px);
-        nn_rgba<T>(sk, safe, s_tab, cb, px);
-        store_row(r + 1, px);
-        continue;
-      }
-    }
     V c[kNnPx];
 #pragma unroll
     for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-    nn_fold_row<T, MASK>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+    nn_fold_row<T, MASK, RAW>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
 
     // output: typed canvas (WCS) or utils.Scale + palette / grey RGBA
     if constexpr (CANVAS) {
@@ -430,133 +414,8 @@ __global__ __launch_bounds__(256, MASK ? 1 : (PAIR ? 7 : 8)) void render_nn_kern
         if (full || 64 * q + lane < ncols) __builtin_nontemporal_store((T)c[q], (GPTR(T))(cdst + 64 * q));
     } else {
       uint32_t px[kNnPx];
-      nn_rgba<T>(sk, safe, s_tab, c, px);
+      rgba(c, px);
       store_row(r, px);
-    }
-  }
-}
-
-// Workgroup barrier for LDS hand-over only: waits for this wave's LDS (and
-// scalar) operations, never for its vector-memory ones, so a store wave does
-// not wait for its RGBA stores to reach memory at every step (a __syncthreads
-// fence would: vmcnt(0)).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// Store wave of the producer / store-wave kernels: n (<= NP) rows of 512
-// 4-byte words from LDS to global rows `stride` elements apart starting at
-// dst, 16 B per lane (1 KB contiguous per instruction) when the rows are
-// 16-B aligned, else a word at a time; columns >= ncols are not written.
-template <int NP>
-__device__ __forceinline__ void ws_store_rows(const uint32_t (*src)[kBandCols], int n, uint32_t *dst, int64_t stride,
-                                              bool vec4, int ncols, int lane) {
-#pragma unroll
-  for (int i = 0; i < NP; i++) {
-    if (i >= n) break;
-#pragma unroll
-    for (int hh = 0; hh < kBandCols / 256; hh++) {
-      const int col = hh * 256 + 4 * lane;
-      const u32x4 v = *(const u32x4 *)&src[i][col];
-      if (vec4 && col + 4 <= ncols) {
-        __builtin_nontemporal_store(v, (GPTR(u32x4))(dst + col));
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; e++)
-          if (col + e < ncols) __builtin_nontemporal_store(v[e], (GPTR(uint32_t))(dst + col + e));
-      }
-    }
-    dst += stride;
-  }
-}
-
-// Producer / store waves (round 3).  gfx9 counts vector loads and stores in
-// one vmcnt, and loads and stores return out of order with respect to each
-// other, so any wave that issues both must wait for its stores before it can
-// use a gather: in render_nn_kernel the gathers of row r + 1 wait for the
-// RGBA stores of row r (s_waitcnt vmcnt(0) before the first gather).  Here
-// waves 0 .. NP-1 only gather: each folds one row per step, applies Scale and
-// the palette and writes the row's 512 RGBA words to LDS; wave NP only
-// stores: it copies the previous step's NP rows from LDS to the tile as
-// 16-B non-temporal stores (1 KB contiguous per instruction).  Two LDS
-// buffers; one lds_barrier() per step.  A block covers NP * STEPS rows of a
-// 512-column block.  RGBA output only, no mask layer (C1, C2 and GetMap
-// stacks without a QA mask).
-template <typename T, int NP, int STEPS>
-__global__ __launch_bounds__(64 * (NP + 1)) void render_nn_ws_kernel(RenderArgs a, const EntryD *__restrict__ ents,
-                                                                     const int32_t *__restrict__ order,
-                                                                     const RowRec *__restrict__ rows,
-                                                                     const Leaf *__restrict__ pool,
-                                                                     const TilePlan *__restrict__ tplans,
-                                                                     const gskyhip_tile *__restrict__ tiles,
-                                                                     int n_items, int xcd_remap) {
-  using V = typename VOf<T>::type;
-  constexpr int kRowsBlk = NP * STEPS;
-  constexpr int kThreads = 64 * (NP + 1);
-  __shared__ uint32_t s_tab[256];
-  __shared__ __attribute__((aligned(16))) uint32_t s_out[2][NP][kBandCols];
-
-  int item = blockIdx.x;
-  if (xcd_remap) {   // workgroups go to the 8 XCDs round robin: give each XCD a contiguous run of items
-    const int q = n_items >> 3, rr = n_items & 7, x = item & 7;
-    item = x * q + min(x, rr) + (item >> 3);
-  }
-  if (item >= n_items) return;
-  const int bands_per_tile = (a.max_h + kRowsBlk - 1) / kRowsBlk;
-  const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
-  const int t = item / (bands_per_tile * col_blocks);
-  const int in_tile = item - t * bands_per_tile * col_blocks;
-  const TilePlan &tp = tplans[t];
-  if (tp.complex || (tp.n_entries > 0 && tp.vt != vt_code<T>())) return;   // empty tiles: written here
-  const gskyhip_tile &tile = tiles[t];
-  const int W = tile.width, H = tile.height;
-  const int band0 = (in_tile / col_blocks) * kRowsBlk;
-  const int xb = (in_tile % col_blocks) * kBandCols;
-  if (band0 >= H || xb >= W) return;
-  const int tid = threadIdx.x;
-  const int ns_out = a.out_ns[0];
-  const bool created = tp.created[ns_out] != 0;
-  for (int i = tid; i < 256; i += kThreads) {   // EncodePNG: 0xFF and canvases never created are transparent
-    const uint32_t col = a.ramp ? a.ramp[i] : (0xFF000000u | ((uint32_t)i * 0x10101u));
-    s_tab[i] = (created && i != 255) ? col : 0u;
-  }
-  __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int ncols = min(kBandCols, W - xb);   // columns of the block inside the tile
-  const int nsteps = min(STEPS, (H - band0 + NP - 1) / NP);
-
-  if (wave < NP) {
-    const V cnod = as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]));
-    const int32_t *ord = order + tile.pair_begin;
-    const int n_entries = tp.n_entries;
-    const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
-    const bool safe = !std::is_same<T, float>::value && (float)max(sk.clp.i, 0) * sk.sc < 2147483648.0f;
-    const int xl = xb + lane;
-#pragma unroll 1
-    for (int p = 0; p < nsteps; p++) {
-      const int r = band0 + p * NP + wave;
-      if (r < H) {
-        V c[kNnPx];
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-        nn_fold_row<T, false>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
-        uint32_t px[kNnPx];
-        nn_rgba<T>(sk, safe, s_tab, c, px);
-        uint32_t *o = &s_out[p & 1][wave][lane];
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) o[64 * q] = px[q];
-      }
-      lds_barrier();
-    }
-  } else {
-    // store wave: step p - 1's rows while the producers fold step p
-    uint32_t *row0 = (uint32_t *)(a.rgba + ((int64_t)t * a.max_h * a.max_w + xb) * 4);
-#pragma unroll 1
-    for (int p = 0; p <= nsteps; p++) {
-      if (p > 0) {
-        const int r = band0 + (p - 1) * NP;
-        ws_store_rows<NP>(s_out[(p - 1) & 1], min(NP, H - r), row0 + (int64_t)r * a.max_w, a.max_w,
-                          (a.max_w & 3) == 0, ncols, lane);
-      }
-      if (p < nsteps) lds_barrier();
     }
   }
 }
@@ -567,11 +426,13 @@ __global__ __launch_bounds__(64 * (NP + 1)) void render_nn_ws_kernel(RenderArgs 
 // canvas batches keep 4 (measured on C5 only).  A/B build: GSKYHIP_NN_RPW.
 constexpr int kNnRpw8MinItems = 32768;
 constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
+constexpr int kNnMaskRpw1Items = 16384;   // masked stacks: one row per wave below this many workgroups
+constexpr int kNnLutMinItems = 1024;      // scale+palette LUT from this many 16-row workgroups
 
-template <typename T, bool M, bool C, int RPW, bool PAIR = false, bool ONE = false>
+template <typename T, bool M, bool C, int RPW, bool LUT = false, bool ONE = false>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, PAIR, ONE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, LUT, ONE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -586,37 +447,43 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   // latency-bound: one row per wave, 4x the workgroups
   const int64_t items4 = (int64_t)a.n_tiles * ((a.max_h + 15) / 16) * ((a.max_w + kBandCols - 1) / kBandCols);
   bool rpw1 = items4 < kNnRpw1MaxItems;
-  int ws = 0, xcd = 0;
+  // the scale+palette LUT for integer RGBA batches big enough to amortise
+  // its build launch (nn_lut_kernel)
+  bool lut = !std::is_same<T, float>::value && !canvas && a.lut && items4 >= kNnLutMinItems;
+  bool one = false;
 #ifdef GSKYHIP_AB
   if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
-  if (const char *w = getenv("GSKYHIP_NN_WS")) ws = atoi(w);
-  if (const char *x = getenv("GSKYHIP_NN_XCD")) xcd = atoi(x);
+  if (const char *lu = getenv("GSKYHIP_NN_LUT")) lut = lut && atoi(lu) != 0;
+  if (const char *on = getenv("GSKYHIP_NN_ONE")) one = atoi(on) != 0;
 #endif
-#ifdef GSKYHIP_AB
-  if (const char *on = getenv("GSKYHIP_NN_ONE")) {
-    if (!mask && !canvas && atoi(on) == 8) { launch_nn_v<T, false, false, 8, false, true>(a, s); return; }
-    if (!mask && !canvas && atoi(on) == 4) { launch_nn_v<T, false, false, 4, false, true>(a, s); return; }
-  }
-  if (const char *pr = getenv("GSKYHIP_NN_PAIR")) {
-    if (!mask && !canvas && atoi(pr) == 8) { launch_nn_v<T, false, false, 8, true>(a, s); return; }
-    if (!mask && !canvas && atoi(pr) == 4) { launch_nn_v<T, false, false, 4, true>(a, s); return; }
-  }
-#endif
-  if (!mask && !canvas && ws > 0) {
-    const int cb = (a.max_w + kBandCols - 1) / kBandCols;
-    if (ws == 3) {
-      const int items = a.n_tiles * ((a.max_h + 23) / 24) * cb;
-      hipLaunchKernelGGL((render_nn_ws_kernel<T, 3, 8>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
-                         a.order, a.rows, a.pool, a.tplans, a.tiles, items, xcd);
+  if constexpr (!std::is_same<T, float>::value) if (lut) {
+    constexpr int n = 1 << (8 * sizeof(T));
+    hipLaunchKernelGGL(nn_lut_kernel<T>, dim3((n + 255) / 256), dim3(256), 0, s, a, a.lut);
+    if (mask) {
+      if (items4 < kNnMaskRpw1Items) launch_nn_v<T, true, false, 1, true>(a, s);
+      else launch_nn_v<T, true, false, 4, true>(a, s);
+    } else if (rpw8) {
+      if (one) launch_nn_v<T, false, false, 8, true, true>(a, s);
+      else launch_nn_v<T, false, false, 8, true>(a, s);
     } else {
-      const int items = a.n_tiles * ((a.max_h + 55) / 56) * cb;
-      hipLaunchKernelGGL((render_nn_ws_kernel<T, 7, 8>), dim3((unsigned)items), dim3(512), 0, s, a, a.entries,
-                         a.order, a.rows, a.pool, a.tplans, a.tiles, items, xcd);
+      launch_nn_v<T, false, false, 4, true>(a, s);
     }
     return;
   }
+  if (one && !mask && !canvas && rpw8) {
+    launch_nn_v<T, false, false, 8, false, true>(a, s);
+    return;
+  }
   if (mask) {
+    // stacks with a mask layer (C5: ~17 entries and a mask raster per tile)
+    // are latency-bound per wave row: below kNnMaskRpw1Items workgroups, one
+    // row per wave (4x the waves in flight)
+    bool m1 = items4 < kNnMaskRpw1Items;
+#ifdef GSKYHIP_AB
+    if (const char *rp = getenv("GSKYHIP_NN_MASK_RPW")) m1 = atoi(rp) == 1;
+#endif
     if (canvas) launch_nn_v<T, true, true, 4>(a, s);
+    else if (m1) launch_nn_v<T, true, false, 1>(a, s);
     else launch_nn_v<T, true, false, 4>(a, s);
   } else if (canvas) {
     launch_nn_v<T, false, true, 4>(a, s);

@@ -306,6 +306,7 @@ def test_gpu_drop_in_opens_geotiff(tmp_path):
     import torch
 
     from gsky_amd import synth, worker
+    from gsky_amd.tiles import bbox_to_geot
     cfg = synth.config_c2(scale=0.05, tiles_per_side=2, tile_px=128)
     g = cfg.granules[0]
     p = str(tmp_path / "granule.tif")
@@ -315,14 +316,16 @@ def test_gpu_drop_in_opens_geotiff(tmp_path):
     worker.unregister_all()
     worker.register_granule("hand", 1, torch.from_numpy(g.data).cuda(), g.geot, "EPSG:3577", g.nodata)
     bbox, w, h = cfg.tiles[0]
-    req = dict(band=1, dst_srs="EPSG:3857", bbox=bbox, width=w, height=h)
+    req = dict(bands=[1], width=w, height=h, dstSRS="EPSG:3857", dstGeot=bbox_to_geot(w, h, bbox))
     a = worker.warp_raster(worker.GeoRPCGranule(path="hand", **req))
     b = worker.warp_raster(worker.GeoRPCGranule(path=p, **req))
-    assert a.error == "OK" and b.error == "OK"
-    assert np.array_equal(np.asarray(a.data), np.asarray(b.data)) and a.bbox == b.bbox
-    assert b.no_data == g.nodata
+    assert a.error == "OK" and b.error == "OK", (a.error, b.error)
+    assert np.array_equal(worker.raster_array(a.raster), worker.raster_array(b.raster))
+    assert a.raster.bbox == b.raster.bbox and b.raster.noData == g.nodata
     assert worker.warp_raster(worker.GeoRPCGranule(path=str(tmp_path / "absent.tif"), **req)).error == \
         "warp_operation() fail: 1"
+    assert worker.warp_raster(worker.GeoRPCGranule(path=p, **dict(req, bands=[2]))).error == \
+        "warp_operation() fail: 2"
     worker.unregister_all()
 
 
@@ -421,6 +424,7 @@ def test_gpu_netcdf_read_and_drop_in(tmp_path):
     import torch
 
     from gsky_amd import worker
+    from gsky_amd.tiles import bbox_to_geot
     rng = np.random.default_rng(4)
     nt, ny, nx = 3, 400, 600
     data = rng.integers(0, 10000, (nt, ny, nx)).astype(np.int16)
@@ -434,10 +438,11 @@ def test_gpu_netcdf_read_and_drop_in(tmp_path):
     worker.unregister_all()
     worker.register_granule("hand", 2, torch.from_numpy(data[1]).cuda(), inf.geot, "EPSG:4326", -1.0)
     bbox = (14471533.8, -2504688.5, 14526000.0, -2450000.0)
-    req = dict(dst_srs="EPSG:3857", bbox=bbox, width=256, height=256)
-    a = worker.warp_raster(worker.GeoRPCGranule(path="hand", band=2, **req))
-    b = worker.warp_raster(worker.GeoRPCGranule(path="NETCDF:%s:v" % p, band=2, **req))
-    assert a.error == "OK" and b.error == "OK"
-    assert np.array_equal(np.asarray(a.data), np.asarray(b.data)) and a.bbox == b.bbox
+    req = dict(bands=[2], width=256, height=256, dstSRS="EPSG:3857", dstGeot=bbox_to_geot(256, 256, bbox))
+    a = worker.warp_raster(worker.GeoRPCGranule(path="hand", **req))
+    b = worker.warp_raster(worker.GeoRPCGranule(path="NETCDF:%s:v" % p, **req))
+    assert a.error == "OK" and b.error == "OK", (a.error, b.error)
+    assert np.array_equal(worker.raster_array(a.raster), worker.raster_array(b.raster))
+    assert a.raster.bbox == b.raster.bbox
     worker.unregister_all()
     torch.cuda.synchronize()
