@@ -312,16 +312,32 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
       }
     }
     __syncthreads();
-    if (tid < nr) {   // the digit bucket holding each rank
-      const uint32_t *h = hist[s_slot[tid]];
-      uint32_t rem = s_rem[tid], cum = 0;
-      int dg = 0;
-      for (; dg < (1 << d) - 1; dg++) {
-        if (cum + h[dg] > rem) break;
-        cum += h[dg];
+    // the digit bucket holding each rank: a wave per rank, lane l sums bins
+    // 4l..4l+3, an inclusive scan over the lanes finds the lane whose range
+    // holds the rank, that lane walks its 4 bins (bins >= 2^d are empty)
+    {
+      const int wv = tid >> 6, ln = tid & 63;
+      for (int r = wv; r < nr; r += kSelThreads / 64) {
+        const uint32_t *h = hist[s_slot[r]];
+        const uint32_t rem = s_rem[r];
+        const uint32_t b0 = h[4 * ln], b1 = h[4 * ln + 1], b2 = h[4 * ln + 2], b3 = h[4 * ln + 3];
+        const uint32_t sum = b0 + b1 + b2 + b3;
+        uint32_t incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t up = __shfl_up(incl, o);
+          if (ln >= o) incl += up;
+        }
+        const uint32_t excl = incl - sum;
+        if (excl <= rem && rem < incl) {   // exactly one lane (the counts of the slot exceed rem)
+          uint32_t cum = excl;
+          int dg = 4 * ln;
+          if (cum + b0 <= rem) { cum += b0; dg++;
+            if (cum + b1 <= rem) { cum += b1; dg++;
+              if (cum + b2 <= rem) { cum += b2; dg++; } } }
+          s_pref[r] = (s_pref[r] << d) | (uint32_t)dg;
+          s_rem[r] = rem - cum;
+        }
       }
-      s_pref[tid] = (s_pref[tid] << d) | (uint32_t)dg;
-      s_rem[tid] = rem - cum;
     }
     __syncthreads();
     pos = shift;

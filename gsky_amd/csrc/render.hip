@@ -1607,11 +1607,6 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.lds_mode = 0;
   a.cov_offsets = rc.cov_offsets;
   a.cov_stride = rc.cov_stride;
-  // the scale+palette LUT (render_nn.h) lives in the split-list region: that
-  // list is planning scratch, read only by plan_split_kernel before any band
-  // kernel runs on this stream
-  a.lut = (int64_t)sizeof(int64_t) * std::max(rc.n_pairs, 1) * rc.max_h >= (int64_t)kLutEntries * 4
-              ? (uint32_t *)cv.split_list : nullptr;
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;

@@ -211,7 +211,6 @@ struct RenderArgs {
   int lds_mode;          // typed band kernels: kBilinear | kCanvas bits of the call
   const int64_t *cov_offsets;  // canvas mode: per tile element offset into one image (NULL: slots)
   int64_t cov_stride;          // ... and that image's row stride (elements)
-  uint32_t *lut;               // 65536 RGBA words of workspace: the scale+palette table (render_nn.h)
 };
 
 // ---------------------------------------------------------------- typed fast path
@@ -443,7 +442,6 @@ __device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const
 }
 
 constexpr int kLdsBandRows = 16;   // rows per block of render_lds_kernel
-constexpr int kLutEntries = 65536;   // RenderArgs.lut: scale+palette table of 16-bit samples (render_nn.h)
 constexpr int kBilinear = 4, kCanvas = 8;   // render_lds_kernel modes (RenderArgs.lds_mode)
 
 // The typed band kernels (render_lds.hip) for value type `vt`.

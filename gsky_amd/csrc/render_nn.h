@@ -70,27 +70,10 @@ __device__ __forceinline__ uint32_t scale_int(const ScaleK &k, int32_t c) {
   return c == k.noData.i ? 0xFFu : b;
 }
 
-// Canvas value domain.  RAW = false: the value as an int (sign-extended for
-// signed T) or float -- what Scale reads.  RAW = true (integer T with the
-// scale+palette LUT): the sample's raw bits, zero-extended -- a load needs
-// no sign extension and the value indexes the LUT directly.  Equality, the
-// only operation the fold applies, means the same in both domains.
-template <typename T, bool RAW>
-__device__ __forceinline__ typename VOf<T>::type dom(typename VOf<T>::type v) {
-  if constexpr (RAW && sizeof(T) < 4) return (typename VOf<T>::type)((uint32_t)v & ((1u << (8 * sizeof(T))) - 1u));
-  else return v;
-}
-template <typename T, bool RAW>
-__device__ __forceinline__ typename VOf<T>::type nn_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  if constexpr (RAW && sizeof(T) == 2) return (typename VOf<T>::type)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
-  else if constexpr (RAW && sizeof(T) == 1) return (typename VOf<T>::type)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
-  else return buf_load<T>(r, off);
-}
-
 // One stack entry e of the ordered fold of tile row r (MergeMaskedRaster,
 // tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
 // (tile column xl + 64 q).
-template <typename T, bool MASK, bool RAW = false>
+template <typename T, bool MASK>
 __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
                                              const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
                                              int ns_out, int r, int xb, int xl, int W, int ncols,
@@ -107,7 +90,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
   const int inside = __builtin_amdgcn_readfirstlane(rr->inside);
   const int bx = e.band_x, by = e.band_y;
-  const V nd = dom<T, RAW>(as_v<T>(e.nd));
+  const V nd = as_v<T>(e.nd);
   const bool fill_mode = e.fill_mode != 0;
   const int ic0 = xl - exoff;   // window column of the lane's pixel 0
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -127,7 +110,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
     }
     V vv[kNnPx];
 #pragma unroll
-    for (int q = 0; q < kNnPx; q++) vv[q] = nn_load<T, RAW>(rs, off[q]);
+    for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
     if (!fill_mode) {
 #pragma unroll
       for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
@@ -140,7 +123,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   // general body: window edges, POOL rows, failed transforms, mask layer;
   // two halves of 4 pixels (4 gathers in flight) keep the register peak
   // of the fast body
-  const V fillv = dom<T, RAW>(as_v<T>(e.fill));
+  const V fillv = as_v<T>(e.fill);
 #pragma unroll
   for (int h = 0; h < kNnPx; h += 4) {
     uint32_t idx[4];
@@ -166,7 +149,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
     }
     V vv[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) vv[q] = nn_load<T, RAW>(rs, idx[q] * (uint32_t)sizeof(T));
+    for (int q = 0; q < 4; q++) vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int ic = ic0 + 64 * (h + q);
@@ -183,7 +166,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
 
 // The ordered fold of tile row r over the tile's entries in ProcessRasterStack
 // order; c[] arrives holding the canvas nodata.
-template <typename T, bool MASK, bool RAW = false>
+template <typename T, bool MASK>
 __device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *__restrict__ ents,
                                             const int32_t *__restrict__ ord, int n_entries,
                                             const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
@@ -191,7 +174,7 @@ __device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *_
                                             typename VOf<T>::type (&c)[kNnPx]) {
 #pragma unroll 1
   for (int k = 0; k < n_entries; k++)
-    nn_entry_row<T, MASK, RAW>(a, ents, ents[ord[k]], rows, pool, ns_out, r, xb, xl, W, ncols, c);
+    nn_entry_row<T, MASK>(a, ents, ents[ord[k]], rows, pool, ns_out, r, xb, xl, W, ncols, c);
 }
 
 // utils.Scale + palette / grey of the lane's 8 canvas values (EncodePNG's
@@ -213,43 +196,15 @@ __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint3
   }
 }
 
-// Scale + palette as one table (integer T, RGBA): entry u = the RGBA of the
-// raw sample u -- utils.Scale of a non-nodata value (raster_scaler.go:30-332:
-// offset wrapping in T, clip, float32 multiply, Go uint8) looked up in the
-// palette / grey ramp with EncodePNG's transparency for 0xFF
-// (ogc_encoders.go:94-133).  The same expressions as scale_int() + s_tab, so
-// the same bytes; one table per launch (it depends on T and the scale
-// parameters only), built by nn_lut_kernel.  A pixel is then one compare with
-// the canvas nodata and one 4-byte load instead of ~10 VALU + an LDS read.
-template <typename T>
-__global__ __launch_bounds__(256) void nn_lut_kernel(RenderArgs a, uint32_t *__restrict__ lut) {
-  constexpr uint32_t n = 1u << (8 * sizeof(T));
-  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
-  if (u >= n) return;
-  const ScaleK sk = make_scale(vt_code<T>(), 0.0, a.sp, false, 0.f, 0.f);
-  const int32_t c = std::is_signed<T>::value ? (sizeof(T) == 1 ? (int32_t)(int8_t)u : (int32_t)(int16_t)u) : (int32_t)u;
-  int32_t value = c + sk.off.i;
-  if constexpr (std::is_same<T, int8_t>::value) value = (int8_t)value;
-  else if constexpr (std::is_same<T, uint8_t>::value) value = (uint8_t)value;
-  else if constexpr (std::is_same<T, int16_t>::value) value = (int16_t)value;
-  else value = (uint16_t)value;
-  value = max(min(value, sk.clp.i), 0);
-  const uint32_t b = go_u8_f32((float)value * sk.sc);
-  const uint32_t col = a.ramp ? a.ramp[b] : (0xFF000000u | (b * 0x10101u));
-  lut[u] = b == 255 ? 0u : col;
-}
-
 // RPW: rows per wave (a block of 4 waves covers 4 * RPW rows of a 512-column
 // block).  Rows are processed one after the other; a row's RGBA stores are
 // issued before the next row's gathers (deferring them behind those gathers
 // measured 0.6 % slower on C2 and C5, profiles/r03b_ab_nn.jsonl).
-// LUT (integer T, RGBA): canvas values in the RAW domain, Scale + palette
-// through a.lut (nn_lut_kernel).
 // ONE (RGBA, no mask layer): tiles with a single stack entry -- most GetMap
 // tiles -- keep the entry's descriptor in scalar registers for all the
 // wave's rows and fetch the next row's record while the current row is
 // gathered, so no row waits for its record.
-template <typename T, bool MASK, bool CANVAS, int RPW, bool LUT = false, bool ONE = false>
+template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, bool STAGE = false>
 __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
@@ -260,6 +215,10 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   using V = typename VOf<T>::type;
   constexpr int kRowsBlk = 4 * RPW;
   __shared__ uint32_t s_tab[256];
+  // STAGE (A/B): a row's 512 RGBA words go through the wave's LDS row so
+  // they leave as two 16-B-per-lane stores (1 KB contiguous each) instead of
+  // eight 4-B ones
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[STAGE ? 4 : 1][STAGE ? kBandCols : 4];
 
   const int item = blockIdx.x;
   if (item >= n_items) return;
@@ -277,8 +236,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int tid = threadIdx.x;
   const int ns_out = a.out_ns[0];
   const bool created = tp.created[ns_out] != 0;
-  constexpr bool RAW = LUT && !std::is_same<T, float>::value && !CANVAS;
-  if constexpr (!CANVAS && !RAW) {   // EncodePNG: utils.Scale 0xFF and canvases never created are transparent
+  if constexpr (!CANVAS) {   // EncodePNG: utils.Scale 0xFF and canvases never created are transparent
     const uint32_t col = a.ramp ? a.ramp[tid] : (0xFF000000u | ((uint32_t)tid * 0x10101u));
     s_tab[tid] = (created && tid != 255) ? col : 0u;
     __syncthreads();
@@ -287,7 +245,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int r0 = band0 + wave * RPW;
   if (r0 >= H) return;
 
-  const V cnod = dom<T, RAW>(as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out])));
+  const V cnod = as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]));
   const int32_t *ord = order + tile.pair_begin;
   const int n_entries = tp.n_entries;
   const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
@@ -297,28 +255,29 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int xl = xb + lane;                     // tile column of the lane's pixel 0
   uint32_t *rgba_lane = (uint32_t *)(a.rgba + (((int64_t)t * a.max_h) * a.max_w + xl) * 4);
 
-  // utils.Scale + palette of the row's 8 values: the LUT (RAW domain; the
-  // canvas nodata is transparent) or scale_int + the LDS table
-  const __amdgpu_buffer_rsrc_t lut_rs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)a.lut, (short)0, kLutEntries * 4, 0x00020000);
-  auto rgba = [&](const V (&c)[kNnPx], uint32_t (&px)[kNnPx]) {
-    if constexpr (RAW) {
-      const V nod = dom<T, RAW>(sk.noData.i);
-      uint32_t v[kNnPx];
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) v[q] = __builtin_amdgcn_raw_buffer_load_b32(lut_rs, (uint32_t)c[q] * 4u, 0, 0);
-      // a canvas never created keeps the canvas nodata everywhere, so the
-      // nodata compare also makes it transparent
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) px[q] = c[q] != nod ? v[q] : 0u;
-    } else {
-      nn_rgba<T>(sk, safe, s_tab, c, px);
-    }
-  };
+  auto rgba = [&](const V (&c)[kNnPx], uint32_t (&px)[kNnPx]) { nn_rgba<T>(sk, safe, s_tab, c, px); };
 
   // RGBA stores of row r
   auto store_row = [&](int r, const uint32_t *px) {
     uint32_t *dst = rgba_lane + (int64_t)r * a.max_w;
+    if constexpr (STAGE && !CANVAS) {
+      if (full && (a.max_w & 3) == 0) {
+        uint32_t *row = s_stage[wave];
+#pragma unroll
+        for (int q = 0; q < kNnPx; q++) row[lane + 64 * q] = px[q];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const u32x4 v0 = *(const u32x4 *)&row[4 * lane], v1 = *(const u32x4 *)&row[256 + 4 * lane];
+        uint32_t *d0 = dst - lane;   // the block's first column of row r
+        __builtin_nontemporal_store(v0, (GPTR(u32x4))(d0 + 4 * lane));
+        __builtin_nontemporal_store(v1, (GPTR(u32x4))(d0 + 256 + 4 * lane));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        return;
+      }
+    }
     if (full) {
 #pragma unroll
       for (int q = 0; q < kNnPx; q++) __builtin_nontemporal_store(px[q], (GPTR(uint32_t))(dst + 64 * q));
@@ -338,7 +297,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
       const bool cols_ok = e.ns == ns_out && ew > 0 && c1 > 0 && c0 < ncols;
       const bool cover = c0 <= 0 && c1 >= ncols;
       const int bx = e.band_x, by = e.band_y;
-      const V nd = dom<T, RAW>(as_v<T>(e.nd));
+      const V nd = as_v<T>(e.nd);
       const bool fill_mode = e.fill_mode != 0;
       const int ic0 = xl - exoff;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -373,7 +332,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
             }
             V vv[kNnPx];
 #pragma unroll
-            for (int q = 0; q < kNnPx; q++) vv[q] = nn_load<T, RAW>(rs, off[q]);
+            for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
             if (!fill_mode) {
 #pragma unroll
               for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
@@ -382,7 +341,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
               for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
             }
           } else {
-            nn_entry_row<T, false, RAW>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+            nn_entry_row<T, false>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
           }
         }
         uint32_t px[kNnPx];
@@ -402,7 +361,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
     V c[kNnPx];
 #pragma unroll
     for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-    nn_fold_row<T, MASK, RAW>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+    nn_fold_row<T, MASK>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
 
     // output: typed canvas (WCS) or utils.Scale + palette / grey RGBA
     if constexpr (CANVAS) {
@@ -427,12 +386,11 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 constexpr int kNnRpw8MinItems = 32768;
 constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
 constexpr int kNnMaskRpw1Items = 16384;   // masked stacks: one row per wave below this many workgroups
-constexpr int kNnLutMinItems = 1024;      // scale+palette LUT from this many 16-row workgroups
 
-template <typename T, bool M, bool C, int RPW, bool LUT = false, bool ONE = false>
+template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = false>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, LUT, ONE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -447,33 +405,20 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   // latency-bound: one row per wave, 4x the workgroups
   const int64_t items4 = (int64_t)a.n_tiles * ((a.max_h + 15) / 16) * ((a.max_w + kBandCols - 1) / kBandCols);
   bool rpw1 = items4 < kNnRpw1MaxItems;
-  // the scale+palette LUT for integer RGBA batches big enough to amortise
-  // its build launch (nn_lut_kernel)
-  bool lut = !std::is_same<T, float>::value && !canvas && a.lut && items4 >= kNnLutMinItems;
-  bool one = false;
+  // single-entry tiles through the prefetching path (C2: 1.445 vs 1.470 ms,
+  // profiles/r03f_ab_c2.jsonl)
+  bool one = true;
 #ifdef GSKYHIP_AB
   if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
-  if (const char *lu = getenv("GSKYHIP_NN_LUT")) lut = lut && atoi(lu) != 0;
   if (const char *on = getenv("GSKYHIP_NN_ONE")) one = atoi(on) != 0;
-#endif
-  if constexpr (!std::is_same<T, float>::value) if (lut) {
-    constexpr int n = 1 << (8 * sizeof(T));
-    hipLaunchKernelGGL(nn_lut_kernel<T>, dim3((n + 255) / 256), dim3(256), 0, s, a, a.lut);
-    if (mask) {
-      if (items4 < kNnMaskRpw1Items) launch_nn_v<T, true, false, 1, true>(a, s);
-      else launch_nn_v<T, true, false, 4, true>(a, s);
-    } else if (rpw8) {
+  if (const char *st = getenv("GSKYHIP_NN_STAGE")) {
+    if (!mask && !canvas && rpw8 && atoi(st) == 1) {
       if (one) launch_nn_v<T, false, false, 8, true, true>(a, s);
-      else launch_nn_v<T, false, false, 8, true>(a, s);
-    } else {
-      launch_nn_v<T, false, false, 4, true>(a, s);
+      else launch_nn_v<T, false, false, 8, false, true>(a, s);
+      return;
     }
-    return;
   }
-  if (one && !mask && !canvas && rpw8) {
-    launch_nn_v<T, false, false, 8, false, true>(a, s);
-    return;
-  }
+#endif
   if (mask) {
     // stacks with a mask layer (C5: ~17 entries and a mask raster per tile)
     // are latency-bound per wave row: below kNnMaskRpw1Items workgroups, one
@@ -488,7 +433,8 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   } else if (canvas) {
     launch_nn_v<T, false, true, 4>(a, s);
   } else if (rpw8) {
-    launch_nn_v<T, false, false, 8>(a, s);
+    if (one) launch_nn_v<T, false, false, 8, true>(a, s);
+    else launch_nn_v<T, false, false, 8>(a, s);
   } else if (rpw1) {
     launch_nn_v<T, false, false, 1>(a, s);
   } else {

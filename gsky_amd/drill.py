@@ -21,6 +21,23 @@ def _stream():
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+_WS = {}
+
+
+def _workspace(dev, nbytes: int) -> torch.Tensor:
+    """The drill workspace of (device, stream), grown as needed and kept:
+    readData with deciles needs gigabytes of it, and a fresh allocation per
+    request costs more than the kernels (calls on one stream are ordered, so
+    they can share it)."""
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        _WS.pop(key, None)
+        t = torch.empty(max(1, int(nbytes)), dtype=torch.uint8, device=dev)
+        _WS[key] = t
+    return t
+
+
 class DrillStack:
     """Float32 time stack (n_bands, ysize, xsize) -> HBM [y][x][t_stride]."""
 
@@ -181,7 +198,7 @@ def read_data(stack: DrillStack, win, mask_off=None, masks=None, clip_lower: flo
     vals = torch.empty((n_polys, rows), dtype=torch.float64, device=dev)
     cnts = torch.empty((n_polys, rows), dtype=torch.int32, device=dev)
     ws_bytes = lib().gskyhip_drill_workspace_size(n_polys, mb.mask_bytes, n_list, band_strides, mode)
-    ws = torch.empty(max(1, int(ws_bytes)), dtype=torch.uint8, device=dev)
+    ws = _workspace(dev, int(ws_bytes))
     check(lib().gskyhip_drill_batch(C.c_void_p(stack.stack.data_ptr()), stack.xsize, stack.ysize, stack.n_bands,
                                     stack.t_stride, C.c_void_p(mb.win.data_ptr()), C.c_void_p(mb.mask_off.data_ptr()),
                                     C.c_void_p(mb.masks.data_ptr()), n_polys, mb.mask_bytes,
@@ -212,7 +229,7 @@ def read_data_deciles(stack: DrillStack, mb: "MaskBatch", clip_lower: float, cli
                                                             decile_count, mode)
     if ws_bytes < 0:
         raise ValueError("readData workspace out of range")
-    ws = torch.empty(max(1, int(ws_bytes)), dtype=torch.uint8, device=dev)
+    ws = _workspace(dev, int(ws_bytes))
     check(lib().gskyhip_drill_read_data(C.c_void_p(stack.stack.data_ptr()), stack.xsize, stack.ysize,
                                         stack.n_bands, stack.t_stride, C.c_void_p(mb.win.data_ptr()),
                                         C.c_void_p(mb.mask_off.data_ptr()), C.c_void_p(mb.masks.data_ptr()),
@@ -243,7 +260,7 @@ def compute_deciles(stack: DrillStack, mb: "MaskBatch", totals: torch.Tensor, de
     ws_bytes = lib().gskyhip_drill_deciles_workspace_size(n_polys, mb.mask_bytes, band_chunk)
     if ws_bytes < 0:
         raise ValueError("deciles workspace: mask_bytes x band_chunk must stay below 2^31")
-    ws = torch.empty(max(1, int(ws_bytes)), dtype=torch.uint8, device=dev)
+    ws = _workspace(dev, int(ws_bytes))
     out = torch.empty((n_polys, n_list, decile_count), dtype=torch.float32, device=dev)
     st = torch.empty((n_polys, n_list), dtype=torch.int32, device=dev)
     tot = totals.to(dev, torch.int32).contiguous()
