@@ -250,55 +250,56 @@ __global__ void drill_rows_kernel(const double *band_value, const int32_t *band_
 // column interpolated between the two bound bands of the group, counts
 // math.Round((c0 + c1) / 2).  status[p]: GSKYHIP_E_RANGE if computeDeciles
 // would have panicked on any read band of the polygon.
-__global__ void drill_timeseries_kernel(const double *band_value, const int32_t *band_count,
-                                        const float *dec, const int32_t *dec_status, int n_polys, int n_list,
-                                        int n_sel, int band_strides, int dc, int rows_per_poly, double *out_value,
-                                        int32_t *out_count, int32_t *status) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+// One thread per (polygon, TimeSeries row): grid (row blocks, polygons).
+// Row k of polygon p for bandStrides <= 1 is read band k; otherwise group g =
+// k / R (R = max(2, bandStrides) rows: the first bound band, the
+// interpolated columns, the last bound band).  status[p] (zeroed by the
+// caller) receives the smallest error code of the polygon's deciles.
+__global__ __launch_bounds__(128) void drill_timeseries_kernel(const double *band_value, const int32_t *band_count,
+                                                               const float *dec, const int32_t *dec_status,
+                                                               int n_polys, int n_list, int n_sel, int band_strides,
+                                                               int dc, int rows_per_poly, double *out_value,
+                                                               int32_t *out_count, int32_t *status) {
+  const int p = blockIdx.y;
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_polys) return;
-  const int nc = 1 + dc;
-  const double *bv = band_value + (int64_t)p * n_sel;
-  const int32_t *bc = band_count + (int64_t)p * n_sel;
-  double *ov = out_value + (int64_t)p * rows_per_poly * nc;
-  int32_t *oc = out_count + (int64_t)p * rows_per_poly * nc;
   int st = 0;
-  auto cell = [&](int j, int ic, double &v, int32_t &c) {
-    if (ic == 0) { v = bv[j]; c = bc[j]; return; }
-    const int64_t sj = (int64_t)p * n_sel + j;
-    const int ds = dec_status[sj];
-    if (ds == 0) { v = (double)dec[sj * dc + ic - 1]; c = 1; }
-    else { v = 0.0; c = 0; if (ds != 1) st = ds; }
-  };
-  int nrow = 0;
-  auto emit = [&](int j) {
-    for (int ic = 0; ic < nc; ic++) cell(j, ic, ov[nrow * nc + ic], oc[nrow * nc + ic]);
-    nrow++;
-  };
-  if (band_strides <= 1) {
-    for (int j = 0; j < n_list; j++) emit(j);
-  } else {
-    int g = 0;
-    for (int ibBgn = 0; ibBgn < n_list; ibBgn += band_strides, g++) {
-      const int j0 = 2 * g, j1 = 2 * g + 1;
-      emit(j0);
-      if (band_strides > 2) {
-        for (int ip = 1; ip < band_strides - 1; ip++) {
-          for (int ic = 0; ic < nc; ic++) {
-            double v0, v1;
-            int32_t c0, c1;
-            cell(j0, ic, v0, c0);
-            cell(j1, ic, v1, c1);
-            const double beta = (v1 - v0) / (double)(band_strides - 1);
-            ov[nrow * nc + ic] = v0 + (double)ip * beta;
-            oc[nrow * nc + ic] = (int32_t)round((double)(c0 + c1) / 2.0);   // math.Round: half away from zero
-          }
-          nrow++;
-        }
+  if (row < rows_per_poly) {
+    const int nc = 1 + dc;
+    const double *bv = band_value + (int64_t)p * n_sel;
+    const int32_t *bc = band_count + (int64_t)p * n_sel;
+    double *ov = out_value + ((int64_t)p * rows_per_poly + row) * nc;
+    int32_t *oc = out_count + ((int64_t)p * rows_per_poly + row) * nc;
+    auto cell = [&](int j, int ic, double &v, int32_t &c) {
+      if (ic == 0) { v = bv[j]; c = bc[j]; return; }
+      const int64_t sj = (int64_t)p * n_sel + j;
+      const int ds = dec_status[sj];
+      if (ds == 0) { v = (double)dec[sj * dc + ic - 1]; c = 1; }
+      else { v = 0.0; c = 0; if (ds != 1) st = min(st, ds); }
+    };
+    int j = row, ip = 0, R = 1;
+    if (band_strides > 1) {
+      R = band_strides > 2 ? band_strides : 2;
+      const int g = row / R, k = row - g * R;
+      j = k == 0 ? 2 * g : (k == R - 1 ? 2 * g + 1 : -1);
+      ip = k;
+    }
+    if (j >= 0) {
+      for (int ic = 0; ic < nc; ic++) cell(j, ic, ov[ic], oc[ic]);
+    } else {   // interpolated column between the group's bound bands (drill.go:197-214)
+      const int g = row / R;
+      for (int ic = 0; ic < nc; ic++) {
+        double v0, v1;
+        int32_t c0, c1;
+        cell(2 * g, ic, v0, c0);
+        cell(2 * g + 1, ic, v1, c1);
+        const double beta = (v1 - v0) / (double)(band_strides - 1);
+        ov[ic] = v0 + (double)ip * beta;
+        oc[ic] = (int32_t)round((double)(c0 + c1) / 2.0);   // math.Round: half away from zero
       }
-      emit(j1);
     }
   }
-  status[p] = st;
+  if (st) atomicMin(&status[p], st);
 }
 
 // DrillMerger weighted mean (drill_merger.go:79-93).
@@ -539,8 +540,9 @@ int launch_drill_read_data(const ReadDataCall &c) {
     if ((rc = launch_drill_deciles(d))) return rc;
   }
   const int rows = drill_rows_per_poly(n_list, band_strides);
-  hipLaunchKernelGGL(drill_timeseries_kernel, dim3((c.n_polys + 127) / 128), dim3(128), 0, c.stream, w.bv, w.bc,
-                     w.dec, w.dst, c.n_polys, n_list, n_sel, band_strides, c.decile_count, rows, c.out_value,
+  if (hipMemsetAsync(c.status, 0, sizeof(int32_t) * (size_t)c.n_polys, c.stream) != hipSuccess) return GSKYHIP_E_HIP;
+  hipLaunchKernelGGL(drill_timeseries_kernel, dim3((rows + 127) / 128, c.n_polys), dim3(128), 0, c.stream, w.bv,
+                     w.bc, w.dec, w.dst, c.n_polys, n_list, n_sel, band_strides, c.decile_count, rows, c.out_value,
                      c.out_count, c.status);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }

@@ -26,17 +26,22 @@
 //                         over the segment counts its non-nodata values and
 //                         finds the bits all their keys share (AND / OR), and
 //                         keeps the keys in LDS when they fit; then the
-//                         distinct ranks the picks need (<= 2 dc), found
-//                         together by MSD radix selection on the order-
-//                         preserving 32-bit keys -- 8-bit digits below the
-//                         shared bits, one LDS histogram per distinct prefix
-//                         of the pending ranks, from the LDS copy (or the
-//                         segment again when it did not fit) -- then the
-//                         reference's picks.
+//                         distinct ranks the picks need (<= 2 dc) on the
+//                         order-preserving 32-bit keys: one 2048-bin
+//                         histogram of the 11 bits below the shared ones,
+//                         scanned once, places every rank in its bucket; the
+//                         keys of those buckets (<= 64 each) are compacted
+//                         into LDS and each rank is the rem-th of its
+//                         bucket by a 64-lane counting compare.  Buckets
+//                         holding more keys (heavy ties, skewed data)
+//                         continue by MSD radix selection with 8-bit digits,
+//                         one LDS histogram per distinct prefix of the
+//                         pending ranks -- then the reference's picks.
 // Keys order -0.0 before +0.0 where Go's sort may leave them in either order;
 // the picked values are then equal as float32 (NaN-free stacks; with NaNs the
 // reference's order is implementation-defined).
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "drill.h"
@@ -46,8 +51,14 @@ namespace gsky {
 
 namespace {
 
-constexpr int kSelThreads = 256;
+constexpr int kSelThreads = 512;
+constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kMaxRanks = 32;        // distinct ranks selected per pass set (2 x decile_count <= 32)
+constexpr int kBinsLog = 11;         // first selection pass: 2048 buckets
+constexpr int kBins = 1 << kBinsLog;
+constexpr int kCandMax = 64;         // keys of one bucket resolved by the counting compare
+static_assert(kBins == 4 * kSelThreads, "the bucket scan gives each thread 4 bins");
+static_assert(kMaxRanks * kCandMax <= kBins, "candidates reuse the bucket histogram");
 constexpr int kTilePad = 65;         // LDS tile row pitch (floats): conflict-free transposed reads
 
 __device__ __forceinline__ uint32_t fkey(float f) {   // order-preserving key of a float
@@ -59,7 +70,9 @@ __device__ __forceinline__ float fdecode(uint32_t k) {
 }
 
 constexpr int kDecChunk = 64;        // pixels per transpose item
-constexpr int kSelLds = 48 * 1024;   // dynamic LDS of a select workgroup (histograms + key cache): 3 per CU
+constexpr int kSelLds = 36 * 1024;   // dynamic LDS of a select workgroup (histograms + key cache): 4 per CU
+constexpr int kSelU = 16;            // segment values per thread in flight (a 6k-value segment: one round)
+constexpr int kHistSlots = kBins / 256;  // radix histograms at once (the region also holds the 2048 buckets)
 
 // Exclusive scan of 64-pixel chunks per polygon (one block; n_polys is modest).
 __global__ __launch_bounds__(1024) void decile_chunk_scan_kernel(const int32_t *__restrict__ count, int n_polys,
@@ -145,7 +158,9 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
 // computeDeciles of one (polygon, band) segment; status 0, 1 (band total 0:
 // zeros, Count 0 in the reference's TimeSeries) or GSKYHIP_E_RANGE (the
 // reference indexes buf[len] and panics: len % (dc + 1) == 0 with step 1).
-// Dynamic LDS: n_slots histograms of 256 bins, then cache_keys keys.
+// Dynamic LDS: n_slots histograms of 256 bins, then cache_keys keys (the
+// segment as it is, nodata included: no compaction, skipped on every pass).
+template <int kU>
 __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float *__restrict__ vals,
                                                                     const int64_t *__restrict__ mask_off,
                                                                     const int32_t *__restrict__ count,
@@ -161,8 +176,14 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   __shared__ int32_t s_rank[kMaxRanks];    // the distinct ranks, ascending
   __shared__ int32_t s_slot[kMaxRanks];    // rank r -> histogram slot (distinct prefix)
   __shared__ uint32_t s_spref[kMaxRanks];  // slot -> prefix (ascending)
-  __shared__ uint32_t red[12];
-  __shared__ int32_t s_nr, s_ns, s_nc;
+  __shared__ int32_t s_bkt[kMaxRanks];    // rank r: its bucket of the first pass
+  __shared__ uint32_t s_bcnt[kMaxRanks];   // rank r: the keys in that bucket
+  __shared__ int32_t s_soff[kMaxRanks];    // slot -> first candidate
+  __shared__ uint32_t s_fill[kMaxRanks];   // slot -> candidates written
+  __shared__ int8_t s_map[kBins];          // bucket -> slot, -1 when no rank needs it
+  __shared__ uint32_t red[3 * kSelWaves];
+  __shared__ uint32_t s_wsum[kSelWaves];
+  __shared__ int32_t s_nr, s_ns, s_fast;
   __shared__ float s_small[64];
 
   const int p = blockIdx.x / n_chunk, j = blockIdx.x % n_chunk;
@@ -177,14 +198,15 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   const int n = count[p];
   const float *buf = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)j * n;
   // pass 1: the non-nodata values (the reference's buf, drill.go:231-237):
-  // their count, the bits all their keys share, and the keys themselves in
+  // their count, the bits all their keys share, and the segment's keys in
   // LDS while they fit (order is irrelevant to order statistics)
-  if (tid == 0) s_nc = 0;
-  __syncthreads();
   const bool fits = n <= cache_keys;
+  // keys of the values `v != nodata` rejects (-0.0 == 0.0; a NaN nodata rejects nothing)
+  const bool skip_on = nodata == nodata;
+  const uint32_t kn1 = fkey(nodata), kn2 = nodata == 0.0f ? fkey(-nodata) : kn1;
+  auto skipk = [&](uint32_t k) { return skip_on && (k == kn1 || k == kn2); };
   uint32_t ka = 0xFFFFFFFFu, ko = 0u;
-  int valid = 0;
-  constexpr int kU = 8;   // values per thread in flight per round
+  int valid = 0;   // kU: values per thread in flight per round
   for (int i0 = 0; i0 < n; i0 += kSelThreads * kU) {
     float v[kU];
 #pragma unroll
@@ -198,13 +220,7 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
       const bool keep = i < n && v[u] != nodata;
       const uint32_t k = fkey(v[u]);
       if (keep) { ka &= k; ko |= k; valid++; }
-      if (fits) {
-        const unsigned long long bal = __ballot(keep);
-        int wbase = 0;
-        if ((tid & 63) == 0 && bal) wbase = atomicAdd(&s_nc, __popcll(bal));
-        wbase = __shfl(wbase, 0);
-        if (keep) cache[wbase + __popcll(bal & ((1ull << (tid & 63)) - 1ull))] = k;
-      }
+      if (fits && i < n) cache[i] = k;
     }
   }
   for (int sh = 32; sh > 0; sh >>= 1) {
@@ -212,23 +228,26 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     ko |= __shfl_xor(ko, sh);
     valid += __shfl_xor(valid, sh);
   }
-  if ((tid & 63) == 0) { red[tid >> 6] = ka; red[4 + (tid >> 6)] = ko; red[8 + (tid >> 6)] = (uint32_t)valid; }
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = ka; red[kSelWaves + (tid >> 6)] = ko; red[2 * kSelWaves + (tid >> 6)] = (uint32_t)valid;
+  }
   __syncthreads();
-  const uint32_t kand = red[0] & red[1] & red[2] & red[3];
-  const uint32_t kor = red[4] | red[5] | red[6] | red[7];
-  const int len = (int)(red[8] + red[9] + red[10] + red[11]);
+  uint32_t kand = 0xFFFFFFFFu, kor = 0u;
+  int len = 0;
+#pragma unroll
+  for (int w = 0; w < kSelWaves; w++) { kand &= red[w]; kor |= red[kSelWaves + w]; len += (int)red[2 * kSelWaves + w]; }
   if (len <= 0) {   // total > 0 implies a non-nodata value; keep the slot defined anyway
     for (int i = tid; i < dc; i += kSelThreads) dst[i] = 0.f;
     if (tid == 0) status[o] = 0;
     return;
   }
-  auto key_at = [&](int i) -> uint32_t { return cache[i]; };
   const int step = len / (dc + 1);
   if (step == 0) {   // len <= dc (<= 16): sort the few values, repeat them in order
     if (tid == 0) {
       int m = 0;
       if (fits) {
-        for (int i = 0; i < len; i++) s_small[m++] = fdecode(key_at(i));
+        for (int i = 0; i < n && m < len; i++)
+          if (!skipk(cache[i])) s_small[m++] = fdecode(cache[i]);
       } else {
         for (int i = 0; i < n && m < len; i++)
           if (buf[i] != nodata) s_small[m++] = buf[i];
@@ -271,6 +290,114 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     s_pref[tid] = pos >= 32 ? 0u : (kand >> pos);
     s_rem[tid] = (uint32_t)s_rank[tid];
   }
+  // every valid key once, from the LDS copy or streamed from the segment
+  auto for_keys = [&](auto &&f) {
+    if (fits) {
+      for (int i = tid; i < n; i += kSelThreads) {
+        const uint32_t k = cache[i];
+        if (!skipk(k)) f(k);
+      }
+    } else {
+      for (int i0 = 0; i0 < n; i0 += kSelThreads * kU) {
+        float v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          const int i = i0 + u * kSelThreads + tid;
+          v[u] = i < n ? buf[i] : nodata;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++)
+          if (i0 + u * kSelThreads + tid < n && v[u] != nodata) f(fkey(v[u]));
+      }
+    }
+  };
+  const int wv = tid >> 6, ln = tid & 63;
+  if (pos > 0) {
+    // first pass: the 11 bits below the shared ones, one histogram
+    const int bitsA = pos < kBinsLog ? pos : kBinsLog;
+    const int shA = pos - bitsA;
+    const uint32_t dmask = (1u << bitsA) - 1u;
+    uint32_t *H = dyn;
+    for (int i = tid; i < kBins; i += kSelThreads) { H[i] = 0u; s_map[i] = -1; }
+    __syncthreads();
+    for_keys([&](uint32_t k) { atomicAdd(&H[(k >> shA) & dmask], 1u); });
+    __syncthreads();
+    {   // inclusive scan of the buckets in place, 4 per thread
+      const int b4 = 4 * tid;
+      const uint32_t h0 = H[b4], h1 = H[b4 + 1], h2 = H[b4 + 2], h3 = H[b4 + 3];
+      const uint32_t sum = h0 + h1 + h2 + h3;
+      uint32_t incl = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t up = __shfl_up(incl, o);
+        if (ln >= o) incl += up;
+      }
+      if (ln == 63) s_wsum[wv] = incl;
+      __syncthreads();
+      uint32_t base = 0;
+      for (int w = 0; w < wv; w++) base += s_wsum[w];
+      const uint32_t ex = base + incl - sum;
+      H[b4] = ex + h0; H[b4 + 1] = ex + h0 + h1; H[b4 + 2] = ex + h0 + h1 + h2; H[b4 + 3] = ex + sum;
+    }
+    __syncthreads();
+    if (tid < nr) {   // the bucket of rank r: the first whose cumulative count exceeds r
+      const uint32_t r = (uint32_t)s_rank[tid];
+      int lo = 0, hi = (int)dmask;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (H[mid] > r) hi = mid; else lo = mid + 1;
+      }
+      const uint32_t before = lo ? H[lo - 1] : 0u;
+      s_bkt[tid] = lo;
+      s_rem[tid] = r - before;
+      s_bcnt[tid] = H[lo] - before;
+    }
+    __syncthreads();
+    if (tid == 0) {   // distinct buckets (ascending with the ranks) -> slots
+      int ns = 0, off = 0, fast = 1;
+      for (int r = 0; r < nr; r++) {
+        if (ns == 0 || s_spref[ns - 1] != (uint32_t)s_bkt[r]) {
+          s_spref[ns] = (uint32_t)s_bkt[r];
+          s_soff[ns] = off;
+          off += (int)s_bcnt[r];
+          if (s_bcnt[r] > (uint32_t)kCandMax) fast = 0;
+          ns++;
+        }
+        s_slot[r] = ns - 1;
+      }
+      s_ns = ns;
+      s_fast = fast;
+    }
+    __syncthreads();
+    if (s_fast) {
+      // the keys of the needed buckets, compacted per slot over the histogram
+      if (tid < s_ns) { s_map[s_spref[tid]] = (int8_t)tid; s_fill[tid] = 0u; }
+      __syncthreads();
+      uint32_t *cand = dyn;
+      for_keys([&](uint32_t k) {
+        const int sl = s_map[(k >> shA) & dmask];
+        if (sl >= 0) cand[s_soff[sl] + atomicAdd(&s_fill[sl], 1u)] = k;
+      });
+      __syncthreads();
+      // rank r is the s_rem[r]-th key of its bucket: lane i counts the keys
+      // ordered before its own (ties by position)
+      for (int r = wv; r < nr; r += kSelWaves) {
+        const int cnt = (int)s_bcnt[r];
+        const uint32_t *c = cand + s_soff[s_slot[r]];
+        const uint32_t ki = ln < cnt ? c[ln] : 0xFFFFFFFFu;
+        int less = 0;
+        for (int j = 0; j < cnt; j++) {
+          const uint32_t kj = c[j];
+          less += (kj < ki || (kj == ki && j < ln)) ? 1 : 0;
+        }
+        if (ln < cnt && less == (int)s_rem[r]) s_pref[r] = ki;
+      }
+      __syncthreads();
+      pos = 0;
+    } else {   // continue below the bucket digit by radix selection
+      if (tid < nr) s_pref[tid] = ((pos >= 32 ? 0u : (kand >> pos)) << bitsA) | (uint32_t)s_bkt[tid];
+      pos = shA;
+    }
+  }
   __syncthreads();
   while (pos > 0) {
     const int d = pos < 8 ? pos : 8;
@@ -285,40 +412,28 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     }
     __syncthreads();
     const int ns = s_ns;
-    for (int i = tid; i < ns * 256; i += kSelThreads) hist[i >> 8][i & 255] = 0u;
-    __syncthreads();
-    auto bin = [&](uint32_t k) {
-      const uint32_t hi = pos >= 32 ? 0u : (k >> pos);
-      int lo = 0, hi_s = ns - 1;   // binary search of the slot with prefix hi
-      while (lo < hi_s) {
-        const int mid = (lo + hi_s) >> 1;
-        if (s_spref[mid] < hi) lo = mid + 1; else hi_s = mid;
-      }
-      if (s_spref[lo] == hi) atomicAdd(&hist[lo][(k >> shift) & ((1u << d) - 1u)], 1u);
-    };
-    if (fits) {
-      for (int i = tid; i < len; i += kSelThreads) bin(key_at(i));
-    } else {   // streamed again from the segment, kU values per thread in flight
-      for (int i0 = 0; i0 < n; i0 += kSelThreads * kU) {
-        float v[kU];
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-          const int i = i0 + u * kSelThreads + tid;
-          v[u] = i < n ? buf[i] : nodata;
+    // kHistSlots prefixes per pass over the keys
+    for (int g0 = 0; g0 < ns; g0 += kHistSlots) {
+      const int g1 = min(ns, g0 + kHistSlots);
+      for (int i = tid; i < (g1 - g0) * 256; i += kSelThreads) hist[i >> 8][i & 255] = 0u;
+      __syncthreads();
+      auto bin = [&](uint32_t k) {
+        const uint32_t hi = pos >= 32 ? 0u : (k >> pos);
+        int lo = 0, hi_s = ns - 1;   // binary search of the slot with prefix hi
+        while (lo < hi_s) {
+          const int mid = (lo + hi_s) >> 1;
+          if (s_spref[mid] < hi) lo = mid + 1; else hi_s = mid;
         }
-#pragma unroll
-        for (int u = 0; u < kU; u++)
-          if (i0 + u * kSelThreads + tid < n && v[u] != nodata) bin(fkey(v[u]));
-      }
-    }
-    __syncthreads();
-    // the digit bucket holding each rank: a wave per rank, lane l sums bins
-    // 4l..4l+3, an inclusive scan over the lanes finds the lane whose range
-    // holds the rank, that lane walks its 4 bins (bins >= 2^d are empty)
-    {
-      const int wv = tid >> 6, ln = tid & 63;
-      for (int r = wv; r < nr; r += kSelThreads / 64) {
-        const uint32_t *h = hist[s_slot[r]];
+        if (s_spref[lo] == hi && lo >= g0 && lo < g1) atomicAdd(&hist[lo - g0][(k >> shift) & ((1u << d) - 1u)], 1u);
+      };
+      for_keys(bin);
+      __syncthreads();
+      // the digit bucket holding each rank: a wave per rank, lane l sums bins
+      // 4l..4l+3, an inclusive scan over the lanes finds the lane whose range
+      // holds the rank, that lane walks its 4 bins (bins >= 2^d are empty)
+      for (int r = wv; r < nr; r += kSelWaves) {
+        if (s_slot[r] < g0 || s_slot[r] >= g1) continue;
+        const uint32_t *h = hist[s_slot[r] - g0];
         const uint32_t rem = s_rem[r];
         const uint32_t b0 = h[4 * ln], b1 = h[4 * ln + 1], b2 = h[4 * ln + 2], b3 = h[4 * ln + 3];
         const uint32_t sum = b0 + b1 + b2 + b3;
@@ -338,8 +453,8 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
           s_rem[r] = rem - cum;
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
     pos = shift;
   }
   // s_pref[r] is now the key of order statistic s_rank[r]
@@ -405,9 +520,14 @@ int launch_drill_deciles(const DecileCall &c) {
                      c.xsize, c.ysize, w.idx, w.count);
   hipLaunchKernelGGL(decile_chunk_scan_kernel, dim3(1), dim3(1024), 0, s, w.count, c.n_polys, w.chunk_base);
   const int64_t max_chunks = c.mask_bytes / kDecChunk + c.n_polys;   // >= sum of ceil(count / 64)
-  const int n_slots = std::min(kMaxRanks, 2 * c.decile_count);
-  const int cache_keys = (kSelLds - n_slots * 256 * 4) / 4;
-  const size_t dyn_lds = (size_t)kSelLds;
+  const int n_slots = kHistSlots;
+  int sel_lds = kSelLds, sel_u = kSelU;
+#ifdef GSKYHIP_AB
+  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(12, std::min(60, atoi(e))) * 1024;
+  if (const char *e = getenv("GSKYHIP_DEC_U")) sel_u = atoi(e);
+#endif
+  const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
+  const size_t dyn_lds = (size_t)sel_lds;
   for (int b0 = 0; b0 < n_list; b0 += c.band_chunk) {
     const int n_chunk = std::min(c.band_chunk, n_list - b0);
     const int n_groups = (n_chunk + 63) / 64;
@@ -418,9 +538,14 @@ int launch_drill_deciles(const DecileCall &c) {
     hipLaunchKernelGGL(decile_transpose_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, c.stack,
                        c.t_stride, w.idx, c.mask_off, w.count, w.chunk_base, c.n_polys, w.tsel, n_chunk, n_groups,
                        w.vals);
-    hipLaunchKernelGGL(decile_select_kernel, dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
-                       c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots, cache_keys, c.out,
-                       c.status);
+    if (sel_u == 8)
+      hipLaunchKernelGGL(decile_select_kernel<8>, dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
+                         c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
+                         cache_keys, c.out, c.status);
+    else
+      hipLaunchKernelGGL(decile_select_kernel<kSelU>, dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
+                         c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
+                         cache_keys, c.out, c.status);
   }
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }

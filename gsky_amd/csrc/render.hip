@@ -1225,6 +1225,15 @@ __global__ __launch_bounds__(256) void plan_exact_kernel(PlanArgs a) {
 __global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
   __shared__ TileLds L[4];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+#ifdef GSKYHIP_AB
+  // phase time stamps (GSKYHIP_PLAN_STAMPS): 100 MHz wall clock into counters[40 + i]
+  uint64_t st[8];
+  int ns = 0;
+  auto stamp = [&]() { if (ns < 8) st[ns++] = wall_clock64(); };
+#else
+  auto stamp = [&]() {};
+#endif
+  stamp();
   if (a.small == 2) {   // the pairs too (one or two): the whole plan is this one launch
     __shared__ double sx[kGrid], sy[kGrid];
     __shared__ int sok[kGrid];
@@ -1234,24 +1243,35 @@ __global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
       __syncthreads();
     }
   }
+  stamp();
   if (tid < 64) a.counters[tid] = 0;
   __syncthreads();
   for (int t = wave; t < a.n_tiles; t += 4) plan_tile_wave(a, t, lane, L[wave]);
   __syncthreads();
+  stamp();
   if (a.sep)
     for (int64_t g = tid; g < 3 * (int64_t)a.n_pairs; g += 256) plan_col(a, g);
   __syncthreads();
+  stamp();
   for (int64_t i = tid; i < (int64_t)a.n_pairs * a.max_h; i += 256) {
     const int p = (int)(i / a.max_h), row = (int)(i % a.max_h);
     const PairPlan &pp = a.pairs[p];
     if (row < pp.h) plan_row(a, p, pp, a.xforms[p], row);
   }
   __syncthreads();
+  stamp();
   const int nsplit = a.counters[1];
   for (int k = tid; k < nsplit; k += 256) plan_split_one(a, k);
   __syncthreads();
+  stamp();
   const int used = min(a.counters[0], a.pool_cap);
   for (int k = tid; k < used; k += 256) plan_exact_one(a, k);
+  __syncthreads();
+  stamp();
+#ifdef GSKYHIP_AB
+  if (tid == 0)
+    for (int i = 1; i < ns; i++) a.counters[40 + i] = (int32_t)(st[i] - st[i - 1]);
+#endif
 }
 
 }  // namespace gsky
@@ -1524,6 +1544,15 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   if (small) {
     if (a.small == 1) hipLaunchKernelGGL(plan_pairs_kernel<256>, dim3(rc.n_pairs), dim3(256), 0, s, a);
     hipLaunchKernelGGL(plan_small_kernel, dim3(1), dim3(256), 0, s, a);
+#ifdef GSKYHIP_AB
+    if (getenv("GSKYHIP_PLAN_STAMPS")) {   // phase times of plan_small_kernel, 10 ns ticks
+      int32_t st[8] = {0};
+      hipStreamSynchronize(s);
+      hipMemcpy(st, a.counters + 40, sizeof(st), hipMemcpyDeviceToHost);
+      fprintf(stderr, "plan_small_stamps_us pairs=%.2f tiles=%.2f cols=%.2f rows=%.2f split=%.2f exact=%.2f\n",
+              st[1] * 0.01, st[2] * 0.01, st[3] * 0.01, st[4] * 0.01, st[5] * 0.01, st[6] * 0.01);
+    }
+#endif
     return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
   }
   bool ge_on = true;   // per-granule edge table; false = per-pair edge transforms

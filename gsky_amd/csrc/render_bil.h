@@ -124,7 +124,9 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
         for (int kk = 0; kk < 4; kk++) {
           const WT w = wx[kk & 1] * wy[kk >> 1];
           const double d = (double)tv[kk];
-          const bool use = ((valid >> kk) & 1u) && !(hnd && (d == nd64 || (nd_nan && d != d)));
+          // bitwise, not short-circuit: no per-pixel exec-mask branches
+          const bool isnd = (d == nd64) | (nd_nan & (d != d));
+          const bool use = (((valid >> kk) & 1u) != 0u) & !(hnd & isnd);
           accDiv += use ? w : (WT)0.0;
           accR += use ? (WT)d * w : (WT)0.0;
         }
@@ -137,22 +139,88 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
         const bool take = ((unsigned)ic < (unsigned)lim) & (v != nd) & (!fill_mode | (c[q] == nd));
         c[q] = take ? v : c[q];
       };
+      // the nodata test of a tap in float32 (exact: the band's nodata is a float32 value or NaN)
+      const bool nd_f32 = !hnd || nd_nan || (double)(float)nd64 == nd64;
+      const float ndf = (float)nd64;
       if (kind == ROW_LINEAR) {   // HP pixels' taps in flight
         const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
 #pragma unroll
         for (int h = 0; h < kNnPx; h += HP) {
+          int ixv[HP], iyv[HP];
           WT rx[HP], ry[HP];
-          uint32_t valid[HP];
-          u32x2 t0[HP], t1[HP];
+          bool allin = true;
 #pragma unroll
           for (int q = 0; q < HP; q++) {
             const int ic = ic0 + 64 * (h + q);
             const double dist = (double)ic;
-            prep(h + q, xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, rx[q], ry[q], valid[q],
-                 t0[q], t1[q]);
+            const double sx = xs0 + dX * dist, sy = ys0 + dY * dist;
+            ixv[q] = (int)floor(sx - 0.5);
+            iyv[q] = (int)floor(sy - 0.5);
+            rx[q] = (WT)(1.5 - (sx - (double)ixv[q]));
+            ry[q] = (WT)(1.5 - (sy - (double)iyv[q]));
+            allin = allin & (((unsigned)ic >= (unsigned)lim) |
+                             (((unsigned)ixv[q] < (unsigned)(bx - 1)) & ((unsigned)iyv[q] < (unsigned)(by - 1))));
           }
+          if (nd_f32 && __all(allin)) {
+            // every sampled pixel of the wave has its 2x2 taps inside the band:
+            // no -1 edge rule, no tap outside; the weights of four valid taps
+            // sum to 1 within fp32 rounding, so the sample is accR unless a
+            // tap holds nodata (then the general renormalisation)
+            u32x2 t0[HP], t1[HP];
 #pragma unroll
-          for (int q = 0; q < HP; q++) finish(h + q, rx[q], ry[q], valid[q], t0[q], t1[q]);
+            for (int q = 0; q < HP; q++) {
+              const int ic = ic0 + 64 * (h + q);
+              const bool ok = (unsigned)ic < (unsigned)lim;
+              const uint32_t o0 = ok ? (uint32_t)(iyv[q] * bx + ixv[q]) * 4u : 0x80000000u;
+              const uint32_t o1 = ok ? o0 + (uint32_t)bx * 4u : 0x80000000u;
+              t0[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, o0, 0, 0);
+              t1[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < HP; q++) {
+              const float tv[4] = {__uint_as_float(t0[q].x), __uint_as_float(t0[q].y), __uint_as_float(t1[q].x),
+                                   __uint_as_float(t1[q].y)};
+              const WT one = (WT)1.0;
+              const WT wx[2] = {rx[q], one - rx[q]}, wy[2] = {ry[q], one - ry[q]};
+              WT accR = (WT)0.0;
+              bool anynd = false;
+#pragma unroll
+              for (int kk = 0; kk < 4; kk++) {
+                accR += (WT)tv[kk] * (wx[kk & 1] * wy[kk >> 1]);
+                anynd = anynd | (nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+              }
+              anynd = anynd & hnd;
+              float v = (float)accR;
+              if (anynd) {   // drop the nodata taps and renormalise (bil_sample's rule)
+                WT aR = (WT)0.0, aD = (WT)0.0;
+#pragma unroll
+                for (int kk = 0; kk < 4; kk++) {
+                  const WT w = wx[kk & 1] * wy[kk >> 1];
+                  const bool use = !(nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+                  aD += use ? w : (WT)0.0;
+                  aR += use ? (WT)tv[kk] * w : (WT)0.0;
+                }
+                v = fillv;
+                if (aD == (WT)1.0) v = (float)aR;
+                else if (aD >= (WT)0.00001) v = (float)(aR / aD);
+              }
+              const int ic = ic0 + 64 * (h + q);
+              const bool take = ((unsigned)ic < (unsigned)lim) & (v != nd) & (!fill_mode | (c[h + q] == nd));
+              c[h + q] = take ? v : c[h + q];
+            }
+          } else {   // the reference's per-tap rules (coordinates recomputed)
+            uint32_t valid[HP];
+            u32x2 t0[HP], t1[HP];
+#pragma unroll
+            for (int q = 0; q < HP; q++) {
+              const int ic = ic0 + 64 * (h + q);
+              const double dist = (double)ic;
+              prep(h + q, xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, rx[q], ry[q], valid[q],
+                   t0[q], t1[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < HP; q++) finish(h + q, rx[q], ry[q], valid[q], t0[q], t1[q]);
+          }
         }
       } else {   // POOL: linear leaves, per-pixel exact points, failed pixels; one pixel at a time
 #pragma unroll

@@ -445,10 +445,11 @@ __global__ __launch_bounds__(256) void render_auto_kernel(RenderArgs a) {
 template <int NOUT, int RES, bool MASK>
 __global__ __launch_bounds__(256) void render_general_kernel(RenderArgs a) {
   __shared__ uint32_t s_ramp[256];
-  if (a.ramp) s_ramp[threadIdx.x] = a.ramp[threadIdx.x];
-  __syncthreads();
   const int bands_per_tile = (a.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const int items = a.counters[2] * bands_per_tile;
+  if ((int)blockIdx.x >= items) return;   // no complex tile for this block (the common case)
+  if (a.ramp) s_ramp[threadIdx.x] = a.ramp[threadIdx.x];
+  __syncthreads();
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
     const int t = a.complex_list[it / bands_per_tile];
     render_band<NOUT, RES, MASK, true>(a, t, (it % bands_per_tile) * a.rows_per_block, s_ramp);
@@ -464,7 +465,11 @@ static void launch_render_kernels(const RenderArgs &a, dim3 grid, bool general_o
       hipLaunchKernelGGL((render_fast_kernel<NOUT, RES, MASK>), grid, dim3(256), 0, s, a, a.entries, a.order,
                          a.rows, a.pool, a.tplans, a.tiles);
   }
-  hipLaunchKernelGGL((render_general_kernel<NOUT, RES, MASK>), dim3(512), dim3(256), 0, s, a);
+  // a grid no larger than the batch's (tile, band) items: small requests (C1)
+  // dispatch a few blocks, not 512
+  const int bpt = (a.max_h + a.rows_per_block - 1) / a.rows_per_block;
+  const int gen_grid = (int)std::max<int64_t>(1, std::min<int64_t>(512, (int64_t)a.n_tiles * bpt));
+  hipLaunchKernelGGL((render_general_kernel<NOUT, RES, MASK>), dim3(gen_grid), dim3(256), 0, s, a);
 }
 
 template <int NOUT>

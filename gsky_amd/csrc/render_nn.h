@@ -73,11 +73,11 @@ __device__ __forceinline__ uint32_t scale_int(const ScaleK &k, int32_t c) {
 // One stack entry e of the ordered fold of tile row r (MergeMaskedRaster,
 // tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
 // (tile column xl + 64 q).
-template <typename T, bool MASK>
+template <typename T, bool MASK, int NPX = kNnPx>
 __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
                                              const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
                                              int ns_out, int r, int xb, int xl, int W, int ncols,
-                                             typename VOf<T>::type (&c)[kNnPx]) {
+                                             typename VOf<T>::type (&c)[NPX]) {
   using V = typename VOf<T>::type;
   const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
   if (e.ns != ns_out || ew <= 0) return;
@@ -100,23 +100,23 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
     // fast body: every pixel of the block is in the window and its source
     // pixel in the band -- lin_coords() + nn_px() reduce to the truncations
     const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
-    uint32_t off[kNnPx];
+    uint32_t off[NPX];
 #pragma unroll
-    for (int q = 0; q < kNnPx; q++) {
+    for (int q = 0; q < NPX; q++) {
       const double dist = (double)(ic0 + 64 * q);
       const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
       const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
       off[q] = (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T);
     }
-    V vv[kNnPx];
+    V vv[NPX];
 #pragma unroll
-    for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
+    for (int q = 0; q < NPX; q++) vv[q] = buf_load<T>(rs, off[q]);
     if (!fill_mode) {
 #pragma unroll
-      for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
+      for (int q = 0; q < NPX; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
     } else {
 #pragma unroll
-      for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
+      for (int q = 0; q < NPX; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
     }
     return;
   }
@@ -125,7 +125,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   // of the fast body
   const V fillv = as_v<T>(e.fill);
 #pragma unroll
-  for (int h = 0; h < kNnPx; h += 4) {
+  for (int h = 0; h < NPX; h += 4) {
     uint32_t idx[4];
     if (kind == ROW_LINEAR) {
       const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
@@ -179,20 +179,20 @@ __device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *_
 
 // utils.Scale + palette / grey of the lane's 8 canvas values (EncodePNG's
 // pixel loop through the LDS table s_tab).
-template <typename T>
+template <typename T, int NPX = kNnPx>
 __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint32_t *s_tab,
-                                        const typename VOf<T>::type (&c)[kNnPx], uint32_t (&px)[kNnPx]) {
+                                        const typename VOf<T>::type (&c)[NPX], uint32_t (&px)[NPX]) {
   if constexpr (!std::is_same<T, float>::value) {
     if (safe) {
 #pragma unroll
-      for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_int<T, true>(sk, c[q])];
+      for (int q = 0; q < NPX; q++) px[q] = s_tab[scale_int<T, true>(sk, c[q])];
     } else {
 #pragma unroll
-      for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_int<T, false>(sk, c[q])];
+      for (int q = 0; q < NPX; q++) px[q] = s_tab[scale_int<T, false>(sk, c[q])];
     }
   } else {
 #pragma unroll
-    for (int q = 0; q < kNnPx; q++) px[q] = s_tab[scale_t<T>(sk, c[q]) & 0xFFu];
+    for (int q = 0; q < NPX; q++) px[q] = s_tab[scale_t<T>(sk, c[q]) & 0xFFu];
   }
 }
 
@@ -394,6 +394,9 @@ void launch_nn_v(const RenderArgs &a, hipStream_t s) {
                      a.order, a.rows, a.pool, a.tplans, a.tiles, items);
 }
 
+// render_nn_stage.h (included by the per-type translation units)
+template <typename T> void launch_nn_stage(const RenderArgs &a, hipStream_t s);
+
 // NN band kernel launch for value type T (RGBA or typed canvas, with or
 // without a mask layer).
 template <typename T>
@@ -408,9 +411,11 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   // single-entry tiles through the prefetching path (C2: 1.445 vs 1.470 ms,
   // profiles/r03f_ab_c2.jsonl)
   bool one = true;
+  bool staged = false;   // large RGBA batches through the LDS-staged kernel (render_nn_stage.h)
 #ifdef GSKYHIP_AB
   if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
   if (const char *on = getenv("GSKYHIP_NN_ONE")) one = atoi(on) != 0;
+  if (const char *sg = getenv("GSKYHIP_NN_STAGED")) staged = atoi(sg) != 0;
   if (const char *st = getenv("GSKYHIP_NN_STAGE")) {
     if (!mask && !canvas && rpw8 && atoi(st) == 1) {
       if (one) launch_nn_v<T, false, false, 8, true, true>(a, s);
@@ -432,6 +437,8 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
     else launch_nn_v<T, true, false, 4>(a, s);
   } else if (canvas) {
     launch_nn_v<T, false, true, 4>(a, s);
+  } else if (rpw8 && staged) {
+    launch_nn_stage<T>(a, s);
   } else if (rpw8) {
     if (one) launch_nn_v<T, false, false, 8, true>(a, s);
     else launch_nn_v<T, false, false, 8>(a, s);

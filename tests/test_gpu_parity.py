@@ -496,13 +496,18 @@ def test_drill_deciles_parity(gpu, oracle, dcount, pc, clip):
 def test_drill_deciles_large_polygon(gpu, oracle, side):
     """Segments past the select workgroup's LDS key cache (~10k keys for 9
     deciles): a 150 x 150 in-mask window streams its values from the segment
-    on every radix pass, a 100 x 100 one selects from LDS; both equal to the
-    oracle for every band, nodata values (-9999 at 1 %) skipped."""
+    on every pass, a 100 x 100 one selects from LDS; both equal to the oracle
+    for every band, nodata values (-9999 at 1 %) skipped.  Bands 0/1/3 take
+    the bucket + counting-compare path (band 3: both signs, no shared key
+    bits); bands 2 and 4 (a handful of distinct values) overflow the 64-key
+    buckets and finish by radix selection."""
     import torch
 
     from gsky_amd import drill
     rng = np.random.default_rng(side)
     data = rng.uniform(0.0, 0.05, size=(5, 160, 160)).astype(np.float32)
+    data[3] = rng.normal(size=(160, 160)) * 1000.0          # both signs, every exponent: no shared key bits
+    data[4] = rng.choice(np.array([-1.0, 0.0, 2.5, 7.0], np.float32), size=(160, 160))   # 4 values: huge buckets
     data[rng.uniform(size=data.shape) < 0.01] = -9999.0
     data[2] = np.round(data[2] * 100) / 100   # many equal values: ties across the ranks
     st = drill.DrillStack(torch.from_numpy(data), -9999.0, gpu)
