@@ -107,10 +107,14 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One wave per (64-pixel chunk ch, group g of 64 bands of the pass); four
+// One wave per (64-pixel chunk ch, group g of 32 bands of the pass); four
 // independent waves per workgroup.  Band j of polygon p: vals[seg0 + j *
 // count[p] + k] for its pixel k, seg0 = mask_off[p] * n_chunk (the compacted
-// pixel list of p holds count[p] <= its window bytes).
+// pixel list of p holds count[p] <= its window bytes).  A load instruction
+// reads the 32 bands (128 contiguous bytes) of two pixels, a store
+// instruction writes one band of the 64 pixels (256 contiguous bytes); the
+// wave's 64 x 32 tile (8.4 KB of LDS) keeps 16 waves per CU.
+constexpr int kTrBands = 32;
 __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__restrict__ stack, int t_stride,
                                                                const int32_t *__restrict__ idx,
                                                                const int64_t *__restrict__ mask_off,
@@ -118,7 +122,8 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
                                                                const int32_t *__restrict__ chunk_base, int n_polys,
                                                                const int32_t *__restrict__ tsel, int n_chunk,
                                                                int n_groups, float *__restrict__ vals) {
-  __shared__ float tile[4][64 * kTilePad];
+  constexpr int kPad = kTrBands + 1;
+  __shared__ float tile[4][64 * kPad];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t item = (int64_t)blockIdx.x * 4 + wave;
   const int ch = (int)(item / n_groups), g = (int)(item % n_groups);
@@ -132,26 +137,30 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
   const int n = count[p];
   const int k0 = (ch - chunk_base[p]) * kDecChunk;
   const int m = min(kDecChunk, n - k0);
-  const int nb = min(64, n_chunk - g * 64);   // bands of this group
+  const int nb = min(kTrBands, n_chunk - g * kTrBands);   // bands of this group
+  const int bl = lane & (kTrBands - 1), half = lane / kTrBands;
   // every lane loads from a valid address (band 0 of the group, pixel 0 of
-  // the chunk) so the loads of a group are unconditional and all in flight
-  const float *base = stack + tsel[g * 64 + (lane < nb ? lane : 0)];
+  // the chunk) so the loads are unconditional and all in flight
+  const float *base = stack + tsel[g * kTrBands + (bl < nb ? bl : 0)];
   const int32_t my_px = idx[mask_off[p] + k0 + (lane < m ? lane : 0)];
   float *T = tile[wave];
-  for (int kb = 0; kb < m; kb += 16) {
+  for (int kb = 0; kb < m; kb += 32) {
     float v[16];
 #pragma unroll
-    for (int u = 0; u < 16; u++) {   // pixel kb + u: its bands, one per lane (256 contiguous bytes)
-      const int px = __builtin_amdgcn_readlane(my_px, kb + u);
-      v[u] = base[(int64_t)px * t_stride];
+    for (int u = 0; u < 16; u++) {   // pixels kb + 2u (lanes 0-31) and kb + 2u + 1 (lanes 32-63)
+      const int k = kb + 2 * u + half;
+      const int px0 = __builtin_amdgcn_readlane(my_px, min(kb + 2 * u, 63));
+      const int px1 = __builtin_amdgcn_readlane(my_px, min(kb + 2 * u + 1, 63));
+      v[u] = base[(int64_t)(half ? px1 : px0) * t_stride];
+      (void)k;
     }
 #pragma unroll
-    for (int u = 0; u < 16; u++) T[(kb + u) * kTilePad + lane] = v[u];
+    for (int u = 0; u < 16; u++) T[(kb + 2 * u + half) * kPad + bl] = v[u];
   }
   wave_lds_sync();
-  float *seg = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)(g * 64) * n + k0;
+  float *seg = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)(g * kTrBands) * n + k0;
   if (lane < m) {
-    for (int j = 0; j < nb; j++) seg[(int64_t)j * n + lane] = T[lane * kTilePad + j];   // lane = pixel
+    for (int j = 0; j < nb; j++) seg[(int64_t)j * n + lane] = T[lane * kPad + j];   // lane = pixel
   }
 }
 
@@ -530,7 +539,7 @@ int launch_drill_deciles(const DecileCall &c) {
   const size_t dyn_lds = (size_t)sel_lds;
   for (int b0 = 0; b0 < n_list; b0 += c.band_chunk) {
     const int n_chunk = std::min(c.band_chunk, n_list - b0);
-    const int n_groups = (n_chunk + 63) / 64;
+    const int n_groups = (n_chunk + kTrBands - 1) / kTrBands;
     const int64_t n_seg = (int64_t)c.n_polys * n_chunk;
     if (hipMemcpyAsync(w.tsel, sel.data() + b0, sizeof(int32_t) * n_chunk, hipMemcpyHostToDevice, s) != hipSuccess)
       return GSKYHIP_E_HIP;

@@ -347,6 +347,9 @@ __device__ int suggested_warp_output2(const Xform &t, int nInX, int nInY, int la
 
 // One border-test sample j of GDALSuggestedWarpOutput2_MustAdjustFor{Right,
 // Bottom}Border: the per-lane expressions of must_adjust().
+// INL: the transforms inlined (workgroup planning of small batches, where a
+// call's register save / restore through scratch sits on the latency path).
+template <bool INL = false>
 __device__ bool border_bad(const Xform &t, const double *ext, int np, int nl, double psx, double psy, bool right,
                            int j) {
   double r1 = 0.0, r2 = 0.0;
@@ -358,12 +361,26 @@ __device__ bool border_bad(const Xform &t, const double *ext, int np, int nl, do
   double ax, ay;
   if (right) { ax = ext[2]; ay = ext[3] - psy * r1 * nl; }
   else { ax = ext[0] + psx * r1 * np; ay = ext[1]; }
-  const bool ok1 = xform_point_nl(t, true, ax, ay);
-  const bool ok2 = ok1 ? xform_point_nl(t, false, ax, ay) : false;
+  bool ok1, ok2;
+  if constexpr (INL) {
+    ok1 = xform_point(t, true, ax, ay);
+    ok2 = ok1 ? xform_point(t, false, ax, ay) : false;
+  } else {
+    ok1 = xform_point_nl(t, true, ax, ay);
+    ok2 = ok1 ? xform_point_nl(t, false, ax, ay) : false;
+  }
   const double ex = right ? ext[2] : ext[0] + psx * r2 * np;
   const double ey = right ? ext[3] - psy * r2 * nl : ext[1];
   return !ok1 || !ok2 || fabs(ax - ex) > psx || fabs(ay - ey) > psy;
 }
+
+#ifdef GSKYHIP_AB
+// phase stamps of plan_pair<256> inside plan_small_kernel (GSKYHIP_PLAN_STAMPS)
+__device__ __forceinline__ void pstamp(uint64_t *ps, int i) { if (ps && threadIdx.x == 0) ps[i] = wall_clock64(); }
+#define PSTAMP(ps, i) pstamp(ps, i)
+#else
+#define PSTAMP(ps, i) ((void)0)
+#endif
 
 // suggested_warp_output2() by a workgroup of NT threads (small batches, where
 // the planning chain is latency-bound): the 21 x 21 grid in kGrid / NT rounds
@@ -375,7 +392,7 @@ __device__ bool border_bad(const Xform &t, const double *ext, int np, int nl, do
 template <int NT>
 __device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, double *sx, double *sy, int *sok,
                                           double ext[4], double &psx, double &psy, int &nPixels, int &nLines,
-                                          const GEdge *ge) {
+                                          const GEdge *ge, uint64_t *stp = nullptr) {
   constexpr int kW = NT / 64;
   __shared__ double s_red[4][kW];
   __shared__ int s_cnt[8];
@@ -398,10 +415,11 @@ __device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, do
     else if (e == 1) { x = r * nInX; y = nInY; }
     else if (e == 2) { x = 0.0; y = r * nInY; }
     else { x = nInX; y = r * nInY; }
-    const int ok = xform_point_nl(t, false, x, y);
+    const int ok = xform_point(t, false, x, y);
     sx[k] = x; sy[k] = y; sok[k] = ok;
   }
   __syncthreads();
+  PSTAMP(stp, 2);
   int failed = 0;
   for (int k = tid; k < ns; k += NT) failed |= sok[k] ? 0 : 1;
   if (__syncthreads_or(failed)) {   // full grid of the source raster
@@ -411,7 +429,7 @@ __device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, do
       const double ry = (iy == kSteps) ? 1.0 : iy * dfStep;
       const double rx = (ix == kSteps) ? 1.0 : ix * dfStep;
       double x = rx * nInX, y = ry * nInY;
-      const int ok = xform_point_nl(t, false, x, y);
+      const int ok = xform_point(t, false, x, y);
       sx[k] = x; sy[k] = y; sok[k] = ok;
     }
     __syncthreads();
@@ -452,6 +470,7 @@ __device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, do
   // pass A: right trials 0..4 (tests 0..4), bottom trial 0 under right trial 0 (test 5)
   if (tid < 8) s_cnt[tid] = 0;
   __syncthreads();
+  PSTAMP(stp, 3);
   const double tryx0 = psx - psx * ratios[0] / nPixels;
   const double tryy0 = psy - psy * ratios[0] / nLines;
   if (tid < 6 * 21) {
@@ -460,14 +479,15 @@ __device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, do
     if (id < 5) {
       const double tryx = psx - psx * ratios[id] / nPixels;
       const double e[4] = {mnx, mxy - nLines * psy, mnx + nPixels * tryx, mxy};
-      bad = border_bad(t, e, nPixels, nLines, tryx, psy, true, j);
+      bad = border_bad<true>(t, e, nPixels, nLines, tryx, psy, true, j);
     } else {
       const double e[4] = {mnx, mxy - nLines * tryy0, mnx + nPixels * tryx0, mxy};
-      bad = border_bad(t, e, nPixels, nLines, tryx0, tryy0, false, j);
+      bad = border_bad<true>(t, e, nPixels, nLines, tryx0, tryy0, false, j);
     }
     if (bad) atomicAdd(&s_cnt[id], 1);
   }
   __syncthreads();
+  PSTAMP(stp, 4);
   int kx = -1;
   for (int k = 0; k < 5; k++)
     if (s_cnt[k] != 21) { kx = k; break; }
@@ -486,7 +506,7 @@ __device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, do
       const int k = ky0 + tid / 21, j = tid % 21;
       const double tryy = psy - psy * ratios[k] / nLines;
       const double e[4] = {mnx, mxy - nLines * tryy, mnx + nPixels * psx, mxy};
-      if (border_bad(t, e, nPixels, nLines, psx, tryy, false, j)) atomicAdd(&s_cnt[k], 1);
+      if (border_bad<true>(t, e, nPixels, nLines, psx, tryy, false, j)) atomicAdd(&s_cnt[k], 1);
     }
     __syncthreads();
     for (int k = ky0; k < 5; k++)
@@ -502,8 +522,10 @@ __device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, do
 // Plan of pair p by one workgroup of NT threads (sx / sy / sok: LDS scratch
 // of kGrid entries, ts: the transformer in LDS).
 template <int NT>
-__device__ void plan_pair(const PlanArgs &a, int p, double *sx, double *sy, int *sok, Xform &ts) {
+__device__ void plan_pair(const PlanArgs &a, int p, double *sx, double *sy, int *sok, Xform &ts,
+                          uint64_t *ps = nullptr) {
   const int lane = threadIdx.x;
+  PSTAMP(ps, 0);
   const int t_idx = a.small ? owning_tile(a.tiles, a.n_tiles, p) : a.pair_tile[p];
   if (t_idx < 0) {   // unreferenced pair: an empty plan nothing reads
     if (lane == 0) {
@@ -538,6 +560,7 @@ __device__ void plan_pair(const PlanArgs &a, int p, double *sx, double *sy, int 
     inv_geot(t.dst_gt, t.dst_igt);
   }
   __syncthreads();
+  PSTAMP(ps, 1);
 
   // ---- GDALSuggestedWarpOutput2 (warp.go:154)
   const int nInX = g.xsize, nInY = g.ysize;
@@ -549,7 +572,8 @@ __device__ void plan_pair(const PlanArgs &a, int p, double *sx, double *sy, int 
                                  a.gedge ? a.gedge + gi : nullptr);
   else
     err = suggested_warp_output2_blk<NT>(t, nInX, nInY, sx, sy, sok, ext, psx, psy, nPixels, nLines,
-                                         a.gedge ? a.gedge + gi : nullptr);
+                                         a.gedge ? a.gedge + gi : nullptr, ps);
+  PSTAMP(ps, 5);
   if (lane != 0) return;
 
   // ---- overview pick (warp.go:156-198)
@@ -1227,7 +1251,7 @@ __global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 #ifdef GSKYHIP_AB
   // phase time stamps (GSKYHIP_PLAN_STAMPS): 100 MHz wall clock into counters[40 + i]
-  uint64_t st[8];
+  uint64_t st[8], st_pair[6] = {0, 0, 0, 0, 0, 0};
   int ns = 0;
   auto stamp = [&]() { if (ns < 8) st[ns++] = wall_clock64(); };
 #else
@@ -1238,10 +1262,19 @@ __global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
     __shared__ double sx[kGrid], sy[kGrid];
     __shared__ int sok[kGrid];
     __shared__ Xform ts;
+#ifdef GSKYHIP_AB
+    __shared__ uint64_t s_ps[8];
+    uint64_t *ps = s_ps;
+#else
+    uint64_t *ps = nullptr;
+#endif
     for (int p = 0; p < a.n_pairs; p++) {
-      plan_pair<256>(a, p, sx, sy, sok, ts);
+      plan_pair<256>(a, p, sx, sy, sok, ts, p == 0 ? ps : nullptr);
       __syncthreads();
     }
+#ifdef GSKYHIP_AB
+    if (tid == 0) for (int i = 1; i < 6; i++) st_pair[i] = s_ps[i] - s_ps[i - 1];
+#endif
   }
   stamp();
   if (tid < 64) a.counters[tid] = 0;
@@ -1269,8 +1302,10 @@ __global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
   __syncthreads();
   stamp();
 #ifdef GSKYHIP_AB
-  if (tid == 0)
+  if (tid == 0) {
     for (int i = 1; i < ns; i++) a.counters[40 + i] = (int32_t)(st[i] - st[i - 1]);
+    for (int i = 1; i < 6; i++) a.counters[50 + i] = (int32_t)st_pair[i];
+  }
 #endif
 }
 
@@ -1546,11 +1581,13 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
     hipLaunchKernelGGL(plan_small_kernel, dim3(1), dim3(256), 0, s, a);
 #ifdef GSKYHIP_AB
     if (getenv("GSKYHIP_PLAN_STAMPS")) {   // phase times of plan_small_kernel, 10 ns ticks
-      int32_t st[8] = {0};
+      int32_t st[16] = {0};
       hipStreamSynchronize(s);
       hipMemcpy(st, a.counters + 40, sizeof(st), hipMemcpyDeviceToHost);
-      fprintf(stderr, "plan_small_stamps_us pairs=%.2f tiles=%.2f cols=%.2f rows=%.2f split=%.2f exact=%.2f\n",
-              st[1] * 0.01, st[2] * 0.01, st[3] * 0.01, st[4] * 0.01, st[5] * 0.01, st[6] * 0.01);
+      fprintf(stderr, "plan_small_stamps_us pairs=%.2f tiles=%.2f cols=%.2f rows=%.2f split=%.2f exact=%.2f"
+              " | pair: setup=%.2f edges=%.2f extent=%.2f borderA=%.2f rest=%.2f\n",
+              st[1] * 0.01, st[2] * 0.01, st[3] * 0.01, st[4] * 0.01, st[5] * 0.01, st[6] * 0.01,
+              st[11] * 0.01, st[12] * 0.01, st[13] * 0.01, st[14] * 0.01, st[15] * 0.01);
     }
 #endif
     return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;

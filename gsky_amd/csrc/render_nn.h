@@ -70,10 +70,45 @@ __device__ __forceinline__ uint32_t scale_int(const ScaleK &k, int32_t c) {
   return c == k.noData.i ? 0xFFu : b;
 }
 
+// The fold of one `inside` LINEAR row whose window edge falls inside the
+// block: the fast body plus the window test (pixels outside the window read
+// nothing and fold nothing; fill mode takes v where c is nodata, which equals
+// the general rule's "v != nd && c == nd" because v == nd == c leaves c
+// unchanged).  Halves of 4 pixels keep the register peak of the fast body.
+template <typename T, int NPX>
+__device__ __forceinline__ void nn_partial_row(__amdgpu_buffer_rsrc_t rs, double xs0, double ys0, double dX, double dY,
+                                               int ic0, int lim, int bx, typename VOf<T>::type nd, bool fill_mode,
+                                               typename VOf<T>::type (&c)[NPX]) {
+  using V = typename VOf<T>::type;
+#pragma unroll
+  for (int h = 0; h < NPX; h += 4) {
+    uint32_t off[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int ic = ic0 + 64 * (h + q);
+      const double dist = (double)ic;
+      const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
+      const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
+      off[q] = (unsigned)ic < (unsigned)lim ? (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T)
+                                            : 0x80000000u;
+    }
+    V vv[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) vv[q] = buf_load<T>(rs, off[q]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const bool inw = (unsigned)(ic0 + 64 * (h + q)) < (unsigned)lim;
+      c[h + q] = (inw & (fill_mode ? (c[h + q] == nd) : (vv[q] != nd))) ? vv[q] : c[h + q];
+    }
+  }
+}
+
 // One stack entry e of the ordered fold of tile row r (MergeMaskedRaster,
 // tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
 // (tile column xl + 64 q).
-template <typename T, bool MASK, int NPX = kNnPx>
+// PARTIAL: with the window-edge body for `inside` rows (the single-entry path
+// of render_nn_kernel has its own and passes false).
+template <typename T, bool MASK, int NPX = kNnPx, bool PARTIAL = true>
 __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
                                              const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
                                              int ns_out, int r, int xb, int xl, int W, int ncols,
@@ -120,7 +155,15 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
     }
     return;
   }
-  // general body: window edges, POOL rows, failed transforms, mask layer;
+  if (PARTIAL && kind == ROW_LINEAR && inside && !masked) {
+    // window edge inside the block on an `inside` row: the fast body plus the
+    // window test (pixels outside the window read nothing and fold nothing;
+    // fill mode takes v where c is nodata, which equals the general rule's
+    // "v != nd && c == nd" because v == nd == c leaves c unchanged)
+    nn_partial_row<T, NPX>(rs, rr->v[0], rr->v[1], rr->v[2], rr->v[3], ic0, lim, bx, nd, fill_mode, c);
+    return;
+  }
+  // general body: POOL rows, rows not inside the band, mask layer;
   // two halves of 4 pixels (4 gathers in flight) keep the register peak
   // of the fast body
   const V fillv = as_v<T>(e.fill);
@@ -340,8 +383,10 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 #pragma unroll
               for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
             }
+          } else if ((cki & 0xFF) == ROW_LINEAR && (cki >> 8)) {
+            nn_partial_row<T, kNnPx>(rs, cv[0], cv[1], cv[2], cv[3], ic0, lim, bx, nd, fill_mode, c);
           } else {
-            nn_entry_row<T, false>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+            nn_entry_row<T, false, kNnPx, false>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
           }
         }
         uint32_t px[kNnPx];
@@ -411,8 +456,10 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   // single-entry tiles through the prefetching path (C2: 1.445 vs 1.470 ms,
   // profiles/r03f_ab_c2.jsonl)
   bool one = true;
-  bool staged = false;   // large RGBA batches through the LDS-staged kernel (render_nn_stage.h)
 #ifdef GSKYHIP_AB
+  // large RGBA batches through the LDS-staged kernel (render_nn_stage.h): 7 %
+  // slower on C2 (1.54 vs 1.44 ms, profiles/r03j_ab_c2_staged.jsonl)
+  bool staged = false;
   if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
   if (const char *on = getenv("GSKYHIP_NN_ONE")) one = atoi(on) != 0;
   if (const char *sg = getenv("GSKYHIP_NN_STAGED")) staged = atoi(sg) != 0;
@@ -437,8 +484,10 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
     else launch_nn_v<T, true, false, 4>(a, s);
   } else if (canvas) {
     launch_nn_v<T, false, true, 4>(a, s);
+#ifdef GSKYHIP_AB
   } else if (rpw8 && staged) {
     launch_nn_stage<T>(a, s);
+#endif
   } else if (rpw8) {
     if (one) launch_nn_v<T, false, false, 8, true>(a, s);
     else launch_nn_v<T, false, false, 8>(a, s);
