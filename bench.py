@@ -461,7 +461,7 @@ def c4_stack(n_bands, size, device):
     synth.c4_band (per-(pixel, slice) U(0, 0.05) noise and 5 % nodata,
     SURVEY 8d)."""
     from gsky_amd import drill
-    ts = (n_bands + 3) // 4 * 4
+    ts = (n_bands + 31) // 32 * 32   # 128-byte aligned pixel rows (gsky_amd.drill.DrillStack)
     st = torch.zeros((size, size, ts), dtype=torch.float32, device=device)
     for t0 in range(0, n_bands, 16):
         bs = synth._pmap(lambda t: synth.c4_band(t, size, n_bands), range(t0, min(n_bands, t0 + 16)))

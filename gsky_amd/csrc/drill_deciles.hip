@@ -387,18 +387,25 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
         if (sl >= 0) cand[s_soff[sl] + atomicAdd(&s_fill[sl], 1u)] = k;
       });
       __syncthreads();
-      // rank r is the s_rem[r]-th key of its bucket: lane i counts the keys
-      // ordered before its own (ties by position)
+      // rank r is the s_rem[r]-th key of its bucket (<= 64 keys, one per
+      // lane): MSB-first selection over the bits below the bucket digit with
+      // wave ballots -- lanes whose bit is 0 come first; equal keys end in
+      // the same candidate set, any of them is the value
       for (int r = wv; r < nr; r += kSelWaves) {
         const int cnt = (int)s_bcnt[r];
         const uint32_t *c = cand + s_soff[s_slot[r]];
         const uint32_t ki = ln < cnt ? c[ln] : 0xFFFFFFFFu;
-        int less = 0;
-        for (int j = 0; j < cnt; j++) {
-          const uint32_t kj = c[j];
-          less += (kj < ki || (kj == ki && j < ln)) ? 1 : 0;
+        uint64_t live = __ballot(ln < cnt);
+        uint32_t rem = s_rem[r];
+        for (int b = shA - 1; b >= 0; b--) {
+          const uint64_t zero = __ballot(((ki >> b) & 1u) == 0u) & live;
+          const uint32_t nz = (uint32_t)__popcll(zero);
+          if (rem < nz) live = zero;
+          else { rem -= nz; live &= ~zero; }
         }
-        if (ln < cnt && less == (int)s_rem[r]) s_pref[r] = ki;
+        const int src = __ffsll((unsigned long long)live) - 1;
+        const uint32_t key = __shfl(ki, src);
+        if (ln == 0) s_pref[r] = key;
       }
       __syncthreads();
       pos = 0;

@@ -1,7 +1,7 @@
 """WPS drill (zonal statistics) on MI355X.
 
 `DrillStack` holds a time stack resident in HBM in the time-innermost layout
-([y][x][t], t padded to a multiple of 4).  `read_data` runs readData
+([y][x][t], t padded to a multiple of 32: 128-byte aligned pixel rows).  `read_data` runs readData
 (worker/gdalprocess/drill.go:90-227) for a batch of polygon windows at once;
 `drill_merge` is the DrillMerger per-date weighted mean
 (processor/drill_merger.go:79-93).
@@ -46,7 +46,7 @@ class DrillStack:
             raise ValueError("stack must be (n_bands, ysize, xsize)")
         nb, ys, xs = bands.shape
         self.n_bands, self.ysize, self.xsize = nb, ys, xs
-        self.t_stride = (nb + 3) // 4 * 4
+        self.t_stride = (nb + 31) // 32 * 32   # 128-byte pixel rows: a slice group never straddles an extra line
         dev = torch.device(device or "cuda")
         st = torch.zeros((ys, xs, self.t_stride), dtype=torch.float32, device=dev)
         st[:, :, :nb] = bands.to(dev, torch.float32).permute(1, 2, 0)

@@ -40,7 +40,7 @@ def build_stack(n_bands, size, device):
     t = torch.arange(n_bands, dtype=torch.float64, device=device)
     base = (0.2 + 0.1 * torch.sin(2 * np.pi * t / 365.0)).float()
     fac = (1.0 + (t % 7) * 0.01).float()
-    ts = (n_bands + 3) // 4 * 4
+    ts = (n_bands + 31) // 32 * 32   # 128-byte aligned pixel rows (gsky_amd.drill.DrillStack)
     st = torch.zeros((size, size, ts), dtype=torch.float32, device=device)
     nz = torch.from_numpy(noise).to(device)
     for y0 in range(0, size, 256):   # bounded temporaries
