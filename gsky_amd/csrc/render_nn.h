@@ -78,10 +78,11 @@ __device__ __forceinline__ uint32_t scale_int(const ScaleK &k, int32_t c) {
 template <typename T, int NPX>
 __device__ __forceinline__ void nn_partial_row(__amdgpu_buffer_rsrc_t rs, double xs0, double ys0, double dX, double dY,
                                                int ic0, int lim, int bx, typename VOf<T>::type nd, bool fill_mode,
-                                               typename VOf<T>::type (&c)[NPX]) {
+                                               int c0, int c1, typename VOf<T>::type (&c)[NPX]) {
   using V = typename VOf<T>::type;
 #pragma unroll
   for (int h = 0; h < NPX; h += 4) {
+    if (c1 <= 64 * h || c0 >= 64 * (h + 4)) continue;   // the half's 256 block columns miss the window
     uint32_t off[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -160,7 +161,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
     // window test (pixels outside the window read nothing and fold nothing;
     // fill mode takes v where c is nodata, which equals the general rule's
     // "v != nd && c == nd" because v == nd == c leaves c unchanged)
-    nn_partial_row<T, NPX>(rs, rr->v[0], rr->v[1], rr->v[2], rr->v[3], ic0, lim, bx, nd, fill_mode, c);
+    nn_partial_row<T, NPX>(rs, rr->v[0], rr->v[1], rr->v[2], rr->v[3], ic0, lim, bx, nd, fill_mode, c0, c1, c);
     return;
   }
   // general body: POOL rows, rows not inside the band, mask layer;
@@ -169,6 +170,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   const V fillv = as_v<T>(e.fill);
 #pragma unroll
   for (int h = 0; h < NPX; h += 4) {
+    if (c1 <= 64 * h || c0 >= 64 * (h + 4)) continue;   // the half's 256 block columns miss the window
     uint32_t idx[4];
     if (kind == ROW_LINEAR) {
       const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
@@ -384,7 +386,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
               for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
             }
           } else if ((cki & 0xFF) == ROW_LINEAR && (cki >> 8)) {
-            nn_partial_row<T, kNnPx>(rs, cv[0], cv[1], cv[2], cv[3], ic0, lim, bx, nd, fill_mode, c);
+            nn_partial_row<T, kNnPx>(rs, cv[0], cv[1], cv[2], cv[3], ic0, lim, bx, nd, fill_mode, c0, c1, c);
           } else {
             nn_entry_row<T, false, kNnPx, false>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
           }
