@@ -439,7 +439,8 @@ def run_c3(ctx: Ctx, args):
            "chunk_rows_rank0": rows[0], "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "plan + bilinear render (rank 0)",
-                        "kernel_ms": round(render_ms, 4), "algorithmic_bytes_per_launch": int(abytes)}}
+                        "kernel_ms": round(render_ms, 4), "algorithmic_bytes_per_launch": int(abytes),
+                        "traffic": pmc_traffic("bil_c3")}}
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
         from oracle import oracle as O
         ids = list(range(0, len(chunks), max(1, len(chunks) // 16)))[:16]

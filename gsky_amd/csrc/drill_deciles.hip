@@ -283,14 +283,16 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     if (tid == 0) status[o] = GSKYHIP_E_RANGE;
     return;
   }
-  if (tid == 0) {   // distinct ranks, ascending
-    int nr = 0;
-    for (int i = 0; i < dc; i++) {
-      const int r = (i + 1) * step;
-      if (nr == 0 || s_rank[nr - 1] != r) s_rank[nr++] = r;
-      if (isEven && s_rank[nr - 1] != r + 1) s_rank[nr++] = r + 1;
-    }
-    s_nr = nr;
+  if (tid < 64) {   // distinct ranks, ascending: the sequence r_0 (, r_0 + 1), r_1, ... is
+    // non-decreasing, so a value is new where it differs from its predecessor
+    const int nc = isEven ? 2 * dc : dc;
+    const int i = isEven ? (tid >> 1) : tid;
+    const int v = (i + 1) * step + (isEven ? (tid & 1) : 0);
+    const int prev = __shfl_up(v, 1);
+    const bool keep = tid < nc && (tid == 0 || v != prev);
+    const uint64_t kb = __ballot(keep);
+    if (keep) s_rank[__popcll(kb & ((1ull << tid) - 1ull))] = v;
+    if (tid == 0) s_nr = __popcll(kb);
   }
   __syncthreads();
   const int nr = s_nr;
@@ -348,33 +350,39 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
       H[b4] = ex + h0; H[b4 + 1] = ex + h0 + h1; H[b4 + 2] = ex + h0 + h1 + h2; H[b4 + 3] = ex + sum;
     }
     __syncthreads();
-    if (tid < nr) {   // the bucket of rank r: the first whose cumulative count exceeds r
-      const uint32_t r = (uint32_t)s_rank[tid];
+    if (tid < 64) {   // wave 0, lane r < nr: the bucket of rank r (the first whose
+      // cumulative count exceeds r), then the distinct buckets (ascending with
+      // the ranks) -> slots and their candidate offsets
+      const bool act = tid < nr;
+      const uint32_t r = act ? (uint32_t)s_rank[tid] : 0u;
       int lo = 0, hi = (int)dmask;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (H[mid] > r) hi = mid; else lo = mid + 1;
       }
       const uint32_t before = lo ? H[lo - 1] : 0u;
-      s_bkt[tid] = lo;
-      s_rem[tid] = r - before;
-      s_bcnt[tid] = H[lo] - before;
-    }
-    __syncthreads();
-    if (tid == 0) {   // distinct buckets (ascending with the ranks) -> slots
-      int ns = 0, off = 0, fast = 1;
-      for (int r = 0; r < nr; r++) {
-        if (ns == 0 || s_spref[ns - 1] != (uint32_t)s_bkt[r]) {
-          s_spref[ns] = (uint32_t)s_bkt[r];
-          s_soff[ns] = off;
-          off += (int)s_bcnt[r];
-          if (s_bcnt[r] > (uint32_t)kCandMax) fast = 0;
-          ns++;
-        }
-        s_slot[r] = ns - 1;
+      const uint32_t bcnt = H[lo] - before;
+      const int prev = __shfl_up(lo, 1);
+      const bool nw = act && (tid == 0 || lo != prev);
+      const uint64_t nb = __ballot(nw);
+      const int slot = __popcll(nb & ((2ull << tid) - 1ull)) - 1;
+      uint32_t incl = nw ? bcnt : 0u;   // candidate offsets: exclusive scan over the new slots
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t up = __shfl_up(incl, o);
+        if (tid >= o) incl += up;
       }
-      s_ns = ns;
-      s_fast = fast;
+      const bool big = __ballot(act && bcnt > (uint32_t)kCandMax) != 0ull;
+      if (act) {
+        s_bkt[tid] = lo;
+        s_rem[tid] = r - before;
+        s_bcnt[tid] = bcnt;
+        s_slot[tid] = slot;
+      }
+      if (nw) {
+        s_spref[slot] = (uint32_t)lo;
+        s_soff[slot] = (int)(incl - bcnt);
+      }
+      if (tid == 0) { s_ns = __popcll(nb); s_fast = big ? 0 : 1; }
     }
     __syncthreads();
     if (s_fast) {

@@ -146,8 +146,6 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
         const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
 #pragma unroll
         for (int h = 0; h < kNnPx; h += HP) {
-          // the group's block columns [64 h, 64 (h + HP)) outside the window: nothing to fold
-          if (c1 <= 64 * h || c0 >= 64 * (h + HP)) continue;
           int ixv[HP], iyv[HP];
           WT rx[HP], ry[HP];
           bool allin = true;

@@ -82,7 +82,6 @@ __device__ __forceinline__ void nn_partial_row(__amdgpu_buffer_rsrc_t rs, double
   using V = typename VOf<T>::type;
 #pragma unroll
   for (int h = 0; h < NPX; h += 4) {
-    if (c1 <= 64 * h || c0 >= 64 * (h + 4)) continue;   // the half's 256 block columns miss the window
     uint32_t off[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -170,7 +169,6 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   const V fillv = as_v<T>(e.fill);
 #pragma unroll
   for (int h = 0; h < NPX; h += 4) {
-    if (c1 <= 64 * h || c0 >= 64 * (h + 4)) continue;   // the half's 256 block columns miss the window
     uint32_t idx[4];
     if (kind == ROW_LINEAR) {
       const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
