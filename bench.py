@@ -422,7 +422,10 @@ def run_c3(ctx: Ctx, args):
         return band
 
     dt = ctx.timed(step, args.c3_steps, 1)
-    render_ms = event_ms(render, 3)
+    # roofline of the band kernel alone (phase 2, planning already in the
+    # workspace), as for C2; planning timed beside it
+    plan_ms = event_ms(lambda: b.render_coverage(sp, band, offs, resample=cfg.resample, phase=1), 3)
+    render_ms = event_ms(lambda: b.render_coverage(sp, band, offs, resample=cfg.resample, phase=2), 3)
     gather_ms = None
     if ctx.world > 1:
         band = step()
@@ -438,8 +441,10 @@ def run_c3(ctx: Ctx, args):
                                                                       if ctx.world > 1 else ""),
            "chunk_rows_rank0": rows[0], "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "plan + bilinear render (rank 0)",
-                        "kernel_ms": round(render_ms, 4), "algorithmic_bytes_per_launch": int(abytes),
+                        "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "kernel": "render_bil_kernel + render_general_kernel (phase 2, rank 0)",
+                        "kernel_ms": round(render_ms, 4), "plan_ms": round(plan_ms, 4),
+                        "algorithmic_bytes_per_launch": int(abytes),
                         "traffic": pmc_traffic("bil_c3")}}
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
         from oracle import oracle as O
