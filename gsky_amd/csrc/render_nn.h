@@ -209,22 +209,12 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
 
 // The ordered fold of tile row r over the tile's entries in ProcessRasterStack
 // order; c[] arrives holding the canvas nodata.
-// U2 (A/B): two-entry stacks as straight-line code, so the second entry's
-// descriptor / record loads and gathers can be scheduled under the first's.
-template <typename T, bool MASK, bool U2 = false>
+template <typename T, bool MASK>
 __device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *__restrict__ ents,
                                             const int32_t *__restrict__ ord, int n_entries,
                                             const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
                                             int ns_out, int r, int xb, int xl, int W, int ncols,
                                             typename VOf<T>::type (&c)[kNnPx]) {
-  if constexpr (U2) {
-    if (n_entries == 2) {
-      const int o0 = ord[0], o1 = ord[1];
-      nn_entry_row<T, MASK>(a, ents, ents[o0], rows, pool, ns_out, r, xb, xl, W, ncols, c);
-      nn_entry_row<T, MASK>(a, ents, ents[o1], rows, pool, ns_out, r, xb, xl, W, ncols, c);
-      return;
-    }
-  }
 #pragma unroll 1
   for (int k = 0; k < n_entries; k++)
     nn_entry_row<T, MASK>(a, ents, ents[ord[k]], rows, pool, ns_out, r, xb, xl, W, ncols, c);
@@ -257,7 +247,7 @@ __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint3
 // tiles -- keep the entry's descriptor in scalar registers for all the
 // wave's rows and fetch the next row's record while the current row is
 // gathered, so no row waits for its record.
-template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, bool STAGE = false, bool U2 = false>
+template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, bool STAGE = false>
 __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
@@ -416,7 +406,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
     V c[kNnPx];
 #pragma unroll
     for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-    nn_fold_row<T, MASK, U2>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+    nn_fold_row<T, MASK>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
 
     // output: typed canvas (WCS) or utils.Scale + palette / grey RGBA
     if constexpr (CANVAS) {
@@ -442,10 +432,10 @@ constexpr int kNnRpw8MinItems = 32768;
 constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
 constexpr int kNnMaskRpw1Items = 16384;   // masked stacks: one row per wave below this many workgroups
 
-template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = false, bool U2 = false>
+template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = false>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE, U2>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -473,13 +463,6 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
   if (const char *on = getenv("GSKYHIP_NN_ONE")) one = atoi(on) != 0;
   if (const char *sg = getenv("GSKYHIP_NN_STAGED")) staged = atoi(sg) != 0;
-  if (const char *u2 = getenv("GSKYHIP_NN_U2")) {
-    if (atoi(u2) != 0 && !mask && !canvas && rpw8) {
-      if (one) launch_nn_v<T, false, false, 8, true, false, true>(a, s);
-      else launch_nn_v<T, false, false, 8, false, false, true>(a, s);
-      return;
-    }
-  }
   if (const char *st = getenv("GSKYHIP_NN_STAGE")) {
     if (!mask && !canvas && rpw8 && atoi(st) == 1) {
       if (one) launch_nn_v<T, false, false, 8, true, true>(a, s);

@@ -83,8 +83,6 @@ print(json.dumps(res))
     {"GSKYHIP_NN_RPW": "8", "GSKYHIP_NN_ONE": "1"}, {"GSKYHIP_NN_RPW": "8", "GSKYHIP_NN_ONE": "0"},
     {"GSKYHIP_NN_MASK_RPW": "1"}, {"GSKYHIP_NN_MASK_RPW": "4"},
     {"GSKYHIP_NN_RPW": "8", "GSKYHIP_NN_STAGED": "1"},
-    {"GSKYHIP_NN_RPW": "8", "GSKYHIP_NN_U2": "1", "GSKYHIP_NN_ONE": "1"},
-    {"GSKYHIP_NN_RPW": "8", "GSKYHIP_NN_U2": "1", "GSKYHIP_NN_ONE": "0"},
 ])
 def test_ab_build_variants_match_oracle(knobs):
     lib = os.path.join(ROOT, "gsky_amd", "libgskyhip_ab.so")

@@ -27,3 +27,9 @@ for c in c2 c3 c4 c1; do
 done
 timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 stop $? bench
+for v in 4 8 4 8; do
+  GSKYHIP_LIB=ab GSKYHIP_BIL_RPW=$v timeout -k 10 300 python -u tools/ab_c3.py --reps 20 --oracle --label "bil_rpw$v" \
+    >> gpurun_out/ab_c3.jsonl 2>> gpurun_out/ab.err
+  stop $? "ab_c3_rpw$v"
+done
+cat gpurun_out/ab_c3.jsonl
