@@ -144,61 +144,12 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
   const float *base = stack + tsel[g * kTrBands + (bl < nb ? bl : 0)];
   const int32_t my_px = idx[mask_off[p] + k0 + (lane < m ? lane : 0)];
   float *T = tile[wave];
-  for (int kb = 0; kb < m; kb += 32) {
-    float v[16];
-#pragma unroll
-    for (int u = 0; u < 16; u++) {   // pixels kb + 2u (lanes 0-31) and kb + 2u + 1 (lanes 32-63)
-      const int k = kb + 2 * u + half;
-      const int px0 = __builtin_amdgcn_readlane(my_px, min(kb + 2 * u, 63));
-      const int px1 = __builtin_amdgcn_readlane(my_px, min(kb + 2 * u + 1, 63));
-      v[u] = base[(int64_t)(half ? px1 : px0) * t_stride];
-      (void)k;
-    }
-#pragma unroll
-    for (int u = 0; u < 16; u++) T[(kb + 2 * u + half) * kPad + bl] = v[u];
-  }
-  wave_lds_sync();
-  float *seg = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)(g * kTrBands) * n + k0;
-  if (lane < m) {
-    for (int j = 0; j < nb; j++) seg[(int64_t)j * n + lane] = T[lane * kPad + j];   // lane = pixel
-  }
-}
-
-#ifdef GSKYHIP_AB
-// A/B (GSKYHIP_DEC_TR1=1): decile_transpose_kernel with one round of 32 loads per lane.
-__global__ __launch_bounds__(256) void decile_transpose1_kernel(const float *__restrict__ stack, int t_stride,
-                                                               const int32_t *__restrict__ idx,
-                                                               const int64_t *__restrict__ mask_off,
-                                                               const int32_t *__restrict__ count,
-                                                               const int32_t *__restrict__ chunk_base, int n_polys,
-                                                               const int32_t *__restrict__ tsel, int n_chunk,
-                                                               int n_groups, float *__restrict__ vals) {
-  constexpr int kPad = kTrBands + 1;
-  __shared__ float tile[4][64 * kPad];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t item = (int64_t)blockIdx.x * 4 + wave;
-  const int ch = (int)(item / n_groups), g = (int)(item % n_groups);
-  if (ch >= chunk_base[n_polys]) return;   // whole waves; no workgroup barrier below
-  int lo = 0, hi = n_polys - 1;            // polygon owning chunk ch
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (chunk_base[mid] <= ch) lo = mid; else hi = mid - 1;
-  }
-  const int p = lo;
-  const int n = count[p];
-  const int k0 = (ch - chunk_base[p]) * kDecChunk;
-  const int m = min(kDecChunk, n - k0);
-  const int nb = min(kTrBands, n_chunk - g * kTrBands);   // bands of this group
-  const int bl = lane & (kTrBands - 1), half = lane / kTrBands;
-  // every lane loads from a valid address (band 0 of the group, pixel 0 of
-  // the chunk) so the loads are unconditional and all in flight
-  const float *base = stack + tsel[g * kTrBands + (bl < nb ? bl : 0)];
-  const int32_t my_px = idx[mask_off[p] + k0 + (lane < m ? lane : 0)];
-  float *T = tile[wave];
-  {   // all 64 pixels' loads in flight at once (pixels past m read pixel 0 of the chunk)
+  {   // all 64 pixels' loads in flight at once (lanes past m hold pixel 0 of the chunk;
+      // their rows are never stored): 3 % faster than two rounds of 16
+      // (profiles/r03u_kernel_stats_c4_tr*.csv)
     float v[32];
 #pragma unroll
-    for (int u = 0; u < 32; u++) {
+    for (int u = 0; u < 32; u++) {   // pixels 2u (lanes 0-31) and 2u + 1 (lanes 32-63)
       const int px0 = __builtin_amdgcn_readlane(my_px, 2 * u);
       const int px1 = __builtin_amdgcn_readlane(my_px, 2 * u + 1);
       v[u] = base[(int64_t)(half ? px1 : px0) * t_stride];
@@ -212,7 +163,6 @@ __global__ __launch_bounds__(256) void decile_transpose1_kernel(const float *__r
     for (int j = 0; j < nb; j++) seg[(int64_t)j * n + lane] = T[lane * kPad + j];   // lane = pixel
   }
 }
-#endif
 
 // computeDeciles of one (polygon, band) segment; status 0, 1 (band total 0:
 // zeros, Count 0 in the reference's TimeSeries) or GSKYHIP_E_RANGE (the
@@ -609,13 +559,6 @@ int launch_drill_deciles(const DecileCall &c) {
     if (hipMemcpyAsync(w.tsel, sel.data() + b0, sizeof(int32_t) * n_chunk, hipMemcpyHostToDevice, s) != hipSuccess)
       return GSKYHIP_E_HIP;
     const int64_t items = max_chunks * n_groups;
-#ifdef GSKYHIP_AB
-    if (getenv("GSKYHIP_DEC_TR1") && atoi(getenv("GSKYHIP_DEC_TR1")) != 0)
-      hipLaunchKernelGGL(decile_transpose1_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, c.stack,
-                       c.t_stride, w.idx, c.mask_off, w.count, w.chunk_base, c.n_polys, w.tsel, n_chunk, n_groups,
-                       w.vals);
-    else
-#endif
     hipLaunchKernelGGL(decile_transpose_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, c.stack,
                        c.t_stride, w.idx, c.mask_off, w.count, w.chunk_base, c.n_polys, w.tsel, n_chunk, n_groups,
                        w.vals);

@@ -407,31 +407,88 @@ __device__ int suggested_warp_output2_blk(const Xform &t, int nInX, int nInY, do
       sy[k] = g2[3] + X * g2[4] + Y * g2[5];
       sok[k] = 1;
     }
-  } else for (int k = tid; k < ns; k += NT) {
-    const int i = k >> 2, e = k & 3;
-    const double r = (i == kSteps) ? 1.0 : i * dfStep;
-    double x, y;
-    if (e == 0) { x = r * nInX; y = 0.0; }
-    else if (e == 1) { x = r * nInX; y = nInY; }
-    else if (e == 2) { x = 0.0; y = r * nInY; }
-    else { x = nInX; y = r * nInY; }
-    const int ok = xform_point(t, false, x, y);
-    sx[k] = x; sy[k] = y; sok[k] = ok;
+  }
+  // the grid point (ix, iy) of the 21 x 21 fallback, source pixel coordinates
+  auto grid_xy = [&](int ix, int iy, double &x, double &y) {
+    const double ry = (iy == kSteps) ? 1.0 : iy * dfStep;
+    const double rx = (ix == kSteps) ? 1.0 : ix * dfStep;
+    x = rx * nInX; y = ry * nInY;
+  };
+  constexpr int kEdge = 4 * (kSteps + 1), kInner = (kSteps - 1) * (kSteps - 1);
+  constexpr bool kSpec = NT >= kEdge;   // one edge sample per thread: the rest speculate on the grid
+  double gx = 0.0, gy = 0.0;            // this thread's edge sample / speculative interior point
+  int gok = 0;
+  if (!(ge && ge->n_fail == 0)) {
+    if constexpr (kSpec) {
+      if (tid < kEdge) {
+        const int i = tid >> 2, e = tid & 3;
+        const double r = (i == kSteps) ? 1.0 : i * dfStep;
+        double x, y;
+        if (e == 0) { x = r * nInX; y = 0.0; }
+        else if (e == 1) { x = r * nInX; y = nInY; }
+        else if (e == 2) { x = 0.0; y = r * nInY; }
+        else { x = nInX; y = r * nInY; }
+        gok = xform_point(t, false, x, y);
+        gx = x; gy = y;
+        sx[tid] = x; sy[tid] = y; sok[tid] = gok;
+      } else if (tid - kEdge < kInner) {   // interior point j of the grid, in case an edge sample fails
+        const int j = tid - kEdge;
+        double x, y;
+        grid_xy(1 + j % (kSteps - 1), 1 + j / (kSteps - 1), x, y);
+        gok = xform_point(t, false, x, y);
+        gx = x; gy = y;
+      }
+    } else {
+      for (int k = tid; k < ns; k += NT) {
+        const int i = k >> 2, e = k & 3;
+        const double r = (i == kSteps) ? 1.0 : i * dfStep;
+        double x, y;
+        if (e == 0) { x = r * nInX; y = 0.0; }
+        else if (e == 1) { x = r * nInX; y = nInY; }
+        else if (e == 2) { x = 0.0; y = r * nInY; }
+        else { x = nInX; y = r * nInY; }
+        const int ok = xform_point(t, false, x, y);
+        sx[k] = x; sy[k] = y; sok[k] = ok;
+      }
+    }
   }
   __syncthreads();
   PSTAMP(stp, 2);
   int failed = 0;
   for (int k = tid; k < ns; k += NT) failed |= sok[k] ? 0 : 1;
   if (__syncthreads_or(failed)) {   // full grid of the source raster
-    ns = kGrid;
-    for (int k = tid; k < ns; k += NT) {
-      const int iy = k / (kSteps + 1), ix = k % (kSteps + 1);
-      const double ry = (iy == kSteps) ? 1.0 : iy * dfStep;
-      const double rx = (ix == kSteps) ? 1.0 : ix * dfStep;
-      double x = rx * nInX, y = ry * nInY;
-      const int ok = xform_point(t, false, x, y);
-      sx[k] = x; sy[k] = y; sok[k] = ok;
+    if constexpr (kSpec) {
+      // the edge samples are the grid's boundary points (the same expressions
+      // of the same coordinates), the first interior points were speculated:
+      // place both, transform the remaining interior points
+      if (tid < kEdge) {
+        const int i = tid >> 2, e = tid & 3;
+        const int g = e == 0 ? i : e == 1 ? kSteps * (kSteps + 1) + i : e == 2 ? i * (kSteps + 1)
+                                                                                  : i * (kSteps + 1) + kSteps;
+        sx[g] = gx; sy[g] = gy; sok[g] = gok;   // corners: two equal writes
+      } else if (tid - kEdge < kInner) {
+        const int j = tid - kEdge;
+        const int g = (1 + j / (kSteps - 1)) * (kSteps + 1) + 1 + j % (kSteps - 1);
+        sx[g] = gx; sy[g] = gy; sok[g] = gok;
+      }
+      for (int j = NT - kEdge + tid; j < kInner; j += NT) {
+        double x, y;
+        const int ix = 1 + j % (kSteps - 1), iy = 1 + j / (kSteps - 1);
+        grid_xy(ix, iy, x, y);
+        const int ok = xform_point(t, false, x, y);
+        const int g = iy * (kSteps + 1) + ix;
+        sx[g] = x; sy[g] = y; sok[g] = ok;
+      }
+    } else {
+      for (int k = tid; k < kGrid; k += NT) {
+        const int iy = k / (kSteps + 1), ix = k % (kSteps + 1);
+        double x, y;
+        grid_xy(ix, iy, x, y);
+        const int ok = xform_point(t, false, x, y);
+        sx[k] = x; sy[k] = y; sok[k] = ok;
+      }
     }
+    ns = kGrid;
     __syncthreads();
   }
   double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
