@@ -13,7 +13,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # GSKYHIP_LIB=ab selects the A/B build (make -C gsky_amd/csrc ab: the same
 # kernels plus the experiment knobs it reads from the environment); tools and
 # A/B scripts only -- the product library reads no knob.
-LIB_PATH = os.path.join(_HERE, "libgskyhip_ab.so" if os.environ.get("GSKYHIP_LIB") == "ab" else "libgskyhip.so")
+# GSKYHIP_LIB=<name> (other than "ab") loads libgskyhip_<name>.so: a kept
+# earlier build, for A/B timing against the current one.
+_SEL = os.environ.get("GSKYHIP_LIB", "")
+LIB_PATH = os.path.join(_HERE, "libgskyhip_%s.so" % _SEL if _SEL and _SEL != "default" else "libgskyhip.so")
 
 # GDALDataType codes (warp.go:428-431) + 100 = SignedByte (warp.go:354-359)
 BYTE, UINT16, INT16, UINT32, INT32, FLOAT32, FLOAT64, SIGNEDBYTE = 1, 2, 3, 4, 5, 6, 7, 100

@@ -489,6 +489,45 @@ __device__ __forceinline__ bool linear_nn_px(const RowRec &r, int dist, int bx, 
 __device__ __forceinline__ bool linear_row_inside(const RowRec &r, int n, int bx, int by) {
   return n > 0 && linear_nn_px(r, 0, bx, by) && linear_nn_px(r, n - 1, bx, by);
 }
+// 32.32 fixed-point form of an `inside` LINEAR row (round 4), written beside
+// the RowRec by plan_row: x0 = round(xs0 * 2^32), dx = round(dX * 2^32), same
+// for y.  Window pixel d's fixed coordinate x0 + d * dx is within
+// 2^-33 * (d + 1) of the real xs0 + dX * d, and the reference's
+// fl(fl(xs0 + fl(dX * d)) + 1e-10) is within 1e-10 + a few ulps of it (every
+// coordinate < 2^20, so an ulp is <= 2^-32): with d < kFixMaxW the two differ
+// by < 2^-20.  Wherever the fixed value's fraction is at least kFixMargin
+// (2^-19) away from an integer, both truncate to the same source pixel, so the
+// NN band kernel takes the integer part of the fixed value and falls back to
+// the fp64 expressions only for a row where some pixel is closer than that
+// (render_nn.h nn_fix_row).  x0 == kFixNone: no fixed form (not LINEAR +
+// inside, coordinates too large, window too wide).
+struct RowFix {
+  int64_t x0, y0, dx, dy;
+};
+constexpr int64_t kFixNone = (int64_t)0x8000000000000000ull;
+constexpr int kFixMaxW = 4096;
+constexpr uint32_t kFixMargin = 1u << 13;   // 2^-19 in units of 2^-32
+
+__device__ __forceinline__ bool fix_range_ok(double v0, double dv, int n) {
+  const double lim = 1048576.0;   // 2^20
+  const double v1 = v0 + dv * (double)n;
+  return fabs(v0) < lim && fabs(v1) < lim && fabs(dv) < 1024.0;
+}
+
+__device__ __forceinline__ RowFix row_fix(const RowRec &r, int n) {
+  RowFix f;
+  f.x0 = kFixNone; f.y0 = 0; f.dx = 0; f.dy = 0;
+  if (r.kind == ROW_LINEAR && r.inside && n > 0 && n <= kFixMaxW && fix_range_ok(r.v[0], r.v[2], n) &&
+      fix_range_ok(r.v[1], r.v[3], n)) {
+    const double s = 4294967296.0;   // scaling by 2^32 is exact
+    f.x0 = __double2ll_rn(r.v[0] * s);
+    f.y0 = __double2ll_rn(r.v[1] * s);
+    f.dx = __double2ll_rn(r.v[2] * s);
+    f.dy = __double2ll_rn(r.v[3] * s);
+  }
+  return f;
+}
+
 struct Leaf {
   double xs0, ys0, dX, dY;
   int32_t start, kind;   // LeafKind

@@ -5,6 +5,7 @@
 // drop-in, and the launch sequences.  All pixel work runs in the HIP kernels
 // of render.hip / stages.hip / drill.hip; nothing here falls back to the CPU.
 #include <hip/hip_runtime.h>
+#include <sys/stat.h>
 
 #include <cmath>
 #include <cstdio>
@@ -264,11 +265,15 @@ struct Registered {
   gskyhip_crs crs;
   bool has_crs;
   std::vector<void *> owned;   // HBM the library allocated for it (ingested files)
+  int64_t bytes = 0;           // ... and its size
+  uint64_t last_use = 0;       // DropIn::tick of the last batch that used it
+  int64_t mtime_ns = 0, fsize = -1;   // the file as ingested (fsize < 0: registered by the caller)
 };
 
 void release(Registered &r) {
   for (void *p : r.owned) hipFree(p);
   r.owned.clear();
+  r.bytes = 0;
 }
 
 struct DropIn {
@@ -277,10 +282,62 @@ struct DropIn {
   hipStream_t stream = nullptr;
   void *dev = nullptr;   // descriptors + workspace + window
   size_t dev_bytes = 0;
+  uint64_t tick = 0;     // one per warp batch: entries it uses are not evicted while it runs
 };
 DropIn &dropin() {
   static DropIn d;
   return d;
+}
+
+// HBM the ingested (library-owned) granules may hold before the least
+// recently used ones are released: GSKYHIP_INGEST_CACHE_MB, default 32 GiB
+// (of 288 GB per MI355X).  Caller-registered granules are never evicted.
+int64_t ingest_cache_cap() {
+  static const int64_t cap = [] {
+    const char *e = std::getenv("GSKYHIP_INGEST_CACHE_MB");
+    const long long mb = e ? std::atoll(e) : 32768;
+    return (int64_t)(mb > 0 ? mb : 32768) << 20;
+  }();
+  return cap;
+}
+
+// Make room for `need` more bytes of ingested granules: release the least
+// recently used ones not used by the running batch (last_use < d.tick).
+void evict_for(DropIn &d, int64_t need) {
+  const int64_t cap = ingest_cache_cap();
+  for (;;) {
+    int64_t held = 0;
+    auto victim = d.reg.end();
+    for (auto it = d.reg.begin(); it != d.reg.end(); ++it) {
+      held += it->second.bytes;
+      if (it->second.bytes > 0 && it->second.last_use < d.tick &&
+          (victim == d.reg.end() || it->second.last_use < victim->second.last_use))
+        victim = it;
+    }
+    if (held + need <= cap || victim == d.reg.end()) return;   // fits, or nothing evictable: exceed the cap
+    release(victim->second);
+    d.reg.erase(victim);
+  }
+}
+
+// mtime (ns) and size of a file; false if it cannot be stat'ed
+bool file_stamp(const std::string &path, int64_t &mtime_ns, int64_t &size) {
+  std::string f = path;
+  if (f.compare(0, 7, "NETCDF:") == 0) {   // NETCDF:file:var / NETCDF:"file":var
+    f = f.substr(7);
+    if (!f.empty() && f[0] == '"') {
+      const size_t q = f.find('"', 1);
+      f = q == std::string::npos ? f.substr(1) : f.substr(1, q - 1);
+    } else {
+      const size_t c = f.rfind(':');
+      if (c != std::string::npos) f = f.substr(0, c);
+    }
+  }
+  struct stat st;
+  if (stat(f.c_str(), &st) != 0) return false;
+  mtime_ns = (int64_t)st.st_mtim.tv_sec * 1000000000 + st.st_mtim.tv_nsec;
+  size = (int64_t)st.st_size;
+  return true;
 }
 
 bool have_gpu() {
@@ -302,6 +359,17 @@ int ingest_geotiff_locked(DropIn &d, const std::string &path, int band) {
   std::memset(&r.g, 0, sizeof(r.g));
   const int ts = type_size(info.dtype);
   if (ts <= 0) return GSKYHIP_E_TYPE;
+  int64_t total = 0;
+  for (int lv = 0; lv <= info.n_ovr; lv++)
+    total += (int64_t)(lv ? info.ovr_xsize[lv - 1] : info.xsize) * (lv ? info.ovr_ysize[lv - 1] : info.ysize) * ts;
+  {
+    auto old = d.reg.find({path, band});
+    if (old != d.reg.end()) { release(old->second); d.reg.erase(old); }
+  }
+  evict_for(d, total);
+  r.bytes = total;
+  r.last_use = d.tick;
+  if (!file_stamp(path, r.mtime_ns, r.fsize)) r.fsize = 0;
   for (int lv = 0; lv <= info.n_ovr; lv++) {
     const int64_t xs = lv ? info.ovr_xsize[lv - 1] : info.xsize, ys = lv ? info.ovr_ysize[lv - 1] : info.ysize;
     void *p = nullptr;
@@ -344,6 +412,14 @@ int ingest_netcdf_locked(DropIn &d, const std::string &path, int band) {
   std::memset(&r.g, 0, sizeof(r.g));
   void *p = nullptr;
   const int64_t bytes = (int64_t)info.xsize * info.ysize * ts;
+  {
+    auto old = d.reg.find({path, band});
+    if (old != d.reg.end()) { release(old->second); d.reg.erase(old); }
+  }
+  evict_for(d, bytes);
+  r.bytes = bytes;
+  r.last_use = d.tick;
+  if (!file_stamp(path, r.mtime_ns, r.fsize)) r.fsize = 0;
   if (hipMalloc(&p, (size_t)bytes) != hipSuccess) return GSKYHIP_E_HIP;
   r.owned.push_back(p);
   if ((rc = gskyhip_netcdf_read(path.c_str(), band, p, bytes, nullptr))) { release(r); return rc; }
@@ -453,6 +529,7 @@ namespace gsky {
 void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
   DropIn &d = dropin();
   std::lock_guard<std::mutex> lk(d.mu);
+  d.tick++;
   struct Item { int req; gskyhip_granule g; gskyhip_crs src; int bx, by; };
   std::map<std::pair<int, std::string>, std::vector<Item>> groups;   // (has dst, dst srs) -> items
   for (int i = 0; i < n; i++) {
@@ -465,11 +542,20 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     const bool netcdf = q.path.compare(0, 7, "NETCDF:") == 0 ||
                         (q.path.size() >= 3 && q.path.compare(q.path.size() - 3, 3, ".nc") == 0);
     auto it = d.reg.find({q.path, q.band});
+    if (it != d.reg.end() && it->second.fsize >= 0) {   // ingested from a file: re-read it if it changed
+      int64_t mt = 0, sz = 0;
+      if (!file_stamp(q.path, mt, sz) || mt != it->second.mtime_ns || sz != it->second.fsize) {
+        release(it->second);
+        d.reg.erase(it);
+        it = d.reg.end();
+      }
+    }
     if (it == d.reg.end() && (netcdf || is_geotiff_path(q.path))) {   // GDALOpenEx of a file nobody registered
       const int irc = netcdf ? ingest_netcdf_locked(d, q.path, q.band) : ingest_geotiff_locked(d, q.path, q.band);
       if (irc == 2) { r.rc = 2; continue; }
+      if (irc < 0) { r.rc = irc; continue; }   // HBM exhausted, unsupported encoding, ...: an error, not "open failed"
       if (irc == 0) it = d.reg.find({q.path, q.band});
-      // else (no such file): the registry rule below -- a path registered
+      // else (1: no such file): the registry rule below -- a path registered
       // with other bands is an open dataset without this band (2), else 1
     }
     if (it == d.reg.end()) {
@@ -478,6 +564,7 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
       r.rc = (netcdf || !path_known) ? 1 : 2;                         // open failed / band failed
       continue;
     }
+    it->second.last_use = d.tick;                                      // pinned for this batch
     const Registered &R = it->second;
     if (!R.g.data) { r.rc = 2; continue; }                             // band failed
     if (q.geoloc) { r.rc = 3; continue; }                              // geolocation arrays: unsupported

@@ -21,7 +21,8 @@
 // geotransform from the 1-D coordinate variables as the driver computes it
 // (netcdfdataset.cpp:3504-3655: actual_range when present, y reversed when
 // increasing -- bBottomUp, rows then read south-up so row 0 is the north);
-// nodata from _FillValue / missing_value; EPSG:4326 for lon / lat axes,
+// nodata from _FillValue / missing_value / the type default and NC_BYTE
+// signedness as netCDFRasterBand sets them; EPSG:4326 for lon / lat axes,
 // else an EPSG from the grid mapping's crs_wkt / spatial_ref AUTHORITY.
 // netCDF-4 (HDF5) files are not read (no HDF5 in the image).
 //
@@ -121,11 +122,12 @@ bool parse(Tiff &t) {
       const int tag = t.u16(e), typ = t.u16(e + 2);
       const uint64_t cnt = t.big ? t.u64(e + 4) : t.u32(e + 4);
       const int tb = type_bytes(typ);
-      if (tb == 0) continue;
+      if (tb == 0 || cnt == 0) continue;   // unknown type; a tag with no value is ignored
+      if (cnt > b.size() / (uint64_t)tb) return false;   // before the multiplication can overflow
       const uint64_t inl = t.big ? 8 : 4;
       const uint64_t voff = e + (t.big ? 12 : 8);
       const uint64_t data = (uint64_t)tb * cnt <= inl ? voff : (t.big ? t.u64(voff) : t.u32(voff));
-      if (data + (uint64_t)tb * cnt > b.size()) return false;
+      if (data > b.size() || (uint64_t)tb * cnt > b.size() - data) return false;
       auto ints = [&]() {
         std::vector<uint64_t> v(cnt);
         for (uint64_t k = 0; k < cnt; k++) {
@@ -136,7 +138,12 @@ bool parse(Tiff &t) {
       };
       auto dbls = [&]() {
         std::vector<double> v(cnt);
-        for (uint64_t k = 0; k < cnt; k++) v[k] = typ == 12 ? t.f64(data + 8 * k) : (double)ints()[k];
+        if (typ == 12) {
+          for (uint64_t k = 0; k < cnt; k++) v[k] = t.f64(data + 8 * k);
+        } else {
+          const std::vector<uint64_t> iv = ints();
+          for (uint64_t k = 0; k < cnt; k++) v[k] = (double)iv[k];
+        }
         return v;
       };
       switch (tag) {
@@ -169,6 +176,13 @@ bool parse(Tiff &t) {
     }
     if (d.width <= 0 || d.height <= 0 || d.block_w <= 0 || d.block_h <= 0 || d.offsets.empty() ||
         d.offsets.size() != d.counts.size())
+      return false;
+    // sizes a corrupt file could make absurd (every decoder buffer is sized
+    // from these): a raster side <= 2^24, a sample of 1-64 bits, <= 64
+    // samples, one decoded block <= 1 GiB
+    if (d.width > (1 << 24) || d.height > (1 << 24) || d.block_w > (1 << 24) || d.block_h > (1 << 24) ||
+        d.bits <= 0 || d.bits > 64 || d.spp <= 0 || d.spp > 64 ||
+        (uint64_t)d.block_w * (uint64_t)d.block_h * (uint64_t)d.spp * (uint64_t)((d.bits + 7) / 8) > (1ull << 30))
       return false;
     t.ifds.push_back(std::move(d));
     off = t.big ? t.u64(off + hdr + n * esz) : t.u32(off + hdr + n * esz);
@@ -354,6 +368,7 @@ bool decode_band(const Tiff &t, const Ifd &d, int band, uint8_t *stage) {
   std::atomic<bool> ok(true);
   const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   auto work = [&]() {
+   try {   // an exception may not leave a std::thread (std::terminate)
     std::vector<uint8_t> blk((size_t)L.bw * L.bh * L.samples * bytes);
     for (int64_t i = next++; i < nblk && ok; i = next++) {
       // strips: the last one holds only the image's remaining rows
@@ -367,6 +382,9 @@ bool decode_band(const Tiff &t, const Ifd &d, int band, uint8_t *stage) {
           std::memcpy(dst + k * bytes, blk.data() + ((size_t)k * L.samples + band) * bytes, bytes);
       }
     }
+   } catch (...) {
+    ok = false;
+   }
   };
   std::vector<std::thread> th;
   for (unsigned k = 1; k < std::min<unsigned>(nth, (unsigned)std::max<int64_t>(1, nblk)); k++) th.emplace_back(work);
@@ -502,7 +520,7 @@ int open_level(const char *path, int band, int level, Tiff &t, const Ifd *&d) {
 
 using namespace gsky;
 
-extern "C" int gskyhip_geotiff_info(const char *path, gskyhip_raster_info *info) {
+static int geotiff_info_impl(const char *path, gskyhip_raster_info *info) {
   if (!path || !info) return GSKYHIP_E_ARG;
   Tiff t;
   if (!read_file(path, t.buf)) return 1;
@@ -510,7 +528,15 @@ extern "C" int gskyhip_geotiff_info(const char *path, gskyhip_raster_info *info)
   return fill_info(t, info);
 }
 
-extern "C" int gskyhip_geotiff_read_host(const char *path, int band, int level, void *out, int64_t out_bytes) {
+extern "C" int gskyhip_geotiff_info(const char *path, gskyhip_raster_info *info) {
+  try {
+    return geotiff_info_impl(path, info);
+  } catch (...) {   // a malformed file (bad_alloc of a size it declares): never through the C ABI
+    return GSKYHIP_E_TYPE;
+  }
+}
+
+static int geotiff_read_host_impl(const char *path, int band, int level, void *out, int64_t out_bytes) {
   Tiff t;
   const Ifd *d = nullptr;
   int rc = open_level(path, band, level, t, d);
@@ -524,7 +550,15 @@ extern "C" int gskyhip_geotiff_read_host(const char *path, int band, int level, 
   return 0;
 }
 
-extern "C" int gskyhip_geotiff_read(const char *path, int band, int level, void *dev_out, int64_t out_bytes,
+extern "C" int gskyhip_geotiff_read_host(const char *path, int band, int level, void *out, int64_t out_bytes) {
+  try {
+    return geotiff_read_host_impl(path, band, level, out, out_bytes);
+  } catch (...) {   // a malformed file (bad_alloc of a size it declares): never through the C ABI
+    return GSKYHIP_E_TYPE;
+  }
+}
+
+static int geotiff_read_impl(const char *path, int band, int level, void *dev_out, int64_t out_bytes,
                                     void *stream) {
   Tiff t;
   const Ifd *d = nullptr;
@@ -557,6 +591,15 @@ extern "C" int gskyhip_geotiff_read(const char *path, int band, int level, void 
   if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GSKYHIP_E_HIP;
   hipHostFree(host);
   return rc;
+}
+
+extern "C" int gskyhip_geotiff_read(const char *path, int band, int level, void *dev_out, int64_t out_bytes,
+                                    void *stream) {
+  try {
+    return geotiff_read_impl(path, band, level, dev_out, out_bytes, stream);
+  } catch (...) {   // a malformed file (bad_alloc of a size it declares): never through the C ABI
+    return GSKYHIP_E_TYPE;
+  }
 }
 
 // ======================================================================== netCDF classic
@@ -662,6 +705,7 @@ bool nc_parse(Nc &f) {
   uint32_t tag = c.u32();
   uint64_t n = ver == 5 ? c.u64() : c.u32();
   if (tag == 0x0A) {
+    if (n > b.size()) return false;
     for (uint64_t i = 0; i < n && c.ok; i++) {
       std::string nm = c.name(ver);
       const uint64_t len = ver == 5 ? c.u64() : c.u32();
@@ -675,11 +719,13 @@ bool nc_parse(Nc &f) {
   tag = c.u32();
   n = ver == 5 ? c.u64() : c.u32();
   if (tag != 0x0B && !(tag == 0 && n == 0)) return false;
+  if (n > b.size()) return false;
   for (uint64_t i = 0; i < n && c.ok; i++) {
     NcVar v;
     v.name = c.name(ver);
     const uint64_t nd = ver == 5 ? c.u64() : c.u32();
-    for (uint64_t k = 0; k < nd; k++) v.dims.push_back((int)(ver == 5 ? c.u64() : c.u32()));
+    if (nd > 64) return false;   // a corrupt count: NC_MAX_VAR_DIMS is 1024, a raster has <= 3
+    for (uint64_t k = 0; k < nd && c.ok; k++) v.dims.push_back((int)(ver == 5 ? c.u64() : c.u32()));
     if (!nc_atts(c, ver, v.atts)) return false;
     v.type = (int)c.u32();
     v.vsize = ver == 5 ? c.u64() : c.u32();
@@ -764,12 +810,91 @@ int nc_open_raster(const char *path, NcRaster &r) {
   return 0;
 }
 
-int nc_dtype(const NcVar &v, int &signed_byte) {
+// bIsGdalFile of the driver (netcdfdataset.cpp:2498-2518): a global "GDAL"
+// attribute of version >= 1.9 (NCDFIsGDALVersionGTE, 8879-8919), or
+// spatial_ref + GeoTransform on the variable's grid_mapping variable.
+bool nc_is_gdal_file(const Nc &f, const NcVar &v) {
+  auto ieq_prefix = [](const std::string &s, const char *p) {
+    size_t n = std::strlen(p);
+    if (s.size() < n) return false;
+    for (size_t i = 0; i < n; i++) if (std::tolower((unsigned char)s[i]) != std::tolower((unsigned char)p[i])) return false;
+    return true;
+  };
+  if (const NcAtt *g = nc_att(f.gatts, "GDAL")) {
+    const std::string ver(g->text.c_str());
+    if (ieq_prefix(ver, "GDAL ")) {
+      int vn = 0;
+      if (ieq_prefix(ver, "GDAL 2.0dev, released 2011/12/29") && ver.size() == 32) vn = 1100000;
+      else if (ieq_prefix(ver, "GDAL 1.9dev")) vn = 1900;
+      else if (ieq_prefix(ver, "GDAL 1.8dev")) vn = 1800;
+      else {
+        int t[4] = {0, 0, 0, 0};
+        const char *c = ver.c_str() + 5;
+        for (int k = 0; k < 4 && *c; k++) {   // CSLTokenizeString2(".", 0) + atoi, clamped to [0, 99]
+          t[k] = std::max(0, std::min(99, std::atoi(c)));
+          const char *d = std::strchr(c, '.');
+          if (!d) break;
+          c = d + 1;
+        }
+        vn = (t[0] > 1 || t[1] >= 10) ? t[0] * 1000000 + t[1] * 10000 + t[2] * 100
+                                      : t[0] * 1000 + t[1] * 100 + t[2] * 10 + t[3];
+      }
+      if (1900 <= vn) return true;
+    }
+  }
+  if (const NcAtt *gm = nc_att(v.atts, "grid_mapping"))
+    for (const NcVar &m : f.vars)
+      if (m.name == std::string(gm->text.c_str()) && nc_att(m.atts, "spatial_ref") && nc_att(m.atts, "GeoTransform"))
+        return true;
+  return false;
+}
+
+// Data type, signedness and nodata of a variable as netCDFRasterBand sets
+// them (netcdfdataset.cpp:386-559): nodata from _FillValue, else
+// missing_value, else NCDFGetDefaultNoDataValue (10182-10225) -- always set;
+// NC_BYTE is PIXELTYPE=SIGNEDBYTE unless the file was written by GDAL,
+// valid_range {0,255} / {-128,127} decides when present, else _Unsigned; an
+// unsigned byte's negative nodata gets +256.
+int nc_dtype(const Nc &f, const NcVar &v, int &signed_byte, double &nodata) {
   signed_byte = 0;
+  const NcAtt *fv = nc_att(v.atts, "_FillValue");
+  if (!fv) fv = nc_att(v.atts, "missing_value");
+  if (fv && !fv->num.empty()) {
+    nodata = fv->num[0];
+  } else {
+    switch (v.type) {
+      case 3: nodata = -32767.0; break;                  // NC_FILL_SHORT
+      case 4: nodata = -2147483647.0; break;             // NC_FILL_INT
+      case 5: nodata = (double)9.9692099683868690e+36f; break;   // NC_FILL_FLOAT
+      case 6: nodata = 9.9692099683868690e+36; break;    // NC_FILL_DOUBLE
+      case 8: nodata = 65535.0; break;                   // NC_FILL_USHORT
+      case 9: nodata = 4294967295.0; break;              // NC_FILL_UINT
+      default: nodata = 0.0; break;                      // bytes, chars
+    }
+  }
   switch (v.type) {
-    case 1: {   // NC_BYTE: GDAL Byte with PIXELTYPE=SIGNEDBYTE unless _Unsigned = "true"
-      const NcAtt *u = nc_att(v.atts, "_Unsigned");
-      signed_byte = (u && (u->text == "true" || u->text == "TRUE")) ? 0 : 1;
+    case 1: {   // NC_BYTE
+      bool sgn = !nc_is_gdal_file(f, v);
+      if (!sgn && nodata < 0) nodata += 256;
+      const NcAtt *vr = nc_att(v.atts, "valid_range");
+      if (vr && vr->num.size() == 2) {   // HONOUR_VALID_RANGE defaults to true; nc_get_att_int
+        const int lo = (int)vr->num[0], hi = (int)vr->num[1];
+        if (lo == 0 && hi == 255) {
+          sgn = false;
+          if (nodata < 0) nodata += 256;
+        } else if (lo == -128 && hi == 127) {
+          sgn = true;
+        }
+      } else {
+        if (const NcAtt *u = nc_att(v.atts, "_Unsigned")) {
+          std::string t(u->text.c_str());
+          for (auto &ch : t) ch = (char)std::tolower((unsigned char)ch);
+          if (t == "true") sgn = false;
+          else if (t == "false") sgn = true;
+        }
+        if (!sgn && nodata < 0) nodata += 256;
+      }
+      signed_byte = sgn ? 1 : 0;
       return GSKYHIP_BYTE;
     }
     case 7: return GSKYHIP_BYTE;
@@ -808,7 +933,8 @@ int nc_fill_info(const NcRaster &r, gskyhip_raster_info *info) {
   std::memset(info, 0, sizeof(*info));
   const NcVar &v = *r.v;
   int sb = 0;
-  info->dtype = nc_dtype(v, sb);
+  double nodata = 0.0;
+  info->dtype = nc_dtype(r.f, v, sb, nodata);
   if (!info->dtype) return GSKYHIP_E_TYPE;
   info->signed_byte = sb;
   info->xsize = (int32_t)r.nx; info->ysize = (int32_t)r.ny; info->n_bands = (int32_t)r.nb;
@@ -848,10 +974,8 @@ int nc_fill_info(const NcRaster &r, gskyhip_raster_info *info) {
     if (!node_offset) { g[0] -= g[1] / 2; g[3] -= g[5] / 2; }
   }
   info->epsg = nc_epsg(f, v);
-  info->nodata = -1e10;
-  const NcAtt *fv = nc_att(v.atts, "_FillValue");
-  if (!fv) fv = nc_att(v.atts, "missing_value");
-  if (fv && !fv->num.empty()) { info->nodata = fv->num[0]; info->has_nodata = 1; }
+  info->nodata = nodata;   // netCDFRasterBand::SetNoDataValue, always (netcdfdataset.cpp:558)
+  info->has_nodata = 1;
   return 0;
 }
 
@@ -892,14 +1016,22 @@ __global__ __launch_bounds__(256) void byteswap_kernel(W *__restrict__ v, int64_
 }  // namespace
 }  // namespace gsky
 
-extern "C" int gskyhip_netcdf_info(const char *path, gskyhip_raster_info *info) {
+static int netcdf_info_impl(const char *path, gskyhip_raster_info *info) {
   if (!path || !info) return GSKYHIP_E_ARG;
   NcRaster r;
   const int rc = nc_open_raster(path, r);
   return rc ? rc : nc_fill_info(r, info);
 }
 
-extern "C" int gskyhip_netcdf_read_host(const char *path, int band, void *out, int64_t out_bytes) {
+extern "C" int gskyhip_netcdf_info(const char *path, gskyhip_raster_info *info) {
+  try {
+    return netcdf_info_impl(path, info);
+  } catch (...) {   // a malformed file (bad_alloc of a size it declares): never through the C ABI
+    return GSKYHIP_E_TYPE;
+  }
+}
+
+static int netcdf_read_host_impl(const char *path, int band, void *out, int64_t out_bytes) {
   NcRaster r;
   int rc = nc_open_raster(path, r);
   if (rc) return rc;
@@ -909,7 +1041,15 @@ extern "C" int gskyhip_netcdf_read_host(const char *path, int band, void *out, i
   return nc_read_rows(r, band - 1, (uint8_t *)out, true) ? 0 : GSKYHIP_E_ARG;
 }
 
-extern "C" int gskyhip_netcdf_read(const char *path, int band, void *dev_out, int64_t out_bytes, void *stream) {
+extern "C" int gskyhip_netcdf_read_host(const char *path, int band, void *out, int64_t out_bytes) {
+  try {
+    return netcdf_read_host_impl(path, band, out, out_bytes);
+  } catch (...) {   // a malformed file (bad_alloc of a size it declares): never through the C ABI
+    return GSKYHIP_E_TYPE;
+  }
+}
+
+static int netcdf_read_impl(const char *path, int band, void *dev_out, int64_t out_bytes, void *stream) {
   NcRaster r;
   int rc = nc_open_raster(path, r);
   if (rc) return rc;
@@ -932,4 +1072,12 @@ extern "C" int gskyhip_netcdf_read(const char *path, int band, void *dev_out, in
   if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GSKYHIP_E_HIP;
   hipHostFree(host);
   return rc;
+}
+
+extern "C" int gskyhip_netcdf_read(const char *path, int band, void *dev_out, int64_t out_bytes, void *stream) {
+  try {
+    return netcdf_read_impl(path, band, dev_out, out_bytes, stream);
+  } catch (...) {   // a malformed file (bad_alloc of a size it declares): never through the C ABI
+    return GSKYHIP_E_TYPE;
+  }
 }

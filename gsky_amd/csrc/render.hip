@@ -43,6 +43,7 @@ struct PlanArgs {
   int32_t *order;              // n_pairs: per tile, stack entries in merge order
   int32_t *pair_tile;          // n_pairs: owning tile of each pair
   RowRec *rows;                // n_pairs * max_h
+  RowFix *rowfix;              // n_pairs * max_h: fixed-point form of `inside` LINEAR rows
   Leaf *pool;
   int32_t *counters;           // [0] pool, [1] split rows, [2] complex tiles
   int pool_cap;
@@ -1126,6 +1127,7 @@ __device__ __forceinline__ void plan_row(const PlanArgs &a, int p, const PairPla
     }
   }
   a.rows[(long)p * a.max_h + row] = rec;
+  a.rowfix[(long)p * a.max_h + row] = row_fix(rec, n);
 }
 
 // Workgroups of one pair (blockIdx.x: pair, blockIdx.y: 256-row chunk): the
@@ -1548,7 +1550,7 @@ static inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 struct Carve {
   PairPlan *pairs; Xform *xforms; TilePlan *tplans; int32_t *order; int32_t *pair_tile;
-  RowRec *rows; Leaf *pool; int32_t *counters; MinMax *minmax; int64_t *split_list; int32_t *complex_list;
+  RowRec *rows; RowFix *rowfix; Leaf *pool; int32_t *counters; MinMax *minmax; int64_t *split_list; int32_t *complex_list;
   EntryD *entries;
   SepCol *sepcols;
   int pool_cap;
@@ -1569,6 +1571,7 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   const int64_t o_ord = take(sizeof(int32_t) * (int64_t)np);
   const int64_t o_pt = take(sizeof(int32_t) * (int64_t)np);
   const int64_t o_rows = take(sizeof(RowRec) * (int64_t)np * max_h);
+  const int64_t o_rfix = take(sizeof(RowFix) * (int64_t)np * max_h);
   const int64_t o_pool = take(sizeof(Leaf) * (int64_t)c.pool_cap);
   const int64_t o_cnt = take(256);
   const int64_t o_mm = take(sizeof(MinMax) * (int64_t)nt * 3);
@@ -1584,6 +1587,7 @@ static Carve carve(void *base, int n_tiles, int n_pairs, int max_h) {
   c.order = (int32_t *)(b + o_ord);
   c.pair_tile = (int32_t *)(b + o_pt);
   c.rows = (RowRec *)(b + o_rows);
+  c.rowfix = (RowFix *)(b + o_rfix);
   c.pool = (Leaf *)(b + o_pool);
   c.counters = (int32_t *)(b + o_cnt);
   c.minmax = (MinMax *)(b + o_mm);
@@ -1612,7 +1616,7 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   a.tiles = rc.tiles; a.n_tiles = rc.n_tiles; a.pair_granule = rc.pair_granule; a.n_pairs = rc.n_pairs;
   a.pair_tile_max = 0; a.max_h = rc.max_h; a.max_w = rc.max_w; a.mask_ns = rc.mask_ns; a.mask_inclusive = rc.mask_inclusive;
   a.pairs = cv.pairs; a.xforms = cv.xforms; a.tplans = cv.tplans; a.order = cv.order;
-  a.pair_tile = cv.pair_tile; a.rows = cv.rows; a.pool = cv.pool; a.counters = cv.counters;
+  a.pair_tile = cv.pair_tile; a.rows = cv.rows; a.rowfix = cv.rowfix; a.pool = cv.pool; a.counters = cv.counters;
   a.pool_cap = cv.pool_cap; a.split_list = cv.split_list; a.complex_list = cv.complex_list;
   a.entries = cv.entries;
   a.sepcols = cv.sepcols;
@@ -1713,7 +1717,7 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   }
   RenderArgs a;
   a.pairs = cv.pairs; a.xforms = cv.xforms; a.tplans = cv.tplans; a.order = cv.order;
-  a.tiles = rc.tiles; a.rows = cv.rows; a.pool = cv.pool; a.counters = cv.counters;
+  a.tiles = rc.tiles; a.rows = cv.rows; a.rowfix = cv.rowfix; a.pool = cv.pool; a.counters = cv.counters;
   a.complex_list = cv.complex_list; a.max_h = rc.max_h; a.max_w = rc.max_w;
   a.n_tiles = rc.n_tiles; a.rows_per_block = 16; a.n_out = n_out;
   for (int k = 0; k < 3; k++) a.out_ns[k] = k < n_out ? out_ns[k] : -1;

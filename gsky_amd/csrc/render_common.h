@@ -190,6 +190,7 @@ struct RenderArgs {
   const int32_t *order;
   const gskyhip_tile *tiles;
   const RowRec *rows;
+  const RowFix *rowfix;  // fixed-point form of `inside` LINEAR rows (render_nn.h)
   const Leaf *pool;
   const int32_t *counters;
   const int32_t *complex_list;

@@ -46,6 +46,12 @@ constexpr uint32_t kNoPx = 0xFFFFFFFFu;
 constexpr int kNnRows = 4;   // rows per wave (a block: 4 waves x 4 rows = kBandRows)
 constexpr int kNnPx = 8;     // pixels per lane per row, 64 columns apart
 
+// a wave-uniform 64-bit value in scalar registers
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // nn_px() of source coordinates (sx, sy): the element index, or kNoPx where
 // the reference's window fill applies.
 __device__ __forceinline__ uint32_t nn_index_sxy(double sx, double sy, bool ok, int bx, int by) {
@@ -103,14 +109,75 @@ __device__ __forceinline__ void nn_partial_row(__amdgpu_buffer_rsrc_t rs, double
   }
 }
 
+// The fold of one `inside` LINEAR row from its fixed-point form (RowFix,
+// gsky_device.h): per pixel two 64-bit integer adds per axis in place of the
+// fp64 multiply, two adds and the conversion of each axis.  The source pixel
+// is the integer part wherever the fraction is at least kFixMargin from an
+// integer -- there it equals the truncation of the reference's fp64
+// expression; if any pixel of the wave's row is closer (about 1 row in 250),
+// nothing is folded and false sends the row to the fp64 bodies.
+// PART: the window edge falls inside the block (pixels outside the window
+// read nothing and fold nothing).
+template <typename T, int NPX, bool PART>
+__device__ __forceinline__ bool nn_fix_row(__amdgpu_buffer_rsrc_t rs, int64_t fx0, int64_t fy0, int64_t fdx,
+                                           int64_t fdy, int ic0, int lim, int bx, typename VOf<T>::type nd,
+                                           bool fill_mode, typename VOf<T>::type (&c)[NPX]) {
+  using V = typename VOf<T>::type;
+  uint64_t X = (uint64_t)(fx0 + (int64_t)ic0 * fdx), Y = (uint64_t)(fy0 + (int64_t)ic0 * fdy);
+  const uint64_t SX = (uint64_t)fdx << 6, SY = (uint64_t)fdy << 6;   // 64 columns
+  uint32_t amin = 0xFFFFFFFFu;
+  uint32_t off[NPX];
+#pragma unroll
+  for (int q = 0; q < NPX; q++) {
+    const uint32_t ix = (uint32_t)(X >> 32), iy = (uint32_t)(Y >> 32);
+    uint32_t a = min((uint32_t)X + kFixMargin, (uint32_t)Y + kFixMargin);
+    off[q] = (__umul24(iy, (uint32_t)bx) + ix) * (uint32_t)sizeof(T);
+    if constexpr (PART) {
+      const bool inw = (unsigned)(ic0 + 64 * q) < (unsigned)lim;
+      off[q] = inw ? off[q] : 0x80000000u;
+      a = inw ? a : 0xFFFFFFFFu;
+    }
+    amin = min(amin, a);
+    // keep the offset here: sunk below the test, it would hold every X, Y
+    // (32 VGPRs) live across it and spill at 8 waves per SIMD
+    asm volatile("" : "+v"(off[q]));
+    X += SX;
+    Y += SY;
+  }
+  // the test comes before the loads: a load left unconsumed on the fallback
+  // path would make the compiler drain vmcnt -- the previous row's RGBA
+  // stores included -- before the next use of its register
+  if (__builtin_amdgcn_ballot_w64(amin < 2u * kFixMargin) != 0) return false;
+  V vv[NPX];
+#pragma unroll
+  for (int q = 0; q < NPX; q++) vv[q] = buf_load<T>(rs, off[q]);
+  if (!fill_mode) {
+#pragma unroll
+    for (int q = 0; q < NPX; q++) {
+      bool take = vv[q] != nd;
+      if constexpr (PART) take = take & ((unsigned)(ic0 + 64 * q) < (unsigned)lim);
+      c[q] = take ? vv[q] : c[q];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NPX; q++) {
+      bool take = c[q] == nd;
+      if constexpr (PART) take = take & ((unsigned)(ic0 + 64 * q) < (unsigned)lim);
+      c[q] = take ? vv[q] : c[q];
+    }
+  }
+  return true;
+}
+
 // One stack entry e of the ordered fold of tile row r (MergeMaskedRaster,
 // tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
 // (tile column xl + 64 q).
 // PARTIAL: with the window-edge body for `inside` rows (the single-entry path
 // of render_nn_kernel has its own and passes false).
-template <typename T, bool MASK, int NPX = kNnPx, bool PARTIAL = true>
+template <typename T, bool MASK, int NPX = kNnPx, bool PARTIAL = true, bool FIX = true>
 __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
-                                             const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
+                                             const RowRec *__restrict__ rows, const RowFix *__restrict__ rowfix,
+                                             const Leaf *__restrict__ pool,
                                              int ns_out, int r, int xb, int xl, int W, int ncols,
                                              typename VOf<T>::type (&c)[NPX]) {
   using V = typename VOf<T>::type;
@@ -121,9 +188,6 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   const int lim = max(0, min(ew, W - exoff));   // window pixel in the tile: (unsigned)ic < lim
   const int c0 = exoff - xb, c1 = exoff + lim - xb;   // the entry's columns of the block: [c0, c1)
   if (c1 <= 0 || c0 >= ncols) return;
-  const RowRec *rr = rows + e.row_base + ir;
-  const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
-  const int inside = __builtin_amdgcn_readfirstlane(rr->inside);
   const int bx = e.band_x, by = e.band_y;
   const V nd = as_v<T>(e.nd);
   const bool fill_mode = e.fill_mode != 0;
@@ -131,6 +195,20 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
   const bool masked = MASK && e.mask_pair >= 0;
+  if (FIX && !masked) {   // fixed-point form of an `inside` LINEAR row
+    const RowFix *fp = rowfix + e.row_base + ir;
+    const int64_t fx0 = uni64(fp->x0);
+    if (fx0 != kFixNone) {
+      const int64_t fy0 = uni64(fp->y0), fdx = uni64(fp->dx), fdy = uni64(fp->dy);
+      const bool done = (c0 <= 0 && c1 >= ncols)
+                            ? nn_fix_row<T, NPX, false>(rs, fx0, fy0, fdx, fdy, ic0, lim, bx, nd, fill_mode, c)
+                            : nn_fix_row<T, NPX, true>(rs, fx0, fy0, fdx, fdy, ic0, lim, bx, nd, fill_mode, c);
+      if (done) return;
+    }
+  }
+  const RowRec *rr = rows + e.row_base + ir;
+  const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
+  const int inside = __builtin_amdgcn_readfirstlane(rr->inside);
   if (kind == ROW_LINEAR && inside && c0 <= 0 && c1 >= ncols && !masked) {
     // fast body: every pixel of the block is in the window and its source
     // pixel in the band -- lin_coords() + nn_px() reduce to the truncations
@@ -212,12 +290,13 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
 template <typename T, bool MASK>
 __device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *__restrict__ ents,
                                             const int32_t *__restrict__ ord, int n_entries,
-                                            const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
+                                            const RowRec *__restrict__ rows, const RowFix *__restrict__ rowfix,
+                                            const Leaf *__restrict__ pool,
                                             int ns_out, int r, int xb, int xl, int W, int ncols,
                                             typename VOf<T>::type (&c)[kNnPx]) {
 #pragma unroll 1
   for (int k = 0; k < n_entries; k++)
-    nn_entry_row<T, MASK>(a, ents, ents[ord[k]], rows, pool, ns_out, r, xb, xl, W, ncols, c);
+    nn_entry_row<T, MASK>(a, ents, ents[ord[k]], rows, rowfix, pool, ns_out, r, xb, xl, W, ncols, c);
 }
 
 // utils.Scale + palette / grey of the lane's 8 canvas values (EncodePNG's
@@ -251,6 +330,7 @@ template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, bool ST
 __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
+                                                                      const RowFix *__restrict__ rowfix,
                                                                       const Leaf *__restrict__ pool,
                                                                       const TilePlan *__restrict__ tplans,
                                                                       const gskyhip_tile *__restrict__ tiles,
@@ -345,56 +425,56 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
       const int ic0 = xl - exoff;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
-      const RowRec *rbase = rows + e.row_base;
-      auto fetch = [&](int ir, double (&v)[4], int &ki) {   // kind | inside << 8, or -1 outside the window
-        if (ir < 0 || ir >= eh) { ki = -1; return; }
-        const RowRec *p = rbase + ir;
-        v[0] = p->v[0]; v[1] = p->v[1]; v[2] = p->v[2]; v[3] = p->v[3];
-        ki = __builtin_amdgcn_readfirstlane(p->kind) | (__builtin_amdgcn_readfirstlane(p->inside) << 8);
+      const RowFix *fbase = rowfix + e.row_base;
+      // the row's fixed-point form, or fk = -1 outside the window / 0 none
+      auto fetch = [&](int ir, int64_t (&f)[4], int &fk) {
+        if (ir < 0 || ir >= eh) { fk = -1; return; }
+        const RowFix *p = fbase + ir;
+        f[0] = uni64(p->x0); f[1] = uni64(p->y0); f[2] = uni64(p->dx); f[3] = uni64(p->dy);
+        fk = f[0] != kFixNone ? 1 : 0;
       };
-      double cv[4] = {0, 0, 0, 0}, nv[4] = {0, 0, 0, 0};
-      int cki = -1, nki = -1;
-      if (cols_ok) fetch(r0 - eyoff, cv, cki);
+      int64_t cf[4] = {0, 0, 0, 0}, nf[4] = {0, 0, 0, 0};
+      int cfk = -1, nfk = -1;
+      // rows left to the fp64 bodies (no fixed form, or a pixel near a
+      // truncation boundary): done in a second loop, so that loop's loads do
+      // not reach the register and wait-count state of this one
+      uint32_t redo = 0;
+      if (cols_ok) fetch(r0 - eyoff, cf, cfk);
 #pragma unroll 1
       for (int j = 0; j < RPW; j++) {
         const int r = r0 + j;
         if (r >= H) break;
-        if (cols_ok && j + 1 < RPW) fetch(r + 1 - eyoff, nv, nki);   // next row's record, in flight now
+        if (cols_ok && j + 1 < RPW) fetch(r + 1 - eyoff, nf, nfk);   // next row's record, in flight now
         V c[kNnPx];
 #pragma unroll
         for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-        if (cki >= 0) {
-          if ((cki & 0xFF) == ROW_LINEAR && (cki >> 8) && cover) {
-            uint32_t off[kNnPx];
-#pragma unroll
-            for (int q = 0; q < kNnPx; q++) {
-              const double dist = (double)(ic0 + 64 * q);
-              const int ix = __double2int_rz(cv[0] + cv[2] * dist + 1.0e-10);
-              const int iy = __double2int_rz(cv[1] + cv[3] * dist + 1.0e-10);
-              off[q] = (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T);
-            }
-            V vv[kNnPx];
-#pragma unroll
-            for (int q = 0; q < kNnPx; q++) vv[q] = buf_load<T>(rs, off[q]);
-            if (!fill_mode) {
-#pragma unroll
-              for (int q = 0; q < kNnPx; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
-            } else {
-#pragma unroll
-              for (int q = 0; q < kNnPx; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
-            }
-          } else if ((cki & 0xFF) == ROW_LINEAR && (cki >> 8)) {
-            nn_partial_row<T, kNnPx>(rs, cv[0], cv[1], cv[2], cv[3], ic0, lim, bx, nd, fill_mode, c0, c1, c);
-          } else {
-            nn_entry_row<T, false, kNnPx, false>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
-          }
+        bool done = cfk < 0;
+        if (cfk == 1)
+          done = cover ? nn_fix_row<T, kNnPx, false>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c)
+                       : nn_fix_row<T, kNnPx, true>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c);
+        if (done) {
+          uint32_t px[kNnPx];
+          rgba(c, px);
+          store_row(r, px);
+        } else {
+          redo |= 1u << j;
         }
+#pragma unroll
+        for (int k = 0; k < 4; k++) cf[k] = nf[k];
+        cfk = nfk;
+      }
+#pragma unroll 1
+      while (redo) {
+        const int j = __builtin_ctz(redo);
+        redo &= redo - 1;
+        const int r = r0 + j;
+        V c[kNnPx];
+#pragma unroll
+        for (int q = 0; q < kNnPx; q++) c[q] = cnod;
+        nn_entry_row<T, false, kNnPx, true, false>(a, ents, e, rows, rowfix, pool, ns_out, r, xb, xl, W, ncols, c);
         uint32_t px[kNnPx];
         rgba(c, px);
         store_row(r, px);
-#pragma unroll
-        for (int k = 0; k < 4; k++) cv[k] = nv[k];
-        cki = nki;
       }
       return;
     }
@@ -406,7 +486,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
     V c[kNnPx];
 #pragma unroll
     for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-    nn_fold_row<T, MASK>(a, ents, ord, n_entries, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+    nn_fold_row<T, MASK>(a, ents, ord, n_entries, rows, rowfix, pool, ns_out, r, xb, xl, W, ncols, c);
 
     // output: typed canvas (WCS) or utils.Scale + palette / grey RGBA
     if constexpr (CANVAS) {
@@ -436,7 +516,7 @@ template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = fa
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
   hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
-                     a.order, a.rows, a.pool, a.tplans, a.tiles, items);
+                     a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
 
 // render_nn_stage.h (included by the per-type translation units)

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256, 8) void render_nn_stage_kernel(RenderArgs a, c
     for (int k = 0; k < n_entries; k++) {
       const EntryD &e = ents[ord[k]];
       if (k >= n_st || !s_ent[k].staged) {
-        nn_entry_row<T, false, kStPx>(a, ents, e, rows, pool, ns_out, r, xb, xl, W, ncols, c);
+        nn_entry_row<T, false, kStPx>(a, ents, e, rows, a.rowfix, pool, ns_out, r, xb, xl, W, ncols, c);
         continue;
       }
       const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;

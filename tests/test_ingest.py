@@ -387,7 +387,9 @@ def test_netcdf_time_bands(tmp_path, record):
     p = str(tmp_path / "t.nc")
     _write_nc(p, "sm", data, np.arange(nx) * 1.0, lat, time=np.arange(nt), record=record)
     inf = ingest.info(p)
-    assert inf.n_bands == nt and inf.nodata is None
+    # no _FillValue / missing_value: the driver's NCDFGetDefaultNoDataValue
+    # (netcdfdataset.cpp:420-430, 10182-10225), NC_FILL_SHORT for a short
+    assert inf.n_bands == nt and inf.nodata == -32767.0
     for b in range(nt):
         assert np.array_equal(ingest.read_host(p, b + 1), data[b]), b
     from gsky_amd import GskyError
@@ -414,6 +416,122 @@ def test_netcdf_projected_grid_mapping(tmp_path):
     inf = ingest.info(p)
     assert inf.epsg == 3577 and inf.geot == (1400000.0, 25.0, 0.0, -3800000.0, 0.0, -25.0)
     assert np.array_equal(ingest.read_host("NETCDF:%s:band" % p), data)
+
+
+@pytest.mark.parametrize("dt,exp", [(np.int16, -32767.0), (np.int32, -2147483647.0),
+                                    (np.float32, float(np.float32(9.9692099683868690e+36))),
+                                    (np.float64, 9.9692099683868690e+36), (np.int8, 0.0)])
+def test_netcdf_default_nodata(tmp_path, dt, exp):
+    """A variable without _FillValue / missing_value still gets the driver's
+    default fill value as its nodata (netcdfdataset.cpp:420-430, 558)."""
+    p = str(tmp_path / "d.nc")
+    _write_nc(p, "v", np.zeros((4, 6), dt), np.arange(6) * 1.0, -np.arange(4) * 1.0)
+    assert ingest.info(p).nodata == exp
+
+
+@pytest.mark.parametrize("attrs,gdal,signed,nodata", [
+    ({}, False, True, -1.0),                                   # netCDF bytes are signed
+    ({"_Unsigned": b"true"}, False, False, 255.0),             # _Unsigned, nodata + 256
+    ({"_Unsigned": b"FALSE"}, False, True, -1.0),
+    ({"valid_range": np.array([0, 255], np.int16)}, False, False, 255.0),
+    ({"valid_range": np.array([-128, 127], np.int16), "_Unsigned": b"true"}, False, True, -1.0),
+    ({}, True, False, 255.0),                                  # a GDAL-written file: unsigned
+    ({"valid_range": np.array([-128, 127], np.int16)}, True, True, 255.0),
+])
+def test_netcdf_byte_signedness(tmp_path, attrs, gdal, signed, nodata):
+    """NC_BYTE signedness and nodata as netCDFRasterBand decides them
+    (netcdfdataset.cpp:466-541): signed unless the file was written by GDAL
+    (a "GDAL" global attribute >= 1.9, 2498-2518, 8879-8919); valid_range
+    {0,255} / {-128,127} decides when present, else _Unsigned; an unsigned
+    band's negative nodata gets +256 (once the signedness is known -- the
+    GDAL-file rule's own +256 stays when valid_range later says signed)."""
+    from scipy.io import netcdf_file
+    p = str(tmp_path / "b.nc")
+    with netcdf_file(p, "w") as f:
+        if gdal:
+            f.GDAL = b"GDAL 3.0.1, released 2019/06/28"
+        f.createDimension("lat", 3)
+        f.createDimension("lon", 4)
+        f.createVariable("lon", "f8", ("lon",))[:] = np.arange(4) * 1.0
+        f.createVariable("lat", "f8", ("lat",))[:] = -np.arange(3) * 1.0
+        v = f.createVariable("v", "b", ("lat", "lon"))
+        v._FillValue = np.int8(-1)
+        for k, val in attrs.items():
+            setattr(v, k, val)
+        v[:] = np.zeros((3, 4), np.int8)
+    inf = ingest.info(p)
+    assert inf.signed_byte == signed and inf.nodata == nodata
+
+
+def _tiff_le(entries, extra=b""):
+    """A minimal little-endian classic TIFF: one IFD of (tag, type, count,
+    value-or-offset) entries at offset 8, then `extra`."""
+    import struct
+    ifd = struct.pack("<H", len(entries))
+    for tag, typ, cnt, val in entries:
+        ifd += struct.pack("<HHII", tag, typ, cnt, val)
+    ifd += struct.pack("<I", 0)
+    return b"II*\x00" + struct.pack("<I", 8) + ifd + extra
+
+
+@pytest.mark.parametrize("name,entries", [
+    ("count0", [(256, 3, 0, 0), (257, 3, 1, 4), (258, 3, 1, 8), (273, 4, 1, 200), (279, 4, 1, 16)]),
+    ("huge_count", [(256, 3, 1, 4), (257, 3, 1, 4), (258, 3, 1, 8), (273, 4, 0x40000000, 8), (279, 4, 1, 16)]),
+    ("huge_dims", [(256, 4, 1, 0xFFFFFFF0), (257, 4, 1, 0xFFFFFFF0), (258, 3, 1, 64), (273, 4, 1, 8),
+                   (279, 4, 1, 16)]),
+    ("huge_tile", [(256, 3, 1, 4), (257, 3, 1, 4), (258, 3, 1, 32), (322, 4, 1, 1 << 20), (323, 4, 1, 1 << 20),
+                   (324, 4, 1, 8), (325, 4, 1, 16)]),
+    ("offset_past_end", [(256, 3, 1, 4), (257, 3, 1, 4), (258, 3, 1, 8), (273, 4, 1, 1 << 30), (279, 4, 1, 16)]),
+    ("bits_odd", [(256, 3, 1, 4), (257, 3, 1, 4), (258, 3, 1, 12), (273, 4, 1, 8), (279, 4, 1, 16)]),
+])
+def test_malformed_tiff_is_an_error_not_a_crash(tmp_path, name, entries):
+    """Malformed headers come back as error codes through the C ABI: a tag
+    with no value, counts or sizes that would overflow or exhaust memory,
+    strips past the end of the file, unsupported sample sizes."""
+    from gsky_amd import GskyError
+    p = str(tmp_path / (name + ".tif"))
+    with open(p, "wb") as f:
+        f.write(_tiff_le(entries, b"\x00" * 64))
+    with pytest.raises(GskyError):
+        ingest.read_host(p)
+
+
+@pytest.mark.gpu
+def test_gpu_drop_in_unsupported_encoding_is_an_error(tmp_path):
+    """A file the reader cannot decode (JPEG compression) is reported as an
+    error by warp_operation_fast, not as an empty "open failed" tile; a
+    missing file stays rc 1 (warp.go:103-110)."""
+    from gsky_amd import worker
+    from gsky_amd.tiles import bbox_to_geot
+    import struct
+    p = str(tmp_path / "jpeg.tif")
+    geo = struct.pack("<3d", 1.0, 1.0, 0.0) + struct.pack("<6d", 0, 0, 0, 130.0, -20.0, 0)
+    n_ent = 9
+    data_off = 8 + 2 + 12 * n_ent + 4
+    entries = [(256, 3, 1, 16), (257, 3, 1, 16), (258, 3, 1, 8), (259, 3, 1, 7), (273, 4, 1, data_off + len(geo)),
+               (277, 3, 1, 1), (279, 4, 1, 256), (33550, 12, 3, data_off), (33922, 12, 6, data_off + 24)]
+    with open(p, "wb") as f:
+        f.write(_tiff_le(entries, geo + b"\x00" * 256))
+    worker.unregister_all()
+    req = dict(bands=[1], width=64, height=64, dstSRS="EPSG:4326",
+               dstGeot=bbox_to_geot(64, 64, (130.0, -36.0, 146.0, -20.0)))
+    r = worker.warp_raster(worker.GeoRPCGranule(path=p, **req))
+    assert r.error == "warp_operation() fail: -2", r.error
+    r = worker.warp_raster(worker.GeoRPCGranule(path=str(tmp_path / "none.tif"), **req))
+    assert r.error == "warp_operation() fail: 1", r.error
+    worker.unregister_all()
+
+
+def test_truncated_netcdf_is_an_error(tmp_path):
+    from gsky_amd import GskyError
+    p = str(tmp_path / "ok.nc")
+    _write_nc(p, "v", np.arange(24, dtype=np.int16).reshape(4, 6), np.arange(6) * 1.0, -np.arange(4) * 1.0)
+    raw = open(p, "rb").read()
+    for cut in (9, 40, 80, len(raw) // 2):
+        q = str(tmp_path / ("cut%d.nc" % cut))
+        open(q, "wb").write(raw[:cut])
+        with pytest.raises(GskyError):
+            ingest.read_host(q)
 
 
 @pytest.mark.gpu
