@@ -300,16 +300,26 @@ def run_c2(ctx: Ctx, args):
     src = sum(g.data.nbytes for g in full.granules) * cfg.out_pixels / full.out_pixels
     abytes = int(src + cfg.out_pixels * 4)
     achieved = abytes / (render_ms / 1e3) / 1e9
-    # p50 GetMap tile latency: evenly spaced tiles of the rank's block, each
-    # as its own request
-    lat_ids = list(range(0, len(ids), max(1, len(ids) // args.c2_lat_tiles)))[: args.c2_lat_tiles]
+    # p50 GetMap tile latency: tiles the index gives at least one granule
+    # (evenly spaced over those of the rank's block), each as its own
+    # request; tiles with no granule (transparent, no planning) apart
+    covered = [i for i in range(len(ids)) if cfg.pairs[i]]
+    empty = [i for i in range(len(ids)) if not cfg.pairs[i]]
+    lat_ids = [covered[k] for k in range(0, len(covered), max(1, len(covered) // args.c2_lat_tiles))][
+        : args.c2_lat_tiles]
     lat = tile_latency(ctx, cfg, gs, sp, pal, lat_ids, args.c2_lat_reps) if lat_ids else [float("nan")]
+    emp_ids = [empty[k] for k in range(0, len(empty), max(1, len(empty) // 8))][:8]
+    lat_e = tile_latency(ctx, cfg, gs, sp, pal, emp_ids, args.c2_lat_reps) if emp_ids else [float("nan")]
     out = {
         "value": round(total_px / dt / 1e6, 1), "ms_per_step": round(dt / args.steps * 1e3, 4),
         "p50_tile_ms": round(float(np.percentile(lat, 50)), 4),
         "p99_tile_ms": round(float(np.percentile(lat, 99)), 4),
-        "p50_timing": "C2 one-tile GetMap requests (%d tiles x %d reps, rank 0): host wall of plan + render + "
-                      "synchronize, granules resident in HBM" % (len(lat_ids), args.c2_lat_reps),
+        "p50_timing": "C2 one-tile GetMap requests over tiles with >= 1 granule (%d of the %d such tiles, evenly "
+                      "spaced, x %d reps, rank 0): host wall of plan + render + synchronize, granules resident in "
+                      "HBM" % (len(lat_ids), len(covered), args.c2_lat_reps),
+        "p50_empty_tile_ms": round(float(np.percentile(lat_e, 50)), 4),
+        "empty_tiles": "%d of the %d tiles have no granule (transparent RGBA, no pair planning); %d timed"
+                       % (len(empty), len(ids), len(emp_ids)),
         "config": {"workload": "C2: %d x 512x512 EPSG:3857 tiles from %d EPSG:3577 int16 4000x4000 granules, "
                                "nearest, time-ordered merge + scale + palette" % (len(full.tiles), len(full.granules)),
                    "tiles_per_step": len(full.tiles), "tiles_per_rank": len(ids), "pairs_rank0": batch.n_pairs,
@@ -518,10 +528,24 @@ def run_c4(ctx: Ctx, args):
     # decileCount = 9 (drill.go:229-273): radix selection of the picks per (polygon, slice)
     if not args.no_deciles:
         dt_dec = ctx.timed(lambda: drill.read_data(st, mb, *CLIP, decile_count=9), 3, 1)
+        k_dec = event_ms(lambda: drill.read_data(st, mb, *CLIP, decile_count=9), 3)
+        # algorithmic bytes: the mean pass (in-mask values + mask bytes) + the
+        # transpose's read of the in-mask values + its band-major write + the
+        # select's read of that copy
+        vals = inside * n_bands * 4
+        dbytes = 4 * vals + px
+        dach = dbytes / (k_dec / 1e3) / 1e9
         res["deciles"] = {"value": round(len(mine) * n_bands * 3 / dt_dec, 1), "unit": "polygon-slices/s",
                           "ms_per_step": round(dt_dec / 3 * 1e3, 3), "decile_count": 9,
                           "step": "readData with decileCount 9: mean pass + transposing gather + radix select "
-                                  "(rank 0)"}
+                                  "(rank 0)",
+                          "roofline": {"bound": "hbm", "achieved": round(dach, 1), "peak": HBM_PEAK_GBS,
+                                       "unit": "GB/s", "frac": round(dach / HBM_PEAK_GBS, 4),
+                                       "kernel_ms": round(k_dec, 4),
+                                       "kernel": "drill compaction + mean + decile transpose + select (rank 0)",
+                                       "algorithmic_bytes_per_launch": int(dbytes),
+                                       "bytes": "mean pass (in-mask values + mask) + transpose read + transpose "
+                                                "write + select read of the in-mask values"}}
     out = {"workload": "C4: WPS drill zonal mean, 1000 star polygons (GeoJSON, EPSG:4326) x 365 daily f32 slices "
                        "of 2048^2, product windows + ALL_TOUCHED masks on the GPU, clip +-MaxFloat32",
            "polygons_rank0": len(mine), "in_mask_px_rank0": inside,

@@ -52,7 +52,7 @@ class Granule(C.Structure):
                 ("ovr_data", C.c_void_p * MAX_OVR), ("ovr_xsize", C.c_int32 * MAX_OVR),
                 ("ovr_ysize", C.c_int32 * MAX_OVR), ("timestamp", C.c_double),
                 ("polygon_hash", C.c_uint32), ("block_x", C.c_int32), ("block_y", C.c_int32),
-                ("_pad2", C.c_int32)]
+                ("geoloc", C.c_int32)]
 
 
 class Tile(C.Structure):
@@ -98,7 +98,7 @@ EXPORTS = [
     "gskyhip_render_tile_info", "gskyhip_compute_reproject_extent",
     "gskyhip_service_run", "gskyhip_service_register_granule", "gskyhip_service_unregister_all",
     "gskyhip_service_stats", "gskyhip_service_shutdown", "gskyhip_drill_deciles_workspace_size",
-    "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device",
+    "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device", "gskyhip_drill_masks_device",
     "gskyhip_drill_read_data_workspace_size", "gskyhip_drill_read_data",
     "gskyhip_png_workspace_size", "gskyhip_png_bound", "gskyhip_encode_png",
     "gskyhip_geotiff_workspace_size", "gskyhip_geotiff_bound", "gskyhip_encode_geotiff",
@@ -170,6 +170,8 @@ def lib() -> C.CDLL:
     L.gskyhip_drill_merge.argtypes = [vp, vp, ci, ci, vp, vp]
     L.gskyhip_drill_descriptors_device.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci,
                                                    vp, vp, C.POINTER(i64), vp, vp, vp]
+    L.gskyhip_drill_masks_device.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci, vp, vp,
+                                             C.POINTER(i64), vp, vp, C.POINTER(vp), vp, vp]
     L.gskyhip_band_math.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(vp), vp, vp, ci, i64, d,
                                     vp, vp]
     L.gskyhip_drill_deciles_workspace_size.argtypes = [ci, i64, ci]

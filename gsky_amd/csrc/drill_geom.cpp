@@ -38,11 +38,14 @@
 // to oracle/ (a separate C restatement that sorts intersections the way GDAL
 // does), not to a running GDAL (absent here).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -342,35 +345,56 @@ struct Descriptor {
   Rings pix;   // rings in the window's pixel space (mask rasterization)
 };
 
-// getDrillFileDescriptor (drill.go:363-423) up to the mask's pixel rings.
-Descriptor describe(const char *geometry, const gskyhip_crs *crs, const double gt[6], int xsize, int ysize) {
-  Descriptor d;
-  Rings r;
-  if (!parse_geometry(geometry, r)) { d.status = GSKYHIP_E_ARG; return d; }
-  if (crs) {   // WGS84 lon/lat -> dataset SRS, the warp's transform (identity for the same CRS)
-    gskyhip_crs wgs;
-    gskyhip_crs_from_srs("EPSG:4326", &wgs);
-    if (!crs_same(wgs, *crs))
-      for (size_t i = 0; i < r.x.size(); i++) {
-        double lam, phi, X, Y;
-        if (!crs_inverse(wgs, r.x[i], r.y[i], lam, phi) || !crs_forward(*crs, lam, phi, X, Y)) {
-          d.status = GSKYHIP_E_CRS;
-          return d;
-        }
-        r.x[i] = X;
-        r.y[i] = Y;
-      }
+// What every polygon of one call shares: the CRS pair, the file envelope
+// (its corners printed with Go "%f" into WKT, drill.go:386-393) and the
+// inverse geotransform -- computed once per call, not per polygon.
+struct DescribeCtx {
+  const gskyhip_crs *crs = nullptr;   // dataset SRS, or NULL (no reprojection)
+  gskyhip_crs wgs;
+  bool reproject = false;
+  double box[4];                      // file envelope: min x, min y, max x, max y
+  double igt[6];
+  const double *gt = nullptr;
+};
+
+DescribeCtx make_ctx(const gskyhip_crs *crs, const double gt[6], int xsize, int ysize) {
+  DescribeCtx c;
+  c.crs = crs;
+  c.gt = gt;
+  if (crs) {
+    gskyhip_crs_from_srs("EPSG:4326", &c.wgs);
+    c.reproject = !crs_same(c.wgs, *crs);
   }
   const double ulX = go_f6(gt[0] + 0 * gt[1] + 0 * gt[2]), ulY = go_f6(gt[3] + 0 * gt[4] + 0 * gt[5]);
   const double lrX = go_f6(gt[0] + xsize * gt[1] + ysize * gt[2]);
   const double lrY = go_f6(gt[3] + xsize * gt[4] + ysize * gt[5]);
+  c.box[0] = std::min(ulX, lrX); c.box[1] = std::min(ulY, lrY);
+  c.box[2] = std::max(ulX, lrX); c.box[3] = std::max(ulY, lrY);
+  inv_geot(gt, c.igt);
+  return c;
+}
+
+// getDrillFileDescriptor (drill.go:363-423) up to the mask's pixel rings.
+Descriptor describe(const char *geometry, const DescribeCtx &c) {
+  Descriptor d;
+  Rings r;
+  if (!parse_geometry(geometry, r)) { d.status = GSKYHIP_E_ARG; return d; }
+  if (c.reproject)   // WGS84 lon/lat -> dataset SRS, the warp's transform
+    for (size_t i = 0; i < r.x.size(); i++) {
+      double lam, phi, X, Y;
+      if (!crs_inverse(c.wgs, r.x[i], r.y[i], lam, phi) || !crs_forward(*c.crs, lam, phi, X, Y)) {
+        d.status = GSKYHIP_E_CRS;
+        return d;
+      }
+      r.x[i] = X;
+      r.y[i] = Y;
+    }
   double env[4];
-  if (!clip_envelope(r, std::min(ulX, lrX), std::min(ulY, lrY), std::max(ulX, lrX), std::max(ulY, lrY), env)) {
+  if (!clip_envelope(r, c.box[0], c.box[1], c.box[2], c.box[3], env)) {
     d.status = GSKYHIP_E_RANGE;   // the polygon misses the file
     return d;
   }
-  double igt[6];
-  inv_geot(gt, igt);
+  const double *igt = c.igt;
   const double omx = igt[0] + env[0] * igt[1] + env[1] * igt[2], omy = igt[3] + env[0] * igt[4] + env[1] * igt[5];
   const double oMx = igt[0] + env[2] * igt[1] + env[3] * igt[2], oMy = igt[3] + env[2] * igt[4] + env[3] * igt[5];
   int32_t offX = go_cvtt32(std::fmin(omx, oMx)), offY = go_cvtt32(std::fmin(omy, oMy));
@@ -384,7 +408,7 @@ Descriptor describe(const char *geometry, const gskyhip_crs *crs, const double g
   // createMask (drill.go:294-308): the MEM raster's geotransform is the
   // dataset's shifted by the window offset (rotation terms kept as they are)
   double mgt[6], migt[6];
-  std::memcpy(mgt, gt, sizeof(mgt));
+  std::memcpy(mgt, c.gt, sizeof(mgt));
   mgt[0] += mgt[1] * (double)offX;
   mgt[3] += mgt[5] * (double)offY;
   inv_geot(mgt, migt);
@@ -395,6 +419,30 @@ Descriptor describe(const char *geometry, const gskyhip_crs *crs, const double g
     d.pix.y[i] = migt[3] + X * migt[4] + Y * migt[5];
   }
   return d;
+}
+
+// describe() of every polygon on up to 16 host threads (polygons are
+// independent; the reference describes one per gRPC call, drill_grpc.go:127-158).
+void describe_all(const char *const *geometries, int n, const DescribeCtx &c, std::vector<Descriptor> &out) {
+  out.assign((size_t)std::max(0, n), Descriptor());
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int nth = (int)std::min<unsigned>(std::min(16u, hw), (unsigned)std::max(1, n / 16));
+  std::atomic<int> next(0);
+  auto work = [&]() {
+    for (int i = next.fetch_add(8); i < n; i = next.fetch_add(8))
+      for (int k = i; k < std::min(n, i + 8); k++) {
+        try {
+          out[k] = describe(geometries[k], c);
+        } catch (...) {   // bad_alloc of a huge ring: that polygon fails, not the process
+          out[k] = Descriptor();
+          out[k].status = GSKYHIP_E_ARG;
+        }
+      }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nth; t++) th.emplace_back(work);
+  work();
+  for (auto &t : th) t.join();
 }
 
 // ---------------------------------------------------------------- GPU rasterizer
@@ -461,74 +509,103 @@ void rasterize_host(const Rings &r, uint8_t *m, int w, int h) {
   for (int y = J.miny; y <= J.maxy; y++) burn_row(J, y);
 }
 
-}  // namespace
-}  // namespace gsky
+// Persistent staging of the GPU rasterizer (polygons | x | y | parts |
+// parity bitmaps): grown, never freed per call; one call at a time uses it
+// (the call synchronizes its stream before releasing the lock).
+struct Staging {
+  std::mutex mu;
+  char *dev = nullptr;
+  size_t dev_cap = 0;
+  char *host = nullptr;   // pinned
+  size_t host_cap = 0;
+};
+Staging &staging() {
+  static Staging st;
+  return st;
+}
 
-using namespace gsky;
-
-// Windows on the host, ALL_TOUCHED masks rasterized on the GPU into masks_dev
-// (every polygon, any vertex count), all on `stream`.
-extern "C" int gskyhip_drill_descriptors_device(const char *const *geometries, int n, const char *dataset_srs,
-                                                const double *geot, int xsize, int ysize, int32_t *win_out,
-                                                int64_t *mask_off_out, int64_t *mask_bytes_out, uint8_t *masks_dev,
-                                                int32_t *status_out, void *stream) {
-  if (n < 0 || !geot || !win_out || !mask_off_out || !mask_bytes_out || !status_out) return GSKYHIP_E_ARG;
-  gskyhip_crs crs;
-  const gskyhip_crs *pc = nullptr;
-  if (dataset_srs && *dataset_srs) {
-    if (gskyhip_crs_from_srs(dataset_srs, &crs)) return GSKYHIP_E_CRS;
-    pc = &crs;
-  }
-  std::vector<PolyDev> polys;
-  std::vector<double> vx, vy;
-  std::vector<int32_t> parts;
-  int64_t off = 0, words = 0;
-  for (int i = 0; i < n; i++) {
-    Descriptor d = describe(geometries[i], pc, geot, xsize, ysize);
+// Windows, mask offsets and statuses of described polygons (16-byte aligned
+// mask regions in polygon order); returns the mask buffer size.
+int64_t layout(const std::vector<Descriptor> &ds, int32_t *win_out, int64_t *mask_off_out, int32_t *status_out) {
+  int64_t off = 0;
+  for (size_t i = 0; i < ds.size(); i++) {
+    const Descriptor &d = ds[i];
     status_out[i] = d.status;
     const int64_t bytes = d.status == 0 ? (int64_t)d.win[2] * d.win[3] : 0;
     for (int k = 0; k < 4; k++) win_out[4 * i + k] = d.status == 0 ? d.win[k] : 0;
     mask_off_out[i] = off;
-    if (masks_dev && bytes > 0 && !d.pix.x.empty()) {
-      PolyDev P;
-      P.mask_off = off;
-      P.w = d.win[2];
-      P.h = d.win[3];
-      P.v0 = (int32_t)vx.size();
-      P.nv = (int32_t)d.pix.x.size();
-      P.p0 = (int32_t)parts.size();
-      P.np = (int32_t)d.pix.part.size();
-      fill_rows(d.pix.y.data(), P.nv, P.h, P.miny, P.maxy);
-      P.wpr = (P.w + 31) / 32;
-      P._pad = 0;
-      P.bits_off = words;
-      if (P.maxy >= P.miny) words += (int64_t)(P.maxy - P.miny + 1) * P.wpr;
-      else P.maxy = P.miny - 1;   // no scanline: only the ALL_TOUCHED lines
-      vx.insert(vx.end(), d.pix.x.begin(), d.pix.x.end());
-      vy.insert(vy.end(), d.pix.y.begin(), d.pix.y.end());
-      parts.insert(parts.end(), d.pix.part.begin(), d.pix.part.end());
-      polys.push_back(P);
-    }
-    off += (bytes + 15) / 16 * 16;   // 16-byte aligned regions, polygon order
+    off += (bytes + 15) / 16 * 16;
   }
-  *mask_bytes_out = off > 0 ? off : 16;
-  if (!masks_dev) return 0;
-  hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(masks_dev, 0, (size_t)*mask_bytes_out, s) != hipSuccess) return GSKYHIP_E_HIP;
+  return off > 0 ? off : 16;
+}
+
+// ALL_TOUCHED masks of described polygons rasterized on the GPU into
+// masks_dev (zeroed first), on `s`.
+int rasterize_device(const std::vector<Descriptor> &ds, const int64_t *mask_off, uint8_t *masks_dev,
+                     int64_t mask_bytes, hipStream_t s) {
+  if (hipMemsetAsync(masks_dev, 0, (size_t)mask_bytes, s) != hipSuccess) return GSKYHIP_E_HIP;
+  std::vector<PolyDev> polys;
+  size_t nv = 0, npart = 0;
+  for (const Descriptor &d : ds)
+    if (d.status == 0 && !d.pix.x.empty()) { nv += d.pix.x.size(); npart += d.pix.part.size(); }
+  polys.reserve(ds.size());
+  int64_t words = 0;
+  int32_t v0 = 0, p0 = 0;
+  for (size_t i = 0; i < ds.size(); i++) {
+    const Descriptor &d = ds[i];
+    if (d.status != 0 || d.pix.x.empty() || (int64_t)d.win[2] * d.win[3] <= 0) continue;
+    PolyDev P;
+    P.mask_off = mask_off[i];
+    P.w = d.win[2];
+    P.h = d.win[3];
+    P.v0 = v0;
+    P.nv = (int32_t)d.pix.x.size();
+    P.p0 = p0;
+    P.np = (int32_t)d.pix.part.size();
+    fill_rows(d.pix.y.data(), P.nv, P.h, P.miny, P.maxy);
+    P.wpr = (P.w + 31) / 32;
+    P._pad = 0;
+    P.bits_off = words;
+    if (P.maxy >= P.miny) words += (int64_t)(P.maxy - P.miny + 1) * P.wpr;
+    else P.maxy = P.miny - 1;   // no scanline: only the ALL_TOUCHED lines
+    v0 += P.nv;
+    p0 += P.np;
+    polys.push_back(P);
+  }
   if (polys.empty()) return 0;
-  // one staging allocation: polygons | x | y | parts | parity bitmaps
-  const size_t b0 = polys.size() * sizeof(PolyDev), b1 = vx.size() * 8, b2 = (parts.size() * 4 + 15) / 16 * 16;
+  const size_t b0 = (polys.size() * sizeof(PolyDev) + 15) / 16 * 16, b1 = nv * 8, b2 = (npart * 4 + 15) / 16 * 16;
   const size_t b3 = (size_t)std::max<int64_t>(words, 1) * 4;
-  char *dev = nullptr;
-  if (hipMalloc(&dev, b0 + 2 * b1 + b2 + b3) != hipSuccess) return GSKYHIP_E_HIP;
-  std::vector<char> host(b0 + 2 * b1 + b2);
-  std::memcpy(host.data(), polys.data(), b0);
-  std::memcpy(host.data() + b0, vx.data(), b1);
-  std::memcpy(host.data() + b0 + b1, vy.data(), b1);
-  std::memcpy(host.data() + b0 + 2 * b1, parts.data(), parts.size() * 4);
+  const size_t hbytes = b0 + 2 * b1 + b2;
+  Staging &st = staging();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (st.dev_cap < hbytes + b3) {
+    if (st.dev) (void)hipFree(st.dev);
+    st.dev = nullptr;
+    st.dev_cap = 0;
+    if (hipMalloc(&st.dev, (hbytes + b3) * 5 / 4) != hipSuccess) return GSKYHIP_E_HIP;
+    st.dev_cap = (hbytes + b3) * 5 / 4;
+  }
+  if (st.host_cap < hbytes) {
+    if (st.host) (void)hipHostFree(st.host);
+    st.host = nullptr;
+    st.host_cap = 0;
+    if (hipHostMalloc((void **)&st.host, hbytes * 5 / 4, hipHostMallocDefault) != hipSuccess) return GSKYHIP_E_HIP;
+    st.host_cap = hbytes * 5 / 4;
+  }
+  char *h = st.host;
+  std::memcpy(h, polys.data(), polys.size() * sizeof(PolyDev));
+  double *hx = (double *)(h + b0), *hy = (double *)(h + b0 + b1);
+  int32_t *hp = (int32_t *)(h + b0 + 2 * b1);
+  for (const Descriptor &d : ds) {
+    if (d.status != 0 || d.pix.x.empty() || (int64_t)d.win[2] * d.win[3] <= 0) continue;
+    std::memcpy(hx, d.pix.x.data(), d.pix.x.size() * 8); hx += d.pix.x.size();
+    std::memcpy(hy, d.pix.y.data(), d.pix.y.size() * 8); hy += d.pix.y.size();
+    std::memcpy(hp, d.pix.part.data(), d.pix.part.size() * 4); hp += d.pix.part.size();
+  }
+  char *dev = st.dev;
   int rc = 0;
-  uint32_t *bits = (uint32_t *)(dev + b0 + 2 * b1 + b2);
-  if (hipMemcpyAsync(dev, host.data(), host.size(), hipMemcpyHostToDevice, s) != hipSuccess) rc = GSKYHIP_E_HIP;
+  uint32_t *bits = (uint32_t *)(dev + hbytes);
+  if (hipMemcpyAsync(dev, h, hbytes, hipMemcpyHostToDevice, s) != hipSuccess) rc = GSKYHIP_E_HIP;
   if (!rc && hipMemsetAsync(bits, 0, b3, s) != hipSuccess) rc = GSKYHIP_E_HIP;
   const PolyDev *dp = (const PolyDev *)dev;
   const double *dx = (const double *)(dev + b0), *dy = (const double *)(dev + b0 + b1);
@@ -539,10 +616,70 @@ extern "C" int gskyhip_drill_descriptors_device(const char *const *geometries, i
     hipLaunchKernelGGL(burn_rows_kernel, dim3((unsigned)polys.size()), dim3(256), 0, s, dp, masks_dev, bits);
     if (hipGetLastError() != hipSuccess) rc = GSKYHIP_E_HIP;
   }
-  // the staging buffers (and `host`, read by the async copy) must outlive the work
+  // the staging buffers are reused by the next call: the work must be done
   if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GSKYHIP_E_HIP;
-  (void)hipFree(dev);
   return rc;
+}
+
+int ctx_of(const char *dataset_srs, gskyhip_crs &crs, const gskyhip_crs *&pc) {
+  pc = nullptr;
+  if (dataset_srs && *dataset_srs) {
+    if (gskyhip_crs_from_srs(dataset_srs, &crs)) return GSKYHIP_E_CRS;
+    pc = &crs;
+  }
+  return 0;
+}
+
+}  // namespace
+}  // namespace gsky
+
+using namespace gsky;
+
+// Windows on the host, ALL_TOUCHED masks rasterized on the GPU into masks_dev
+// (every polygon, any vertex count), all on `stream`.  masks_dev == NULL:
+// windows, offsets and the buffer size only.
+extern "C" int gskyhip_drill_descriptors_device(const char *const *geometries, int n, const char *dataset_srs,
+                                                const double *geot, int xsize, int ysize, int32_t *win_out,
+                                                int64_t *mask_off_out, int64_t *mask_bytes_out, uint8_t *masks_dev,
+                                                int32_t *status_out, void *stream) {
+  if (n < 0 || !geot || !win_out || !mask_off_out || !mask_bytes_out || !status_out) return GSKYHIP_E_ARG;
+  try {
+    gskyhip_crs crs;
+    const gskyhip_crs *pc;
+    if (ctx_of(dataset_srs, crs, pc)) return GSKYHIP_E_CRS;
+    std::vector<Descriptor> ds;
+    describe_all(geometries, n, make_ctx(pc, geot, xsize, ysize), ds);
+    *mask_bytes_out = layout(ds, win_out, mask_off_out, status_out);
+    if (!masks_dev) return 0;
+    return rasterize_device(ds, mask_off_out, masks_dev, *mask_bytes_out, (hipStream_t)stream);
+  } catch (...) {
+    return GSKYHIP_E_ARG;
+  }
+}
+
+// The same in one pass: the polygons are described once, then alloc(ctx,
+// bytes) supplies the device mask buffer of the size that needs.
+extern "C" int gskyhip_drill_masks_device(const char *const *geometries, int n, const char *dataset_srs,
+                                          const double *geot, int xsize, int ysize, int32_t *win_out,
+                                          int64_t *mask_off_out, int64_t *mask_bytes_out, gskyhip_alloc_fn alloc,
+                                          void *alloc_ctx, uint8_t **masks_dev_out, int32_t *status_out,
+                                          void *stream) {
+  if (n < 0 || !geot || !win_out || !mask_off_out || !mask_bytes_out || !status_out || !alloc || !masks_dev_out)
+    return GSKYHIP_E_ARG;
+  try {
+    gskyhip_crs crs;
+    const gskyhip_crs *pc;
+    if (ctx_of(dataset_srs, crs, pc)) return GSKYHIP_E_CRS;
+    std::vector<Descriptor> ds;
+    describe_all(geometries, n, make_ctx(pc, geot, xsize, ysize), ds);
+    *mask_bytes_out = layout(ds, win_out, mask_off_out, status_out);
+    uint8_t *m = (uint8_t *)alloc(alloc_ctx, *mask_bytes_out);
+    *masks_dev_out = m;
+    if (!m) return GSKYHIP_E_HIP;
+    return rasterize_device(ds, mask_off_out, m, *mask_bytes_out, (hipStream_t)stream);
+  } catch (...) {
+    return GSKYHIP_E_ARG;
+  }
 }
 
 extern "C" int gskyhip_drill_descriptors(const char *const *geometries, int n, const char *dataset_srs,
@@ -550,25 +687,23 @@ extern "C" int gskyhip_drill_descriptors(const char *const *geometries, int n, c
                                          int64_t *mask_off_out, int64_t *mask_bytes_out, uint8_t *masks_out,
                                          int32_t *status_out) {
   if (n < 0 || !geot || !win_out || !mask_off_out || !mask_bytes_out || !status_out) return GSKYHIP_E_ARG;
-  gskyhip_crs crs;
-  const gskyhip_crs *pc = nullptr;
-  if (dataset_srs && *dataset_srs) {
-    if (gskyhip_crs_from_srs(dataset_srs, &crs)) return GSKYHIP_E_CRS;
-    pc = &crs;
+  try {
+    gskyhip_crs crs;
+    const gskyhip_crs *pc;
+    if (ctx_of(dataset_srs, crs, pc)) return GSKYHIP_E_CRS;
+    std::vector<Descriptor> ds;
+    describe_all(geometries, n, make_ctx(pc, geot, xsize, ysize), ds);
+    *mask_bytes_out = layout(ds, win_out, mask_off_out, status_out);
+    if (masks_out)
+      for (int i = 0; i < n; i++) {
+        const Descriptor &d = ds[i];
+        const int64_t bytes = d.status == 0 ? (int64_t)d.win[2] * d.win[3] : 0;
+        if (bytes <= 0) continue;
+        std::memset(masks_out + mask_off_out[i], 0, (size_t)bytes);
+        rasterize_host(d.pix, masks_out + mask_off_out[i], d.win[2], d.win[3]);   // ALL_TOUCHED lines + fill
+      }
+    return 0;
+  } catch (...) {
+    return GSKYHIP_E_ARG;
   }
-  int64_t off = 0;
-  for (int i = 0; i < n; i++) {
-    Descriptor d = describe(geometries[i], pc, geot, xsize, ysize);
-    status_out[i] = d.status;
-    const int64_t bytes = d.status == 0 ? (int64_t)d.win[2] * d.win[3] : 0;
-    for (int k = 0; k < 4; k++) win_out[4 * i + k] = d.status == 0 ? d.win[k] : 0;
-    mask_off_out[i] = off;
-    if (masks_out && bytes > 0) {
-      std::memset(masks_out + off, 0, (size_t)bytes);
-      rasterize_host(d.pix, masks_out + off, d.win[2], d.win[3]);   // ALL_TOUCHED lines + scanline fill
-    }
-    off += (bytes + 15) / 16 * 16;   // 16-byte aligned regions, polygon order
-  }
-  *mask_bytes_out = off > 0 ? off : 16;
-  return 0;
 }

@@ -232,11 +232,97 @@ __host__ __device__ inline bool crs_forward(const gskyhip_crs &c, double lam, do
   return true;
 }
 
-// GenImgProj transformer state of one (tile, granule) pair.
+// ---------------------------------------------------------------- geolocation arrays
+// GDAL 3.0.1's geolocation-array transformer (alg/gdalgeoloc.cpp, [ext]: not
+// in /root/reference; restated from its published algorithm, parity
+// unpinned), selected by warp.go:128-141 when the request carries GeoLocOpts
+// (tile_grpc.go:338-350: X_DATASET / Y_DATASET / X_BAND / Y_BAND /
+// PIXEL_OFFSET / LINE_OFFSET / PIXEL_STEP / LINE_STEP).  The source side of
+// the GenImgProj transformer is then this instead of the source geotransform
+// (createGeoLocTransformer, warp.go:52-67):
+//   forward  (source pixel/line -> georeferenced): bilinear interpolation of
+//            the geolocation arrays at ((x - PIXEL_OFFSET) / PIXEL_STEP,
+//            (y - LINE_OFFSET) / LINE_STEP), the nearest grid square
+//            extended beyond the arrays, nodata corners dropping to the
+//            edge / corner rules;
+//   inverse  (georeferenced -> source pixel/line): the backmap (a regular
+//            grid over the arrays' extent, ~1.3 cells per geolocation sample,
+//            built by bilinear splatting, averaging and three hole-filling
+//            passes -- host.cpp geoloc_backmap), bilinearly interpolated
+//            where its four cells are set, else its nearest cell.
+struct GeoLocD {
+  const double *gx, *gy;       // geolocation arrays, ny rows x nx (device)
+  const float *bmx, *bmy;      // backmap, bm_h rows x bm_w: source pixel / line (< 0: none)
+  int32_t nx, ny, bm_w, bm_h;
+  int32_t has_nodata, _pad;
+  double nodata_x;             // GDALGetRasterNoDataValue of the X band
+  double pixel_offset, line_offset, pixel_step, line_step;
+  double bm_gt[6];             // backmap geotransform (north up)
+};
+
+__host__ __device__ inline bool geoloc_forward(const GeoLocD &g, double &x, double &y) {
+  if (x == HUGE_VAL || y == HUGE_VAL) return false;
+  const double px = (x - g.pixel_offset) / g.pixel_step;
+  const double ln = (y - g.line_offset) / g.line_step;
+  int ix = go_cvtt32(px), iy = go_cvtt32(ln);   // static_cast<int> on x86: out of range -> INT_MIN
+  ix = ix < 0 ? 0 : ix;
+  ix = ix > g.nx - 1 ? g.nx - 1 : ix;
+  iy = iy < 0 ? 0 : iy;
+  iy = iy > g.ny - 1 ? g.ny - 1 : iy;
+  const int64_t o = (int64_t)iy * g.nx + ix;
+  const double *gx = g.gx + o, *gy = g.gy + o;
+  const double nd = g.nodata_x;
+  if (g.has_nodata && gx[0] == nd) return false;
+  const double fx = px - ix, fy = ln - iy;
+  if (ix + 1 < g.nx && iy + 1 < g.ny &&
+      (!g.has_nodata || (gx[1] != nd && gx[g.nx] != nd && gx[g.nx + 1] != nd))) {
+    x = (1 - fy) * (gx[0] + fx * (gx[1] - gx[0])) + fy * (gx[g.nx] + fx * (gx[g.nx + 1] - gx[g.nx]));
+    y = (1 - fy) * (gy[0] + fx * (gy[1] - gy[0])) + fy * (gy[g.nx] + fx * (gy[g.nx + 1] - gy[g.nx]));
+  } else if (ix + 1 < g.nx && (!g.has_nodata || gx[1] != nd)) {
+    x = gx[0] + fx * (gx[1] - gx[0]);
+    y = gy[0] + fx * (gy[1] - gy[0]);
+  } else if (iy + 1 < g.ny && (!g.has_nodata || gx[g.nx] != nd)) {
+    x = gx[0] + fy * (gx[g.nx] - gx[0]);
+    y = gy[0] + fy * (gy[g.nx] - gy[0]);
+  } else {
+    x = gx[0];
+    y = gy[0];
+  }
+  return true;
+}
+
+__host__ __device__ inline bool geoloc_inverse(const GeoLocD &g, double &x, double &y) {
+  if (x == HUGE_VAL || y == HUGE_VAL) return false;
+  const double bx = (x - g.bm_gt[0]) / g.bm_gt[1] - 0.5;
+  const double by = (y - g.bm_gt[3]) / g.bm_gt[5] - 0.5;
+  if (!(bx > -0.5 && by > -0.5 && bx < g.bm_w - 0.5 && by < g.bm_h - 0.5)) return false;   // NaN too
+  const int ix = (int)floor(bx), iy = (int)floor(by);
+  const int64_t w = g.bm_w;
+  if (ix >= 0 && iy >= 0 && ix + 1 < g.bm_w && iy + 1 < g.bm_h) {
+    const int64_t o = iy * w + ix;
+    const float *mx = g.bmx + o, *my = g.bmy + o;
+    if (mx[0] >= 0 && mx[1] >= 0 && mx[w] >= 0 && mx[w + 1] >= 0) {
+      const double fx = bx - ix, fy = by - iy;
+      x = (1 - fx) * (1 - fy) * mx[0] + fx * (1 - fy) * mx[1] + (1 - fx) * fy * mx[w] + fx * fy * mx[w + 1];
+      y = (1 - fx) * (1 - fy) * my[0] + fx * (1 - fy) * my[1] + (1 - fx) * fy * my[w] + fx * fy * my[w + 1];
+      return true;
+    }
+  }
+  const int nx = (int)floor(bx + 0.5), ny = (int)floor(by + 0.5);   // nearest cell (in range by the test above)
+  const int64_t o = (int64_t)ny * w + nx;
+  if (g.bmx[o] < 0) return false;
+  x = g.bmx[o];
+  y = g.bmy[o];
+  return true;
+}
+
+// GenImgProj transformer state of one (tile, granule) pair.  gl: a
+// geolocation-array source transformer in place of src_gt (warp.go:128-141).
 struct Xform {
   gskyhip_crs src, dst;
   double src_gt[6], src_igt[6], dst_gt[6], dst_igt[6];
   int reproject;
+  const GeoLocD *gl;   // set at every construction (NULL: the source geotransform)
 };
 
 __host__ __device__ inline void inv_geot(const double *gt, double *o) {  // GDALInvGeoTransform
@@ -268,8 +354,14 @@ __host__ __device__ inline bool crs_same(const gskyhip_crs &a, const gskyhip_crs
 __device__ inline bool xform_point(const Xform &t, bool dst_to_src, double &x, double &y) {
   const double *g1 = dst_to_src ? t.dst_gt : t.src_gt;
   const double *g2 = dst_to_src ? t.src_igt : t.dst_igt;
-  double X = g1[0] + x * g1[1] + y * g1[2];
-  double Y = g1[3] + x * g1[4] + y * g1[5];
+  double X, Y;
+  if (!dst_to_src && t.gl) {   // geolocation arrays: source pixel/line -> georeferenced
+    X = x; Y = y;
+    if (!geoloc_forward(*t.gl, X, Y)) return false;
+  } else {
+    X = g1[0] + x * g1[1] + y * g1[2];
+    Y = g1[3] + x * g1[4] + y * g1[5];
+  }
   if (t.reproject) {
     double lam, phi;
     if (dst_to_src) {
@@ -279,6 +371,10 @@ __device__ inline bool xform_point(const Xform &t, bool dst_to_src, double &x, d
       if (!crs_inverse(t.src, X, Y, lam, phi)) return false;
       if (!crs_forward(t.dst, lam, phi, X, Y)) return false;
     }
+  }
+  if (dst_to_src && t.gl) {    // georeferenced -> source pixel/line through the backmap
+    x = X; y = Y;
+    return geoloc_inverse(*t.gl, x, y);
   }
   x = g2[0] + X * g2[1] + Y * g2[2];
   y = g2[3] + X * g2[4] + Y * g2[5];
@@ -299,7 +395,7 @@ struct SepRow { double phi, r1, r2; int32_t ok, _pad; };
 
 __host__ __device__ inline bool sep_possible(const Xform &t) {
   const int dk = t.dst.kind, sk = t.src.kind;
-  return t.reproject && t.dst_gt[2] == 0.0 && t.dst_gt[4] == 0.0 &&
+  return t.reproject && !t.gl && t.dst_gt[2] == 0.0 && t.dst_gt[4] == 0.0 &&
          (dk == GSKYHIP_CRS_WEBMERC || dk == GSKYHIP_CRS_LONGLAT) &&
          (sk == GSKYHIP_CRS_WEBMERC || sk == GSKYHIP_CRS_LONGLAT || sk == GSKYHIP_CRS_AEA ||
           sk == GSKYHIP_CRS_SINU);

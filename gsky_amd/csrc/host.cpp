@@ -283,6 +283,7 @@ struct DropIn {
   void *dev = nullptr;   // descriptors + workspace + window
   size_t dev_bytes = 0;
   uint64_t tick = 0;     // one per warp batch: entries it uses are not evicted while it runs
+  std::map<std::string, struct GeoLocEntry *> geolocs;   // by GeoLocOpts (geoloc_entry)
 };
 DropIn &dropin() {
   static DropIn d;
@@ -439,6 +440,222 @@ int ingest_netcdf_locked(DropIn &d, const std::string &path, int band) {
   return 0;
 }
 
+// ---------------------------------------------------------------- geolocation arrays
+// GDALCreateGeoLocTransformer (GDAL 3.0.1 alg/gdalgeoloc.cpp [ext], called by
+// createGeoLocTransformer, warp.go:52-67) for the drop-in: the X / Y bands
+// named by GeoLocOpts (registered, or opened like any source file), read as
+// double (GeoLocLoadFullData: a 1-row X and a 1-row Y band form a regular
+// grid), then the backmap (GeoLocGenerateBackMap), kept in HBM and cached by
+// the option strings.  Parity unpinned (GDAL is absent; oracle/ restates the
+// same algorithm independently).
+struct GeoLocEntry {
+  GeoLocD d;
+  std::vector<void *> owned;
+};
+
+void release_geoloc(GeoLocEntry *e) {
+  if (!e) return;
+  for (void *p : e->owned) (void)hipFree(p);
+  delete e;
+}
+
+bool band_as_double(const Registered &R, std::vector<double> &out) {
+  const gskyhip_granule &g = R.g;
+  const int ts = type_size(g.dtype);
+  if (ts <= 0 || !g.data) return false;
+  const size_t n = (size_t)g.xsize * g.ysize;
+  std::vector<uint8_t> raw(n * ts);
+  if (hipMemcpy(raw.data(), g.data, raw.size(), hipMemcpyDeviceToHost) != hipSuccess) return false;
+  out.resize(n);
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t *p = raw.data() + i * ts;
+    switch (g.dtype) {
+      case GSKYHIP_BYTE: out[i] = g.signed_byte ? (double)(int8_t)p[0] : (double)p[0]; break;
+      case GSKYHIP_INT16: { int16_t v; std::memcpy(&v, p, 2); out[i] = v; break; }
+      case GSKYHIP_UINT16: { uint16_t v; std::memcpy(&v, p, 2); out[i] = v; break; }
+      case GSKYHIP_INT32: { int32_t v; std::memcpy(&v, p, 4); out[i] = v; break; }
+      case GSKYHIP_UINT32: { uint32_t v; std::memcpy(&v, p, 4); out[i] = v; break; }
+      case GSKYHIP_FLOAT32: { float v; std::memcpy(&v, p, 4); out[i] = v; break; }
+      default: { double v; std::memcpy(&v, p, 8); out[i] = v; break; }
+    }
+  }
+  return true;
+}
+
+// GeoLocGenerateBackMap: extent of the valid geolocation points, a grid of
+// ~1.3 cells per point, every point splatted bilinearly into its 4 cells
+// (source pixel / line weighted), cells with weight > 0.25 averaged (the
+// others -1), then 3 passes filling holes from their set 4-neighbours (a cell
+// filled in pass k is used from pass k+1 on).
+bool geoloc_backmap(const std::vector<double> &gx, const std::vector<double> &gy, int nx, int ny, bool has_nd,
+                    double nd, double pix_off, double line_off, double pix_step, double line_step,
+                    std::vector<float> &bmx, std::vector<float> &bmy, int &bw, int &bh, double gt[6]) {
+  const int nMaxIter = 3;
+  double minX = 0, maxX = 0, minY = 0, maxY = 0;
+  bool init = false;
+  for (int64_t i = (int64_t)nx * ny - 1; i >= 0; i--) {
+    if (has_nd && gx[i] == nd) continue;
+    if (init) {
+      minX = std::min(minX, gx[i]); maxX = std::max(maxX, gx[i]);
+      minY = std::min(minY, gy[i]); maxY = std::max(maxY, gy[i]);
+    } else {
+      init = true;
+      minX = maxX = gx[i];
+      minY = maxY = gy[i];
+    }
+  }
+  const double target = (double)nx * ny * 1.3;
+  const double ps = std::sqrt((maxX - minX) * (maxY - minY) / target);
+  if (!(ps > 0.0) || !std::isfinite(ps)) return false;
+  const double fw = std::ceil((maxX - minX) / ps) + 1, fh = std::ceil((maxY - minY) / ps) + 1;
+  if (!(fw > 0 && fw < 65536.0 * 64) || !(fh > 0 && fh < 65536.0 * 64) || fw * fh > 4.0e9) return false;
+  bw = (int)fw;
+  bh = (int)fh;
+  minX -= ps / 2.0;
+  maxY += ps / 2.0;
+  gt[0] = minX; gt[1] = ps; gt[2] = 0.0; gt[3] = maxY; gt[4] = 0.0; gt[5] = -ps;
+  const size_t nbm = (size_t)bw * bh;
+  bmx.assign(nbm, 0.0f);
+  bmy.assign(nbm, 0.0f);
+  std::vector<float> wgt(nbm, 0.0f);
+  for (int iY = 0; iY < ny; iY++)
+    for (int iX = 0; iX < nx; iX++) {
+      const size_t o = (size_t)iX + (size_t)iY * nx;
+      if (has_nd && gx[o] == nd) continue;
+      const double dBMX = (gx[o] - minX) / ps - 0.5;
+      const double dBMY = (maxY - gy[o]) / ps - 0.5;
+      const int iBMX = (int)std::floor(dBMX), iBMY = (int)std::floor(dBMY);
+      const double fx = dBMX - iBMX, fy = dBMY - iBMY;
+      const double sp = iX * pix_step + pix_off, sl = iY * line_step + line_off;
+      for (int k = 0; k < 4; k++) {
+        const int cx = iBMX + (k & 1), cy = iBMY + (k >> 1);
+        if (cx < 0 || cx >= bw || cy < 0 || cy >= bh) continue;
+        const double w = ((k & 1) ? fx : 1.0 - fx) * ((k >> 1) ? fy : 1.0 - fy);
+        const size_t c = (size_t)cx + (size_t)cy * bw;
+        bmx[c] += (float)(sp * w);
+        bmy[c] += (float)(sl * w);
+        wgt[c] += (float)w;
+      }
+    }
+  for (size_t i = 0; i < nbm; i++) {
+    if (wgt[i] > 0.25f) {
+      bmx[i] /= wgt[i];
+      bmy[i] /= wgt[i];
+      wgt[i] = (float)(nMaxIter + 1);
+    } else {
+      bmx[i] = -1.0f;
+      bmy[i] = -1.0f;
+      wgt[i] = 0.0f;
+    }
+  }
+  for (int iter = 0; iter < nMaxIter; iter++) {
+    size_t valid = 0;
+    const int mark = nMaxIter - iter;
+    for (int y = 0; y < bh; y++)
+      for (int x = 0; x < bw; x++) {
+        const size_t c = (size_t)x + (size_t)y * bw;
+        if (bmx[c] >= 0) { valid++; continue; }
+        int n = 0;
+        double sx = 0.0, sy = 0.0;
+        auto take = [&](size_t j) { if (wgt[j] > mark) { sx += bmx[j]; sy += bmy[j]; n++; } };
+        if (x > 0) take(c - 1);
+        if (x + 1 < bw) take(c + 1);
+        if (y > 0) take(c - bw);
+        if (y + 1 < bh) take(c + bw);
+        if (n > 0) {
+          bmx[c] = (float)(sx / n);
+          bmy[c] = (float)(sy / n);
+          wgt[c] = (float)mark;
+        }
+      }
+    if (valid == nbm) break;
+  }
+  return true;
+}
+
+int ingest_geotiff_locked(DropIn &d, const std::string &path, int band);
+int ingest_netcdf_locked(DropIn &d, const std::string &path, int band);
+bool is_geotiff_path(const std::string &p);
+
+// The transformer of one GeoLocOpts list (cached), or NULL (the reference's
+// GDALCreateGeoLocTransformer failure: warp_operation_fast returns 3).
+GeoLocEntry *geoloc_entry(DropIn &d, const std::vector<std::string> &opts) {
+  std::string key;
+  for (const std::string &o : opts) key += o + '\n';
+  auto hit = d.geolocs.find(key);
+  if (hit != d.geolocs.end()) return hit->second;
+  std::map<std::string, std::string> kv;
+  for (const std::string &o : opts) {
+    const size_t e = o.find('=');
+    if (e != std::string::npos) kv[o.substr(0, e)] = o.substr(e + 1);   // CSLFetchNameValue: KEY=VALUE
+  }
+  for (const char *k : {"PIXEL_OFFSET", "LINE_OFFSET", "PIXEL_STEP", "LINE_STEP", "X_BAND", "Y_BAND",
+                        "X_DATASET", "Y_DATASET"})
+    if (!kv.count(k)) return nullptr;   // "Missing some geolocation fields"
+  auto dataset = [&](const std::string &path, int band) -> const Registered * {
+    auto it = d.reg.find({path, band});
+    if (it == d.reg.end()) {
+      const bool nc = path.compare(0, 7, "NETCDF:") == 0 ||
+                      (path.size() >= 3 && path.compare(path.size() - 3, 3, ".nc") == 0);
+      if (nc) { if (ingest_netcdf_locked(d, path, band)) return nullptr; }
+      else if (is_geotiff_path(path)) { if (ingest_geotiff_locked(d, path, band)) return nullptr; }
+      else return nullptr;
+      it = d.reg.find({path, band});
+      if (it == d.reg.end()) return nullptr;
+    }
+    it->second.last_use = d.tick;
+    return &it->second;
+  };
+  const Registered *X = dataset(kv["X_DATASET"], std::atoi(kv["X_BAND"].c_str()));
+  const Registered *Y = dataset(kv["Y_DATASET"], std::atoi(kv["Y_BAND"].c_str()));
+  if (!X || !Y) return nullptr;
+  std::vector<double> ax, ay;
+  if (!band_as_double(*X, ax) || !band_as_double(*Y, ay)) return nullptr;
+  // GeoLocLoadFullData: a regular grid when both bands are one row
+  const bool regular = X->g.ysize == 1 && Y->g.ysize == 1;
+  const int nx = X->g.xsize, ny = regular ? Y->g.xsize : X->g.ysize;
+  if (!regular && (Y->g.xsize != nx || Y->g.ysize != ny)) return nullptr;
+  std::vector<double> gx((size_t)nx * ny), gy((size_t)nx * ny);
+  for (int j = 0; j < ny; j++)
+    for (int i = 0; i < nx; i++) {
+      const size_t o = (size_t)j * nx + i;
+      gx[o] = regular ? ax[i] : ax[o];
+      gy[o] = regular ? ay[j] : ay[o];
+    }
+  GeoLocEntry *e = new GeoLocEntry();
+  GeoLocD &g = e->d;
+  std::memset(&g, 0, sizeof(g));
+  g.nx = nx; g.ny = ny;
+  g.has_nodata = X->g.has_nodata ? 1 : 0;
+  g.nodata_x = X->g.nodata;
+  g.pixel_offset = std::atof(kv["PIXEL_OFFSET"].c_str());   // CPLAtof
+  g.line_offset = std::atof(kv["LINE_OFFSET"].c_str());
+  g.pixel_step = std::atof(kv["PIXEL_STEP"].c_str());
+  g.line_step = std::atof(kv["LINE_STEP"].c_str());
+  std::vector<float> bmx, bmy;
+  int bw = 0, bh = 0;
+  if (!geoloc_backmap(gx, gy, nx, ny, g.has_nodata != 0, g.nodata_x, g.pixel_offset, g.line_offset, g.pixel_step,
+                      g.line_step, bmx, bmy, bw, bh, g.bm_gt)) {
+    delete e;
+    return nullptr;
+  }
+  g.bm_w = bw; g.bm_h = bh;
+  auto up = [&](const void *src, size_t bytes) -> void * {
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    e->owned.push_back(p);
+    if (hipMemcpy(p, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return p;
+  };
+  g.gx = (const double *)up(gx.data(), gx.size() * 8);
+  g.gy = (const double *)up(gy.data(), gy.size() * 8);
+  g.bmx = (const float *)up(bmx.data(), bmx.size() * 4);
+  g.bmy = (const float *)up(bmy.data(), bmy.size() * 4);
+  if (!g.gx || !g.gy || !g.bmx || !g.bmy) { release_geoloc(e); return nullptr; }
+  d.geolocs[key] = e;
+  return e;
+}
+
 bool is_geotiff_path(const std::string &p) {
   auto ends = [&](const char *suf) {
     const size_t n = std::strlen(suf);
@@ -499,6 +716,8 @@ int gskyhip_unregister_all(void) {
   std::lock_guard<std::mutex> lk(d.mu);
   for (auto &kv : d.reg) release(kv.second);
   d.reg.clear();
+  for (auto &kv : d.geolocs) release_geoloc(kv.second);
+  d.geolocs.clear();
   return 0;
 }
 
@@ -530,7 +749,7 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
   DropIn &d = dropin();
   std::lock_guard<std::mutex> lk(d.mu);
   d.tick++;
-  struct Item { int req; gskyhip_granule g; gskyhip_crs src; int bx, by; };
+  struct Item { int req; gskyhip_granule g; gskyhip_crs src; int bx, by; const GeoLocEntry *gl; };
   std::map<std::pair<int, std::string>, std::vector<Item>> groups;   // (has dst, dst srs) -> items
   for (int i = 0; i < n; i++) {
     const WarpReq &q = reqs[i];
@@ -567,10 +786,14 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     it->second.last_use = d.tick;                                      // pinned for this batch
     const Registered &R = it->second;
     if (!R.g.data) { r.rc = 2; continue; }                             // band failed
-    if (q.geoloc) { r.rc = 3; continue; }                              // geolocation arrays: unsupported
     if (q.width <= 0 || q.height <= 0) { r.rc = GSKYHIP_E_ARG; continue; }
     Item it2;
     it2.req = i;
+    it2.gl = nullptr;
+    if (q.geoloc) {   // warp.go:134-140: createGeoLocTransformer, 3 when it fails
+      it2.gl = geoloc_entry(d, q.geoloc_opts);
+      if (!it2.gl) { r.rc = 3; continue; }
+    }
     if (q.has_src_srs) {
       if (parse_srs(q.src_srs.c_str(), &it2.src)) { r.rc = 3; continue; }
     } else if (R.has_crs) {
@@ -616,9 +839,11 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
       n_px[k] = (int64_t)q.width * q.height;
       st_bytes = std::max(st_bytes, a256(block_stats_scratch_bytes(n_px[k], n_words[k])));
     }
-    // device layout: granules | crs (m sources + dst) | tiles | pairs | bbox | dtype | nodata | stats
+    // device layout: granules | geolocation transformers | crs (m sources + dst) | tiles | pairs | bbox
+    //                | dtype | nodata | stats
     //                | workspace | windows (m x stride) | block-stats scratch
-    const int64_t o_crs = a256((int64_t)m * sizeof(gskyhip_granule));
+    const int64_t o_gl = a256((int64_t)m * sizeof(gskyhip_granule));
+    const int64_t o_crs = o_gl + a256((int64_t)m * sizeof(GeoLocD));
     const int64_t o_tiles = o_crs + a256((int64_t)(m + 1) * sizeof(gskyhip_crs));
     const int64_t o_pairs = o_tiles + a256((int64_t)m * sizeof(gskyhip_tile));
     const int64_t o_bbox = o_pairs + a256((int64_t)m * 4);
@@ -650,10 +875,18 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
       parse_srs(kv.first.second.c_str(), &hc[m]);
       dst_crs = m;
     }
+    GeoLocD *hgl = (GeoLocD *)(hdr.data() + o_gl);
+    bool any_gl = false;
     for (int k = 0; k < m; k++) {
       const WarpReq &q = reqs[items[k].req];
       hg[k] = items[k].g;
       hg[k].crs = k;
+      hg[k].geoloc = 0;
+      if (items[k].gl) {
+        hgl[k] = items[k].gl->d;
+        hg[k].geoloc = k + 1;
+        any_gl = true;
+      }
       hc[k] = items[k].src;
       std::memcpy(ht[k].dst_geot, q.dst_gt, sizeof(ht[k].dst_geot));
       ht[k].width = q.width;
@@ -681,6 +914,7 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     rc.cov_stride = 0;
     rc.workspace = base + o_ws; rc.workspace_bytes = ws;
     rc.stream = d.stream;
+    rc.geolocs = any_gl ? (const GeoLocD *)(base + o_gl) : nullptr;
     int32_t *dbbox = (int32_t *)(base + o_bbox), *ddt = (int32_t *)(base + o_dtype);
     double *dnd = (double *)(base + o_nodata);
     int32_t *dst = (int32_t *)(base + o_stats);
@@ -738,6 +972,8 @@ int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGe
   q.has_src_gt = srcGeot ? 1 : 0;
   if (srcGeot) std::memcpy(q.src_gt, srcGeot, sizeof(q.src_gt));
   q.geoloc = geoLocOpts ? 1 : 0;
+  if (geoLocOpts)   // NULL-terminated (warp.go:514-526)
+    for (int k = 0; geoLocOpts[k] && k < 64; k++) q.geoloc_opts.push_back(geoLocOpts[k]);
   q.has_dst_srs = dstProjRef ? 1 : 0;
   if (dstProjRef) q.dst_srs = dstProjRef;
   std::memcpy(q.dst_gt, dstGeot, sizeof(q.dst_gt));

@@ -27,6 +27,7 @@ struct RenderCall {
   int64_t cov_stride;           // that image's row stride in elements
   void *workspace; int64_t workspace_bytes;
   hipStream_t stream;
+  const GeoLocD *geolocs = nullptr;   // geolocation transformers of the granules (dev), or NULL
 };
 
 int launch_render(const RenderCall &c, const int32_t *out_ns, int n_out, const gskyhip_scale_params &sp,

@@ -54,6 +54,7 @@ struct PlanArgs {
   int sep;                     // 1: plan_rows uses the separable transform where it applies
   int n_granules;
   struct GEdge *gedge;         // per granule: SuggestedWarpOutput2 edge samples in dst georef (or NULL)
+  const GeoLocD *geolocs;      // granule.geoloc k > 0: entry k - 1 (device), or NULL
   int small;                   // 1: plan_pairs finds each pair's tile itself, plan_small_kernel plans the rest
 };
 
@@ -172,8 +173,13 @@ constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 // georeferenced coordinates (the same expressions and order).
 __device__ __forceinline__ bool src_to_dst_georef(const Xform &t, double x, double y, double &X, double &Y) {
   const double *g1 = t.src_gt;
-  X = g1[0] + x * g1[1] + y * g1[2];
-  Y = g1[3] + x * g1[4] + y * g1[5];
+  if (t.gl) {
+    X = x; Y = y;
+    if (!geoloc_forward(*t.gl, X, Y)) return false;
+  } else {
+    X = g1[0] + x * g1[1] + y * g1[2];
+    Y = g1[3] + x * g1[4] + y * g1[5];
+  }
   if (t.reproject) {
     double lam, phi;
     if (!crs_inverse(t.src, X, Y, lam, phi)) return false;
@@ -200,6 +206,7 @@ __global__ __launch_bounds__(128) void plan_prologue_kernel(PlanArgs a, int n_ed
   const gskyhip_granule &gr = a.granules[g];
   Xform t;
   t.src = a.crs[gr.crs];
+  t.gl = (gr.geoloc > 0 && a.geolocs) ? a.geolocs + (gr.geoloc - 1) : nullptr;
   t.reproject = 0;
   if (a.dst_crs >= 0) {
     t.dst = a.crs[a.dst_crs];
@@ -606,6 +613,7 @@ __device__ void plan_pair(const PlanArgs &a, int p, double *sx, double *sy, int 
   Xform &t = ts;
   if (lane == 0) {
     t.src = a.crs[g.crs];
+    t.gl = (g.geoloc > 0 && a.geolocs) ? a.geolocs + (g.geoloc - 1) : nullptr;
     t.reproject = 0;
     if (a.dst_crs >= 0) {
       t.dst = a.crs[a.dst_crs];
@@ -637,7 +645,7 @@ __device__ void plan_pair(const PlanArgs &a, int p, double *sx, double *sy, int 
   // ---- overview pick (warp.go:156-198)
   const void *band = g.data;
   int bandX = g.xsize, bandY = g.ysize;
-  if (err == 0 && g.n_ovr > 0) {
+  if (!t.gl && err == 0 && g.n_ovr > 0) {   // never with geolocation arrays (warp.go:158)
     const double targetRatio = 1.0 / psx;
     if (targetRatio > 1.0) {
       int iOvr = -1;
@@ -738,6 +746,7 @@ __global__ __launch_bounds__(64) void extent_kernel(const gskyhip_granule *granu
   const gskyhip_granule &g = granules[i];
   Xform t;
   t.src = crs[g.crs];
+  t.gl = nullptr;   // ComputeReprojectExtent: no geolocation arrays (warp.go:433-487)
   t.reproject = 0;
   if (dst_crs >= 0) {
     t.dst = crs[dst_crs];
@@ -1620,6 +1629,7 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   a.pool_cap = cv.pool_cap; a.split_list = cv.split_list; a.complex_list = cv.complex_list;
   a.entries = cv.entries;
   a.sepcols = cv.sepcols;
+  a.geolocs = rc.geolocs;
   a.sep = 1;   // separable row transform (plan_cols_kernel); 0 = three full transforms per row
 #ifdef GSKYHIP_AB
   if (const char *sep = getenv("GSKYHIP_PLAN_SEP")) a.sep = atoi(sep);

@@ -164,6 +164,8 @@ void put_req(Out &o, const WarpReq &q) {
   for (double v : q.src_gt) o.put(v);
   for (double v : q.dst_gt) o.put(v);
   o.put(q.width); o.put(q.height); o.put(q.srs_cf);
+  o.put((int32_t)q.geoloc_opts.size());
+  for (const std::string &g : q.geoloc_opts) o.put_str(g);
 }
 
 bool get_req(In &in, WarpReq &q) {
@@ -176,6 +178,9 @@ bool get_req(In &in, WarpReq &q) {
   for (double &v : q.src_gt) v = in.get<double>();
   for (double &v : q.dst_gt) v = in.get<double>();
   q.width = in.get<int32_t>(); q.height = in.get<int32_t>(); q.srs_cf = in.get<int32_t>();
+  const int32_t ng = in.get<int32_t>();
+  if (ng < 0 || ng > 64) return false;
+  for (int32_t k = 0; k < ng && in.ok; k++) q.geoloc_opts.push_back(in.get_str());
   return in.ok;
 }
 

@@ -21,6 +21,7 @@ struct WarpReq {
   double src_gt[6] = {0, 0, 0, 0, 0, 0};
   double dst_gt[6] = {0, 0, 0, 0, 0, 0};
   int32_t width = 0, height = 0, srs_cf = 0;
+  std::vector<std::string> geoloc_opts;   // GeoLocOpts "KEY=VALUE" strings (geoloc != 0)
 };
 
 // Its outputs: return code (0, 1 open failed, 2 band failed, 3 transformer

@@ -160,16 +160,25 @@ def drill_dataset(geometries: Sequence[str], dataset_srs: Optional[str], geot: S
     total = C.c_int64()
     srs = dataset_srs.encode() if dataset_srs else None
     L = lib()
-    args = (arr, n, srs, gt, xsize, ysize, win.ctypes.data_as(C.c_void_p), off.ctypes.data_as(C.c_void_p),
-            C.byref(total))
-    check(L.gskyhip_drill_descriptors_device(*args, None, st.ctypes.data_as(C.c_void_p), _stream()),
-          "drill_descriptors_device")
-    masks = torch.empty(int(total.value), dtype=torch.uint8, device=dev)
-    check(L.gskyhip_drill_descriptors_device(*args, C.c_void_p(masks.data_ptr()), st.ctypes.data_as(C.c_void_p),
-                                             _stream()), "drill_descriptors_device")
+    # one pass: the library describes every polygon once and asks for the
+    # mask buffer through the callback (a torch tensor kept here)
+    held = []
+
+    def alloc(_ctx, nbytes):
+        t = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
+        held.append(t)
+        return t.data_ptr()
+    cb = _ALLOC_FN(alloc)
+    mptr = C.c_void_p()
+    check(L.gskyhip_drill_masks_device(arr, n, srs, gt, xsize, ysize, win.ctypes.data_as(C.c_void_p),
+                                       off.ctypes.data_as(C.c_void_p), C.byref(total), cb, None, C.byref(mptr),
+                                       st.ctypes.data_as(C.c_void_p), _stream()), "drill_masks_device")
+    masks = held[0]
     mb = MaskBatch(torch.from_numpy(win[:n].copy()).to(dev), torch.from_numpy(off[:n].copy()).to(dev), masks)
     return mb, st[:n]
 
+
+_ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int64)
 
 REFERENCE_ORDER, WAVE_SPLIT = 0, 1
 

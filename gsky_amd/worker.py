@@ -115,9 +115,10 @@ def warp_raster(req: GeoRPCGranule) -> Result:
     nod = C.c_double()
     dt = C.c_int()
     br = C.c_int()
-    if req.geoLocOpts:
-        return Result(error="warp_operation() fail: 3")
-    rc = L.warp_operation_fast(req.path.encode(), src, src_gt, None, dst, dst_gt, req.width, req.height,
+    geo = None
+    if req.geoLocOpts:   # NULL-terminated C strings (warp.go:514-526)
+        geo = (C.c_char_p * (len(req.geoLocOpts) + 1))(*[o.encode() for o in req.geoLocOpts], None)
+    rc = L.warp_operation_fast(req.path.encode(), src, src_gt, geo, dst, dst_gt, req.width, req.height,
                                req.bands[0], req.sRSCf, C.byref(buf), C.byref(size), bbox, C.byref(nod),
                                C.byref(dt), C.byref(br))
     if rc != 0:

@@ -89,7 +89,8 @@ typedef struct {
     uint32_t polygon_hash;       /* fnv32a(GeoTileGranule.Polygon)               */
     int32_t block_x, block_y;    /* GDALGetBlockSize of the band (0: xsize x 1);  *
                                   * only bytesRead (warp.go:347) depends on it    */
-    int32_t _pad2;
+    int32_t geoloc;              /* 0; k > 0: the k-th geolocation transformer of *
+                                  * the call (the drop-in's GeoLocOpts requests) */
 } gskyhip_granule;
 
 /* One output tile of a GetMap batch.  Granules of the tile are
@@ -538,6 +539,22 @@ int gskyhip_drill_descriptors_device(const char *const *geometries, int n, const
                                      const double *geot, int xsize, int ysize, int32_t *win_out,
                                      int64_t *mask_off_out, int64_t *mask_bytes_out, uint8_t *masks_dev,
                                      int32_t *status_out, void *stream);
+
+/* Device memory supplier of gskyhip_drill_masks_device: returns at least
+ * `bytes` of device memory (or NULL), owned by the caller (cgo: a hipMalloc
+ * wrapper; Python: a torch tensor kept alive by the caller). */
+typedef void *(*gskyhip_alloc_fn)(void *ctx, int64_t bytes);
+
+/* gskyhip_drill_descriptors_device in one pass (getDrillFileDescriptor +
+ * createMask, drill.go:363-423 / 275-327, for a whole WPS request): every
+ * polygon described once on up to 16 host threads, then alloc(alloc_ctx,
+ * *mask_bytes_out) supplies the mask buffer (returned in *masks_dev_out) and
+ * the masks are rasterized into it on `stream`.  GSKYHIP_E_HIP if alloc
+ * returns NULL. */
+int gskyhip_drill_masks_device(const char *const *geometries, int n, const char *dataset_srs, const double *geot,
+                               int xsize, int ysize, int32_t *win_out, int64_t *mask_off_out,
+                               int64_t *mask_bytes_out, gskyhip_alloc_fn alloc, void *alloc_ctx,
+                               uint8_t **masks_dev_out, int32_t *status_out, void *stream);
 int gskyhip_drill_merge(const double *values, const int32_t *counts, int n_files,
                         int n_dates, double *out, void *stream);
 

@@ -857,10 +857,172 @@ static void inv_geot(const double *gt, double *o) {   /* GDALInvGeoTransform */
     o[5] = gt[1] * inv_det;
 }
 
+/* ---- GDAL 3.0.1 geolocation-array transformer (alg/gdalgeoloc.cpp) [ext]
+ * selected by warp.go:128-141 (createGeoLocTransformer, 52-67) for requests
+ * with GeoLocOpts (tile_grpc.go:338-350).  Restated from the published
+ * algorithm; parity unpinned (GDAL absent).
+ *   GeoLocLoadFullData: X / Y bands as double; one-row X and Y bands form a
+ *     regular grid (X per column, Y per row).
+ *   GeoLocGenerateBackMap: extent of the valid points (X nodata excluded),
+ *     pixel size sqrt(area / (nx * ny * 1.3)), a grid of ceil(extent / size)
+ *     + 1 cells whose origin is half a cell outside the extent; every point
+ *     splatted bilinearly onto the 4 cells around it with its source
+ *     pixel / line (i * STEP + OFFSET); cells of weight > 0.25 averaged,
+ *     the rest -1; 3 hole-filling sweeps, a hole taking the mean of its set
+ *     4-neighbours (cells filled in a sweep are used from the next one).
+ *   GDALGeoLocTransform: pixel/line -> georef by bilinear interpolation of
+ *     the arrays (nearest square extended beyond them, nodata corners
+ *     falling back to the edge / corner rules); georef -> pixel/line by
+ *     bilinear interpolation of the backmap where its 4 cells are set, else
+ *     its nearest cell. */
+int oracle_geoloc_init(oracle_geoloc *g, const double *xb, int xw, int xh, const double *yb, int yw, int yh,
+                       int has_nodata, double nodata_x, double pixel_offset, double line_offset,
+                       double pixel_step, double line_step) {
+    memset(g, 0, sizeof(*g));
+    const int regular = xh == 1 && yh == 1;
+    const int nx = xw, ny = regular ? yw : xh;
+    if (nx <= 0 || ny <= 0 || (!regular && (yw != xw || yh != xh))) return 3;
+    g->nx = nx; g->ny = ny;
+    g->gx = (double *)malloc(sizeof(double) * (size_t)nx * ny);
+    g->gy = (double *)malloc(sizeof(double) * (size_t)nx * ny);
+    for (int j = 0; j < ny; j++)
+        for (int i = 0; i < nx; i++) {
+            g->gx[(size_t)j * nx + i] = regular ? xb[i] : xb[(size_t)j * nx + i];
+            g->gy[(size_t)j * nx + i] = regular ? yb[j] : yb[(size_t)j * nx + i];
+        }
+    g->has_nodata = has_nodata; g->nodata_x = nodata_x;
+    g->pixel_offset = pixel_offset; g->line_offset = line_offset;
+    g->pixel_step = pixel_step; g->line_step = line_step;
+    /* the backmap */
+    double mnx = 0, mxx = 0, mny = 0, mxy = 0;
+    int any = 0;
+    for (long i = (long)nx * ny - 1; i >= 0; i--) {
+        const double X = g->gx[i], Y = g->gy[i];
+        if (has_nodata && X == nodata_x) continue;
+        if (!any) { mnx = mxx = X; mny = mxy = Y; any = 1; continue; }
+        if (X < mnx) mnx = X;
+        if (X > mxx) mxx = X;
+        if (Y < mny) mny = Y;
+        if (Y > mxy) mxy = Y;
+    }
+    const double size = sqrt((mxx - mnx) * (mxy - mny) / ((double)nx * ny * 1.3));
+    if (!(size > 0.0) || isinf(size)) return 3;
+    const double fw = ceil((mxx - mnx) / size) + 1, fh = ceil((mxy - mny) / size) + 1;
+    if (!(fw > 0 && fw < 4194304.0) || !(fh > 0 && fh < 4194304.0) || fw * fh > 4.0e9) return 3;
+    const int bw = (int)fw, bh = (int)fh;
+    const double x0 = mnx - size / 2.0, y0 = mxy + size / 2.0;
+    g->bw = bw; g->bh = bh;
+    g->bgt[0] = x0; g->bgt[1] = size; g->bgt[2] = 0.0; g->bgt[3] = y0; g->bgt[4] = 0.0; g->bgt[5] = -size;
+    const size_t nc = (size_t)bw * bh;
+    g->bmx = (float *)calloc(nc, sizeof(float));
+    g->bmy = (float *)calloc(nc, sizeof(float));
+    float *w = (float *)calloc(nc, sizeof(float));
+    for (int iy = 0; iy < ny; iy++)
+        for (int ix = 0; ix < nx; ix++) {
+            const size_t k = (size_t)iy * nx + ix;
+            if (has_nodata && g->gx[k] == nodata_x) continue;
+            const double cx = (g->gx[k] - x0) / size - 0.5, cy = (y0 - g->gy[k]) / size - 0.5;
+            const int c0 = (int)floor(cx), r0 = (int)floor(cy);
+            const double ax = cx - c0, ay = cy - r0;
+            const double p = ix * pixel_step + pixel_offset, l = iy * line_step + line_offset;
+            const double wt[4] = {(1.0 - ax) * (1.0 - ay), ax * (1.0 - ay), (1.0 - ax) * ay, ax * ay};
+            for (int q = 0; q < 4; q++) {
+                const int c = c0 + (q & 1), r = r0 + (q >> 1);
+                if (c < 0 || c >= bw || r < 0 || r >= bh) continue;
+                const size_t o = (size_t)r * bw + c;
+                g->bmx[o] += (float)(p * wt[q]);
+                g->bmy[o] += (float)(l * wt[q]);
+                w[o] += (float)wt[q];
+            }
+        }
+    for (size_t o = 0; o < nc; o++) {
+        if (w[o] > 0.25f) { g->bmx[o] /= w[o]; g->bmy[o] /= w[o]; w[o] = 4.0f; }
+        else { g->bmx[o] = -1.0f; g->bmy[o] = -1.0f; w[o] = 0.0f; }
+    }
+    for (int pass = 0; pass < 3; pass++) {
+        const float mark = (float)(3 - pass);
+        size_t set = 0;
+        for (int r = 0; r < bh; r++)
+            for (int c = 0; c < bw; c++) {
+                const size_t o = (size_t)r * bw + c;
+                if (g->bmx[o] >= 0) { set++; continue; }
+                const long nb[4] = {c > 0 ? (long)o - 1 : -1, c + 1 < bw ? (long)o + 1 : -1,
+                                    r > 0 ? (long)o - bw : -1, r + 1 < bh ? (long)o + bw : -1};
+                double sx = 0.0, sy = 0.0;
+                int n = 0;
+                for (int q = 0; q < 4; q++)
+                    if (nb[q] >= 0 && w[nb[q]] > mark) { sx += g->bmx[nb[q]]; sy += g->bmy[nb[q]]; n++; }
+                if (n) { g->bmx[o] = (float)(sx / n); g->bmy[o] = (float)(sy / n); w[o] = mark; }
+            }
+        if (set == nc) break;
+    }
+    free(w);
+    return 0;
+}
+
+void oracle_geoloc_free(oracle_geoloc *g) {
+    free(g->gx); free(g->gy); free(g->bmx); free(g->bmy);
+    memset(g, 0, sizeof(*g));
+}
+
+static int geoloc_fwd(const oracle_geoloc *g, double *x, double *y) {
+    if (*x == HUGE_VAL || *y == HUGE_VAL) return 0;
+    const double gp = (*x - g->pixel_offset) / g->pixel_step, gl = (*y - g->line_offset) / g->line_step;
+    int ix = go_cvtt32(gp), iy = go_cvtt32(gl);
+    if (ix < 0) ix = 0;
+    if (ix > g->nx - 1) ix = g->nx - 1;
+    if (iy < 0) iy = 0;
+    if (iy > g->ny - 1) iy = g->ny - 1;
+    const size_t k = (size_t)iy * g->nx + ix;
+    const double *X = g->gx + k, *Y = g->gy + k;
+    const int nx = g->nx;
+    const double nd = g->nodata_x;
+    if (g->has_nodata && X[0] == nd) return 0;
+    const double u = gp - ix, v = gl - iy;
+    if (ix + 1 < g->nx && iy + 1 < g->ny && (!g->has_nodata || (X[1] != nd && X[nx] != nd && X[nx + 1] != nd))) {
+        *x = (1 - v) * (X[0] + u * (X[1] - X[0])) + v * (X[nx] + u * (X[nx + 1] - X[nx]));
+        *y = (1 - v) * (Y[0] + u * (Y[1] - Y[0])) + v * (Y[nx] + u * (Y[nx + 1] - Y[nx]));
+    } else if (ix + 1 < g->nx && (!g->has_nodata || X[1] != nd)) {
+        *x = X[0] + u * (X[1] - X[0]);
+        *y = Y[0] + u * (Y[1] - Y[0]);
+    } else if (iy + 1 < g->ny && (!g->has_nodata || X[nx] != nd)) {
+        *x = X[0] + v * (X[nx] - X[0]);
+        *y = Y[0] + v * (Y[nx] - Y[0]);
+    } else {
+        *x = X[0];
+        *y = Y[0];
+    }
+    return 1;
+}
+
+static int geoloc_inv(const oracle_geoloc *g, double *x, double *y) {
+    if (*x == HUGE_VAL || *y == HUGE_VAL) return 0;
+    const double cx = (*x - g->bgt[0]) / g->bgt[1] - 0.5, cy = (*y - g->bgt[3]) / g->bgt[5] - 0.5;
+    if (!(cx > -0.5 && cy > -0.5 && cx < g->bw - 0.5 && cy < g->bh - 0.5)) return 0;
+    const int c = (int)floor(cx), r = (int)floor(cy);
+    const long bw = g->bw;
+    if (c >= 0 && r >= 0 && c + 1 < g->bw && r + 1 < g->bh) {
+        const size_t o = (size_t)r * bw + c;
+        const float *MX = g->bmx + o, *MY = g->bmy + o;
+        if (MX[0] >= 0 && MX[1] >= 0 && MX[bw] >= 0 && MX[bw + 1] >= 0) {
+            const double u = cx - c, v = cy - r;
+            *x = (1 - u) * (1 - v) * MX[0] + u * (1 - v) * MX[1] + (1 - u) * v * MX[bw] + u * v * MX[bw + 1];
+            *y = (1 - u) * (1 - v) * MY[0] + u * (1 - v) * MY[1] + (1 - u) * v * MY[bw] + u * v * MY[bw + 1];
+            return 1;
+        }
+    }
+    const size_t o = (size_t)floor(cy + 0.5) * bw + (size_t)floor(cx + 0.5);
+    if (g->bmx[o] < 0) return 0;
+    *x = g->bmx[o];
+    *y = g->bmy[o];
+    return 1;
+}
+
 typedef struct {
     oracle_crs src, dst;
     int reproject;
     double src_gt[6], src_igt[6], dst_gt[6], dst_igt[6];
+    const oracle_geoloc *gl;   /* geolocation arrays in place of src_gt, or NULL */
 } gip_t;
 
 static void gip_init(gip_t *t, const oracle_crs *src, const oracle_crs *dst,
@@ -879,12 +1041,22 @@ static void gip_init(gip_t *t, const oracle_crs *src, const oracle_crs *dst,
 static int gip_point(const gip_t *t, int dst_to_src, double *x, double *y) {
     const double *g1 = dst_to_src ? t->dst_gt : t->src_gt;
     const double *g2 = dst_to_src ? t->src_igt : t->dst_igt;
-    double X = g1[0] + *x * g1[1] + *y * g1[2];
-    double Y = g1[3] + *x * g1[4] + *y * g1[5];
+    double X, Y;
+    if (t->gl && !dst_to_src) {
+        X = *x; Y = *y;
+        if (!geoloc_fwd(t->gl, &X, &Y)) return 0;
+    } else {
+        X = g1[0] + *x * g1[1] + *y * g1[2];
+        Y = g1[3] + *x * g1[4] + *y * g1[5];
+    }
     if (t->reproject) {
         const oracle_crs *from = dst_to_src ? &t->dst : &t->src;
         const oracle_crs *to = dst_to_src ? &t->src : &t->dst;
         if (!oracle_crs_transform(from, to, &X, &Y)) return 0;
+    }
+    if (t->gl && dst_to_src) {
+        *x = X; *y = Y;
+        return geoloc_inv(t->gl, x, y);
     }
     *x = g2[0] + X * g2[1] + Y * g2[2];
     *y = g2[3] + X * g2[4] + Y * g2[5];
@@ -1144,24 +1316,25 @@ static int bilinear_sample(const void *band, int dtype, int nx, int ny, int has_
     return 1;
 }
 
-int oracle_warp(const oracle_granule *g, const oracle_crs *src,
-                const oracle_crs *dst, const double dst_geot[6],
-                int dst_w, int dst_h, int resample,
-                void **out_buf, int *out_size, int32_t bbox[4],
-                double *nodata, int *dtype, int *bytes_read) {
+int oracle_warp_geoloc(const oracle_granule *g, const oracle_crs *src,
+                       const oracle_crs *dst, const double dst_geot[6],
+                       int dst_w, int dst_h, int resample, const oracle_geoloc *gl,
+                       void **out_buf, int *out_size, int32_t bbox[4],
+                       double *nodata, int *dtype, int *bytes_read) {
     *bytes_read = 0;
     double srcGeot[6];
     memcpy(srcGeot, g->geot, sizeof(srcGeot));
     gip_t t;
-    gip_init(&t, src, dst, srcGeot, dst_geot);                  /* warp.go:130 */
+    gip_init(&t, src, dst, srcGeot, dst_geot);                  /* warp.go:130 / 136 */
+    t.gl = gl;
     double geotOut[6], ext[4];
     int nPixels = 0, nLines = 0;
     const int err = suggested_warp_output(&t, g->xsize, g->ysize, geotOut, &nPixels, &nLines, ext);
 
-    /* overview pick, warp.go:156-198 */
+    /* overview pick, warp.go:156-198 (never with geolocation arrays, 158) */
     const void *band = g->data;
     int bandX = g->xsize, bandY = g->ysize;
-    if (err == 0 && g->n_ovr > 0) {
+    if (!gl && err == 0 && g->n_ovr > 0) {
         const double targetRatio = 1.0 / geotOut[1];
         if (targetRatio > 1.0) {
             const int srcXSize = g->xsize, srcYSize = g->ysize;
@@ -1277,6 +1450,15 @@ int oracle_warp(const oracle_granule *g, const oracle_crs *src,
     *dtype = outType;
     *out_buf = buf;
     return 0;
+}
+
+int oracle_warp(const oracle_granule *g, const oracle_crs *src,
+                const oracle_crs *dst, const double dst_geot[6],
+                int dst_w, int dst_h, int resample,
+                void **out_buf, int *out_size, int32_t bbox[4],
+                double *nodata, int *dtype, int *bytes_read) {
+    return oracle_warp_geoloc(g, src, dst, dst_geot, dst_w, dst_h, resample, NULL, out_buf, out_size, bbox,
+                              nodata, dtype, bytes_read);
 }
 
 /* ======================================================================== */

@@ -164,6 +164,31 @@ int oracle_warp(const oracle_granule *g, const oracle_crs *src,
                 void **out_buf, int *out_size, int32_t bbox[4],
                 double *nodata, int *dtype, int *bytes_read);
 
+/* GDAL 3.0.1 geolocation-array transformer (GDALCreateGeoLocTransformer,
+ * called by warp.go:52-67 for GeoLocOpts requests): the X / Y bands as
+ * double (xh == yh == 1: a regular grid), the X band's nodata, the
+ * PIXEL/LINE OFFSET/STEP options; builds the backmap.  Returns 0 or 3. */
+typedef struct {
+    double *gx, *gy;             /* ny x nx */
+    int nx, ny, has_nodata;
+    double nodata_x, pixel_offset, line_offset, pixel_step, line_step;
+    float *bmx, *bmy;            /* backmap bh x bw */
+    int bw, bh;
+    double bgt[6];
+} oracle_geoloc;
+int oracle_geoloc_init(oracle_geoloc *g, const double *x_band, int xw, int xh, const double *y_band, int yw,
+                       int yh, int has_nodata, double nodata_x, double pixel_offset, double line_offset,
+                       double pixel_step, double line_step);
+void oracle_geoloc_free(oracle_geoloc *g);
+
+/* oracle_warp with the geolocation transformer as the source side
+ * (warp.go:134-140; no overview, 158); gl NULL = oracle_warp. */
+int oracle_warp_geoloc(const oracle_granule *g, const oracle_crs *src,
+                       const oracle_crs *dst, const double dst_geot[6],
+                       int dst_w, int dst_h, int resample, const oracle_geoloc *gl,
+                       void **out_buf, int *out_size, int32_t bbox[4],
+                       double *nodata, int *dtype, int *bytes_read);
+
 /* GDALSuggestedWarpOutput2 restatement: extent in dst pixel space plus the
  * suggested geotransform.  Returns 0 on success (CE_None). */
 int oracle_suggested_warp_output(const oracle_granule *g, const oracle_crs *src,

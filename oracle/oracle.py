@@ -44,6 +44,14 @@ class Granule(C.Structure):
                 ("ovr_ysize", C.c_int32 * MAX_OVR), ("block_x", C.c_int32), ("block_y", C.c_int32)]
 
 
+class GeoLoc(C.Structure):
+    _fields_ = [("gx", C.c_void_p), ("gy", C.c_void_p), ("nx", C.c_int), ("ny", C.c_int),
+                ("has_nodata", C.c_int), ("nodata_x", C.c_double), ("pixel_offset", C.c_double),
+                ("line_offset", C.c_double), ("pixel_step", C.c_double), ("line_step", C.c_double),
+                ("bmx", C.c_void_p), ("bmy", C.c_void_p), ("bw", C.c_int), ("bh", C.c_int),
+                ("bgt", C.c_double * 6)]
+
+
 class FlexRaster(C.Structure):
     _fields_ = [("data", C.c_void_p), ("data_w", C.c_int32), ("data_h", C.c_int32),
                 ("width", C.c_int32), ("height", C.c_int32), ("off_x", C.c_int32),
@@ -90,6 +98,11 @@ def lib():
         L.oracle_warp.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp,
                                   C.POINTER(C.c_int), vp, C.POINTER(d), C.POINTER(C.c_int),
                                   C.POINTER(C.c_int)]
+        L.oracle_warp_geoloc.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, vp,
+                                         C.POINTER(C.c_int), vp, C.POINTER(d), C.POINTER(C.c_int),
+                                         C.POINTER(C.c_int)]
+        L.oracle_geoloc_init.argtypes = [vp, vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, d, d, d, d, d]
+        L.oracle_geoloc_free.argtypes = [vp]
         L.oracle_suggested_warp_output.argtypes = [vp, vp, vp, vp, vp, vp, C.POINTER(C.c_int),
                                                    C.POINTER(C.c_int), vp]
         L.oracle_approx_row.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, vp]
@@ -279,6 +292,49 @@ def warp(g: Granule, src: Crs, dst, dst_geot, w, h, resample=0):
     arr = arr.reshape(int(bbox[3]), int(bbox[2]))
     warp.bytes_read = br.value        # warp.go:347 of the last call
     return arr, bbox.copy(), nd.value, dt.value
+
+
+def geoloc(x_band: np.ndarray, y_band: np.ndarray, nodata_x=None, pixel_offset=0.0, line_offset=0.0,
+           pixel_step=1.0, line_step=1.0) -> GeoLoc:
+    """GDALCreateGeoLocTransformer restated (oracle_geoloc_init): the X / Y
+    bands (2-D, or both one row: a regular grid) and the GeoLocOpts numbers
+    (tile_grpc.go:338-350).  Freed with the returned object."""
+    gl = GeoLoc()
+    xb = np.ascontiguousarray(x_band, np.float64)
+    yb = np.ascontiguousarray(y_band, np.float64)
+    xb2, yb2 = xb.reshape(-1, xb.shape[-1]), yb.reshape(-1, yb.shape[-1])
+    rc = lib().oracle_geoloc_init(C.byref(gl), _ptr(xb2), xb2.shape[1], xb2.shape[0], _ptr(yb2), yb2.shape[1],
+                                  yb2.shape[0], int(nodata_x is not None),
+                                  float(nodata_x if nodata_x is not None else 0.0), pixel_offset, line_offset,
+                                  pixel_step, line_step)
+    if rc:
+        raise RuntimeError("GDALCreateGeoLocTransformer failed")
+    gl._lib = lib()
+    return gl
+
+
+def free_geoloc(gl: GeoLoc) -> None:
+    lib().oracle_geoloc_free(C.byref(gl))
+
+
+def warp_geoloc(g: Granule, src: Crs, dst, dst_geot, w, h, gl: GeoLoc, resample=0):
+    """warp_operation_fast with GeoLocOpts (warp.go:128-141, 158)."""
+    buf = C.c_void_p()
+    size = C.c_int()
+    bbox = np.zeros(4, np.int32)
+    nd = C.c_double()
+    dt = C.c_int()
+    br = C.c_int()
+    gt = np.ascontiguousarray(dst_geot, np.float64)
+    rc = lib().oracle_warp_geoloc(C.byref(g), C.byref(src), C.byref(dst) if dst is not None else None,
+                                  _ptr(gt), w, h, resample, C.byref(gl), C.byref(buf), C.byref(size), _ptr(bbox),
+                                  C.byref(nd), C.byref(dt), C.byref(br))
+    if rc:
+        raise RuntimeError("warp_operation() fail: %d" % rc)
+    arr = np.frombuffer(C.string_at(buf, size.value), dtype=NP_OF[dt.value]).copy()
+    C.CDLL(None).free(buf)
+    warp_geoloc.bytes_read = br.value
+    return arr.reshape(int(bbox[3]), int(bbox[2])), bbox.copy(), nd.value, dt.value
 
 
 def suggested_warp_output(g: Granule, src: Crs, dst: Crs, dst_geot):

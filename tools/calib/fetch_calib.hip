@@ -8,6 +8,8 @@
 //            upsampling pattern of render_nn_kernel over an int16 granule)
 //   gather4  4 B per lane, the same pattern over a float32 granule
 //   read2    2 B per lane, consecutive (1:1)
+//   read8    8 B per lane, consecutive (the 2-tap loads of render_bil_kernel)
+//   gather8  8 B per lane, lane i reads element i/2
 //   store4   4 B per lane consecutive stores (the RGBA tile rows)
 //   store16  16 B per lane streaming stores (the guide's known case: exact)
 // Run: fetch_calib <launches>, under rocprofv3 --pmc FETCH_SIZE (one pass)
@@ -51,6 +53,24 @@ __global__ __launch_bounds__(256) void read2(const uint16_t *__restrict__ in, si
   if (acc == 0x1234u) sink[0] = acc;   // reachable for 16-bit values too (else the loop is dead code)
 }
 
+__global__ __launch_bounds__(256) void read8(const uint2 *__restrict__ in, size_t n, uint32_t *__restrict__ sink) {
+  uint32_t acc = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const uint2 v = in[i];
+    acc ^= v.x ^ v.y;
+  }
+  if (acc == 0x1234u) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void gather8(const uint2 *__restrict__ in, size_t n_out, uint32_t *__restrict__ sink) {
+  uint32_t acc = 0;
+  for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < n_out; o += (size_t)gridDim.x * blockDim.x) {
+    const uint2 v = in[o >> 1];
+    acc ^= v.x ^ v.y;
+  }
+  if (acc == 0x1234u) sink[0] = acc;
+}
+
 __global__ __launch_bounds__(256) void store4(uint32_t *__restrict__ out, size_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     out[i] = (uint32_t)i;
@@ -75,13 +95,15 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(gather_half<uint16_t>, grid, block, 0, 0, (const uint16_t *)buf, bytes / 2 * 2, sink);
     hipLaunchKernelGGL(gather_half<float>, grid, block, 0, 0, (const float *)buf, bytes / 4 * 2, sink);
     hipLaunchKernelGGL(read2, grid, block, 0, 0, (const uint16_t *)buf, bytes / 2, sink);
+    hipLaunchKernelGGL(read8, grid, block, 0, 0, (const uint2 *)buf, bytes / 8, sink);
+    hipLaunchKernelGGL(gather8, grid, block, 0, 0, (const uint2 *)buf, bytes / 8 * 2, sink);
     hipLaunchKernelGGL(store4, grid, block, 0, 0, (uint32_t *)buf, bytes / 4);
     hipLaunchKernelGGL(store16, grid, block, 0, 0, (uint4 *)buf, bytes / 16);
   }
   CHECK(hipGetLastError());
   CHECK(hipDeviceSynchronize());
   std::printf("{\"distinct_bytes_per_launch\": %zu, \"kernels\": [\"read16\", \"gather_half<ushort>\", "
-              "\"gather_half<float>\", \"read2\", \"store4\", \"store16\"], \"launches\": %d}\n",
+              "\"gather_half<float>\", \"read2\", \"read8\", \"gather8\", \"store4\", \"store16\"], \"launches\": %d}\n",
               bytes, launches);
   CHECK(hipFree(buf));
   CHECK(hipFree(sink));
