@@ -170,8 +170,9 @@ def lib() -> C.CDLL:
     L.gskyhip_drill_merge.argtypes = [vp, vp, ci, ci, vp, vp]
     L.gskyhip_drill_descriptors_device.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci,
                                                    vp, vp, C.POINTER(i64), vp, vp, vp]
-    L.gskyhip_drill_masks_device.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci, vp, vp,
-                                             C.POINTER(i64), vp, vp, C.POINTER(vp), vp, vp]
+    if hasattr(L, "gskyhip_drill_masks_device"):   # absent from kept earlier builds (GSKYHIP_LIB=<name>)
+        L.gskyhip_drill_masks_device.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci, vp,
+                                                 vp, C.POINTER(i64), vp, vp, C.POINTER(vp), vp, vp]
     L.gskyhip_band_math.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(vp), vp, vp, ci, i64, d,
                                     vp, vp]
     L.gskyhip_drill_deciles_workspace_size.argtypes = [ci, i64, ci]

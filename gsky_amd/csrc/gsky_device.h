@@ -610,10 +610,12 @@ __device__ __forceinline__ bool fix_range_ok(double v0, double dv, int n) {
   return fabs(v0) < lim && fabs(v1) < lim && fabs(dv) < 1024.0;
 }
 
-__device__ __forceinline__ RowFix row_fix(const RowRec &r, int n) {
+// need_inside: the NN kernel's rows (their fixed form is used only where
+// every source pixel lies in the band); the bilinear kernel takes any LINEAR row.
+__device__ __forceinline__ RowFix row_fix(const RowRec &r, int n, bool need_inside) {
   RowFix f;
   f.x0 = kFixNone; f.y0 = 0; f.dx = 0; f.dy = 0;
-  if (r.kind == ROW_LINEAR && r.inside && n > 0 && n <= kFixMaxW && fix_range_ok(r.v[0], r.v[2], n) &&
+  if (r.kind == ROW_LINEAR && (r.inside || !need_inside) && n > 0 && n <= kFixMaxW && fix_range_ok(r.v[0], r.v[2], n) &&
       fix_range_ok(r.v[1], r.v[3], n)) {
     const double s = 4294967296.0;   // scaling by 2^32 is exact
     f.x0 = __double2ll_rn(r.v[0] * s);

@@ -55,6 +55,7 @@ struct PlanArgs {
   int n_granules;
   struct GEdge *gedge;         // per granule: SuggestedWarpOutput2 edge samples in dst georef (or NULL)
   const GeoLocD *geolocs;      // granule.geoloc k > 0: entry k - 1 (device), or NULL
+  int resample;                // GSKYHIP_RESAMPLE_* of the call (the rows' fixed forms)
   int small;                   // 1: plan_pairs finds each pair's tile itself, plan_small_kernel plans the rest
 };
 
@@ -1136,7 +1137,7 @@ __device__ __forceinline__ void plan_row(const PlanArgs &a, int p, const PairPla
     }
   }
   a.rows[(long)p * a.max_h + row] = rec;
-  a.rowfix[(long)p * a.max_h + row] = row_fix(rec, n);
+  a.rowfix[(long)p * a.max_h + row] = row_fix(rec, n, a.resample != GSKYHIP_RESAMPLE_BILINEAR);
 }
 
 // Workgroups of one pair (blockIdx.x: pair, blockIdx.y: 256-row chunk): the
@@ -1630,6 +1631,7 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   a.entries = cv.entries;
   a.sepcols = cv.sepcols;
   a.geolocs = rc.geolocs;
+  a.resample = rc.resample;
   a.sep = 1;   // separable row transform (plan_cols_kernel); 0 = three full transforms per row
 #ifdef GSKYHIP_AB
   if (const char *sep = getenv("GSKYHIP_PLAN_SEP")) a.sep = atoi(sep);

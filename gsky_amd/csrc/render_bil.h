@@ -30,12 +30,81 @@ namespace gsky {
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
+// The same with a NaN nodata allowed (the fp64 row path, round 3's code).
+template <typename WT>
+__device__ __forceinline__ void bil_fold4_any(u32x2 t0, u32x2 t1, WT rx, WT ry, int ic, int lim, float nd, float ndf,
+                                              bool nd_nan, bool hnd, float fillv, bool fill_mode, float &c) {
+  const float tv[4] = {__uint_as_float(t0.x), __uint_as_float(t0.y), __uint_as_float(t1.x), __uint_as_float(t1.y)};
+  const WT one = (WT)1.0;
+  const WT wx[2] = {rx, one - rx}, wy[2] = {ry, one - ry};
+  WT accR = (WT)0.0;
+  bool anynd = false;
+#pragma unroll
+  for (int kk = 0; kk < 4; kk++) {
+    accR += (WT)tv[kk] * (wx[kk & 1] * wy[kk >> 1]);
+    anynd = anynd | (nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+  }
+  anynd = anynd & hnd;
+  float v = (float)accR;
+  if (anynd) {
+    WT aR = (WT)0.0, aD = (WT)0.0;
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) {
+      const WT w = wx[kk & 1] * wy[kk >> 1];
+      const bool use = !(nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+      aD += use ? w : (WT)0.0;
+      aR += use ? (WT)tv[kk] * w : (WT)0.0;
+    }
+    v = fillv;
+    if (aD == (WT)1.0) v = (float)aR;
+    else if (aD >= (WT)0.00001) v = (float)(aR / aD);
+  }
+  const bool take = ((unsigned)ic < (unsigned)lim) & (v != nd) & (!fill_mode | (c == nd));
+  c = take ? v : c;
+}
+
+// The sample of one pixel whose 2x2 taps are all inside the band (t0: x and
+// x + 1 of the upper source row, t1 of the lower; rx / ry the weights of x
+// and y) and its fold into the canvas value c: the four weights sum to 1
+// within fp32 rounding, so the sample is accR unless a tap holds nodata
+// (then the taps are dropped and the weights renormalised: bil_sample's
+// rule).  The dropped-tap sums are formed for every pixel (a few selects);
+// only their division sits behind a branch.  NaN nodata: the fp64 path.
+template <typename WT>
+__device__ __forceinline__ void bil_fold4(u32x2 t0, u32x2 t1, WT rx, WT ry, int ic, int lim, float nd, float ndf,
+                                          bool hnd, float fillv, bool fill_mode, float &c) {
+  const float tv[4] = {__uint_as_float(t0.x), __uint_as_float(t0.y), __uint_as_float(t1.x), __uint_as_float(t1.y)};
+  const WT one = (WT)1.0;
+  const WT wx[2] = {rx, one - rx}, wy[2] = {ry, one - ry};
+  WT accR = (WT)0.0, aR = (WT)0.0, aD = (WT)0.0;
+  bool anynd = false;
+#pragma unroll
+  for (int kk = 0; kk < 4; kk++) {
+    const WT w = wx[kk & 1] * wy[kk >> 1];
+    const WT p = (WT)tv[kk] * w;
+    const bool isnd = hnd & (tv[kk] == ndf);
+    accR += p;
+    aR += isnd ? (WT)0.0 : p;
+    aD += isnd ? (WT)0.0 : w;
+    anynd = anynd | isnd;
+  }
+  float v = (float)accR;
+  if (anynd) {
+    v = fillv;
+    if (aD == (WT)1.0) v = (float)aR;
+    else if (aD >= (WT)0.00001) v = (float)(aR / aD);
+  }
+  const bool take = ((unsigned)ic < (unsigned)lim) & (v != nd) & (!fill_mode | (c == nd));
+  c = take ? v : c;
+}
+
 // HP: pixels whose taps are in flight together; WPS: waves per SIMD the
 // register budget is sized for.
-template <typename WT, int RPW, int HP, int WPS>
+template <typename WT, int RPW, int HP, int WPS, bool FIX = true>
 __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                             const int32_t *__restrict__ order,
                                                             const RowRec *__restrict__ rows,
+                                                            const RowFix *__restrict__ rowfix,
                                                             const Leaf *__restrict__ pool,
                                                             const TilePlan *__restrict__ tplans,
                                                             const gskyhip_tile *__restrict__ tiles, int n_items) {
@@ -142,7 +211,69 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
       // the nodata test of a tap in float32 (exact: the band's nodata is a float32 value or NaN)
       const bool nd_f32 = !hnd || nd_nan || (double)(float)nd64 == nd64;
       const float ndf = (float)nd64;
-      if (kind == ROW_LINEAR) {   // HP pixels' taps in flight
+      bool fixed_done = false;
+      if (FIX && kind == ROW_LINEAR && nd_f32 && !nd_nan) {
+        // the row's fixed-point form (RowFix): s - 0.5 as 32.32 integers --
+        // the tap is the integer part, the fraction gives the weight
+        // (rx = 1.5 - (s - floor(s - 0.5)) = 1 - frac), two 64-bit adds per
+        // axis and pixel instead of the fp64 coordinate, floor and weight
+        // expressions.  Rows where some sampled pixel is within kFixMargin of
+        // a tap boundary, or has a tap outside the band, take the fp64 code.
+        const RowFix *fp = rowfix + e.row_base + ir;
+        const int64_t fx0 = uni64(fp->x0);
+        if (fx0 != kFixNone) {
+          const int64_t fy0 = uni64(fp->y0), fdx = uni64(fp->dx), fdy = uni64(fp->dy);
+          const uint64_t X0 = (uint64_t)(fx0 + (int64_t)ic0 * fdx) - 0x80000000ull;
+          const uint64_t Y0 = (uint64_t)(fy0 + (int64_t)ic0 * fdy) - 0x80000000ull;
+          const uint64_t SX = (uint64_t)fdx << 6, SY = (uint64_t)fdy << 6;
+          uint32_t amin = 0xFFFFFFFFu;
+          bool allin = true;
+          {
+            uint64_t X = X0, Y = Y0;
+#pragma unroll
+            for (int q = 0; q < kNnPx; q++) {
+              const bool inw = (unsigned)(ic0 + 64 * q) < (unsigned)lim;
+              const int ix = (int)(int32_t)(X >> 32), iy = (int)(int32_t)(Y >> 32);
+              const uint32_t am = min((uint32_t)X + kFixMargin, (uint32_t)Y + kFixMargin);
+              amin = inw ? min(amin, am) : amin;
+              allin = allin & (!inw | (((unsigned)ix < (unsigned)(bx - 1)) & ((unsigned)iy < (unsigned)(by - 1))));
+              X += SX;
+              Y += SY;
+            }
+          }
+          if (__builtin_amdgcn_ballot_w64(amin < 2u * kFixMargin) == 0 && __all(allin)) {
+            uint64_t X = X0, Y = Y0;
+            // recomputed, not carried over from the test pass (kept live, its
+            // 8 pixels' coordinates spill at 8 waves per SIMD)
+            asm volatile("" : "+v"(X), "+v"(Y));
+#pragma unroll
+            for (int h = 0; h < kNnPx; h += HP) {
+              u32x2 t0[HP], t1[HP];
+              WT rx[HP], ry[HP];
+#pragma unroll
+              for (int q = 0; q < HP; q++) {
+                const int ic = ic0 + 64 * (h + q);
+                const bool ok = (unsigned)ic < (unsigned)lim;
+                const uint32_t ix = (uint32_t)(X >> 32), iy = (uint32_t)(Y >> 32);
+                rx[q] = (WT)1.0 - (WT)((float)(uint32_t)X * 2.3283064365386963e-10f);   // 2^-32
+                ry[q] = (WT)1.0 - (WT)((float)(uint32_t)Y * 2.3283064365386963e-10f);
+                const uint32_t o0 = ok ? (iy * (uint32_t)bx + ix) * 4u : 0x80000000u;
+                const uint32_t o1 = ok ? o0 + (uint32_t)bx * 4u : 0x80000000u;
+                t0[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, o0, 0, 0);
+                t1[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, 0);
+                X += SX;
+                Y += SY;
+              }
+#pragma unroll
+              for (int q = 0; q < HP; q++) bil_fold4(t0[q], t1[q], rx[q], ry[q], ic0 + 64 * (h + q), lim, nd, ndf,
+                                                     hnd, fillv, fill_mode, c[h + q]);
+            }
+            fixed_done = true;
+          }
+        }
+      }
+      if (fixed_done) {
+      } else if (kind == ROW_LINEAR) {   // HP pixels' taps in flight
         const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
 #pragma unroll
         for (int h = 0; h < kNnPx; h += HP) {
@@ -177,37 +308,8 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
               t1[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, 0);
             }
 #pragma unroll
-            for (int q = 0; q < HP; q++) {
-              const float tv[4] = {__uint_as_float(t0[q].x), __uint_as_float(t0[q].y), __uint_as_float(t1[q].x),
-                                   __uint_as_float(t1[q].y)};
-              const WT one = (WT)1.0;
-              const WT wx[2] = {rx[q], one - rx[q]}, wy[2] = {ry[q], one - ry[q]};
-              WT accR = (WT)0.0;
-              bool anynd = false;
-#pragma unroll
-              for (int kk = 0; kk < 4; kk++) {
-                accR += (WT)tv[kk] * (wx[kk & 1] * wy[kk >> 1]);
-                anynd = anynd | (nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
-              }
-              anynd = anynd & hnd;
-              float v = (float)accR;
-              if (anynd) {   // drop the nodata taps and renormalise (bil_sample's rule)
-                WT aR = (WT)0.0, aD = (WT)0.0;
-#pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-                  const WT w = wx[kk & 1] * wy[kk >> 1];
-                  const bool use = !(nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
-                  aD += use ? w : (WT)0.0;
-                  aR += use ? (WT)tv[kk] * w : (WT)0.0;
-                }
-                v = fillv;
-                if (aD == (WT)1.0) v = (float)aR;
-                else if (aD >= (WT)0.00001) v = (float)(aR / aD);
-              }
-              const int ic = ic0 + 64 * (h + q);
-              const bool take = ((unsigned)ic < (unsigned)lim) & (v != nd) & (!fill_mode | (c[h + q] == nd));
-              c[h + q] = take ? v : c[h + q];
-            }
+            for (int q = 0; q < HP; q++) bil_fold4_any(t0[q], t1[q], rx[q], ry[q], ic0 + 64 * (h + q), lim, nd, ndf,
+                                                       nd_nan, hnd, fillv, fill_mode, c[h + q]);
           } else {   // the reference's per-tap rules (coordinates recomputed)
             uint32_t valid[HP];
             u32x2 t0[HP], t1[HP];
@@ -257,11 +359,11 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
 // 4 pixels' taps in flight at 8 waves per SIMD; the A/B build also has the
 // fp64 weights (GSKYHIP_BIL_F32=0: 6 waves per SIMD, or 8 with 2 pixels in
 // flight, GSKYHIP_BIL_HP=2) and 8 rows per wave (GSKYHIP_BIL_RPW=8).
-template <typename WT, int RPW, int HP, int WPS>
+template <typename WT, int RPW, int HP, int WPS, bool FIX = true>
 void launch_bil_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_bil_kernel<WT, RPW, HP, WPS>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
-                     a.order, a.rows, a.pool, a.tplans, a.tiles, items);
+  hipLaunchKernelGGL((render_bil_kernel<WT, RPW, HP, WPS, FIX>), dim3((unsigned)items), dim3(256), 0, s, a,
+                     a.entries, a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
 
 void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
@@ -273,6 +375,8 @@ void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   const bool f32 = !f || atoi(f) != 0;
   const int rpw = rp ? atoi(rp) : 4;
   const int hpx = hp ? atoi(hp) : 4;
+  const char *fx = getenv("GSKYHIP_BIL_FIX");   // 0: the fp64 row code only (round 3)
+  if (fx && atoi(fx) == 0) { launch_bil_v<float, 4, 4, 8, false>(a, s); return; }
   if (f32) {
     if (rpw == 8) launch_bil_v<float, 8, 4, 8>(a, s); else launch_bil_v<float, 4, 4, 8>(a, s);
   } else if (hpx == 2) {

@@ -16,6 +16,14 @@ for i in 1 2; do
     done
   done
 done
+for i in 1 2; do
+  for lib in default r03; do
+    GSKYHIP_LIB=$lib timeout -k 10 120 python3 tools/ab_c3.py --reps 10 --label "c3_$lib" >> gpurun_out/ab.jsonl
+    stop $? "ab_c3_$lib"
+  done
+done
+timeout -k 10 300 python3 tools/ab_c3.py --reps 3 --oracle --label c3_fix >> gpurun_out/ab.jsonl
+stop $? oracle_c3
 timeout -k 10 200 python3 tools/ab_render.py --config c2 --reps 5 --oracle --label fix >> gpurun_out/ab.jsonl
 stop $? oracle_c2
 timeout -k 10 200 python3 tools/ab_render.py --config c5 --reps 5 --oracle --label fix >> gpurun_out/ab.jsonl
@@ -30,7 +38,7 @@ stop $? calib
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run --output-format csv -- \
   python3 bench.py --only c5 --no-cpu --steps 5 --warmup 2 > gpurun_out/prof_c5.log 2>&1
 stop $? prof_c5
-timeout -k 10 300 python -u -m pytest tests/test_drill_geom.py tests/test_ingest.py -m gpu -q -rf -x --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_geom.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_drill_geom.py tests/test_ingest.py tests/test_geoloc.py -m gpu -q -rf -x --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_geom.log 2>&1
 rc=$?; tail -3 gpurun_out/gpu_tests_geom.log; stop $rc tests_geom
 timeout -k 10 300 python3 bench.py --only c4 --no-cpu --no-deciles --steps 3 --warmup 1 > gpurun_out/c4.json 2> gpurun_out/c4.err
 stop $? c4
