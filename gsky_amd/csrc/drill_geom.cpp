@@ -62,6 +62,79 @@ struct Rings {
 };
 
 // ---------------------------------------------------------------- GeoJSON
+// A decimal number, correctly rounded to double (what strtod returns) for
+// up to 19 significant digits and a decimal exponent in [-19, 19], by one
+// 128-bit division; false (the caller uses strtod) otherwise.  GeoJSON
+// coordinates are 15-18 digit decimals, where glibc's strtod takes its
+// multi-precision path.
+bool fast_decimal(const char *p, const char **end, double *out) {
+  const char *s = p;
+  bool neg = false;
+  if (*s == '-' || *s == '+') { neg = *s == '-'; s++; }
+  uint64_t m = 0;
+  int nd = 0, dexp = 0;
+  bool lost = false;   // a nonzero digit past the 19th
+  const char *d0 = s;
+  while (*s >= '0' && *s <= '9') {
+    if (nd < 19) { m = m * 10 + (uint64_t)(*s - '0'); if (m) nd++; }
+    else { dexp++; lost |= *s != '0'; }
+    s++;
+  }
+  const char *digits_end = s;
+  if (*s == '.') {
+    s++;
+    while (*s >= '0' && *s <= '9') {
+      if (nd < 19) { m = m * 10 + (uint64_t)(*s - '0'); if (m) nd++; dexp--; }
+      else lost |= *s != '0';
+      s++;
+    }
+  }
+  if (digits_end == d0 && s == d0 + 1) return false;   // "." alone
+  if (s == d0) return false;
+  if (*s == 'e' || *s == 'E') {
+    const char *e = s + 1;
+    bool en = false;
+    if (*e == '-' || *e == '+') { en = *e == '-'; e++; }
+    if (!(*e >= '0' && *e <= '9')) return false;
+    int ev = 0;
+    while (*e >= '0' && *e <= '9') { if (ev < 10000) ev = ev * 10 + (*e - '0'); e++; }
+    dexp += en ? -ev : ev;
+    s = e;
+  }
+  if (lost || dexp < -19 || dexp > 19) return false;
+  *end = s;
+  if (m == 0) { *out = neg ? -0.0 : 0.0; return true; }
+  static const uint64_t p10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
+                                   100000000ull, 1000000000ull, 10000000000ull, 100000000000ull, 1000000000000ull,
+                                   10000000000000ull, 100000000000000ull, 1000000000000000ull,
+                                   10000000000000000ull, 100000000000000000ull, 1000000000000000000ull,
+                                   10000000000000000000ull};
+  unsigned __int128 num;
+  uint64_t den = 1;
+  if (dexp >= 0) num = (unsigned __int128)m * p10[dexp];
+  else { num = m; den = p10[-dexp]; }
+  // value = num * 2^bexp / den; scale num to 127 bits so the quotient keeps >= 63 bits
+  const int lz = (num >> 64) ? __builtin_clzll((uint64_t)(num >> 64)) : 64 + __builtin_clzll((uint64_t)num);
+  const int sh = lz - 1;
+  num <<= sh;
+  const unsigned __int128 q = num / den, r = num % den;
+  const int qlz = (q >> 64) ? __builtin_clzll((uint64_t)(q >> 64)) : 64 + __builtin_clzll((uint64_t)q);
+  const int drop = (128 - qlz) - 53;
+  unsigned __int128 mant = q >> drop;
+  const unsigned __int128 rem = q & (((unsigned __int128)1 << drop) - 1), half = (unsigned __int128)1 << (drop - 1);
+  if (rem > half || (rem == half && (r != 0 || (mant & 1)))) mant++;   // round half to even, r: sticky
+  const double v = std::ldexp((double)(uint64_t)mant, drop - sh);
+  *out = neg ? -v : v;
+  return true;
+}
+
+double parse_number(const char *p, char **end) {
+  double v;
+  const char *e;
+  if (fast_decimal(p, &e, &v)) { *end = (char *)e; return v; }
+  return std::strtod(p, end);
+}
+
 struct Parser {
   const char *p;
   bool ok = true;
@@ -79,7 +152,7 @@ struct Parser {
       for (int k = 0; k < 2; k++) {
         ws();
         char *e;
-        v[k] = std::strtod(p, &e);
+        v[k] = parse_number(p, &e);
         if (e == p) { ok = false; return; }
         p = e;
         ws();
@@ -91,7 +164,7 @@ struct Parser {
       while (*p == ',') {   // z ignored
         p++;
         char *e;
-        std::strtod(p, &e);
+        parse_number(p, &e);
         if (e == p) { ok = false; return; }
         p = e;
         ws();
@@ -128,6 +201,9 @@ bool parse_geometry(const char *js, Rings &r) {
   const char *c = std::strstr(base, "\"coordinates\"");
   if (!c || !(c = std::strchr(c, ':'))) return false;
   Parser ps{c + 1};
+  const size_t guess = std::strlen(c) / 24 + 4;   // ~2 numbers of ~12+ characters per vertex
+  r.x.reserve(guess);
+  r.y.reserve(guess);
   ps.coords(0, multi ? 2 : 1, r);
   return ps.ok && !r.part.empty();
 }
