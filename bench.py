@@ -419,7 +419,11 @@ def run_c3(ctx: Ctx, args):
     sp = ScaleParams(*cfg.scale)
     top, bottom = extents[ctx.rank]
 
-    band = torch.empty((bottom - top, W), dtype=torch.float32, device=ctx.device)
+    # rank 0 renders its band in place, as rows of the coverage the others'
+    # bands are received into (no assembly copy)
+    full = torch.empty((H, W), dtype=torch.float32, device=ctx.device) if ctx.rank == 0 and ctx.world > 1 else None
+    band = full[top:bottom] if full is not None else torch.empty((bottom - top, W), dtype=torch.float32,
+                                                                   device=ctx.device)
     offs = torch.tensor(coverage.band_offsets(sel, top, W), dtype=torch.int64, device=ctx.device)
 
     def render():   # chunks straight into the band at their offsets (gskyhip_render_coverage)
@@ -428,7 +432,7 @@ def run_c3(ctx: Ctx, args):
     def step():
         render()
         if ctx.world > 1:
-            coverage.gather_coverage(band, extents, H, W)
+            coverage.gather_coverage(band, extents, H, W, out=full)
         return band
 
     dt = ctx.timed(step, args.c3_steps, 1)
@@ -440,7 +444,7 @@ def run_c3(ctx: Ctx, args):
     if ctx.world > 1:
         band = step()
         torch.cuda.synchronize()
-        gather_ms = ctx.max_over_ranks(event_ms(lambda: coverage.gather_coverage(band, extents, H, W), 3))
+        gather_ms = ctx.max_over_ranks(event_ms(lambda: coverage.gather_coverage(band, extents, H, W, out=full), 3))
     src = sum(cfg.granules[0].data.nbytes for _ in sub.granules)
     abytes = src + sub.out_pixels * 4
     ach = abytes / (render_ms / 1e3) / 1e9

@@ -82,25 +82,49 @@ def place_chunks(canvases, chunks: Sequence[Chunk], top: int, n_rows: int, width
     return band
 
 
-def gather_coverage(band, extents: Sequence[Tuple[int, int]], height: int, width: int, group=None):
+def gather_coverage(band, extents: Sequence[Tuple[int, int]], height: int, width: int, group=None, out=None):
     """Gathers every rank's row band to rank 0 and returns the full
-    (height, width) coverage there (None elsewhere).  Bands are padded to
-    the largest band so one fixed-size gather serves uneven and empty bands."""
+    (height, width) coverage there (None elsewhere): rank 0 receives each
+    band straight into its rows of the coverage (point-to-point receives of
+    exactly that band's size, RCCL over xGMI on a node: no padded buffers,
+    no copy afterwards; the WCS reference instead merges per-node GeoTIFF
+    files over HTTP, ows.go:930-995, 1094-1150).  `out`: a preallocated
+    coverage on rank 0; when rank 0's own band is already a view of its rows
+    (rendered in place) it is not copied either.  A gloo group with device
+    tensors stages through host memory (tests; gloo has no device p2p)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    max_rows = max(1, max(b - t for t, b in extents))
-    pad = torch.zeros((max_rows, width), dtype=band.dtype, device=band.device)
-    pad[: band.shape[0]] = band
-    bufs = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
-    dist.gather(pad, bufs, dst=0, group=group)
+    via_host = band.is_cuda and dist.get_backend(group) == "gloo"
     if rank != 0:
-        return None
-    full = torch.empty((height, width), dtype=band.dtype, device=band.device)
-    for r, (t, b) in enumerate(extents):
+        t, b = extents[rank]
         if b > t:
-            full[t:b] = bufs[r][: b - t]
+            src = band[: b - t].contiguous()
+            if via_host:
+                src = src.cpu()
+            dist.send(src, 0, group=group)
+        return None
+    full = out if out is not None else torch.empty((height, width), dtype=band.dtype, device=band.device)
+    t0, b0 = extents[0]
+    if b0 > t0 and band.data_ptr() != full[t0].data_ptr():
+        full[t0:b0] = band[: b0 - t0]
+    ops, staged = [], []
+    for r in range(1, world):
+        t, b = extents[r]
+        if b <= t:
+            continue
+        if via_host:
+            h = torch.empty((b - t, width), dtype=band.dtype)
+            staged.append((h, t, b))
+            ops.append(dist.P2POp(dist.irecv, h, r, group))
+        else:
+            ops.append(dist.P2POp(dist.irecv, full[t:b], r, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for h, t, b in staged:
+        full[t:b] = h.to(full.device)
     return full
 
 

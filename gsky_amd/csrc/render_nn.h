@@ -169,6 +169,90 @@ __device__ __forceinline__ bool nn_fix_row(__amdgpu_buffer_rsrc_t rs, int64_t fx
   return true;
 }
 
+// The fold of one `inside` LINEAR row covering the block (nn_fix_row's cover
+// case) with cooperative loads instead of per-lane gathers: for each of the
+// lane's 8 pixels the wave's 64 consecutive output columns read a source run
+// of at most 2 rows and 32 * (4 / sizeof(T)) - 2 columns; lanes 0-31 load
+// that run of the upper row and lanes 32-63 of the lower as consecutive
+// dwords (one coalesced load instruction), and every lane picks its value
+// with ds_bpermute.  The same source pixels as the gathers (the fixed-point
+// indices), so the same result bit for bit.  false: ambiguous (nothing
+// folded, the fp64 bodies follow) -- or, with nothing loaded yet, a run that
+// does not fit, where the per-lane gathers are used.  A/B (GSKYHIP_NN_COOP).
+template <typename T, int NPX>
+__device__ __forceinline__ bool nn_fix_row_coop(__amdgpu_buffer_rsrc_t rs, int64_t fx0, int64_t fy0, int64_t fdx,
+                                                int64_t fdy, int ic0, int lim, int bx, typename VOf<T>::type nd,
+                                                bool fill_mode, typename VOf<T>::type (&c)[NPX], int lane) {
+  using V = typename VOf<T>::type;
+  constexpr int K = 4 / (int)sizeof(T);   // elements per dword
+  uint64_t X = (uint64_t)(fx0 + (int64_t)ic0 * fdx), Y = (uint64_t)(fy0 + (int64_t)ic0 * fdy);
+  const uint64_t SX = (uint64_t)fdx << 6, SY = (uint64_t)fdy << 6;
+  uint32_t amin = 0xFFFFFFFFu;
+  int ix[NPX], iy[NPX];
+#pragma unroll
+  for (int q = 0; q < NPX; q++) {
+    ix[q] = (int)(uint32_t)(X >> 32);
+    iy[q] = (int)(uint32_t)(Y >> 32);
+    amin = min(amin, min((uint32_t)X + kFixMargin, (uint32_t)Y + kFixMargin));
+    X += SX;
+    Y += SY;
+  }
+  if (__builtin_amdgcn_ballot_w64(amin < 2u * kFixMargin) != 0) return false;
+  // per pixel slot: the run's rows and columns (monotone in the column: the
+  // end lanes hold the extremes)
+  int base0[NPX], base1[NPX], r0s[NPX];
+  bool fits = true;
+#pragma unroll
+  for (int q = 0; q < NPX; q++) {
+    const int xa = __builtin_amdgcn_readlane(ix[q], 0), xb2 = __builtin_amdgcn_readlane(ix[q], 63);
+    const int ya = __builtin_amdgcn_readlane(iy[q], 0), yb = __builtin_amdgcn_readlane(iy[q], 63);
+    const int lo = min(xa, xb2), hi = max(xa, xb2), r0 = min(ya, yb), r1 = max(ya, yb);
+    fits = fits & (hi - lo <= 32 * K - 2 * K) & (r1 - r0 <= 1);
+    const int e0 = r0 * bx + lo, e1 = (r0 + 1) * bx + lo;
+    base0[q] = e0 & ~(K - 1);
+    base1[q] = e1 & ~(K - 1);
+    r0s[q] = r0;
+  }
+  V vv[NPX];
+  if (fits) {
+    uint32_t w[NPX];
+#pragma unroll
+    for (int q = 0; q < NPX; q++) {
+      const int mybase = lane < 32 ? base0[q] : base1[q];
+      w[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(mybase / K + (lane & 31)) * 4u, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < NPX; q++) {
+      const bool upper = iy[q] == r0s[q];
+      const int rel = iy[q] * bx + ix[q] - (upper ? base0[q] : base1[q]);
+      const int src = (upper ? 0 : 32) + rel / K;
+      const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(src * 4, (int)w[q]);
+      const uint32_t sh = (uint32_t)(rel % K) * 8u * (uint32_t)sizeof(T);
+      if constexpr (sizeof(T) == 4) {
+        vv[q] = __builtin_bit_cast(V, got);
+      } else if constexpr (sizeof(T) == 2) {
+        const uint32_t h = (got >> sh) & 0xFFFFu;
+        vv[q] = std::is_signed<T>::value ? (V)(int16_t)h : (V)h;
+      } else {
+        const uint32_t b = (got >> sh) & 0xFFu;
+        vv[q] = std::is_signed<T>::value ? (V)(int8_t)b : (V)b;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NPX; q++)
+      vv[q] = buf_load<T>(rs, (__umul24((uint32_t)iy[q], (uint32_t)bx) + (uint32_t)ix[q]) * (uint32_t)sizeof(T));
+  }
+  if (!fill_mode) {
+#pragma unroll
+    for (int q = 0; q < NPX; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
+  } else {
+#pragma unroll
+    for (int q = 0; q < NPX; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
+  }
+  return true;
+}
+
 // One stack entry e of the ordered fold of tile row r (MergeMaskedRaster,
 // tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
 // (tile column xl + 64 q).
@@ -326,7 +410,7 @@ __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint3
 // tiles -- keep the entry's descriptor in scalar registers for all the
 // wave's rows and fetch the next row's record while the current row is
 // gathered, so no row waits for its record.
-template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, bool STAGE = false>
+template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, bool STAGE = false, bool COOP = false>
 __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
@@ -450,7 +534,10 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         for (int q = 0; q < kNnPx; q++) c[q] = cnod;
         bool done = cfk < 0;
         if (cfk == 1)
-          done = cover ? nn_fix_row<T, kNnPx, false>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c)
+          done = cover ? (COOP ? nn_fix_row_coop<T, kNnPx>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode,
+                                                           c, lane)
+                               : nn_fix_row<T, kNnPx, false>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
+                                                             fill_mode, c))
                        : nn_fix_row<T, kNnPx, true>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c);
         if (done) {
           uint32_t px[kNnPx];
@@ -512,10 +599,10 @@ constexpr int kNnRpw8MinItems = 32768;
 constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
 constexpr int kNnMaskRpw1Items = 16384;   // masked stacks: one row per wave below this many workgroups
 
-template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = false>
+template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = false, bool COOP = false>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE, COOP>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -569,6 +656,11 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
     launch_nn_stage<T>(a, s);
 #endif
   } else if (rpw8) {
+#ifdef GSKYHIP_AB
+    if (const char *co = getenv("GSKYHIP_NN_COOP")) {
+      if (one && atoi(co) != 0) { launch_nn_v<T, false, false, 8, true, false, true>(a, s); return; }
+    }
+#endif
     if (one) launch_nn_v<T, false, false, 8, true>(a, s);
     else launch_nn_v<T, false, false, 8>(a, s);
   } else if (rpw1) {

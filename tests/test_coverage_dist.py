@@ -128,3 +128,47 @@ def test_coverage_band_gpu_matches_oracle(gpu, oracle, w, h):
     assert v.mean() > 0.5
     rel = np.abs(got[v].astype(np.float64) - exp[v]) / np.maximum(np.abs(exp[v].astype(np.float64)), 1e-30)
     assert rel.max() <= 1e-4, rel.max()
+
+
+def _gpu_worker(rank, world, port, q, w, h, ch):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gsky_amd import synth
+        torch.cuda.set_device(0)
+        cfg = synth.config_c3(scale=0.05, chunk_px=ch, out_px=w, out_h=h, grid=3)
+        full, ext = coverage.render_coverage(cfg, w, h, device=torch.device("cuda", 0), max_x=ch, max_y=ch)
+        torch.cuda.synchronize()
+        q.put((rank, full.cpu().numpy() if rank == 0 else None, ext))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_coverage_hip_ranks_match_single_process(world):
+    """The multi-rank GetCoverage through the HIP path: `world` processes on
+    the one device each render their row band with the product kernels and
+    gather it to rank 0 (exact-size point-to-point receives into the
+    coverage; gloo stages the device bands through host memory), and rank 0's
+    coverage equals the single-process render bit for bit."""
+    from gsky_amd import synth
+    w, h, ch = 250, 300, 96
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q, w, h, ch)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, arr, ext = q.get(timeout=240)
+        got[r] = (arr, ext)
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    cfg = synth.config_c3(scale=0.05, chunk_px=ch, out_px=w, out_h=h, grid=3)
+    one, _ = coverage.render_coverage(cfg, w, h, device=torch.device("cuda", 0), max_x=ch, max_y=ch)
+    full, ext = got[0]
+    assert sum(b - t for t, b in ext) == h and len([e for e in ext if e[1] > e[0]]) == world
+    assert np.array_equal(full, one.cpu().numpy())
