@@ -617,6 +617,63 @@ def run_c5(ctx: Ctx, args):
     return out
 
 
+# ---------------------------------------------------------------- the per-node warp service
+def run_service(ctx: Ctx, args):
+    """The path GSKY calls: N worker processes (gsky-rpc's gsky-gdal-process
+    pool, grpc-server/main.go:58) each sending C2 (tile, granule) warp
+    requests through warp_operation_fast -> Unix socket -> gskyhipd, which
+    batches across workers (service.cpp); the window bytes come back to the
+    worker in host memory as warp.go:573-574 expects.  Beside it the oracle's
+    warp_operation_fast on one thread per worker (the reference's CPU path)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from gsky_amd import WarpService
+    from gsky_amd.loadgen import service_load
+    from gsky_amd.tiles import bbox_to_geot
+    cfg = synth.config_c2()
+    sock = "/tmp/gskyhip-bench-%d.sock" % os.getpid()
+    svc = WarpService(sock, max_batch=64, window_us=args.svc_window_us)
+    out = {"workload": "C2 (tile, granule) warp requests, 512x512 EPSG:3857 windows from 16 EPSG:3577 int16 "
+                       "4000x4000 granules resident in the daemon's HBM; %d requests per run, dealt round-robin "
+                       "to the workers, each worker one request at a time" % args.svc_jobs,
+           "daemon": "gskyhipd max_batch 64, window %d us" % args.svc_window_us}
+    try:
+        for k, g in enumerate(cfg.granules):
+            svc.register_granule("/g/data/c2/g%d.tif" % k, 1, g.data, g.geot, "EPSG:3577", g.nodata, block=(256, 256))
+        pairs = [(k, bb, w, h) for (bb, w, h), ks in zip(cfg.tiles, cfg.pairs) for k in ks]
+        step = max(1, len(pairs) // args.svc_jobs)
+        sel = pairs[::step][: args.svc_jobs]
+        jobs = [("/g/data/c2/g%d.tif" % k, 1, list(bbox_to_geot(w, h, bb)), w, h, "EPSG:3857") for k, bb, w, h in sel]
+        for n in (16, 64):
+            s0 = svc.stats()
+            r = service_load(sock, jobs, n)
+            s1 = svc.stats()
+            r["mean_batch"] = round((s1["requests"] - s0["requests"]) / max(1, s1["batches"] - s0["batches"]), 2)
+            r["max_batch"] = s1["max_batch"]
+            out["workers_%d" % n] = r
+    finally:
+        svc.shutdown()
+    if not args.no_cpu:
+        from oracle import oracle as O
+        cores = host_cores()
+        aea, wm = O.crs("EPSG:3577"), O.crs("EPSG:3857")
+        ogs = [O.make_granule(g.data, g.geot, g.nodata, block=(256, 256)) for g in cfg.granules]
+        sub = sel[:: max(1, len(sel) // 256)]
+
+        def one(job):
+            k, bb, w, h = job
+            O.warp(ogs[k], aea, wm, list(bbox_to_geot(w, h, bb)), w, h)
+        with ThreadPoolExecutor(cores) as ex:
+            list(ex.map(one, sub[:cores]))          # warm
+            t0 = time.perf_counter()
+            list(ex.map(one, sub))
+            ct = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(sub) / ct, 1), "unit": "requests/s", "cores": cores,
+                               "kind": "port", "sample": "%d of the requests, oracle warp_operation_fast, one "
+                                                         "thread per worker (%d)" % (len(sub), cores)}
+    return out
+
+
 def run_dry(ctx: Ctx, args):
     """CPU dry run of the launch / timing contract (tests): a trivial step per
     rank over gloo, timed like the real ones."""
@@ -634,7 +691,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--only", default="c2,c1,c3,c4,c5", help="comma list of configs (c2 is the headline)")
+    ap.add_argument("--only", default="c2,c1,c3,c4,c5,svc", help="comma list of configs (c2 is the headline)")
+    ap.add_argument("--svc-jobs", type=int, default=1024, help="service leg: C2 (tile, granule) requests per run")
+    ap.add_argument("--svc-window-us", type=int, default=500, help="service leg: gskyhipd batching window")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c1", action="store_true", help="(compat) drop C1")
     ap.add_argument("--cpu-runs", type=int, default=5)
@@ -667,7 +726,16 @@ def main():
     if "c2" in only:
         out.update(run_c2(ctx, args))
     configs = {}
-    for name, fn in (("C1", run_c1), ("C3", run_c3), ("C4", run_c4), ("C5", run_c5)):
+    for name, fn in (("C1", run_c1), ("C3", run_c3), ("C4", run_c4), ("C5", run_c5), ("service", run_service)):
+        if name == "service":
+            if "svc" not in only or ctx.world > 1:
+                continue
+            try:
+                configs[name] = fn(ctx, args)
+            except Exception as ex:   # noqa: BLE001
+                traceback.print_exc()
+                configs[name] = {"error": "%s: %s" % (type(ex).__name__, ex)}
+            continue
         if name.lower() not in only:
             continue
         try:

@@ -212,6 +212,7 @@ struct RenderArgs {
   int lds_mode;          // typed band kernels: kBilinear | kCanvas bits of the call
   const int64_t *cov_offsets;  // canvas mode: per tile element offset into one image (NULL: slots)
   int64_t cov_stride;          // ... and that image's row stride (elements)
+  int st_pol;                  // A/B build only: RGBA store cache policy (0 nt, 1 sc1, 2 sc0 sc1, 3 plain)
 };
 
 // ---------------------------------------------------------------- typed fast path

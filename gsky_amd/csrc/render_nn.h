@@ -485,13 +485,23 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         return;
       }
     }
+    auto st = [&](uint32_t *p, uint32_t v) {
+#ifdef GSKYHIP_AB
+      // A/B: the store's L2 policy (nt / plain keep the line in the XCD's
+      // L2; sc1 / sc0 sc1 drop it, MI355X_MICROARCH.md)
+      if (a.st_pol == 1) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); return; }
+      if (a.st_pol == 2) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); return; }
+      if (a.st_pol == 3) { *p = v; return; }
+#endif
+      __builtin_nontemporal_store(v, (GPTR(uint32_t))p);
+    };
     if (full) {
 #pragma unroll
-      for (int q = 0; q < kNnPx; q++) __builtin_nontemporal_store(px[q], (GPTR(uint32_t))(dst + 64 * q));
+      for (int q = 0; q < kNnPx; q++) st(dst + 64 * q, px[q]);
     } else {
 #pragma unroll
       for (int q = 0; q < kNnPx; q++)
-        if (64 * q + lane < ncols) __builtin_nontemporal_store(px[q], (GPTR(uint32_t))(dst + 64 * q));
+        if (64 * q + lane < ncols) st(dst + 64 * q, px[q]);
     }
   };
 
