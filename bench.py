@@ -650,6 +650,9 @@ def run_service(ctx: Ctx, args):
             s1 = svc.stats()
             r["mean_batch"] = round((s1["requests"] - s0["requests"]) / max(1, s1["batches"] - s0["batches"]), 2)
             r["max_batch"] = s1["max_batch"]
+            nb, nr = max(1, s1["batches"] - s0["batches"]), max(1, s1["requests"] - s0["requests"])
+            r["daemon_batch_ms_mean"] = round((s1["batch_s"] - s0["batch_s"]) * 1e3 / nb, 3)
+            r["daemon_resident_ms_mean"] = round((s1["resident_s"] - s0["resident_s"]) * 1e3 / nr, 3)
             out["workers_%d" % n] = r
     finally:
         svc.shutdown()

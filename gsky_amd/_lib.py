@@ -97,8 +97,8 @@ EXPORTS = [
     "gskyhip_render_status",
     "gskyhip_render_tile_info", "gskyhip_compute_reproject_extent",
     "gskyhip_service_run", "gskyhip_service_register_granule", "gskyhip_service_unregister_all",
-    "gskyhip_service_stats", "gskyhip_service_shutdown", "gskyhip_drill_deciles_workspace_size",
-    "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device", "gskyhip_drill_masks_device",
+    "gskyhip_service_stats", "gskyhip_service_stats_n", "gskyhip_service_shutdown", "gskyhip_drill_deciles_workspace_size",
+    "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device", "gskyhip_drill_masks_device", "gskyhip_parse_numbers",
     "gskyhip_drill_read_data_workspace_size", "gskyhip_drill_read_data",
     "gskyhip_png_workspace_size", "gskyhip_png_bound", "gskyhip_encode_png",
     "gskyhip_geotiff_workspace_size", "gskyhip_geotiff_bound", "gskyhip_encode_geotiff",
@@ -149,6 +149,8 @@ def lib() -> C.CDLL:
                                                    C.POINTER(vp), C.c_char_p]
     L.gskyhip_service_unregister_all.argtypes = [C.c_char_p]
     L.gskyhip_service_stats.argtypes = [C.c_char_p, C.POINTER(i64)]
+    if hasattr(L, "gskyhip_service_stats_n"):
+        L.gskyhip_service_stats_n.argtypes = [C.c_char_p, C.POINTER(i64), C.c_int]
     L.gskyhip_service_shutdown.argtypes = [C.c_char_p]
     L.gskyhip_render_tile_info.argtypes = [vp, ci, ci, ci, vp, vp, vp]
     L.gskyhip_merge_rasters.argtypes = [C.POINTER(FlexRasterC), ci, C.POINTER(Mask), C.POINTER(vp), ci,
@@ -170,6 +172,8 @@ def lib() -> C.CDLL:
     L.gskyhip_drill_merge.argtypes = [vp, vp, ci, ci, vp, vp]
     L.gskyhip_drill_descriptors_device.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci,
                                                    vp, vp, C.POINTER(i64), vp, vp, vp]
+    if hasattr(L, "gskyhip_parse_numbers"):
+        L.gskyhip_parse_numbers.argtypes = [C.c_char_p, ci, C.c_void_p, C.c_void_p]
     if hasattr(L, "gskyhip_drill_masks_device"):   # absent from kept earlier builds (GSKYHIP_LIB=<name>)
         L.gskyhip_drill_masks_device.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci, vp,
                                                  vp, C.POINTER(i64), vp, vp, C.POINTER(vp), vp, vp]

@@ -63,10 +63,66 @@ struct Rings {
 
 // ---------------------------------------------------------------- GeoJSON
 // A decimal number, correctly rounded to double (what strtod returns) for
-// up to 19 significant digits and a decimal exponent in [-19, 19], by one
-// 128-bit division; false (the caller uses strtod) otherwise.  GeoJSON
-// coordinates are 15-18 digit decimals, where glibc's strtod takes its
-// multi-precision path.
+// up to 19 significant digits and a decimal exponent in [-19, 19]; false (the
+// caller uses strtod) otherwise.  GeoJSON coordinates are 15-18 digit
+// decimals, where glibc's strtod takes its multi-precision path.
+//
+// m * 10^-k (k > 0): the 64-bit normalized m times a 128-bit truncated
+// reciprocal R_k = floor(2^(127+b_k) / 10^k) in [2^127, 2^128) gives the
+// quotient's leading 128 bits to within 2 units of the last; the 53-bit
+// rounding is decided from them unless the bits below the mantissa sit
+// within that error of the halfway point, which goes to an exact 128-bit
+// division.  m * 10^k (k >= 0) is an exact 128-bit product.
+struct Recip {
+  uint64_t hi[20], lo[20];
+  int b[20];
+  Recip() {
+    uint64_t p = 1;
+    for (int k = 1; k < 20; k++) {
+      p *= 10;   // 10^k < 2^64
+      int bk = 0;
+      while (bk < 64 && (((unsigned __int128)1 << bk) < p)) bk++;
+      b[k] = bk;
+      // floor(2^(127+bk) / p) by shift-subtract over the numerator's bits
+      unsigned __int128 q = 0, rem = 0;
+      for (int bit = 127 + bk; bit >= 0; bit--) {
+        rem = (rem << 1) | (bit == 127 + bk ? 1u : 0u);
+        q <<= 1;
+        if (rem >= p) { rem -= p; q |= 1; }
+      }
+      hi[k] = (uint64_t)(q >> 64);
+      lo[k] = (uint64_t)q;
+    }
+  }
+};
+const Recip &recip() {
+  static const Recip r;
+  return r;
+}
+
+inline double from_mant(uint64_t mant, int e) {   // mant in [2^52, 2^53], value mant * 2^e, normal range
+  if (mant >> 53) { mant >>= 1; e++; }
+  const uint64_t bits = ((uint64_t)(e + 52 + 1023) << 52) | (mant & ((1ull << 52) - 1));
+  double v;
+  std::memcpy(&v, &bits, 8);
+  return v;
+}
+
+// exact m / 10^k by one 128-bit division (the rare near-halfway case)
+double div_exact(uint64_t m, uint64_t den) {
+  unsigned __int128 num = m;
+  const int lz = 64 + __builtin_clzll(m);
+  const int sh = lz - 1;
+  num <<= sh;
+  const unsigned __int128 q = num / den, r = num % den;
+  const int qlz = (q >> 64) ? __builtin_clzll((uint64_t)(q >> 64)) : 64 + __builtin_clzll((uint64_t)q);
+  const int drop = (128 - qlz) - 53;
+  unsigned __int128 mant = q >> drop;
+  const unsigned __int128 rem = q & (((unsigned __int128)1 << drop) - 1), half = (unsigned __int128)1 << (drop - 1);
+  if (rem > half || (rem == half && (r != 0 || (mant & 1)))) mant++;   // round half to even, r: sticky
+  return std::ldexp((double)(uint64_t)mant, drop - sh);
+}
+
 bool fast_decimal(const char *p, const char **end, double *out) {
   const char *s = p;
   bool neg = false;
@@ -109,21 +165,40 @@ bool fast_decimal(const char *p, const char **end, double *out) {
                                    10000000000000ull, 100000000000000ull, 1000000000000000ull,
                                    10000000000000000ull, 100000000000000000ull, 1000000000000000000ull,
                                    10000000000000000000ull};
-  unsigned __int128 num;
-  uint64_t den = 1;
-  if (dexp >= 0) num = (unsigned __int128)m * p10[dexp];
-  else { num = m; den = p10[-dexp]; }
-  // value = num * 2^bexp / den; scale num to 127 bits so the quotient keeps >= 63 bits
-  const int lz = (num >> 64) ? __builtin_clzll((uint64_t)(num >> 64)) : 64 + __builtin_clzll((uint64_t)num);
-  const int sh = lz - 1;
-  num <<= sh;
-  const unsigned __int128 q = num / den, r = num % den;
-  const int qlz = (q >> 64) ? __builtin_clzll((uint64_t)(q >> 64)) : 64 + __builtin_clzll((uint64_t)q);
-  const int drop = (128 - qlz) - 53;
-  unsigned __int128 mant = q >> drop;
-  const unsigned __int128 rem = q & (((unsigned __int128)1 << drop) - 1), half = (unsigned __int128)1 << (drop - 1);
-  if (rem > half || (rem == half && (r != 0 || (mant & 1)))) mant++;   // round half to even, r: sticky
-  const double v = std::ldexp((double)(uint64_t)mant, drop - sh);
+  double v;
+  if (dexp >= 0) {   // exact integer m * 10^dexp < 2^128
+    const unsigned __int128 num = (unsigned __int128)m * p10[dexp];
+    const uint64_t nh = (uint64_t)(num >> 64);
+    const int lz = nh ? __builtin_clzll(nh) : 64 + __builtin_clzll((uint64_t)num);
+    const int drop = 128 - lz - 53;
+    if (drop <= 0) {
+      v = (double)(uint64_t)num;   // < 2^53: exact
+    } else {
+      uint64_t mant = (uint64_t)(num >> drop);
+      const unsigned __int128 rem = num & (((unsigned __int128)1 << drop) - 1), half = (unsigned __int128)1 << (drop - 1);
+      if (rem > half || (rem == half && (mant & 1))) mant++;
+      v = from_mant(mant, drop);
+    }
+  } else {
+    const int k = -dexp;
+    const Recip &R = recip();
+    const int lz = __builtin_clzll(m);
+    const uint64_t M = m << lz;
+    const unsigned __int128 ph = (unsigned __int128)M * R.hi[k], pl = (unsigned __int128)M * R.lo[k];
+    const unsigned __int128 mid = (ph & 0xFFFFFFFFFFFFFFFFull) + (pl >> 64);
+    const uint64_t U = (uint64_t)mid;
+    const uint64_t T = (uint64_t)(ph >> 64) + (uint64_t)(mid >> 64);
+    const int drop = 11 - __builtin_clzll(T);   // 11 or 10: T's top bit is 63 or 62
+    const uint64_t half = 1ull << (drop - 1), rT = T & ((1ull << drop) - 1);
+    uint64_t mant = T >> drop;
+    // the exact product exceeds (T, U) by less than 2 units of U
+    if ((rT == half && U < 4) || (rT == half - 1 && U >= ~3ull)) {
+      v = div_exact(m, p10[k]);
+    } else {
+      if (rT >= half) mant++;
+      v = from_mant(mant, drop + 1 - lz - R.b[k]);
+    }
+  }
   *out = neg ? -v : v;
   return true;
 }
@@ -196,8 +271,24 @@ bool parse_geometry(const char *js, Rings &r) {
   if (!js) return false;
   const char *g = std::strstr(js, "\"geometry\"");
   const char *base = g ? g : js;
-  const bool multi = std::strstr(base, "\"MultiPolygon\"") != nullptr;
-  if (!multi && !std::strstr(base, "\"Polygon\"")) return false;
+  // the geometry's "type" value (one short scan: it precedes the coordinates
+  // in every GeoJSON writer); anything else -> a search of the whole text
+  int kind = -1;   // 1 MultiPolygon, 0 Polygon
+  if (const char *t = std::strstr(base, "\"type\"")) {
+    t += 6;
+    while (*t == ' ' || *t == '\n' || *t == '\t' || *t == '\r') t++;
+    if (*t == ':') {
+      t++;
+      while (*t == ' ' || *t == '\n' || *t == '\t' || *t == '\r') t++;
+      if (std::strncmp(t, "\"MultiPolygon\"", 14) == 0) kind = 1;
+      else if (std::strncmp(t, "\"Polygon\"", 9) == 0) kind = 0;
+    }
+  }
+  if (kind < 0) {
+    kind = std::strstr(base, "\"MultiPolygon\"") != nullptr ? 1 : 0;
+    if (!kind && !std::strstr(base, "\"Polygon\"")) return false;
+  }
+  const bool multi = kind == 1;
   const char *c = std::strstr(base, "\"coordinates\"");
   if (!c || !(c = std::strchr(c, ':'))) return false;
   Parser ps{c + 1};
@@ -501,8 +592,13 @@ Descriptor describe(const char *geometry, const DescribeCtx &c) {
 // independent; the reference describes one per gRPC call, drill_grpc.go:127-158).
 void describe_all(const char *const *geometries, int n, const DescribeCtx &c, std::vector<Descriptor> &out) {
   out.assign((size_t)std::max(0, n), Descriptor());
+  static const unsigned cap = [] {   // GSKYHIP_DRILL_THREADS: at most this many (default 16)
+    const char *e = std::getenv("GSKYHIP_DRILL_THREADS");
+    const int v = e ? std::atoi(e) : 16;
+    return (unsigned)std::max(1, std::min(64, v));
+  }();
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const int nth = (int)std::min<unsigned>(std::min(16u, hw), (unsigned)std::max(1, n / 16));
+  const int nth = (int)std::min<unsigned>(std::min(cap, hw), (unsigned)std::max(1, n / 16));
   std::atomic<int> next(0);
   auto work = [&]() {
     for (int i = next.fetch_add(8); i < n; i = next.fetch_add(8))
@@ -710,6 +806,20 @@ int ctx_of(const char *dataset_srs, gskyhip_crs &crs, const gskyhip_crs *&pc) {
 }  // namespace gsky
 
 using namespace gsky;
+
+// The GeoJSON number parser on n NUL-separated strings packed in `text` (test
+// hook: checked against strtod / Python float by tests/test_drill_geom.py);
+// consumed[i] = characters parsed.
+extern "C" int gskyhip_parse_numbers(const char *text, int n, double *out, int32_t *consumed) {
+  if (!text || n < 0 || !out || !consumed) return GSKYHIP_E_ARG;
+  for (int i = 0; i < n; i++) {
+    char *e;
+    out[i] = parse_number(text, &e);
+    consumed[i] = (int32_t)(e - text);
+    text += std::strlen(text) + 1;
+  }
+  return 0;
+}
 
 // Windows on the host, ALL_TOUCHED masks rasterized on the GPU into masks_dev
 // (every polygon, any vertex count), all on `stream`.  masks_dev == NULL:

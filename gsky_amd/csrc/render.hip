@@ -1747,8 +1747,10 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.cov_offsets = rc.cov_offsets;
   a.cov_stride = rc.cov_stride;
   a.st_pol = 0;
+  a.ab_mode = 0;
 #ifdef GSKYHIP_AB
   if (const char *sp = getenv("GSKYHIP_NN_STPOL")) a.st_pol = atoi(sp);
+  if (const char *am = getenv("GSKYHIP_AB_MODE")) a.ab_mode = atoi(am);
 #endif
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));

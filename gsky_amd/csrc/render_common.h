@@ -213,6 +213,7 @@ struct RenderArgs {
   const int64_t *cov_offsets;  // canvas mode: per tile element offset into one image (NULL: slots)
   int64_t cov_stride;          // ... and that image's row stride (elements)
   int st_pol;                  // A/B build only: RGBA store cache policy (0 nt, 1 sc1, 2 sc0 sc1, 3 plain)
+  int ab_mode;                 // A/B build only: 1 skip the NN gathers, 2 skip the RGBA stores
 };
 
 // ---------------------------------------------------------------- typed fast path

@@ -495,6 +495,14 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 #endif
       __builtin_nontemporal_store(v, (GPTR(uint32_t))p);
     };
+#ifdef GSKYHIP_AB
+    if (a.ab_mode == 2) {   // A/B: no stores (the values stay live)
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++)
+        if (px[q] == 0x9E3779B9u) st(dst + 64 * q, px[q]);
+      return;
+    }
+#endif
     if (full) {
 #pragma unroll
       for (int q = 0; q < kNnPx; q++) st(dst + 64 * q, px[q]);
@@ -543,6 +551,10 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 #pragma unroll
         for (int q = 0; q < kNnPx; q++) c[q] = cnod;
         bool done = cfk < 0;
+#ifdef GSKYHIP_AB
+        if (a.ab_mode == 1) done = true;   // A/B: no gathers
+        else
+#endif
         if (cfk == 1)
           done = cover ? (COOP ? nn_fix_row_coop<T, kNnPx>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode,
                                                            c, lane)

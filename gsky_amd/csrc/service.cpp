@@ -221,6 +221,8 @@ struct Service {
   int listen_fd = -1;
   // statistics: warp requests, batches, largest batch, registered granules
   std::atomic<int64_t> n_req{0}, n_batches{0}, max_seen{0}, n_reg{0};
+  // time in warp_batch, and request residence (enqueued -> answer ready), ns
+  std::atomic<int64_t> batch_ns{0}, resident_ns{0};
   std::atomic<int> active{0};          // connection threads still running (detached)
   std::mutex reg_mu;
   // granule data uploaded through SVC_REGISTER, per (path, band): freed when
@@ -268,7 +270,9 @@ void batch_loop(Service *s) {
     for (int i = 0; i < m; i++) reqs[i] = take[i]->q;
     {
       std::lock_guard<std::mutex> rl(s->reg_mu);   // registrations do not race a batch
+      const auto t0 = std::chrono::steady_clock::now();
       warp_batch(reqs.data(), m, resps.data());
+      s->batch_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     }
     s->n_batches++;
     int64_t prev = s->max_seen.load();
@@ -342,6 +346,7 @@ void conn_serve(Service *s, int fd) {
       auto pd = std::make_shared<Pending>();
       if (!get_req(in, pd->q)) break;
       s->n_req++;
+      const auto t0 = std::chrono::steady_clock::now();
       {
         std::unique_lock<std::mutex> lk(s->mu);
         if (s->stop) {   // shutting down: the batcher may be gone, answer now
@@ -353,6 +358,7 @@ void conn_serve(Service *s, int fd) {
           s->cv_done.wait(lk, [&] { return pd->done; });
         }
       }
+      s->resident_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
       put_resp(o, pd->r);
     } else if (op == SVC_REGISTER) {
       o.put<int32_t>(do_register(s, in));
@@ -365,6 +371,7 @@ void conn_serve(Service *s, int fd) {
     } else if (op == SVC_STATS) {
       o.put<int64_t>(s->n_req.load()); o.put<int64_t>(s->n_batches.load());
       o.put<int64_t>(s->max_seen.load()); o.put<int64_t>(s->n_reg.load());
+      o.put<int64_t>(s->batch_ns.load()); o.put<int64_t>(s->resident_ns.load());
     } else if (op == SVC_SHUTDOWN) {
       o.put<int32_t>(0);
       send_msg(fd, op, o.b);
@@ -490,10 +497,16 @@ int gskyhip_service_unregister_all(const char *socket_path) {
 }
 
 int gskyhip_service_stats(const char *socket_path, int64_t *stats) {
+  return gskyhip_service_stats_n(socket_path, stats, 4);
+}
+
+int gskyhip_service_stats_n(const char *socket_path, int64_t *stats, int n_stats) {
   std::vector<char> rep;
-  if (!socket_path || !stats || !exchange(socket_path, SVC_STATS, {}, rep) || rep.size() < 32)
+  if (!socket_path || !stats || n_stats < 0 || !exchange(socket_path, SVC_STATS, {}, rep) || rep.size() < 32)
     return GSKYHIP_E_SERVICE;
-  std::memcpy(stats, rep.data(), 32);
+  const size_t n = std::min<size_t>((size_t)n_stats, rep.size() / 8);
+  std::memcpy(stats, rep.data(), 8 * n);
+  for (int k = (int)n; k < n_stats; k++) stats[k] = 0;
   return 0;
 }
 

@@ -329,6 +329,10 @@ int gskyhip_service_register_granule(const char *socket_path, const char *path, 
 int gskyhip_service_unregister_all(const char *socket_path);
 /* stats[4]: warp requests served, batches run, largest batch, registered granules */
 int gskyhip_service_stats(const char *socket_path, int64_t *stats);
+/* the same and, at [4], nanoseconds the daemon spent in warp batches, at [5]
+ * the summed residence of requests (enqueued -> answer ready); the first
+ * n_stats values are written (0 past what the daemon reports) */
+int gskyhip_service_stats_n(const char *socket_path, int64_t *stats, int n_stats);
 int gskyhip_service_shutdown(const char *socket_path);
 
 /* Band-math on merged canvases (processor/tile_merger.go:523-731): evaluate
@@ -555,6 +559,10 @@ int gskyhip_drill_masks_device(const char *const *geometries, int n, const char 
                                int xsize, int ysize, int32_t *win_out, int64_t *mask_off_out,
                                int64_t *mask_bytes_out, gskyhip_alloc_fn alloc, void *alloc_ctx,
                                uint8_t **masks_dev_out, int32_t *status_out, void *stream);
+/* Test hook: the GeoJSON number parser of the drill descriptors on n
+ * NUL-separated strings packed in `text`; out[i] the value, consumed[i] the
+ * characters parsed (strtod semantics). */
+int gskyhip_parse_numbers(const char *text, int n, double *out, int32_t *consumed);
 int gskyhip_drill_merge(const double *values, const int32_t *counts, int n_files,
                         int n_dates, double *out, void *stream);
 

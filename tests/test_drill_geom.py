@@ -226,3 +226,41 @@ def test_wps_acceptance_polygons_on_gpu(oracle, ds):
         assert np.array_equal(gm[off[i]:off[i] + ew[2] * ew[3]].reshape(ew[3], ew[2]), em), names[i]
         n_ok += 1
     assert n_ok >= 32
+
+
+def test_geojson_number_parser_matches_float():
+    """The descriptor step's decimal parser (drill_geom.cpp fast_decimal:
+    64x128-bit reciprocal products, exact division near halfway, strtod past
+    19 digits) returns what Python's float() (correctly rounded) returns, bit
+    for bit, on GeoJSON-style coordinates, integers, exponents and long
+    mantissas."""
+    import ctypes as C
+
+    from gsky_amd._lib import lib
+    rng = np.random.default_rng(11)
+    strs = []
+    for _ in range(60000):
+        nd = int(rng.integers(1, 22))
+        d = "".join(map(str, rng.integers(0, 10, nd)))
+        pt = int(rng.integers(0, nd + 1))
+        s = ("-" if rng.random() < 0.5 else "") + d[:pt] + "." + d[pt:]
+        if pt == 0:
+            s = s.replace(".", "0.", 1)
+        if rng.random() < 0.25:
+            s += "e%d" % int(rng.integers(-25, 26))
+        strs.append(s)
+    # round-trip reprs of doubles (17 significant digits) and halfway-adjacent ones
+    for v in rng.standard_normal(20000) * 10.0 ** rng.integers(-8, 9, 20000):
+        strs.append(repr(float(v)))
+        strs.append("%.17e" % v)
+    strs += ["0", "-0.0", "1e19", "9007199254740993", "9007199254740993.0", "0.1", "123456789012345678",
+             "1.7976931348623157e308", "4.9e-324", "18446744073709551615", "0.30000000000000004"]
+    buf = b"\0".join(s.encode() for s in strs) + b"\0"
+    out = np.zeros(len(strs), np.float64)
+    used = np.zeros(len(strs), np.int32)
+    assert lib().gskyhip_parse_numbers(buf, len(strs), out.ctypes.data_as(C.c_void_p),
+                                       used.ctypes.data_as(C.c_void_p)) == 0
+    exp = np.array([float(s) for s in strs])
+    assert (used == np.array([len(s) for s in strs])).all()
+    bad = np.nonzero(out.view(np.uint64) != exp.view(np.uint64))[0]
+    assert bad.size == 0, [(strs[i], out[i], exp[i]) for i in bad[:5]]
