@@ -653,6 +653,8 @@ def run_service(ctx: Ctx, args):
             nb, nr = max(1, s1["batches"] - s0["batches"]), max(1, s1["requests"] - s0["requests"])
             r["daemon_batch_ms_mean"] = round((s1["batch_s"] - s0["batch_s"]) * 1e3 / nb, 3)
             r["daemon_resident_ms_mean"] = round((s1["resident_s"] - s0["resident_s"]) * 1e3 / nr, 3)
+            r["daemon_batch_phases_ms_mean"] = {k: round((s1[k + "_s"] - s0[k + "_s"]) * 1e3 / nb, 3)
+                                                for k in ("prep", "gpu", "readback")}
             out["workers_%d" % n] = r
     finally:
         svc.shutdown()

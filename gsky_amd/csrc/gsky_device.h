@@ -547,6 +547,8 @@ struct TilePlan {
   int32_t created[4];
   int32_t dtype[4];
   double nodata[4];           // canvas NoData (first raster of the ns)
+  int32_t e0;                 // first merge entry (order[pair_begin]), -1 when none
+  int32_t _pad;
 };
 
 // Render-time descriptor of one pair (indexed by pair), written by

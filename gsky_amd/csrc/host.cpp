@@ -7,6 +7,9 @@
 #include <hip/hip_runtime.h>
 #include <sys/stat.h>
 
+#include <atomic>
+#include <chrono>
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -745,9 +748,28 @@ namespace gsky {
 // every request with the same destination SRS planned and warped in one set
 // of launches (one tile + one pair per request), bytesRead per request, and
 // one read-back.  The device buffer grows as needed and is kept.
+namespace {
+std::atomic<int64_t> g_wb_ns[4];
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+}  // namespace
+
+void warp_batch_timers(int64_t out[4]) {
+  for (int k = 0; k < 4; k++) out[k] = g_wb_ns[k].load();
+}
+
 void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
   DropIn &d = dropin();
   std::lock_guard<std::mutex> lk(d.mu);
+  int64_t t_prev = now_ns();
+  auto lap = [&](int k) {
+    const int64_t t = now_ns();
+    g_wb_ns[k] += t - t_prev;
+    t_prev = t;
+  };
+  g_wb_ns[3]++;
   d.tick++;
   struct Item { int req; gskyhip_granule g; gskyhip_crs src; int bx, by; const GeoLocEntry *gl; };
   std::map<std::pair<int, std::string>, std::vector<Item>> groups;   // (has dst, dst srs) -> items
@@ -918,6 +940,7 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     int32_t *dbbox = (int32_t *)(base + o_bbox), *ddt = (int32_t *)(base + o_dtype);
     double *dnd = (double *)(base + o_nodata);
     int32_t *dst = (int32_t *)(base + o_stats);
+    lap(0);
     int code = launch_warp_windows(rc, dbbox, ddt, dnd, base + o_win, stride);
     for (int k = 0; k < m && !code; k++)
       code = launch_block_stats(rc, k, items[k].bx, items[k].by, base + o_scr, n_px[k], n_words[k], dst + 4 * k);
@@ -932,6 +955,7 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     // PairPlan[] opens the workspace; its src_gt is the overview-rescaled geotransform
     hipMemcpyAsync(pps.data(), rc.workspace, sizeof(PairPlan) * m, hipMemcpyDeviceToHost, d.stream);
     if (hipStreamSynchronize(d.stream) != hipSuccess) { fail(GSKYHIP_E_HIP); continue; }
+    lap(1);
     for (int k = 0; k < m; k++) {
       WarpResp &r = out[items[k].req];
       for (int j = 0; j < 4; j++) r.bbox[j] = bb[4 * k + j];
@@ -946,6 +970,7 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
         r.rc = GSKYHIP_E_HIP;
     }
     if (hipStreamSynchronize(d.stream) != hipSuccess) fail(GSKYHIP_E_HIP);
+    lap(2);
   }
 }
 

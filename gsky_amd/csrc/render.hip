@@ -817,6 +817,8 @@ __device__ void plan_tile_serial(const PlanArgs &a, int t) {
   tp.status = 0;
   tp.complex = 0;
   tp.vt = 0;
+  tp.e0 = -1;
+  tp._pad = 0;
   double canvas_ts[4];
   for (int k = 0; k < 4; k++) { tp.created[k] = 0; tp.dtype[k] = 0; tp.nodata[k] = 0; canvas_ts[k] = 0; }
   const int b = tile.pair_begin, e = tile.pair_end;
@@ -839,6 +841,7 @@ __device__ void plan_tile_serial(const PlanArgs &a, int t) {
     n++;
   }
   tp.n_entries = n;
+  tp.e0 = n > 0 ? ord[0] : -1;
   for (int k = 0; k < n; k++) {
     PairPlan &pp = a.pairs[ord[k]];
     // maskMap[geoStamp]: the last mask raster of that key (tile_merger.go:478-484)
@@ -1016,6 +1019,8 @@ __device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lan
   tp.n_entries = n;
   tp.status = err_code;
   tp.complex = 0;
+  tp.e0 = n > 0 ? a.order[b] : -1;
+  tp._pad = 0;
   for (int s2 = 0; s2 < 4; s2++) {
     tp.created[s2] = first_k[s2] != 0x7FFFFFFF ? 1 : 0;
     tp.dtype[s2] = 0;
@@ -1748,9 +1753,11 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.cov_stride = rc.cov_stride;
   a.st_pol = 0;
   a.ab_mode = 0;
+  a.ab_vfetch = 1;
 #ifdef GSKYHIP_AB
   if (const char *sp = getenv("GSKYHIP_NN_STPOL")) a.st_pol = atoi(sp);
   if (const char *am = getenv("GSKYHIP_AB_MODE")) a.ab_mode = atoi(am);
+  if (const char *vf = getenv("GSKYHIP_NN_VFETCH")) a.ab_vfetch = atoi(vf);
 #endif
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));

@@ -433,18 +433,42 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
   const int t = item / (bands_per_tile * col_blocks);
   const int in_tile = item - t * bands_per_tile * col_blocks;
-  const TilePlan &tp = tplans[t];
-  if (tp.complex || (tp.n_entries > 0 && tp.vt != vt_code<T>())) return;   // empty tiles: written here
-  const gskyhip_tile &tile = tiles[t];
-  const int W = tile.width, H = tile.height;
-  const int band0 = (in_tile / col_blocks) * kRowsBlk;
-  const int xb = (in_tile % col_blocks) * kBandCols;
-  if (band0 >= H || xb >= W) return;
+  // the block's per-tile values in one round of scalar loads, and the
+  // palette word in flight beside them, before the first branch on any of
+  // them (each dependent load round costs a memory latency per workgroup)
   const int tid = threadIdx.x;
   const int ns_out = a.out_ns[0];
-  const bool created = tp.created[ns_out] != 0;
+  const TilePlan *tpp = tplans + t;
+  const int tp_complex = tpp->complex, n_entries = tpp->n_entries, tp_vt = tpp->vt;
+  const bool created = tpp->created[ns_out] != 0;
+  const int tp_dtype = tpp->dtype[ns_out];
+  const double tp_nodata = tpp->nodata[ns_out];
+  const int e0 = tpp->e0;
+  const int W = tiles[t].width, H = tiles[t].height, pair_begin = tiles[t].pair_begin;
+  uint32_t col = 0;
+  if constexpr (!CANVAS) col = a.ramp ? a.ramp[tid] : (0xFF000000u | ((uint32_t)tid * 0x10101u));
+  const int band0 = (in_tile / col_blocks) * kRowsBlk;
+  const int xb = (in_tile % col_blocks) * kBandCols;
+  // every value above loaded before the first branch (asm: the compiler
+  // would sink the ones used later past it, one more latency each)
+  asm volatile("" ::"s"((int)created), "s"(tp_dtype), "s"(__double_as_longlong(tp_nodata)), "s"(e0));
+  // empty tiles: written here; bitwise, so that no branch splits the loads
+  if ((tp_complex != 0) | ((n_entries > 0) & (tp_vt != vt_code<T>())) | (band0 >= H) | (xb >= W)) return;
+  // ONE: the single entry's descriptor, loaded in the round after the tile's
+  // (its index is the tile plan's e0) and before the palette barrier
+  const EntryD *e1 = ents + max(e0, 0);
+  int e1_yoff = 0, e1_h = 0, e1_xoff = 0, e1_w = 0, e1_ns = 0, e1_bx = 0, e1_by = 0, e1_fill = 0;
+  uint32_t e1_nd = 0;
+  const void *e1_band = nullptr;
+  int64_t e1_row_base = 0;
+  if constexpr (ONE && !MASK && !CANVAS) {
+    e1_yoff = e1->yoff; e1_h = e1->h; e1_xoff = e1->xoff; e1_w = e1->w; e1_ns = e1->ns;
+    e1_bx = e1->band_x; e1_by = e1->band_y; e1_fill = e1->fill_mode; e1_nd = e1->nd.u;
+    e1_band = e1->band; e1_row_base = e1->row_base;
+    asm volatile("" ::"s"(e1_yoff), "s"(e1_h), "s"(e1_xoff), "s"(e1_w), "s"(e1_ns), "s"(e1_bx), "s"(e1_by),
+                 "s"(e1_fill), "s"(e1_nd), "s"(e1_band), "s"(e1_row_base));
+  }
   if constexpr (!CANVAS) {   // EncodePNG: utils.Scale 0xFF and canvases never created are transparent
-    const uint32_t col = a.ramp ? a.ramp[tid] : (0xFF000000u | ((uint32_t)tid * 0x10101u));
     s_tab[tid] = (created && tid != 255) ? col : 0u;
     __syncthreads();
   }
@@ -452,10 +476,9 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int r0 = band0 + wave * RPW;
   if (r0 >= H) return;
 
-  const V cnod = as_v<T>(go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]));
-  const int32_t *ord = order + tile.pair_begin;
-  const int n_entries = tp.n_entries;
-  const ScaleK sk = make_scale(tp.dtype[ns_out], tp.nodata[ns_out], a.sp, false, 0.f, 0.f);
+  const V cnod = as_v<T>(go_conv_to(tp_nodata, tp_dtype));
+  const int32_t *ord = order + pair_begin;
+  const ScaleK sk = make_scale(tp_dtype, tp_nodata, a.sp, false, 0.f, 0.f);
   const bool safe = !std::is_same<T, float>::value && (float)max(sk.clp.i, 0) * sk.sc < 2147483648.0f;
   const int ncols = min(kBandCols, W - xb);     // columns of the block inside the tile
   const bool full = ncols == kBandCols;
@@ -515,19 +538,21 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 
   if constexpr (ONE && !MASK && !CANVAS) {
     if (n_entries == 1) {
-      const EntryD &e = ents[ord[0]];
-      const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
+      const EntryD &e = *e1;   // the fp64 fallback rows read the rest of it
+      const int eyoff = e1_yoff, eh = e1_h, exoff = e1_xoff, ew = e1_w;
       const int lim = max(0, min(ew, W - exoff));
       const int c0 = exoff - xb, c1 = exoff + lim - xb;
-      const bool cols_ok = e.ns == ns_out && ew > 0 && c1 > 0 && c0 < ncols;
+      const bool cols_ok = e1_ns == ns_out && ew > 0 && c1 > 0 && c0 < ncols;
       const bool cover = c0 <= 0 && c1 >= ncols;
-      const int bx = e.band_x, by = e.band_y;
-      const V nd = as_v<T>(e.nd);
-      const bool fill_mode = e.fill_mode != 0;
+      const int bx = e1_bx, by = e1_by;
+      Val ndv;
+      ndv.u = e1_nd;
+      const V nd = as_v<T>(ndv);
+      const bool fill_mode = e1_fill != 0;
       const int ic0 = xl - exoff;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
-      const RowFix *fbase = rowfix + e.row_base;
+          (void *)uniform_ptr(e1_band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
+      const RowFix *fbase = rowfix + e1_row_base;
       // the row's fixed-point form, or fk = -1 outside the window / 0 none
       auto fetch = [&](int ir, int64_t (&f)[4], int &fk) {
         if (ir < 0 || ir >= eh) { fk = -1; return; }
@@ -541,12 +566,43 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
       // truncation boundary): done in a second loop, so that loop's loads do
       // not reach the register and wait-count state of this one
       uint32_t redo = 0;
-      if (cols_ok) fetch(r0 - eyoff, cf, cfk);
+      // VFETCH: the RowFix records of all RPW rows in one coalesced vector
+      // load (lane 4j + k: field k of row j), read out per row with
+      // v_readlane -- one memory latency per wave instead of one per row
+      // (the scalar fetch of the next row is still in flight when a row's
+      // stores are issued)
+      bool vfetch = RPW <= 16;
+#ifdef GSKYHIP_AB
+      vfetch = vfetch && a.ab_vfetch;
+#endif
+      int64_t fv = kFixNone;
+      if (vfetch) {
+        const int jj = lane >> 2, kk = lane & 3, ir = r0 - eyoff + jj;
+        if (cols_ok && lane < 4 * RPW && ir >= 0 && ir < eh)
+          fv = __builtin_nontemporal_load((const int64_t *)(fbase + ir) + kk);
+      } else if (cols_ok) {
+        fetch(r0 - eyoff, cf, cfk);
+      }
 #pragma unroll 1
       for (int j = 0; j < RPW; j++) {
         const int r = r0 + j;
         if (r >= H) break;
-        if (cols_ok && j + 1 < RPW) fetch(r + 1 - eyoff, nf, nfk);   // next row's record, in flight now
+        if (vfetch) {
+          const int ir = r - eyoff;
+          if (!cols_ok || ir < 0 || ir >= eh) {
+            cfk = -1;
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)fv, 4 * j + k);
+              const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)fv >> 32), 4 * j + k);
+              cf[k] = (int64_t)(((uint64_t)hi << 32) | lo);
+            }
+            cfk = cf[0] != kFixNone ? 1 : 0;
+          }
+        } else if (cols_ok && j + 1 < RPW) {
+          fetch(r + 1 - eyoff, nf, nfk);   // next row's record, in flight now
+        }
         V c[kNnPx];
 #pragma unroll
         for (int q = 0; q < kNnPx; q++) c[q] = cnod;
@@ -568,9 +624,11 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         } else {
           redo |= 1u << j;
         }
+        if (!vfetch) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) cf[k] = nf[k];
-        cfk = nfk;
+          for (int k = 0; k < 4; k++) cf[k] = nf[k];
+          cfk = nfk;
+        }
       }
 #pragma unroll 1
       while (redo) {
@@ -649,7 +707,10 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   // large RGBA batches through the LDS-staged kernel (render_nn_stage.h): 7 %
   // slower on C2 (1.54 vs 1.44 ms, profiles/r03j_ab_c2_staged.jsonl)
   bool staged = false;
-  if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
+  if (const char *rp = getenv("GSKYHIP_NN_RPW")) {
+    rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1;
+    if (atoi(rp) == 16 && !mask && !canvas && one) { launch_nn_v<T, false, false, 16, true>(a, s); return; }
+  }
   if (const char *on = getenv("GSKYHIP_NN_ONE")) one = atoi(on) != 0;
   if (const char *sg = getenv("GSKYHIP_NN_STAGED")) staged = atoi(sg) != 0;
   if (const char *st = getenv("GSKYHIP_NN_STAGE")) {

@@ -372,6 +372,9 @@ void conn_serve(Service *s, int fd) {
       o.put<int64_t>(s->n_req.load()); o.put<int64_t>(s->n_batches.load());
       o.put<int64_t>(s->max_seen.load()); o.put<int64_t>(s->n_reg.load());
       o.put<int64_t>(s->batch_ns.load()); o.put<int64_t>(s->resident_ns.load());
+      int64_t wb[4];
+      warp_batch_timers(wb);
+      for (int k = 0; k < 3; k++) o.put<int64_t>(wb[k]);
     } else if (op == SVC_SHUTDOWN) {
       o.put<int32_t>(0);
       send_msg(fd, op, o.b);

@@ -42,4 +42,10 @@ struct WarpResp {
 // gskyhip_register_granule).  Thread-safe (one batch at a time).
 void warp_batch(const WarpReq *reqs, int n, WarpResp *out);
 
+// Nanoseconds this process spent in warp_batch by phase, summed over calls:
+// [0] host preparation (registry, SRS parsing, header upload issued),
+// [1] launches through the first read-back (GPU work + small copies),
+// [2] window read-back into the responses, [3] calls.
+void warp_batch_timers(int64_t out[4]);
+
 }  // namespace gsky

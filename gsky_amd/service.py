@@ -98,10 +98,11 @@ class WarpService:
         check(lib().gskyhip_service_unregister_all(self.socket_path.encode()), "service unregister")
 
     def stats(self) -> Dict[str, int]:
-        st = (C.c_int64 * 6)()
-        check(lib().gskyhip_service_stats_n(self.socket_path.encode(), st, 6), "service stats")
+        st = (C.c_int64 * 9)()
+        check(lib().gskyhip_service_stats_n(self.socket_path.encode(), st, 9), "service stats")
         return {"requests": st[0], "batches": st[1], "max_batch": st[2], "granules": st[3],
-                "batch_s": st[4] * 1e-9, "resident_s": st[5] * 1e-9}
+                "batch_s": st[4] * 1e-9, "resident_s": st[5] * 1e-9, "prep_s": st[6] * 1e-9,
+                "gpu_s": st[7] * 1e-9, "readback_s": st[8] * 1e-9}
 
     def shutdown(self, timeout: float = 60.0) -> Optional[int]:
         """Stops the daemon; returns its exit code when this handle started it."""

@@ -330,8 +330,10 @@ int gskyhip_service_unregister_all(const char *socket_path);
 /* stats[4]: warp requests served, batches run, largest batch, registered granules */
 int gskyhip_service_stats(const char *socket_path, int64_t *stats);
 /* the same and, at [4], nanoseconds the daemon spent in warp batches, at [5]
- * the summed residence of requests (enqueued -> answer ready); the first
- * n_stats values are written (0 past what the daemon reports) */
+ * the summed residence of requests (enqueued -> answer ready), at [6..8] the
+ * warp batches' host preparation, launches through the first read-back, and
+ * window read-back (ns); the first n_stats values are written (0 past what
+ * the daemon reports) */
 int gskyhip_service_stats_n(const char *socket_path, int64_t *stats, int n_stats);
 int gskyhip_service_shutdown(const char *socket_path);
 
