@@ -286,6 +286,8 @@ struct DropIn {
   void *dev = nullptr;   // descriptors + workspace + window
   size_t dev_bytes = 0;
   uint64_t tick = 0;     // one per warp batch: entries it uses are not evicted while it runs
+  char *pin = nullptr;   // pinned read-back staging (metadata + windows), grown as needed
+  size_t pin_bytes = 0;
   std::map<std::string, struct GeoLocEntry *> geolocs;   // by GeoLocOpts (geoloc_entry)
 };
 DropIn &dropin() {
@@ -848,8 +850,9 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     const std::vector<Item> &items = kv.second;
     const int m = (int)items.size();
     int max_w = 1, max_h = 1;
-    int64_t st_bytes = 0;
+    int64_t st_bytes = 0, max_px = 0;
     std::vector<int64_t> n_px(m), n_words(m);
+    std::vector<BlockStatsJob> jobs(m);
     for (int k = 0; k < m; k++) {
       const WarpReq &q = reqs[items[k].req];
       max_w = std::max(max_w, q.width);
@@ -859,10 +862,20 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
       const int64_t nblocks = ((int64_t)(g.xsize + bx0 - 1) / bx0) * ((g.ysize + items[k].by - 1) / items[k].by);
       n_words[k] = (nblocks + 31) / 32;
       n_px[k] = (int64_t)q.width * q.height;
-      st_bytes = std::max(st_bytes, a256(block_stats_scratch_bytes(n_px[k], n_words[k])));
+      max_px = std::max(max_px, n_px[k]);
+      jobs[k].bx = items[k].bx;
+      jobs[k].by = items[k].by;
+      jobs[k].n_words = (int32_t)n_words[k];
+      jobs[k]._pad = 0;
+      jobs[k].xsrc_off = st_bytes;                 // xsrc of every job, then every job's bitmap
+      st_bytes += a256(n_px[k] * 4);
+    }
+    for (int k = 0; k < m; k++) {
+      jobs[k].bits_off = st_bytes;
+      st_bytes += a256(n_words[k] * 4);
     }
     // device layout: granules | geolocation transformers | crs (m sources + dst) | tiles | pairs | bbox
-    //                | dtype | nodata | stats
+    //                | dtype | nodata | stats | block-stats jobs
     //                | workspace | windows (m x stride) | block-stats scratch
     const int64_t o_gl = a256((int64_t)m * sizeof(gskyhip_granule));
     const int64_t o_crs = o_gl + a256((int64_t)m * sizeof(GeoLocD));
@@ -872,7 +885,8 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     const int64_t o_dtype = o_bbox + a256((int64_t)m * 16);
     const int64_t o_nodata = o_dtype + a256((int64_t)m * 4);
     const int64_t o_stats = o_nodata + a256((int64_t)m * 8);
-    const int64_t o_ws = o_stats + a256((int64_t)m * 16);
+    const int64_t o_jobs = o_stats + a256((int64_t)m * 16);
+    const int64_t o_ws = o_jobs + a256((int64_t)m * sizeof(BlockStatsJob));
     const int64_t ws = render_workspace_size(m, m, max_h);
     const int64_t stride = a256((int64_t)max_w * max_h * 4);
     const int64_t o_win = o_ws + a256(ws);
@@ -897,6 +911,7 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
       parse_srs(kv.first.second.c_str(), &hc[m]);
       dst_crs = m;
     }
+    std::memcpy(hdr.data() + o_jobs, jobs.data(), (size_t)m * sizeof(BlockStatsJob));
     GeoLocD *hgl = (GeoLocD *)(hdr.data() + o_gl);
     bool any_gl = false;
     for (int k = 0; k < m; k++) {
@@ -942,20 +957,38 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     int32_t *dst = (int32_t *)(base + o_stats);
     lap(0);
     int code = launch_warp_windows(rc, dbbox, ddt, dnd, base + o_win, stride);
-    for (int k = 0; k < m && !code; k++)
-      code = launch_block_stats(rc, k, items[k].bx, items[k].by, base + o_scr, n_px[k], n_words[k], dst + 4 * k);
+    if (!code)
+      code = launch_block_stats_batch(rc, (const BlockStatsJob *)(base + o_jobs), m, max_px, base + o_scr, dst);
     if (code) { fail(code); continue; }
-    std::vector<int32_t> bb(4 * m), dt(m), stv(4 * m);
-    std::vector<double> nd(m), gts(6 * m);
-    std::vector<PairPlan> pps(m);
-    hipMemcpyAsync(bb.data(), dbbox, 16 * m, hipMemcpyDeviceToHost, d.stream);
-    hipMemcpyAsync(dt.data(), ddt, 4 * m, hipMemcpyDeviceToHost, d.stream);
-    hipMemcpyAsync(nd.data(), dnd, 8 * m, hipMemcpyDeviceToHost, d.stream);
-    hipMemcpyAsync(stv.data(), dst, 16 * m, hipMemcpyDeviceToHost, d.stream);
-    // PairPlan[] opens the workspace; its src_gt is the overview-rescaled geotransform
-    hipMemcpyAsync(pps.data(), rc.workspace, sizeof(PairPlan) * m, hipMemcpyDeviceToHost, d.stream);
-    if (hipStreamSynchronize(d.stream) != hipSuccess) { fail(GSKYHIP_E_HIP); continue; }
+    // read-back through pinned staging: bbox | dtype | nodata | stats in one
+    // copy, the PairPlans (their src_gt is the overview-rescaled
+    // geotransform) in another, then every window -- one wait each phase
+    const int64_t meta = o_jobs - o_bbox, o_pp = a256(meta), o_wins = o_pp + a256((int64_t)sizeof(PairPlan) * m);
+    const size_t pin_need = (size_t)(o_wins + stride * m);
+    if (d.pin_bytes < pin_need) {
+      if (d.pin) (void)hipHostFree(d.pin);
+      d.pin = nullptr;
+      d.pin_bytes = 0;
+      if (hipHostMalloc((void **)&d.pin, pin_need, hipHostMallocDefault) != hipSuccess) {
+        fail(GSKYHIP_E_HIP);
+        continue;
+      }
+      d.pin_bytes = pin_need;
+    }
+    char *hp0 = d.pin;
+    if (hipMemcpyAsync(hp0, dbbox, (size_t)meta, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
+        hipMemcpyAsync(hp0 + o_pp, rc.workspace, sizeof(PairPlan) * m, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
+        hipStreamSynchronize(d.stream) != hipSuccess) {
+      fail(GSKYHIP_E_HIP);
+      continue;
+    }
     lap(1);
+    const int32_t *bb = (const int32_t *)hp0, *dt = (const int32_t *)(hp0 + (o_dtype - o_bbox));
+    const double *nd = (const double *)(hp0 + (o_nodata - o_bbox));
+    const int32_t *stv = (const int32_t *)(hp0 + (o_stats - o_bbox));
+    const PairPlan *pps = (const PairPlan *)(hp0 + o_pp);
+    std::vector<int64_t> szs(m, 0);
+    bool copy_ok = true;
     for (int k = 0; k < m; k++) {
       WarpResp &r = out[items[k].req];
       for (int j = 0; j < 4; j++) r.bbox[j] = bb[4 * k + j];
@@ -963,13 +996,16 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
       r.nodata = nd[k];
       r.bytes_read = stv[4 * k + 2];
       std::memcpy(r.src_gt, pps[k].src_gt, sizeof(r.src_gt));
-      const int64_t sz = (int64_t)r.bbox[2] * r.bbox[3] * type_size(r.dtype);
-      r.data.resize((size_t)std::max<int64_t>(sz, 0));
-      if (sz > 0 && hipMemcpyAsync(r.data.data(), base + o_win + stride * k, (size_t)sz, hipMemcpyDeviceToHost,
-                                   d.stream) != hipSuccess)
-        r.rc = GSKYHIP_E_HIP;
+      szs[k] = std::min<int64_t>(std::max<int64_t>((int64_t)r.bbox[2] * r.bbox[3] * type_size(r.dtype), 0), stride);
+      if (szs[k] > 0 && hipMemcpyAsync(hp0 + o_wins + stride * k, base + o_win + stride * k, (size_t)szs[k],
+                                       hipMemcpyDeviceToHost, d.stream) != hipSuccess)
+        copy_ok = false;
     }
-    if (hipStreamSynchronize(d.stream) != hipSuccess) fail(GSKYHIP_E_HIP);
+    if (!copy_ok || hipStreamSynchronize(d.stream) != hipSuccess) { fail(GSKYHIP_E_HIP); continue; }
+    for (int k = 0; k < m; k++) {
+      WarpResp &r = out[items[k].req];
+      r.data.assign(hp0 + o_wins + stride * k, hp0 + o_wins + stride * k + szs[k]);
+    }
     lap(2);
   }
 }

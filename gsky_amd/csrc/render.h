@@ -36,9 +36,16 @@ int launch_extent(const gskyhip_granule *granules, int n, const gskyhip_crs *crs
                   int32_t *out, int32_t *status, hipStream_t s);
 int launch_warp_windows(const RenderCall &c, int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
                         void *win_out, int64_t win_stride);
-// bytesRead of the drop-in (pair `pair` of a planned call): stats[2] receives it.
-int64_t block_stats_scratch_bytes(int64_t n_px, int64_t n_words);
-int launch_block_stats(const RenderCall &c, int pair, int bx, int by, void *scratch, int64_t n_px,
-                       int64_t n_words, int32_t *stats);
+// bytesRead of the drop-in for the pairs of a planned call, job k = pair k
+// (one request each): stats[4k + 2] receives it.  `jobs` (device) give each
+// job's block size, its bitmap words and its xsrc / bitmap regions (byte
+// offsets into `scratch`, 4-byte aligned, xsrc max_px words); max_px bounds
+// every pair's window (w * h).
+struct BlockStatsJob {
+  int32_t bx, by, n_words, _pad;
+  int64_t xsrc_off, bits_off;
+};
+int launch_block_stats_batch(const RenderCall &c, const BlockStatsJob *jobs, int n_jobs, int64_t max_px,
+                             void *scratch, int32_t *stats);
 
 }  // namespace gsky

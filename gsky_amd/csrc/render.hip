@@ -1482,47 +1482,94 @@ __global__ __launch_bounds__(256) void warp_window_kernel(const PairPlan *pairs,
 // reference's two tests -- the cache heuristic's x test (success, dx >= 0,
 // iSrcX < srcXSize; no dy test) and the full gather test -- plus the set of
 // source blocks that valid pixels touch.
-__global__ __launch_bounds__(256) void block_stats_kernel(const PairPlan *pairs, const Xform *xforms,
-                                                          const RowRec *rows, const Leaf *pool, int bx, int by,
-                                                          int32_t *xsrc, uint32_t *bits, int32_t *stats) {
-  const PairPlan &pp = pairs[0];
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (long)pp.w * pp.h) return;
-  const int row = (int)(gid / pp.w), i = (int)(gid % pp.w);
-  double sx, sy;
-  const bool ok = src_coords<true>(rows[row], pool, xforms, pp.xoff, pp.yoff, pp.w, i, row, sx, sy);
-  int xs = -1;
-  bool valid = false;
-  int ix = 0, iy = 0;
-  if (ok && !(sx < 0)) {
-    const double ax = sx + 1.0e-10;
-    if (ax < 2147483647.0) {
-      ix = (int)ax;
-      if (ix < pp.band_x) xs = ix;
-    }
+// warp.go:281-347 bytesRead of every (single-pair) request of a warp batch,
+// blockIdx.y = job = pair: per valid pixel the source x (xsrc, for the
+// cache decision), the first valid pixel, the valid count and the touched
+// block bits.  The counters are reduced per workgroup (ballots, one atomic
+// each) and the bits per wave (a lane ORs its block only where it differs
+// from the previous lane's), so neighbouring pixels do not serialize on one
+// address.
+__global__ __launch_bounds__(256) void block_stats_init_kernel(const BlockStatsJob *jobs, char *scratch,
+                                                               int32_t *stats) {
+  const BlockStatsJob J = jobs[blockIdx.x];
+  uint32_t *bits = (uint32_t *)(scratch + J.bits_off);
+  for (int k = threadIdx.x; k < J.n_words; k += blockDim.x) bits[k] = 0u;
+  if (threadIdx.x == 0) {
+    int32_t *st = stats + 4 * blockIdx.x;
+    st[0] = 0x7FFFFFFF; st[1] = 0; st[2] = 0; st[3] = 0;
   }
-  if (xs >= 0 && !(sy < 0)) {
-    const double ay = sy + 1.0e-10;
-    if (ay < 2147483647.0) {
-      iy = (int)ay;
-      valid = iy < pp.band_y;
-    }
-  }
-  xsrc[gid] = xs;
-  if (!valid) return;
-  atomicMin(&stats[0], (int32_t)gid);
-  atomicAdd(&stats[1], 1);
-  if (bx <= 0) bx = pp.band_x;        // default block: one scanline of the chosen level
-  const int nxb = (pp.band_x + bx - 1) / bx;
-  const long blk = (long)(ix / bx) + (long)(iy / by) * nxb;
-  atomicOr(&bits[blk >> 5], 1u << (blk & 31));
 }
 
-// warp.go:281-313 (the cache decision at the first valid pixel) and 347.
-__global__ void block_stats_resolve_kernel(const PairPlan *pairs, int bx, int by, const int32_t *xsrc,
-                                           const uint32_t *bits, int n_words, int32_t *stats) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const PairPlan &pp = pairs[0];
+__global__ __launch_bounds__(256) void block_stats_kernel(const PairPlan *pairs, const Xform *xforms,
+                                                          const RowRec *rows, const Leaf *pool, int max_h,
+                                                          const BlockStatsJob *jobs, char *scratch, int32_t *stats) {
+  const int job = blockIdx.y;
+  const PairPlan &pp = pairs[job];
+  const BlockStatsJob J = jobs[job];
+  int32_t *xsrc = (int32_t *)(scratch + J.xsrc_off);
+  uint32_t *bits = (uint32_t *)(scratch + J.bits_off);
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)pp.w * pp.h;
+  bool valid = false;
+  int ix = 0, iy = 0;
+  if (gid < n) {
+    const int row = (int)(gid / pp.w), i = (int)(gid % pp.w);
+    double sx, sy;
+    const bool ok = src_coords<true>(rows[(int64_t)job * max_h + row], pool, xforms + job, pp.xoff, pp.yoff, pp.w, i,
+                                     row, sx, sy);
+    int xs = -1;
+    if (ok && !(sx < 0)) {
+      const double ax = sx + 1.0e-10;
+      if (ax < 2147483647.0) {
+        ix = (int)ax;
+        if (ix < pp.band_x) xs = ix;
+      }
+    }
+    if (xs >= 0 && !(sy < 0)) {
+      const double ay = sy + 1.0e-10;
+      if (ay < 2147483647.0) {
+        iy = (int)ay;
+        valid = iy < pp.band_y;
+      }
+    }
+    xsrc[gid] = xs;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long bal = __ballot(valid);
+  __shared__ int s_first[4], s_count[4];
+  if (lane == 0) {
+    s_first[wave] = bal ? (int)(gid + __ffsll((long long)bal) - 1) : 0x7FFFFFFF;
+    s_count[wave] = __popcll(bal);
+  }
+  int bx = J.bx;
+  if (bx <= 0) bx = pp.band_x;        // default block: one scanline of the chosen level
+  const int nxb = (pp.band_x + bx - 1) / bx;
+  const long long blk = valid ? (long long)(ix / bx) + (long long)(iy / J.by) * nxb : -1;
+  const long long prev = __shfl_up(blk, 1, 64);
+  if (valid && (lane == 0 || prev != blk)) atomicOr(&bits[blk >> 5], 1u << (blk & 31));
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int first = s_first[0], count = s_count[0];
+    for (int w = 1; w < 4; w++) { first = min(first, s_first[w]); count += s_count[w]; }
+    if (count > 0) {
+      atomicMin(&stats[4 * job], first);
+      atomicAdd(&stats[4 * job + 1], count);
+    }
+  }
+}
+
+// warp.go:281-313 (the cache decision at the first valid pixel) and 347, a
+// workgroup (one thread) per job.
+__global__ void block_stats_resolve_kernel(const PairPlan *pairs, const BlockStatsJob *jobs, const char *scratch,
+                                           int32_t *stats_all) {
+  if (threadIdx.x != 0) return;
+  const int job = blockIdx.x;
+  const PairPlan &pp = pairs[job];
+  const BlockStatsJob J = jobs[job];
+  const int32_t *xsrc = (const int32_t *)(scratch + J.xsrc_off);
+  const uint32_t *bits = (const uint32_t *)(scratch + J.bits_off);
+  int32_t *stats = stats_all + 4 * job;
+  int bx = J.bx;
   if (bx <= 0) bx = pp.band_x;
   const int i0 = stats[0];
   if (i0 == 0x7FFFFFFF) { stats[2] = 0; return; }
@@ -1538,12 +1585,12 @@ __global__ void block_stats_resolve_kernel(const PairPlan *pairs, int bx, int by
   const bool cache = stride >= 0 && stride < bx;
   long nread = 0;
   if (cache) {
-    for (int k = 0; k < n_words; k++) nread += __popc(bits[k]);
+    for (int k = 0; k < J.n_words; k++) nread += __popc(bits[k]);
   } else {
     nread = stats[1];   // one GDALReadBlock per valid pixel (warp.go:319-322)
   }
   // C int arithmetic of warp.go:347 (wraps like the reference's 32-bit int)
-  const long long b = (long long)bx * by * type_size(pp.src_dtype) * nread;
+  const long long b = (long long)bx * J.by * type_size(pp.src_dtype) * nread;
   stats[2] = (int32_t)(uint32_t)(unsigned long long)b;
 }
 
@@ -1797,24 +1844,19 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 
-int launch_block_stats(const RenderCall &rc, int pair, int bx, int by, void *scratch, int64_t n_px,
-                       int64_t n_words, int32_t *stats) {
+int launch_block_stats_batch(const RenderCall &rc, const BlockStatsJob *jobs, int n_jobs, int64_t max_px,
+                             void *scratch, int32_t *stats) {
+  if (n_jobs <= 0) return 0;
   const Carve cv = carve(rc.workspace, rc.n_tiles, rc.n_pairs, rc.max_h);
-  int32_t *xsrc = (int32_t *)scratch;
-  uint32_t *bits = (uint32_t *)((char *)scratch + align256(n_px * 4));
   hipStream_t s = rc.stream;
-  const int32_t init[3] = {0x7FFFFFFF, 0, 0};
-  if (hipMemsetAsync(bits, 0, (size_t)n_words * 4, s) != hipSuccess) return GSKYHIP_E_HIP;
-  if (hipMemcpyAsync(stats, init, sizeof(init), hipMemcpyHostToDevice, s) != hipSuccess) return GSKYHIP_E_HIP;
-  if (n_px > 0)
-    hipLaunchKernelGGL(block_stats_kernel, dim3((unsigned)((n_px + 255) / 256)), dim3(256), 0, s, cv.pairs + pair,
-                       cv.xforms + pair, cv.rows + (int64_t)pair * rc.max_h, cv.pool, bx, by, xsrc, bits, stats);
-  hipLaunchKernelGGL(block_stats_resolve_kernel, dim3(1), dim3(64), 0, s, cv.pairs + pair, bx, by, xsrc, bits,
-                     (int)n_words, stats);
+  hipLaunchKernelGGL(block_stats_init_kernel, dim3(n_jobs), dim3(256), 0, s, jobs, (char *)scratch, stats);
+  if (max_px > 0)
+    hipLaunchKernelGGL(block_stats_kernel, dim3((unsigned)((max_px + 255) / 256), n_jobs), dim3(256), 0, s, cv.pairs,
+                       cv.xforms, cv.rows, cv.pool, rc.max_h, jobs, (char *)scratch, stats);
+  hipLaunchKernelGGL(block_stats_resolve_kernel, dim3(n_jobs), dim3(64), 0, s, cv.pairs, jobs,
+                     (const char *)scratch, stats);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
-
-int64_t block_stats_scratch_bytes(int64_t n_px, int64_t n_words) { return align256(n_px * 4) + n_words * 4; }
 
 int launch_warp_windows(const RenderCall &rc, int32_t *bbox_out, int32_t *dtype_out, double *nodata_out,
                         void *win_out, int64_t win_stride) {

@@ -34,3 +34,8 @@ rc=$?; tail -3 gpurun_out/gpu_tests.log; stop $rc gpu_tests
 timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/prof_svc -o run --output-format csv -- \
   python3 bench.py --only svc --no-cpu --svc-jobs 256 > gpurun_out/prof_svc.log 2>&1
 stop $? prof_svc
+timeout -k 10 400 python3 bench.py --only svc --no-cpu --steps 3 --warmup 1 > gpurun_out/svc.json 2> gpurun_out/svc.err
+stop $? svc
+python3 -c "
+import json; d=json.load(open('gpurun_out/svc.json'))['configs']['service']
+for k in ('workers_16','workers_64'): print(k, json.dumps(d[k]))"
