@@ -103,7 +103,7 @@ EXPORTS = [
     "gskyhip_png_workspace_size", "gskyhip_png_bound", "gskyhip_encode_png",
     "gskyhip_geotiff_workspace_size", "gskyhip_geotiff_bound", "gskyhip_encode_geotiff",
     "gskyhip_geotiff_info", "gskyhip_geotiff_read_host", "gskyhip_geotiff_read", "gskyhip_register_geotiff",
-    "gskyhip_netcdf_info", "gskyhip_netcdf_read_host", "gskyhip_netcdf_read", "gskyhip_register_netcdf",
+    "gskyhip_netcdf_info", "gskyhip_netcdf_srs", "gskyhip_netcdf_read_host", "gskyhip_netcdf_read", "gskyhip_register_netcdf",
 ]
 
 _lib = None
@@ -126,6 +126,8 @@ def lib() -> C.CDLL:
     L.gskyhip_geotiff_read.argtypes = [C.c_char_p, ci, ci, vp, i64, vp]
     L.gskyhip_register_geotiff.argtypes = [C.c_char_p, ci]
     L.gskyhip_netcdf_info.argtypes = [C.c_char_p, C.POINTER(RasterInfo)]
+    if hasattr(L, "gskyhip_netcdf_srs"):
+        L.gskyhip_netcdf_srs.argtypes = [C.c_char_p, ci, C.c_char_p, ci]
     L.gskyhip_netcdf_read_host.argtypes = [C.c_char_p, ci, vp, i64]
     L.gskyhip_netcdf_read.argtypes = [C.c_char_p, ci, vp, i64, vp]
     L.gskyhip_register_netcdf.argtypes = [C.c_char_p, ci]

@@ -23,6 +23,7 @@
 #include "../../include/gskyhip.h"
 #include "drill.h"
 #include "gsky_device.h"
+#include "ingest.h"
 #include "render.h"
 #include "stages.h"
 #include "service.h"
@@ -267,6 +268,10 @@ struct Registered {
   gskyhip_granule g;
   gskyhip_crs crs;
   bool has_crs;
+  // netCDF: the SRS under srs_cf=yes (netcdfdataset.cpp:3666), and whether
+  // either SRS is a projection the warp cannot represent (-> GSKYHIP_E_CRS)
+  gskyhip_crs crs_cf;
+  bool has_crs_cf = false, bad_crs = false, bad_crs_cf = false;
   std::vector<void *> owned;   // HBM the library allocated for it (ingested files)
   int64_t bytes = 0;           // ... and its size
   uint64_t last_use = 0;       // DropIn::tick of the last batch that used it
@@ -408,7 +413,8 @@ int ingest_geotiff_locked(DropIn &d, const std::string &path, int band) {
 // warp.go:89-101: the band is registered under (path, band)).
 int ingest_netcdf_locked(DropIn &d, const std::string &path, int band) {
   gskyhip_raster_info info;
-  int rc = gskyhip_netcdf_info(path.c_str(), &info);
+  std::string srs_no, srs_cf;
+  int rc = netcdf_info_srs(path.c_str(), &info, &srs_no, &srs_cf);
   if (rc) return rc;
   if (band < 1 || band > info.n_bands) return 1;   // band_query past the variable: the open fails
   if (!have_gpu()) return GSKYHIP_E_NOGPU;
@@ -435,10 +441,17 @@ int ingest_netcdf_locked(DropIn &d, const std::string &path, int band) {
   for (int k = 0; k < 6; k++) g.geot[k] = info.geot[k];
   g.nodata = info.nodata; g.has_nodata = info.has_nodata;
   g.block_x = info.block_x; g.block_y = info.block_y;
-  r.has_crs = false;
-  char srs[32] = {0};
-  if (info.epsg > 0) std::snprintf(srs, sizeof(srs), "EPSG:%d", info.epsg);
-  if (srs[0] && parse_srs(srs, &r.crs) == 0) r.has_crs = true;
+  // "" -> no SRS (the warp takes WGS84, warp.go:107-112); "?" or one the
+  // warp cannot parse -> the request fails with GSKYHIP_E_CRS
+  auto set_crs = [](const std::string &srs, gskyhip_crs &c, bool &has, bool &bad) {
+    has = false;
+    bad = false;
+    if (srs.empty()) return;
+    if (srs != "?" && parse_srs(srs.c_str(), &c) == 0) has = true;
+    else bad = true;
+  };
+  set_crs(srs_no, r.crs, r.has_crs, r.bad_crs);
+  set_crs(srs_cf, r.crs_cf, r.has_crs_cf, r.bad_crs_cf);
   auto it = d.reg.find({path, band});
   if (it != d.reg.end()) release(it->second);
   d.reg[{path, band}] = std::move(r);
@@ -818,10 +831,17 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
       it2.gl = geoloc_entry(d, q.geoloc_opts);
       if (!it2.gl) { r.rc = 3; continue; }
     }
+    // the dataset SRS: GSKY_netCDF opened with srs_cf=yes takes the CF
+    // grid mapping only (warp.go:95, netcdfdataset.cpp:3666)
+    const bool cf = netcdf && q.srs_cf > 0 && R.fsize >= 0;
+    const bool has_crs = cf ? R.has_crs_cf : R.has_crs, bad_crs = cf ? R.bad_crs_cf : R.bad_crs;
     if (q.has_src_srs) {
       if (parse_srs(q.src_srs.c_str(), &it2.src)) { r.rc = 3; continue; }
-    } else if (R.has_crs) {
-      it2.src = R.crs;
+    } else if (bad_crs) {
+      r.rc = GSKYHIP_E_CRS;                                            // a projection outside the four families
+      continue;
+    } else if (has_crs) {
+      it2.src = cf ? R.crs_cf : R.crs;
     } else {
       crs_epsg(4326, &it2.src);                                        // warp.go:107-112
     }

@@ -929,6 +929,98 @@ int nc_epsg(const Nc &f, const NcVar &v) {
   return 0;
 }
 
+// The SRS of the variable's CF grid mapping (grid_mapping_name and its
+// parameters, CF-1.x Appendix F, as GSKY_netCDF's SetProjectionFromVar reads
+// them), as a PROJ string of the projection families the warp supports;
+// "" without a grid mapping (lon / lat axes: EPSG:4326, else none -- the
+// warp then takes WGS84, warp.go:107-112), "?" for a mapping it cannot
+// represent.  Parity unpinned (netCDF-C / GDAL are absent).
+std::string nc_cf_srs(const Nc &f, const NcVar &v) {
+  auto num = [](const NcVar &m, const char *k, int i, double dflt) {
+    const NcAtt *a = nc_att(m.atts, k);
+    return (a && (int)a->num.size() > i) ? a->num[i] : dflt;
+  };
+  auto has = [](const NcVar &m, const char *k) {
+    const NcAtt *a = nc_att(m.atts, k);
+    return a && !a->num.empty();
+  };
+  if (const NcAtt *gm = nc_att(v.atts, "grid_mapping"))
+    for (const NcVar &m : f.vars) {
+      if (m.name != std::string(gm->text.c_str())) continue;
+      const NcAtt *gn = nc_att(m.atts, "grid_mapping_name");
+      if (!gn) break;
+      std::string name(gn->text.c_str());
+      for (auto &ch : name) ch = (char)std::tolower((unsigned char)ch);
+      // the ellipsoid: earth_radius, else semi_major_axis with
+      // inverse_flattening or semi_minor_axis (a sphere without either),
+      // else WGS84
+      char ell[96];
+      bool sphere = false;
+      if (has(m, "earth_radius")) {
+        std::snprintf(ell, sizeof(ell), "+R=%.17g", num(m, "earth_radius", 0, 0));
+        sphere = true;
+      } else if (has(m, "semi_major_axis")) {
+        const double a = num(m, "semi_major_axis", 0, 0);
+        double rf = num(m, "inverse_flattening", 0, 0);
+        if (rf == 0 && has(m, "semi_minor_axis")) {
+          const double b = num(m, "semi_minor_axis", 0, a);
+          rf = a != b ? a / (a - b) : 0;
+        }
+        if (rf > 0) std::snprintf(ell, sizeof(ell), "+a=%.17g +rf=%.17g", a, rf);
+        else { std::snprintf(ell, sizeof(ell), "+R=%.17g", a); sphere = true; }
+      } else {
+        std::snprintf(ell, sizeof(ell), "+ellps=WGS84");
+      }
+      const double fe = num(m, "false_easting", 0, 0), fn = num(m, "false_northing", 0, 0);
+      char buf[384];
+      if (name == "latitude_longitude") {
+        std::snprintf(buf, sizeof(buf), "+proj=longlat %s", ell);
+        return buf;
+      }
+      if (name == "albers_conical_equal_area") {
+        const NcAtt *sp = nc_att(m.atts, "standard_parallel");
+        if (!sp || sp->num.empty()) return "?";
+        const double p1 = sp->num[0], p2 = sp->num.size() > 1 ? sp->num[1] : sp->num[0];
+        std::snprintf(buf, sizeof(buf), "+proj=aea +lat_1=%.17g +lat_2=%.17g +lat_0=%.17g +lon_0=%.17g +x_0=%.17g "
+                      "+y_0=%.17g %s", p1, p2, num(m, "latitude_of_projection_origin", 0, 0),
+                      num(m, "longitude_of_central_meridian", 0, 0), fe, fn, ell);
+        return buf;
+      }
+      if (name == "sinusoidal" && sphere) {
+        std::snprintf(buf, sizeof(buf), "+proj=sinu +lon_0=%.17g +x_0=%.17g +y_0=%.17g %s",
+                      num(m, "longitude_of_central_meridian", 0, num(m, "longitude_of_projection_origin", 0, 0)),
+                      fe, fn, ell);
+        return buf;
+      }
+      return "?";
+    }
+  const size_t nd = v.dims.size();
+  auto low = [](std::string s) { for (auto &ch : s) ch = (char)std::tolower((unsigned char)ch); return s; };
+  const std::string x = low(f.dims[v.dims[nd - 1]].first), y = low(f.dims[v.dims[nd - 2]].first);
+  if ((x == "lon" || x == "longitude" || x == "x") && (y == "lat" || y == "latitude" || y == "y") &&
+      (x != "x" || y != "y"))
+    return "EPSG:4326";
+  return "";
+}
+
+// The dataset SRS for the srs_cf open option (netcdfdataset.cpp:7023-7025,
+// 3661-3720): srs_cf=no -- the GDAL-written WKT (spatial_ref / crs_wkt) of
+// the grid mapping wins when it names an EPSG code, else the CF mapping;
+// srs_cf=yes -- the CF mapping only.
+std::string nc_srs(const Nc &f, const NcVar &v, bool srs_cf) {
+  if (!srs_cf)
+    if (const NcAtt *gm = nc_att(v.atts, "grid_mapping"))
+      for (const NcVar &m : f.vars)
+        if (m.name == std::string(gm->text.c_str()))
+          for (const char *k : {"crs_wkt", "spatial_ref"}) {
+            const NcAtt *w = nc_att(m.atts, k);
+            if (!w) continue;
+            const size_t a = w->text.rfind("AUTHORITY[\"EPSG\",\"");
+            if (a != std::string::npos) return "EPSG:" + std::to_string(std::atoi(w->text.c_str() + a + 18));
+          }
+  return nc_cf_srs(f, v);
+}
+
 int nc_fill_info(const NcRaster &r, gskyhip_raster_info *info) {
   std::memset(info, 0, sizeof(*info));
   const NcVar &v = *r.v;
@@ -1039,6 +1131,42 @@ static int netcdf_read_host_impl(const char *path, int band, void *out, int64_t 
   const int64_t need = r.nx * r.ny * nc_type_size(r.v->type);
   if (!out || out_bytes < need) return GSKYHIP_E_ARG;
   return nc_read_rows(r, band - 1, (uint8_t *)out, true) ? 0 : GSKYHIP_E_ARG;
+}
+
+namespace gsky {
+int netcdf_info_srs(const char *path, gskyhip_raster_info *info, std::string *srs_no, std::string *srs_cf) {
+  try {
+    if (!path || !info) return GSKYHIP_E_ARG;
+    NcRaster r;
+    int rc = nc_open_raster(path, r);
+    if (!rc) rc = nc_fill_info(r, info);
+    if (rc) return rc;
+    if (srs_no) *srs_no = nc_srs(r.f, *r.v, false);
+    if (srs_cf) *srs_cf = nc_srs(r.f, *r.v, true);
+    return 0;
+  } catch (...) {
+    return GSKYHIP_E_TYPE;
+  }
+}
+}  // namespace gsky
+
+static int netcdf_srs_impl(const char *path, int srs_cf, char *out, int cap) {
+  if (!path || !out || cap <= 0) return GSKYHIP_E_ARG;
+  NcRaster r;
+  const int rc = nc_open_raster(path, r);
+  if (rc) return rc;
+  const std::string srs = nc_srs(r.f, *r.v, srs_cf > 0);
+  if ((int)srs.size() >= cap) return GSKYHIP_E_ARG;
+  std::memcpy(out, srs.c_str(), srs.size() + 1);
+  return 0;
+}
+
+extern "C" int gskyhip_netcdf_srs(const char *path, int srs_cf, char *out, int cap) {
+  try {
+    return netcdf_srs_impl(path, srs_cf, out, cap);
+  } catch (...) {
+    return GSKYHIP_E_TYPE;
+  }
 }
 
 extern "C" int gskyhip_netcdf_read_host(const char *path, int band, void *out, int64_t out_bytes) {

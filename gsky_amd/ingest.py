@@ -62,6 +62,17 @@ def info(path: str) -> GeoTiffInfo:
                        [(r.ovr_xsize[k], r.ovr_ysize[k]) for k in range(r.n_ovr)])
 
 
+def netcdf_srs(path: str, srs_cf: int = 0) -> str:
+    """The dataset SRS GSKY_netCDF reports under the srs_cf open option
+    (warp.go:95): "EPSG:<n>", a PROJ string, "" (none) or "?" (a CF grid
+    mapping outside the supported projections)."""
+    buf = C.create_string_buffer(1024)
+    rc = lib().gskyhip_netcdf_srs(path.encode(), int(srs_cf), buf, len(buf))
+    if rc:
+        raise GskyError(rc, "netcdf_srs")
+    return buf.value.decode()
+
+
 def read_host(path: str, band: int = 1, level: int = 0) -> np.ndarray:
     """Band `band` (1-based) of `level` decoded on the host (no device work)."""
     inf = info(path)

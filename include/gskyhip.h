@@ -162,6 +162,13 @@ int gskyhip_register_geotiff(const char *path, int band);
  * rows returned north first); nodata from _FillValue / missing_value. */
 int gskyhip_netcdf_info(const char *path, gskyhip_raster_info *info);
 int gskyhip_netcdf_read_host(const char *path, int band, void *out, int64_t out_bytes);
+/* The dataset SRS GSKY_netCDF reports for the srs_cf open option
+ * (warp.go:95, netcdfdataset.cpp:7023-7025, 3661-3720): srs_cf = 0 -- the
+ * grid mapping's GDAL WKT (spatial_ref / crs_wkt) when it names an EPSG
+ * code, else the CF grid-mapping attributes; srs_cf = 1 -- the CF attributes
+ * only.  out: "EPSG:<n>", a PROJ string, "" (none: the warp takes WGS84) or
+ * "?" (a CF mapping outside the supported projections). */
+int gskyhip_netcdf_srs(const char *path, int srs_cf, char *out, int cap);
 int gskyhip_netcdf_read(const char *path, int band, void *dev_out, int64_t out_bytes, void *stream);
 /* Decode (path, band) into library-owned HBM and register it; what
  * warp_operation_fast does itself for an unregistered netCDF path. */

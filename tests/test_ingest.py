@@ -418,6 +418,114 @@ def test_netcdf_projected_grid_mapping(tmp_path):
     assert np.array_equal(ingest.read_host("NETCDF:%s:band" % p), data)
 
 
+def _write_albers_nc(path, data, x, y, wkt=None, cf=None):
+    """A projected netCDF grid whose grid mapping carries a GDAL WKT
+    (spatial_ref) and / or CF grid-mapping attributes."""
+    from scipy.io import netcdf_file
+    ny, nx = data.shape
+    with netcdf_file(path, "w") as f:
+        f.createDimension("y", ny)
+        f.createDimension("x", nx)
+        f.createVariable("x", "f8", ("x",))[:] = x
+        f.createVariable("y", "f8", ("y",))[:] = y
+        crs = f.createVariable("crs", "i", ())
+        if wkt:
+            crs.spatial_ref = wkt
+        for k, val in (cf or {}).items():
+            setattr(crs, k, val)
+        v = f.createVariable("band", data.dtype.char, ("y", "x"))
+        v.grid_mapping = "crs"
+        v._FillValue = data.dtype.type(-999)
+        v[:] = data
+
+
+ALBERS_CF = {"grid_mapping_name": "albers_conical_equal_area", "standard_parallel": np.array([-18.0, -36.0]),
+             "longitude_of_central_meridian": np.array([132.0]), "latitude_of_projection_origin": np.array([0.0]),
+             "false_easting": np.array([0.0]), "false_northing": np.array([0.0]),
+             "semi_major_axis": np.array([6378137.0]), "inverse_flattening": np.array([298.257222101])}
+
+
+def test_netcdf_srs_cf_option(tmp_path):
+    """srs_cf (warp.go:95 -> netcdfdataset.cpp:7023-7025, 3666): without it
+    the GDAL WKT's EPSG code wins; with it only the CF grid mapping counts.
+    No grid mapping on lon / lat axes: EPSG:4326 either way; an unsupported
+    CF mapping is "?"."""
+    data = np.zeros((4, 5), np.int16)
+    x, y = 1400012.5 + 25.0 * np.arange(5), -3800012.5 - 25.0 * np.arange(4)
+    p = str(tmp_path / "a.nc")
+    wkt = 'PROJCS["GDA94 / Australian Albers",AUTHORITY["EPSG","3577"]]'
+    cf = dict(ALBERS_CF, longitude_of_central_meridian=np.array([131.0]))
+    _write_albers_nc(p, data, x, y, wkt=wkt, cf=cf)
+    assert ingest.netcdf_srs(p, 0) == "EPSG:3577"
+    got = ingest.netcdf_srs(p, 1)
+    assert got.startswith("+proj=aea ") and "+lon_0=131 " in got and "+lat_1=-18 " in got and "+lat_2=-36 " in got
+    assert "+a=6378137 +rf=298.25722210100002" in got
+    p2 = str(tmp_path / "b.nc")
+    _write_albers_nc(p2, data, x, y, cf=cf)          # CF only: both options agree
+    assert ingest.netcdf_srs(p2, 0) == ingest.netcdf_srs(p2, 1) == got
+    p3 = str(tmp_path / "c.nc")
+    _write_albers_nc(p3, data, x, y, wkt=wkt, cf={"grid_mapping_name": "lambert_conformal_conic"})
+    assert ingest.netcdf_srs(p3, 0) == "EPSG:3577" and ingest.netcdf_srs(p3, 1) == "?"
+    p4 = str(tmp_path / "d.nc")
+    _write_albers_nc(p4, data, x, y, cf={"grid_mapping_name": "sinusoidal", "longitude_of_central_meridian": np.array([0.0]),
+                                         "earth_radius": np.array([6371007.181])})
+    s4 = ingest.netcdf_srs(p4, 1)
+    assert s4.startswith("+proj=sinu +lon_0=0 +x_0=0 +y_0=0 +R=") and float(s4.split("+R=")[1]) == 6371007.181
+    p5 = str(tmp_path / "e.nc")
+    _write_nc(p5, "v", data, np.arange(5.0), np.arange(4.0))
+    assert ingest.netcdf_srs(p5, 0) == ingest.netcdf_srs(p5, 1) == "EPSG:4326"
+
+
+@pytest.mark.gpu
+def test_gpu_netcdf_srs_cf_drop_in(tmp_path):
+    """warp_operation_fast with srsCf: the granule whose GDAL WKT says
+    EPSG:3577 but whose CF mapping has its central meridian at 131 E warps
+    as EPSG:3577 without srsCf and through the CF Albers with it -- each
+    bit-identical to the oracle with that SRS; an unsupported CF mapping is
+    an error (GSKYHIP_E_CRS), not a silent WGS84."""
+    import torch
+
+    from gsky_amd import worker
+    from gsky_amd.tiles import bbox_to_geot
+    from oracle import oracle as O
+    rng = np.random.default_rng(21)
+    ny, nx = 300, 400
+    data = rng.integers(0, 10000, (ny, nx)).astype(np.int16)
+    x = 1000012.5 + 25.0 * np.arange(nx)
+    y = -2500012.5 - 25.0 * np.arange(ny)
+    wkt = 'PROJCS["GDA94 / Australian Albers",AUTHORITY["EPSG","3577"]]'
+    p = str(tmp_path / "g.nc")
+    _write_albers_nc(p, data, x, y, wkt=wkt, cf=dict(ALBERS_CF, longitude_of_central_meridian=np.array([131.99])))
+    gt = (1000000.0, 25.0, 0.0, -2500000.0, 0.0, -25.0)
+    g = O.make_granule(data, gt, -999.0)
+    wm = O.crs("EPSG:3857")
+    x0, y0 = O.crs_transform(O.crs("EPSG:3577"), wm, 1001000.0, -2507000.0)
+    x1, y1 = O.crs_transform(O.crs("EPSG:3577"), wm, 1009000.0, -2501000.0)
+    dgt = bbox_to_geot(256, 256, (x0, y0, x1, y1))
+    worker.unregister_all()
+    outs = {}
+    for cf in (0, 1):
+        r = worker.warp_raster(worker.GeoRPCGranule(path=p, bands=[1], width=256, height=256, dstSRS="EPSG:3857",
+                                                    dstGeot=dgt, sRSCf=cf))
+        assert r.error == "OK", (cf, r.error)
+        src = O.crs(ingest.netcdf_srs(p, cf))
+        exp, ebbox, end, edt = O.warp(g, src, wm, dgt, 256, 256)
+        got = worker.raster_array(r.raster)
+        assert list(r.raster.bbox) == list(ebbox), cf
+        assert np.array_equal(got, exp), (cf, int((got != exp).sum()))
+        outs[cf] = got
+    assert not np.array_equal(outs[0], outs[1])      # the 0.01 degree meridian shift moves the picks
+    p2 = str(tmp_path / "h.nc")
+    _write_albers_nc(p2, data, x, y, wkt=wkt, cf={"grid_mapping_name": "lambert_conformal_conic"})
+    ok = worker.warp_raster(worker.GeoRPCGranule(path=p2, bands=[1], width=64, height=64, dstSRS="EPSG:3857",
+                                                 dstGeot=dgt, sRSCf=0))
+    bad = worker.warp_raster(worker.GeoRPCGranule(path=p2, bands=[1], width=64, height=64, dstSRS="EPSG:3857",
+                                                  dstGeot=dgt, sRSCf=1))
+    assert ok.error == "OK" and bad.error.startswith("warp_operation() fail: -"), (ok.error, bad.error)
+    worker.unregister_all()
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("dt,exp", [(np.int16, -32767.0), (np.int32, -2147483647.0),
                                     (np.float32, float(np.float32(9.9692099683868690e+36))),
                                     (np.float64, 9.9692099683868690e+36), (np.int8, 0.0)])

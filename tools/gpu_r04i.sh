@@ -29,7 +29,7 @@ done
 GSKYHIP_LIB=ab GSKYHIP_NN_RPW=16 timeout -k 10 200 python3 tools/ab_render.py --config c2 --reps 3 --oracle --label rpw16 >> gpurun_out/ab.jsonl
 stop $? oracle_rpw16
 cat gpurun_out/ab.jsonl
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_variants.py tests/test_gpu_graph.py tests/test_service.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_variants.py tests/test_gpu_graph.py tests/test_service.py tests/test_ingest.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/gpu_tests.log; stop $rc gpu_tests
 timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/prof_svc -o run --output-format csv -- \
   python3 bench.py --only svc --no-cpu --svc-jobs 256 > gpurun_out/prof_svc.log 2>&1
