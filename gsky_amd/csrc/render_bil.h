@@ -375,18 +375,20 @@ void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   const bool f32 = !f || atoi(f) != 0;
   const int rpw = rp ? atoi(rp) : 4;
   const int hpx = hp ? atoi(hp) : 4;
-  const char *fx = getenv("GSKYHIP_BIL_FIX");   // 0: the fp64 row code only (round 3)
-  if (fx && atoi(fx) == 0) { launch_bil_v<float, 4, 4, 8, false>(a, s); return; }
+  const char *fx = getenv("GSKYHIP_BIL_FIX");   // 1: the fixed-point LINEAR rows
+  if (fx && atoi(fx) == 1) { launch_bil_v<float, 4, 4, 8, true>(a, s); return; }
   if (f32) {
-    if (rpw == 8) launch_bil_v<float, 8, 4, 8>(a, s); else launch_bil_v<float, 4, 4, 8>(a, s);
+    if (rpw == 8) launch_bil_v<float, 8, 4, 8, false>(a, s); else launch_bil_v<float, 4, 4, 8, false>(a, s);
   } else if (hpx == 2) {
-    launch_bil_v<double, 4, 2, 8>(a, s);
+    launch_bil_v<double, 4, 2, 8, false>(a, s);
   } else {
-    if (rpw == 8) launch_bil_v<double, 8, 4, 6>(a, s); else launch_bil_v<double, 4, 4, 6>(a, s);
+    if (rpw == 8) launch_bil_v<double, 8, 4, 6, false>(a, s); else launch_bil_v<double, 4, 4, 6, false>(a, s);
   }
   return;
 #endif
-  launch_bil_v<float, 4, 4, 8>(a, s);
+  // the fp64 row code: the fixed-point LINEAR rows cut VALU but measured
+  // slower on C3 (profiles/r04b_ab_c2c3c5.jsonl: 0.93 vs 0.82 ms)
+  launch_bil_v<float, 4, 4, 8, false>(a, s);
 }
 
 }  // namespace gsky

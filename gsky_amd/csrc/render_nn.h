@@ -378,9 +378,13 @@ __device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *_
                                             const Leaf *__restrict__ pool,
                                             int ns_out, int r, int xb, int xl, int W, int ncols,
                                             typename VOf<T>::type (&c)[kNnPx]) {
+  // FIX off: in a stack the RowFix load is one more dependent latency per
+  // entry row before the row record's (C5 0.47 vs 0.435 ms with it,
+  // profiles/r04i_ab.jsonl); the fixed-point rows serve the single-entry path
 #pragma unroll 1
   for (int k = 0; k < n_entries; k++)
-    nn_entry_row<T, MASK>(a, ents, ents[ord[k]], rows, rowfix, pool, ns_out, r, xb, xl, W, ncols, c);
+    nn_entry_row<T, MASK, kNnPx, true, false>(a, ents, ents[ord[k]], rows, rowfix, pool, ns_out, r, xb, xl, W, ncols,
+                                              c);
 }
 
 // utils.Scale + palette / grey of the lane's 8 canvas values (EncodePNG's

@@ -21,7 +21,7 @@ from typing import List, Sequence, Tuple
 Job = Tuple[str, int, Sequence[float], int, int, str]
 
 
-def _client(sock: str, jobs: List[Job], start_at: float, q) -> None:
+def _client(sock: str, jobs: List[Job], ready, go, q) -> None:
     os.environ["GSKYHIP_SERVICE"] = sock
     from gsky_amd._lib import lib
     L = lib()
@@ -29,8 +29,8 @@ def _client(sock: str, jobs: List[Job], start_at: float, q) -> None:
     buf, size, nd, dt, br = C.c_void_p(), C.c_int(), C.c_double(), C.c_int(), C.c_int()
     bbox = (C.c_int * 4)()
     lat, errs, nbytes = [], 0, 0
-    while time.time() < start_at:   # all workers start together
-        time.sleep(0.001)
+    ready.put(os.getpid())
+    go.wait()                       # all workers start together, once every one has imported
     for path, band, gt, w, h, srs in jobs:
         g = (C.c_double * 6)(*gt)
         t0 = time.perf_counter()
@@ -52,18 +52,20 @@ def service_load(sock: str, jobs: Sequence[Job], n_workers: int, timeout: float 
 
     import numpy as np
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    start_at = time.time() + 2.0 + 0.05 * n_workers   # after every client has imported and connected
-    procs = [ctx.Process(target=_client, args=(sock, list(jobs[r::n_workers]), start_at, q))
+    q, ready, go = ctx.Queue(), ctx.Queue(), ctx.Event()
+    procs = [ctx.Process(target=_client, args=(sock, list(jobs[r::n_workers]), ready, go, q))
              for r in range(n_workers)]
     for p in procs:
         p.start()
+    for _ in procs:                 # every client has imported the library
+        ready.get(timeout=timeout)
+    t0 = time.perf_counter()
+    go.set()
     res = [q.get(timeout=timeout) for _ in procs]
-    end = time.time()
+    wall = time.perf_counter() - t0
     for p in procs:
         p.join(60)
     lat = np.concatenate([np.asarray(r[0], np.float64) for r in res]) * 1e3
-    wall = end - start_at
     return {"workers": n_workers, "requests": int(lat.size), "errors": int(sum(r[1] for r in res)),
             "wall_s": round(wall, 3), "requests_per_s": round(lat.size / wall, 1),
             "p50_ms": round(float(np.percentile(lat, 50)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3),

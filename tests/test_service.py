@@ -72,6 +72,27 @@ def test_service_protocol_and_batching_queue():
     assert not os.path.exists(sock)
 
 
+def test_loadgen_counts_and_timing():
+    """gsky_amd.loadgen (bench.py's service leg): every job answered once,
+    failures counted, the clock started only after every client imported
+    the library; the daemon's stats carry the batch / residence timers."""
+    from gsky_amd import WarpService
+    from gsky_amd.loadgen import service_load
+    sock = _sock_path()
+    svc = WarpService(sock, max_batch=16, window_us=500)
+    try:
+        jobs = [("/nope/%d.tif" % i, 1, [0.0, 1.0, 0.0, 0.0, 0.0, -1.0], 8, 8, "EPSG:3857") for i in range(40)]
+        s0 = svc.stats()
+        r = service_load(sock, jobs, 4)
+        s1 = svc.stats()
+        assert r["requests"] == 40 and r["errors"] == 40 and r["workers"] == 4
+        assert r["wall_s"] > 0 and r["requests_per_s"] > 0 and r["p99_ms"] >= r["p50_ms"] > 0
+        assert s1["requests"] - s0["requests"] == 40
+        assert s1["batch_s"] >= s0["batch_s"] and s1["resident_s"] > s0["resident_s"]
+    finally:
+        assert svc.shutdown() == 0
+
+
 def _spin_unknown(sock):
     os.environ["GSKYHIP_SERVICE"] = sock
     from gsky_amd import worker as W
