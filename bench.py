@@ -334,6 +334,28 @@ def run_c2(ctx: Ctx, args):
                      "kernel_ms": round(render_ms, 4), "plan_ms": round(plan_ms, 4),
                      "algorithmic_bytes_per_launch": abytes, "lib_sha16": lib_sha()},
     }
+    if ctx.rank == 0 and args.png_tiles > 0:
+        # EncodePNG's png.Encode (ogc_encoders.go:139) of rendered C2 tiles:
+        # colour type + Go's filter rows on the GPU, deflate on host threads
+        from gsky_amd.encode import encode_png
+        rgba = batch.render(sp, pal)
+        sample = [covered[k] for k in range(0, len(covered), max(1, len(covered) // args.png_tiles))][
+            : args.png_tiles]
+        sub = rgba[torch.tensor(sample, device=rgba.device)].contiguous()
+        sizes = [batch.tile_sizes[i] for i in sample]
+        threads = host_cores()
+        encode_png(sub[:2], sizes[:2], n_threads=threads)                   # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pngs = encode_png(sub, sizes, n_threads=threads)
+        pt = time.perf_counter() - t0
+        raw = sum(w * h * 4 for w, h in sizes)
+        out["png"] = {"tiles": len(sample), "threads": threads, "tiles_per_s": round(len(sample) / pt, 1),
+                      "rgba_MB_per_s": round(raw / pt / 1e6, 1), "png_bytes_mean": int(np.mean([len(b) for b in pngs])),
+                      "projected_batch_s": round(len(ids) / (len(sample) / pt), 3),
+                      "timing": "gskyhip_encode_png of %d covered C2 tiles already rendered in HBM: GPU colour-type "
+                                "+ filter pass, zlib level 6 on %d host threads, host wall" % (len(sample), threads)}
+        del sub, rgba
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
         from oracle import oracle as O
         cores = host_cores()
@@ -710,6 +732,7 @@ def main():
     ap.add_argument("--no-deciles", action="store_true", help="C4: skip the decileCount=9 line")
     ap.add_argument("--c2-lat-tiles", type=int, default=32, help="C2 p50: one-tile requests over this many tiles")
     ap.add_argument("--c2-lat-reps", type=int, default=10)
+    ap.add_argument("--png-tiles", type=int, default=256, help="C2: PNG-encode this many rendered tiles (0: skip)")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
