@@ -30,39 +30,6 @@ namespace gsky {
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-// The same with a NaN nodata allowed (the fp64 row path, round 3's code).
-template <typename WT>
-__device__ __forceinline__ void bil_fold4_any(u32x2 t0, u32x2 t1, WT rx, WT ry, int ic, int lim, float nd, float ndf,
-                                              bool nd_nan, bool hnd, float fillv, bool fill_mode, float &c) {
-  const float tv[4] = {__uint_as_float(t0.x), __uint_as_float(t0.y), __uint_as_float(t1.x), __uint_as_float(t1.y)};
-  const WT one = (WT)1.0;
-  const WT wx[2] = {rx, one - rx}, wy[2] = {ry, one - ry};
-  WT accR = (WT)0.0;
-  bool anynd = false;
-#pragma unroll
-  for (int kk = 0; kk < 4; kk++) {
-    accR += (WT)tv[kk] * (wx[kk & 1] * wy[kk >> 1]);
-    anynd = anynd | (nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
-  }
-  anynd = anynd & hnd;
-  float v = (float)accR;
-  if (anynd) {
-    WT aR = (WT)0.0, aD = (WT)0.0;
-#pragma unroll
-    for (int kk = 0; kk < 4; kk++) {
-      const WT w = wx[kk & 1] * wy[kk >> 1];
-      const bool use = !(nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
-      aD += use ? w : (WT)0.0;
-      aR += use ? (WT)tv[kk] * w : (WT)0.0;
-    }
-    v = fillv;
-    if (aD == (WT)1.0) v = (float)aR;
-    else if (aD >= (WT)0.00001) v = (float)(aR / aD);
-  }
-  const bool take = ((unsigned)ic < (unsigned)lim) & (v != nd) & (!fill_mode | (c == nd));
-  c = take ? v : c;
-}
-
 // The sample of one pixel whose 2x2 taps are all inside the band (t0: x and
 // x + 1 of the upper source row, t1 of the lower; rx / ry the weights of x
 // and y) and its fold into the canvas value c: the four weights sum to 1
@@ -308,8 +275,37 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
               t1[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, 0);
             }
 #pragma unroll
-            for (int q = 0; q < HP; q++) bil_fold4_any(t0[q], t1[q], rx[q], ry[q], ic0 + 64 * (h + q), lim, nd, ndf,
-                                                       nd_nan, hnd, fillv, fill_mode, c[h + q]);
+            for (int q = 0; q < HP; q++) {
+              const float tv[4] = {__uint_as_float(t0[q].x), __uint_as_float(t0[q].y), __uint_as_float(t1[q].x),
+                                   __uint_as_float(t1[q].y)};
+              const WT one = (WT)1.0;
+              const WT wx[2] = {rx[q], one - rx[q]}, wy[2] = {ry[q], one - ry[q]};
+              WT accR = (WT)0.0;
+              bool anynd = false;
+#pragma unroll
+              for (int kk = 0; kk < 4; kk++) {
+                accR += (WT)tv[kk] * (wx[kk & 1] * wy[kk >> 1]);
+                anynd = anynd | (nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+              }
+              anynd = anynd & hnd;
+              float v = (float)accR;
+              if (anynd) {   // drop the nodata taps and renormalise (bil_sample's rule)
+                WT aR = (WT)0.0, aD = (WT)0.0;
+#pragma unroll
+                for (int kk = 0; kk < 4; kk++) {
+                  const WT w = wx[kk & 1] * wy[kk >> 1];
+                  const bool use = !(nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+                  aD += use ? w : (WT)0.0;
+                  aR += use ? (WT)tv[kk] * w : (WT)0.0;
+                }
+                v = fillv;
+                if (aD == (WT)1.0) v = (float)aR;
+                else if (aD >= (WT)0.00001) v = (float)(aR / aD);
+              }
+              const int ic = ic0 + 64 * (h + q);
+              const bool take = ((unsigned)ic < (unsigned)lim) & (v != nd) & (!fill_mode | (c[h + q] == nd));
+              c[h + q] = take ? v : c[h + q];
+            }
           } else {   // the reference's per-tap rules (coordinates recomputed)
             uint32_t valid[HP];
             u32x2 t0[HP], t1[HP];

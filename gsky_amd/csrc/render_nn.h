@@ -118,7 +118,7 @@ __device__ __forceinline__ void nn_partial_row(__amdgpu_buffer_rsrc_t rs, double
 // nothing is folded and false sends the row to the fp64 bodies.
 // PART: the window edge falls inside the block (pixels outside the window
 // read nothing and fold nothing).
-template <typename T, int NPX, bool PART>
+template <typename T, int NPX, bool PART, bool WIDE = false>
 __device__ __forceinline__ bool nn_fix_row(__amdgpu_buffer_rsrc_t rs, int64_t fx0, int64_t fy0, int64_t fdx,
                                            int64_t fdy, int ic0, int lim, int bx, typename VOf<T>::type nd,
                                            bool fill_mode, typename VOf<T>::type (&c)[NPX]) {
@@ -150,7 +150,7 @@ __device__ __forceinline__ bool nn_fix_row(__amdgpu_buffer_rsrc_t rs, int64_t fx
   if (__builtin_amdgcn_ballot_w64(amin < 2u * kFixMargin) != 0) return false;
   V vv[NPX];
 #pragma unroll
-  for (int q = 0; q < NPX; q++) vv[q] = buf_load<T>(rs, off[q]);
+  for (int q = 0; q < NPX; q++) vv[q] = WIDE ? buf_load_w<T>(rs, off[q]) : buf_load<T>(rs, off[q]);
   if (!fill_mode) {
 #pragma unroll
     for (int q = 0; q < NPX; q++) {
@@ -414,7 +414,8 @@ __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint3
 // tiles -- keep the entry's descriptor in scalar registers for all the
 // wave's rows and fetch the next row's record while the current row is
 // gathered, so no row waits for its record.
-template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, bool STAGE = false, bool COOP = false>
+template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, bool STAGE = false, bool COOP = false,
+          bool WIDE = false>
 __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
@@ -489,7 +490,21 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int xl = xb + lane;                     // tile column of the lane's pixel 0
   uint32_t *rgba_lane = (uint32_t *)(a.rgba + (((int64_t)t * a.max_h) * a.max_w + xl) * 4);
 
-  auto rgba = [&](const V (&c)[kNnPx], uint32_t (&px)[kNnPx]) { nn_rgba<T>(sk, safe, s_tab, c, px); };
+  auto rgba = [&](const V (&c)[kNnPx], uint32_t (&px)[kNnPx]) {
+#ifdef GSKYHIP_AB
+    if (a.ab_mode == 3) {   // A/B: Scale without the palette's LDS lookup
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) px[q] = 0xFF000000u | scale_int<T, false>(sk, c[q]) * 0x10101u;
+      return;
+    }
+    if (a.ab_mode == 4) {   // A/B: neither Scale nor palette
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) px[q] = (uint32_t)c[q];
+      return;
+    }
+#endif
+    nn_rgba<T>(sk, safe, s_tab, c, px);
+  };
 
   // RGBA stores of row r
   auto store_row = [&](int r, const uint32_t *px) {
@@ -554,8 +569,11 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
       const V nd = as_v<T>(ndv);
       const bool fill_mode = e1_fill != 0;
       const int ic0 = xl - exoff;
+      // WIDE: the band's last dword whole (buf_load_w)
+      const int64_t band_bytes = (int64_t)bx * by * (int64_t)sizeof(T);
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)uniform_ptr(e1_band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
+          (void *)uniform_ptr(e1_band), (short)0, (int)(WIDE ? (band_bytes + 3) & ~(int64_t)3 : band_bytes),
+          0x00020000);
       const RowFix *fbase = rowfix + e1_row_base;
       // the row's fixed-point form, or fk = -1 outside the window / 0 none
       auto fetch = [&](int ir, int64_t (&f)[4], int &fk) {
@@ -618,9 +636,10 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         if (cfk == 1)
           done = cover ? (COOP ? nn_fix_row_coop<T, kNnPx>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode,
                                                            c, lane)
-                               : nn_fix_row<T, kNnPx, false>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
-                                                             fill_mode, c))
-                       : nn_fix_row<T, kNnPx, true>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c);
+                               : nn_fix_row<T, kNnPx, false, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
+                                                                   fill_mode, c))
+                       : nn_fix_row<T, kNnPx, true, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode,
+                                                          c);
         if (done) {
           uint32_t px[kNnPx];
           rgba(c, px);
@@ -683,10 +702,11 @@ constexpr int kNnRpw8MinItems = 32768;
 constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
 constexpr int kNnMaskRpw1Items = 16384;   // masked stacks: one row per wave below this many workgroups
 
-template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = false, bool COOP = false>
+template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = false, bool COOP = false,
+          bool WIDE = false>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE, COOP>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE, COOP, WIDE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -746,6 +766,9 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
 #ifdef GSKYHIP_AB
     if (const char *co = getenv("GSKYHIP_NN_COOP")) {
       if (one && atoi(co) != 0) { launch_nn_v<T, false, false, 8, true, false, true>(a, s); return; }
+    }
+    if (const char *wd = getenv("GSKYHIP_NN_WIDE")) {
+      if (one && atoi(wd) != 0) { launch_nn_v<T, false, false, 8, true, false, false, true>(a, s); return; }
     }
 #endif
     if (one) launch_nn_v<T, false, false, 8, true>(a, s);
