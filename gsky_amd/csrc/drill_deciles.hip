@@ -24,19 +24,23 @@
 //                         skipped by the selection
 //   decile_select_kernel  one workgroup per (polygon, band) segment: one pass
 //                         over the segment counts its non-nodata values and
-//                         finds the bits all their keys share (AND / OR), and
-//                         keeps the keys in LDS when they fit; then the
-//                         distinct ranks the picks need (<= 2 dc) on the
-//                         order-preserving 32-bit keys: one 2048-bin
-//                         histogram of the 11 bits below the shared ones,
-//                         scanned once, places every rank in its bucket; the
-//                         keys of those buckets (<= 64 each) are compacted
-//                         into LDS and each rank is the rem-th of its
-//                         bucket by a 64-lane counting compare.  Buckets
-//                         holding more keys (heavy ties, skewed data)
-//                         continue by MSD radix selection with 8-bit digits,
-//                         one LDS histogram per distinct prefix of the
-//                         pending ranks -- then the reference's picks.
+//                         finds their smallest and largest order-preserving
+//                         32-bit keys, and keeps the keys in LDS when they
+//                         fit; then the distinct ranks the picks need
+//                         (<= 2 dc): one 2048-bucket histogram of the key
+//                         range [min, max] in buckets of 2^sh consecutive
+//                         keys (>= 1024 buckets used, whatever bits the keys
+//                         share), scanned once, places every rank in its
+//                         bucket; the keys of those buckets (<= 64 each) are
+//                         compacted into LDS and each rank is the rem-th of
+//                         its bucket by a 64-lane counting select.  A rank
+//                         whose bucket holds more keys (heavy ties, skew)
+//                         continues on that bucket's key range, 11 bits
+//                         finer per pass -- then the reference's picks.
+//                         (Round 3 bucketed the 11 bits below the shared key
+//                         prefix: where a band's values straddle a binary
+//                         exponent most keys fell in a few buckets and 81 of
+//                         the 365 C4 bands took the slow radix passes.)
 // Keys order -0.0 before +0.0 where Go's sort may leave them in either order;
 // the picked values are then equal as float32 (NaN-free stacks; with NaNs the
 // reference's order is implementation-defined).
@@ -73,6 +77,7 @@ constexpr int kDecChunk = 64;        // pixels per transpose item
 constexpr int kSelLds = 36 * 1024;   // dynamic LDS of a select workgroup (histograms + key cache): 4 per CU
 constexpr int kSelU = 16;            // segment values per thread in flight (a 6k-value segment: one round)
 constexpr int kHistSlots = kBins / 256;  // radix histograms at once (the region also holds the 2048 buckets)
+constexpr bool kDecDirect = false;       // product: select from the stack directly (A/B: GSKYHIP_DEC_DIRECT)
 
 // Exclusive scan of 64-pixel chunks per polygon (one block; n_polys is modest).
 __global__ __launch_bounds__(1024) void decile_chunk_scan_kernel(const int32_t *__restrict__ count, int n_polys,
@@ -169,33 +174,47 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
 // reference indexes buf[len] and panics: len % (dc + 1) == 0 with step 1).
 // Dynamic LDS: n_slots histograms of 256 bins, then cache_keys keys (the
 // segment as it is, nodata included: no compaction, skipped on every pass).
-template <int kU>
+// DIRECT: no transposed copy -- the segment's values are gathered from the
+// time-innermost stack through the polygon's compacted pixel list, and the
+// workgroups of one polygon run back to back on one XCD (blockIdx % 8 is the
+// XCD the dispatcher picks), so the 32 bands sharing a pixel's 128-byte line
+// are read from that XCD's L2 after the first.
+template <int kU, bool DIRECT = false>
 __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float *__restrict__ vals,
                                                                     const int64_t *__restrict__ mask_off,
                                                                     const int32_t *__restrict__ count,
                                                                     const int32_t *__restrict__ totals, int n_chunk,
                                                                     int b0, int n_list, int dc, float nodata,
                                                                     int n_slots, int cache_keys, float *__restrict__ out,
-                                                                    int32_t *__restrict__ status) {
+                                                                    int32_t *__restrict__ status,
+                                                                    const float *__restrict__ stack, int t_stride,
+                                                                    const int32_t *__restrict__ pix_idx,
+                                                                    const int32_t *__restrict__ tsel, int n_seg) {
   extern __shared__ uint32_t dyn[];
-  uint32_t (*hist)[256] = (uint32_t (*)[256])dyn;
-  uint32_t *cache = dyn + n_slots * 256;
-  __shared__ uint32_t s_pref[kMaxRanks];   // rank r: its key's bits above `pos`
-  __shared__ uint32_t s_rem[kMaxRanks];    // rank r: its rank among the keys sharing that prefix
+  uint32_t *cache = dyn + n_slots * 256;   // dyn[0, 2048): the buckets, then the candidates
+  __shared__ uint32_t s_pref[kMaxRanks];   // rank r: its key, once resolved
+  __shared__ uint32_t s_rem[kMaxRanks];    // rank r: its rank within its open range / bucket
   __shared__ int32_t s_rank[kMaxRanks];    // the distinct ranks, ascending
-  __shared__ int32_t s_slot[kMaxRanks];    // rank r -> histogram slot (distinct prefix)
-  __shared__ uint32_t s_spref[kMaxRanks];  // slot -> prefix (ascending)
-  __shared__ int32_t s_bkt[kMaxRanks];    // rank r: its bucket of the first pass
+  __shared__ int32_t s_slot[kMaxRanks];    // rank r -> candidate slot (its bucket)
+  __shared__ uint32_t s_spref[kMaxRanks];  // slot -> bucket (ascending)
   __shared__ uint32_t s_bcnt[kMaxRanks];   // rank r: the keys in that bucket
   __shared__ int32_t s_soff[kMaxRanks];    // slot -> first candidate
   __shared__ uint32_t s_fill[kMaxRanks];   // slot -> candidates written
   __shared__ int8_t s_map[kBins];          // bucket -> slot, -1 when no rank needs it
   __shared__ uint32_t red[3 * kSelWaves];
   __shared__ uint32_t s_wsum[kSelWaves];
-  __shared__ int32_t s_nr, s_ns, s_fast;
+  __shared__ int32_t s_nr, s_ns, s_nsl;
+  __shared__ uint32_t s_lo[kMaxRanks], s_hi[kMaxRanks];   // rank r: its open key range
+  __shared__ int32_t s_done[kMaxRanks], s_small_r[64];
   __shared__ float s_small[64];
 
-  const int p = blockIdx.x / n_chunk, j = blockIdx.x % n_chunk;
+  int item = blockIdx.x;
+  if constexpr (DIRECT) {   // XCD x takes the contiguous item range x * per .. (x + 1) * per - 1
+    const int per = (n_seg + 7) >> 3;
+    item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (item >= n_seg) return;
+  }
+  const int p = item / n_chunk, j = item % n_chunk;
   const int64_t o = (int64_t)p * n_list + b0 + j;
   float *dst = out + o * dc;
   const int tid = threadIdx.x;
@@ -205,7 +224,10 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     return;
   }
   const int n = count[p];
-  const float *buf = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)j * n;
+  const float *buf = DIRECT ? nullptr : vals + mask_off[p] * (int64_t)n_chunk + (int64_t)j * n;
+  const int32_t *pix = DIRECT ? pix_idx + mask_off[p] : nullptr;
+  const float *bandp = DIRECT ? stack + tsel[j] : nullptr;
+  auto ld = [&](int i) -> float { return DIRECT ? bandp[(int64_t)pix[i] * t_stride] : buf[i]; };
   // pass 1: the non-nodata values (the reference's buf, drill.go:231-237):
   // their count, the bits all their keys share, and the segment's keys in
   // LDS while they fit (order is irrelevant to order statistics)
@@ -214,37 +236,39 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   const bool skip_on = nodata == nodata;
   const uint32_t kn1 = fkey(nodata), kn2 = nodata == 0.0f ? fkey(-nodata) : kn1;
   auto skipk = [&](uint32_t k) { return skip_on && (k == kn1 || k == kn2); };
-  uint32_t ka = 0xFFFFFFFFu, ko = 0u;
+  uint32_t ka = 0xFFFFFFFFu, ko = 0u;   // smallest / largest valid key
   int valid = 0;   // kU: values per thread in flight per round
   for (int i0 = 0; i0 < n; i0 += kSelThreads * kU) {
     float v[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
       const int i = i0 + u * kSelThreads + tid;
-      v[u] = i < n ? buf[i] : nodata;
+      v[u] = i < n ? ld(i) : nodata;
     }
 #pragma unroll
     for (int u = 0; u < kU; u++) {
       const int i = i0 + u * kSelThreads + tid;
       const bool keep = i < n && v[u] != nodata;
       const uint32_t k = fkey(v[u]);
-      if (keep) { ka &= k; ko |= k; valid++; }
+      if (keep) { ka = min(ka, k); ko = max(ko, k); valid++; }
       if (fits && i < n) cache[i] = k;
     }
   }
   for (int sh = 32; sh > 0; sh >>= 1) {
-    ka &= __shfl_xor(ka, sh);
-    ko |= __shfl_xor(ko, sh);
+    ka = min(ka, (uint32_t)__shfl_xor(ka, sh));
+    ko = max(ko, (uint32_t)__shfl_xor(ko, sh));
     valid += __shfl_xor(valid, sh);
   }
   if ((tid & 63) == 0) {
     red[tid >> 6] = ka; red[kSelWaves + (tid >> 6)] = ko; red[2 * kSelWaves + (tid >> 6)] = (uint32_t)valid;
   }
   __syncthreads();
-  uint32_t kand = 0xFFFFFFFFu, kor = 0u;
+  uint32_t kmn = 0xFFFFFFFFu, kmx = 0u;
   int len = 0;
 #pragma unroll
-  for (int w = 0; w < kSelWaves; w++) { kand &= red[w]; kor |= red[kSelWaves + w]; len += (int)red[2 * kSelWaves + w]; }
+  for (int w = 0; w < kSelWaves; w++) {
+    kmn = min(kmn, red[w]); kmx = max(kmx, red[kSelWaves + w]); len += (int)red[2 * kSelWaves + w];
+  }
   if (len <= 0) {   // total > 0 implies a non-nodata value; keep the slot defined anyway
     for (int i = tid; i < dc; i += kSelThreads) dst[i] = 0.f;
     if (tid == 0) status[o] = 0;
@@ -259,7 +283,7 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
           if (!skipk(cache[i])) s_small[m++] = fdecode(cache[i]);
       } else {
         for (int i = 0; i < n && m < len; i++)
-          if (buf[i] != nodata) s_small[m++] = buf[i];
+          if (ld(i) != nodata) s_small[m++] = ld(i);
       }
       for (int a = 1; a < len; a++) {
         const float v = s_small[a];
@@ -296,11 +320,6 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   }
   __syncthreads();
   const int nr = s_nr;
-  int pos = (kand == kor) ? 0 : 32 - __clz(kand ^ kor);   // bits below pos differ somewhere
-  if (tid < nr) {
-    s_pref[tid] = pos >= 32 ? 0u : (kand >> pos);
-    s_rem[tid] = (uint32_t)s_rank[tid];
-  }
   // every valid key once, from the LDS copy or streamed from the segment
   auto for_keys = [&](auto &&f) {
     if (fits) {
@@ -314,7 +333,7 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
 #pragma unroll
         for (int u = 0; u < kU; u++) {
           const int i = i0 + u * kSelThreads + tid;
-          v[u] = i < n ? buf[i] : nodata;
+          v[u] = i < n ? ld(i) : nodata;
         }
 #pragma unroll
         for (int u = 0; u < kU; u++)
@@ -323,15 +342,41 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     }
   };
   const int wv = tid >> 6, ln = tid & 63;
-  if (pos > 0) {
-    // first pass: the 11 bits below the shared ones, one histogram
-    const int bitsA = pos < kBinsLog ? pos : kBinsLog;
-    const int shA = pos - bitsA;
-    const uint32_t dmask = (1u << bitsA) - 1u;
-    uint32_t *H = dyn;
+  // Range refinement: rank r is the s_rem[r]-th key in [s_lo[r], s_hi[r]].
+  // A pass takes the ranks sharing the first open range [L, Hk], counts the
+  // keys of the range in 2048 buckets of 2^sh consecutive keys from L (at
+  // least 1024 of them used: the buckets follow the data, not a bit
+  // prefix), and gives each rank its bucket; ranks whose bucket holds <= 64
+  // keys are resolved by gathering those keys and a 64-lane counting select,
+  // the others continue on their bucket's range (one more pass per 11 bits,
+  // only under heavy ties or skew).
+  if (tid < nr) { s_lo[tid] = kmn; s_hi[tid] = kmx; s_rem[tid] = (uint32_t)s_rank[tid]; s_done[tid] = 0; }
+  __syncthreads();
+  uint32_t *H = dyn;
+  for (int guard = 0; guard < 4 * kMaxRanks; guard++) {
+    if (tid == 0) {
+      int f = -1;
+      for (int r = 0; r < nr; r++)
+        if (!s_done[r]) { f = r; break; }
+      s_ns = f;
+    }
+    __syncthreads();
+    const int f = s_ns;
+    if (f < 0) break;
+    const uint32_t L = s_lo[f], Hk = s_hi[f];
+    const bool grp = tid < nr && !s_done[tid] && s_lo[tid] == L && s_hi[tid] == Hk;   // lane r of wave 0
+    if (L == Hk) {   // one key value: every rank of the range is it
+      if (grp) { s_pref[tid] = L; s_done[tid] = 1; }
+      __syncthreads();
+      continue;
+    }
+    const uint32_t span = Hk - L;                       // W - 1, W = keys in the range
+    const int sh = max(0, 32 - __clz(span) - kBinsLog);  // bucket = (k - L) >> sh < 2048
     for (int i = tid; i < kBins; i += kSelThreads) { H[i] = 0u; s_map[i] = -1; }
     __syncthreads();
-    for_keys([&](uint32_t k) { atomicAdd(&H[(k >> shA) & dmask], 1u); });
+    for_keys([&](uint32_t k) {
+      if (k >= L && k <= Hk) atomicAdd(&H[(k - L) >> sh], 1u);
+    });
     __syncthreads();
     {   // inclusive scan of the buckets in place, 4 per thread
       const int b4 = 4 * tid;
@@ -350,20 +395,27 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
       H[b4] = ex + h0; H[b4 + 1] = ex + h0 + h1; H[b4 + 2] = ex + h0 + h1 + h2; H[b4 + 3] = ex + sum;
     }
     __syncthreads();
-    if (tid < 64) {   // wave 0, lane r < nr: the bucket of rank r (the first whose
-      // cumulative count exceeds r), then the distinct buckets (ascending with
-      // the ranks) -> slots and their candidate offsets
-      const bool act = tid < nr;
-      const uint32_t r = act ? (uint32_t)s_rank[tid] : 0u;
-      int lo = 0, hi = (int)dmask;
+    if (tid < 64) {   // wave 0, lane r of the group: its bucket, then the small
+      // buckets (ascending with the ranks) -> slots and their candidate offsets
+      const uint32_t r = grp ? s_rem[tid] : 0u;
+      int lo = 0, hi = kBins - 1;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (H[mid] > r) hi = mid; else lo = mid + 1;
       }
       const uint32_t before = lo ? H[lo - 1] : 0u;
       const uint32_t bcnt = H[lo] - before;
-      const int prev = __shfl_up(lo, 1);
-      const bool nw = act && (tid == 0 || lo != prev);
+      const bool small = grp && bcnt <= (uint32_t)kCandMax;
+      const uint64_t sm = __ballot(small);
+      // consecutive small ranks of one bucket share its slot: a rank opens a
+      // slot unless the previous small rank (same bucket) already did
+      int last_small = -1;   // the nearest small rank below this lane
+      {
+        const uint64_t below = sm & ((1ull << tid) - 1ull);
+        last_small = below ? 63 - __clzll(below) : -1;
+      }
+      const int last_b = __shfl(small ? lo : -1, last_small < 0 ? 0 : last_small);
+      const bool nw = small && (last_small < 0 || last_b != lo);
       const uint64_t nb = __ballot(nw);
       const int slot = __popcll(nb & ((2ull << tid) - 1ull)) - 1;
       uint32_t incl = nw ? bcnt : 0u;   // candidate offsets: exclusive scan over the new slots
@@ -371,41 +423,56 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
         const uint32_t up = __shfl_up(incl, o);
         if (tid >= o) incl += up;
       }
-      const bool big = __ballot(act && bcnt > (uint32_t)kCandMax) != 0ull;
-      if (act) {
-        s_bkt[tid] = lo;
+      if (small) {
         s_rem[tid] = r - before;
         s_bcnt[tid] = bcnt;
         s_slot[tid] = slot;
+      } else if (grp) {   // continue on the bucket's key range
+        const uint32_t blo = L + ((uint32_t)lo << sh);
+        const uint32_t bhi = (sh >= 32 || ((uint64_t)(lo + 1) << sh) - 1u >= (uint64_t)span)
+                                 ? Hk : L + (uint32_t)(((uint64_t)(lo + 1) << sh) - 1u);
+        s_lo[tid] = blo;
+        s_hi[tid] = bhi;
+        s_rem[tid] = r - before;
       }
       if (nw) {
         s_spref[slot] = (uint32_t)lo;
         s_soff[slot] = (int)(incl - bcnt);
       }
-      if (tid == 0) { s_ns = __popcll(nb); s_fast = big ? 0 : 1; }
+      if (tid == 0) s_nsl = __popcll(nb);
+      s_small_r[tid] = small ? 1 : 0;
     }
     __syncthreads();
-    if (s_fast) {
-      // the keys of the needed buckets, compacted per slot over the histogram
-      if (tid < s_ns) { s_map[s_spref[tid]] = (int8_t)tid; s_fill[tid] = 0u; }
+    const int nsl = s_nsl;
+    if (nsl > 0) {
+      if (tid < nsl) { s_map[s_spref[tid]] = (int8_t)tid; s_fill[tid] = 0u; }
       __syncthreads();
-      uint32_t *cand = dyn;
+      uint32_t *cand = dyn;   // the bucket counts are no longer needed
       for_keys([&](uint32_t k) {
-        const int sl = s_map[(k >> shA) & dmask];
-        if (sl >= 0) cand[s_soff[sl] + atomicAdd(&s_fill[sl], 1u)] = k;
+        if (k >= L && k <= Hk) {
+          const int sl = s_map[(k - L) >> sh];
+          if (sl >= 0) cand[s_soff[sl] + atomicAdd(&s_fill[sl], 1u)] = k;
+        }
       });
       __syncthreads();
       // rank r is the s_rem[r]-th key of its bucket (<= 64 keys, one per
-      // lane): MSB-first selection over the bits below the bucket digit with
-      // wave ballots -- lanes whose bit is 0 come first; equal keys end in
-      // the same candidate set, any of them is the value
+      // lane): MSB-first selection with wave ballots over the bits where the
+      // candidates differ -- lanes whose bit is 0 come first; equal keys end
+      // in the same candidate set, any of them is the value
       for (int r = wv; r < nr; r += kSelWaves) {
+        if (!s_small_r[r]) continue;
         const int cnt = (int)s_bcnt[r];
         const uint32_t *c = cand + s_soff[s_slot[r]];
-        const uint32_t ki = ln < cnt ? c[ln] : 0xFFFFFFFFu;
-        uint64_t live = __ballot(ln < cnt);
+        const bool in = ln < cnt;
+        const uint32_t ki = in ? c[ln] : 0u;
+        uint32_t a = in ? ki : 0xFFFFFFFFu, o = in ? ki : 0u;
+        for (int sft = 32; sft > 0; sft >>= 1) {
+          a &= (uint32_t)__shfl_xor(a, sft);
+          o |= (uint32_t)__shfl_xor(o, sft);
+        }
+        uint64_t live = __ballot(in);
         uint32_t rem = s_rem[r];
-        for (int b = shA - 1; b >= 0; b--) {
+        for (int b = (a == o) ? -1 : 31 - __clz(a ^ o); b >= 0; b--) {
           const uint64_t zero = __ballot(((ki >> b) & 1u) == 0u) & live;
           const uint32_t nz = (uint32_t)__popcll(zero);
           if (rem < nz) live = zero;
@@ -413,73 +480,10 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
         }
         const int src = __ffsll((unsigned long long)live) - 1;
         const uint32_t key = __shfl(ki, src);
-        if (ln == 0) s_pref[r] = key;
-      }
-      __syncthreads();
-      pos = 0;
-    } else {   // continue below the bucket digit by radix selection
-      if (tid < nr) s_pref[tid] = ((pos >= 32 ? 0u : (kand >> pos)) << bitsA) | (uint32_t)s_bkt[tid];
-      pos = shA;
-    }
-  }
-  __syncthreads();
-  while (pos > 0) {
-    const int d = pos < 8 ? pos : 8;
-    const int shift = pos - d;
-    if (tid == 0) {   // slots: the distinct prefixes of the ranks (ascending with the ranks)
-      int ns = 0;
-      for (int r = 0; r < nr; r++) {
-        if (ns == 0 || s_spref[ns - 1] != s_pref[r]) s_spref[ns++] = s_pref[r];
-        s_slot[r] = ns - 1;
-      }
-      s_ns = ns;
-    }
-    __syncthreads();
-    const int ns = s_ns;
-    // kHistSlots prefixes per pass over the keys
-    for (int g0 = 0; g0 < ns; g0 += kHistSlots) {
-      const int g1 = min(ns, g0 + kHistSlots);
-      for (int i = tid; i < (g1 - g0) * 256; i += kSelThreads) hist[i >> 8][i & 255] = 0u;
-      __syncthreads();
-      auto bin = [&](uint32_t k) {
-        const uint32_t hi = pos >= 32 ? 0u : (k >> pos);
-        int lo = 0, hi_s = ns - 1;   // binary search of the slot with prefix hi
-        while (lo < hi_s) {
-          const int mid = (lo + hi_s) >> 1;
-          if (s_spref[mid] < hi) lo = mid + 1; else hi_s = mid;
-        }
-        if (s_spref[lo] == hi && lo >= g0 && lo < g1) atomicAdd(&hist[lo - g0][(k >> shift) & ((1u << d) - 1u)], 1u);
-      };
-      for_keys(bin);
-      __syncthreads();
-      // the digit bucket holding each rank: a wave per rank, lane l sums bins
-      // 4l..4l+3, an inclusive scan over the lanes finds the lane whose range
-      // holds the rank, that lane walks its 4 bins (bins >= 2^d are empty)
-      for (int r = wv; r < nr; r += kSelWaves) {
-        if (s_slot[r] < g0 || s_slot[r] >= g1) continue;
-        const uint32_t *h = hist[s_slot[r] - g0];
-        const uint32_t rem = s_rem[r];
-        const uint32_t b0 = h[4 * ln], b1 = h[4 * ln + 1], b2 = h[4 * ln + 2], b3 = h[4 * ln + 3];
-        const uint32_t sum = b0 + b1 + b2 + b3;
-        uint32_t incl = sum;
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t up = __shfl_up(incl, o);
-          if (ln >= o) incl += up;
-        }
-        const uint32_t excl = incl - sum;
-        if (excl <= rem && rem < incl) {   // exactly one lane (the counts of the slot exceed rem)
-          uint32_t cum = excl;
-          int dg = 4 * ln;
-          if (cum + b0 <= rem) { cum += b0; dg++;
-            if (cum + b1 <= rem) { cum += b1; dg++;
-              if (cum + b2 <= rem) { cum += b2; dg++; } } }
-          s_pref[r] = (s_pref[r] << d) | (uint32_t)dg;
-          s_rem[r] = rem - cum;
-        }
+        if (ln == 0) { s_pref[r] = key; s_done[r] = 1; }
       }
       __syncthreads();
     }
-    pos = shift;
   }
   // s_pref[r] is now the key of order statistic s_rank[r]
   if (tid < dc) {
@@ -552,6 +556,23 @@ int launch_drill_deciles(const DecileCall &c) {
 #endif
   const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
   const size_t dyn_lds = (size_t)sel_lds;
+  bool direct = kDecDirect;
+#ifdef GSKYHIP_AB
+  if (const char *e = getenv("GSKYHIP_DEC_DIRECT")) direct = atoi(e) != 0;
+#endif
+  if (direct) {   // no transposed copy: a launch per band chunk straight from the stack
+    for (int b0 = 0; b0 < n_list; b0 += c.band_chunk) {
+      const int n_chunk = std::min(c.band_chunk, n_list - b0);
+      const int n_seg = c.n_polys * n_chunk;
+      if (hipMemcpyAsync(w.tsel, sel.data() + b0, sizeof(int32_t) * n_chunk, hipMemcpyHostToDevice, s) != hipSuccess)
+        return GSKYHIP_E_HIP;
+      const unsigned grid = (unsigned)(((int64_t)n_seg + 7) / 8 * 8);
+      hipLaunchKernelGGL((decile_select_kernel<kSelU, true>), dim3(grid), dim3(kSelThreads), dyn_lds, s, w.vals,
+                         c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
+                         cache_keys, c.out, c.status, c.stack, c.t_stride, w.idx, w.tsel, n_seg);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+  }
   for (int b0 = 0; b0 < n_list; b0 += c.band_chunk) {
     const int n_chunk = std::min(c.band_chunk, n_list - b0);
     const int n_groups = (n_chunk + kTrBands - 1) / kTrBands;
@@ -565,11 +586,11 @@ int launch_drill_deciles(const DecileCall &c) {
     if (sel_u == 8)
       hipLaunchKernelGGL(decile_select_kernel<8>, dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
                          c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status);
+                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
     else
       hipLaunchKernelGGL(decile_select_kernel<kSelU>, dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
                          c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status);
+                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
   }
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
