@@ -39,16 +39,20 @@
 // does), not to a running GDAL (absent here).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include "../../include/gskyhip.h"
 #include "gsky_device.h"
@@ -541,17 +545,22 @@ DescribeCtx make_ctx(const gskyhip_crs *crs, const double gt[6], int xsize, int 
   return c;
 }
 
-// getDrillFileDescriptor (drill.go:363-423) up to the mask's pixel rings.
-Descriptor describe(const char *geometry, const DescribeCtx &c) {
-  Descriptor d;
-  Rings r;
-  if (!parse_geometry(geometry, r)) { d.status = GSKYHIP_E_ARG; return d; }
+// getDrillFileDescriptor (drill.go:363-423) up to the mask's pixel rings,
+// into `d` (its ring vectors keep their capacity from earlier calls).
+void describe(const char *geometry, const DescribeCtx &c, Descriptor &d) {
+  d.status = 0;
+  for (int k = 0; k < 4; k++) d.win[k] = 0;
+  Rings &r = d.pix;
+  r.x.clear();
+  r.y.clear();
+  r.part.clear();
+  if (!parse_geometry(geometry, r)) { d.status = GSKYHIP_E_ARG; return; }
   if (c.reproject)   // WGS84 lon/lat -> dataset SRS, the warp's transform
     for (size_t i = 0; i < r.x.size(); i++) {
       double lam, phi, X, Y;
       if (!crs_inverse(c.wgs, r.x[i], r.y[i], lam, phi) || !crs_forward(*c.crs, lam, phi, X, Y)) {
         d.status = GSKYHIP_E_CRS;
-        return d;
+        return;
       }
       r.x[i] = X;
       r.y[i] = Y;
@@ -559,7 +568,7 @@ Descriptor describe(const char *geometry, const DescribeCtx &c) {
   double env[4];
   if (!clip_envelope(r, c.box[0], c.box[1], c.box[2], c.box[3], env)) {
     d.status = GSKYHIP_E_RANGE;   // the polygon misses the file
-    return d;
+    return;
   }
   const double *igt = c.igt;
   const double omx = igt[0] + env[0] * igt[1] + env[1] * igt[2], omy = igt[3] + env[0] * igt[4] + env[1] * igt[5];
@@ -571,7 +580,7 @@ Descriptor describe(const char *geometry, const DescribeCtx &c) {
   if (offX < 0) offX = 0;
   if (offY < 0) offY = 0;
   d.win[0] = offX; d.win[1] = offY; d.win[2] = cX; d.win[3] = cY;
-  if (cX <= 0 || cY <= 0) { d.status = GSKYHIP_E_RANGE; return d; }
+  if (cX <= 0 || cY <= 0) { d.status = GSKYHIP_E_RANGE; return; }
   // createMask (drill.go:294-308): the MEM raster's geotransform is the
   // dataset's shifted by the window offset (rotation terms kept as they are)
   double mgt[6], migt[6];
@@ -579,42 +588,117 @@ Descriptor describe(const char *geometry, const DescribeCtx &c) {
   mgt[0] += mgt[1] * (double)offX;
   mgt[3] += mgt[5] * (double)offY;
   inv_geot(mgt, migt);
-  d.pix = std::move(r);
-  for (size_t i = 0; i < d.pix.x.size(); i++) {
-    const double X = d.pix.x[i], Y = d.pix.y[i];
-    d.pix.x[i] = migt[0] + X * migt[1] + Y * migt[2];
-    d.pix.y[i] = migt[3] + X * migt[4] + Y * migt[5];
+  for (size_t i = 0; i < r.x.size(); i++) {
+    const double X = r.x[i], Y = r.y[i];
+    r.x[i] = migt[0] + X * migt[1] + Y * migt[2];
+    r.y[i] = migt[3] + X * migt[4] + Y * migt[5];
   }
-  return d;
 }
 
-// describe() of every polygon on up to 16 host threads (polygons are
-// independent; the reference describes one per gRPC call, drill_grpc.go:127-158).
-void describe_all(const char *const *geometries, int n, const DescribeCtx &c, std::vector<Descriptor> &out) {
-  out.assign((size_t)std::max(0, n), Descriptor());
-  static const unsigned cap = [] {   // GSKYHIP_DRILL_THREADS: at most this many (default 16)
+// A persistent pool of host threads for describe_all: created once (again
+// in a forked child, whose copy has no threads), woken per call through a
+// generation counter; the caller works too and waits until every worker has
+// left the job.  Thread creation per call cost 300 us of a 0.5 ms describe
+// (16 threads, r04r); a wake costs a few microseconds.
+struct DescribePool {
+  std::mutex mu;
+  std::condition_variable cv_go, cv_done;
+  uint64_t gen = 0;
+  int busy = 0;                       // workers inside the current job
+  int n_workers = 0;
+  pid_t pid = 0;
+  std::function<void()> job;
+  std::mutex call_mu;                 // one describe_all at a time (the storage below is shared)
+  std::vector<Descriptor> store;      // descriptors of the last call, capacity kept
+
+  void worker(uint64_t seen) {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_go.wait(lk, [&] { return gen != seen; });
+        seen = gen;
+        f = job;
+      }
+      if (f) f();
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (--busy == 0) cv_done.notify_all();
+      }
+    }
+  }
+  // run f on the caller and up to `want` workers; returns once all are done
+  void run(int want, const std::function<void()> &f) {
+    if (pid != getpid()) {   // first use, or a forked child: (re)start the workers
+      pid = getpid();
+      n_workers = 0;
+    }
+    while (n_workers < want) {
+      uint64_t g;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        g = gen;
+      }
+      std::thread(&DescribePool::worker, this, g).detach();
+      n_workers++;
+    }
+    if (n_workers == 0) { f(); return; }
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      job = f;
+      busy = n_workers;
+      gen++;
+    }
+    cv_go.notify_all();
+    f();
+    std::unique_lock<std::mutex> lk(mu);
+    cv_done.wait(lk, [&] { return busy == 0; });
+    job = nullptr;
+  }
+};
+DescribePool &describe_pool() {
+  static DescribePool *p = new DescribePool();   // never destroyed: its threads are detached
+  return *p;
+}
+
+// describe() of every polygon on the pool (polygons are independent; the
+// reference describes one per gRPC call, drill_grpc.go:127-158).  The result
+// lives in the pool's storage; the caller holds `lk` (DescribePool::call_mu)
+// while it uses it.
+std::vector<Descriptor> &describe_all(const char *const *geometries, int n, const DescribeCtx &c,
+                                      std::unique_lock<std::mutex> &lk) {
+  DescribePool &P = describe_pool();
+  lk = std::unique_lock<std::mutex>(P.call_mu);
+  std::vector<Descriptor> &out = P.store;
+  if ((int)out.size() < n) out.resize((size_t)n);
+  static const int cap = [] {   // GSKYHIP_DRILL_THREADS: at most this many (default 16)
     const char *e = std::getenv("GSKYHIP_DRILL_THREADS");
     const int v = e ? std::atoi(e) : 16;
-    return (unsigned)std::max(1, std::min(64, v));
+    return std::max(1, std::min(64, v));
   }();
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const int nth = (int)std::min<unsigned>(std::min(cap, hw), (unsigned)std::max(1, n / 16));
+  const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+  const int nth = std::min(std::min(cap, hw), std::max(1, n / 32));
   std::atomic<int> next(0);
   auto work = [&]() {
     for (int i = next.fetch_add(8); i < n; i = next.fetch_add(8))
       for (int k = i; k < std::min(n, i + 8); k++) {
         try {
-          out[k] = describe(geometries[k], c);
+          describe(geometries[k], c, out[k]);
         } catch (...) {   // bad_alloc of a huge ring: that polygon fails, not the process
-          out[k] = Descriptor();
+          out[k].pix = Rings();
           out[k].status = GSKYHIP_E_ARG;
         }
       }
   };
-  std::vector<std::thread> th;
-  for (int t = 1; t < nth; t++) th.emplace_back(work);
-  work();
-  for (auto &t : th) t.join();
+  static const bool trace = std::getenv("GSKYHIP_DRILL_TRACE") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  P.run(nth - 1, work);
+  if (trace) {
+    const auto t1 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "describe_all n=%d threads=%d us=%.1f\n", n, nth,
+                 std::chrono::duration<double, std::micro>(t1 - t0).count());
+  }
+  return out;
 }
 
 // ---------------------------------------------------------------- GPU rasterizer
@@ -698,9 +782,10 @@ Staging &staging() {
 
 // Windows, mask offsets and statuses of described polygons (16-byte aligned
 // mask regions in polygon order); returns the mask buffer size.
-int64_t layout(const std::vector<Descriptor> &ds, int32_t *win_out, int64_t *mask_off_out, int32_t *status_out) {
+int64_t layout(const std::vector<Descriptor> &ds, int n, int32_t *win_out, int64_t *mask_off_out,
+               int32_t *status_out) {
   int64_t off = 0;
-  for (size_t i = 0; i < ds.size(); i++) {
+  for (size_t i = 0; i < (size_t)n; i++) {
     const Descriptor &d = ds[i];
     status_out[i] = d.status;
     const int64_t bytes = d.status == 0 ? (int64_t)d.win[2] * d.win[3] : 0;
@@ -713,17 +798,19 @@ int64_t layout(const std::vector<Descriptor> &ds, int32_t *win_out, int64_t *mas
 
 // ALL_TOUCHED masks of described polygons rasterized on the GPU into
 // masks_dev (zeroed first), on `s`.
-int rasterize_device(const std::vector<Descriptor> &ds, const int64_t *mask_off, uint8_t *masks_dev,
+int rasterize_device(const std::vector<Descriptor> &ds, int n, const int64_t *mask_off, uint8_t *masks_dev,
                      int64_t mask_bytes, hipStream_t s) {
   if (hipMemsetAsync(masks_dev, 0, (size_t)mask_bytes, s) != hipSuccess) return GSKYHIP_E_HIP;
   std::vector<PolyDev> polys;
   size_t nv = 0, npart = 0;
-  for (const Descriptor &d : ds)
+  for (int di = 0; di < n; di++) {
+    const Descriptor &d = ds[di];
     if (d.status == 0 && !d.pix.x.empty()) { nv += d.pix.x.size(); npart += d.pix.part.size(); }
-  polys.reserve(ds.size());
+  }
+  polys.reserve((size_t)n);
   int64_t words = 0;
   int32_t v0 = 0, p0 = 0;
-  for (size_t i = 0; i < ds.size(); i++) {
+  for (size_t i = 0; i < (size_t)n; i++) {
     const Descriptor &d = ds[i];
     if (d.status != 0 || d.pix.x.empty() || (int64_t)d.win[2] * d.win[3] <= 0) continue;
     PolyDev P;
@@ -768,7 +855,8 @@ int rasterize_device(const std::vector<Descriptor> &ds, const int64_t *mask_off,
   std::memcpy(h, polys.data(), polys.size() * sizeof(PolyDev));
   double *hx = (double *)(h + b0), *hy = (double *)(h + b0 + b1);
   int32_t *hp = (int32_t *)(h + b0 + 2 * b1);
-  for (const Descriptor &d : ds) {
+  for (int di = 0; di < n; di++) {
+    const Descriptor &d = ds[di];
     if (d.status != 0 || d.pix.x.empty() || (int64_t)d.win[2] * d.win[3] <= 0) continue;
     std::memcpy(hx, d.pix.x.data(), d.pix.x.size() * 8); hx += d.pix.x.size();
     std::memcpy(hy, d.pix.y.data(), d.pix.y.size() * 8); hy += d.pix.y.size();
@@ -833,11 +921,11 @@ extern "C" int gskyhip_drill_descriptors_device(const char *const *geometries, i
     gskyhip_crs crs;
     const gskyhip_crs *pc;
     if (ctx_of(dataset_srs, crs, pc)) return GSKYHIP_E_CRS;
-    std::vector<Descriptor> ds;
-    describe_all(geometries, n, make_ctx(pc, geot, xsize, ysize), ds);
-    *mask_bytes_out = layout(ds, win_out, mask_off_out, status_out);
+    std::unique_lock<std::mutex> lk;
+    std::vector<Descriptor> &ds = describe_all(geometries, n, make_ctx(pc, geot, xsize, ysize), lk);
+    *mask_bytes_out = layout(ds, n, win_out, mask_off_out, status_out);
     if (!masks_dev) return 0;
-    return rasterize_device(ds, mask_off_out, masks_dev, *mask_bytes_out, (hipStream_t)stream);
+    return rasterize_device(ds, n, mask_off_out, masks_dev, *mask_bytes_out, (hipStream_t)stream);
   } catch (...) {
     return GSKYHIP_E_ARG;
   }
@@ -856,13 +944,13 @@ extern "C" int gskyhip_drill_masks_device(const char *const *geometries, int n, 
     gskyhip_crs crs;
     const gskyhip_crs *pc;
     if (ctx_of(dataset_srs, crs, pc)) return GSKYHIP_E_CRS;
-    std::vector<Descriptor> ds;
-    describe_all(geometries, n, make_ctx(pc, geot, xsize, ysize), ds);
-    *mask_bytes_out = layout(ds, win_out, mask_off_out, status_out);
+    std::unique_lock<std::mutex> lk;
+    std::vector<Descriptor> &ds = describe_all(geometries, n, make_ctx(pc, geot, xsize, ysize), lk);
+    *mask_bytes_out = layout(ds, n, win_out, mask_off_out, status_out);
     uint8_t *m = (uint8_t *)alloc(alloc_ctx, *mask_bytes_out);
     *masks_dev_out = m;
     if (!m) return GSKYHIP_E_HIP;
-    return rasterize_device(ds, mask_off_out, m, *mask_bytes_out, (hipStream_t)stream);
+    return rasterize_device(ds, n, mask_off_out, m, *mask_bytes_out, (hipStream_t)stream);
   } catch (...) {
     return GSKYHIP_E_ARG;
   }
@@ -877,9 +965,9 @@ extern "C" int gskyhip_drill_descriptors(const char *const *geometries, int n, c
     gskyhip_crs crs;
     const gskyhip_crs *pc;
     if (ctx_of(dataset_srs, crs, pc)) return GSKYHIP_E_CRS;
-    std::vector<Descriptor> ds;
-    describe_all(geometries, n, make_ctx(pc, geot, xsize, ysize), ds);
-    *mask_bytes_out = layout(ds, win_out, mask_off_out, status_out);
+    std::unique_lock<std::mutex> lk;
+    std::vector<Descriptor> &ds = describe_all(geometries, n, make_ctx(pc, geot, xsize, ysize), lk);
+    *mask_bytes_out = layout(ds, n, win_out, mask_off_out, status_out);
     if (masks_out)
       for (int i = 0; i < n; i++) {
         const Descriptor &d = ds[i];

@@ -180,6 +180,7 @@ def drill_dataset(geometries: Sequence[str], dataset_srs: Optional[str], geot: S
 
 _ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int64)
 
+
 REFERENCE_ORDER, WAVE_SPLIT = 0, 1
 
 

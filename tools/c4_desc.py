@@ -47,7 +47,21 @@ def main():
         drill.drill_dataset(geoms, "EPSG:4326", gt, size, size, dev)
         torch.cuda.synchronize()
     whole()
+    from gsky_amd._lib import lib
+    arr = marshal()
+    gta = (C.c_double * 6)(*gt)
+    n = len(geoms)
+    win = np.zeros((n, 4), np.int32)
+    off = np.zeros(n, np.int64)
+    st = np.zeros(n, np.int32)
+    total = C.c_int64()
+
+    def c_call():   # the host describe alone, strings already marshalled
+        lib().gskyhip_drill_descriptors_device(arr, n, b"EPSG:4326", gta, size, size,
+                                               win.ctypes.data_as(C.c_void_p), off.ctypes.data_as(C.c_void_p),
+                                               C.byref(total), None, st.ctypes.data_as(C.c_void_p), None)
     out = {"label": args.label, "threads_env": os.environ.get("GSKYHIP_DRILL_THREADS", "16"),
+           "c_call_ms": med(c_call, args.reps),
            "polygons": len(geoms), "geojson_bytes": sum(len(g) for g in geoms),
            "marshal_ms": med(marshal, args.reps),
            "windows_ms": med(lambda: drill.drill_windows(geoms, "EPSG:4326", gt, size, size), args.reps),

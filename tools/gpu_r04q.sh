@@ -13,3 +13,8 @@ for kb in 36 20 12; do
 import json; d=json.load(open('gpurun_out/c4_$kb.json')); c=d.get('configs',{}).get('C4',d)
 print('lds_kb=$kb', c['deciles']['ms_per_step'], c['deciles']['roofline']['kernel_ms'])"
 done
+for th in 16 1; do
+  GSKYHIP_DRILL_THREADS=$th timeout -k 10 200 python3 tools/c4_desc.py --label "th$th" >> gpurun_out/c4_desc.jsonl
+  stop $? c4_desc_$th
+done
+cat gpurun_out/c4_desc.jsonl
