@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -146,6 +147,268 @@ __global__ __launch_bounds__(256) void png_filter_kernel(const uint8_t *__restri
   }
 }
 
+// ------------------------------------------------------------------ GPU deflate
+// The zlib stream of each tile's filtered rows built on the GPU: one final
+// block of fixed Huffman codes (RFC 1951 3.2.6) whose LZ77 matches are
+// searched at the distances a PNG row offers -- 1 (runs), the pixel size
+// (the pixel to the left) and the row stride (the pixel above) -- greedily,
+// longest first, within the row (so rows are encoded independently: a
+// workgroup per tile, a thread per row, matches may reach back into earlier
+// rows).  Pass 1 counts each row's bits; their prefix sums place every row
+// in the tile's bit stream and every tile in one packed buffer (so only the
+// compressed bytes cross PCIe); pass 2 writes the codes (the words two rows
+// share by OR).  Adler-32 from per-row sums.  The stream is valid DEFLATE /
+// zlib; its bytes are neither zlib's nor Go's compress/flate (parity
+// unpinned; the tests inflate it and compare the rows).
+__constant__ uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59,
+                                      67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t kDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769,
+                                       1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10,
+                                       11, 11, 12, 12, 13, 13};
+
+constexpr int kPngMaxRows = 4096;    // rows of a tile the deflate kernels handle (LDS scan)
+
+struct BitSink {   // LSB-first bit writer over 32-bit words; first and last words by OR
+  uint32_t *out;
+  uint64_t acc;
+  int nacc;
+  int64_t word;
+  bool first;
+  __device__ void init(uint32_t *o, int64_t bitpos) {
+    out = o; word = bitpos >> 5; nacc = (int)(bitpos & 31); acc = 0; first = true;
+  }
+  __device__ __forceinline__ void put(uint32_t bits, int n) {
+    acc |= (uint64_t)bits << nacc;
+    nacc += n;
+    if (nacc >= 32) {
+      if (first) { atomicOr(out + word, (uint32_t)acc); first = false; }
+      else out[word] = (uint32_t)acc;
+      acc >>= 32;
+      nacc -= 32;
+      word++;
+    }
+  }
+  __device__ void finish() {
+    if (nacc > 0) atomicOr(out + word, (uint32_t)acc);
+  }
+};
+
+__device__ __forceinline__ uint32_t rev_bits(uint32_t code, int len) { return __brev(code) >> (32 - len); }
+
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t *p) { return *(const u32_unaligned *)p; }
+
+// fixed Huffman code of a literal / length symbol, bit-reversed for LSB-first output
+__device__ __forceinline__ void lit_code(int v, uint32_t &code, int &len) {
+  if (v < 144) { code = 0x30 + v; len = 8; }
+  else if (v < 256) { code = 0x190 + (v - 144); len = 9; }
+  else if (v < 280) { code = v - 256; len = 7; }
+  else { code = 0xC0 + (v - 280); len = 8; }
+  code = rev_bits(code, len);
+}
+
+// One row's tokens: bits returned; WRITE emits them into `bs`.
+template <bool WRITE>
+__device__ uint32_t deflate_row(const uint8_t *__restrict__ data, int64_t p0, int64_t p1, int bpp, int stride,
+                                BitSink &bs) {
+  uint32_t bits = 0;
+  int64_t p = p0;
+  while (p < p1) {
+    int best = 0, bd = 0;
+    const int dists[3] = {1, bpp, stride};
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const int d = dists[c];
+      if (p - d < 0 || d > 32768) continue;
+      int l = 0;
+      const int lim = (int)min((int64_t)258, p1 - p);
+      // 4 bytes per compare (unaligned dword loads), the first difference by ctz
+      while (l + 4 <= lim) {
+        const uint32_t x = ld_u32(data + p + l) ^ ld_u32(data + p + l - d);
+        if (x) { l += __builtin_ctz(x) >> 3; goto done; }
+        l += 4;
+      }
+      while (l < lim && data[p + l] == data[p + l - d]) l++;
+    done:
+      if (l > best) { best = l; bd = d; }
+    }
+    if (best >= 3) {
+      int lc = 0;
+      while (lc < 28 && kLenBase[lc + 1] <= best) lc++;
+      int dc = 0;
+      while (dc < 29 && kDistBase[dc + 1] <= bd) dc++;
+      uint32_t code;
+      int len;
+      lit_code(257 + lc, code, len);
+      const int le = kLenExtra[lc], de = kDistExtra[dc];
+      bits += len + le + 5 + de;
+      if (WRITE) {
+        bs.put(code, len);
+        if (le) bs.put((uint32_t)(best - kLenBase[lc]), le);
+        bs.put(rev_bits((uint32_t)dc, 5), 5);
+        if (de) bs.put((uint32_t)(bd - kDistBase[dc]), de);
+      }
+      p += best;
+    } else {
+      uint32_t code;
+      int len;
+      lit_code(data[p], code, len);
+      bits += len;
+      if (WRITE) bs.put(code, len);
+      p++;
+    }
+  }
+  return bits;
+}
+
+// Pass 1: per row its bits and Adler-32 sums; per tile the stream length.
+// Tile stream: zlib header (2 B), block header (3 bits), rows, end of block
+// (7 bits), pad to a byte, Adler-32 (4 B).
+__global__ __launch_bounds__(256) void png_deflate_count_kernel(const uint8_t *__restrict__ filt,
+                                                                const int64_t *__restrict__ off,
+                                                                const int32_t *__restrict__ wh,
+                                                                const int32_t *__restrict__ opaque, int max_h,
+                                                                int32_t *__restrict__ row_bits,
+                                                                uint32_t *__restrict__ adler,
+                                                                int64_t *__restrict__ zlen) {
+  const int t = blockIdx.x;
+  const int w = wh[2 * t], h = wh[2 * t + 1];
+  const int bpp = opaque[t] ? 3 : 4;
+  const int stride = 1 + bpp * w;
+  const uint8_t *data = filt + off[t];
+  __shared__ uint32_t s_a[kPngMaxRows], s_b[kPngMaxRows];
+  __shared__ int64_t s_bits[256];
+  int64_t mine = 0;
+  BitSink dummy;
+  for (int y = threadIdx.x; y < h; y += blockDim.x) {
+    const int64_t p0 = (int64_t)y * stride;
+    const uint32_t b = deflate_row<false>(data, p0, p0 + stride, bpp, stride, dummy);
+    row_bits[(int64_t)t * max_h + y] = (int32_t)b;
+    mine += b;
+    uint64_t a = 0, bb = 0;   // sum of bytes, sum of (n - i) * byte (exact: < 2^40), then mod 65521
+    int i = 0;
+    for (; i + 4 <= stride; i += 4) {
+      const uint32_t v = ld_u32(data + p0 + i);
+      const uint32_t c0 = v & 0xFFu, c1 = (v >> 8) & 0xFFu, c2 = (v >> 16) & 0xFFu, c3 = v >> 24;
+      a += c0 + c1 + c2 + c3;
+      bb += (uint64_t)(stride - i) * c0 + (uint64_t)(stride - i - 1) * c1 + (uint64_t)(stride - i - 2) * c2 +
+            (uint64_t)(stride - i - 3) * c3;
+    }
+    for (; i < stride; i++) {
+      a += data[p0 + i];
+      bb += (uint64_t)(stride - i) * data[p0 + i];
+    }
+    s_a[y] = (uint32_t)(a % 65521u);
+    s_b[y] = (uint32_t)(bb % 65521u);
+  }
+  s_bits[threadIdx.x] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t total = 0;
+    for (int k = 0; k < (int)blockDim.x; k++) total += s_bits[k];
+    uint32_t A = 1, B = 0;   // adler32 of the rows in order
+    for (int y = 0; y < h; y++) {
+      B = (uint32_t)((B + (uint64_t)stride * A + s_b[y]) % 65521u);
+      A = (A + s_a[y]) % 65521u;
+    }
+    adler[t] = (B << 16) | A;
+    zlen[t] = 2 + (3 + total + 7 + 7) / 8 + 4;
+  }
+}
+
+// Pass 2: the codes of every row at its bit offset in the tile's stream, at
+// the tile's byte offset zoff[t] of the packed buffer (zeroed).
+__global__ __launch_bounds__(256) void png_deflate_write_kernel(const uint8_t *__restrict__ filt,
+                                                                const int64_t *__restrict__ off,
+                                                                const int32_t *__restrict__ wh,
+                                                                const int32_t *__restrict__ opaque, int max_h,
+                                                                const int32_t *__restrict__ row_bits,
+                                                                const uint32_t *__restrict__ adler,
+                                                                const int64_t *__restrict__ zoff,
+                                                                const int64_t *__restrict__ zlen,
+                                                                uint8_t *__restrict__ packed) {
+  const int t = blockIdx.x;
+  const int w = wh[2 * t], h = wh[2 * t + 1];
+  const int bpp = opaque[t] ? 3 : 4;
+  const int stride = 1 + bpp * w;
+  const uint8_t *data = filt + off[t];
+  uint8_t *z = packed + zoff[t];
+  // the tile's stream starts on a 4-byte boundary of the packed buffer
+  uint32_t *words = (uint32_t *)z;
+  __shared__ int64_t s_start[kPngMaxRows + 1];
+  if (threadIdx.x == 0) {   // row bit offsets (serial: h <= 4096 adds)
+    int64_t b = 16 + 3;
+    for (int y = 0; y < h; y++) { s_start[y] = b; b += row_bits[(int64_t)t * max_h + y]; }
+    s_start[h] = b;
+  }
+  __syncthreads();
+  // every byte by OR into the zeroed buffer, so no write order matters
+  auto or_byte = [&](int64_t pos, uint32_t v) { atomicOr(words + (pos >> 2), (v & 0xFFu) << (8 * (pos & 3))); };
+  if (threadIdx.x == 0) {
+    or_byte(0, 0x78);   // CMF: deflate, 32 KiB window
+    or_byte(1, 0x01);   // FLG: (0x78 * 256 + 0x01) % 31 == 0
+    BitSink bs;         // block header: BFINAL 1, BTYPE 01 (fixed codes)
+    bs.init(words, 16);
+    bs.put(0x3u, 3);
+    bs.finish();
+    bs.init(words, s_start[h]);   // end of block
+    bs.put(0u, 7);
+    bs.finish();
+    const int64_t end = (s_start[h] + 7 + 7) / 8;   // Adler-32 after the byte padding
+    const uint32_t ad = adler[t];
+    or_byte(end, ad >> 24); or_byte(end + 1, ad >> 16); or_byte(end + 2, ad >> 8); or_byte(end + 3, ad);
+  }
+  for (int y = threadIdx.x; y < h; y += blockDim.x) {
+    BitSink bs;
+    bs.init(words, s_start[y]);
+    const int64_t p0 = (int64_t)y * stride;
+    deflate_row<true>(data, p0, p0 + stride, bpp, stride, bs);
+    bs.finish();
+  }
+  (void)zlen;
+}
+
+// CRC-32 (PNG / zlib polynomial 0xEDB88320) of each 32 KiB IDAT chunk of
+// every tile's stream, type bytes "IDAT" included: a thread per chunk,
+// slicing by 4 over dword loads (the stream starts 4-byte aligned and so
+// does every chunk), tables in LDS.
+__global__ __launch_bounds__(256) void png_idat_crc_kernel(const uint8_t *__restrict__ packed,
+                                                           const int64_t *__restrict__ zoff,
+                                                           const int64_t *__restrict__ zlen, int n_tiles,
+                                                           int max_chunks, uint32_t *__restrict__ crc) {
+  __shared__ uint32_t T[4][256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = (uint32_t)i;
+    for (int k = 0; k < 8; k++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+    T[0][i] = c;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = T[0][i];
+    for (int k = 1; k < 4; k++) { c = T[0][c & 0xFFu] ^ (c >> 8); T[k][i] = c; }
+  }
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (int64_t)n_tiles * max_chunks) return;
+  const int t = (int)(g / max_chunks), ch = (int)(g % max_chunks);
+  const int64_t n_all = zlen[t], p0 = (int64_t)ch * 32768;
+  if (p0 >= n_all) return;
+  const int64_t n = min((int64_t)32768, n_all - p0);
+  const uint8_t *d = packed + zoff[t] + p0;
+  uint32_t c = 0xFFFFFFFFu;
+  const uint8_t idat[4] = {'I', 'D', 'A', 'T'};
+  for (int k = 0; k < 4; k++) c = T[0][(c ^ idat[k]) & 0xFFu] ^ (c >> 8);
+  int64_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    c ^= *(const uint32_t *)(d + i);
+    c = T[3][c & 0xFFu] ^ T[2][(c >> 8) & 0xFFu] ^ T[1][(c >> 16) & 0xFFu] ^ T[0][c >> 24];
+  }
+  for (; i < n; i++) c = T[0][(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+  crc[g] = c ^ 0xFFFFFFFFu;
+}
+
 // ------------------------------------------------------------------ GeoTIFF
 // PackBits (TIFF 6.0 section 9) of one tile row (libtiff encodes tiled
 // PackBits row by row): runs of 3+ equal bytes as replicate runs, the rest
@@ -215,8 +478,8 @@ void chunk(std::vector<uint8_t> &o, const char *type, const uint8_t *data, size_
   put32(o, (uint32_t)crc32(0L, o.data() + at, (uInt)(n + 4)));
 }
 
-// One tile: PNG signature, IHDR, the zlib stream in 32 KiB IDAT chunks, IEND.
-int png_tile(const uint8_t *filtered, size_t n_filtered, int w, int h, bool opq, std::vector<uint8_t> &o) {
+// PNG signature + IHDR of a w x h 8-bit truecolour (alpha) image.
+void png_head(int w, int h, bool opq, std::vector<uint8_t> &o) {
   static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
   o.assign(sig, sig + 8);
   uint8_t ihdr[13];
@@ -227,6 +490,42 @@ int png_tile(const uint8_t *filtered, size_t n_filtered, int w, int h, bool opq,
   ihdr[9] = opq ? 2 : 6;       // truecolour / truecolour + alpha
   ihdr[10] = 0; ihdr[11] = 0; ihdr[12] = 0;
   chunk(o, "IHDR", ihdr, 13);
+}
+
+// A whole PNG around a finished zlib stream, written straight into dst
+// (cap bytes): 32 KiB IDAT chunks (Go's bufio.Writer size), IEND; returns
+// its size, 0 when it does not fit.
+size_t png_frame(const uint8_t *z, size_t zn, int w, int h, bool opq, uint8_t *dst, size_t cap,
+                 const uint32_t *idat_crc) {
+  std::vector<uint8_t> head;
+  png_head(w, h, opq, head);
+  const size_t need = head.size() + (zn / 32768 + 1) * 12 + zn + 12;
+  if (need > cap) return 0;
+  uint8_t *o = dst;
+  std::memcpy(o, head.data(), head.size());
+  o += head.size();
+  auto be32 = [&](uint32_t v) { o[0] = v >> 24; o[1] = v >> 16; o[2] = v >> 8; o[3] = v; o += 4; };
+  const uLong crc_idat = crc32(0L, (const Bytef *)"IDAT", 4);
+  for (size_t p = 0; p < zn; p += 32768) {
+    const size_t n = std::min<size_t>(32768, zn - p);
+    be32((uint32_t)n);
+    std::memcpy(o, "IDAT", 4);
+    o += 4;
+    std::memcpy(o, z + p, n);
+    o += n;
+    be32(idat_crc ? idat_crc[p / 32768] : (uint32_t)crc32(crc_idat, z + p, (uInt)n));
+  }
+  be32(0);
+  std::memcpy(o, "IEND", 4);
+  o += 4;
+  be32((uint32_t)crc32(0L, (const Bytef *)"IEND", 4));
+  return (size_t)(o - dst);
+}
+
+// One tile through host zlib: PNG signature, IHDR, the zlib stream in 32 KiB
+// IDAT chunks, IEND.
+int png_tile(const uint8_t *filtered, size_t n_filtered, int w, int h, bool opq, std::vector<uint8_t> &o) {
+  png_head(w, h, opq, o);
   std::vector<uint8_t> z(compressBound((uLong)n_filtered) + 64);
   z_stream s;
   std::memset(&s, 0, sizeof(s));
@@ -312,16 +611,23 @@ using namespace gsky;
 
 extern "C" {
 
+// Workspace: filtered rows | per-tile offsets, sizes, opacity | per-row bit
+// counts | Adler-32, zlib lengths and offsets | the packed zlib streams (at
+// most 9/8 of the filtered bytes + 16 per tile with fixed codes).
+static int64_t png_deflate_cap(int64_t per) { return (per * 9 + 7) / 8 + 64 + (per / 32768 + 1) * 4 + 256; }
+
 int64_t gskyhip_png_workspace_size(int n_tiles, int max_w, int max_h) {
   if (n_tiles <= 0 || max_w <= 0 || max_h <= 0) return 0;
   const int64_t per = (int64_t)max_h * (1 + 4 * (int64_t)max_w);
-  return ((int64_t)n_tiles * per + 255) / 256 * 256 + (int64_t)n_tiles * (8 + 8 + 4) + 1024;
+  const int64_t a = ((int64_t)n_tiles * per + 255) / 256 * 256 + (int64_t)n_tiles * (8 + 8 + 4) + 1024;
+  const int64_t b = ((int64_t)n_tiles * max_h * 4 + 255) / 256 * 256 + (int64_t)n_tiles * (4 + 8 + 8) + 1024;
+  return a + b + (int64_t)n_tiles * png_deflate_cap(per) + 1024;
 }
 
 int64_t gskyhip_png_bound(int width, int height) {
   if (width <= 0 || height <= 0) return 0;
   const uLong raw = (uLong)height * (1 + 4 * (uLong)width);
-  const uLong z = compressBound(raw) + 64;
+  const uLong z = std::max<uLong>(compressBound(raw) + 64, (uLong)png_deflate_cap((int64_t)raw));
   return 8 + 25 + (int64_t)(z / 32768 + 1) * 12 + (int64_t)z + 12;
 }
 
@@ -356,6 +662,91 @@ int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, i
   hipLaunchKernelGGL(png_filter_kernel, dim3((unsigned)((int64_t)n_tiles * max_h)), dim3(256), 0, s, rgba,
                      tile_stride, row_stride, d_wh, d_opq, max_h, d_off, filt);
   if (hipGetLastError() != hipSuccess) return GSKYHIP_E_HIP;
+  // GSKYHIP_PNG_ZLIB=1: deflate with zlib level 6 on host threads (round 3)
+  const char *zl = std::getenv("GSKYHIP_PNG_ZLIB");
+  const bool host_zlib = zl && std::atoi(zl) != 0;
+  const bool trace = std::getenv("GSKYHIP_PNG_TRACE") != nullptr;
+  auto now_us = [] {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  const double t_start = now_us();
+  if (!host_zlib && max_h <= kPngMaxRows) {
+    char *b = tail + (int64_t)n_tiles * (8 + 8 + 4) + 1024;
+    b = (char *)(((uintptr_t)b + 255) & ~(uintptr_t)255);
+    int32_t *d_rowbits = (int32_t *)b;
+    b += ((int64_t)n_tiles * max_h * 4 + 255) / 256 * 256;
+    uint32_t *d_adler = (uint32_t *)b;
+    int64_t *d_zlen = (int64_t *)(b + (((int64_t)n_tiles * 4 + 7) & ~(int64_t)7));
+    int64_t *d_zoff = d_zlen + n_tiles;
+    uint8_t *d_packed = (uint8_t *)(((uintptr_t)(d_zoff + n_tiles) + 255) & ~(uintptr_t)255);
+    if ((char *)d_packed + (int64_t)n_tiles * png_deflate_cap(per) > ws + workspace_bytes) return GSKYHIP_E_ARG;
+    hipLaunchKernelGGL(png_deflate_count_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, filt, d_off, d_wh, d_opq,
+                       max_h, d_rowbits, d_adler, d_zlen);
+    std::vector<int64_t> zlen(n_tiles), zoff(n_tiles);
+    std::vector<int32_t> opq(n_tiles);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(zlen.data(), d_zlen, (size_t)n_tiles * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(opq.data(), d_opq, (size_t)n_tiles * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return GSKYHIP_E_HIP;
+    const double t_count = now_us();
+    int64_t total = 0, max_zlen = 0;
+    for (int t = 0; t < n_tiles; t++) {
+      zoff[t] = total;
+      total += (zlen[t] + 3) & ~(int64_t)3;
+      max_zlen = std::max(max_zlen, zlen[t]);
+    }
+    const int max_chunks = (int)((max_zlen + 32767) / 32768);
+    if (hipMemcpyAsync(d_zoff, zoff.data(), (size_t)n_tiles * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(d_packed, 0, (size_t)std::max<int64_t>(total, 4), s) != hipSuccess)
+      return GSKYHIP_E_HIP;
+    hipLaunchKernelGGL(png_deflate_write_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, filt, d_off, d_wh, d_opq,
+                       max_h, d_rowbits, d_adler, d_zoff, d_zlen, d_packed);
+    // IDAT CRCs behind the packed streams (the pinned read-back holds both)
+    const int64_t crc_at = (total + 255) & ~(int64_t)255;
+    const int64_t n_crc = (int64_t)n_tiles * max_chunks;
+    if (crc_at + n_crc * 4 > (int64_t)n_tiles * png_deflate_cap(per)) return GSKYHIP_E_ARG;
+    uint32_t *d_crc = (uint32_t *)(d_packed + crc_at);
+    if (n_crc > 0)
+      hipLaunchKernelGGL(png_idat_crc_kernel, dim3((unsigned)((n_crc + 255) / 256)), dim3(256), 0, s, d_packed, d_zoff,
+                         d_zlen, n_tiles, max_chunks, d_crc);
+    uint8_t *zhost = nullptr;
+    const int64_t back = crc_at + n_crc * 4;
+    if (hipGetLastError() != hipSuccess || hipHostMalloc((void **)&zhost, (size_t)std::max<int64_t>(back, 4),
+                                                         hipHostMallocDefault) != hipSuccess)
+      return GSKYHIP_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) { hipHostFree(zhost); return GSKYHIP_E_HIP; }
+    const double t_write = now_us();
+    if (hipMemcpyAsync(zhost, d_packed, (size_t)back, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      hipHostFree(zhost);
+      return GSKYHIP_E_HIP;
+    }
+    const double t_copy = now_us();
+    // PNG framing on host threads: IHDR, 32 KiB IDAT chunks with CRC-32, IEND
+    std::atomic<int> next(0), err(0);
+    auto frame = [&]() {
+      for (;;) {
+        const int t = next++;
+        if (t >= n_tiles) return;
+        const size_t n = png_frame(zhost + zoff[t], (size_t)zlen[t], sizes[2 * t], sizes[2 * t + 1], opq[t] != 0,
+                                   png_out + (int64_t)t * png_capacity, (size_t)png_capacity,
+                                   (const uint32_t *)(zhost + crc_at) + (int64_t)t * max_chunks);
+        if (!n) err = GSKYHIP_E_ARG;
+        png_sizes[t] = (int64_t)n;
+      }
+    };
+    const int nt = std::max(1, std::min(n_threads > 0 ? n_threads : 1, n_tiles));
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nt; i++) pool.emplace_back(frame);
+    frame();
+    for (auto &th : pool) th.join();
+    hipHostFree(zhost);
+    if (trace)
+      std::fprintf(stderr, "png tiles=%d filter+count_us=%.0f write_us=%.0f d2h_us=%.0f (%.1f MB) frame_us=%.0f\n",
+                   n_tiles, t_count - t_start, t_write - t_count, t_copy - t_write, total / 1e6, now_us() - t_copy);
+    return err.load();
+  }
   std::vector<uint8_t> host((size_t)n_tiles * per);
   std::vector<int32_t> opq(n_tiles);
   if (hipMemcpyAsync(host.data(), filt, host.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
