@@ -9,9 +9,9 @@ estimate bench.py reports as roofline.traffic:
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  The factor 2 is the gfx950 correction of
 MI355X_MICROARCH.md ("FETCH_SIZE reports exactly 1/2 of the bytes of a wide
-coalesced streaming read"); it is calibrated for 16-B streaming loads, not
-for the 2-byte gathers of the warp, so the read half of `traffic` is an
-estimate bracketed by [FETCH_SIZE, 2 * FETCH_SIZE].
+coalesced streaming read"); tools/calib/fetch_calib.hip measured the same
+0.5 for 2-, 4-, 8- and 16-byte reads and gathers of known distinct bytes
+(profiles/r04b_fetch_calibration.json), so it applies to the warp's gathers.
 
 usage: python tools/pmc_summary.py [pmc_dir] [kernel_substring] [out.json]
 """
@@ -51,7 +51,8 @@ def main():
         res["fetch_bytes_raw"] = fetch
         res["write_bytes"] = write
         res["hbm_bytes_per_launch"] = 2.0 * fetch + write
-        res["note"] = "traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE correction; gathers uncalibrated)"
+        res["note"] = ("traffic = 2*FETCH_SIZE + WRITE_SIZE: FETCH_SIZE reports 0.5 of the distinct bytes for 2/4/8/16-B "
+                       "reads and gathers on gfx950, WRITE_SIZE exact (profiles/r04b_fetch_calibration.json)")
     s = json.dumps(res, indent=1, sort_keys=True)
     if out:
         with open(out, "w") as fh:
