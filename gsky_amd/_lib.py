@@ -98,7 +98,7 @@ EXPORTS = [
     "gskyhip_render_tile_info", "gskyhip_compute_reproject_extent",
     "gskyhip_service_run", "gskyhip_service_register_granule", "gskyhip_service_unregister_all",
     "gskyhip_service_stats", "gskyhip_service_stats_n", "gskyhip_service_shutdown", "gskyhip_drill_deciles_workspace_size",
-    "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device", "gskyhip_drill_masks_device", "gskyhip_parse_numbers",
+    "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device", "gskyhip_drill_masks_device", "gskyhip_drill_masks_device_packed", "gskyhip_parse_numbers",
     "gskyhip_drill_read_data_workspace_size", "gskyhip_drill_read_data",
     "gskyhip_png_workspace_size", "gskyhip_png_bound", "gskyhip_encode_png",
     "gskyhip_geotiff_workspace_size", "gskyhip_geotiff_bound", "gskyhip_encode_geotiff",
@@ -176,6 +176,9 @@ def lib() -> C.CDLL:
                                                    vp, vp, C.POINTER(i64), vp, vp, vp]
     if hasattr(L, "gskyhip_parse_numbers"):
         L.gskyhip_parse_numbers.argtypes = [C.c_char_p, ci, C.c_void_p, C.c_void_p]
+    if hasattr(L, "gskyhip_drill_masks_device_packed"):
+        L.gskyhip_drill_masks_device_packed.argtypes = [C.c_char_p, i64, ci, C.c_char_p, C.POINTER(d), ci, ci, vp,
+                                                        vp, C.POINTER(i64), vp, vp, C.POINTER(vp), vp, vp]
     if hasattr(L, "gskyhip_drill_masks_device"):   # absent from kept earlier builds (GSKYHIP_LIB=<name>)
         L.gskyhip_drill_masks_device.argtypes = [C.POINTER(C.c_char_p), ci, C.c_char_p, C.POINTER(d), ci, ci, vp,
                                                  vp, C.POINTER(i64), vp, vp, C.POINTER(vp), vp, vp]

@@ -956,6 +956,32 @@ extern "C" int gskyhip_drill_masks_device(const char *const *geometries, int n, 
   }
 }
 
+// The same with the n geometries packed NUL-separated in one buffer (a
+// caller with the strings in one allocation -- Python's one join + encode --
+// builds no pointer array).
+extern "C" int gskyhip_drill_masks_device_packed(const char *packed, int64_t packed_bytes, int n,
+                                                 const char *dataset_srs, const double *geot, int xsize, int ysize,
+                                                 int32_t *win_out, int64_t *mask_off_out, int64_t *mask_bytes_out,
+                                                 gskyhip_alloc_fn alloc, void *alloc_ctx, uint8_t **masks_dev_out,
+                                                 int32_t *status_out, void *stream) {
+  if (n < 0 || !packed || packed_bytes < 0) return GSKYHIP_E_ARG;
+  try {
+    std::vector<const char *> ptr((size_t)std::max(1, n));
+    const char *p = packed, *end = packed + packed_bytes;
+    for (int i = 0; i < n; i++) {
+      if (p >= end) return GSKYHIP_E_ARG;
+      ptr[(size_t)i] = p;
+      const void *z = std::memchr(p, 0, (size_t)(end - p));
+      if (!z) return GSKYHIP_E_ARG;   // every string NUL-terminated inside the buffer
+      p = (const char *)z + 1;
+    }
+    return gskyhip_drill_masks_device(ptr.data(), n, dataset_srs, geot, xsize, ysize, win_out, mask_off_out,
+                                      mask_bytes_out, alloc, alloc_ctx, masks_dev_out, status_out, stream);
+  } catch (...) {
+    return GSKYHIP_E_ARG;
+  }
+}
+
 extern "C" int gskyhip_drill_descriptors(const char *const *geometries, int n, const char *dataset_srs,
                                          const double *geot, int xsize, int ysize, int32_t *win_out,
                                          int64_t *mask_off_out, int64_t *mask_bytes_out, uint8_t *masks_out,

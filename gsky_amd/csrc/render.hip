@@ -1801,10 +1801,12 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.st_pol = 0;
   a.ab_mode = 0;
   a.ab_vfetch = 1;
+  a.ab_xcd = 0;
 #ifdef GSKYHIP_AB
   if (const char *sp = getenv("GSKYHIP_NN_STPOL")) a.st_pol = atoi(sp);
   if (const char *am = getenv("GSKYHIP_AB_MODE")) a.ab_mode = atoi(am);
   if (const char *vf = getenv("GSKYHIP_NN_VFETCH")) a.ab_vfetch = atoi(vf);
+  if (const char *xc = getenv("GSKYHIP_NN_XCD")) a.ab_xcd = atoi(xc);
 #endif
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));

@@ -432,10 +432,17 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   // eight 4-B ones
   __shared__ __attribute__((aligned(16))) uint32_t s_stage[STAGE ? 4 : 1][STAGE ? kBandCols : 4];
 
-  const int item = blockIdx.x;
-  if (item >= n_items) return;
   const int bands_per_tile = (a.max_h + kRowsBlk - 1) / kRowsBlk;
   const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
+  int item = blockIdx.x;
+#ifdef GSKYHIP_AB
+  if (a.ab_xcd) {   // A/B: every block of a tile on one XCD (blockIdx % 8), tiles dealt round-robin over the XCDs
+    const int per = bands_per_tile * col_blocks;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    item = ((slot / per) * 8 + xcd) * per + slot % per;
+  }
+#endif
+  if (item >= n_items) return;
   const int t = item / (bands_per_tile * col_blocks);
   const int in_tile = item - t * bands_per_tile * col_blocks;
   // the block's per-tile values in one round of scalar loads, and the
@@ -706,7 +713,10 @@ template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = fa
           bool WIDE = false>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE, COOP, WIDE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  // the XCD order (A/B) maps blocks over whole groups of 8 tiles: round the grid up
+  const int per = ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
+  const int grid = a.ab_xcd ? (a.n_tiles + 7) / 8 * 8 * per : items;
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE, COOP, WIDE>), dim3((unsigned)grid), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
 

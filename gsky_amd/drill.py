@@ -152,11 +152,16 @@ def drill_dataset(geometries: Sequence[str], dataset_srs: Optional[str], geot: S
         return MaskBatch(torch.from_numpy(win.copy()).to(dev), torch.from_numpy(off.copy()).to(dev),
                          torch.from_numpy(buf).to(dev)), st
     n = len(geometries)
-    arr = (C.c_char_p * max(1, n))(*[g.encode() for g in geometries])
+    packed = ("\0".join(geometries) + "\0").encode()   # one buffer, no per-string objects
     gt = (C.c_double * 6)(*geot)
-    win = np.zeros((max(1, n), 4), np.int32)
-    off = np.zeros(max(1, n), np.int64)
-    st = np.zeros(max(1, n), np.int32)
+    # windows and mask offsets written by the library straight into pinned
+    # memory, then one asynchronous upload (no pageable copies, no wait)
+    m = max(1, n)
+    pin = _pinned_meta(24 * m)
+    hb = pin.numpy()
+    win = hb[:16 * m].view(np.int32).reshape(m, 4)
+    off = hb[16 * m:24 * m].view(np.int64)
+    st = np.zeros(m, np.int32)
     total = C.c_int64()
     srs = dataset_srs.encode() if dataset_srs else None
     L = lib()
@@ -170,12 +175,32 @@ def drill_dataset(geometries: Sequence[str], dataset_srs: Optional[str], geot: S
         return t.data_ptr()
     cb = _ALLOC_FN(alloc)
     mptr = C.c_void_p()
-    check(L.gskyhip_drill_masks_device(arr, n, srs, gt, xsize, ysize, win.ctypes.data_as(C.c_void_p),
-                                       off.ctypes.data_as(C.c_void_p), C.byref(total), cb, None, C.byref(mptr),
-                                       st.ctypes.data_as(C.c_void_p), _stream()), "drill_masks_device")
+    check(L.gskyhip_drill_masks_device_packed(packed, len(packed), n, srs, gt, xsize, ysize,
+                                              win.ctypes.data_as(C.c_void_p), off.ctypes.data_as(C.c_void_p),
+                                              C.byref(total), cb, None, C.byref(mptr), st.ctypes.data_as(C.c_void_p),
+                                              _stream()), "drill_masks_device")
     masks = held[0]
-    mb = MaskBatch(torch.from_numpy(win[:n].copy()).to(dev), torch.from_numpy(off[:n].copy()).to(dev), masks)
+    meta = torch.empty(24 * m, dtype=torch.uint8, device=dev)
+    meta.copy_(pin[:24 * m], non_blocking=True)
+    _META_EVENT[0] = torch.cuda.Event()
+    _META_EVENT[0].record()
+    mb = MaskBatch(meta[:16 * n].view(torch.int32).view(n, 4), meta[16 * m:16 * m + 8 * n].view(torch.int64), masks)
     return mb, st[:n]
+
+
+_META_PIN: List[torch.Tensor] = []
+_META_EVENT: List[Optional[torch.cuda.Event]] = [None]
+
+
+def _pinned_meta(nbytes: int) -> torch.Tensor:
+    """A pinned host buffer of at least nbytes for drill_dataset's windows
+    and offsets, reused across calls once the previous upload from it is
+    done."""
+    if _META_EVENT[0] is not None:
+        _META_EVENT[0].synchronize()
+    if not _META_PIN or _META_PIN[0].numel() < nbytes:
+        _META_PIN[:] = [torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8).pin_memory()]
+    return _META_PIN[0]
 
 
 _ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int64)

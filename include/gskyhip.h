@@ -568,6 +568,12 @@ int gskyhip_drill_masks_device(const char *const *geometries, int n, const char 
                                int xsize, int ysize, int32_t *win_out, int64_t *mask_off_out,
                                int64_t *mask_bytes_out, gskyhip_alloc_fn alloc, void *alloc_ctx,
                                uint8_t **masks_dev_out, int32_t *status_out, void *stream);
+/* The same with the n geometries packed NUL-separated in one buffer of
+ * packed_bytes (every string NUL-terminated inside it). */
+int gskyhip_drill_masks_device_packed(const char *packed, int64_t packed_bytes, int n, const char *dataset_srs,
+                                      const double *geot, int xsize, int ysize, int32_t *win_out,
+                                      int64_t *mask_off_out, int64_t *mask_bytes_out, gskyhip_alloc_fn alloc,
+                                      void *alloc_ctx, uint8_t **masks_dev_out, int32_t *status_out, void *stream);
 /* Test hook: the GeoJSON number parser of the drill descriptors on n
  * NUL-separated strings packed in `text`; out[i] the value, consumed[i] the
  * characters parsed (strtod semantics). */
