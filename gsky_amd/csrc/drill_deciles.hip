@@ -55,13 +55,12 @@ namespace gsky {
 
 namespace {
 
-constexpr int kSelThreads = 512;
-constexpr int kSelWaves = kSelThreads / 64;
+constexpr int kSelThreads = 256;   // r04y sweep: 256 x 20 KB 14.9 ms vs 512 x 36 KB 19.1 ms (C4)
 constexpr int kMaxRanks = 32;        // distinct ranks selected per pass set (2 x decile_count <= 32)
 constexpr int kBinsLog = 11;         // first selection pass: 2048 buckets
 constexpr int kBins = 1 << kBinsLog;
 constexpr int kCandMax = 64;         // keys of one bucket resolved by the counting compare
-static_assert(kBins == 4 * kSelThreads, "the bucket scan gives each thread 4 bins");
+static_assert(kBins % kSelThreads == 0, "the bucket scan gives each thread kBins / NT buckets");
 static_assert(kMaxRanks * kCandMax <= kBins, "candidates reuse the bucket histogram");
 constexpr int kTilePad = 65;         // LDS tile row pitch (floats): conflict-free transposed reads
 
@@ -74,7 +73,7 @@ __device__ __forceinline__ float fdecode(uint32_t k) {
 }
 
 constexpr int kDecChunk = 64;        // pixels per transpose item
-constexpr int kSelLds = 36 * 1024;   // dynamic LDS of a select workgroup (histograms + key cache): 4 per CU
+constexpr int kSelLds = 20 * 1024;   // dynamic LDS of a select workgroup (histograms + key cache): 7 per CU
 constexpr int kSelU = 16;            // segment values per thread in flight (a 6k-value segment: one round)
 constexpr int kHistSlots = kBins / 256;  // radix histograms at once (the region also holds the 2048 buckets)
 constexpr bool kDecDirect = false;       // product: select from the stack directly (A/B: GSKYHIP_DEC_DIRECT)
@@ -179,8 +178,8 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
 // workgroups of one polygon run back to back on one XCD (blockIdx % 8 is the
 // XCD the dispatcher picks), so the 32 bands sharing a pixel's 128-byte line
 // are read from that XCD's L2 after the first.
-template <int kU, bool DIRECT = false>
-__global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float *__restrict__ vals,
+template <int kU, bool DIRECT = false, int NT = kSelThreads>
+__global__ __launch_bounds__(NT) void decile_select_kernel(const float *__restrict__ vals,
                                                                     const int64_t *__restrict__ mask_off,
                                                                     const int32_t *__restrict__ count,
                                                                     const int32_t *__restrict__ totals, int n_chunk,
@@ -201,8 +200,8 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   __shared__ int32_t s_soff[kMaxRanks];    // slot -> first candidate
   __shared__ uint32_t s_fill[kMaxRanks];   // slot -> candidates written
   __shared__ int8_t s_map[kBins];          // bucket -> slot, -1 when no rank needs it
-  __shared__ uint32_t red[3 * kSelWaves];
-  __shared__ uint32_t s_wsum[kSelWaves];
+  __shared__ uint32_t red[3 * (NT / 64)];
+  __shared__ uint32_t s_wsum[(NT / 64)];
   __shared__ int32_t s_nr, s_ns, s_nsl;
   __shared__ uint32_t s_lo[kMaxRanks], s_hi[kMaxRanks];   // rank r: its open key range
   __shared__ int32_t s_done[kMaxRanks], s_small_r[64];
@@ -219,7 +218,7 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   float *dst = out + o * dc;
   const int tid = threadIdx.x;
   if (totals[o] <= 0) {   // drill.go:186-190
-    for (int i = tid; i < dc; i += kSelThreads) dst[i] = 0.f;
+    for (int i = tid; i < dc; i += NT) dst[i] = 0.f;
     if (tid == 0) status[o] = 1;
     return;
   }
@@ -238,16 +237,16 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   auto skipk = [&](uint32_t k) { return skip_on && (k == kn1 || k == kn2); };
   uint32_t ka = 0xFFFFFFFFu, ko = 0u;   // smallest / largest valid key
   int valid = 0;   // kU: values per thread in flight per round
-  for (int i0 = 0; i0 < n; i0 += kSelThreads * kU) {
+  for (int i0 = 0; i0 < n; i0 += NT * kU) {
     float v[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
-      const int i = i0 + u * kSelThreads + tid;
+      const int i = i0 + u * NT + tid;
       v[u] = i < n ? ld(i) : nodata;
     }
 #pragma unroll
     for (int u = 0; u < kU; u++) {
-      const int i = i0 + u * kSelThreads + tid;
+      const int i = i0 + u * NT + tid;
       const bool keep = i < n && v[u] != nodata;
       const uint32_t k = fkey(v[u]);
       if (keep) { ka = min(ka, k); ko = max(ko, k); valid++; }
@@ -260,17 +259,17 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     valid += __shfl_xor(valid, sh);
   }
   if ((tid & 63) == 0) {
-    red[tid >> 6] = ka; red[kSelWaves + (tid >> 6)] = ko; red[2 * kSelWaves + (tid >> 6)] = (uint32_t)valid;
+    red[tid >> 6] = ka; red[(NT / 64) + (tid >> 6)] = ko; red[2 * (NT / 64) + (tid >> 6)] = (uint32_t)valid;
   }
   __syncthreads();
   uint32_t kmn = 0xFFFFFFFFu, kmx = 0u;
   int len = 0;
 #pragma unroll
-  for (int w = 0; w < kSelWaves; w++) {
-    kmn = min(kmn, red[w]); kmx = max(kmx, red[kSelWaves + w]); len += (int)red[2 * kSelWaves + w];
+  for (int w = 0; w < (NT / 64); w++) {
+    kmn = min(kmn, red[w]); kmx = max(kmx, red[(NT / 64) + w]); len += (int)red[2 * (NT / 64) + w];
   }
   if (len <= 0) {   // total > 0 implies a non-nodata value; keep the slot defined anyway
-    for (int i = tid; i < dc; i += kSelThreads) dst[i] = 0.f;
+    for (int i = tid; i < dc; i += NT) dst[i] = 0.f;
     if (tid == 0) status[o] = 0;
     return;
   }
@@ -303,7 +302,7 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   }
   const bool isEven = len % (dc + 1) == 0;
   if (isEven && dc * step + 1 >= len) {   // buf[iStep + 1] past the end for the last pick
-    for (int i = tid; i < dc; i += kSelThreads) dst[i] = 0.f;
+    for (int i = tid; i < dc; i += NT) dst[i] = 0.f;
     if (tid == 0) status[o] = GSKYHIP_E_RANGE;
     return;
   }
@@ -323,21 +322,21 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
   // every valid key once, from the LDS copy or streamed from the segment
   auto for_keys = [&](auto &&f) {
     if (fits) {
-      for (int i = tid; i < n; i += kSelThreads) {
+      for (int i = tid; i < n; i += NT) {
         const uint32_t k = cache[i];
         if (!skipk(k)) f(k);
       }
     } else {
-      for (int i0 = 0; i0 < n; i0 += kSelThreads * kU) {
+      for (int i0 = 0; i0 < n; i0 += NT * kU) {
         float v[kU];
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-          const int i = i0 + u * kSelThreads + tid;
+          const int i = i0 + u * NT + tid;
           v[u] = i < n ? ld(i) : nodata;
         }
 #pragma unroll
         for (int u = 0; u < kU; u++)
-          if (i0 + u * kSelThreads + tid < n && v[u] != nodata) f(fkey(v[u]));
+          if (i0 + u * NT + tid < n && v[u] != nodata) f(fkey(v[u]));
       }
     }
   };
@@ -372,16 +371,18 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
     }
     const uint32_t span = Hk - L;                       // W - 1, W = keys in the range
     const int sh = max(0, 32 - __clz(span) - kBinsLog);  // bucket = (k - L) >> sh < 2048
-    for (int i = tid; i < kBins; i += kSelThreads) { H[i] = 0u; s_map[i] = -1; }
+    for (int i = tid; i < kBins; i += NT) { H[i] = 0u; s_map[i] = -1; }
     __syncthreads();
     for_keys([&](uint32_t k) {
       if (k >= L && k <= Hk) atomicAdd(&H[(k - L) >> sh], 1u);
     });
     __syncthreads();
     {   // inclusive scan of the buckets in place, 4 per thread
-      const int b4 = 4 * tid;
-      const uint32_t h0 = H[b4], h1 = H[b4 + 1], h2 = H[b4 + 2], h3 = H[b4 + 3];
-      const uint32_t sum = h0 + h1 + h2 + h3;
+      constexpr int BPT = kBins / NT;   // buckets per thread
+      const int b4 = BPT * tid;
+      uint32_t hb[BPT], sum = 0;
+#pragma unroll
+      for (int k = 0; k < BPT; k++) { hb[k] = H[b4 + k]; sum += hb[k]; }
       uint32_t incl = sum;
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t up = __shfl_up(incl, o);
@@ -392,7 +393,9 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
       uint32_t base = 0;
       for (int w = 0; w < wv; w++) base += s_wsum[w];
       const uint32_t ex = base + incl - sum;
-      H[b4] = ex + h0; H[b4 + 1] = ex + h0 + h1; H[b4 + 2] = ex + h0 + h1 + h2; H[b4 + 3] = ex + sum;
+      uint32_t run = ex;
+#pragma unroll
+      for (int k = 0; k < BPT; k++) { run += hb[k]; H[b4 + k] = run; }
     }
     __syncthreads();
     if (tid < 64) {   // wave 0, lane r of the group: its bucket, then the small
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(kSelThreads) void decile_select_kernel(const float 
       // lane): MSB-first selection with wave ballots over the bits where the
       // candidates differ -- lanes whose bit is 0 come first; equal keys end
       // in the same candidate set, any of them is the value
-      for (int r = wv; r < nr; r += kSelWaves) {
+      for (int r = wv; r < nr; r += (NT / 64)) {
         if (!s_small_r[r]) continue;
         const int cnt = (int)s_bcnt[r];
         const uint32_t *c = cand + s_soff[s_slot[r]];
@@ -560,6 +563,10 @@ int launch_drill_deciles(const DecileCall &c) {
 #ifdef GSKYHIP_AB
   if (const char *e = getenv("GSKYHIP_DEC_DIRECT")) direct = atoi(e) != 0;
 #endif
+  int nt = kSelThreads;
+#ifdef GSKYHIP_AB
+  if (const char *e = getenv("GSKYHIP_DEC_NT")) nt = atoi(e) == 512 ? 512 : atoi(e) == 128 ? 128 : kSelThreads;
+#endif
   if (direct) {   // no transposed copy: a launch per band chunk straight from the stack
     for (int b0 = 0; b0 < n_list; b0 += c.band_chunk) {
       const int n_chunk = std::min(c.band_chunk, n_list - b0);
@@ -583,7 +590,15 @@ int launch_drill_deciles(const DecileCall &c) {
     hipLaunchKernelGGL(decile_transpose_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, c.stack,
                        c.t_stride, w.idx, c.mask_off, w.count, w.chunk_base, c.n_polys, w.tsel, n_chunk, n_groups,
                        w.vals);
-    if (sel_u == 8)
+    if (nt == 512)
+      hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 512>), dim3((unsigned)n_seg), dim3(512), dyn_lds, s,
+                         w.vals, c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
+                         n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
+    else if (nt == 128)
+      hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 128>), dim3((unsigned)n_seg), dim3(128), dyn_lds, s,
+                         w.vals, c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
+                         n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
+    else if (sel_u == 8)
       hipLaunchKernelGGL(decile_select_kernel<8>, dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
                          c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
                          cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
