@@ -479,7 +479,11 @@ static ReadWs read_carve(void *base, int n_polys, int64_t mask_bytes, int n_list
   ReadWs w;
   const int n_sel = read_count(n_list, band_strides <= 0 ? 1 : band_strides);
   const int np = n_polys > 0 ? n_polys : 1;
-  w.chunk = (int)std::max<int64_t>(1, std::min<int64_t>(n_sel, (1LL << 30) / std::max<int64_t>(1, mask_bytes)));
+  int ws_log2 = 30;   // the deciles' band-major segment buffer: <= 2^ws_log2 values
+#ifdef GSKYHIP_AB
+  if (const char *e = getenv("GSKYHIP_DEC_WS_LOG2")) ws_log2 = std::max(20, std::min(34, atoi(e)));
+#endif
+  w.chunk = (int)std::max<int64_t>(1, std::min<int64_t>(n_sel, (1LL << ws_log2) / std::max<int64_t>(1, mask_bytes)));
   w.mean_bytes = drill_workspace_size(np, mask_bytes, n_sel, 1, mode);
   w.dec_bytes = dc > 0 ? drill_deciles_workspace_size(np, mask_bytes, w.chunk) : 0;
   int64_t off = 0;

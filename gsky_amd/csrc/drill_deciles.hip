@@ -73,8 +73,9 @@ __device__ __forceinline__ float fdecode(uint32_t k) {
 }
 
 constexpr int kDecChunk = 64;        // pixels per transpose item
-constexpr int kSelLds = 20 * 1024;   // dynamic LDS of a select workgroup (histograms + key cache): 7 per CU
-constexpr int kSelU = 16;            // segment values per thread in flight (a 6k-value segment: one round)
+constexpr int kSelLds = 16 * 1024;   // dynamic LDS of a select workgroup (histograms + key cache): 8 per CU
+constexpr int kSelU = 8;             // segment values per thread in flight per round
+constexpr int kSelWpe = 8;           // select compiled for 8 waves per SIMD (63 VGPRs): r04ab sweep 14.9 -> 13.5 ms
 constexpr int kHistSlots = kBins / 256;  // radix histograms at once (the region also holds the 2048 buckets)
 constexpr bool kDecDirect = false;       // product: select from the stack directly (A/B: GSKYHIP_DEC_DIRECT)
 
@@ -103,6 +104,26 @@ __global__ __launch_bounds__(1024) void decile_chunk_scan_kernel(const int32_t *
   if (tid == 0) base[n_polys] = carry;
 }
 
+// One record per 64-pixel chunk, so a transpose wave finds its polygon's
+// pixels with one load (round 3-4 waves binary-searched chunk_base: ten
+// dependent loads before the first stack read).
+struct ChunkRec {
+  int64_t moff;   // mask_off[p]: the polygon's first compacted pixel
+  int32_t n;      // count[p]
+  int32_t cb;     // chunk_base[p]: the polygon's first chunk
+};
+
+__global__ __launch_bounds__(256) void decile_chunk_rec_kernel(const int32_t *__restrict__ count,
+                                                               const int64_t *__restrict__ mask_off,
+                                                               const int32_t *__restrict__ base,
+                                                               ChunkRec *__restrict__ rec) {
+  const int p = blockIdx.x;
+  const int c0 = base[p], nc = base[p + 1] - c0;
+  const int64_t mo = mask_off[p];
+  const int n = count[p];
+  for (int i = threadIdx.x; i < nc; i += 256) rec[c0 + i] = ChunkRec{mo, n, c0};
+}
+
 // The 64 lanes of one wavefront see each other's LDS writes in program
 // order: keep the compiler from moving LDS accesses across this point.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -113,16 +134,17 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // One wave per (64-pixel chunk ch, group g of 32 bands of the pass); four
 // independent waves per workgroup.  Band j of polygon p: vals[seg0 + j *
-// count[p] + k] for its pixel k, seg0 = mask_off[p] * n_chunk (the compacted
-// pixel list of p holds count[p] <= its window bytes).  A load instruction
+// npad + k] for its pixel k, seg0 = chunk_base[p] * 64 * n_chunk, npad =
+// count[p] rounded up to 64 (rows start on 256-byte boundaries, so a chunk's
+// store covers two whole lines: unaligned rows left partial lines that the
+// L2s of two XCDs wrote back separately).  A load instruction
 // reads the 32 bands (128 contiguous bytes) of two pixels, a store
 // instruction writes one band of the 64 pixels (256 contiguous bytes); the
 // wave's 64 x 32 tile (8.4 KB of LDS) keeps 16 waves per CU.
 constexpr int kTrBands = 32;
 __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__restrict__ stack, int t_stride,
                                                                const int32_t *__restrict__ idx,
-                                                               const int64_t *__restrict__ mask_off,
-                                                               const int32_t *__restrict__ count,
+                                                               const ChunkRec *__restrict__ rec,
                                                                const int32_t *__restrict__ chunk_base, int n_polys,
                                                                const int32_t *__restrict__ tsel, int n_chunk,
                                                                int n_groups, float *__restrict__ vals) {
@@ -131,22 +153,17 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t item = (int64_t)blockIdx.x * 4 + wave;
   const int ch = (int)(item / n_groups), g = (int)(item % n_groups);
-  if (ch >= chunk_base[n_polys]) return;   // whole waves; no workgroup barrier below
-  int lo = 0, hi = n_polys - 1;            // polygon owning chunk ch
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (chunk_base[mid] <= ch) lo = mid; else hi = mid - 1;
-  }
-  const int p = lo;
-  const int n = count[p];
-  const int k0 = (ch - chunk_base[p]) * kDecChunk;
+  const int64_t n_ch = chunk_base[n_polys];
+  if (item >= n_ch * n_groups) return;     // whole waves; no workgroup barrier below
+  const ChunkRec r = rec[ch];
+  const int n = r.n, k0 = (ch - r.cb) * kDecChunk;
   const int m = min(kDecChunk, n - k0);
   const int nb = min(kTrBands, n_chunk - g * kTrBands);   // bands of this group
   const int bl = lane & (kTrBands - 1), half = lane / kTrBands;
   // every lane loads from a valid address (band 0 of the group, pixel 0 of
   // the chunk) so the loads are unconditional and all in flight
   const float *base = stack + tsel[g * kTrBands + (bl < nb ? bl : 0)];
-  const int32_t my_px = idx[mask_off[p] + k0 + (lane < m ? lane : 0)];
+  const int32_t my_px = idx[r.moff + k0 + (lane < m ? lane : 0)];
   float *T = tile[wave];
   {   // all 64 pixels' loads in flight at once (lanes past m hold pixel 0 of the chunk;
       // their rows are never stored): 3 % faster than two rounds of 16
@@ -162,9 +179,10 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
     for (int u = 0; u < 32; u++) T[(2 * u + half) * kPad + bl] = v[u];
   }
   wave_lds_sync();
-  float *seg = vals + mask_off[p] * (int64_t)n_chunk + (int64_t)(g * kTrBands) * n + k0;
+  const int64_t npad = (int64_t)(n + kDecChunk - 1) / kDecChunk * kDecChunk;   // aligned band rows
+  float *seg = vals + (int64_t)r.cb * kDecChunk * n_chunk + (int64_t)(g * kTrBands) * npad + k0;
   if (lane < m) {
-    for (int j = 0; j < nb; j++) seg[(int64_t)j * n + lane] = T[lane * kPad + j];   // lane = pixel
+    for (int j = 0; j < nb; j++) seg[(int64_t)j * npad + lane] = T[lane * kPad + j];   // lane = pixel
   }
 }
 
@@ -178,9 +196,10 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
 // workgroups of one polygon run back to back on one XCD (blockIdx % 8 is the
 // XCD the dispatcher picks), so the 32 bands sharing a pixel's 128-byte line
 // are read from that XCD's L2 after the first.
-template <int kU, bool DIRECT = false, int NT = kSelThreads>
-__global__ __launch_bounds__(NT) void decile_select_kernel(const float *__restrict__ vals,
+template <int kU, bool DIRECT = false, int NT = kSelThreads, int WPE = 1>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void decile_select_kernel(const float *__restrict__ vals,
                                                                     const int64_t *__restrict__ mask_off,
+                                                                    const int32_t *__restrict__ chunk_base,
                                                                     const int32_t *__restrict__ count,
                                                                     const int32_t *__restrict__ totals, int n_chunk,
                                                                     int b0, int n_list, int dc, float nodata,
@@ -223,7 +242,8 @@ __global__ __launch_bounds__(NT) void decile_select_kernel(const float *__restri
     return;
   }
   const int n = count[p];
-  const float *buf = DIRECT ? nullptr : vals + mask_off[p] * (int64_t)n_chunk + (int64_t)j * n;
+  const int64_t npad = (int64_t)(n + kDecChunk - 1) / kDecChunk * kDecChunk;
+  const float *buf = DIRECT ? nullptr : vals + (int64_t)chunk_base[p] * kDecChunk * n_chunk + (int64_t)j * npad;
   const int32_t *pix = DIRECT ? pix_idx + mask_off[p] : nullptr;
   const float *bandp = DIRECT ? stack + tsel[j] : nullptr;
   auto ld = [&](int i) -> float { return DIRECT ? bandp[(int64_t)pix[i] * t_stride] : buf[i]; };
@@ -504,13 +524,14 @@ inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 struct DecWs {
   int32_t *idx, *count, *chunk_base, *tsel;
+  ChunkRec *rec;
   float *vals;
   int64_t total;
 };
 
 DecWs decile_carve(void *base, int n_polys, int64_t mask_bytes, int chunk) {
   DecWs w;
-  const int64_t cap = mask_bytes * chunk;
+  const int64_t cap = (mask_bytes + (int64_t)kDecChunk * n_polys) * chunk;   // rows padded to 64 values
   char *b = (char *)base;
   int64_t o = 0;
   auto take = [&](int64_t bytes) { char *p = b ? b + o : nullptr; o += al256(bytes); return p; };
@@ -518,6 +539,7 @@ DecWs decile_carve(void *base, int n_polys, int64_t mask_bytes, int chunk) {
   w.count = (int32_t *)take((int64_t)n_polys * 4);
   w.chunk_base = (int32_t *)take((mask_bytes / kDecChunk + n_polys + 1) * 4);
   w.tsel = (int32_t *)take((int64_t)chunk * 4);
+  w.rec = (ChunkRec *)take((mask_bytes / kDecChunk + n_polys) * (int64_t)sizeof(ChunkRec));
   w.vals = (float *)take(cap * 4);
   w.total = o;
   return w;
@@ -550,11 +572,13 @@ int launch_drill_deciles(const DecileCall &c) {
   hipLaunchKernelGGL(drill_compact_kernel, dim3(c.n_polys), dim3(256), 0, s, c.win, c.mask_off, c.masks, c.n_polys,
                      c.xsize, c.ysize, w.idx, w.count);
   hipLaunchKernelGGL(decile_chunk_scan_kernel, dim3(1), dim3(1024), 0, s, w.count, c.n_polys, w.chunk_base);
+  hipLaunchKernelGGL(decile_chunk_rec_kernel, dim3(c.n_polys), dim3(256), 0, s, w.count, c.mask_off, w.chunk_base,
+                     w.rec);
   const int64_t max_chunks = c.mask_bytes / kDecChunk + c.n_polys;   // >= sum of ceil(count / 64)
   const int n_slots = kHistSlots;
   int sel_lds = kSelLds, sel_u = kSelU;
 #ifdef GSKYHIP_AB
-  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(12, std::min(60, atoi(e))) * 1024;
+  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(8, std::min(60, atoi(e))) * 1024;
   if (const char *e = getenv("GSKYHIP_DEC_U")) sel_u = atoi(e);
 #endif
   const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
@@ -575,7 +599,7 @@ int launch_drill_deciles(const DecileCall &c) {
         return GSKYHIP_E_HIP;
       const unsigned grid = (unsigned)(((int64_t)n_seg + 7) / 8 * 8);
       hipLaunchKernelGGL((decile_select_kernel<kSelU, true>), dim3(grid), dim3(kSelThreads), dyn_lds, s, w.vals,
-                         c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
+                         c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
                          cache_keys, c.out, c.status, c.stack, c.t_stride, w.idx, w.tsel, n_seg);
     }
     return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
@@ -588,23 +612,27 @@ int launch_drill_deciles(const DecileCall &c) {
       return GSKYHIP_E_HIP;
     const int64_t items = max_chunks * n_groups;
     hipLaunchKernelGGL(decile_transpose_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, c.stack,
-                       c.t_stride, w.idx, c.mask_off, w.count, w.chunk_base, c.n_polys, w.tsel, n_chunk, n_groups,
+                       c.t_stride, w.idx, w.rec, w.chunk_base, c.n_polys, w.tsel, n_chunk, n_groups,
                        w.vals);
     if (nt == 512)
-      hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 512>), dim3((unsigned)n_seg), dim3(512), dyn_lds, s,
-                         w.vals, c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
+      hipLaunchKernelGGL((decile_select_kernel<16, false, 512>), dim3((unsigned)n_seg), dim3(512), dyn_lds, s,
+                         w.vals, c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
                          n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
     else if (nt == 128)
-      hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 128>), dim3((unsigned)n_seg), dim3(128), dyn_lds, s,
-                         w.vals, c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
+      hipLaunchKernelGGL((decile_select_kernel<16, false, 128>), dim3((unsigned)n_seg), dim3(128), dyn_lds, s,
+                         w.vals, c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
                          n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
-    else if (sel_u == 8)
-      hipLaunchKernelGGL(decile_select_kernel<8>, dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
-                         c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
+    else if (sel_u == 16)
+      hipLaunchKernelGGL((decile_select_kernel<16, false, kSelThreads, 1>), dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
+                         c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
+                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
+    else if (sel_u == 4)
+      hipLaunchKernelGGL((decile_select_kernel<8, false, kSelThreads, 1>), dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
+                         c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
                          cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
     else
-      hipLaunchKernelGGL(decile_select_kernel<kSelU>, dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
-                         c.mask_off, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
+      hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe>), dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
+                         c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
                          cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
   }
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
