@@ -26,7 +26,21 @@ struct DrillCall {
   void *workspace;
   int64_t workspace_bytes;
   hipStream_t stream;
+  // readData with deciles in reference order (mode 0): the mean pass also
+  // writes every in-mask value band-major -- polygon p's rows start at
+  // emit_chunk_base[p] * 64 * n_sel, one row of count[p] values (padded to
+  // 64) per read band -- and each (polygon, band)'s smallest / largest order
+  // key and count of non-nodata values (emit_stats[p * n_sel + j])
+  float *emit_vals = nullptr;
+  int32_t *emit_chunk_base = nullptr;
+  uint4 *emit_stats = nullptr;
 };
+
+// Order-preserving 32-bit key of a float (the deciles' radix selection).
+__device__ __forceinline__ uint32_t order_key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
 
 // computeDeciles (drill.go:229-273) for a batch of polygons: see
 // gskyhip_drill_deciles in include/gskyhip.h.
@@ -82,6 +96,12 @@ __global__ __launch_bounds__(256) void drill_compact_kernel(const int32_t *__res
                                                             int32_t *__restrict__ count);
 int64_t drill_deciles_workspace_size(int n_polys, int64_t mask_bytes, int band_chunk);
 int launch_drill_deciles(const DecileCall &c);
+// The fused path (DrillCall::emit_*): 64-pixel chunk offsets per polygon, and
+// the selection over the mean pass's band-major rows and key ranges.
+void launch_decile_chunk_scan(const int32_t *count, int n_polys, int32_t *chunk_base, hipStream_t s);
+int launch_decile_select_fused(const float *vals, const int32_t *chunk_base, const int32_t *count,
+                               const int32_t *totals, int n_polys, int n_sel, int decile_count, float nodata,
+                               const uint4 *stats, float *out, int32_t *status, hipStream_t s);
 
 int drill_rows_per_poly(int n_list, int band_strides);
 int64_t drill_workspace_size(int n_polys, int64_t mask_bytes, int n_list, int band_strides, int mode);

@@ -115,9 +115,53 @@ __device__ __forceinline__ void drill_walk(const float *__restrict__ base, int t
   for (; k < k1; k++) drill_acc<PC>(base[(int64_t)ip[k] * t_stride], nodata, lo, hi, sum, total);
 }
 
+// The same walk for readData with deciles (DrillCall::emit_*): each lane
+// also keeps its band's smallest / largest order key and count of
+// non-nodata values, and the wave writes the values band-major: 32 pixels x
+// 64 bands through an LDS tile, then two band rows of 128 contiguous bytes
+// per store instruction (rows are 256-byte aligned and padded to 64 values,
+// so the last block's padding lanes may write; per-lane 16-byte stores
+// straight from the walk ran at a third of the rate, r04af).
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool PC>
+__device__ __forceinline__ void drill_walk_emit(const float *__restrict__ base, int t_stride,
+                                                const int32_t *__restrict__ ip, int n, float nodata, float lo,
+                                                float hi, float &sum, int32_t &total, float *__restrict__ rows,
+                                                int64_t npad, int nb, float *T, uint32_t &ka, uint32_t &ko,
+                                                int32_t &valid) {
+  constexpr int kB = 32, kP = 65;
+  const int lane = threadIdx.x & 63, px = lane & 31, hb = lane >> 5;
+  for (int k0 = 0; k0 < n; k0 += kB) {
+    float v[kB];
+#pragma unroll
+    for (int q = 0; q < kB; q++) v[q] = base[(int64_t)ip[min(k0 + q, n - 1)] * t_stride];
+#pragma unroll
+    for (int q = 0; q < kB; q++) {
+      if (k0 + q < n) {   // uniform
+        drill_acc<PC>(v[q], nodata, lo, hi, sum, total);
+        const uint32_t key = order_key(v[q]);
+        if (v[q] != nodata) { ka = min(ka, key); ko = max(ko, key); valid++; }
+      }
+      T[q * kP + lane] = v[q];
+    }
+    wave_lds_fence();
+#pragma unroll 4
+    for (int i = 0; i < 32; i++) {
+      const int jj = 2 * i + hb;
+      if (jj < nb) rows[(int64_t)jj * npad + k0 + px] = T[px * kP + jj];
+    }
+    wave_lds_fence();
+  }
+}
+
 // Mode 0, reference order: one wave per (polygon, group of 64 selected bands),
 // polygons largest first.
-template <bool PC>
+template <bool PC, bool EMIT = false>
 __global__ __launch_bounds__(64) void drill_sum_kernel(const float *__restrict__ stack, int t_stride,
                                                        const int32_t *__restrict__ idx,
                                                        const int64_t *__restrict__ mask_off,
@@ -126,7 +170,10 @@ __global__ __launch_bounds__(64) void drill_sum_kernel(const float *__restrict__
                                                        const int32_t *__restrict__ tsel, int n_sel, int n_groups,
                                                        float nodata, float lo, float hi,
                                                        double *__restrict__ band_value,
-                                                       int32_t *__restrict__ band_count) {
+                                                       int32_t *__restrict__ band_count,
+                                                       float *__restrict__ emit_vals,
+                                                       const int32_t *__restrict__ emit_cb,
+                                                       uint4 *__restrict__ emit_stats) {
   const int item = blockIdx.x;
   const int p = order[item / n_groups];
   const int j = (item % n_groups) * 64 + threadIdx.x;
@@ -134,7 +181,20 @@ __global__ __launch_bounds__(64) void drill_sum_kernel(const float *__restrict__
   const int t = active ? tsel[j] : 0;
   float sum = 0.f;
   int32_t total = 0;
-  drill_walk<PC>(stack + t, t_stride, idx + mask_off[p], 0, count[p], nodata, lo, hi, sum, total);
+  if constexpr (EMIT) {
+    __shared__ float T[32 * 65];
+    const int n = count[p];
+    const int64_t npad = (int64_t)(n + 63) / 64 * 64;
+    const int g0 = (item % n_groups) * 64;
+    float *rows = emit_vals + (int64_t)emit_cb[p] * 64 * n_sel + (int64_t)g0 * npad;
+    uint32_t ka = 0xFFFFFFFFu, ko = 0u;
+    int32_t valid = 0;
+    drill_walk_emit<PC>(stack + t, t_stride, idx + mask_off[p], n, nodata, lo, hi, sum, total, rows, npad,
+                        min(64, n_sel - g0), T, ka, ko, valid);
+    if (active) emit_stats[(int64_t)p * n_sel + j] = make_uint4(ka, ko, (uint32_t)valid, 0u);
+  } else {
+    drill_walk<PC>(stack + t, t_stride, idx + mask_off[p], 0, count[p], nodata, lo, hi, sum, total);
+  }
   if (!active) return;
   const int64_t o = (int64_t)p * n_sel + j;
   band_value[o] = total > 0 ? (double)(sum / (float)total) : 0.0;   // drill.go:172-177
@@ -432,12 +492,12 @@ int launch_drill_batch(const DrillCall &c) {
                                                      c.n_polys, 0, 32, s) != hipSuccess)
       return GSKYHIP_E_HIP;
     const dim3 grid((unsigned)((int64_t)c.n_polys * n_groups));
-    if (pc)
-      hipLaunchKernelGGL(drill_sum_kernel<true>, grid, dim3(64), 0, s, c.stack, c.t_stride, w.idx, c.mask_off,
-                         w.count, w.order, w.tsel, n_sel, n_groups, c.nodata, c.lo, c.hi, bv, bc);
-    else
-      hipLaunchKernelGGL(drill_sum_kernel<false>, grid, dim3(64), 0, s, c.stack, c.t_stride, w.idx, c.mask_off,
-                         w.count, w.order, w.tsel, n_sel, n_groups, c.nodata, c.lo, c.hi, bv, bc);
+    const bool emit = c.emit_vals != nullptr;
+    if (emit) launch_decile_chunk_scan(w.count, c.n_polys, c.emit_chunk_base, s);
+    auto *kf = emit ? (pc ? drill_sum_kernel<true, true> : drill_sum_kernel<false, true>)
+                    : (pc ? drill_sum_kernel<true, false> : drill_sum_kernel<false, false>);
+    hipLaunchKernelGGL(kf, grid, dim3(64), 0, s, c.stack, c.t_stride, w.idx, c.mask_off, w.count, w.order, w.tsel,
+                       n_sel, n_groups, c.nodata, c.lo, c.hi, bv, bc, c.emit_vals, c.emit_chunk_base, c.emit_stats);
   } else {
     hipLaunchKernelGGL(drill_seg_scan_kernel, dim3(1), dim3(1024), 0, s, w.count, c.n_polys, w.seg_base);
     const int64_t n_seg_max = c.mask_bytes / kSeg + c.n_polys;
@@ -472,6 +532,10 @@ struct ReadWs {
   void *mean_ws, *dec_ws;
   int64_t mean_bytes, dec_bytes, total;
   int chunk;
+  bool fused;   // mode 0 with deciles: the mean pass writes the band-major rows (DrillCall::emit_*)
+  float *f_vals;
+  int32_t *f_cb;
+  uint4 *f_stats;
 };
 
 static ReadWs read_carve(void *base, int n_polys, int64_t mask_bytes, int n_list, int band_strides, int dc,
@@ -485,7 +549,20 @@ static ReadWs read_carve(void *base, int n_polys, int64_t mask_bytes, int n_list
 #endif
   w.chunk = (int)std::max<int64_t>(1, std::min<int64_t>(n_sel, (1LL << ws_log2) / std::max<int64_t>(1, mask_bytes)));
   w.mean_bytes = drill_workspace_size(np, mask_bytes, n_sel, 1, mode);
-  w.dec_bytes = dc > 0 ? drill_deciles_workspace_size(np, mask_bytes, w.chunk) : 0;
+  // fused: every read band's rows at once, up to 2^33 values (32 GB of the 288)
+  int fused_log2 = 33;
+#ifdef GSKYHIP_AB
+  if (const char *e = getenv("GSKYHIP_DEC_FUSED_LOG2")) fused_log2 = std::max(0, std::min(36, atoi(e)));
+#endif
+  const int64_t f_vals = (mask_bytes + 64 * (int64_t)np) * n_sel;
+  w.fused = mode == 0 && dc > 0 && fused_log2 > 0 && f_vals <= (1LL << fused_log2);
+  int64_t f_cb = 0, f_st = 0, f_end = 0;
+  if (w.fused) {
+    f_cb = al256(4 * f_vals);
+    f_st = f_cb + al256(4 * (mask_bytes / 64 + np + 1));
+    f_end = f_st + al256(16 * (int64_t)np * n_sel);
+  }
+  w.dec_bytes = dc <= 0 ? 0 : w.fused ? f_end : drill_deciles_workspace_size(np, mask_bytes, w.chunk);
   int64_t off = 0;
   auto take = [&](int64_t bytes) { const int64_t o = off; off = al256(off + (bytes > 0 ? bytes : 0)); return o; };
   const int64_t o_bv = take(8 * (int64_t)np * n_sel);
@@ -499,6 +576,9 @@ static ReadWs read_carve(void *base, int n_polys, int64_t mask_bytes, int n_list
   w.sel_dummy = nullptr;
   w.bv = (double *)(b + o_bv); w.bc = (int32_t *)(b + o_bc); w.dst = (int32_t *)(b + o_dst);
   w.dec = (float *)(b + o_dec); w.mean_ws = b + o_mw; w.dec_ws = b + o_dw;
+  w.f_vals = w.fused ? (float *)(b + o_dw) : nullptr;
+  w.f_cb = w.fused ? (int32_t *)(b + o_dw + f_cb) : nullptr;
+  w.f_stats = w.fused ? (uint4 *)(b + o_dw + f_st) : nullptr;
   return w;
 }
 
@@ -532,9 +612,15 @@ int launch_drill_read_data(const ReadDataCall &c) {
   m.pixel_count = c.pixel_count; m.band_strides = 1; m.mode = c.mode;
   m.out_value = w.bv; m.out_count = w.bc; m.workspace = w.mean_ws; m.workspace_bytes = w.mean_bytes;
   m.stream = c.stream;
+  if (w.fused) { m.emit_vals = w.f_vals; m.emit_chunk_base = w.f_cb; m.emit_stats = w.f_stats; }
   int rc = launch_drill_batch(m);
   if (rc) return rc;
-  if (c.decile_count > 0) {
+  if (c.decile_count > 0 && w.fused) {
+    const DrillWs mw = drill_carve(w.mean_ws, c.n_polys, c.mask_bytes, n_sel, 1, c.mode);
+    if ((rc = launch_decile_select_fused(w.f_vals, w.f_cb, mw.count, w.bc, c.n_polys, n_sel, c.decile_count,
+                                         c.nodata, w.f_stats, w.dec, w.dst, c.stream)))
+      return rc;
+  } else if (c.decile_count > 0) {
     DecileCall d;
     d.stack = c.stack; d.xsize = c.xsize; d.ysize = c.ysize; d.n_bands = c.n_bands; d.t_stride = c.t_stride;
     d.win = c.win; d.mask_off = c.mask_off; d.masks = c.masks; d.n_polys = c.n_polys; d.mask_bytes = c.mask_bytes;

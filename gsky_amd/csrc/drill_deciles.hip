@@ -64,10 +64,7 @@ static_assert(kBins % kSelThreads == 0, "the bucket scan gives each thread kBins
 static_assert(kMaxRanks * kCandMax <= kBins, "candidates reuse the bucket histogram");
 constexpr int kTilePad = 65;         // LDS tile row pitch (floats): conflict-free transposed reads
 
-__device__ __forceinline__ uint32_t fkey(float f) {   // order-preserving key of a float
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
+__device__ __forceinline__ uint32_t fkey(float f) { return order_key(f); }
 __device__ __forceinline__ float fdecode(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
@@ -147,7 +144,8 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
                                                                const ChunkRec *__restrict__ rec,
                                                                const int32_t *__restrict__ chunk_base, int n_polys,
                                                                const int32_t *__restrict__ tsel, int n_chunk,
-                                                               int n_groups, float *__restrict__ vals) {
+                                                               int n_groups, float *__restrict__ vals, float nodata,
+                                                               uint4 *__restrict__ part) {
   constexpr int kPad = kTrBands + 1;
   __shared__ float tile[4][64 * kPad];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -177,6 +175,19 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
     }
 #pragma unroll
     for (int u = 0; u < 32; u++) T[(2 * u + half) * kPad + bl] = v[u];
+    if (part) {   // the select's first pass, per (chunk, band): smallest / largest key, count of non-nodata values
+      uint32_t pa = 0xFFFFFFFFu, po = 0u, pc = 0u;
+#pragma unroll
+      for (int u = 0; u < 32; u++) {
+        const bool ok = 2 * u + half < m && v[u] != nodata;
+        const uint32_t k = fkey(v[u]);
+        if (ok) { pa = min(pa, k); po = max(po, k); pc++; }
+      }
+      pa = min(pa, (uint32_t)__shfl_xor(pa, 32));
+      po = max(po, (uint32_t)__shfl_xor(po, 32));
+      pc += (uint32_t)__shfl_xor(pc, 32);
+      if (half == 0 && bl < nb) part[(int64_t)ch * n_chunk + g * kTrBands + bl] = make_uint4(pa, po, pc, 0u);
+    }
   }
   wave_lds_sync();
   const int64_t npad = (int64_t)(n + kDecChunk - 1) / kDecChunk * kDecChunk;   // aligned band rows
@@ -207,7 +218,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                                                                     int32_t *__restrict__ status,
                                                                     const float *__restrict__ stack, int t_stride,
                                                                     const int32_t *__restrict__ pix_idx,
-                                                                    const int32_t *__restrict__ tsel, int n_seg) {
+                                                                    const int32_t *__restrict__ tsel, int n_seg,
+                                                                    const uint4 *__restrict__ part, int part_poly) {
   extern __shared__ uint32_t dyn[];
   uint32_t *cache = dyn + n_slots * 256;   // dyn[0, 2048): the buckets, then the candidates
   __shared__ uint32_t s_pref[kMaxRanks];   // rank r: its key, once resolved
@@ -251,13 +263,28 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   // their count, the bits all their keys share, and the segment's keys in
   // LDS while they fit (order is irrelevant to order statistics)
   const bool fits = n <= cache_keys;
+  // with the transpose's per-chunk partials there is no first pass: the
+  // first histogram pass streams the segment and fills the key cache
+  bool filled = part == nullptr;
   // keys of the values `v != nodata` rejects (-0.0 == 0.0; a NaN nodata rejects nothing)
   const bool skip_on = nodata == nodata;
   const uint32_t kn1 = fkey(nodata), kn2 = nodata == 0.0f ? fkey(-nodata) : kn1;
   auto skipk = [&](uint32_t k) { return skip_on && (k == kn1 || k == kn2); };
   uint32_t ka = 0xFFFFFFFFu, ko = 0u;   // smallest / largest valid key
   int valid = 0;   // kU: values per thread in flight per round
-  for (int i0 = 0; i0 < n; i0 += NT * kU) {
+  if (part && part_poly) {   // the fused mean pass's range and count of the whole segment
+    if (tid == 0) {
+      const uint4 q = part[o];
+      ka = q.x; ko = q.y; valid = (int)q.z;
+    }
+  } else if (part) {         // the transpose's per-chunk partials
+    const int cb = chunk_base[p], nc = (n + kDecChunk - 1) / kDecChunk;
+    for (int i = tid; i < nc; i += NT) {
+      const uint4 q = part[(int64_t)(cb + i) * n_chunk + j];
+      ka = min(ka, q.x); ko = max(ko, q.y); valid += (int)q.z;
+    }
+  }
+  for (int i0 = 0; i0 < (part ? 0 : n); i0 += NT * kU) {
     float v[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
@@ -297,7 +324,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   if (step == 0) {   // len <= dc (<= 16): sort the few values, repeat them in order
     if (tid == 0) {
       int m = 0;
-      if (fits) {
+      if (fits && filled) {
         for (int i = 0; i < n && m < len; i++)
           if (!skipk(cache[i])) s_small[m++] = fdecode(cache[i]);
       } else {
@@ -341,7 +368,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const int nr = s_nr;
   // every valid key once, from the LDS copy or streamed from the segment
   auto for_keys = [&](auto &&f) {
-    if (fits) {
+    if (fits && filled) {
       for (int i = tid; i < n; i += NT) {
         const uint32_t k = cache[i];
         if (!skipk(k)) f(k);
@@ -355,8 +382,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           v[u] = i < n ? ld(i) : nodata;
         }
 #pragma unroll
-        for (int u = 0; u < kU; u++)
-          if (i0 + u * NT + tid < n && v[u] != nodata) f(fkey(v[u]));
+        for (int u = 0; u < kU; u++) {
+          const int i = i0 + u * NT + tid;
+          if (!filled && fits && i < n) cache[i] = fkey(v[u]);
+          if (i < n && v[u] != nodata) f(fkey(v[u]));
+        }
       }
     }
   };
@@ -397,6 +427,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       if (k >= L && k <= Hk) atomicAdd(&H[(k - L) >> sh], 1u);
     });
     __syncthreads();
+    filled = true;
     {   // inclusive scan of the buckets in place, 4 per thread
       constexpr int BPT = kBins / NT;   // buckets per thread
       const int b4 = BPT * tid;
@@ -525,6 +556,7 @@ inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 struct DecWs {
   int32_t *idx, *count, *chunk_base, *tsel;
   ChunkRec *rec;
+  uint4 *part;   // per (chunk, band of the pass): the transpose's key range and count
   float *vals;
   int64_t total;
 };
@@ -540,6 +572,7 @@ DecWs decile_carve(void *base, int n_polys, int64_t mask_bytes, int chunk) {
   w.chunk_base = (int32_t *)take((mask_bytes / kDecChunk + n_polys + 1) * 4);
   w.tsel = (int32_t *)take((int64_t)chunk * 4);
   w.rec = (ChunkRec *)take((mask_bytes / kDecChunk + n_polys) * (int64_t)sizeof(ChunkRec));
+  w.part = (uint4 *)take((mask_bytes / kDecChunk + n_polys) * (int64_t)chunk * (int64_t)sizeof(uint4));
   w.vals = (float *)take(cap * 4);
   w.total = o;
   return w;
@@ -588,7 +621,9 @@ int launch_drill_deciles(const DecileCall &c) {
   if (const char *e = getenv("GSKYHIP_DEC_DIRECT")) direct = atoi(e) != 0;
 #endif
   int nt = kSelThreads;
+  bool use_part = true;
 #ifdef GSKYHIP_AB
+  if (const char *e = getenv("GSKYHIP_DEC_PART")) use_part = atoi(e) != 0;
   if (const char *e = getenv("GSKYHIP_DEC_NT")) nt = atoi(e) == 512 ? 512 : atoi(e) == 128 ? 128 : kSelThreads;
 #endif
   if (direct) {   // no transposed copy: a launch per band chunk straight from the stack
@@ -600,7 +635,7 @@ int launch_drill_deciles(const DecileCall &c) {
       const unsigned grid = (unsigned)(((int64_t)n_seg + 7) / 8 * 8);
       hipLaunchKernelGGL((decile_select_kernel<kSelU, true>), dim3(grid), dim3(kSelThreads), dyn_lds, s, w.vals,
                          c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status, c.stack, c.t_stride, w.idx, w.tsel, n_seg);
+                         cache_keys, c.out, c.status, c.stack, c.t_stride, w.idx, w.tsel, n_seg, nullptr, 0);
     }
     return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
   }
@@ -613,28 +648,52 @@ int launch_drill_deciles(const DecileCall &c) {
     const int64_t items = max_chunks * n_groups;
     hipLaunchKernelGGL(decile_transpose_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, c.stack,
                        c.t_stride, w.idx, w.rec, w.chunk_base, c.n_polys, w.tsel, n_chunk, n_groups,
-                       w.vals);
+                       w.vals, c.nodata, use_part ? w.part : nullptr);
     if (nt == 512)
       hipLaunchKernelGGL((decile_select_kernel<16, false, 512>), dim3((unsigned)n_seg), dim3(512), dyn_lds, s,
                          w.vals, c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
-                         n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
+                         n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
+                         use_part ? (const uint4 *)w.part : nullptr, 0);
     else if (nt == 128)
       hipLaunchKernelGGL((decile_select_kernel<16, false, 128>), dim3((unsigned)n_seg), dim3(128), dyn_lds, s,
                          w.vals, c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
-                         n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
+                         n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
+                         use_part ? (const uint4 *)w.part : nullptr, 0);
     else if (sel_u == 16)
       hipLaunchKernelGGL((decile_select_kernel<16, false, kSelThreads, 1>), dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
                          c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
+                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
+                         use_part ? (const uint4 *)w.part : nullptr, 0);
     else if (sel_u == 4)
       hipLaunchKernelGGL((decile_select_kernel<8, false, kSelThreads, 1>), dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
                          c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
+                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
+                         use_part ? (const uint4 *)w.part : nullptr, 0);
     else
       hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe>), dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
                          c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0);
+                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
+                         use_part ? (const uint4 *)w.part : nullptr, 0);
   }
+  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+}
+
+void launch_decile_chunk_scan(const int32_t *count, int n_polys, int32_t *chunk_base, hipStream_t s) {
+  hipLaunchKernelGGL(decile_chunk_scan_kernel, dim3(1), dim3(1024), 0, s, count, n_polys, chunk_base);
+}
+
+int launch_decile_select_fused(const float *vals, const int32_t *chunk_base, const int32_t *count,
+                               const int32_t *totals, int n_polys, int n_sel, int decile_count, float nodata,
+                               const uint4 *stats, float *out, int32_t *status, hipStream_t s) {
+  if (n_polys <= 0 || n_sel <= 0) return 0;
+  if (decile_count < 1 || 2 * decile_count > kMaxRanks) return GSKYHIP_E_ARG;
+  const int64_t n_seg = (int64_t)n_polys * n_sel;
+  if (n_seg >= 2147483647LL) return GSKYHIP_E_ARG;
+  const int n_slots = kHistSlots;
+  const int cache_keys = (kSelLds - n_slots * 256 * 4) / 4;
+  hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe>), dim3((unsigned)n_seg),
+                     dim3(kSelThreads), (size_t)kSelLds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
+                     decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 
