@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) void tiff_rows_kernel(const uint8_t *const *__
   const uint8_t *src = bands[b];
   for (int x = 0; x < bx; x++) {
     const int gx = tx * bx + x;
-    const bool in = gx < width && y < height;
+    const bool in = src && gx < width && y < height;   // no source: an EmptyTile band, all `pad`
     for (int k = 0; k < ts; k++) line[x * ts + k] = in ? src[((int64_t)y * width + gx) * ts + k] : pad[b * 8 + k];
   }
   len[r] = packbits_row(line, rb, enc + r * slot);
@@ -834,12 +834,23 @@ int gskyhip_encode_geotiff(const void *const *bands, int n_bands, int dtype, int
   int32_t *len = (int32_t *)(enc + n_rows * slot);
   const uint8_t **d_bands = (const uint8_t **)(((uintptr_t)(len + n_rows) + 15) & ~(uintptr_t)15);
   uint8_t *d_pad = (uint8_t *)(d_bands + n_bands);
-  // edge-tile padding: the band's nodata in the band type (0 without one)
+  // EncodeGdal (ogc_encoders.go:357-436) skips EmptyTile bands: no nodata, no
+  // long_name, no pixels -- GTiff fills their blocks at close with the
+  // dataset nodata, the last value SetNoDataValue stored (one per GeoTIFF).
+  std::vector<char> empty((size_t)n_bands, 0);
+  int last_nd = -1;   // the band whose nodata the file keeps
+  for (int b = 0; b < n_bands; b++) {
+    empty[b] = names && names[b] && std::strncmp(names[b], "EmptyTile", 9) == 0;
+    if (!empty[b] && nodata) last_nd = b;
+  }
+  // edge-tile padding: the band's nodata in the band type (0 without one);
+  // an EmptyTile band is all the dataset nodata
   std::vector<char> meta((size_t)n_bands * 8 + (size_t)n_bands * 8, 0);
   std::memcpy(meta.data(), bands, (size_t)n_bands * 8);
   for (int b = 0; b < n_bands; b++) {
     uint8_t *pb = (uint8_t *)meta.data() + (size_t)n_bands * 8 + 8 * b;
-    const double v = nodata ? nodata[b] : 0.0;
+    if (empty[b]) std::memset(meta.data() + 8 * (size_t)b, 0, 8);
+    const double v = empty[b] ? (last_nd >= 0 ? nodata[last_nd] : 0.0) : nodata ? nodata[b] : 0.0;
     if (dtype == GSKYHIP_FLOAT32) { const float f = (float)v; std::memcpy(pb, &f, 4); }
     else if (ts == 2) { const int16_t h = (int16_t)(dtype == GSKYHIP_UINT16 ? (int32_t)(uint16_t)v : (int32_t)v); std::memcpy(pb, &h, 2); }
     else pb[0] = (uint8_t)(int)v;
@@ -876,14 +887,19 @@ int gskyhip_encode_geotiff(const void *const *bands, int n_bands, int dtype, int
   ents.push_back(tiff_long(257, (uint32_t)height));
   ents.push_back(tiff_shorts(258, std::vector<uint16_t>((size_t)n_bands, (uint16_t)(8 * ts))));
   ents.push_back(tiff_shorts(259, {32773}));   // PackBits
-  ents.push_back(tiff_shorts(262, {1}));       // BlackIsZero
+  // GTiff Create's default photometric: RGB for 3 or 4 Byte bands (the 4th
+  // an associated alpha extra sample), MinIsBlack otherwise
+  const bool byte = dtype == GSKYHIP_BYTE || dtype == GSKYHIP_SIGNEDBYTE;
+  const bool rgb = byte && (n_bands == 3 || n_bands == 4);
+  ents.push_back(tiff_shorts(262, {(uint16_t)(rgb ? 2 : 1)}));
   ents.push_back(tiff_shorts(277, {(uint16_t)n_bands}));
   ents.push_back(tiff_shorts(284, {(uint16_t)(n_bands > 1 ? 2 : 1)}));   // INTERLEAVE=BAND
   ents.push_back(tiff_long(322, (uint32_t)block_x));
   ents.push_back(tiff_long(323, (uint32_t)block_y));
   ents.push_back(tiff_long8s(324, toff));
   ents.push_back(tiff_long8s(325, tcnt));
-  if (n_bands > 1) ents.push_back(tiff_shorts(338, std::vector<uint16_t>((size_t)n_bands - 1, 0)));
+  if (rgb && n_bands == 4) ents.push_back(tiff_shorts(338, {1}));
+  else if (!rgb && n_bands > 1) ents.push_back(tiff_shorts(338, std::vector<uint16_t>((size_t)n_bands - 1, 0)));
   ents.push_back(tiff_shorts(339, std::vector<uint16_t>((size_t)n_bands, fmt)));
   if (geot[2] == 0.0 && geot[4] == 0.0) {
     ents.push_back(tiff_doubles(33550, {geot[1], -geot[5], 0.0}));
@@ -900,14 +916,14 @@ int gskyhip_encode_geotiff(const void *const *bands, int n_bands, int dtype, int
   if (names) {   // GDALSetMetadataItem("long_name", NameSpace) per band
     std::string md = "<GDALMetadata>\n";
     for (int b = 0; b < n_bands; b++)
-      if (names[b])
+      if (names[b] && !empty[b])
         md += "  <Item name=\"long_name\" sample=\"" + std::to_string(b) + "\">" + xml_escape(names[b]) + "</Item>\n";
     md += "</GDALMetadata>";
     ents.push_back(tiff_ascii(42112, md));
   }
-  if (nodata) {   // GDAL_NODATA (a single dataset value in GeoTIFF: band 1's)
+  if (last_nd >= 0) {   // GDAL_NODATA: a single dataset value, the last band's that set one
     char buf[64];
-    std::snprintf(buf, sizeof(buf), "%.18g", nodata[0]);
+    std::snprintf(buf, sizeof(buf), "%.18g", nodata[last_nd]);
     ents.push_back(tiff_ascii(42113, buf));
   }
   std::sort(ents.begin(), ents.end(), [](const TiffEntry &a, const TiffEntry &b) { return a.tag < b.tag; });

@@ -46,7 +46,10 @@ class DrillStack:
             raise ValueError("stack must be (n_bands, ysize, xsize)")
         nb, ys, xs = bands.shape
         self.n_bands, self.ysize, self.xsize = nb, ys, xs
-        self.t_stride = (nb + 31) // 32 * 32   # 128-byte pixel rows: a slice group never straddles an extra line
+        # many slices: 128-byte pixel rows, so a 32-slice group never straddles
+        # an extra line; few slices: 16 bytes (padding to 32 would multiply a
+        # 1-band stack's HBM by 32)
+        self.t_stride = (nb + 31) // 32 * 32 if nb > 16 else (nb + 3) // 4 * 4
         dev = torch.device(device or "cuda")
         st = torch.zeros((ys, xs, self.t_stride), dtype=torch.float32, device=dev)
         st[:, :, :nb] = bands.to(dev, torch.float32).permute(1, 2, 0)

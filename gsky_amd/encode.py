@@ -66,7 +66,7 @@ def encode_geotiff(bands: Sequence[torch.Tensor], geot: Sequence[float], epsg: i
         raise ValueError("encode_geotiff: bad size / block")
     out = np.empty(cap, np.uint8)
     size = C.c_int64(0)
-    ptrs = (C.c_void_p * n)(*[b.data_ptr() for b in bands])
+    ptrs = (C.c_void_p * n)(*[b.data_ptr() for b in bands])   # EmptyTile bands: skipped by the writer
     gt = (C.c_double * 6)(*[float(v) for v in geot])
     nd = np.asarray(nodata, np.float64) if nodata is not None else None
     nm = (C.c_char_p * n)(*[s.encode() for s in names]) if names is not None else None

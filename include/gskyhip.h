@@ -423,8 +423,12 @@ int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, i
  * INTERLEAVE=BAND, BLOCKXSIZE / BLOCKYSIZE (ows.go passes 1024 x 256),
  * PIXELTYPE=SIGNEDBYTE for int8; the geotransform (ModelPixelScale +
  * ModelTiepoint, ModelTransformation when rotated), EPSG code as GeoKeys,
- * per-band long_name (GDAL_METADATA) and nodata (GDAL_NODATA, band 1's value:
- * GeoTIFF holds one).
+ * per-band long_name (GDAL_METADATA) and nodata (GDAL_NODATA: GeoTIFF holds
+ * one, the last band's value), Photometric RGB for 3 or 4 Byte bands (the 4th
+ * an associated alpha), MinIsBlack otherwise.  A band whose name starts with
+ * "EmptyTile" is skipped as EncodeGdal skips it (ogc_encoders.go:364): no
+ * nodata, no long_name, its pointer may be NULL and its samples are the
+ * dataset nodata (0 without one).
  *   bands: HOST array of n_bands dev pointers, each height x width samples of
  *     dtype (GSKYHIP_BYTE / SIGNEDBYTE / INT16 / UINT16 / FLOAT32), row-major;
  *   geot: HOST 6 doubles (GDAL order); epsg <= 0 writes no GeoKeys;

@@ -136,6 +136,9 @@ def test_geotiff_roundtrip(dtype, w, h, nb):
     kd = {keys[4 + 4 * i]: keys[4 + 4 * i + 3] for i in range(keys[3])}
     assert kd == {1024: 1, 1025: 1, 3072: 3577}
     assert float(tags[42113]) == nodata[0]
+    rgb = dtype in ("uint8", "int8") and nb in (3, 4)   # GTiff Create's default photometric
+    assert tags[262] == [2 if rgb else 1]
+    assert (338 in tags) == (nb > 1 and not rgb)
     for i in range(nb):
         assert ('<Item name="long_name" sample="%d">band_%d&amp;&lt;x&gt;</Item>' % (i, i)) in tags[42112]
     got = decode_bands(buf, tags)
@@ -156,3 +159,29 @@ def test_geotiff_geographic_rotated():
     assert kd == {1024: 2, 1025: 1, 2048: 4326}
     assert 42112 not in tags and 42113 not in tags
     np.testing.assert_array_equal(decode_bands(buf, tags)[0], a.cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_geotiff_empty_tile_bands_rgba():
+    """EncodeGdal skips EmptyTile bands (ogc_encoders.go:364-366): no nodata,
+    no long_name, no pixels -- GTiff fills them with the dataset nodata, the
+    last value SetNoDataValue stored.  4 Byte bands: RGB + associated alpha
+    (GTiff Create's default; parity unpinned: no GDAL in the image)."""
+    import torch
+    from gsky_amd.encode import encode_geotiff
+    rng = np.random.default_rng(7)
+    arrs = [rng.integers(0, 255, size=(40, 70), endpoint=True).astype(np.uint8) for _ in range(4)]
+    dev = [torch.from_numpy(a).cuda() for a in arrs]
+    names = ["red", "EmptyTile_green", "blue", "EmptyTile"]
+    nodata = [1.0, 2.0, 7.0, 9.0]
+    buf = encode_geotiff(dev, [0.0, 1.0, 0.0, 0.0, 0.0, -1.0], 4326, nodata, names, block=(32, 16))
+    tags = read_bigtiff(buf)
+    assert tags[262] == [2] and tags[338] == [1]
+    assert float(tags[42113]) == 7.0                     # "blue": the last band that set one
+    md = tags[42112]
+    assert 'sample="0">red<' in md and 'sample="2">blue<' in md
+    assert "sample=\"1\"" not in md and "sample=\"3\"" not in md
+    got = decode_bands(buf, tags)
+    np.testing.assert_array_equal(got[0], arrs[0])
+    np.testing.assert_array_equal(got[2], arrs[2])
+    assert (got[1] == 7).all() and (got[3] == 7).all()
