@@ -350,6 +350,14 @@ def run_c2(ctx: Ctx, args):
         pngs = encode_png(sub, sizes, n_threads=threads)
         pt = time.perf_counter() - t0
         raw = sum(w * h * 4 for w, h in sizes)
+        # fixed Huffman codes only (round 4's first GPU deflate) on the same tiles
+        os.environ["GSKYHIP_PNG_FIXED"] = "1"
+        try:
+            t0 = time.perf_counter()
+            fp = encode_png(sub, sizes, n_threads=threads)
+            ft = time.perf_counter() - t0
+        finally:
+            del os.environ["GSKYHIP_PNG_FIXED"]
         # the round-3 path beside it: zlib level 6 on the host threads
         zs = sub[: max(2, len(sample) // 4)]
         os.environ["GSKYHIP_PNG_ZLIB"] = "1"
@@ -362,11 +370,14 @@ def run_c2(ctx: Ctx, args):
         out["png"] = {"tiles": len(sample), "threads": threads, "tiles_per_s": round(len(sample) / pt, 1),
                       "rgba_MB_per_s": round(raw / pt / 1e6, 1), "png_bytes_mean": int(np.mean([len(b) for b in pngs])),
                       "projected_batch_s": round(len(ids) / (len(sample) / pt), 3),
+                      "fixed_codes": {"tiles_per_s": round(len(sample) / ft, 1),
+                                      "png_bytes_mean": int(np.mean([len(b) for b in fp]))},
                       "zlib_host": {"tiles": int(zs.shape[0]), "tiles_per_s": round(zs.shape[0] / zt, 1),
                                     "png_bytes_mean": int(np.mean([len(b) for b in zp])),
                                     "same_tiles_gpu_bytes_mean": int(np.mean([len(b) for b in pngs[: zs.shape[0]]]))},
                       "timing": "gskyhip_encode_png of %d covered C2 tiles already rendered in HBM: GPU colour-type "
-                                "+ filter pass, GPU deflate (fixed Huffman, row-distance LZ77) + IDAT CRC-32, PNG framing on "
+                                "+ filter pass, GPU deflate (row-distance LZ77, per-tile dynamic Huffman codes or the fixed ones where "
+                                "shorter) + IDAT CRC-32, PNG framing on "
                                 "%d host threads, host wall; zlib_host = the same tiles through host zlib level 6"
                                 % (len(sample), threads)}
         del sub, rgba

@@ -149,7 +149,9 @@ __global__ __launch_bounds__(256) void png_filter_kernel(const uint8_t *__restri
 
 // ------------------------------------------------------------------ GPU deflate
 // The zlib stream of each tile's filtered rows built on the GPU: one final
-// block of fixed Huffman codes (RFC 1951 3.2.6) whose LZ77 matches are
+// block -- Huffman codes built for the tile from its symbol frequencies
+// (RFC 1951 3.2.7), or the fixed codes (3.2.6) where those come out shorter
+// -- whose LZ77 matches are
 // searched at the distances a PNG row offers -- 1 (runs), the pixel size
 // (the pixel to the left) and the row stride (the pixel above) -- greedily,
 // longest first, within the row (so rows are encoded independently: a
@@ -209,11 +211,11 @@ __device__ __forceinline__ void lit_code(int v, uint32_t &code, int &len) {
   code = rev_bits(code, len);
 }
 
-// One row's tokens: bits returned; WRITE emits them into `bs`.
-template <bool WRITE>
-__device__ uint32_t deflate_row(const uint8_t *__restrict__ data, int64_t p0, int64_t p1, int bpp, int stride,
-                                BitSink &bs) {
-  uint32_t bits = 0;
+// One row's LZ77 tokens, in order, to f(sym, len_extra, n_len_extra, dcode,
+// dist_extra, n_dist_extra): dcode < 0 for a literal.
+template <class F>
+__device__ __forceinline__ void deflate_tokens(const uint8_t *__restrict__ data, int64_t p0, int64_t p1, int bpp,
+                                               int stride, F &&f) {
   int64_t p = p0;
   while (p < p1) {
     int best = 0, bd = 0;
@@ -239,54 +241,169 @@ __device__ uint32_t deflate_row(const uint8_t *__restrict__ data, int64_t p0, in
       while (lc < 28 && kLenBase[lc + 1] <= best) lc++;
       int dc = 0;
       while (dc < 29 && kDistBase[dc + 1] <= bd) dc++;
-      uint32_t code;
-      int len;
-      lit_code(257 + lc, code, len);
-      const int le = kLenExtra[lc], de = kDistExtra[dc];
-      bits += len + le + 5 + de;
-      if (WRITE) {
-        bs.put(code, len);
-        if (le) bs.put((uint32_t)(best - kLenBase[lc]), le);
-        bs.put(rev_bits((uint32_t)dc, 5), 5);
-        if (de) bs.put((uint32_t)(bd - kDistBase[dc]), de);
-      }
+      f(257 + lc, (uint32_t)(best - kLenBase[lc]), (int)kLenExtra[lc], dc, (uint32_t)(bd - kDistBase[dc]),
+        (int)kDistExtra[dc]);
       p += best;
     } else {
-      uint32_t code;
-      int len;
-      lit_code(data[p], code, len);
-      bits += len;
-      if (WRITE) bs.put(code, len);
+      f((int)data[p], 0u, 0, -1, 0u, 0);
       p++;
     }
   }
-  return bits;
 }
 
-// Pass 1: per row its bits and Adler-32 sums; per tile the stream length.
-// Tile stream: zlib header (2 B), block header (3 bits), rows, end of block
-// (7 bits), pad to a byte, Adler-32 (4 B).
+// ---- per-tile Huffman codes (round 4: one dynamic block per tile, RFC 1951
+// 3.2.7, or the fixed codes where those are shorter)
+constexpr int kLitN = 286, kDistN = 30, kClN = 19, kSymN = kLitN + kDistN;
+__constant__ uint8_t kClOrder[kClN] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct PngTab {   // a tile's codes (global, written by pass 1, read by pass 2)
+  uint32_t hdr[160];        // the block header, LSB-first: BFINAL, BTYPE and (dynamic) the code lengths
+  uint16_t code[kSymN];     // literal / length codes then distance codes, bit-reversed
+  uint8_t len[kSymN];
+  int32_t hdr_bits;
+};
+
+struct HuffLds {   // scratch of one code construction (thread 0 but the rank sort)
+  uint32_t wf[kLitN];       // frequencies, at least two of them non-zero
+  int16_t sorted[kLitN];    // symbols by ascending (frequency, symbol)
+  uint32_t weight[2 * kLitN];
+  int16_t parent[2 * kLitN];
+  uint8_t depth[2 * kLitN];
+  int32_t m, ok;
+};
+
+// Code lengths <= maxbits of the n symbols with frequencies `freq` (a
+// Huffman tree by the two-queue merge over the sorted leaves; lengths past
+// maxbits folded back as zlib's gen_bitlen does; least frequent symbols take
+// the longest codes).  All threads call it; H.ok = 0 if the result is not a
+// complete prefix code (the caller then uses the fixed codes).
+__device__ void huff_lengths(const uint32_t *freq, int n, int maxbits, uint8_t *len, HuffLds &H) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int m = 0;
+    for (int s = 0; s < n; s++) { H.wf[s] = freq[s]; m += freq[s] ? 1 : 0; }
+    for (int s = 0; m < 2 && s < n; s++)   // a code needs two leaves (zlib forces them too)
+      if (!H.wf[s]) { H.wf[s] = 1; m++; }
+    H.m = m;
+  }
+  __syncthreads();
+  for (int s = tid; s < n; s += blockDim.x) {   // rank of (freq, symbol) among the used symbols
+    len[s] = 0;
+    if (!H.wf[s]) continue;
+    const uint64_t key = ((uint64_t)H.wf[s] << 9) | (uint64_t)s;
+    int r = 0;
+    for (int q = 0; q < n; q++)
+      if (H.wf[q] && (((uint64_t)H.wf[q] << 9) | (uint64_t)q) < key) r++;
+    H.sorted[r] = (int16_t)s;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int m = H.m;
+    for (int i = 0; i < m; i++) H.weight[i] = H.wf[H.sorted[i]];
+    int il = 0, in = m, nx = m;   // leaf queue, internal queue (ascending by construction)
+    auto take = [&]() {
+      if (il < m && (in >= nx || H.weight[il] <= H.weight[in])) return il++;
+      return in++;
+    };
+    for (int k = 0; k < m - 1; k++) {
+      const int a = take(), b = take();
+      H.weight[nx] = H.weight[a] + H.weight[b];
+      H.parent[a] = (int16_t)nx; H.parent[b] = (int16_t)nx;
+      nx++;
+    }
+    const int root = nx - 1;
+    int bl_count[16] = {0};
+    int overflow = 0;
+    H.depth[root] = 0;
+    for (int i = root - 1; i >= 0; i--) {
+      const int d = H.depth[H.parent[i]] + 1;
+      H.depth[i] = (uint8_t)min(d, 255);
+      if (i < m) {
+        if (d > maxbits) overflow++;
+        bl_count[min(d, maxbits)]++;
+      }
+    }
+    while (overflow > 0) {   // zlib gen_bitlen: move leaves until the code fits
+      int bits = maxbits - 1;
+      while (bits > 0 && bl_count[bits] == 0) bits--;
+      if (bits == 0) break;
+      bl_count[bits]--;
+      bl_count[bits + 1] += 2;
+      bl_count[maxbits]--;
+      overflow -= 2;
+    }
+    // longest codes to the least frequent symbols
+    int i = 0;
+    for (int bits = maxbits; bits >= 1; bits--)
+      for (int c = bl_count[bits]; c > 0 && i < m; c--) len[H.sorted[i++]] = (uint8_t)bits;
+    uint64_t kraft = 0;   // complete: sum 2^(maxbits - len) == 2^maxbits
+    for (int s = 0; s < n; s++)
+      if (len[s]) kraft += 1ull << (maxbits - len[s]);
+    H.ok = (i == m && kraft == (1ull << maxbits)) ? 1 : 0;
+  }
+  __syncthreads();
+}
+
+// canonical codes (RFC 1951 3.2.2), bit-reversed for LSB-first output
+__device__ void huff_codes(const uint8_t *len, int n, uint16_t *code) {
+  int bl[16] = {0}, next[16];
+  for (int s = 0; s < n; s++) bl[len[s]]++;
+  bl[0] = 0;
+  int c = 0;
+  for (int b = 1; b < 16; b++) { c = (c + bl[b - 1]) << 1; next[b] = c; }
+  for (int s = 0; s < n; s++)
+    code[s] = len[s] ? (uint16_t)rev_bits((uint32_t)next[len[s]]++, len[s]) : 0;
+}
+
+__device__ void fixed_table(PngTab &T) {
+  for (int v = 0; v < kLitN; v++) {
+    uint32_t c;
+    int l;
+    lit_code(v, c, l);
+    T.code[v] = (uint16_t)c; T.len[v] = (uint8_t)l;
+  }
+  for (int d = 0; d < kDistN; d++) { T.code[kLitN + d] = (uint16_t)rev_bits((uint32_t)d, 5); T.len[kLitN + d] = 5; }
+  T.hdr[0] = 0x3u;   // BFINAL 1, BTYPE 01
+  T.hdr_bits = 3;
+}
+
+// Pass 1, a workgroup per tile: the rows' symbol frequencies and Adler-32
+// sums; the tile's dynamic code (or the fixed one where that is shorter,
+// header included) into tab[t]; each row's bits under it; the stream length.
+// Tile stream: zlib header (2 B), block header, rows, end of block, pad to a
+// byte, Adler-32 (4 B).
 __global__ __launch_bounds__(256) void png_deflate_count_kernel(const uint8_t *__restrict__ filt,
                                                                 const int64_t *__restrict__ off,
                                                                 const int32_t *__restrict__ wh,
                                                                 const int32_t *__restrict__ opaque, int max_h,
                                                                 int32_t *__restrict__ row_bits,
                                                                 uint32_t *__restrict__ adler,
-                                                                int64_t *__restrict__ zlen) {
-  const int t = blockIdx.x;
+                                                                int64_t *__restrict__ zlen, PngTab *__restrict__ tab,
+                                                                int dynamic) {
+  const int t = blockIdx.x, tid = threadIdx.x;
   const int w = wh[2 * t], h = wh[2 * t + 1];
   const int bpp = opaque[t] ? 3 : 4;
   const int stride = 1 + bpp * w;
   const uint8_t *data = filt + off[t];
   __shared__ uint32_t s_a[kPngMaxRows], s_b[kPngMaxRows];
   __shared__ int64_t s_bits[256];
-  int64_t mine = 0;
-  BitSink dummy;
-  for (int y = threadIdx.x; y < h; y += blockDim.x) {
+  __shared__ uint32_t s_freq[kSymN], s_clf[kClN];
+  __shared__ uint8_t s_len[kSymN], s_cll[kClN];
+  __shared__ uint16_t s_code[kSymN], s_clc[kClN];
+  __shared__ uint8_t s_rs[kSymN];     // code-length RLE: symbols
+  __shared__ uint8_t s_rx[kSymN];     // and their extra values
+  __shared__ int32_t s_nr, s_hlit, s_hdist, s_use_fixed;
+  __shared__ HuffLds H;
+  PngTab &T = tab[t];
+  for (int i = tid; i < kSymN; i += blockDim.x) s_freq[i] = 0;
+  __syncthreads();
+  for (int y = tid; y < h; y += blockDim.x) {
     const int64_t p0 = (int64_t)y * stride;
-    const uint32_t b = deflate_row<false>(data, p0, p0 + stride, bpp, stride, dummy);
-    row_bits[(int64_t)t * max_h + y] = (int32_t)b;
-    mine += b;
+    if (dynamic)
+      deflate_tokens(data, p0, p0 + stride, bpp, stride, [&](int sym, uint32_t, int, int dc, uint32_t, int) {
+        atomicAdd(&s_freq[sym], 1u);
+        if (dc >= 0) atomicAdd(&s_freq[kLitN + dc], 1u);
+      });
     uint64_t a = 0, bb = 0;   // sum of bytes, sum of (n - i) * byte (exact: < 2^40), then mod 65521
     int i = 0;
     for (; i + 4 <= stride; i += 4) {
@@ -303,9 +420,117 @@ __global__ __launch_bounds__(256) void png_deflate_count_kernel(const uint8_t *_
     s_a[y] = (uint32_t)(a % 65521u);
     s_b[y] = (uint32_t)(bb % 65521u);
   }
-  s_bits[threadIdx.x] = mine;
+  if (tid == 0) { s_freq[256] = 1; s_use_fixed = dynamic ? 0 : 1; }   // end of block
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (dynamic) {
+    huff_lengths(s_freq, kLitN, 15, s_len, H);
+    int ok = H.ok;
+    huff_lengths(s_freq + kLitN, kDistN, 15, s_len + kLitN, H);
+    ok &= H.ok;
+    if (tid == 0) {   // HLIT / HDIST, then the run-length coded lengths (16 / 17 / 18)
+      int hlit = kLitN, hdist = kDistN;
+      while (hlit > 257 && !s_len[hlit - 1]) hlit--;
+      while (hdist > 1 && !s_len[kLitN + hdist - 1]) hdist--;
+      s_hlit = hlit; s_hdist = hdist;
+      for (int k = 0; k < kClN; k++) s_clf[k] = 0;
+      const int N = hlit + hdist;
+      auto L = [&](int i) { return i < hlit ? s_len[i] : s_len[kLitN + i - hlit]; };
+      int nr = 0;
+      auto emit = [&](int sym, int x) { s_rs[nr] = (uint8_t)sym; s_rx[nr] = (uint8_t)x; nr++; s_clf[sym]++; };
+      for (int i = 0; i < N;) {
+        const int v = L(i);
+        int run = 1;
+        while (i + run < N && L(i + run) == v) run++;
+        int r = run;
+        if (v == 0) {
+          while (r >= 11) { const int k = min(r, 138); emit(18, k - 11); r -= k; }
+          if (r >= 3) { emit(17, r - 3); r = 0; }
+          while (r > 0) { emit(0, 0); r--; }
+        } else {
+          emit(v, 0); r--;
+          while (r >= 3) { const int k = min(r, 6); emit(16, k - 3); r -= k; }
+          while (r > 0) { emit(v, 0); r--; }
+        }
+        i += run;
+      }
+      s_nr = nr;
+    }
+    __syncthreads();
+    huff_lengths(s_clf, kClN, 7, s_cll, H);
+    ok &= H.ok;
+    if (tid == 0) {
+      huff_codes(s_len, kLitN, s_code);
+      huff_codes(s_len + kLitN, kDistN, s_code + kLitN);
+      huff_codes(s_cll, kClN, s_clc);
+      int hclen = kClN;
+      while (hclen > 4 && !s_cll[kClOrder[hclen - 1]]) hclen--;
+      int64_t hb = 3 + 5 + 5 + 4 + 3 * hclen;
+      for (int k = 0; k < s_nr; k++) {
+        const int sym = s_rs[k];
+        hb += s_cll[sym] + (sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0);
+      }
+      // compare with the fixed codes (extra bits are the same under both)
+      int64_t dyn = hb, fix = 3;
+      for (int v = 0; v < kLitN; v++) {
+        uint32_t c;
+        int l;
+        lit_code(v, c, l);
+        dyn += (int64_t)s_freq[v] * s_len[v];
+        fix += (int64_t)s_freq[v] * l;
+      }
+      for (int d = 0; d < kDistN; d++) {
+        dyn += (int64_t)s_freq[kLitN + d] * s_len[kLitN + d];
+        fix += (int64_t)s_freq[kLitN + d] * 5;
+      }
+      if (!ok || hb > 160 * 32 || fix <= dyn) {
+        s_use_fixed = 1;
+      } else {   // the header bits into tab[t].hdr
+        uint64_t acc = 0;
+        int nacc = 0, word = 0;
+        auto put = [&](uint32_t bits, int nb) {
+          acc |= (uint64_t)bits << nacc;
+          nacc += nb;
+          if (nacc >= 32) { T.hdr[word++] = (uint32_t)acc; acc >>= 32; nacc -= 32; }
+        };
+        put(0x5u, 3);   // BFINAL 1, BTYPE 10
+        put((uint32_t)(s_hlit - 257), 5);
+        put((uint32_t)(s_hdist - 1), 5);
+        put((uint32_t)(hclen - 4), 4);
+        for (int k = 0; k < hclen; k++) put(s_cll[kClOrder[k]], 3);
+        for (int k = 0; k < s_nr; k++) {
+          const int sym = s_rs[k];
+          put(s_clc[sym], s_cll[sym]);
+          if (sym == 16) put(s_rx[k], 2);
+          else if (sym == 17) put(s_rx[k], 3);
+          else if (sym == 18) put(s_rx[k], 7);
+        }
+        if (nacc > 0) T.hdr[word] = (uint32_t)acc;
+        T.hdr_bits = (int32_t)hb;
+      }
+    }
+    __syncthreads();
+  }
+  if (s_use_fixed) {
+    if (tid == 0) fixed_table(T);
+    __syncthreads();
+    for (int i = tid; i < kSymN; i += blockDim.x) { s_len[i] = T.len[i]; s_code[i] = T.code[i]; }
+  } else {
+    for (int i = tid; i < kSymN; i += blockDim.x) { T.len[i] = s_len[i]; T.code[i] = s_code[i]; }
+  }
+  __syncthreads();
+  int64_t mine = 0;
+  for (int y = tid; y < h; y += blockDim.x) {
+    const int64_t p0 = (int64_t)y * stride;
+    uint32_t b = 0;
+    deflate_tokens(data, p0, p0 + stride, bpp, stride, [&](int sym, uint32_t, int le, int dc, uint32_t, int de) {
+      b += s_len[sym] + le + (dc >= 0 ? s_len[kLitN + dc] + de : 0);
+    });
+    row_bits[(int64_t)t * max_h + y] = (int32_t)b;
+    mine += b;
+  }
+  s_bits[tid] = mine;
+  __syncthreads();
+  if (tid == 0) {
     int64_t total = 0;
     for (int k = 0; k < (int)blockDim.x; k++) total += s_bits[k];
     uint32_t A = 1, B = 0;   // adler32 of the rows in order
@@ -314,7 +539,8 @@ __global__ __launch_bounds__(256) void png_deflate_count_kernel(const uint8_t *_
       A = (A + s_a[y]) % 65521u;
     }
     adler[t] = (B << 16) | A;
-    zlen[t] = 2 + (3 + total + 7 + 7) / 8 + 4;
+    const int hdr_bits = s_use_fixed ? 3 : T.hdr_bits;
+    zlen[t] = 2 + (hdr_bits + total + s_len[256] + 7) / 8 + 4;
   }
 }
 
@@ -328,7 +554,8 @@ __global__ __launch_bounds__(256) void png_deflate_write_kernel(const uint8_t *_
                                                                 const uint32_t *__restrict__ adler,
                                                                 const int64_t *__restrict__ zoff,
                                                                 const int64_t *__restrict__ zlen,
-                                                                uint8_t *__restrict__ packed) {
+                                                                uint8_t *__restrict__ packed,
+                                                                const PngTab *__restrict__ tab) {
   const int t = blockIdx.x;
   const int w = wh[2 * t], h = wh[2 * t + 1];
   const int bpp = opaque[t] ? 3 : 4;
@@ -338,8 +565,13 @@ __global__ __launch_bounds__(256) void png_deflate_write_kernel(const uint8_t *_
   // the tile's stream starts on a 4-byte boundary of the packed buffer
   uint32_t *words = (uint32_t *)z;
   __shared__ int64_t s_start[kPngMaxRows + 1];
+  __shared__ uint16_t s_code[kSymN];
+  __shared__ uint8_t s_len[kSymN];
+  const PngTab &T = tab[t];
+  for (int i = threadIdx.x; i < kSymN; i += blockDim.x) { s_code[i] = T.code[i]; s_len[i] = T.len[i]; }
+  const int hdr_bits = T.hdr_bits;
   if (threadIdx.x == 0) {   // row bit offsets (serial: h <= 4096 adds)
-    int64_t b = 16 + 3;
+    int64_t b = 16 + hdr_bits;
     for (int y = 0; y < h; y++) { s_start[y] = b; b += row_bits[(int64_t)t * max_h + y]; }
     s_start[h] = b;
   }
@@ -349,14 +581,16 @@ __global__ __launch_bounds__(256) void png_deflate_write_kernel(const uint8_t *_
   if (threadIdx.x == 0) {
     or_byte(0, 0x78);   // CMF: deflate, 32 KiB window
     or_byte(1, 0x01);   // FLG: (0x78 * 256 + 0x01) % 31 == 0
-    BitSink bs;         // block header: BFINAL 1, BTYPE 01 (fixed codes)
+    BitSink bs;         // block header
     bs.init(words, 16);
-    bs.put(0x3u, 3);
+    int k = 0;
+    for (; k + 32 <= hdr_bits; k += 32) bs.put(T.hdr[k >> 5], 32);
+    if (k < hdr_bits) bs.put(T.hdr[k >> 5] & ((1u << (hdr_bits - k)) - 1u), hdr_bits - k);
     bs.finish();
     bs.init(words, s_start[h]);   // end of block
-    bs.put(0u, 7);
+    bs.put(s_code[256], s_len[256]);
     bs.finish();
-    const int64_t end = (s_start[h] + 7 + 7) / 8;   // Adler-32 after the byte padding
+    const int64_t end = (s_start[h] + s_len[256] + 7) / 8;   // Adler-32 after the byte padding
     const uint32_t ad = adler[t];
     or_byte(end, ad >> 24); or_byte(end + 1, ad >> 16); or_byte(end + 2, ad >> 8); or_byte(end + 3, ad);
   }
@@ -364,7 +598,15 @@ __global__ __launch_bounds__(256) void png_deflate_write_kernel(const uint8_t *_
     BitSink bs;
     bs.init(words, s_start[y]);
     const int64_t p0 = (int64_t)y * stride;
-    deflate_row<true>(data, p0, p0 + stride, bpp, stride, bs);
+    deflate_tokens(data, p0, p0 + stride, bpp, stride,
+                   [&](int sym, uint32_t lx, int le, int dc, uint32_t dx, int de) {
+                     bs.put(s_code[sym], s_len[sym]);
+                     if (dc >= 0) {
+                       if (le) bs.put(lx, le);
+                       bs.put(s_code[kLitN + dc], s_len[kLitN + dc]);
+                       if (de) bs.put(dx, de);
+                     }
+                   });
     bs.finish();
   }
   (void)zlen;
@@ -612,15 +854,17 @@ using namespace gsky;
 extern "C" {
 
 // Workspace: filtered rows | per-tile offsets, sizes, opacity | per-row bit
-// counts | Adler-32, zlib lengths and offsets | the packed zlib streams (at
-// most 9/8 of the filtered bytes + 16 per tile with fixed codes).
+// counts | Adler-32, zlib lengths and offsets | per-tile codes | the packed
+// zlib streams (at most 9/8 of the filtered bytes + 16 per tile: a dynamic
+// block is only used where it is shorter than the fixed one).
 static int64_t png_deflate_cap(int64_t per) { return (per * 9 + 7) / 8 + 64 + (per / 32768 + 1) * 4 + 256; }
 
 int64_t gskyhip_png_workspace_size(int n_tiles, int max_w, int max_h) {
   if (n_tiles <= 0 || max_w <= 0 || max_h <= 0) return 0;
   const int64_t per = (int64_t)max_h * (1 + 4 * (int64_t)max_w);
   const int64_t a = ((int64_t)n_tiles * per + 255) / 256 * 256 + (int64_t)n_tiles * (8 + 8 + 4) + 1024;
-  const int64_t b = ((int64_t)n_tiles * max_h * 4 + 255) / 256 * 256 + (int64_t)n_tiles * (4 + 8 + 8) + 1024;
+  const int64_t b = ((int64_t)n_tiles * max_h * 4 + 255) / 256 * 256 + (int64_t)n_tiles * (4 + 8 + 8) + 1024 +
+                    (int64_t)n_tiles * (int64_t)sizeof(PngTab) + 256;
   return a + b + (int64_t)n_tiles * png_deflate_cap(per) + 1024;
 }
 
@@ -678,10 +922,14 @@ int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, i
     uint32_t *d_adler = (uint32_t *)b;
     int64_t *d_zlen = (int64_t *)(b + (((int64_t)n_tiles * 4 + 7) & ~(int64_t)7));
     int64_t *d_zoff = d_zlen + n_tiles;
-    uint8_t *d_packed = (uint8_t *)(((uintptr_t)(d_zoff + n_tiles) + 255) & ~(uintptr_t)255);
+    PngTab *d_tab = (PngTab *)(((uintptr_t)(d_zoff + n_tiles) + 255) & ~(uintptr_t)255);
+    uint8_t *d_packed = (uint8_t *)(((uintptr_t)(d_tab + n_tiles) + 255) & ~(uintptr_t)255);
+    // per-tile dynamic Huffman codes where they are shorter (GSKYHIP_PNG_FIXED=1: fixed codes only)
+    const char *fx = std::getenv("GSKYHIP_PNG_FIXED");
+    const int dynamic = (fx && std::atoi(fx) != 0) ? 0 : 1;
     if ((char *)d_packed + (int64_t)n_tiles * png_deflate_cap(per) > ws + workspace_bytes) return GSKYHIP_E_ARG;
     hipLaunchKernelGGL(png_deflate_count_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, filt, d_off, d_wh, d_opq,
-                       max_h, d_rowbits, d_adler, d_zlen);
+                       max_h, d_rowbits, d_adler, d_zlen, d_tab, dynamic);
     std::vector<int64_t> zlen(n_tiles), zoff(n_tiles);
     std::vector<int32_t> opq(n_tiles);
     if (hipGetLastError() != hipSuccess ||
@@ -701,7 +949,7 @@ int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, i
         hipMemsetAsync(d_packed, 0, (size_t)std::max<int64_t>(total, 4), s) != hipSuccess)
       return GSKYHIP_E_HIP;
     hipLaunchKernelGGL(png_deflate_write_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, filt, d_off, d_wh, d_opq,
-                       max_h, d_rowbits, d_adler, d_zoff, d_zlen, d_packed);
+                       max_h, d_rowbits, d_adler, d_zoff, d_zlen, d_packed, d_tab);
     // IDAT CRCs behind the packed streams (the pinned read-back holds both)
     const int64_t crc_at = (total + 255) & ~(int64_t)255;
     const int64_t n_crc = (int64_t)n_tiles * max_chunks;
