@@ -1063,17 +1063,22 @@ int warp_operation_fast(const char *srcFilePath, char *srcProjRef, double *srcGe
   q.srs_cf = srsCf;
   WarpResp r;
   const char *svc = std::getenv("GSKYHIP_SERVICE");
-  if (svc && *svc) {
-    const int e = service_warp(svc, q, r);
+  if (svc && *svc) {   // the window arrives straight in the malloc'd buffer
+    void *mb = nullptr;
+    size_t ml = 0;
+    const int e = service_warp(svc, q, r, &mb, &ml);
     if (e) return e;
+    if (r.rc) { std::free(mb); return r.rc; }
+    *dstBuf = mb;
+    *dstBufSize = (int)ml;
   } else {
     warp_batch(&q, 1, &r);
+    if (r.rc) return r.rc;
+    *dstBufSize = (int)r.data.size();
+    *dstBuf = std::malloc(r.data.empty() ? 1 : r.data.size());
+    if (!*dstBuf) return GSKYHIP_E_ARG;
+    if (!r.data.empty()) std::memcpy(*dstBuf, r.data.data(), r.data.size());
   }
-  if (r.rc) return r.rc;
-  *dstBufSize = (int)r.data.size();
-  *dstBuf = std::malloc(r.data.empty() ? 1 : r.data.size());
-  if (!*dstBuf) return GSKYHIP_E_ARG;
-  if (!r.data.empty()) std::memcpy(*dstBuf, r.data.data(), r.data.size());
   for (int k = 0; k < 4; k++) dstBbox[k] = r.bbox[k];
   *noData = r.nodata;
   *dType = r.dtype;

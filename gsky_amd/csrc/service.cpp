@@ -4,6 +4,7 @@
 #include <errno.h>
 #include <signal.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <sys/un.h>
 #include <unistd.h>
 
@@ -78,6 +79,22 @@ bool write_all(int fd, const void *buf, size_t n) {
     if (k <= 0) return false;
     p += k;
     n -= (size_t)k;
+  }
+  return true;
+}
+
+// sendmsg over an iovec list until every byte is out (no copy into one buffer)
+bool write_allv(int fd, iovec *iov, int cnt) {
+  while (cnt > 0) {
+    msghdr m;
+    std::memset(&m, 0, sizeof(m));
+    m.msg_iov = iov;
+    m.msg_iovlen = (size_t)cnt;
+    ssize_t k = ::sendmsg(fd, &m, MSG_NOSIGNAL);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    while (cnt > 0 && (size_t)k >= iov->iov_len) { k -= (ssize_t)iov->iov_len; iov++; cnt--; }
+    if (cnt > 0) { iov->iov_base = (char *)iov->iov_base + k; iov->iov_len -= (size_t)k; }
   }
   return true;
 }
@@ -184,24 +201,39 @@ bool get_req(In &in, WarpReq &q) {
   return in.ok;
 }
 
-void put_resp(Out &o, const WarpResp &r) {
+// A warp reply: the fixed fields, the window length, then the window bytes --
+// sent with one sendmsg from the batch's result (no copy into a message
+// buffer) and received straight into the caller's memory.
+constexpr size_t kRespFixed = 4 + 16 + 8 + 4 + 4 + 48 + 8;
+
+void put_resp_fixed(Out &o, const WarpResp &r) {
   o.put(r.rc);
   for (int32_t v : r.bbox) o.put(v);
   o.put(r.nodata); o.put(r.dtype); o.put(r.bytes_read);
   for (double v : r.src_gt) o.put(v);
-  o.put_bytes(r.data.data(), r.data.size());
+  o.put<uint64_t>(r.data.size());
 }
 
-bool get_resp(In &in, WarpResp &r) {
+bool send_resp(int fd, const WarpResp &r) {
+  Out o;
+  put_resp_fixed(o, r);
+  char hdr[16];
+  const uint32_t op = SVC_WARP;
+  const uint64_t n = o.b.size() + r.data.size();
+  std::memcpy(hdr, &kSvcMagic, 4);
+  std::memcpy(hdr + 4, &op, 4);
+  std::memcpy(hdr + 8, &n, 8);
+  iovec iov[3] = {{hdr, 16}, {o.b.data(), o.b.size()}, {(void *)r.data.data(), r.data.size()}};
+  return write_allv(fd, iov, r.data.empty() ? 2 : 3);
+}
+
+bool get_resp_fixed(In &in, WarpResp &r, uint64_t &n_data) {
   r.rc = in.get<int32_t>();
   for (int32_t &v : r.bbox) v = in.get<int32_t>();
   r.nodata = in.get<double>(); r.dtype = in.get<int32_t>(); r.bytes_read = in.get<int32_t>();
   for (double &v : r.src_gt) v = in.get<double>();
-  uint64_t n = 0;
-  const char *p = in.get_bytes(n);
-  if (!in.ok) return false;
-  r.data.assign(p, p + n);
-  return true;
+  n_data = in.get<uint64_t>();
+  return in.ok;
 }
 
 // ---------------------------------------------------------------- daemon state
@@ -359,7 +391,8 @@ void conn_serve(Service *s, int fd) {
         }
       }
       s->resident_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-      put_resp(o, pd->r);
+      if (!send_resp(fd, pd->r)) break;   // the worker died (SIGKILL): drop the reply
+      continue;
     } else if (op == SVC_REGISTER) {
       o.put<int32_t>(do_register(s, in));
     } else if (op == SVC_UNREGISTER_ALL) {
@@ -399,13 +432,72 @@ void conn_loop(Service *s, int fd) {
 
 }  // namespace
 
-int service_warp(const char *sock, const WarpReq &q, WarpResp &r) {
+namespace {
+// the calling thread's connection to the service (reused across requests;
+// round 4 connected per request, and the daemon started a thread per
+// connection)
+struct ClientConn {
+  std::string sock;
+  int fd = -1;
+  pid_t pid = 0;
+  ~ClientConn() { if (fd >= 0) ::close(fd); }
+};
+thread_local ClientConn t_conn;
+
+int client_fd(const char *sock, bool fresh) {
+  ClientConn &c = t_conn;
+  if (c.fd >= 0 && (fresh || c.pid != ::getpid() || c.sock != sock)) { ::close(c.fd); c.fd = -1; }
+  if (c.fd < 0) { c.fd = connect_to(sock); c.sock = sock; c.pid = ::getpid(); }
+  return c.fd;
+}
+void client_drop() {
+  if (t_conn.fd >= 0) ::close(t_conn.fd);
+  t_conn.fd = -1;
+}
+}  // namespace
+
+int service_warp(const char *sock, const WarpReq &q, WarpResp &r, void **mbuf, size_t *mlen) {
   Out o;
   put_req(o, q);
-  std::vector<char> rep;
-  if (!exchange(sock, SVC_WARP, o.b, rep)) return GSKYHIP_E_SERVICE;
-  In in{rep.data(), rep.data() + rep.size()};
-  return get_resp(in, r) ? 0 : GSKYHIP_E_SERVICE;
+  // a kept connection may have been closed by a restarted daemon: one retry
+  // on a fresh connection (a warp request only reads, so a repeat is harmless)
+  for (int attempt = 0; attempt < 2; attempt++) {
+    const int fd = client_fd(sock, attempt > 0);
+    if (fd < 0) return GSKYHIP_E_SERVICE;
+    char hdr[16];
+    if (!send_msg(fd, SVC_WARP, o.b) || !read_all(fd, hdr, 16)) { client_drop(); continue; }
+    uint32_t magic, op;
+    uint64_t n;
+    std::memcpy(&magic, hdr, 4);
+    std::memcpy(&op, hdr + 4, 4);
+    std::memcpy(&n, hdr + 8, 8);
+    char fixed[kRespFixed];
+    if (magic != kSvcMagic || op != SVC_WARP || n < kRespFixed || n > (1ull << 36) ||
+        !read_all(fd, fixed, kRespFixed)) {
+      client_drop();
+      return GSKYHIP_E_SERVICE;
+    }
+    In in{fixed, fixed + kRespFixed};
+    uint64_t nd = 0;
+    if (!get_resp_fixed(in, r, nd) || nd != n - kRespFixed) { client_drop(); return GSKYHIP_E_SERVICE; }
+    char *dst;
+    if (mbuf) {
+      *mbuf = std::malloc(nd ? nd : 1);
+      if (!*mbuf) { client_drop(); return GSKYHIP_E_SERVICE; }
+      dst = (char *)*mbuf;
+      *mlen = (size_t)nd;
+    } else {
+      r.data.resize(nd);
+      dst = r.data.data();
+    }
+    if (nd && !read_all(fd, dst, nd)) {
+      if (mbuf) { std::free(*mbuf); *mbuf = nullptr; }
+      client_drop();
+      return GSKYHIP_E_SERVICE;
+    }
+    return 0;
+  }
+  return GSKYHIP_E_SERVICE;
 }
 
 }  // namespace gsky
@@ -454,8 +546,8 @@ int gskyhip_service_run(const char *socket_path, int max_batch, int window_us) {
     s.queue.clear();
   }
   s.cv_done.notify_all();
-  // clients connect per request, so their threads end within one exchange;
-  // give them a few seconds, then leave any idle persistent connection behind
+  // workers keep their connections: give busy ones a few seconds, then leave
+  // any idle persistent connection behind (its thread ends when it closes)
   for (int k = 0; k < 500 && s.active.load() > 0; k++) std::this_thread::sleep_for(std::chrono::milliseconds(10));
   ::close(fd);
   ::unlink(socket_path);

@@ -27,7 +27,11 @@ enum SvcOp : uint32_t { SVC_WARP = 1, SVC_REGISTER = 2, SVC_UNREGISTER_ALL = 3, 
 
 // Forward one request to the service at `sock`; 0, or GSKYHIP_E_SERVICE when
 // the service cannot be reached (the worker reports the failure and the OWS
-// retries, process.go:147-150).
-int service_warp(const char *sock, const WarpReq &q, WarpResp &r);
+// retries, process.go:147-150).  The thread keeps its connection for the next
+// request (a fresh one after fork or a broken pipe).  With `mbuf`, the window
+// bytes are received straight into malloc'd memory (*mbuf, *mlen; the caller
+// frees it, as warp.go:573-574 frees the worker's buffer) and r.data stays
+// empty.
+int service_warp(const char *sock, const WarpReq &q, WarpResp &r, void **mbuf = nullptr, size_t *mlen = nullptr);
 
 }  // namespace gsky
