@@ -612,19 +612,33 @@ __device__ void plan_pair(const PlanArgs &a, int p, double *sx, double *sy, int 
   // would otherwise live in scratch (xform_point selects its geotransforms
   // through pointers) or cost ~130 VGPRs
   Xform &t = ts;
-  if (lane == 0) {
-    t.src = a.crs[g.crs];
-    t.gl = (g.geoloc > 0 && a.geolocs) ? a.geolocs + (g.geoloc - 1) : nullptr;
-    t.reproject = 0;
-    if (a.dst_crs >= 0) {
-      t.dst = a.crs[a.dst_crs];
-      t.reproject = crs_same(t.src, t.dst) ? 0 : 1;
-    } else {
-      t.dst = t.src;
+  {   // set up by the lanes side by side (round 3 had lane 0 copy ~90 words
+      // and invert both geotransforms in series): lanes 0-35 the two CRS
+      // records a word each, 36-47 the geotransforms, 48 / 49 the inverses
+      // (from global), 50 the reprojection flag and the geolocation arrays
+    static_assert(sizeof(gskyhip_crs) % 8 == 0 && sizeof(gskyhip_crs) / 8 * 2 + 15 <= 64, "crs words");
+    constexpr int kCw = (int)(sizeof(gskyhip_crs) / 8);   // 18 words
+    const int dsti = a.dst_crs >= 0 ? a.dst_crs : g.crs;
+    if (lane < kCw) {
+      ((uint64_t *)&t.src)[lane] = ((const uint64_t *)&a.crs[g.crs])[lane];
+    } else if (lane < 2 * kCw) {
+      ((uint64_t *)&t.dst)[lane - kCw] = ((const uint64_t *)&a.crs[dsti])[lane - kCw];
+    } else if (lane < 2 * kCw + 6) {
+      t.src_gt[lane - 2 * kCw] = g.geot[lane - 2 * kCw];
+    } else if (lane < 2 * kCw + 12) {
+      t.dst_gt[lane - 2 * kCw - 6] = tile.dst_geot[lane - 2 * kCw - 6];
+    } else if (lane == 2 * kCw + 12) {
+      double gt[6];
+      for (int k = 0; k < 6; k++) gt[k] = g.geot[k];
+      inv_geot(gt, t.src_igt);
+    } else if (lane == 2 * kCw + 13) {
+      double gt[6];
+      for (int k = 0; k < 6; k++) gt[k] = tile.dst_geot[k];
+      inv_geot(gt, t.dst_igt);
+    } else if (lane == 2 * kCw + 14) {
+      t.gl = (g.geoloc > 0 && a.geolocs) ? a.geolocs + (g.geoloc - 1) : nullptr;
+      t.reproject = a.dst_crs >= 0 ? (crs_same(a.crs[g.crs], a.crs[a.dst_crs]) ? 0 : 1) : 0;
     }
-    for (int k = 0; k < 6; k++) { t.src_gt[k] = g.geot[k]; t.dst_gt[k] = tile.dst_geot[k]; }
-    inv_geot(t.src_gt, t.src_igt);
-    inv_geot(t.dst_gt, t.dst_igt);
   }
   __syncthreads();
   PSTAMP(ps, 1);
