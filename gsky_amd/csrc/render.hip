@@ -167,6 +167,7 @@ __device__ int must_adjust2(const Xform &t, const double *er, double psxr, doubl
 constexpr int kSteps = 20;
 constexpr int kSmallBatchPairs = 512;   // plan_pairs_kernel<256> up to this many pairs
 constexpr int kSmallBatchTiles = 8, kSmallBatchPlanPairs = 32;   // plan_small_kernel batches
+constexpr int64_t kSmallBatchPlanRows = 2048;                      // pairs x tile rows it plans
 constexpr int kFusedPlanPairs = 2;   // ... that plan their pairs in the same launch
 constexpr int kGrid = (kSteps + 1) * (kSteps + 1);
 
@@ -1710,7 +1711,11 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
   a.gedge = nullptr;
   // small batches: pairs (a workgroup each, own edge samples and owning
   // tile), then every later planning step in one workgroup -- 2 launches
-  bool small = rc.n_tiles <= kSmallBatchTiles && rc.n_pairs > 0 && rc.n_pairs <= kSmallBatchPlanPairs;
+  // (and few rows to plan: the one workgroup plans every pair's rows, so a
+  // tile over many granules goes faster through the multi-launch planner,
+  // profiles/r04al_ab_plan_small_c5_c1.txt)
+  bool small = rc.n_tiles <= kSmallBatchTiles && rc.n_pairs > 0 && rc.n_pairs <= kSmallBatchPlanPairs &&
+               (int64_t)rc.n_pairs * rc.max_h <= kSmallBatchPlanRows;
 #ifdef GSKYHIP_AB
   if (const char *sm = getenv("GSKYHIP_PLAN_SMALL")) small = small && atoi(sm) != 0;
 #endif

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04zzz: validation + closing run on the final library build in one call:
+# r04zzz (also r04zzzz): validation + closing run on the final library build in one call:
 # oracle-free warp checks, the GPU suite, PMC passes of render_nn_kernel (C2) /
 # render_bil_kernel (C3) summarised into the box's profiles/ (so the bench line
 # carries `traffic`), the bench line, rocprofv3 kernel stats of C1-C5.
