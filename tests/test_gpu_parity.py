@@ -486,6 +486,11 @@ def test_drill_deciles_parity(gpu, oracle, dcount, pc, clip):
             assert (cnts[p, j, 1:] == 1).all()
             small += int(((dc.masks[p] == 255) & (sub != dc.nodata)).sum() < dcount + 1)
     assert small >= len(bands)
+    # wave-split means: the deciles take the transposing path (the fused
+    # band-major rows come with the reference-order walk only) -- same picks
+    vw, cw = drill.read_data(st, mb, clip_lower=clip[0], clip_upper=clip[1], pixel_count=pc,
+                             decile_count=dcount, bands=bands, mode=drill.WAVE_SPLIT)
+    assert np.array_equal(vw.cpu().numpy()[..., 1:], vals[..., 1:]) and np.array_equal(cw.cpu().numpy(), cnts)
     # several sort passes over the band list
     dec, stt = drill.compute_deciles(st, mb, mc, dcount, bands, band_chunk=2)
     assert np.array_equal(dec.cpu().numpy()[stt.cpu().numpy() == 0],
