@@ -336,7 +336,7 @@ def run_c2(ctx: Ctx, args):
     }
     if ctx.rank == 0 and args.png_tiles > 0:
         # EncodePNG's png.Encode (ogc_encoders.go:139) of rendered C2 tiles:
-        # colour type + Go's filter rows on the GPU, deflate on host threads
+        # colour type + Go's filter rows and the deflate (LZ77 + per-tile Huffman codes) on the GPU, PNG framing on host threads
         from gsky_amd.encode import encode_png
         rgba = batch.render(sp, pal)
         sample = [covered[k] for k in range(0, len(covered), max(1, len(covered) // args.png_tiles))][
