@@ -690,9 +690,13 @@ int launch_decile_select_fused(const float *vals, const int32_t *chunk_base, con
   const int64_t n_seg = (int64_t)n_polys * n_sel;
   if (n_seg >= 2147483647LL) return GSKYHIP_E_ARG;
   const int n_slots = kHistSlots;
-  const int cache_keys = (kSelLds - n_slots * 256 * 4) / 4;
+  int sel_lds = kSelLds;
+#ifdef GSKYHIP_AB
+  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(8, std::min(60, atoi(e))) * 1024;
+#endif
+  const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
   hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe>), dim3((unsigned)n_seg),
-                     dim3(kSelThreads), (size_t)kSelLds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
+                     dim3(kSelThreads), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
                      decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
