@@ -201,6 +201,44 @@ __global__ __launch_bounds__(64) void drill_sum_kernel(const float *__restrict__
   band_count[o] = total;
 }
 
+// Mode 0 without deciles: the reference-order walk with U pixel loads in
+// flight per lane, in a kernel of its own (69 VGPRs at U = 32: 7 waves per
+// SIMD; drill_sum_kernel's walk at 32 needs 86).  r04ap: 2.21 -> 1.99 ms per
+// C4 step against drill_sum_kernel at 16.
+template <bool PC, int U>
+__global__ __launch_bounds__(64) void drill_sum_u_kernel(const float *__restrict__ stack, int t_stride,
+                                                         const int32_t *__restrict__ idx,
+                                                         const int64_t *__restrict__ mask_off,
+                                                         const int32_t *__restrict__ count,
+                                                         const int32_t *__restrict__ order,
+                                                         const int32_t *__restrict__ tsel, int n_sel, int n_groups,
+                                                         float nodata, float lo, float hi,
+                                                         double *__restrict__ band_value,
+                                                         int32_t *__restrict__ band_count) {
+  const int item = blockIdx.x;
+  const int p = order[item / n_groups];
+  const int j = (item % n_groups) * 64 + threadIdx.x;
+  const bool active = j < n_sel;
+  const float *base = stack + (active ? tsel[j] : 0);
+  const int32_t *ip = idx + mask_off[p];
+  const int n = count[p];
+  float sum = 0.f;
+  int32_t total = 0;
+  int k = 0;
+  for (; k + U <= n; k += U) {
+    float v[U];
+#pragma unroll
+    for (int q = 0; q < U; q++) v[q] = base[(int64_t)ip[k + q] * t_stride];
+#pragma unroll
+    for (int q = 0; q < U; q++) drill_acc<PC>(v[q], nodata, lo, hi, sum, total);
+  }
+  for (; k < n; k++) drill_acc<PC>(base[(int64_t)ip[k] * t_stride], nodata, lo, hi, sum, total);
+  if (!active) return;
+  const int64_t o = (int64_t)p * n_sel + j;
+  band_value[o] = total > 0 ? (double)(sum / (float)total) : 0.0;
+  band_count[o] = total;
+}
+
 // ---------------------------------------------------------------- wave split
 // Exclusive scan of segments per polygon (one block; n_polys is modest).
 __global__ __launch_bounds__(1024) void drill_seg_scan_kernel(const int32_t *__restrict__ count, int n_polys,
@@ -496,8 +534,17 @@ int launch_drill_batch(const DrillCall &c) {
     if (emit) launch_decile_chunk_scan(w.count, c.n_polys, c.emit_chunk_base, s);
     auto *kf = emit ? (pc ? drill_sum_kernel<true, true> : drill_sum_kernel<false, true>)
                     : (pc ? drill_sum_kernel<true, false> : drill_sum_kernel<false, false>);
-    hipLaunchKernelGGL(kf, grid, dim3(64), 0, s, c.stack, c.t_stride, w.idx, c.mask_off, w.count, w.order, w.tsel,
-                       n_sel, n_groups, c.nodata, c.lo, c.hi, bv, bc, c.emit_vals, c.emit_chunk_base, c.emit_stats);
+    bool walk32 = !emit;
+#ifdef GSKYHIP_AB
+    if (const char *ue = getenv("GSKYHIP_DRILL_U")) walk32 = walk32 && atoi(ue) != 16;   // 16: drill_sum_kernel
+#endif
+    if (walk32)
+      hipLaunchKernelGGL((pc ? drill_sum_u_kernel<true, 32> : drill_sum_u_kernel<false, 32>), grid, dim3(64), 0, s,
+                         c.stack, c.t_stride, w.idx, c.mask_off, w.count, w.order, w.tsel, n_sel, n_groups, c.nodata,
+                         c.lo, c.hi, bv, bc);
+    else
+      hipLaunchKernelGGL(kf, grid, dim3(64), 0, s, c.stack, c.t_stride, w.idx, c.mask_off, w.count, w.order, w.tsel,
+                         n_sel, n_groups, c.nodata, c.lo, c.hi, bv, bc, c.emit_vals, c.emit_chunk_base, c.emit_stats);
   } else {
     hipLaunchKernelGGL(drill_seg_scan_kernel, dim3(1), dim3(1024), 0, s, w.count, c.n_polys, w.seg_base);
     const int64_t n_seg_max = c.mask_bytes / kSeg + c.n_polys;
