@@ -680,9 +680,12 @@ def run_service(ctx: Ctx, args):
     sock = "/tmp/gskyhip-bench-%d.sock" % os.getpid()
     svc = WarpService(sock, max_batch=64, window_us=args.svc_window_us)
     out = {"workload": "C2 (tile, granule) warp requests, 512x512 EPSG:3857 windows from 16 EPSG:3577 int16 "
-                       "4000x4000 granules resident in the daemon's HBM; %d requests per run, dealt round-robin "
-                       "to the workers, each worker one request at a time" % args.svc_jobs,
-           "daemon": "gskyhipd max_batch 64, window %d us" % args.svc_window_us}
+                       "4000x4000 granules resident in the daemon's HBM; %d distinct requests dealt round-robin to "
+                       "the workers, each worker one request at a time, cycling through its share: %d untimed "
+                       "requests per worker, then %.1f s timed (steady state)" %
+                       (args.svc_jobs, args.svc_warmup, args.svc_seconds),
+           "daemon": "gskyhipd max_batch 64, window %d us (only while a batch is on the GPU), two batches in "
+                     "flight, windows written by the GPU into each worker's shared reply arena" % args.svc_window_us}
     try:
         for k, g in enumerate(cfg.granules):
             svc.register_granule("/g/data/c2/g%d.tif" % k, 1, g.data, g.geot, "EPSG:3577", g.nodata, block=(256, 256))
@@ -692,15 +695,17 @@ def run_service(ctx: Ctx, args):
         jobs = [("/g/data/c2/g%d.tif" % k, 1, list(bbox_to_geot(w, h, bb)), w, h, "EPSG:3857") for k, bb, w, h in sel]
         for n in (16, 64):
             s0 = svc.stats()
-            r = service_load(sock, jobs, n)
+            r = service_load(sock, jobs, n, seconds=args.svc_seconds, warmup=args.svc_warmup)
             s1 = svc.stats()
             r["mean_batch"] = round((s1["requests"] - s0["requests"]) / max(1, s1["batches"] - s0["batches"]), 2)
             r["max_batch"] = s1["max_batch"]
             nb, nr = max(1, s1["batches"] - s0["batches"]), max(1, s1["requests"] - s0["requests"])
-            r["daemon_batch_ms_mean"] = round((s1["batch_s"] - s0["batch_s"]) * 1e3 / nb, 3)
+            r["daemon_dispatch_ms_mean"] = round((s1["batch_s"] - s0["batch_s"]) * 1e3 / nb, 3)
             r["daemon_resident_ms_mean"] = round((s1["resident_s"] - s0["resident_s"]) * 1e3 / nr, 3)
             r["daemon_batch_phases_ms_mean"] = {k: round((s1[k + "_s"] - s0[k + "_s"]) * 1e3 / nb, 3)
-                                                for k in ("prep", "gpu", "readback")}
+                                                for k in ("launch", "gpu_wait", "readback")}
+            r["replies_in_place"] = s1["in_place"] - s0["in_place"]
+            r["replies_copied"] = s1["copied"] - s0["copied"]
             out["workers_%d" % n] = r
     finally:
         svc.shutdown()
@@ -744,7 +749,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--only", default="c2,c1,c3,c4,c5,svc", help="comma list of configs (c2 is the headline)")
     ap.add_argument("--svc-jobs", type=int, default=1024, help="service leg: C2 (tile, granule) requests per run")
-    ap.add_argument("--svc-window-us", type=int, default=500, help="service leg: gskyhipd batching window")
+    ap.add_argument("--svc-window-us", type=int, default=0,
+                    help="service leg: gskyhipd batching window (taken only while a batch is on the GPU)")
+    ap.add_argument("--svc-seconds", type=float, default=2.0, help="service leg: timed seconds per worker count")
+    ap.add_argument("--svc-warmup", type=int, default=8, help="service leg: untimed requests per worker")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c1", action="store_true", help="(compat) drop C1")
     ap.add_argument("--cpu-runs", type=int, default=5)

@@ -98,12 +98,16 @@ def gather_coverage(band, extents: Sequence[Tuple[int, int]], height: int, width
     rank = dist.get_rank(group)
     via_host = band.is_cuda and dist.get_backend(group) == "gloo"
     if rank != 0:
+        # posted through batch_isend_irecv like rank 0's receives: under
+        # NCCL/RCCL a batched P2P that is the group's first collective must be
+        # entered by every rank
         t, b = extents[rank]
         if b > t:
             src = band[: b - t].contiguous()
             if via_host:
                 src = src.cpu()
-            dist.send(src, 0, group=group)
+            for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, src, 0, group)]):
+                w.wait()
         return None
     full = out if out is not None else torch.empty((height, width), dtype=band.dtype, device=band.device)
     t0, b0 = extents[0]
@@ -128,11 +132,12 @@ def gather_coverage(band, extents: Sequence[Tuple[int, int]], height: int, width
     return full
 
 
-def render_band_gpu(cfg, chunks: Sequence[Chunk], rows: Tuple[int, int], width: int, device):
+def render_band_gpu(cfg, chunks: Sequence[Chunk], rows: Tuple[int, int], width: int, device, out=None):
     """Renders the chunks of chunk rows [rows) of a synth-style coverage config
     on `device` (one namespace, Float32 canvases, cfg.resample) and returns the
     (band rows, width) band.  Only granules intersecting the band's chunks are
-    uploaded."""
+    uploaded.  `out`: a (band rows, width) float32 view to render into -- rank
+    0 passes its rows of the coverage, so its band is never copied."""
     import numpy as np
     import torch
 
@@ -152,7 +157,9 @@ def render_band_gpu(cfg, chunks: Sequence[Chunk], rows: Tuple[int, int], width: 
                gr.polygon, gr.namespace)
     tiles = [(c.bbox, c.width, c.height) for c in sel]
     tb = TileBatch(gs, cfg.dst_srs, tiles, [[remap[g] for g in p] for p in pairs], cfg.namespaces)
-    band = torch.empty((bottom - top, width), dtype=torch.float32, device=device)
+    band = out if out is not None else torch.empty((bottom - top, width), dtype=torch.float32, device=device)
+    if tuple(band.shape) != (bottom - top, width) or band.dtype != torch.float32 or not band.is_contiguous():
+        raise ValueError("render_band_gpu: out must be a contiguous (%d, %d) float32 band" % (bottom - top, width))
     # every chunk is rendered straight into the band at its offset (no assembly copy)
     tb.render_coverage(ScaleParams(*cfg.scale), band, band_offsets(sel, top, width), resample=cfg.resample)
     return band
@@ -175,6 +182,13 @@ def render_coverage(cfg, width: int, height: int, renderer: Callable = render_ba
     nrows = n_chunk_rows(chunks)
     rows = [band_of_rank(nrows, r, world) for r in range(world)]
     extents = [band_extent(chunks, rw) for rw in rows]
+    if world > 1 and rank == 0 and renderer is render_band_gpu:
+        # rank 0 renders its band in place inside the coverage (no copy)
+        import torch
+        full = torch.empty((height, width), dtype=torch.float32, device=device)
+        t0, b0 = extents[0]
+        band = renderer(cfg, chunks, rows[rank], width, device, out=full[t0:b0])
+        return gather_coverage(band, extents, height, width, group, out=full), extents
     band = renderer(cfg, chunks, rows[rank], width, device)
     if world == 1:
         return band, extents

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -276,28 +277,29 @@ struct Registered {
   int64_t bytes = 0;           // ... and its size
   uint64_t last_use = 0;       // DropIn::tick of the last batch that used it
   int64_t mtime_ns = 0, fsize = -1;   // the file as ingested (fsize < 0: registered by the caller)
+  bool stamped = false;                // the stamp could be taken: re-read the file when it changes
+  Registered() { std::memset(&g, 0, sizeof(g)); }
+  Registered(const Registered &) = delete;
+  Registered &operator=(const Registered &) = delete;
+  // The registry and every warp batch in flight that reads the granule hold
+  // it (shared_ptr): its HBM is freed when the last of them lets go, so a
+  // re-ingest, an eviction or unregister_all never frees what a launched
+  // batch still reads.
+  ~Registered() {
+    for (void *p : owned) (void)hipFree(p);
+  }
 };
-
-void release(Registered &r) {
-  for (void *p : r.owned) hipFree(p);
-  r.owned.clear();
-  r.bytes = 0;
-}
+using RegPtr = std::shared_ptr<Registered>;
 
 struct DropIn {
   std::mutex mu;
-  std::map<std::pair<std::string, int>, Registered> reg;
-  hipStream_t stream = nullptr;
-  void *dev = nullptr;   // descriptors + workspace + window
-  size_t dev_bytes = 0;
-  uint64_t tick = 0;     // one per warp batch: entries it uses are not evicted while it runs
-  char *pin = nullptr;   // pinned read-back staging (metadata + windows), grown as needed
-  size_t pin_bytes = 0;
-  std::map<std::string, struct GeoLocEntry *> geolocs;   // by GeoLocOpts (geoloc_entry)
+  std::map<std::pair<std::string, int>, RegPtr> reg;
+  uint64_t tick = 0;     // one per warp batch (LRU order of the ingest cache)
+  std::map<std::string, std::shared_ptr<struct GeoLocEntry>> geolocs;   // by GeoLocOpts (geoloc_entry)
 };
 DropIn &dropin() {
-  static DropIn d;
-  return d;
+  static DropIn *d = new DropIn();   // never destroyed: its entries would call HIP at process exit
+  return *d;
 }
 
 // HBM the ingested (library-owned) granules may hold before the least
@@ -312,21 +314,22 @@ int64_t ingest_cache_cap() {
   return cap;
 }
 
-// Make room for `need` more bytes of ingested granules: release the least
-// recently used ones not used by the running batch (last_use < d.tick).
+// Make room for `need` more bytes of ingested granules: drop the least
+// recently used ones that no batch holds (in flight, or being assembled:
+// last_use == d.tick).
 void evict_for(DropIn &d, int64_t need) {
   const int64_t cap = ingest_cache_cap();
   for (;;) {
     int64_t held = 0;
     auto victim = d.reg.end();
     for (auto it = d.reg.begin(); it != d.reg.end(); ++it) {
-      held += it->second.bytes;
-      if (it->second.bytes > 0 && it->second.last_use < d.tick &&
-          (victim == d.reg.end() || it->second.last_use < victim->second.last_use))
+      const Registered &R = *it->second;
+      held += R.bytes;
+      if (R.bytes > 0 && R.last_use < d.tick && it->second.use_count() == 1 &&
+          (victim == d.reg.end() || R.last_use < victim->second->last_use))
         victim = it;
     }
     if (held + need <= cap || victim == d.reg.end()) return;   // fits, or nothing evictable: exceed the cap
-    release(victim->second);
     d.reg.erase(victim);
   }
 }
@@ -366,27 +369,25 @@ int ingest_geotiff_locked(DropIn &d, const std::string &path, int band) {
   if (rc) return rc;
   if (band < 1 || band > info.n_bands) return 2;
   if (!have_gpu()) return GSKYHIP_E_NOGPU;
-  Registered r;
-  std::memset(&r.g, 0, sizeof(r.g));
+  RegPtr rp = std::make_shared<Registered>();
+  Registered &r = *rp;
   const int ts = type_size(info.dtype);
   if (ts <= 0) return GSKYHIP_E_TYPE;
   int64_t total = 0;
   for (int lv = 0; lv <= info.n_ovr; lv++)
     total += (int64_t)(lv ? info.ovr_xsize[lv - 1] : info.xsize) * (lv ? info.ovr_ysize[lv - 1] : info.ysize) * ts;
-  {
-    auto old = d.reg.find({path, band});
-    if (old != d.reg.end()) { release(old->second); d.reg.erase(old); }
-  }
+  d.reg.erase({path, band});   // a batch still holding the old entry keeps it alive
   evict_for(d, total);
   r.bytes = total;
   r.last_use = d.tick;
-  if (!file_stamp(path, r.mtime_ns, r.fsize)) r.fsize = 0;
+  r.stamped = file_stamp(path, r.mtime_ns, r.fsize);
+  if (!r.stamped) r.fsize = 0;
   for (int lv = 0; lv <= info.n_ovr; lv++) {
     const int64_t xs = lv ? info.ovr_xsize[lv - 1] : info.xsize, ys = lv ? info.ovr_ysize[lv - 1] : info.ysize;
     void *p = nullptr;
-    if (hipMalloc(&p, (size_t)(xs * ys * ts)) != hipSuccess) { release(r); return GSKYHIP_E_HIP; }
+    if (hipMalloc(&p, (size_t)(xs * ys * ts)) != hipSuccess) return GSKYHIP_E_HIP;
     r.owned.push_back(p);
-    if ((rc = gskyhip_geotiff_read(path.c_str(), band, lv, p, xs * ys * ts, nullptr))) { release(r); return rc; }
+    if ((rc = gskyhip_geotiff_read(path.c_str(), band, lv, p, xs * ys * ts, nullptr))) return rc;
   }
   gskyhip_granule &g = r.g;
   g.data = r.owned[0];
@@ -403,9 +404,7 @@ int ingest_geotiff_locked(DropIn &d, const std::string &path, int band) {
   if (info.epsg > 0) std::snprintf(srs, sizeof(srs), "EPSG:%d", info.epsg);
   else if (info.epsg == -1) std::snprintf(srs, sizeof(srs), "MODIS");
   if (srs[0] && parse_srs(srs, &r.crs) == 0) r.has_crs = true;
-  auto it = d.reg.find({path, band});
-  if (it != d.reg.end()) release(it->second);
-  d.reg[{path, band}] = std::move(r);
+  d.reg[{path, band}] = std::move(rp);
   return 0;
 }
 
@@ -420,21 +419,19 @@ int ingest_netcdf_locked(DropIn &d, const std::string &path, int band) {
   if (!have_gpu()) return GSKYHIP_E_NOGPU;
   const int ts = type_size(info.dtype);
   if (ts <= 0) return GSKYHIP_E_TYPE;
-  Registered r;
-  std::memset(&r.g, 0, sizeof(r.g));
+  RegPtr rp = std::make_shared<Registered>();
+  Registered &r = *rp;
   void *p = nullptr;
   const int64_t bytes = (int64_t)info.xsize * info.ysize * ts;
-  {
-    auto old = d.reg.find({path, band});
-    if (old != d.reg.end()) { release(old->second); d.reg.erase(old); }
-  }
+  d.reg.erase({path, band});   // a batch still holding the old entry keeps it alive
   evict_for(d, bytes);
   r.bytes = bytes;
   r.last_use = d.tick;
-  if (!file_stamp(path, r.mtime_ns, r.fsize)) r.fsize = 0;
+  r.stamped = file_stamp(path, r.mtime_ns, r.fsize);
+  if (!r.stamped) r.fsize = 0;
   if (hipMalloc(&p, (size_t)bytes) != hipSuccess) return GSKYHIP_E_HIP;
   r.owned.push_back(p);
-  if ((rc = gskyhip_netcdf_read(path.c_str(), band, p, bytes, nullptr))) { release(r); return rc; }
+  if ((rc = gskyhip_netcdf_read(path.c_str(), band, p, bytes, nullptr))) return rc;
   gskyhip_granule &g = r.g;
   g.data = p;
   g.dtype = info.dtype; g.xsize = info.xsize; g.ysize = info.ysize; g.signed_byte = info.signed_byte;
@@ -452,9 +449,7 @@ int ingest_netcdf_locked(DropIn &d, const std::string &path, int band) {
   };
   set_crs(srs_no, r.crs, r.has_crs, r.bad_crs);
   set_crs(srs_cf, r.crs_cf, r.has_crs_cf, r.bad_crs_cf);
-  auto it = d.reg.find({path, band});
-  if (it != d.reg.end()) release(it->second);
-  d.reg[{path, band}] = std::move(r);
+  d.reg[{path, band}] = std::move(rp);
   return 0;
 }
 
@@ -469,12 +464,47 @@ int ingest_netcdf_locked(DropIn &d, const std::string &path, int band) {
 struct GeoLocEntry {
   GeoLocD d;
   std::vector<void *> owned;
+  RegPtr x_src, y_src;   // the X / Y datasets it was built from: rebuilt when either is re-read
+  GeoLocEntry() { std::memset(&d, 0, sizeof(d)); }
+  GeoLocEntry(const GeoLocEntry &) = delete;
+  GeoLocEntry &operator=(const GeoLocEntry &) = delete;
+  ~GeoLocEntry() {
+    for (void *p : owned) (void)hipFree(p);
+  }
 };
+using GeoLocPtr = std::shared_ptr<GeoLocEntry>;
 
-void release_geoloc(GeoLocEntry *e) {
-  if (!e) return;
-  for (void *p : e->owned) (void)hipFree(p);
-  delete e;
+int ingest_geotiff_locked(DropIn &d, const std::string &path, int band);
+int ingest_netcdf_locked(DropIn &d, const std::string &path, int band);
+bool is_geotiff_path(const std::string &p);
+
+bool is_netcdf_path(const std::string &p) {
+  return p.compare(0, 7, "NETCDF:") == 0 || (p.size() >= 3 && p.compare(p.size() - 3, 3, ".nc") == 0);
+}
+
+// The registry entry of (path, band) as GDALOpenEx would see it now: an
+// ingested file that changed on disk is dropped and read again (never an
+// entry this batch already uses: last_use == d.tick); an unregistered
+// GeoTIFF / netCDF path is opened and ingested.  *irc: the ingest's code (0,
+// 1 no such file, 2 no such band, GSKYHIP_E_*), or 0 when nothing was read.
+RegPtr lookup_dataset(DropIn &d, const std::string &path, int band, int *irc) {
+  *irc = 0;
+  auto it = d.reg.find({path, band});
+  if (it != d.reg.end() && it->second->fsize >= 0 && it->second->stamped && it->second->last_use != d.tick) {
+    int64_t mt = 0, sz = 0;
+    if (!file_stamp(path, mt, sz) || mt != it->second->mtime_ns || sz != it->second->fsize) {
+      d.reg.erase(it);   // batches in flight keep their reference
+      it = d.reg.end();
+    }
+  }
+  const bool nc = is_netcdf_path(path);
+  if (it == d.reg.end() && (nc || is_geotiff_path(path))) {
+    *irc = nc ? ingest_netcdf_locked(d, path, band) : ingest_geotiff_locked(d, path, band);
+    if (*irc == 0) it = d.reg.find({path, band});
+  }
+  if (it == d.reg.end()) return RegPtr();
+  it->second->last_use = d.tick;
+  return it->second;
 }
 
 bool band_as_double(const Registered &R, std::vector<double> &out) {
@@ -591,17 +621,12 @@ bool geoloc_backmap(const std::vector<double> &gx, const std::vector<double> &gy
   return true;
 }
 
-int ingest_geotiff_locked(DropIn &d, const std::string &path, int band);
-int ingest_netcdf_locked(DropIn &d, const std::string &path, int band);
-bool is_geotiff_path(const std::string &p);
-
-// The transformer of one GeoLocOpts list (cached), or NULL (the reference's
-// GDALCreateGeoLocTransformer failure: warp_operation_fast returns 3).
-GeoLocEntry *geoloc_entry(DropIn &d, const std::vector<std::string> &opts) {
+// The transformer of one GeoLocOpts list (cached while its X / Y datasets
+// are unchanged), or NULL (the reference's GDALCreateGeoLocTransformer
+// failure: warp_operation_fast returns 3).
+GeoLocPtr geoloc_entry(DropIn &d, const std::vector<std::string> &opts) {
   std::string key;
   for (const std::string &o : opts) key += o + '\n';
-  auto hit = d.geolocs.find(key);
-  if (hit != d.geolocs.end()) return hit->second;
   std::map<std::string, std::string> kv;
   for (const std::string &o : opts) {
     const size_t e = o.find('=');
@@ -610,23 +635,15 @@ GeoLocEntry *geoloc_entry(DropIn &d, const std::vector<std::string> &opts) {
   for (const char *k : {"PIXEL_OFFSET", "LINE_OFFSET", "PIXEL_STEP", "LINE_STEP", "X_BAND", "Y_BAND",
                         "X_DATASET", "Y_DATASET"})
     if (!kv.count(k)) return nullptr;   // "Missing some geolocation fields"
-  auto dataset = [&](const std::string &path, int band) -> const Registered * {
-    auto it = d.reg.find({path, band});
-    if (it == d.reg.end()) {
-      const bool nc = path.compare(0, 7, "NETCDF:") == 0 ||
-                      (path.size() >= 3 && path.compare(path.size() - 3, 3, ".nc") == 0);
-      if (nc) { if (ingest_netcdf_locked(d, path, band)) return nullptr; }
-      else if (is_geotiff_path(path)) { if (ingest_geotiff_locked(d, path, band)) return nullptr; }
-      else return nullptr;
-      it = d.reg.find({path, band});
-      if (it == d.reg.end()) return nullptr;
-    }
-    it->second.last_use = d.tick;
-    return &it->second;
-  };
-  const Registered *X = dataset(kv["X_DATASET"], std::atoi(kv["X_BAND"].c_str()));
-  const Registered *Y = dataset(kv["Y_DATASET"], std::atoi(kv["Y_BAND"].c_str()));
+  int irc = 0;
+  const RegPtr X = lookup_dataset(d, kv["X_DATASET"], std::atoi(kv["X_BAND"].c_str()), &irc);
+  const RegPtr Y = lookup_dataset(d, kv["Y_DATASET"], std::atoi(kv["Y_BAND"].c_str()), &irc);
   if (!X || !Y) return nullptr;
+  auto hit = d.geolocs.find(key);
+  if (hit != d.geolocs.end()) {
+    if (hit->second->x_src == X && hit->second->y_src == Y) return hit->second;
+    d.geolocs.erase(hit);   // a dataset was re-read: build the transformer again
+  }
   std::vector<double> ax, ay;
   if (!band_as_double(*X, ax) || !band_as_double(*Y, ay)) return nullptr;
   // GeoLocLoadFullData: a regular grid when both bands are one row
@@ -640,9 +657,10 @@ GeoLocEntry *geoloc_entry(DropIn &d, const std::vector<std::string> &opts) {
       gx[o] = regular ? ax[i] : ax[o];
       gy[o] = regular ? ay[j] : ay[o];
     }
-  GeoLocEntry *e = new GeoLocEntry();
+  GeoLocPtr e = std::make_shared<GeoLocEntry>();
+  e->x_src = X;
+  e->y_src = Y;
   GeoLocD &g = e->d;
-  std::memset(&g, 0, sizeof(g));
   g.nx = nx; g.ny = ny;
   g.has_nodata = X->g.has_nodata ? 1 : 0;
   g.nodata_x = X->g.nodata;
@@ -653,10 +671,8 @@ GeoLocEntry *geoloc_entry(DropIn &d, const std::vector<std::string> &opts) {
   std::vector<float> bmx, bmy;
   int bw = 0, bh = 0;
   if (!geoloc_backmap(gx, gy, nx, ny, g.has_nodata != 0, g.nodata_x, g.pixel_offset, g.line_offset, g.pixel_step,
-                      g.line_step, bmx, bmy, bw, bh, g.bm_gt)) {
-    delete e;
+                      g.line_step, bmx, bmy, bw, bh, g.bm_gt))
     return nullptr;
-  }
   g.bm_w = bw; g.bm_h = bh;
   auto up = [&](const void *src, size_t bytes) -> void * {
     void *p = nullptr;
@@ -669,7 +685,7 @@ GeoLocEntry *geoloc_entry(DropIn &d, const std::vector<std::string> &opts) {
   g.gy = (const double *)up(gy.data(), gy.size() * 8);
   g.bmx = (const float *)up(bmx.data(), bmx.size() * 4);
   g.bmy = (const float *)up(bmy.data(), bmy.size() * 4);
-  if (!g.gx || !g.gy || !g.bmx || !g.bmy) { release_geoloc(e); return nullptr; }
+  if (!g.gx || !g.gy || !g.bmx || !g.bmy) return nullptr;
   d.geolocs[key] = e;
   return e;
 }
@@ -714,27 +730,23 @@ int gskyhip_register_granule(const char *path, int band, const gskyhip_granule *
   if (g->n_ovr < 0 || g->n_ovr > GSKYHIP_MAX_OVR) return GSKYHIP_E_ARG;
   for (int k = 0; k < g->n_ovr; k++)
     if (!g->ovr_data[k] || g->ovr_xsize[k] <= 0 || g->ovr_ysize[k] <= 0) return GSKYHIP_E_ARG;
-  Registered r;
-  r.g = *g;
-  r.has_crs = false;
+  RegPtr r = std::make_shared<Registered>();
+  r->g = *g;
+  r->has_crs = false;
   if (srs && *srs) {
-    if (parse_srs(srs, &r.crs)) return GSKYHIP_E_CRS;
-    r.has_crs = true;
+    if (parse_srs(srs, &r->crs)) return GSKYHIP_E_CRS;
+    r->has_crs = true;
   }
   DropIn &d = dropin();
   std::lock_guard<std::mutex> lk(d.mu);
-  auto it = d.reg.find({std::string(path), band});
-  if (it != d.reg.end()) release(it->second);
-  d.reg[{std::string(path), band}] = r;
+  d.reg[{std::string(path), band}] = std::move(r);
   return 0;
 }
 
 int gskyhip_unregister_all(void) {
   DropIn &d = dropin();
   std::lock_guard<std::mutex> lk(d.mu);
-  for (auto &kv : d.reg) release(kv.second);
-  d.reg.clear();
-  for (auto &kv : d.geolocs) release_geoloc(kv.second);
+  d.reg.clear();       // HBM of ingested granules is freed once no batch in flight holds it
   d.geolocs.clear();
   return 0;
 }
@@ -761,30 +773,90 @@ namespace gsky {
 // warp.go:82-382 for n requests at once: per request the registry lookup and
 // the reference's early returns (open / band / transformer failures), then
 // every request with the same destination SRS planned and warped in one set
-// of launches (one tile + one pair per request), bytesRead per request, and
-// one read-back.  The device buffer grows as needed and is kept.
+// of launches (one tile + one pair each), the window and bytesRead of every
+// request in one pass, one read-back of the reply records.  Split in
+// launch / finish so the service keeps two batches in flight (service.cpp).
 namespace {
 std::atomic<int64_t> g_wb_ns[4];
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
+int64_t a256(int64_t v) { return (v + 255) & ~(int64_t)255; }
 }  // namespace
 
 void warp_batch_timers(int64_t out[4]) {
   for (int k = 0; k < 4; k++) out[k] = g_wb_ns[k].load();
 }
 
-void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
+// One batch's device, upload and read-back buffers, stream and completion
+// event.  A slot carries one batch at a time; the buffers grow and are kept.
+struct WarpSlot {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev = nullptr;
+  char *dev = nullptr;   // per group: header | results | stats | workspace | staged windows | scratch
+  size_t dev_bytes = 0;
+  char *up = nullptr;    // pinned: the groups' headers
+  size_t up_bytes = 0;
+  char *pin = nullptr;   // pinned: reply records, then staged windows
+  size_t pin_bytes = 0;
+  struct Job {
+    int req;
+    int err;                       // a launch failure of its group (GSKYHIP_E_*), else 0
+    int64_t res_pin;               // reply record in `pin`
+    int64_t win_dev, win_pin;      // staged window: device / pinned offsets (-1: written in place)
+    int64_t stride;
+  };
+  std::vector<Job> jobs;
+  std::vector<RegPtr> hold;        // granules the batch reads (freed only after it finished)
+  std::vector<GeoLocPtr> hold_gl;
+  WarpResp *out = nullptr;
+  bool inflight = false;
+};
+
+WarpSlot *warp_slot_create() { return new WarpSlot(); }
+
+void warp_slot_destroy(WarpSlot *s) {
+  if (!s) return;
+  warp_batch_finish(*s);
+  if (s->dev) (void)hipFree(s->dev);
+  if (s->up) (void)hipHostFree(s->up);
+  if (s->pin) (void)hipHostFree(s->pin);
+  if (s->ev) (void)hipEventDestroy(s->ev);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+namespace {
+template <typename T> bool grow_dev(T *&p, size_t &have, size_t need) {
+  if (have >= need) return true;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  have = 0;
+  if (hipMalloc((void **)&p, need) != hipSuccess) return false;
+  have = need;
+  return true;
+}
+bool grow_pin(char *&p, size_t &have, size_t need) {
+  if (have >= need) return true;
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  have = 0;
+  if (hipHostMalloc((void **)&p, need, hipHostMallocDefault) != hipSuccess) return false;
+  have = need;
+  return true;
+}
+}  // namespace
+
+void warp_batch_launch(WarpSlot &S, const WarpReq *reqs, int n, WarpResp *out, uint8_t *const *direct,
+                       const int64_t *direct_cap) {
+  const int64_t t0 = now_ns();
+  g_wb_ns[3]++;
+  S.jobs.clear();
+  S.out = out;
+  S.inflight = false;
   DropIn &d = dropin();
   std::lock_guard<std::mutex> lk(d.mu);
-  int64_t t_prev = now_ns();
-  auto lap = [&](int k) {
-    const int64_t t = now_ns();
-    g_wb_ns[k] += t - t_prev;
-    t_prev = t;
-  };
-  g_wb_ns[3]++;
   d.tick++;
   struct Item { int req; gskyhip_granule g; gskyhip_crs src; int bx, by; const GeoLocEntry *gl; };
   std::map<std::pair<int, std::string>, std::vector<Item>> groups;   // (has dst, dst srs) -> items
@@ -795,41 +867,28 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     // warp.go:89-101: "NETCDF:..." and "*.nc" are opened through GSKY_netCDF
     // with band_query=<band>, which exposes that band as band 1; any other
     // path is opened whole and GDALGetRasterBand(band) may fail (114-118).
-    const bool netcdf = q.path.compare(0, 7, "NETCDF:") == 0 ||
-                        (q.path.size() >= 3 && q.path.compare(q.path.size() - 3, 3, ".nc") == 0);
-    auto it = d.reg.find({q.path, q.band});
-    if (it != d.reg.end() && it->second.fsize >= 0) {   // ingested from a file: re-read it if it changed
-      int64_t mt = 0, sz = 0;
-      if (!file_stamp(q.path, mt, sz) || mt != it->second.mtime_ns || sz != it->second.fsize) {
-        release(it->second);
-        d.reg.erase(it);
-        it = d.reg.end();
-      }
-    }
-    if (it == d.reg.end() && (netcdf || is_geotiff_path(q.path))) {   // GDALOpenEx of a file nobody registered
-      const int irc = netcdf ? ingest_netcdf_locked(d, q.path, q.band) : ingest_geotiff_locked(d, q.path, q.band);
-      if (irc == 2) { r.rc = 2; continue; }
-      if (irc < 0) { r.rc = irc; continue; }   // HBM exhausted, unsupported encoding, ...: an error, not "open failed"
-      if (irc == 0) it = d.reg.find({q.path, q.band});
-      // else (1: no such file): the registry rule below -- a path registered
-      // with other bands is an open dataset without this band (2), else 1
-    }
-    if (it == d.reg.end()) {
+    const bool netcdf = is_netcdf_path(q.path);
+    int irc = 0;
+    const RegPtr RP = lookup_dataset(d, q.path, q.band, &irc);
+    if (irc == 2) { r.rc = 2; continue; }
+    if (irc < 0) { r.rc = irc; continue; }   // HBM exhausted, unsupported encoding, ...: an error, not "open failed"
+    if (!RP) {   // (irc 1: no such file) a path registered with other bands is an open dataset without this band
       bool path_known = false;
       for (const auto &kv : d.reg) if (kv.first.first == q.path) { path_known = true; break; }
       r.rc = (netcdf || !path_known) ? 1 : 2;                         // open failed / band failed
       continue;
     }
-    it->second.last_use = d.tick;                                      // pinned for this batch
-    const Registered &R = it->second;
+    const Registered &R = *RP;
     if (!R.g.data) { r.rc = 2; continue; }                             // band failed
     if (q.width <= 0 || q.height <= 0) { r.rc = GSKYHIP_E_ARG; continue; }
     Item it2;
     it2.req = i;
     it2.gl = nullptr;
     if (q.geoloc) {   // warp.go:134-140: createGeoLocTransformer, 3 when it fails
-      it2.gl = geoloc_entry(d, q.geoloc_opts);
-      if (!it2.gl) { r.rc = 3; continue; }
+      GeoLocPtr gl = geoloc_entry(d, q.geoloc_opts);
+      if (!gl) { r.rc = 3; continue; }
+      it2.gl = gl.get();
+      S.hold_gl.push_back(std::move(gl));
     }
     // the dataset SRS: GSKY_netCDF opened with srs_cf=yes takes the CF
     // grid mapping only (warp.go:95, netcdfdataset.cpp:3666)
@@ -854,86 +913,119 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     if (q.has_src_gt) std::memcpy(it2.g.geot, q.src_gt, sizeof(it2.g.geot));
     it2.bx = R.g.block_x > 0 ? R.g.block_x : 0;                      // 0: one scanline of the chosen level
     it2.by = R.g.block_y > 0 ? R.g.block_y : 1;
+    S.hold.push_back(RP);
     groups[{q.has_dst_srs, q.has_dst_srs ? q.dst_srs : std::string()}].push_back(it2);
   }
-  if (groups.empty()) return;
-  if (!have_gpu()) {
-    for (auto &kv : groups) for (const Item &it : kv.second) out[it.req].rc = GSKYHIP_E_NOGPU;
+  if (groups.empty()) { g_wb_ns[0] += now_ns() - t0; return; }
+  auto fail_all = [&](int code) {
+    for (auto &kv : groups) for (const Item &it : kv.second) out[it.req].rc = code;
+  };
+  if (!have_gpu()) { fail_all(GSKYHIP_E_NOGPU); return; }
+  if ((!S.stream && hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) ||
+      (!S.ev && hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)) {
+    fail_all(GSKYHIP_E_HIP);
     return;
   }
-  if (!d.stream && hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess) {
-    for (auto &kv : groups) for (const Item &it : kv.second) out[it.req].rc = GSKYHIP_E_HIP;
-    return;
-  }
-  auto a256 = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
+  // ---- layout of every group in the slot's three buffers
+  // device group: granules | geolocation transformers | crs (m sources + dst) | tiles | pairs
+  //               | block-stats jobs | window destinations (uploaded up to here) | reply records
+  //               | stats | workspace | staged windows | block-stats scratch
+  struct Lay {
+    const std::vector<Item> *items;
+    const std::string *dst;
+    int has_dst, m, max_w, max_h, n_staged;
+    int64_t o_gl, o_crs, o_tiles, o_pairs, o_jobs, o_outs, o_res, o_stats, o_ws, ws, stride, o_win, o_scr, max_px;
+    int64_t dev_base, up_base, pin_res, pin_win;
+    std::vector<BlockStatsJob> jobs;
+    std::vector<char> staged;
+  };
+  std::vector<Lay> lays;
+  int64_t dev_total = 0, up_total = 0, pin_total = 0;
   for (auto &kv : groups) {
+    Lay L;
+    L.items = &kv.second;
+    L.has_dst = kv.first.first;
+    L.dst = &kv.first.second;
     const std::vector<Item> &items = kv.second;
-    const int m = (int)items.size();
-    int max_w = 1, max_h = 1;
-    int64_t st_bytes = 0, max_px = 0;
-    std::vector<int64_t> n_px(m), n_words(m);
-    std::vector<BlockStatsJob> jobs(m);
+    const int m = L.m = (int)items.size();
+    L.max_w = 1; L.max_h = 1; L.max_px = 0; L.n_staged = 0;
+    int64_t st_bytes = 0;
+    std::vector<int64_t> n_words(m);
+    L.jobs.resize(m);
+    L.staged.assign(m, 0);
     for (int k = 0; k < m; k++) {
       const WarpReq &q = reqs[items[k].req];
-      max_w = std::max(max_w, q.width);
-      max_h = std::max(max_h, q.height);
+      L.max_w = std::max(L.max_w, q.width);
+      L.max_h = std::max(L.max_h, q.height);
       const gskyhip_granule &g = items[k].g;
       const int bx0 = items[k].bx > 0 ? items[k].bx : g.xsize;
       const int64_t nblocks = ((int64_t)(g.xsize + bx0 - 1) / bx0) * ((g.ysize + items[k].by - 1) / items[k].by);
       n_words[k] = (nblocks + 31) / 32;
-      n_px[k] = (int64_t)q.width * q.height;
-      max_px = std::max(max_px, n_px[k]);
-      jobs[k].bx = items[k].bx;
-      jobs[k].by = items[k].by;
-      jobs[k].n_words = (int32_t)n_words[k];
-      jobs[k]._pad = 0;
-      jobs[k].xsrc_off = st_bytes;                 // xsrc of every job, then every job's bitmap
-      st_bytes += a256(n_px[k] * 4);
+      const int64_t px = (int64_t)q.width * q.height;
+      L.max_px = std::max(L.max_px, px);
+      BlockStatsJob &J = L.jobs[k];
+      J.bx = items[k].bx; J.by = items[k].by; J.n_words = (int32_t)n_words[k]; J._pad = 0;
+      J.xsrc_off = st_bytes;                     // xsrc of every job, then every job's bitmap
+      st_bytes += a256(px * 4);
+      const int i = items[k].req;
+      // a window is written in place when the caller gave a destination big
+      // enough for any value type (8 bytes per pixel)
+      const bool in_place = direct && direct[i] && direct_cap && direct_cap[i] >= px * 8;
+      if (!in_place) { L.staged[k] = 1; L.n_staged++; }
     }
     for (int k = 0; k < m; k++) {
-      jobs[k].bits_off = st_bytes;
+      L.jobs[k].bits_off = st_bytes;
       st_bytes += a256(n_words[k] * 4);
     }
-    // device layout: granules | geolocation transformers | crs (m sources + dst) | tiles | pairs | bbox
-    //                | dtype | nodata | stats | block-stats jobs
-    //                | workspace | windows (m x stride) | block-stats scratch
-    const int64_t o_gl = a256((int64_t)m * sizeof(gskyhip_granule));
-    const int64_t o_crs = o_gl + a256((int64_t)m * sizeof(GeoLocD));
-    const int64_t o_tiles = o_crs + a256((int64_t)(m + 1) * sizeof(gskyhip_crs));
-    const int64_t o_pairs = o_tiles + a256((int64_t)m * sizeof(gskyhip_tile));
-    const int64_t o_bbox = o_pairs + a256((int64_t)m * 4);
-    const int64_t o_dtype = o_bbox + a256((int64_t)m * 16);
-    const int64_t o_nodata = o_dtype + a256((int64_t)m * 4);
-    const int64_t o_stats = o_nodata + a256((int64_t)m * 8);
-    const int64_t o_jobs = o_stats + a256((int64_t)m * 16);
-    const int64_t o_ws = o_jobs + a256((int64_t)m * sizeof(BlockStatsJob));
-    const int64_t ws = render_workspace_size(m, m, max_h);
-    const int64_t stride = a256((int64_t)max_w * max_h * 4);
-    const int64_t o_win = o_ws + a256(ws);
-    const int64_t o_scr = o_win + stride * m;
-    const size_t need = (size_t)(o_scr + st_bytes);
-    auto fail = [&](int code) { for (const Item &it : items) out[it.req].rc = code; };
-    if (d.dev_bytes < need) {
-      if (d.dev) hipFree(d.dev);
-      d.dev = nullptr;
-      d.dev_bytes = 0;
-      if (hipMalloc(&d.dev, need) != hipSuccess) { fail(GSKYHIP_E_HIP); continue; }
-      d.dev_bytes = need;
-    }
-    char *base = (char *)d.dev;
-    std::vector<char> hdr((size_t)o_ws, 0);
-    gskyhip_granule *hg = (gskyhip_granule *)hdr.data();
-    gskyhip_crs *hc = (gskyhip_crs *)(hdr.data() + o_crs);
-    gskyhip_tile *ht = (gskyhip_tile *)(hdr.data() + o_tiles);
-    int32_t *hp = (int32_t *)(hdr.data() + o_pairs);
+    L.o_gl = a256((int64_t)m * sizeof(gskyhip_granule));
+    L.o_crs = L.o_gl + a256((int64_t)m * sizeof(GeoLocD));
+    L.o_tiles = L.o_crs + a256((int64_t)(m + 1) * sizeof(gskyhip_crs));
+    L.o_pairs = L.o_tiles + a256((int64_t)m * sizeof(gskyhip_tile));
+    L.o_jobs = L.o_pairs + a256((int64_t)m * 4);
+    L.o_outs = L.o_jobs + a256((int64_t)m * sizeof(BlockStatsJob));
+    L.o_res = L.o_outs + a256((int64_t)m * sizeof(void *));
+    L.o_stats = L.o_res + a256((int64_t)m * sizeof(WarpResult));
+    L.o_ws = L.o_stats + a256((int64_t)m * 16);
+    L.ws = render_workspace_size(m, m, L.max_h);
+    L.stride = a256((int64_t)L.max_w * L.max_h * 8);
+    L.o_win = L.o_ws + a256(L.ws);
+    L.o_scr = L.o_win + L.stride * L.n_staged;
+    L.dev_base = dev_total;
+    dev_total += a256(L.o_scr + st_bytes);
+    L.up_base = up_total;
+    up_total += a256(L.o_res);
+    L.pin_res = pin_total;
+    pin_total += a256((int64_t)m * sizeof(WarpResult));
+    L.pin_win = pin_total;
+    pin_total += L.stride * L.n_staged;
+    lays.push_back(std::move(L));
+  }
+  if (!grow_dev(S.dev, S.dev_bytes, (size_t)dev_total) || !grow_pin(S.up, S.up_bytes, (size_t)up_total) ||
+      !grow_pin(S.pin, S.pin_bytes, (size_t)pin_total)) {
+    fail_all(GSKYHIP_E_HIP);
+    return;
+  }
+  // ---- headers, launches, reply read-back
+  for (Lay &L : lays) {
+    const std::vector<Item> &items = *L.items;
+    const int m = L.m;
+    char *base = S.dev + L.dev_base;
+    char *hdr = S.up + L.up_base;
+    std::memset(hdr, 0, (size_t)L.o_res);
+    gskyhip_granule *hg = (gskyhip_granule *)hdr;
+    gskyhip_crs *hc = (gskyhip_crs *)(hdr + L.o_crs);
+    gskyhip_tile *ht = (gskyhip_tile *)(hdr + L.o_tiles);
+    int32_t *hp = (int32_t *)(hdr + L.o_pairs);
+    uint8_t **houts = (uint8_t **)(hdr + L.o_outs);
     int dst_crs = -1;
-    if (kv.first.first) {
-      parse_srs(kv.first.second.c_str(), &hc[m]);
+    if (L.has_dst) {
+      parse_srs(L.dst->c_str(), &hc[m]);
       dst_crs = m;
     }
-    std::memcpy(hdr.data() + o_jobs, jobs.data(), (size_t)m * sizeof(BlockStatsJob));
-    GeoLocD *hgl = (GeoLocD *)(hdr.data() + o_gl);
+    std::memcpy(hdr + L.o_jobs, L.jobs.data(), (size_t)m * sizeof(BlockStatsJob));
+    GeoLocD *hgl = (GeoLocD *)(hdr + L.o_gl);
     bool any_gl = false;
+    int si = 0;
     for (int k = 0; k < m; k++) {
       const WarpReq &q = reqs[items[k].req];
       hg[k] = items[k].g;
@@ -951,8 +1043,25 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
       ht[k].pair_begin = k;
       ht[k].pair_end = k + 1;
       hp[k] = k;
+      WarpSlot::Job J;
+      J.req = items[k].req;
+      J.err = 0;
+      J.res_pin = L.pin_res + (int64_t)k * sizeof(WarpResult);
+      J.stride = L.stride;
+      if (L.staged[k]) {
+        J.win_dev = L.dev_base + L.o_win + L.stride * si;
+        J.win_pin = L.pin_win + L.stride * si;
+        si++;
+        houts[k] = (uint8_t *)(S.dev + J.win_dev);
+      } else {
+        J.win_dev = J.win_pin = -1;
+        houts[k] = direct[J.req];
+      }
+      S.jobs.push_back(J);
     }
-    if (hipMemcpyAsync(base, hdr.data(), hdr.size(), hipMemcpyHostToDevice, d.stream) != hipSuccess) {
+    const size_t first_job = S.jobs.size() - (size_t)m;
+    auto fail = [&](int code) { for (size_t j = first_job; j < S.jobs.size(); j++) S.jobs[j].err = code; };
+    if (hipMemcpyAsync(base, hdr, (size_t)L.o_res, hipMemcpyHostToDevice, S.stream) != hipSuccess) {
       fail(GSKYHIP_E_HIP);
       continue;
     }
@@ -960,74 +1069,96 @@ void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
     std::memset(ms, 0, sizeof(ms));
     RenderCall rc;
     rc.granules = (const gskyhip_granule *)base; rc.n_granules = m;
-    rc.crs = (const gskyhip_crs *)(base + o_crs); rc.n_crs = m + 1; rc.dst_crs = dst_crs;
-    rc.tiles = (const gskyhip_tile *)(base + o_tiles); rc.n_tiles = m;
-    rc.pair_granule = (const int32_t *)(base + o_pairs); rc.n_pairs = m;
-    rc.max_w = max_w; rc.max_h = max_h;
+    rc.crs = (const gskyhip_crs *)(base + L.o_crs); rc.n_crs = m + 1; rc.dst_crs = dst_crs;
+    rc.tiles = (const gskyhip_tile *)(base + L.o_tiles); rc.n_tiles = m;
+    rc.pair_granule = (const int32_t *)(base + L.o_pairs); rc.n_pairs = m;
+    rc.max_w = L.max_w; rc.max_h = L.max_h;
     rc.mask_ns = -1; rc.mask_inclusive = 0; rc.mask_specs = ms;
     rc.resample = GSKYHIP_RESAMPLE_NEAREST;
     rc.value_types = 0;
     rc.cov_offsets = nullptr;
     rc.cov_stride = 0;
-    rc.workspace = base + o_ws; rc.workspace_bytes = ws;
-    rc.stream = d.stream;
-    rc.geolocs = any_gl ? (const GeoLocD *)(base + o_gl) : nullptr;
-    int32_t *dbbox = (int32_t *)(base + o_bbox), *ddt = (int32_t *)(base + o_dtype);
-    double *dnd = (double *)(base + o_nodata);
-    int32_t *dst = (int32_t *)(base + o_stats);
-    lap(0);
-    int code = launch_warp_windows(rc, dbbox, ddt, dnd, base + o_win, stride);
-    if (!code)
-      code = launch_block_stats_batch(rc, (const BlockStatsJob *)(base + o_jobs), m, max_px, base + o_scr, dst);
-    if (code) { fail(code); continue; }
-    // read-back through pinned staging: bbox | dtype | nodata | stats in one
-    // copy, the PairPlans (their src_gt is the overview-rescaled
-    // geotransform) in another, then every window -- one wait each phase
-    const int64_t meta = o_jobs - o_bbox, o_pp = a256(meta), o_wins = o_pp + a256((int64_t)sizeof(PairPlan) * m);
-    const size_t pin_need = (size_t)(o_wins + stride * m);
-    if (d.pin_bytes < pin_need) {
-      if (d.pin) (void)hipHostFree(d.pin);
-      d.pin = nullptr;
-      d.pin_bytes = 0;
-      if (hipHostMalloc((void **)&d.pin, pin_need, hipHostMallocDefault) != hipSuccess) {
-        fail(GSKYHIP_E_HIP);
-        continue;
-      }
-      d.pin_bytes = pin_need;
-    }
-    char *hp0 = d.pin;
-    if (hipMemcpyAsync(hp0, dbbox, (size_t)meta, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
-        hipMemcpyAsync(hp0 + o_pp, rc.workspace, sizeof(PairPlan) * m, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
-        hipStreamSynchronize(d.stream) != hipSuccess) {
-      fail(GSKYHIP_E_HIP);
-      continue;
-    }
-    lap(1);
-    const int32_t *bb = (const int32_t *)hp0, *dt = (const int32_t *)(hp0 + (o_dtype - o_bbox));
-    const double *nd = (const double *)(hp0 + (o_nodata - o_bbox));
-    const int32_t *stv = (const int32_t *)(hp0 + (o_stats - o_bbox));
-    const PairPlan *pps = (const PairPlan *)(hp0 + o_pp);
-    std::vector<int64_t> szs(m, 0);
-    bool copy_ok = true;
-    for (int k = 0; k < m; k++) {
-      WarpResp &r = out[items[k].req];
-      for (int j = 0; j < 4; j++) r.bbox[j] = bb[4 * k + j];
-      r.dtype = dt[k];
-      r.nodata = nd[k];
-      r.bytes_read = stv[4 * k + 2];
-      std::memcpy(r.src_gt, pps[k].src_gt, sizeof(r.src_gt));
-      szs[k] = std::min<int64_t>(std::max<int64_t>((int64_t)r.bbox[2] * r.bbox[3] * type_size(r.dtype), 0), stride);
-      if (szs[k] > 0 && hipMemcpyAsync(hp0 + o_wins + stride * k, base + o_win + stride * k, (size_t)szs[k],
-                                       hipMemcpyDeviceToHost, d.stream) != hipSuccess)
-        copy_ok = false;
-    }
-    if (!copy_ok || hipStreamSynchronize(d.stream) != hipSuccess) { fail(GSKYHIP_E_HIP); continue; }
-    for (int k = 0; k < m; k++) {
-      WarpResp &r = out[items[k].req];
-      r.data.assign(hp0 + o_wins + stride * k, hp0 + o_wins + stride * k + szs[k]);
-    }
-    lap(2);
+    rc.workspace = base + L.o_ws; rc.workspace_bytes = L.ws;
+    rc.stream = S.stream;
+    rc.geolocs = any_gl ? (const GeoLocD *)(base + L.o_gl) : nullptr;
+    int code = launch_warp_jobs(rc, (const BlockStatsJob *)(base + L.o_jobs), L.max_px, base + L.o_scr,
+                                (int32_t *)(base + L.o_stats), (uint8_t *const *)(base + L.o_outs),
+                                (WarpResult *)(base + L.o_res));
+    if (!code && hipMemcpyAsync(S.pin + L.pin_res, base + L.o_res, (size_t)m * sizeof(WarpResult),
+                                hipMemcpyDeviceToHost, S.stream) != hipSuccess)
+      code = GSKYHIP_E_HIP;
+    if (code) fail(code);
   }
+  if (hipEventRecord(S.ev, S.stream) != hipSuccess) {
+    for (WarpSlot::Job &J : S.jobs) J.err = GSKYHIP_E_HIP;
+    (void)hipStreamSynchronize(S.stream);
+  }
+  S.inflight = true;
+  g_wb_ns[0] += now_ns() - t0;
+}
+
+void warp_batch_finish(WarpSlot &S) {
+  if (!S.inflight) {
+    if (!S.hold.empty() || !S.hold_gl.empty()) {
+      std::lock_guard<std::mutex> lk(dropin().mu);
+      S.hold.clear();
+      S.hold_gl.clear();
+    }
+    return;
+  }
+  const int64_t t0 = now_ns();
+  const bool ok = hipEventSynchronize(S.ev) == hipSuccess;
+  const int64_t t1 = now_ns();
+  g_wb_ns[1] += t1 - t0;
+  bool copy_ok = true;
+  std::vector<int64_t> staged(S.jobs.size(), 0);   // staged window bytes to take per job
+  int n_copies = 0;
+  for (size_t j = 0; j < S.jobs.size(); j++) {
+    const WarpSlot::Job &J = S.jobs[j];
+    WarpResp &r = S.out[J.req];
+    if (J.err || !ok) { r.rc = J.err ? J.err : GSKYHIP_E_HIP; continue; }
+    WarpResult w;
+    std::memcpy(&w, S.pin + J.res_pin, sizeof(w));
+    for (int k = 0; k < 4; k++) r.bbox[k] = w.bbox[k];
+    r.dtype = w.dtype;
+    r.nodata = w.nodata;
+    r.bytes_read = w.bytes_read;
+    std::memcpy(r.src_gt, w.src_gt, sizeof(r.src_gt));
+    const int64_t bytes = std::min<int64_t>(std::max<int64_t>((int64_t)w.bbox[2] * w.bbox[3] * type_size(w.dtype), 0),
+                                            J.stride);
+    if (J.win_dev < 0) {
+      r.in_place = bytes;   // already in the caller's destination
+    } else if (bytes > 0) {
+      if (hipMemcpyAsync(S.pin + J.win_pin, S.dev + J.win_dev, (size_t)bytes, hipMemcpyDeviceToHost, S.stream) !=
+          hipSuccess)
+        copy_ok = false;
+      staged[j] = bytes;
+      n_copies++;
+    }
+  }
+  if (n_copies && (!copy_ok || hipStreamSynchronize(S.stream) != hipSuccess)) copy_ok = false;
+  for (size_t j = 0; j < S.jobs.size(); j++) {
+    if (!staged[j]) continue;
+    const WarpSlot::Job &J = S.jobs[j];
+    WarpResp &r = S.out[J.req];
+    if (!copy_ok) { r.rc = GSKYHIP_E_HIP; continue; }
+    r.data.assign(S.pin + J.win_pin, S.pin + J.win_pin + staged[j]);
+  }
+  {
+    std::lock_guard<std::mutex> lk(dropin().mu);
+    S.hold.clear();
+    S.hold_gl.clear();
+  }
+  S.inflight = false;
+  g_wb_ns[2] += now_ns() - t1;
+}
+
+void warp_batch(const WarpReq *reqs, int n, WarpResp *out) {
+  static std::mutex mu;
+  static WarpSlot *slot = new WarpSlot();   // never destroyed: no HIP calls at process exit
+  std::lock_guard<std::mutex> lk(mu);
+  warp_batch_launch(*slot, reqs, n, out, nullptr, nullptr);
+  warp_batch_finish(*slot);
 }
 
 }  // namespace gsky

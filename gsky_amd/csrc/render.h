@@ -48,4 +48,18 @@ struct BlockStatsJob {
 int launch_block_stats_batch(const RenderCall &c, const BlockStatsJob *jobs, int n_jobs, int64_t max_px,
                              void *scratch, int32_t *stats);
 
+// One reply of a warp batch (warp_operation_fast's outputs but the window).
+struct WarpResult {
+  int32_t bbox[4];
+  int32_t dtype, bytes_read;
+  double nodata;
+  double src_gt[6];
+};
+// The service's warp batch: plan, then per job (= pair, one request each)
+// the window into outs[job] (device addresses: staging or registered host
+// memory) with its bytesRead inputs in the same pass, then results[job].
+// max_px bounds every pair's window (w * h).  3 launches after planning.
+int launch_warp_jobs(const RenderCall &c, const BlockStatsJob *jobs, int64_t max_px, void *scratch,
+                     int32_t *stats, uint8_t *const *outs, WarpResult *results);
+
 }  // namespace gsky

@@ -1609,6 +1609,140 @@ __global__ void block_stats_resolve_kernel(const PairPlan *pairs, const BlockSta
   stats[2] = (int32_t)(uint32_t)(unsigned long long)b;
 }
 
+// The per-node service's warp batch (warp_batch_launch, host.cpp): for every
+// request (job = pair) its window values AND its bytesRead inputs from ONE
+// source-coordinate evaluation per pixel -- round 4 ran warp_window_kernel
+// and block_stats_kernel, each deriving the same coordinates again.  The
+// window goes straight to the job's destination `outs[job]`: a device staging
+// slot, or the requesting worker's shared reply arena (host memory registered
+// with HIP, written over PCIe: no read-back copy).  Values follow
+// warped_value (warp.go:271-344), the statistics block_stats_kernel's rules
+// (warp.go:281-347).
+template <int RES>
+__global__ __launch_bounds__(256) void warp_job_kernel(const PairPlan *pairs, const Xform *xforms,
+                                                       const RowRec *rows, const Leaf *pool, int max_h,
+                                                       const BlockStatsJob *jobs, char *scratch, int32_t *stats,
+                                                       uint8_t *const *outs) {
+  const int job = blockIdx.y;
+  const PairPlan &pp = pairs[job];
+  const BlockStatsJob J = jobs[job];
+  int32_t *xsrc = (int32_t *)(scratch + J.xsrc_off);
+  uint32_t *bits = (uint32_t *)(scratch + J.bits_off);
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)pp.w * pp.h;
+  bool valid = false;
+  int ix = 0, iy = 0;
+  if (gid < n) {
+    const int row = (int)(gid / pp.w), i = (int)(gid % pp.w);
+    double sx, sy;
+    const bool ok = src_coords<true>(rows[(int64_t)job * max_h + row], pool, xforms + job, pp.xoff, pp.yoff, pp.w,
+                                     i, row, sx, sy);
+    // bytesRead: the cache heuristic's x test and the full gather test
+    int xs = -1;
+    if (ok && !(sx < 0)) {
+      const double ax = sx + 1.0e-10;
+      if (ax < 2147483647.0) {
+        ix = (int)ax;
+        if (ix < pp.band_x) xs = ix;
+      }
+    }
+    if (xs >= 0 && !(sy < 0)) {
+      const double ay = sy + 1.0e-10;
+      if (ay < 2147483647.0) {
+        iy = (int)ay;
+        valid = iy < pp.band_y;
+      }
+    }
+    xsrc[gid] = xs;
+    // the window value, exactly as warped_value<true, RES>
+    Val v = pp.fill;
+    if (ok) {
+      if (RES == GSKYHIP_RESAMPLE_BILINEAR) {
+        v = bilinear_value(pp, sx, sy);
+      } else if (!(sx < 0 || sy < 0)) {
+        const double ax = sx + 1.0e-10, ay = sy + 1.0e-10;
+        if (!(ax >= 2147483647.0 || ay >= 2147483647.0)) {
+          const int jx = (int)ax, jy = (int)ay;
+          if (jx < pp.band_x && jy < pp.band_y) {
+            v = load_val(pp.band, pp.src_dtype, (long)jy * pp.band_x + jx);
+            if (pp.out_dtype == GSKYHIP_SIGNEDBYTE) v.i = (int32_t)(int8_t)(uint8_t)v.i;
+          }
+        }
+      }
+    }
+    uint8_t *o = outs[job];
+    const int dsz = type_size(pp.out_dtype);
+    if (dsz == 1) o[gid] = (uint8_t)v.i;
+    else if (dsz == 2) ((uint16_t *)o)[gid] = (uint16_t)v.i;
+    else ((uint32_t *)o)[gid] = v.u;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long bal = __ballot(valid);
+  __shared__ int s_first[4], s_count[4];
+  if (lane == 0) {
+    s_first[wave] = bal ? (int)(gid + __ffsll((long long)bal) - 1) : 0x7FFFFFFF;
+    s_count[wave] = __popcll(bal);
+  }
+  int bx = J.bx;
+  if (bx <= 0) bx = pp.band_x;
+  const int nxb = (pp.band_x + bx - 1) / bx;
+  const long long blk = valid ? (long long)(ix / bx) + (long long)(iy / J.by) * nxb : -1;
+  const long long prev = __shfl_up(blk, 1, 64);
+  if (valid && (lane == 0 || prev != blk)) atomicOr(&bits[blk >> 5], 1u << (blk & 31));
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int first = s_first[0], count = s_count[0];
+    for (int w = 1; w < 4; w++) { first = min(first, s_first[w]); count += s_count[w]; }
+    if (count > 0) {
+      atomicMin(&stats[4 * job], first);
+      atomicAdd(&stats[4 * job + 1], count);
+    }
+  }
+}
+
+// bytesRead (block_stats_resolve_kernel's rules) and the job's reply record
+// (bbox, dtype, nodata, overview-rescaled geotransform): one thread per job.
+__global__ void warp_job_resolve_kernel(const PairPlan *pairs, const BlockStatsJob *jobs, const char *scratch,
+                                        int32_t *stats_all, int n_jobs, WarpResult *res) {
+  const int job = blockIdx.x * blockDim.x + threadIdx.x;
+  if (job >= n_jobs) return;
+  const PairPlan &pp = pairs[job];
+  const BlockStatsJob J = jobs[job];
+  const int32_t *xsrc = (const int32_t *)(scratch + J.xsrc_off);
+  const uint32_t *bits = (const uint32_t *)(scratch + J.bits_off);
+  int32_t *stats = stats_all + 4 * job;
+  int bx = J.bx;
+  if (bx <= 0) bx = pp.band_x;
+  const int i0 = stats[0];
+  int32_t br = 0;
+  if (i0 != 0x7FFFFFFF) {
+    const int r0 = i0 / pp.w, c0 = i0 % pp.w;
+    const int prev = xsrc[i0];
+    int curr = -1;
+    for (int c = c0 + 1; c < pp.w; c++) {
+      const int v = xsrc[(long)r0 * pp.w + c];
+      if (v >= 0) { curr = v; break; }
+    }
+    if (curr < prev) curr = prev;
+    const int stride = curr - prev;
+    const bool cache = stride >= 0 && stride < bx;
+    long nread = 0;
+    if (cache) {
+      for (int k = 0; k < J.n_words; k++) nread += __popc(bits[k]);
+    } else {
+      nread = stats[1];
+    }
+    const long long b = (long long)bx * J.by * type_size(pp.src_dtype) * nread;
+    br = (int32_t)(uint32_t)(unsigned long long)b;
+  }
+  WarpResult &r = res[job];
+  r.bbox[0] = pp.xoff; r.bbox[1] = pp.yoff; r.bbox[2] = pp.w; r.bbox[3] = pp.h;
+  r.dtype = pp.out_dtype;
+  r.bytes_read = br;
+  r.nodata = pp.nodata;
+  for (int k = 0; k < 6; k++) r.src_gt[k] = pp.src_gt[k];
+}
+
 __global__ void pair_meta_kernel(const PairPlan *pairs, int n_pairs, int32_t *bbox, int32_t *dtype, double *nodata) {
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
@@ -1876,6 +2010,28 @@ int launch_block_stats_batch(const RenderCall &rc, const BlockStatsJob *jobs, in
                        cv.xforms, cv.rows, cv.pool, rc.max_h, jobs, (char *)scratch, stats);
   hipLaunchKernelGGL(block_stats_resolve_kernel, dim3(n_jobs), dim3(64), 0, s, cv.pairs, jobs,
                      (const char *)scratch, stats);
+  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+}
+
+int launch_warp_jobs(const RenderCall &rc, const BlockStatsJob *jobs, int64_t max_px, void *scratch,
+                     int32_t *stats, uint8_t *const *outs, WarpResult *results) {
+  Carve cv;
+  int rcode = plan_all(rc, cv);
+  if (rcode || rc.n_pairs <= 0) return rcode;
+  hipStream_t s = rc.stream;
+  const int n = rc.n_pairs;
+  hipLaunchKernelGGL(block_stats_init_kernel, dim3(n), dim3(256), 0, s, jobs, (char *)scratch, stats);
+  if (max_px > 0) {
+    const dim3 grid((unsigned)((max_px + 255) / 256), n);
+    if (rc.resample == GSKYHIP_RESAMPLE_BILINEAR)
+      hipLaunchKernelGGL(warp_job_kernel<GSKYHIP_RESAMPLE_BILINEAR>, grid, dim3(256), 0, s, cv.pairs, cv.xforms,
+                         cv.rows, cv.pool, rc.max_h, jobs, (char *)scratch, stats, outs);
+    else
+      hipLaunchKernelGGL(warp_job_kernel<GSKYHIP_RESAMPLE_NEAREST>, grid, dim3(256), 0, s, cv.pairs, cv.xforms,
+                         cv.rows, cv.pool, rc.max_h, jobs, (char *)scratch, stats, outs);
+  }
+  hipLaunchKernelGGL(warp_job_resolve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, cv.pairs, jobs,
+                     (const char *)scratch, stats, n, results);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 

@@ -23,7 +23,12 @@
 namespace gsky {
 
 constexpr uint32_t kSvcMagic = 0x594B5347u;   // "GSKY"
-enum SvcOp : uint32_t { SVC_WARP = 1, SVC_REGISTER = 2, SVC_UNREGISTER_ALL = 3, SVC_STATS = 4, SVC_SHUTDOWN = 5 };
+// SVC_WARP_SHM: a warp whose window comes back in the worker's reply arena
+// (a sealed memfd passed with SCM_RIGHTS on the first request of a
+// connection, or when it grows); SVC_WARP carries the window in the socket.
+enum SvcOp : uint32_t {
+  SVC_WARP = 1, SVC_REGISTER = 2, SVC_UNREGISTER_ALL = 3, SVC_STATS = 4, SVC_SHUTDOWN = 5, SVC_WARP_SHM = 6
+};
 
 // Forward one request to the service at `sock`; 0, or GSKYHIP_E_SERVICE when
 // the service cannot be reached (the worker reports the failure and the OWS

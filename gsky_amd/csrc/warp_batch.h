@@ -36,16 +36,36 @@ struct WarpResp {
   int32_t bytes_read = 0;
   double src_gt[6] = {0, 0, 0, 0, 0, 0};
   std::vector<char> data;
+  int64_t in_place = -1;   // >= 0: the window (this many bytes) was written to the caller's destination
 };
 
 // Runs the batch against this process's granule registry (HBM-resident,
-// gskyhip_register_granule).  Thread-safe (one batch at a time).
+// gskyhip_register_granule) and waits for it.  Thread-safe (one batch at a
+// time).
 void warp_batch(const WarpReq *reqs, int n, WarpResp *out);
 
-// Nanoseconds this process spent in warp_batch by phase, summed over calls:
-// [0] host preparation (registry, SRS parsing, header upload issued),
-// [1] launches through the first read-back (GPU work + small copies),
-// [2] window read-back into the responses, [3] calls.
+// The same in two halves, for a caller that keeps several batches in flight
+// (the service, service.cpp): a slot holds one batch's buffers, stream and
+// completion event.  warp_batch_launch does the registry lookups (requests
+// that fail early get their rc at once), uploads the headers and queues every
+// launch and the reply read-back on the slot's stream without waiting;
+// warp_batch_finish waits for the slot and fills `out` (the array given to
+// launch, which must live until then).  Request i's window is written to
+// direct[i] -- a device-visible address with direct_cap[i] >= width * height
+// * 8 bytes, e.g. host memory registered with HIP -- and out[i].in_place set;
+// without one it lands in out[i].data.  The granules a batch reads stay
+// allocated until its finish.  Different slots may be in flight together.
+struct WarpSlot;
+WarpSlot *warp_slot_create();
+void warp_slot_destroy(WarpSlot *s);   // finishes a batch still in flight
+void warp_batch_launch(WarpSlot &s, const WarpReq *reqs, int n, WarpResp *out, uint8_t *const *direct,
+                       const int64_t *direct_cap);
+void warp_batch_finish(WarpSlot &s);
+
+// Nanoseconds this process spent in warp batches by phase, summed over calls:
+// [0] launch (registry, SRS parsing, headers, launches queued), [1] waiting
+// for the GPU in finish, [2] staged window read-back into the responses and
+// release, [3] batches.
 void warp_batch_timers(int64_t out[4]);
 
 }  // namespace gsky

@@ -9,7 +9,8 @@ HBM-resident granules; workers keep calling the unchanged
 INTEGRATION.md in Go) with GSKYHIP_SERVICE=<socket> in their environment, so
 they forward each request over a Unix socket and never open the GPU.  The
 daemon batches the requests of all workers that arrive within its window into
-one plan + warp launch set.
+one plan + warp launch set, keeps two batches in flight, and has the GPU
+write each window straight into the worker's shared reply arena.
 
     svc = WarpService("/tmp/gskyhip-0.sock")        # starts gskyhipd
     svc.register_granule("NETCDF:/g/x.nc:v", 1, array, geot, "EPSG:3577", -999.0)
@@ -39,18 +40,20 @@ _NP_DTYPE = {np.dtype(np.uint8): _lib.BYTE, np.dtype(np.int8): _lib.BYTE, np.dty
 class WarpService:
     """Handle on one gskyhipd daemon (start=True launches it as a child)."""
 
-    def __init__(self, socket_path: str, max_batch: int = 64, window_us: int = 500, start: bool = True,
-                 device: Optional[int] = None, timeout: float = 60.0):
+    def __init__(self, socket_path: str, max_batch: int = 64, window_us: int = 0, start: bool = True,
+                 device: Optional[int] = None, timeout: float = 60.0, env: Optional[Dict[str, str]] = None):
         self.socket_path = socket_path
         self.proc = None
         if start:
             if not os.path.exists(DAEMON):
                 raise FileNotFoundError("gskyhipd not built: run __graft_entry__.build() (%s)" % DAEMON)
-            env = dict(os.environ)
+            env_extra = dict(env or {})
+            env = denv = dict(os.environ)
             env.pop("GSKYHIP_SERVICE", None)
             if device is not None:
                 env["HIP_VISIBLE_DEVICES"] = str(device)
-            self.proc = subprocess.Popen([DAEMON, socket_path, str(int(max_batch)), str(int(window_us))], env=env)
+            denv.update(env_extra)
+            self.proc = subprocess.Popen([DAEMON, socket_path, str(int(max_batch)), str(int(window_us))], env=denv)
             t0 = time.time()
             while True:
                 if os.path.exists(socket_path):
@@ -98,11 +101,11 @@ class WarpService:
         check(lib().gskyhip_service_unregister_all(self.socket_path.encode()), "service unregister")
 
     def stats(self) -> Dict[str, int]:
-        st = (C.c_int64 * 9)()
-        check(lib().gskyhip_service_stats_n(self.socket_path.encode(), st, 9), "service stats")
+        st = (C.c_int64 * 11)()
+        check(lib().gskyhip_service_stats_n(self.socket_path.encode(), st, 11), "service stats")
         return {"requests": st[0], "batches": st[1], "max_batch": st[2], "granules": st[3],
-                "batch_s": st[4] * 1e-9, "resident_s": st[5] * 1e-9, "prep_s": st[6] * 1e-9,
-                "gpu_s": st[7] * 1e-9, "readback_s": st[8] * 1e-9}
+                "batch_s": st[4] * 1e-9, "resident_s": st[5] * 1e-9, "launch_s": st[6] * 1e-9,
+                "gpu_wait_s": st[7] * 1e-9, "readback_s": st[8] * 1e-9, "in_place": st[9], "copied": st[10]}
 
     def shutdown(self, timeout: float = 60.0) -> Optional[int]:
         """Stops the daemon; returns its exit code when this handle started it."""

@@ -191,8 +191,11 @@ int gskyhip_unregister_all(void);
  *       double *noData, GDALDataType *dType, int *bytesRead)
  * (worker/gdalprocess/warp.go:82).  *dstBuf is host memory from malloc(); the
  * caller frees it with free() (warp.go:573-574).  srcGeot, when given, may be
- * overwritten by the overview pick (warp.go:186-189).  geoLocOpts != NULL is
- * not supported (returns 3).  Nearest-neighbour, like the reference.
+ * overwritten by the overview pick (warp.go:186-189).  geoLocOpts (a
+ * NULL-terminated GDAL geolocation option list, warp.go:128-141) selects the
+ * geolocation-array transformer; 3 only when the options are incomplete or
+ * their X / Y datasets cannot be read (createGeoLocTransformer fails,
+ * warp.go:134-140).  Nearest-neighbour, like the reference.
  * Lookup (warp.go:89-118): "NETCDF:..." / "*.nc" paths are opened per band
  * (band_query) and read as band 1, i.e. (path, band) is looked up; other
  * paths: unregistered path -> 1, registered path without that band -> 2.
@@ -327,8 +330,15 @@ int gskyhip_compute_reproject_extent(const gskyhip_granule *granules, int n, con
  * granules; a worker whose environment has GSKYHIP_SERVICE=<socket> sends
  * each warp_operation_fast call there over a Unix socket and never touches
  * the GPU, so N workers share one context and a SIGKILLed worker leaves no
- * device state.  The daemon plans and warps every request that arrived within
- * `window_us` (up to `max_batch`) in one launch set.  All pointers are host. */
+ * device state.  The daemon keeps two batches in flight: whenever requests
+ * are queued and a batch slot is free it plans and warps up to `max_batch`
+ * of them in one launch set (while the other batch is still on the GPU it may
+ * first wait up to `window_us` for the batch to grow; with the GPU idle it
+ * dispatches at once).  Each worker thread passes a sealed memfd reply arena
+ * with its first request; the daemon registers it with HIP and the warp
+ * kernel writes the window straight into it (GSKYHIP_SVC_DIRECT=0 in the
+ * daemon's environment: staged in HBM and copied instead).  All pointers are
+ * host. */
 int gskyhip_service_run(const char *socket_path, int max_batch, int window_us);   /* blocks until shutdown */
 int gskyhip_service_register_granule(const char *socket_path, const char *path, int band,
                                      const gskyhip_granule *g, const void *data, const void *const *ovr_data,
@@ -336,11 +346,12 @@ int gskyhip_service_register_granule(const char *socket_path, const char *path, 
 int gskyhip_service_unregister_all(const char *socket_path);
 /* stats[4]: warp requests served, batches run, largest batch, registered granules */
 int gskyhip_service_stats(const char *socket_path, int64_t *stats);
-/* the same and, at [4], nanoseconds the daemon spent in warp batches, at [5]
- * the summed residence of requests (enqueued -> answer ready), at [6..8] the
- * warp batches' host preparation, launches through the first read-back, and
- * window read-back (ns); the first n_stats values are written (0 past what
- * the daemon reports) */
+/* the same and, at [4], nanoseconds the dispatcher spent preparing and
+ * launching batches, at [5] the summed residence of requests (enqueued ->
+ * answer ready), at [6..8] the warp batches' launch, wait for the GPU and
+ * staged window read-back (ns), at [9] replies whose window the GPU wrote into
+ * the worker's arena, at [10] replies whose window was copied; the first
+ * n_stats values are written (0 past what the daemon reports) */
 int gskyhip_service_stats_n(const char *socket_path, int64_t *stats, int n_stats);
 int gskyhip_service_shutdown(const char *socket_path);
 

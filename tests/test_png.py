@@ -3,8 +3,9 @@ the GPU path (gskyhip_encode_png): PNG structure (signature, IHDR colour type
 RGB for opaque tiles / RGBA otherwise, IDAT chunks of 32768 bytes but the
 last, IEND, CRCs), and the decompressed IDAT stream equal byte for byte to
 the oracle's restatement of Go's writeImage (NRGBA conversion, per-row filter
-choice).  The deflate bytes are zlib's, not Go's compress/flate (parity
-unpinned); PIL decodes every PNG to the expected pixels."""
+choice).  The deflate bytes are the GPU deflate's (encode.hip), neither
+zlib's nor Go's compress/flate (parity unpinned); every stream is inflated by
+zlib and PIL decodes every PNG to the expected pixels."""
 import io
 import struct
 import zlib

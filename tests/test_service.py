@@ -89,6 +89,12 @@ def test_loadgen_counts_and_timing():
         assert r["wall_s"] > 0 and r["requests_per_s"] > 0 and r["p99_ms"] >= r["p50_ms"] > 0
         assert s1["requests"] - s0["requests"] == 40
         assert s1["batch_s"] >= s0["batch_s"] and s1["resident_s"] > s0["resident_s"]
+        # steady state: 3 untimed requests per worker, then a timed window
+        r = service_load(sock, jobs, 4, seconds=0.5, warmup=3)
+        s2 = svc.stats()
+        assert r["requests"] > 0 and r["errors"] == r["requests"] and r["warmup_per_worker"] == 3
+        assert s2["requests"] - s1["requests"] == r["requests"] + 4 * 3
+        assert 0.5 <= r["wall_s"] < 5.0
     finally:
         assert svc.shutdown() == 0
 
@@ -185,16 +191,19 @@ def _spin(sock, job):
 
 
 @pytest.mark.gpu
-def test_service_workers_share_one_gpu(oracle):
+@pytest.mark.parametrize("direct", [1, 0])
+def test_service_workers_share_one_gpu(oracle, direct):
     """8 worker processes (no HIP context of their own) warp every (tile,
     granule) pair of a C2 batch through one gskyhipd: each window bit-exact
     against the oracle, requests batched across workers, a SIGKILLed worker
-    leaving the daemon serving."""
+    leaving the daemon serving.  direct=1: the warp kernel writes every
+    window into the worker's registered reply arena; direct=0
+    (GSKYHIP_SVC_DIRECT=0): staged in HBM, read back and copied."""
     from gsky_amd import WarpService
     from gsky_amd.tiles import bbox_to_geot
     cfg = synth.config_c2(scale=0.1, tiles_per_side=4, tile_px=256)
     sock = _sock_path()
-    svc = WarpService(sock, max_batch=64, window_us=2000)
+    svc = WarpService(sock, max_batch=64, window_us=2000, env={"GSKYHIP_SVC_DIRECT": str(direct)})
     try:
         for k, g in enumerate(cfg.granules):
             svc.register_granule("/g/data/c2/g%d.tif" % k, 1, g.data, g.geot, "EPSG:3577", g.nodata,
@@ -225,6 +234,9 @@ def test_service_workers_share_one_gpu(oracle):
         assert n_checked == len(jobs)
         st = svc.stats()
         assert st["requests"] == len(jobs) and st["max_batch"] > 1 and st["batches"] < len(jobs), st
+        n_ok = st["in_place"] + st["copied"]
+        assert n_ok == len(jobs), st
+        assert st["in_place"] == (len(jobs) if direct else 0), st
         # a worker SIGKILLed while its requests are in flight (gdal-process is killed after 120 s,
         # gdal-process/main.go:57-68): the daemon keeps serving
         p = ctx.Process(target=_spin, args=(sock, jobs[0]))
