@@ -65,9 +65,25 @@ __device__ __forceinline__ void bil_fold4(u32x2 t0, u32x2 t1, WT rx, WT ry, int 
   c = take ? v : c;
 }
 
+// Typed float canvas row (tile_merger.go:562-652), at the chunk's place in
+// the coverage: 8 non-temporal stores per lane, each covering 64 columns.
+__device__ __forceinline__ void bil_store(const RenderArgs &a, int t, int r, int xl, int lane, bool full, int ncols,
+                                          const float (&c)[kNnPx]) {
+  const int64_t eo = a.cov_offsets ? a.cov_offsets[t] + (int64_t)r * a.cov_stride + xl : (int64_t)r * a.max_w + xl;
+  float *cdst = (float *)(a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride) + eo;
+  if (full) {
+#pragma unroll
+    for (int q = 0; q < kNnPx; q++) __builtin_nontemporal_store(__float_as_uint(c[q]), (GPTR(uint32_t))(cdst + 64 * q));
+  } else {
+#pragma unroll
+    for (int q = 0; q < kNnPx; q++)
+      if (64 * q + lane < ncols) __builtin_nontemporal_store(__float_as_uint(c[q]), (GPTR(uint32_t))(cdst + 64 * q));
+  }
+}
+
 // HP: pixels whose taps are in flight together; WPS: waves per SIMD the
 // register budget is sized for.
-template <typename WT, int RPW, int HP, int WPS, bool FIX = true>
+template <typename WT, int RPW, int HP, int WPS, bool FIX = true, bool SEP = true>
 __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                             const int32_t *__restrict__ order,
                                                             const RowRec *__restrict__ rows,
@@ -100,6 +116,123 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
   const int ncols = min(kBandCols, W - xb);
   const bool full = ncols == kBandCols;
   const int xl = xb + lane;
+
+  // Separable rows (EPSG:4326 -> 3857: the source x depends on the
+  // destination column only, the source y on the row only): when the tile has
+  // one entry and every row of this wave is LINEAR with the same (xs0, dX) and
+  // dY == 0 -- bit for bit, as plan_row writes them from the shared column
+  // parts -- and every tap lies inside the band, each lane's x taps and
+  // weights are computed once for all RPW rows and a row's y tap and weight
+  // are one uniform value.  Every value is the one the per-row code below
+  // computes (the same expressions); the wave then stores and leaves, so the
+  // per-row code's registers are not shared with this path's.
+  if (SEP && n_entries == 1) {
+    const EntryD &e = ents[ord[0]];
+    const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
+    const int nrows = min(RPW, H - r0);
+    const int lim = max(0, min(ew, W - exoff));
+    const int c0 = exoff - xb, c1 = exoff + lim - xb;
+    const double nd64 = e.nodata64;
+    const bool nd_f32 = e.has_nodata == 0 || nd64 != nd64 || (double)(float)nd64 == nd64;
+    const int bx = e.band_x, by = e.band_y;
+    bool sep = e.ns == ns_out && ew > 0 && r0 - eyoff >= 0 && r0 + nrows - eyoff <= eh && c1 > 0 && c0 < ncols &&
+               nd_f32;
+    const RowRec *rr0 = rows + e.row_base + (r0 - eyoff);
+    const int ic0 = xl - exoff;
+    double xs0 = 0.0, dX = 0.0;
+    if (sep) {
+      xs0 = uni64d(rr0->v[0]);
+      dX = uni64d(rr0->v[2]);
+      for (int j = 0; j < nrows; j++) {
+        const RowRec *rj = rr0 + j;
+        const double sy = uni64d(rj->v[1]) + uni64d(rj->v[3]) * (double)ic0;
+        const int iy = (int)floor(sy - 0.5);
+        sep = sep & (__builtin_amdgcn_readfirstlane(rj->kind) == ROW_LINEAR) & (uni64d(rj->v[0]) == xs0) &
+              (uni64d(rj->v[2]) == dX) & (uni64d(rj->v[3]) == 0.0) & ((unsigned)iy < (unsigned)(by - 1));
+      }
+    }
+    if (sep) {
+      // per lane and pixel: the x tap's byte offset (past the buffer for a
+      // pixel outside the window: its loads read 0 and it is not taken) and
+      // the x weight
+      uint32_t xo[kNnPx];
+      WT rxv[kNnPx];
+      bool xin = true;
+#pragma unroll
+      for (int q = 0; q < kNnPx; q++) {
+        const int ic = ic0 + 64 * q;
+        const double sx = xs0 + dX * (double)ic;
+        const int ix = (int)floor(sx - 0.5);
+        rxv[q] = (WT)(1.5 - (sx - (double)ix));
+        const bool ok = (unsigned)ic < (unsigned)lim;
+        xo[q] = ok ? (uint32_t)ix * 4u : 0x80000000u;
+        xin = xin & (!ok | ((unsigned)ix < (unsigned)(bx - 1)));
+      }
+      if (__all(xin)) {
+        const float nd = e.nd.f, fillv = e.fill.f, ndf = (float)nd64;
+        const bool fill_mode = e.fill_mode != 0, hnd = e.has_nodata != 0, nd_nan = nd64 != nd64;
+        const bool take_any = !fill_mode | (cnod == nd);   // one entry: the canvas holds its nodata
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * 4), 0x00020000);
+#pragma unroll 1
+        for (int j = 0; j < nrows; j++) {
+          const int r = r0 + j;
+          const RowRec *rj = rr0 + j;
+          const double sy = uni64d(rj->v[1]) + uni64d(rj->v[3]) * (double)ic0;
+          const int iy = (int)floor(sy - 0.5);
+          const WT ry = (WT)(1.5 - (sy - (double)iy));
+          const WT one = (WT)1.0;
+          const WT wy[2] = {ry, one - ry};
+          const uint32_t base0 = (uint32_t)(iy * bx) * 4u, base1 = base0 + (uint32_t)bx * 4u;
+          const int64_t eo = a.cov_offsets ? a.cov_offsets[t] + (int64_t)r * a.cov_stride + xl
+                                           : (int64_t)r * a.max_w + xl;
+          float *cdst = (float *)(a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride) + eo;
+#pragma unroll
+          for (int h = 0; h < kNnPx; h += HP) {
+            u32x2 t0[HP], t1[HP];
+#pragma unroll
+            for (int q = 0; q < HP; q++) {
+              t0[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, base0 + xo[h + q], 0, 0);
+              t1[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, base1 + xo[h + q], 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < HP; q++) {
+              const float tv[4] = {__uint_as_float(t0[q].x), __uint_as_float(t0[q].y), __uint_as_float(t1[q].x),
+                                   __uint_as_float(t1[q].y)};
+              const WT wx[2] = {rxv[h + q], one - rxv[h + q]};
+              WT accR = (WT)0.0;
+              bool anynd = false;
+#pragma unroll
+              for (int kk = 0; kk < 4; kk++) {
+                accR += (WT)tv[kk] * (wx[kk & 1] * wy[kk >> 1]);
+                anynd = anynd | (nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+              }
+              anynd = anynd & hnd;
+              float v = (float)accR;
+              if (anynd) {   // drop the nodata taps and renormalise (bil_sample's rule)
+                WT aR = (WT)0.0, aD = (WT)0.0;
+#pragma unroll
+                for (int kk = 0; kk < 4; kk++) {
+                  const WT w = wx[kk & 1] * wy[kk >> 1];
+                  const bool use = !(nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+                  aD += use ? w : (WT)0.0;
+                  aR += use ? (WT)tv[kk] * w : (WT)0.0;
+                }
+                v = fillv;
+                if (aD == (WT)1.0) v = (float)aR;
+                else if (aD >= (WT)0.00001) v = (float)(aR / aD);
+              }
+              const bool take = (xo[h + q] != 0x80000000u) & (v != nd) & take_any;
+              const float o = take ? v : cnod;
+              if (full || 64 * (h + q) + lane < ncols)
+                __builtin_nontemporal_store(__float_as_uint(o), (GPTR(uint32_t))(cdst + 64 * (h + q)));
+            }
+          }
+        }
+        return;
+      }
+    }
+  }
 
 #pragma unroll 1
   for (int j = 0; j < RPW; j++) {
@@ -336,18 +469,7 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
       }
     }
 
-    // typed float canvas (tile_merger.go:562-652), at the chunk's place in the coverage
-    const int64_t eo = a.cov_offsets ? a.cov_offsets[t] + (int64_t)r * a.cov_stride + xl
-                                     : (int64_t)r * a.max_w + xl;
-    float *cdst = (float *)(a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride) + eo;
-    if (full) {
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) __builtin_nontemporal_store(__float_as_uint(c[q]), (GPTR(uint32_t))(cdst + 64 * q));
-    } else {
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++)
-        if (64 * q + lane < ncols) __builtin_nontemporal_store(__float_as_uint(c[q]), (GPTR(uint32_t))(cdst + 64 * q));
-    }
+    bil_store(a, t, r, xl, lane, full, ncols, c);
   }
 }
 
@@ -355,10 +477,10 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
 // 4 pixels' taps in flight at 8 waves per SIMD; the A/B build also has the
 // fp64 weights (GSKYHIP_BIL_F32=0: 6 waves per SIMD, or 8 with 2 pixels in
 // flight, GSKYHIP_BIL_HP=2) and 8 rows per wave (GSKYHIP_BIL_RPW=8).
-template <typename WT, int RPW, int HP, int WPS, bool FIX = true>
+template <typename WT, int RPW, int HP, int WPS, bool FIX = true, bool SEP = true>
 void launch_bil_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_bil_kernel<WT, RPW, HP, WPS, FIX>), dim3((unsigned)items), dim3(256), 0, s, a,
+  hipLaunchKernelGGL((render_bil_kernel<WT, RPW, HP, WPS, FIX, SEP>), dim3((unsigned)items), dim3(256), 0, s, a,
                      a.entries, a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -368,13 +490,18 @@ void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   const char *f = getenv("GSKYHIP_BIL_F32");
   const char *rp = getenv("GSKYHIP_BIL_RPW");
   const char *hp = getenv("GSKYHIP_BIL_HP");
+  const char *sp = getenv("GSKYHIP_BIL_SEP");   // 0: no separable-row reuse (round 4's kernel)
   const bool f32 = !f || atoi(f) != 0;
   const int rpw = rp ? atoi(rp) : 4;
   const int hpx = hp ? atoi(hp) : 4;
+  const bool sep = !sp || atoi(sp) != 0;
   const char *fx = getenv("GSKYHIP_BIL_FIX");   // 1: the fixed-point LINEAR rows
   if (fx && atoi(fx) == 1) { launch_bil_v<float, 4, 4, 8, true>(a, s); return; }
   if (f32) {
-    if (rpw == 8) launch_bil_v<float, 8, 4, 8, false>(a, s); else launch_bil_v<float, 4, 4, 8, false>(a, s);
+    if (!sep) launch_bil_v<float, 4, 4, 8, false, false>(a, s);
+    else if (rpw == 8) launch_bil_v<float, 8, 4, 8, false>(a, s);
+    else if (rpw == 16) launch_bil_v<float, 16, 4, 8, false>(a, s);
+    else launch_bil_v<float, 4, 4, 8, false>(a, s);
   } else if (hpx == 2) {
     launch_bil_v<double, 4, 2, 8, false>(a, s);
   } else {
@@ -383,7 +510,8 @@ void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   return;
 #endif
   // the fp64 row code: the fixed-point LINEAR rows cut VALU but measured
-  // slower on C3 (profiles/r04b_ab_c2c3c5.jsonl: 0.93 vs 0.82 ms)
+  // slower on C3 (profiles/r04b_ab_c2c5.jsonl: 0.93 vs 0.82 ms); separable
+  // rows reuse each lane's x taps across the wave's rows
   launch_bil_v<float, 4, 4, 8, false>(a, s);
 }
 

@@ -52,6 +52,10 @@ __device__ __forceinline__ int64_t uni64(int64_t v) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+__device__ __forceinline__ double uni64d(double v) {
+  return __longlong_as_double(uni64(__double_as_longlong(v)));
+}
+
 // nn_px() of source coordinates (sx, sy): the element index, or kNoPx where
 // the reference's window fill applies.
 __device__ __forceinline__ uint32_t nn_index_sxy(double sx, double sy, bool ok, int bx, int by) {
