@@ -81,6 +81,180 @@ __device__ __forceinline__ void bil_store(const RenderArgs &a, int t, int r, int
   }
 }
 
+// Separable rows (EPSG:4326 -> 3857: the source x depends on the
+// destination column only, the source y on the row only).  A wave (rows r0 ..
+// r0 + nrows - 1 of the block's columns) is eligible when exactly one entry
+// reaches those rows and columns, it covers every one of the rows, the rows
+// are LINEAR with the same (xs0, dX) and dY == 0 -- bit for bit, as plan_row
+// writes them from the shared column parts -- the band's nodata is exact in
+// float32, and every sampled pixel's 2x2 taps lie inside the band (no -1 edge
+// rule, no tap outside).  Then each lane's x taps and weights serve all the
+// wave's rows and a row's y tap and weight are one uniform value.  Wave-uniform.
+struct BilSep {
+  int entry;
+  double xs0, dX;
+};
+template <typename WT>
+__device__ __forceinline__ bool bil_sep_eligible(const EntryD *__restrict__ ents, const int32_t *__restrict__ ord,
+                                                 int n_entries, const RowRec *__restrict__ rows, int ns_out, int r0,
+                                                 int nrows, int xb, int ncols, int W, int xl, BilSep &sp) {
+  int found = -1, n_touch = 0;
+  for (int k = 0; k < n_entries; k++) {
+    const int ek = ord[k];
+    const EntryD &e = ents[ek];
+    if (e.ns != ns_out || e.w <= 0) continue;
+    if (r0 + nrows <= e.yoff || r0 >= e.yoff + e.h) continue;   // no row of the wave in the entry's window
+    const int lim = max(0, min(e.w, W - e.xoff));
+    const int c0 = e.xoff - xb, c1 = e.xoff + lim - xb;
+    if (c1 <= 0 || c0 >= ncols) continue;                        // no column of the block
+    n_touch++;
+    found = ek;
+  }
+  if (n_touch != 1) return false;
+  const EntryD &e = ents[found];
+  const double nd64 = e.nodata64;
+  const bool nd_f32 = e.has_nodata == 0 || nd64 != nd64 || (double)(float)nd64 == nd64;
+  if (!nd_f32 || r0 < e.yoff || r0 + nrows > e.yoff + e.h) return false;
+  const RowRec *rr0 = rows + e.row_base + (r0 - e.yoff);
+  const double xs0 = uni64d(rr0->v[0]), dX = uni64d(rr0->v[2]);
+  const int ic0 = xl - e.xoff;
+  bool ok = true;
+  for (int j = 0; j < nrows; j++) {
+    const RowRec *rj = rr0 + j;
+    const double sy = uni64d(rj->v[1]) + uni64d(rj->v[3]) * (double)ic0;
+    const int iy = (int)floor(sy - 0.5);
+    ok = ok & (__builtin_amdgcn_readfirstlane(rj->kind) == ROW_LINEAR) & (uni64d(rj->v[0]) == xs0) &
+         (uni64d(rj->v[2]) == dX) & (uni64d(rj->v[3]) == 0.0) & ((unsigned)iy < (unsigned)(e.band_y - 1));
+  }
+  if (!ok) return false;
+  const int lim = max(0, min(e.w, W - e.xoff));
+  bool xin = true;
+#pragma unroll
+  for (int q = 0; q < kNnPx; q++) {
+    const int ic = ic0 + 64 * q;
+    const double sx = xs0 + dX * (double)ic;
+    const int ix = (int)floor(sx - 0.5);
+    xin = xin & (((unsigned)ic >= (unsigned)lim) | ((unsigned)ix < (unsigned)(e.band_x - 1)));
+  }
+  if (!__all(xin)) return false;
+  sp.entry = found;
+  sp.xs0 = xs0;
+  sp.dX = dX;
+  return true;
+}
+
+// The waves render_bil_kernel leaves to it (bil_sep_eligible): per lane the 8
+// pixels' x tap offsets and weights once, then per row one uniform y tap and
+// weight, HP pixels' taps in flight, the same expressions as
+// render_bil_kernel's all-inside path (so the same values), 8 stores a row.
+template <typename WT, int RPW, int HP, int WPS>
+__global__ __launch_bounds__(256, WPS) void render_bil_sep_kernel(RenderArgs a, const EntryD *__restrict__ ents,
+                                                                const int32_t *__restrict__ order,
+                                                                const RowRec *__restrict__ rows,
+                                                                const TilePlan *__restrict__ tplans,
+                                                                const gskyhip_tile *__restrict__ tiles, int n_items) {
+  constexpr int kRowsBlk = 4 * RPW;
+  const int item = blockIdx.x;
+  if (item >= n_items) return;
+  const int bands_per_tile = (a.max_h + kRowsBlk - 1) / kRowsBlk;
+  const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
+  const int t = item / (bands_per_tile * col_blocks);
+  const int in_tile = item - t * bands_per_tile * col_blocks;
+  const TilePlan &tp = tplans[t];
+  if (tp.complex || tp.n_entries <= 0 || tp.vt != GSKYHIP_FLOAT32) return;
+  const gskyhip_tile &tile = tiles[t];
+  const int W = tile.width, H = tile.height;
+  const int band0 = (in_tile / col_blocks) * kRowsBlk;
+  const int xb = (in_tile % col_blocks) * kBandCols;
+  if (band0 >= H || xb >= W) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r0 = band0 + wave * RPW;
+  if (r0 >= H) return;
+  const int ns_out = a.out_ns[0];
+  const int32_t *ord = order + tile.pair_begin;
+  const int ncols = min(kBandCols, W - xb);
+  const bool full = ncols == kBandCols;
+  const int xl = xb + lane;
+  const int nrows = min(RPW, H - r0);
+  BilSep sp;
+  if (!bil_sep_eligible<WT>(ents, ord, tp.n_entries, rows, ns_out, r0, nrows, xb, ncols, W, xl, sp)) return;
+  const float cnod = go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]).f;
+  const EntryD &e = ents[sp.entry];
+  const int bx = e.band_x, by = e.band_y;
+  const int lim = max(0, min(e.w, W - e.xoff));
+  const int ic0 = xl - e.xoff;
+  const RowRec *rr0 = rows + e.row_base + (r0 - e.yoff);
+  // per lane and pixel: the x tap's byte offset (past the buffer for a pixel
+  // outside the window: its loads read 0 and it is not taken), the x weight
+  uint32_t xo[kNnPx];
+  WT rxv[kNnPx];
+#pragma unroll
+  for (int q = 0; q < kNnPx; q++) {
+    const int ic = ic0 + 64 * q;
+    const double sx = sp.xs0 + sp.dX * (double)ic;
+    const int ix = (int)floor(sx - 0.5);
+    rxv[q] = (WT)(1.5 - (sx - (double)ix));
+    xo[q] = (unsigned)ic < (unsigned)lim ? (uint32_t)ix * 4u : 0x80000000u;
+  }
+  const double nd64 = e.nodata64;
+  const float nd = e.nd.f, fillv = e.fill.f, ndf = (float)nd64;
+  const bool hnd = e.has_nodata != 0, nd_nan = nd64 != nd64;
+  const bool take_any = (e.fill_mode == 0) | (cnod == nd);   // one entry: the canvas holds its nodata
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)uniform_ptr(e.band), (short)0,
+                                                                      (int)((int64_t)bx * by * 4), 0x00020000);
+#pragma unroll 1
+  for (int j = 0; j < nrows; j++) {
+    const RowRec *rj = rr0 + j;
+    const double sy = uni64d(rj->v[1]) + uni64d(rj->v[3]) * (double)ic0;
+    const int iy = (int)floor(sy - 0.5);
+    const WT ry = (WT)(1.5 - (sy - (double)iy));
+    const WT one = (WT)1.0;
+    const WT wy[2] = {ry, one - ry};
+    const uint32_t base0 = (uint32_t)(iy * bx) * 4u, base1 = base0 + (uint32_t)bx * 4u;
+    float c[kNnPx];
+#pragma unroll
+    for (int h = 0; h < kNnPx; h += HP) {
+      u32x2 t0[HP], t1[HP];
+#pragma unroll
+      for (int q = 0; q < HP; q++) {
+        t0[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, base0 + xo[h + q], 0, 0);
+        t1[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, base1 + xo[h + q], 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < HP; q++) {
+        const float tv[4] = {__uint_as_float(t0[q].x), __uint_as_float(t0[q].y), __uint_as_float(t1[q].x),
+                             __uint_as_float(t1[q].y)};
+        const WT wx[2] = {rxv[h + q], one - rxv[h + q]};
+        WT accR = (WT)0.0;
+        bool anynd = false;
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+          accR += (WT)tv[kk] * (wx[kk & 1] * wy[kk >> 1]);
+          anynd = anynd | (nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+        }
+        anynd = anynd & hnd;
+        float v = (float)accR;
+        if (anynd) {   // drop the nodata taps and renormalise (bil_sample's rule)
+          WT aR = (WT)0.0, aD = (WT)0.0;
+#pragma unroll
+          for (int kk = 0; kk < 4; kk++) {
+            const WT w = wx[kk & 1] * wy[kk >> 1];
+            const bool use = !(nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+            aD += use ? w : (WT)0.0;
+            aR += use ? (WT)tv[kk] * w : (WT)0.0;
+          }
+          v = fillv;
+          if (aD == (WT)1.0) v = (float)aR;
+          else if (aD >= (WT)0.00001) v = (float)(aR / aD);
+        }
+        const bool take = (xo[h + q] != 0x80000000u) & (v != nd) & take_any;
+        c[h + q] = take ? v : cnod;
+      }
+    }
+    bil_store(a, t, r0 + j, xl, lane, full, ncols, c);
+  }
+}
+
 // HP: pixels whose taps are in flight together; WPS: waves per SIMD the
 // register budget is sized for.
 template <typename WT, int RPW, int HP, int WPS, bool FIX = true, bool SEP = true>
@@ -117,121 +291,10 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
   const bool full = ncols == kBandCols;
   const int xl = xb + lane;
 
-  // Separable rows (EPSG:4326 -> 3857: the source x depends on the
-  // destination column only, the source y on the row only): when the tile has
-  // one entry and every row of this wave is LINEAR with the same (xs0, dX) and
-  // dY == 0 -- bit for bit, as plan_row writes them from the shared column
-  // parts -- and every tap lies inside the band, each lane's x taps and
-  // weights are computed once for all RPW rows and a row's y tap and weight
-  // are one uniform value.  Every value is the one the per-row code below
-  // computes (the same expressions); the wave then stores and leaves, so the
-  // per-row code's registers are not shared with this path's.
-  if (SEP && n_entries == 1) {
-    const EntryD &e = ents[ord[0]];
-    const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
-    const int nrows = min(RPW, H - r0);
-    const int lim = max(0, min(ew, W - exoff));
-    const int c0 = exoff - xb, c1 = exoff + lim - xb;
-    const double nd64 = e.nodata64;
-    const bool nd_f32 = e.has_nodata == 0 || nd64 != nd64 || (double)(float)nd64 == nd64;
-    const int bx = e.band_x, by = e.band_y;
-    bool sep = e.ns == ns_out && ew > 0 && r0 - eyoff >= 0 && r0 + nrows - eyoff <= eh && c1 > 0 && c0 < ncols &&
-               nd_f32;
-    const RowRec *rr0 = rows + e.row_base + (r0 - eyoff);
-    const int ic0 = xl - exoff;
-    double xs0 = 0.0, dX = 0.0;
-    if (sep) {
-      xs0 = uni64d(rr0->v[0]);
-      dX = uni64d(rr0->v[2]);
-      for (int j = 0; j < nrows; j++) {
-        const RowRec *rj = rr0 + j;
-        const double sy = uni64d(rj->v[1]) + uni64d(rj->v[3]) * (double)ic0;
-        const int iy = (int)floor(sy - 0.5);
-        sep = sep & (__builtin_amdgcn_readfirstlane(rj->kind) == ROW_LINEAR) & (uni64d(rj->v[0]) == xs0) &
-              (uni64d(rj->v[2]) == dX) & (uni64d(rj->v[3]) == 0.0) & ((unsigned)iy < (unsigned)(by - 1));
-      }
-    }
-    if (sep) {
-      // per lane and pixel: the x tap's byte offset (past the buffer for a
-      // pixel outside the window: its loads read 0 and it is not taken) and
-      // the x weight
-      uint32_t xo[kNnPx];
-      WT rxv[kNnPx];
-      bool xin = true;
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) {
-        const int ic = ic0 + 64 * q;
-        const double sx = xs0 + dX * (double)ic;
-        const int ix = (int)floor(sx - 0.5);
-        rxv[q] = (WT)(1.5 - (sx - (double)ix));
-        const bool ok = (unsigned)ic < (unsigned)lim;
-        xo[q] = ok ? (uint32_t)ix * 4u : 0x80000000u;
-        xin = xin & (!ok | ((unsigned)ix < (unsigned)(bx - 1)));
-      }
-      if (__all(xin)) {
-        const float nd = e.nd.f, fillv = e.fill.f, ndf = (float)nd64;
-        const bool fill_mode = e.fill_mode != 0, hnd = e.has_nodata != 0, nd_nan = nd64 != nd64;
-        const bool take_any = !fill_mode | (cnod == nd);   // one entry: the canvas holds its nodata
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * 4), 0x00020000);
-#pragma unroll 1
-        for (int j = 0; j < nrows; j++) {
-          const int r = r0 + j;
-          const RowRec *rj = rr0 + j;
-          const double sy = uni64d(rj->v[1]) + uni64d(rj->v[3]) * (double)ic0;
-          const int iy = (int)floor(sy - 0.5);
-          const WT ry = (WT)(1.5 - (sy - (double)iy));
-          const WT one = (WT)1.0;
-          const WT wy[2] = {ry, one - ry};
-          const uint32_t base0 = (uint32_t)(iy * bx) * 4u, base1 = base0 + (uint32_t)bx * 4u;
-          const int64_t eo = a.cov_offsets ? a.cov_offsets[t] + (int64_t)r * a.cov_stride + xl
-                                           : (int64_t)r * a.max_w + xl;
-          float *cdst = (float *)(a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride) + eo;
-#pragma unroll
-          for (int h = 0; h < kNnPx; h += HP) {
-            u32x2 t0[HP], t1[HP];
-#pragma unroll
-            for (int q = 0; q < HP; q++) {
-              t0[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, base0 + xo[h + q], 0, 0);
-              t1[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, base1 + xo[h + q], 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < HP; q++) {
-              const float tv[4] = {__uint_as_float(t0[q].x), __uint_as_float(t0[q].y), __uint_as_float(t1[q].x),
-                                   __uint_as_float(t1[q].y)};
-              const WT wx[2] = {rxv[h + q], one - rxv[h + q]};
-              WT accR = (WT)0.0;
-              bool anynd = false;
-#pragma unroll
-              for (int kk = 0; kk < 4; kk++) {
-                accR += (WT)tv[kk] * (wx[kk & 1] * wy[kk >> 1]);
-                anynd = anynd | (nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
-              }
-              anynd = anynd & hnd;
-              float v = (float)accR;
-              if (anynd) {   // drop the nodata taps and renormalise (bil_sample's rule)
-                WT aR = (WT)0.0, aD = (WT)0.0;
-#pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-                  const WT w = wx[kk & 1] * wy[kk >> 1];
-                  const bool use = !(nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
-                  aD += use ? w : (WT)0.0;
-                  aR += use ? (WT)tv[kk] * w : (WT)0.0;
-                }
-                v = fillv;
-                if (aD == (WT)1.0) v = (float)aR;
-                else if (aD >= (WT)0.00001) v = (float)(aR / aD);
-              }
-              const bool take = (xo[h + q] != 0x80000000u) & (v != nd) & take_any;
-              const float o = take ? v : cnod;
-              if (full || 64 * (h + q) + lane < ncols)
-                __builtin_nontemporal_store(__float_as_uint(o), (GPTR(uint32_t))(cdst + 64 * (h + q)));
-            }
-          }
-        }
-        return;
-      }
-    }
+  // waves whose rows are separable run in render_bil_sep_kernel
+  if (SEP && n_entries > 0) {
+    BilSep sp;
+    if (bil_sep_eligible<WT>(ents, ord, n_entries, rows, ns_out, r0, min(RPW, H - r0), xb, ncols, W, xl, sp)) return;
   }
 
 #pragma unroll 1
@@ -477,11 +540,14 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
 // 4 pixels' taps in flight at 8 waves per SIMD; the A/B build also has the
 // fp64 weights (GSKYHIP_BIL_F32=0: 6 waves per SIMD, or 8 with 2 pixels in
 // flight, GSKYHIP_BIL_HP=2) and 8 rows per wave (GSKYHIP_BIL_RPW=8).
-template <typename WT, int RPW, int HP, int WPS, bool FIX = true, bool SEP = true>
+template <typename WT, int RPW, int HP, int WPS, bool FIX = true, bool SEP = true, int SHP = 4, int SWPS = 8>
 void launch_bil_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
   hipLaunchKernelGGL((render_bil_kernel<WT, RPW, HP, WPS, FIX, SEP>), dim3((unsigned)items), dim3(256), 0, s, a,
                      a.entries, a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
+  if (SEP)
+    hipLaunchKernelGGL((render_bil_sep_kernel<WT, RPW, SHP, SWPS>), dim3((unsigned)items), dim3(256), 0, s, a,
+                       a.entries, a.order, a.rows, a.tplans, a.tiles, items);
 }
 
 void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
@@ -499,6 +565,7 @@ void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   if (fx && atoi(fx) == 1) { launch_bil_v<float, 4, 4, 8, true>(a, s); return; }
   if (f32) {
     if (!sep) launch_bil_v<float, 4, 4, 8, false, false>(a, s);
+    else if (hpx == 8) launch_bil_v<float, 4, 4, 8, false, true, 8, 6>(a, s);
     else if (rpw == 8) launch_bil_v<float, 8, 4, 8, false>(a, s);
     else if (rpw == 16) launch_bil_v<float, 16, 4, 8, false>(a, s);
     else launch_bil_v<float, 4, 4, 8, false>(a, s);

@@ -211,17 +211,17 @@ bool get_req(In &in, WarpReq &q) {
 // buffer) and received straight into the caller's memory.
 constexpr size_t kRespFixed = 4 + 16 + 8 + 4 + 4 + 48 + 8;
 
-void put_resp_fixed(Out &o, const WarpResp &r) {
+void put_resp_fixed(Out &o, const WarpResp &r, uint64_t n_data) {
   o.put(r.rc);
   for (int32_t v : r.bbox) o.put(v);
   o.put(r.nodata); o.put(r.dtype); o.put(r.bytes_read);
   for (double v : r.src_gt) o.put(v);
-  o.put<uint64_t>(r.data.size());
+  o.put<uint64_t>(n_data);
 }
 
 bool send_resp(int fd, const WarpResp &r) {
   Out o;
-  put_resp_fixed(o, r);
+  put_resp_fixed(o, r, r.data.size());
   char hdr[16];
   const uint32_t op = SVC_WARP;
   const uint64_t n = o.b.size() + r.data.size();
@@ -595,7 +595,8 @@ bool read_all_fd(int fd, void *buf, size_t n, int &passed) {
 // offset 0 of the worker's arena; 0: inline after this word).
 bool send_resp_shm(int fd, const WarpResp &r, const ArenaPtr &arena, Service *s) {
   Out o;
-  put_resp_fixed(o, r);   // its length word is the window length wherever it is
+  // the length word is the window's length wherever it is
+  put_resp_fixed(o, r, r.rc == 0 && r.in_place >= 0 ? (uint64_t)r.in_place : r.data.size());
   const char *inl = nullptr;
   size_t n_inl = 0;
   uint32_t where = 0;

@@ -168,10 +168,13 @@ def test_service_unreachable():
 
 
 # ---------------------------------------------------------------- GPU
-def _warp_jobs(sock, wid, jobs, q):
-    """A worker process: warp_raster over the service for its (tile, granule) jobs."""
+def _warp_jobs(sock, wid, jobs, q, go=None):
+    """A worker process: warp_raster over the service for its (tile, granule)
+    jobs (all workers start together when `go` is given)."""
     os.environ["GSKYHIP_SERVICE"] = sock
     from gsky_amd import worker as W
+    if go is not None:
+        go.wait(120)
     res = []
     for (k, gt, w, h) in jobs:
         r = W.warp_raster(W.GeoRPCGranule(path="/g/data/c2/g%d.tif" % k, bands=[1], width=w, height=h,
@@ -211,11 +214,13 @@ def test_service_workers_share_one_gpu(oracle, direct):
         assert svc.stats()["granules"] == len(cfg.granules)
         jobs = [(k, bbox_to_geot(w, h, bb), w, h) for (bb, w, h), ks in zip(cfg.tiles, cfg.pairs) for k in ks]
         ctx = mp.get_context("spawn")
-        q = ctx.Queue()
+        q, go = ctx.Queue(), ctx.Event()
         n_workers = 8
-        procs = [ctx.Process(target=_warp_jobs, args=(sock, r, jobs[r::n_workers], q)) for r in range(n_workers)]
+        procs = [ctx.Process(target=_warp_jobs, args=(sock, r, jobs[r::n_workers], q, go)) for r in range(n_workers)]
         for p in procs:
             p.start()
+        time.sleep(5.0)   # every worker imported and waiting: their requests meet in the daemon's queue
+        go.set()
         got = dict(q.get(timeout=300) for _ in procs)
         for p in procs:
             p.join(60)
