@@ -611,7 +611,7 @@ int launch_drill_deciles(const DecileCall &c) {
   const int n_slots = kHistSlots;
   int sel_lds = kSelLds, sel_u = kSelU;
 #ifdef GSKYHIP_AB
-  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(8, std::min(60, atoi(e))) * 1024;
+  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(8, std::min(64, atoi(e))) * 1024;
   if (const char *e = getenv("GSKYHIP_DEC_U")) sel_u = atoi(e);
 #endif
   const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
@@ -692,12 +692,25 @@ int launch_decile_select_fused(const float *vals, const int32_t *chunk_base, con
   const int n_slots = kHistSlots;
   int sel_lds = kSelLds;
 #ifdef GSKYHIP_AB
-  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(8, std::min(60, atoi(e))) * 1024;
+  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(8, std::min(64, atoi(e))) * 1024;
+#endif
+  int nt = kSelThreads;
+#ifdef GSKYHIP_AB
+  if (const char *e = getenv("GSKYHIP_DEC_FNT")) nt = atoi(e);   // fused select workgroup: 256 / 512 / 1024 threads
 #endif
   const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
-  hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe>), dim3((unsigned)n_seg),
-                     dim3(kSelThreads), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
-                     decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
+  if (nt == 1024)
+    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 1024, 8>), dim3((unsigned)n_seg),
+                       dim3(1024), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
+                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
+  else if (nt == 512)
+    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 512, 8>), dim3((unsigned)n_seg),
+                       dim3(512), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
+                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
+  else
+    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe>), dim3((unsigned)n_seg),
+                       dim3(kSelThreads), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
+                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 

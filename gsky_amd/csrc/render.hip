@@ -1960,6 +1960,7 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   if (const char *am = getenv("GSKYHIP_AB_MODE")) a.ab_mode = atoi(am);
   if (const char *vf = getenv("GSKYHIP_NN_VFETCH")) a.ab_vfetch = atoi(vf);
   if (const char *xc = getenv("GSKYHIP_NN_XCD")) a.ab_xcd = atoi(xc);
+  if (getenv("GSKYHIP_BIL_SEPSTAT")) a.ab_mode = 0x5E9;   // render_bil_sep_kernel's eligibility counters
 #endif
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));

@@ -94,10 +94,20 @@ struct BilSep {
   int entry;
   double xs0, dX;
 };
+#ifdef GSKYHIP_AB
+// A/B build, GSKYHIP_BIL_SEPSTAT=1: waves reaching each eligibility test
+// (0 checked, 1 one entry, 2 rows covered, 3 rows same / in band, 4 taps in band)
+__device__ unsigned long long g_bil_sep_stat[8];
+#define SEPSTAT(i) do { if (stat && __lane_id() == 0) atomicAdd(&g_bil_sep_stat[i], 1ull); } while (0)
+#else
+#define SEPSTAT(i) ((void)0)
+#endif
 template <typename WT>
 __device__ __forceinline__ bool bil_sep_eligible(const EntryD *__restrict__ ents, const int32_t *__restrict__ ord,
                                                  int n_entries, const RowRec *__restrict__ rows, int ns_out, int r0,
-                                                 int nrows, int xb, int ncols, int W, int xl, BilSep &sp) {
+                                                 int nrows, int xb, int ncols, int W, int xl, BilSep &sp,
+                                                 bool stat = false) {
+  SEPSTAT(0);
   int found = -1, n_touch = 0;
   for (int k = 0; k < n_entries; k++) {
     const int ek = ord[k];
@@ -111,10 +121,12 @@ __device__ __forceinline__ bool bil_sep_eligible(const EntryD *__restrict__ ents
     found = ek;
   }
   if (n_touch != 1) return false;
+  SEPSTAT(1);
   const EntryD &e = ents[found];
   const double nd64 = e.nodata64;
   const bool nd_f32 = e.has_nodata == 0 || nd64 != nd64 || (double)(float)nd64 == nd64;
   if (!nd_f32 || r0 < e.yoff || r0 + nrows > e.yoff + e.h) return false;
+  SEPSTAT(2);
   const RowRec *rr0 = rows + e.row_base + (r0 - e.yoff);
   const double xs0 = uni64d(rr0->v[0]), dX = uni64d(rr0->v[2]);
   const int ic0 = xl - e.xoff;
@@ -127,6 +139,7 @@ __device__ __forceinline__ bool bil_sep_eligible(const EntryD *__restrict__ ents
          (uni64d(rj->v[2]) == dX) & (uni64d(rj->v[3]) == 0.0) & ((unsigned)iy < (unsigned)(e.band_y - 1));
   }
   if (!ok) return false;
+  SEPSTAT(3);
   const int lim = max(0, min(e.w, W - e.xoff));
   bool xin = true;
 #pragma unroll
@@ -137,16 +150,19 @@ __device__ __forceinline__ bool bil_sep_eligible(const EntryD *__restrict__ ents
     xin = xin & (((unsigned)ic >= (unsigned)lim) | ((unsigned)ix < (unsigned)(e.band_x - 1)));
   }
   if (!__all(xin)) return false;
+  SEPSTAT(4);
   sp.entry = found;
   sp.xs0 = xs0;
   sp.dX = dX;
   return true;
 }
 
-// The waves render_bil_kernel leaves to it (bil_sep_eligible): per lane the 8
-// pixels' x tap offsets and weights once, then per row one uniform y tap and
-// weight, HP pixels' taps in flight, the same expressions as
-// render_bil_kernel's all-inside path (so the same values), 8 stores a row.
+// The waves render_bil_kernel leaves to it (bil_sep_eligible): per lane the
+// pixels' x tap offsets and weights once for all the wave's rows, per row one
+// uniform y tap and weight, the next row's taps in flight while a row is
+// folded and stored (HP == 0), or 8 pixels a lane with HP pixels' taps in
+// flight and 8 stores a row; the same expressions as render_bil_kernel's
+// all-inside path, so the same values.
 template <typename WT, int RPW, int HP, int WPS>
 __global__ __launch_bounds__(256, WPS) void render_bil_sep_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                 const int32_t *__restrict__ order,
@@ -177,13 +193,106 @@ __global__ __launch_bounds__(256, WPS) void render_bil_sep_kernel(RenderArgs a, 
   const int xl = xb + lane;
   const int nrows = min(RPW, H - r0);
   BilSep sp;
-  if (!bil_sep_eligible<WT>(ents, ord, tp.n_entries, rows, ns_out, r0, nrows, xb, ncols, W, xl, sp)) return;
+  if (!bil_sep_eligible<WT>(ents, ord, tp.n_entries, rows, ns_out, r0, nrows, xb, ncols, W, xl, sp,
+                           a.ab_mode == 0x5E9)) return;
   const float cnod = go_conv_to(tp.nodata[ns_out], tp.dtype[ns_out]).f;
   const EntryD &e = ents[sp.entry];
   const int bx = e.band_x, by = e.band_y;
   const int lim = max(0, min(e.w, W - e.xoff));
   const int ic0 = xl - e.xoff;
   const RowRec *rr0 = rows + e.row_base + (r0 - e.yoff);
+  if constexpr (HP == 0) {   // pipelined halves
+  const double nd64 = e.nodata64;
+  const float nd = e.nd.f, fillv = e.fill.f, ndf = (float)nd64;
+  const bool hnd = e.has_nodata != 0, nd_nan = nd64 != nd64;
+  const bool take_any = (e.fill_mode == 0) | (cnod == nd);   // one entry: the canvas holds its nodata
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)uniform_ptr(e.band), (short)0,
+                                                                      (int)((int64_t)bx * by * 4), 0x00020000);
+  // each row's y tap (byte offset of its upper source row) and weight: uniform
+  uint32_t ybase[RPW];
+  WT ryv[RPW];
+#pragma unroll
+  for (int j = 0; j < RPW; j++) {
+    const RowRec *rj = rr0 + (j < nrows ? j : 0);
+    const double sy = uni64d(rj->v[1]) + uni64d(rj->v[3]) * (double)ic0;
+    const int iy = (int)floor(sy - 0.5);
+    ryv[j] = (WT)(1.5 - (sy - (double)iy));
+    ybase[j] = (uint32_t)(iy * bx) * 4u;
+  }
+  const int64_t eo0 = a.cov_offsets ? a.cov_offsets[t] + (int64_t)r0 * a.cov_stride + xl : (int64_t)r0 * a.max_w + xl;
+  const int64_t row_stride = a.cov_offsets ? a.cov_stride : a.max_w;
+  float *cbase = (float *)(a.cov_offsets ? a.canvas : a.canvas + t * a.canvas_tile_stride) + eo0;
+  // the block's 512 columns in two halves of 4 pixels per lane, each half
+  // down all the rows with the next row's taps loaded while this row's are
+  // folded and stored (so a row's loads never wait on the stores before them)
+#pragma unroll 1
+  for (int hh = 0; hh < kNnPx; hh += 4) {
+    // per lane and pixel: the x tap's byte offset (past the buffer for a pixel
+    // outside the window: its loads read 0 and it is not taken), the x weight
+    uint32_t xo[4];
+    WT rxv[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int ic = ic0 + 64 * (hh + q);
+      const double sx = sp.xs0 + sp.dX * (double)ic;
+      const int ix = (int)floor(sx - 0.5);
+      rxv[q] = (WT)(1.5 - (sx - (double)ix));
+      xo[q] = (unsigned)ic < (unsigned)lim ? (uint32_t)ix * 4u : 0x80000000u;
+    }
+    u32x2 ta[2][4], tb[2][4];
+    auto issue = [&](int j, u32x2 (&A)[4], u32x2 (&B)[4]) {
+      const uint32_t b0 = ybase[j], b1 = b0 + (uint32_t)bx * 4u;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        A[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, b0 + xo[q], 0, 0);
+        B[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, b1 + xo[q], 0, 0);
+      }
+    };
+    issue(0, ta[0], tb[0]);
+#pragma unroll
+    for (int j = 0; j < RPW; j++) {
+      if (j >= nrows) break;
+      if (j + 1 < nrows) issue(j + 1, ta[(j + 1) & 1], tb[(j + 1) & 1]);
+      const WT one = (WT)1.0;
+      const WT wy[2] = {ryv[j], one - ryv[j]};
+      float *cdst = cbase + (int64_t)j * row_stride;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const u32x2 t0 = ta[j & 1][q], t1 = tb[j & 1][q];
+        const float tv[4] = {__uint_as_float(t0.x), __uint_as_float(t0.y), __uint_as_float(t1.x),
+                             __uint_as_float(t1.y)};
+        const WT wx[2] = {rxv[q], one - rxv[q]};
+        WT accR = (WT)0.0;
+        bool anynd = false;
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+          accR += (WT)tv[kk] * (wx[kk & 1] * wy[kk >> 1]);
+          anynd = anynd | (nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+        }
+        anynd = anynd & hnd;
+        float v = (float)accR;
+        if (anynd) {   // drop the nodata taps and renormalise (bil_sample's rule)
+          WT aR = (WT)0.0, aD = (WT)0.0;
+#pragma unroll
+          for (int kk = 0; kk < 4; kk++) {
+            const WT w = wx[kk & 1] * wy[kk >> 1];
+            const bool use = !(nd_nan ? (tv[kk] != tv[kk]) : (tv[kk] == ndf));
+            aD += use ? w : (WT)0.0;
+            aR += use ? (WT)tv[kk] * w : (WT)0.0;
+          }
+          v = fillv;
+          if (aD == (WT)1.0) v = (float)aR;
+          else if (aD >= (WT)0.00001) v = (float)(aR / aD);
+        }
+        const bool take = (xo[q] != 0x80000000u) & (v != nd) & take_any;
+        const float o = take ? v : cnod;
+        if (full || 64 * (hh + q) + lane < ncols)
+          __builtin_nontemporal_store(__float_as_uint(o), (GPTR(uint32_t))(cdst + 64 * (hh + q)));
+      }
+      __builtin_amdgcn_sched_barrier(0);   // rows stay in order: two rows' taps live, not all of them
+    }
+  }
+  } else {   // 8 pixels a lane, HP taps in flight, 8 stores a row
   // per lane and pixel: the x tap's byte offset (past the buffer for a pixel
   // outside the window: its loads read 0 and it is not taken), the x weight
   uint32_t xo[kNnPx];
@@ -252,6 +361,7 @@ __global__ __launch_bounds__(256, WPS) void render_bil_sep_kernel(RenderArgs a, 
       }
     }
     bil_store(a, t, r0 + j, xl, lane, full, ncols, c);
+  }
   }
 }
 
@@ -548,6 +658,17 @@ void launch_bil_v(const RenderArgs &a, hipStream_t s) {
   if (SEP)
     hipLaunchKernelGGL((render_bil_sep_kernel<WT, RPW, SHP, SWPS>), dim3((unsigned)items), dim3(256), 0, s, a,
                        a.entries, a.order, a.rows, a.tplans, a.tiles, items);
+#ifdef GSKYHIP_AB
+  if (SEP && a.ab_mode == 0x5E9) {   // counts of the sep kernel's checks (both kernels count: / 2)
+    unsigned long long st[8];
+    hipStreamSynchronize(s);
+    hipMemcpyFromSymbol(st, HIP_SYMBOL(g_bil_sep_stat), sizeof(st));
+    fprintf(stderr, "bil_sep_stat waves=%llu one_entry=%llu rows_covered=%llu rows_same=%llu taps_in=%llu\n",
+            st[0] / 2, st[1] / 2, st[2] / 2, st[3] / 2, st[4] / 2);
+    unsigned long long z[8] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_bil_sep_stat), z, sizeof(z));
+  }
+#endif
 }
 
 void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
@@ -566,6 +687,8 @@ void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   if (f32) {
     if (!sep) launch_bil_v<float, 4, 4, 8, false, false>(a, s);
     else if (hpx == 8) launch_bil_v<float, 4, 4, 8, false, true, 8, 6>(a, s);
+    else if (hpx == 0) launch_bil_v<float, 4, 4, 8, false, true, 0, 8>(a, s);
+    else if (hpx == 10) launch_bil_v<float, 4, 4, 8, false, true, 0, 6>(a, s);
     else if (rpw == 8) launch_bil_v<float, 8, 4, 8, false>(a, s);
     else if (rpw == 16) launch_bil_v<float, 16, 4, 8, false>(a, s);
     else launch_bil_v<float, 4, 4, 8, false>(a, s);
@@ -577,9 +700,10 @@ void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   return;
 #endif
   // the fp64 row code: the fixed-point LINEAR rows cut VALU but measured
-  // slower on C3 (profiles/r04b_ab_c2c5.jsonl: 0.93 vs 0.82 ms); separable
-  // rows reuse each lane's x taps across the wave's rows
-  launch_bil_v<float, 4, 4, 8, false>(a, s);
+  // slower on C3 (profiles/r04b_ab_c2c5.jsonl: 0.93 vs 0.82 ms); so did the
+  // separable-row kernel (72 % of C3's waves eligible, 0.86-0.93 vs 0.81 ms
+  // total, profiles/r05b_ab_c3.jsonl): no separable split in the product
+  launch_bil_v<float, 4, 4, 8, false, false>(a, s);
 }
 
 }  // namespace gsky
