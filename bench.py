@@ -642,6 +642,21 @@ def run_c5(ctx: Ctx, args):
     b = build_batch(cfg, ctx.device, gs=gs)
     sp = ScaleParams(*cfg.scale)
     dt = ctx.timed(lambda: b.render(sp), args.steps, args.warmup)
+    plan_ms = event_ms(lambda: b.render(sp, phase=1), max(3, args.steps))
+    render_ms = event_ms(lambda: b.render(sp, phase=2), max(3, args.steps))
+    # algorithmic bytes of the render launch: every (granule, picked overview
+    # level) the batch samples, the bounding box of its pairs' source
+    # footprints read once (data and QA granules alike), + the RGBA out
+    fp = {}
+    for g, lx, ly, es, x0, y0, x1, y1 in b.pair_info().tolist():
+        if x1 <= x0 or y1 <= y0:
+            continue
+        k = (g, lx, ly, es)
+        a = fp.get(k)
+        fp[k] = (x0, y0, x1, y1) if a is None else (min(a[0], x0), min(a[1], y0), max(a[2], x1), max(a[3], y1))
+    src = sum((x1 - x0) * (y1 - y0) * k[3] for k, (x0, y0, x1, y1) in fp.items())
+    abytes = int(src + cfg.out_pixels * 4)
+    achieved = abytes / (render_ms / 1e3) / 1e9
     # p50 single-tile latency: each sampled tile as its own request
     lat = tile_latency(ctx, cfg, gs, sp, None, list(range(0, len(cfg.tiles), max(1, len(cfg.tiles) // 8))), 10)
     out = {"workload": "C5: 80 512x512 EPSG:3857 overview tiles (z4+z5) from 256 MODIS sinusoidal int16 granules + "
@@ -650,7 +665,17 @@ def run_c5(ctx: Ctx, args):
            "value": round(full.out_pixels * args.steps / dt / 1e6, 1), "unit": "Mpix/s",
            "ms_per_step": round(dt / args.steps * 1e3, 4),
            "p50_tile_ms": round(float(np.percentile(lat, 50)), 4),
-           "p50_timing": "host wall of a one-tile request (plan + render + synchronize), rank 0"}
+           "p50_timing": "host wall of a one-tile request (plan + render + synchronize), rank 0",
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "traffic": pmc_traffic("render_c5") if ctx.world == 1 else None,
+                        "kernel": "render_nn_kernel<int16, mask> + render_general_kernel (phase 2, rank 0)",
+                        "kernel_ms": round(render_ms, 4), "plan_ms": round(plan_ms, 4),
+                        "algorithmic_bytes_per_launch": abytes, "source_bytes": int(src),
+                        "source_levels": len(fp),
+                        "bytes": "per (granule, picked overview level) the bounding box of the pairs' source "
+                                 "footprints (gskyhip_render_pair_info) x element size, once; + 4 B RGBA per "
+                                 "output pixel", "lib_sha16": lib_sha()}}
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
         from oracle import oracle as O
         cores = host_cores()

@@ -1352,6 +1352,22 @@ int gskyhip_render_tile_info(void *workspace, int n_tiles, int n_pairs, int max_
   return 0;
 }
 
+int gskyhip_render_pair_info(void *workspace, int n_tiles, int n_pairs, int max_tile_height, int32_t *info_out,
+                             void *stream) {
+  if (n_tiles < 0 || n_pairs < 0 || (n_pairs > 0 && (!workspace || !info_out))) return GSKYHIP_E_ARG;
+  if (n_pairs == 0) return 0;
+  int32_t *dev = nullptr;
+  if (hipMalloc((void **)&dev, (size_t)n_pairs * 8 * sizeof(int32_t)) != hipSuccess) return GSKYHIP_E_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  int rc = launch_pair_footprint(workspace, n_tiles, n_pairs, max_tile_height, dev, s);
+  if (!rc && (hipMemcpyAsync(info_out, dev, (size_t)n_pairs * 8 * sizeof(int32_t), hipMemcpyDeviceToHost, s) !=
+                  hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess))
+    rc = GSKYHIP_E_HIP;
+  (void)hipFree(dev);
+  return rc;
+}
+
 int gskyhip_warp_windows(const gskyhip_granule *granules, int n_granules, const gskyhip_crs *crs_table,
                          int n_crs, int dst_crs, const gskyhip_tile *tiles, int n_tiles,
                          const int32_t *pair_granule, int n_pairs, int max_tile_width, int max_tile_height,

@@ -1743,6 +1743,49 @@ __global__ void warp_job_resolve_kernel(const PairPlan *pairs, const BlockStatsJ
   for (int k = 0; k < 6; k++) r.src_gt[k] = pp.src_gt[k];
 }
 
+// Source footprint of every planned pair (gskyhip_render_pair_info, an
+// observability hook for the algorithmic bytes of a batch): the picked
+// level, its element size and the bounding box of the source pixels the
+// pair's LINEAR rows and linear leaves sample (first and last pixel of each
+// row or leaf: the interpolation is linear along a row), clamped to the
+// level.  One thread per pair.
+__global__ void pair_footprint_kernel(const PairPlan *pairs, const RowRec *rows, const Leaf *pool, int n_pairs,
+                                      int max_h, int32_t *out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  const PairPlan &pp = pairs[p];
+  double x0 = INFINITY, y0 = INFINITY, x1 = -INFINITY, y1 = -INFINITY;
+  auto take = [&](double xs, double ys, double dx, double dy, int n) {
+    const double xe = xs + dx * (n - 1), ye = ys + dy * (n - 1);
+    x0 = fmin(x0, fmin(xs, xe)); x1 = fmax(x1, fmax(xs, xe));
+    y0 = fmin(y0, fmin(ys, ye)); y1 = fmax(y1, fmax(ys, ye));
+  };
+  for (int r = 0; r < pp.h && pp.w > 0; r++) {
+    const RowRec &rr = rows[(int64_t)p * max_h + r];
+    if (rr.kind == ROW_LINEAR) {
+      take(rr.v[0], rr.v[1], rr.v[2], rr.v[3], pp.w);
+    } else if (rr.kind == ROW_POOL) {
+      const Leaf *lv = pool + rr.pool_off;
+      for (int k = 0; k < rr.nleaf; k++) {
+        const Leaf &L = lv[k];
+        if (L.kind != LEAF_LINEAR) continue;
+        const int end = k + 1 < rr.nleaf ? lv[k + 1].start : pp.w;
+        if (end > L.start) take(L.xs0, L.ys0, L.dX, L.dY, end - L.start);
+      }
+    }
+  }
+  int32_t *o = out + 8 * p;
+  o[0] = pp.granule; o[1] = pp.band_x; o[2] = pp.band_y; o[3] = type_size(pp.src_dtype);
+  if (x0 <= x1 && y0 <= y1) {
+    o[4] = (int32_t)fmax(0.0, fmin((double)pp.band_x, floor(x0)));
+    o[5] = (int32_t)fmax(0.0, fmin((double)pp.band_y, floor(y0)));
+    o[6] = (int32_t)fmax(0.0, fmin((double)pp.band_x, floor(x1) + 1.0));
+    o[7] = (int32_t)fmax(0.0, fmin((double)pp.band_y, floor(y1) + 1.0));
+  } else {
+    o[4] = o[5] = o[6] = o[7] = 0;
+  }
+}
+
 __global__ void pair_meta_kernel(const PairPlan *pairs, int n_pairs, int32_t *bbox, int32_t *dtype, double *nodata) {
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
@@ -2011,6 +2054,14 @@ int launch_block_stats_batch(const RenderCall &rc, const BlockStatsJob *jobs, in
                        cv.xforms, cv.rows, cv.pool, rc.max_h, jobs, (char *)scratch, stats);
   hipLaunchKernelGGL(block_stats_resolve_kernel, dim3(n_jobs), dim3(64), 0, s, cv.pairs, jobs,
                      (const char *)scratch, stats);
+  return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+}
+
+int launch_pair_footprint(void *workspace, int n_tiles, int n_pairs, int max_h, int32_t *out, hipStream_t s) {
+  if (n_pairs <= 0) return 0;
+  const Carve cv = carve(workspace, n_tiles, n_pairs, max_h);
+  hipLaunchKernelGGL(pair_footprint_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, cv.pairs, cv.rows, cv.pool,
+                     n_pairs, max_h, out);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 

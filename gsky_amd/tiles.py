@@ -297,6 +297,16 @@ class TileBatch:
         self.plan_counters = {"pool_leaves": int(cnt[0]), "split_rows": int(cnt[1]), "complex_tiles": int(cnt[2])}
         return info[: self.n_tiles]
 
+    def pair_info(self):
+        """Per pair of the last plan (gskyhip_render_pair_info): int32 numpy
+        array (n_pairs, 8) = granule, picked level width / height, element
+        bytes, source footprint x0, y0, x1, y1 at that level."""
+        out = np.zeros((max(1, self.n_pairs), 8), dtype=np.int32)
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().gskyhip_render_pair_info(C.c_void_p(self._ws.data_ptr()), self.n_tiles, self.n_pairs, self.max_h,
+                                             out.ctypes.data_as(C.c_void_p), stream), "render_pair_info")
+        return out[: self.n_pairs]
+
     def canvas_view(self, cv: torch.Tensor, tile: int, k: int, type_name: str) -> torch.Tensor:
         nb = {"Byte": 1, "SignedByte": 1, "Int16": 2, "UInt16": 2, "Float32": 4}[type_name]
         return cv[tile, k, : self.max_w * self.max_h * nb].view(TORCH_OF[type_name]).reshape(self.max_h,

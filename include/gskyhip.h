@@ -612,6 +612,14 @@ int gskyhip_render_status(void *workspace, int n_tiles, int n_pairs, int max_til
 int gskyhip_render_tile_info(void *workspace, int n_tiles, int n_pairs, int max_tile_height, int32_t *info_out,
                              int32_t *counters_out, void *stream);
 
+/* Source footprint of every pair of a planned batch: info_out (n_pairs x 8
+ * int32) = {granule, picked level width, height, element bytes, x0, y0, x1,
+ * y1}: the bounding box [x0, x1) x [y0, y1) at that level of the source
+ * pixels the pair's linear rows sample.  For the algorithmic bytes of a
+ * batch (bench.py C5).  No reference counterpart (an observability hook). */
+int gskyhip_render_pair_info(void *workspace, int n_tiles, int n_pairs, int max_tile_height, int32_t *info_out,
+                             void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -772,3 +772,33 @@ def test_drill_window_past_stack_edge(gpu, oracle):
         sub = dc.bands[:, ya:yb, xa:xb]
         ev, ec = oracle.drill_read_data(sub, np.full((yb - ya, xb - xa), 255, np.uint8), dc.nodata, -1e30, 1e30)
         assert np.array_equal(cnts[p], ec) and np.array_equal(vals[p].view(np.uint64), ev.view(np.uint64))
+
+
+def test_pair_info_footprint_covers_samples(gpu):
+    """gskyhip_render_pair_info (bench.py's C5 algorithmic bytes): each pair's
+    source footprint lies inside its picked level and holds every value its
+    warped window sampled (C2-style pairs, int16 data with few repeats)."""
+    import gsky_amd
+    cfg = synth.config_c2(scale=0.05, tiles_per_side=3, tile_px=128)
+    b = gpu_batch(cfg)
+    b.render(gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True))
+    info = b.pair_info()
+    assert info.shape == (b.n_pairs, 8)
+    wins = b.warp_windows()
+    flat = [k for ks in cfg.pairs for k in ks]
+    n_checked = 0
+    for p, (win, bbox, tname, nd) in enumerate(wins):
+        g, lx, ly, es, x0, y0, x1, y1 = info[p].tolist()
+        gr = cfg.granules[flat[p]]
+        levels = [gr.data] + list(gr.overviews)
+        lv = [a for a in levels if (a.shape[1], a.shape[0]) == (lx, ly)]
+        assert g == flat[p] and lv and es == 2
+        assert 0 <= x0 <= x1 <= lx and 0 <= y0 <= y1 <= ly
+        vals = win.cpu().numpy().ravel()
+        vals = vals[vals != nd]
+        if vals.size == 0:
+            continue
+        inside = np.isin(vals, lv[0][y0:y1, x0:x1])
+        assert inside.all(), (p, bbox, (x0, y0, x1, y1))
+        n_checked += 1
+    assert n_checked > 0
