@@ -24,7 +24,9 @@
 // nodata from _FillValue / missing_value / the type default and NC_BYTE
 // signedness as netCDFRasterBand sets them; EPSG:4326 for lon / lat axes,
 // else an EPSG from the grid mapping's crs_wkt / spatial_ref AUTHORITY.
-// netCDF-4 (HDF5) files are not read (no HDF5 in the image).
+// netCDF-4 (HDF5) files: the HDF5 subset of hdf5.h (host parse, chunks
+// inflated / unshuffled on host threads), mapped to the same variables,
+// dimensions and attributes netCDF-C reports.
 //
 // Device path: the band's blocks are decompressed and un-predicted by host
 // threads (zlib / LZW / PackBits are byte-serial), staged block-major in
@@ -34,6 +36,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <map>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -44,6 +47,7 @@
 #include <vector>
 
 #include "../../include/gskyhip.h"
+#include "hdf5.h"
 
 namespace gsky {
 namespace {
@@ -614,10 +618,12 @@ struct NcVar {
   int type = 0;
   uint64_t vsize = 0, begin = 0;
   bool record = false;
+  int h5v = -1;          // netCDF-4: the HDF5 dataset (Nc::h5.vars index)
 };
 struct Nc {
   std::vector<uint8_t> buf;
-  int version = 1;
+  int version = 1;       // 1, 2, 5: classic; 4: netCDF-4 (HDF5)
+  h5::File h5;
   uint64_t numrecs = 0, recsize = 0;
   std::vector<std::pair<std::string, uint64_t>> dims;
   int rec_dim = -1;
@@ -694,7 +700,81 @@ bool nc_atts(NcCursor &c, int ver, std::vector<NcAtt> &out) {
   return c.ok;
 }
 
+// netCDF-4: the HDF5 datasets of the root group as netCDF-C presents them
+// (nc4hdf.c / nc4file.c of netCDF-C 4.x [ext]): dimension scales are the
+// dimensions (ordered by _Netcdf4Dimid when every scale has one), a
+// variable's dimensions are its DIMENSION_LIST references, a dimension
+// without a coordinate variable is not a variable, the bookkeeping
+// attributes are hidden.
+bool nc_from_h5(Nc &f) {
+  f.h5.buf.swap(f.buf);
+  if (!h5::open(f.h5)) return false;
+  f.version = 4;
+  const auto &hv = f.h5.vars;
+  std::vector<int> scales;
+  for (int i = 0; i < (int)hv.size(); i++)
+    if (hv[i].is_scale && hv[i].shape.size() == 1) scales.push_back(i);
+  auto dimid = [&](int i) {
+    for (const h5::Att &a : hv[i].atts)
+      if (a.name == "_Netcdf4Dimid" && !a.num.empty()) return (int)a.num[0];
+    return -1;
+  };
+  bool all_ids = !scales.empty();
+  for (int i : scales) all_ids = all_ids && dimid(i) >= 0;
+  if (all_ids) std::stable_sort(scales.begin(), scales.end(), [&](int a, int b) { return dimid(a) < dimid(b); });
+  std::map<uint64_t, int> by_ohdr;
+  for (int i : scales) {
+    by_ohdr[hv[i].ohdr] = (int)f.dims.size();
+    f.dims.emplace_back(hv[i].name, hv[i].shape[0]);
+  }
+  auto hidden = [](const std::string &n) {
+    return n == "DIMENSION_LIST" || n == "REFERENCE_LIST" || n == "CLASS" || n == "NAME" || n == "_Netcdf4Dimid" ||
+           n == "_Netcdf4Coordinates" || n == "_nc3_strict" || n == "_NCProperties" || n == "_IsNetcdf4";
+  };
+  auto conv = [&](const std::vector<h5::Att> &in, std::vector<NcAtt> &out) {
+    for (const h5::Att &a : in) {
+      if (hidden(a.name) || a.nctype == 0) continue;
+      NcAtt n;
+      n.name = a.name;
+      n.type = a.nctype;
+      n.num = a.num;
+      n.text = a.text;
+      out.push_back(std::move(n));
+    }
+  };
+  conv(f.h5.gatts, f.gatts);
+  for (int i = 0; i < (int)hv.size(); i++) {
+    const h5::Var &h = hv[i];
+    if (h.pure_dim || h.nctype == 0) continue;
+    NcVar v;
+    v.name = h.name;
+    v.type = h.nctype;
+    v.h5v = i;
+    if (!h.dim_refs.empty()) {
+      if (h.dim_refs.size() != h.shape.size()) return false;
+      for (uint64_t ref : h.dim_refs) {
+        auto it = by_ohdr.find(ref);
+        if (it == by_ohdr.end()) return false;
+        v.dims.push_back(it->second);
+      }
+    } else if (h.is_scale) {
+      v.dims.push_back(by_ohdr[h.ohdr]);
+    } else {   // anonymous dimensions (a plain HDF5 dataset): phony_dim_k as netCDF-C names them
+      for (uint64_t n : h.shape) {
+        v.dims.push_back((int)f.dims.size());
+        f.dims.emplace_back("phony_dim_" + std::to_string(f.dims.size()), n);
+      }
+    }
+    for (size_t k = 0; k < v.dims.size(); k++)
+      if (f.dims[v.dims[k]].second != h.shape[k]) return false;
+    conv(h.atts, v.atts);
+    f.vars.push_back(std::move(v));
+  }
+  return true;
+}
+
 bool nc_parse(Nc &f) {
+  if (h5::is_hdf5(f.buf)) return nc_from_h5(f);
   const std::vector<uint8_t> &b = f.buf;
   if (b.size() < 8 || b[0] != 'C' || b[1] != 'D' || b[2] != 'F') return false;
   f.version = b[3];
@@ -753,6 +833,24 @@ const NcAtt *nc_att(const std::vector<NcAtt> &atts, const char *name) {
   return nullptr;
 }
 
+// Element i of a non-record variable as a double (coordinate values).
+bool nc_elem(const Nc &f, const NcVar &v, uint64_t i, double &out) {
+  const int ts = nc_type_size(v.type);
+  if (!ts) return false;
+  if (v.h5v >= 0) {
+    const h5::Var &h = f.h5.vars[v.h5v];
+    uint8_t e[8];
+    if (!h5::read(f.h5, h, i, 1, e)) return false;
+    uint8_t be[8];
+    for (int k = 0; k < ts; k++) be[k] = h.big_endian ? e[k] : e[ts - 1 - k];   // nc_value reads big-endian
+    out = nc_value(be, v.type);
+    return true;
+  }
+  if (v.record || v.begin + (i + 1) * ts > f.buf.size()) return false;
+  out = nc_value(&f.buf[v.begin + i * ts], v.type);
+  return true;
+}
+
 // "NETCDF:file:var" / "NETCDF:\"file\":var" / "file" -> file, var
 void nc_split(const char *path, std::string &file, std::string &var) {
   std::string p(path);
@@ -803,9 +901,8 @@ int nc_open_raster(const char *path, NcRaster &r) {
   const std::string &ydim = r.f.dims[pick->dims[nd - 2]].first;
   for (const NcVar &cv : r.f.vars)
     if (cv.name == ydim && cv.dims.size() == 1 && r.ny >= 2 && !cv.record) {
-      const int ts = nc_type_size(cv.type);
-      if (cv.begin + 2 * ts <= r.f.buf.size())
-        r.bottom_up = nc_value(&r.f.buf[cv.begin], cv.type) <= nc_value(&r.f.buf[cv.begin + ts], cv.type);
+      double y0, y1;
+      if (nc_elem(r.f, cv, 0, y0) && nc_elem(r.f, cv, 1, y1)) r.bottom_up = y0 <= y1;
     }
   return 0;
 }
@@ -1039,11 +1136,10 @@ int nc_fill_info(const NcRaster &r, gskyhip_raster_info *info) {
   auto coord = [&](const std::string &dn, int64_t n, double mm[2]) {
     for (const NcVar &cv : f.vars)
       if (cv.name == dn && cv.dims.size() == 1 && !cv.record) {
-        const int ts = nc_type_size(cv.type);
-        if (cv.begin + (uint64_t)n * ts > f.buf.size() || n < 2) return false;
+        if (n < 2) return false;
         const NcAtt *ar = nc_att(cv.atts, "actual_range");
         if (ar && ar->num.size() >= 2) { mm[0] = ar->num[0]; mm[1] = ar->num[1]; }
-        else { mm[0] = nc_value(&f.buf[cv.begin], cv.type); mm[1] = nc_value(&f.buf[cv.begin + (n - 1) * ts], cv.type); }
+        else if (!nc_elem(f, cv, 0, mm[0]) || !nc_elem(f, cv, (uint64_t)n - 1, mm[1])) return false;
         const NcAtt *ao = nc_att(cv.atts, "add_offset"), *sf = nc_att(cv.atts, "scale_factor");
         if (ao && sf && !ao->num.empty() && !sf->num.empty()) {
           mm[0] = ao->num[0] + mm[0] * sf->num[0];
@@ -1084,6 +1180,23 @@ uint64_t nc_row_offset(const NcRaster &r, int64_t b, int64_t y) {
 bool nc_read_rows(const NcRaster &r, int64_t b, uint8_t *out, bool swap) {
   const int ts = nc_type_size(r.v->type);
   const uint64_t row = (uint64_t)r.nx * ts;
+  if (r.v->h5v >= 0) {   // netCDF-4: the band's plane from its chunks (file byte order)
+    const h5::Var &h = r.f.h5.vars[r.v->h5v];
+    const uint64_t plane = (uint64_t)r.nx * r.ny;
+    if (!h5::read(r.f.h5, h, (uint64_t)b * plane, plane, out)) return false;
+    if (r.bottom_up) {
+      std::vector<uint8_t> tmp(row);
+      for (int64_t y = 0; y < r.ny / 2; y++) {
+        uint8_t *a = out + (uint64_t)y * row, *c = out + (uint64_t)(r.ny - 1 - y) * row;
+        std::memcpy(tmp.data(), a, row);
+        std::memcpy(a, c, row);
+        std::memcpy(c, tmp.data(), row);
+      }
+    }
+    if (swap && h.big_endian && ts > 1)
+      for (uint64_t i = 0; i < plane * ts; i += ts) std::reverse(out + i, out + i + ts);
+    return true;
+  }
   for (int64_t y = 0; y < r.ny; y++) {
     const uint64_t o = nc_row_offset(r, b, r.bottom_up ? r.ny - 1 - y : y);
     if (o + row > r.f.buf.size()) return false;
@@ -1190,7 +1303,8 @@ static int netcdf_read_impl(const char *path, int band, void *dev_out, int64_t o
   if (!nc_read_rows(r, band - 1, (uint8_t *)host, false)) { hipHostFree(host); return GSKYHIP_E_ARG; }
   hipStream_t s = (hipStream_t)stream;
   rc = hipMemcpyAsync(dev_out, host, (size_t)(n * ts), hipMemcpyHostToDevice, s) == hipSuccess ? 0 : GSKYHIP_E_HIP;
-  if (!rc && ts > 1) {   // big-endian file order -> device order on the GPU
+  const bool file_be = r.v->h5v < 0 || r.f.h5.vars[r.v->h5v].big_endian;   // classic: always big-endian
+  if (!rc && ts > 1 && file_be) {   // big-endian file order -> device order on the GPU
     const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
     if (ts == 2) hipLaunchKernelGGL(byteswap_kernel<uint16_t>, grid, blk, 0, s, (uint16_t *)dev_out, n);
     else if (ts == 4) hipLaunchKernelGGL(byteswap_kernel<uint32_t>, grid, blk, 0, s, (uint32_t *)dev_out, n);

@@ -1,0 +1,213 @@
+"""netCDF-4 (HDF5) granules (GSKY_netCDF opens them
+through netCDF-C, libs/gdal/frmts/gsky_netcdf/netcdfdataset.cpp:8711-8870,
+and warp.go:89-101 sends every NETCDF: / *.nc path there).
+
+No HDF5 library is importable here, so the reader (gsky_amd/csrc/hdf5.cpp)
+is checked against tests/h5write.py, written from the HDF5 file format
+specification -- parity unpinned.  The anchor: the same logical dataset
+written once as netCDF classic by scipy.io.netcdf_file (an independent
+writer the classic reader is tested against, test_ingest.py) and once as
+netCDF-4 here must give the same raster info, SRS and band values; the
+netCDF-4 variants cover both superblock generations, compact and dense
+attributes / links, every chunk-index and filter combination the writer
+has, big-endian data and unwritten chunks.
+"""
+import numpy as np
+import pytest
+
+from gsky_amd import GskyError, ingest
+
+from .h5write import Var, write_nc4
+from .test_ingest import _write_nc
+
+
+def _pair(tmp_path, data, lon, lat, name="v", fill=None, atts=None, time=None, **kw):
+    """The dataset as classic netCDF (scipy) and as netCDF-4 (h5write)."""
+    c = str(tmp_path / "classic.nc")
+    _write_nc(c, name, data, lon, lat, fill=fill, attrs=atts, time=time)
+    dims = ([("time", len(time))] if time is not None else []) + [("lat", len(lat)), ("lon", len(lon))]
+    vatts = dict(atts or {})
+    if fill is not None:
+        vatts["_FillValue"] = data.dtype.type(fill)
+    variables = [Var("lat", ("lat",), np.asarray(lat, np.float64), filters=()),
+                 Var("lon", ("lon",), np.asarray(lon, np.float64), filters=())]
+    if time is not None:
+        variables.append(Var("time", ("time",), np.asarray(time, np.float64), filters=()))
+    variables.append(Var(name, tuple(d for d, _ in dims), data, atts=vatts,
+                         chunks=kw.pop("chunks", tuple(min(8, s) for s in data.shape)),
+                         filters=kw.pop("filters", ("shuffle", "deflate")), compact=kw.pop("compact", False),
+                         skip_chunks=kw.pop("skip_chunks", ())))
+    n4 = str(tmp_path / "nc4.nc")
+    write_nc4(n4, dims, variables, {"Conventions": "CF-1.6", "history": ("__vstr__", "written by h5write")}, **kw)
+    return c, n4
+
+
+def _same_info(a, b):
+    for k in ("xsize", "ysize", "n_bands", "dtype", "signed_byte", "epsg", "nodata"):
+        assert getattr(a, k) == getattr(b, k), k
+    assert np.allclose(a.geot, b.geot, rtol=0, atol=1e-12)
+
+
+VARIANTS = [dict(superblock=0), dict(superblock=2), dict(superblock=2, dense_atts=True, dense_links=True),
+            dict(superblock=3, crt_order=False)]
+
+
+@pytest.mark.parametrize("kw", VARIANTS, ids=["sb0", "sb2", "sb2-dense", "sb3"])
+@pytest.mark.parametrize("dt", [np.int16, np.float32, np.int32, np.float64])
+def test_netcdf4_matches_classic(tmp_path, kw, dt):
+    rng = np.random.default_rng(int(np.dtype(dt).itemsize) * 7 + kw["superblock"])
+    nt, ny, nx = 3, 37, 52
+    data = (rng.standard_normal((nt, ny, nx)) * 60).astype(dt)
+    lon = 112.0 + 0.25 * np.arange(nx)
+    lat = -44.0 + 0.2 * np.arange(ny)          # increasing: bBottomUp, rows come back north first
+    c, n4 = _pair(tmp_path, data, lon, lat, fill=7, time=np.arange(nt), chunks=(1, 10, 16), **kw)
+    _same_info(ingest.info(c), ingest.info(n4))
+    for b in range(1, nt + 1):
+        exp = ingest.read_host(c, b)
+        got = ingest.read_host(n4, b)
+        assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), b
+        assert np.array_equal(got.view(dt), data[b - 1][::-1])
+    assert np.array_equal(ingest.read_host("NETCDF:%s:v" % n4, 2).view(np.uint8),
+                          ingest.read_host(n4, 2).view(np.uint8))
+    assert ingest.netcdf_srs(n4, 0) == ingest.netcdf_srs(c, 0) == "EPSG:4326"
+
+
+@pytest.mark.parametrize("filters", [(), ("deflate",), ("shuffle", "deflate"), ("fletcher32", "shuffle", "deflate")],
+                         ids=["none", "deflate", "shuffle-deflate", "fletcher-shuffle-deflate"])
+@pytest.mark.parametrize("chunks", [(1, 7, 9), (2, 64, 64), (1, 3, 5)], ids=["edge", "one-chunk", "many"])
+def test_netcdf4_chunks_and_filters(tmp_path, filters, chunks):
+    """Chunk shapes that leave partial edge chunks, one chunk, and more than
+    64 chunks (a two-level v1 B-tree), under every filter chain."""
+    rng = np.random.default_rng(len(filters) * 10 + chunks[1])
+    data = rng.integers(-30000, 30000, (2, 41, 53)).astype(np.int16)
+    lon = np.arange(53) * 0.1
+    lat = -np.arange(41) * 0.1                # decreasing: file row order
+    _, n4 = _pair(tmp_path, data, lon, lat, time=np.arange(2), chunks=chunks, filters=filters)
+    for b in (1, 2):
+        assert np.array_equal(ingest.read_host(n4, b).view(np.int16), data[b - 1])
+
+
+@pytest.mark.parametrize("layout", ["contiguous", "compact"])
+def test_netcdf4_contiguous_and_compact(tmp_path, layout):
+    data = np.arange(2 * 6 * 8, dtype=np.float32).reshape(2, 6, 8) * 0.5
+    c, n4 = _pair(tmp_path, data, np.arange(8) * 1.0, -np.arange(6) * 1.0, time=np.arange(2),
+                  chunks=None, filters=(), compact=layout == "compact")
+    _same_info(ingest.info(c), ingest.info(n4))
+    assert np.array_equal(ingest.read_host(n4, 2).view(np.float32), data[1])
+
+
+def test_netcdf4_big_endian_and_unwritten_chunks(tmp_path):
+    """Big-endian data comes back in host order; a chunk never written reads
+    as the variable's _FillValue (netCDF-C's fill)."""
+    data = np.arange(20 * 30, dtype=">i4").reshape(1, 20, 30)
+    _, n4 = _pair(tmp_path, data, np.arange(30) * 1.0, -np.arange(20) * 1.0, fill=-5, time=np.arange(1),
+                  chunks=(1, 10, 10), skip_chunks=(4,))
+    got = ingest.read_host(n4, 1).view(np.int32)
+    exp = data[0].astype(np.int32).copy()
+    exp[10:20, 10:20] = -5                      # chunk 4 of the 2 x 3 chunk grid
+    assert np.array_equal(got, exp)
+    assert ingest.info(n4).nodata == -5.0
+
+
+def test_netcdf4_many_attributes_dense_btree(tmp_path):
+    """Enough attributes that the dense name index needs an internal v2
+    B-tree node; a CF grid mapping read from them."""
+    data = np.ones((1, 8, 9), np.int16)
+    atts = {"att_%02d" % k: np.float64(k) for k in range(60)}
+    atts["grid_mapping"] = "crs"
+    c = str(tmp_path / "m.nc")
+    dims = [("time", 1), ("y", 8), ("x", 9)]
+    crs = Var("crs", (), np.array(0, np.int32), filters=(),
+              atts={"grid_mapping_name": "albers_conical_equal_area", "standard_parallel": np.array([-18.0, -36.0]),
+                    "longitude_of_central_meridian": 132.0, "latitude_of_projection_origin": 0.0,
+                    "false_easting": 0.0, "false_northing": 0.0, "semi_major_axis": 6378137.0,
+                    "inverse_flattening": 298.257222101})
+    variables = [Var("y", ("y",), -np.arange(8) * 25.0 - 12.5, filters=()),
+                 Var("x", ("x",), np.arange(9) * 25.0 + 12.5, filters=()), crs,
+                 Var("v", ("time", "y", "x"), data, atts=atts, chunks=(1, 8, 9))]
+    gatts = {"g_%02d" % k: "value %d" % k for k in range(40)}
+    write_nc4(c, dims, variables, gatts, superblock=2, dense_atts=True, dense_links=True)
+    inf = ingest.info(c)
+    assert (inf.xsize, inf.ysize, inf.n_bands) == (9, 8, 1)
+    srs = ingest.netcdf_srs(c, 1)
+    assert srs.startswith("+proj=aea") and "+lat_1=-18" in srs and "+lon_0=132" in srs
+    assert np.array_equal(ingest.read_host(c, 1).view(np.int16), data[0])
+
+
+@pytest.mark.parametrize("dt,gdal_dt", [(np.uint16, 2), (np.uint8, 1)])
+def test_netcdf4_unsigned_types(tmp_path, dt, gdal_dt):
+    """NC_USHORT / NC_UBYTE (netCDF-4 only: classic files have no unsigned
+    types) -> UInt16 / Byte, default nodata NC_FILL_USHORT / 0 with no
+    _FillValue (netcdfdataset.cpp:420-430)."""
+    data = (np.arange(2 * 9 * 11) % 251).astype(dt).reshape(2, 9, 11)
+    p = str(tmp_path / "u.nc")
+    write_nc4(p, [("time", 2), ("lat", 9), ("lon", 11)],
+              [Var("lat", ("lat",), -np.arange(9) * 1.0, filters=()), Var("lon", ("lon",), np.arange(11) * 1.0,
+                                                                         filters=()),
+               Var("v", ("time", "lat", "lon"), data, chunks=(1, 4, 4))], {}, superblock=2)
+    inf = ingest.info(p)
+    assert inf.dtype == gdal_dt and not inf.signed_byte
+    assert inf.nodata == (65535.0 if dt == np.uint16 else 0.0)
+    assert np.array_equal(ingest.read_host(p, 2).view(dt), data[1])
+
+
+def test_netcdf4_byte_signedness(tmp_path):
+    """NC_BYTE is signed and NC_UBYTE unsigned in netCDF-4 (HDF5 carries the
+    sign); _Unsigned on a signed byte flips it as for classic files."""
+    d = np.arange(-4, 4, dtype=np.int8).reshape(1, 2, 4)
+    _, n4 = _pair(tmp_path, d, np.arange(4) * 1.0, -np.arange(2) * 1.0, time=np.arange(1))
+    assert ingest.info(n4).signed_byte
+    _, n4u = _pair(tmp_path, d, np.arange(4) * 1.0, -np.arange(2) * 1.0, time=np.arange(1),
+                   atts={"_Unsigned": "true"})
+    assert not ingest.info(n4u).signed_byte
+
+
+def test_truncated_netcdf4_is_an_error(tmp_path):
+    data = np.arange(2 * 30 * 40, dtype=np.int16).reshape(2, 30, 40)
+    _, n4 = _pair(tmp_path, data, np.arange(40) * 1.0, -np.arange(30) * 1.0, time=np.arange(2), superblock=2)
+    raw = open(n4, "rb").read()
+    for cut in (9, 48, 200, 1000, len(raw) // 2, len(raw) - 1000):
+        q = str(tmp_path / ("cut%d.nc" % cut))
+        open(q, "wb").write(raw[:cut])
+        with pytest.raises(GskyError):
+            ingest.read_host(q)
+    # a flipped byte anywhere in the metadata: an error or a value, never a crash
+    rng = np.random.default_rng(1)
+    for k in range(300):
+        b = bytearray(raw)
+        for i in rng.integers(0, len(raw), 1 + k % 3):
+            b[int(i)] ^= int(rng.integers(1, 256))
+        q = str(tmp_path / ("flip%d.nc" % k))
+        open(q, "wb").write(bytes(b))
+        try:
+            ingest.read_host(q)
+        except GskyError:
+            pass
+
+
+@pytest.mark.gpu
+def test_gpu_netcdf4_read_and_drop_in(tmp_path):
+    """A netCDF-4 band decoded into HBM and opened by warp_operation_fast
+    itself: bit-identical to the classic file of the same data."""
+    import torch
+
+    from gsky_amd import worker
+    from gsky_amd.tiles import bbox_to_geot
+    rng = np.random.default_rng(4)
+    nt, ny, nx = 3, 400, 600
+    data = rng.integers(0, 10000, (nt, ny, nx)).astype(np.int16)
+    lon = 130.0 + 0.01 * (np.arange(nx) + 0.5)
+    lat = -20.0 - 0.01 * (np.arange(ny) + 0.5)
+    c, n4 = _pair(tmp_path, data, lon, lat, fill=-1, time=np.arange(nt), chunks=(1, 128, 128), superblock=2)
+    for b in range(nt):
+        assert np.array_equal(ingest.read("NETCDF:%s:v" % n4, b + 1).cpu().numpy(), data[b])
+    worker.unregister_all()
+    bbox = (14471533.8, -2504688.5, 14526000.0, -2450000.0)
+    req = dict(bands=[2], width=256, height=256, dstSRS="EPSG:3857", dstGeot=bbox_to_geot(256, 256, bbox))
+    a = worker.warp_raster(worker.GeoRPCGranule(path="NETCDF:%s:v" % c, **req))
+    b = worker.warp_raster(worker.GeoRPCGranule(path="NETCDF:%s:v" % n4, **req))
+    assert a.error == "OK" and b.error == "OK", (a.error, b.error)
+    assert np.array_equal(worker.raster_array(a.raster), worker.raster_array(b.raster))
+    assert a.raster.bbox == b.raster.bbox and a.raster.noData == b.raster.noData
+    worker.unregister_all()
+    torch.cuda.synchronize()
