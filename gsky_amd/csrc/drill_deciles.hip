@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
 // workgroups of one polygon run back to back on one XCD (blockIdx % 8 is the
 // XCD the dispatcher picks), so the 32 bands sharing a pixel's 128-byte line
 // are read from that XCD's L2 after the first.
-template <int kU, bool DIRECT = false, int NT = kSelThreads, int WPE = 1>
+template <int kU, bool DIRECT = false, int NT = kSelThreads, int WPE = 1, bool VEC = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void decile_select_kernel(const float *__restrict__ vals,
                                                                     const int64_t *__restrict__ mask_off,
                                                                     const int32_t *__restrict__ chunk_base,
@@ -390,6 +390,44 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
     }
   };
+  // VEC (band-major segments, 256-byte aligned rows): every valid key four at
+  // a time -- one 16-byte load per thread and slot (a quarter of the load
+  // instructions), g(k[4], valid bits)
+  auto for_keys4 = [&](auto &&g) {
+    if (fits && filled) {
+      for (int i = tid * 4; i < n; i += NT * 4) {
+        const uint4 c4 = *(const uint4 *)(cache + i);
+        const uint32_t k[4] = {c4.x, c4.y, c4.z, c4.w};
+        uint32_t m = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) m |= (i + c < n && !skipk(k[c])) ? (1u << c) : 0u;
+        g(k, m);
+      }
+    } else {
+      constexpr int kU4 = kU / 4 > 0 ? kU / 4 : 1;
+      for (int i0 = 0; i0 < n; i0 += NT * 4 * kU4) {
+        float4 v[kU4];
+#pragma unroll
+        for (int u = 0; u < kU4; u++) {
+          const int i = i0 + (u * NT + tid) * 4;
+          v[u] = i < n ? *(const float4 *)(buf + i) : make_float4(nodata, nodata, nodata, nodata);
+        }
+#pragma unroll
+        for (int u = 0; u < kU4; u++) {
+          const int i = i0 + (u * NT + tid) * 4;
+          const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+          uint32_t k[4], m = 0;
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            k[c] = fkey(x[c]);
+            if (!filled && fits && i + c < n) cache[i + c] = k[c];
+            m |= (i + c < n && x[c] != nodata) ? (1u << c) : 0u;
+          }
+          if (i < n) g(k, m);
+        }
+      }
+    }
+  };
   const int wv = tid >> 6, ln = tid & 63;
   // Range refinement: rank r is the s_rem[r]-th key in [s_lo[r], s_hi[r]].
   // A pass takes the ranks sharing the first open range [L, Hk], counts the
@@ -423,9 +461,28 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     const int sh = max(0, 32 - __clz(span) - kBinsLog);  // bucket = (k - L) >> sh < 2048
     for (int i = tid; i < kBins; i += NT) { H[i] = 0u; s_map[i] = -1; }
     __syncthreads();
-    for_keys([&](uint32_t k) {
-      if (k >= L && k <= Hk) atomicAdd(&H[(k - L) >> sh], 1u);
-    });
+    if constexpr (VEC && !DIRECT) {
+      // one atomic per run of equal buckets among a thread's four neighbouring
+      // pixels (spatially correlated values share buckets: fewer same-address
+      // atomics)
+      for_keys4([&](const uint32_t *k, uint32_t m) {
+        int cur = -1;
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const int b = (((m >> c) & 1u) && k[c] >= L && k[c] <= Hk) ? (int)((k[c] - L) >> sh) : -1;
+          if (b == cur) { cnt++; continue; }
+          if (cur >= 0) atomicAdd(&H[cur], cnt);
+          cur = b;
+          cnt = 1;
+        }
+        if (cur >= 0) atomicAdd(&H[cur], cnt);
+      });
+    } else {
+      for_keys([&](uint32_t k) {
+        if (k >= L && k <= Hk) atomicAdd(&H[(k - L) >> sh], 1u);
+      });
+    }
     __syncthreads();
     filled = true;
     {   // inclusive scan of the buckets in place, 4 per thread
@@ -502,12 +559,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       if (tid < nsl) { s_map[s_spref[tid]] = (int8_t)tid; s_fill[tid] = 0u; }
       __syncthreads();
       uint32_t *cand = dyn;   // the bucket counts are no longer needed
-      for_keys([&](uint32_t k) {
+      auto take = [&](uint32_t k) {
         if (k >= L && k <= Hk) {
           const int sl = s_map[(k - L) >> sh];
           if (sl >= 0) cand[s_soff[sl] + atomicAdd(&s_fill[sl], 1u)] = k;
         }
-      });
+      };
+      if constexpr (VEC && !DIRECT) {
+        for_keys4([&](const uint32_t *k, uint32_t m) {
+#pragma unroll
+          for (int c = 0; c < 4; c++)
+            if ((m >> c) & 1u) take(k[c]);
+        });
+      } else {
+        for_keys(take);
+      }
       __syncthreads();
       // rank r is the s_rem[r]-th key of its bucket (<= 64 keys, one per
       // lane): MSB-first selection with wave ballots over the bits where the
@@ -695,8 +761,10 @@ int launch_decile_select_fused(const float *vals, const int32_t *chunk_base, con
   if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(8, std::min(64, atoi(e))) * 1024;
 #endif
   int nt = kSelThreads;
+  bool vec = false;
 #ifdef GSKYHIP_AB
   if (const char *e = getenv("GSKYHIP_DEC_FNT")) nt = atoi(e);   // fused select workgroup: 256 / 512 / 1024 threads
+  if (const char *e = getenv("GSKYHIP_DEC_VEC")) vec = atoi(e) != 0;   // 16-byte segment loads, merged bucket runs
 #endif
   const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
   if (nt == 1024)
@@ -706,6 +774,14 @@ int launch_decile_select_fused(const float *vals, const int32_t *chunk_base, con
   else if (nt == 512)
     hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 512, 8>), dim3((unsigned)n_seg),
                        dim3(512), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
+                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
+  else if (vec && getenv("GSKYHIP_DEC_U") && atoi(getenv("GSKYHIP_DEC_U")) == 16)
+    hipLaunchKernelGGL((decile_select_kernel<16, false, kSelThreads, kSelWpe, true>), dim3((unsigned)n_seg),
+                       dim3(kSelThreads), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
+                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
+  else if (vec)
+    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe, true>), dim3((unsigned)n_seg),
+                       dim3(kSelThreads), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
                        decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
   else
     hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe>), dim3((unsigned)n_seg),
