@@ -1609,16 +1609,61 @@ __global__ void block_stats_resolve_kernel(const PairPlan *pairs, const BlockSta
   stats[2] = (int32_t)(uint32_t)(unsigned long long)b;
 }
 
+// One window pixel of a job: its value (warped_value's rules, warp.go:271-344)
+// and the bytesRead inputs (block_stats_kernel's, warp.go:281-347).
+template <int RES>
+__device__ __forceinline__ Val warp_job_pixel(const PairPlan &pp, const RowRec &rr, const Leaf *pool, const Xform *xf,
+                                              int i, int row, int &xs, bool &valid, int &ix, int &iy) {
+  double sx, sy;
+  const bool ok = src_coords<true>(rr, pool, xf, pp.xoff, pp.yoff, pp.w, i, row, sx, sy);
+  // bytesRead: the cache heuristic's x test and the full gather test
+  xs = -1;
+  valid = false;
+  ix = 0;
+  iy = 0;
+  if (ok && !(sx < 0)) {
+    const double ax = sx + 1.0e-10;
+    if (ax < 2147483647.0) {
+      ix = (int)ax;
+      if (ix < pp.band_x) xs = ix;
+    }
+  }
+  if (xs >= 0 && !(sy < 0)) {
+    const double ay = sy + 1.0e-10;
+    if (ay < 2147483647.0) {
+      iy = (int)ay;
+      valid = iy < pp.band_y;
+    }
+  }
+  // the window value, exactly as warped_value<true, RES>
+  Val v = pp.fill;
+  if (ok) {
+    if (RES == GSKYHIP_RESAMPLE_BILINEAR) {
+      v = bilinear_value(pp, sx, sy);
+    } else if (!(sx < 0 || sy < 0)) {
+      const double ax = sx + 1.0e-10, ay = sy + 1.0e-10;
+      if (!(ax >= 2147483647.0 || ay >= 2147483647.0)) {
+        const int jx = (int)ax, jy = (int)ay;
+        if (jx < pp.band_x && jy < pp.band_y) {
+          v = load_val(pp.band, pp.src_dtype, (long)jy * pp.band_x + jx);
+          if (pp.out_dtype == GSKYHIP_SIGNEDBYTE) v.i = (int32_t)(int8_t)(uint8_t)v.i;
+        }
+      }
+    }
+  }
+  return v;
+}
+
 // The per-node service's warp batch (warp_batch_launch, host.cpp): for every
 // request (job = pair) its window values AND its bytesRead inputs from ONE
 // source-coordinate evaluation per pixel -- round 4 ran warp_window_kernel
 // and block_stats_kernel, each deriving the same coordinates again.  The
 // window goes straight to the job's destination `outs[job]`: a device staging
 // slot, or the requesting worker's shared reply arena (host memory registered
-// with HIP, written over PCIe: no read-back copy).  Values follow
-// warped_value (warp.go:271-344), the statistics block_stats_kernel's rules
-// (warp.go:281-347).
-template <int RES>
+// with HIP, written over PCIe: no read-back copy).  PX pixels per thread
+// (consecutive in the packed window): with PX = 4 a thread's values leave in
+// one store of 4 * element bytes (wider writes over PCIe).
+template <int RES, int PX = 1>
 __global__ __launch_bounds__(256) void warp_job_kernel(const PairPlan *pairs, const Xform *xforms,
                                                        const RowRec *rows, const Leaf *pool, int max_h,
                                                        const BlockStatsJob *jobs, char *scratch, int32_t *stats,
@@ -1630,72 +1675,94 @@ __global__ __launch_bounds__(256) void warp_job_kernel(const PairPlan *pairs, co
   uint32_t *bits = (uint32_t *)(scratch + J.bits_off);
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long n = (long)pp.w * pp.h;
-  bool valid = false;
-  int ix = 0, iy = 0;
-  if (gid < n) {
-    const int row = (int)(gid / pp.w), i = (int)(gid % pp.w);
-    double sx, sy;
-    const bool ok = src_coords<true>(rows[(int64_t)job * max_h + row], pool, xforms + job, pp.xoff, pp.yoff, pp.w,
-                                     i, row, sx, sy);
-    // bytesRead: the cache heuristic's x test and the full gather test
-    int xs = -1;
-    if (ok && !(sx < 0)) {
-      const double ax = sx + 1.0e-10;
-      if (ax < 2147483647.0) {
-        ix = (int)ax;
-        if (ix < pp.band_x) xs = ix;
-      }
-    }
-    if (xs >= 0 && !(sy < 0)) {
-      const double ay = sy + 1.0e-10;
-      if (ay < 2147483647.0) {
-        iy = (int)ay;
-        valid = iy < pp.band_y;
-      }
-    }
-    xsrc[gid] = xs;
-    // the window value, exactly as warped_value<true, RES>
-    Val v = pp.fill;
-    if (ok) {
-      if (RES == GSKYHIP_RESAMPLE_BILINEAR) {
-        v = bilinear_value(pp, sx, sy);
-      } else if (!(sx < 0 || sy < 0)) {
-        const double ax = sx + 1.0e-10, ay = sy + 1.0e-10;
-        if (!(ax >= 2147483647.0 || ay >= 2147483647.0)) {
-          const int jx = (int)ax, jy = (int)ay;
-          if (jx < pp.band_x && jy < pp.band_y) {
-            v = load_val(pp.band, pp.src_dtype, (long)jy * pp.band_x + jx);
-            if (pp.out_dtype == GSKYHIP_SIGNEDBYTE) v.i = (int32_t)(int8_t)(uint8_t)v.i;
-          }
-        }
-      }
-    }
-    uint8_t *o = outs[job];
-    const int dsz = type_size(pp.out_dtype);
-    if (dsz == 1) o[gid] = (uint8_t)v.i;
-    else if (dsz == 2) ((uint16_t *)o)[gid] = (uint16_t)v.i;
-    else ((uint32_t *)o)[gid] = v.u;
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const unsigned long long bal = __ballot(valid);
-  __shared__ int s_first[4], s_count[4];
-  if (lane == 0) {
-    s_first[wave] = bal ? (int)(gid + __ffsll((long long)bal) - 1) : 0x7FFFFFFF;
-    s_count[wave] = __popcll(bal);
-  }
+  const long p0 = gid * PX;
   int bx = J.bx;
   if (bx <= 0) bx = pp.band_x;
   const int nxb = (pp.band_x + bx - 1) / bx;
-  const long long blk = valid ? (long long)(ix / bx) + (long long)(iy / J.by) * nxb : -1;
-  const long long prev = __shfl_up(blk, 1, 64);
-  if (valid && (lane == 0 || prev != blk)) atomicOr(&bits[blk >> 5], 1u << (blk & 31));
+  const int dsz = type_size(pp.out_dtype);
+  uint8_t *o = outs[job];
+  int first = 0x7FFFFFFF, count = 0;
+  long long blk[PX];
+  Val v[PX];
+#pragma unroll
+  for (int q = 0; q < PX; q++) {
+    blk[q] = -1;
+    v[q].u = 0;
+    const long p = p0 + q;
+    if (p >= n) continue;
+    const int row = (int)(p / pp.w), i = (int)(p % pp.w);
+    int xs, ix, iy;
+    bool valid;
+    v[q] = warp_job_pixel<RES>(pp, rows[(int64_t)job * max_h + row], pool, xforms + job, i, row, xs, valid, ix, iy);
+    xsrc[p] = xs;
+    if (valid) {
+      first = min(first, (int)p);
+      count++;
+      blk[q] = (long long)(ix / bx) + (long long)(iy / J.by) * nxb;
+    }
+  }
+  const int wbytes = PX * dsz;   // the thread's window bytes
+  if (PX > 1 && p0 + PX <= n && ((uintptr_t)(o + p0 * dsz) & ((wbytes < 16 ? wbytes : 16) - 1)) == 0) {
+    // packed into 32-bit words, stored 4, 8 or 16 bytes at a time
+    uint32_t w[PX];
+#pragma unroll
+    for (int k = 0; k < PX; k++) {
+      if (dsz == 1)
+        w[k] = k < PX / 4 ? (v[4 * k].u & 0xFFu) | (v[4 * k + 1].u & 0xFFu) << 8 | (v[4 * k + 2].u & 0xFFu) << 16 |
+                                v[4 * k + 3].u << 24
+                          : 0u;
+      else if (dsz == 2)
+        w[k] = k < PX / 2 ? (v[2 * k].u & 0xFFFFu) | v[2 * k + 1].u << 16 : 0u;
+      else
+        w[k] = v[k].u;
+    }
+    uint8_t *d = o + p0 * dsz;
+    if (wbytes == 4) {
+      *(uint32_t *)d = w[0];
+    } else if (wbytes == 8) {
+      *(uint2 *)d = make_uint2(w[0], w[1]);
+    } else {
+#pragma unroll
+      for (int k = 0; k + 3 < PX; k += 4)
+        if (4 * k < wbytes) *(uint4 *)(d + 4 * k) = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < PX; q++) {
+      const long p = p0 + q;
+      if (p >= n) continue;
+      if (dsz == 1) o[p] = (uint8_t)v[q].i;
+      else if (dsz == 2) ((uint16_t *)o)[p] = (uint16_t)v[q].i;
+      else ((uint32_t *)o)[p] = v[q].u;
+    }
+  }
+  // touched blocks: a pixel ORs its block's bit where it differs from the
+  // pixel before it (the previous lane's last pixel for the first)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  long long prev = __shfl_up(blk[PX - 1], 1, 64);
+  if (lane == 0) prev = -2;
+#pragma unroll
+  for (int q = 0; q < PX; q++) {
+    if (blk[q] >= 0 && blk[q] != prev) atomicOr(&bits[blk[q] >> 5], 1u << (blk[q] & 31));
+    prev = blk[q];
+  }
+  // first valid pixel and valid count: per wave, then per workgroup
+  for (int sft = 32; sft > 0; sft >>= 1) {
+    first = min(first, __shfl_xor(first, sft, 64));
+    count += __shfl_xor(count, sft, 64);
+  }
+  __shared__ int s_first[4], s_count[4];
+  if (lane == 0) {
+    s_first[wave] = first;
+    s_count[wave] = count;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int first = s_first[0], count = s_count[0];
-    for (int w = 1; w < 4; w++) { first = min(first, s_first[w]); count += s_count[w]; }
-    if (count > 0) {
-      atomicMin(&stats[4 * job], first);
-      atomicAdd(&stats[4 * job + 1], count);
+    int f = s_first[0], c = s_count[0];
+    for (int w = 1; w < 4; w++) { f = min(f, s_first[w]); c += s_count[w]; }
+    if (c > 0) {
+      atomicMin(&stats[4 * job], f);
+      atomicAdd(&stats[4 * job + 1], c);
     }
   }
 }
@@ -2074,9 +2141,25 @@ int launch_warp_jobs(const RenderCall &rc, const BlockStatsJob *jobs, int64_t ma
   const int n = rc.n_pairs;
   hipLaunchKernelGGL(block_stats_init_kernel, dim3(n), dim3(256), 0, s, jobs, (char *)scratch, stats);
   if (max_px > 0) {
-    const dim3 grid((unsigned)((max_px + 255) / 256), n);
+    // eight pixels per thread, 8-32 bytes in one or two stores (service leg,
+    // 16 / 64 workers: 1 px 32.3k / 48.4k req/s, 4 px 42.1-43.4k / 61.3-66.2k,
+    // 8 px 44.8k / 62.7-63.4k; profiles/r05f_svc.txt, r05g_svc.txt);
+    // GSKYHIP_SVC_PX=1/4 selects the others
+    static const int env_px = [] {
+      const char *e = getenv("GSKYHIP_SVC_PX");
+      const int v = e ? atoi(e) : 8;
+      return v == 1 || v == 4 ? v : 8;
+    }();
+    const int px = rc.resample == GSKYHIP_RESAMPLE_BILINEAR ? 1 : env_px;
+    const dim3 grid((unsigned)((max_px + 256 * px - 1) / (256 * px)), n);
     if (rc.resample == GSKYHIP_RESAMPLE_BILINEAR)
       hipLaunchKernelGGL(warp_job_kernel<GSKYHIP_RESAMPLE_BILINEAR>, grid, dim3(256), 0, s, cv.pairs, cv.xforms,
+                         cv.rows, cv.pool, rc.max_h, jobs, (char *)scratch, stats, outs);
+    else if (px == 4)
+      hipLaunchKernelGGL((warp_job_kernel<GSKYHIP_RESAMPLE_NEAREST, 4>), grid, dim3(256), 0, s, cv.pairs, cv.xforms,
+                         cv.rows, cv.pool, rc.max_h, jobs, (char *)scratch, stats, outs);
+    else if (px == 8)
+      hipLaunchKernelGGL((warp_job_kernel<GSKYHIP_RESAMPLE_NEAREST, 8>), grid, dim3(256), 0, s, cv.pairs, cv.xforms,
                          cv.rows, cv.pool, rc.max_h, jobs, (char *)scratch, stats, outs);
     else
       hipLaunchKernelGGL(warp_job_kernel<GSKYHIP_RESAMPLE_NEAREST>, grid, dim3(256), 0, s, cv.pairs, cv.xforms,

@@ -518,7 +518,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   };
 
   // RGBA stores of row r
-  auto store_row = [&](int r, const uint32_t *px) {
+  auto store_row = [&](int r, const uint32_t *px, bool full_known = false) {
     uint32_t *dst = rgba_lane + (int64_t)r * a.max_w;
     if constexpr (STAGE && !CANVAS) {
       if (full && (a.max_w & 3) == 0) {
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
       return;
     }
 #endif
-    if (full) {
+    if (full_known || full) {
 #pragma unroll
       for (int q = 0; q < kNnPx; q++) st(dst + 64 * q, px[q]);
     } else {
@@ -616,54 +616,72 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
       } else if (cols_ok) {
         fetch(r0 - eyoff, cf, cfk);
       }
+      // the row loop, once for blocks whose every row the entry's window
+      // covers in a full-width block (CF: the fast fold and unconditional
+      // stores as straight-line code -- merged with the window-edge and
+      // ragged-block forms, the compiler predicated every pixel on spilled
+      // per-pixel masks) and once for the rest
+      auto row_loop = [&](auto cf_tag) {
+        constexpr bool CF = decltype(cf_tag)::value;
 #pragma unroll 1
-      for (int j = 0; j < RPW; j++) {
-        const int r = r0 + j;
-        if (r >= H) break;
-        if (vfetch) {
-          const int ir = r - eyoff;
-          if (!cols_ok || ir < 0 || ir >= eh) {
-            cfk = -1;
-          } else {
+        for (int j = 0; j < RPW; j++) {
+          const int r = r0 + j;
+          if (r >= H) break;
+          if (vfetch) {
+            const int ir = r - eyoff;
+            if (!cols_ok || ir < 0 || ir >= eh) {
+              cfk = -1;
+            } else {
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-              const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)fv, 4 * j + k);
-              const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)fv >> 32), 4 * j + k);
-              cf[k] = (int64_t)(((uint64_t)hi << 32) | lo);
+              for (int k = 0; k < 4; k++) {
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)fv, 4 * j + k);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)fv >> 32), 4 * j + k);
+                cf[k] = (int64_t)(((uint64_t)hi << 32) | lo);
+              }
+              cfk = cf[0] != kFixNone ? 1 : 0;
             }
-            cfk = cf[0] != kFixNone ? 1 : 0;
+          } else if (cols_ok && j + 1 < RPW) {
+            fetch(r + 1 - eyoff, nf, nfk);   // next row's record, in flight now
           }
-        } else if (cols_ok && j + 1 < RPW) {
-          fetch(r + 1 - eyoff, nf, nfk);   // next row's record, in flight now
-        }
-        V c[kNnPx];
+          V c[kNnPx];
 #pragma unroll
-        for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-        bool done = cfk < 0;
+          for (int q = 0; q < kNnPx; q++) c[q] = cnod;
+          bool done = cfk < 0;
 #ifdef GSKYHIP_AB
-        if (a.ab_mode == 1) done = true;   // A/B: no gathers
-        else
+          if (a.ab_mode == 1) done = true;   // A/B: no gathers
+          else
 #endif
-        if (cfk == 1)
-          done = cover ? (COOP ? nn_fix_row_coop<T, kNnPx>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode,
-                                                           c, lane)
-                               : nn_fix_row<T, kNnPx, false, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
-                                                                   fill_mode, c))
-                       : nn_fix_row<T, kNnPx, true, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode,
-                                                          c);
-        if (done) {
-          uint32_t px[kNnPx];
-          rgba(c, px);
-          store_row(r, px);
-        } else {
-          redo |= 1u << j;
-        }
-        if (!vfetch) {
+          if (cfk == 1) {
+            if constexpr (CF)
+              done = nn_fix_row<T, kNnPx, false, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c);
+            else
+              done = cover ? (COOP ? nn_fix_row_coop<T, kNnPx>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
+                                                               fill_mode, c, lane)
+                                   : nn_fix_row<T, kNnPx, false, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
+                                                                       fill_mode, c))
+                           : nn_fix_row<T, kNnPx, true, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
+                                                              fill_mode, c);
+          }
+          if (done) {
+            uint32_t px[kNnPx];
+            rgba(c, px);
+            store_row(r, px, CF);
+          } else {
+            redo |= 1u << j;
+          }
+          if (!vfetch) {
 #pragma unroll
-          for (int k = 0; k < 4; k++) cf[k] = nf[k];
-          cfk = nfk;
+            for (int k = 0; k < 4; k++) cf[k] = nf[k];
+            cfk = nfk;
+          }
         }
-      }
+      };
+      bool cf_on = cover && full && !COOP;
+#ifdef GSKYHIP_AB
+      if (a.ab_mode == 7) cf_on = false;   // A/B: one merged row loop (round 4)
+#endif
+      if (cf_on) row_loop(std::true_type{});
+      else row_loop(std::false_type{});
 #pragma unroll 1
       while (redo) {
         const int j = __builtin_ctz(redo);

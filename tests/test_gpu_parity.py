@@ -431,6 +431,46 @@ def test_warp_operation_fast_dropin(gpu, oracle):
     worker.unregister_all()
 
 
+@pytest.mark.parametrize("dtype,rtype", [("uint8", "Byte"), ("int16", "Int16"), ("float32", "Float32")])
+@pytest.mark.parametrize("w,h", [(256, 256), (257, 131), (33, 7)])
+def test_warp_operation_fast_dtypes_and_ragged_windows(gpu, oracle, dtype, rtype, w, h):
+    """warp.go:82 through the warp batch for 1-, 2- and 4-byte rasters and
+    window sizes whose pixel count is not a multiple of the kernel's pixels
+    per thread (the packed wide stores and the per-pixel tail)."""
+    import torch
+
+    from gsky_amd import worker
+    from gsky_amd.tiles import bbox_to_geot
+    cfg = synth.config_c2(scale=0.1, tiles_per_side=4, tile_px=256)
+    g = cfg.granules[5]
+    nod = g.data == g.nodata
+    if dtype == "uint8":
+        data, nodata = np.clip(g.data // 16, 0, 254).astype(np.uint8), 255.0
+    elif dtype == "float32":
+        data, nodata = g.data.astype(np.float32) * np.float32(0.25), float(g.nodata) * 0.25
+    else:
+        data, nodata = g.data, float(g.nodata)
+    data = data.copy()
+    data[nod] = nodata
+    path = "/g/data/c2/dt_%s.tif" % dtype
+    worker.register_granule(path, 1, torch.from_numpy(data).to(gpu), g.geot, "EPSG:3577", nodata, block=(128, 64))
+    try:
+        bb, _, _ = cfg.tiles[5]
+        dst_gt = bbox_to_geot(w, h, bb)
+        res = worker.warp_raster(worker.GeoRPCGranule(path=path, bands=[1], width=w, height=h,
+                                                      dstSRS="EPSG:3857", dstGeot=dst_gt))
+        assert res.error == "OK", res.error
+        og = oracle.make_granule(data, g.geot, nodata, block=(128, 64))
+        arr, bbox, nd, dt = oracle.warp(og, oracle.crs("EPSG:3577"), oracle.crs("EPSG:3857"), dst_gt, w, h)
+        assert res.raster.bbox == list(bbox) and res.raster.rasterType == rtype and res.raster.noData == nd
+        got = worker.raster_array(res.raster)
+        assert got.dtype == np.dtype(dtype) and got.size == arr.size
+        assert identity(got, arr) >= NN_IDENTITY
+        assert res.bytesRead == oracle.warp.bytes_read
+    finally:
+        worker.unregister_all()
+
+
 # ---------------------------------------------------------------- drill
 @pytest.mark.parametrize("strides,pc,clip", [(1, 0, (-1e30, 1e30)), (1, 1, (0.21, 0.26)), (3, 0, (0.2, 0.3)),
                                              (2, 0, (-1e30, 1e30))])
