@@ -42,7 +42,8 @@ class GskyError(RuntimeError):
 class Crs(C.Structure):
     _fields_ = [("kind", C.c_int32), ("_pad", C.c_int32)] + [
         (n, C.c_double) for n in ("a", "ra", "es", "e", "one_es", "lam0", "phi0", "phi1", "phi2",
-                                  "x0", "y0", "k0", "n", "c", "dd", "rho0", "ec")]
+                                  "x0", "y0", "k0", "n", "c", "dd", "rho0", "ec", "tm_qn", "tm_zb")] + [
+        (n, C.c_double * 6) for n in ("tm_cgb", "tm_cbg", "tm_utg", "tm_gtu")]
 
 
 class Granule(C.Structure):
@@ -87,7 +88,7 @@ class FlexRasterC(C.Structure):
 
 # every symbol include/gskyhip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "gskyhip_crs_from_srs", "gskyhip_register_granule", "gskyhip_unregister_all", "warp_operation_fast",
+    "gskyhip_crs_from_srs", "gskyhip_crs_transform", "gskyhip_register_granule", "gskyhip_unregister_all", "warp_operation_fast",
     "gskyhip_render_workspace_size", "gskyhip_render_tiles", "gskyhip_render_tiles_phase",
     "gskyhip_render_tiles_typed", "gskyhip_render_coverage", "gskyhip_warp_windows",
     "gskyhip_merge_rasters", "gskyhip_scale", "gskyhip_scale_legacy", "gskyhip_gradient_palette",
@@ -120,6 +121,8 @@ def lib() -> C.CDLL:
     vp, i32, i64, d = C.c_void_p, C.c_int32, C.c_int64, C.c_double
     ci = C.c_int
     L.gskyhip_crs_from_srs.argtypes = [C.c_char_p, C.POINTER(Crs)]
+    L.gskyhip_crs_transform.argtypes = [C.POINTER(Crs), C.POINTER(Crs), C.c_int, C.c_void_p, C.c_void_p,
+                                        C.c_void_p]
     L.gskyhip_register_granule.argtypes = [C.c_char_p, ci, C.POINTER(Granule), C.c_char_p]
     L.gskyhip_geotiff_info.argtypes = [C.c_char_p, C.POINTER(RasterInfo)]
     L.gskyhip_geotiff_read_host.argtypes = [C.c_char_p, ci, ci, vp, i64]

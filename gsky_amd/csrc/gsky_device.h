@@ -1,6 +1,6 @@
 // gsky_device.h -- device-side building blocks of the MI355X raster hot path.
 //
-// Projection math restates PROJ 6.1.1 (merc/webmerc, aea, gn_sinu and the
+// Projection math restates PROJ 6.1.1 (merc/webmerc, aea, gn_sinu, tmerc and the
 // pj_fwd / pj_inv wrappers) and GDAL 3.0.1's GenImgProj transformer; numeric
 // conversions restate Go 1.12 on amd64.  All of it
 // is compiled with -ffp-contract=off so every double expression rounds once
@@ -144,6 +144,97 @@ __host__ __device__ inline double aea_phi1(double qs, double Te, double Tone_es)
   return i ? Phi : HUGE_VAL;
 }
 
+// Transverse Mercator, ellipsoidal: the Poder / Engsager algorithm that
+// PROJ 6 runs for +proj=tmerc and +proj=utm (tmerc.cpp exact_e_fwd /
+// exact_e_inv / setup_exact, [ext]: not in /root/reference; restated from the
+// published algorithm -- Engsager & Poder, ICC 2007; Krueger series to n^6 as
+// in Karney 2011 -- parity unpinned beyond the known-answer points of
+// tests/test_tmerc.py).  Gaussian <-> geodetic latitude: a real Clenshaw sum
+// of sin(2k B); spherical <-> ellipsoidal N, E: a complex one.
+__host__ __device__ inline double tm_gatg(const double *p1, int len, double B) {
+  const double cos_2B = 2 * cos(2 * B);
+  const double *p = p1 + len;
+  double h = 0, h1 = *--p, h2 = 0;
+  while (p - p1) {
+    h = -h2 + cos_2B * h1 + *--p;
+    h2 = h1;
+    h1 = h;
+  }
+  return B + h * sin(2 * B);
+}
+
+__host__ __device__ inline double tm_clens(const double *a, int size, double arg_r) {
+  const double *p = a + size;
+  const double r = 2 * cos(arg_r);
+  double hr1 = 0, hr = *--p, hr2;
+  for (; a - p;) {
+    hr2 = hr1;
+    hr1 = hr;
+    hr = -hr2 + r * hr1 + *--p;
+  }
+  return sin(arg_r) * hr;
+}
+
+__host__ __device__ inline double tm_clenS(const double *a, int size, double arg_r, double arg_i, double *R,
+                                           double *I) {
+  const double *p = a + size;
+  const double sin_arg_r = sin(arg_r), cos_arg_r = cos(arg_r);
+  const double sinh_arg_i = sinh(arg_i), cosh_arg_i = cosh(arg_i);
+  double r = 2 * cos_arg_r * cosh_arg_i;
+  double i = -2 * sin_arg_r * sinh_arg_i;
+  double hi1 = 0, hr1 = 0, hi = 0, hr = *--p, hr2, hi2;
+  for (; a - p;) {
+    hr2 = hr1;
+    hi2 = hi1;
+    hr1 = hr;
+    hi1 = hi;
+    hr = -hr2 + r * hr1 - i * hi1 + *--p;
+    hi = -hi2 + i * hr1 + r * hi1;
+  }
+  r = sin_arg_r * cosh_arg_i;
+  i = cos_arg_r * sinh_arg_i;
+  *R = r * hr - i * hi;
+  *I = r * hi + i * hr;
+  return *R;
+}
+
+constexpr double kTmMaxCe = 2.623395162778;   // 150 degrees of spherical easting
+
+// (lam, phi) -> normalised (E, N) (before pj_fwd's a * x + x0).  Not inlined:
+// inlined, its transcendental chain raised the register peak of every kernel
+// carrying the projection switch (plan_small 350 -> 360 VGPRs, plan_pairs<256>
+// 198 -> 230); called, only the tmerc path pays for it.
+__host__ __device__ inline __attribute__((noinline)) bool tm_fwd(const gskyhip_crs &c, double lam, double phi, double &xn, double &yn) {
+  double Cn = tm_gatg(c.tm_cbg, 6, phi);   // ellipsoidal -> Gaussian latitude
+  const double sin_Cn = sin(Cn), cos_Cn = cos(Cn), sin_Ce = sin(lam), cos_Ce = cos(lam);
+  Cn = atan2(sin_Cn, cos_Ce * cos_Cn);     // Gaussian -> complementary spherical
+  double Ce = atan2(sin_Ce * cos_Cn, hypot(sin_Cn, cos_Cn * cos_Ce));
+  Ce = asinh(tan(Ce));
+  double dCn, dCe;
+  Cn += tm_clenS(c.tm_gtu, 6, 2 * Cn, 2 * Ce, &dCn, &dCe);
+  Ce += dCe;
+  if (!(fabs(Ce) <= kTmMaxCe)) return false;
+  yn = c.tm_qn * Cn + c.tm_zb;
+  xn = c.tm_qn * Ce;
+  return true;
+}
+
+// normalised (E, N) -> (lam, phi) (after pj_inv's (x - x0) / a).
+__host__ __device__ inline __attribute__((noinline)) bool tm_inv(const gskyhip_crs &c, double xn, double yn, double &lam, double &phi) {
+  double Cn = (yn - c.tm_zb) / c.tm_qn, Ce = xn / c.tm_qn;
+  if (!(fabs(Ce) <= kTmMaxCe)) return false;
+  double dCn, dCe;
+  Cn += tm_clenS(c.tm_utg, 6, 2 * Cn, 2 * Ce, &dCn, &dCe);
+  Ce += dCe;
+  Ce = atan(sinh(Ce));
+  const double sin_Cn = sin(Cn), cos_Cn = cos(Cn), sin_Ce = sin(Ce), cos_Ce = cos(Ce);
+  Ce = atan2(sin_Ce, cos_Ce * cos_Cn);
+  Cn = atan2(sin_Cn * cos_Ce, hypot(sin_Ce, cos_Ce * cos_Cn));
+  phi = tm_gatg(c.tm_cgb, 6, Cn);
+  lam = Ce;
+  return true;
+}
+
 // pj_inv: CRS coordinates -> (lam, phi) in radians.
 __host__ __device__ inline bool crs_inverse(const gskyhip_crs &c, double x, double y, double &lam, double &phi) {
   if (x == HUGE_VAL || y == HUGE_VAL) return false;
@@ -185,6 +276,8 @@ __host__ __device__ inline bool crs_inverse(const gskyhip_crs &c, double x, doub
   } else if (c.kind == GSKYHIP_CRS_SINU) {  // gn_sinu.cpp s_inverse (m=0, n=1)
     p = yn;
     l = xn / cos(yn);
+  } else if (c.kind == GSKYHIP_CRS_TMERC) {  // tmerc.cpp exact_e_inv
+    if (!tm_inv(c, xn, yn, l, p)) return false;
   } else {
     return false;
   }
@@ -223,6 +316,8 @@ __host__ __device__ inline bool crs_forward(const gskyhip_crs &c, double lam, do
   } else if (c.kind == GSKYHIP_CRS_SINU) {  // gn_sinu.cpp s_forward (m=0, n=1)
     xn = lam * cos(phi);
     yn = phi;
+  } else if (c.kind == GSKYHIP_CRS_TMERC) {  // tmerc.cpp exact_e_fwd
+    if (!tm_fwd(c, lam, phi, xn, yn)) return false;
   } else {
     return false;
   }

@@ -88,6 +88,69 @@ int aea_setup(gskyhip_crs *c) {
   return 0;
 }
 
+// tmerc.cpp setup_exact() of PROJ 6.1.1 (the Poder / Engsager series,
+// gsky_device.h tm_fwd / tm_inv): third flattening n, the 6th-order series
+// coefficients, the normalised meridian quadrant Qn and the northing of the
+// origin latitude Zb.  Ellipsoids only (the spherical tmerc is not carried).
+int tmerc_setup(gskyhip_crs *c) {
+  if (!(c->es > 0)) return GSKYHIP_E_CRS;
+  c->kind = GSKYHIP_CRS_TMERC;
+  const double f = c->es / (1 + std::sqrt(1 - c->es));
+  const double n = f / (2 - f);
+  double np = n;
+  double *cgb = c->tm_cgb, *cbg = c->tm_cbg, *utg = c->tm_utg, *gtu = c->tm_gtu;
+  cgb[0] = n * (2 + n * (-2 / 3.0 + n * (-2 + n * (116 / 45.0 + n * (26 / 45.0 + n * (-2854 / 675.0))))));
+  cbg[0] = n * (-2 + n * (2 / 3.0 + n * (4 / 3.0 + n * (-82 / 45.0 + n * (32 / 45.0 + n * (4642 / 4725.0))))));
+  np *= n;
+  cgb[1] = np * (7 / 3.0 + n * (-8 / 5.0 + n * (-227 / 45.0 + n * (2704 / 315.0 + n * (2323 / 945.0)))));
+  cbg[1] = np * (5 / 3.0 + n * (-16 / 15.0 + n * (-13 / 9.0 + n * (904 / 315.0 + n * (-1522 / 945.0)))));
+  np *= n;
+  cgb[2] = np * (56 / 15.0 + n * (-136 / 35.0 + n * (-1262 / 105.0 + n * (73814 / 2835.0))));
+  cbg[2] = np * (-26 / 15.0 + n * (34 / 21.0 + n * (8 / 5.0 + n * (-12686 / 2835.0))));
+  np *= n;
+  cgb[3] = np * (4279 / 630.0 + n * (-332 / 35.0 + n * (-399572 / 14175.0)));
+  cbg[3] = np * (1237 / 630.0 + n * (-12 / 5.0 + n * (-24832 / 14175.0)));
+  np *= n;
+  cgb[4] = np * (4174 / 315.0 + n * (-144838 / 6237.0));
+  cbg[4] = np * (-734 / 315.0 + n * (109598 / 31185.0));
+  np *= n;
+  cgb[5] = np * (601676 / 22275.0);
+  cbg[5] = np * (444337 / 155925.0);
+  np = n * n;
+  c->tm_qn = c->k0 / (1 + n) * (1 + np * (1 / 4.0 + np * (1 / 64.0 + np / 256.0)));
+  utg[0] = n * (-0.5 + n * (2 / 3.0 + n * (-37 / 96.0 + n * (1 / 360.0 + n * (81 / 512.0 + n * (-96199 / 604800.0))))));
+  gtu[0] = n * (0.5 + n * (-2 / 3.0 + n * (5 / 16.0 + n * (41 / 180.0 + n * (-127 / 288.0 + n * (7891 / 37800.0))))));
+  utg[1] = np * (-1 / 48.0 + n * (-1 / 15.0 + n * (437 / 1440.0 + n * (-46 / 105.0 + n * (1118711 / 3870720.0)))));
+  gtu[1] = np * (13 / 48.0 + n * (-3 / 5.0 + n * (557 / 1440.0 + n * (281 / 630.0 + n * (-1983433 / 1935360.0)))));
+  np *= n;
+  utg[2] = np * (-17 / 480.0 + n * (37 / 840.0 + n * (209 / 4480.0 + n * (-5569 / 90720.0))));
+  gtu[2] = np * (61 / 240.0 + n * (-103 / 140.0 + n * (15061 / 26880.0 + n * (167603 / 181440.0))));
+  np *= n;
+  utg[3] = np * (-4397 / 161280.0 + n * (11 / 504.0 + n * (830251 / 7257600.0)));
+  gtu[3] = np * (49561 / 161280.0 + n * (-179 / 168.0 + n * (6601661 / 7257600.0)));
+  np *= n;
+  utg[4] = np * (-4583 / 161280.0 + n * (108847 / 3991680.0));
+  gtu[4] = np * (34729 / 80640.0 + n * (-3418889 / 1995840.0));
+  np *= n;
+  utg[5] = np * (-20648693 / 638668800.0);
+  gtu[5] = np * (212378941 / 319334400.0);
+  const double Z = tm_gatg(cbg, 6, c->phi0);   // Gaussian latitude of the origin
+  c->tm_zb = -c->tm_qn * (Z + tm_clens(gtu, 6, 2 * Z));
+  return 0;
+}
+
+// utm.cpp setup: zone -> central meridian, k0 0.9996, false easting 500 km,
+// false northing 10,000 km in the south.
+int utm_setup(gskyhip_crs *c, int zone, bool south) {
+  if (zone < 1 || zone > 60) return GSKYHIP_E_CRS;
+  c->lam0 = (zone - 0.5) * (kPi / 30.0) - kPi;   // PROJ: (zone - .5) * M_PI / 30. - M_PI
+  c->phi0 = 0.0;
+  c->k0 = 0.9996;
+  c->x0 = 500000.0;
+  c->y0 = south ? 10000000.0 : 0.0;
+  return tmerc_setup(c);
+}
+
 double proj_param(const std::string &s, const char *key, double dflt, bool *found = nullptr) {
   const std::string k = std::string(key) + "=";
   size_t pos = 0;
@@ -114,8 +177,16 @@ int crs_epsg(int code, gskyhip_crs *c) {
       set_ellps(c, 6378137.0, 298.257222101);
       c->lam0 = 132.0 * kD2R_h; c->phi0 = 0.0; c->phi1 = -18.0 * kD2R_h; c->phi2 = -36.0 * kD2R_h;
       return aea_setup(c);
-    default: return GSKYHIP_E_CRS;
+    default: break;
   }
+  // Transverse Mercator zones: WGS 84 / UTM north (326zz) and south (327zz),
+  // GDA94 / MGA (283zz, zones 48-58) and GDA2020 / MGA (78zz, zones 46-59);
+  // both GDA datums on GRS80, taken without a datum shift like EPSG:3577
+  if (code >= 32601 && code <= 32660) { set_ellps(c, 6378137.0, 298.257223563); return utm_setup(c, code - 32600, false); }
+  if (code >= 32701 && code <= 32760) { set_ellps(c, 6378137.0, 298.257223563); return utm_setup(c, code - 32700, true); }
+  if (code >= 28348 && code <= 28358) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 28300, true); }
+  if (code >= 7846 && code <= 7859) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 7800, true); }
+  return GSKYHIP_E_CRS;
 }
 
 int crs_proj4(const std::string &s, gskyhip_crs *c) {
@@ -151,6 +222,21 @@ int crs_proj4(const std::string &s, gskyhip_crs *c) {
     c->kind = GSKYHIP_CRS_SINU; set_ellps(c, a, rf);
     return c->es == 0 ? 0 : GSKYHIP_E_CRS;  // only the spherical form (MODIS)
   }
+  if (s.find("+proj=utm") != std::string::npos) {
+    set_ellps(c, a, rf);
+    bool has_zone = false;
+    const double zone = proj_param(s, "+zone", 0, &has_zone);
+    if (!has_zone || zone != std::floor(zone)) return GSKYHIP_E_CRS;   // PROJ guesses from lon_0: not carried
+    return utm_setup(c, (int)zone, s.find("+south") != std::string::npos);
+  }
+  if (s.find("+proj=tmerc") != std::string::npos || s.find("+proj=etmerc") != std::string::npos) {
+    if (s.find("+approx") != std::string::npos) return GSKYHIP_E_CRS;   // Evenden / Snyder series: not carried
+    set_ellps(c, a, rf);
+    bool has_k = false;
+    c->k0 = proj_param(s, "+k_0", 1.0, &has_k);
+    if (!has_k) c->k0 = proj_param(s, "+k", 1.0);
+    return tmerc_setup(c);
+  }
   return GSKYHIP_E_CRS;
 }
 
@@ -161,7 +247,7 @@ int parse_srs(const char *srs, gskyhip_crs *c) {
   if (ieq(s, "MODIS") || ieq(s, "SR-ORG:6842")) return crs_proj4("+proj=sinu +R=6371007.181", c);
   if (s.size() > 5 && strncasecmp(s.c_str(), "EPSG:", 5) == 0) return crs_epsg(std::atoi(s.c_str() + 5), c);
   if (s.find("+proj=") != std::string::npos) return crs_proj4(s, c);
-  // WKT: a Sinusoidal / Albers projection, else the top-level (last) EPSG authority
+  // WKT: a Sinusoidal / Transverse Mercator projection, else the top-level (last) EPSG authority
   if (s.find("PROJECTION[\"Sinusoidal\"]") != std::string::npos) {
     size_t p = s.find("SPHEROID[");
     double a = 6371007.181;
@@ -172,6 +258,38 @@ int parse_srs(const char *srs, gskyhip_crs *c) {
     char buf[96];
     std::snprintf(buf, sizeof(buf), "+proj=sinu +R=%.17g", a);
     return crs_proj4(buf, c);
+  }
+  if (s.find("PROJECTION[\"Transverse_Mercator\"]") != std::string::npos) {   // WKT1 TM: its parameters
+    auto param = [&](const char *name, double dflt) {
+      const std::string k = std::string("PARAMETER[\"") + name + "\",";
+      const size_t p = s.find(k);
+      return p == std::string::npos ? dflt : std::strtod(s.c_str() + p + k.size(), nullptr);
+    };
+    double a = 6378137.0, rf = 298.257223563;
+    const size_t p = s.find("SPHEROID[");
+    if (p != std::string::npos) {
+      const size_t q = s.find(',', p);
+      if (q != std::string::npos) {
+        char *end = nullptr;
+        a = std::strtod(s.c_str() + q + 1, &end);
+        if (end && *end == ',') rf = std::strtod(end + 1, nullptr);
+      }
+    }
+    std::memset(c, 0, sizeof(*c));
+    set_ellps(c, a, rf);
+    const double lat0 = param("latitude_of_origin", 0), cm = param("central_meridian", 0);
+    c->k0 = param("scale_factor", 1.0);
+    c->x0 = param("false_easting", 0);
+    c->y0 = param("false_northing", 0);
+    // a UTM zone's parameters become +proj=utm in PROJ 6 (Conversion's
+    // isUTM when exporting the PROJ string): the zone's own central meridian
+    const double zone = (cm + 183.0) / 6.0;
+    if (lat0 == 0 && c->k0 == 0.9996 && c->x0 == 500000.0 && (c->y0 == 0 || c->y0 == 10000000.0) &&
+        zone == std::floor(zone) && zone >= 1 && zone <= 60)
+      return utm_setup(c, (int)zone, c->y0 != 0);
+    c->phi0 = lat0 * kD2R_h;
+    c->lam0 = cm * kD2R_h;
+    return tmerc_setup(c);
   }
   size_t pos = s.rfind("AUTHORITY[\"EPSG\",\"");
   if (pos != std::string::npos) return crs_epsg(std::atoi(s.c_str() + pos + 18), c);
@@ -707,6 +825,16 @@ bool is_geotiff_path(const std::string &p) {
 extern "C" {
 
 int gskyhip_crs_from_srs(const char *srs, gskyhip_crs *out) { return parse_srs(srs, out); }
+
+int gskyhip_crs_transform(const gskyhip_crs *src, const gskyhip_crs *dst, int n, double *x, double *y,
+                          int32_t *ok) {
+  if (!src || !dst || n < 0 || (n > 0 && (!x || !y || !ok))) return GSKYHIP_E_ARG;
+  for (int i = 0; i < n; i++) {
+    double lam, phi;
+    ok[i] = crs_inverse(*src, x[i], y[i], lam, phi) && crs_forward(*dst, lam, phi, x[i], y[i]) ? 1 : 0;
+  }
+  return 0;
+}
 
 uint32_t gskyhip_fnv32a(const char *s, int64_t n) {
   uint32_t h = 2166136261u;  // Go hash/fnv New32a (tile_merger.go:473-475)

@@ -614,31 +614,33 @@ __device__ void plan_pair(const PlanArgs &a, int p, double *sx, double *sy, int 
   // through pointers) or cost ~130 VGPRs
   Xform &t = ts;
   {   // set up by the lanes side by side (round 3 had lane 0 copy ~90 words
-      // and invert both geotransforms in series): lanes 0-35 the two CRS
-      // records a word each, 36-47 the geotransforms, 48 / 49 the inverses
-      // (from global), 50 the reprojection flag and the geolocation arrays
-    static_assert(sizeof(gskyhip_crs) % 8 == 0 && sizeof(gskyhip_crs) / 8 * 2 + 15 <= 64, "crs words");
-    constexpr int kCw = (int)(sizeof(gskyhip_crs) / 8);   // 18 words
+      // and invert both geotransforms in series): work item w < 2 kCw is a
+      // word of the two CRS records, then 6 + 6 geotransform words, the two
+      // inverses (from global) and the reprojection flag / geolocation arrays
+    static_assert(sizeof(gskyhip_crs) % 8 == 0, "crs words");
+    constexpr int kCw = (int)(sizeof(gskyhip_crs) / 8);   // 43 words
     const int dsti = a.dst_crs >= 0 ? a.dst_crs : g.crs;
-    if (lane < kCw) {
-      ((uint64_t *)&t.src)[lane] = ((const uint64_t *)&a.crs[g.crs])[lane];
-    } else if (lane < 2 * kCw) {
-      ((uint64_t *)&t.dst)[lane - kCw] = ((const uint64_t *)&a.crs[dsti])[lane - kCw];
-    } else if (lane < 2 * kCw + 6) {
-      t.src_gt[lane - 2 * kCw] = g.geot[lane - 2 * kCw];
-    } else if (lane < 2 * kCw + 12) {
-      t.dst_gt[lane - 2 * kCw - 6] = tile.dst_geot[lane - 2 * kCw - 6];
-    } else if (lane == 2 * kCw + 12) {
-      double gt[6];
-      for (int k = 0; k < 6; k++) gt[k] = g.geot[k];
-      inv_geot(gt, t.src_igt);
-    } else if (lane == 2 * kCw + 13) {
-      double gt[6];
-      for (int k = 0; k < 6; k++) gt[k] = tile.dst_geot[k];
-      inv_geot(gt, t.dst_igt);
-    } else if (lane == 2 * kCw + 14) {
-      t.gl = (g.geoloc > 0 && a.geolocs) ? a.geolocs + (g.geoloc - 1) : nullptr;
-      t.reproject = a.dst_crs >= 0 ? (crs_same(a.crs[g.crs], a.crs[a.dst_crs]) ? 0 : 1) : 0;
+    for (int w = lane; w < 2 * kCw + 15; w += NT) {
+      if (w < kCw) {
+        ((uint64_t *)&t.src)[w] = ((const uint64_t *)&a.crs[g.crs])[w];
+      } else if (w < 2 * kCw) {
+        ((uint64_t *)&t.dst)[w - kCw] = ((const uint64_t *)&a.crs[dsti])[w - kCw];
+      } else if (w < 2 * kCw + 6) {
+        t.src_gt[w - 2 * kCw] = g.geot[w - 2 * kCw];
+      } else if (w < 2 * kCw + 12) {
+        t.dst_gt[w - 2 * kCw - 6] = tile.dst_geot[w - 2 * kCw - 6];
+      } else if (w == 2 * kCw + 12) {
+        double gt[6];
+        for (int k = 0; k < 6; k++) gt[k] = g.geot[k];
+        inv_geot(gt, t.src_igt);
+      } else if (w == 2 * kCw + 13) {
+        double gt[6];
+        for (int k = 0; k < 6; k++) gt[k] = tile.dst_geot[k];
+        inv_geot(gt, t.dst_igt);
+      } else if (w == 2 * kCw + 14) {
+        t.gl = (g.geoloc > 0 && a.geolocs) ? a.geolocs + (g.geoloc - 1) : nullptr;
+        t.reproject = a.dst_crs >= 0 ? (crs_same(a.crs[g.crs], a.crs[a.dst_crs]) ? 0 : 1) : 0;
+      }
     }
   }
   __syncthreads();
@@ -2065,7 +2067,9 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.ab_mode = 0;
   a.ab_vfetch = 1;
   a.ab_xcd = 0;
+  a.nn_colg = 0;
 #ifdef GSKYHIP_AB
+  if (const char *cg = getenv("GSKYHIP_NN_COLG")) a.nn_colg = atoi(cg);
   if (const char *sp = getenv("GSKYHIP_NN_STPOL")) a.st_pol = atoi(sp);
   if (const char *am = getenv("GSKYHIP_AB_MODE")) a.ab_mode = atoi(am);
   if (const char *vf = getenv("GSKYHIP_NN_VFETCH")) a.ab_vfetch = atoi(vf);

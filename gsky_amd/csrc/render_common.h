@@ -216,6 +216,7 @@ struct RenderArgs {
   int ab_mode;                 // A/B build only: 1 skip the NN gathers, 2 skip the RGBA stores
   int ab_vfetch;               // A/B build only: 0 = per-row scalar RowFix fetch in the NN kernel
   int ab_xcd;                  // A/B build only: 1 = a tile's blocks on one XCD (NN kernel item order)
+  int nn_colg;                 // A/B build only: NN single-entry blocks in column-group-major order
 };
 
 // ---------------------------------------------------------------- typed fast path

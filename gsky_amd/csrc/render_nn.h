@@ -649,7 +649,20 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
           bool done = cfk < 0;
 #ifdef GSKYHIP_AB
           if (a.ab_mode == 1) done = true;   // A/B: no gathers
-          else
+          else if (a.ab_mode == 8 && cfk == 1) {
+            // A/B lower bound: the same number of gathers, fold, Scale,
+            // palette and stores, with near-free index math -- an unrotated
+            // 0.47 source px per output px pattern from the row's first pixel
+            const uint32_t ix0 = (uint32_t)(cf[0] >> 32), iy0 = (uint32_t)(cf[1] >> 32);
+            const uint32_t rb = (__umul24(iy0, (uint32_t)bx) + ix0) * (uint32_t)sizeof(T);
+            V vv[kNnPx];
+#pragma unroll
+            for (int q = 0; q < kNnPx; q++)
+              vv[q] = buf_load<T>(rs, rb + (((uint32_t)(lane + 64 * q) * 15u) >> 5) * (uint32_t)sizeof(T));
+#pragma unroll
+            for (int q = 0; q < kNnPx; q++) c[q] = vv[q] != nd ? vv[q] : c[q];
+            done = true;
+          } else
 #endif
           if (cfk == 1) {
             if constexpr (CF)
@@ -680,8 +693,75 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 #ifdef GSKYHIP_AB
       if (a.ab_mode == 7) cf_on = false;   // A/B: one merged row loop (round 4)
 #endif
-      if (cf_on) row_loop(std::true_type{});
-      else row_loop(std::false_type{});
+      // COLG (A/B build, GSKYHIP_NN_COLG=1; measured slower): the block's 8
+      // rows x 512 columns in column-group-major order -- for each 64-column
+      // group the wave's RPW rows back to back, so the RPW gathers in flight
+      // read the few source lines under that group.  Row-major, L1 -> L2
+      // reads are 7x the unique source bytes (32 waves per CU evict a wave's
+      // lines before its next row); this order halves them (57.4 M -> 31.5 M
+      // requests) and still runs 1.64 vs 1.57 ms: the texture data unit stays
+      // busy ~97 % of the kernel at ~21 L1 accesses per 64-lane gather
+      // (profiles/r05j_pmc_c2_l1.json, r05k_*).  The same fixed-point values
+      // and margin test as nn_fix_row, the same fp64 redo of a row with an
+      // ambiguous pixel: the same result bit for bit (0 px differ on C2, C5).
+      bool colg_done = false;
+#ifdef GSKYHIP_AB
+      if constexpr (RPW == kNnPx && !COOP && !WIDE) {
+        bool colg = a.nn_colg && cf_on && vfetch && r0 + RPW <= H && r0 - eyoff >= 0 && r0 + RPW - eyoff <= eh;
+        if (colg) {
+          const bool missing = lane < 4 * RPW && (lane & 3) == 0 && fv == kFixNone;
+          colg = __builtin_amdgcn_ballot_w64(missing) == 0;
+        }
+        if (colg) {
+          colg_done = true;
+          uint32_t amb = 0;   // per lane: bit j = row j has an ambiguous pixel
+          uint32_t *const dst0 = rgba_lane + (int64_t)r0 * a.max_w;
+#pragma unroll 1
+          for (int g = 0; g < kNnPx; g++) {
+            // the row records come by scalar loads each group (held across the
+            // loop they would be 64 SGPRs)
+            int jb = r0 - eyoff;
+            asm volatile("" : "+s"(jb));   // (the index, not the pointer: that keeps its address space)
+            const RowFix *rb = fbase + jb;
+            const uint32_t ic = (uint32_t)(ic0 + 64 * g);
+            uint32_t off[RPW];
+#pragma unroll
+            for (int j = 0; j < RPW; j++) {
+              const uint64_t x0 = (uint64_t)uni64(rb[j].x0), y0 = (uint64_t)uni64(rb[j].y0);
+              const uint64_t dx = (uint64_t)uni64(rb[j].dx), dy = (uint64_t)uni64(rb[j].dy);
+              const uint64_t X = x0 + (uint64_t)ic * dx, Y = y0 + (uint64_t)ic * dy;
+              const uint32_t m = min((uint32_t)X + kFixMargin, (uint32_t)Y + kFixMargin);
+              amb |= (m < 2u * kFixMargin ? 1u : 0u) << j;
+              off[j] = (__umul24((uint32_t)(Y >> 32), (uint32_t)bx) + (uint32_t)(X >> 32)) * (uint32_t)sizeof(T);
+            }
+            V vv[RPW];
+#pragma unroll
+            for (int j = 0; j < RPW; j++) vv[j] = buf_load<T>(rs, off[j]);
+            V c[RPW];
+            if (!fill_mode) {
+#pragma unroll
+              for (int j = 0; j < RPW; j++) c[j] = vv[j] != nd ? vv[j] : cnod;
+            } else {
+              const bool take = cnod == nd;
+#pragma unroll
+              for (int j = 0; j < RPW; j++) c[j] = take ? vv[j] : cnod;
+            }
+            uint32_t px[RPW];
+            rgba(c, px);
+#pragma unroll
+            for (int j = 0; j < RPW; j++)
+              __builtin_nontemporal_store(px[j], (GPTR(uint32_t))(dst0 + (int64_t)j * a.max_w + 64 * g));
+          }
+#pragma unroll
+          for (int j = 0; j < RPW; j++)
+            if (__builtin_amdgcn_ballot_w64((amb >> j) & 1u) != 0) redo |= 1u << j;
+        }
+      }
+#endif
+      if (!colg_done) {
+        if (cf_on) row_loop(std::true_type{});
+        else row_loop(std::false_type{});
+      }
 #pragma unroll 1
       while (redo) {
         const int j = __builtin_ctz(redo);

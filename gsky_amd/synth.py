@@ -159,9 +159,12 @@ def _footprint_merc(g: SynthGranule, n=16):
         lon, lat = AEA.inv(X, Y)
     elif g.srs == "EPSG:4326":
         lon, lat = X, np.clip(Y, -85.05, 85.05)
-    else:
+    elif g.srs.upper() in ("MODIS", "SR-ORG:6842") or "+proj=sinu" in g.srs:
         lon, lat = sinu_inv(X, Y)
         lon = np.clip(lon, -180, 180)
+    else:   # any other SRS the library parses (UTM / MGA zones): its host transform
+        from .tiles import crs_transform
+        lon, lat, _ = crs_transform(g.srs, "EPSG:4326", X, Y)
     mx, my = merc_fwd(lon, lat)
     return mx.min(), my.min(), mx.max(), my.max()
 
@@ -279,6 +282,42 @@ def config_c2(scale: float = 1.0, tiles_per_side: int = 64, tile_px: int = 512, 
     tiles = _grid_tiles(bbox, tiles_per_side, tiles_per_side, tile_px)
     pairs = _index_pairs(granules, tiles)
     return SynthConfig("C2", granules, "EPSG:3857", tiles, pairs, [""], (0.0, 0.0, 10000.0, 0), PALETTE_GSKY)
+
+
+# ---------------------------------------------------------------- UTM (widening)
+def config_utm(scale: float = 1.0, tiles_per_side: int = 16, tile_px: int = 256, grid: int = 2,
+               srs: str = "EPSG:28355") -> SynthConfig:
+    """C2's shape from Transverse Mercator granules: `grid`^2 int16 granules
+    of GDA94 / MGA zone 55 (default; 4000^2 at 25 m at full size, 100 km
+    each, 5 km overlaps, over Victoria around 144-147 E), EPSG:3857 tiles over
+    their union, nearest, the C2 scale and palette."""
+    n = int(round(4000 * scale))
+    psize = 100000.0 / n
+    def make(k):
+        j, i = divmod(k, grid)
+        x0 = 250000.0 + 95000.0 * i
+        y0 = 5900000.0 - 95000.0 * j
+        idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + 0x7A00 + k) << 32)
+        v = (splitmix64(idx) % np.uint64(10000)).astype(np.int16)
+        v[uniform01(splitmix64(idx)) < 0.02] = -999
+        poly = "POLYGON ((%.1f %.1f,%.1f %.1f,%.1f %.1f,%.1f %.1f,%.1f %.1f))" % (
+            x0, y0, x0 + 100000, y0, x0 + 100000, y0 - 100000, x0, y0 - 100000, x0, y0)
+        return SynthGranule(v, [x0, psize, 0.0, y0, 0.0, -psize], srs, -999.0, 1577836800.0 + 86400.0 * k, poly)
+
+    granules = [make(k) for k in range(grid * grid)]
+    from .tiles import crs_transform
+    ux0, uy1 = 250000.0, 5900000.0
+    ux1, uy0 = ux0 + 95000.0 * (grid - 1) + 100000.0, uy1 - 95000.0 * (grid - 1) - 100000.0
+    t = np.linspace(0, 1, 64)
+    X = np.concatenate([ux0 + t * (ux1 - ux0)] * 2 + [np.full(64, ux0), np.full(64, ux1)])
+    Y = np.concatenate([np.full(64, uy0), np.full(64, uy1)] + [uy0 + t * (uy1 - uy0)] * 2)
+    lon, lat, _ = crs_transform(srs, "EPSG:4326", X, Y)
+    mx, my = merc_fwd(lon, lat)
+    bbox = (float(np.floor(mx.min())), float(np.floor(my.min())), float(np.ceil(mx.max())),
+            float(np.ceil(my.max())))
+    tiles = _grid_tiles(bbox, tiles_per_side, tiles_per_side, tile_px)
+    pairs = _index_pairs(granules, tiles)
+    return SynthConfig("UTM", granules, "EPSG:3857", tiles, pairs, [""], (0.0, 0.0, 10000.0, 0), PALETTE_GSKY)
 
 
 def subset(cfg: SynthConfig, tile_ids) -> SynthConfig:

@@ -39,6 +39,21 @@ def parse_crs(srs: str) -> _lib.Crs:
     return c
 
 
+def crs_transform(src_srs: str, dst_srs: str, x, y):
+    """Points from one SRS to another on the host, through the functions the
+    kernels run (gskyhip_crs_transform; OGRCoordinateTransformation's place in
+    the warp, warp.go:130).  Returns (x, y, ok) float64 / bool arrays."""
+    a, b = parse_crs(src_srs), parse_crs(dst_srs)
+    xs = np.array(x, dtype=np.float64).ravel().copy()
+    ys = np.array(y, dtype=np.float64).ravel().copy()
+    if xs.size != ys.size:
+        raise ValueError("crs_transform: x and y differ in length")
+    ok = np.zeros(xs.size, np.int32)
+    check(lib().gskyhip_crs_transform(C.byref(a), C.byref(b), xs.size, xs.ctypes.data, ys.ctypes.data,
+                                      ok.ctypes.data), "crs_transform")
+    return xs, ys, ok.astype(bool)
+
+
 def _to_device_bytes(obj, device) -> torch.Tensor:
     raw = np.frombuffer(bytes(obj), dtype=np.uint8).copy()
     return torch.from_numpy(raw).to(device)

@@ -55,6 +55,9 @@ extern "C" {
 #define GSKYHIP_CRS_WEBMERC 1      /* EPSG:3857                                 */
 #define GSKYHIP_CRS_AEA 2          /* EPSG:3577 (GDA94 / Australian Albers)    */
 #define GSKYHIP_CRS_SINU 3         /* MODIS sinusoidal, sphere R=6371007.181    */
+#define GSKYHIP_CRS_TMERC 4        /* Transverse Mercator, ellipsoidal: UTM     *
+                                    * (EPSG:326zz / 327zz), GDA94 / GDA2020 MGA *
+                                    * (EPSG:283zz / 78zz), +proj=tmerc / utm    */
 
 typedef struct {
     int32_t kind;
@@ -62,12 +65,26 @@ typedef struct {
     double a, ra, es, e, one_es;
     double lam0, phi0, phi1, phi2, x0, y0, k0;
     double n, c, dd, rho0, ec;      /* aea constants                           */
+    /* tmerc (Poder / Engsager, 6th order): normalised meridian quadrant,
+     * northing of the origin latitude, and the trigonometric series
+     * Gaussian <-> geodetic latitude (cgb, cbg) and ellipsoidal <->
+     * spherical northing / easting (utg, gtu)                                */
+    double tm_qn, tm_zb;
+    double tm_cgb[6], tm_cbg[6], tm_utg[6], tm_gtu[6];
 } gskyhip_crs;
 
 /* Parse an SRS as handed over by gsky-ows (tile_grpc.go:127-136 exports the
  * request CRS as WKT): WKT with a top-level AUTHORITY["EPSG",...], "EPSG:n",
  * a proj4 string, or "MODIS".  Returns 0 or GSKYHIP_E_CRS. */
 int gskyhip_crs_from_srs(const char *srs, gskyhip_crs *out);
+
+/* The coordinate transformation of the warp's GenImgProj transformer between
+ * two parsed CRSs (PROJ pj_inv of src, then pj_fwd of dst; the
+ * OGRCoordinateTransformation step of warp.go:130), on the host with the same
+ * functions the kernels run: x[i], y[i] in place, ok[i] = 1 or 0 (the
+ * transform failed; x / y then undefined).  Returns 0 or GSKYHIP_E_ARG. */
+int gskyhip_crs_transform(const gskyhip_crs *src, const gskyhip_crs *dst, int n, double *x, double *y,
+                          int32_t *ok);
 
 /* ---- granules (the HBM-resident stand-in for an opened GDAL dataset) ----- */
 #define GSKYHIP_MAX_OVR 12

@@ -667,6 +667,111 @@ static int aea_setup(oracle_crs *c) {
     return 0;
 }
 
+/* ---- tmerc.cpp (PROJ 6.1.1), the exact ellipsoidal algorithm [ext] ------
+ * Poder / Engsager: geodetic <-> Gaussian latitude by a trigonometric series,
+ * Gaussian <-> complementary spherical by spherical trigonometry, spherical
+ * <-> ellipsoidal (N, E) by a complex trigonometric series; all series of
+ * 6th order in the third flattening n (the Krueger series), summed by
+ * Clenshaw.  Restated from the published algorithm; pinned by the
+ * known-answer points of tests/test_tmerc.py.  Coefficient k of each series
+ * is n^(k+1) * (c[0] + n * (c[1] + ...)): the rational coefficients below. */
+typedef struct { int len; double c[6]; } or_poly;
+static const or_poly OR_CGB[6] = {
+    {6, {2, -2 / 3.0, -2, 116 / 45.0, 26 / 45.0, -2854 / 675.0}},
+    {5, {7 / 3.0, -8 / 5.0, -227 / 45.0, 2704 / 315.0, 2323 / 945.0}},
+    {4, {56 / 15.0, -136 / 35.0, -1262 / 105.0, 73814 / 2835.0}},
+    {3, {4279 / 630.0, -332 / 35.0, -399572 / 14175.0}},
+    {2, {4174 / 315.0, -144838 / 6237.0}},
+    {1, {601676 / 22275.0}}};
+static const or_poly OR_CBG[6] = {
+    {6, {-2, 2 / 3.0, 4 / 3.0, -82 / 45.0, 32 / 45.0, 4642 / 4725.0}},
+    {5, {5 / 3.0, -16 / 15.0, -13 / 9.0, 904 / 315.0, -1522 / 945.0}},
+    {4, {-26 / 15.0, 34 / 21.0, 8 / 5.0, -12686 / 2835.0}},
+    {3, {1237 / 630.0, -12 / 5.0, -24832 / 14175.0}},
+    {2, {-734 / 315.0, 109598 / 31185.0}},
+    {1, {444337 / 155925.0}}};
+static const or_poly OR_UTG[6] = {
+    {6, {-0.5, 2 / 3.0, -37 / 96.0, 1 / 360.0, 81 / 512.0, -96199 / 604800.0}},
+    {5, {-1 / 48.0, -1 / 15.0, 437 / 1440.0, -46 / 105.0, 1118711 / 3870720.0}},
+    {4, {-17 / 480.0, 37 / 840.0, 209 / 4480.0, -5569 / 90720.0}},
+    {3, {-4397 / 161280.0, 11 / 504.0, 830251 / 7257600.0}},
+    {2, {-4583 / 161280.0, 108847 / 3991680.0}},
+    {1, {-20648693 / 638668800.0}}};
+static const or_poly OR_GTU[6] = {
+    {6, {0.5, -2 / 3.0, 5 / 16.0, 41 / 180.0, -127 / 288.0, 7891 / 37800.0}},
+    {5, {13 / 48.0, -3 / 5.0, 557 / 1440.0, 281 / 630.0, -1983433 / 1935360.0}},
+    {4, {61 / 240.0, -103 / 140.0, 15061 / 26880.0, 167603 / 181440.0}},
+    {3, {49561 / 161280.0, -179 / 168.0, 6601661 / 7257600.0}},
+    {2, {34729 / 80640.0, -3418889 / 1995840.0}},
+    {1, {212378941 / 319334400.0}}};
+
+/* n^(k+1) * poly in the nesting order of setup_exact (innermost first). */
+static void or_series(const or_poly *P, double n, double *out, int utg_gtu) {
+    double np = n;
+    for (int k = 0; k < 6; k++) {
+        /* setup_exact's powers: cgb / cbg step np by n each k; utg / gtu use
+         * n (k = 0), then n^2 for k = 0..1's second term onwards */
+        if (utg_gtu) np = k == 0 ? n : k == 1 ? n * n : np * n;
+        else if (k > 0) np *= n;
+        double h = P[k].c[P[k].len - 1];
+        for (int j = P[k].len - 2; j >= 0; j--) h = P[k].c[j] + n * h;
+        out[k] = np * h;
+    }
+}
+
+static double or_gatg(const double *p1, int len, double B) {
+    double h = 0, h1, h2 = 0, cos_2B = 2 * cos(2 * B);
+    const double *p = p1 + len;
+    h1 = *--p;
+    while (p - p1) { h = -h2 + cos_2B * h1 + *--p; h2 = h1; h1 = h; }
+    return B + h * sin(2 * B);
+}
+
+static double or_clens(const double *a, int size, double arg_r) {
+    const double *p = a + size;
+    double r = 2 * cos(arg_r), hr1 = 0, hr = *--p, hr2;
+    while (a - p) { hr2 = hr1; hr1 = hr; hr = -hr2 + r * hr1 + *--p; }
+    return sin(arg_r) * hr;
+}
+
+static void or_clenS(const double *a, int size, double ar, double ai, double *R, double *I) {
+    const double *p = a + size;
+    double sr = sin(ar), cr = cos(ar), sh = sinh(ai), ch = cosh(ai);
+    double r = 2 * cr * ch, i = -2 * sr * sh;
+    double hr = *--p, hi = 0, hr1 = 0, hi1 = 0, hr2, hi2;
+    while (a - p) {
+        hr2 = hr1; hi2 = hi1; hr1 = hr; hi1 = hi;
+        hr = -hr2 + r * hr1 - i * hi1 + *--p;
+        hi = -hi2 + i * hr1 + r * hi1;
+    }
+    r = sr * ch; i = cr * sh;
+    *R = r * hr - i * hi;
+    *I = r * hi + i * hr;
+}
+
+static int tmerc_setup(oracle_crs *c) {
+    if (!(c->es > 0)) return -1;
+    c->kind = OR_CRS_TMERC;
+    double f = c->es / (1 + sqrt(1 - c->es));
+    double n = f / (2 - f);
+    or_series(OR_CGB, n, c->tm_cgb, 0);
+    or_series(OR_CBG, n, c->tm_cbg, 0);
+    or_series(OR_UTG, n, c->tm_utg, 1);
+    or_series(OR_GTU, n, c->tm_gtu, 1);
+    double n2 = n * n;
+    c->tm_qn = c->k0 / (1 + n) * (1 + n2 * (1 / 4.0 + n2 * (1 / 64.0 + n2 / 256.0)));
+    double Z = or_gatg(c->tm_cbg, 6, c->phi0);
+    c->tm_zb = -c->tm_qn * (Z + or_clens(c->tm_gtu, 6, 2 * Z));
+    return 0;
+}
+
+static int utm_setup(oracle_crs *c, int zone, int south) {   /* utm.cpp */
+    if (zone < 1 || zone > 60) return -1;
+    c->lam0 = (zone - .5) * OR_PI / 30. - OR_PI;
+    c->phi0 = 0; c->k0 = 0.9996; c->x0 = 500000; c->y0 = south ? 10000000 : 0;
+    return tmerc_setup(c);
+}
+
 static double param_of(const char *s, const char *key, double dflt, int *found) {
     const char *p = s;
     size_t kl = strlen(key);
@@ -697,6 +802,14 @@ int oracle_crs_init(oracle_crs *c, const char *spec) {
     if (!strcasecmp(spec, "SR-ORG:6842") || !strcasecmp(spec, "MODIS")) {
         c->kind = OR_CRS_SINU; set_ellps(c, 6371007.181, 0.0); return 0;
     }
+    if (!strcasecmp(spec, "EPSG:4283")) { c->kind = OR_CRS_LONGLAT; set_ellps(c, 6378137.0, 298.257222101); return 0; }
+    if (!strncasecmp(spec, "EPSG:", 5)) {      /* UTM / MGA zones */
+        int code = atoi(spec + 5);
+        if (code > 32600 && code <= 32660) { set_ellps(c, 6378137.0, 298.257223563); return utm_setup(c, code - 32600, 0); }
+        if (code > 32700 && code <= 32760) { set_ellps(c, 6378137.0, 298.257223563); return utm_setup(c, code - 32700, 1); }
+        if (code >= 28348 && code <= 28358) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 28300, 1); }
+        if (code >= 7846 && code <= 7859) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 7800, 1); }
+    }
     if (strstr(spec, "+proj=")) {
         int f = 0;
         double a = param_of(spec, "+a", 0, &f);
@@ -725,6 +838,20 @@ int oracle_crs_init(oracle_crs *c, const char *spec) {
             return aea_setup(c);
         }
         if (strstr(spec, "+proj=sinu")) { c->kind = OR_CRS_SINU; set_ellps(c, a, rf == 0 ? 0 : rf); if (c->es != 0) return -1; return 0; }
+        if (strstr(spec, "+proj=utm")) {
+            int fz = 0;
+            double zone = param_of(spec, "+zone", 0, &fz);
+            set_ellps(c, a, rf);
+            if (!fz || zone != floor(zone)) return -1;
+            return utm_setup(c, (int)zone, strstr(spec, "+south") != NULL);
+        }
+        if ((strstr(spec, "+proj=tmerc") || strstr(spec, "+proj=etmerc")) && !strstr(spec, "+approx")) {
+            int fk = 0;
+            set_ellps(c, a, rf);
+            c->k0 = param_of(spec, "+k_0", 1.0, &fk);
+            if (!fk) c->k0 = param_of(spec, "+k", 1.0, NULL);
+            return tmerc_setup(c);
+        }
     }
     return -1;
 }
@@ -776,6 +903,20 @@ static int crs_inverse(const oracle_crs *c, double x, double y, double *lam, dou
         p = yn;
         l = xn / cos(yn);
         break;
+    case OR_CRS_TMERC: {                        /* tmerc.cpp exact_e_inv */
+        double Cn = (yn - c->tm_zb) / c->tm_qn, Ce = xn / c->tm_qn, dCn, dCe;
+        if (!(fabs(Ce) <= 2.623395162778)) return 0;   /* 150 degrees */
+        or_clenS(c->tm_utg, 6, 2 * Cn, 2 * Ce, &dCn, &dCe);
+        Cn += dCn;
+        Ce += dCe;
+        Ce = atan(sinh(Ce));
+        double sCn = sin(Cn), cCn = cos(Cn), sCe = sin(Ce), cCe = cos(Ce);
+        Ce = atan2(sCe, cCe * cCn);
+        Cn = atan2(sCn * cCe, hypot(sCe, cCe * cCn));
+        p = or_gatg(c->tm_cgb, 6, Cn);
+        l = Ce;
+        break;
+    }
     default:
         return 0;
     }
@@ -818,6 +959,20 @@ static int crs_forward(const oracle_crs *c, double lam, double phi, double *x, d
         xn = lam * cos(phi);
         yn = phi;
         break;
+    case OR_CRS_TMERC: {                        /* tmerc.cpp exact_e_fwd */
+        double Cn = or_gatg(c->tm_cbg, 6, phi), dCn, dCe;
+        double sCn = sin(Cn), cCn = cos(Cn), sCe = sin(lam), cCe = cos(lam);
+        Cn = atan2(sCn, cCe * cCn);
+        double Ce = atan2(sCe * cCn, hypot(sCn, cCn * cCe));
+        Ce = asinh(tan(Ce));
+        or_clenS(c->tm_gtu, 6, 2 * Cn, 2 * Ce, &dCn, &dCe);
+        Cn += dCn;
+        Ce += dCe;
+        if (!(fabs(Ce) <= 2.623395162778)) return 0;
+        yn = c->tm_qn * Cn + c->tm_zb;
+        xn = c->tm_qn * Ce;
+        break;
+    }
     default:
         return 0;
     }

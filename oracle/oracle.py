@@ -33,7 +33,9 @@ def build(force: bool = False) -> str:
 class Crs(C.Structure):
     _fields_ = [("kind", C.c_int32), ("_pad", C.c_int32)] + [
         (n, C.c_double) for n in ("a", "ra", "es", "e", "one_es", "lam0", "phi0", "phi1",
-                                  "phi2", "x0", "y0", "k0", "n", "c", "dd", "rho0", "ec")]
+                                  "phi2", "x0", "y0", "k0", "n", "c", "dd", "rho0", "ec",
+                                  "tm_qn", "tm_zb")] + [
+        (n, C.c_double * 6) for n in ("tm_cgb", "tm_cbg", "tm_utg", "tm_gtu")]
 
 
 class Granule(C.Structure):

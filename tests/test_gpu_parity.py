@@ -237,6 +237,58 @@ def test_warp_windows_bilinear_c3_small(gpu, oracle):
     assert frac >= NN_IDENTITY
 
 
+def test_warp_windows_utm_small(gpu, oracle):
+    """GDA94 / MGA zone 55 (Transverse Mercator) granules -> EPSG:3857."""
+    cfg = synth.config_utm(scale=0.05, tiles_per_side=4, tile_px=128)
+    frac = _check_windows(oracle, cfg, gpu_batch(cfg))
+    assert frac >= NN_IDENTITY
+
+
+def test_render_utm_small(gpu, oracle):
+    import gsky_amd
+    cfg = synth.config_utm(scale=0.1, tiles_per_side=4, tile_px=256)
+    b = gpu_batch(cfg)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True)).cpu().numpy()
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg)
+    assert identity(got, exp) >= NN_IDENTITY
+    assert (exp[..., 3] > 0).mean() > 0.3
+
+
+def test_warp_operation_fast_utm_dropin(gpu, oracle):
+    """warp.go:82 for a UTM granule given as WKT (the source SRS a GDAL
+    dataset reports), to EPSG:3857 and to another MGA zone."""
+    import torch
+
+    from gsky_amd import worker
+    from gsky_amd.tiles import bbox_to_geot
+    cfg = synth.config_utm(scale=0.1, tiles_per_side=4, tile_px=256)
+    g = cfg.granules[0]
+    wkt = ('PROJCS["GDA94 / MGA zone 55",GEOGCS["GDA94",DATUM["Geocentric_Datum_of_Australia_1994",'
+           'SPHEROID["GRS 1980",6378137,298.257222101]],PRIMEM["Greenwich",0],UNIT["degree",0.0174532925199433]],'
+           'PROJECTION["Transverse_Mercator"],PARAMETER["latitude_of_origin",0],PARAMETER["central_meridian",147],'
+           'PARAMETER["scale_factor",0.9996],PARAMETER["false_easting",500000],'
+           'PARAMETER["false_northing",10000000],UNIT["metre",1]]')
+    worker.register_granule("/g/data/utm/g0.tif", 1, torch.from_numpy(g.data).to(gpu), g.geot, wkt, g.nodata,
+                            block=(128, 64))
+    try:
+        og = oracle.make_granule(g.data, g.geot, g.nodata, block=(128, 64))
+        bb, w, h = cfg.tiles[5]
+        for dst, dst_gt in (("EPSG:3857", bbox_to_geot(w, h, bb)),
+                            ("EPSG:28354", [830000.0, 40.0, 0.0, 5880000.0, 0.0, -40.0])):
+            res = worker.warp_raster(worker.GeoRPCGranule(path="/g/data/utm/g0.tif", bands=[1], width=w, height=h,
+                                                          dstSRS=dst, dstGeot=dst_gt))
+            assert res.error == "OK", (dst, res.error)
+            arr, bbox, nd, dt = oracle.warp(og, oracle.crs("EPSG:28355"), oracle.crs(dst), dst_gt, w, h)
+            assert res.raster.bbox == list(bbox), (dst, res.raster.bbox, bbox)
+            got = worker.raster_array(res.raster)
+            assert identity(got, arr) >= NN_IDENTITY, dst
+            assert (got != g.nodata).mean() > 0.3, dst
+            assert res.bytesRead == oracle.warp.bytes_read > 0
+    finally:
+        worker.unregister_all()
+
+
 def test_render_c1(gpu, oracle):
     import gsky_amd
     cfg = synth.config_c1(scale=1.0)
