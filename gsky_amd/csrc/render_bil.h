@@ -170,7 +170,11 @@ __global__ __launch_bounds__(256, WPS) void render_bil_sep_kernel(RenderArgs a, 
                                                                 const TilePlan *__restrict__ tplans,
                                                                 const gskyhip_tile *__restrict__ tiles, int n_items) {
   constexpr int kRowsBlk = 4 * RPW;
-  const int item = blockIdx.x;
+  int item = blockIdx.x;
+  if (a.ab_xcd == 2) {   // A/B: XCD x (blockIdx % 8) takes the x-th contiguous eighth of the items
+    const int per = (n_items + 7) >> 3;
+    item = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  }
   if (item >= n_items) return;
   const int bands_per_tile = (a.max_h + kRowsBlk - 1) / kRowsBlk;
   const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
@@ -653,7 +657,8 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
 template <typename WT, int RPW, int HP, int WPS, bool FIX = true, bool SEP = true, int SHP = 4, int SWPS = 8>
 void launch_bil_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_bil_kernel<WT, RPW, HP, WPS, FIX, SEP>), dim3((unsigned)items), dim3(256), 0, s, a,
+  const int grid = a.ab_xcd == 2 ? (items + 7) / 8 * 8 : items;
+  hipLaunchKernelGGL((render_bil_kernel<WT, RPW, HP, WPS, FIX, SEP>), dim3((unsigned)grid), dim3(256), 0, s, a,
                      a.entries, a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
   if (SEP)
     hipLaunchKernelGGL((render_bil_sep_kernel<WT, RPW, SHP, SWPS>), dim3((unsigned)items), dim3(256), 0, s, a,

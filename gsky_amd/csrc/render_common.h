@@ -215,7 +215,8 @@ struct RenderArgs {
   int st_pol;                  // A/B build only: RGBA store cache policy (0 nt, 1 sc1, 2 sc0 sc1, 3 plain)
   int ab_mode;                 // A/B build only: 1 skip the NN gathers, 2 skip the RGBA stores
   int ab_vfetch;               // A/B build only: 0 = per-row scalar RowFix fetch in the NN kernel
-  int ab_xcd;                  // A/B build only: 1 = a tile's blocks on one XCD (NN kernel item order)
+  int ab_xcd;                  // A/B build only: item order over the XCDs (1: a tile's blocks on one XCD, NN;
+                               //   2: XCD x the x-th contiguous eighth of the items, NN and bilinear)
   int nn_colg;                 // A/B build only: NN single-entry blocks in column-group-major order
 };
 

@@ -440,10 +440,13 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
   int item = blockIdx.x;
 #ifdef GSKYHIP_AB
-  if (a.ab_xcd) {   // A/B: every block of a tile on one XCD (blockIdx % 8), tiles dealt round-robin over the XCDs
+  if (a.ab_xcd == 1) {   // A/B: every block of a tile on one XCD (blockIdx % 8), tiles dealt round-robin over the XCDs
     const int per = bands_per_tile * col_blocks;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
     item = ((slot / per) * 8 + xcd) * per + slot % per;
+  } else if (a.ab_xcd == 2) {   // A/B: XCD x takes the x-th contiguous eighth of the items (a strip of tiles)
+    const int per = (n_items + 7) >> 3;
+    item = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
   }
 #endif
   if (item >= n_items) return;
@@ -817,7 +820,7 @@ void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
   // the XCD order (A/B) maps blocks over whole groups of 8 tiles: round the grid up
   const int per = ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  const int grid = a.ab_xcd ? (a.n_tiles + 7) / 8 * 8 * per : items;
+  const int grid = a.ab_xcd == 1 ? (a.n_tiles + 7) / 8 * 8 * per : a.ab_xcd == 2 ? (items + 7) / 8 * 8 : items;
   hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE, COOP, WIDE>), dim3((unsigned)grid), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
