@@ -2068,8 +2068,10 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.ab_vfetch = 1;
   a.ab_xcd = 0;
   a.nn_colg = 0;
+  a.nn_pair = 0;
 #ifdef GSKYHIP_AB
   if (const char *cg = getenv("GSKYHIP_NN_COLG")) a.nn_colg = atoi(cg);
+  if (const char *np = getenv("GSKYHIP_NN_PAIR")) a.nn_pair = atoi(np);
   if (const char *sp = getenv("GSKYHIP_NN_STPOL")) a.st_pol = atoi(sp);
   if (const char *am = getenv("GSKYHIP_AB_MODE")) a.ab_mode = atoi(am);
   if (const char *vf = getenv("GSKYHIP_NN_VFETCH")) a.ab_vfetch = atoi(vf);

@@ -28,7 +28,6 @@
 
 namespace gsky {
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // The sample of one pixel whose 2x2 taps are all inside the band (t0: x and
 // x + 1 of the upper source row, t1 of the lower; rx / ry the weights of x

@@ -218,6 +218,7 @@ struct RenderArgs {
   int ab_xcd;                  // A/B build only: item order over the XCDs (1: a tile's blocks on one XCD, NN;
                                //   2: XCD x the x-th contiguous eighth of the items, NN and bilinear)
   int nn_colg;                 // A/B build only: NN single-entry blocks in column-group-major order
+  int nn_pair;                 // A/B build only: NN 16-bit single-entry rows by column pairs
 };
 
 // ---------------------------------------------------------------- typed fast path
@@ -227,6 +228,7 @@ struct RenderArgs {
 // a branch-free ordered fold, the scale and the palette lookup.
 #define GPTR(T) __attribute__((address_space(1))) T *
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <typename T> struct VOf { using type = int32_t; };
 template <> struct VOf<float> { using type = float; };
 

@@ -173,6 +173,61 @@ __device__ __forceinline__ bool nn_fix_row(__amdgpu_buffer_rsrc_t rs, int64_t fx
   return true;
 }
 
+// nn_fix_row's cover case for 2-byte T with a lane owning column PAIRS
+// (A/B, GSKYHIP_NN_PAIR=1): the lane's pixels are columns icp + 128 q + k
+// (k = 0, 1) -> c[2 q + k], so one aligned dword gather serves both pixels of
+// a pair whenever their source pixels share it (C2: ~70 % of pairs; the
+// rest take a second, lane-masked gather) and the RGBA leaves as 8-byte
+// stores: half the 64-lane gather and store instructions, whose per-quad L1
+// work bounds the row-major body.  Same fixed-point values,
+// margin test and fold as nn_fix_row: the same result bit for bit.
+template <typename T, int NPX>
+__device__ __forceinline__ bool nn_fix_row_pair(__amdgpu_buffer_rsrc_t rs, int64_t fx0, int64_t fy0, int64_t fdx,
+                                                int64_t fdy, int icp, int bx, typename VOf<T>::type nd,
+                                                bool fill_mode, typename VOf<T>::type (&c)[NPX]) {
+  static_assert(sizeof(T) == 2 && NPX % 2 == 0, "pairs of 16-bit pixels");
+  using V = typename VOf<T>::type;
+  constexpr int NQ = NPX / 2;
+  uint64_t X = (uint64_t)(fx0 + (int64_t)icp * fdx), Y = (uint64_t)(fy0 + (int64_t)icp * fdy);
+  const uint64_t SX = (uint64_t)fdx << 7, SY = (uint64_t)fdy << 7;   // 128 columns
+  uint32_t amin = 0xFFFFFFFFu;
+  uint32_t e0[NQ], e1[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; q++) {
+    const uint64_t X1 = X + (uint64_t)fdx, Y1 = Y + (uint64_t)fdy;
+    e0[q] = __umul24((uint32_t)(Y >> 32), (uint32_t)bx) + (uint32_t)(X >> 32);
+    e1[q] = __umul24((uint32_t)(Y1 >> 32), (uint32_t)bx) + (uint32_t)(X1 >> 32);
+    amin = min(amin, min(min((uint32_t)X + kFixMargin, (uint32_t)Y + kFixMargin),
+                         min((uint32_t)X1 + kFixMargin, (uint32_t)Y1 + kFixMargin)));
+    asm volatile("" : "+v"(e0[q]), "+v"(e1[q]));
+    X += SX;
+    Y += SY;
+  }
+  if (__builtin_amdgcn_ballot_w64(amin < 2u * kFixMargin) != 0) return false;
+  uint32_t w0[NQ], w1[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; q++) w0[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (e0[q] * 2u) & ~3u, 0, 0);
+#pragma unroll
+  for (int q = 0; q < NQ; q++) {
+    w1[q] = w0[q];
+    if ((e1[q] ^ e0[q]) > 1u) w1[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (e1[q] * 2u) & ~3u, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; q++) {
+    const uint32_t h0 = (w0[q] >> ((e0[q] & 1u) * 16u)) & 0xFFFFu, h1 = (w1[q] >> ((e1[q] & 1u) * 16u)) & 0xFFFFu;
+    const V v0 = std::is_signed<T>::value ? (V)(int16_t)h0 : (V)h0;
+    const V v1 = std::is_signed<T>::value ? (V)(int16_t)h1 : (V)h1;
+    if (!fill_mode) {
+      c[2 * q] = v0 != nd ? v0 : c[2 * q];
+      c[2 * q + 1] = v1 != nd ? v1 : c[2 * q + 1];
+    } else {
+      c[2 * q] = c[2 * q] == nd ? v0 : c[2 * q];
+      c[2 * q + 1] = c[2 * q + 1] == nd ? v1 : c[2 * q + 1];
+    }
+  }
+  return true;
+}
+
 // The fold of one `inside` LINEAR row covering the block (nn_fix_row's cover
 // case) with cooperative loads instead of per-lane gathers: for each of the
 // lane's 8 pixels the wave's 64 consecutive output columns read a source run
@@ -583,11 +638,16 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
       const V nd = as_v<T>(ndv);
       const bool fill_mode = e1_fill != 0;
       const int ic0 = xl - exoff;
-      // WIDE: the band's last dword whole (buf_load_w)
+      bool pair_on = false;   // A/B: nn_fix_row_pair (column pairs, 8-byte stores)
+#ifdef GSKYHIP_AB
+      pair_on = a.nn_pair != 0 && (a.max_w & 1) == 0;
+#endif
+      // WIDE / pairs: the band's last dword whole (buf_load_w; a dword never
+      // straddles a page)
       const int64_t band_bytes = (int64_t)bx * by * (int64_t)sizeof(T);
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)uniform_ptr(e1_band), (short)0, (int)(WIDE ? (band_bytes + 3) & ~(int64_t)3 : band_bytes),
-          0x00020000);
+          (void *)uniform_ptr(e1_band), (short)0,
+          (int)((WIDE || pair_on) ? (band_bytes + 3) & ~(int64_t)3 : band_bytes), 0x00020000);
       const RowFix *fbase = rowfix + e1_row_base;
       // the row's fixed-point form, or fk = -1 outside the window / 0 none
       auto fetch = [&](int ir, int64_t (&f)[4], int &fk) {
@@ -650,6 +710,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 #pragma unroll
           for (int q = 0; q < kNnPx; q++) c[q] = cnod;
           bool done = cfk < 0;
+          bool paired = false;
 #ifdef GSKYHIP_AB
           if (a.ab_mode == 1) done = true;   // A/B: no gathers
           else if (a.ab_mode == 8 && cfk == 1) {
@@ -668,7 +729,15 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
           } else
 #endif
           if (cfk == 1) {
-            if constexpr (CF)
+            if constexpr (CF && sizeof(T) == 2 && !WIDE) {
+              if (pair_on) {
+                done = nn_fix_row_pair<T, kNnPx>(rs, cf[0], cf[1], cf[2], cf[3], ic0 + lane, bx, nd, fill_mode, c);
+                paired = true;
+              } else {
+                done = nn_fix_row<T, kNnPx, false, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode,
+                                                         c);
+              }
+            } else if constexpr (CF)
               done = nn_fix_row<T, kNnPx, false, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c);
             else
               done = cover ? (COOP ? nn_fix_row_coop<T, kNnPx>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
@@ -681,7 +750,14 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
           if (done) {
             uint32_t px[kNnPx];
             rgba(c, px);
-            store_row(r, px, CF);
+            if (paired) {   // columns 2 lane + 128 q + {0, 1}: 8-byte stores
+              uint32_t *d = rgba_lane - lane + (int64_t)r * a.max_w + 2 * lane;
+#pragma unroll
+              for (int q = 0; q < kNnPx / 2; q++)
+                __builtin_nontemporal_store(u32x2{px[2 * q], px[2 * q + 1]}, (GPTR(u32x2))(d + 128 * q));
+            } else {
+              store_row(r, px, CF);
+            }
           } else {
             redo |= 1u << j;
           }
