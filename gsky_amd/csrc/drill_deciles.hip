@@ -763,7 +763,7 @@ int launch_decile_select_fused(const float *vals, const int32_t *chunk_base, con
   int nt = kSelThreads;
   bool vec = false;
 #ifdef GSKYHIP_AB
-  if (const char *e = getenv("GSKYHIP_DEC_FNT")) nt = atoi(e);   // fused select workgroup: 256 / 512 / 1024 threads
+  if (const char *e = getenv("GSKYHIP_DEC_FNT")) nt = atoi(e);   // fused select workgroup: 128 / 256 / 512 / 1024 threads
   if (const char *e = getenv("GSKYHIP_DEC_VEC")) vec = atoi(e) != 0;   // 16-byte segment loads, merged bucket runs
 #endif
   const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
@@ -774,6 +774,10 @@ int launch_decile_select_fused(const float *vals, const int32_t *chunk_base, con
   else if (nt == 512)
     hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 512, 8>), dim3((unsigned)n_seg),
                        dim3(512), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
+                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
+  else if (nt == 128)
+    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 128, 8>), dim3((unsigned)n_seg),
+                       dim3(128), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
                        decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
   else if (vec && getenv("GSKYHIP_DEC_U") && atoi(getenv("GSKYHIP_DEC_U")) == 16)
     hipLaunchKernelGGL((decile_select_kernel<16, false, kSelThreads, kSelWpe, true>), dim3((unsigned)n_seg),

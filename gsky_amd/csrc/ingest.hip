@@ -1083,6 +1083,20 @@ std::string nc_cf_srs(const Nc &f, const NcVar &v) {
                       num(m, "longitude_of_central_meridian", 0, 0), fe, fn, ell);
         return buf;
       }
+      if (name == "transverse_mercator" && !sphere) {   // ellipsoidal only (as the warp's tmerc)
+        const double k0 = num(m, "scale_factor_at_central_meridian", 0, 1.0);
+        const double cm = num(m, "longitude_of_central_meridian", 0, 0);
+        const double lat0 = num(m, "latitude_of_projection_origin", 0, 0);
+        // a UTM zone's parameters: +proj=utm, as PROJ 6 exports the conversion
+        const double zone = (cm + 183.0) / 6.0;
+        if (lat0 == 0 && k0 == 0.9996 && fe == 500000.0 && (fn == 0 || fn == 10000000.0) && zone == std::floor(zone) &&
+            zone >= 1 && zone <= 60)
+          std::snprintf(buf, sizeof(buf), "+proj=utm +zone=%d%s %s", (int)zone, fn != 0 ? " +south" : "", ell);
+        else
+          std::snprintf(buf, sizeof(buf), "+proj=tmerc +lat_0=%.17g +lon_0=%.17g +k_0=%.17g +x_0=%.17g +y_0=%.17g %s",
+                        lat0, cm, k0, fe, fn, ell);
+        return buf;
+      }
       if (name == "sinusoidal" && sphere) {
         std::snprintf(buf, sizeof(buf), "+proj=sinu +lon_0=%.17g +x_0=%.17g +y_0=%.17g %s",
                       num(m, "longitude_of_central_meridian", 0, num(m, "longitude_of_projection_origin", 0, 0)),

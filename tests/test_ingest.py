@@ -445,6 +445,12 @@ ALBERS_CF = {"grid_mapping_name": "albers_conical_equal_area", "standard_paralle
              "semi_major_axis": np.array([6378137.0]), "inverse_flattening": np.array([298.257222101])}
 
 
+UTM55_CF = {"grid_mapping_name": "transverse_mercator", "scale_factor_at_central_meridian": np.array([0.9996]),
+            "longitude_of_central_meridian": np.array([147.0]), "latitude_of_projection_origin": np.array([0.0]),
+            "false_easting": np.array([500000.0]), "false_northing": np.array([10000000.0]),
+            "semi_major_axis": np.array([6378137.0]), "inverse_flattening": np.array([298.257222101])}
+
+
 def test_netcdf_srs_cf_option(tmp_path):
     """srs_cf (warp.go:95 -> netcdfdataset.cpp:7023-7025, 3666): without it
     the GDAL WKT's EPSG code wins; with it only the CF grid mapping counts.
@@ -474,6 +480,17 @@ def test_netcdf_srs_cf_option(tmp_path):
     p5 = str(tmp_path / "e.nc")
     _write_nc(p5, "v", data, np.arange(5.0), np.arange(4.0))
     assert ingest.netcdf_srs(p5, 0) == ingest.netcdf_srs(p5, 1) == "EPSG:4326"
+    # transverse_mercator: a UTM zone's parameters as +proj=utm, others as tmerc
+    p6 = str(tmp_path / "f.nc")
+    _write_albers_nc(p6, data, x, y, cf=UTM55_CF)
+    assert ingest.netcdf_srs(p6, 1) == "+proj=utm +zone=55 +south +a=6378137 +rf=298.25722210100002"
+    p7 = str(tmp_path / "g.nc")
+    _write_albers_nc(p7, data, x, y, cf=dict(UTM55_CF, scale_factor_at_central_meridian=np.array([0.99994]),
+                                             false_northing=np.array([5000000.0])))
+    s7 = ingest.netcdf_srs(p7, 1)
+    assert s7.startswith("+proj=tmerc +lat_0=0 +lon_0=147 +k_0=0.99994") and "+y_0=5000000 " in s7
+    from gsky_amd.tiles import parse_crs
+    assert parse_crs(s7).kind == 4 and parse_crs(ingest.netcdf_srs(p6, 1)).kind == 4
 
 
 @pytest.mark.gpu
@@ -524,6 +541,44 @@ def test_gpu_netcdf_srs_cf_drop_in(tmp_path):
     assert ok.error == "OK" and bad.error.startswith("warp_operation() fail: -"), (ok.error, bad.error)
     worker.unregister_all()
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_gpu_netcdf_cf_transverse_mercator(tmp_path):
+    """A netCDF granule in GDA94 / MGA zone 55 known only by its CF
+    transverse_mercator grid mapping warps to EPSG:3857 bit-identically to
+    the oracle through EPSG:28355."""
+    import torch
+
+    from gsky_amd import worker
+    from gsky_amd.tiles import bbox_to_geot
+    from oracle import oracle as O
+    rng = np.random.default_rng(22)
+    ny, nx = 300, 400
+    data = rng.integers(0, 10000, (ny, nx)).astype(np.int16)
+    x = 300012.5 + 25.0 * np.arange(nx)
+    y = 5850000.0 - 12.5 - 25.0 * np.arange(ny)
+    p = str(tmp_path / "utm.nc")
+    _write_albers_nc(p, data, x, y, cf=UTM55_CF)
+    gt = (300000.0, 25.0, 0.0, 5850000.0, 0.0, -25.0)
+    g = O.make_granule(data, gt, -999.0)
+    wm = O.crs("EPSG:3857")
+    x0, y0 = O.crs_transform(O.crs("EPSG:28355"), wm, 301000.0, 5843000.0)
+    x1, y1 = O.crs_transform(O.crs("EPSG:28355"), wm, 309000.0, 5849000.0)
+    dgt = bbox_to_geot(256, 256, (x0, y0, x1, y1))
+    worker.unregister_all()
+    try:
+        r = worker.warp_raster(worker.GeoRPCGranule(path=p, bands=[1], width=256, height=256, dstSRS="EPSG:3857",
+                                                    dstGeot=dgt, sRSCf=1))
+        assert r.error == "OK", r.error
+        exp, ebbox, end, edt = O.warp(g, O.crs("EPSG:28355"), wm, dgt, 256, 256)
+        got = worker.raster_array(r.raster)
+        assert list(r.raster.bbox) == list(ebbox)
+        assert np.array_equal(got, exp), int((got != exp).sum())
+        assert (got != -999).mean() > 0.5
+    finally:
+        worker.unregister_all()
+        torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("dt,exp", [(np.int16, -32767.0), (np.int32, -2147483647.0),
