@@ -2070,6 +2070,8 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.nn_colg = 0;
   a.nn_pair = 0;
 #ifdef GSKYHIP_AB
+  a.nn_maskb = 0;
+  if (const char *mb = getenv("GSKYHIP_NN_MASKB")) a.nn_maskb = atoi(mb);
   if (const char *cg = getenv("GSKYHIP_NN_COLG")) a.nn_colg = atoi(cg);
   if (const char *np = getenv("GSKYHIP_NN_PAIR")) a.nn_pair = atoi(np);
   if (const char *sp = getenv("GSKYHIP_NN_STPOL")) a.st_pol = atoi(sp);

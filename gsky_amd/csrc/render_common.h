@@ -219,6 +219,9 @@ struct RenderArgs {
                                //   2: XCD x the x-th contiguous eighth of the items, NN and bilinear)
   int nn_colg;                 // A/B build only: NN single-entry blocks in column-group-major order
   int nn_pair;                 // A/B build only: NN 16-bit single-entry rows by column pairs
+#ifdef GSKYHIP_AB
+  int nn_maskb;                // A/B build only: NN entries with a mask layer, all data + mask gathers at once
+#endif
 };
 
 // ---------------------------------------------------------------- typed fast path

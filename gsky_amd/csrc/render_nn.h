@@ -312,6 +312,111 @@ __device__ __forceinline__ bool nn_fix_row_coop(__amdgpu_buffer_rsrc_t rs, int64
   return true;
 }
 
+// A/B (GSKYHIP_NN_MASKB=1; 0.526 vs 0.494 ms on C5, profiles/r05o_c5.jsonl):
+// the general body for an entry carrying a mask layer (C5's QA stacks), all
+// NPX pixels at once: every data index and every mask index first, then all
+// 2 x NPX gathers in flight together, then the fold -- mask_fast() per pixel
+// inside the fold chained the mask entry's descriptor, row record and gather
+// behind each taken pixel (4 dependent memory latencies per half row).  The
+// same expressions as the general body + mask_fast(): the same result.
+template <typename T, int NPX>
+__device__ __forceinline__ void nn_masked_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
+                                              const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
+                                              __amdgpu_buffer_rsrc_t rs, const RowRec *rr, int kind, int ic0, int lim,
+                                              int bx, int by, typename VOf<T>::type nd, bool fill_mode, int ir,
+                                              typename VOf<T>::type (&c)[NPX]) {
+  using V = typename VOf<T>::type;
+  constexpr uint32_t kMaskOff = 0xFFFFFFFEu;   // mask row past the mask's height: not masked
+  const EntryD &m = ents[e.mask_pair];
+  const int ew = e.w, mw = m.w, mh = m.h, mbx = m.band_x, mby = m.band_y, mdt = m.out_dtype;
+  const int msz = type_size(mdt);
+  const int slot = mask_slot(mdt);
+  const int32_t mfill = m.fill.i;
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)uniform_ptr(m.band), (short)0, (int)((int64_t)mbx * mby * (int64_t)msz), 0x00020000);
+  uint32_t idx[NPX], midx[NPX];
+  if (kind == ROW_LINEAR) {
+    const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
+#pragma unroll
+    for (int q = 0; q < NPX; q++) {
+      const int ic = ic0 + 64 * q;
+      const double dist = (double)ic;
+      idx[q] = nn_index_sxy(xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, bx, by);
+    }
+  } else {   // POOL: the leaf of each pixel
+    const int nleaf = __builtin_amdgcn_readfirstlane(rr->nleaf);
+    const Leaf *lv = pool + __builtin_amdgcn_readfirstlane(rr->pool_off);
+#pragma unroll 1
+    for (int q = 0; q < NPX; q++) {
+      const int ic = ic0 + 64 * q;
+      const bool in = (unsigned)ic < (unsigned)lim;
+      const Leaf &L = lv[leaf_of(lv, nleaf, in ? ic : 0)];
+      const double dist = (double)(ic - L.start);
+      idx[q] = nn_index_sxy(L.xs0 + L.dX * dist, L.ys0 + L.dY * dist, in && L.kind != LEAF_FAILED, bx, by);
+    }
+  }
+  // mask_fast(): the mask window index of data pixel (ic, ir) -- the same
+  // index when the widths agree, else through the row-major data index
+  if (mw == ew) {
+    if (ir >= mh) {
+#pragma unroll
+      for (int q = 0; q < NPX; q++) midx[q] = kMaskOff;
+    } else {
+      const RowRec *mr = rows + m.row_base + ir;
+#pragma unroll
+      for (int q = 0; q < NPX; q++) {
+        const int ic = ic0 + 64 * q;
+        double sx, sy;
+        const bool ok = lin_coords(*mr, pool, (unsigned)ic < (unsigned)lim ? ic : 0, sx, sy);
+        midx[q] = ok ? nn_index_sxy(sx, sy, true, mbx, mby) : kNoPx;
+      }
+    }
+  } else {
+#pragma unroll 1
+    for (int q = 0; q < NPX; q++) {
+      const int ic = ic0 + 64 * q;
+      midx[q] = kMaskOff;
+      if ((unsigned)ic < (unsigned)lim) {
+        const long iSrc = (long)ir * ew + ic;
+        const int mx = (int)(iSrc % mw), my = (int)(iSrc / mw);
+        if (my < mh) {
+          double sx, sy;
+          midx[q] = lin_coords(rows[m.row_base + my], pool, mx, sx, sy) ? nn_index_sxy(sx, sy, true, mbx, mby) : kNoPx;
+        }
+      }
+    }
+  }
+  V vv[NPX];
+  uint32_t mraw[NPX];
+#pragma unroll
+  for (int q = 0; q < NPX; q++) vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
+  if (msz == 1) {
+#pragma unroll
+    for (int q = 0; q < NPX; q++) mraw[q] = __builtin_amdgcn_raw_buffer_load_b8(mrs, midx[q], 0, 0);
+  } else {
+#pragma unroll
+    for (int q = 0; q < NPX; q++) mraw[q] = __builtin_amdgcn_raw_buffer_load_b16(mrs, midx[q] * 2u, 0, 0);
+  }
+  const V fillv = as_v<T>(e.fill);
+#pragma unroll
+  for (int q = 0; q < NPX; q++) {
+    const int ic = ic0 + 64 * q;
+    const V v = idx[q] != kNoPx ? vv[q] : fillv;
+    int32_t mv;
+    switch (mdt) {   // nn_fetch<mask type>'s value
+      case GSKYHIP_SIGNEDBYTE: mv = (int32_t)(int8_t)(uint8_t)mraw[q]; break;
+      case GSKYHIP_INT16: mv = (int32_t)(int16_t)(uint16_t)mraw[q]; break;
+      case GSKYHIP_BYTE: mv = (int32_t)(uint8_t)mraw[q]; break;
+      default: mv = (int32_t)(uint16_t)mraw[q]; break;
+    }
+    if (midx[q] == kNoPx) mv = mfill;
+    const bool mk = midx[q] != kMaskOff && slot >= 0 && mask_bit(a.mask[slot], mdt, mv);
+    const bool take = (unsigned)ic < (unsigned)lim && (v != nd) && !mk;
+    const bool t2 = take && (!fill_mode || c[q] == nd);
+    c[q] = t2 ? v : c[q];
+  }
+}
+
 // One stack entry e of the ordered fold of tile row r (MergeMaskedRaster,
 // tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
 // (tile column xl + 64 q).
@@ -384,6 +489,14 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
     nn_partial_row<T, NPX>(rs, rr->v[0], rr->v[1], rr->v[2], rr->v[3], ic0, lim, bx, nd, fill_mode, c0, c1, c);
     return;
   }
+#ifdef GSKYHIP_AB
+  if constexpr (MASK) {
+    if (masked && a.nn_maskb) {   // A/B (GSKYHIP_NN_MASKB=1): measured slower on C5, 0.526 vs 0.494 ms
+      nn_masked_row<T, NPX>(a, ents, e, rows, pool, rs, rr, kind, ic0, lim, bx, by, nd, fill_mode, ir, c);
+      return;
+    }
+  }
+#endif
   // general body: POOL rows, rows not inside the band, mask layer;
   // two halves of 4 pixels (4 gathers in flight) keep the register peak
   // of the fast body
