@@ -430,12 +430,28 @@ def run_c1(ctx: Ctx, args):
         rg.replay()
         torch.cuda.synchronize()
         gts.append((time.perf_counter() - t0) * 1e3)
+    # the replay alone (the same request again, no descriptor upload): what
+    # the graph costs beside the upload (verdict r4: graph slower than eager)
+    rts = []
+    for _ in range(args.c1_reps):
+        t0 = time.perf_counter()
+        rg.replay()
+        torch.cuda.synchronize()
+        rts.append((time.perf_counter() - t0) * 1e3)
+    ups = []
+    for _ in range(args.c1_reps):
+        t0 = time.perf_counter()
+        b.set_tiles(cfg.tiles)
+        torch.cuda.synchronize()
+        ups.append((time.perf_counter() - t0) * 1e3)
     out = {"workload": "C1: one 256x256 EPSG:3857 tile from a 3600x1800 EPSG:4326 f32 granule, nearest, scale",
            "p50_tile_ms": round(float(np.percentile(ts, 50)), 4), "p99_tile_ms": round(float(np.percentile(ts, 99)), 4),
            "reps": args.c1_reps, "timing": "host wall per call incl. launch + synchronize",
            "p50_tile_ms_graph": round(float(np.percentile(gts, 50)), 4),
            "p99_tile_ms_graph": round(float(np.percentile(gts, 99)), 4),
-           "graph_timing": "host wall per request: tile descriptor upload + HIP graph replay + synchronize"}
+           "graph_timing": "host wall per request: tile descriptor upload + HIP graph replay + synchronize",
+           "p50_graph_replay_only_ms": round(float(np.percentile(rts, 50)), 4),
+           "p50_descriptor_upload_ms": round(float(np.percentile(ups, 50)), 4)}
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
         from oracle import oracle as O
         cts = []
