@@ -31,7 +31,8 @@ import numpy as np
 from . import _lib
 from ._lib import check, lib
 
-DAEMON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gskyhipd")
+# GSKYHIP_DAEMON: another daemon binary (tools: gskyhipd_ab, on the A/B build)
+DAEMON = os.environ.get("GSKYHIP_DAEMON") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "gskyhipd")
 
 _NP_DTYPE = {np.dtype(np.uint8): _lib.BYTE, np.dtype(np.int8): _lib.BYTE, np.dtype(np.int16): _lib.INT16,
              np.dtype(np.uint16): _lib.UINT16, np.dtype(np.float32): _lib.FLOAT32}
