@@ -411,16 +411,18 @@ def test_render_empty_tiles_written(gpu, oracle, typed):
     assert not got[-1].any() and not got[2].any()
 
 
-@pytest.mark.parametrize("dst", ["EPSG:3857", "EPSG:4326", "EPSG:3577", ""])
+@pytest.mark.parametrize("dst", ["EPSG:3857", "EPSG:4326", "EPSG:3577", "EPSG:28355", ""])
 def test_compute_reproject_extent(gpu, oracle, dst):
     """The worker's `extent` op (ComputeReprojectExtent, warp.go:433-487)
     through the C-ABI, against the oracle restatement, for the C1 / C2 / C5
-    granule kinds (lon/lat, Albers, MODIS sinusoidal) and several bboxes."""
+    granule kinds (lon/lat, Albers, MODIS sinusoidal), a GDA94 / MGA zone 55
+    granule and several bboxes."""
     import torch
 
     import gsky_amd.worker as W
     cases = [synth.config_c1(scale=0.2).granules[0], synth.config_c2(scale=0.05, tiles_per_side=2).granules[0],
-             synth.config_c5(scale=0.05, dates=1, zooms=((4, 11, 8, 1),), tile_px=64).granules[0]]
+             synth.config_c5(scale=0.05, dates=1, zooms=((4, 11, 8, 1),), tile_px=64).granules[0],
+             synth.config_utm(scale=0.05, tiles_per_side=2).granules[0]]
     W.unregister_all()
     try:
         for k, g in enumerate(cases):
@@ -431,7 +433,8 @@ def test_compute_reproject_extent(gpu, oracle, dst):
             src = oracle.crs(g.srs)
             dc = oracle.crs(dst) if dst else src
             for bb in ([12245143.98, -4865942.28, 15584728.71, -1118889.97], [110.0, -45.0, 155.0, -10.0],
-                       [-2000000.0, -4000000.0, 2200000.0, -1000000.0], [0.0, 0.0, 0.0, 0.0]):
+                       [-2000000.0, -4000000.0, 2200000.0, -1000000.0], [200000.0, 5700000.0, 500000.0, 5950000.0],
+                       [0.0, 0.0, 0.0, 0.0]):
                 req = W.GeoRPCGranule(operation="extent", path=path, dstSRS=dst, dstGeot=list(bb))
                 res = W.compute_reproject_extent(req)
                 exp = oracle.compute_reproject_extent(og, src, dc, bb)
