@@ -77,11 +77,19 @@ def test_descriptor_known_answers(oracle):
     assert (m == 255).sum() >= win[0][2]      # at least one pixel per column along the long edge
 
 
-@pytest.mark.parametrize("srs,seed", [("EPSG:4326", 1), ("EPSG:4326", 2), ("EPSG:3577", 3)])
+@pytest.mark.parametrize("srs,seed", [("EPSG:4326", 1), ("EPSG:4326", 2), ("EPSG:3577", 3), ("EPSG:28355", 4)])
 def test_descriptor_matches_oracle(oracle, srs, seed):
     if srs == "EPSG:4326":
         gt, size = GT4326, 2048
         geoms = stars(120, gt, size, seed)
+    elif srs == "EPSG:28355":   # GDA94 / MGA zone 55 dataset: polygons around lon 145.5, lat -36.5
+        gt, size = [230000.0, 100.0, 0.0, 6080000.0, 0.0, -100.0], 2400
+        rng = np.random.default_rng(seed)
+        geoms = []
+        for p in range(60):
+            lon0, lat0 = rng.uniform(144.2, 146.8), rng.uniform(-37.8, -35.6)
+            pts = synth.star_polygon(lon0, lat0, rng.uniform(0.02, 0.3), k=9, seed=p)
+            geoms.append(feature([close(pts)]))
     else:   # Albers dataset: polygons in lon/lat around lon 132, lat -27
         gt, size = [-300000.0, 250.0, 0.0, -2800000.0, 0.0, -250.0], 2400
         rng = np.random.default_rng(seed)
