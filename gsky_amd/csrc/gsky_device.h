@@ -1,6 +1,6 @@
 // gsky_device.h -- device-side building blocks of the MI355X raster hot path.
 //
-// Projection math restates PROJ 6.1.1 (merc/webmerc, aea, gn_sinu, tmerc and the
+// Projection math restates PROJ 6.1.1 (merc/webmerc, aea, gn_sinu, tmerc, lcc and the
 // pj_fwd / pj_inv wrappers) and GDAL 3.0.1's GenImgProj transformer; numeric
 // conversions restate Go 1.12 on amd64.  All of it
 // is compiled with -ffp-contract=off so every double expression rounds once
@@ -235,6 +235,58 @@ __host__ __device__ inline __attribute__((noinline)) bool tm_inv(const gskyhip_c
   return true;
 }
 
+// Lambert Conformal Conic, ellipsoidal (PROJ 6.1.1 lcc.cpp e_forward /
+// e_inverse with pj_tsfn / pj_phi2, [ext]; restated from the published
+// algorithm -- Snyder, Map Projections: A Working Manual, 15-1..15-11 --
+// pinned by Snyder's worked example in tests/test_lcc.py).  Out of line for
+// the same register reason as tm_fwd.
+__host__ __device__ inline double lcc_tsfn(double phi, double sinphi, double e) {
+  sinphi *= e;
+  return tan(.5 * (kHalfPi - phi)) / pow((1. - sinphi) / (1. + sinphi), .5 * e);
+}
+
+__host__ __device__ inline __attribute__((noinline)) bool lcc_fwd(const gskyhip_crs &c, double lam, double phi,
+                                                                   double &xn, double &yn) {
+  double rho;
+  if (fabs(fabs(phi) - kHalfPi) < 1.e-10) {
+    if (phi * c.n <= 0.) return false;
+    rho = 0.;
+  } else {
+    rho = c.c * pow(lcc_tsfn(phi, sin(phi), c.e), c.n);
+  }
+  lam *= c.n;
+  xn = c.k0 * (rho * sin(lam));
+  yn = c.k0 * (c.rho0 - rho * cos(lam));
+  return true;
+}
+
+__host__ __device__ inline __attribute__((noinline)) bool lcc_inv(const gskyhip_crs &c, double xn, double yn,
+                                                                   double &lam, double &phi) {
+  xn /= c.k0;
+  yn /= c.k0;
+  yn = c.rho0 - yn;
+  double rho = hypot(xn, yn);
+  if (rho != 0.) {
+    if (c.n < 0.) { rho = -rho; xn = -xn; yn = -yn; }
+    const double ts = pow(rho / c.c, 1. / c.n);   // pj_phi2
+    const double eccnth = .5 * c.e;
+    double Phi = kHalfPi - 2. * atan(ts), dphi;
+    int i = 15;
+    do {
+      const double con = c.e * sin(Phi);
+      dphi = kHalfPi - 2. * atan(ts * pow((1. - con) / (1. + con), eccnth)) - Phi;
+      Phi += dphi;
+    } while (fabs(dphi) > 1.0e-10 && --i);
+    if (i <= 0) return false;
+    phi = Phi;
+    lam = atan2(xn, yn) / c.n;
+  } else {
+    lam = 0.;
+    phi = c.n > 0. ? kHalfPi : -kHalfPi;
+  }
+  return true;
+}
+
 // pj_inv: CRS coordinates -> (lam, phi) in radians.
 __host__ __device__ inline bool crs_inverse(const gskyhip_crs &c, double x, double y, double &lam, double &phi) {
   if (x == HUGE_VAL || y == HUGE_VAL) return false;
@@ -278,6 +330,8 @@ __host__ __device__ inline bool crs_inverse(const gskyhip_crs &c, double x, doub
     l = xn / cos(yn);
   } else if (c.kind == GSKYHIP_CRS_TMERC) {  // tmerc.cpp exact_e_inv
     if (!tm_inv(c, xn, yn, l, p)) return false;
+  } else if (c.kind == GSKYHIP_CRS_LCC) {  // lcc.cpp e_inverse
+    if (!lcc_inv(c, xn, yn, l, p)) return false;
   } else {
     return false;
   }
@@ -318,6 +372,8 @@ __host__ __device__ inline bool crs_forward(const gskyhip_crs &c, double lam, do
     yn = phi;
   } else if (c.kind == GSKYHIP_CRS_TMERC) {  // tmerc.cpp exact_e_fwd
     if (!tm_fwd(c, lam, phi, xn, yn)) return false;
+  } else if (c.kind == GSKYHIP_CRS_LCC) {  // lcc.cpp e_forward
+    if (!lcc_fwd(c, lam, phi, xn, yn)) return false;
   } else {
     return false;
   }

@@ -139,6 +139,32 @@ int tmerc_setup(gskyhip_crs *c) {
   return 0;
 }
 
+// lcc.cpp setup() of PROJ 6.1.1 for an ellipsoid (pj_msfn / pj_tsfn): the
+// cone constant n (one standard parallel: its sine; two: the secant form),
+// c and rho0.  phi1 / phi2 / phi0 / k0 set by the caller.
+int lcc_setup(gskyhip_crs *c) {
+  if (!(c->es > 0)) return GSKYHIP_E_CRS;   // the spherical lcc is not carried
+  c->kind = GSKYHIP_CRS_LCC;
+  const double phi1 = c->phi1, phi2 = c->phi2;
+  if (std::fabs(phi1 + phi2) < 1e-10) return GSKYHIP_E_CRS;
+  double sinphi = std::sin(phi1);
+  const double cosphi = std::cos(phi1);
+  c->n = sinphi;
+  const bool secant = std::fabs(phi1 - phi2) >= 1e-10;
+  auto msfn = [&](double s, double co) { return co / std::sqrt(1. - c->es * s * s); };
+  const double m1 = msfn(sinphi, cosphi);
+  const double ml1 = lcc_tsfn(phi1, sinphi, c->e);
+  if (secant) {
+    sinphi = std::sin(phi2);
+    c->n = std::log(m1 / msfn(sinphi, std::cos(phi2)));
+    c->n /= std::log(ml1 / lcc_tsfn(phi2, sinphi, c->e));
+  }
+  c->c = c->rho0 = m1 * std::pow(ml1, -c->n) / c->n;
+  c->rho0 *= (std::fabs(std::fabs(c->phi0) - kHalfPi) < 1e-10) ? 0.
+                                                                : std::pow(lcc_tsfn(c->phi0, std::sin(c->phi0), c->e), c->n);
+  return 0;
+}
+
 // utm.cpp setup: zone -> central meridian, k0 0.9996, false easting 500 km,
 // false northing 10,000 km in the south.
 int utm_setup(gskyhip_crs *c, int zone, bool south) {
@@ -186,6 +212,11 @@ int crs_epsg(int code, gskyhip_crs *c) {
   if (code >= 32701 && code <= 32760) { set_ellps(c, 6378137.0, 298.257223563); return utm_setup(c, code - 32700, true); }
   if (code >= 28348 && code <= 28358) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 28300, true); }
   if (code >= 7846 && code <= 7859) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 7800, true); }
+  if (code == 3112 || code == 7845) {   // GDA94 / GDA2020 Geoscience Australia Lambert
+    set_ellps(c, 6378137.0, 298.257222101);
+    c->phi1 = -18.0 * kD2R_h; c->phi2 = -36.0 * kD2R_h; c->phi0 = 0.0; c->lam0 = 134.0 * kD2R_h;
+    return lcc_setup(c);
+  }
   return GSKYHIP_E_CRS;
 }
 
@@ -229,6 +260,20 @@ int crs_proj4(const std::string &s, gskyhip_crs *c) {
     if (!has_zone || zone != std::floor(zone)) return GSKYHIP_E_CRS;   // PROJ guesses from lon_0: not carried
     return utm_setup(c, (int)zone, s.find("+south") != std::string::npos);
   }
+  if (s.find("+proj=lcc") != std::string::npos) {   // lcc.cpp: one parallel -> the tangent cone at it
+    set_ellps(c, a, rf);
+    bool has_l1 = false, has_l2 = false, has_l0 = false, has_k = false;
+    c->phi1 = proj_param(s, "+lat_1", 0, &has_l1) * kD2R_h;
+    c->phi2 = proj_param(s, "+lat_2", 0, &has_l2) * kD2R_h;
+    proj_param(s, "+lat_0", 0, &has_l0);
+    if (!has_l2) {
+      c->phi2 = c->phi1;
+      if (!has_l0) c->phi0 = c->phi1;
+    }
+    c->k0 = proj_param(s, "+k_0", 1.0, &has_k);
+    if (!has_k) c->k0 = proj_param(s, "+k", 1.0);
+    return lcc_setup(c);
+  }
   if (s.find("+proj=tmerc") != std::string::npos || s.find("+proj=etmerc") != std::string::npos) {
     if (s.find("+approx") != std::string::npos) return GSKYHIP_E_CRS;   // Evenden / Snyder series: not carried
     set_ellps(c, a, rf);
@@ -247,7 +292,8 @@ int parse_srs(const char *srs, gskyhip_crs *c) {
   if (ieq(s, "MODIS") || ieq(s, "SR-ORG:6842")) return crs_proj4("+proj=sinu +R=6371007.181", c);
   if (s.size() > 5 && strncasecmp(s.c_str(), "EPSG:", 5) == 0) return crs_epsg(std::atoi(s.c_str() + 5), c);
   if (s.find("+proj=") != std::string::npos) return crs_proj4(s, c);
-  // WKT: a Sinusoidal / Transverse Mercator projection, else the top-level (last) EPSG authority
+  // WKT: a Sinusoidal / Lambert Conformal Conic / Transverse Mercator projection, else the top-level (last) EPSG
+  // authority
   if (s.find("PROJECTION[\"Sinusoidal\"]") != std::string::npos) {
     size_t p = s.find("SPHEROID[");
     double a = 6371007.181;
@@ -258,6 +304,40 @@ int parse_srs(const char *srs, gskyhip_crs *c) {
     char buf[96];
     std::snprintf(buf, sizeof(buf), "+proj=sinu +R=%.17g", a);
     return crs_proj4(buf, c);
+  }
+  const bool lcc2 = s.find("PROJECTION[\"Lambert_Conformal_Conic_2SP\"]") != std::string::npos;
+  const bool lcc1 = s.find("PROJECTION[\"Lambert_Conformal_Conic_1SP\"]") != std::string::npos;
+  if (lcc1 || lcc2) {   // WKT1 Lambert Conformal Conic: its parameters
+    auto param = [&](const char *name, double dflt) {
+      const std::string k = std::string("PARAMETER[\"") + name + "\",";
+      const size_t p = s.find(k);
+      return p == std::string::npos ? dflt : std::strtod(s.c_str() + p + k.size(), nullptr);
+    };
+    double a = 6378137.0, rf = 298.257223563;
+    const size_t p = s.find("SPHEROID[");
+    if (p != std::string::npos) {
+      const size_t q = s.find(',', p);
+      if (q != std::string::npos) {
+        char *end = nullptr;
+        a = std::strtod(s.c_str() + q + 1, &end);
+        if (end && *end == ',') rf = std::strtod(end + 1, nullptr);
+      }
+    }
+    std::memset(c, 0, sizeof(*c));
+    set_ellps(c, a, rf);
+    c->phi0 = param("latitude_of_origin", 0) * kD2R_h;
+    c->lam0 = param("central_meridian", 0) * kD2R_h;
+    c->x0 = param("false_easting", 0);
+    c->y0 = param("false_northing", 0);
+    if (lcc2) {
+      c->k0 = 1.0;
+      c->phi1 = param("standard_parallel_1", 0) * kD2R_h;
+      c->phi2 = param("standard_parallel_2", 0) * kD2R_h;
+    } else {
+      c->k0 = param("scale_factor", 1.0);
+      c->phi1 = c->phi2 = c->phi0;
+    }
+    return lcc_setup(c);
   }
   if (s.find("PROJECTION[\"Transverse_Mercator\"]") != std::string::npos) {   // WKT1 TM: its parameters
     auto param = [&](const char *name, double dflt) {

@@ -1083,6 +1083,20 @@ std::string nc_cf_srs(const Nc &f, const NcVar &v) {
                       num(m, "longitude_of_central_meridian", 0, 0), fe, fn, ell);
         return buf;
       }
+      if (name == "lambert_conformal_conic" && !sphere) {   // ellipsoidal only (as the warp's lcc)
+        const NcAtt *sp = nc_att(m.atts, "standard_parallel");
+        if (!sp || sp->num.empty()) return "?";
+        const double lat0 = num(m, "latitude_of_projection_origin", 0, 0);
+        const double cm = num(m, "longitude_of_central_meridian", 0, 0);
+        if (sp->num.size() > 1)
+          std::snprintf(buf, sizeof(buf), "+proj=lcc +lat_1=%.17g +lat_2=%.17g +lat_0=%.17g +lon_0=%.17g +x_0=%.17g "
+                        "+y_0=%.17g %s", sp->num[0], sp->num[1], lat0, cm, fe, fn, ell);
+        else   // one standard parallel: the tangent cone (LCC 1SP)
+          std::snprintf(buf, sizeof(buf), "+proj=lcc +lat_1=%.17g +lat_0=%.17g +lon_0=%.17g +k_0=%.17g +x_0=%.17g "
+                        "+y_0=%.17g %s", sp->num[0], lat0, cm, num(m, "scale_factor_at_projection_origin", 0, 1.0),
+                        fe, fn, ell);
+        return buf;
+      }
       if (name == "transverse_mercator" && !sphere) {   // ellipsoidal only (as the warp's tmerc)
         const double k0 = num(m, "scale_factor_at_central_meridian", 0, 1.0);
         const double cm = num(m, "longitude_of_central_meridian", 0, 0);

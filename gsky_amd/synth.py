@@ -286,17 +286,18 @@ def config_c2(scale: float = 1.0, tiles_per_side: int = 64, tile_px: int = 512, 
 
 # ---------------------------------------------------------------- UTM (widening)
 def config_utm(scale: float = 1.0, tiles_per_side: int = 16, tile_px: int = 256, grid: int = 2,
-               srs: str = "EPSG:28355") -> SynthConfig:
-    """C2's shape from Transverse Mercator granules: `grid`^2 int16 granules
-    of GDA94 / MGA zone 55 (default; 4000^2 at 25 m at full size, 100 km
-    each, 5 km overlaps, over Victoria around 144-147 E), EPSG:3857 tiles over
-    their union, nearest, the C2 scale and palette."""
+               srs: str = "EPSG:28355", origin=(250000.0, 5900000.0)) -> SynthConfig:
+    """C2's shape from projected granules of another family: `grid`^2 int16
+    granules of GDA94 / MGA zone 55 (default; 4000^2 at 25 m at full size,
+    100 km each, 5 km overlaps, over Victoria around 144-147 E) -- or any
+    `srs` with the union's top-left corner at `origin` (config_lambert) --
+    EPSG:3857 tiles over their union, nearest, the C2 scale and palette."""
     n = int(round(4000 * scale))
     psize = 100000.0 / n
     def make(k):
         j, i = divmod(k, grid)
-        x0 = 250000.0 + 95000.0 * i
-        y0 = 5900000.0 - 95000.0 * j
+        x0 = origin[0] + 95000.0 * i
+        y0 = origin[1] - 95000.0 * j
         idx = np.arange(n * n, dtype=np.uint64).reshape(n, n) + np.uint64((SEED0 + 0x7A00 + k) << 32)
         v = (splitmix64(idx) % np.uint64(10000)).astype(np.int16)
         v[uniform01(splitmix64(idx)) < 0.02] = -999
@@ -306,7 +307,7 @@ def config_utm(scale: float = 1.0, tiles_per_side: int = 16, tile_px: int = 256,
 
     granules = [make(k) for k in range(grid * grid)]
     from .tiles import crs_transform
-    ux0, uy1 = 250000.0, 5900000.0
+    ux0, uy1 = origin
     ux1, uy0 = ux0 + 95000.0 * (grid - 1) + 100000.0, uy1 - 95000.0 * (grid - 1) - 100000.0
     t = np.linspace(0, 1, 64)
     X = np.concatenate([ux0 + t * (ux1 - ux0)] * 2 + [np.full(64, ux0), np.full(64, ux1)])
@@ -318,6 +319,14 @@ def config_utm(scale: float = 1.0, tiles_per_side: int = 16, tile_px: int = 256,
     tiles = _grid_tiles(bbox, tiles_per_side, tiles_per_side, tile_px)
     pairs = _index_pairs(granules, tiles)
     return SynthConfig("UTM", granules, "EPSG:3857", tiles, pairs, [""], (0.0, 0.0, 10000.0, 0), PALETTE_GSKY)
+
+
+def config_lambert(scale: float = 1.0, tiles_per_side: int = 16, tile_px: int = 256, grid: int = 2) -> SynthConfig:
+    """config_utm's shape from GDA94 / Geoscience Australia Lambert (EPSG:3112)
+    granules around Sydney (x 1.40-1.60 Mm, y -3.82 to -4.02 Mm)."""
+    cfg = config_utm(scale, tiles_per_side, tile_px, grid, srs="EPSG:3112", origin=(1400000.0, -3820000.0))
+    cfg.name = "LCC"
+    return cfg
 
 
 def subset(cfg: SynthConfig, tile_ids) -> SynthConfig:

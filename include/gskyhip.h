@@ -58,6 +58,10 @@ extern "C" {
 #define GSKYHIP_CRS_TMERC 4        /* Transverse Mercator, ellipsoidal: UTM     *
                                     * (EPSG:326zz / 327zz), GDA94 / GDA2020 MGA *
                                     * (EPSG:283zz / 78zz), +proj=tmerc / utm    */
+#define GSKYHIP_CRS_LCC 5          /* Lambert Conformal Conic, ellipsoidal, 1SP *
+                                    * or 2SP: GDA94 / GDA2020 GA Lambert        *
+                                    * (EPSG:3112 / 7845), +proj=lcc; constants   *
+                                    * in n, c, rho0                              */
 
 typedef struct {
     int32_t kind;

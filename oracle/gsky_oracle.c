@@ -772,6 +772,32 @@ static int utm_setup(oracle_crs *c, int zone, int south) {   /* utm.cpp */
     return tmerc_setup(c);
 }
 
+/* ---- lcc.cpp (PROJ 6.1.1), ellipsoidal [ext] -----------------------------
+ * Snyder 15-1..15-11 as PROJ states them: t(phi) = pj_tsfn, m(phi) =
+ * pj_msfn, the inverse latitude by pj_phi2's fixed-point iteration. */
+static double or_tsfn(double phi, double sinphi, double e) {
+    sinphi *= e;
+    return tan(.5 * (OR_HALFPI - phi)) / pow((1. - sinphi) / (1. + sinphi), .5 * e);
+}
+
+static int lcc_setup(oracle_crs *c) {
+    if (!(c->es > 0)) return -1;
+    c->kind = OR_CRS_LCC;
+    if (fabs(c->phi1 + c->phi2) < 1e-10) return -1;
+    double sinphi = sin(c->phi1), cosphi = cos(c->phi1);
+    c->n = sinphi;
+    double m1 = cosphi / sqrt(1. - c->es * sinphi * sinphi);
+    double ml1 = or_tsfn(c->phi1, sinphi, c->e);
+    if (fabs(c->phi1 - c->phi2) >= 1e-10) {
+        sinphi = sin(c->phi2);
+        c->n = log(m1 / (cos(c->phi2) / sqrt(1. - c->es * sinphi * sinphi)));
+        c->n /= log(ml1 / or_tsfn(c->phi2, sinphi, c->e));
+    }
+    c->c = c->rho0 = m1 * pow(ml1, -c->n) / c->n;
+    c->rho0 *= fabs(fabs(c->phi0) - OR_HALFPI) < 1e-10 ? 0. : pow(or_tsfn(c->phi0, sin(c->phi0), c->e), c->n);
+    return 0;
+}
+
 static double param_of(const char *s, const char *key, double dflt, int *found) {
     const char *p = s;
     size_t kl = strlen(key);
@@ -809,6 +835,11 @@ int oracle_crs_init(oracle_crs *c, const char *spec) {
         if (code > 32700 && code <= 32760) { set_ellps(c, 6378137.0, 298.257223563); return utm_setup(c, code - 32700, 1); }
         if (code >= 28348 && code <= 28358) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 28300, 1); }
         if (code >= 7846 && code <= 7859) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 7800, 1); }
+        if (code == 3112 || code == 7845) {
+            set_ellps(c, 6378137.0, 298.257222101);
+            c->phi1 = -18.0 * OR_D2R; c->phi2 = -36.0 * OR_D2R; c->phi0 = 0.0; c->lam0 = 134.0 * OR_D2R;
+            return lcc_setup(c);
+        }
     }
     if (strstr(spec, "+proj=")) {
         int f = 0;
@@ -844,6 +875,17 @@ int oracle_crs_init(oracle_crs *c, const char *spec) {
             set_ellps(c, a, rf);
             if (!fz || zone != floor(zone)) return -1;
             return utm_setup(c, (int)zone, strstr(spec, "+south") != NULL);
+        }
+        if (strstr(spec, "+proj=lcc")) {
+            int f1 = 0, f2 = 0, f0 = 0, fk = 0;
+            set_ellps(c, a, rf);
+            c->phi1 = param_of(spec, "+lat_1", 0, &f1) * OR_D2R;
+            c->phi2 = param_of(spec, "+lat_2", 0, &f2) * OR_D2R;
+            param_of(spec, "+lat_0", 0, &f0);
+            if (!f2) { c->phi2 = c->phi1; if (!f0) c->phi0 = c->phi1; }
+            c->k0 = param_of(spec, "+k_0", 1.0, &fk);
+            if (!fk) c->k0 = param_of(spec, "+k", 1.0, NULL);
+            return lcc_setup(c);
         }
         if ((strstr(spec, "+proj=tmerc") || strstr(spec, "+proj=etmerc")) && !strstr(spec, "+approx")) {
             int fk = 0;
@@ -903,6 +945,27 @@ static int crs_inverse(const oracle_crs *c, double x, double y, double *lam, dou
         p = yn;
         l = xn / cos(yn);
         break;
+    case OR_CRS_LCC: {                          /* lcc.cpp e_inverse */
+        double X = xn / c->k0, Y = c->rho0 - yn / c->k0;
+        double rho = hypot(X, Y);
+        if (rho != 0.) {
+            if (c->n < 0.) { rho = -rho; X = -X; Y = -Y; }
+            double ts = pow(rho / c->c, 1. / c->n), Phi = OR_HALFPI - 2. * atan(ts), dphi;
+            int i = 15;
+            do {
+                double con = c->e * sin(Phi);
+                dphi = OR_HALFPI - 2. * atan(ts * pow((1. - con) / (1. + con), .5 * c->e)) - Phi;
+                Phi += dphi;
+            } while (fabs(dphi) > 1.0e-10 && --i);
+            if (i <= 0) return 0;
+            p = Phi;
+            l = atan2(X, Y) / c->n;
+        } else {
+            l = 0.;
+            p = c->n > 0. ? OR_HALFPI : -OR_HALFPI;
+        }
+        break;
+    }
     case OR_CRS_TMERC: {                        /* tmerc.cpp exact_e_inv */
         double Cn = (yn - c->tm_zb) / c->tm_qn, Ce = xn / c->tm_qn, dCn, dCe;
         if (!(fabs(Ce) <= 2.623395162778)) return 0;   /* 150 degrees */
@@ -959,6 +1022,19 @@ static int crs_forward(const oracle_crs *c, double lam, double phi, double *x, d
         xn = lam * cos(phi);
         yn = phi;
         break;
+    case OR_CRS_LCC: {                          /* lcc.cpp e_forward */
+        double rho;
+        if (fabs(fabs(phi) - OR_HALFPI) < 1.e-10) {
+            if (phi * c->n <= 0.) return 0;
+            rho = 0.;
+        } else {
+            rho = c->c * pow(or_tsfn(phi, sin(phi), c->e), c->n);
+        }
+        double L = lam * c->n;
+        xn = c->k0 * (rho * sin(L));
+        yn = c->k0 * (c->rho0 - rho * cos(L));
+        break;
+    }
     case OR_CRS_TMERC: {                        /* tmerc.cpp exact_e_fwd */
         double Cn = or_gatg(c->tm_cbg, 6, phi), dCn, dCe;
         double sCn = sin(Cn), cCn = cos(Cn), sCe = sin(lam), cCe = cos(lam);

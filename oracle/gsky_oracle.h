@@ -115,14 +115,14 @@ int oracle_merge_batch(const oracle_flex_raster *rasters, int n,
                        int mask_inclusive, oracle_canvas *canvases, int n_ns);
 
 /* ---- projections (PROJ 6.1.1 formulas, restated) ------------------------ */
-enum { OR_CRS_LONGLAT = 0, OR_CRS_WEBMERC = 1, OR_CRS_AEA = 2, OR_CRS_SINU = 3, OR_CRS_TMERC = 4 };
+enum { OR_CRS_LONGLAT = 0, OR_CRS_WEBMERC = 1, OR_CRS_AEA = 2, OR_CRS_SINU = 3, OR_CRS_TMERC = 4, OR_CRS_LCC = 5 };
 
 typedef struct {
     int32_t kind;
     int32_t _pad;
     double a, ra, es, e, one_es;
     double lam0, phi0, phi1, phi2, x0, y0, k0;
-    /* aea constants */
+    /* aea constants (lcc: n, c, rho0) */
     double n, c, dd, rho0, ec;
     /* tmerc (PROJ 6 exact: Poder / Engsager) constants */
     double tm_qn, tm_zb;
@@ -130,9 +130,10 @@ typedef struct {
 } oracle_crs;
 
 /* spec: "EPSG:4326", "EPSG:4283", "EPSG:3857", "EPSG:3577", "EPSG:900913",
- * the UTM / MGA zones "EPSG:326zz" / "327zz" / "283zz" / "78zz",
+ * the UTM / MGA zones "EPSG:326zz" / "327zz" / "283zz" / "78zz", the GA
+ * Lambert "EPSG:3112" / "7845",
  * "SR-ORG:6842" / "MODIS" (sinusoidal R=6371007.181), or a proj4 string
- * (+proj=longlat|merc|webmerc|aea|sinu|tmerc|utm ...).  Returns 0 or -1. */
+ * (+proj=longlat|merc|webmerc|aea|sinu|tmerc|utm|lcc ...).  Returns 0 or -1. */
 int oracle_crs_init(oracle_crs *crs, const char *spec);
 
 /* Whole transformation src CRS -> dst CRS for one point (degrees for

@@ -77,13 +77,15 @@ def test_descriptor_known_answers(oracle):
     assert (m == 255).sum() >= win[0][2]      # at least one pixel per column along the long edge
 
 
-@pytest.mark.parametrize("srs,seed", [("EPSG:4326", 1), ("EPSG:4326", 2), ("EPSG:3577", 3), ("EPSG:28355", 4)])
+@pytest.mark.parametrize("srs,seed", [("EPSG:4326", 1), ("EPSG:4326", 2), ("EPSG:3577", 3), ("EPSG:28355", 4),
+                                      ("EPSG:3112", 5)])
 def test_descriptor_matches_oracle(oracle, srs, seed):
     if srs == "EPSG:4326":
         gt, size = GT4326, 2048
         geoms = stars(120, gt, size, seed)
-    elif srs == "EPSG:28355":   # GDA94 / MGA zone 55 dataset: polygons around lon 145.5, lat -36.5
-        gt, size = [230000.0, 100.0, 0.0, 6080000.0, 0.0, -100.0], 2400
+    elif srs in ("EPSG:28355", "EPSG:3112"):   # MGA zone 55 / GA Lambert: polygons around lon 145.5, lat -36.5
+        gt, size = ([230000.0, 100.0, 0.0, 6080000.0, 0.0, -100.0] if srs == "EPSG:28355"
+                    else [880000.0, 150.0, 0.0, -3990000.0, 0.0, -150.0]), 2400
         rng = np.random.default_rng(seed)
         geoms = []
         for p in range(60):

@@ -451,6 +451,12 @@ UTM55_CF = {"grid_mapping_name": "transverse_mercator", "scale_factor_at_central
             "semi_major_axis": np.array([6378137.0]), "inverse_flattening": np.array([298.257222101])}
 
 
+GALCC_CF = {"grid_mapping_name": "lambert_conformal_conic", "standard_parallel": np.array([-18.0, -36.0]),
+            "longitude_of_central_meridian": np.array([134.0]), "latitude_of_projection_origin": np.array([0.0]),
+            "false_easting": np.array([0.0]), "false_northing": np.array([0.0]),
+            "semi_major_axis": np.array([6378137.0]), "inverse_flattening": np.array([298.257222101])}
+
+
 def test_netcdf_srs_cf_option(tmp_path):
     """srs_cf (warp.go:95 -> netcdfdataset.cpp:7023-7025, 3666): without it
     the GDAL WKT's EPSG code wins; with it only the CF grid mapping counts.
@@ -470,7 +476,7 @@ def test_netcdf_srs_cf_option(tmp_path):
     _write_albers_nc(p2, data, x, y, cf=cf)          # CF only: both options agree
     assert ingest.netcdf_srs(p2, 0) == ingest.netcdf_srs(p2, 1) == got
     p3 = str(tmp_path / "c.nc")
-    _write_albers_nc(p3, data, x, y, wkt=wkt, cf={"grid_mapping_name": "lambert_conformal_conic"})
+    _write_albers_nc(p3, data, x, y, wkt=wkt, cf={"grid_mapping_name": "polar_stereographic"})
     assert ingest.netcdf_srs(p3, 0) == "EPSG:3577" and ingest.netcdf_srs(p3, 1) == "?"
     p4 = str(tmp_path / "d.nc")
     _write_albers_nc(p4, data, x, y, cf={"grid_mapping_name": "sinusoidal", "longitude_of_central_meridian": np.array([0.0]),
@@ -491,6 +497,16 @@ def test_netcdf_srs_cf_option(tmp_path):
     assert s7.startswith("+proj=tmerc +lat_0=0 +lon_0=147 +k_0=0.99994") and "+y_0=5000000 " in s7
     from gsky_amd.tiles import parse_crs
     assert parse_crs(s7).kind == 4 and parse_crs(ingest.netcdf_srs(p6, 1)).kind == 4
+    # lambert_conformal_conic: two standard parallels (GA Lambert), or one (the tangent cone)
+    p8 = str(tmp_path / "h.nc")
+    _write_albers_nc(p8, data, x, y, cf=GALCC_CF)
+    s8 = ingest.netcdf_srs(p8, 1)
+    assert s8.startswith("+proj=lcc +lat_1=-18 +lat_2=-36 +lat_0=0 +lon_0=134 ")
+    c8, e3112 = parse_crs(s8), parse_crs("EPSG:3112")
+    assert c8.kind == 5 and (c8.n, c8.c, c8.rho0) == (e3112.n, e3112.c, e3112.rho0)
+    p9 = str(tmp_path / "i.nc")
+    _write_albers_nc(p9, data, x, y, cf=dict(GALCC_CF, standard_parallel=np.array([-30.0])))
+    assert ingest.netcdf_srs(p9, 1).startswith("+proj=lcc +lat_1=-30 +lat_0=0 +lon_0=134 +k_0=1 ")
 
 
 @pytest.mark.gpu
@@ -533,7 +549,7 @@ def test_gpu_netcdf_srs_cf_drop_in(tmp_path):
         outs[cf] = got
     assert not np.array_equal(outs[0], outs[1])      # the 0.01 degree meridian shift moves the picks
     p2 = str(tmp_path / "h.nc")
-    _write_albers_nc(p2, data, x, y, wkt=wkt, cf={"grid_mapping_name": "lambert_conformal_conic"})
+    _write_albers_nc(p2, data, x, y, wkt=wkt, cf={"grid_mapping_name": "polar_stereographic"})
     ok = worker.warp_raster(worker.GeoRPCGranule(path=p2, bands=[1], width=64, height=64, dstSRS="EPSG:3857",
                                                  dstGeot=dgt, sRSCf=0))
     bad = worker.warp_raster(worker.GeoRPCGranule(path=p2, bands=[1], width=64, height=64, dstSRS="EPSG:3857",
