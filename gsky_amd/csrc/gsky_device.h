@@ -1,6 +1,6 @@
 // gsky_device.h -- device-side building blocks of the MI355X raster hot path.
 //
-// Projection math restates PROJ 6.1.1 (merc/webmerc, aea, gn_sinu, tmerc, lcc and the
+// Projection math restates PROJ 6.1.1 (merc/webmerc, aea, gn_sinu, tmerc, lcc, polar stere and the
 // pj_fwd / pj_inv wrappers) and GDAL 3.0.1's GenImgProj transformer; numeric
 // conversions restate Go 1.12 on amd64.  All of it
 // is compiled with -ffp-contract=off so every double expression rounds once
@@ -287,6 +287,44 @@ __host__ __device__ inline __attribute__((noinline)) bool lcc_inv(const gskyhip_
   return true;
 }
 
+// Polar stereographic, ellipsoidal (PROJ 6.1.1 stere.cpp e_forward /
+// e_inverse, N_POLE / S_POLE modes, [ext]; Snyder 21-33..21-39, pinned by
+// Snyder's worked example in tests/test_stere.py): akm1 in c.c, the pole by
+// the sign of phi0.
+__host__ __device__ inline __attribute__((noinline)) bool stere_fwd(const gskyhip_crs &c, double lam, double phi,
+                                                                     double &xn, double &yn) {
+  double coslam = cos(lam);
+  const double sinlam = sin(lam);
+  double sinphi = sin(phi);
+  if (c.phi0 < 0) {   // S_POLE
+    phi = -phi;
+    coslam = -coslam;
+    sinphi = -sinphi;
+  }
+  double x = c.c * lcc_tsfn(phi, sinphi, c.e);
+  yn = -x * coslam;
+  xn = x * sinlam;
+  return true;
+}
+
+__host__ __device__ inline __attribute__((noinline)) bool stere_inv(const gskyhip_crs &c, double xn, double yn,
+                                                                     double &lam, double &phi) {
+  const double rho = hypot(xn, yn);
+  if (c.phi0 >= 0) yn = -yn;   // N_POLE
+  const double tp = -rho / c.c, halfpi = -kHalfPi, halfe = -.5 * c.e;
+  double phi_l = kHalfPi - 2. * atan(tp);
+  for (int i = 8; i--; phi_l = phi) {
+    const double sinphi = c.e * sin(phi_l);
+    phi = 2. * atan(tp * pow((1. + sinphi) / (1. - sinphi), halfe)) - halfpi;
+    if (fabs(phi_l - phi) < 1.e-10) {
+      if (c.phi0 < 0) phi = -phi;
+      lam = (xn == 0. && yn == 0.) ? 0. : atan2(xn, yn);
+      return true;
+    }
+  }
+  return false;
+}
+
 // pj_inv: CRS coordinates -> (lam, phi) in radians.
 __host__ __device__ inline bool crs_inverse(const gskyhip_crs &c, double x, double y, double &lam, double &phi) {
   if (x == HUGE_VAL || y == HUGE_VAL) return false;
@@ -332,6 +370,8 @@ __host__ __device__ inline bool crs_inverse(const gskyhip_crs &c, double x, doub
     if (!tm_inv(c, xn, yn, l, p)) return false;
   } else if (c.kind == GSKYHIP_CRS_LCC) {  // lcc.cpp e_inverse
     if (!lcc_inv(c, xn, yn, l, p)) return false;
+  } else if (c.kind == GSKYHIP_CRS_STERE_POLAR) {  // stere.cpp e_inverse (polar)
+    if (!stere_inv(c, xn, yn, l, p)) return false;
   } else {
     return false;
   }
@@ -374,6 +414,8 @@ __host__ __device__ inline bool crs_forward(const gskyhip_crs &c, double lam, do
     if (!tm_fwd(c, lam, phi, xn, yn)) return false;
   } else if (c.kind == GSKYHIP_CRS_LCC) {  // lcc.cpp e_forward
     if (!lcc_fwd(c, lam, phi, xn, yn)) return false;
+  } else if (c.kind == GSKYHIP_CRS_STERE_POLAR) {  // stere.cpp e_forward (polar)
+    if (!stere_fwd(c, lam, phi, xn, yn)) return false;
   } else {
     return false;
   }

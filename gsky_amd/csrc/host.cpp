@@ -165,6 +165,28 @@ int lcc_setup(gskyhip_crs *c) {
   return 0;
 }
 
+// stere.cpp setup() of PROJ 6.1.1, polar aspects on an ellipsoid: phi0 =
+// +-pi/2 picks the pole, |lat_ts| the true-scale parallel (pi/2: k0 at the
+// pole); akm1 into c->c.
+int stere_polar_setup(gskyhip_crs *c, double phi0, bool has_ts, double lat_ts) {
+  if (!(c->es > 0)) return GSKYHIP_E_CRS;   // the spherical stere is not carried
+  if (std::fabs(std::fabs(phi0) - kHalfPi) >= 1e-10) return GSKYHIP_E_CRS;   // oblique / equatorial: not carried
+  c->kind = GSKYHIP_CRS_STERE_POLAR;
+  c->phi0 = phi0 < 0 ? -kHalfPi : kHalfPi;
+  const double phits = std::fabs(has_ts ? lat_ts : kHalfPi);
+  c->phi1 = phits;
+  const double e = c->e;
+  if (std::fabs(phits - kHalfPi) < 1e-10) {
+    c->c = 2. * c->k0 / std::sqrt(std::pow(1 + e, 1 + e) * std::pow(1 - e, 1 - e));
+  } else {
+    double t = std::sin(phits);
+    c->c = std::cos(phits) / lcc_tsfn(phits, t, e);
+    t *= e;
+    c->c /= std::sqrt(1. - t * t);
+  }
+  return 0;
+}
+
 // utm.cpp setup: zone -> central meridian, k0 0.9996, false easting 500 km,
 // false northing 10,000 km in the south.
 int utm_setup(gskyhip_crs *c, int zone, bool south) {
@@ -212,6 +234,17 @@ int crs_epsg(int code, gskyhip_crs *c) {
   if (code >= 32701 && code <= 32760) { set_ellps(c, 6378137.0, 298.257223563); return utm_setup(c, code - 32700, true); }
   if (code >= 28348 && code <= 28358) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 28300, true); }
   if (code >= 7846 && code <= 7859) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 7800, true); }
+  if (code == 3031 || code == 3413 || code == 3976) {   // WGS 84 polar stereographic (Antarctic, NSIDC)
+    set_ellps(c, 6378137.0, 298.257223563);
+    c->lam0 = (code == 3413 ? -45.0 : 0.0) * kD2R_h;
+    const double ts = code == 3031 ? -71.0 : code == 3413 ? 70.0 : -70.0;
+    return stere_polar_setup(c, (ts < 0 ? -90.0 : 90.0) * kD2R_h, true, ts * kD2R_h);
+  }
+  if (code == 32661 || code == 32761) {   // WGS 84 / UPS North / South
+    set_ellps(c, 6378137.0, 298.257223563);
+    c->k0 = 0.994; c->x0 = 2000000.0; c->y0 = 2000000.0;
+    return stere_polar_setup(c, (code == 32661 ? 90.0 : -90.0) * kD2R_h, false, 0.0);
+  }
   if (code == 3112 || code == 7845) {   // GDA94 / GDA2020 Geoscience Australia Lambert
     set_ellps(c, 6378137.0, 298.257222101);
     c->phi1 = -18.0 * kD2R_h; c->phi2 = -36.0 * kD2R_h; c->phi0 = 0.0; c->lam0 = 134.0 * kD2R_h;
@@ -260,6 +293,20 @@ int crs_proj4(const std::string &s, gskyhip_crs *c) {
     if (!has_zone || zone != std::floor(zone)) return GSKYHIP_E_CRS;   // PROJ guesses from lon_0: not carried
     return utm_setup(c, (int)zone, s.find("+south") != std::string::npos);
   }
+  if (s.find("+proj=ups") != std::string::npos) {   // ups: stere at a pole, k0 0.994, false E / N 2000 km
+    set_ellps(c, a, rf);
+    c->k0 = 0.994; c->x0 = 2000000.0; c->y0 = 2000000.0; c->lam0 = 0.0;
+    return stere_polar_setup(c, (s.find("+south") != std::string::npos ? -90.0 : 90.0) * kD2R_h, false, 0.0);
+  }
+  if (s.find("+proj=stere ") != std::string::npos ||
+      (s.size() >= 11 && s.compare(s.size() - 11, 11, "+proj=stere") == 0)) {
+    set_ellps(c, a, rf);
+    bool has_ts = false, has_k = false;
+    const double ts = proj_param(s, "+lat_ts", 0, &has_ts) * kD2R_h;
+    c->k0 = proj_param(s, "+k_0", 1.0, &has_k);
+    if (!has_k) c->k0 = proj_param(s, "+k", 1.0);
+    return stere_polar_setup(c, c->phi0, has_ts, ts);
+  }
   if (s.find("+proj=lcc") != std::string::npos) {   // lcc.cpp: one parallel -> the tangent cone at it
     set_ellps(c, a, rf);
     bool has_l1 = false, has_l2 = false, has_l0 = false, has_k = false;
@@ -304,6 +351,32 @@ int parse_srs(const char *srs, gskyhip_crs *c) {
     char buf[96];
     std::snprintf(buf, sizeof(buf), "+proj=sinu +R=%.17g", a);
     return crs_proj4(buf, c);
+  }
+  if (s.find("PROJECTION[\"Polar_Stereographic\"]") != std::string::npos) {   // WKT1 (GDAL): latitude_of_origin = lat_ts
+    auto param = [&](const char *name, double dflt) {
+      const std::string k = std::string("PARAMETER[\"") + name + "\",";
+      const size_t p = s.find(k);
+      return p == std::string::npos ? dflt : std::strtod(s.c_str() + p + k.size(), nullptr);
+    };
+    double a = 6378137.0, rf = 298.257223563;
+    const size_t p = s.find("SPHEROID[");
+    if (p != std::string::npos) {
+      const size_t q = s.find(',', p);
+      if (q != std::string::npos) {
+        char *end = nullptr;
+        a = std::strtod(s.c_str() + q + 1, &end);
+        if (end && *end == ',') rf = std::strtod(end + 1, nullptr);
+      }
+    }
+    std::memset(c, 0, sizeof(*c));
+    set_ellps(c, a, rf);
+    const double ts = param("latitude_of_origin", 90.0);
+    c->lam0 = param("central_meridian", 0) * kD2R_h;
+    c->k0 = param("scale_factor", 1.0);
+    c->x0 = param("false_easting", 0);
+    c->y0 = param("false_northing", 0);
+    return stere_polar_setup(c, (ts < 0 ? -90.0 : 90.0) * kD2R_h, std::fabs(std::fabs(ts) - 90.0) > 1e-12,
+                             ts * kD2R_h);
   }
   const bool lcc2 = s.find("PROJECTION[\"Lambert_Conformal_Conic_2SP\"]") != std::string::npos;
   const bool lcc1 = s.find("PROJECTION[\"Lambert_Conformal_Conic_1SP\"]") != std::string::npos;

@@ -1111,6 +1111,20 @@ std::string nc_cf_srs(const Nc &f, const NcVar &v) {
                         lat0, cm, k0, fe, fn, ell);
         return buf;
       }
+      if (name == "polar_stereographic" && !sphere && has(m, "latitude_of_projection_origin")) {
+        // polar aspects only (as the warp's stere): the pole, then the
+        // true-scale parallel or the scale at the pole
+        const double lat0 = num(m, "latitude_of_projection_origin", 0, 0);
+        if (lat0 != 90.0 && lat0 != -90.0) return "?";
+        const double cm = num(m, "straight_vertical_longitude_from_pole", 0, 0);
+        if (has(m, "standard_parallel"))
+          std::snprintf(buf, sizeof(buf), "+proj=stere +lat_0=%.17g +lat_ts=%.17g +lon_0=%.17g +x_0=%.17g +y_0=%.17g %s",
+                        lat0, num(m, "standard_parallel", 0, lat0), cm, fe, fn, ell);
+        else
+          std::snprintf(buf, sizeof(buf), "+proj=stere +lat_0=%.17g +lon_0=%.17g +k_0=%.17g +x_0=%.17g +y_0=%.17g %s",
+                        lat0, cm, num(m, "scale_factor_at_projection_origin", 0, 1.0), fe, fn, ell);
+        return buf;
+      }
       if (name == "sinusoidal" && sphere) {
         std::snprintf(buf, sizeof(buf), "+proj=sinu +lon_0=%.17g +x_0=%.17g +y_0=%.17g %s",
                       num(m, "longitude_of_central_meridian", 0, num(m, "longitude_of_projection_origin", 0, 0)),

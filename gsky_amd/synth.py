@@ -329,6 +329,17 @@ def config_lambert(scale: float = 1.0, tiles_per_side: int = 16, tile_px: int = 
     return cfg
 
 
+def config_polar(scale: float = 1.0, tiles_per_side: int = 16, tile_px: int = 256, grid: int = 2,
+                 srs: str = "EPSG:3031", origin=(-2400000.0, 1400000.0)) -> SynthConfig:
+    """config_utm's shape from polar stereographic granules: WGS 84 / Antarctic
+    Polar Stereographic (EPSG:3031) off the Antarctic Peninsula by default
+    (about 66-68 S, 58-62 W), or NSIDC North (EPSG:3413, origin (-200000,
+    -2000000): western Greenland)."""
+    cfg = config_utm(scale, tiles_per_side, tile_px, grid, srs=srs, origin=origin)
+    cfg.name = "STERE"
+    return cfg
+
+
 def subset(cfg: SynthConfig, tile_ids) -> SynthConfig:
     """The same config restricted to some tiles (for bounded CPU samples)."""
     tiles = [cfg.tiles[i] for i in tile_ids]

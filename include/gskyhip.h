@@ -62,6 +62,10 @@ extern "C" {
                                     * or 2SP: GDA94 / GDA2020 GA Lambert        *
                                     * (EPSG:3112 / 7845), +proj=lcc; constants   *
                                     * in n, c, rho0                              */
+#define GSKYHIP_CRS_STERE_POLAR 6  /* polar stereographic, ellipsoidal: EPSG:3031 *
+                                    * / 3413 / 3976, UPS 32661 / 32761,          *
+                                    * +proj=stere +lat_0=+-90 / +proj=ups; akm1  *
+                                    * in c, |lat_ts| in phi1                     */
 
 typedef struct {
     int32_t kind;

@@ -798,6 +798,24 @@ static int lcc_setup(oracle_crs *c) {
     return 0;
 }
 
+/* ---- stere.cpp (PROJ 6.1.1), polar aspects on an ellipsoid [ext] ----------
+ * Snyder 21-33..21-40: rho = akm1 t(phi) about the pole phi0 = +-pi/2;
+ * |lat_ts| = pi/2 puts k0 at the pole, else true scale on lat_ts. */
+static int stere_polar_setup(oracle_crs *c, int south, int has_ts, double lat_ts) {
+    if (!(c->es > 0)) return -1;
+    c->kind = OR_CRS_STERE_POLAR;
+    c->phi0 = south ? -OR_HALFPI : OR_HALFPI;
+    c->phi1 = fabs(has_ts ? lat_ts : OR_HALFPI);
+    if (fabs(c->phi1 - OR_HALFPI) < 1e-10) {
+        c->c = 2. * c->k0 / sqrt(pow(1 + c->e, 1 + c->e) * pow(1 - c->e, 1 - c->e));
+    } else {
+        double s1 = sin(c->phi1);
+        c->c = cos(c->phi1) / or_tsfn(c->phi1, s1, c->e);
+        c->c /= sqrt(1. - (c->e * s1) * (c->e * s1));
+    }
+    return 0;
+}
+
 static double param_of(const char *s, const char *key, double dflt, int *found) {
     const char *p = s;
     size_t kl = strlen(key);
@@ -835,6 +853,20 @@ int oracle_crs_init(oracle_crs *c, const char *spec) {
         if (code > 32700 && code <= 32760) { set_ellps(c, 6378137.0, 298.257223563); return utm_setup(c, code - 32700, 1); }
         if (code >= 28348 && code <= 28358) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 28300, 1); }
         if (code >= 7846 && code <= 7859) { set_ellps(c, 6378137.0, 298.257222101); return utm_setup(c, code - 7800, 1); }
+        if (code == 3031 || code == 3976) {
+            set_ellps(c, 6378137.0, 298.257223563);
+            return stere_polar_setup(c, 1, 1, (code == 3031 ? -71.0 : -70.0) * OR_D2R);
+        }
+        if (code == 3413) {
+            set_ellps(c, 6378137.0, 298.257223563);
+            c->lam0 = -45.0 * OR_D2R;
+            return stere_polar_setup(c, 0, 1, 70.0 * OR_D2R);
+        }
+        if (code == 32661 || code == 32761) {
+            set_ellps(c, 6378137.0, 298.257223563);
+            c->k0 = 0.994; c->x0 = c->y0 = 2000000.0;
+            return stere_polar_setup(c, code == 32761, 0, 0.0);
+        }
         if (code == 3112 || code == 7845) {
             set_ellps(c, 6378137.0, 298.257222101);
             c->phi1 = -18.0 * OR_D2R; c->phi2 = -36.0 * OR_D2R; c->phi0 = 0.0; c->lam0 = 134.0 * OR_D2R;
@@ -886,6 +918,20 @@ int oracle_crs_init(oracle_crs *c, const char *spec) {
             c->k0 = param_of(spec, "+k_0", 1.0, &fk);
             if (!fk) c->k0 = param_of(spec, "+k", 1.0, NULL);
             return lcc_setup(c);
+        }
+        if (strstr(spec, "+proj=ups")) {
+            set_ellps(c, a, rf);
+            c->k0 = 0.994; c->x0 = c->y0 = 2000000.0; c->lam0 = 0;
+            return stere_polar_setup(c, strstr(spec, "+south") != NULL, 0, 0.0);
+        }
+        if (strstr(spec, "+proj=stere ") || (strlen(spec) >= 11 && !strcmp(spec + strlen(spec) - 11, "+proj=stere"))) {
+            int fts = 0, fk = 0;
+            double ts = param_of(spec, "+lat_ts", 0, &fts) * OR_D2R;
+            set_ellps(c, a, rf);
+            if (fabs(fabs(c->phi0) - OR_HALFPI) >= 1e-10) return -1;
+            c->k0 = param_of(spec, "+k_0", 1.0, &fk);
+            if (!fk) c->k0 = param_of(spec, "+k", 1.0, NULL);
+            return stere_polar_setup(c, c->phi0 < 0, fts, ts);
         }
         if ((strstr(spec, "+proj=tmerc") || strstr(spec, "+proj=etmerc")) && !strstr(spec, "+approx")) {
             int fk = 0;
@@ -966,6 +1012,22 @@ static int crs_inverse(const oracle_crs *c, double x, double y, double *lam, dou
         }
         break;
     }
+    case OR_CRS_STERE_POLAR: {                  /* stere.cpp e_inverse, S_POLE / N_POLE */
+        double sg = c->phi0 < 0 ? -1. : 1.;     /* south: work on the mirrored (north) problem */
+        double ts = hypot(xn, yn) / c->c;
+        double Phi = OR_HALFPI + 2. * atan(ts), prev;   /* PROJ's start: sin() equals the sphere's */
+        int i = 8, done = 0;
+        while (i--) {
+            prev = Phi;
+            double es = c->e * sin(prev);
+            Phi = OR_HALFPI - 2. * atan(ts * pow((1. - es) / (1. + es), .5 * c->e));
+            if (fabs(prev - Phi) < 1e-10) { done = 1; break; }
+        }
+        if (!done) return 0;
+        p = sg * Phi;
+        l = (xn == 0. && yn == 0.) ? 0. : atan2(xn, sg > 0 ? -yn : yn);
+        break;
+    }
     case OR_CRS_TMERC: {                        /* tmerc.cpp exact_e_inv */
         double Cn = (yn - c->tm_zb) / c->tm_qn, Ce = xn / c->tm_qn, dCn, dCe;
         if (!(fabs(Ce) <= 2.623395162778)) return 0;   /* 150 degrees */
@@ -1033,6 +1095,13 @@ static int crs_forward(const oracle_crs *c, double lam, double phi, double *x, d
         double L = lam * c->n;
         xn = c->k0 * (rho * sin(L));
         yn = c->k0 * (c->rho0 - rho * cos(L));
+        break;
+    }
+    case OR_CRS_STERE_POLAR: {                  /* stere.cpp e_forward, S_POLE / N_POLE */
+        double sg = c->phi0 < 0 ? -1. : 1.;
+        double rho = c->c * or_tsfn(sg * phi, sg * sin(phi), c->e);
+        xn = rho * sin(lam);
+        yn = -sg * rho * cos(lam);
         break;
     }
     case OR_CRS_TMERC: {                        /* tmerc.cpp exact_e_fwd */

@@ -115,7 +115,7 @@ int oracle_merge_batch(const oracle_flex_raster *rasters, int n,
                        int mask_inclusive, oracle_canvas *canvases, int n_ns);
 
 /* ---- projections (PROJ 6.1.1 formulas, restated) ------------------------ */
-enum { OR_CRS_LONGLAT = 0, OR_CRS_WEBMERC = 1, OR_CRS_AEA = 2, OR_CRS_SINU = 3, OR_CRS_TMERC = 4, OR_CRS_LCC = 5 };
+enum { OR_CRS_LONGLAT = 0, OR_CRS_WEBMERC = 1, OR_CRS_AEA = 2, OR_CRS_SINU = 3, OR_CRS_TMERC = 4, OR_CRS_LCC = 5, OR_CRS_STERE_POLAR = 6 };
 
 typedef struct {
     int32_t kind;

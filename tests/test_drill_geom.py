@@ -78,7 +78,7 @@ def test_descriptor_known_answers(oracle):
 
 
 @pytest.mark.parametrize("srs,seed", [("EPSG:4326", 1), ("EPSG:4326", 2), ("EPSG:3577", 3), ("EPSG:28355", 4),
-                                      ("EPSG:3112", 5)])
+                                      ("EPSG:3112", 5), ("EPSG:3031", 6)])
 def test_descriptor_matches_oracle(oracle, srs, seed):
     if srs == "EPSG:4326":
         gt, size = GT4326, 2048
@@ -90,6 +90,14 @@ def test_descriptor_matches_oracle(oracle, srs, seed):
         geoms = []
         for p in range(60):
             lon0, lat0 = rng.uniform(144.2, 146.8), rng.uniform(-37.8, -35.6)
+            pts = synth.star_polygon(lon0, lat0, rng.uniform(0.02, 0.3), k=9, seed=p)
+            geoms.append(feature([close(pts)]))
+    elif srs == "EPSG:3031":   # Antarctic polar stereographic: polygons off the Peninsula
+        gt, size = [-2500000.0, 150.0, 0.0, 1500000.0, 0.0, -150.0], 2400
+        rng = np.random.default_rng(seed)
+        geoms = []
+        for p in range(60):
+            lon0, lat0 = rng.uniform(-61.5, -59.3), rng.uniform(-66.8, -65.0)
             pts = synth.star_polygon(lon0, lat0, rng.uniform(0.02, 0.3), k=9, seed=p)
             geoms.append(feature([close(pts)]))
     else:   # Albers dataset: polygons in lon/lat around lon 132, lat -27

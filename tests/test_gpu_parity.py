@@ -251,6 +251,27 @@ def test_warp_windows_lambert_small(gpu, oracle):
     assert frac >= NN_IDENTITY
 
 
+@pytest.mark.parametrize("srs,origin", [("EPSG:3031", (-2400000.0, 1400000.0)),
+                                        ("EPSG:3413", (-200000.0, -2000000.0)),
+                                        ("EPSG:32761", (-400000.0, 4400000.0))])
+def test_warp_windows_polar_small(gpu, oracle, srs, origin):
+    """Polar stereographic granules (Antarctic, NSIDC North, UPS South) -> EPSG:3857."""
+    cfg = synth.config_polar(scale=0.05, tiles_per_side=4, tile_px=128, srs=srs, origin=origin)
+    frac = _check_windows(oracle, cfg, gpu_batch(cfg))
+    assert frac >= NN_IDENTITY
+
+
+def test_render_polar_small(gpu, oracle):
+    import gsky_amd
+    cfg = synth.config_polar(scale=0.1, tiles_per_side=4, tile_px=256)
+    b = gpu_batch(cfg)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True)).cpu().numpy()
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg)
+    assert identity(got, exp) >= NN_IDENTITY
+    assert (exp[..., 3] > 0).mean() > 0.3
+
+
 def test_render_lambert_small(gpu, oracle):
     import gsky_amd
     cfg = synth.config_lambert(scale=0.1, tiles_per_side=4, tile_px=256)
@@ -429,19 +450,21 @@ def test_render_empty_tiles_written(gpu, oracle, typed):
     assert not got[-1].any() and not got[2].any()
 
 
-@pytest.mark.parametrize("dst", ["EPSG:3857", "EPSG:4326", "EPSG:3577", "EPSG:28355", "EPSG:3112", ""])
+@pytest.mark.parametrize("dst", ["EPSG:3857", "EPSG:4326", "EPSG:3577", "EPSG:28355", "EPSG:3112", "EPSG:3031", ""])
 def test_compute_reproject_extent(gpu, oracle, dst):
     """The worker's `extent` op (ComputeReprojectExtent, warp.go:433-487)
     through the C-ABI, against the oracle restatement, for the C1 / C2 / C5
-    granule kinds (lon/lat, Albers, MODIS sinusoidal), a GDA94 / MGA zone 55
-    and a GA Lambert granule and several bboxes."""
+    granule kinds (lon/lat, Albers, MODIS sinusoidal), a GDA94 / MGA zone 55,
+    a GA Lambert and an Antarctic polar stereographic granule and several
+    bboxes."""
     import torch
 
     import gsky_amd.worker as W
     cases = [synth.config_c1(scale=0.2).granules[0], synth.config_c2(scale=0.05, tiles_per_side=2).granules[0],
              synth.config_c5(scale=0.05, dates=1, zooms=((4, 11, 8, 1),), tile_px=64).granules[0],
              synth.config_utm(scale=0.05, tiles_per_side=2).granules[0],
-             synth.config_lambert(scale=0.05, tiles_per_side=2).granules[0]]
+             synth.config_lambert(scale=0.05, tiles_per_side=2).granules[0],
+             synth.config_polar(scale=0.05, tiles_per_side=2).granules[0]]
     W.unregister_all()
     try:
         for k, g in enumerate(cases):
@@ -454,6 +477,7 @@ def test_compute_reproject_extent(gpu, oracle, dst):
             for bb in ([12245143.98, -4865942.28, 15584728.71, -1118889.97], [110.0, -45.0, 155.0, -10.0],
                        [-2000000.0, -4000000.0, 2200000.0, -1000000.0], [200000.0, 5700000.0, 500000.0, 5950000.0],
                        [1350000.0, -4100000.0, 1700000.0, -3750000.0],
+                       [-2500000.0, 1100000.0, -2100000.0, 1500000.0],
                        [0.0, 0.0, 0.0, 0.0]):
                 req = W.GeoRPCGranule(operation="extent", path=path, dstSRS=dst, dstGeot=list(bb))
                 res = W.compute_reproject_extent(req)

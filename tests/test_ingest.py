@@ -457,6 +457,12 @@ GALCC_CF = {"grid_mapping_name": "lambert_conformal_conic", "standard_parallel":
             "semi_major_axis": np.array([6378137.0]), "inverse_flattening": np.array([298.257222101])}
 
 
+PSN_CF = {"grid_mapping_name": "polar_stereographic", "latitude_of_projection_origin": np.array([90.0]),
+          "standard_parallel": np.array([70.0]), "straight_vertical_longitude_from_pole": np.array([-45.0]),
+          "false_easting": np.array([0.0]), "false_northing": np.array([0.0]),
+          "semi_major_axis": np.array([6378137.0]), "inverse_flattening": np.array([298.257223563])}
+
+
 def test_netcdf_srs_cf_option(tmp_path):
     """srs_cf (warp.go:95 -> netcdfdataset.cpp:7023-7025, 3666): without it
     the GDAL WKT's EPSG code wins; with it only the CF grid mapping counts.
@@ -476,7 +482,7 @@ def test_netcdf_srs_cf_option(tmp_path):
     _write_albers_nc(p2, data, x, y, cf=cf)          # CF only: both options agree
     assert ingest.netcdf_srs(p2, 0) == ingest.netcdf_srs(p2, 1) == got
     p3 = str(tmp_path / "c.nc")
-    _write_albers_nc(p3, data, x, y, wkt=wkt, cf={"grid_mapping_name": "polar_stereographic"})
+    _write_albers_nc(p3, data, x, y, wkt=wkt, cf={"grid_mapping_name": "rotated_latitude_longitude"})
     assert ingest.netcdf_srs(p3, 0) == "EPSG:3577" and ingest.netcdf_srs(p3, 1) == "?"
     p4 = str(tmp_path / "d.nc")
     _write_albers_nc(p4, data, x, y, cf={"grid_mapping_name": "sinusoidal", "longitude_of_central_meridian": np.array([0.0]),
@@ -507,6 +513,23 @@ def test_netcdf_srs_cf_option(tmp_path):
     p9 = str(tmp_path / "i.nc")
     _write_albers_nc(p9, data, x, y, cf=dict(GALCC_CF, standard_parallel=np.array([-30.0])))
     assert ingest.netcdf_srs(p9, 1).startswith("+proj=lcc +lat_1=-30 +lat_0=0 +lon_0=134 +k_0=1 ")
+    # polar_stereographic: the polar aspects, by standard parallel or scale at the pole
+    p10 = str(tmp_path / "j.nc")
+    _write_albers_nc(p10, data, x, y, cf=PSN_CF)
+    s10 = ingest.netcdf_srs(p10, 1)
+    assert s10 == "+proj=stere +lat_0=90 +lat_ts=70 +lon_0=-45 +x_0=0 +y_0=0 +a=6378137 +rf=298.25722356300003"
+    c10, e3413 = parse_crs(s10), parse_crs("EPSG:3413")
+    assert c10.kind == 6 and all(getattr(c10, f) == getattr(e3413, f) for f in ("phi0", "phi1", "lam0", "c", "k0"))
+    p11 = str(tmp_path / "k.nc")
+    ups = {k: v for k, v in PSN_CF.items() if k != "standard_parallel"}
+    ups.update(scale_factor_at_projection_origin=np.array([0.994]), straight_vertical_longitude_from_pole=np.array([0.0]),
+               false_easting=np.array([2000000.0]), false_northing=np.array([2000000.0]))
+    _write_albers_nc(p11, data, x, y, cf=ups)
+    c11, e32661 = parse_crs(ingest.netcdf_srs(p11, 1)), parse_crs("EPSG:32661")
+    assert c11.kind == 6 and all(getattr(c11, f) == getattr(e32661, f) for f in ("phi0", "phi1", "lam0", "c", "k0", "x0"))
+    p12 = str(tmp_path / "l.nc")
+    _write_albers_nc(p12, data, x, y, cf=dict(PSN_CF, latitude_of_projection_origin=np.array([60.0])))
+    assert ingest.netcdf_srs(p12, 1) == "?"            # oblique stereographic: not carried
 
 
 @pytest.mark.gpu
@@ -549,7 +572,7 @@ def test_gpu_netcdf_srs_cf_drop_in(tmp_path):
         outs[cf] = got
     assert not np.array_equal(outs[0], outs[1])      # the 0.01 degree meridian shift moves the picks
     p2 = str(tmp_path / "h.nc")
-    _write_albers_nc(p2, data, x, y, wkt=wkt, cf={"grid_mapping_name": "polar_stereographic"})
+    _write_albers_nc(p2, data, x, y, wkt=wkt, cf={"grid_mapping_name": "rotated_latitude_longitude"})
     ok = worker.warp_raster(worker.GeoRPCGranule(path=p2, bands=[1], width=64, height=64, dstSRS="EPSG:3857",
                                                  dstGeot=dgt, sRSCf=0))
     bad = worker.warp_raster(worker.GeoRPCGranule(path=p2, bands=[1], width=64, height=64, dstSRS="EPSG:3857",

@@ -136,7 +136,7 @@ def test_tmerc_srs_forms():
     # without the authority the parameters still define it
     c = P(wkt.replace(',AUTHORITY["EPSG","28355"]]', "]"))
     assert c.kind == 4 and c.lam0 == b.lam0 and c.y0 == b.y0 and c.tm_zb == b.tm_zb
-    for bad in ("EPSG:32600", "EPSG:32661", "EPSG:28347", "+proj=utm +ellps=GRS80", "+proj=utm +zone=61",
+    for bad in ("EPSG:32600", "EPSG:32662", "EPSG:28347", "+proj=utm +ellps=GRS80", "+proj=utm +zone=61",
                 "+proj=tmerc +R=6371000", "+proj=tmerc +approx +ellps=GRS80"):
         with pytest.raises(Exception):
             P(bad)

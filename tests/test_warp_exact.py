@@ -7,8 +7,10 @@ Working Manual, 14-1..14-12; phi1 -18, phi2 -36, phi0 0, lambda0 132),
 EPSG:4326 longitude / latitude for the reference's acceptance tiles (C1 /
 C3's pair), the MODIS sinusoidal sphere (R 6371007.181, Snyder 30-1) for C5's
 tiles, GDA94 / MGA zone 55 Transverse Mercator (Karney 2011's form,
-tests/test_tmerc.py) for UTM granules and Snyder's Lambert Conformal Conic
-equations (tests/test_lcc.py) for GA Lambert granules.  The reference warps through
+tests/test_tmerc.py) for UTM granules, Snyder's Lambert Conformal Conic
+equations (tests/test_lcc.py) for GA Lambert granules and his polar
+stereographic equations (tests/test_stere.py) for Antarctic granules.  The
+reference warps through
 GDAL's approximate transformer with a 0.125-pixel error bound
 (warp.go:219); so for every pixel the picked cell [i, i+1) x [j, j+1) must
 reach within 0.125 px of the exact coordinate, and only pixels whose exact
@@ -219,5 +221,19 @@ def test_warp_lambert_within_the_approximation_bound(gpu):
     assert n_px > 500_000, n_px
     assert worst <= 0.125 + 1e-6, worst
     print("lambert warp vs exact: %d px, %d (%.4f %%) another cell, worst %.4f px"
+          % (n_px, n_diff, 100.0 * n_diff / n_px, worst))
+    assert n_diff / n_px < 0.15
+
+
+def test_warp_polar_within_the_approximation_bound(gpu):
+    """WGS 84 / Antarctic Polar Stereographic (EPSG:3031) -> EPSG:3857: the
+    exact transform is Snyder's polar equations (tests/test_stere.py)."""
+    from .test_stere import WGS84, snyder_polar
+    cfg = synth.config_polar(scale=0.25, tiles_per_side=8, tile_px=256)
+    n_px, n_diff, worst = _check_picks(
+        cfg, gpu, lambda lon, lat: snyder_polar(np.degrees(lon), np.degrees(lat), WGS84, -71.0, 0.0, True))
+    assert n_px > 500_000, n_px
+    assert worst <= 0.125 + 1e-6, worst
+    print("polar stereographic warp vs exact: %d px, %d (%.4f %%) another cell, worst %.4f px"
           % (n_px, n_diff, 100.0 * n_diff / n_px, worst))
     assert n_diff / n_px < 0.15
