@@ -4,12 +4,12 @@
 // gskyhip_drill_descriptors (include/gskyhip.h).
 //
 // The reference goes through OGR/GEOS/GDAL:
-//   OGR_G_Buffer(g, 0, 30)        taken as the identity: for a valid simple
-//                                 polygon GEOS buffer(0) keeps the vertex set
-//                                 (ring start / orientation may change, which
-//                                 the rasterizer below does not depend on,
-//                                 except for edges lying exactly on a pixel-
-//                                 centre line);
+//   OGR_G_Buffer(g, 0, 30)        GEOS 3.7.2's zero-distance buffer
+//                                 (repair.cpp): a valid polygon keeps its
+//                                 vertices (rings turned interior-right);
+//                                 self-intersecting, multiply-wound,
+//                                 overlapping or inside-out rings become the
+//                                 region of depth >= 1;
 //   OGR_G_Transform WGS84 -> SRS  the same PROJ formulas the warp uses
 //                                 (gsky_device.h crs_forward), traditional
 //                                 lon/lat order (drill.go:376);
@@ -56,6 +56,7 @@
 
 #include "../../include/gskyhip.h"
 #include "gsky_device.h"
+#include "repair.h"
 
 namespace gsky {
 namespace {
@@ -63,6 +64,7 @@ namespace {
 struct Rings {
   std::vector<double> x, y;
   std::vector<int> part;   // points per ring
+  std::vector<int> poly;   // polygon of each ring (its first ring is the shell)
 };
 
 // ---------------------------------------------------------------- GeoJSON
@@ -217,6 +219,7 @@ double parse_number(const char *p, char **end) {
 struct Parser {
   const char *p;
   bool ok = true;
+  int npoly = 0;
   void ws() {
     while (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r') p++;
   }
@@ -225,7 +228,11 @@ struct Parser {
     ws();
     if (*p != '[') { ok = false; return; }
     p++;
-    if (depth == ring_depth) r.part.push_back(0);
+    if (depth == ring_depth - 1) npoly++;
+    if (depth == ring_depth) {
+      r.part.push_back(0);
+      r.poly.push_back(npoly);
+    }
     if (depth == ring_depth + 1) {   // [x, y(, z)]
       double v[2];
       for (int k = 0; k < 2; k++) {
@@ -554,7 +561,9 @@ void describe(const char *geometry, const DescribeCtx &c, Descriptor &d) {
   r.x.clear();
   r.y.clear();
   r.part.clear();
+  r.poly.clear();
   if (!parse_geometry(geometry, r)) { d.status = GSKYHIP_E_ARG; return; }
+  buffer0_rings(r.x, r.y, r.part, r.poly);   // OGR_G_Buffer(g, 0, 30); empty -> the rings as drawn
   if (c.reproject)   // WGS84 lon/lat -> dataset SRS, the warp's transform
     for (size_t i = 0; i < r.x.size(); i++) {
       double lam, phi, X, Y;

@@ -1968,10 +1968,10 @@ void oracle_drill_merge(const double *values, const int32_t *counts,
 /* worker/gdalprocess/drill.go:363-423 getDrillFileDescriptor + 275-327      */
 /* createMask, with GDAL 3.0.1's rasterizer (alg/llrasterize.cpp             */
 /* GDALdllImageFilledPolygon + GDALdllImageLineAllTouched, ALL_TOUCHED=TRUE) */
-/* restated [ext].  OGR_G_Buffer(g, 0, 30) is taken as the identity for a    */
-/* valid simple polygon (GEOS buffer(0) keeps its vertex set).               */
+/* restated [ext], after OGR_G_Buffer(g, 0, 30) as GEOS 3.7.2 computes it  */
+/* (rings_buffer0 below).                                                    */
 /* ======================================================================== */
-typedef struct { double *x, *y; int *part_size; int n_parts, n_pts, cap_pts, cap_parts; } or_rings;
+typedef struct { double *x, *y; int *part_size, *part_poly; int n_parts, n_pts, cap_pts, cap_parts, n_polys; } or_rings;
 
 static void rings_push(or_rings *r, double x, double y) {
     if (r->n_pts == r->cap_pts) {
@@ -1986,10 +1986,14 @@ static void rings_new_part(or_rings *r) {
     if (r->n_parts == r->cap_parts) {
         r->cap_parts = r->cap_parts ? 2 * r->cap_parts : 8;
         r->part_size = (int *)realloc(r->part_size, sizeof(int) * r->cap_parts);
+        r->part_poly = (int *)realloc(r->part_poly, sizeof(int) * r->cap_parts);
     }
+    r->part_poly[r->n_parts] = r->n_polys;
     r->part_size[r->n_parts++] = 0;
 }
-static void rings_free(or_rings *r) { free(r->x); free(r->y); free(r->part_size); memset(r, 0, sizeof(*r)); }
+static void rings_free(or_rings *r) {
+    free(r->x); free(r->y); free(r->part_size); free(r->part_poly); memset(r, 0, sizeof(*r));
+}
 
 /* Nested JSON arrays of numbers: depth of the first '[' below `p` decides
  * the level of a ring (Polygon 3 = [ring][pt][xy], MultiPolygon 4). */
@@ -1999,6 +2003,7 @@ static const char *parse_coords(const char *p, int depth, int ring_depth, or_rin
     p = skip_ws(p);
     if (*p != '[') return NULL;
     p++;
+    if (depth == ring_depth - 1) r->n_polys++;  /* a polygon: its first ring is the shell */
     if (depth == ring_depth) rings_new_part(r);
     if (depth == ring_depth + 1) {               /* a point [x, y(, z)] */
         char *e;
@@ -2045,6 +2050,248 @@ static int parse_geojson(const char *js, or_rings *r) {
     const int ring_depth = mp ? 2 : 1;            /* depth (from 0) at which rings start */
     if (!parse_coords(c + 1, 0, ring_depth, r)) return -1;
     return r->n_parts > 0 ? 0 : -1;
+}
+
+/* ---- OGR_G_Buffer(g, 0, 30) (drill.go:364-367) as GEOS 3.7.2 computes a
+ * zero-distance polygon buffer [ext, parity unpinned: GEOS is absent]:
+ * every ring (repeated points removed; a shell under 3 points drops its
+ * polygon, a ring under 4 points is skipped) is a curve whose sides carry a
+ * depth step: +1 across it from the right to the left for a shell that
+ * CGAlgorithms::isCCW calls counter-clockwise (interior left) or a hole it
+ * calls clockwise, -1 otherwise.  The curves are noded (crossings, touches,
+ * collinear overlaps), equal edges merged with their steps added, and the
+ * result is the region of depth >= 1 (depth 0 far outside): its boundary
+ * edges, interior on their right.  Here the depth at a point is the step-
+ * weighted winding number over all edges, brute force; a polygon already
+ * valid keeps its vertices (rings turned interior-right).  An empty result
+ * keeps the rings as drawn (drill.go:366). */
+typedef struct { double ax, ay, bx, by; int q, ring; } or_seg;
+
+static int or_orient(double ax, double ay, double bx, double by, double cx, double cy) {
+    const long double d = (long double)(bx - ax) * (long double)(cy - ay) - (long double)(by - ay) * (long double)(cx - ax);
+    return (d > 0) - (d < 0);
+}
+
+/* CGAlgorithms::isCCW: the turn at the first highest vertex of a closed ring */
+static int or_ring_ccw(const double *x, const double *y, int n) {
+    int hi = 0, last = n - 1;
+    for (int i = 1; i <= last; i++) if (y[i] > y[hi]) hi = i;
+    int a = hi, b = hi;
+    do { a = a == 0 ? last : a - 1; } while (x[a] == x[hi] && y[a] == y[hi] && a != hi);
+    do { b = (b + 1) % last; } while (x[b] == x[hi] && y[b] == y[hi] && b != hi);
+    if ((x[a] == x[hi] && y[a] == y[hi]) || (x[b] == x[hi] && y[b] == y[hi]) || (x[a] == x[b] && y[a] == y[b])) return 0;
+    const int o = or_orient(x[a], y[a], x[hi], y[hi], x[b], y[b]);
+    return o == 0 ? x[a] > x[b] : o > 0;
+}
+
+/* Sunday's winding rule, one edge, weight q */
+static int or_wind(const or_seg *e, double px, double py) {
+    if (e->ay <= py) return (e->by > py && or_orient(e->ax, e->ay, e->bx, e->by, px, py) > 0) ? e->q : 0;
+    return (e->by <= py && or_orient(e->ax, e->ay, e->bx, e->by, px, py) < 0) ? -e->q : 0;
+}
+
+/* depth just right of edge k: the other edges' winding at its midpoint plus its own share */
+static int or_depth_right(const or_seg *s, int n, int k) {
+    const double mx = 0.5 * (s[k].ax + s[k].bx), my = 0.5 * (s[k].ay + s[k].by);
+    int d = 0;
+    for (int f = 0; f < n; f++) if (f != k) d += or_wind(&s[f], mx, my);
+    if (s[k].ay == s[k].by) return s[k].ax < s[k].bx ? d - s[k].q : d;   /* d = depth above */
+    return s[k].by < s[k].ay ? d - s[k].q : d;
+}
+
+static int on_open_seg(double ax, double ay, double bx, double by, double px, double py) {
+    if ((px == ax && py == ay) || (px == bx && py == by)) return 0;
+    return fmin(ax, bx) <= px && px <= fmax(ax, bx) && fmin(ay, by) <= py && py <= fmax(ay, by);
+}
+
+typedef struct { double x, y; } or_pt;
+typedef struct { or_pt *p; int n, cap; } or_ptlist;
+static void ptl_push(or_ptlist *l, double x, double y) {
+    if (l->n == l->cap) { l->cap = l->cap ? 2 * l->cap : 4; l->p = (or_pt *)realloc(l->p, sizeof(or_pt) * l->cap); }
+    l->p[l->n].x = x; l->p[l->n].y = y; l->n++;
+}
+static int pt_lt(double ax, double ay, double bx, double by) { return ax < bx || (ax == bx && ay < by); }
+static int cmp_seg_key(const void *u, const void *v) {
+    const or_seg *a = (const or_seg *)u, *b = (const or_seg *)v;
+    if (pt_lt(a->ax, a->ay, b->ax, b->ay)) return -1;
+    if (pt_lt(b->ax, b->ay, a->ax, a->ay)) return 1;
+    if (pt_lt(a->bx, a->by, b->bx, b->by)) return -1;
+    if (pt_lt(b->bx, b->by, a->bx, a->by)) return 1;
+    return 0;
+}
+static const or_seg *g_sort_seg;
+static int cmp_by_xmin(const void *u, const void *v) {
+    const or_seg *a = &g_sort_seg[*(const int *)u], *b = &g_sort_seg[*(const int *)v];
+    const double x = fmin(a->ax, a->bx), y = fmin(b->ax, b->bx);
+    return (x > y) - (x < y);
+}
+static double g_dx, g_dy, g_ox, g_oy;
+static int cmp_along(const void *u, const void *v) {
+    const or_pt *a = (const or_pt *)u, *b = (const or_pt *)v;
+    const double s = (a->x - g_ox) * g_dx + (a->y - g_oy) * g_dy, t = (b->x - g_ox) * g_dx + (b->y - g_oy) * g_dy;
+    return (s > t) - (s < t);
+}
+
+static void rings_buffer0(or_rings *r) {
+    /* the curves */
+    int cap = r->n_pts + 8, ns = 0, ncurves = 0;
+    or_seg *s = (or_seg *)malloc(sizeof(or_seg) * cap);
+    int *cstart = (int *)malloc(sizeof(int) * (r->n_parts + 1)), *cq = (int *)malloc(sizeof(int) * (r->n_parts + 1));
+    double *cx = (double *)malloc(sizeof(double) * (r->n_pts + 1)), *cy = (double *)malloc(sizeof(double) * (r->n_pts + 1));
+    int skip = 0;
+    for (int k = 0, off = 0; k < r->n_parts; off += r->part_size[k++]) {
+        const int shell = k == 0 || r->part_poly[k] != r->part_poly[k - 1];
+        int n = 0;
+        for (int i = 0; i < r->part_size[k]; i++)
+            if (n == 0 || cx[n - 1] != r->x[off + i] || cy[n - 1] != r->y[off + i]) { cx[n] = r->x[off + i]; cy[n] = r->y[off + i]; n++; }
+        if (shell) skip = n < 3;
+        if (skip) continue;
+        if (n > 0 && (cx[0] != cx[n - 1] || cy[0] != cy[n - 1])) { cx[n] = cx[0]; cy[n] = cy[0]; n++; }
+        if (n < 4) continue;
+        const int q = (shell ? 1 : -1) * (or_ring_ccw(cx, cy, n) ? 1 : -1);
+        cstart[ncurves] = ns; cq[ncurves] = q;
+        for (int i = 0; i + 1 < n; i++) {
+            or_seg e = {cx[i], cy[i], cx[i + 1], cy[i + 1], q, ncurves};
+            s[ns++] = e;
+        }
+        ncurves++;
+    }
+    cstart[ncurves] = ns;
+    free(cx); free(cy);
+    if (ns == 0) { free(s); free(cstart); free(cq); return; }
+
+    /* noding: pairs from a sweep in x */
+    or_ptlist *sp = (or_ptlist *)calloc(ns, sizeof(or_ptlist));
+    int *ord = (int *)malloc(sizeof(int) * ns), split = 0, overlap = 0, touch = 0;
+    for (int i = 0; i < ns; i++) ord[i] = i;
+    g_sort_seg = s;
+    qsort(ord, ns, sizeof(int), cmp_by_xmin);
+    for (int u = 0; u < ns; u++) {
+        for (int v = u + 1; v < ns && fmin(s[ord[v]].ax, s[ord[v]].bx) <= fmax(s[ord[u]].ax, s[ord[u]].bx); v++) {
+            const int i = ord[u] < ord[v] ? ord[u] : ord[v], j = ord[u] < ord[v] ? ord[v] : ord[u];
+            const or_seg *a = &s[i], *b = &s[j];
+            if (fmax(a->ay, a->by) < fmin(b->ay, b->by) || fmax(b->ay, b->by) < fmin(a->ay, a->by)) continue;
+            const int o1 = or_orient(b->ax, b->ay, b->bx, b->by, a->ax, a->ay), o2 = or_orient(b->ax, b->ay, b->bx, b->by, a->bx, a->by);
+            const int o3 = or_orient(a->ax, a->ay, a->bx, a->by, b->ax, b->ay), o4 = or_orient(a->ax, a->ay, a->bx, a->by, b->bx, b->by);
+            if (!o1 && !o2 && !o3 && !o4) {
+                const int alongx = fabs(a->bx - a->ax) >= fabs(a->by - a->ay);
+                const double a0 = alongx ? fmin(a->ax, a->bx) : fmin(a->ay, a->by), a1 = alongx ? fmax(a->ax, a->bx) : fmax(a->ay, a->by);
+                const double b0 = alongx ? fmin(b->ax, b->bx) : fmin(b->ay, b->by), b1 = alongx ? fmax(b->ax, b->bx) : fmax(b->ay, b->by);
+                if (fmin(a1, b1) > fmax(a0, b0)) overlap = 1;
+                if (on_open_seg(a->ax, a->ay, a->bx, a->by, b->ax, b->ay)) { ptl_push(&sp[i], b->ax, b->ay); split = 1; }
+                if (on_open_seg(a->ax, a->ay, a->bx, a->by, b->bx, b->by)) { ptl_push(&sp[i], b->bx, b->by); split = 1; }
+                if (on_open_seg(b->ax, b->ay, b->bx, b->by, a->ax, a->ay)) { ptl_push(&sp[j], a->ax, a->ay); split = 1; }
+                if (on_open_seg(b->ax, b->ay, b->bx, b->by, a->bx, a->by)) { ptl_push(&sp[j], a->bx, a->by); split = 1; }
+                continue;
+            }
+            if (o1 * o2 < 0 && o3 * o4 < 0) {
+                const double dx = a->bx - a->ax, dy = a->by - a->ay, ex = b->bx - b->ax, ey = b->by - b->ay;
+                const double kk = ((b->ax - a->ax) * ey - (b->ay - a->ay) * ex) / (dx * ey - dy * ex);
+                double px = a->ax + kk * dx, py = a->ay + kk * dy;
+                px = fmin(fmax(px, fmax(fmin(a->ax, a->bx), fmin(b->ax, b->bx))), fmin(fmax(a->ax, a->bx), fmax(b->ax, b->bx)));
+                py = fmin(fmax(py, fmax(fmin(a->ay, a->by), fmin(b->ay, b->by))), fmin(fmax(a->ay, a->by), fmax(b->ay, b->by)));
+                ptl_push(&sp[i], px, py); ptl_push(&sp[j], px, py);
+                split = 1;
+                continue;
+            }
+            if (!o3 && on_open_seg(a->ax, a->ay, a->bx, a->by, b->ax, b->ay)) { ptl_push(&sp[i], b->ax, b->ay); split = 1; }
+            if (!o4 && on_open_seg(a->ax, a->ay, a->bx, a->by, b->bx, b->by)) { ptl_push(&sp[i], b->bx, b->by); split = 1; }
+            if (!o1 && on_open_seg(b->ax, b->ay, b->bx, b->by, a->ax, a->ay)) { ptl_push(&sp[j], a->ax, a->ay); split = 1; }
+            if (!o2 && on_open_seg(b->ax, b->ay, b->bx, b->by, a->bx, a->by)) { ptl_push(&sp[j], a->bx, a->by); split = 1; }
+            const int shares = (a->ax == b->ax && a->ay == b->ay) || (a->ax == b->bx && a->ay == b->by) ||
+                               (a->bx == b->ax && a->by == b->ay) || (a->bx == b->bx && a->by == b->by);
+            const int len = a->ring == b->ring ? cstart[a->ring + 1] - cstart[a->ring] : 0;
+            if (shares && !(a->ring == b->ring && (j - i == 1 || j - i == len - 1))) touch = 1;
+        }
+    }
+    free(ord);
+
+    int done = 0;
+    if (!split && !overlap && !touch) {            /* valid: keep the vertices, interior right */
+        int ok = 1;
+        int *flip = (int *)malloc(sizeof(int) * ncurves);
+        for (int c = 0; c < ncurves && ok; c++) {
+            const int dr = or_depth_right(s, ns, cstart[c]), dl = dr + cq[c];
+            ok = (dr == 1 && dl == 0) || (dr == 0 && dl == 1);
+            flip[c] = dl == 1;
+        }
+        if (ok) {
+            or_rings out;
+            memset(&out, 0, sizeof(out));
+            for (int c = 0; c < ncurves; c++) {
+                rings_new_part(&out);
+                const int a = cstart[c], b = cstart[c + 1];
+                if (!flip[c]) { for (int k = a; k < b; k++) rings_push(&out, s[k].ax, s[k].ay); rings_push(&out, s[b - 1].bx, s[b - 1].by); }
+                else { for (int k = b - 1; k >= a; k--) rings_push(&out, s[k].bx, s[k].by); rings_push(&out, s[a].ax, s[a].ay); }
+            }
+            rings_free(r);
+            *r = out;
+            done = 1;
+        }
+        free(flip);
+    }
+    if (!done) {
+        /* noded edges in canonical direction (lesser point first), merged */
+        int ne = 0, ecap = ns + 16;
+        or_seg *e = (or_seg *)malloc(sizeof(or_seg) * ecap);
+        for (int k = 0; k < ns; k++) {
+            g_ox = s[k].ax; g_oy = s[k].ay; g_dx = s[k].bx - s[k].ax; g_dy = s[k].by - s[k].ay;
+            if (sp[k].n) qsort(sp[k].p, sp[k].n, sizeof(or_pt), cmp_along);
+            double px = s[k].ax, py = s[k].ay;
+            for (int t = 0; t <= sp[k].n; t++) {
+                const double qx = t < sp[k].n ? sp[k].p[t].x : s[k].bx, qy = t < sp[k].n ? sp[k].p[t].y : s[k].by;
+                if (qx == px && qy == py) continue;
+                if (ne == ecap) { ecap *= 2; e = (or_seg *)realloc(e, sizeof(or_seg) * ecap); }
+                if (pt_lt(px, py, qx, qy)) { or_seg x = {px, py, qx, qy, s[k].q, -1}; e[ne++] = x; }
+                else { or_seg x = {qx, qy, px, py, -s[k].q, -1}; e[ne++] = x; }
+                px = qx; py = qy;
+            }
+        }
+        qsort(e, ne, sizeof(or_seg), cmp_seg_key);
+        int nu = 0;
+        for (int k = 0; k < ne; k++) {
+            if (nu && !cmp_seg_key(&e[nu - 1], &e[k])) e[nu - 1].q += e[k].q;
+            else e[nu++] = e[k];
+        }
+        int m = 0;
+        for (int k = 0; k < nu; k++) if (e[k].q) e[m++] = e[k];
+        /* result edges, directed interior-right */
+        or_seg *res = (or_seg *)malloc(sizeof(or_seg) * (m + 1));
+        int nr = 0;
+        for (int k = 0; k < m; k++) {
+            const int dr = or_depth_right(e, m, k), dl = dr + e[k].q;
+            if (dr >= 1 && dl <= 0) { or_seg x = {e[k].ax, e[k].ay, e[k].bx, e[k].by, 0, 0}; res[nr++] = x; }
+            else if (dl >= 1 && dr <= 0) { or_seg x = {e[k].bx, e[k].by, e[k].ax, e[k].ay, 0, 0}; res[nr++] = x; }
+        }
+        if (nr) {                                  /* chain them into closed rings */
+            or_rings out;
+            memset(&out, 0, sizeof(out));
+            char *used = (char *)calloc(nr, 1);
+            for (int k0 = 0; k0 < nr; k0++) {
+                if (used[k0]) continue;
+                rings_new_part(&out);
+                rings_push(&out, res[k0].ax, res[k0].ay);
+                int k = k0;
+                for (;;) {
+                    used[k] = 1;
+                    rings_push(&out, res[k].bx, res[k].by);
+                    if (res[k].bx == res[k0].ax && res[k].by == res[k0].ay) break;
+                    int nxt = -1;
+                    for (int t = 0; t < nr && nxt < 0; t++)
+                        if (!used[t] && res[t].ax == res[k].bx && res[t].ay == res[k].by) nxt = t;
+                    if (nxt < 0) { rings_push(&out, res[k0].ax, res[k0].ay); break; }
+                    k = nxt;
+                }
+            }
+            free(used);
+            rings_free(r);
+            *r = out;
+        }
+        free(res);
+        free(e);
+    }
+    for (int k = 0; k < ns; k++) free(sp[k].p);
+    free(sp); free(s); free(cstart); free(cq);
 }
 
 static int point_in_rings(const or_rings *r, double px, double py) {   /* even-odd over all rings */
@@ -2237,6 +2484,7 @@ int oracle_drill_descriptor(const char *geometry_json, const oracle_crs *ds_crs,
     or_rings r;
     memset(&r, 0, sizeof(r));
     if (parse_geojson(geometry_json, &r)) { rings_free(&r); return -1; }
+    rings_buffer0(&r);                              /* drill.go:364-367 */
     if (ds_crs) {                                   /* drill.go:371-380: WGS84 lon/lat -> dataset SRS */
         oracle_crs wgs;
         oracle_crs_init(&wgs, "EPSG:4326");
