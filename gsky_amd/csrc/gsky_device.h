@@ -240,9 +240,17 @@ __host__ __device__ inline __attribute__((noinline)) bool tm_inv(const gskyhip_c
 // algorithm -- Snyder, Map Projections: A Working Manual, 15-1..15-11 --
 // pinned by Snyder's worked example in tests/test_lcc.py).  Out of line for
 // the same register reason as tm_fwd.
+// The transcendental calls of lcc / stere out of line: inlined, the
+// scheduler overlapped their bodies and took lcc_inv / stere_inv to 248 VGPRs,
+// which the planners that may call them inherit (same functions, same bits).
+__host__ __device__ inline __attribute__((noinline)) double ext_pow(double a, double b) { return pow(a, b); }
+__host__ __device__ inline __attribute__((noinline)) double ext_atan(double a) { return atan(a); }
+__host__ __device__ inline __attribute__((noinline)) double ext_tan(double a) { return tan(a); }
+__host__ __device__ inline __attribute__((noinline)) double ext_sin(double a) { return sin(a); }
+
 __host__ __device__ inline double lcc_tsfn(double phi, double sinphi, double e) {
   sinphi *= e;
-  return tan(.5 * (kHalfPi - phi)) / pow((1. - sinphi) / (1. + sinphi), .5 * e);
+  return ext_tan(.5 * (kHalfPi - phi)) / ext_pow((1. - sinphi) / (1. + sinphi), .5 * e);
 }
 
 __host__ __device__ inline __attribute__((noinline)) bool lcc_fwd(const gskyhip_crs &c, double lam, double phi,
@@ -252,10 +260,10 @@ __host__ __device__ inline __attribute__((noinline)) bool lcc_fwd(const gskyhip_
     if (phi * c.n <= 0.) return false;
     rho = 0.;
   } else {
-    rho = c.c * pow(lcc_tsfn(phi, sin(phi), c.e), c.n);
+    rho = c.c * ext_pow(lcc_tsfn(phi, ext_sin(phi), c.e), c.n);
   }
   lam *= c.n;
-  xn = c.k0 * (rho * sin(lam));
+  xn = c.k0 * (rho * ext_sin(lam));
   yn = c.k0 * (c.rho0 - rho * cos(lam));
   return true;
 }
@@ -268,13 +276,13 @@ __host__ __device__ inline __attribute__((noinline)) bool lcc_inv(const gskyhip_
   double rho = hypot(xn, yn);
   if (rho != 0.) {
     if (c.n < 0.) { rho = -rho; xn = -xn; yn = -yn; }
-    const double ts = pow(rho / c.c, 1. / c.n);   // pj_phi2
+    const double ts = ext_pow(rho / c.c, 1. / c.n);   // pj_phi2
     const double eccnth = .5 * c.e;
-    double Phi = kHalfPi - 2. * atan(ts), dphi;
+    double Phi = kHalfPi - 2. * ext_atan(ts), dphi;
     int i = 15;
     do {
-      const double con = c.e * sin(Phi);
-      dphi = kHalfPi - 2. * atan(ts * pow((1. - con) / (1. + con), eccnth)) - Phi;
+      const double con = c.e * ext_sin(Phi);
+      dphi = kHalfPi - 2. * ext_atan(ts * ext_pow((1. - con) / (1. + con), eccnth)) - Phi;
       Phi += dphi;
     } while (fabs(dphi) > 1.0e-10 && --i);
     if (i <= 0) return false;
@@ -294,8 +302,8 @@ __host__ __device__ inline __attribute__((noinline)) bool lcc_inv(const gskyhip_
 __host__ __device__ inline __attribute__((noinline)) bool stere_fwd(const gskyhip_crs &c, double lam, double phi,
                                                                      double &xn, double &yn) {
   double coslam = cos(lam);
-  const double sinlam = sin(lam);
-  double sinphi = sin(phi);
+  const double sinlam = ext_sin(lam);
+  double sinphi = ext_sin(phi);
   if (c.phi0 < 0) {   // S_POLE
     phi = -phi;
     coslam = -coslam;
@@ -312,10 +320,11 @@ __host__ __device__ inline __attribute__((noinline)) bool stere_inv(const gskyhi
   const double rho = hypot(xn, yn);
   if (c.phi0 >= 0) yn = -yn;   // N_POLE
   const double tp = -rho / c.c, halfpi = -kHalfPi, halfe = -.5 * c.e;
-  double phi_l = kHalfPi - 2. * atan(tp);
+  double phi_l = kHalfPi - 2. * ext_atan(tp);
+#pragma unroll 1
   for (int i = 8; i--; phi_l = phi) {
-    const double sinphi = c.e * sin(phi_l);
-    phi = 2. * atan(tp * pow((1. + sinphi) / (1. - sinphi), halfe)) - halfpi;
+    const double sinphi = c.e * ext_sin(phi_l);
+    phi = 2. * ext_atan(tp * ext_pow((1. + sinphi) / (1. - sinphi), halfe)) - halfpi;
     if (fabs(phi_l - phi) < 1.e-10) {
       if (c.phi0 < 0) phi = -phi;
       lam = (xn == 0. && yn == 0.) ? 0. : atan2(xn, yn);
