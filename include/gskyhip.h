@@ -565,7 +565,10 @@ int gskyhip_drill(const float *stack, int xsize, int ysize, int n_bands, int t_s
 /* getDrillFileDescriptor + createMask (drill.go:363-423, 275-327) for n
  * request geometries against one dataset (HOST function, no device work):
  *   geometries: GeoJSON (a Feature or a bare Polygon / MultiPolygon) in
- *     WGS84 lon/lat, as GeoRPCGranule.Geometry;
+ *     WGS84 lon/lat, as GeoRPCGranule.Geometry; first repaired as
+ *     OGR_G_Buffer(g, 0, 30) does it (drill.go:364-367, GEOS 3.7.2's
+ *     zero-distance buffer: self-intersecting / overlapping rings become the
+ *     region of depth >= 1; an empty buffer keeps the rings as drawn);
  *   dataset_srs: the dataset's SRS (NULL / "" = no projection: no transform);
  *   geot, xsize, ysize: the dataset's geotransform and size.
  * Per polygon: win_out[4*i..] = {off_x, off_y, count_x, count_y} with the
