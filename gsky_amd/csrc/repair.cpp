@@ -74,6 +74,7 @@ inline DD dd_sub(DD a, DD b) {
   return {r, e - (r - s)};
 }
 int orient(const Pt &a, const Pt &b, const Pt &c) {
+  if (same(c, a) || same(c, b)) return 0;
   const double l = (b.x - a.x) * (c.y - a.y), r = (b.y - a.y) * (c.x - a.x);
   const double det = l - r, bound = 1e-15 * (std::fabs(l) + std::fabs(r));
   if (det > bound) return 1;
@@ -163,19 +164,23 @@ inline int winding(const Seg &e, const Pt &p) {
 struct Depth {
   const std::vector<Seg> &s;
   Bands b;
-  explicit Depth(const std::vector<Seg> &s_) : s(s_) { b.build(s_); }
-  // depth just right of segment k (at its midpoint): the winding sum of the
-  // other segments of the midpoint's band, plus k's own share
+  const bool banded;
+  explicit Depth(const std::vector<Seg> &s_) : s(s_), banded(s_.size() >= 48) { if (banded) b.build(s_); }
   int right_of(size_t k) const {
     const Seg &e = s[k];
     const Pt m{0.5 * (e.a.x + e.b.x), 0.5 * (e.a.y + e.b.y)};
-    const int j = b.band(m.y);
     int d = 0;
-    for (int t = b.start[j]; t < b.start[j + 1]; t++)
-      if ((size_t)b.ids[t] != k) d += winding(s[b.ids[t]], m);
-    if (e.a.y == e.b.y)   // horizontal: d is the depth above; above is left when a.x < b.x
+    if (banded) {
+      const int j = b.band(m.y);
+      for (int t = b.start[j]; t < b.start[j + 1]; t++)
+        if ((size_t)b.ids[t] != k) d += winding(s[b.ids[t]], m);
+    } else {
+      for (size_t t = 0; t < s.size(); t++)
+        if (t != k) d += winding(s[t], m);
+    }
+    if (e.a.y == e.b.y)
       return e.a.x < e.b.x ? d - e.q : d;
-    return e.b.y < e.a.y ? d - e.q : d;   // a downward edge's right side sees it on the ray
+    return e.b.y < e.a.y ? d - e.q : d;
   }
 };
 
@@ -190,18 +195,26 @@ inline bool strictly_inside(const Pt &a, const Pt &b, const Pt &p) {
 
 bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<int> &part,
                    const std::vector<int> &poly) {
+  // per-thread scratch (the descriptors run on a thread pool, a polygon per
+  // call): grown, never freed, so a valid polygon allocates nothing
+  thread_local std::vector<std::vector<Pt>> curves_s;
+  thread_local std::vector<int> curve_q_s, order_s;
+  thread_local std::vector<Seg> segs_s;
+  thread_local std::vector<std::vector<Pt>> splits_s;
+  std::vector<int> &curve_q = curve_q_s, &order = order_s;
+  std::vector<Seg> &segs = segs_s;
+  curve_q.clear();
+  segs.clear();
+  size_t ncurves = 0;
   // ---- the offset curves: rings without repeated points, closed
-  std::vector<std::vector<Pt>> curves;
-  std::vector<int> curve_q;
-  std::vector<Seg> segs;
-  segs.reserve(X.size());
   {
     size_t off = 0;
     bool skip_poly = false;
     for (size_t r = 0; r < part.size(); off += part[r], r++) {
       const bool shell = r == 0 || poly[r] != poly[r - 1];
-      std::vector<Pt> c;
-      c.reserve(part[r] + 1);
+      if (curves_s.size() <= ncurves) curves_s.resize(ncurves + 1);
+      std::vector<Pt> &c = curves_s[ncurves];
+      c.clear();
       for (int i = 0; i < part[r]; i++) {
         const Pt p{X[off + i], Y[off + i]};
         if (c.empty() || !same(c.back(), p)) c.push_back(p);
@@ -211,22 +224,25 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
       if (!c.empty() && !same(c.front(), c.back())) c.push_back(c.front());
       if (c.size() < 4) continue;
       const int q = (shell ? 1 : -1) * (is_ccw(c.data(), (int)c.size()) ? 1 : -1);
-      const int id = (int)curves.size();
+      const int id = (int)ncurves;
       for (size_t i = 0; i + 1 < c.size(); i++) segs.push_back({c[i], c[i + 1], q, id});
-      curves.push_back(std::move(c));
+      ncurves++;
       curve_q.push_back(q);
     }
   }
+  const std::vector<std::vector<Pt>> &curves = curves_s;
   if (segs.empty()) return false;
 
   // ---- noding: split points of every segment, candidate pairs from a sweep
   // over the segments sorted by their least x
   const size_t M = segs.size();
-  std::vector<int> order(M);
+  order.resize(M);
   for (size_t k = 0; k < M; k++) order[k] = (int)k;
   auto xlo = [&](int k) { return std::min(segs[k].a.x, segs[k].b.x); };
   std::sort(order.begin(), order.end(), [&](int u, int v) { return xlo(u) < xlo(v); });
-  std::vector<std::vector<Pt>> splits(M);
+  if (splits_s.size() < M) splits_s.resize(M);
+  for (size_t k = 0; k < M; k++) splits_s[k].clear();
+  std::vector<std::vector<Pt>> &splits = splits_s;
   bool any_split = false, overlap = false, touch = false;
   for (size_t u = 0; u < M; u++) {
     const int i0 = order[u];
@@ -236,8 +252,10 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
       const Seg &s = segs[i], &t = segs[j];
       if (std::max(s.a.y, s.b.y) < std::min(t.a.y, t.b.y) || std::max(t.a.y, t.b.y) < std::min(s.a.y, s.b.y))
         continue;
-      const int o1 = orient(t.a, t.b, s.a), o2 = orient(t.a, t.b, s.b);
       const int o3 = orient(s.a, s.b, t.a), o4 = orient(s.a, s.b, t.b);
+      if (o3 * o4 > 0) continue;   // t wholly on one side of s: no contact
+      const int o1 = orient(t.a, t.b, s.a), o2 = orient(t.a, t.b, s.b);
+      if (o1 * o2 > 0) continue;
       if (o1 == 0 && o2 == 0 && o3 == 0 && o4 == 0) {   // collinear
         const bool xs = std::fabs(s.b.x - s.a.x) >= std::fabs(s.b.y - s.a.y);
         const double s0 = xs ? std::min(s.a.x, s.b.x) : std::min(s.a.y, s.b.y);
@@ -282,19 +300,19 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
   // ---- a valid polygon: vertices kept, each ring turned interior-right
   if (!any_split && !overlap && !touch) {
     const Depth dep(segs);
-    std::vector<int> first(curves.size(), -1);
+    std::vector<int> first(ncurves, -1);
     for (size_t k = 0; k < segs.size(); k++)
       if (first[segs[k].ring] < 0) first[segs[k].ring] = (int)k;
     bool valid = true;
-    std::vector<bool> flip(curves.size());
-    for (size_t c = 0; c < curves.size() && valid; c++) {
+    std::vector<bool> flip(ncurves);
+    for (size_t c = 0; c < ncurves && valid; c++) {
       const int dr = dep.right_of(first[c]), dl = dr + curve_q[c];
       valid = (dr == 1 && dl == 0) || (dr == 0 && dl == 1);
       flip[c] = dl == 1;
     }
     if (valid) {
       X.clear(); Y.clear(); part.clear();
-      for (size_t c = 0; c < curves.size(); c++) {
+      for (size_t c = 0; c < ncurves; c++) {
         const std::vector<Pt> &v = curves[c];
         for (size_t i = 0; i < v.size(); i++) {
           const Pt &p = flip[c] ? v[v.size() - 1 - i] : v[i];
