@@ -7,6 +7,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 stop() { echo "[$2] rc=$1"; if [ "$1" -ne 0 ]; then echo "stopping after $2"; exit "$1"; fi; }
+# part 1's PMC summaries of this build, when run in the same call (bench.py
+# reads profiles/ and takes them only when their lib_sha16 is this library's)
+for f in pmc_render_c2.json pmc_bil_c3.json pmc_render_c5.json; do
+  if [ -f gpurun_out/$f ]; then cp gpurun_out/$f profiles/$f; fi
+done
 timeout -k 10 900 python -u bench.py > gpurun_out/r05z_bench.json 2> gpurun_out/r05z_bench.err
 stop $? bench
 python3 -c "
