@@ -34,7 +34,8 @@
 // from the rings as drawn for self-intersecting or multiply-wound rings (a
 // bow-tie keeps only the lobe of its highest vertex's orientation), holes
 // outside their shell, nested or overlapping polygons (unioned), and
-// zero-area spikes (removed).  Parity unpinned beyond the oracle's separate
+// zero-area spikes (removed).  A geometry with more than 2^16 self-crossings
+// is left as drawn.  Parity unpinned beyond the oracle's separate
 // restatement: GEOS is absent from this image.
 #include "repair.h"
 
@@ -104,6 +105,10 @@ bool is_ccw(const Pt *p, int n) {
   return d == 0 ? p[ip].x > p[in].x : d > 0;
 }
 
+// a ring crossing itself more often than this (a hostile request, not a
+// boundary) is left as drawn rather than noded without bound
+constexpr size_t kMaxCrossings = size_t(1) << 16;   // per geometry
+
 struct Seg {
   Pt a, b;
   int q;      // depth(left) - depth(right)
@@ -118,7 +123,7 @@ struct Bands {
   std::vector<int> start, ids;
   int band(double y) const {
     const double v = (y - y0) / sy;
-    return v <= 0 ? 0 : v >= n - 1 ? n - 1 : (int)v;
+    return !(v > 0) ? 0 : v >= n - 1 ? n - 1 : (int)v;   // NaN (non-finite input) -> band 0
   }
   void build(const std::vector<Seg> &s) {
     const size_t m = s.size();
@@ -161,11 +166,33 @@ inline int winding(const Seg &e, const Pt &p) {
   return 0;
 }
 
+// Depth just right of segment k (at its midpoint): the winding sum of the
+// other segments -- those of the midpoint's band, or all of them for a small
+// set -- plus k's own share.  A set wider than tall is cast in a frame turned
+// by -90 degrees ((x, y) -> (y, -x), exact), so the rays run across its short
+// side; the winding numbers are the same.
 struct Depth {
   const std::vector<Seg> &s;
   Bands b;
   const bool banded;
-  explicit Depth(const std::vector<Seg> &s_) : s(s_), banded(s_.size() >= 48) { if (banded) b.build(s_); }
+  Depth(const std::vector<Seg> &s0, std::vector<Seg> &turned) : s(pick(s0, turned)), banded(s.size() >= 48) {
+    if (banded) b.build(s);
+  }
+  static const std::vector<Seg> &pick(const std::vector<Seg> &s0, std::vector<Seg> &turned) {
+    if (s0.size() < 48) return s0;
+    double x0 = HUGE_VAL, x1 = -HUGE_VAL, y0 = HUGE_VAL, y1 = -HUGE_VAL;
+    for (const Seg &e : s0) {
+      x0 = std::min(x0, std::min(e.a.x, e.b.x)); x1 = std::max(x1, std::max(e.a.x, e.b.x));
+      y0 = std::min(y0, std::min(e.a.y, e.b.y)); y1 = std::max(y1, std::max(e.a.y, e.b.y));
+    }
+    if (!(x1 - x0 > y1 - y0)) return s0;
+    turned.resize(s0.size());
+    for (size_t k = 0; k < s0.size(); k++) {
+      const Seg &e = s0[k];
+      turned[k] = {{e.a.y, -e.a.x}, {e.b.y, -e.b.x}, e.q, e.ring};
+    }
+    return turned;
+  }
   int right_of(size_t k) const {
     const Seg &e = s[k];
     const Pt m{0.5 * (e.a.x + e.b.x), 0.5 * (e.a.y + e.b.y)};
@@ -244,6 +271,7 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
   for (size_t k = 0; k < M; k++) splits_s[k].clear();
   std::vector<std::vector<Pt>> &splits = splits_s;
   bool any_split = false, overlap = false, touch = false;
+  size_t crossings = 0;
   for (size_t u = 0; u < M; u++) {
     const int i0 = order[u];
     const double xhi = std::max(segs[i0].a.x, segs[i0].b.x);
@@ -270,10 +298,17 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
         continue;
       }
       if (o1 * o2 < 0 && o3 * o4 < 0) {   // proper crossing: one point for both
-        const double dx = s.b.x - s.a.x, dy = s.b.y - s.a.y, ex = t.b.x - t.a.x, ey = t.b.y - t.a.y;
+        // computed from the two segments in a canonical order and direction,
+        // so every copy of a segment (a spike, a shared boundary) meets a
+        // third one at the same point
+        Pt sa = s.a, sb = s.b, ta = t.a, tb = t.b;
+        if (before(sb, sa)) std::swap(sa, sb);
+        if (before(tb, ta)) std::swap(ta, tb);
+        if (before(ta, sa) || (same(ta, sa) && before(tb, sb))) { std::swap(sa, ta); std::swap(sb, tb); }
+        const double dx = sb.x - sa.x, dy = sb.y - sa.y, ex = tb.x - ta.x, ey = tb.y - ta.y;
         const double den = dx * ey - dy * ex;
-        const double k = ((t.a.x - s.a.x) * ey - (t.a.y - s.a.y) * ex) / den;
-        Pt p{s.a.x + k * dx, s.a.y + k * dy};
+        const double k = ((ta.x - sa.x) * ey - (ta.y - sa.y) * ex) / den;
+        Pt p{sa.x + k * dx, sa.y + k * dy};
         // keep it within both segments' envelopes (LineIntersector's guard)
         p.x = std::min(std::max(p.x, std::max(std::min(s.a.x, s.b.x), std::min(t.a.x, t.b.x))),
                        std::min(std::max(s.a.x, s.b.x), std::max(t.a.x, t.b.x)));
@@ -282,6 +317,7 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
         splits[i].push_back(p);
         splits[j].push_back(p);
         any_split = true;
+        if (++crossings > kMaxCrossings) return false;
         continue;
       }
       // touches: an endpoint on the other segment's interior splits it
@@ -299,7 +335,8 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
 
   // ---- a valid polygon: vertices kept, each ring turned interior-right
   if (!any_split && !overlap && !touch) {
-    const Depth dep(segs);
+    thread_local std::vector<Seg> turned_s;
+    const Depth dep(segs, turned_s);
     std::vector<int> first(ncurves, -1);
     for (size_t k = 0; k < segs.size(); k++)
       if (first[segs[k].ring] < 0) first[segs[k].ring] = (int)k;
@@ -333,7 +370,8 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
     std::vector<Pt> &sp = splits[k];
     const double dx = s.b.x - s.a.x, dy = s.b.y - s.a.y;
     std::sort(sp.begin(), sp.end(), [&](const Pt &p, const Pt &q) {
-      return (p.x - s.a.x) * dx + (p.y - s.a.y) * dy < (q.x - s.a.x) * dx + (q.y - s.a.y) * dy;
+      const double u = (p.x - s.a.x) * dx + (p.y - s.a.y) * dy, v = (q.x - s.a.x) * dx + (q.y - s.a.y) * dy;
+      return u < v || (u == v && before(p, q));
     });
     Pt prev = s.a;
     auto emit = [&](const Pt &p) {
@@ -357,7 +395,8 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
   if (uniq.empty()) return false;
 
   // ---- result edges: depth >= 1 on the right, <= 0 on the left
-  const Depth dep(uniq);
+  thread_local std::vector<Seg> turned_u;
+  const Depth dep(uniq, turned_u);
   std::vector<Seg> res;
   for (size_t k = 0; k < uniq.size(); k++) {
     const int dr = dep.right_of(k), dl = dr + uniq[k].q;
@@ -366,28 +405,33 @@ bool buffer0_rings(std::vector<double> &X, std::vector<double> &Y, std::vector<i
   }
   if (res.empty()) return false;
 
-  // ---- rings: follow unused edges out of each edge's end until back at the start
-  std::sort(res.begin(), res.end(), [](const Seg &u, const Seg &v) { return before(u.a, v.a); });
+  // ---- rings: from each unused edge in order, follow the first unused edge
+  // out of the current end (in the same order) until back at the start
+  thread_local std::vector<int> by_start_s;
+  std::vector<int> &by_start = by_start_s;
+  by_start.resize(res.size());
+  for (size_t k = 0; k < res.size(); k++) by_start[k] = (int)k;
+  std::stable_sort(by_start.begin(), by_start.end(), [&](int u, int v) { return before(res[u].a, res[v].a); });
   std::vector<char> used(res.size(), 0);
   auto next_from = [&](const Pt &p) -> int {
-    size_t lo = 0, hi = res.size();
+    size_t lo = 0, hi = by_start.size();
     while (lo < hi) {
       const size_t mid = (lo + hi) / 2;
-      if (before(res[mid].a, p)) lo = mid + 1;
+      if (before(res[by_start[mid]].a, p)) lo = mid + 1;
       else hi = mid;
     }
-    for (size_t k = lo; k < res.size() && same(res[k].a, p); k++)
-      if (!used[k]) return (int)k;
+    for (size_t k = lo; k < by_start.size() && same(res[by_start[k]].a, p); k++)
+      if (!used[by_start[k]]) return by_start[k];
     return -1;
   };
   X.clear(); Y.clear(); part.clear();
-  for (size_t s = 0; s < res.size(); s++) {
-    if (used[s]) continue;
-    const Pt start = res[s].a;
+  for (size_t s0 = 0; s0 < res.size(); s0++) {
+    if (used[s0]) continue;
+    const Pt start = res[s0].a;
     int n = 1;
     X.push_back(start.x);
     Y.push_back(start.y);
-    for (int cur = (int)s; cur >= 0;) {
+    for (int cur = (int)s0; cur >= 0;) {
       used[cur] = 1;
       const Pt b = res[cur].b;
       X.push_back(b.x);

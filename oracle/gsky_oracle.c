@@ -2067,9 +2067,35 @@ static int parse_geojson(const char *js, or_rings *r) {
  * keeps the rings as drawn (drill.go:366). */
 typedef struct { double ax, ay, bx, by; int q, ring; } or_seg;
 
+/* sign of (b - a) x (c - a): the double value when it clears its rounding
+ * bound, else the differences exactly (two-diff) and the products and their
+ * difference in double-double arithmetic -- the product's predicate, so the
+ * two agree on every degenerate configuration */
+static void or_two_diff(double a, double b, double *hi, double *lo) {
+    const double s = a - b, bb = s - a;
+    *hi = s; *lo = (a - (s - bb)) - (b + bb);
+}
+static void or_dd_mul(double ah, double al, double bh, double bl, double *hi, double *lo) {
+    const double p = ah * bh;
+    const double e = fma(ah, bh, -p) + (ah * bl + al * bh);
+    *hi = p + e; *lo = e - (*hi - p);
+}
 static int or_orient(double ax, double ay, double bx, double by, double cx, double cy) {
-    const long double d = (long double)(bx - ax) * (long double)(cy - ay) - (long double)(by - ay) * (long double)(cx - ax);
-    return (d > 0) - (d < 0);
+    if ((cx == ax && cy == ay) || (cx == bx && cy == by)) return 0;
+    const double l = (bx - ax) * (cy - ay), r = (by - ay) * (cx - ax);
+    const double det = l - r, bound = 1e-15 * (fabs(l) + fabs(r));
+    if (det > bound) return 1;
+    if (det < -bound) return -1;
+    if (l == 0 && r == 0) return 0;
+    double d1h, d1l, d2h, d2l, d3h, d3l, d4h, d4l, ph, pl, qh, ql;
+    or_two_diff(bx, ax, &d1h, &d1l); or_two_diff(cy, ay, &d2h, &d2l);
+    or_two_diff(by, ay, &d3h, &d3l); or_two_diff(cx, ax, &d4h, &d4l);
+    or_dd_mul(d1h, d1l, d2h, d2l, &ph, &pl);
+    or_dd_mul(d3h, d3l, d4h, d4l, &qh, &ql);
+    const double s = ph - qh, bb = s - ph;
+    const double e = ((ph - (s - bb)) - (qh + bb)) + pl - ql;
+    const double v = s + e;
+    return (v > 0) - (v < 0);
 }
 
 /* CGAlgorithms::isCCW: the turn at the first highest vertex of a closed ring */
@@ -2090,13 +2116,33 @@ static int or_wind(const or_seg *e, double px, double py) {
     return (e->by <= py && or_orient(e->ax, e->ay, e->bx, e->by, px, py) < 0) ? -e->q : 0;
 }
 
-/* depth just right of edge k: the other edges' winding at its midpoint plus its own share */
-static int or_depth_right(const or_seg *s, int n, int k) {
+/* depth just right of edge k: the other edges' winding at its midpoint plus
+ * its own share.  Edge sets of 48 or more that are wider than tall are cast
+ * in the frame (x, y) -> (y, -x), as the product does (its rays then run
+ * across the short side); the winding numbers agree off the edges. */
+static int or_depth_right_raw(const or_seg *s, int n, int k) {
     const double mx = 0.5 * (s[k].ax + s[k].bx), my = 0.5 * (s[k].ay + s[k].by);
     int d = 0;
     for (int f = 0; f < n; f++) if (f != k) d += or_wind(&s[f], mx, my);
     if (s[k].ay == s[k].by) return s[k].ax < s[k].bx ? d - s[k].q : d;   /* d = depth above */
     return s[k].by < s[k].ay ? d - s[k].q : d;
+}
+static int or_turned(const or_seg *s, int n) {
+    if (n < 48) return 0;
+    double x0 = HUGE_VAL, x1 = -HUGE_VAL, y0 = HUGE_VAL, y1 = -HUGE_VAL;
+    for (int k = 0; k < n; k++) {
+        x0 = fmin(x0, fmin(s[k].ax, s[k].bx)); x1 = fmax(x1, fmax(s[k].ax, s[k].bx));
+        y0 = fmin(y0, fmin(s[k].ay, s[k].by)); y1 = fmax(y1, fmax(s[k].ay, s[k].by));
+    }
+    return x1 - x0 > y1 - y0;
+}
+static or_seg *or_turn(const or_seg *s, int n) {
+    or_seg *t = (or_seg *)malloc(sizeof(or_seg) * (n > 0 ? n : 1));
+    for (int k = 0; k < n; k++) {
+        or_seg e = {s[k].ay, -s[k].ax, s[k].by, -s[k].bx, s[k].q, s[k].ring};
+        t[k] = e;
+    }
+    return t;
 }
 
 static int on_open_seg(double ax, double ay, double bx, double by, double px, double py) {
@@ -2129,7 +2175,8 @@ static double g_dx, g_dy, g_ox, g_oy;
 static int cmp_along(const void *u, const void *v) {
     const or_pt *a = (const or_pt *)u, *b = (const or_pt *)v;
     const double s = (a->x - g_ox) * g_dx + (a->y - g_oy) * g_dy, t = (b->x - g_ox) * g_dx + (b->y - g_oy) * g_dy;
-    return (s > t) - (s < t);
+    if (s != t) return (s > t) - (s < t);
+    return pt_lt(a->x, a->y, b->x, b->y) ? -1 : pt_lt(b->x, b->y, a->x, a->y) ? 1 : 0;
 }
 
 static void rings_buffer0(or_rings *r) {
@@ -2185,9 +2232,18 @@ static void rings_buffer0(or_rings *r) {
                 continue;
             }
             if (o1 * o2 < 0 && o3 * o4 < 0) {
-                const double dx = a->bx - a->ax, dy = a->by - a->ay, ex = b->bx - b->ax, ey = b->by - b->ay;
-                const double kk = ((b->ax - a->ax) * ey - (b->ay - a->ay) * ex) / (dx * ey - dy * ex);
-                double px = a->ax + kk * dx, py = a->ay + kk * dy;
+                /* both segments lesser point first, the lesser segment first: every
+                 * copy of a segment meets a third one at the same point */
+                double s0x = a->ax, s0y = a->ay, s1x = a->bx, s1y = a->by, t0x = b->ax, t0y = b->ay, t1x = b->bx, t1y = b->by, tmp;
+                if (pt_lt(s1x, s1y, s0x, s0y)) { tmp = s0x; s0x = s1x; s1x = tmp; tmp = s0y; s0y = s1y; s1y = tmp; }
+                if (pt_lt(t1x, t1y, t0x, t0y)) { tmp = t0x; t0x = t1x; t1x = tmp; tmp = t0y; t0y = t1y; t1y = tmp; }
+                if (pt_lt(t0x, t0y, s0x, s0y) || (t0x == s0x && t0y == s0y && pt_lt(t1x, t1y, s1x, s1y))) {
+                    tmp = s0x; s0x = t0x; t0x = tmp; tmp = s0y; s0y = t0y; t0y = tmp;
+                    tmp = s1x; s1x = t1x; t1x = tmp; tmp = s1y; s1y = t1y; t1y = tmp;
+                }
+                const double dx = s1x - s0x, dy = s1y - s0y, ex = t1x - t0x, ey = t1y - t0y;
+                const double kk = ((t0x - s0x) * ey - (t0y - s0y) * ex) / (dx * ey - dy * ex);
+                double px = s0x + kk * dx, py = s0y + kk * dy;
                 px = fmin(fmax(px, fmax(fmin(a->ax, a->bx), fmin(b->ax, b->bx))), fmin(fmax(a->ax, a->bx), fmax(b->ax, b->bx)));
                 py = fmin(fmax(py, fmax(fmin(a->ay, a->by), fmin(b->ay, b->by))), fmin(fmax(a->ay, a->by), fmax(b->ay, b->by)));
                 ptl_push(&sp[i], px, py); ptl_push(&sp[j], px, py);
@@ -2210,11 +2266,13 @@ static void rings_buffer0(or_rings *r) {
     if (!split && !overlap && !touch) {            /* valid: keep the vertices, interior right */
         int ok = 1;
         int *flip = (int *)malloc(sizeof(int) * ncurves);
+        or_seg *ts = or_turned(s, ns) ? or_turn(s, ns) : NULL;
         for (int c = 0; c < ncurves && ok; c++) {
-            const int dr = or_depth_right(s, ns, cstart[c]), dl = dr + cq[c];
+            const int dr = or_depth_right_raw(ts ? ts : s, ns, cstart[c]), dl = dr + cq[c];
             ok = (dr == 1 && dl == 0) || (dr == 0 && dl == 1);
             flip[c] = dl == 1;
         }
+        free(ts);
         if (ok) {
             or_rings out;
             memset(&out, 0, sizeof(out));
@@ -2258,11 +2316,13 @@ static void rings_buffer0(or_rings *r) {
         /* result edges, directed interior-right */
         or_seg *res = (or_seg *)malloc(sizeof(or_seg) * (m + 1));
         int nr = 0;
+        or_seg *te = or_turned(e, m) ? or_turn(e, m) : NULL;
         for (int k = 0; k < m; k++) {
-            const int dr = or_depth_right(e, m, k), dl = dr + e[k].q;
+            const int dr = or_depth_right_raw(te ? te : e, m, k), dl = dr + e[k].q;
             if (dr >= 1 && dl <= 0) { or_seg x = {e[k].ax, e[k].ay, e[k].bx, e[k].by, 0, 0}; res[nr++] = x; }
             else if (dl >= 1 && dr <= 0) { or_seg x = {e[k].bx, e[k].by, e[k].ax, e[k].ay, 0, 0}; res[nr++] = x; }
         }
+        free(te);
         if (nr) {                                  /* chain them into closed rings */
             or_rings out;
             memset(&out, 0, sizeof(out));
