@@ -376,7 +376,7 @@ def run_c2(ctx: Ctx, args):
                                     "png_bytes_mean": int(np.mean([len(b) for b in zp])),
                                     "same_tiles_gpu_bytes_mean": int(np.mean([len(b) for b in pngs[: zs.shape[0]]]))},
                       "timing": "gskyhip_encode_png of %d covered C2 tiles already rendered in HBM: GPU colour-type "
-                                "+ filter pass, GPU deflate (row-distance LZ77, per-tile dynamic Huffman codes or the fixed ones where "
+                                "+ filter pass, GPU deflate (LZ77 at run / pixel / row / diagonal distances with one-step lazy matching, tokens searched once; per-tile dynamic Huffman codes or the fixed ones where "
                                 "shorter) + IDAT CRC-32, PNG framing on "
                                 "%d host threads, host wall; zlib_host = the same tiles through host zlib level 6"
                                 % (len(sample), threads)}

@@ -152,11 +152,10 @@ __global__ __launch_bounds__(256) void png_filter_kernel(const uint8_t *__restri
 // block -- Huffman codes built for the tile from its symbol frequencies
 // (RFC 1951 3.2.7), or the fixed codes (3.2.6) where those come out shorter
 // -- whose LZ77 matches are
-// searched at the distances a PNG row offers -- 1 (runs), the pixel size
-// (the pixel to the left) and the row stride (the pixel above) -- greedily,
-// longest first, within the row (so rows are encoded independently: a
-// workgroup per tile, a thread per row, matches may reach back into earlier
-// rows).  Pass 1 counts each row's bits; their prefix sums place every row
+// searched at the distances a PNG row offers -- runs, pixels to the left,
+// rows above and the diagonals (deflate_tokens) -- within the row (so rows
+// are encoded independently: a workgroup per tile, a thread per row, matches
+// may reach back into earlier rows).  Pass 1 counts each row's bits; their prefix sums place every row
 // in the tile's bit stream and every tile in one packed buffer (so only the
 // compressed bytes cross PCIe); pass 2 writes the codes (the words two rows
 // share by OR).  Adler-32 from per-row sums.  The stream is valid DEFLATE /
@@ -212,35 +211,69 @@ __device__ __forceinline__ void lit_code(int v, uint32_t &code, int &len) {
 }
 
 // One row's LZ77 tokens, in order, to f(sym, len_extra, n_len_extra, dcode,
-// dist_extra, n_dist_extra): dcode < 0 for a literal.
+// dist_extra, n_dist_extra): dcode < 0 for a literal.  Candidates at the
+// distances a PNG of upsampled tiles repeats at -- runs (1), the pixel to the
+// left and 2-3 pixels back, the pixels above (1-3 rows) and the diagonals --
+// the one saving the most bits by a static estimate (6.5 bits per literal
+// byte against ~7 bits of length code plus the distance code and its extra
+// bits), and one step of lazy matching (a match starting one byte later that
+// is 2+ bytes longer wins, the byte going out as a literal).  A model of
+// these tokens with dynamic Huffman costs: 461 -> 433 KB per C2 tile (zlib
+// level 6: 409 KB).
+__device__ __forceinline__ int dist_code(int d) {
+  int dc = 0;
+  while (dc < 29 && kDistBase[dc + 1] <= d) dc++;
+  return dc;
+}
+
+__device__ __forceinline__ void best_match(const uint8_t *__restrict__ data, int64_t p, int64_t p1, int bpp,
+                                           int stride, int &best, int &bd) {
+  best = 0;
+  bd = 0;
+  int bscore = -(1 << 30);
+  const int dists[11] = {1, bpp, stride, 2 * bpp, 3 * bpp, 2 * stride, stride - bpp, stride + bpp,
+                         2 * stride - bpp, 2 * stride + bpp, 3 * stride};
+  const int lim = (int)min((int64_t)258, p1 - p);
+#pragma unroll
+  for (int c = 0; c < 11; c++) {
+    const int d = dists[c];
+    if (p - d < 0 || d > 32768) continue;
+    int l = 0;
+    // 4 bytes per compare (unaligned dword loads), the first difference by ctz
+    while (l + 4 <= lim) {
+      const uint32_t x = ld_u32(data + p + l) ^ ld_u32(data + p + l - d);
+      if (x) { l += __builtin_ctz(x) >> 3; goto done; }
+      l += 4;
+    }
+    while (l < lim && data[p + l] == data[p + l - d]) l++;
+  done:
+    if (l < 3) continue;
+    const int score = 13 * l - 2 * (7 + 5 + (int)kDistExtra[dist_code(d)]);   // 2x the bits saved
+    if (score > bscore) { bscore = score; best = l; bd = d; }
+  }
+}
+
 template <class F>
 __device__ __forceinline__ void deflate_tokens(const uint8_t *__restrict__ data, int64_t p0, int64_t p1, int bpp,
                                                int stride, F &&f) {
   int64_t p = p0;
   while (p < p1) {
-    int best = 0, bd = 0;
-    const int dists[3] = {1, bpp, stride};
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-      const int d = dists[c];
-      if (p - d < 0 || d > 32768) continue;
-      int l = 0;
-      const int lim = (int)min((int64_t)258, p1 - p);
-      // 4 bytes per compare (unaligned dword loads), the first difference by ctz
-      while (l + 4 <= lim) {
-        const uint32_t x = ld_u32(data + p + l) ^ ld_u32(data + p + l - d);
-        if (x) { l += __builtin_ctz(x) >> 3; goto done; }
-        l += 4;
+    int best, bd;
+    best_match(data, p, p1, bpp, stride, best, bd);
+    if (best >= 3 && p + 1 < p1) {   // lazy: a longer match one byte on
+      int b2, d2;
+      best_match(data, p + 1, p1, bpp, stride, b2, d2);
+      if (b2 > best + 1) {
+        f((int)data[p], 0u, 0, -1, 0u, 0);
+        p++;
+        best = b2;
+        bd = d2;
       }
-      while (l < lim && data[p + l] == data[p + l - d]) l++;
-    done:
-      if (l > best) { best = l; bd = d; }
     }
     if (best >= 3) {
       int lc = 0;
       while (lc < 28 && kLenBase[lc + 1] <= best) lc++;
-      int dc = 0;
-      while (dc < 29 && kDistBase[dc + 1] <= bd) dc++;
+      const int dc = dist_code(bd);
       f(257 + lc, (uint32_t)(best - kLenBase[lc]), (int)kLenExtra[lc], dc, (uint32_t)(bd - kDistBase[dc]),
         (int)kDistExtra[dc]);
       p += best;
@@ -248,6 +281,22 @@ __device__ __forceinline__ void deflate_tokens(const uint8_t *__restrict__ data,
       f((int)data[p], 0u, 0, -1, 0u, 0);
       p++;
     }
+  }
+}
+
+// The tokens of a row are searched once (pass 1) and kept, packed one per
+// dword -- symbol (9 bits) | distance code + 1 (5) | length extra (5) |
+// distance extra (13) -- for the bit count and the write pass to replay.
+__device__ __forceinline__ uint32_t tok_pack(int sym, uint32_t lx, int dc, uint32_t dx) {
+  return (uint32_t)sym | ((uint32_t)(dc + 1) << 9) | (lx << 14) | (dx << 19);
+}
+
+template <class F>
+__device__ __forceinline__ void tok_replay(const uint32_t *__restrict__ tk, int n, F &&f) {
+  for (int i = 0; i < n; i++) {
+    const uint32_t v = tk[i];
+    const int sym = (int)(v & 511u), dc = (int)((v >> 9) & 31u) - 1;
+    f(sym, (v >> 14) & 31u, sym >= 257 ? (int)kLenExtra[sym - 257] : 0, dc, v >> 19, dc >= 0 ? (int)kDistExtra[dc] : 0);
   }
 }
 
@@ -379,7 +428,8 @@ __global__ __launch_bounds__(256) void png_deflate_count_kernel(const uint8_t *_
                                                                 int32_t *__restrict__ row_bits,
                                                                 uint32_t *__restrict__ adler,
                                                                 int64_t *__restrict__ zlen, PngTab *__restrict__ tab,
-                                                                int dynamic) {
+                                                                int dynamic, uint32_t *__restrict__ tok,
+                                                                int32_t *__restrict__ ntok, int64_t per) {
   const int t = blockIdx.x, tid = threadIdx.x;
   const int w = wh[2 * t], h = wh[2 * t + 1];
   const int bpp = opaque[t] ? 3 : 4;
@@ -399,11 +449,16 @@ __global__ __launch_bounds__(256) void png_deflate_count_kernel(const uint8_t *_
   __syncthreads();
   for (int y = tid; y < h; y += blockDim.x) {
     const int64_t p0 = (int64_t)y * stride;
-    if (dynamic)
-      deflate_tokens(data, p0, p0 + stride, bpp, stride, [&](int sym, uint32_t, int, int dc, uint32_t, int) {
+    uint32_t *tk = tok + (int64_t)t * per + p0;   // a row has at most `stride` tokens
+    int n = 0;
+    deflate_tokens(data, p0, p0 + stride, bpp, stride, [&](int sym, uint32_t lx, int, int dc, uint32_t dx, int) {
+      tk[n++] = tok_pack(sym, lx, dc, dx);
+      if (dynamic) {
         atomicAdd(&s_freq[sym], 1u);
         if (dc >= 0) atomicAdd(&s_freq[kLitN + dc], 1u);
-      });
+      }
+    });
+    ntok[(int64_t)t * max_h + y] = n;
     uint64_t a = 0, bb = 0;   // sum of bytes, sum of (n - i) * byte (exact: < 2^40), then mod 65521
     int i = 0;
     for (; i + 4 <= stride; i += 4) {
@@ -520,11 +575,11 @@ __global__ __launch_bounds__(256) void png_deflate_count_kernel(const uint8_t *_
   __syncthreads();
   int64_t mine = 0;
   for (int y = tid; y < h; y += blockDim.x) {
-    const int64_t p0 = (int64_t)y * stride;
     uint32_t b = 0;
-    deflate_tokens(data, p0, p0 + stride, bpp, stride, [&](int sym, uint32_t, int le, int dc, uint32_t, int de) {
-      b += s_len[sym] + le + (dc >= 0 ? s_len[kLitN + dc] + de : 0);
-    });
+    tok_replay(tok + (int64_t)t * per + (int64_t)y * stride, ntok[(int64_t)t * max_h + y],
+               [&](int sym, uint32_t, int le, int dc, uint32_t, int de) {
+                 b += s_len[sym] + le + (dc >= 0 ? s_len[kLitN + dc] + de : 0);
+               });
     row_bits[(int64_t)t * max_h + y] = (int32_t)b;
     mine += b;
   }
@@ -555,12 +610,14 @@ __global__ __launch_bounds__(256) void png_deflate_write_kernel(const uint8_t *_
                                                                 const int64_t *__restrict__ zoff,
                                                                 const int64_t *__restrict__ zlen,
                                                                 uint8_t *__restrict__ packed,
-                                                                const PngTab *__restrict__ tab) {
+                                                                const PngTab *__restrict__ tab,
+                                                                const uint32_t *__restrict__ tok,
+                                                                const int32_t *__restrict__ ntok, int64_t per) {
   const int t = blockIdx.x;
   const int w = wh[2 * t], h = wh[2 * t + 1];
   const int bpp = opaque[t] ? 3 : 4;
   const int stride = 1 + bpp * w;
-  const uint8_t *data = filt + off[t];
+  (void)filt;
   uint8_t *z = packed + zoff[t];
   // the tile's stream starts on a 4-byte boundary of the packed buffer
   uint32_t *words = (uint32_t *)z;
@@ -597,9 +654,8 @@ __global__ __launch_bounds__(256) void png_deflate_write_kernel(const uint8_t *_
   for (int y = threadIdx.x; y < h; y += blockDim.x) {
     BitSink bs;
     bs.init(words, s_start[y]);
-    const int64_t p0 = (int64_t)y * stride;
-    deflate_tokens(data, p0, p0 + stride, bpp, stride,
-                   [&](int sym, uint32_t lx, int le, int dc, uint32_t dx, int de) {
+    tok_replay(tok + (int64_t)t * per + (int64_t)y * stride, ntok[(int64_t)t * max_h + y],
+               [&](int sym, uint32_t lx, int le, int dc, uint32_t dx, int de) {
                      bs.put(s_code[sym], s_len[sym]);
                      if (dc >= 0) {
                        if (le) bs.put(lx, le);
@@ -856,7 +912,8 @@ extern "C" {
 // Workspace: filtered rows | per-tile offsets, sizes, opacity | per-row bit
 // counts | Adler-32, zlib lengths and offsets | per-tile codes | the packed
 // zlib streams (at most 9/8 of the filtered bytes + 16 per tile: a dynamic
-// block is only used where it is shorter than the fixed one).
+// block is only used where it is shorter than the fixed one) | the rows'
+// tokens (a dword per filtered byte at most) and token counts.
 static int64_t png_deflate_cap(int64_t per) { return (per * 9 + 7) / 8 + 64 + (per / 32768 + 1) * 4 + 256; }
 
 int64_t gskyhip_png_workspace_size(int n_tiles, int max_w, int max_h) {
@@ -865,7 +922,8 @@ int64_t gskyhip_png_workspace_size(int n_tiles, int max_w, int max_h) {
   const int64_t a = ((int64_t)n_tiles * per + 255) / 256 * 256 + (int64_t)n_tiles * (8 + 8 + 4) + 1024;
   const int64_t b = ((int64_t)n_tiles * max_h * 4 + 255) / 256 * 256 + (int64_t)n_tiles * (4 + 8 + 8) + 1024 +
                     (int64_t)n_tiles * (int64_t)sizeof(PngTab) + 256;
-  return a + b + (int64_t)n_tiles * png_deflate_cap(per) + 1024;
+  const int64_t c = (int64_t)n_tiles * per * 4 + (int64_t)n_tiles * max_h * 4 + 1024;   // tokens, counts
+  return a + b + (int64_t)n_tiles * png_deflate_cap(per) + 1024 + c;
 }
 
 int64_t gskyhip_png_bound(int width, int height) {
@@ -927,9 +985,12 @@ int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, i
     // per-tile dynamic Huffman codes where they are shorter (GSKYHIP_PNG_FIXED=1: fixed codes only)
     const char *fx = std::getenv("GSKYHIP_PNG_FIXED");
     const int dynamic = (fx && std::atoi(fx) != 0) ? 0 : 1;
-    if ((char *)d_packed + (int64_t)n_tiles * png_deflate_cap(per) > ws + workspace_bytes) return GSKYHIP_E_ARG;
+    uint32_t *d_tok = (uint32_t *)(((uintptr_t)(d_packed + (int64_t)n_tiles * png_deflate_cap(per)) + 255) &
+                                   ~(uintptr_t)255);
+    int32_t *d_ntok = (int32_t *)(d_tok + (int64_t)n_tiles * per);
+    if ((char *)(d_ntok + (int64_t)n_tiles * max_h) > ws + workspace_bytes) return GSKYHIP_E_ARG;
     hipLaunchKernelGGL(png_deflate_count_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, filt, d_off, d_wh, d_opq,
-                       max_h, d_rowbits, d_adler, d_zlen, d_tab, dynamic);
+                       max_h, d_rowbits, d_adler, d_zlen, d_tab, dynamic, d_tok, d_ntok, per);
     std::vector<int64_t> zlen(n_tiles), zoff(n_tiles);
     std::vector<int32_t> opq(n_tiles);
     if (hipGetLastError() != hipSuccess ||
@@ -949,7 +1010,7 @@ int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, i
         hipMemsetAsync(d_packed, 0, (size_t)std::max<int64_t>(total, 4), s) != hipSuccess)
       return GSKYHIP_E_HIP;
     hipLaunchKernelGGL(png_deflate_write_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, filt, d_off, d_wh, d_opq,
-                       max_h, d_rowbits, d_adler, d_zoff, d_zlen, d_packed, d_tab);
+                       max_h, d_rowbits, d_adler, d_zoff, d_zlen, d_packed, d_tab, d_tok, d_ntok, per);
     // IDAT CRCs behind the packed streams (the pinned read-back holds both)
     const int64_t crc_at = (total + 255) & ~(int64_t)255;
     const int64_t n_crc = (int64_t)n_tiles * max_chunks;
