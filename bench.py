@@ -30,6 +30,7 @@ host cores, rank 0, N=1 only.
 from __future__ import annotations
 
 import argparse
+import gc
 import hashlib
 import json
 import os
@@ -827,7 +828,19 @@ def main():
     if "c2" in only:
         out.update(run_c2(ctx, args))
     configs = {}
+
+    def settle():
+        # between legs, outside every timed region: the previous leg's host
+        # arrays and cached device blocks released, so a leg's timing never
+        # overlaps the host's reclaim of the last one's (a C5 step once read
+        # 13-17 ms instead of 0.6 after C4's CPU baseline freed its copies)
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        time.sleep(0.2)
     for name, fn in (("C1", run_c1), ("C3", run_c3), ("C4", run_c4), ("C5", run_c5), ("service", run_service)):
+        if name.lower() in only or (name == "service" and "svc" in only):
+            settle()
         if name == "service":
             if "svc" not in only or ctx.world > 1:
                 continue
