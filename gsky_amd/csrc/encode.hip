@@ -416,8 +416,46 @@ __device__ void fixed_table(PngTab &T) {
   T.hdr_bits = 3;
 }
 
-// Pass 1, a workgroup per tile: the rows' symbol frequencies and Adler-32
-// sums; the tile's dynamic code (or the fixed one where that is shorter,
+// Pass 0, a thread per row (a wave per 64 rows of a tile, so every CU holds
+// many rows in flight): the row's tokens, kept for pass 1's bit count and
+// pass 2, and -- for a dynamic code -- their symbol frequencies, summed per
+// workgroup in LDS and added to the tile's global histogram.
+__global__ __launch_bounds__(64) void png_tokenize_kernel(const uint8_t *__restrict__ filt,
+                                                          const int64_t *__restrict__ off,
+                                                          const int32_t *__restrict__ wh,
+                                                          const int32_t *__restrict__ opaque, int max_h,
+                                                          uint32_t *__restrict__ tok, int32_t *__restrict__ ntok,
+                                                          int64_t per, uint32_t *__restrict__ freq, int dynamic) {
+  const int groups = (max_h + 63) / 64;
+  const int t = (int)(blockIdx.x / groups), tid = threadIdx.x, y = (int)(blockIdx.x % groups) * 64 + tid;
+  const int h = wh[2 * t + 1];
+  const int bpp = opaque[t] ? 3 : 4;
+  const int stride = 1 + bpp * wh[2 * t];
+  const uint8_t *data = filt + off[t];
+  __shared__ uint32_t s_freq[kSymN];
+  for (int i = tid; i < kSymN; i += 64) s_freq[i] = 0;
+  __syncthreads();
+  if (y < h) {
+    const int64_t p0 = (int64_t)y * stride;
+    uint32_t *tk = tok + (int64_t)t * per + p0;   // a row has at most `stride` tokens
+    int n = 0;
+    deflate_tokens(data, p0, p0 + stride, bpp, stride, [&](int sym, uint32_t lx, int, int dc, uint32_t dx, int) {
+      tk[n++] = tok_pack(sym, lx, dc, dx);
+      if (dynamic) {
+        atomicAdd(&s_freq[sym], 1u);
+        if (dc >= 0) atomicAdd(&s_freq[kLitN + dc], 1u);
+      }
+    });
+    ntok[(int64_t)t * max_h + y] = n;
+  }
+  __syncthreads();
+  if (dynamic)
+    for (int i = tid; i < kSymN; i += 64)
+      if (s_freq[i]) atomicAdd(&freq[(int64_t)t * kSymN + i], s_freq[i]);
+}
+
+// Pass 1, a workgroup per tile: the rows' Adler-32 sums; the tile's dynamic
+// code from pass 0's frequencies (or the fixed one where that is shorter,
 // header included) into tab[t]; each row's bits under it; the stream length.
 // Tile stream: zlib header (2 B), block header, rows, end of block, pad to a
 // byte, Adler-32 (4 B).
@@ -428,8 +466,9 @@ __global__ __launch_bounds__(256) void png_deflate_count_kernel(const uint8_t *_
                                                                 int32_t *__restrict__ row_bits,
                                                                 uint32_t *__restrict__ adler,
                                                                 int64_t *__restrict__ zlen, PngTab *__restrict__ tab,
-                                                                int dynamic, uint32_t *__restrict__ tok,
-                                                                int32_t *__restrict__ ntok, int64_t per) {
+                                                                int dynamic, const uint32_t *__restrict__ tok,
+                                                                const int32_t *__restrict__ ntok, int64_t per,
+                                                                const uint32_t *__restrict__ freq) {
   const int t = blockIdx.x, tid = threadIdx.x;
   const int w = wh[2 * t], h = wh[2 * t + 1];
   const int bpp = opaque[t] ? 3 : 4;
@@ -445,20 +484,10 @@ __global__ __launch_bounds__(256) void png_deflate_count_kernel(const uint8_t *_
   __shared__ int32_t s_nr, s_hlit, s_hdist, s_use_fixed;
   __shared__ HuffLds H;
   PngTab &T = tab[t];
-  for (int i = tid; i < kSymN; i += blockDim.x) s_freq[i] = 0;
+  for (int i = tid; i < kSymN; i += blockDim.x) s_freq[i] = dynamic ? freq[(int64_t)t * kSymN + i] : 0u;
   __syncthreads();
   for (int y = tid; y < h; y += blockDim.x) {
     const int64_t p0 = (int64_t)y * stride;
-    uint32_t *tk = tok + (int64_t)t * per + p0;   // a row has at most `stride` tokens
-    int n = 0;
-    deflate_tokens(data, p0, p0 + stride, bpp, stride, [&](int sym, uint32_t lx, int, int dc, uint32_t dx, int) {
-      tk[n++] = tok_pack(sym, lx, dc, dx);
-      if (dynamic) {
-        atomicAdd(&s_freq[sym], 1u);
-        if (dc >= 0) atomicAdd(&s_freq[kLitN + dc], 1u);
-      }
-    });
-    ntok[(int64_t)t * max_h + y] = n;
     uint64_t a = 0, bb = 0;   // sum of bytes, sum of (n - i) * byte (exact: < 2^40), then mod 65521
     int i = 0;
     for (; i + 4 <= stride; i += 4) {
@@ -922,7 +951,8 @@ int64_t gskyhip_png_workspace_size(int n_tiles, int max_w, int max_h) {
   const int64_t a = ((int64_t)n_tiles * per + 255) / 256 * 256 + (int64_t)n_tiles * (8 + 8 + 4) + 1024;
   const int64_t b = ((int64_t)n_tiles * max_h * 4 + 255) / 256 * 256 + (int64_t)n_tiles * (4 + 8 + 8) + 1024 +
                     (int64_t)n_tiles * (int64_t)sizeof(PngTab) + 256;
-  const int64_t c = (int64_t)n_tiles * per * 4 + (int64_t)n_tiles * max_h * 4 + 1024;   // tokens, counts
+  const int64_t c = (int64_t)n_tiles * per * 4 + (int64_t)n_tiles * max_h * 4 + 1024 +   // tokens, counts,
+                    (int64_t)n_tiles * kSymN * 4 + 256;                                  // symbol frequencies
   return a + b + (int64_t)n_tiles * png_deflate_cap(per) + 1024 + c;
 }
 
@@ -988,9 +1018,13 @@ int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, i
     uint32_t *d_tok = (uint32_t *)(((uintptr_t)(d_packed + (int64_t)n_tiles * png_deflate_cap(per)) + 255) &
                                    ~(uintptr_t)255);
     int32_t *d_ntok = (int32_t *)(d_tok + (int64_t)n_tiles * per);
-    if ((char *)(d_ntok + (int64_t)n_tiles * max_h) > ws + workspace_bytes) return GSKYHIP_E_ARG;
+    uint32_t *d_freq = (uint32_t *)(((uintptr_t)(d_ntok + (int64_t)n_tiles * max_h) + 255) & ~(uintptr_t)255);
+    if ((char *)(d_freq + (int64_t)n_tiles * kSymN) > ws + workspace_bytes) return GSKYHIP_E_ARG;
+    if (hipMemsetAsync(d_freq, 0, (size_t)n_tiles * kSymN * 4, s) != hipSuccess) return GSKYHIP_E_HIP;
+    hipLaunchKernelGGL(png_tokenize_kernel, dim3((unsigned)((int64_t)n_tiles * ((max_h + 63) / 64))), dim3(64), 0, s, filt,
+                       d_off, d_wh, d_opq, max_h, d_tok, d_ntok, per, d_freq, dynamic);
     hipLaunchKernelGGL(png_deflate_count_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, filt, d_off, d_wh, d_opq,
-                       max_h, d_rowbits, d_adler, d_zlen, d_tab, dynamic, d_tok, d_ntok, per);
+                       max_h, d_rowbits, d_adler, d_zlen, d_tab, dynamic, d_tok, d_ntok, per, d_freq);
     std::vector<int64_t> zlen(n_tiles), zoff(n_tiles);
     std::vector<int32_t> opq(n_tiles);
     if (hipGetLastError() != hipSuccess ||
