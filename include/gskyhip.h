@@ -444,9 +444,11 @@ int gskyhip_compute_mask(const void *data, int dtype, int64_t n, const gskyhip_m
  *   png_out: HOST, png_capacity bytes per tile (>= gskyhip_png_bound(w, h));
  *   png_sizes: HOST int64 per tile, the PNG's length.
  * Colour type RGB when every alpha is 0xff else RGBA (NRGBA bytes), Go's
- * per-row filter choice, zlib level 6, 32 KiB IDAT chunks (see encode.hip:
- * the filtered rows are Go's bytes, the deflate stream is zlib's).
- * n_threads host threads deflate the tiles; `stream` runs the GPU pass. */
+ * per-row filter choice, 32 KiB IDAT chunks (see encode.hip: the filtered
+ * rows are Go's bytes; the zlib stream is deflated on the GPU -- LZ77 at run
+ * / pixel / row / diagonal distances, per-tile Huffman codes -- so its bytes
+ * are neither zlib's nor Go's compress/flate, parity unpinned).
+ * n_threads host threads frame the PNGs; `stream` runs the GPU passes. */
 int64_t gskyhip_png_workspace_size(int n_tiles, int max_w, int max_h);
 int64_t gskyhip_png_bound(int width, int height);
 int gskyhip_encode_png(const uint8_t *rgba, int n_tiles, int max_w, int max_h, int64_t tile_stride,
