@@ -42,6 +42,10 @@ struct Rd {
   bool has(uint64_t p, uint64_t n) { return p <= f.buf.size() && f.buf.size() - p >= n; }
 };
 
+// Nodes one tree walk may visit: a corrupt or crafted index (children that
+// point back into the tree) fails the open instead of running for ever.
+constexpr uint64_t kMaxNodes = 1u << 16;
+
 int bytes_for(uint64_t x) {   // H5VM_limit_enc_size: (log2(x) / 8) + 1
   int l = 0;
   while (x >>= 1) l++;
@@ -218,14 +222,15 @@ bool btree2_records(Rd &r, uint64_t hdr, std::vector<uint64_t> &recs, uint32_t &
   cum_max[0] = max_nrec[0];
   cum_sz[0] = nrec_sz[0];
   for (int d = 1; d <= depth; d++) {
-    const uint64_t ptr = (uint64_t)r.f.off_size + nrec_sz[d - 1] + (d > 1 ? cum_sz[d - 1] : 0);
+    const uint64_t ptr = (uint64_t)r.f.off_size + nrec_sz[0] + (d > 1 ? cum_sz[d - 1] : 0);
     max_nrec[d] = (node_size - 10 - ptr) / (rsize + ptr);
     nrec_sz[d] = bytes_for(max_nrec[d]);
     cum_max[d] = (max_nrec[d] + 1) * cum_max[d - 1] + max_nrec[d];
     cum_sz[d] = bytes_for(cum_max[d]);
   }
+  uint64_t visited = 0;   // nodes of this walk (a crafted tree can point back into itself)
   std::function<bool(uint64_t, uint64_t, int)> walk = [&](uint64_t node, uint64_t n, int d) -> bool {
-    if (recs.size() > (1u << 20)) return false;
+    if (recs.size() > (1u << 20) || ++visited > kMaxNodes) return false;
     if (d == 0) {
       if (!r.sig(node, "BTLF")) return false;
       for (uint64_t i = 0; i < n; i++) recs.push_back(node + 6 + i * rsize);
@@ -233,10 +238,10 @@ bool btree2_records(Rd &r, uint64_t hdr, std::vector<uint64_t> &recs, uint32_t &
     }
     if (!r.sig(node, "BTIN")) return false;
     uint64_t p = node + 6 + n * rsize;
-    const int ps = r.f.off_size + nrec_sz[d - 1] + (d > 1 ? cum_sz[d - 1] : 0);
+    const int ps = r.f.off_size + nrec_sz[0] + (d > 1 ? cum_sz[d - 1] : 0);
     for (uint64_t i = 0; i <= n; i++) {
       const uint64_t child = r.addr(p + i * ps);
-      const uint64_t cn = r.u(p + i * ps + r.f.off_size, nrec_sz[d - 1]);
+      const uint64_t cn = r.u(p + i * ps + r.f.off_size, nrec_sz[0]);
       if (!walk(child, cn, d - 1)) return false;
       if (i < n) recs.push_back(node + 6 + i * rsize);
     }
@@ -284,8 +289,9 @@ uint64_t row_block(const FHeap &h, int row) {
 uint64_t fheap_locate(Rd &r, const FHeap &h, uint64_t off) {
   if (h.root == kUndef) return kUndef;
   if (h.cur_rows == 0) return h.root + off;   // the root is a direct block at heap offset 0
+  int visited = 0;
   std::function<uint64_t(uint64_t, uint64_t, int)> find = [&](uint64_t ib, uint64_t ib_off, int nrows) -> uint64_t {
-    if (!r.sig(ib, "FHIB")) return kUndef;
+    if (++visited > 64 || !r.sig(ib, "FHIB")) return kUndef;
     const uint64_t ents = ib + 5 + r.f.off_size + h.off_sz;
     const int nd = std::min(nrows, h.max_drows) * h.width;
     uint64_t pos = ib_off;
@@ -421,8 +427,9 @@ bool symbol_table_links(Rd &r, uint64_t btree, uint64_t heap, std::vector<Link> 
   const uint64_t hdata = r.addr(heap + 8 + 2 * (uint64_t)r.f.len_size);
   const uint64_t hsize = r.len(heap + 8);
   const int O = r.f.off_size, L = r.f.len_size;
+  uint64_t visited = 0;
   std::function<bool(uint64_t, int)> walk = [&](uint64_t node, int guard) -> bool {
-    if (guard > 32 || !r.sig(node, "TREE") || r.u(node + 4, 1) != 0) return false;
+    if (guard > 32 || ++visited > kMaxNodes || !r.sig(node, "TREE") || r.u(node + 4, 1) != 0) return false;
     const int level = (int)r.u(node + 5, 1);
     const uint64_t n = r.u(node + 6, 2);
     const uint64_t kc = node + 8 + 2 * (uint64_t)O;   // key0, child0, key1, ...
@@ -501,6 +508,7 @@ struct Obj {
   bool single_filtered = false;
   std::vector<Filter> filters;
   std::vector<Att> atts;
+  std::vector<uint8_t> fill;   // fill-value message's value (empty: none defined)
   std::vector<uint64_t> dim_refs;
 };
 
@@ -597,6 +605,31 @@ bool parse_object(Rd &r, uint64_t oh, Obj &o) {
       case 0x03: if (!parse_dtype(r, p, p + sz, o.type)) return false; break;
       case 0x08: o.dataset = true; if (!parse_layout(r, p, sz, o)) return false; break;
       case 0x0B: if (!parse_filters(r, p, o.filters)) return false; break;
+      case 0x04: {   // old fill value: size, value
+        const uint64_t n = r.u(p, 4);
+        if (n > 0 && n <= 16 && n + 4 <= sz && r.has(p + 4, n)) o.fill.assign(r.f.buf.begin() + (p + 4), r.f.buf.begin() + (p + 4 + n));
+        break;
+      }
+      case 0x05: {   // fill value (IV.A.2.f): v1/v2 allocation / write time bytes + "defined"; v3 flags
+        const int ver = (int)r.u(p, 1);
+        uint64_t q = 0;
+        bool defined = false;
+        if (ver == 1 || ver == 2) {
+          defined = r.u(p + 3, 1) != 0;
+          q = p + 4;
+          if (ver == 1) defined = true;   // v1: size (+ value) always present
+        } else if (ver == 3) {
+          defined = (r.u(p + 1, 1) & 0x20) != 0;
+          q = p + 2;
+        }
+        if (defined && q + 4 <= p + sz) {
+          const uint64_t n = r.u(q, 4);
+          if (n > 0 && n <= 16 && q + 4 + n <= p + sz && r.has(q + 4, n))
+            o.fill.assign(r.f.buf.begin() + (q + 4), r.f.buf.begin() + (q + 4 + n));
+          else if (n == 0) o.fill.clear();
+        }
+        break;
+      }
       case 0x0C: {
         Att a;
         std::vector<uint64_t> refs;
@@ -641,8 +674,9 @@ bool parse_object(Rd &r, uint64_t oh, Obj &o) {
 // ---------------------------------------------------------------- chunks (III.A.1, VII.B filters)
 struct ChunkRef { uint64_t addr, size; uint32_t mask; };
 
-bool chunk_index_v1(Rd &r, uint64_t node, int rank, std::map<std::vector<uint64_t>, ChunkRef> &out, int guard) {
-  if (guard > 32 || !r.sig(node, "TREE") || r.u(node + 4, 1) != 1) return false;
+bool chunk_index_v1(Rd &r, uint64_t node, int rank, std::map<std::vector<uint64_t>, ChunkRef> &out, int guard,
+                    uint64_t &visited) {
+  if (guard > 32 || ++visited > kMaxNodes || !r.sig(node, "TREE") || r.u(node + 4, 1) != 1) return false;
   const int level = (int)r.u(node + 5, 1);
   const uint64_t n = r.u(node + 6, 2);
   const int O = r.f.off_size;
@@ -652,7 +686,7 @@ bool chunk_index_v1(Rd &r, uint64_t node, int rank, std::map<std::vector<uint64_
     const uint64_t key = q + i * (ksz + O);
     const uint64_t child = r.addr(key + ksz);
     if (level > 0) {
-      if (!chunk_index_v1(r, child, rank, out, guard + 1)) return false;
+      if (!chunk_index_v1(r, child, rank, out, guard + 1, visited)) return false;
       continue;
     }
     ChunkRef c;
@@ -716,19 +750,39 @@ bool unfilter(const Var &v, const std::vector<uint8_t> &in, uint32_t mask, uint6
   return true;
 }
 
-// Fill bytes of one element (the _FillValue attribute, else zeros), file order.
+// Fill bytes of one element, file order: the dataset's fill-value message
+// (what HDF5 returns for storage never written, and what netCDF-C reads back),
+// else the _FillValue attribute, else netCDF-C's NC_FILL_* default of the
+// type (netcdf.h), which netCDF-C stores in that message itself.
 std::vector<uint8_t> fill_bytes(const Var &v) {
+  if ((int)v.fill_msg.size() == v.esize && v.esize > 0) return v.fill_msg;
   std::vector<uint8_t> b(v.esize, 0);
+  bool have = false;
+  double x = 0.0;
   for (const Att &a : v.atts)
-    if (a.name == "_FillValue" && !a.num.empty()) {
-      const double x = a.num[0];
-      uint64_t u = 0;
-      if (v.nctype == 5) { float f = (float)x; uint32_t w; std::memcpy(&w, &f, 4); u = w; }
-      else if (v.nctype == 6) std::memcpy(&u, &x, 8);
-      else if (v.nctype == 1 || v.nctype == 3 || v.nctype == 4 || v.nctype == 10) u = (uint64_t)(int64_t)x;
-      else u = (uint64_t)x;
-      for (int k = 0; k < v.esize; k++) b[v.big_endian ? v.esize - 1 - k : k] = (uint8_t)(u >> (8 * k));
+    if (a.name == "_FillValue" && !a.num.empty()) { x = a.num[0]; have = true; }
+  uint64_t u = 0;
+  if (have) {
+    if (v.nctype == 5) { float f = (float)x; uint32_t w; std::memcpy(&w, &f, 4); u = w; }
+    else if (v.nctype == 6) std::memcpy(&u, &x, 8);
+    else if (v.nctype == 1 || v.nctype == 3 || v.nctype == 4 || v.nctype == 10) u = (uint64_t)(int64_t)x;
+    else u = (uint64_t)x;
+  } else {
+    switch (v.nctype) {
+      case 1: u = (uint64_t)(int64_t)-127; break;                   // NC_FILL_BYTE
+      case 3: u = (uint64_t)(int64_t)-32767; break;                 // NC_FILL_SHORT
+      case 4: u = (uint64_t)(int64_t)-2147483647; break;            // NC_FILL_INT
+      case 5: { float f = 9.9692099683868690e+36f; uint32_t w; std::memcpy(&w, &f, 4); u = w; break; }
+      case 6: { double d = 9.9692099683868690e+36; std::memcpy(&u, &d, 8); break; }
+      case 7: u = 255u; break;                                      // NC_FILL_UBYTE
+      case 8: u = 65535u; break;                                    // NC_FILL_USHORT
+      case 9: u = 4294967295u; break;                               // NC_FILL_UINT
+      case 10: u = (uint64_t)(int64_t)-9223372036854775806LL; break;  // NC_FILL_INT64
+      case 11: u = 18446744073709551614ull; break;                  // NC_FILL_UINT64
+      default: u = 0; break;                                        // NC_FILL_CHAR
     }
+  }
+  for (int k = 0; k < v.esize && k < 8; k++) b[v.big_endian ? v.esize - 1 - k : k] = (uint8_t)(u >> (8 * k));
   return b;
 }
 
@@ -802,6 +856,7 @@ bool open(File &f) {
     v.single_mask = o.single_mask;
     v.fa_page_bits = o.fa_bits;
     v.filters = o.filters;
+    if ((int)o.fill.size() == v.esize) v.fill_msg = o.fill;
     if (v.layout == 2 && v.chunk.size() != v.shape.size()) { f.err = "chunk rank of " + l.name; return false; }
     f.vars.push_back(std::move(v));
   }
@@ -858,7 +913,8 @@ bool read(const File &f, const Var &v, uint64_t start, uint64_t count, uint8_t *
   };
   std::vector<ChunkRef> by_linear;   // implicit / fixed array: by linear chunk index
   if (v.index_type == 0) {
-    if (v.addr != kUndef && !chunk_index_v1(r, v.addr, rank, idx, 0)) return false;
+    uint64_t visited = 0;
+    if (v.addr != kUndef && !chunk_index_v1(r, v.addr, rank, idx, 0, visited)) return false;
   } else if (v.index_type == 1) {
     if (v.addr != kUndef) {
       ChunkRef c{v.addr, v.single_size ? v.single_size : cbytes, v.single_mask};

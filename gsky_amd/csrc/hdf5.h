@@ -60,6 +60,10 @@ struct Var {
   uint32_t single_mask = 0;
   int fa_page_bits = 0;
   std::vector<Filter> filters;
+  // the fill-value message (0x05, or the old 0x04) when it defines a value:
+  // one element in the file's byte order; netCDF-C writes its NC_FILL_*
+  // default there for variables without _FillValue
+  std::vector<uint8_t> fill_msg;
 };
 
 struct File {

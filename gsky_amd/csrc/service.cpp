@@ -377,9 +377,13 @@ void dispatch_loop(Service *s) {
       if (s->inflight > 0 && s->window_us > 0 && (int)s->queue.size() < s->max_batch) {
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(s->window_us);
         s->cv_work.wait_until(lk, until, [&] {
-          return s->stop || (int)s->queue.size() >= s->max_batch || s->inflight == 0;
+          return s->stop || (int)s->queue.size() >= s->max_batch || s->inflight == 0 || s->reg_waiting > 0;
         });
         if (s->stop) break;
+        // a registration that started waiting during the window (it woke on
+        // inflight == 0 too) changes the registry now: launching here would
+        // run a batch beside it, reading uploads it may free
+        if (s->reg_waiting > 0) continue;
       }
       k = s->free_slots.front();
       s->free_slots.pop_front();

@@ -144,6 +144,14 @@ class Var:
     filters: Tuple[str, ...] = ("shuffle", "deflate")
     compact: bool = False
     skip_chunks: Tuple[int, ...] = ()               # linear chunk indices never written (read as the fill value)
+    fill_msg: bool = True                           # the fill-value message (0x05), as netCDF-C always writes it
+
+
+def nc_fill_default(dt: np.dtype):
+    """netCDF-C's NC_FILL_* default of a numpy type (netcdf.h)."""
+    return {"i1": -127, "u1": 255, "i2": -32767, "u2": 65535, "i4": -2147483647, "u4": 4294967295,
+            "i8": -9223372036854775806, "u8": 18446744073709551614, "f4": 9.9692099683868690e+36,
+            "f8": 9.9692099683868690e+36}[np.dtype(dt).str[1:]]
 
 
 class _Heap:
@@ -313,6 +321,16 @@ class Writer:
         arr = np.ascontiguousarray(v.data)
         es = arr.dtype.itemsize
         msgs = [(0x01, dspace_msg(arr.shape, 1 if self.sb < 2 else 2)), (0x03, dtype_msg(arr.dtype))]
+        if v.fill_msg:
+            # netCDF-C sets the dataset's fill value to _FillValue, else to the
+            # type's NC_FILL_* default; version 2 for superblocks 0 / 1, else 3
+            fv = v.atts.get("_FillValue")
+            fv = np.asarray(fv if fv is not None else nc_fill_default(arr.dtype), arr.dtype.newbyteorder("="))
+            raw = fv.astype(arr.dtype).tobytes()
+            if self.sb < 2:
+                msgs.append((0x05, bytes([2, 2, 2, 1]) + struct.pack("<I", len(raw)) + raw))
+            else:
+                msgs.append((0x05, bytes([3, 2 | (2 << 2) | 0x20]) + struct.pack("<I", len(raw)) + raw))
         if v.compact:
             raw = arr.tobytes()
             msgs.append((0x08, bytes([3, 0]) + struct.pack("<H", len(raw)) + raw))

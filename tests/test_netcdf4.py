@@ -36,7 +36,7 @@ def _pair(tmp_path, data, lon, lat, name="v", fill=None, atts=None, time=None, *
     variables.append(Var(name, tuple(d for d, _ in dims), data, atts=vatts,
                          chunks=kw.pop("chunks", tuple(min(8, s) for s in data.shape)),
                          filters=kw.pop("filters", ("shuffle", "deflate")), compact=kw.pop("compact", False),
-                         skip_chunks=kw.pop("skip_chunks", ())))
+                         skip_chunks=kw.pop("skip_chunks", ()), fill_msg=kw.pop("fill_msg", True)))
     n4 = str(tmp_path / "nc4.nc")
     write_nc4(n4, dims, variables, {"Conventions": "CF-1.6", "history": ("__vstr__", "written by h5write")}, **kw)
     return c, n4
@@ -107,6 +107,27 @@ def test_netcdf4_big_endian_and_unwritten_chunks(tmp_path):
     exp[10:20, 10:20] = -5                      # chunk 4 of the 2 x 3 chunk grid
     assert np.array_equal(got, exp)
     assert ingest.info(n4).nodata == -5.0
+
+
+@pytest.mark.parametrize("fill_msg", [True, False])
+@pytest.mark.parametrize("dt", [">i4", "<i2", "<f4", ">f8", "u1"])
+@pytest.mark.parametrize("superblock", [0, 2])
+def test_netcdf4_unwritten_chunks_without_fillvalue(tmp_path, fill_msg, dt, superblock):
+    """A variable without _FillValue: unwritten chunks read as netCDF-C's
+    NC_FILL_* default of the type -- from the dataset's fill-value message
+    (which netCDF-C writes), or from the type's default when the message is
+    absent -- never as zeros."""
+    from .h5write import nc_fill_default
+    data = (np.arange(20 * 30) % 97 + 1).astype(dt).reshape(1, 20, 30)
+    _, n4 = _pair(tmp_path, data, np.arange(30) * 1.0, -np.arange(20) * 1.0, fill=None, time=np.arange(1),
+                  chunks=(1, 10, 10), skip_chunks=(1, 4), fill_msg=fill_msg, superblock=superblock)
+    ndt = np.dtype(dt).newbyteorder("=")
+    got = ingest.read_host(n4, 1).view(ndt)
+    exp = data[0].astype(ndt).copy()
+    fv = np.asarray(nc_fill_default(ndt), ndt)
+    exp[0:10, 10:20] = fv                        # chunk 1 of the 2 x 3 chunk grid
+    exp[10:20, 10:20] = fv                       # chunk 4
+    assert np.array_equal(got.reshape(exp.shape), exp)
 
 
 def test_netcdf4_many_attributes_dense_btree(tmp_path):

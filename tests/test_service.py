@@ -258,3 +258,71 @@ def test_service_workers_share_one_gpu(oracle, direct):
         assert svc.stats()["requests"] > st["requests"] + 3
     finally:
         assert svc.shutdown() == 0
+
+
+def _warp_loop(sock, wid, jobs, rounds, q, go):
+    """A worker process: its jobs `rounds` times over (all workers start on `go`)."""
+    os.environ["GSKYHIP_SERVICE"] = sock
+    from gsky_amd import worker as W
+    go.wait(120)
+    res = []
+    for _ in range(rounds):
+        for (k, gt, w, h) in jobs:
+            r = W.warp_raster(W.GeoRPCGranule(path="/g/data/c2/g%d.tif" % k, bands=[1], width=w, height=h,
+                                              dstSRS="EPSG:3857", dstGeot=list(gt)))
+            res.append((r.error, r.raster.data if r.raster else b""))
+    q.put((wid, res))
+
+
+@pytest.mark.gpu
+def test_service_register_while_batches_in_flight(oracle):
+    """with a batching window (window_us > 0) a registration that
+    arrives while batches are in flight must not run beside a newly launched
+    batch -- a granule refresh frees the old upload.  6 workers warp in a
+    loop while the granules are registered again and again; every window
+    stays bit-exact against the oracle."""
+    from gsky_amd import WarpService
+    from gsky_amd.tiles import bbox_to_geot
+    cfg = synth.config_c2(scale=0.1, tiles_per_side=4, tile_px=256)
+    sock = _sock_path()
+    svc = WarpService(sock, max_batch=16, window_us=300)
+    try:
+        def reg_all():
+            for k, g in enumerate(cfg.granules):
+                svc.register_granule("/g/data/c2/g%d.tif" % k, 1, g.data, g.geot, "EPSG:3577", g.nodata,
+                                     block=(128, 64))
+        reg_all()
+        jobs = [(k, bbox_to_geot(w, h, bb), w, h) for (bb, w, h), ks in zip(cfg.tiles, cfg.pairs) for k in ks]
+        ctx = mp.get_context("spawn")
+        q, go = ctx.Queue(), ctx.Event()
+        n_workers, rounds = 6, 6
+        procs = [ctx.Process(target=_warp_loop, args=(sock, r, jobs[r::n_workers], rounds, q, go))
+                 for r in range(n_workers)]
+        for p in procs:
+            p.start()
+        time.sleep(5.0)
+        go.set()
+        n_reg = 0
+        t_end = time.time() + 60
+        while n_reg < 12 and time.time() < t_end:   # refreshes while the workers' batches run
+            reg_all()
+            n_reg += 1
+        got = dict(q.get(timeout=300) for _ in procs)
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+        aea, wm = oracle.crs("EPSG:3577"), oracle.crs("EPSG:3857")
+        want = {}
+        for (k, gt, w, h) in jobs:
+            g = cfg.granules[k]
+            arr, _, _, _ = oracle.warp(oracle.make_granule(g.data, g.geot, g.nodata, block=(128, 64)), aea, wm,
+                                       list(gt), w, h)
+            want[(k, tuple(gt))] = arr.tobytes()
+        for r in range(n_workers):
+            mine = jobs[r::n_workers] * rounds
+            assert len(got[r]) == len(mine)
+            for (k, gt, w, h), (err, data) in zip(mine, got[r]):
+                assert err == "OK" and data == want[(k, tuple(gt))], (k, gt, err)
+        assert n_reg >= 1 and svc.stats()["granules"] == len(cfg.granules)
+    finally:
+        assert svc.shutdown() == 0
