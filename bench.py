@@ -661,17 +661,11 @@ def run_c5(ctx: Ctx, args):
     dt = ctx.timed(lambda: b.render(sp), args.steps, args.warmup)
     plan_ms = event_ms(lambda: b.render(sp, phase=1), max(3, args.steps))
     render_ms = event_ms(lambda: b.render(sp, phase=2), max(3, args.steps))
-    # algorithmic bytes of the render launch: every (granule, picked overview
-    # level) the batch samples, the bounding box of its pairs' source
-    # footprints read once (data and QA granules alike), + the RGBA out
-    fp = {}
-    for g, lx, ly, es, x0, y0, x1, y1 in b.pair_info().tolist():
-        if x1 <= x0 or y1 <= y0:
-            continue
-        k = (g, lx, ly, es)
-        a = fp.get(k)
-        fp[k] = (x0, y0, x1, y1) if a is None else (min(a[0], x0), min(a[1], y0), max(a[2], x1), max(a[3], y1))
-    src = sum((x1 - x0) * (y1 - y0) * k[3] for k, (x0, y0, x1, y1) in fp.items())
+    # algorithmic bytes of the render launch: the distinct
+    # source elements every pair's window pixels pick at the picked level,
+    # data and QA rasters alike (gskyhip_render_touched), x element bytes,
+    # + 4 B RGBA per output pixel; the 128-B lines holding them beside it
+    src, src_lines = b.touched_bytes()
     abytes = int(src + cfg.out_pixels * 4)
     achieved = abytes / (render_ms / 1e3) / 1e9
     # p50 single-tile latency: each sampled tile as its own request
@@ -689,10 +683,10 @@ def run_c5(ctx: Ctx, args):
                         "kernel": "render_nn_kernel<int16, mask> + render_general_kernel (phase 2, rank 0)",
                         "kernel_ms": round(render_ms, 4), "plan_ms": round(plan_ms, 4),
                         "algorithmic_bytes_per_launch": abytes, "source_bytes": int(src),
-                        "source_levels": len(fp),
-                        "bytes": "per (granule, picked overview level) the bounding box of the pairs' source "
-                                 "footprints (gskyhip_render_pair_info) x element size, once; + 4 B RGBA per "
-                                 "output pixel", "lib_sha16": lib_sha()}}
+                        "source_line_bytes": int(src_lines),
+                        "bytes": "distinct source elements picked by every pair's window pixels (data and QA, "
+                                 "picked overview level; gskyhip_render_touched) x element size, + 4 B RGBA per "
+                                 "output pixel; source_line_bytes: the 128-B lines holding them", "lib_sha16": lib_sha()}}
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
         from oracle import oracle as O
         cores = host_cores()

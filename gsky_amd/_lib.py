@@ -96,7 +96,7 @@ EXPORTS = [
     "gskyhip_drill_workspace_size", "gskyhip_drill_batch", "gskyhip_drill_descriptors",
     "gskyhip_drill_merge", "gskyhip_fnv32a", "gskyhip_version", "gskyhip_device_count",
     "gskyhip_render_status",
-    "gskyhip_render_tile_info", "gskyhip_render_pair_info", "gskyhip_compute_reproject_extent",
+    "gskyhip_render_tile_info", "gskyhip_render_pair_info", "gskyhip_render_touched", "gskyhip_compute_reproject_extent",
     "gskyhip_service_run", "gskyhip_service_register_granule", "gskyhip_service_unregister_all",
     "gskyhip_service_stats", "gskyhip_service_stats_n", "gskyhip_service_shutdown", "gskyhip_drill_deciles_workspace_size",
     "gskyhip_drill_deciles", "gskyhip_band_math", "gskyhip_drill_descriptors_device", "gskyhip_drill_masks_device", "gskyhip_drill_masks_device_packed", "gskyhip_parse_numbers",
@@ -159,6 +159,8 @@ def lib() -> C.CDLL:
     L.gskyhip_service_shutdown.argtypes = [C.c_char_p]
     L.gskyhip_render_tile_info.argtypes = [vp, ci, ci, ci, vp, vp, vp]
     L.gskyhip_render_pair_info.argtypes = [vp, ci, ci, ci, vp, vp]
+    if hasattr(L, "gskyhip_render_touched"):   # (an older A/B library for timing comparisons lacks it)
+        L.gskyhip_render_touched.argtypes = [vp, ci, ci, ci, vp, vp]
     L.gskyhip_merge_rasters.argtypes = [C.POINTER(FlexRasterC), ci, C.POINTER(Mask), C.POINTER(vp), ci,
                                         C.POINTER(i32), C.POINTER(i32), C.POINTER(d), vp]
     L.gskyhip_scale.argtypes = [vp, ci, i64, d, C.POINTER(ScaleParams), vp, vp]

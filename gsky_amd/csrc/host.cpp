@@ -1633,6 +1633,12 @@ int gskyhip_render_tile_info(void *workspace, int n_tiles, int n_pairs, int max_
   return 0;
 }
 
+int gskyhip_render_touched(void *workspace, int n_tiles, int n_pairs, int max_tile_height, int64_t *bytes_out,
+                           void *stream) {
+  if (n_tiles < 0 || n_pairs < 0 || !bytes_out || (n_pairs > 0 && !workspace)) return GSKYHIP_E_ARG;
+  return launch_pair_touched(workspace, n_tiles, n_pairs, max_tile_height, bytes_out, (hipStream_t)stream);
+}
+
 int gskyhip_render_pair_info(void *workspace, int n_tiles, int n_pairs, int max_tile_height, int32_t *info_out,
                              void *stream) {
   if (n_tiles < 0 || n_pairs < 0 || (n_pairs > 0 && (!workspace || !info_out))) return GSKYHIP_E_ARG;

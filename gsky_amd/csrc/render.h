@@ -51,6 +51,7 @@ int launch_block_stats_batch(const RenderCall &c, const BlockStatsJob *jobs, int
 // Per pair of a planned batch: granule, picked level (x, y), element bytes,
 // source footprint [x0, y0, x1, y1) at that level (8 int32 per pair, device).
 int launch_pair_footprint(void *workspace, int n_tiles, int n_pairs, int max_h, int32_t *out, hipStream_t s);
+int launch_pair_touched(void *workspace, int n_tiles, int n_pairs, int max_h, int64_t *out2, hipStream_t s);
 
 // One reply of a warp batch (warp_operation_fast's outputs but the window).
 struct WarpResult {

@@ -18,6 +18,8 @@
 #include "stages.h"
 #include "render_common.h"
 #include <algorithm>
+#include <map>
+#include <vector>
 #include <cstdlib>
 #include <type_traits>
 
@@ -1855,6 +1857,57 @@ __global__ void pair_footprint_kernel(const PairPlan *pairs, const RowRec *rows,
   }
 }
 
+// Source elements and 128-byte lines the pairs of a planned batch touch
+// (gskyhip_render_touched: the algorithmic bytes of a batch, SURVEY.md 8(d)
+// "unique source bytes touched ... at the chosen overview level"): every
+// window pixel of every pair -- data and mask rasters alike, as GDAL reads
+// each granule's window -- picks its source element by the nearest-neighbour
+// rule of warp.go:271-300 (lin_coords + truncation + bounds); the element and
+// its line are set in per-level bitmaps (base[p]: bit offsets of pair p's
+// level in the element / line maps).  ROW_LINEAR and ROW_POOL rows (what the
+// band kernels render); rows computed exactly at render time are not counted.
+// Block = (pair, 4 rows), 256 threads over the window columns.
+__global__ void pair_touch_kernel(const PairPlan *pairs, const RowRec *rows, const Leaf *pool, int max_h,
+                                  const int64_t *base, uint32_t *ebits, uint32_t *lbits) {
+  const int p = blockIdx.x;
+  const PairPlan &pp = pairs[p];
+  const int64_t eb = base[2 * p], lb = base[2 * p + 1];
+  if (eb < 0 || pp.w <= 0) return;
+  const int es = type_size(pp.src_dtype);
+  for (int r = blockIdx.y * 4; r < min(pp.h, (int)blockIdx.y * 4 + 4); r++) {
+    const RowRec &rr = rows[(int64_t)p * max_h + r];
+    if (rr.kind != ROW_LINEAR && rr.kind != ROW_POOL) continue;
+    for (int ic = threadIdx.x; ic < pp.w; ic += blockDim.x) {
+      double sx, sy;
+      if (!lin_coords(rr, pool, ic, sx, sy) || sx < 0.0 || sy < 0.0) continue;
+      const double ax = sx + 1.0e-10, ay = sy + 1.0e-10;
+      if (ax >= (double)pp.band_x || ay >= (double)pp.band_y) continue;
+      const int64_t idx = (int64_t)(int)ay * pp.band_x + (int)ax;
+      const int64_t e = eb + idx, l = lb + idx * es / 128;
+      atomicOr(&ebits[e >> 5], 1u << (e & 31));
+      atomicOr(&lbits[l >> 5], 1u << (l & 31));
+    }
+  }
+}
+
+__global__ void popcount_kernel(const uint32_t *bits, int64_t n_words, const int64_t *word_es, int n_seg,
+                                unsigned long long *out) {
+  // word_es: n_seg x (first word, element bytes) of each level's segment
+  unsigned long long acc = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_words; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = bits[i];
+    if (!w) continue;
+    int lo = 0, hi = n_seg - 1;   // the segment holding word i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (word_es[2 * mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    acc += (unsigned long long)__popc(w) * (unsigned long long)word_es[2 * lo + 1];
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
 __global__ void pair_meta_kernel(const PairPlan *pairs, int n_pairs, int32_t *bbox, int32_t *dtype, double *nodata) {
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
@@ -2063,23 +2116,6 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   a.lds_mode = 0;
   a.cov_offsets = rc.cov_offsets;
   a.cov_stride = rc.cov_stride;
-  a.st_pol = 0;
-  a.ab_mode = 0;
-  a.ab_vfetch = 1;
-  a.ab_xcd = 0;
-  a.nn_colg = 0;
-  a.nn_pair = 0;
-#ifdef GSKYHIP_AB
-  a.nn_maskb = 0;
-  if (const char *mb = getenv("GSKYHIP_NN_MASKB")) a.nn_maskb = atoi(mb);
-  if (const char *cg = getenv("GSKYHIP_NN_COLG")) a.nn_colg = atoi(cg);
-  if (const char *np = getenv("GSKYHIP_NN_PAIR")) a.nn_pair = atoi(np);
-  if (const char *sp = getenv("GSKYHIP_NN_STPOL")) a.st_pol = atoi(sp);
-  if (const char *am = getenv("GSKYHIP_AB_MODE")) a.ab_mode = atoi(am);
-  if (const char *vf = getenv("GSKYHIP_NN_VFETCH")) a.ab_vfetch = atoi(vf);
-  if (const char *xc = getenv("GSKYHIP_NN_XCD")) a.ab_xcd = atoi(xc);
-  if (getenv("GSKYHIP_BIL_SEPSTAT")) a.ab_mode = 0x5E9;   // render_bil_sep_kernel's eligibility counters
-#endif
   const int bands = (rc.max_h + a.rows_per_block - 1) / a.rows_per_block;
   const dim3 grid((unsigned)(rc.n_tiles * bands));
   hipStream_t s = rc.stream;
@@ -2104,7 +2140,7 @@ int launch_render(const RenderCall &rc, const int32_t *out_ns, int n_out, const 
   if (lds_mode >= 0) {
     a.lds_mode = lds_mode;
     const int n_items = rc.n_tiles * ((rc.max_h + kLdsBandRows - 1) / kLdsBandRows) * ((rc.max_w + 511) / 512);
-    launch_lds_kernels(a, vt, mask, n_items, s);
+    launch_band_kernels(a, vt, mask, n_items, s);
     dispatch_render_1(a, rc.resample, mask, grid, true, s);
   } else if (n_out == 1) {
     dispatch_render_1(a, rc.resample, mask, grid, false, s);
@@ -2138,6 +2174,67 @@ int launch_pair_footprint(void *workspace, int n_tiles, int n_pairs, int max_h, 
   hipLaunchKernelGGL(pair_footprint_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, cv.pairs, cv.rows, cv.pool,
                      n_pairs, max_h, out);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
+}
+
+int launch_pair_touched(void *workspace, int n_tiles, int n_pairs, int max_h, int64_t *out2, hipStream_t s) {
+  out2[0] = out2[1] = 0;
+  if (n_pairs <= 0) return 0;
+  const Carve cv = carve(workspace, n_tiles, n_pairs, max_h);
+  std::vector<PairPlan> hp(n_pairs);
+  if (hipMemcpyAsync(hp.data(), cv.pairs, sizeof(PairPlan) * n_pairs, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return GSKYHIP_E_HIP;
+  // one element map and one line map per distinct level (band pointer), 32-bit aligned segments
+  struct Seg { int64_t ebit, lbit; };
+  std::map<const void *, Seg> segs;
+  std::vector<int64_t> base(2 * (size_t)n_pairs, -1), ew, lw;   // ew / lw: (first word, bytes per bit)
+  int64_t ebits = 0, lbits = 0;
+  for (int p = 0; p < n_pairs; p++) {
+    const PairPlan &pp = hp[p];
+    if (!pp.band || pp.w <= 0 || pp.h <= 0 || pp.band_x <= 0 || pp.band_y <= 0) continue;
+    auto it = segs.find(pp.band);
+    if (it == segs.end()) {
+      const int es = type_size(pp.src_dtype);
+      const int64_t n = (int64_t)pp.band_x * pp.band_y, nl = (n * es + 127) / 128;
+      ew.push_back(ebits / 32); ew.push_back(es);
+      lw.push_back(lbits / 32); lw.push_back(128);
+      it = segs.emplace(pp.band, Seg{ebits, lbits}).first;
+      ebits += (n + 31) / 32 * 32;
+      lbits += (nl + 31) / 32 * 32;
+    }
+    base[2 * p] = it->second.ebit;
+    base[2 * p + 1] = it->second.lbit;
+  }
+  if (segs.empty()) return 0;
+  const int64_t ew_words = ebits / 32, lw_words = lbits / 32;
+  const size_t bytes = (size_t)(ew_words + lw_words) * 4 + base.size() * 8 + (ew.size() + lw.size()) * 8 + 16;
+  char *dev = nullptr;
+  if (hipMalloc((void **)&dev, bytes) != hipSuccess) return GSKYHIP_E_HIP;
+  uint32_t *eb = (uint32_t *)dev, *lb = eb + ew_words;
+  int64_t *dbase = (int64_t *)(lb + lw_words + ((ew_words + lw_words) & 1));
+  int64_t *dew = dbase + base.size(), *dlw = dew + ew.size();
+  unsigned long long *cnt = (unsigned long long *)(dlw + lw.size());
+  int rc = 0;
+  if (hipMemsetAsync(dev, 0, (size_t)(ew_words + lw_words) * 4, s) != hipSuccess ||
+      hipMemsetAsync(cnt, 0, 16, s) != hipSuccess ||
+      hipMemcpyAsync(dbase, base.data(), base.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(dew, ew.data(), ew.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(dlw, lw.data(), lw.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+    rc = GSKYHIP_E_HIP;
+  if (!rc) {
+    hipLaunchKernelGGL(pair_touch_kernel, dim3((unsigned)n_pairs, (unsigned)((max_h + 3) / 4)), dim3(256), 0, s,
+                       cv.pairs, cv.rows, cv.pool, max_h, dbase, eb, lb);
+    hipLaunchKernelGGL(popcount_kernel, dim3(1024), dim3(256), 0, s, eb, ew_words, dew, (int)(ew.size() / 2), cnt);
+    hipLaunchKernelGGL(popcount_kernel, dim3(1024), dim3(256), 0, s, lb, lw_words, dlw, (int)(lw.size() / 2), cnt + 1);
+    unsigned long long h[2] = {0, 0};
+    if (hipGetLastError() != hipSuccess || hipMemcpyAsync(h, cnt, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = GSKYHIP_E_HIP;
+    out2[0] = (int64_t)h[0];
+    out2[1] = (int64_t)h[1];
+  }
+  (void)hipFree(dev);
+  return rc;
 }
 
 int launch_warp_jobs(const RenderCall &rc, const BlockStatsJob *jobs, int64_t max_px, void *scratch,

@@ -212,16 +212,6 @@ struct RenderArgs {
   int lds_mode;          // typed band kernels: kBilinear | kCanvas bits of the call
   const int64_t *cov_offsets;  // canvas mode: per tile element offset into one image (NULL: slots)
   int64_t cov_stride;          // ... and that image's row stride (elements)
-  int st_pol;                  // A/B build only: RGBA store cache policy (0 nt, 1 sc1, 2 sc0 sc1, 3 plain)
-  int ab_mode;                 // A/B build only: 1 skip the NN gathers, 2 skip the RGBA stores
-  int ab_vfetch;               // A/B build only: 0 = per-row scalar RowFix fetch in the NN kernel
-  int ab_xcd;                  // A/B build only: item order over the XCDs (1: a tile's blocks on one XCD, NN;
-                               //   2: XCD x the x-th contiguous eighth of the items, NN and bilinear)
-  int nn_colg;                 // A/B build only: NN single-entry blocks in column-group-major order
-  int nn_pair;                 // A/B build only: NN 16-bit single-entry rows by column pairs
-#ifdef GSKYHIP_AB
-  int nn_maskb;                // A/B build only: NN entries with a mask layer, all data + mask gathers at once
-#endif
 };
 
 // ---------------------------------------------------------------- typed fast path
@@ -424,15 +414,16 @@ __device__ __forceinline__ bool src_coords(const RowRec &rr, const Leaf *pool, c
   return false;
 }
 
-// Mask raster value (its own dtype, NN) for data window index (ic, ir).
+// Mask raster value (its own dtype, NN) for data window index (ic, ir) of an
+// entry of window width ew whose mask pair is mask_pair.
 template <int RES>
-__device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const RowRec *__restrict__ rows,
-                                          const Leaf *__restrict__ pool, const MaskSpecS *ms, const EntryD &e,
-                                          int ic, int ir) {
-  const EntryD &m = ents[e.mask_pair];
+__device__ __forceinline__ bool mask_fast_pair(const EntryD *__restrict__ ents, const RowRec *__restrict__ rows,
+                                               const Leaf *__restrict__ pool, const MaskSpecS *ms, int mask_pair,
+                                               int ew, int ic, int ir) {
+  const EntryD &m = ents[mask_pair];
   int mx = ic, my = ir;
-  if (m.w != e.w) {
-    const long iSrc = (long)ir * e.w + ic;
+  if (m.w != ew) {
+    const long iSrc = (long)ir * ew + ic;
     mx = (int)(iSrc % m.w);
     my = (int)(iSrc / m.w);
   }
@@ -453,11 +444,18 @@ __device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const
   return slot >= 0 && mask_bit(ms[slot], m.out_dtype, v);
 }
 
+template <int RES>
+__device__ __forceinline__ bool mask_fast(const EntryD *__restrict__ ents, const RowRec *__restrict__ rows,
+                                          const Leaf *__restrict__ pool, const MaskSpecS *ms, const EntryD &e,
+                                          int ic, int ir) {
+  return mask_fast_pair<RES>(ents, rows, pool, ms, e.mask_pair, e.w, ic, ir);
+}
+
 constexpr int kLdsBandRows = 16;   // rows per block of render_lds_kernel
 constexpr int kBilinear = 4, kCanvas = 8;   // render_lds_kernel modes (RenderArgs.lds_mode)
 
 // The typed band kernels (render_lds.hip) for value type `vt`.
-void launch_lds_kernels(const RenderArgs &a, int vt, bool mask, int n_items, hipStream_t s);
+void launch_band_kernels(const RenderArgs &a, int vt, bool mask, int n_items, hipStream_t s);
 // Generic kernels (render_generic{1,3}.hip); general_only: complex tiles only.
 void dispatch_render_1(const RenderArgs &a, int resample, bool mask, dim3 grid, bool general_only, hipStream_t s);
 void dispatch_render_3(const RenderArgs &a, int resample, bool mask, dim3 grid, bool general_only, hipStream_t s);

@@ -317,10 +317,10 @@ void launch_lds_t(const RenderArgs &a, bool mask, int n_items, hipStream_t s) {
 #undef GSKY_LDS_LAUNCH
 }
 
-void launch_lds_i16(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
-void launch_lds_u16(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
-void launch_lds_f32(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
-void launch_lds_i8(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
-void launch_lds_u8(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
+void launch_band_i16(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
+void launch_band_u16(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
+void launch_band_f32(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
+void launch_band_i8(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
+void launch_band_u8(const RenderArgs &a, bool mask, int n_items, hipStream_t s);
 
 }  // namespace gsky

@@ -25,8 +25,15 @@
 //     mode (c == nd) ? v : c, which is "v != nd && c == nd" without the
 //     second compare -- so no lane-mask logic lands on the scalar unit;
 //   * everything else (window edges inside the block, POOL rows with their
-//     leaves, failed transforms, entries carrying a mask layer) takes the
-//     general body with the per-pixel tests of the reference;
+//     leaves, failed transforms) takes the general body with the per-pixel
+//     tests of the reference;
+//   * stacks (round 6): an entry in fill mode whose block row holds no pixel
+//     its nodata could fill is skipped before its row record is read; an
+//     entry with a mask layer whose mask row picks the same source element
+//     (C5's QA granules) gathers data and mask from one index, a 64-column
+//     slot only where some lane can still change; masked stacks prefetch
+//     every entry's descriptor, row record and mask row in one round of
+//     vector loads (nn_fold_row_stack) instead of the serial scalar chain;
 //   * output: Scale in the canvas type, the uint8(float32) range test only
 //     when clip * scale can reach 2^31 (wave-uniform), and one LDS read of a
 //     256-entry table that has EncodePNG's transparency rule baked in (entry
@@ -122,7 +129,7 @@ __device__ __forceinline__ void nn_partial_row(__amdgpu_buffer_rsrc_t rs, double
 // nothing is folded and false sends the row to the fp64 bodies.
 // PART: the window edge falls inside the block (pixels outside the window
 // read nothing and fold nothing).
-template <typename T, int NPX, bool PART, bool WIDE = false>
+template <typename T, int NPX, bool PART>
 __device__ __forceinline__ bool nn_fix_row(__amdgpu_buffer_rsrc_t rs, int64_t fx0, int64_t fy0, int64_t fdx,
                                            int64_t fdy, int ic0, int lim, int bx, typename VOf<T>::type nd,
                                            bool fill_mode, typename VOf<T>::type (&c)[NPX]) {
@@ -154,7 +161,7 @@ __device__ __forceinline__ bool nn_fix_row(__amdgpu_buffer_rsrc_t rs, int64_t fx
   if (__builtin_amdgcn_ballot_w64(amin < 2u * kFixMargin) != 0) return false;
   V vv[NPX];
 #pragma unroll
-  for (int q = 0; q < NPX; q++) vv[q] = WIDE ? buf_load_w<T>(rs, off[q]) : buf_load<T>(rs, off[q]);
+  for (int q = 0; q < NPX; q++) vv[q] = buf_load<T>(rs, off[q]);
   if (!fill_mode) {
 #pragma unroll
     for (int q = 0; q < NPX; q++) {
@@ -173,294 +180,183 @@ __device__ __forceinline__ bool nn_fix_row(__amdgpu_buffer_rsrc_t rs, int64_t fx
   return true;
 }
 
-// nn_fix_row's cover case for 2-byte T with a lane owning column PAIRS
-// (A/B, GSKYHIP_NN_PAIR=1): the lane's pixels are columns icp + 128 q + k
-// (k = 0, 1) -> c[2 q + k], so one aligned dword gather serves both pixels of
-// a pair whenever their source pixels share it (C2: ~70 % of pairs; the
-// rest take a second, lane-masked gather) and the RGBA leaves as 8-byte
-// stores: half the 64-lane gather and store instructions, whose per-quad L1
-// work bounds the row-major body.  Same fixed-point values,
-// margin test and fold as nn_fix_row: the same result bit for bit.
+// The fold of one LINEAR row of an entry carrying a mask layer whose mask row
+// picks the same source element (C5's QA stacks: the QA granule shares the
+// data granule's grid, picked level and window, so the planner gives both
+// pairs the same row record): each window pixel's element index once, the
+// data and mask gathers from it side by side, and only for 64-column slots
+// where some lane can still change -- in fill mode (tile_merger.go:47-58) a
+// pixel whose canvas no longer holds this raster's nodata can take nothing,
+// so a slot with no such lane issues neither gather.  The same rule per
+// pixel as the general body + mask_fast(): in window, v != nodata, not
+// masked (ComputeMask, tile_merger.go:314-445), and in fill mode canvas ==
+// nodata; a pixel whose element is outside the band takes the window fill
+// and the mask's fill (warp.go:246-247), as nn_fetch() does.
 template <typename T, int NPX>
-__device__ __forceinline__ bool nn_fix_row_pair(__amdgpu_buffer_rsrc_t rs, int64_t fx0, int64_t fy0, int64_t fdx,
-                                                int64_t fdy, int icp, int bx, typename VOf<T>::type nd,
-                                                bool fill_mode, typename VOf<T>::type (&c)[NPX]) {
-  static_assert(sizeof(T) == 2 && NPX % 2 == 0, "pairs of 16-bit pixels");
+__device__ __forceinline__ void nn_masked_same_row(const MaskSpecS &ms, int mdt, int32_t mfill,
+                                                   __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t mrs,
+                                                   double xs0, double ys0, double dX, double dY, int ic0, int lim,
+                                                   int bx, int by, typename VOf<T>::type nd,
+                                                   typename VOf<T>::type fillv, bool fill_mode,
+                                                   typename VOf<T>::type (&c)[NPX]) {
   using V = typename VOf<T>::type;
-  constexpr int NQ = NPX / 2;
-  uint64_t X = (uint64_t)(fx0 + (int64_t)icp * fdx), Y = (uint64_t)(fy0 + (int64_t)icp * fdy);
-  const uint64_t SX = (uint64_t)fdx << 7, SY = (uint64_t)fdy << 7;   // 128 columns
-  uint32_t amin = 0xFFFFFFFFu;
-  uint32_t e0[NQ], e1[NQ];
+  const bool m8 = mdt == GSKYHIP_BYTE || mdt == GSKYHIP_SIGNEDBYTE;
 #pragma unroll
-  for (int q = 0; q < NQ; q++) {
-    const uint64_t X1 = X + (uint64_t)fdx, Y1 = Y + (uint64_t)fdy;
-    e0[q] = __umul24((uint32_t)(Y >> 32), (uint32_t)bx) + (uint32_t)(X >> 32);
-    e1[q] = __umul24((uint32_t)(Y1 >> 32), (uint32_t)bx) + (uint32_t)(X1 >> 32);
-    amin = min(amin, min(min((uint32_t)X + kFixMargin, (uint32_t)Y + kFixMargin),
-                         min((uint32_t)X1 + kFixMargin, (uint32_t)Y1 + kFixMargin)));
-    asm volatile("" : "+v"(e0[q]), "+v"(e1[q]));
-    X += SX;
-    Y += SY;
-  }
-  if (__builtin_amdgcn_ballot_w64(amin < 2u * kFixMargin) != 0) return false;
-  uint32_t w0[NQ], w1[NQ];
+  for (int h = 0; h < NPX; h += 4) {
+    uint32_t idx[4];
+    bool need[4];
 #pragma unroll
-  for (int q = 0; q < NQ; q++) w0[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (e0[q] * 2u) & ~3u, 0, 0);
-#pragma unroll
-  for (int q = 0; q < NQ; q++) {
-    w1[q] = w0[q];
-    if ((e1[q] ^ e0[q]) > 1u) w1[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (e1[q] * 2u) & ~3u, 0, 0);
-  }
-#pragma unroll
-  for (int q = 0; q < NQ; q++) {
-    const uint32_t h0 = (w0[q] >> ((e0[q] & 1u) * 16u)) & 0xFFFFu, h1 = (w1[q] >> ((e1[q] & 1u) * 16u)) & 0xFFFFu;
-    const V v0 = std::is_signed<T>::value ? (V)(int16_t)h0 : (V)h0;
-    const V v1 = std::is_signed<T>::value ? (V)(int16_t)h1 : (V)h1;
-    if (!fill_mode) {
-      c[2 * q] = v0 != nd ? v0 : c[2 * q];
-      c[2 * q + 1] = v1 != nd ? v1 : c[2 * q + 1];
-    } else {
-      c[2 * q] = c[2 * q] == nd ? v0 : c[2 * q];
-      c[2 * q + 1] = c[2 * q + 1] == nd ? v1 : c[2 * q + 1];
+    for (int q = 0; q < 4; q++) {
+      const int ic = ic0 + 64 * (h + q);
+      const double dist = (double)ic;
+      const bool inw = (unsigned)ic < (unsigned)lim;
+      idx[q] = nn_index_sxy(xs0 + dX * dist, ys0 + dY * dist, inw, bx, by);
+      need[q] = inw & (!fill_mode | (c[h + q] == nd));
     }
-  }
-  return true;
-}
-
-// The fold of one `inside` LINEAR row covering the block (nn_fix_row's cover
-// case) with cooperative loads instead of per-lane gathers: for each of the
-// lane's 8 pixels the wave's 64 consecutive output columns read a source run
-// of at most 2 rows and 32 * (4 / sizeof(T)) - 2 columns; lanes 0-31 load
-// that run of the upper row and lanes 32-63 of the lower as consecutive
-// dwords (one coalesced load instruction), and every lane picks its value
-// with ds_bpermute.  The same source pixels as the gathers (the fixed-point
-// indices), so the same result bit for bit.  false: ambiguous (nothing
-// folded, the fp64 bodies follow) -- or, with nothing loaded yet, a run that
-// does not fit, where the per-lane gathers are used.  A/B (GSKYHIP_NN_COOP).
-template <typename T, int NPX>
-__device__ __forceinline__ bool nn_fix_row_coop(__amdgpu_buffer_rsrc_t rs, int64_t fx0, int64_t fy0, int64_t fdx,
-                                                int64_t fdy, int ic0, int lim, int bx, typename VOf<T>::type nd,
-                                                bool fill_mode, typename VOf<T>::type (&c)[NPX], int lane) {
-  using V = typename VOf<T>::type;
-  constexpr int K = 4 / (int)sizeof(T);   // elements per dword
-  uint64_t X = (uint64_t)(fx0 + (int64_t)ic0 * fdx), Y = (uint64_t)(fy0 + (int64_t)ic0 * fdy);
-  const uint64_t SX = (uint64_t)fdx << 6, SY = (uint64_t)fdy << 6;
-  uint32_t amin = 0xFFFFFFFFu;
-  int ix[NPX], iy[NPX];
+    V vv[4];
+    uint32_t mraw[4];
 #pragma unroll
-  for (int q = 0; q < NPX; q++) {
-    ix[q] = (int)(uint32_t)(X >> 32);
-    iy[q] = (int)(uint32_t)(Y >> 32);
-    amin = min(amin, min((uint32_t)X + kFixMargin, (uint32_t)Y + kFixMargin));
-    X += SX;
-    Y += SY;
-  }
-  if (__builtin_amdgcn_ballot_w64(amin < 2u * kFixMargin) != 0) return false;
-  // per pixel slot: the run's rows and columns (monotone in the column: the
-  // end lanes hold the extremes)
-  int base0[NPX], base1[NPX], r0s[NPX];
-  bool fits = true;
-#pragma unroll
-  for (int q = 0; q < NPX; q++) {
-    const int xa = __builtin_amdgcn_readlane(ix[q], 0), xb2 = __builtin_amdgcn_readlane(ix[q], 63);
-    const int ya = __builtin_amdgcn_readlane(iy[q], 0), yb = __builtin_amdgcn_readlane(iy[q], 63);
-    const int lo = min(xa, xb2), hi = max(xa, xb2), r0 = min(ya, yb), r1 = max(ya, yb);
-    fits = fits & (hi - lo <= 32 * K - 2 * K) & (r1 - r0 <= 1);
-    const int e0 = r0 * bx + lo, e1 = (r0 + 1) * bx + lo;
-    base0[q] = e0 & ~(K - 1);
-    base1[q] = e1 & ~(K - 1);
-    r0s[q] = r0;
-  }
-  V vv[NPX];
-  if (fits) {
-    uint32_t w[NPX];
-#pragma unroll
-    for (int q = 0; q < NPX; q++) {
-      const int mybase = lane < 32 ? base0[q] : base1[q];
-      w[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(mybase / K + (lane & 31)) * 4u, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < NPX; q++) {
-      const bool upper = iy[q] == r0s[q];
-      const int rel = iy[q] * bx + ix[q] - (upper ? base0[q] : base1[q]);
-      const int src = (upper ? 0 : 32) + rel / K;
-      const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(src * 4, (int)w[q]);
-      const uint32_t sh = (uint32_t)(rel % K) * 8u * (uint32_t)sizeof(T);
-      if constexpr (sizeof(T) == 4) {
-        vv[q] = __builtin_bit_cast(V, got);
-      } else if constexpr (sizeof(T) == 2) {
-        const uint32_t h = (got >> sh) & 0xFFFFu;
-        vv[q] = std::is_signed<T>::value ? (V)(int16_t)h : (V)h;
-      } else {
-        const uint32_t b = (got >> sh) & 0xFFu;
-        vv[q] = std::is_signed<T>::value ? (V)(int8_t)b : (V)b;
+    for (int q = 0; q < 4; q++) {
+      vv[q] = 0;
+      mraw[q] = 0;
+      if (__builtin_amdgcn_ballot_w64(need[q]) != 0) {
+        // kNoPx reads nothing: its offset is past every band (range-checked)
+        vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
+        mraw[q] = m8 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(mrs, idx[q], 0, 0)
+                     : (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(mrs, idx[q] * 2u, 0, 0);
       }
     }
-  } else {
 #pragma unroll
-    for (int q = 0; q < NPX; q++)
-      vv[q] = buf_load<T>(rs, (__umul24((uint32_t)iy[q], (uint32_t)bx) + (uint32_t)ix[q]) * (uint32_t)sizeof(T));
+    for (int q = 0; q < 4; q++) {
+      const bool hit = idx[q] != kNoPx;
+      const V v = hit ? vv[q] : fillv;
+      int32_t mv;
+      switch (mdt) {   // nn_fetch<mask type>'s value
+        case GSKYHIP_SIGNEDBYTE: mv = (int32_t)(int8_t)(uint8_t)mraw[q]; break;
+        case GSKYHIP_INT16: mv = (int32_t)(int16_t)(uint16_t)mraw[q]; break;
+        case GSKYHIP_BYTE: mv = (int32_t)(uint8_t)mraw[q]; break;
+        default: mv = (int32_t)(uint16_t)mraw[q]; break;
+      }
+      mv = hit ? mv : mfill;
+      const bool take = need[q] & (v != nd) && !mask_bit(ms, mdt, mv);
+      c[h + q] = take ? v : c[h + q];
+    }
   }
-  if (!fill_mode) {
-#pragma unroll
-    for (int q = 0; q < NPX; q++) c[q] = (vv[q] != nd) ? vv[q] : c[q];
-  } else {
-#pragma unroll
-    for (int q = 0; q < NPX; q++) c[q] = (c[q] == nd) ? vv[q] : c[q];
-  }
-  return true;
 }
 
-// A/B (GSKYHIP_NN_MASKB=1; 0.526 vs 0.494 ms on C5, profiles/r05o_c5.jsonl):
-// the general body for an entry carrying a mask layer (C5's QA stacks), all
-// NPX pixels at once: every data index and every mask index first, then all
-// 2 x NPX gathers in flight together, then the fold -- mask_fast() per pixel
-// inside the fold chained the mask entry's descriptor, row record and gather
-// behind each taken pixel (4 dependent memory latencies per half row).  The
-// same expressions as the general body + mask_fast(): the same result.
-template <typename T, int NPX>
-__device__ __forceinline__ void nn_masked_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
+// One stack entry's render descriptor (EntryD) and its row record (RowRec)
+// for one tile row, as wave-uniform values: loaded from memory by
+// nn_entry_row(), or read out of a wave's prefetched lanes by
+// nn_fold_row_stack().
+struct EntryU {
+  const void *band;
+  int64_t row_base;
+  int bx, by, xoff, yoff, w, h, ns, fill_mode, mask_pair;
+  uint32_t nd, fill;
+};
+struct RowU {
+  double v[4];
+  int kind, inside, nleaf, pool_off;
+};
+// the mask pair of a masked entry on this row: its window width / height,
+// level size, type, fill, band and the row record's kind + LINEAR values
+struct MaskU {
+  const void *band;
+  double v[4];
+  int w, h, bx, by, dt, kind;
+  int32_t fill;
+};
+
+// Where nn_entry_core() takes the row's fixed-point form and record from:
+// RowMem reads them from memory at first use (scalar loads of a uniform
+// pointer: the fixed-point form first, the record only for the fp64 bodies),
+// RowVal holds values read out of a prefetched lane.
+struct RowMem {
+  const RowRec *rr;
+  const RowFix *fp;   // nullptr: no fixed-point form
+  __device__ __forceinline__ bool fix(int64_t (&f)[4]) const {
+    if (!fp) return false;
+    f[0] = uni64(fp->x0);
+    if (f[0] == kFixNone) return false;
+    f[1] = uni64(fp->y0); f[2] = uni64(fp->dx); f[3] = uni64(fp->dy);
+    return true;
+  }
+  __device__ __forceinline__ int kind() const { return __builtin_amdgcn_readfirstlane(rr->kind); }
+  __device__ __forceinline__ int inside() const { return __builtin_amdgcn_readfirstlane(rr->inside); }
+  __device__ __forceinline__ int nleaf() const { return __builtin_amdgcn_readfirstlane(rr->nleaf); }
+  __device__ __forceinline__ int pool_off() const { return __builtin_amdgcn_readfirstlane(rr->pool_off); }
+  __device__ __forceinline__ double v(int k) const { return rr->v[k]; }
+};
+struct RowVal {
+  RowU ru;
+  RowFix fx;
+  __device__ __forceinline__ bool fix(int64_t (&f)[4]) const {
+    f[0] = fx.x0; f[1] = fx.y0; f[2] = fx.dx; f[3] = fx.dy;
+    return fx.x0 != kFixNone;
+  }
+  __device__ __forceinline__ int kind() const { return ru.kind; }
+  __device__ __forceinline__ int inside() const { return ru.inside; }
+  __device__ __forceinline__ int nleaf() const { return ru.nleaf; }
+  __device__ __forceinline__ int pool_off() const { return ru.pool_off; }
+  __device__ __forceinline__ double v(int k) const { return ru.v[k]; }
+};
+
+__device__ __forceinline__ EntryU entry_u(const EntryD &e) {
+  EntryU u;
+  u.band = uniform_ptr(e.band);
+  u.row_base = uni64(e.row_base);
+  u.bx = e.band_x; u.by = e.band_y; u.xoff = e.xoff; u.yoff = e.yoff; u.w = e.w; u.h = e.h;
+  u.ns = e.ns; u.fill_mode = e.fill_mode; u.mask_pair = e.mask_pair; u.nd = e.nd.u; u.fill = e.fill.u;
+  return u;
+}
+
+// One stack entry of the ordered fold of tile row r (MergeMaskedRaster,
+// tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
+// (tile column xl + 64 q).  fix: the row's 32.32 fixed-point form (RowFix,
+// x0 == kFixNone: none); mu: the mask pair's row when the entry is masked and
+// the mask row was prefetched (else mask_fast() reads it per pixel).
+template <typename T, bool MASK, int NPX, typename RS, bool SKIP = true>
+__device__ __forceinline__ void nn_entry_core(const RenderArgs &a, const EntryD *__restrict__ ents,
                                               const RowRec *__restrict__ rows, const Leaf *__restrict__ pool,
-                                              __amdgpu_buffer_rsrc_t rs, const RowRec *rr, int kind, int ic0, int lim,
-                                              int bx, int by, typename VOf<T>::type nd, bool fill_mode, int ir,
+                                              const EntryU &e, const RS &ru, const MaskU *mu,
+                                              int r, int xb, int xl, int W, int ncols,
                                               typename VOf<T>::type (&c)[NPX]) {
   using V = typename VOf<T>::type;
-  constexpr uint32_t kMaskOff = 0xFFFFFFFEu;   // mask row past the mask's height: not masked
-  const EntryD &m = ents[e.mask_pair];
-  const int ew = e.w, mw = m.w, mh = m.h, mbx = m.band_x, mby = m.band_y, mdt = m.out_dtype;
-  const int msz = type_size(mdt);
-  const int slot = mask_slot(mdt);
-  const int32_t mfill = m.fill.i;
-  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)uniform_ptr(m.band), (short)0, (int)((int64_t)mbx * mby * (int64_t)msz), 0x00020000);
-  uint32_t idx[NPX], midx[NPX];
-  if (kind == ROW_LINEAR) {
-    const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
-#pragma unroll
-    for (int q = 0; q < NPX; q++) {
-      const int ic = ic0 + 64 * q;
-      const double dist = (double)ic;
-      idx[q] = nn_index_sxy(xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, bx, by);
-    }
-  } else {   // POOL: the leaf of each pixel
-    const int nleaf = __builtin_amdgcn_readfirstlane(rr->nleaf);
-    const Leaf *lv = pool + __builtin_amdgcn_readfirstlane(rr->pool_off);
-#pragma unroll 1
-    for (int q = 0; q < NPX; q++) {
-      const int ic = ic0 + 64 * q;
-      const bool in = (unsigned)ic < (unsigned)lim;
-      const Leaf &L = lv[leaf_of(lv, nleaf, in ? ic : 0)];
-      const double dist = (double)(ic - L.start);
-      idx[q] = nn_index_sxy(L.xs0 + L.dX * dist, L.ys0 + L.dY * dist, in && L.kind != LEAF_FAILED, bx, by);
-    }
-  }
-  // mask_fast(): the mask window index of data pixel (ic, ir) -- the same
-  // index when the widths agree, else through the row-major data index
-  if (mw == ew) {
-    if (ir >= mh) {
-#pragma unroll
-      for (int q = 0; q < NPX; q++) midx[q] = kMaskOff;
-    } else {
-      const RowRec *mr = rows + m.row_base + ir;
-#pragma unroll
-      for (int q = 0; q < NPX; q++) {
-        const int ic = ic0 + 64 * q;
-        double sx, sy;
-        const bool ok = lin_coords(*mr, pool, (unsigned)ic < (unsigned)lim ? ic : 0, sx, sy);
-        midx[q] = ok ? nn_index_sxy(sx, sy, true, mbx, mby) : kNoPx;
-      }
-    }
-  } else {
-#pragma unroll 1
-    for (int q = 0; q < NPX; q++) {
-      const int ic = ic0 + 64 * q;
-      midx[q] = kMaskOff;
-      if ((unsigned)ic < (unsigned)lim) {
-        const long iSrc = (long)ir * ew + ic;
-        const int mx = (int)(iSrc % mw), my = (int)(iSrc / mw);
-        if (my < mh) {
-          double sx, sy;
-          midx[q] = lin_coords(rows[m.row_base + my], pool, mx, sx, sy) ? nn_index_sxy(sx, sy, true, mbx, mby) : kNoPx;
-        }
-      }
-    }
-  }
-  V vv[NPX];
-  uint32_t mraw[NPX];
-#pragma unroll
-  for (int q = 0; q < NPX; q++) vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
-  if (msz == 1) {
-#pragma unroll
-    for (int q = 0; q < NPX; q++) mraw[q] = __builtin_amdgcn_raw_buffer_load_b8(mrs, midx[q], 0, 0);
-  } else {
-#pragma unroll
-    for (int q = 0; q < NPX; q++) mraw[q] = __builtin_amdgcn_raw_buffer_load_b16(mrs, midx[q] * 2u, 0, 0);
-  }
-  const V fillv = as_v<T>(e.fill);
-#pragma unroll
-  for (int q = 0; q < NPX; q++) {
-    const int ic = ic0 + 64 * q;
-    const V v = idx[q] != kNoPx ? vv[q] : fillv;
-    int32_t mv;
-    switch (mdt) {   // nn_fetch<mask type>'s value
-      case GSKYHIP_SIGNEDBYTE: mv = (int32_t)(int8_t)(uint8_t)mraw[q]; break;
-      case GSKYHIP_INT16: mv = (int32_t)(int16_t)(uint16_t)mraw[q]; break;
-      case GSKYHIP_BYTE: mv = (int32_t)(uint8_t)mraw[q]; break;
-      default: mv = (int32_t)(uint16_t)mraw[q]; break;
-    }
-    if (midx[q] == kNoPx) mv = mfill;
-    const bool mk = midx[q] != kMaskOff && slot >= 0 && mask_bit(a.mask[slot], mdt, mv);
-    const bool take = (unsigned)ic < (unsigned)lim && (v != nd) && !mk;
-    const bool t2 = take && (!fill_mode || c[q] == nd);
-    c[q] = t2 ? v : c[q];
-  }
-}
-
-// One stack entry e of the ordered fold of tile row r (MergeMaskedRaster,
-// tile_merger.go:38-225): c[q] is the canvas value of the lane's pixel q
-// (tile column xl + 64 q).
-// PARTIAL: with the window-edge body for `inside` rows (the single-entry path
-// of render_nn_kernel has its own and passes false).
-template <typename T, bool MASK, int NPX = kNnPx, bool PARTIAL = true, bool FIX = true>
-__device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
-                                             const RowRec *__restrict__ rows, const RowFix *__restrict__ rowfix,
-                                             const Leaf *__restrict__ pool,
-                                             int ns_out, int r, int xb, int xl, int W, int ncols,
-                                             typename VOf<T>::type (&c)[NPX]) {
-  using V = typename VOf<T>::type;
-  const int eyoff = e.yoff, eh = e.h, exoff = e.xoff, ew = e.w;
-  if (e.ns != ns_out || ew <= 0) return;
-  const int ir = r - eyoff;
-  if (ir < 0 || ir >= eh) return;
-  const int lim = max(0, min(ew, W - exoff));   // window pixel in the tile: (unsigned)ic < lim
-  const int c0 = exoff - xb, c1 = exoff + lim - xb;   // the entry's columns of the block: [c0, c1)
-  if (c1 <= 0 || c0 >= ncols) return;
-  const int bx = e.band_x, by = e.band_y;
-  const V nd = as_v<T>(e.nd);
+  const int ir = r - e.yoff, ew = e.w;
+  const int lim = max(0, min(ew, W - e.xoff));   // window pixel in the tile: (unsigned)ic < lim
+  const int c0 = e.xoff - xb, c1 = e.xoff + lim - xb;   // the entry's columns of the block: [c0, c1)
+  const int bx = e.bx, by = e.by;
+  Val ndv;
+  ndv.u = e.nd;
+  const V nd = as_v<T>(ndv);
   const bool fill_mode = e.fill_mode != 0;
-  const int ic0 = xl - exoff;   // window column of the lane's pixel 0
+  const int ic0 = xl - e.xoff;   // window column of the lane's pixel 0
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
+      (void *)e.band, (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
   const bool masked = MASK && e.mask_pair >= 0;
-  if (FIX && !masked) {   // fixed-point form of an `inside` LINEAR row
-    const RowFix *fp = rowfix + e.row_base + ir;
-    const int64_t fx0 = uni64(fp->x0);
-    if (fx0 != kFixNone) {
-      const int64_t fy0 = uni64(fp->y0), fdx = uni64(fp->dx), fdy = uni64(fp->dy);
-      const bool done = (c0 <= 0 && c1 >= ncols)
-                            ? nn_fix_row<T, NPX, false>(rs, fx0, fy0, fdx, fdy, ic0, lim, bx, nd, fill_mode, c)
-                            : nn_fix_row<T, NPX, true>(rs, fx0, fy0, fdx, fdy, ic0, lim, bx, nd, fill_mode, c);
-      if (done) return;
-    }
+  // fill mode: only pixels whose canvas still holds this raster's nodata can
+  // change (tile_merger.go:47-58); a row of the block with none skips the
+  // entry's gathers (a NaN nodata never compares equal: such an entry never
+  // fills, as in the reference)
+  if (SKIP && fill_mode) {
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < NPX; q++) any |= c[q] == nd;
+    if (__builtin_amdgcn_ballot_w64(any) == 0) return;
   }
-  const RowRec *rr = rows + e.row_base + ir;
-  const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
-  const int inside = __builtin_amdgcn_readfirstlane(rr->inside);
-  if (kind == ROW_LINEAR && inside && c0 <= 0 && c1 >= ncols && !masked) {
+  const bool cover = c0 <= 0 && c1 >= ncols;
+  int64_t f[4];
+  if (!masked && ru.fix(f)) {   // fixed-point form of an `inside` LINEAR row
+    const bool done = cover ? nn_fix_row<T, NPX, false>(rs, f[0], f[1], f[2], f[3], ic0, lim, bx, nd, fill_mode, c)
+                            : nn_fix_row<T, NPX, true>(rs, f[0], f[1], f[2], f[3], ic0, lim, bx, nd, fill_mode, c);
+    if (done) return;
+  }
+  const int kind = ru.kind();
+  const int inside = ru.inside();
+  if (kind == ROW_LINEAR && inside && cover && !masked) {
     // fast body: every pixel of the block is in the window and its source
     // pixel in the band -- lin_coords() + nn_px() reduce to the truncations
-    const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
+    const double xs0 = ru.v(0), ys0 = ru.v(1), dX = ru.v(2), dY = ru.v(3);
     uint32_t off[NPX];
 #pragma unroll
     for (int q = 0; q < NPX; q++) {
@@ -481,31 +377,59 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
     }
     return;
   }
-  if (PARTIAL && kind == ROW_LINEAR && inside && !masked) {
+  if (kind == ROW_LINEAR && inside && !masked) {
     // window edge inside the block on an `inside` row: the fast body plus the
     // window test (pixels outside the window read nothing and fold nothing;
     // fill mode takes v where c is nodata, which equals the general rule's
     // "v != nd && c == nd" because v == nd == c leaves c unchanged)
-    nn_partial_row<T, NPX>(rs, rr->v[0], rr->v[1], rr->v[2], rr->v[3], ic0, lim, bx, nd, fill_mode, c0, c1, c);
+    nn_partial_row<T, NPX>(rs, ru.v(0), ru.v(1), ru.v(2), ru.v(3), ic0, lim, bx, nd, fill_mode, c0, c1, c);
     return;
   }
-#ifdef GSKYHIP_AB
+  Val fv;
+  fv.u = e.fill;
+  const V fillv = as_v<T>(fv);
   if constexpr (MASK) {
-    if (masked && a.nn_maskb) {   // A/B (GSKYHIP_NN_MASKB=1): measured slower on C5, 0.526 vs 0.494 ms
-      nn_masked_row<T, NPX>(a, ents, e, rows, pool, rs, rr, kind, ic0, lim, bx, by, nd, fill_mode, ir, c);
-      return;
+    if (masked && kind == ROW_LINEAR) {
+      // the mask pair's row: the same element index when it has the data
+      // row's width, level size and row record (bit for bit)
+      MaskU m;
+      if (mu) {
+        m = *mu;
+      } else {
+        const EntryD &me = ents[e.mask_pair];
+        m.w = me.w; m.h = me.h; m.bx = me.band_x; m.by = me.band_y; m.dt = me.out_dtype; m.fill = me.fill.i;
+        m.band = uniform_ptr(me.band);
+        m.kind = -1;
+        if (ir < m.h) {
+          const RowRec &mr = rows[uni64(me.row_base) + ir];
+          m.kind = __builtin_amdgcn_readfirstlane(mr.kind);
+#pragma unroll
+          for (int k = 0; k < 4; k++) m.v[k] = uni64d(mr.v[k]);
+        }
+      }
+      const int slot = mask_slot(m.dt);
+      const bool same = m.w == ew && ir < m.h && m.bx == bx && m.by == by && m.kind == ROW_LINEAR &&
+                        __double_as_longlong(m.v[0]) == __double_as_longlong(ru.v(0)) &&
+                        __double_as_longlong(m.v[1]) == __double_as_longlong(ru.v(1)) &&
+                        __double_as_longlong(m.v[2]) == __double_as_longlong(ru.v(2)) &&
+                        __double_as_longlong(m.v[3]) == __double_as_longlong(ru.v(3));
+      if (same && slot >= 0) {
+        const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)m.band, (short)0, (int)((int64_t)m.bx * m.by * (int64_t)type_size(m.dt)), 0x00020000);
+        nn_masked_same_row<T, NPX>(a.mask[slot], m.dt, m.fill, rs, mrs, ru.v(0), ru.v(1), ru.v(2), ru.v(3), ic0, lim,
+                                   bx, by, nd, fillv, fill_mode, c);
+        return;
+      }
     }
   }
-#endif
   // general body: POOL rows, rows not inside the band, mask layer;
   // two halves of 4 pixels (4 gathers in flight) keep the register peak
   // of the fast body
-  const V fillv = as_v<T>(e.fill);
 #pragma unroll
   for (int h = 0; h < NPX; h += 4) {
     uint32_t idx[4];
     if (kind == ROW_LINEAR) {
-      const double xs0 = rr->v[0], ys0 = rr->v[1], dX = rr->v[2], dY = rr->v[3];
+      const double xs0 = ru.v(0), ys0 = ru.v(1), dX = ru.v(2), dY = ru.v(3);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int ic = ic0 + 64 * (h + q);
@@ -513,8 +437,8 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
         idx[q] = nn_index_sxy(xs0 + dX * dist, ys0 + dY * dist, (unsigned)ic < (unsigned)lim, bx, by);
       }
     } else {   // POOL (the only other kind of a simple tile): the leaf of each pixel
-      const int nleaf = __builtin_amdgcn_readfirstlane(rr->nleaf);
-      const Leaf *lv = pool + __builtin_amdgcn_readfirstlane(rr->pool_off);
+      const int nleaf = ru.nleaf();
+      const Leaf *lv = pool + ru.pool_off();
 #pragma unroll 1
       for (int q = 0; q < 4; q++) {
         const int ic = ic0 + 64 * (h + q);
@@ -533,7 +457,7 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
       const V v = idx[q] != kNoPx ? vv[q] : fillv;
       bool take = (unsigned)ic < (unsigned)lim && (v != nd);
       if (masked) {
-        if (take) take = !mask_fast<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, e, ic, ir);
+        if (take) take = !mask_fast_pair<GSKYHIP_RESAMPLE_NEAREST>(ents, rows, pool, a.mask, e.mask_pair, ew, ic, ir);
       }
       const bool t2 = take && (!fill_mode || c[h + q] == nd);
       c[h + q] = t2 ? v : c[h + q];
@@ -541,22 +465,113 @@ __device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *
   }
 }
 
-// The ordered fold of tile row r over the tile's entries in ProcessRasterStack
-// order; c[] arrives holding the canvas nodata.
+// nn_entry_core() of entry e on tile row r, its descriptor and row records
+// read from memory (the single-entry path's fp64 redo rows).
+template <typename T, bool MASK, int NPX = kNnPx, bool SKIP = true>
+__device__ __forceinline__ void nn_entry_row(const RenderArgs &a, const EntryD *__restrict__ ents, const EntryD &e,
+                                             const RowRec *__restrict__ rows, const RowFix *__restrict__ rowfix,
+                                             const Leaf *__restrict__ pool, bool use_fix,
+                                             int ns_out, int r, int xb, int xl, int W, int ncols,
+                                             typename VOf<T>::type (&c)[NPX]) {
+  const EntryU u = entry_u(e);
+  if (u.ns != ns_out || u.w <= 0) return;
+  const int ir = r - u.yoff;
+  if (ir < 0 || ir >= u.h) return;
+  const int lim = max(0, min(u.w, W - u.xoff));
+  const int c0 = u.xoff - xb, c1 = u.xoff + lim - xb;
+  if (c1 <= 0 || c0 >= ncols) return;
+  RowMem rm;
+  rm.rr = rows + u.row_base + ir;
+  rm.fp = use_fix ? rowfix + u.row_base + ir : nullptr;
+  nn_entry_core<T, MASK, NPX, RowMem, SKIP>(a, ents, rows, pool, u, rm, nullptr, r, xb, xl, W, ncols, c);
+}
+
+// The ordered fold of tile row r over the tile's entries in
+// ProcessRasterStack order (tile_merger.go:281-312); c[] arrives holding the
+// canvas nodata.  Entries are taken 64 at a time, lane j holding entry
+// k0 + j: one round of vector loads reads every entry's window and, for the
+// entries that touch this row of the block, the row record, the fixed-point
+// form and (masked stacks) the mask pair's descriptor and row -- the
+// dependent scalar chain order -> descriptor -> row -> mask -> mask row of
+// the serial walk costs four memory latencies per entry; here about four per
+// 64 entries.  The fold then walks the active entries in order, each one's
+// values read out of its lane.
 template <typename T, bool MASK>
-__device__ __forceinline__ void nn_fold_row(const RenderArgs &a, const EntryD *__restrict__ ents,
-                                            const int32_t *__restrict__ ord, int n_entries,
-                                            const RowRec *__restrict__ rows, const RowFix *__restrict__ rowfix,
-                                            const Leaf *__restrict__ pool,
-                                            int ns_out, int r, int xb, int xl, int W, int ncols,
-                                            typename VOf<T>::type (&c)[kNnPx]) {
-  // FIX off: in a stack the RowFix load is one more dependent latency per
-  // entry row before the row record's (C5 0.47 vs 0.435 ms with it,
-  // profiles/r04i_ab.jsonl); the fixed-point rows serve the single-entry path
+__device__ __forceinline__ void nn_fold_row_stack(const RenderArgs &a, const EntryD *__restrict__ ents,
+                                                  const int32_t *__restrict__ ord, int n_entries,
+                                                  const RowRec *__restrict__ rows, const RowFix *__restrict__ rowfix,
+                                                  const Leaf *__restrict__ pool, int ns_out, int r, int xb, int xl,
+                                                  int W, int ncols, int lane, typename VOf<T>::type (&c)[kNnPx]) {
 #pragma unroll 1
-  for (int k = 0; k < n_entries; k++)
-    nn_entry_row<T, MASK, kNnPx, true, false>(a, ents, ents[ord[k]], rows, rowfix, pool, ns_out, r, xb, xl, W, ncols,
-                                              c);
+  for (int k0 = 0; k0 < n_entries; k0 += 64) {
+    const bool has = k0 + lane < n_entries;
+    const int p = has ? ord[k0 + lane] : 0;
+    const EntryD &E = ents[p];
+    const int yoff = E.yoff, eh = E.h, xoff = E.xoff, ew = E.w, ens = E.ns;
+    const int ir = r - yoff;
+    const int lim = max(0, min(ew, W - xoff));
+    const int c0 = xoff - xb, c1 = xoff + lim - xb;
+    const bool act = has & (ens == ns_out) & (ew > 0) & (ir >= 0) & (ir < eh) & (c1 > 0) & (c0 < ncols);
+    uint64_t am = __builtin_amdgcn_ballot_w64(act);
+    if (am == 0) continue;
+    // the active lanes' descriptors, row records (and mask rows), in flight together
+    const int64_t rb = act ? E.row_base + ir : 0;
+    const RowRec &R = rows[rb];
+    const double v0 = R.v[0], v1 = R.v[1], v2 = R.v[2], v3 = R.v[3];
+    const int kind = R.kind, inside = R.inside, nleaf = R.nleaf, pool_off = R.pool_off;
+    const void *band = E.band;
+    const int bx = E.band_x, by = E.band_y, fill_mode = E.fill_mode, mask_pair = E.mask_pair;
+    const uint32_t nd = E.nd.u, fill = E.fill.u;
+    int64_t fx0 = kFixNone, fy0 = 0, fdx = 0, fdy = 0;
+    int mw = 0, mh = 0, mbx = 0, mby = 0, mdt = 0, mkind = -1;
+    int32_t mfill = 0;
+    const void *mband = nullptr;
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
+    if constexpr (!MASK) {
+      const RowFix &F = rowfix[rb];
+      fx0 = act ? F.x0 : kFixNone; fy0 = F.y0; fdx = F.dx; fdy = F.dy;
+    } else {
+      const bool mk = act & (mask_pair >= 0);
+      const EntryD &M = ents[mk ? mask_pair : p];
+      mw = M.w; mh = M.h; mbx = M.band_x; mby = M.band_y; mdt = M.out_dtype; mfill = M.fill.i; mband = M.band;
+      const bool mrow = mk & (ir < mh);
+      const RowRec &MR = rows[mrow ? M.row_base + ir : 0];
+      mkind = mrow ? MR.kind : -1;
+      m0 = MR.v[0]; m1 = MR.v[1]; m2 = MR.v[2]; m3 = MR.v[3];
+    }
+    auto rl = [](int v, int j) { return __builtin_amdgcn_readlane(v, j); };
+    auto rl64 = [](int64_t v, int j) {
+      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, j);
+      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), j);
+      return (int64_t)(((uint64_t)hi << 32) | lo);
+    };
+    auto rld = [&](double v, int j) { return __longlong_as_double(rl64(__double_as_longlong(v), j)); };
+    auto rlp = [&](const void *v, int j) { return (const void *)rl64((int64_t)(uintptr_t)v, j); };
+#pragma unroll 1
+    while (am) {
+      const int j = __builtin_ctzll(am);
+      am &= am - 1;
+      EntryU u;
+      u.band = rlp(band, j); u.row_base = 0;
+      u.bx = rl(bx, j); u.by = rl(by, j); u.xoff = rl(xoff, j); u.yoff = rl(yoff, j); u.w = rl(ew, j);
+      u.h = rl(eh, j); u.ns = ns_out; u.fill_mode = rl(fill_mode, j); u.mask_pair = rl(mask_pair, j);
+      u.nd = (uint32_t)rl((int)nd, j); u.fill = (uint32_t)rl((int)fill, j);
+      RowVal rv;
+      rv.ru.v[0] = rld(v0, j); rv.ru.v[1] = rld(v1, j); rv.ru.v[2] = rld(v2, j); rv.ru.v[3] = rld(v3, j);
+      rv.ru.kind = rl(kind, j); rv.ru.inside = rl(inside, j); rv.ru.nleaf = rl(nleaf, j);
+      rv.ru.pool_off = rl(pool_off, j);
+      rv.fx.x0 = rl64(fx0, j); rv.fx.y0 = rl64(fy0, j); rv.fx.dx = rl64(fdx, j); rv.fx.dy = rl64(fdy, j);
+      if constexpr (MASK) {
+        MaskU m;
+        m.band = rlp(mband, j); m.w = rl(mw, j); m.h = rl(mh, j); m.bx = rl(mbx, j); m.by = rl(mby, j);
+        m.dt = rl(mdt, j); m.kind = rl(mkind, j); m.fill = rl(mfill, j);
+        m.v[0] = rld(m0, j); m.v[1] = rld(m1, j); m.v[2] = rld(m2, j); m.v[3] = rld(m3, j);
+        nn_entry_core<T, MASK, kNnPx>(a, ents, rows, pool, u, rv, &m, r, xb, xl, W, ncols, c);
+      } else {
+        nn_entry_core<T, MASK, kNnPx>(a, ents, rows, pool, u, rv, nullptr, r, xb, xl, W, ncols, c);
+      }
+    }
+  }
 }
 
 // utils.Scale + palette / grey of the lane's 8 canvas values (EncodePNG's
@@ -584,10 +599,10 @@ __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint3
 // measured 0.6 % slower on C2 and C5, profiles/r03b_ab_nn.jsonl).
 // ONE (RGBA, no mask layer): tiles with a single stack entry -- most GetMap
 // tiles -- keep the entry's descriptor in scalar registers for all the
-// wave's rows and fetch the next row's record while the current row is
-// gathered, so no row waits for its record.
-template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, bool STAGE = false, bool COOP = false,
-          bool WIDE = false>
+// wave's rows and take all RPW rows' fixed-point forms in one vector load,
+// so no row waits for its record.  Tiles with more entries (or a mask layer)
+// fold through nn_fold_row_stack().
+template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false>
 __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
@@ -599,24 +614,10 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   using V = typename VOf<T>::type;
   constexpr int kRowsBlk = 4 * RPW;
   __shared__ uint32_t s_tab[256];
-  // STAGE (A/B): a row's 512 RGBA words go through the wave's LDS row so
-  // they leave as two 16-B-per-lane stores (1 KB contiguous each) instead of
-  // eight 4-B ones
-  __shared__ __attribute__((aligned(16))) uint32_t s_stage[STAGE ? 4 : 1][STAGE ? kBandCols : 4];
 
   const int bands_per_tile = (a.max_h + kRowsBlk - 1) / kRowsBlk;
   const int col_blocks = (a.max_w + kBandCols - 1) / kBandCols;
-  int item = blockIdx.x;
-#ifdef GSKYHIP_AB
-  if (a.ab_xcd == 1) {   // A/B: every block of a tile on one XCD (blockIdx % 8), tiles dealt round-robin over the XCDs
-    const int per = bands_per_tile * col_blocks;
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    item = ((slot / per) * 8 + xcd) * per + slot % per;
-  } else if (a.ab_xcd == 2) {   // A/B: XCD x takes the x-th contiguous eighth of the items (a strip of tiles)
-    const int per = (n_items + 7) >> 3;
-    item = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  }
-#endif
+  const int item = blockIdx.x;
   if (item >= n_items) return;
   const int t = item / (bands_per_tile * col_blocks);
   const int in_tile = item - t * bands_per_tile * col_blocks;
@@ -672,68 +673,16 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
   const int xl = xb + lane;                     // tile column of the lane's pixel 0
   uint32_t *rgba_lane = (uint32_t *)(a.rgba + (((int64_t)t * a.max_h) * a.max_w + xl) * 4);
 
-  auto rgba = [&](const V (&c)[kNnPx], uint32_t (&px)[kNnPx]) {
-#ifdef GSKYHIP_AB
-    if (a.ab_mode == 3) {   // A/B: Scale without the palette's LDS lookup
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) px[q] = 0xFF000000u | scale_int<T, false>(sk, c[q]) * 0x10101u;
-      return;
-    }
-    if (a.ab_mode == 4) {   // A/B: neither Scale nor palette
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++) px[q] = (uint32_t)c[q];
-      return;
-    }
-#endif
-    nn_rgba<T>(sk, safe, s_tab, c, px);
-  };
-
   // RGBA stores of row r
   auto store_row = [&](int r, const uint32_t *px, bool full_known = false) {
     uint32_t *dst = rgba_lane + (int64_t)r * a.max_w;
-    if constexpr (STAGE && !CANVAS) {
-      if (full && (a.max_w & 3) == 0) {
-        uint32_t *row = s_stage[wave];
-#pragma unroll
-        for (int q = 0; q < kNnPx; q++) row[lane + 64 * q] = px[q];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const u32x4 v0 = *(const u32x4 *)&row[4 * lane], v1 = *(const u32x4 *)&row[256 + 4 * lane];
-        uint32_t *d0 = dst - lane;   // the block's first column of row r
-        __builtin_nontemporal_store(v0, (GPTR(u32x4))(d0 + 4 * lane));
-        __builtin_nontemporal_store(v1, (GPTR(u32x4))(d0 + 256 + 4 * lane));
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        return;
-      }
-    }
-    auto st = [&](uint32_t *p, uint32_t v) {
-#ifdef GSKYHIP_AB
-      // A/B: the store's L2 policy (nt / plain keep the line in the XCD's
-      // L2; sc1 / sc0 sc1 drop it, MI355X_MICROARCH.md)
-      if (a.st_pol == 1) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); return; }
-      if (a.st_pol == 2) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); return; }
-      if (a.st_pol == 3) { *p = v; return; }
-#endif
-      __builtin_nontemporal_store(v, (GPTR(uint32_t))p);
-    };
-#ifdef GSKYHIP_AB
-    if (a.ab_mode == 2) {   // A/B: no stores (the values stay live)
-#pragma unroll
-      for (int q = 0; q < kNnPx; q++)
-        if (px[q] == 0x9E3779B9u) st(dst + 64 * q, px[q]);
-      return;
-    }
-#endif
     if (full_known || full) {
 #pragma unroll
-      for (int q = 0; q < kNnPx; q++) st(dst + 64 * q, px[q]);
+      for (int q = 0; q < kNnPx; q++) __builtin_nontemporal_store(px[q], (GPTR(uint32_t))(dst + 64 * q));
     } else {
 #pragma unroll
       for (int q = 0; q < kNnPx; q++)
-        if (64 * q + lane < ncols) st(dst + 64 * q, px[q]);
+        if (64 * q + lane < ncols) __builtin_nontemporal_store(px[q], (GPTR(uint32_t))(dst + 64 * q));
     }
   };
 
@@ -751,47 +700,23 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
       const V nd = as_v<T>(ndv);
       const bool fill_mode = e1_fill != 0;
       const int ic0 = xl - exoff;
-      bool pair_on = false;   // A/B: nn_fix_row_pair (column pairs, 8-byte stores)
-#ifdef GSKYHIP_AB
-      pair_on = a.nn_pair != 0 && (a.max_w & 1) == 0;
-#endif
-      // WIDE / pairs: the band's last dword whole (buf_load_w; a dword never
-      // straddles a page)
-      const int64_t band_bytes = (int64_t)bx * by * (int64_t)sizeof(T);
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)uniform_ptr(e1_band), (short)0,
-          (int)((WIDE || pair_on) ? (band_bytes + 3) & ~(int64_t)3 : band_bytes), 0x00020000);
+          (void *)uniform_ptr(e1_band), (short)0, (int)((int64_t)bx * by * (int64_t)sizeof(T)), 0x00020000);
       const RowFix *fbase = rowfix + e1_row_base;
-      // the row's fixed-point form, or fk = -1 outside the window / 0 none
-      auto fetch = [&](int ir, int64_t (&f)[4], int &fk) {
-        if (ir < 0 || ir >= eh) { fk = -1; return; }
-        const RowFix *p = fbase + ir;
-        f[0] = uni64(p->x0); f[1] = uni64(p->y0); f[2] = uni64(p->dx); f[3] = uni64(p->dy);
-        fk = f[0] != kFixNone ? 1 : 0;
-      };
-      int64_t cf[4] = {0, 0, 0, 0}, nf[4] = {0, 0, 0, 0};
-      int cfk = -1, nfk = -1;
+      // the RowFix records of all RPW rows in one coalesced vector load
+      // (lane 4j + k: field k of row j), read out per row with v_readlane --
+      // one memory latency per wave instead of one per row
+      static_assert(RPW <= 16, "4 RowFix fields of each row in one lane group");
+      int64_t fv = kFixNone;
+      {
+        const int jj = lane >> 2, kk = lane & 3, ir = r0 - eyoff + jj;
+        if (cols_ok && lane < 4 * RPW && ir >= 0 && ir < eh)
+          fv = __builtin_nontemporal_load((const int64_t *)(fbase + ir) + kk);
+      }
       // rows left to the fp64 bodies (no fixed form, or a pixel near a
       // truncation boundary): done in a second loop, so that loop's loads do
       // not reach the register and wait-count state of this one
       uint32_t redo = 0;
-      // VFETCH: the RowFix records of all RPW rows in one coalesced vector
-      // load (lane 4j + k: field k of row j), read out per row with
-      // v_readlane -- one memory latency per wave instead of one per row
-      // (the scalar fetch of the next row is still in flight when a row's
-      // stores are issued)
-      bool vfetch = RPW <= 16;
-#ifdef GSKYHIP_AB
-      vfetch = vfetch && a.ab_vfetch;
-#endif
-      int64_t fv = kFixNone;
-      if (vfetch) {
-        const int jj = lane >> 2, kk = lane & 3, ir = r0 - eyoff + jj;
-        if (cols_ok && lane < 4 * RPW && ir >= 0 && ir < eh)
-          fv = __builtin_nontemporal_load((const int64_t *)(fbase + ir) + kk);
-      } else if (cols_ok) {
-        fetch(r0 - eyoff, cf, cfk);
-      }
       // the row loop, once for blocks whose every row the entry's window
       // covers in a full-width block (CF: the fast fold and unconditional
       // stores as straight-line code -- merged with the window-edge and
@@ -803,157 +728,40 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         for (int j = 0; j < RPW; j++) {
           const int r = r0 + j;
           if (r >= H) break;
-          if (vfetch) {
-            const int ir = r - eyoff;
-            if (!cols_ok || ir < 0 || ir >= eh) {
-              cfk = -1;
-            } else {
+          const int ir = r - eyoff;
+          int64_t cf[4] = {0, 0, 0, 0};
+          int cfk = -1;   // -1: outside the window, 0: no fixed form, 1: fixed form
+          if (cols_ok && ir >= 0 && ir < eh) {
 #pragma unroll
-              for (int k = 0; k < 4; k++) {
-                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)fv, 4 * j + k);
-                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)fv >> 32), 4 * j + k);
-                cf[k] = (int64_t)(((uint64_t)hi << 32) | lo);
-              }
-              cfk = cf[0] != kFixNone ? 1 : 0;
+            for (int k = 0; k < 4; k++) {
+              const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)fv, 4 * j + k);
+              const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)fv >> 32), 4 * j + k);
+              cf[k] = (int64_t)(((uint64_t)hi << 32) | lo);
             }
-          } else if (cols_ok && j + 1 < RPW) {
-            fetch(r + 1 - eyoff, nf, nfk);   // next row's record, in flight now
+            cfk = cf[0] != kFixNone ? 1 : 0;
           }
           V c[kNnPx];
 #pragma unroll
           for (int q = 0; q < kNnPx; q++) c[q] = cnod;
           bool done = cfk < 0;
-          bool paired = false;
-#ifdef GSKYHIP_AB
-          if (a.ab_mode == 1) done = true;   // A/B: no gathers
-          else if (a.ab_mode == 8 && cfk == 1) {
-            // A/B lower bound: the same number of gathers, fold, Scale,
-            // palette and stores, with near-free index math -- an unrotated
-            // 0.47 source px per output px pattern from the row's first pixel
-            const uint32_t ix0 = (uint32_t)(cf[0] >> 32), iy0 = (uint32_t)(cf[1] >> 32);
-            const uint32_t rb = (__umul24(iy0, (uint32_t)bx) + ix0) * (uint32_t)sizeof(T);
-            V vv[kNnPx];
-#pragma unroll
-            for (int q = 0; q < kNnPx; q++)
-              vv[q] = buf_load<T>(rs, rb + (((uint32_t)(lane + 64 * q) * 15u) >> 5) * (uint32_t)sizeof(T));
-#pragma unroll
-            for (int q = 0; q < kNnPx; q++) c[q] = vv[q] != nd ? vv[q] : c[q];
-            done = true;
-          } else
-#endif
           if (cfk == 1) {
-            if constexpr (CF && sizeof(T) == 2 && !WIDE) {
-              if (pair_on) {
-                done = nn_fix_row_pair<T, kNnPx>(rs, cf[0], cf[1], cf[2], cf[3], ic0 + lane, bx, nd, fill_mode, c);
-                paired = true;
-              } else {
-                done = nn_fix_row<T, kNnPx, false, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode,
-                                                         c);
-              }
-            } else if constexpr (CF)
-              done = nn_fix_row<T, kNnPx, false, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c);
+            if constexpr (CF)
+              done = nn_fix_row<T, kNnPx, false>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c);
             else
-              done = cover ? (COOP ? nn_fix_row_coop<T, kNnPx>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
-                                                               fill_mode, c, lane)
-                                   : nn_fix_row<T, kNnPx, false, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
-                                                                       fill_mode, c))
-                           : nn_fix_row<T, kNnPx, true, WIDE>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd,
-                                                              fill_mode, c);
+              done = cover ? nn_fix_row<T, kNnPx, false>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c)
+                           : nn_fix_row<T, kNnPx, true>(rs, cf[0], cf[1], cf[2], cf[3], ic0, lim, bx, nd, fill_mode, c);
           }
           if (done) {
             uint32_t px[kNnPx];
-            rgba(c, px);
-            if (paired) {   // columns 2 lane + 128 q + {0, 1}: 8-byte stores
-              uint32_t *d = rgba_lane - lane + (int64_t)r * a.max_w + 2 * lane;
-#pragma unroll
-              for (int q = 0; q < kNnPx / 2; q++)
-                __builtin_nontemporal_store(u32x2{px[2 * q], px[2 * q + 1]}, (GPTR(u32x2))(d + 128 * q));
-            } else {
-              store_row(r, px, CF);
-            }
+            nn_rgba<T>(sk, safe, s_tab, c, px);
+            store_row(r, px, CF);
           } else {
             redo |= 1u << j;
           }
-          if (!vfetch) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) cf[k] = nf[k];
-            cfk = nfk;
-          }
         }
       };
-      bool cf_on = cover && full && !COOP;
-#ifdef GSKYHIP_AB
-      if (a.ab_mode == 7) cf_on = false;   // A/B: one merged row loop (round 4)
-#endif
-      // COLG (A/B build, GSKYHIP_NN_COLG=1; measured slower): the block's 8
-      // rows x 512 columns in column-group-major order -- for each 64-column
-      // group the wave's RPW rows back to back, so the RPW gathers in flight
-      // read the few source lines under that group.  Row-major, L1 -> L2
-      // reads are 7x the unique source bytes (32 waves per CU evict a wave's
-      // lines before its next row); this order halves them (57.4 M -> 31.5 M
-      // requests) and still runs 1.64 vs 1.57 ms: the texture data unit stays
-      // busy ~97 % of the kernel at ~21 L1 accesses per 64-lane gather
-      // (profiles/r05j_pmc_c2_l1.json, r05k_*).  The same fixed-point values
-      // and margin test as nn_fix_row, the same fp64 redo of a row with an
-      // ambiguous pixel: the same result bit for bit (0 px differ on C2, C5).
-      bool colg_done = false;
-#ifdef GSKYHIP_AB
-      if constexpr (RPW == kNnPx && !COOP && !WIDE) {
-        bool colg = a.nn_colg && cf_on && vfetch && r0 + RPW <= H && r0 - eyoff >= 0 && r0 + RPW - eyoff <= eh;
-        if (colg) {
-          const bool missing = lane < 4 * RPW && (lane & 3) == 0 && fv == kFixNone;
-          colg = __builtin_amdgcn_ballot_w64(missing) == 0;
-        }
-        if (colg) {
-          colg_done = true;
-          uint32_t amb = 0;   // per lane: bit j = row j has an ambiguous pixel
-          uint32_t *const dst0 = rgba_lane + (int64_t)r0 * a.max_w;
-#pragma unroll 1
-          for (int g = 0; g < kNnPx; g++) {
-            // the row records come by scalar loads each group (held across the
-            // loop they would be 64 SGPRs)
-            int jb = r0 - eyoff;
-            asm volatile("" : "+s"(jb));   // (the index, not the pointer: that keeps its address space)
-            const RowFix *rb = fbase + jb;
-            const uint32_t ic = (uint32_t)(ic0 + 64 * g);
-            uint32_t off[RPW];
-#pragma unroll
-            for (int j = 0; j < RPW; j++) {
-              const uint64_t x0 = (uint64_t)uni64(rb[j].x0), y0 = (uint64_t)uni64(rb[j].y0);
-              const uint64_t dx = (uint64_t)uni64(rb[j].dx), dy = (uint64_t)uni64(rb[j].dy);
-              const uint64_t X = x0 + (uint64_t)ic * dx, Y = y0 + (uint64_t)ic * dy;
-              const uint32_t m = min((uint32_t)X + kFixMargin, (uint32_t)Y + kFixMargin);
-              amb |= (m < 2u * kFixMargin ? 1u : 0u) << j;
-              off[j] = (__umul24((uint32_t)(Y >> 32), (uint32_t)bx) + (uint32_t)(X >> 32)) * (uint32_t)sizeof(T);
-            }
-            V vv[RPW];
-#pragma unroll
-            for (int j = 0; j < RPW; j++) vv[j] = buf_load<T>(rs, off[j]);
-            V c[RPW];
-            if (!fill_mode) {
-#pragma unroll
-              for (int j = 0; j < RPW; j++) c[j] = vv[j] != nd ? vv[j] : cnod;
-            } else {
-              const bool take = cnod == nd;
-#pragma unroll
-              for (int j = 0; j < RPW; j++) c[j] = take ? vv[j] : cnod;
-            }
-            uint32_t px[RPW];
-            rgba(c, px);
-#pragma unroll
-            for (int j = 0; j < RPW; j++)
-              __builtin_nontemporal_store(px[j], (GPTR(uint32_t))(dst0 + (int64_t)j * a.max_w + 64 * g));
-          }
-#pragma unroll
-          for (int j = 0; j < RPW; j++)
-            if (__builtin_amdgcn_ballot_w64((amb >> j) & 1u) != 0) redo |= 1u << j;
-        }
-      }
-#endif
-      if (!colg_done) {
-        if (cf_on) row_loop(std::true_type{});
-        else row_loop(std::false_type{});
-      }
+      if (cover && full) row_loop(std::true_type{});
+      else row_loop(std::false_type{});
 #pragma unroll 1
       while (redo) {
         const int j = __builtin_ctz(redo);
@@ -962,9 +770,9 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         V c[kNnPx];
 #pragma unroll
         for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-        nn_entry_row<T, false, kNnPx, true, false>(a, ents, e, rows, rowfix, pool, ns_out, r, xb, xl, W, ncols, c);
+        nn_entry_row<T, false, kNnPx, false>(a, ents, e, rows, rowfix, pool, false, ns_out, r, xb, xl, W, ncols, c);
         uint32_t px[kNnPx];
-        rgba(c, px);
+        nn_rgba<T>(sk, safe, s_tab, c, px);
         store_row(r, px);
       }
       return;
@@ -977,7 +785,19 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
     V c[kNnPx];
 #pragma unroll
     for (int q = 0; q < kNnPx; q++) c[q] = cnod;
-    nn_fold_row<T, MASK>(a, ents, ord, n_entries, rows, rowfix, pool, ns_out, r, xb, xl, W, ncols, c);
+    if constexpr (MASK) {
+      nn_fold_row_stack<T, true>(a, ents, ord, n_entries, rows, rowfix, pool, ns_out, r, xb, xl, W, ncols, lane, c);
+    } else {
+      // entries without a mask layer (C2's granule seams: 2-4 entries) one
+      // after the other: the prefetched fold's per-lane descriptors would
+      // not fit the 64 VGPRs of this kernel at 8 waves per SIMD
+      // (the fixed-point rows here too: 1.50 vs 1.48 ms on C2, one more
+      // dependent load per entry row, profiles/r06i_render.jsonl)
+#pragma unroll 1
+      for (int k = 0; k < n_entries; k++)
+        nn_entry_row<T, false, kNnPx>(a, ents, ents[ord[k]], rows, rowfix, pool, false, ns_out, r, xb, xl, W, ncols,
+                                      c);
+    }
 
     // output: typed canvas (WCS) or utils.Scale + palette / grey RGBA
     if constexpr (CANVAS) {
@@ -989,7 +809,7 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
         if (full || 64 * q + lane < ncols) __builtin_nontemporal_store((T)c[q], (GPTR(T))(cdst + 64 * q));
     } else {
       uint32_t px[kNnPx];
-      rgba(c, px);
+      nn_rgba<T>(sk, safe, s_tab, c, px);
       store_row(r, px);
     }
   }
@@ -998,24 +818,17 @@ __global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs
 // Rows per wave of the NN band kernel: 8 when the batch has work for every
 // CU many times over (C2: 1.473 vs 1.506 ms), else 4 (C5, 80 tiles: 0.66 vs
 // 0.86 ms at 8 -- too few blocks); profiles/r03b_ab_nn.jsonl.  Masked and
-// canvas batches keep 4 (measured on C5 only).  A/B build: GSKYHIP_NN_RPW.
+// canvas batches keep 4 (measured on C5 only).
 constexpr int kNnRpw8MinItems = 32768;
 constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
 constexpr int kNnMaskRpw1Items = 16384;   // masked stacks: one row per wave below this many workgroups
 
-template <typename T, bool M, bool C, int RPW, bool ONE = false, bool STAGE = false, bool COOP = false,
-          bool WIDE = false>
+template <typename T, bool M, bool C, int RPW, bool ONE = false>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  // the XCD order (A/B) maps blocks over whole groups of 8 tiles: round the grid up
-  const int per = ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  const int grid = a.ab_xcd == 1 ? (a.n_tiles + 7) / 8 * 8 * per : a.ab_xcd == 2 ? (items + 7) / 8 * 8 : items;
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, STAGE, COOP, WIDE>), dim3((unsigned)grid), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
-
-// render_nn_stage.h (included by the per-type translation units)
-template <typename T> void launch_nn_stage(const RenderArgs &a, hipStream_t s);
 
 // NN band kernel launch for value type T (RGBA or typed canvas, with or
 // without a mask layer).
@@ -1028,53 +841,27 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   // latency-bound: one row per wave, 4x the workgroups
   const int64_t items4 = (int64_t)a.n_tiles * ((a.max_h + 15) / 16) * ((a.max_w + kBandCols - 1) / kBandCols);
   bool rpw1 = items4 < kNnRpw1MaxItems;
-  // single-entry tiles through the prefetching path (C2: 1.445 vs 1.470 ms,
-  // profiles/r03f_ab_c2.jsonl)
+  bool m1 = items4 < kNnMaskRpw1Items;
   bool one = true;
 #ifdef GSKYHIP_AB
-  // large RGBA batches through the LDS-staged kernel (render_nn_stage.h): 7 %
-  // slower on C2 (1.54 vs 1.44 ms, profiles/r03j_ab_c2_staged.jsonl)
-  bool staged = false;
-  if (const char *rp = getenv("GSKYHIP_NN_RPW")) {
-    rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1;
-    if (atoi(rp) == 16 && !mask && !canvas && one) { launch_nn_v<T, false, false, 16, true>(a, s); return; }
-  }
+  // shape forcing for tests/test_gpu_variants.py: small test batches never
+  // reach the thresholds that pick these shapes in production
+  if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
   if (const char *on = getenv("GSKYHIP_NN_ONE")) one = atoi(on) != 0;
-  if (const char *sg = getenv("GSKYHIP_NN_STAGED")) staged = atoi(sg) != 0;
-  if (const char *st = getenv("GSKYHIP_NN_STAGE")) {
-    if (!mask && !canvas && rpw8 && atoi(st) == 1) {
-      if (one) launch_nn_v<T, false, false, 8, true, true>(a, s);
-      else launch_nn_v<T, false, false, 8, false, true>(a, s);
-      return;
-    }
-  }
+  if (const char *mr = getenv("GSKYHIP_NN_MASK_RPW")) m1 = atoi(mr) == 1;
 #endif
   if (mask) {
     // stacks with a mask layer (C5: ~17 entries and a mask raster per tile)
     // are latency-bound per wave row: below kNnMaskRpw1Items workgroups, one
     // row per wave (4x the waves in flight)
-    bool m1 = items4 < kNnMaskRpw1Items;
-#ifdef GSKYHIP_AB
-    if (const char *rp = getenv("GSKYHIP_NN_MASK_RPW")) m1 = atoi(rp) == 1;
-#endif
     if (canvas) launch_nn_v<T, true, true, 4>(a, s);
     else if (m1) launch_nn_v<T, true, false, 1>(a, s);
     else launch_nn_v<T, true, false, 4>(a, s);
   } else if (canvas) {
     launch_nn_v<T, false, true, 4>(a, s);
-#ifdef GSKYHIP_AB
-  } else if (rpw8 && staged) {
-    launch_nn_stage<T>(a, s);
-#endif
   } else if (rpw8) {
-#ifdef GSKYHIP_AB
-    if (const char *co = getenv("GSKYHIP_NN_COOP")) {
-      if (one && atoi(co) != 0) { launch_nn_v<T, false, false, 8, true, false, true>(a, s); return; }
-    }
-    if (const char *wd = getenv("GSKYHIP_NN_WIDE")) {
-      if (one && atoi(wd) != 0) { launch_nn_v<T, false, false, 8, true, false, false, true>(a, s); return; }
-    }
-#endif
+    // single-entry tiles through the prefetching path (C2: 1.445 vs 1.470 ms,
+    // profiles/r03f_ab_c2.jsonl)
     if (one) launch_nn_v<T, false, false, 8, true>(a, s);
     else launch_nn_v<T, false, false, 8>(a, s);
   } else if (rpw1) {
@@ -1084,7 +871,7 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   }
 }
 
-void launch_bil(const RenderArgs &a, int n_items, hipStream_t s);   // render_bil.h, render_lds_f32.hip
+void launch_bil(const RenderArgs &a, int n_items, hipStream_t s);   // render_bil.h, band_f32.hip
 
 // Band kernel of one call: bilinear float canvases without a mask layer ->
 // render_bil_kernel; other bilinear work -> render_lds_kernel; nearest

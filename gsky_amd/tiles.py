@@ -322,6 +322,16 @@ class TileBatch:
                                              out.ctypes.data_as(C.c_void_p), stream), "render_pair_info")
         return out[: self.n_pairs]
 
+    def touched_bytes(self):
+        """Algorithmic source bytes of the last plan (gskyhip_render_touched):
+        (distinct source elements x element bytes, distinct 128-byte lines x
+        128) over every pair's window pixels at the picked levels."""
+        out = np.zeros(2, dtype=np.int64)
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().gskyhip_render_touched(C.c_void_p(self._ws.data_ptr()), self.n_tiles, self.n_pairs, self.max_h,
+                                           out.ctypes.data_as(C.c_void_p), stream), "render_touched")
+        return int(out[0]), int(out[1])
+
     def canvas_view(self, cv: torch.Tensor, tile: int, k: int, type_name: str) -> torch.Tensor:
         nb = {"Byte": 1, "SignedByte": 1, "Int16": 2, "UInt16": 2, "Float32": 4}[type_name]
         return cv[tile, k, : self.max_w * self.max_h * nb].view(TORCH_OF[type_name]).reshape(self.max_h,

@@ -650,6 +650,16 @@ int gskyhip_render_tile_info(void *workspace, int n_tiles, int n_pairs, int max_
 int gskyhip_render_pair_info(void *workspace, int n_tiles, int n_pairs, int max_tile_height, int32_t *info_out,
                              void *stream);
 
+/* Algorithmic source bytes of a planned batch (unique
+ * source bytes touched at the chosen overview level): bytes_out[0] = the
+ * distinct source elements x element bytes that the window pixels of every
+ * pair (data and mask rasters) pick by the nearest-neighbour rule of
+ * warp.go:271-300; bytes_out[1] = the distinct 128-byte lines holding them
+ * x 128.  Counted over each picked level once, however many pairs share it
+ * (bench.py C5).  No reference counterpart (an observability hook). */
+int gskyhip_render_touched(void *workspace, int n_tiles, int n_pairs, int max_tile_height, int64_t *bytes_out,
+                           void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -941,3 +941,33 @@ def test_pair_info_footprint_covers_samples(gpu):
         assert inside.all(), (p, bbox, (x0, y0, x1, y1))
         n_checked += 1
     assert n_checked > 0
+
+
+def test_render_touched_bytes_match_warped_windows(gpu):
+    """gskyhip_render_touched (bench.py's C5 algorithmic bytes) against the
+    warped windows themselves: float32 granules whose every element holds its
+    own index, so the distinct values of all windows of a granule are exactly
+    the source elements its pairs pick -- their count x 4 B and the 128-B
+    lines holding them must equal what the device bitmaps count."""
+    import dataclasses
+
+    import gsky_amd
+    cfg = synth.config_c2(scale=0.05, tiles_per_side=3, tile_px=128)
+    gran = []
+    for g in cfg.granules:
+        n = g.data.shape[0] * g.data.shape[1]
+        gran.append(dataclasses.replace(g, data=np.arange(n, dtype=np.float32).reshape(g.data.shape), nodata=-1.0,
+                                        overviews=[]))
+    cfg = dataclasses.replace(cfg, granules=gran)
+    b = gpu_batch(cfg)
+    b.render(gsky_amd.ScaleParams(0.0, 0.0, 40000.0, 0), None)
+    flat = [k for ks in cfg.pairs for k in ks]
+    seen = {}
+    for p, (win, bbox, tname, nd) in enumerate(b.warp_windows()):
+        vals = win.cpu().numpy().ravel()
+        vals = vals[vals != nd].astype(np.int64)
+        seen.setdefault(flat[p], set()).update(vals.tolist())
+    exp_bytes = sum(len(v) * 4 for v in seen.values())
+    exp_lines = sum(len({x * 4 // 128 for x in v}) * 128 for v in seen.values())
+    assert exp_bytes > 0
+    assert b.touched_bytes() == (exp_bytes, exp_lines)

@@ -5,9 +5,9 @@ partial 512-column blocks, tiles narrower than one slot) and a C5 batch
 in one child process per setting -- by the A/B build (libgskyhip_ab.so, the
 only build that reads GSKYHIP_* knobs) with every shape forced: rows per wave
 1 / 4 / 8, the single-entry prefetch path on and off, masked stacks at one or
-four rows per wave, the LDS-staged kernel (render_nn_stage.h).  The small batches never reach the size thresholds that
-pick those shapes in production, so without the knobs these code paths would
-only run in the full-size tests.  Measurements: profiles/r03*_ab_*.jsonl."""
+four rows per wave.  The small batches never reach the size thresholds
+that pick those shapes in production, so without the knobs these code paths
+would only run in the full-size tests.  Measurements: profiles/r03*_ab_*.jsonl."""
 import json
 import os
 import subprocess
@@ -82,7 +82,6 @@ print(json.dumps(res))
     {"GSKYHIP_NN_RPW": "1"}, {"GSKYHIP_NN_RPW": "4"},
     {"GSKYHIP_NN_RPW": "8", "GSKYHIP_NN_ONE": "1"}, {"GSKYHIP_NN_RPW": "8", "GSKYHIP_NN_ONE": "0"},
     {"GSKYHIP_NN_MASK_RPW": "1"}, {"GSKYHIP_NN_MASK_RPW": "4"},
-    {"GSKYHIP_NN_RPW": "8", "GSKYHIP_NN_STAGED": "1"},
 ])
 def test_ab_build_variants_match_oracle(knobs):
     lib = os.path.join(ROOT, "gsky_amd", "libgskyhip_ab.so")
