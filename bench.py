@@ -154,18 +154,36 @@ class Ctx:
 
     def timed(self, step, steps: int, warmup: int) -> float:
         """W untimed steps, then K steps bracketed by barrier + synchronize;
-        returns the max-over-ranks seconds of the K steps."""
+        returns the max-over-ranks seconds of the K steps.  Each timed step is
+        also bracketed by HIP events on the current (launch) stream, so an
+        outlier step is recorded (self.step_stats: min / median / max ms of
+        this rank's steps) instead of averaged away."""
         for _ in range(warmup):
             step()
         self.sync()
         self.barrier()
         self.sync()
+        evs = None
+        if not self.dry:
+            s = torch.cuda.current_stream()
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
         t0 = time.perf_counter()
-        for _ in range(steps):
+        if evs:
+            evs[0].record(s)
+        for k in range(steps):
             step()
+            if evs:
+                evs[k + 1].record(s)
         self.sync()
         self.barrier()
-        return self.max_over_ranks(time.perf_counter() - t0)
+        dt = self.max_over_ranks(time.perf_counter() - t0)
+        if evs and steps > 0:
+            ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(steps)]
+            self.step_stats = {"min": round(float(np.min(ms)), 4), "median": round(float(np.median(ms)), 4),
+                               "max": round(float(np.max(ms)), 4)}
+        else:
+            self.step_stats = None
+        return dt
 
 
 def event_ms(fn, reps: int = 10) -> float:
@@ -296,9 +314,10 @@ def run_c2(ctx: Ctx, args):
     total_px = full.out_pixels * args.steps
     plan_ms = event_ms(lambda: batch.render(sp, pal, phase=1), max(3, args.steps))
     render_ms = event_ms(lambda: batch.render(sp, pal, phase=2), max(3, args.steps))
-    # algorithmic bytes of rank 0's launch: unique source bytes under its tiles
-    # (its share of the 0.512 GB, by output pixels; exact at N=1) + RGBA out
-    src = sum(g.data.nbytes for g in full.granules) * cfg.out_pixels / full.out_pixels
+    # algorithmic bytes of rank 0's launch: the distinct
+    # source elements its tiles' windows pick (gskyhip_render_touched; at
+    # N=1 nearly all of the 0.512 GB) + RGBA out
+    src, src_lines = batch.touched_bytes()
     abytes = int(src + cfg.out_pixels * 4)
     achieved = abytes / (render_ms / 1e3) / 1e9
     # p50 GetMap tile latency: tiles the index gives at least one granule
@@ -313,6 +332,7 @@ def run_c2(ctx: Ctx, args):
     lat_e = tile_latency(ctx, cfg, gs, sp, pal, emp_ids, args.c2_lat_reps) if emp_ids else [float("nan")]
     out = {
         "value": round(total_px / dt / 1e6, 1), "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "step_ms": ctx.step_stats,
         "p50_tile_ms": round(float(np.percentile(lat, 50)), 4),
         "p99_tile_ms": round(float(np.percentile(lat, 99)), 4),
         "p50_timing": "C2 one-tile GetMap requests over tiles with >= 1 granule (%d of the %d such tiles, evenly "
@@ -333,7 +353,11 @@ def run_c2(ctx: Ctx, args):
                      if ctx.world == 1 else None,
                      "kernel": "render_nn_kernel<int16> + render_general_kernel (phase 2, one batch, rank 0)",
                      "kernel_ms": round(render_ms, 4), "plan_ms": round(plan_ms, 4),
-                     "algorithmic_bytes_per_launch": abytes, "lib_sha16": lib_sha()},
+                     "algorithmic_bytes_per_launch": abytes, "source_bytes": int(src),
+                     "source_line_bytes": int(src_lines),
+                     "bytes": "distinct source elements the tiles' windows pick (gskyhip_render_touched) x 2 B "
+                              "+ 4 B RGBA per output pixel; source_line_bytes: the 128-B lines holding them",
+                     "lib_sha16": lib_sha()},
     }
     if ctx.rank == 0 and args.png_tiles > 0:
         # EncodePNG's png.Encode (ogc_encoders.go:139) of rendered C2 tiles:
@@ -515,6 +539,7 @@ def run_c3(ctx: Ctx, args):
     out = {"workload": "C3: WCS GetCoverage %dx%d float32 bilinear EPSG:4326->3857 mosaic from %d granules, "
                        "%d chunks of <=1024^2 (ows.go:817-831)" % (W, H, len(cfg.granules), len(chunks)),
            "value": round(W * H * args.c3_steps / dt / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(dt / args.c3_steps * 1e3, 3),
+           "step_ms": ctx.step_stats,
            "step": "render own chunk rows straight into the band" + (" + RCCL gather to rank 0"
                                                                       if ctx.world > 1 else ""),
            "chunk_rows_rank0": rows[0], "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
@@ -588,7 +613,7 @@ def run_c4(ctx: Ctx, args):
         abytes = inside * n_bands * 4 + px
         ach = abytes / (k_ms / 1e3) / 1e9
         res[name] = {"value": round(len(geoms) * n_bands * args.steps / dt, 1), "unit": "polygon-slices/s",
-                     "ms_per_step": round(dt / args.steps * 1e3, 4),
+                     "ms_per_step": round(dt / args.steps * 1e3, 4), "step_ms": ctx.step_stats,
                      "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(k_ms, 4),
                                   "kernel": "drill compaction + %s reduction (rank 0)" % name,
@@ -603,7 +628,8 @@ def run_c4(ctx: Ctx, args):
         dbytes = 3 * vals + px
         dach = dbytes / (k_dec / 1e3) / 1e9
         res["deciles"] = {"value": round(len(mine) * n_bands * 3 / dt_dec, 1), "unit": "polygon-slices/s",
-                          "ms_per_step": round(dt_dec / 3 * 1e3, 3), "decile_count": 9,
+                          "ms_per_step": round(dt_dec / 3 * 1e3, 3), "step_ms": ctx.step_stats,
+                          "decile_count": 9,
                           "step": "readData with decileCount 9: mean pass writing the band-major rows + radix select "
                                   "(rank 0)",
                           "roofline": {"bound": "hbm", "achieved": round(dach, 1), "peak": HBM_PEAK_GBS,
@@ -674,7 +700,7 @@ def run_c5(ctx: Ctx, args):
                        "256 QA mask granules with overview pyramids, mask 00000001, grey scaling",
            "tiles_per_s": round(len(full.tiles) * args.steps / dt, 1),
            "value": round(full.out_pixels * args.steps / dt / 1e6, 1), "unit": "Mpix/s",
-           "ms_per_step": round(dt / args.steps * 1e3, 4),
+           "ms_per_step": round(dt / args.steps * 1e3, 4), "step_ms": ctx.step_stats,
            "p50_tile_ms": round(float(np.percentile(lat, 50)), 4),
            "p50_timing": "host wall of a one-tile request (plan + render + synchronize), rank 0",
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
