@@ -103,6 +103,7 @@ EXPORTS = [
     "gskyhip_drill_read_data_workspace_size", "gskyhip_drill_read_data",
     "gskyhip_png_workspace_size", "gskyhip_png_bound", "gskyhip_encode_png",
     "gskyhip_geotiff_workspace_size", "gskyhip_geotiff_bound", "gskyhip_encode_geotiff",
+    "gskyhip_netcdf_bound", "gskyhip_encode_netcdf", "gskyhip_encode_netcdf_host",
     "gskyhip_geotiff_info", "gskyhip_geotiff_read_host", "gskyhip_geotiff_read", "gskyhip_register_geotiff",
     "gskyhip_netcdf_info", "gskyhip_netcdf_srs", "gskyhip_netcdf_read_host", "gskyhip_netcdf_read", "gskyhip_register_netcdf",
 ]
@@ -209,6 +210,13 @@ def lib() -> C.CDLL:
     L.gskyhip_geotiff_bound.restype = i64
     L.gskyhip_encode_geotiff.argtypes = [C.POINTER(vp), ci, ci, ci, ci, C.POINTER(d), ci, vp,
                                          C.POINTER(C.c_char_p), ci, ci, vp, i64, vp, i64, C.POINTER(i64), vp]
+    if hasattr(L, "gskyhip_encode_netcdf"):   # (an older A/B library for timing comparisons lacks it)
+        L.gskyhip_netcdf_bound.argtypes = [ci, ci, ci, ci]
+        L.gskyhip_netcdf_bound.restype = i64
+        L.gskyhip_encode_netcdf.argtypes = [C.POINTER(vp), ci, ci, ci, ci, C.POINTER(d), ci, vp,
+                                            C.POINTER(C.c_char_p), ci, ci, vp, i64, C.POINTER(i64), vp]
+        L.gskyhip_encode_netcdf_host.argtypes = [C.POINTER(vp), ci, ci, ci, ci, C.POINTER(d), ci, vp,
+                                                 C.POINTER(C.c_char_p), ci, ci, vp, i64, C.POINTER(i64)]
     L.gskyhip_fnv32a.argtypes = [C.c_char_p, i64]
     L.gskyhip_fnv32a.restype = C.c_uint32
     L.gskyhip_version.restype = C.c_char_p

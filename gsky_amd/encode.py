@@ -76,3 +76,66 @@ def encode_geotiff(bands: Sequence[torch.Tensor], geot: Sequence[float], epsg: i
                                    C.byref(size), C.c_void_p(torch.cuda.current_stream().cuda_stream)),
           "encode_geotiff")
     return out[:size.value].tobytes()
+
+
+def encode_netcdf(bands: Sequence[torch.Tensor], geot: Sequence[float], epsg: int,
+                  nodata: Optional[Sequence[float]] = None, names: Optional[Sequence[str]] = None,
+                  zlevel: int = 6, uint16: bool = False, threads: int = 16) -> bytes:
+    """netCDF bytes of a coverage: what EncodeGdal writes for format
+    "netcdf" with COMPRESS=DEFLATE, ZLEVEL=6 (utils/ogc_encoders.go:263-301):
+    `bands` (height, width) device tensors of one dtype (uint8, int8, int16 --
+    uint16 when `uint16`, the bits held in int16 --, float32)."""
+    if not bands:
+        raise ValueError("encode_netcdf: no bands")
+    dt = bands[0].dtype
+    if dt not in _TIFF_DTYPES or any(b.dtype != dt or b.shape != bands[0].shape or not b.is_cuda for b in bands):
+        raise ValueError("encode_netcdf: bands must be device tensors of one shape and a supported dtype")
+    code = 2 if (uint16 and dt == torch.int16) else _TIFF_DTYPES[dt]
+    h, w = int(bands[0].shape[0]), int(bands[0].shape[1])
+    bands = [b.contiguous() for b in bands]
+    n = len(bands)
+    L = lib()
+    cap = int(L.gskyhip_netcdf_bound(w, h, n, code))
+    if cap <= 0:
+        raise ValueError("encode_netcdf: bad size / type")
+    out = np.empty(cap, np.uint8)
+    size = C.c_int64(0)
+    ptrs = (C.c_void_p * n)(*[b.data_ptr() for b in bands])
+    gt = (C.c_double * 6)(*[float(v) for v in geot])
+    nd = np.asarray(nodata, np.float64) if nodata is not None else None
+    nm = (C.c_char_p * n)(*[s.encode() for s in names]) if names is not None else None
+    check(L.gskyhip_encode_netcdf(ptrs, n, code, w, h, gt, int(epsg),
+                                  nd.ctypes.data_as(C.c_void_p) if nd is not None else None, nm, int(zlevel),
+                                  int(threads), out.ctypes.data_as(C.c_void_p), cap, C.byref(size),
+                                  C.c_void_p(torch.cuda.current_stream().cuda_stream)), "encode_netcdf")
+    return out[:size.value].tobytes()
+
+
+def encode_netcdf_host(bands: Sequence[np.ndarray], geot: Sequence[float], epsg: int,
+                       nodata: Optional[Sequence[float]] = None, names: Optional[Sequence[str]] = None,
+                       zlevel: int = 6, uint16: bool = False, threads: int = 4) -> bytes:
+    """encode_netcdf of host numpy bands (gskyhip_encode_netcdf_host; no device)."""
+    codes = {np.dtype(np.uint8): 1, np.dtype(np.int8): 100, np.dtype(np.int16): 3, np.dtype(np.float32): 6,
+             np.dtype(np.uint16): 2}
+    if not bands:
+        raise ValueError("encode_netcdf_host: no bands")
+    dt = np.dtype(bands[0].dtype)
+    if dt not in codes or any(b.dtype != dt or b.shape != bands[0].shape for b in bands):
+        raise ValueError("encode_netcdf_host: bands must be arrays of one shape and a supported dtype")
+    code = codes[dt]
+    h, w = int(bands[0].shape[0]), int(bands[0].shape[1])
+    bands = [np.ascontiguousarray(b) for b in bands]
+    n = len(bands)
+    L = lib()
+    cap = int(L.gskyhip_netcdf_bound(w, h, n, code))
+    out = np.empty(cap, np.uint8)
+    size = C.c_int64(0)
+    ptrs = (C.c_void_p * n)(*[b.ctypes.data for b in bands])
+    gt = (C.c_double * 6)(*[float(v) for v in geot])
+    nd = np.asarray(nodata, np.float64) if nodata is not None else None
+    nm = (C.c_char_p * n)(*[s.encode() for s in names]) if names is not None else None
+    check(L.gskyhip_encode_netcdf_host(ptrs, n, code, w, h, gt, int(epsg),
+                                       nd.ctypes.data_as(C.c_void_p) if nd is not None else None, nm, int(zlevel),
+                                       int(threads), out.ctypes.data_as(C.c_void_p), cap, C.byref(size)),
+          "encode_netcdf_host")
+    return out[:size.value].tobytes()

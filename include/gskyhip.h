@@ -485,6 +485,32 @@ int gskyhip_encode_geotiff(const void *const *bands, int n_bands, int dtype, int
                            int block_x, int block_y, void *workspace, int64_t workspace_bytes, uint8_t *out,
                            int64_t capacity, int64_t *size, void *stream);
 
+/* EncodeGdalOpen + EncodeGdal for format "netcdf" (utils/ogc_encoders.go:
+ * 263-301, creation options COMPRESS=DEFLATE, ZLEVEL=6; ows.go:1172) of one
+ * WCS coverage held in HBM: the netCDF-4 classic-model file GDAL 3.0.1's
+ * netCDF driver creates for those options -- one variable per band
+ * ("Band1", ...) with long_name = names[k] and _FillValue = nodata[k] (an
+ * "EmptyTile" band skipped as EncodeGdal skips it), chunks of one row,
+ * shuffle + deflate at zlevel, rows bottom-up with increasing y (GDAL's
+ * WRITE_BOTTOMUP default), x / y (lon / lat) coordinate variables at pixel
+ * centres, the "crs" grid mapping (CF attributes of `epsg`, spatial_ref
+ * naming the EPSG code, GeoTransform).  Byte is NC_BYTE + _Unsigned "true",
+ * UInt16 widens to NC_INT (the classic model has no unsigned types).
+ *   bands: HOST array of n_bands dev pointers, height x width of dtype;
+ *   out: HOST, capacity >= gskyhip_netcdf_bound bytes; *size = file length.
+ * The rows are deflated by n_threads host threads after one copy of each
+ * band to the host.  Parity with GDAL's bytes unpinned (no netCDF / HDF5
+ * library here): checked by reading the file back (gskyhip_netcdf_read_host). */
+int64_t gskyhip_netcdf_bound(int width, int height, int n_bands, int dtype);
+int gskyhip_encode_netcdf(const void *const *bands, int n_bands, int dtype, int width, int height,
+                          const double *geot, int epsg, const double *nodata, const char *const *names, int zlevel,
+                          int n_threads, uint8_t *out, int64_t capacity, int64_t *size, void *stream);
+/* The same from HOST bands (EncodeGdal's rasters are host memory in the
+ * reference): no device involved. */
+int gskyhip_encode_netcdf_host(const void *const *bands, int n_bands, int dtype, int width, int height,
+                               const double *geot, int epsg, const double *nodata, const char *const *names,
+                               int zlevel, int n_threads, uint8_t *out, int64_t capacity, int64_t *size);
+
 /* ---- drill (WPS zonal statistics) --------------------------------------- */
 /* readData (worker/gdalprocess/drill.go:90-227), mean / pixel-count mode,
  * decileCount = 0, for a batch of polygons over one time stack.
