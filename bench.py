@@ -163,6 +163,11 @@ class Ctx:
         self.sync()
         self.barrier()
         self.sync()
+        # no collector pause inside the timed region: the steps only launch
+        # (host-side stalls there stretch the wall time while the per-step
+        # device times stay normal -- round 5's one-off 16.8 ms C5 step)
+        gc.collect()
+        gc.disable()
         evs = None
         if not self.dry:
             s = torch.cuda.current_stream()
@@ -176,7 +181,9 @@ class Ctx:
                 evs[k + 1].record(s)
         self.sync()
         self.barrier()
-        dt = self.max_over_ranks(time.perf_counter() - t0)
+        wall = time.perf_counter() - t0
+        gc.enable()
+        dt = self.max_over_ranks(wall)
         if evs and steps > 0:
             ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(steps)]
             self.step_stats = {"min": round(float(np.min(ms)), 4), "median": round(float(np.median(ms)), 4),
