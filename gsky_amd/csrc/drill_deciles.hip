@@ -74,7 +74,6 @@ constexpr int kSelLds = 16 * 1024;   // dynamic LDS of a select workgroup (histo
 constexpr int kSelU = 8;             // segment values per thread in flight per round
 constexpr int kSelWpe = 8;           // select compiled for 8 waves per SIMD (63 VGPRs): r04ab sweep 14.9 -> 13.5 ms
 constexpr int kHistSlots = kBins / 256;  // radix histograms at once (the region also holds the 2048 buckets)
-constexpr bool kDecDirect = false;       // product: select from the stack directly (A/B: GSKYHIP_DEC_DIRECT)
 
 // Exclusive scan of 64-pixel chunks per polygon (one block; n_polys is modest).
 __global__ __launch_bounds__(1024) void decile_chunk_scan_kernel(const int32_t *__restrict__ count, int n_polys,
@@ -202,23 +201,14 @@ __global__ __launch_bounds__(256) void decile_transpose_kernel(const float *__re
 // reference indexes buf[len] and panics: len % (dc + 1) == 0 with step 1).
 // Dynamic LDS: n_slots histograms of 256 bins, then cache_keys keys (the
 // segment as it is, nodata included: no compaction, skipped on every pass).
-// DIRECT: no transposed copy -- the segment's values are gathered from the
-// time-innermost stack through the polygon's compacted pixel list, and the
-// workgroups of one polygon run back to back on one XCD (blockIdx % 8 is the
-// XCD the dispatcher picks), so the 32 bands sharing a pixel's 128-byte line
-// are read from that XCD's L2 after the first.
-template <int kU, bool DIRECT = false, int NT = kSelThreads, int WPE = 1, bool VEC = false>
+template <int kU, int NT = kSelThreads, int WPE = 1>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void decile_select_kernel(const float *__restrict__ vals,
-                                                                    const int64_t *__restrict__ mask_off,
                                                                     const int32_t *__restrict__ chunk_base,
                                                                     const int32_t *__restrict__ count,
                                                                     const int32_t *__restrict__ totals, int n_chunk,
                                                                     int b0, int n_list, int dc, float nodata,
                                                                     int n_slots, int cache_keys, float *__restrict__ out,
                                                                     int32_t *__restrict__ status,
-                                                                    const float *__restrict__ stack, int t_stride,
-                                                                    const int32_t *__restrict__ pix_idx,
-                                                                    const int32_t *__restrict__ tsel, int n_seg,
                                                                     const uint4 *__restrict__ part, int part_poly) {
   extern __shared__ uint32_t dyn[];
   uint32_t *cache = dyn + n_slots * 256;   // dyn[0, 2048): the buckets, then the candidates
@@ -238,12 +228,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   __shared__ int32_t s_done[kMaxRanks], s_small_r[64];
   __shared__ float s_small[64];
 
-  int item = blockIdx.x;
-  if constexpr (DIRECT) {   // XCD x takes the contiguous item range x * per .. (x + 1) * per - 1
-    const int per = (n_seg + 7) >> 3;
-    item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (item >= n_seg) return;
-  }
+  const int item = blockIdx.x;
   const int p = item / n_chunk, j = item % n_chunk;
   const int64_t o = (int64_t)p * n_list + b0 + j;
   float *dst = out + o * dc;
@@ -255,10 +240,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
   const int n = count[p];
   const int64_t npad = (int64_t)(n + kDecChunk - 1) / kDecChunk * kDecChunk;
-  const float *buf = DIRECT ? nullptr : vals + (int64_t)chunk_base[p] * kDecChunk * n_chunk + (int64_t)j * npad;
-  const int32_t *pix = DIRECT ? pix_idx + mask_off[p] : nullptr;
-  const float *bandp = DIRECT ? stack + tsel[j] : nullptr;
-  auto ld = [&](int i) -> float { return DIRECT ? bandp[(int64_t)pix[i] * t_stride] : buf[i]; };
+  const float *buf = vals + (int64_t)chunk_base[p] * kDecChunk * n_chunk + (int64_t)j * npad;
+  auto ld = [&](int i) -> float { return buf[i]; };
   // pass 1: the non-nodata values (the reference's buf, drill.go:231-237):
   // their count, the bits all their keys share, and the segment's keys in
   // LDS while they fit (order is irrelevant to order statistics)
@@ -390,44 +373,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
     }
   };
-  // VEC (band-major segments, 256-byte aligned rows): every valid key four at
-  // a time -- one 16-byte load per thread and slot (a quarter of the load
-  // instructions), g(k[4], valid bits)
-  auto for_keys4 = [&](auto &&g) {
-    if (fits && filled) {
-      for (int i = tid * 4; i < n; i += NT * 4) {
-        const uint4 c4 = *(const uint4 *)(cache + i);
-        const uint32_t k[4] = {c4.x, c4.y, c4.z, c4.w};
-        uint32_t m = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) m |= (i + c < n && !skipk(k[c])) ? (1u << c) : 0u;
-        g(k, m);
-      }
-    } else {
-      constexpr int kU4 = kU / 4 > 0 ? kU / 4 : 1;
-      for (int i0 = 0; i0 < n; i0 += NT * 4 * kU4) {
-        float4 v[kU4];
-#pragma unroll
-        for (int u = 0; u < kU4; u++) {
-          const int i = i0 + (u * NT + tid) * 4;
-          v[u] = i < n ? *(const float4 *)(buf + i) : make_float4(nodata, nodata, nodata, nodata);
-        }
-#pragma unroll
-        for (int u = 0; u < kU4; u++) {
-          const int i = i0 + (u * NT + tid) * 4;
-          const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-          uint32_t k[4], m = 0;
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            k[c] = fkey(x[c]);
-            if (!filled && fits && i + c < n) cache[i + c] = k[c];
-            m |= (i + c < n && x[c] != nodata) ? (1u << c) : 0u;
-          }
-          if (i < n) g(k, m);
-        }
-      }
-    }
-  };
   const int wv = tid >> 6, ln = tid & 63;
   // Range refinement: rank r is the s_rem[r]-th key in [s_lo[r], s_hi[r]].
   // A pass takes the ranks sharing the first open range [L, Hk], counts the
@@ -461,28 +406,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     const int sh = max(0, 32 - __clz(span) - kBinsLog);  // bucket = (k - L) >> sh < 2048
     for (int i = tid; i < kBins; i += NT) { H[i] = 0u; s_map[i] = -1; }
     __syncthreads();
-    if constexpr (VEC && !DIRECT) {
-      // one atomic per run of equal buckets among a thread's four neighbouring
-      // pixels (spatially correlated values share buckets: fewer same-address
-      // atomics)
-      for_keys4([&](const uint32_t *k, uint32_t m) {
-        int cur = -1;
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          const int b = (((m >> c) & 1u) && k[c] >= L && k[c] <= Hk) ? (int)((k[c] - L) >> sh) : -1;
-          if (b == cur) { cnt++; continue; }
-          if (cur >= 0) atomicAdd(&H[cur], cnt);
-          cur = b;
-          cnt = 1;
-        }
-        if (cur >= 0) atomicAdd(&H[cur], cnt);
-      });
-    } else {
-      for_keys([&](uint32_t k) {
-        if (k >= L && k <= Hk) atomicAdd(&H[(k - L) >> sh], 1u);
-      });
-    }
+    for_keys([&](uint32_t k) {
+      if (k >= L && k <= Hk) atomicAdd(&H[(k - L) >> sh], 1u);
+    });
     __syncthreads();
     filled = true;
     {   // inclusive scan of the buckets in place, 4 per thread
@@ -565,15 +491,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           if (sl >= 0) cand[s_soff[sl] + atomicAdd(&s_fill[sl], 1u)] = k;
         }
       };
-      if constexpr (VEC && !DIRECT) {
-        for_keys4([&](const uint32_t *k, uint32_t m) {
-#pragma unroll
-          for (int c = 0; c < 4; c++)
-            if ((m >> c) & 1u) take(k[c]);
-        });
-      } else {
-        for_keys(take);
-      }
+      for_keys(take);
       __syncthreads();
       // rank r is the s_rem[r]-th key of its bucket (<= 64 keys, one per
       // lane): MSB-first selection with wave ballots over the bits where the
@@ -675,36 +593,7 @@ int launch_drill_deciles(const DecileCall &c) {
                      w.rec);
   const int64_t max_chunks = c.mask_bytes / kDecChunk + c.n_polys;   // >= sum of ceil(count / 64)
   const int n_slots = kHistSlots;
-  int sel_lds = kSelLds, sel_u = kSelU;
-#ifdef GSKYHIP_AB
-  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(8, std::min(64, atoi(e))) * 1024;
-  if (const char *e = getenv("GSKYHIP_DEC_U")) sel_u = atoi(e);
-#endif
-  const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
-  const size_t dyn_lds = (size_t)sel_lds;
-  bool direct = kDecDirect;
-#ifdef GSKYHIP_AB
-  if (const char *e = getenv("GSKYHIP_DEC_DIRECT")) direct = atoi(e) != 0;
-#endif
-  int nt = kSelThreads;
-  bool use_part = true;
-#ifdef GSKYHIP_AB
-  if (const char *e = getenv("GSKYHIP_DEC_PART")) use_part = atoi(e) != 0;
-  if (const char *e = getenv("GSKYHIP_DEC_NT")) nt = atoi(e) == 512 ? 512 : atoi(e) == 128 ? 128 : kSelThreads;
-#endif
-  if (direct) {   // no transposed copy: a launch per band chunk straight from the stack
-    for (int b0 = 0; b0 < n_list; b0 += c.band_chunk) {
-      const int n_chunk = std::min(c.band_chunk, n_list - b0);
-      const int n_seg = c.n_polys * n_chunk;
-      if (hipMemcpyAsync(w.tsel, sel.data() + b0, sizeof(int32_t) * n_chunk, hipMemcpyHostToDevice, s) != hipSuccess)
-        return GSKYHIP_E_HIP;
-      const unsigned grid = (unsigned)(((int64_t)n_seg + 7) / 8 * 8);
-      hipLaunchKernelGGL((decile_select_kernel<kSelU, true>), dim3(grid), dim3(kSelThreads), dyn_lds, s, w.vals,
-                         c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status, c.stack, c.t_stride, w.idx, w.tsel, n_seg, nullptr, 0);
-    }
-    return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
-  }
+  const int cache_keys = (kSelLds - n_slots * 256 * 4) / 4;
   for (int b0 = 0; b0 < n_list; b0 += c.band_chunk) {
     const int n_chunk = std::min(c.band_chunk, n_list - b0);
     const int n_groups = (n_chunk + kTrBands - 1) / kTrBands;
@@ -714,32 +603,10 @@ int launch_drill_deciles(const DecileCall &c) {
     const int64_t items = max_chunks * n_groups;
     hipLaunchKernelGGL(decile_transpose_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, c.stack,
                        c.t_stride, w.idx, w.rec, w.chunk_base, c.n_polys, w.tsel, n_chunk, n_groups,
-                       w.vals, c.nodata, use_part ? w.part : nullptr);
-    if (nt == 512)
-      hipLaunchKernelGGL((decile_select_kernel<16, false, 512>), dim3((unsigned)n_seg), dim3(512), dyn_lds, s,
-                         w.vals, c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
-                         n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
-                         use_part ? (const uint4 *)w.part : nullptr, 0);
-    else if (nt == 128)
-      hipLaunchKernelGGL((decile_select_kernel<16, false, 128>), dim3((unsigned)n_seg), dim3(128), dyn_lds, s,
-                         w.vals, c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata,
-                         n_slots, cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
-                         use_part ? (const uint4 *)w.part : nullptr, 0);
-    else if (sel_u == 16)
-      hipLaunchKernelGGL((decile_select_kernel<16, false, kSelThreads, 1>), dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
-                         c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
-                         use_part ? (const uint4 *)w.part : nullptr, 0);
-    else if (sel_u == 4)
-      hipLaunchKernelGGL((decile_select_kernel<8, false, kSelThreads, 1>), dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
-                         c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
-                         use_part ? (const uint4 *)w.part : nullptr, 0);
-    else
-      hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe>), dim3((unsigned)n_seg), dim3(kSelThreads), dyn_lds, s, w.vals,
-                         c.mask_off, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list, c.decile_count, c.nodata, n_slots,
-                         cache_keys, c.out, c.status, nullptr, 0, nullptr, nullptr, 0,
-                         use_part ? (const uint4 *)w.part : nullptr, 0);
+                       w.vals, c.nodata, w.part);
+    hipLaunchKernelGGL((decile_select_kernel<kSelU, kSelThreads, kSelWpe>), dim3((unsigned)n_seg), dim3(kSelThreads),
+                       (size_t)kSelLds, s, w.vals, w.chunk_base, w.count, c.totals, n_chunk, b0, n_list,
+                       c.decile_count, c.nodata, n_slots, cache_keys, c.out, c.status, (const uint4 *)w.part, 0);
   }
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
@@ -756,41 +623,10 @@ int launch_decile_select_fused(const float *vals, const int32_t *chunk_base, con
   const int64_t n_seg = (int64_t)n_polys * n_sel;
   if (n_seg >= 2147483647LL) return GSKYHIP_E_ARG;
   const int n_slots = kHistSlots;
-  int sel_lds = kSelLds;
-#ifdef GSKYHIP_AB
-  if (const char *e = getenv("GSKYHIP_DEC_LDS_KB")) sel_lds = std::max(8, std::min(64, atoi(e))) * 1024;
-#endif
-  int nt = kSelThreads;
-  bool vec = false;
-#ifdef GSKYHIP_AB
-  if (const char *e = getenv("GSKYHIP_DEC_FNT")) nt = atoi(e);   // fused select workgroup: 128 / 256 / 512 / 1024 threads
-  if (const char *e = getenv("GSKYHIP_DEC_VEC")) vec = atoi(e) != 0;   // 16-byte segment loads, merged bucket runs
-#endif
-  const int cache_keys = (sel_lds - n_slots * 256 * 4) / 4;
-  if (nt == 1024)
-    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 1024, 8>), dim3((unsigned)n_seg),
-                       dim3(1024), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
-                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
-  else if (nt == 512)
-    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 512, 8>), dim3((unsigned)n_seg),
-                       dim3(512), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
-                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
-  else if (nt == 128)
-    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, 128, 8>), dim3((unsigned)n_seg),
-                       dim3(128), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
-                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
-  else if (vec && getenv("GSKYHIP_DEC_U") && atoi(getenv("GSKYHIP_DEC_U")) == 16)
-    hipLaunchKernelGGL((decile_select_kernel<16, false, kSelThreads, kSelWpe, true>), dim3((unsigned)n_seg),
-                       dim3(kSelThreads), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
-                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
-  else if (vec)
-    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe, true>), dim3((unsigned)n_seg),
-                       dim3(kSelThreads), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
-                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
-  else
-    hipLaunchKernelGGL((decile_select_kernel<kSelU, false, kSelThreads, kSelWpe>), dim3((unsigned)n_seg),
-                       dim3(kSelThreads), (size_t)sel_lds, s, vals, nullptr, chunk_base, count, totals, n_sel, 0, n_sel,
-                       decile_count, nodata, n_slots, cache_keys, out, status, nullptr, 0, nullptr, nullptr, 0, stats, 1);
+  const int cache_keys = (kSelLds - n_slots * 256 * 4) / 4;
+  hipLaunchKernelGGL((decile_select_kernel<kSelU, kSelThreads, kSelWpe>), dim3((unsigned)n_seg), dim3(kSelThreads),
+                     (size_t)kSelLds, s, vals, chunk_base, count, totals, n_sel, 0, n_sel, decile_count, nodata,
+                     n_slots, cache_keys, out, status, stats, 1);
   return hipGetLastError() == hipSuccess ? 0 : GSKYHIP_E_HIP;
 }
 

@@ -226,17 +226,29 @@ class TileBatch:
             ramp = gradient_rgba_palette(palette) if (palette is not None and n_out == 1) else None
             self._ramp = torch.from_numpy(ramp).to(self.device) if ramp is not None else None
             self._ramp_key = id(palette)
-        out_ns = (C.c_int32 * 3)(*[self.slots.index(ns) for ns in self.namespaces] + [0] * (3 - n_out))
-        sp = params.c()
-        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-        check(lib().gskyhip_render_tiles_typed(
-            phase, self.value_types if self.typed else 0, C.c_void_p(self._gran.data_ptr()), self.n_granules, C.c_void_p(self._crs.data_ptr()),
-            self.n_crs, self.dst_crs, C.c_void_p(self._tiles.data_ptr()), self.n_tiles,
-            C.c_void_p(self._pairs.data_ptr()), self.n_pairs, self.max_w, self.max_h, out_ns, n_out,
-            C.byref(self._mask_c) if self._mask_c is not None else None, resample, C.byref(sp),
-            C.c_void_p(self._ramp.data_ptr()) if self._ramp is not None else None,
-            C.c_void_p(out.data_ptr()) if rgba else None, C.c_void_p(cv.data_ptr()) if cv is not None else None,
-            C.c_void_p(self._ws.data_ptr()), self._ws.numel(), stream), "render_tiles")
+        # the call's arguments, built once per distinct request shape (a
+        # one-tile GetMap is latency-bound: building ~25 ctypes objects per
+        # call cost as much host time as the planning kernel takes on the GPU)
+        stream = torch.cuda.current_stream().cuda_stream
+        key = (phase, self.typed, out.data_ptr() if rgba else 0, cv.data_ptr() if cv is not None else 0,
+               self._ramp.data_ptr() if self._ramp is not None else 0, resample, params.offset, params.scale,
+               params.clip, params.colour_scale, stream, self._ws.data_ptr())
+        cache = self.__dict__.setdefault("_call_cache", {})
+        args = cache.get(key)
+        if args is None:
+            out_ns = (C.c_int32 * 3)(*[self.slots.index(ns) for ns in self.namespaces] + [0] * (3 - n_out))
+            sp = params.c()
+            args = (phase, self.value_types if self.typed else 0, self._gran.data_ptr(), self.n_granules,
+                    self._crs.data_ptr(), self.n_crs, self.dst_crs, self._tiles.data_ptr(), self.n_tiles,
+                    self._pairs.data_ptr(), self.n_pairs, self.max_w, self.max_h, out_ns, n_out,
+                    C.byref(self._mask_c) if self._mask_c is not None else None, resample, C.byref(sp),
+                    self._ramp.data_ptr() if self._ramp is not None else None,
+                    out.data_ptr() if rgba else None, cv.data_ptr() if cv is not None else None,
+                    self._ws.data_ptr(), self._ws.numel(), stream)
+            if len(cache) > 64:
+                cache.clear()
+            cache[key] = args = (args, sp, out_ns)   # the structs the byrefs point at stay alive with them
+        check(lib().gskyhip_render_tiles_typed(*args[0]), "render_tiles")
         if not rgba:
             return cv
         return (out, cv) if canvas else out

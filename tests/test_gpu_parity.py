@@ -338,6 +338,32 @@ def test_render_c1(gpu, oracle):
     assert identity(got, exp) >= NN_IDENTITY
 
 
+@pytest.mark.parametrize("n_tiles", [1, 2, 3])
+def test_render_small_batch_complex_tiles(gpu, oracle, n_tiles):
+    """Small batches (the one-workgroup planner, one-row-per-wave band
+    kernel) with a complex tile beside simple ones: an Int32 granule, which
+    the merge promotes to a Float32 canvas (vt 0: render_general_kernel's
+    body); the other tiles are the same request moved east over float32
+    data.  One tile also takes the planner's one-tile schedule (tile plan
+    beside the row records)."""
+    import dataclasses
+
+    import gsky_amd
+    cfg = synth.config_c1(scale=0.5)
+    g0 = cfg.granules[0]
+    gi = dataclasses.replace(g0, data=np.where(g0.data == -9999.0, -9999, g0.data * 7.0).astype(np.int32))
+    x0, y0, x1, y1 = cfg.tiles[0][0]
+    tiles = [((x0 + k * (x1 - x0), y0, x1 + k * (x1 - x0), y1), 256, 256) for k in range(n_tiles)]
+    cfg = dataclasses.replace(cfg, granules=[gi, g0], tiles=tiles, pairs=[[0]] + [[1]] * (n_tiles - 1),
+                              scale=(0.0, 0.0, 7000.0, 0))
+    b = gpu_batch(cfg)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale)).cpu().numpy()
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg)
+    assert identity(got, exp) >= NN_IDENTITY
+    assert (exp[0, ..., 3] > 0).mean() > 0.5
+
+
 def test_render_c2_small(gpu, oracle):
     import gsky_amd
     cfg = synth.config_c2(scale=0.1, tiles_per_side=4, tile_px=256)
@@ -636,12 +662,13 @@ def test_drill_deciles_parity(gpu, oracle, dcount, pc, clip):
                           vals[..., 1:].astype(np.float32)[stt.cpu().numpy() == 0])
 
 
-@pytest.mark.parametrize("side", [100, 150])
+@pytest.mark.parametrize("side", [100, 150, 290])
 def test_drill_deciles_large_polygon(gpu, oracle, side):
-    """Segments past the select workgroup's LDS key cache (~10k keys for 9
-    deciles): a 150 x 150 in-mask window streams its values from the segment
-    on every pass, a 100 x 100 one selects from LDS; both equal to the oracle
-    for every band, nodata values (-9999 at 1 %) skipped.  Bands 0/1/3 take
+    """Long segments: 100 x 100 and 150 x 150 in-mask windows (~9.5k / ~21k
+    keys) take the wave-per-segment select, 290 x 290 (~80k keys, past its
+    2^16 limit) the 256-thread workgroup select streaming its values on every
+    pass; all equal to the oracle for every band, nodata values (-9999 at
+    1 %) skipped.  Bands 0/1/3 take
     the bucket + counting-compare path (band 3: both signs, no shared key
     bits); bands 2 and 4 (a handful of distinct values) overflow the 64-key
     buckets and finish by radix selection."""
@@ -649,9 +676,10 @@ def test_drill_deciles_large_polygon(gpu, oracle, side):
 
     from gsky_amd import drill
     rng = np.random.default_rng(side)
-    data = rng.uniform(0.0, 0.05, size=(5, 160, 160)).astype(np.float32)
-    data[3] = rng.normal(size=(160, 160)) * 1000.0          # both signs, every exponent: no shared key bits
-    data[4] = rng.choice(np.array([-1.0, 0.0, 2.5, 7.0], np.float32), size=(160, 160))   # 4 values: huge buckets
+    sz = side + 10
+    data = rng.uniform(0.0, 0.05, size=(5, sz, sz)).astype(np.float32)
+    data[3] = rng.normal(size=(sz, sz)) * 1000.0          # both signs, every exponent: no shared key bits
+    data[4] = rng.choice(np.array([-1.0, 0.0, 2.5, 7.0], np.float32), size=(sz, sz))   # 4 values: huge buckets
     data[rng.uniform(size=data.shape) < 0.01] = -9999.0
     data[2] = np.round(data[2] * 100) / 100   # many equal values: ties across the ranks
     st = drill.DrillStack(torch.from_numpy(data), -9999.0, gpu)
