@@ -82,7 +82,7 @@ __device__ __forceinline__ void bil_store(const RenderArgs &a, int t, int r, int
 
 // HP: pixels whose taps are in flight together; WPS: waves per SIMD the
 // register budget is sized for.
-template <typename WT, int RPW, int HP, int WPS>
+template <typename WT, int RPW, int HP, int WPS, bool SEP = false>
 __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                             const int32_t *__restrict__ order,
                                                             const RowRec *__restrict__ rows,
@@ -116,6 +116,16 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
   const bool full = ncols == kBandCols;
   const int xl = xb + lane;
 
+  // Single-entry tiles, separable rows (round 6): a LINEAR row with dY == 0
+  // samples one source row pair (iy, iy + 1) at every pixel, at the same
+  // columns on every row with the same (xs0, dX) bits -- C3's EPSG:4326 ->
+  // 3857 chunks at 1:1 -- so the next row down (iy + 1, iy + 2) finds its
+  // upper taps already in registers: one 8-byte tap load per pixel instead
+  // of two.  Same coordinates, addresses and fold as the fast path below.
+  bool sp_have = false;
+  int sp_iy = 0;
+  double sp_xs0 = 0.0, sp_dX = 0.0;
+  u32x2 sp_t1[kNnPx];
 #pragma unroll 1
   for (int j = 0; j < RPW; j++) {
     const int r = r0 + j;
@@ -123,6 +133,82 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
     float c[kNnPx];
 #pragma unroll
     for (int q = 0; q < kNnPx; q++) c[q] = cnod;
+
+    if constexpr (SEP) {
+      bool done = false;
+      if (n_entries == 1) {
+        const EntryD &e = ents[ord[0]];
+        const int ir = r - e.yoff, ew = e.w, exoff = e.xoff;
+        const int lim = max(0, min(ew, W - exoff));
+        const int c0 = exoff - xb, c1 = exoff + lim - xb;
+        const double nd64 = e.nodata64;
+        const bool hnd = e.has_nodata != 0, nd_nan = nd64 != nd64;
+        // a NaN nodata takes the per-entry path (bil_fold4 compares taps with ==)
+        const bool nd_f32 = !hnd || (!nd_nan && (double)(float)nd64 == nd64);
+        if (e.ns == ns_out && ew > 0 && ir >= 0 && ir < e.h && c1 > 0 && c0 < ncols && nd_f32) {
+          const RowRec *rr = rows + e.row_base + ir;
+          const int kind = __builtin_amdgcn_readfirstlane(rr->kind);
+          const double xs0 = uni64d(rr->v[0]), ys0 = uni64d(rr->v[1]), dX = uni64d(rr->v[2]), dY = uni64d(rr->v[3]);
+          const int bx = e.band_x, by = e.band_y;
+          if (kind == ROW_LINEAR && dY == 0.0) {
+            const int ic0 = xl - exoff;
+            const int iy = (int)floor(ys0 - 0.5);   // sy == ys0 at every pixel (dY * dist is a signed zero)
+            const WT ry = (WT)(1.5 - (ys0 - (double)iy));
+            int ixv[kNnPx];
+            WT rx[kNnPx];
+            bool allin = (unsigned)iy < (unsigned)(by - 1);
+#pragma unroll
+            for (int q = 0; q < kNnPx; q++) {
+              const int ic = ic0 + 64 * q;
+              const double sx = xs0 + dX * (double)ic;
+              ixv[q] = (int)floor(sx - 0.5);
+              rx[q] = (WT)(1.5 - (sx - (double)ixv[q]));
+              allin = allin & (((unsigned)ic >= (unsigned)lim) | ((unsigned)ixv[q] < (unsigned)(bx - 1)));
+            }
+            if (__all(allin)) {
+              const bool reuse = sp_have & (iy == sp_iy + 1) & (__double_as_longlong(xs0) == __double_as_longlong(sp_xs0)) &
+                                 (__double_as_longlong(dX) == __double_as_longlong(sp_dX));
+              const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                  (void *)uniform_ptr(e.band), (short)0, (int)((int64_t)bx * by * 4), 0x00020000);
+              const float nd = e.nd.f, fillv = e.fill.f;
+              const bool fill_mode = e.fill_mode != 0;
+              const float ndf = (float)nd64;
+              // HP pixels' taps in flight at a time (the register peak of the fast path)
+#pragma unroll
+              for (int h = 0; h < kNnPx; h += HP) {
+                u32x2 t0[HP], t1[HP];
+#pragma unroll
+                for (int q = 0; q < HP; q++) {
+                  const int ic = ic0 + 64 * (h + q);
+                  const bool ok = (unsigned)ic < (unsigned)lim;
+                  const uint32_t o0 = ok ? (uint32_t)(iy * bx + ixv[h + q]) * 4u : 0x80000000u;
+                  const uint32_t o1 = ok ? o0 + (uint32_t)bx * 4u : 0x80000000u;
+                  if (reuse) t0[q] = sp_t1[h + q];
+                  else t0[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, o0, 0, 0);
+                  t1[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, 0);
+                }
+#pragma unroll
+                for (int q = 0; q < HP; q++) {
+                  bil_fold4<WT>(t0[q], t1[q], rx[h + q], ry, ic0 + 64 * (h + q), lim, nd, ndf, hnd, fillv, fill_mode,
+                                c[h + q]);
+                  sp_t1[h + q] = t1[q];
+                }
+              }
+              sp_have = true;
+              sp_iy = iy;
+              sp_xs0 = xs0;
+              sp_dX = dX;
+              done = true;
+            }
+          }
+        }
+      }
+      if (done) {
+        bil_store(a, t, r, xl, lane, full, ncols, c);
+        continue;
+      }
+      sp_have = false;
+    }
 
 #pragma unroll 1
     for (int k = 0; k < n_entries; k++) {
@@ -302,8 +388,19 @@ __global__ __launch_bounds__(256, WPS) void render_bil_kernel(RenderArgs a, cons
 void launch_bil(const RenderArgs &a, int n_items, hipStream_t s) {
   (void)n_items;
   const int items = a.n_tiles * ((a.max_h + 15) / 16) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_bil_kernel<float, 4, 4, 8>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
-                     a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
+  int sep = 6;
+#ifdef GSKYHIP_AB
+  if (const char *e = getenv("GSKYHIP_BIL_REUSE")) sep = atoi(e);   // 0: round 5's kernel; 8: reuse at 8 waves / SIMD
+#endif
+  if (sep == 6)
+    hipLaunchKernelGGL((render_bil_kernel<float, 4, 4, 6, true>), dim3((unsigned)items), dim3(256), 0, s, a,
+                       a.entries, a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
+  else if (sep)
+    hipLaunchKernelGGL((render_bil_kernel<float, 4, 4, 8, true>), dim3((unsigned)items), dim3(256), 0, s, a,
+                       a.entries, a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
+  else
+    hipLaunchKernelGGL((render_bil_kernel<float, 4, 4, 8>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+                       a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
 
 }  // namespace gsky

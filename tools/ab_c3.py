@@ -5,6 +5,7 @@ HIP events on the launch stream over the whole coverage launch (plan +
 bilinear band kernel), with --oracle the nodata-mask identity and the largest
 relative difference of the valid pixels against oracle/.  One JSON line."""
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -54,7 +55,11 @@ def main():
             ts.append(ev[0].elapsed_time(ev[1]))
         res[name + "_ms_median"] = round(float(np.median(ts)), 4)
         res[name + "_ms_min"] = round(float(np.min(ts)), 4)
-    rec = {"label": args.label, "config": "c3", "lib": os.environ.get("GSKYHIP_LIB", "default"), **res}
+    rec = {"label": args.label, "config": "c3", "lib": os.environ.get("GSKYHIP_LIB", "default"),
+           "variant": os.environ.get("GSKYHIP_BIL_REUSE", ""), **res}
+    run()
+    torch.cuda.synchronize()
+    rec["canvas_sha16"] = hashlib.sha256(band.cpu().numpy().tobytes()).hexdigest()[:16]   # bit identity across variants
     if args.oracle:
         from oracle import oracle as O
         from tests.helpers import oracle_render
