@@ -265,6 +265,7 @@ struct MaskU {
   double v[4];
   int w, h, bx, by, dt, kind;
   int32_t fill;
+  int same;   // -1: test v / w / h / bx / by / kind here; 0 / 1: tested where the mask row was read
 };
 
 // Where nn_entry_core() takes the row's fixed-point form and record from:
@@ -400,6 +401,7 @@ __device__ __forceinline__ void nn_entry_core(const RenderArgs &a, const EntryD 
         m.w = me.w; m.h = me.h; m.bx = me.band_x; m.by = me.band_y; m.dt = me.out_dtype; m.fill = me.fill.i;
         m.band = uniform_ptr(me.band);
         m.kind = -1;
+        m.same = -1;
         if (ir < m.h) {
           const RowRec &mr = rows[uni64(me.row_base) + ir];
           m.kind = __builtin_amdgcn_readfirstlane(mr.kind);
@@ -408,11 +410,12 @@ __device__ __forceinline__ void nn_entry_core(const RenderArgs &a, const EntryD 
         }
       }
       const int slot = mask_slot(m.dt);
-      const bool same = m.w == ew && ir < m.h && m.bx == bx && m.by == by && m.kind == ROW_LINEAR &&
-                        __double_as_longlong(m.v[0]) == __double_as_longlong(ru.v(0)) &&
-                        __double_as_longlong(m.v[1]) == __double_as_longlong(ru.v(1)) &&
-                        __double_as_longlong(m.v[2]) == __double_as_longlong(ru.v(2)) &&
-                        __double_as_longlong(m.v[3]) == __double_as_longlong(ru.v(3));
+      const bool same = m.same >= 0 ? m.same != 0
+                                    : m.w == ew && ir < m.h && m.bx == bx && m.by == by && m.kind == ROW_LINEAR &&
+                                          __double_as_longlong(m.v[0]) == __double_as_longlong(ru.v(0)) &&
+                                          __double_as_longlong(m.v[1]) == __double_as_longlong(ru.v(1)) &&
+                                          __double_as_longlong(m.v[2]) == __double_as_longlong(ru.v(2)) &&
+                                          __double_as_longlong(m.v[3]) == __double_as_longlong(ru.v(3));
       if (same && slot >= 0) {
         const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)m.band, (short)0, (int)((int64_t)m.bx * m.by * (int64_t)type_size(m.dt)), 0x00020000);
@@ -523,21 +526,30 @@ __device__ __forceinline__ void nn_fold_row_stack(const RenderArgs &a, const Ent
     const int bx = E.band_x, by = E.band_y, fill_mode = E.fill_mode, mask_pair = E.mask_pair;
     const uint32_t nd = E.nd.u, fill = E.fill.u;
     int64_t fx0 = kFixNone, fy0 = 0, fdx = 0, fdy = 0;
-    int mw = 0, mh = 0, mbx = 0, mby = 0, mdt = 0, mkind = -1;
+    int mdt = 0;
     int32_t mfill = 0;
     const void *mband = nullptr;
-    double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
+    uint64_t msame = 0;   // entries whose mask row picks the data row's elements (nn_masked_same_row)
     if constexpr (!MASK) {
       const RowFix &F = rowfix[rb];
       fx0 = act ? F.x0 : kFixNone; fy0 = F.y0; fdx = F.dx; fdy = F.dy;
     } else {
+      // the mask pair's descriptor and row, tested here against the data
+      // row in each lane: only the result, the mask's type, fill and band
+      // stay live through the fold (the mask row's values held across it
+      // took the kernel to 87 VGPRs, 5 waves per SIMD)
       const bool mk = act & (mask_pair >= 0);
       const EntryD &M = ents[mk ? mask_pair : p];
-      mw = M.w; mh = M.h; mbx = M.band_x; mby = M.band_y; mdt = M.out_dtype; mfill = M.fill.i; mband = M.band;
+      const int mw = M.w, mh = M.h, mbx = M.band_x, mby = M.band_y;
+      mdt = M.out_dtype; mfill = M.fill.i; mband = M.band;
       const bool mrow = mk & (ir < mh);
       const RowRec &MR = rows[mrow ? M.row_base + ir : 0];
-      mkind = mrow ? MR.kind : -1;
-      m0 = MR.v[0]; m1 = MR.v[1]; m2 = MR.v[2]; m3 = MR.v[3];
+      const bool same = mrow & (mw == ew) & (mbx == bx) & (mby == by) & (MR.kind == ROW_LINEAR) &
+                        (__double_as_longlong(MR.v[0]) == __double_as_longlong(v0)) &
+                        (__double_as_longlong(MR.v[1]) == __double_as_longlong(v1)) &
+                        (__double_as_longlong(MR.v[2]) == __double_as_longlong(v2)) &
+                        (__double_as_longlong(MR.v[3]) == __double_as_longlong(v3));
+      msame = __builtin_amdgcn_ballot_w64(same);
     }
     auto rl = [](int v, int j) { return __builtin_amdgcn_readlane(v, j); };
     auto rl64 = [](int64_t v, int j) {
@@ -563,9 +575,10 @@ __device__ __forceinline__ void nn_fold_row_stack(const RenderArgs &a, const Ent
       rv.fx.x0 = rl64(fx0, j); rv.fx.y0 = rl64(fy0, j); rv.fx.dx = rl64(fdx, j); rv.fx.dy = rl64(fdy, j);
       if constexpr (MASK) {
         MaskU m;
-        m.band = rlp(mband, j); m.w = rl(mw, j); m.h = rl(mh, j); m.bx = rl(mbx, j); m.by = rl(mby, j);
-        m.dt = rl(mdt, j); m.kind = rl(mkind, j); m.fill = rl(mfill, j);
-        m.v[0] = rld(m0, j); m.v[1] = rld(m1, j); m.v[2] = rld(m2, j); m.v[3] = rld(m3, j);
+        m.band = rlp(mband, j); m.bx = u.bx; m.by = u.by; m.dt = rl(mdt, j); m.fill = rl(mfill, j);
+        m.same = (int)((msame >> j) & 1ull);
+        m.w = 0; m.h = 0; m.kind = -1;
+        m.v[0] = m.v[1] = m.v[2] = m.v[3] = 0.0;
         nn_entry_core<T, MASK, kNnPx>(a, ents, rows, pool, u, rv, &m, r, xb, xl, W, ncols, c);
       } else {
         nn_entry_core<T, MASK, kNnPx>(a, ents, rows, pool, u, rv, nullptr, r, xb, xl, W, ncols, c);
@@ -602,8 +615,10 @@ __device__ __forceinline__ void nn_rgba(const ScaleK &sk, bool safe, const uint3
 // wave's rows and take all RPW rows' fixed-point forms in one vector load,
 // so no row waits for its record.  Tiles with more entries (or a mask layer)
 // fold through nn_fold_row_stack().
-template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false>
-__global__ __launch_bounds__(256, MASK ? 1 : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
+// MW (masked stacks): waves per SIMD the kernel is compiled for (0: as the
+// registers fall, 87 VGPRs = 5 for C5's int16 kernel).
+template <typename T, bool MASK, bool CANVAS, int RPW, bool ONE = false, int MW = 0>
+__global__ __launch_bounds__(256, MASK ? (MW > 0 ? MW : 1) : 8) void render_nn_kernel(RenderArgs a, const EntryD *__restrict__ ents,
                                                                       const int32_t *__restrict__ order,
                                                                       const RowRec *__restrict__ rows,
                                                                       const RowFix *__restrict__ rowfix,
@@ -823,10 +838,10 @@ constexpr int kNnRpw8MinItems = 32768;
 constexpr int kNnRpw1MaxItems = 256;   // below one workgroup per CU at 4 rows per wave
 constexpr int kNnMaskRpw1Items = 16384;   // masked stacks: one row per wave below this many workgroups
 
-template <typename T, bool M, bool C, int RPW, bool ONE = false>
+template <typename T, bool M, bool C, int RPW, bool ONE = false, int MW = 0>
 void launch_nn_v(const RenderArgs &a, hipStream_t s) {
   const int items = a.n_tiles * ((a.max_h + 4 * RPW - 1) / (4 * RPW)) * ((a.max_w + kBandCols - 1) / kBandCols);
-  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
+  hipLaunchKernelGGL((render_nn_kernel<T, M, C, RPW, ONE, MW>), dim3((unsigned)items), dim3(256), 0, s, a, a.entries,
                      a.order, a.rows, a.rowfix, a.pool, a.tplans, a.tiles, items);
 }
 
@@ -842,6 +857,11 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   const int64_t items4 = (int64_t)a.n_tiles * ((a.max_h + 15) / 16) * ((a.max_w + kBandCols - 1) / kBandCols);
   bool rpw1 = items4 < kNnRpw1MaxItems;
   bool m1 = items4 < kNnMaskRpw1Items;
+  // masked one-row kernel compiled for 7 waves per SIMD (71 VGPRs): C5 band
+  // kernel 0.270 ms vs 0.281 at the 6 its registers fall to and 0.277 at 8
+  // (15 VGPRs spilled), profiles/r06y_c5.jsonl; A/B: 0 (as the registers
+  // fall) or 8
+  int mw = 7;
   bool one = true;
 #ifdef GSKYHIP_AB
   // shape forcing for tests/test_gpu_variants.py: small test batches never
@@ -849,13 +869,16 @@ void launch_nn_t(const RenderArgs &a, bool mask, hipStream_t s) {
   if (const char *rp = getenv("GSKYHIP_NN_RPW")) { rpw8 = atoi(rp) == 8; rpw1 = atoi(rp) == 1; }
   if (const char *on = getenv("GSKYHIP_NN_ONE")) one = atoi(on) != 0;
   if (const char *mr = getenv("GSKYHIP_NN_MASK_RPW")) m1 = atoi(mr) == 1;
+  if (const char *mv = getenv("GSKYHIP_NN_MASK_WPE")) mw = atoi(mv);
 #endif
   if (mask) {
     // stacks with a mask layer (C5: ~17 entries and a mask raster per tile)
     // are latency-bound per wave row: below kNnMaskRpw1Items workgroups, one
     // row per wave (4x the waves in flight)
     if (canvas) launch_nn_v<T, true, true, 4>(a, s);
-    else if (m1) launch_nn_v<T, true, false, 1>(a, s);
+    else if (m1 && mw == 8) launch_nn_v<T, true, false, 1, false, 8>(a, s);
+    else if (m1 && mw == 0) launch_nn_v<T, true, false, 1>(a, s);
+    else if (m1) launch_nn_v<T, true, false, 1, false, 7>(a, s);
     else launch_nn_v<T, true, false, 4>(a, s);
   } else if (canvas) {
     launch_nn_v<T, false, true, 4>(a, s);
