@@ -22,28 +22,25 @@ __device__ __forceinline__ int mask_slot(int dtype) {
   }
 }
 
+// A mask raster's value as its type reads it (tile_merger.go's int8 / uint8 /
+// int16 / uint16 views of the masked bits): sign or zero extension of the low
+// 8 or 16 bits, without a branch on the (wave-uniform) type.
+__device__ __forceinline__ int32_t mask_typed(int dtype, int32_t a) {
+  const int sh = (dtype == GSKYHIP_SIGNEDBYTE || dtype == GSKYHIP_BYTE) ? 24 : 16;
+  const bool sgn = dtype == GSKYHIP_SIGNEDBYTE || dtype == GSKYHIP_INT16;
+  const uint32_t u = (uint32_t)a << sh;
+  return sgn ? ((int32_t)u >> sh) : (int32_t)(u >> sh);
+}
+
+// ComputeMask (tile_merger.go:314-445) of one mask value: value & mask > 0, or
+// any bit test (value & filter == want).  Branch-free over the tests (no
+// early exit), so a wave's lanes never diverge inside it -- with `return
+// true` per lane the compiler built exec-mask branches around every pixel.
 __device__ __forceinline__ bool mask_bit(const MaskSpecS &m, int dtype, int32_t v) {
-  if (m.has_value) {
-    int32_t a = v & m.value;
-    switch (dtype) {
-      case GSKYHIP_SIGNEDBYTE: return (int8_t)a > 0;
-      case GSKYHIP_INT16: return (int16_t)a > 0;
-      case GSKYHIP_BYTE: return (uint8_t)a > 0;
-      default: return (uint16_t)a > 0;
-    }
-  }
-  for (int j = 0; j < m.n_tests; j++) {
-    int32_t a = v & m.filt[j];
-    bool eq;
-    switch (dtype) {
-      case GSKYHIP_SIGNEDBYTE: eq = (int8_t)a == (int8_t)m.want[j]; break;
-      case GSKYHIP_INT16: eq = (int16_t)a == (int16_t)m.want[j]; break;
-      case GSKYHIP_BYTE: eq = (uint8_t)a == (uint8_t)m.want[j]; break;
-      default: eq = (uint16_t)a == (uint16_t)m.want[j]; break;
-    }
-    if (eq) return true;
-  }
-  return false;
+  if (m.has_value) return mask_typed(dtype, v & m.value) > 0;
+  bool hit = false;
+  for (int j = 0; j < m.n_tests; j++) hit |= mask_typed(dtype, v & m.filt[j]) == mask_typed(dtype, m.want[j]);
+  return hit;
 }
 
 // ---------------------------------------------------------------- scale

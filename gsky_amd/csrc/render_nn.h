@@ -192,7 +192,7 @@ __device__ __forceinline__ bool nn_fix_row(__amdgpu_buffer_rsrc_t rs, int64_t fx
 // masked (ComputeMask, tile_merger.go:314-445), and in fill mode canvas ==
 // nodata; a pixel whose element is outside the band takes the window fill
 // and the mask's fill (warp.go:246-247), as nn_fetch() does.
-template <typename T, int NPX>
+template <typename T, int NPX, bool M8>
 __device__ __forceinline__ void nn_masked_same_row(const MaskSpecS &ms, int mdt, int32_t mfill,
                                                    __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t mrs,
                                                    double xs0, double ys0, double dX, double dY, int ic0, int lim,
@@ -200,7 +200,6 @@ __device__ __forceinline__ void nn_masked_same_row(const MaskSpecS &ms, int mdt,
                                                    typename VOf<T>::type fillv, bool fill_mode,
                                                    typename VOf<T>::type (&c)[NPX]) {
   using V = typename VOf<T>::type;
-  const bool m8 = mdt == GSKYHIP_BYTE || mdt == GSKYHIP_SIGNEDBYTE;
 #pragma unroll
   for (int h = 0; h < NPX; h += 4) {
     uint32_t idx[4];
@@ -222,7 +221,7 @@ __device__ __forceinline__ void nn_masked_same_row(const MaskSpecS &ms, int mdt,
       if (__builtin_amdgcn_ballot_w64(need[q]) != 0) {
         // kNoPx reads nothing: its offset is past every band (range-checked)
         vv[q] = buf_load<T>(rs, idx[q] * (uint32_t)sizeof(T));
-        mraw[q] = m8 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(mrs, idx[q], 0, 0)
+        mraw[q] = M8 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(mrs, idx[q], 0, 0)
                      : (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(mrs, idx[q] * 2u, 0, 0);
       }
     }
@@ -230,15 +229,10 @@ __device__ __forceinline__ void nn_masked_same_row(const MaskSpecS &ms, int mdt,
     for (int q = 0; q < 4; q++) {
       const bool hit = idx[q] != kNoPx;
       const V v = hit ? vv[q] : fillv;
-      int32_t mv;
-      switch (mdt) {   // nn_fetch<mask type>'s value
-        case GSKYHIP_SIGNEDBYTE: mv = (int32_t)(int8_t)(uint8_t)mraw[q]; break;
-        case GSKYHIP_INT16: mv = (int32_t)(int16_t)(uint16_t)mraw[q]; break;
-        case GSKYHIP_BYTE: mv = (int32_t)(uint8_t)mraw[q]; break;
-        default: mv = (int32_t)(uint16_t)mraw[q]; break;
-      }
-      mv = hit ? mv : mfill;
-      const bool take = need[q] & (v != nd) && !mask_bit(ms, mdt, mv);
+      // nn_fetch<mask type>'s value; the pixel's take rule bitwise (a
+      // short-circuit && put an exec-mask branch around each pixel's test)
+      const int32_t mv = hit ? mask_typed(mdt, (int32_t)mraw[q]) : mfill;
+      const bool take = need[q] & (v != nd) & !mask_bit(ms, mdt, mv);
       c[h + q] = take ? v : c[h + q];
     }
   }
@@ -419,8 +413,14 @@ __device__ __forceinline__ void nn_entry_core(const RenderArgs &a, const EntryD 
       if (same && slot >= 0) {
         const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)m.band, (short)0, (int)((int64_t)m.bx * m.by * (int64_t)type_size(m.dt)), 0x00020000);
-        nn_masked_same_row<T, NPX>(a.mask[slot], m.dt, m.fill, rs, mrs, ru.v(0), ru.v(1), ru.v(2), ru.v(3), ic0, lim,
-                                   bx, by, nd, fillv, fill_mode, c);
+        // the mask's element width chosen once per entry row (per pixel, the
+        // compiler branched on the type around every mask gather)
+        if (m.dt == GSKYHIP_BYTE || m.dt == GSKYHIP_SIGNEDBYTE)
+          nn_masked_same_row<T, NPX, true>(a.mask[slot], m.dt, m.fill, rs, mrs, ru.v(0), ru.v(1), ru.v(2), ru.v(3), ic0,
+                                           lim, bx, by, nd, fillv, fill_mode, c);
+        else
+          nn_masked_same_row<T, NPX, false>(a.mask[slot], m.dt, m.fill, rs, mrs, ru.v(0), ru.v(1), ru.v(2), ru.v(3), ic0,
+                                            lim, bx, by, nd, fillv, fill_mode, c);
         return;
       }
     }
