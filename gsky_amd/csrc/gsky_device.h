@@ -789,6 +789,50 @@ __device__ __forceinline__ bool linear_nn_px(const RowRec &r, int dist, int bx, 
 __device__ __forceinline__ bool linear_row_inside(const RowRec &r, int n, int bx, int by) {
   return n > 0 && linear_nn_px(r, 0, bx, by) && linear_nn_px(r, n - 1, bx, by);
 }
+
+// The in-band span of a LINEAR row (round 6): the window pixels [lo, hi) whose
+// NN source pixel lies in the band -- every other pixel of the row takes the
+// window fill.  Kept in RowRec.v[4] as the bits lo | hi << 32 (v[4..5] only
+// carry DESCEND rows' points); kSpanNone: not computed.  Each of the four
+// tests of linear_nn_px() (sx >= 0, trunc(sx + 1e-10) < bx, same in y) is
+// monotone in d (the argument of linear_row_inside()), so the pixels passing
+// them form one interval: lo is the first pixel passing the tests that turn
+// true as d grows, hi the first one after it failing a test that turns false.
+// The NN band kernel folds such a row of a multi-entry tile like a window
+// edge row over the span, and drops the row outright when the span is empty
+// (the window fill equal to the nodata, render_nn.h).
+constexpr int64_t kSpanNone = -1;
+__device__ __forceinline__ int64_t span_bits(int lo, int hi) {
+  return (int64_t)(uint32_t)lo | ((int64_t)(uint32_t)hi << 32);
+}
+__device__ __forceinline__ int64_t linear_row_span(const RowRec &r, int n, int bx, int by) {
+  if (n <= 0) return span_bits(0, 0);
+  if (!(isfinite(r.v[0]) && isfinite(r.v[1]) && isfinite(r.v[2]) && isfinite(r.v[3]))) return kSpanNone;
+  const bool xup = r.v[2] >= 0.0, yup = r.v[3] >= 0.0;
+  // rising tests: true from some d on; falling: true up to some d
+  auto tests = [&](int d, bool &rise, bool &fall) {
+    const double sx = r.v[0] + r.v[2] * (double)d, sy = r.v[1] + r.v[3] * (double)d;
+    const int ix = __double2int_rz(sx + 1.0e-10), iy = __double2int_rz(sy + 1.0e-10);
+    const bool x0 = sx >= 0.0, x1 = ix < bx, y0 = sy >= 0.0, y1 = iy < by;
+    rise = (xup ? x0 : x1) && (yup ? y0 : y1);
+    fall = (xup ? x1 : x0) && (yup ? y1 : y0);
+  };
+  bool rs, fl;
+  int a = 0, b = n;   // lo: first d in [0, n) with the rising tests true (n: none)
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    tests(m, rs, fl);
+    if (rs) b = m; else a = m + 1;
+  }
+  const int lo = a;
+  b = n;              // hi: first d in [lo, n) with a falling test false (n: none)
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    tests(m, rs, fl);
+    if (!fl) b = m; else a = m + 1;
+  }
+  return lo < a ? span_bits(lo, a) : span_bits(0, 0);
+}
 // 32.32 fixed-point form of an `inside` LINEAR row (round 4), written beside
 // the RowRec by plan_row: x0 = round(xs0 * 2^32), dx = round(dX * 2^32), same
 // for y.  Window pixel d's fixed coordinate x0 + d * dx is within

@@ -1152,6 +1152,7 @@ __device__ __forceinline__ void plan_row(const PlanArgs &a, int p, const PairPla
         rec.kind = ROW_LINEAR;
         rec.v[0] = xs[0]; rec.v[1] = ys[0]; rec.v[2] = dX; rec.v[3] = dY;
         rec.inside = linear_row_inside(rec, n, pp.band_x, pp.band_y) ? 1 : 0;
+        rec.v[4] = __longlong_as_double(rec.inside ? span_bits(0, n) : linear_row_span(rec, n, pp.band_x, pp.band_y));
       } else {
         rec.kind = ROW_DESCEND;  // provisional: root SME kept for the split pass
         rec.v[0] = xs[0]; rec.v[1] = ys[0]; rec.v[2] = xs[1];

@@ -92,11 +92,14 @@ __device__ __forceinline__ uint32_t scale_int(const ScaleK &k, int32_t c) {
 // nothing and fold nothing; fill mode takes v where c is nodata, which equals
 // the general rule's "v != nd && c == nd" because v == nd == c leaves c
 // unchanged).  Halves of 4 pixels keep the register peak of the fast body.
+// The window is [wlo, whi) (wlo 0 and whi the window width, or a row's
+// in-band span).
 template <typename T, int NPX>
 __device__ __forceinline__ void nn_partial_row(__amdgpu_buffer_rsrc_t rs, double xs0, double ys0, double dX, double dY,
-                                               int ic0, int lim, int bx, typename VOf<T>::type nd, bool fill_mode,
-                                               int c0, int c1, typename VOf<T>::type (&c)[NPX]) {
+                                               int ic0, int wlo, int whi, int bx, typename VOf<T>::type nd,
+                                               bool fill_mode, typename VOf<T>::type (&c)[NPX]) {
   using V = typename VOf<T>::type;
+  const unsigned wn = (unsigned)(whi - wlo);
 #pragma unroll
   for (int h = 0; h < NPX; h += 4) {
     uint32_t off[4];
@@ -106,15 +109,15 @@ __device__ __forceinline__ void nn_partial_row(__amdgpu_buffer_rsrc_t rs, double
       const double dist = (double)ic;
       const int ix = __double2int_rz(xs0 + dX * dist + 1.0e-10);
       const int iy = __double2int_rz(ys0 + dY * dist + 1.0e-10);
-      off[q] = (unsigned)ic < (unsigned)lim ? (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T)
-                                            : 0x80000000u;
+      off[q] = (unsigned)(ic - wlo) < wn ? (__umul24((uint32_t)iy, (uint32_t)bx) + (uint32_t)ix) * (uint32_t)sizeof(T)
+                                         : 0x80000000u;
     }
     V vv[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) vv[q] = buf_load<T>(rs, off[q]);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const bool inw = (unsigned)(ic0 + 64 * (h + q)) < (unsigned)lim;
+      const bool inw = (unsigned)(ic0 + 64 * (h + q) - wlo) < wn;
       c[h + q] = (inw & (fill_mode ? (c[h + q] == nd) : (vv[q] != nd))) ? vv[q] : c[h + q];
     }
   }
@@ -281,6 +284,7 @@ struct RowMem {
   __device__ __forceinline__ int nleaf() const { return __builtin_amdgcn_readfirstlane(rr->nleaf); }
   __device__ __forceinline__ int pool_off() const { return __builtin_amdgcn_readfirstlane(rr->pool_off); }
   __device__ __forceinline__ double v(int k) const { return rr->v[k]; }
+  __device__ __forceinline__ int64_t span() const { return uni64(__double_as_longlong(rr->v[4])); }
 };
 struct RowVal {
   RowU ru;
@@ -294,6 +298,8 @@ struct RowVal {
   __device__ __forceinline__ int nleaf() const { return ru.nleaf; }
   __device__ __forceinline__ int pool_off() const { return ru.pool_off; }
   __device__ __forceinline__ double v(int k) const { return ru.v[k]; }
+  // the prefetching fold drops empty spans from its walk; no span here
+  __device__ __forceinline__ int64_t span() const { return kSpanNone; }
 };
 
 __device__ __forceinline__ EntryU entry_u(const EntryD &e) {
@@ -377,8 +383,22 @@ __device__ __forceinline__ void nn_entry_core(const RenderArgs &a, const EntryD 
     // window test (pixels outside the window read nothing and fold nothing;
     // fill mode takes v where c is nodata, which equals the general rule's
     // "v != nd && c == nd" because v == nd == c leaves c unchanged)
-    nn_partial_row<T, NPX>(rs, ru.v(0), ru.v(1), ru.v(2), ru.v(3), ic0, lim, bx, nd, fill_mode, c0, c1, c);
+    nn_partial_row<T, NPX>(rs, ru.v(0), ru.v(1), ru.v(2), ru.v(3), ic0, 0, lim, bx, nd, fill_mode, c);
     return;
+  }
+  if (kind == ROW_LINEAR && !masked && e.fill == e.nd && !(nd != nd)) {
+    // a row leaving the band (granule seams, bounding-box window corners):
+    // outside its in-band span every pixel takes the window fill, which is
+    // the nodata here and folds nothing (v == nd in either mode; a NaN
+    // nodata would fold), so the row is a window edge row over the span
+    const int64_t sp = ru.span();
+    if (sp != kSpanNone) {
+      const int lo = (int)(uint32_t)sp, hi = min((int)(sp >> 32), lim);
+      const int s0 = e.xoff + lo - xb, s1 = e.xoff + hi - xb;   // the span's columns of the block
+      if (hi <= lo || s1 <= 0 || s0 >= ncols) return;
+      nn_partial_row<T, NPX>(rs, ru.v(0), ru.v(1), ru.v(2), ru.v(3), ic0, lo, hi, bx, nd, fill_mode, c);
+      return;
+    }
   }
   Val fv;
   fv.u = e.fill;
@@ -525,6 +545,18 @@ __device__ __forceinline__ void nn_fold_row_stack(const RenderArgs &a, const Ent
     const void *band = E.band;
     const int bx = E.band_x, by = E.band_y, fill_mode = E.fill_mode, mask_pair = E.mask_pair;
     const uint32_t nd = E.nd.u, fill = E.fill.u;
+    {
+      // a LINEAR row whose in-band span misses the block's columns folds
+      // nothing when the window fill is the (non-NaN) nodata: off the walk
+      const int64_t sp = __double_as_longlong(R.v[4]);
+      const int slo = (int)(uint32_t)sp, shi = min((int)(sp >> 32), lim);
+      Val ndv;
+      ndv.u = nd;
+      const typename VOf<T>::type ndt = as_v<T>(ndv);
+      const bool empty = (kind == ROW_LINEAR) & (inside == 0) & (fill == nd) & (ndt == ndt) & (sp != kSpanNone) &
+                         ((shi <= slo) | (xoff + shi - xb <= 0) | (xoff + slo - xb >= ncols));
+      am &= __builtin_amdgcn_ballot_w64(!empty);
+    }
     int64_t fx0 = kFixNone, fy0 = 0, fdx = 0, fdy = 0;
     int mdt = 0;
     int32_t mfill = 0;
