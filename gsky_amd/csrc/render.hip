@@ -910,32 +910,37 @@ __device__ void plan_tile_serial(const PlanArgs &a, int t) {
 }
 
 
-constexpr int kWavePairs = 256;   // pairs per tile the wave-parallel merge planner holds in LDS
+constexpr int kWavePairs = 256;   // pairs per tile the wave-parallel merge planner holds in registers
+constexpr int kTileSlots = kWavePairs / 64;
 
 // One wavefront per tile: RasterMerger.Run's merge order (tile_merger.go:281-312:
 // stable sort by geoStamp descending), maskMap links (478-484), canvas
 // creation and the fill / overwrite mode of MergeMaskedRaster (47), as data-
-// parallel scans over the tile's pairs instead of the serial walk:
+// parallel passes over the tile's pairs instead of the serial walk:
 //   rank(p)   = #{q: stamp_q > stamp_p} + #{q < p: stamp_q == stamp_p}
 //   fill(k)   = ts_k < max(0, max{ts_j: j before k in the order, same ns})
 //   status    = the last error in merge order (the serial walk's last write).
-// The LDS of one wave's tile (plan_tile_wave).
-struct TileLds {
-  double stamp[kWavePairs], ts[kWavePairs];
-  int32_t info[kWavePairs];   // in_stack | is_mask << 1 | (ns + 1) << 2 | out_dtype << 8
-  int32_t rank[kWavePairs];   // merge position of an in-stack pair, -1 otherwise
-};
+// Lane l holds pairs l, l + 64, ... in registers; each pass walks the tile's
+// pairs q in index order, q's values read out of its lane (v_readlane), and
+// every lane updates its own pairs -- no memory access inside the passes
+// (round 6: the LDS form's dependent loads took 70 us for C5's 128-pair
+// tiles).
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
-// Synchronisation of the 64 lanes of one wavefront: its LDS and global
-// accesses are performed in program order, so this only keeps the compiler
-// from moving memory operations across it.
+// Synchronisation of the 64 lanes of one wavefront: its global accesses are
+// performed in program order, so this only keeps the compiler from moving
+// memory operations across it.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lane, TileLds &L) {
+__device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lane) {
   const gskyhip_tile &tile = a.tiles[t];
   const int b = tile.pair_begin, e = tile.pair_end, np = e - b;
   const bool bad_size = tile.width <= 0 || tile.height <= 0 || tile.width > a.max_w || tile.height > a.max_h;
@@ -943,74 +948,109 @@ __device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lan
     if (lane == 0) plan_tile_serial(a, t);
     return;
   }
-  double *s_stamp = L.stamp, *s_ts = L.ts;
-  int32_t *s_info = L.info, *s_rank = L.rank;
-  for (int i = lane; i < np; i += 64) {
-    const PairPlan &pp = a.pairs[b + i];
-    s_stamp[i] = pp.stamp;
-    s_ts[i] = pp.ts;
-    s_info[i] = (pp.in_stack ? 1 : 0) | (pp.is_mask ? 2 : 0) | ((pp.ns + 1) << 2) | (pp.out_dtype << 8);
-  }
-  wave_sync();
-  // merge order
-  for (int i = lane; i < np; i += 64) {
-    int rk = -1;
-    if (s_info[i] & 1) {
-      const double s = s_stamp[i];
-      rk = 0;
-      for (int q = 0; q < np; q++)
-        if ((s_info[q] & 1) && (s_stamp[q] > s || (q < i && s_stamp[q] == s))) rk++;
-      a.order[b + rk] = b + i;
+  const int S = (np + 63) >> 6;   // register slots in use
+  double st[kTileSlots], tsv[kTileSlots];
+  int inf[kTileSlots];            // in_stack | is_mask << 1 | (ns + 1) << 2 | out_dtype << 8
+#pragma unroll
+  for (int j = 0; j < kTileSlots; j++) {
+    const int i = 64 * j + lane;
+    st[j] = 0.0; tsv[j] = 0.0; inf[j] = 0;
+    if (j < S && i < np) {
+      const PairPlan &pp = a.pairs[b + i];
+      st[j] = pp.stamp;
+      tsv[j] = pp.ts;
+      inf[j] = (pp.in_stack ? 1 : 0) | (pp.is_mask ? 2 : 0) | ((pp.ns + 1) << 2) | (pp.out_dtype << 8);
     }
-    s_rank[i] = rk;
   }
-  wave_sync();
-  // per merged entry: maskMap link, fill mode, first-of-namespace, error
+  // pass 1: merge rank and maskMap link (the last mask pair of the same key)
+  int rk[kTileSlots], mpi[kTileSlots];
+#pragma unroll
+  for (int j = 0; j < kTileSlots; j++) { rk[j] = 0; mpi[j] = -1; }
+#pragma unroll
+  for (int jq = 0; jq < kTileSlots; jq++) {
+    if (jq >= S) break;
+    const int nq = min(64, np - 64 * jq);
+#pragma unroll 1
+    for (int l = 0; l < nq; l++) {
+      const double sq = readlane_d(st[jq], l);
+      const int iq = __builtin_amdgcn_readlane(inf[jq], l);
+      const int q = 64 * jq + l;
+#pragma unroll
+      for (int j = 0; j < kTileSlots; j++) {
+        if (j >= S) break;
+        const int i = 64 * j + lane;
+        rk[j] += ((iq & 1) && (sq > st[j] || (q < i && sq == st[j]))) ? 1 : 0;
+        mpi[j] = ((iq & 2) && sq == st[j]) ? q : mpi[j];
+      }
+    }
+  }
   int n_local = 0;
-  for (int i = lane; i < np; i += 64) n_local += (s_info[i] & 1);
+#pragma unroll
+  for (int j = 0; j < kTileSlots; j++) {
+    const int i = 64 * j + lane;
+    const bool in = j < S && i < np && (inf[j] & 1);
+    if (in) a.order[b + rk[j]] = b + i;
+    rk[j] = in ? rk[j] : -1;
+    n_local += in ? 1 : 0;
+  }
   for (int o = 32; o > 0; o >>= 1) n_local += __shfl_xor(n_local, o, 64);
   const int n = n_local;
+  // pass 2: the canvas timestamp before each entry (running max of its
+  // namespace's earlier entries, from 0) and its namespace's first entry
+  double cts[kTileSlots];
+  int fk[kTileSlots], fdt[kTileSlots];
+#pragma unroll
+  for (int j = 0; j < kTileSlots; j++) { cts[j] = 0.0; fk[j] = 0x7FFFFFFF; fdt[j] = 0; }
+#pragma unroll
+  for (int jq = 0; jq < kTileSlots; jq++) {
+    if (jq >= S) break;
+    const int nq = min(64, np - 64 * jq);
+#pragma unroll 1
+    for (int l = 0; l < nq; l++) {
+      const int kq = __builtin_amdgcn_readlane(rk[jq], l);
+      if (kq < 0) continue;
+      const int iq = __builtin_amdgcn_readlane(inf[jq], l);
+      const double tq = readlane_d(tsv[jq], l);
+#pragma unroll
+      for (int j = 0; j < kTileSlots; j++) {
+        if (j >= S) break;
+        const bool same = ((iq ^ inf[j]) & (63 << 2)) == 0;
+        if (same && kq < rk[j]) cts[j] = fmax(cts[j], tq);
+        if (same && kq < fk[j]) { fk[j] = kq; fdt[j] = iq >> 8; }
+      }
+    }
+  }
+  // per merged entry: maskMap link, fill mode, error
   int err_k = -1, err_code = 0;                  // this lane's last error (largest merge position)
   int first_k[4] = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
-  for (int i = lane; i < np; i += 64) {
-    const int k = s_rank[i];
-    if (k < 0) continue;
-    const int p = b + i;
-    PairPlan &pp = a.pairs[p];
-    const double s = s_stamp[i];
-    int mp = -1;
-    for (int q = 0; q < np; q++)
-      if ((s_info[q] & 2) && s_stamp[q] == s) mp = b + q;
+#pragma unroll
+  for (int j = 0; j < kTileSlots; j++) {
+    const int k = rk[j];
+    if (j >= S || k < 0) continue;
+    const int i = 64 * j + lane;
+    PairPlan &pp = a.pairs[b + i];
+    const int mp = mpi[j] >= 0 ? b + mpi[j] : -1;
     pp.mask_pair = mp;
-    int st = 0;
+    int st_code = 0;
     if (mp >= 0) {
       const PairPlan &mq = a.pairs[mp];
       const int mdt = mq.out_dtype;
       if (!(mdt == GSKYHIP_SIGNEDBYTE || mdt == GSKYHIP_BYTE || mdt == GSKYHIP_INT16 || mdt == GSKYHIP_UINT16))
-        st = GSKYHIP_E_MASK;
+        st_code = GSKYHIP_E_MASK;
       else if ((long)pp.w * pp.h > (long)mq.w * mq.h)
-        st = GSKYHIP_E_RANGE;
+        st_code = GSKYHIP_E_RANGE;
     }
-    const int ns = ((s_info[i] >> 2) & 63) - 1;
+    const int ns = ((inf[j] >> 2) & 63) - 1;
     int fill = 0;
     if (ns < 0 || ns >= 4) {
-      st = GSKYHIP_E_RANGE;
+      st_code = GSKYHIP_E_RANGE;
     } else {
       first_k[ns] = min(first_k[ns], k);
-      // canvas timestamp before k: running max of the namespace's earlier entries, from 0
-      double cts = 0.0;
-      int first_q = -1, first_qk = 0x7FFFFFFF;
-      for (int q = 0; q < np; q++) {
-        const int kq = s_rank[q];
-        if (kq < 0 || ((s_info[q] >> 2) & 63) - 1 != ns) continue;
-        if (kq < k) cts = fmax(cts, s_ts[q]);
-        if (kq < first_qk) { first_qk = kq; first_q = q; }
-      }
-      fill = s_ts[i] < cts ? 1 : 0;
-      if (first_qk < k && (s_info[first_q] >> 8) != (s_info[i] >> 8)) st = GSKYHIP_E_TYPE;
+      fill = tsv[j] < cts[j] ? 1 : 0;
+      if (fk[j] < k && fdt[j] != (inf[j] >> 8)) st_code = GSKYHIP_E_TYPE;
     }
     pp.fill_mode = fill;
-    if (st && k > err_k) { err_k = k; err_code = st; }
+    if (st_code && k > err_k) { err_k = k; err_code = st_code; }
   }
   // wave reductions: last error, first entry of each namespace
   for (int o = 32; o > 0; o >>= 1) {
@@ -1062,8 +1102,7 @@ __device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lan
 __global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
   const int t = blockIdx.x;
   if (t >= a.n_tiles) return;
-  __shared__ TileLds L;
-  plan_tile_wave(a, t, threadIdx.x, L);
+  plan_tile_wave(a, t, threadIdx.x);
 }
 
 // ---------------------------------------------------------------- row plans
@@ -1341,7 +1380,6 @@ __global__ __launch_bounds__(256) void plan_exact_kernel(PlanArgs a) {
 // barrier between phases).  The same device bodies as the separate kernels,
 // so the same plan.  Also zeroes the counters (the prologue does not run).
 __global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
-  __shared__ TileLds L[4];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 #ifdef GSKYHIP_AB
   // phase time stamps (GSKYHIP_PLAN_STAMPS): 100 MHz wall clock into counters[40 + i]
@@ -1373,7 +1411,7 @@ __global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
   stamp();
   if (tid < 64) a.counters[tid] = 0;
   __syncthreads();
-  for (int t = wave; t < a.n_tiles; t += 4) plan_tile_wave(a, t, lane, L[wave]);
+  for (int t = wave; t < a.n_tiles; t += 4) plan_tile_wave(a, t, lane);
   __syncthreads();
   stamp();
   if (a.sep)
