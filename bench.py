@@ -691,7 +691,8 @@ def run_c5(ctx: Ctx, args):
     gs = build_granules(cfg, ctx.device)
     b = build_batch(cfg, ctx.device, gs=gs)
     sp = ScaleParams(*cfg.scale)
-    dt = ctx.timed(lambda: b.render(sp), args.steps, args.warmup)
+    steps = args.c5_steps or args.steps
+    dt = ctx.timed(lambda: b.render(sp), steps, args.warmup)
     plan_ms = event_ms(lambda: b.render(sp, phase=1), max(3, args.steps))
     render_ms = event_ms(lambda: b.render(sp, phase=2), max(3, args.steps))
     # algorithmic bytes of the render launch: the distinct
@@ -705,9 +706,9 @@ def run_c5(ctx: Ctx, args):
     lat = tile_latency(ctx, cfg, gs, sp, None, list(range(0, len(cfg.tiles), max(1, len(cfg.tiles) // 8))), 10)
     out = {"workload": "C5: 80 512x512 EPSG:3857 overview tiles (z4+z5) from 256 MODIS sinusoidal int16 granules + "
                        "256 QA mask granules with overview pyramids, mask 00000001, grey scaling",
-           "tiles_per_s": round(len(full.tiles) * args.steps / dt, 1),
-           "value": round(full.out_pixels * args.steps / dt / 1e6, 1), "unit": "Mpix/s",
-           "ms_per_step": round(dt / args.steps * 1e3, 4), "step_ms": ctx.step_stats,
+           "tiles_per_s": round(len(full.tiles) * steps / dt, 1),
+           "value": round(full.out_pixels * steps / dt / 1e6, 1), "unit": "Mpix/s",
+           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "step_ms": ctx.step_stats,
            "p50_tile_ms": round(float(np.percentile(lat, 50)), 4),
            "p50_timing": "host wall of a one-tile request (plan + render + synchronize), rank 0",
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -829,6 +830,9 @@ def main():
     ap.add_argument("--c1-cpu-reps", type=int, default=200)
     ap.add_argument("--c2-chunks", type=int, default=1, help="C2 step: tile chunks pipelined on 2 streams (1: one batch; measured no gain, profiles/r02o_*)")
     ap.add_argument("--c3-steps", type=int, default=3)
+    ap.add_argument("--c5-steps", type=int, default=50,
+                    help="C5 timed steps (0: --steps); a 0.33 ms step would carry the timed region's ~0.8 ms of "
+                         "start / end latency at 10 steps")
     ap.add_argument("--c4-cpu-polys", type=int, default=160)
     ap.add_argument("--no-deciles", action="store_true", help="C4: skip the decileCount=9 line")
     ap.add_argument("--c2-lat-tiles", type=int, default=32, help="C2 p50: one-tile requests over this many tiles")
