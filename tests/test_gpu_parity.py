@@ -375,6 +375,27 @@ def test_render_c2_small(gpu, oracle):
     assert (exp[..., 3] > 0).mean() > 0.3      # the test exercises real data
 
 
+@pytest.mark.parametrize("nodata", [40000.0, -999.0])
+def test_render_seams_window_fill(gpu, oracle, nodata):
+    """Granule seams (tiles with 2+ stack entries whose window rows leave the
+    band): with the nodata in range the band kernel folds those rows over
+    their in-band spans (RowRec.v[4]); with an int16 nodata out of range the
+    window fill (GDALCopyWords: clamped, 32767) differs from the merge nodata
+    (Go int16(): wrapped, -25536), the pixels off the span fold the fill, and
+    the span path must stay off.  Both against the oracle."""
+    import dataclasses
+
+    import gsky_amd
+    cfg = synth.config_c2(scale=0.1, tiles_per_side=4, tile_px=256)
+    cfg = dataclasses.replace(cfg, granules=[dataclasses.replace(g, nodata=nodata) for g in cfg.granules])
+    assert any(len(p) >= 2 for p in cfg.pairs)   # the batch has seam tiles
+    b = gpu_batch(cfg)
+    got = b.render(gsky_amd.ScaleParams(*cfg.scale), gsky_amd.Palette(cfg.palette, True)).cpu().numpy()
+    assert b.status() == 0
+    exp = oracle_render(oracle, cfg)
+    assert identity(got, exp) >= NN_IDENTITY
+
+
 def test_render_acceptance_requests(gpu, oracle):
     """The reference's own 500 acceptance GetMap requests
     (acceptance_tests/acpt_url.tpl -> tests/golden/acpt_bboxes.json: 256^2
