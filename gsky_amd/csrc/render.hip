@@ -940,12 +940,21 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lane) {
+// The per-wave partials of the passes when NW waves share a tile (wave w
+// walks the pairs q = w, w + NW, ... of each register slot).
+template <int NW>
+struct TileRed {
+  int32_t rk[NW][kWavePairs], mp[NW][kWavePairs], fk[NW][kWavePairs], fdt[NW][kWavePairs];
+  double cts[NW][kWavePairs];
+};
+
+template <int NW>
+__device__ __forceinline__ void plan_tile_waves(const PlanArgs &a, int t, int w, int lane, TileRed<NW> *red) {
   const gskyhip_tile &tile = a.tiles[t];
   const int b = tile.pair_begin, e = tile.pair_end, np = e - b;
   const bool bad_size = tile.width <= 0 || tile.height <= 0 || tile.width > a.max_w || tile.height > a.max_h;
   if (np > kWavePairs || bad_size) {
-    if (lane == 0) plan_tile_serial(a, t);
+    if (w == 0 && lane == 0) plan_tile_serial(a, t);
     return;
   }
   const int S = (np + 63) >> 6;   // register slots in use
@@ -971,7 +980,7 @@ __device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lan
     if (jq >= S) break;
     const int nq = min(64, np - 64 * jq);
 #pragma unroll 1
-    for (int l = 0; l < nq; l++) {
+    for (int l = w; l < nq; l += NW) {
       const double sq = readlane_d(st[jq], l);
       const int iq = __builtin_amdgcn_readlane(inf[jq], l);
       const int q = 64 * jq + l;
@@ -984,12 +993,28 @@ __device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lan
       }
     }
   }
+  if constexpr (NW > 1) {   // the waves' partial counts and last links, summed / maxed
+#pragma unroll
+    for (int j = 0; j < kTileSlots; j++) {
+      red->rk[w][64 * j + lane] = rk[j];
+      red->mp[w][64 * j + lane] = mpi[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kTileSlots; j++) {
+      int sr = 0, sm = -1;
+#pragma unroll
+      for (int v = 0; v < NW; v++) { sr += red->rk[v][64 * j + lane]; sm = max(sm, red->mp[v][64 * j + lane]); }
+      rk[j] = sr;
+      mpi[j] = sm;
+    }
+  }
   int n_local = 0;
 #pragma unroll
   for (int j = 0; j < kTileSlots; j++) {
     const int i = 64 * j + lane;
     const bool in = j < S && i < np && (inf[j] & 1);
-    if (in) a.order[b + rk[j]] = b + i;
+    if (in && w == 0) a.order[b + rk[j]] = b + i;
     rk[j] = in ? rk[j] : -1;
     n_local += in ? 1 : 0;
   }
@@ -1006,7 +1031,7 @@ __device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lan
     if (jq >= S) break;
     const int nq = min(64, np - 64 * jq);
 #pragma unroll 1
-    for (int l = 0; l < nq; l++) {
+    for (int l = w; l < nq; l += NW) {
       const int kq = __builtin_amdgcn_readlane(rk[jq], l);
       if (kq < 0) continue;
       const int iq = __builtin_amdgcn_readlane(inf[jq], l);
@@ -1017,6 +1042,24 @@ __device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lan
         const bool same = ((iq ^ inf[j]) & (63 << 2)) == 0;
         if (same && kq < rk[j]) cts[j] = fmax(cts[j], tq);
         if (same && kq < fk[j]) { fk[j] = kq; fdt[j] = iq >> 8; }
+      }
+    }
+  }
+  if constexpr (NW > 1) {   // the waves' partial canvas timestamps and first entries; wave 0 goes on
+#pragma unroll
+    for (int j = 0; j < kTileSlots; j++) {
+      red->cts[w][64 * j + lane] = cts[j];
+      red->fk[w][64 * j + lane] = fk[j];
+      red->fdt[w][64 * j + lane] = fdt[j];
+    }
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int j = 0; j < kTileSlots; j++) {
+      for (int v = 1; v < NW; v++) {
+        cts[j] = fmax(cts[j], red->cts[v][64 * j + lane]);
+        const int k2 = red->fk[v][64 * j + lane];
+        if (k2 < fk[j]) { fk[j] = k2; fdt[j] = red->fdt[v][64 * j + lane]; }
       }
     }
   }
@@ -1102,7 +1145,18 @@ __device__ __forceinline__ void plan_tile_wave(const PlanArgs &a, int t, int lan
 __global__ __launch_bounds__(64) void plan_tiles_kernel(PlanArgs a) {
   const int t = blockIdx.x;
   if (t >= a.n_tiles) return;
-  plan_tile_wave(a, t, threadIdx.x);
+  plan_tile_waves<1>(a, t, 0, threadIdx.x, nullptr);
+}
+
+// Tiles of many pairs (C5's overview tiles: 34 on average, up to 128): the
+// passes of a tile spread over 4 waves (70 -> 37 -> ~20 us on C5; one wave
+// per tile stays for batches of few pairs per tile, C2's 1.2).
+constexpr int kTiles4MinPairsPerTile = 8;
+__global__ __launch_bounds__(256) void plan_tiles4_kernel(PlanArgs a) {
+  const int t = blockIdx.x;
+  if (t >= a.n_tiles) return;
+  __shared__ TileRed<4> red;
+  plan_tile_waves<4>(a, t, threadIdx.x >> 6, threadIdx.x & 63, &red);
 }
 
 // ---------------------------------------------------------------- row plans
@@ -1411,7 +1465,7 @@ __global__ __launch_bounds__(256) void plan_small_kernel(PlanArgs a) {
   stamp();
   if (tid < 64) a.counters[tid] = 0;
   __syncthreads();
-  for (int t = wave; t < a.n_tiles; t += 4) plan_tile_wave(a, t, lane);
+  for (int t = wave; t < a.n_tiles; t += 4) plan_tile_waves<1>(a, t, 0, lane, nullptr);
   __syncthreads();
   stamp();
   if (a.sep)
@@ -2093,7 +2147,10 @@ static int plan_all(const RenderCall &rc, Carve &cv) {
     hipLaunchKernelGGL(plan_pairs_kernel<256>, dim3(rc.n_pairs), dim3(256), 0, s, a);
   else if (rc.n_pairs > 0)
     hipLaunchKernelGGL(plan_pairs_kernel<64>, dim3(rc.n_pairs), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(plan_tiles_kernel, dim3(rc.n_tiles), dim3(64), 0, s, a);
+  if (rc.n_pairs >= kTiles4MinPairsPerTile * rc.n_tiles)
+    hipLaunchKernelGGL(plan_tiles4_kernel, dim3(rc.n_tiles), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(plan_tiles_kernel, dim3(rc.n_tiles), dim3(64), 0, s, a);
   if (rc.n_pairs > 0) {
     if (a.sep)
       hipLaunchKernelGGL(plan_cols_kernel, dim3((unsigned)((3 * (int64_t)rc.n_pairs + 255) / 256)), dim3(256), 0, s,

@@ -1,0 +1,27 @@
+#!/bin/bash
+# r06: plan_tiles_kernel's passes spread over 4 waves per tile -- the whole
+# GPU suite, then bench C5 / C2 on the previous build (libgskyhip_prev.so)
+# and this one, alternating, + C5 kernel stats.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${1:-r06t4}
+stop() { echo "[$2] rc=$1"; if [ "$1" -ne 0 ]; then echo "stopping after $2"; exit "$1"; fi; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread --ignore=tests/test_warp_exact.py > gpurun_out/${T}_gpu_tests.txt 2>&1
+stop $? gpu_tests
+for rep in 1 2; do
+  for lib in prev default; do
+    for c in c5 c2; do
+      GSKYHIP_LIB=$([ $lib = default ] && echo "" || echo $lib) timeout -k 10 300 python -u bench.py --only $c --no-cpu --steps 20 --warmup 3 --png-tiles 0 > gpurun_out/${T}_bench_${c}_${lib}_$rep.json 2>/dev/null
+      stop $? bench_${c}_${lib}
+      python3 -c "
+import json; d=json.load(open('gpurun_out/${T}_bench_${c}_${lib}_$rep.json')); x=d['configs']['${c}'.upper()] if '${c}' != 'c2' else d
+print('$lib', '$c', x['ms_per_step'], x['step_ms'], x['roofline']['kernel_ms'], x['roofline']['plan_ms'])"
+    done
+  done
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_c5 -o run --output-format csv -- \
+  python3 bench.py --only c5 --no-cpu --steps 5 --warmup 2 --png-tiles 0 > gpurun_out/${T}_prof_c5.txt 2>&1
+stop $? prof_c5
+tail -1 gpurun_out/${T}_gpu_tests.txt
